@@ -1,0 +1,195 @@
+"""ctypes view of the C restatement oracle (oracle/build/liboracle.so).
+
+Test infrastructure: only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg import this module.  All arrays are numpy uint64 in the
+halo2curves layout (Montgomery limbs; Fr = 4 limbs, G1Affine = 8 limbs).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(REPO, "oracle", "build", "liboracle.so")
+
+_lib = None
+U64P = ctypes.POINTER(ctypes.c_uint64)
+
+
+def _p(a):
+    if a is None:
+        return None
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"], (a.dtype, a.flags)
+    return a.ctypes.data_as(U64P)
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "oracle")])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        u64, u32, i32 = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+        sig = {
+            "or_g1_is_on_curve": ([U64P], i32),
+            "or_g1_mul": ([U64P, U64P, U64P], None),
+            "or_g1_add": ([U64P, U64P, U64P], None),
+            "or_srs_powers": ([U64P, u64, U64P], None),
+            "or_msm_naive": ([U64P, U64P, u64, U64P], None),
+            "or_msm_best": ([U64P, U64P, u64, i32, U64P], None),
+            "or_fft": ([U64P, u32, U64P, i32], None),
+            "or_domain_constants": ([u32, u32, U64P, U64P], u32),
+            "or_lagrange_to_coeff": ([U64P, u32, u32, i32], None),
+            "or_coeff_to_extended": ([U64P, U64P, u32, u32, i32], None),
+            "or_extended_to_coeff": ([U64P, U64P, u32, u32, i32], None),
+            "or_divide_by_vanishing_poly": ([U64P, u32, u32], None),
+            "or_fr_add": ([U64P, U64P, U64P, u64], None),
+            "or_fr_sub": ([U64P, U64P, U64P, u64], None),
+            "or_fr_mul": ([U64P, U64P, U64P, u64], None),
+            "or_fr_scale": ([U64P, U64P, U64P, u64], None),
+            "or_fr_from_canonical": ([U64P, U64P, u64], None),
+            "or_fr_to_canonical": ([U64P, U64P, u64], None),
+            "or_fq_from_canonical": ([U64P, U64P, u64], None),
+            "or_fr_eval": ([U64P, u64, U64P, U64P], None),
+            "or_kate_division": ([U64P, u64, U64P, U64P], None),
+            "or_fr_batch_invert": ([U64P, u64], None),
+            "or_fr_prefix_product": ([U64P, U64P, u64], None),
+            "or_num_threads": ([], i32),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def fr_arr(n):
+    return np.zeros((n, 4), dtype=np.uint64)
+
+
+def msm_naive(scalars, bases):
+    out = np.zeros(8, dtype=np.uint64)
+    lib().or_msm_naive(_p(np.ascontiguousarray(scalars)), _p(np.ascontiguousarray(bases)), len(scalars), _p(out))
+    return out
+
+
+def msm_best(scalars, bases, threads=1):
+    out = np.zeros(8, dtype=np.uint64)
+    lib().or_msm_best(_p(np.ascontiguousarray(scalars)), _p(np.ascontiguousarray(bases)), len(scalars), threads, _p(out))
+    return out
+
+
+def fft(a, omega, threads=1):
+    a = np.ascontiguousarray(a.copy())
+    k = int(len(a)).bit_length() - 1
+    lib().or_fft(_p(a), k, _p(np.ascontiguousarray(omega)), threads)
+    return a
+
+
+def domain_constants(j, k):
+    c = np.zeros((9, 4), dtype=np.uint64)
+    t = np.zeros((1 << 12, 4), dtype=np.uint64)
+    ek = lib().or_domain_constants(j, k, _p(c), _p(t))
+    return ek, c, t[: 1 << (ek - k)].copy()
+
+
+def lagrange_to_coeff(a, j, k, threads=1):
+    a = np.ascontiguousarray(a.copy())
+    lib().or_lagrange_to_coeff(_p(a), j, k, threads)
+    return a
+
+
+def coeff_to_extended(a, j, k, threads=1):
+    ek = domain_constants(j, k)[0]
+    out = fr_arr(1 << ek)
+    lib().or_coeff_to_extended(_p(np.ascontiguousarray(a)), _p(out), j, k, threads)
+    return out
+
+
+def extended_to_coeff(a, j, k, threads=1):
+    a = np.ascontiguousarray(a.copy())
+    out = fr_arr((1 << k) * (j - 1))
+    lib().or_extended_to_coeff(_p(a), _p(out), j, k, threads)
+    return out
+
+
+def divide_by_vanishing_poly(a, j, k):
+    a = np.ascontiguousarray(a.copy())
+    lib().or_divide_by_vanishing_poly(_p(a), j, k)
+    return a
+
+
+def binop(name, a, b):
+    out = fr_arr(len(a))
+    getattr(lib(), name)(_p(np.ascontiguousarray(a)), _p(np.ascontiguousarray(b)), _p(out), len(a))
+    return out
+
+
+def scale(a, x):
+    out = fr_arr(len(a))
+    lib().or_fr_scale(_p(np.ascontiguousarray(a)), _p(np.ascontiguousarray(x)), _p(out), len(a))
+    return out
+
+
+def eval_poly(a, x):
+    out = np.zeros(4, dtype=np.uint64)
+    lib().or_fr_eval(_p(np.ascontiguousarray(a)), len(a), _p(np.ascontiguousarray(x)), _p(out))
+    return out
+
+
+def kate_division(a, b):
+    q = fr_arr(len(a) - 1)
+    lib().or_kate_division(_p(np.ascontiguousarray(a)), len(a), _p(np.ascontiguousarray(b)), _p(q))
+    return q
+
+
+def batch_invert(a):
+    a = np.ascontiguousarray(a.copy())
+    lib().or_fr_batch_invert(_p(a), len(a))
+    return a
+
+
+def prefix_product(a):
+    out = fr_arr(len(a))
+    lib().or_fr_prefix_product(_p(np.ascontiguousarray(a)), _p(out), len(a))
+    return out
+
+
+def srs_powers(s, n):
+    out = np.zeros((n, 8), dtype=np.uint64)
+    lib().or_srs_powers(_p(np.ascontiguousarray(s)), n, _p(out))
+    return out
+
+
+def g1_mul(pt, s):
+    out = np.zeros(8, dtype=np.uint64)
+    lib().or_g1_mul(_p(np.ascontiguousarray(pt)), _p(np.ascontiguousarray(s)), _p(out))
+    return out
+
+
+def g1_add(a, b):
+    out = np.zeros(8, dtype=np.uint64)
+    lib().or_g1_add(_p(np.ascontiguousarray(a)), _p(np.ascontiguousarray(b)), _p(out))
+    return out
+
+
+def fr_from_canonical(c):
+    c = np.ascontiguousarray(c, dtype=np.uint64).reshape(-1, 4)
+    out = fr_arr(len(c))
+    lib().or_fr_from_canonical(_p(c), _p(out), len(c))
+    return out
+
+
+def random_fr(rng, n):
+    """Uniform-ish Fr elements (Montgomery form) from a numpy Generator: canonical
+    values below 2^253 < r, then converted to Montgomery form by the oracle."""
+    c = rng.integers(0, 2**63, size=(n, 4), dtype=np.int64).astype(np.uint64)
+    c[:, 3] &= np.uint64((1 << 61) - 1)  # < 2^253 < r
+    c[:, 0] = rng.integers(0, 2**63, size=n, dtype=np.int64).astype(np.uint64) * np.uint64(2) + (c[:, 0] & np.uint64(1))
+    return fr_from_canonical(c)
