@@ -1,0 +1,144 @@
+/*
+ * h2g.h -- C ABI of the MI355X-native halo2 prover hot path (libh2g.so).
+ *
+ * This is the drop-in boundary a halo2 (yetanotherco/yet-another-halo2-fork)
+ * host binds over FFI.  Plain pointers and sizes only; no torch or HIP types.
+ *
+ * Data layout (identical to halo2curves 0.6 in memory, so Rust slices are passed
+ * by pointer with no conversion):
+ *   Fr  : 4 x uint64_t little-endian limbs, Montgomery form (R = 2^256), < r
+ *   G1Affine : x[4], y[4] Fq limbs, Montgomery form; identity = (0, 0)
+ * Host-pointer entry points copy in/out and return when the result is ready.
+ * `_dev` entry points take device pointers (hipMalloc'd, or torch tensors'
+ * data_ptr()) and a `stream` (hipStream_t; NULL = the library's stream for the
+ * current device); they are asynchronous unless noted.
+ *
+ * Every function returns H2G_OK (0) or an error code; h2g_last_error() gives a
+ * message.  Reference interfaces replaced are cited per entry point
+ * (paths relative to the reference snapshot root).
+ */
+#ifndef H2G_H
+#define H2G_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  H2G_OK = 0,
+  H2G_ERR_ARG = 1,     /* invalid argument (the reference panics: assert_eq! in best_multiexp/commit) */
+  H2G_ERR_DEVICE = 2,  /* HIP runtime error */
+  H2G_ERR_NOMEM = 3,
+  H2G_ERR_STATE = 4,   /* not initialised */
+  H2G_ERR_HANDLE = 5   /* unknown descriptor / domain handle */
+};
+
+int h2g_abi_version(void);
+const char* h2g_last_error(void);
+
+/* ---- engine lifecycle ---------------------------------------------------
+ * Replaces PlonkEngineConfig::new().set_curve::<G1Affine>().set_msm(engine).build()
+ * (halo2_middleware/src/zal.rs:204-243): initialises the listed HIP devices
+ * (NULL/0 = device 0). */
+int h2g_init(const int* devices, int ndev);
+int h2g_shutdown(void);
+int h2g_device_count(int* out);
+int h2g_set_device(int index); /* index into the h2g_init list */
+
+/* ---- MsmAccel<G1Affine> (halo2_middleware/src/zal.rs:57-103) ----------------
+ * msm(coeffs, base) -> C::Curve  (zal.rs:58; H2cEngine::msm = best_multiexp, zal.rs:136-138).
+ * Result returned affine (out[8]) + identity flag; the shim converts with G1::from. */
+int h2g_msm(const uint64_t* coeffs, const uint64_t* bases, size_t n, uint64_t out_affine[8],
+            int* out_is_identity);
+/* get_coeffs_descriptor / get_base_descriptor (zal.rs:83-84): upload once, keep on device */
+int h2g_msm_coeffs_descriptor(const uint64_t* coeffs, size_t n, uint64_t* handle);
+int h2g_msm_base_descriptor(const uint64_t* bases, size_t n, uint64_t* handle);
+int h2g_msm_descriptor_free(uint64_t handle); /* Drop of a descriptor (zal.rs:47) */
+/* msm_with_cached_scalars / _base / _inputs (zal.rs:86-102); base_offset selects the
+ * prefix/sub-slice &bases[off..off+n] used by commit / commit_lagrange
+ * (halo2_backend/src/poly/kzg/commitment.rs:316, 365) */
+int h2g_msm_with_cached_scalars(uint64_t coeffs, const uint64_t* bases, size_t n, uint64_t out_affine[8],
+                                int* out_is_identity);
+int h2g_msm_with_cached_base(const uint64_t* coeffs, size_t n, uint64_t base, size_t base_offset,
+                             uint64_t out_affine[8], int* out_is_identity);
+int h2g_msm_with_cached_inputs(uint64_t coeffs, uint64_t base, size_t base_offset, uint64_t out_affine[8],
+                               int* out_is_identity);
+/* device-resident MSM: d_out receives 8 u64 (affine, identity = zeros) */
+int h2g_msm_dev(const void* d_coeffs, const void* d_bases, size_t n, void* d_out_affine, void* stream);
+/* same, with an explicit Pippenger window size c (0 = automatic) */
+int h2g_msm_dev_cfg(const void* d_coeffs, const void* d_bases, size_t n, int window_bits, void* d_out_affine,
+                    void* stream);
+int h2g_descriptor_device_ptr(uint64_t handle, void** d_ptr, size_t* n);
+
+/* ---- SRS generation on device: g_i = [s^i] G, i < n
+ * (ParamsKZG::setup, halo2_backend/src/poly/kzg/commitment.rs:64-90). s in Montgomery form. */
+int h2g_srs_setup_dev(const uint64_t s[4], size_t n, void* d_out_affine, void* stream);
+
+/* ---- NTT boundary (new seam; best_fft call sites halo2_backend/src/poly/domain.rs:238, 344
+ * and halo2_backend/src/arithmetic.rs:38).  In place, natural order in and out:
+ * a_k <- sum_i a_i omega^(ik), n = 2^log_n. */
+int h2g_fft(uint64_t* a, uint32_t log_n, const uint64_t omega[4]);
+int h2g_fft_dev(void* d_a, uint32_t log_n, const uint64_t omega[4], void* stream);
+
+/* ---- EvaluationDomain (halo2_backend/src/poly/domain.rs) -------------------- */
+/* EvaluationDomain::new(j, k) (domain.rs:38-144) */
+int h2g_domain_create(uint32_t j, uint32_t k, uint64_t* handle);
+int h2g_domain_free(uint64_t handle);
+/* consts9 = omega, omega_inv, extended_omega, extended_omega_inv, g_coset, g_coset_inv,
+ * ifft_divisor, extended_ifft_divisor, barycentric_weight (Fr, 4 limbs each) */
+int h2g_domain_info(uint64_t handle, uint32_t* k, uint32_t* extended_k, uint64_t consts9[36]);
+/* lagrange_to_coeff (domain.rs:216-226): in place, n = 2^k */
+int h2g_lagrange_to_coeff(uint64_t dom, uint64_t* a);
+int h2g_lagrange_to_coeff_dev(uint64_t dom, void* d_a, void* stream);
+/* coeff_to_extended (domain.rs:230-244): in n, out 2^extended_k */
+int h2g_coeff_to_extended(uint64_t dom, const uint64_t* a, uint64_t* out);
+int h2g_coeff_to_extended_dev(uint64_t dom, const void* d_a, void* d_out, void* stream);
+/* extended_to_coeff (domain.rs:271-293): in 2^extended_k, out n*(j-1) (truncated) */
+int h2g_extended_to_coeff(uint64_t dom, const uint64_t* a, uint64_t* out);
+int h2g_extended_to_coeff_dev(uint64_t dom, const void* d_a, void* d_out, void* stream);
+/* divide_by_vanishing_poly (domain.rs:297-316): in place on 2^extended_k */
+int h2g_divide_by_vanishing_poly(uint64_t dom, uint64_t* a);
+int h2g_divide_by_vanishing_poly_dev(uint64_t dom, void* d_a, void* stream);
+
+/* ---- Polynomial<F, B> arithmetic (halo2_backend/src/poly.rs:200-276) ---------
+ * op: 0 add a+b, 1 sub a-b, 2 mul a*b, 3 scale a*c, 4 sub_const a-c, 5 add_const a+c,
+ *     6 axpy a*c+b.  c is a host Fr (4 limbs), ignored by ops 0-2. */
+int h2g_fr_op(int op, const uint64_t* a, const uint64_t* b, const uint64_t c[4], uint64_t* out, size_t n);
+int h2g_fr_op_dev(int op, const void* d_a, const void* d_b, const uint64_t c[4], void* d_out, size_t n,
+                  void* stream);
+/* ff::BatchInvert (zeros stay zero); permutation/prover.rs:124, lookup/prover.rs:225 */
+int h2g_fr_batch_invert(uint64_t* a, size_t n);
+int h2g_fr_batch_invert_dev(void* d_a, size_t n, void* stream);
+/* out_i = prod_{j<=i} a_j; grand products permutation/prover.rs:160-166 */
+int h2g_fr_prefix_product(const uint64_t* a, uint64_t* out, size_t n);
+int h2g_fr_prefix_product_dev(const void* d_a, void* d_out, size_t n, void* stream);
+
+/* ---- device memory / stream helpers --------------------------------------- */
+int h2g_dev_alloc(size_t bytes, void** d_ptr);
+int h2g_dev_free(void* d_ptr);
+int h2g_memcpy_htod(void* d_dst, const void* h_src, size_t bytes);
+int h2g_memcpy_dtoh(void* h_dst, const void* d_src, size_t bytes);
+int h2g_synchronize(void);
+/* elapsed time (ms) of `fn`-free timing: record events on a stream */
+int h2g_event_create(void** ev);
+int h2g_event_destroy(void* ev);
+int h2g_event_record(void* ev, void* stream);
+int h2g_event_elapsed_ms(void* start, void* stop, float* ms);
+
+/* ---- profiling: per-phase HIP-event times of MSM calls made while enabled.
+ * Phases (in order): digits, sort, bucket_bounds, accumulate, bucket_sum, reduce.
+ * collect() synchronises, returns the per-phase sums (ms) over `calls` MSMs and resets. */
+int h2g_profile_enable(int on);
+int h2g_profile_msm_collect(float* ms, int max_phases, int* n_phases, int* calls);
+
+/* ---- host-side point helpers (used to combine per-GPU MSM partials) -------- */
+int h2g_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* H2G_H */

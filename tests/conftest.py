@@ -6,6 +6,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "yet-another-halo2-fork_amd"))
 
 
 def pytest_configure(config):

@@ -1,0 +1,252 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden fixtures and
+the C restatement oracle, bit-exact (integer modular arithmetic).
+
+At sizes the oracle finishes in seconds the comparison is element-for-element;
+at BASELINE sizes (2^20..2^24) size-independent properties are used:
+  MSM  : sum_i c_i [s^i]G == [c(s)]G  (SRS structure; c(s) by the CPU oracle)
+  NTT  : ifft(fft(a)) == a, and fft(a)[j] == a(w^j) at sampled j (CPU Horner)
+"""
+import numpy as np
+import pytest
+
+import _oracle as O
+import h2g
+
+pytestmark = pytest.mark.gpu
+
+GEN = np.array([0xd35d438dc58f0d9d, 0x0a78eb28f5c70b3d, 0x666ea36f7879462c, 0x0e0a77c19a07df2f,
+                0xa6ba871b8b1e1b3a, 0x14f1d651eb8e167b, 0xccdd46def0f28c58, 0x1c14ef83340fbe5e], dtype=np.uint64)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def engine():
+    h2g.init()
+    yield
+    h2g.shutdown()
+
+
+def rng(seed=1):
+    return np.random.default_rng(seed)
+
+
+# ---------------------------------------------------------------- MSM
+def test_msm_golden_all_cases(golden):
+    g = golden["msm"]
+    for name in g["__names"]:
+        got = h2g.msm(g[f"{name}__scalars"], g[f"{name}__bases"])
+        assert np.array_equal(got, g[f"{name}__result"]), name
+
+
+def test_msm_descriptor_api(golden):
+    """MsmAccel caching API (zal.rs:83-102) == msm()."""
+    g = golden["msm"]
+    sc, bs = g["srs_random_k10__scalars"], g["srs_random_k10__bases"]
+    want = g["srs_random_k10__result"]
+    hb = h2g.base_descriptor(bs)
+    hc = h2g.coeffs_descriptor(sc)
+    try:
+        assert np.array_equal(h2g.msm_with_cached_base(sc, hb), want)
+        assert np.array_equal(h2g.msm_with_cached_scalars(hc, bs), want)
+        assert np.array_equal(h2g.msm_with_cached_inputs(hc, hb), want)
+        # prefix of a registered SRS, as commit_lagrange uses &g_lagrange[0..n]
+        n = 256
+        assert np.array_equal(h2g.msm_with_cached_base(sc[:n], hb, 0), O.msm_best(sc[:n], bs[:n], 8))
+        assert np.array_equal(h2g.msm_with_cached_base(sc[:n], hb, 100), O.msm_best(sc[:n], bs[100:100 + n], 8))
+    finally:
+        h2g.descriptor_free(hb)
+        h2g.descriptor_free(hc)
+    with pytest.raises(h2g.H2GError):
+        h2g.msm_with_cached_base(sc, 987654)
+
+
+def _srs(n, s):
+    d = h2g.DevBuf(n * 64)
+    h2g.srs_setup_dev(s, n, d.ptr)
+    return d
+
+
+def test_srs_setup_matches_golden(golden):
+    g = golden["msm"]
+    want = g["srs_random_k10__bases"]
+    d = _srs(len(want), g["srs_s"])
+    assert np.array_equal(d.download((len(want), 8)), want)
+
+
+@pytest.mark.parametrize("k", [11, 14, 16])
+def test_msm_random_vs_oracle(k):
+    r = rng(k)
+    n = 1 << k
+    s = O.random_fr(r, 1)[0]
+    bases = _srs(n, s).download((n, 8))
+    sc = O.random_fr(r, n)
+    assert np.array_equal(h2g.msm(sc, bases), O.msm_best(sc, bases, 8))
+
+
+@pytest.mark.parametrize("dist", ["ones", "small", "repeated", "sparse", "rminus1", "powers"])
+def test_msm_skewed_distributions(dist):
+    """Skewed scalars (many equal digits) exercise the big-bucket path."""
+    r = rng(7)
+    n = 1 << 13
+    s = O.random_fr(r, 1)[0]
+    bases = _srs(n, s).download((n, 8))
+    if dist == "ones":
+        sc = O.fr_from_canonical(np.tile(np.array([1, 0, 0, 0], dtype=np.uint64), (n, 1)))
+    elif dist == "small":
+        c = np.zeros((n, 4), dtype=np.uint64)
+        c[:, 0] = r.integers(0, 16, size=n).astype(np.uint64)
+        sc = O.fr_from_canonical(c)
+    elif dist == "repeated":
+        sc = np.tile(O.random_fr(r, 3), (n // 3 + 1, 1))[:n].copy()
+    elif dist == "sparse":
+        sc = O.random_fr(r, n)
+        sc[r.random(n) < 0.9] = 0
+    elif dist == "rminus1":
+        rm1 = O.fr_from_canonical(np.array([0x43e1f593f0000000, 0x2833e84879b97091, 0xb85045b68181585d,
+                                            0x30644e72e131a029], dtype=np.uint64))
+        sc = np.tile(rm1, (n, 1))
+    else:
+        c = np.zeros((n, 4), dtype=np.uint64)
+        bit = r.integers(0, 253, size=n)
+        for i, b in enumerate(bit):
+            c[i, b // 64] = np.uint64(1) << np.uint64(b % 64)
+        sc = O.fr_from_canonical(c)
+    assert np.array_equal(h2g.msm(sc, bases), O.msm_best(sc, bases, 8)), dist
+
+
+@pytest.mark.parametrize("window_bits", [4, 9, 13, 17])
+def test_msm_window_sizes(window_bits):
+    r = rng(window_bits)
+    n = 3000  # not a power of two
+    s = O.random_fr(r, 1)[0]
+    bases = _srs(n, s).download((n, 8))
+    sc = O.random_fr(r, n)
+    want = O.msm_best(sc, bases, 8)
+    dsc, dbs, dout = h2g.DevBuf.from_array(sc), h2g.DevBuf.from_array(bases), h2g.DevBuf(64)
+    h2g.msm_dev(dsc.ptr, dbs.ptr, n, dout.ptr, window_bits=window_bits)
+    assert np.array_equal(dout.download(8), want)
+
+
+@pytest.mark.parametrize("k", [20, 22])
+def test_msm_full_size_srs_identity(k):
+    """sum_i c_i [s^i] G == [c(s)] G at BASELINE sizes (no O(n) CPU MSM needed)."""
+    r = rng(100 + k)
+    n = 1 << k
+    s = O.random_fr(r, 1)[0]
+    dbs = _srs(n, s)
+    sc = O.random_fr(r, n)
+    dsc, dout = h2g.DevBuf.from_array(sc), h2g.DevBuf(64)
+    h2g.msm_dev(dsc.ptr, dbs.ptr, n, dout.ptr)
+    got = dout.download(8)
+    want = O.g1_mul(GEN, O.eval_poly(sc, s))
+    assert np.array_equal(got, want)
+
+
+# ---------------------------------------------------------------- NTT
+def test_fft_golden(golden):
+    g = golden["ntt"]
+    for name in g["__names"]:
+        got = h2g.fft(g[f"{name}__input"], g[f"{name}__omega"])
+        assert np.array_equal(got, g[f"{name}__fft"]), name
+
+
+@pytest.mark.parametrize("k", [11, 12, 13, 15, 16, 17, 18, 19, 20])
+def test_fft_random_vs_oracle(k):
+    r = rng(k)
+    a = O.random_fr(r, 1 << k)
+    _, consts, _ = O.domain_constants(2, k)
+    w = consts[0]
+    assert np.array_equal(h2g.fft(a, w), O.fft(a, w, 8)), k
+
+
+def test_domain_golden(golden):
+    g = golden["ntt"]
+    for name in g["__domains"]:
+        j, k, ek = (int(v) for v in g[f"{name}__meta"])
+        d = h2g.Domain(j, k)
+        try:
+            assert d.extended_k == ek
+            assert np.array_equal(d.consts, g[f"{name}__consts"]), name
+            assert np.array_equal(d.lagrange_to_coeff(g[f"{name}__lagrange"]), g[f"{name}__coeff"]), name
+            assert np.array_equal(d.coeff_to_extended(g[f"{name}__coeff"]), g[f"{name}__extended"]), name
+            assert np.array_equal(d.divide_by_vanishing_poly(g[f"{name}__ext_in"]), g[f"{name}__divided"]), name
+            assert np.array_equal(d.extended_to_coeff(g[f"{name}__ext_in"]), g[f"{name}__ext_to_coeff"]), name
+        finally:
+            d.close()
+
+
+@pytest.mark.parametrize("j,k", [(3, 11), (3, 14), (5, 12), (3, 18), (9, 13)])
+def test_domain_ops_vs_oracle(j, k):
+    r = rng(j * 100 + k)
+    d = h2g.Domain(j, k)
+    try:
+        lag = O.random_fr(r, 1 << k)
+        coeff = d.lagrange_to_coeff(lag)
+        assert np.array_equal(coeff, O.lagrange_to_coeff(lag, j, k, 8))
+        ext = d.coeff_to_extended(coeff)
+        assert np.array_equal(ext, O.coeff_to_extended(coeff, j, k, 8))
+        h = O.random_fr(r, d.extended_len)
+        assert np.array_equal(d.divide_by_vanishing_poly(h), O.divide_by_vanishing_poly(h, j, k))
+        assert np.array_equal(d.extended_to_coeff(h), O.extended_to_coeff(h, j, k, 8))
+        rt = d.extended_to_coeff(ext)
+        assert np.array_equal(rt[: 1 << k], coeff) and not rt[1 << k:].any()
+    finally:
+        d.close()
+
+
+@pytest.mark.parametrize("k", [22, 24])
+def test_fft_full_size_properties(k):
+    r = rng(k)
+    n = 1 << k
+    a = O.random_fr(r, n)
+    _, consts, _ = O.domain_constants(2, k)
+    w, winv = consts[0], consts[1]
+    da = h2g.DevBuf.from_array(a)
+    h2g.fft_dev(da.ptr, k, w)
+    y = da.download((n, 4))
+    # sampled evaluations y_j = a(w^j)
+    for j in [0, 1, 2, n // 2 + 3, n - 1, int(r.integers(0, n))]:
+        x = _fr_pow(w, j)  # w^j by square-and-multiply on the oracle
+        assert np.array_equal(y[j], O.eval_poly(a, x)), j
+    # inverse transform round trip (times n)
+    h2g.fft_dev(da.ptr, k, winv)
+    back = da.download((n, 4))
+    ninv = O.domain_constants(2, k)[1][6]
+    assert np.array_equal(O.scale(back, ninv), a)
+
+
+def _fr_pow(x, e):
+    acc = O.fr_from_canonical(np.array([1, 0, 0, 0], dtype=np.uint64))[0]
+    base = x.copy()
+    while e:
+        if e & 1:
+            acc = O.binop("or_fr_mul", acc.reshape(1, 4), base.reshape(1, 4))[0]
+        base = O.binop("or_fr_mul", base.reshape(1, 4), base.reshape(1, 4))[0]
+        e >>= 1
+    return acc
+
+
+# ---------------------------------------------------------------- poly ops
+def test_poly_golden(golden):
+    g = golden["poly"]
+    for name in g["__names"]:
+        a, b, x = g[f"{name}__a"], g[f"{name}__b"], g[f"{name}__x"]
+        assert np.array_equal(h2g.fr_op(h2g.OP_ADD, a, b), g[f"{name}__add"])
+        assert np.array_equal(h2g.fr_op(h2g.OP_SUB, a, b), g[f"{name}__sub"])
+        assert np.array_equal(h2g.fr_op(h2g.OP_MUL, a, b), g[f"{name}__mul"])
+        assert np.array_equal(h2g.fr_op(h2g.OP_SCALE, a, c=x), g[f"{name}__scale"])
+        assert np.array_equal(h2g.batch_invert(a), g[f"{name}__inv"])
+        assert np.array_equal(h2g.prefix_product(a), g[f"{name}__prefix_product"])
+
+
+@pytest.mark.parametrize("n", [1, 63, 4097, 1 << 16, (1 << 20) + 5])
+def test_poly_ops_vs_oracle(n):
+    r = rng(n)
+    a, b = O.random_fr(r, n), O.random_fr(r, n)
+    c = O.random_fr(r, 1)[0]
+    a[:: 7] = 0  # zeros must stay zero under batch inversion
+    assert np.array_equal(h2g.fr_op(h2g.OP_SUB_CONST, a, c=c), O.binop("or_fr_sub", a, np.tile(c, (n, 1))))
+    assert np.array_equal(h2g.fr_op(h2g.OP_ADD_CONST, a, c=c), O.binop("or_fr_add", a, np.tile(c, (n, 1))))
+    assert np.array_equal(h2g.fr_op(h2g.OP_AXPY, a, b, c), O.binop("or_fr_add", O.scale(a, c), b))
+    assert np.array_equal(h2g.batch_invert(a), O.batch_invert(a))
+    b[:: 5] = O.fr_from_canonical(np.array([1, 0, 0, 0], dtype=np.uint64))[0]
+    assert np.array_equal(h2g.prefix_product(b), O.prefix_product(b))

@@ -1,0 +1,753 @@
+// abi.cpp -- implementation of include/h2g.h (the FFI boundary).
+//
+// Host-side plumbing only: device selection, descriptor/domain handle tables,
+// grow-only device buffers for the host-pointer entry points, and argument
+// validation mirroring the reference's assertions (best_multiexp's equal
+// lengths, commit's `bases.len() >= size`, EvaluationDomain's length asserts).
+// All arithmetic runs in the HIP kernels (msm.hip, ntt.hip, poly.hip, srs.hip);
+// there is no CPU fallback: without a usable device every call fails loudly.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/h2g.h"
+#include "bn254.h"
+#include "msm.h"
+#include "ntt.h"
+#include "poly.h"
+#include "srs.h"
+
+using namespace h2g;
+
+namespace {
+
+thread_local std::string g_err;
+std::recursive_mutex g_mu;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+  return fail(H2G_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(expr)                                       \
+  do {                                                     \
+    hipError_t _e = (expr);                                \
+    if (_e != hipSuccess) return hip_fail(_e, #expr);      \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct NttKey {
+  int L;
+  uint32_t w[8];
+  bool operator<(const NttKey& o) const {
+    if (L != o.L) return L < o.L;
+    return std::memcmp(w, o.w, sizeof(w)) < 0;
+  }
+};
+
+struct Domain {
+  uint32_t j, k, ek;
+  Fr omega, omega_inv, ext_omega, ext_omega_inv, g_coset, g_coset_inv, ifft_div, ext_ifft_div, bary;
+  std::vector<Fr> t_evals;
+  Fr* d_t = nullptr;
+};
+
+struct Descriptor {
+  int device;
+  void* d = nullptr;
+  size_t n = 0;
+  bool is_base = false;
+};
+
+struct Device {
+  int id = 0;
+  hipStream_t stream = nullptr;
+  MsmWorkspace msm;
+  DevBuf a, b, c, work, out;
+  std::map<NttKey, NttTables> ntt_tables;
+};
+
+std::vector<std::unique_ptr<Device>> g_devs;
+bool g_profile = false;
+std::vector<MsmPhaseEvents> g_msm_prof;
+int g_cur = 0;
+std::map<uint64_t, Descriptor> g_desc;
+std::map<uint64_t, std::unique_ptr<Domain>> g_dom;
+uint64_t g_next_handle = 1;
+
+Device* cur() {
+  if (g_devs.empty()) return nullptr;
+  return g_devs[g_cur].get();
+}
+
+hipStream_t pick_stream(Device* d, void* s) { return s ? reinterpret_cast<hipStream_t>(s) : d->stream; }
+
+Fr fr_from_limbs(const uint64_t* v) {
+  Fr r;
+  for (int i = 0; i < 4; i++) {
+    r.l[2 * i] = (uint32_t)v[i];
+    r.l[2 * i + 1] = (uint32_t)(v[i] >> 32);
+  }
+  return r;
+}
+void fr_to_limbs(const Fr& a, uint64_t* v) {
+  for (int i = 0; i < 4; i++) v[i] = (uint64_t)a.l[2 * i] | ((uint64_t)a.l[2 * i + 1] << 32);
+}
+
+// halo2curves bn256::Fr constants (Montgomery form, 32-bit limbs) -- SURVEY A.1
+Fr root_of_unity() {
+  const uint64_t v[4] = {0x9632c7c5b639feb8ULL, 0x985ce3400d0ff299ULL, 0xb2dd880001b0ecd8ULL, 0x1d69070d6d98ce29ULL};
+  return fr_from_limbs(v);
+}
+Fr zeta() {
+  const uint64_t v[4] = {0x93e7cede4a0329b3ULL, 0x7d4fdca77a96c167ULL, 0x8be4ba08b19a750aULL, 0x1cbd5653a5661c25ULL};
+  return fr_from_limbs(v);
+}
+constexpr uint32_t FR_S = 28;
+
+int get_tables(Device* d, const Fr& omega, int L, hipStream_t st, NttTables* out) {
+  NttKey key{L, {}};
+  std::memcpy(key.w, omega.l, sizeof(key.w));
+  auto it = d->ntt_tables.find(key);
+  if (it != d->ntt_tables.end()) {
+    *out = it->second;
+    return H2G_OK;
+  }
+  NttTables t;
+  hipError_t e = ntt_build_tables(&t, omega, L, st);
+  if (e != hipSuccess) return hip_fail(e, "ntt_build_tables");
+  d->ntt_tables[key] = t;
+  *out = t;
+  return H2G_OK;
+}
+
+int msm_dev_impl(Device* d, const void* sc, const void* bs, size_t n, int c, void* out, hipStream_t st) {
+  if (n == 0) {
+    HIPCHK(hipMemsetAsync(out, 0, 64, st));
+    return H2G_OK;
+  }
+  if (n > 0x7fffffffULL) return fail(H2G_ERR_ARG, "msm: n too large");
+  MsmConfig cfg;
+  cfg.c = c;
+  MsmPhaseEvents* pe = nullptr;
+  if (g_profile) {
+    MsmPhaseEvents ev;
+    for (auto& e : ev.ev) HIPCHK(hipEventCreate(&e));
+    g_msm_prof.push_back(ev);
+    pe = &g_msm_prof.back();
+  }
+  HIPCHK(msm_run(reinterpret_cast<const Fr*>(sc), reinterpret_cast<const G1Affine*>(bs), n, &d->msm, cfg,
+                 reinterpret_cast<G1Affine*>(out), st, pe));
+  return H2G_OK;
+}
+
+int finish_host_msm(Device* d, uint64_t* out, int* is_id) {
+  HIPCHK(hipMemcpyAsync(out, d->out.p, 64, hipMemcpyDeviceToHost, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  if (is_id) {
+    uint64_t x = 0;
+    for (int i = 0; i < 8; i++) x |= out[i];
+    *is_id = x == 0;
+  }
+  return H2G_OK;
+}
+
+int ntt_dev_impl(Device* d, const Fr* src, uint64_t n_in, Fr* dst, uint64_t out_len, int L, const Fr& omega,
+                 int in_dist, const Fr& iz1, const Fr& iz2, int has_scale, const Fr& scale, int out_dist,
+                 const Fr& oz1, const Fr& oz2, hipStream_t st) {
+  NttArgs a;
+  int rc = get_tables(d, omega, L, st, &a.tab);
+  if (rc) return rc;
+  const size_t N = (size_t)1 << L;
+  if (L > NTT_SMALL_MAX_LOG) {
+    hipError_t e = d->work.ensure(N * sizeof(Fr));
+    if (e != hipSuccess) return hip_fail(e, "ntt work buffer");
+  }
+  a.src = src;
+  a.n_in = n_in;
+  a.work = reinterpret_cast<Fr*>(d->work.p);
+  a.dst = dst;
+  a.out_len = out_len;
+  a.in_distribute = in_dist;
+  a.in_z1 = iz1;
+  a.in_z2 = iz2;
+  a.has_scale = has_scale;
+  a.scale = scale;
+  a.out_distribute = out_dist;
+  a.out_z1 = oz1;
+  a.out_z2 = oz2;
+  HIPCHK(ntt_run(a, st));
+  return H2G_OK;
+}
+
+Domain* get_dom(uint64_t h) {
+  auto it = g_dom.find(h);
+  return it == g_dom.end() ? nullptr : it->second.get();
+}
+
+}  // namespace
+
+#define NEED_DEV()                                                            \
+  std::lock_guard<std::recursive_mutex> _lk(g_mu);                            \
+  Device* d = cur();                                                          \
+  if (!d) return fail(H2G_ERR_STATE, "h2g_init has not been called");         \
+  HIPCHK(hipSetDevice(d->id));
+
+extern "C" {
+
+int h2g_abi_version(void) { return 1; }
+const char* h2g_last_error(void) { return g_err.c_str(); }
+
+int h2g_init(const int* devices, int ndev) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!g_devs.empty()) return H2G_OK;
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count <= 0) return fail(H2G_ERR_DEVICE, "no HIP device available");
+  std::vector<int> ids;
+  if (!devices || ndev <= 0) ids.push_back(0);
+  else ids.assign(devices, devices + ndev);
+  for (int id : ids) {
+    if (id < 0 || id >= count) return fail(H2G_ERR_ARG, "device index out of range");
+    auto dev = std::make_unique<Device>();
+    dev->id = id;
+    HIPCHK(hipSetDevice(id));
+    HIPCHK(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
+    HIPCHK(ntt_init_attributes());
+    g_devs.push_back(std::move(dev));
+  }
+  g_cur = 0;
+  return H2G_OK;
+}
+
+int h2g_shutdown(void) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  for (auto& kv : g_desc) {
+    if (kv.second.d) (void)hipFree(kv.second.d);
+  }
+  g_desc.clear();
+  for (auto& kv : g_dom) {
+    if (kv.second->d_t) (void)hipFree(kv.second->d_t);
+  }
+  g_dom.clear();
+  for (auto& dev : g_devs) {
+    (void)hipSetDevice(dev->id);
+    (void)hipStreamSynchronize(dev->stream);
+    msm_free(&dev->msm);
+    dev->a.release();
+    dev->b.release();
+    dev->c.release();
+    dev->work.release();
+    dev->out.release();
+    for (auto& kv : dev->ntt_tables) ntt_free_tables(&kv.second);
+    (void)hipStreamDestroy(dev->stream);
+  }
+  g_devs.clear();
+  return H2G_OK;
+}
+
+int h2g_device_count(int* out) {
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+  *out = c;
+  return H2G_OK;
+}
+
+int h2g_set_device(int index) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (index < 0 || index >= (int)g_devs.size()) return fail(H2G_ERR_ARG, "device index");
+  g_cur = index;
+  return H2G_OK;
+}
+
+// ---------------------------------------------------------------- MSM
+int h2g_msm(const uint64_t* coeffs, const uint64_t* bases, size_t n, uint64_t out[8], int* is_id) {
+  NEED_DEV();
+  if (n && (!coeffs || !bases)) return fail(H2G_ERR_ARG, "msm: null input");
+  HIPCHK(d->a.ensure(n * 32 + 32));
+  HIPCHK(d->b.ensure(n * 64 + 64));
+  HIPCHK(d->out.ensure(64));
+  HIPCHK(hipMemcpyAsync(d->a.p, coeffs, n * 32, hipMemcpyHostToDevice, d->stream));
+  HIPCHK(hipMemcpyAsync(d->b.p, bases, n * 64, hipMemcpyHostToDevice, d->stream));
+  int rc = msm_dev_impl(d, d->a.p, d->b.p, n, 0, d->out.p, d->stream);
+  if (rc) return rc;
+  return finish_host_msm(d, out, is_id);
+}
+
+static int make_desc(const uint64_t* data, size_t n, size_t elem_bytes, bool is_base, uint64_t* handle) {
+  NEED_DEV();
+  if (!handle || (n && !data)) return fail(H2G_ERR_ARG, "descriptor: null argument");
+  Descriptor ds;
+  ds.device = g_cur;
+  ds.n = n;
+  ds.is_base = is_base;
+  HIPCHK(hipMalloc(&ds.d, n * elem_bytes + 64));
+  HIPCHK(hipMemcpyAsync(ds.d, data, n * elem_bytes, hipMemcpyHostToDevice, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  *handle = g_next_handle++;
+  g_desc[*handle] = ds;
+  return H2G_OK;
+}
+
+int h2g_msm_coeffs_descriptor(const uint64_t* coeffs, size_t n, uint64_t* handle) {
+  return make_desc(coeffs, n, 32, false, handle);
+}
+int h2g_msm_base_descriptor(const uint64_t* bases, size_t n, uint64_t* handle) {
+  return make_desc(bases, n, 64, true, handle);
+}
+int h2g_msm_descriptor_free(uint64_t handle) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  auto it = g_desc.find(handle);
+  if (it == g_desc.end()) return fail(H2G_ERR_HANDLE, "unknown descriptor");
+  if (it->second.d) (void)hipFree(it->second.d);
+  g_desc.erase(it);
+  return H2G_OK;
+}
+int h2g_descriptor_device_ptr(uint64_t handle, void** d_ptr, size_t* n) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  auto it = g_desc.find(handle);
+  if (it == g_desc.end()) return fail(H2G_ERR_HANDLE, "unknown descriptor");
+  if (d_ptr) *d_ptr = it->second.d;
+  if (n) *n = it->second.n;
+  return H2G_OK;
+}
+
+int h2g_msm_with_cached_scalars(uint64_t coeffs, const uint64_t* bases, size_t n, uint64_t out[8], int* is_id) {
+  NEED_DEV();
+  auto it = g_desc.find(coeffs);
+  if (it == g_desc.end() || it->second.is_base) return fail(H2G_ERR_HANDLE, "unknown coeffs descriptor");
+  if (it->second.n != n) return fail(H2G_ERR_ARG, "msm: coeffs.len() != bases.len()");
+  HIPCHK(d->b.ensure(n * 64 + 64));
+  HIPCHK(d->out.ensure(64));
+  HIPCHK(hipMemcpyAsync(d->b.p, bases, n * 64, hipMemcpyHostToDevice, d->stream));
+  int rc = msm_dev_impl(d, it->second.d, d->b.p, n, 0, d->out.p, d->stream);
+  if (rc) return rc;
+  return finish_host_msm(d, out, is_id);
+}
+
+int h2g_msm_with_cached_base(const uint64_t* coeffs, size_t n, uint64_t base, size_t off, uint64_t out[8],
+                             int* is_id) {
+  NEED_DEV();
+  auto it = g_desc.find(base);
+  if (it == g_desc.end() || !it->second.is_base) return fail(H2G_ERR_HANDLE, "unknown base descriptor");
+  if (off + n > it->second.n) return fail(H2G_ERR_ARG, "msm: bases.len() < size");
+  HIPCHK(d->a.ensure(n * 32 + 32));
+  HIPCHK(d->out.ensure(64));
+  HIPCHK(hipMemcpyAsync(d->a.p, coeffs, n * 32, hipMemcpyHostToDevice, d->stream));
+  int rc = msm_dev_impl(d, d->a.p, (const char*)it->second.d + off * 64, n, 0, d->out.p, d->stream);
+  if (rc) return rc;
+  return finish_host_msm(d, out, is_id);
+}
+
+int h2g_msm_with_cached_inputs(uint64_t coeffs, uint64_t base, size_t off, uint64_t out[8], int* is_id) {
+  NEED_DEV();
+  auto ic = g_desc.find(coeffs);
+  auto ib = g_desc.find(base);
+  if (ic == g_desc.end() || ic->second.is_base) return fail(H2G_ERR_HANDLE, "unknown coeffs descriptor");
+  if (ib == g_desc.end() || !ib->second.is_base) return fail(H2G_ERR_HANDLE, "unknown base descriptor");
+  const size_t n = ic->second.n;
+  if (off + n > ib->second.n) return fail(H2G_ERR_ARG, "msm: bases.len() < size");
+  HIPCHK(d->out.ensure(64));
+  int rc = msm_dev_impl(d, ic->second.d, (const char*)ib->second.d + off * 64, n, 0, d->out.p, d->stream);
+  if (rc) return rc;
+  return finish_host_msm(d, out, is_id);
+}
+
+int h2g_msm_dev(const void* sc, const void* bs, size_t n, void* out, void* stream) {
+  return h2g_msm_dev_cfg(sc, bs, n, 0, out, stream);
+}
+
+int h2g_msm_dev_cfg(const void* sc, const void* bs, size_t n, int c, void* out, void* stream) {
+  NEED_DEV();
+  if (!out || (n && (!sc || !bs))) return fail(H2G_ERR_ARG, "msm_dev: null pointer");
+  if (c < 0 || c > 24) return fail(H2G_ERR_ARG, "msm_dev: window_bits out of range");
+  return msm_dev_impl(d, sc, bs, n, c, out, pick_stream(d, stream));
+}
+
+int h2g_srs_setup_dev(const uint64_t s[4], size_t n, void* d_out, void* stream) {
+  NEED_DEV();
+  if (!s || (n && !d_out)) return fail(H2G_ERR_ARG, "srs: null pointer");
+  HIPCHK(srs_setup(fr_from_limbs(s), n, reinterpret_cast<G1Affine*>(d_out), pick_stream(d, stream)));
+  return H2G_OK;
+}
+
+// ---------------------------------------------------------------- FFT
+int h2g_fft_dev(void* a, uint32_t log_n, const uint64_t omega[4], void* stream) {
+  NEED_DEV();
+  if (!a || !omega || log_n > FR_S) return fail(H2G_ERR_ARG, "fft: bad argument");
+  const Fr w = fr_from_limbs(omega);
+  const Fr one = Fr::one();
+  const uint64_t N = 1ull << log_n;
+  return ntt_dev_impl(d, (const Fr*)a, N, (Fr*)a, N, (int)log_n, w, 0, one, one, 0, one, 0, one, one,
+                      pick_stream(d, stream));
+}
+
+int h2g_fft(uint64_t* a, uint32_t log_n, const uint64_t omega[4]) {
+  NEED_DEV();
+  if (!a || !omega || log_n > FR_S) return fail(H2G_ERR_ARG, "fft: bad argument");
+  const size_t bytes = ((size_t)1 << log_n) * 32;
+  HIPCHK(d->a.ensure(bytes));
+  HIPCHK(hipMemcpyAsync(d->a.p, a, bytes, hipMemcpyHostToDevice, d->stream));
+  int rc = h2g_fft_dev(d->a.p, log_n, omega, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(a, d->a.p, bytes, hipMemcpyDeviceToHost, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return H2G_OK;
+}
+
+// ---------------------------------------------------------------- EvaluationDomain
+int h2g_domain_create(uint32_t j, uint32_t k, uint64_t* handle) {
+  NEED_DEV();
+  if (!handle || j < 2 || k > FR_S) return fail(H2G_ERR_ARG, "domain: bad j/k");
+  auto dm = std::make_unique<Domain>();
+  dm->j = j;
+  dm->k = k;
+  const uint64_t n = 1ull << k;
+  const uint64_t qdeg = j - 1;
+  uint32_t ek = k;
+  while ((1ull << ek) < n * qdeg) ek++;
+  if (ek > FR_S) return fail(H2G_ERR_ARG, "domain: extended_k > S");
+  dm->ek = ek;
+  Fr eo = root_of_unity();
+  for (uint32_t i = ek; i < FR_S; i++) eo = sqr(eo);
+  Fr o = eo;
+  for (uint32_t i = k; i < ek; i++) o = sqr(o);
+  dm->ext_omega = eo;
+  dm->omega = o;
+  dm->g_coset = zeta();
+  dm->g_coset_inv = sqr(dm->g_coset);
+  const uint64_t tlen = 1ull << (ek - k);
+  const Fr orig = pow_u64(dm->g_coset, n), step = pow_u64(eo, n);
+  Fr cur = orig;
+  dm->t_evals.resize(tlen);
+  for (uint64_t i = 0; i < tlen; i++) {
+    dm->t_evals[i] = inv(cur - Fr::one());
+    cur = cur * step;
+  }
+  dm->ifft_div = inv(from_u64<FrParams>(n));
+  dm->ext_ifft_div = inv(from_u64<FrParams>(1ull << ek));
+  dm->bary = inv(from_u64<FrParams>(n));
+  dm->ext_omega_inv = inv(eo);
+  dm->omega_inv = inv(o);
+  HIPCHK(hipMalloc(&dm->d_t, tlen * sizeof(Fr)));
+  HIPCHK(hipMemcpy(dm->d_t, dm->t_evals.data(), tlen * sizeof(Fr), hipMemcpyHostToDevice));
+  *handle = g_next_handle++;
+  g_dom[*handle] = std::move(dm);
+  return H2G_OK;
+}
+
+int h2g_domain_free(uint64_t handle) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  auto it = g_dom.find(handle);
+  if (it == g_dom.end()) return fail(H2G_ERR_HANDLE, "unknown domain");
+  if (it->second->d_t) (void)hipFree(it->second->d_t);
+  g_dom.erase(it);
+  return H2G_OK;
+}
+
+int h2g_domain_info(uint64_t handle, uint32_t* k, uint32_t* ek, uint64_t consts[36]) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  Domain* dm = get_dom(handle);
+  if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
+  if (k) *k = dm->k;
+  if (ek) *ek = dm->ek;
+  if (consts) {
+    const Fr c[9] = {dm->omega, dm->omega_inv, dm->ext_omega, dm->ext_omega_inv, dm->g_coset,
+                     dm->g_coset_inv, dm->ifft_div, dm->ext_ifft_div, dm->bary};
+    for (int i = 0; i < 9; i++) fr_to_limbs(c[i], consts + 4 * i);
+  }
+  return H2G_OK;
+}
+
+int h2g_lagrange_to_coeff_dev(uint64_t dom, void* a, void* stream) {
+  NEED_DEV();
+  Domain* dm = get_dom(dom);
+  if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
+  if (!a) return fail(H2G_ERR_ARG, "null");
+  const Fr one = Fr::one();
+  const uint64_t n = 1ull << dm->k;
+  return ntt_dev_impl(d, (const Fr*)a, n, (Fr*)a, n, (int)dm->k, dm->omega_inv, 0, one, one, 1, dm->ifft_div, 0,
+                      one, one, pick_stream(d, stream));
+}
+
+int h2g_coeff_to_extended_dev(uint64_t dom, const void* a, void* out, void* stream) {
+  NEED_DEV();
+  Domain* dm = get_dom(dom);
+  if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
+  if (!a || !out) return fail(H2G_ERR_ARG, "null");
+  if (a == out) return fail(H2G_ERR_ARG, "coeff_to_extended: in and out must differ");
+  const Fr one = Fr::one();
+  const uint64_t n = 1ull << dm->k, ext = 1ull << dm->ek;
+  return ntt_dev_impl(d, (const Fr*)a, n, (Fr*)out, ext, (int)dm->ek, dm->ext_omega, 1, dm->g_coset,
+                      dm->g_coset_inv, 0, one, 0, one, one, pick_stream(d, stream));
+}
+
+int h2g_extended_to_coeff_dev(uint64_t dom, const void* a, void* out, void* stream) {
+  NEED_DEV();
+  Domain* dm = get_dom(dom);
+  if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
+  if (!a || !out) return fail(H2G_ERR_ARG, "null");
+  const Fr one = Fr::one();
+  const uint64_t ext = 1ull << dm->ek;
+  const uint64_t out_len = (1ull << dm->k) * (dm->j - 1);
+  // inverse FFT, * 1/2^ek, then distribute_powers_zeta(into_coset = false): [zeta^2, zeta]
+  return ntt_dev_impl(d, (const Fr*)a, ext, (Fr*)out, out_len, (int)dm->ek, dm->ext_omega_inv, 0, one, one, 1,
+                      dm->ext_ifft_div, 1, dm->g_coset_inv, dm->g_coset, pick_stream(d, stream));
+}
+
+int h2g_divide_by_vanishing_poly_dev(uint64_t dom, void* a, void* stream) {
+  NEED_DEV();
+  Domain* dm = get_dom(dom);
+  if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
+  if (!a) return fail(H2G_ERR_ARG, "null");
+  HIPCHK(poly_mul_cyclic((Fr*)a, 1ull << dm->ek, dm->d_t, dm->t_evals.size(), pick_stream(d, stream)));
+  return H2G_OK;
+}
+
+// host-pointer domain wrappers
+static int host_roundtrip(size_t in_elems, const uint64_t* in, size_t out_elems, uint64_t* out,
+                          int (*fn)(uint64_t, const void*, void*, void*), uint64_t dom) {
+  NEED_DEV();
+  HIPCHK(d->b.ensure(in_elems * 32 + 32));
+  HIPCHK(d->c.ensure(out_elems * 32 + 32));
+  HIPCHK(hipMemcpyAsync(d->b.p, in, in_elems * 32, hipMemcpyHostToDevice, d->stream));
+  int rc = fn(dom, d->b.p, d->c.p, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(out, d->c.p, out_elems * 32, hipMemcpyDeviceToHost, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return H2G_OK;
+}
+
+int h2g_lagrange_to_coeff(uint64_t dom, uint64_t* a) {
+  NEED_DEV();
+  Domain* dm = get_dom(dom);
+  if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
+  const size_t n = 1ull << dm->k;
+  HIPCHK(d->b.ensure(n * 32));
+  HIPCHK(hipMemcpyAsync(d->b.p, a, n * 32, hipMemcpyHostToDevice, d->stream));
+  int rc = h2g_lagrange_to_coeff_dev(dom, d->b.p, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(a, d->b.p, n * 32, hipMemcpyDeviceToHost, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return H2G_OK;
+}
+
+int h2g_coeff_to_extended(uint64_t dom, const uint64_t* a, uint64_t* out) {
+  Domain* dm;
+  {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    dm = get_dom(dom);
+    if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
+  }
+  return host_roundtrip(1ull << dm->k, a, 1ull << dm->ek, out, h2g_coeff_to_extended_dev, dom);
+}
+
+int h2g_extended_to_coeff(uint64_t dom, const uint64_t* a, uint64_t* out) {
+  Domain* dm;
+  {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    dm = get_dom(dom);
+    if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
+  }
+  return host_roundtrip(1ull << dm->ek, a, (1ull << dm->k) * (dm->j - 1), out, h2g_extended_to_coeff_dev, dom);
+}
+
+int h2g_divide_by_vanishing_poly(uint64_t dom, uint64_t* a) {
+  NEED_DEV();
+  Domain* dm = get_dom(dom);
+  if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
+  const size_t n = 1ull << dm->ek;
+  HIPCHK(d->b.ensure(n * 32));
+  HIPCHK(hipMemcpyAsync(d->b.p, a, n * 32, hipMemcpyHostToDevice, d->stream));
+  int rc = h2g_divide_by_vanishing_poly_dev(dom, d->b.p, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(a, d->b.p, n * 32, hipMemcpyDeviceToHost, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return H2G_OK;
+}
+
+// ---------------------------------------------------------------- poly ops
+int h2g_fr_op_dev(int op, const void* a, const void* b, const uint64_t c[4], void* out, size_t n, void* stream) {
+  NEED_DEV();
+  if (op < 0 || op > 6) return fail(H2G_ERR_ARG, "fr_op: unknown op");
+  if (n && (!a || !out || ((op <= 2 || op == 6) && !b) || (op >= 3 && !c)))
+    return fail(H2G_ERR_ARG, "fr_op: null pointer");
+  hipStream_t st = pick_stream(d, stream);
+  const Fr cv = op >= 3 ? fr_from_limbs(c) : Fr::zero();
+  HIPCHK(poly_binop(op, (const Fr*)a, (const Fr*)b, cv, (Fr*)out, n, st));
+  return H2G_OK;
+}
+
+int h2g_fr_op(int op, const uint64_t* a, const uint64_t* b, const uint64_t c[4], uint64_t* out, size_t n) {
+  NEED_DEV();
+  HIPCHK(d->a.ensure(n * 32 + 32));
+  HIPCHK(d->b.ensure(n * 32 + 32));
+  HIPCHK(d->c.ensure(n * 32 + 32));
+  HIPCHK(hipMemcpyAsync(d->a.p, a, n * 32, hipMemcpyHostToDevice, d->stream));
+  if (b) HIPCHK(hipMemcpyAsync(d->b.p, b, n * 32, hipMemcpyHostToDevice, d->stream));
+  int rc = h2g_fr_op_dev(op, d->a.p, b ? d->b.p : nullptr, c, d->c.p, n, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(out, d->c.p, n * 32, hipMemcpyDeviceToHost, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return H2G_OK;
+}
+
+int h2g_fr_batch_invert_dev(void* a, size_t n, void* stream) {
+  NEED_DEV();
+  if (n && !a) return fail(H2G_ERR_ARG, "null");
+  HIPCHK(d->work.ensure(n * 32 + 32));
+  HIPCHK(poly_batch_invert((Fr*)a, n, (Fr*)d->work.p, pick_stream(d, stream)));
+  return H2G_OK;
+}
+
+int h2g_fr_batch_invert(uint64_t* a, size_t n) {
+  NEED_DEV();
+  HIPCHK(d->a.ensure(n * 32 + 32));
+  HIPCHK(hipMemcpyAsync(d->a.p, a, n * 32, hipMemcpyHostToDevice, d->stream));
+  int rc = h2g_fr_batch_invert_dev(d->a.p, n, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(a, d->a.p, n * 32, hipMemcpyDeviceToHost, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return H2G_OK;
+}
+
+int h2g_fr_prefix_product_dev(const void* a, void* out, size_t n, void* stream) {
+  NEED_DEV();
+  if (n && (!a || !out)) return fail(H2G_ERR_ARG, "null");
+  const size_t sl = poly_prefix_scratch_len(n);
+  HIPCHK(d->work.ensure(sl * 32 + 32));
+  HIPCHK(poly_prefix_product((const Fr*)a, (Fr*)out, n, (Fr*)d->work.p, sl, pick_stream(d, stream)));
+  return H2G_OK;
+}
+
+int h2g_fr_prefix_product(const uint64_t* a, uint64_t* out, size_t n) {
+  NEED_DEV();
+  HIPCHK(d->a.ensure(n * 32 + 32));
+  HIPCHK(d->c.ensure(n * 32 + 32));
+  HIPCHK(hipMemcpyAsync(d->a.p, a, n * 32, hipMemcpyHostToDevice, d->stream));
+  int rc = h2g_fr_prefix_product_dev(d->a.p, d->c.p, n, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(out, d->c.p, n * 32, hipMemcpyDeviceToHost, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  return H2G_OK;
+}
+
+// ---------------------------------------------------------------- memory / events
+int h2g_dev_alloc(size_t bytes, void** p) {
+  NEED_DEV();
+  HIPCHK(hipMalloc(p, bytes ? bytes : 16));
+  return H2G_OK;
+}
+int h2g_dev_free(void* p) {
+  NEED_DEV();
+  HIPCHK(hipFree(p));
+  return H2G_OK;
+}
+int h2g_memcpy_htod(void* dst, const void* src, size_t bytes) {
+  NEED_DEV();
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+  return H2G_OK;
+}
+int h2g_memcpy_dtoh(void* dst, const void* src, size_t bytes) {
+  NEED_DEV();
+  HIPCHK(hipStreamSynchronize(d->stream));
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+  return H2G_OK;
+}
+int h2g_synchronize(void) {
+  NEED_DEV();
+  HIPCHK(hipStreamSynchronize(d->stream));
+  HIPCHK(hipDeviceSynchronize());
+  return H2G_OK;
+}
+int h2g_event_create(void** ev) {
+  NEED_DEV();
+  hipEvent_t e;
+  HIPCHK(hipEventCreate(&e));
+  *ev = e;
+  return H2G_OK;
+}
+int h2g_event_destroy(void* ev) {
+  NEED_DEV();
+  HIPCHK(hipEventDestroy((hipEvent_t)ev));
+  return H2G_OK;
+}
+int h2g_event_record(void* ev, void* stream) {
+  NEED_DEV();
+  HIPCHK(hipEventRecord((hipEvent_t)ev, pick_stream(d, stream)));
+  return H2G_OK;
+}
+int h2g_event_elapsed_ms(void* a, void* b, float* ms) {
+  NEED_DEV();
+  HIPCHK(hipEventSynchronize((hipEvent_t)b));
+  HIPCHK(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b));
+  return H2G_OK;
+}
+
+// ---------------------------------------------------------------- profiling
+int h2g_profile_enable(int on) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  g_profile = on != 0;
+  return H2G_OK;
+}
+
+int h2g_profile_msm_collect(float* ms, int max_phases, int* n_phases, int* calls) {
+  NEED_DEV();
+  const int np = MSM_NPHASES < max_phases ? MSM_NPHASES : max_phases;
+  for (int i = 0; i < np; i++) ms[i] = 0.f;
+  for (auto& pe : g_msm_prof) {
+    HIPCHK(hipEventSynchronize(pe.ev[MSM_NPHASES]));
+    for (int i = 0; i < np; i++) {
+      float t = 0.f;
+      HIPCHK(hipEventElapsedTime(&t, pe.ev[i], pe.ev[i + 1]));
+      ms[i] += t;
+    }
+  }
+  if (calls) *calls = (int)g_msm_prof.size();
+  if (n_phases) *n_phases = np;
+  for (auto& pe : g_msm_prof)
+    for (auto& e : pe.ev) (void)hipEventDestroy(e);
+  g_msm_prof.clear();
+  return H2G_OK;
+}
+
+// ---------------------------------------------------------------- host point helper
+int h2g_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]) {
+  G1Affine pa, pb;
+  std::memcpy(&pa, a, 64);
+  std::memcpy(&pb, b, 64);
+  const G1xyzz s = xyzz_madd(G1xyzz::from_affine(pa), pb);
+  const G1Affine r = xyzz_to_affine(s);
+  std::memcpy(out, &r, 64);
+  return H2G_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,382 @@
+// bn254.h -- BN254 Fr/Fq Montgomery arithmetic and G1 group law for gfx950.
+//
+// 8 x 32-bit little-endian limbs, Montgomery form with R = 2^256: bit-for-bit
+// the halo2curves 0.6 in-memory layout (4 x u64 LE limbs), so host slices of
+// Fr / G1Affine are consumed and produced with no conversion pass.
+// All values are kept fully reduced (< modulus); equality is limb equality.
+//
+// The same code compiles for the host (used only for O(1) glue such as
+// combining per-GPU MSM partials and constants) and for the device.
+//
+// Limb arithmetic is written for the CDNA4 VALU: 32x32->64 products map onto
+// v_mad_u64_u32, carry chains onto v_add_co_u32 / v_addc_co_u32.  No MFMA is
+// involved (integer modular arithmetic, not a floating-point contraction).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define H2G_HD __host__ __device__ __forceinline__
+
+namespace h2g {
+
+struct FrParams {
+  static constexpr uint32_t M[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t INV = 0xefffffffu;  // -M^-1 mod 2^32
+  static constexpr uint32_t ONE[8] = {0x4ffffffbu, 0xac96341cu, 0x9f60cd29u, 0x36fc7695u,
+                                      0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
+                                     0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+};
+struct FqParams {
+  static constexpr uint32_t M[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
+                                    0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr uint32_t INV = 0xe4866389u;
+  static constexpr uint32_t ONE[8] = {0xc58f0d9du, 0xd35d438du, 0xf5c70b3du, 0x0a78eb28u,
+                                      0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr uint32_t R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
+                                     0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
+};
+
+template <class P>
+struct Fe {
+  uint32_t l[8];
+
+  H2G_HD static Fe zero() {
+    Fe r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.l[i] = 0;
+    return r;
+  }
+  H2G_HD static Fe one() {
+    Fe r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.l[i] = P::ONE[i];
+    return r;
+  }
+  H2G_HD bool is_zero() const {
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) x |= l[i];
+    return x == 0;
+  }
+  H2G_HD bool operator==(const Fe& o) const {
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) x |= l[i] ^ o.l[i];
+    return x == 0;
+  }
+  H2G_HD bool operator!=(const Fe& o) const { return !(*this == o); }
+};
+
+using Fr = Fe<FrParams>;
+using Fq = Fe<FqParams>;
+
+// ---------------------------------------------------------------- add / sub
+template <class P>
+H2G_HD Fe<P> operator+(const Fe<P>& a, const Fe<P>& b) {
+  Fe<P> s, d;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c += (uint64_t)a.l[i] + b.l[i];
+    s.l[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  // a + b < 2M < 2^255: no carry out; subtract M, keep if no borrow
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    int64_t t = (int64_t)s.l[i] - P::M[i] + br;
+    d.l[i] = (uint32_t)t;
+    br = t >> 32;
+  }
+  return br ? s : d;
+}
+
+template <class P>
+H2G_HD Fe<P> operator-(const Fe<P>& a, const Fe<P>& b) {
+  Fe<P> d, s;
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    int64_t t = (int64_t)a.l[i] - b.l[i] + br;
+    d.l[i] = (uint32_t)t;
+    br = t >> 32;
+  }
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c += (uint64_t)d.l[i] + P::M[i];
+    s.l[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  return br ? s : d;
+}
+
+template <class P>
+H2G_HD Fe<P> neg(const Fe<P>& a) {
+  return Fe<P>::zero() - a;
+}
+template <class P>
+H2G_HD Fe<P> dbl(const Fe<P>& a) {
+  return a + a;
+}
+
+// ---------------------------------------------------------------- Montgomery multiply
+// CIOS with the "no final carry" shortcut (top modulus limb < 2^31 - 1 for both
+// BN254 moduli), 32-bit limbs.  Returns a*b*2^-256 mod M, fully reduced.
+template <class P>
+H2G_HD Fe<P> operator*(const Fe<P>& a, const Fe<P>& b) {
+  uint32_t t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t bi = b.l[i];
+    uint64_t x = (uint64_t)a.l[0] * bi + t[0];
+    uint32_t A = (uint32_t)(x >> 32);
+    const uint32_t t0 = (uint32_t)x;
+    const uint32_t m = t0 * P::INV;
+    uint64_t y = (uint64_t)m * P::M[0] + t0;
+    uint32_t C = (uint32_t)(y >> 32);
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      x = (uint64_t)a.l[j] * bi + t[j] + A;
+      A = (uint32_t)(x >> 32);
+      y = (uint64_t)m * P::M[j] + (uint32_t)x + C;
+      C = (uint32_t)(y >> 32);
+      t[j - 1] = (uint32_t)y;
+    }
+    t[7] = C + A;
+  }
+  Fe<P> r, d;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = t[i];
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    int64_t u = (int64_t)r.l[i] - P::M[i] + br;
+    d.l[i] = (uint32_t)u;
+    br = u >> 32;
+  }
+  return br ? r : d;
+}
+
+template <class P>
+H2G_HD Fe<P> sqr(const Fe<P>& a) {
+  return a * a;
+}
+
+// Montgomery -> canonical integer (little-endian limbs): a * 1 * 2^-256.
+template <class P>
+H2G_HD Fe<P> to_canonical(const Fe<P>& a) {
+  Fe<P> one = Fe<P>::zero();
+  one.l[0] = 1;
+  return a * one;
+}
+template <class P>
+H2G_HD Fe<P> from_canonical(const Fe<P>& a) {
+  Fe<P> r2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r2.l[i] = P::R2[i];
+  return a * r2;
+}
+template <class P>
+H2G_HD Fe<P> from_u64(uint64_t v) {
+  Fe<P> c = Fe<P>::zero();
+  c.l[0] = (uint32_t)v;
+  c.l[1] = (uint32_t)(v >> 32);
+  return from_canonical(c);
+}
+
+// a^e, e given as 8 little-endian 32-bit limbs (vartime in e; e is public).
+template <class P>
+H2G_HD Fe<P> pow_limbs(const Fe<P>& a, const uint32_t e[8]) {
+  Fe<P> acc = Fe<P>::one();
+  for (int i = 7; i >= 0; i--)
+    for (int b = 31; b >= 0; b--) {
+      acc = sqr(acc);
+      if ((e[i] >> b) & 1) acc = acc * a;
+    }
+  return acc;
+}
+template <class P>
+H2G_HD Fe<P> pow_u64(const Fe<P>& a, uint64_t e) {
+  Fe<P> acc = Fe<P>::one();
+  for (int b = 63; b >= 0; b--) {
+    acc = sqr(acc);
+    if ((e >> b) & 1) acc = acc * a;
+  }
+  return acc;
+}
+// Fermat inversion; inv(0) = 0 (matches ff's invert().unwrap_or(ZERO) use in batch_invert).
+template <class P>
+H2G_HD Fe<P> inv(const Fe<P>& a) {
+  uint32_t e[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) e[i] = P::M[i];
+  e[0] -= 2;
+  return pow_limbs(a, e);
+}
+
+// ---------------------------------------------------------------- G1 (y^2 = x^3 + 3 over Fq)
+
+struct G1Affine {  // halo2curves layout; identity = (0, 0)
+  Fq x, y;
+  H2G_HD bool is_identity() const { return x.is_zero() && y.is_zero(); }
+};
+
+// Extended Jacobian "XYZZ": x = X/ZZ, y = Y/ZZZ, ZZ^3 = ZZZ^2; identity: ZZ = 0.
+struct G1xyzz {
+  Fq X, Y, ZZ, ZZZ;
+  H2G_HD static G1xyzz identity() {
+    G1xyzz r;
+    r.X = Fq::one();
+    r.Y = Fq::one();
+    r.ZZ = Fq::zero();
+    r.ZZZ = Fq::zero();
+    return r;
+  }
+  H2G_HD bool is_identity() const { return ZZ.is_zero(); }
+  H2G_HD static G1xyzz from_affine(const G1Affine& a) {
+    if (a.is_identity()) return identity();
+    G1xyzz r;
+    r.X = a.x;
+    r.Y = a.y;
+    r.ZZ = Fq::one();
+    r.ZZZ = Fq::one();
+    return r;
+  }
+};
+
+// dbl-2008-s-1 (a = 0)
+H2G_HD G1xyzz xyzz_dbl(const G1xyzz& p) {
+  if (p.is_identity()) return p;
+  const Fq U = dbl(p.Y);
+  const Fq V = sqr(U);
+  const Fq W = U * V;
+  const Fq S = p.X * V;
+  const Fq X2 = sqr(p.X);
+  const Fq M = X2 + dbl(X2);
+  G1xyzz r;
+  r.X = sqr(M) - dbl(S);
+  r.Y = M * (S - r.X) - W * p.Y;
+  r.ZZ = V * p.ZZ;
+  r.ZZZ = W * p.ZZZ;
+  return r;
+}
+
+// mdbl-2008-s-1: double an affine point (not identity)
+H2G_HD G1xyzz xyzz_mdbl(const G1Affine& a) {
+  const Fq U = dbl(a.y);
+  const Fq V = sqr(U);
+  const Fq W = U * V;
+  const Fq S = a.x * V;
+  const Fq X2 = sqr(a.x);
+  const Fq M = X2 + dbl(X2);
+  G1xyzz r;
+  r.X = sqr(M) - dbl(S);
+  r.Y = M * (S - r.X) - W * a.y;
+  r.ZZ = V;
+  r.ZZZ = W;
+  return r;
+}
+
+// madd-2008-s: p + affine q
+H2G_HD G1xyzz xyzz_madd(const G1xyzz& p, const G1Affine& q) {
+  if (q.is_identity()) return p;
+  if (p.is_identity()) return G1xyzz::from_affine(q);
+  const Fq U2 = q.x * p.ZZ;
+  const Fq S2 = q.y * p.ZZZ;
+  const Fq Pp = U2 - p.X;
+  const Fq R = S2 - p.Y;
+  if (Pp.is_zero()) {
+    if (R.is_zero()) return xyzz_mdbl(q);
+    return G1xyzz::identity();
+  }
+  const Fq PP = sqr(Pp);
+  const Fq PPP = Pp * PP;
+  const Fq Q = p.X * PP;
+  G1xyzz r;
+  r.X = sqr(R) - PPP - dbl(Q);
+  r.Y = R * (Q - r.X) - p.Y * PPP;
+  r.ZZ = p.ZZ * PP;
+  r.ZZZ = p.ZZZ * PPP;
+  return r;
+}
+
+// add-2008-s: p + q
+H2G_HD G1xyzz xyzz_add(const G1xyzz& p, const G1xyzz& q) {
+  if (q.is_identity()) return p;
+  if (p.is_identity()) return q;
+  const Fq U1 = p.X * q.ZZ;
+  const Fq U2 = q.X * p.ZZ;
+  const Fq S1 = p.Y * q.ZZZ;
+  const Fq S2 = q.Y * p.ZZZ;
+  const Fq Pp = U2 - U1;
+  const Fq R = S2 - S1;
+  if (Pp.is_zero()) {
+    if (R.is_zero()) return xyzz_dbl(p);
+    return G1xyzz::identity();
+  }
+  const Fq PP = sqr(Pp);
+  const Fq PPP = Pp * PP;
+  const Fq Q = U1 * PP;
+  G1xyzz r;
+  r.X = sqr(R) - PPP - dbl(Q);
+  r.Y = R * (Q - r.X) - S1 * PPP;
+  r.ZZ = p.ZZ * q.ZZ * PP;
+  r.ZZZ = p.ZZZ * q.ZZZ * PPP;
+  return r;
+}
+
+H2G_HD G1xyzz xyzz_neg(const G1xyzz& p) {
+  G1xyzz r = p;
+  r.Y = neg(p.Y);
+  return r;
+}
+
+H2G_HD G1Affine affine_neg(const G1Affine& a) {
+  G1Affine r = a;
+  if (!a.is_identity()) r.y = neg(a.y);
+  return r;
+}
+
+H2G_HD G1Affine xyzz_to_affine(const G1xyzz& p) {
+  G1Affine r;
+  if (p.is_identity()) {
+    r.x = Fq::zero();
+    r.y = Fq::zero();
+    return r;
+  }
+  const Fq i = inv(p.ZZ * p.ZZZ);  // 1/(ZZ*ZZZ)
+  const Fq izz = i * p.ZZZ;        // 1/ZZ
+  const Fq izzz = i * p.ZZ;        // 1/ZZZ
+  r.x = p.X * izz;
+  r.y = p.Y * izzz;
+  return r;
+}
+
+// [k] P for a small unsigned k (double-and-add, MSB first)
+H2G_HD G1xyzz xyzz_mul_u32(const G1xyzz& p, uint32_t k) {
+  G1xyzz acc = G1xyzz::identity();
+  for (int b = 31; b >= 0; b--) {
+    acc = xyzz_dbl(acc);
+    if ((k >> b) & 1) acc = xyzz_add(acc, p);
+  }
+  return acc;
+}
+
+// [s] P for a full canonical scalar s (8 LE limbs)
+H2G_HD G1xyzz xyzz_mul_canonical(const G1xyzz& p, const uint32_t s[8]) {
+  G1xyzz acc = G1xyzz::identity();
+  for (int i = 7; i >= 0; i--)
+    for (int b = 31; b >= 0; b--) {
+      acc = xyzz_dbl(acc);
+      if ((s[i] >> b) & 1) acc = xyzz_add(acc, p);
+    }
+  return acc;
+}
+
+}  // namespace h2g

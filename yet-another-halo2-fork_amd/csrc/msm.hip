@@ -1,0 +1,369 @@
+// msm.hip -- Pippenger multi-scalar multiplication over BN254 G1 for gfx950.
+//
+// Computes MsmAccel::msm(coeffs, bases) = sum_i coeffs[i] * bases[i]
+// (halo2_middleware/src/zal.rs:58; CPU reference halo2curves best_multiexp,
+// zal.rs:136-138) for the commitment call sites listed in SURVEY 8a-1.
+//
+// Pipeline (one stream, no host round trips):
+//   1. digits     : Montgomery -> canonical, signed c-bit windows (|d| <= 2^(c-1)),
+//                   key = window*NB + |d|-1, value = point index | sign << 31
+//   2. sort       : LSD radix sort of (key, value) over the key bits (rocprim)
+//   3. bounds     : bucket [start, end) from the sorted keys
+//   4. items      : buckets split into work items of <= item_len points
+//                   (load balance for skewed scalar distributions)
+//   5. accumulate : one thread per item, XYZZ += affine (madd-2008-s), with the
+//                   bases gathered by sorted index (64 B per point read)
+//   6. bucket sum : per bucket, sum its item partials
+//   7. segments   : per (window, segment of SEG buckets) running sums
+//                   sum_j (j+1) B_j = S_local + offset * R
+//   8. windows    : per window tree reduction of segment results in LDS
+//   9. final      : Horner over windows (c doublings each), to affine
+// The result is the unique affine point, so it is bit-identical to any other
+// correct MSM (e.g. the CPU restatement in oracle/) regardless of summation order.
+#include <hipcub/hipcub.hpp>
+
+#include "msm.h"
+
+namespace h2g {
+
+static constexpr int MSM_SEG = 64;        // buckets per reduction segment
+static constexpr int MSM_THREADS = 256;
+
+static inline int windows_for(int c) { return (255 + c - 1) / c; }
+
+int msm_choose_c(size_t n) {
+  if (n < 4) return 2;
+  int best_c = 2;
+  double best = 1e300;
+  for (int c = 2; c <= 22; c++) {
+    const double W = windows_for(c);
+    const double cost = W * ((double)n + 2.8 * (double)(1ull << (c - 1)));
+    if (cost < best) {
+      best = cost;
+      best_c = c;
+    }
+  }
+  return best_c;
+}
+
+__device__ __forceinline__ G1Affine ld_aff(const G1Affine* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+  G1Affine r;
+  r.x.l[0] = a.x; r.x.l[1] = a.y; r.x.l[2] = a.z; r.x.l[3] = a.w;
+  r.x.l[4] = b.x; r.x.l[5] = b.y; r.x.l[6] = b.z; r.x.l[7] = b.w;
+  r.y.l[0] = c.x; r.y.l[1] = c.y; r.y.l[2] = c.z; r.y.l[3] = c.w;
+  r.y.l[4] = d.x; r.y.l[5] = d.y; r.y.l[6] = d.z; r.y.l[7] = d.w;
+  return r;
+}
+
+// 1. signed digits ----------------------------------------------------------
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_digits_kernel(const Fr* __restrict__ scalars, size_t n, int c, int W, uint32_t NB,
+                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint4* q = reinterpret_cast<const uint4*>(scalars + i);
+  uint4 a = q[0], b = q[1];
+  Fr s;
+  s.l[0] = a.x; s.l[1] = a.y; s.l[2] = a.z; s.l[3] = a.w;
+  s.l[4] = b.x; s.l[5] = b.y; s.l[6] = b.z; s.l[7] = b.w;
+  Fr v = to_canonical(s);
+  const uint32_t mask = (1u << c) - 1;
+  const uint32_t half = 1u << (c - 1);
+  const uint32_t sentinel = (uint32_t)W * NB;
+  uint32_t carry = 0;
+  for (int w = 0; w < W; w++) {
+    uint32_t d = (v.l[0] & mask) + carry;
+    // shift the 256-bit value right by c (c < 32)
+#pragma unroll
+    for (int k = 0; k < 7; k++) v.l[k] = (v.l[k] >> c) | (v.l[k + 1] << (32 - c));
+    v.l[7] >>= c;
+    uint32_t key, val = (uint32_t)i;
+    if (d > half) {  // negative digit d - 2^c (d == 2^c gives digit 0, carry 1)
+      const uint32_t mag = (1u << c) - d;
+      carry = 1;
+      key = mag ? (uint32_t)w * NB + mag - 1 : sentinel;
+      val |= 0x80000000u;
+    } else {
+      carry = 0;
+      key = d ? (uint32_t)w * NB + d - 1 : sentinel;
+    }
+    keys[(size_t)w * n + i] = key;
+    vals[(size_t)w * n + i] = val;
+  }
+}
+
+// 3. bucket bounds ------------------------------------------------------------
+__global__ void msm_bounds_kernel(const uint32_t* __restrict__ keys, size_t total, uint32_t sentinel,
+                                  uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t k = keys[i];
+  if (k == sentinel) return;
+  if (i == 0 || keys[i - 1] != k) start[k] = (uint32_t)i;
+  if (i == total - 1 || keys[i + 1] != k) end[k] = (uint32_t)(i + 1);
+}
+
+// 4. work items ---------------------------------------------------------------
+__global__ void msm_item_count_kernel(const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
+                                      uint32_t nbt, uint32_t L, uint32_t* __restrict__ cnt) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > nbt) return;
+  if (b == nbt) {
+    cnt[b] = 0;
+    return;
+  }
+  const uint32_t c = end[b] - start[b];
+  cnt[b] = (c + L - 1) / L;
+}
+
+// 5. accumulation ---------------------------------------------------------------
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ vals,
+               const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
+               const uint32_t* __restrict__ item_off, uint32_t nbt,
+               uint32_t L, G1xyzz* __restrict__ partials) {
+  const uint32_t it = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t total = item_off[nbt];
+  if (it >= total) return;
+  // bucket of this item: largest b with item_off[b] <= it
+  uint32_t lo = 0, hi = nbt;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (item_off[mid] <= it) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t b = lo;
+  const uint32_t j = it - item_off[b];
+  const uint32_t s = start[b] + j * L;
+  uint32_t e = s + L;
+  if (e > end[b]) e = end[b];
+  G1xyzz acc = G1xyzz::identity();
+  for (uint32_t p = s; p < e; p++) {
+    const uint32_t v = vals[p];
+    G1Affine pt = ld_aff(bases + (v & 0x7fffffffu));
+    if (v >> 31) pt = affine_neg(pt);
+    acc = xyzz_madd(acc, pt);
+  }
+  partials[it] = acc;
+}
+
+// 6. per-bucket sum of item partials ------------------------------------------------
+//    Buckets with <= MSM_SMALL items are summed by one thread; larger ones (skewed
+//    scalar distributions, e.g. many equal coefficients) are queued and reduced by
+//    whole workgroups in msm_big_bucket_kernel.
+static constexpr uint32_t MSM_SMALL = 32;
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_bucket_sum_kernel(const G1xyzz* __restrict__ partials, const uint32_t* __restrict__ item_off, uint32_t nbt,
+                      G1xyzz* __restrict__ buckets, uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nbt) return;
+  const uint32_t o = item_off[b], e = item_off[b + 1];
+  if (e - o > MSM_SMALL) {
+    const uint32_t slot = atomicAdd(big_count, 1u);
+    big_list[slot] = b;
+    return;
+  }
+  G1xyzz acc = G1xyzz::identity();
+  if (e > o) acc = partials[o];
+  for (uint32_t j = o + 1; j < e; j++) acc = xyzz_add(acc, partials[j]);
+  buckets[b] = acc;
+}
+
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_big_bucket_kernel(const G1xyzz* __restrict__ partials, const uint32_t* __restrict__ item_off,
+                      const uint32_t* __restrict__ big_list, const uint32_t* __restrict__ big_count,
+                      G1xyzz* __restrict__ buckets) {
+  __shared__ G1xyzz sh[MSM_THREADS];
+  const uint32_t nbig = *big_count;
+  for (uint32_t q = blockIdx.x; q < nbig; q += gridDim.x) {
+    const uint32_t b = big_list[q];
+    const uint32_t o = item_off[b], e = item_off[b + 1];
+    G1xyzz acc = G1xyzz::identity();
+    for (uint32_t j = o + threadIdx.x; j < e; j += blockDim.x) acc = xyzz_add(acc, partials[j]);
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
+      if ((int)threadIdx.x < h) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + h]);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) buckets[b] = sh[0];
+    __syncthreads();
+  }
+}
+
+// 7. segment running sums: seg result = sum_{j in seg} (j+1) B_j ------------------
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_segment_kernel(const G1xyzz* __restrict__ buckets, uint32_t NB, int W, G1xyzz* __restrict__ segs) {
+  const uint32_t nseg = NB / MSM_SEG > 0 ? NB / MSM_SEG : 1;
+  const uint32_t seglen = NB / nseg;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (uint32_t)W * nseg) return;
+  const uint32_t w = t / nseg, sg = t % nseg;
+  const G1xyzz* B = buckets + (size_t)w * NB;
+  const uint32_t lo = sg * seglen;
+  G1xyzz R = G1xyzz::identity(), S = G1xyzz::identity();
+  for (int j = (int)(lo + seglen) - 1; j >= (int)lo; j--) {
+    R = xyzz_add(R, B[j]);
+    S = xyzz_add(S, R);
+  }
+  // S = sum (j - lo + 1) B_j ; add lo * R
+  if (lo) S = xyzz_add(S, xyzz_mul_u32(R, lo));
+  segs[t] = S;
+}
+
+// 8. per-window reduction ------------------------------------------------------------
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_window_kernel(const G1xyzz* __restrict__ segs, uint32_t nseg, G1xyzz* __restrict__ windows) {
+  __shared__ G1xyzz sh[MSM_THREADS];
+  const uint32_t w = blockIdx.x;
+  G1xyzz acc = G1xyzz::identity();
+  for (uint32_t s = threadIdx.x; s < nseg; s += blockDim.x) acc = xyzz_add(acc, segs[(size_t)w * nseg + s]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) windows[w] = sh[0];
+}
+
+// 9. final Horner over windows -------------------------------------------------------
+__global__ void msm_final_kernel(const G1xyzz* __restrict__ windows, int W, int c, G1Affine* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  G1xyzz acc = windows[W - 1];
+  for (int w = W - 2; w >= 0; w--) {
+    for (int d = 0; d < c; d++) acc = xyzz_dbl(acc);
+    acc = xyzz_add(acc, windows[w]);
+  }
+  *out = xyzz_to_affine(acc);
+}
+
+// ------------------------------------------------------------------------------------
+static hipError_t grow(void** p, size_t bytes) {
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  return hipMalloc(p, bytes > 0 ? bytes : 16);
+}
+
+void msm_free(MsmWorkspace* ws) {
+  void** ptrs[] = {&ws->keys_in, &ws->keys_out, &ws->vals_in, &ws->vals_out, &ws->bucket_start,
+                   &ws->bucket_end, &ws->item_off, &ws->item_bucket, &ws->partials, &ws->buckets,
+                   &ws->segs, &ws->windows, &ws->result, &ws->total_items, &ws->sort_tmp, &ws->scan_tmp};
+  for (void** p : ptrs) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+  }
+  ws->cap_n = 0;
+  ws->cap_c = 0;
+  ws->sort_tmp_bytes = ws->scan_tmp_bytes = 0;
+}
+
+#define H2G_TRY(x)                      \
+  do {                                  \
+    hipError_t _e = (x);                \
+    if (_e != hipSuccess) return _e;    \
+  } while (0)
+
+hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWorkspace* ws,
+                   const MsmConfig& cfg, G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof) {
+#define H2G_PHASE(i) \
+  if (prof) H2G_TRY(hipEventRecord(prof->ev[i], st))
+  const int c = cfg.c > 0 ? cfg.c : msm_choose_c(n);
+  const int W = windows_for(c);
+  const uint32_t NB = 1u << (c - 1);
+  const uint32_t nbt = (uint32_t)W * NB;
+  const size_t total = n * (size_t)W;
+  uint32_t L = (uint32_t)cfg.item_len;
+  if (L == 0) {
+    const double avg = (double)n / (double)NB;
+    L = 16;
+    while (L < 2 * avg && L < 1024) L <<= 1;
+  }
+  const size_t max_items = total / L + nbt + 1;
+  const uint32_t nseg = NB / MSM_SEG > 0 ? NB / MSM_SEG : 1;
+
+  if (ws->cap_n < n || ws->cap_c != c) {
+    H2G_TRY(grow(&ws->keys_in, total * 4));
+    H2G_TRY(grow(&ws->keys_out, total * 4));
+    H2G_TRY(grow(&ws->vals_in, total * 4));
+    H2G_TRY(grow(&ws->vals_out, total * 4));
+    H2G_TRY(grow(&ws->bucket_start, (size_t)nbt * 4));
+    H2G_TRY(grow(&ws->bucket_end, (size_t)nbt * 4));
+    H2G_TRY(grow(&ws->item_off, ((size_t)nbt + 1) * 4));
+    H2G_TRY(grow(&ws->item_bucket, (size_t)nbt * 4));  // big-bucket list
+    H2G_TRY(grow(&ws->result, 16));                     // big-bucket counter
+    H2G_TRY(grow(&ws->partials, max_items * sizeof(G1xyzz)));
+    H2G_TRY(grow(&ws->buckets, (size_t)nbt * sizeof(G1xyzz)));
+    H2G_TRY(grow(&ws->segs, (size_t)W * nseg * sizeof(G1xyzz)));
+    H2G_TRY(grow(&ws->windows, (size_t)W * sizeof(G1xyzz)));
+    H2G_TRY(grow(&ws->total_items, ((size_t)nbt + 1) * 4));  // item counts (scan input)
+    ws->cap_n = n;
+    ws->cap_c = c;
+  }
+  uint32_t* keys_in = (uint32_t*)ws->keys_in;
+  uint32_t* keys_out = (uint32_t*)ws->keys_out;
+  uint32_t* vals_in = (uint32_t*)ws->vals_in;
+  uint32_t* vals_out = (uint32_t*)ws->vals_out;
+  uint32_t* bstart = (uint32_t*)ws->bucket_start;
+  uint32_t* bend = (uint32_t*)ws->bucket_end;
+  uint32_t* item_cnt = (uint32_t*)ws->total_items;
+  uint32_t* item_off = (uint32_t*)ws->item_off;
+
+  int key_bits = 1;
+  while ((1ull << key_bits) <= (uint64_t)nbt) key_bits++;
+
+  size_t sort_bytes = 0, scan_bytes = 0;
+  H2G_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, keys_in, keys_out, vals_in, vals_out,
+                                             (int)total, 0, key_bits, st));
+  H2G_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, item_cnt, item_off, (int)nbt + 1, st));
+  if (sort_bytes > ws->sort_tmp_bytes) {
+    H2G_TRY(grow(&ws->sort_tmp, sort_bytes));
+    ws->sort_tmp_bytes = sort_bytes;
+  }
+  if (scan_bytes > ws->scan_tmp_bytes) {
+    H2G_TRY(grow(&ws->scan_tmp, scan_bytes));
+    ws->scan_tmp_bytes = scan_bytes;
+  }
+
+  const int T = MSM_THREADS;
+  H2G_PHASE(0);
+  hipLaunchKernelGGL(msm_digits_kernel, dim3((unsigned)((n + T - 1) / T)), dim3(T), 0, st, d_scalars, n, c, W, NB,
+                     keys_in, vals_in);
+  H2G_TRY(hipGetLastError());
+  H2G_PHASE(1);
+  H2G_TRY(hipcub::DeviceRadixSort::SortPairs(ws->sort_tmp, sort_bytes, keys_in, keys_out, vals_in, vals_out,
+                                             (int)total, 0, key_bits, st));
+  H2G_PHASE(2);
+  H2G_TRY(hipMemsetAsync(bstart, 0, (size_t)nbt * 4, st));
+  H2G_TRY(hipMemsetAsync(bend, 0, (size_t)nbt * 4, st));
+  hipLaunchKernelGGL(msm_bounds_kernel, dim3((unsigned)((total + T - 1) / T)), dim3(T), 0, st, keys_out, total,
+                     nbt, bstart, bend);
+  hipLaunchKernelGGL(msm_item_count_kernel, dim3((nbt + 1 + T - 1) / T), dim3(T), 0, st, bstart, bend, nbt, L,
+                     item_cnt);
+  H2G_TRY(hipcub::DeviceScan::ExclusiveSum(ws->scan_tmp, scan_bytes, item_cnt, item_off, (int)nbt + 1, st));
+  H2G_PHASE(3);
+  hipLaunchKernelGGL(msm_acc_kernel, dim3((unsigned)((max_items + T - 1) / T)), dim3(T), 0, st, d_bases, vals_out,
+                     bstart, bend, item_off, nbt, L, (G1xyzz*)ws->partials);
+  H2G_PHASE(4);
+  uint32_t* big_list = (uint32_t*)ws->item_bucket;
+  uint32_t* big_count = (uint32_t*)ws->result;
+  H2G_TRY(hipMemsetAsync(big_count, 0, 4, st));
+  hipLaunchKernelGGL(msm_bucket_sum_kernel, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)ws->partials,
+                     item_off, nbt, (G1xyzz*)ws->buckets, big_list, big_count);
+  hipLaunchKernelGGL(msm_big_bucket_kernel, dim3(256), dim3(T), 0, st, (const G1xyzz*)ws->partials, item_off,
+                     (const uint32_t*)big_list, (const uint32_t*)big_count, (G1xyzz*)ws->buckets);
+  H2G_PHASE(5);
+  hipLaunchKernelGGL(msm_segment_kernel, dim3(((uint32_t)W * nseg + T - 1) / T), dim3(T), 0, st,
+                     (const G1xyzz*)ws->buckets, NB, W, (G1xyzz*)ws->segs);
+  hipLaunchKernelGGL(msm_window_kernel, dim3(W), dim3(MSM_THREADS), 0, st, (const G1xyzz*)ws->segs, nseg,
+                     (G1xyzz*)ws->windows);
+  hipLaunchKernelGGL(msm_final_kernel, dim3(1), dim3(64), 0, st, (const G1xyzz*)ws->windows, W, c, d_out);
+  H2G_TRY(hipGetLastError());
+  H2G_PHASE(6);
+#undef H2G_PHASE
+  return hipSuccess;
+}
+
+}  // namespace h2g

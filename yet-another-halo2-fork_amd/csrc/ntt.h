@@ -1,0 +1,42 @@
+// ntt.h -- NTT plan/launch interface (see ntt.hip).
+#pragma once
+#include "bn254.h"
+
+namespace h2g {
+
+static constexpr int NTT_SMALL_MAX_LOG = 10;  // whole transform in one block up to 2^10
+static constexpr int NTT_MAX_PASS_LOG = 8;    // LDS sub-transform size per HBM pass
+
+struct NttTables {
+  int L = 0;  // log2 N
+  int b = 0;  // split of the 2-level table
+  Fr* lo = nullptr;
+  Fr* hi = nullptr;
+};
+
+// One transform y = DFT_w(x) of size N = 2^tab.L with fused maps:
+//   x_i = src[i] * (in_distribute ? zeta-power(i mod 3) : 1) for i < n_in, 0 beyond
+//   dst[k] = y_k * (has_scale ? scale : 1) * (out_distribute ? zeta-power(k mod 3) : 1), k < out_len
+// `work` is an N-element scratch buffer distinct from src and dst (src may alias dst).
+struct NttArgs {
+  const Fr* src = nullptr;
+  uint64_t n_in = 0;
+  Fr* work = nullptr;
+  Fr* dst = nullptr;
+  uint64_t out_len = 0;
+  NttTables tab;
+  int in_distribute = 0;
+  Fr in_z1, in_z2;
+  int has_scale = 0;
+  Fr scale;
+  int out_distribute = 0;
+  Fr out_z1, out_z2;
+};
+
+void ntt_split(int L, int* P, int lg[4]);
+hipError_t ntt_build_tables(NttTables* t, const Fr& omega, int L, hipStream_t st);
+void ntt_free_tables(NttTables* t);
+hipError_t ntt_run(const NttArgs& a, hipStream_t st);
+hipError_t ntt_init_attributes();
+
+}  // namespace h2g

@@ -1,0 +1,363 @@
+"""ctypes binding of libh2g.so (include/h2g.h) -- what a Python host (tests,
+bench.py, smoke) uses to call the MI355X hot path through the C ABI.
+
+No fallback: if the library or a GPU is missing, calls raise.  Arrays are numpy
+uint64 in the halo2curves layout (Fr = 4 Montgomery limbs, G1Affine = 8 limbs);
+device buffers are raw pointers (ints) from h2g_dev_alloc or torch tensors'
+data_ptr().
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "lib", "libh2g.so")
+HEADER = os.path.join(REPO, "include", "h2g.h")
+
+U64P = ctypes.POINTER(ctypes.c_uint64)
+VP = ctypes.c_void_p
+SZ = ctypes.c_size_t
+I32 = ctypes.c_int
+U32 = ctypes.c_uint32
+U64 = ctypes.c_uint64
+
+OP_ADD, OP_SUB, OP_MUL, OP_SCALE, OP_SUB_CONST, OP_ADD_CONST, OP_AXPY = range(7)
+
+_SIGS = {
+    "h2g_abi_version": ([], I32),
+    "h2g_last_error": ([], ctypes.c_char_p),
+    "h2g_init": ([ctypes.POINTER(I32), I32], I32),
+    "h2g_shutdown": ([], I32),
+    "h2g_device_count": ([ctypes.POINTER(I32)], I32),
+    "h2g_set_device": ([I32], I32),
+    "h2g_msm": ([U64P, U64P, SZ, U64P, ctypes.POINTER(I32)], I32),
+    "h2g_msm_coeffs_descriptor": ([U64P, SZ, ctypes.POINTER(U64)], I32),
+    "h2g_msm_base_descriptor": ([U64P, SZ, ctypes.POINTER(U64)], I32),
+    "h2g_msm_descriptor_free": ([U64], I32),
+    "h2g_msm_with_cached_scalars": ([U64, U64P, SZ, U64P, ctypes.POINTER(I32)], I32),
+    "h2g_msm_with_cached_base": ([U64P, SZ, U64, SZ, U64P, ctypes.POINTER(I32)], I32),
+    "h2g_msm_with_cached_inputs": ([U64, U64, SZ, U64P, ctypes.POINTER(I32)], I32),
+    "h2g_msm_dev": ([VP, VP, SZ, VP, VP], I32),
+    "h2g_msm_dev_cfg": ([VP, VP, SZ, I32, VP, VP], I32),
+    "h2g_descriptor_device_ptr": ([U64, ctypes.POINTER(VP), ctypes.POINTER(SZ)], I32),
+    "h2g_srs_setup_dev": ([U64P, SZ, VP, VP], I32),
+    "h2g_fft": ([U64P, U32, U64P], I32),
+    "h2g_fft_dev": ([VP, U32, U64P, VP], I32),
+    "h2g_domain_create": ([U32, U32, ctypes.POINTER(U64)], I32),
+    "h2g_domain_free": ([U64], I32),
+    "h2g_domain_info": ([U64, ctypes.POINTER(U32), ctypes.POINTER(U32), U64P], I32),
+    "h2g_lagrange_to_coeff": ([U64, U64P], I32),
+    "h2g_lagrange_to_coeff_dev": ([U64, VP, VP], I32),
+    "h2g_coeff_to_extended": ([U64, U64P, U64P], I32),
+    "h2g_coeff_to_extended_dev": ([U64, VP, VP, VP], I32),
+    "h2g_extended_to_coeff": ([U64, U64P, U64P], I32),
+    "h2g_extended_to_coeff_dev": ([U64, VP, VP, VP], I32),
+    "h2g_divide_by_vanishing_poly": ([U64, U64P], I32),
+    "h2g_divide_by_vanishing_poly_dev": ([U64, VP, VP], I32),
+    "h2g_fr_op": ([I32, U64P, U64P, U64P, U64P, SZ], I32),
+    "h2g_fr_op_dev": ([I32, VP, VP, U64P, VP, SZ, VP], I32),
+    "h2g_fr_batch_invert": ([U64P, SZ], I32),
+    "h2g_fr_batch_invert_dev": ([VP, SZ, VP], I32),
+    "h2g_fr_prefix_product": ([U64P, U64P, SZ], I32),
+    "h2g_fr_prefix_product_dev": ([VP, VP, SZ, VP], I32),
+    "h2g_dev_alloc": ([SZ, ctypes.POINTER(VP)], I32),
+    "h2g_dev_free": ([VP], I32),
+    "h2g_memcpy_htod": ([VP, VP, SZ], I32),
+    "h2g_memcpy_dtoh": ([VP, VP, SZ], I32),
+    "h2g_synchronize": ([], I32),
+    "h2g_event_create": ([ctypes.POINTER(VP)], I32),
+    "h2g_event_destroy": ([VP], I32),
+    "h2g_event_record": ([VP, VP], I32),
+    "h2g_event_elapsed_ms": ([VP, VP, ctypes.POINTER(ctypes.c_float)], I32),
+    "h2g_g1_add_affine": ([U64P, U64P, U64P], I32),
+    "h2g_profile_enable": ([I32], I32),
+    "h2g_profile_msm_collect": ([ctypes.POINTER(ctypes.c_float), I32, ctypes.POINTER(I32), ctypes.POINTER(I32)], I32),
+}
+
+MSM_PHASES = ("digits", "sort", "bucket_bounds", "accumulate", "bucket_sum", "reduce")
+
+_lib = None
+
+
+class H2GError(RuntimeError):
+    pass
+
+
+def header_symbols():
+    """Function names declared in include/h2g.h."""
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(?:int|const char\*)\s+(h2g_\w+)\s*\(", text)))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise H2GError(f"{LIB_PATH} not built: run __graft_entry__.build() "
+                           "(yet-another-halo2-fork_amd/build_lib.py)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGS.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        raise H2GError(f"h2g error {rc}: {lib().h2g_last_error().decode()}")
+
+
+def p64(a):
+    if a is None:
+        return None
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"], "need C-contiguous uint64"
+    return a.ctypes.data_as(U64P)
+
+
+_inited = False
+
+
+def init(devices=None):
+    global _inited
+    if devices:
+        arr = (I32 * len(devices))(*devices)
+        check(lib().h2g_init(arr, len(devices)))
+    else:
+        check(lib().h2g_init(None, 0))
+    _inited = True
+
+
+def shutdown():
+    global _inited
+    check(lib().h2g_shutdown())
+    _inited = False
+
+
+# ----------------------------------------------------------------- MSM (host API)
+def msm(scalars, bases):
+    sc = np.ascontiguousarray(scalars, dtype=np.uint64)
+    bs = np.ascontiguousarray(bases, dtype=np.uint64)
+    assert sc.shape[0] == bs.shape[0]
+    out = np.zeros(8, dtype=np.uint64)
+    ident = I32(0)
+    check(lib().h2g_msm(p64(sc), p64(bs), sc.shape[0], p64(out), ctypes.byref(ident)))
+    return out
+
+
+def base_descriptor(bases):
+    h = U64(0)
+    bs = np.ascontiguousarray(bases, dtype=np.uint64)
+    check(lib().h2g_msm_base_descriptor(p64(bs), bs.shape[0], ctypes.byref(h)))
+    return h.value
+
+
+def coeffs_descriptor(scalars):
+    h = U64(0)
+    sc = np.ascontiguousarray(scalars, dtype=np.uint64)
+    check(lib().h2g_msm_coeffs_descriptor(p64(sc), sc.shape[0], ctypes.byref(h)))
+    return h.value
+
+
+def descriptor_free(h):
+    check(lib().h2g_msm_descriptor_free(h))
+
+
+def msm_with_cached_base(scalars, base_handle, offset=0):
+    sc = np.ascontiguousarray(scalars, dtype=np.uint64)
+    out = np.zeros(8, dtype=np.uint64)
+    ident = I32(0)
+    check(lib().h2g_msm_with_cached_base(p64(sc), sc.shape[0], base_handle, offset, p64(out), ctypes.byref(ident)))
+    return out
+
+
+def msm_with_cached_scalars(coeff_handle, bases):
+    bs = np.ascontiguousarray(bases, dtype=np.uint64)
+    out = np.zeros(8, dtype=np.uint64)
+    ident = I32(0)
+    check(lib().h2g_msm_with_cached_scalars(coeff_handle, p64(bs), bs.shape[0], p64(out), ctypes.byref(ident)))
+    return out
+
+
+def msm_with_cached_inputs(coeff_handle, base_handle, offset=0):
+    out = np.zeros(8, dtype=np.uint64)
+    ident = I32(0)
+    check(lib().h2g_msm_with_cached_inputs(coeff_handle, base_handle, offset, p64(out), ctypes.byref(ident)))
+    return out
+
+
+# ----------------------------------------------------------------- device buffers
+class DevBuf:
+    """Device allocation owned by Python (freed on close / GC)."""
+
+    def __init__(self, nbytes):
+        p = VP()
+        check(lib().h2g_dev_alloc(nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+        self.nbytes = nbytes
+
+    @classmethod
+    def from_array(cls, a):
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes)
+        b.upload(a)
+        return b
+
+    def upload(self, a):
+        a = np.ascontiguousarray(a)
+        assert a.nbytes <= self.nbytes
+        check(lib().h2g_memcpy_htod(VP(self.ptr), a.ctypes.data_as(VP), a.nbytes))
+
+    def download(self, shape, dtype=np.uint64):
+        out = np.empty(shape, dtype=dtype)
+        check(lib().h2g_memcpy_dtoh(out.ctypes.data_as(VP), VP(self.ptr), out.nbytes))
+        return out
+
+    def close(self):
+        if self.ptr:
+            try:
+                lib().h2g_dev_free(VP(self.ptr))
+            finally:
+                self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def msm_dev(d_scalars, d_bases, n, d_out, window_bits=0, stream=None):
+    check(lib().h2g_msm_dev_cfg(VP(d_scalars), VP(d_bases), n, window_bits, VP(d_out), VP(stream) if stream else None))
+
+
+def srs_setup_dev(s, n, d_out, stream=None):
+    s = np.ascontiguousarray(s, dtype=np.uint64)
+    check(lib().h2g_srs_setup_dev(p64(s), n, VP(d_out), VP(stream) if stream else None))
+
+
+# ----------------------------------------------------------------- FFT / domain
+def fft(a, omega):
+    a = np.ascontiguousarray(a, dtype=np.uint64).copy()
+    k = int(a.shape[0]).bit_length() - 1
+    assert a.shape[0] == 1 << k
+    check(lib().h2g_fft(p64(a), k, p64(np.ascontiguousarray(omega, dtype=np.uint64))))
+    return a
+
+
+def fft_dev(d_a, log_n, omega, stream=None):
+    check(lib().h2g_fft_dev(VP(d_a), log_n, p64(np.ascontiguousarray(omega, dtype=np.uint64)),
+                            VP(stream) if stream else None))
+
+
+class Domain:
+    """EvaluationDomain::new(j, k) mirror (halo2_backend/src/poly/domain.rs:38-144)."""
+
+    def __init__(self, j, k):
+        h = U64(0)
+        check(lib().h2g_domain_create(j, k, ctypes.byref(h)))
+        self.h = h.value
+        self.j = j
+        kk, ek = U32(0), U32(0)
+        self.consts = np.zeros((9, 4), dtype=np.uint64)
+        check(lib().h2g_domain_info(self.h, ctypes.byref(kk), ctypes.byref(ek), p64(self.consts)))
+        self.k, self.extended_k = kk.value, ek.value
+        self.n = 1 << self.k
+        self.extended_len = 1 << self.extended_k
+
+    def lagrange_to_coeff(self, a):
+        a = np.ascontiguousarray(a, dtype=np.uint64).copy()
+        assert a.shape[0] == self.n
+        check(lib().h2g_lagrange_to_coeff(self.h, p64(a)))
+        return a
+
+    def coeff_to_extended(self, a):
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        assert a.shape[0] == self.n
+        out = np.zeros((self.extended_len, 4), dtype=np.uint64)
+        check(lib().h2g_coeff_to_extended(self.h, p64(a), p64(out)))
+        return out
+
+    def extended_to_coeff(self, a):
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        assert a.shape[0] == self.extended_len
+        out = np.zeros((self.n * (self.j - 1), 4), dtype=np.uint64)
+        check(lib().h2g_extended_to_coeff(self.h, p64(a), p64(out)))
+        return out
+
+    def divide_by_vanishing_poly(self, a):
+        a = np.ascontiguousarray(a, dtype=np.uint64).copy()
+        assert a.shape[0] == self.extended_len
+        check(lib().h2g_divide_by_vanishing_poly(self.h, p64(a)))
+        return a
+
+    def close(self):
+        if self.h:
+            lib().h2g_domain_free(self.h)
+            self.h = 0
+
+
+# ----------------------------------------------------------------- poly ops
+def fr_op(op, a, b=None, c=None):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    out = np.zeros_like(a)
+    bb = np.ascontiguousarray(b, dtype=np.uint64) if b is not None else None
+    cc = np.ascontiguousarray(c, dtype=np.uint64) if c is not None else None
+    check(lib().h2g_fr_op(op, p64(a), p64(bb), p64(cc), p64(out), a.shape[0]))
+    return out
+
+
+def batch_invert(a):
+    a = np.ascontiguousarray(a, dtype=np.uint64).copy()
+    check(lib().h2g_fr_batch_invert(p64(a), a.shape[0]))
+    return a
+
+
+def prefix_product(a):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    out = np.zeros_like(a)
+    check(lib().h2g_fr_prefix_product(p64(a), p64(out), a.shape[0]))
+    return out
+
+
+def g1_add_affine(a, b):
+    out = np.zeros(8, dtype=np.uint64)
+    check(lib().h2g_g1_add_affine(p64(np.ascontiguousarray(a, dtype=np.uint64)),
+                                  p64(np.ascontiguousarray(b, dtype=np.uint64)), p64(out)))
+    return out
+
+
+def profile_enable(on=True):
+    check(lib().h2g_profile_enable(1 if on else 0))
+
+
+def profile_msm_collect():
+    """-> (calls, {phase: total_ms}) for MSMs run since profiling was enabled."""
+    ms = (ctypes.c_float * 8)()
+    npz, calls = I32(0), I32(0)
+    check(lib().h2g_profile_msm_collect(ms, 8, ctypes.byref(npz), ctypes.byref(calls)))
+    return calls.value, {MSM_PHASES[i]: ms[i] for i in range(npz.value)}
+
+
+class Timer:
+    """HIP-event timing on the library stream (or a given stream)."""
+
+    def __init__(self, stream=None):
+        self.stream = VP(stream) if stream else None
+        a, b = VP(), VP()
+        check(lib().h2g_event_create(ctypes.byref(a)))
+        check(lib().h2g_event_create(ctypes.byref(b)))
+        self.a, self.b = a, b
+
+    def start(self):
+        check(lib().h2g_event_record(self.a, self.stream))
+
+    def stop_ms(self):
+        check(lib().h2g_event_record(self.b, self.stream))
+        ms = ctypes.c_float(0)
+        check(lib().h2g_event_elapsed_ms(self.a, self.b, ctypes.byref(ms)))
+        return ms.value
