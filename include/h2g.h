@@ -71,6 +71,10 @@ int h2g_msm_dev(const void* d_coeffs, const void* d_bases, size_t n, void* d_out
 /* same, with an explicit Pippenger window size c (0 = automatic) */
 int h2g_msm_dev_cfg(const void* d_coeffs, const void* d_bases, size_t n, int window_bits, void* d_out_affine,
                     void* stream);
+/* device-resident inputs, result returned to the host (synchronous) -- the path
+ * MsmAccel::msm takes when the prover keeps polynomials in HBM */
+int h2g_msm_dev_host(const void* d_coeffs, const void* d_bases, size_t n, int window_bits, uint64_t out_affine[8],
+                     int* out_is_identity, void* stream);
 int h2g_descriptor_device_ptr(uint64_t handle, void** d_ptr, size_t* n);
 
 /* ---- SRS generation on device: g_i = [s^i] G, i < n

@@ -122,8 +122,9 @@ def test_msm_window_sizes(window_bits):
     sc = O.random_fr(r, n)
     want = O.msm_best(sc, bases, 8)
     dsc, dbs, dout = h2g.DevBuf.from_array(sc), h2g.DevBuf.from_array(bases), h2g.DevBuf(64)
-    h2g.msm_dev(dsc.ptr, dbs.ptr, n, dout.ptr, window_bits=window_bits)
+    h2g.msm_dev(dsc.ptr, dbs.ptr, n, dout.ptr, window_bits=window_bits)  # device-side final combine
     assert np.array_equal(dout.download(8), want)
+    assert np.array_equal(h2g.msm_dev_host(dsc.ptr, dbs.ptr, n, window_bits), want)  # host-side combine
 
 
 @pytest.mark.parametrize("k", [20, 22])
@@ -134,9 +135,8 @@ def test_msm_full_size_srs_identity(k):
     s = O.random_fr(r, 1)[0]
     dbs = _srs(n, s)
     sc = O.random_fr(r, n)
-    dsc, dout = h2g.DevBuf.from_array(sc), h2g.DevBuf(64)
-    h2g.msm_dev(dsc.ptr, dbs.ptr, n, dout.ptr)
-    got = dout.download(8)
+    dsc = h2g.DevBuf.from_array(sc)
+    got = h2g.msm_dev_host(dsc.ptr, dbs.ptr, n)
     want = O.g1_mul(GEN, O.eval_poly(sc, s))
     assert np.array_equal(got, want)
 

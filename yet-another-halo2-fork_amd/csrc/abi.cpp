@@ -92,6 +92,7 @@ struct Device {
   MsmWorkspace msm;
   DevBuf a, b, c, work, out;
   std::map<NttKey, NttTables> ntt_tables;
+  void* h_windows = nullptr;  // pinned host copy of MSM window sums
 };
 
 std::vector<std::unique_ptr<Device>> g_devs;
@@ -150,7 +151,7 @@ int get_tables(Device* d, const Fr& omega, int L, hipStream_t st, NttTables* out
 
 int msm_dev_impl(Device* d, const void* sc, const void* bs, size_t n, int c, void* out, hipStream_t st) {
   if (n == 0) {
-    HIPCHK(hipMemsetAsync(out, 0, 64, st));
+    if (out) HIPCHK(hipMemsetAsync(out, 0, 64, st));
     return H2G_OK;
   }
   if (n > 0x7fffffffULL) return fail(H2G_ERR_ARG, "msm: n too large");
@@ -168,9 +169,23 @@ int msm_dev_impl(Device* d, const void* sc, const void* bs, size_t n, int c, voi
   return H2G_OK;
 }
 
-int finish_host_msm(Device* d, uint64_t* out, int* is_id) {
-  HIPCHK(hipMemcpyAsync(out, d->out.p, 64, hipMemcpyDeviceToHost, d->stream));
-  HIPCHK(hipStreamSynchronize(d->stream));
+// Host-returning MSM: device phases, then the W window sums (W x 128 B) come back
+// to the host and are combined there (msm_windows_host_finish); synchronous.
+int msm_host_impl(Device* d, const void* sc, const void* bs, size_t n, int c, uint64_t* out, int* is_id,
+                  hipStream_t st) {
+  if (n == 0) {
+    std::memset(out, 0, 64);
+    if (is_id) *is_id = 1;
+    return H2G_OK;
+  }
+  int rc = msm_dev_impl(d, sc, bs, n, c, nullptr, st);
+  if (rc) return rc;
+  const int W = d->msm.last_W;
+  if (!d->h_windows) HIPCHK(hipHostMalloc(&d->h_windows, 256 * sizeof(G1xyzz), hipHostMallocDefault));
+  HIPCHK(hipMemcpyAsync(d->h_windows, d->msm.windows, (size_t)W * sizeof(G1xyzz), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const G1Affine r = msm_windows_host_finish(reinterpret_cast<const G1xyzz*>(d->h_windows), W, d->msm.last_c);
+  std::memcpy(out, &r, 64);
   if (is_id) {
     uint64_t x = 0;
     for (int i = 0; i < 8; i++) x |= out[i];
@@ -267,6 +282,7 @@ int h2g_shutdown(void) {
     dev->work.release();
     dev->out.release();
     for (auto& kv : dev->ntt_tables) ntt_free_tables(&kv.second);
+    if (dev->h_windows) (void)hipHostFree(dev->h_windows);
     (void)hipStreamDestroy(dev->stream);
   }
   g_devs.clear();
@@ -297,9 +313,7 @@ int h2g_msm(const uint64_t* coeffs, const uint64_t* bases, size_t n, uint64_t ou
   HIPCHK(d->out.ensure(64));
   HIPCHK(hipMemcpyAsync(d->a.p, coeffs, n * 32, hipMemcpyHostToDevice, d->stream));
   HIPCHK(hipMemcpyAsync(d->b.p, bases, n * 64, hipMemcpyHostToDevice, d->stream));
-  int rc = msm_dev_impl(d, d->a.p, d->b.p, n, 0, d->out.p, d->stream);
-  if (rc) return rc;
-  return finish_host_msm(d, out, is_id);
+  return msm_host_impl(d, d->a.p, d->b.p, n, 0, out, is_id, d->stream);
 }
 
 static int make_desc(const uint64_t* data, size_t n, size_t elem_bytes, bool is_base, uint64_t* handle) {
@@ -348,9 +362,7 @@ int h2g_msm_with_cached_scalars(uint64_t coeffs, const uint64_t* bases, size_t n
   HIPCHK(d->b.ensure(n * 64 + 64));
   HIPCHK(d->out.ensure(64));
   HIPCHK(hipMemcpyAsync(d->b.p, bases, n * 64, hipMemcpyHostToDevice, d->stream));
-  int rc = msm_dev_impl(d, it->second.d, d->b.p, n, 0, d->out.p, d->stream);
-  if (rc) return rc;
-  return finish_host_msm(d, out, is_id);
+  return msm_host_impl(d, it->second.d, d->b.p, n, 0, out, is_id, d->stream);
 }
 
 int h2g_msm_with_cached_base(const uint64_t* coeffs, size_t n, uint64_t base, size_t off, uint64_t out[8],
@@ -362,9 +374,7 @@ int h2g_msm_with_cached_base(const uint64_t* coeffs, size_t n, uint64_t base, si
   HIPCHK(d->a.ensure(n * 32 + 32));
   HIPCHK(d->out.ensure(64));
   HIPCHK(hipMemcpyAsync(d->a.p, coeffs, n * 32, hipMemcpyHostToDevice, d->stream));
-  int rc = msm_dev_impl(d, d->a.p, (const char*)it->second.d + off * 64, n, 0, d->out.p, d->stream);
-  if (rc) return rc;
-  return finish_host_msm(d, out, is_id);
+  return msm_host_impl(d, d->a.p, (const char*)it->second.d + off * 64, n, 0, out, is_id, d->stream);
 }
 
 int h2g_msm_with_cached_inputs(uint64_t coeffs, uint64_t base, size_t off, uint64_t out[8], int* is_id) {
@@ -376,9 +386,7 @@ int h2g_msm_with_cached_inputs(uint64_t coeffs, uint64_t base, size_t off, uint6
   const size_t n = ic->second.n;
   if (off + n > ib->second.n) return fail(H2G_ERR_ARG, "msm: bases.len() < size");
   HIPCHK(d->out.ensure(64));
-  int rc = msm_dev_impl(d, ic->second.d, (const char*)ib->second.d + off * 64, n, 0, d->out.p, d->stream);
-  if (rc) return rc;
-  return finish_host_msm(d, out, is_id);
+  return msm_host_impl(d, ic->second.d, (const char*)ib->second.d + off * 64, n, 0, out, is_id, d->stream);
 }
 
 int h2g_msm_dev(const void* sc, const void* bs, size_t n, void* out, void* stream) {
@@ -390,6 +398,13 @@ int h2g_msm_dev_cfg(const void* sc, const void* bs, size_t n, int c, void* out, 
   if (!out || (n && (!sc || !bs))) return fail(H2G_ERR_ARG, "msm_dev: null pointer");
   if (c < 0 || c > 24) return fail(H2G_ERR_ARG, "msm_dev: window_bits out of range");
   return msm_dev_impl(d, sc, bs, n, c, out, pick_stream(d, stream));
+}
+
+int h2g_msm_dev_host(const void* sc, const void* bs, size_t n, int c, uint64_t out[8], int* is_id, void* stream) {
+  NEED_DEV();
+  if (!out || (n && (!sc || !bs))) return fail(H2G_ERR_ARG, "msm_dev_host: null pointer");
+  if (c < 0 || c > 24) return fail(H2G_ERR_ARG, "msm_dev_host: window_bits out of range");
+  return msm_host_impl(d, sc, bs, n, c, out, is_id, pick_stream(d, stream));
 }
 
 int h2g_srs_setup_dev(const uint64_t s[4], size_t n, void* d_out, void* stream) {

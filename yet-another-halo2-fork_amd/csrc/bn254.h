@@ -124,10 +124,68 @@ H2G_HD Fe<P> dbl(const Fe<P>& a) {
 }
 
 // ---------------------------------------------------------------- Montgomery multiply
-// CIOS with the "no final carry" shortcut (top modulus limb < 2^31 - 1 for both
-// BN254 moduli), 32-bit limbs.  Returns a*b*2^-256 mod M, fully reduced.
+// Device: FIPS (finely integrated product scanning) Montgomery multiplication.
+// A 96-bit column accumulator (lo64:hi32) takes every 32x32 product through one
+// v_mad_u64_u32 whose carry-out (vcc) feeds one v_addc_co_u32: 128 mads + 128
+// addcs + 8 mul_lo per product, no register shuffling (the compiler's own
+// lowering of the CIOS loop spends ~2/3 of its instructions on v_mov/64-bit
+// shifts: 86 vs 125 Gmodmul/s measured on MI355X, tools/microbench).
+// One inline-asm block per product: hipcc pads each block boundary with an
+// s_nop, but grouping a whole column per block measured
+// slower (118 vs 125 Gmodmul/s) -- the compiler interleaves small blocks better.
+__device__ __forceinline__ void h2g_mac(uint64_t& lo, uint32_t& hi, uint32_t a, uint32_t b) {
+  asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+               : "+v"(lo), "+v"(hi)
+               : "v"(a), "v"(b)
+               : "vcc");
+}
+
 template <class P>
-H2G_HD Fe<P> operator*(const Fe<P>& a, const Fe<P>& b) {
+__device__ __forceinline__ Fe<P> operator*(const Fe<P>& A, const Fe<P>& B) {
+  const uint32_t* a = A.l;
+  const uint32_t* b = B.l;
+  uint32_t m[8];
+  Fe<P> r, d;
+  uint64_t lo = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#pragma unroll
+    for (int i = 0; i < k; i++) {
+      h2g_mac(lo, hi, a[i], b[k - i]);
+      h2g_mac(lo, hi, m[i], P::M[k - i]);
+    }
+    h2g_mac(lo, hi, a[k], b[0]);
+    m[k] = (uint32_t)lo * P::INV;
+    h2g_mac(lo, hi, m[k], P::M[0]);
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+#pragma unroll
+  for (int k = 8; k < 15; k++) {
+#pragma unroll
+    for (int i = k - 7; i < 8; i++) {
+      h2g_mac(lo, hi, a[i], b[k - i]);
+      h2g_mac(lo, hi, m[i], P::M[k - i]);
+    }
+    r.l[k - 8] = (uint32_t)lo;
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  r.l[7] = (uint32_t)lo;  // result < 2M < 2^255
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    int64_t u = (int64_t)r.l[i] - P::M[i] + br;
+    d.l[i] = (uint32_t)u;
+    br = u >> 32;
+  }
+  return br ? r : d;
+}
+// Host: CIOS with the "no final carry" shortcut (top modulus limb < 2^31 - 1 for
+// both BN254 moduli), 32-bit limbs.  Returns a*b*2^-256 mod M, fully reduced.
+template <class P>
+__host__ inline Fe<P> operator*(const Fe<P>& a, const Fe<P>& b) {
   uint32_t t[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) t[i] = 0;
@@ -360,8 +418,11 @@ H2G_HD G1Affine xyzz_to_affine(const G1xyzz& p) {
 
 // [k] P for a small unsigned k (double-and-add, MSB first)
 H2G_HD G1xyzz xyzz_mul_u32(const G1xyzz& p, uint32_t k) {
-  G1xyzz acc = G1xyzz::identity();
-  for (int b = 31; b >= 0; b--) {
+  if (k == 0) return G1xyzz::identity();
+  int top = 31;
+  while (!((k >> top) & 1)) top--;
+  G1xyzz acc = p;
+  for (int b = top - 1; b >= 0; b--) {
     acc = xyzz_dbl(acc);
     if ((k >> b) & 1) acc = xyzz_add(acc, p);
   }

@@ -5,28 +5,30 @@
 namespace h2g {
 
 struct MsmConfig {
-  int c = 0;          // window bits (0: choose from n)
-  int item_len = 0;   // max points per accumulation work item (0: choose)
+  int c = 0;         // window bits (0: choose from n)
+  int item_len = 0;  // entries per accumulation chunk (0: choose)
 };
 
 // Device workspace, grown on demand and reused across calls.
 struct MsmWorkspace {
   size_t cap_n = 0;
   int cap_c = 0;
-  void* keys_in = nullptr;     // u32 [n*W]
-  void* keys_out = nullptr;    // u32 [n*W]
-  void* vals_in = nullptr;     // u32 [n*W]
-  void* vals_out = nullptr;    // u32 [n*W]
+  uint32_t cap_L = 0;
+  int last_c = 0, last_W = 0;    // window config of the most recent msm_run
+  void* keys_in = nullptr;       // u32 [n*W]
+  void* keys_out = nullptr;      // u32 [n*W]
+  void* vals_in = nullptr;       // u32 [n*W]
+  void* vals_out = nullptr;      // u32 [n*W]
   void* bucket_start = nullptr;  // u32 [W*NB]
   void* bucket_end = nullptr;    // u32 [W*NB]
-  void* item_off = nullptr;      // u32 [W*NB + 1]
-  void* item_bucket = nullptr;   // u32 [max items]
-  void* partials = nullptr;      // G1xyzz [max items]
+  void* item_off = nullptr;      // (unused)
+  void* item_bucket = nullptr;   // u32 [W*NB] big-bucket list
+  void* partials = nullptr;      // G1xyzz [2 * chunks] boundary slots
   void* buckets = nullptr;       // G1xyzz [W*NB]
   void* segs = nullptr;          // G1xyzz [W*SEGS]
   void* windows = nullptr;       // G1xyzz [W]
-  void* result = nullptr;        // G1Affine + flag
-  void* total_items = nullptr;   // u32
+  void* result = nullptr;        // counters
+  void* total_items = nullptr;   // (unused)
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   void* scan_tmp = nullptr;
@@ -34,18 +36,22 @@ struct MsmWorkspace {
 };
 
 int msm_choose_c(size_t n);
+int msm_windows_for(int c);
 
 // Optional per-phase HIP events (profiling).  Phases: digits, sort, bucket_bounds,
-// accumulate, bucket_sum, reduce -> 7 events, recorded on the MSM's stream.
+// accumulate, bucket_fixup, reduce -> 7 events, recorded on the MSM's stream.
 static constexpr int MSM_NPHASES = 6;
 struct MsmPhaseEvents {
   hipEvent_t ev[MSM_NPHASES + 1];
 };
 
-// result (device, G1Affine) = sum_i scalars[i] * bases[i]; scalars Montgomery Fr,
-// bases affine Montgomery Fq (halo2curves layout).  Asynchronous on `st`.
+// sum_i scalars[i] * bases[i]; scalars Montgomery Fr, bases affine Montgomery Fq
+// (halo2curves layout).  Asynchronous on `st`.  If d_out != nullptr the affine
+// result is written there by one device lane; otherwise the W window sums are
+// left in ws->windows (G1xyzz[ws->last_W]) for msm_windows_host_finish.
 hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWorkspace* ws,
                    const MsmConfig& cfg, G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof = nullptr);
+G1Affine msm_windows_host_finish(const G1xyzz* h_windows, int W, int c);
 void msm_free(MsmWorkspace* ws);
 
 }  // namespace h2g

@@ -8,16 +8,22 @@
 //   1. digits     : Montgomery -> canonical, signed c-bit windows (|d| <= 2^(c-1)),
 //                   key = window*NB + |d|-1, value = point index | sign << 31
 //   2. sort       : LSD radix sort of (key, value) over the key bits (rocprim)
-//   3. bounds     : bucket [start, end) from the sorted keys
-//   4. items      : buckets split into work items of <= item_len points
-//                   (load balance for skewed scalar distributions)
-//   5. accumulate : one thread per item, XYZZ += affine (madd-2008-s), with the
-//                   bases gathered by sorted index (64 B per point read)
-//   6. bucket sum : per bucket, sum its item partials
-//   7. segments   : per (window, segment of SEG buckets) running sums
+//   3. bounds     : bucket [start, end) from the sorted keys, count of valid entries
+//   4. accumulate : the sorted array is cut into fixed chunks of L entries, one
+//                   thread per chunk (every thread does exactly L mixed additions,
+//                   whatever the bucket sizes -> no load imbalance, also for skewed
+//                   scalars).  XYZZ += affine (madd-2008-s), bases gathered by
+//                   sorted index.  Buckets wholly inside a chunk are written
+//                   directly; a chunk's first/last run that crosses a chunk
+//                   boundary is written to a boundary slot.
+//   5. fixup      : buckets spanning chunks sum their boundary slots (one thread,
+//                   or a whole workgroup for buckets spanning > 32 chunks)
+//   6. segments   : per (window, segment of SEG buckets) running sums
 //                   sum_j (j+1) B_j = S_local + offset * R
-//   8. windows    : per window tree reduction of segment results in LDS
-//   9. final      : Horner over windows (c doublings each), to affine
+//   7. windows    : per window tree reduction of segment results in LDS
+//   8. final      : Horner over windows (c doublings each), to affine -- on the
+//                   host for host-returning entry points (a single-lane chain of
+//                   ~250 doublings is latency-bound on the GPU), else one device lane.
 // The result is the unique affine point, so it is bit-identical to any other
 // correct MSM (e.g. the CPU restatement in oracle/) regardless of summation order.
 #include <hipcub/hipcub.hpp>
@@ -26,17 +32,18 @@
 
 namespace h2g {
 
-static constexpr int MSM_SEG = 64;        // buckets per reduction segment
+static constexpr int MSM_SEG = 64;  // buckets per reduction segment
 static constexpr int MSM_THREADS = 256;
+static constexpr uint32_t MSM_SMALL = 32;  // fixup: max chunk pieces summed by one thread
 
-static inline int windows_for(int c) { return (255 + c - 1) / c; }
+int msm_windows_for(int c) { return (255 + c - 1) / c; }
 
 int msm_choose_c(size_t n) {
   if (n < 4) return 2;
   int best_c = 2;
   double best = 1e300;
   for (int c = 2; c <= 22; c++) {
-    const double W = windows_for(c);
+    const double W = msm_windows_for(c);
     const double cost = W * ((double)n + 2.8 * (double)(1ull << (c - 1)));
     if (cost < best) {
       best = cost;
@@ -94,94 +101,99 @@ msm_digits_kernel(const Fr* __restrict__ scalars, size_t n, int c, int W, uint32
   }
 }
 
-// 3. bucket bounds ------------------------------------------------------------
+// 3. bucket bounds + valid count -------------------------------------------------
 __global__ void msm_bounds_kernel(const uint32_t* __restrict__ keys, size_t total, uint32_t sentinel,
-                                  uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
+                                  uint32_t* __restrict__ start, uint32_t* __restrict__ end,
+                                  uint32_t* __restrict__ valid) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= total) return;
   const uint32_t k = keys[i];
   if (k == sentinel) return;
+  const bool last = (i == total - 1) || keys[i + 1] != k;
   if (i == 0 || keys[i - 1] != k) start[k] = (uint32_t)i;
-  if (i == total - 1 || keys[i + 1] != k) end[k] = (uint32_t)(i + 1);
-}
-
-// 4. work items ---------------------------------------------------------------
-__global__ void msm_item_count_kernel(const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
-                                      uint32_t nbt, uint32_t L, uint32_t* __restrict__ cnt) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b > nbt) return;
-  if (b == nbt) {
-    cnt[b] = 0;
-    return;
+  if (last) {
+    end[k] = (uint32_t)(i + 1);
+    if (i == total - 1 || keys[i + 1] == sentinel) *valid = (uint32_t)(i + 1);
   }
-  const uint32_t c = end[b] - start[b];
-  cnt[b] = (c + L - 1) / L;
 }
 
-// 5. accumulation ---------------------------------------------------------------
+// 4. chunked accumulation ----------------------------------------------------------
+__device__ __forceinline__ void msm_emit(uint32_t key, const G1xyzz& acc, bool first, uint32_t lo, uint32_t hi,
+                                         uint32_t t, const uint32_t* __restrict__ start,
+                                         const uint32_t* __restrict__ end, G1xyzz* __restrict__ buckets,
+                                         G1xyzz* __restrict__ bnd) {
+  if (start[key] >= lo && end[key] <= hi) buckets[key] = acc;
+  else bnd[2 * (size_t)t + (first ? 0 : 1)] = acc;
+}
+
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ vals,
-               const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
-               const uint32_t* __restrict__ item_off, uint32_t nbt,
-               uint32_t L, G1xyzz* __restrict__ partials) {
-  const uint32_t it = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t total = item_off[nbt];
-  if (it >= total) return;
-  // bucket of this item: largest b with item_off[b] <= it
-  uint32_t lo = 0, hi = nbt;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (item_off[mid] <= it) lo = mid;
-    else hi = mid;
-  }
-  const uint32_t b = lo;
-  const uint32_t j = it - item_off[b];
-  const uint32_t s = start[b] + j * L;
-  uint32_t e = s + L;
-  if (e > end[b]) e = end[b];
+msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ keys,
+               const uint32_t* __restrict__ vals, const uint32_t* __restrict__ start,
+               const uint32_t* __restrict__ end, const uint32_t* __restrict__ valid_p, uint32_t L,
+               G1xyzz* __restrict__ buckets, G1xyzz* __restrict__ bnd) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t valid = *valid_p;
+  const uint32_t lo = t * L;
+  if (lo >= valid) return;
+  const uint32_t hi = lo + L < valid ? lo + L : valid;
+  uint32_t key = keys[lo];
+  bool first = true;
   G1xyzz acc = G1xyzz::identity();
-  for (uint32_t p = s; p < e; p++) {
+  for (uint32_t p = lo; p < hi; p++) {
+    const uint32_t k2 = keys[p];
     const uint32_t v = vals[p];
     G1Affine pt = ld_aff(bases + (v & 0x7fffffffu));
+    if (k2 != key) {
+      msm_emit(key, acc, first, lo, hi, t, start, end, buckets, bnd);
+      first = false;
+      key = k2;
+      acc = G1xyzz::identity();
+    }
     if (v >> 31) pt = affine_neg(pt);
     acc = xyzz_madd(acc, pt);
   }
-  partials[it] = acc;
+  msm_emit(key, acc, first, lo, hi, t, start, end, buckets, bnd);
 }
 
-// 6. per-bucket sum of item partials ------------------------------------------------
-//    Buckets with <= MSM_SMALL items are summed by one thread; larger ones (skewed
-//    scalar distributions, e.g. many equal coefficients) are queued and reduced by
-//    whole workgroups in msm_big_bucket_kernel.
-static constexpr uint32_t MSM_SMALL = 32;
+// 5. buckets spanning chunks -----------------------------------------------------
+__device__ __forceinline__ const G1xyzz& msm_piece(const G1xyzz* bnd, uint32_t t, uint32_t t0, uint32_t bs,
+                                                   uint32_t L) {
+  // chunk t0: the bucket is its last run (slot 1) unless it also starts the chunk
+  // (slot 0); every later chunk sees it as its first run (slot 0).
+  return bnd[2 * (size_t)t + ((t == t0 && bs != t0 * L) ? 1 : 0)];
+}
+
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_bucket_sum_kernel(const G1xyzz* __restrict__ partials, const uint32_t* __restrict__ item_off, uint32_t nbt,
-                      G1xyzz* __restrict__ buckets, uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ start,
+                 const uint32_t* __restrict__ end, uint32_t nbt, uint32_t L, G1xyzz* __restrict__ buckets,
+                 uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nbt) return;
-  const uint32_t o = item_off[b], e = item_off[b + 1];
-  if (e - o > MSM_SMALL) {
-    const uint32_t slot = atomicAdd(big_count, 1u);
-    big_list[slot] = b;
+  const uint32_t bs = start[b], be = end[b];
+  if (be <= bs) return;  // empty (buckets[] is zero = identity)
+  const uint32_t t0 = bs / L, t1 = (be - 1) / L;
+  if (t0 == t1) return;  // written by the accumulation kernel
+  if (t1 - t0 + 1 > MSM_SMALL) {
+    big_list[atomicAdd(big_count, 1u)] = b;
     return;
   }
-  G1xyzz acc = G1xyzz::identity();
-  if (e > o) acc = partials[o];
-  for (uint32_t j = o + 1; j < e; j++) acc = xyzz_add(acc, partials[j]);
+  G1xyzz acc = msm_piece(bnd, t0, t0, bs, L);
+  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, msm_piece(bnd, t, t0, bs, L));
   buckets[b] = acc;
 }
 
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_big_bucket_kernel(const G1xyzz* __restrict__ partials, const uint32_t* __restrict__ item_off,
-                      const uint32_t* __restrict__ big_list, const uint32_t* __restrict__ big_count,
-                      G1xyzz* __restrict__ buckets) {
+msm_big_bucket_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ start,
+                      const uint32_t* __restrict__ end, uint32_t L, const uint32_t* __restrict__ big_list,
+                      const uint32_t* __restrict__ big_count, G1xyzz* __restrict__ buckets) {
   __shared__ G1xyzz sh[MSM_THREADS];
   const uint32_t nbig = *big_count;
   for (uint32_t q = blockIdx.x; q < nbig; q += gridDim.x) {
     const uint32_t b = big_list[q];
-    const uint32_t o = item_off[b], e = item_off[b + 1];
+    const uint32_t bs = start[b], be = end[b];
+    const uint32_t t0 = bs / L, t1 = (be - 1) / L;
     G1xyzz acc = G1xyzz::identity();
-    for (uint32_t j = o + threadIdx.x; j < e; j += blockDim.x) acc = xyzz_add(acc, partials[j]);
+    for (uint32_t t = t0 + threadIdx.x; t <= t1; t += blockDim.x) acc = xyzz_add(acc, msm_piece(bnd, t, t0, bs, L));
     sh[threadIdx.x] = acc;
     __syncthreads();
     for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
@@ -193,7 +205,7 @@ msm_big_bucket_kernel(const G1xyzz* __restrict__ partials, const uint32_t* __res
   }
 }
 
-// 7. segment running sums: seg result = sum_{j in seg} (j+1) B_j ------------------
+// 6. segment running sums: seg result = sum_{j in seg} (j+1) B_j ------------------
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_segment_kernel(const G1xyzz* __restrict__ buckets, uint32_t NB, int W, G1xyzz* __restrict__ segs) {
   const uint32_t nseg = NB / MSM_SEG > 0 ? NB / MSM_SEG : 1;
@@ -213,7 +225,7 @@ msm_segment_kernel(const G1xyzz* __restrict__ buckets, uint32_t NB, int W, G1xyz
   segs[t] = S;
 }
 
-// 8. per-window reduction ------------------------------------------------------------
+// 7. per-window reduction ------------------------------------------------------------
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_window_kernel(const G1xyzz* __restrict__ segs, uint32_t nseg, G1xyzz* __restrict__ windows) {
   __shared__ G1xyzz sh[MSM_THREADS];
@@ -229,15 +241,23 @@ msm_window_kernel(const G1xyzz* __restrict__ segs, uint32_t nseg, G1xyzz* __rest
   if (threadIdx.x == 0) windows[w] = sh[0];
 }
 
-// 9. final Horner over windows -------------------------------------------------------
-__global__ void msm_final_kernel(const G1xyzz* __restrict__ windows, int W, int c, G1Affine* out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// 8. final Horner over windows -------------------------------------------------------
+__host__ __device__ G1Affine msm_combine_windows(const G1xyzz* windows, int W, int c) {
   G1xyzz acc = windows[W - 1];
   for (int w = W - 2; w >= 0; w--) {
     for (int d = 0; d < c; d++) acc = xyzz_dbl(acc);
     acc = xyzz_add(acc, windows[w]);
   }
-  *out = xyzz_to_affine(acc);
+  return xyzz_to_affine(acc);
+}
+
+__global__ void msm_final_kernel(const G1xyzz* __restrict__ windows, int W, int c, G1Affine* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  *out = msm_combine_windows(windows, W, c);
+}
+
+G1Affine msm_windows_host_finish(const G1xyzz* h_windows, int W, int c) {
+  return msm_combine_windows(h_windows, W, c);
 }
 
 // ------------------------------------------------------------------------------------
@@ -257,6 +277,7 @@ void msm_free(MsmWorkspace* ws) {
   }
   ws->cap_n = 0;
   ws->cap_c = 0;
+  ws->cap_L = 0;
   ws->sort_tmp_bytes = ws->scan_tmp_bytes = 0;
 }
 
@@ -266,65 +287,68 @@ void msm_free(MsmWorkspace* ws) {
     if (_e != hipSuccess) return _e;    \
   } while (0)
 
+uint32_t msm_chunk_len(size_t total) {
+  // ~4 resident waves per SIMD x 256 CUs x 64 lanes, several rounds deep
+  uint64_t L = total / (256ull * 4 * 4 * 64 * 4);
+  if (L < 8) L = 8;
+  if (L > 128) L = 128;
+  return (uint32_t)L;
+}
+
 hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWorkspace* ws,
                    const MsmConfig& cfg, G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof) {
 #define H2G_PHASE(i) \
   if (prof) H2G_TRY(hipEventRecord(prof->ev[i], st))
   const int c = cfg.c > 0 ? cfg.c : msm_choose_c(n);
-  const int W = windows_for(c);
+  const int W = msm_windows_for(c);
   const uint32_t NB = 1u << (c - 1);
   const uint32_t nbt = (uint32_t)W * NB;
   const size_t total = n * (size_t)W;
-  uint32_t L = (uint32_t)cfg.item_len;
-  if (L == 0) {
-    const double avg = (double)n / (double)NB;
-    L = 16;
-    while (L < 2 * avg && L < 1024) L <<= 1;
-  }
-  const size_t max_items = total / L + nbt + 1;
+  const uint32_t L = cfg.item_len > 0 ? (uint32_t)cfg.item_len : msm_chunk_len(total);
+  const size_t nchunks = (total + L - 1) / L;
   const uint32_t nseg = NB / MSM_SEG > 0 ? NB / MSM_SEG : 1;
 
-  if (ws->cap_n < n || ws->cap_c != c) {
+  if (ws->cap_n < n || ws->cap_c != c || ws->cap_L != L) {
     H2G_TRY(grow(&ws->keys_in, total * 4));
     H2G_TRY(grow(&ws->keys_out, total * 4));
     H2G_TRY(grow(&ws->vals_in, total * 4));
     H2G_TRY(grow(&ws->vals_out, total * 4));
     H2G_TRY(grow(&ws->bucket_start, (size_t)nbt * 4));
     H2G_TRY(grow(&ws->bucket_end, (size_t)nbt * 4));
-    H2G_TRY(grow(&ws->item_off, ((size_t)nbt + 1) * 4));
-    H2G_TRY(grow(&ws->item_bucket, (size_t)nbt * 4));  // big-bucket list
-    H2G_TRY(grow(&ws->result, 16));                     // big-bucket counter
-    H2G_TRY(grow(&ws->partials, max_items * sizeof(G1xyzz)));
+    H2G_TRY(grow(&ws->item_bucket, (size_t)nbt * 4));         // big-bucket list
+    H2G_TRY(grow(&ws->partials, 2 * nchunks * sizeof(G1xyzz)));  // boundary slots
     H2G_TRY(grow(&ws->buckets, (size_t)nbt * sizeof(G1xyzz)));
     H2G_TRY(grow(&ws->segs, (size_t)W * nseg * sizeof(G1xyzz)));
     H2G_TRY(grow(&ws->windows, (size_t)W * sizeof(G1xyzz)));
-    H2G_TRY(grow(&ws->total_items, ((size_t)nbt + 1) * 4));  // item counts (scan input)
+    H2G_TRY(grow(&ws->result, 16));  // [0] big-bucket count, [1] valid count
     ws->cap_n = n;
     ws->cap_c = c;
+    ws->cap_L = L;
   }
+  ws->last_c = c;
+  ws->last_W = W;
   uint32_t* keys_in = (uint32_t*)ws->keys_in;
   uint32_t* keys_out = (uint32_t*)ws->keys_out;
   uint32_t* vals_in = (uint32_t*)ws->vals_in;
   uint32_t* vals_out = (uint32_t*)ws->vals_out;
   uint32_t* bstart = (uint32_t*)ws->bucket_start;
   uint32_t* bend = (uint32_t*)ws->bucket_end;
-  uint32_t* item_cnt = (uint32_t*)ws->total_items;
-  uint32_t* item_off = (uint32_t*)ws->item_off;
+  uint32_t* counters = (uint32_t*)ws->result;
+  uint32_t* big_count = counters;
+  uint32_t* valid = counters + 1;
+  uint32_t* big_list = (uint32_t*)ws->item_bucket;
+  G1xyzz* buckets = (G1xyzz*)ws->buckets;
+  G1xyzz* bnd = (G1xyzz*)ws->partials;
 
   int key_bits = 1;
   while ((1ull << key_bits) <= (uint64_t)nbt) key_bits++;
 
-  size_t sort_bytes = 0, scan_bytes = 0;
+  size_t sort_bytes = 0;
   H2G_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, keys_in, keys_out, vals_in, vals_out,
                                              (int)total, 0, key_bits, st));
-  H2G_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, item_cnt, item_off, (int)nbt + 1, st));
   if (sort_bytes > ws->sort_tmp_bytes) {
     H2G_TRY(grow(&ws->sort_tmp, sort_bytes));
     ws->sort_tmp_bytes = sort_bytes;
-  }
-  if (scan_bytes > ws->scan_tmp_bytes) {
-    H2G_TRY(grow(&ws->scan_tmp, scan_bytes));
-    ws->scan_tmp_bytes = scan_bytes;
   }
 
   const int T = MSM_THREADS;
@@ -338,28 +362,25 @@ hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWo
   H2G_PHASE(2);
   H2G_TRY(hipMemsetAsync(bstart, 0, (size_t)nbt * 4, st));
   H2G_TRY(hipMemsetAsync(bend, 0, (size_t)nbt * 4, st));
+  H2G_TRY(hipMemsetAsync(counters, 0, 8, st));
+  H2G_TRY(hipMemsetAsync(buckets, 0, (size_t)nbt * sizeof(G1xyzz), st));
   hipLaunchKernelGGL(msm_bounds_kernel, dim3((unsigned)((total + T - 1) / T)), dim3(T), 0, st, keys_out, total,
-                     nbt, bstart, bend);
-  hipLaunchKernelGGL(msm_item_count_kernel, dim3((nbt + 1 + T - 1) / T), dim3(T), 0, st, bstart, bend, nbt, L,
-                     item_cnt);
-  H2G_TRY(hipcub::DeviceScan::ExclusiveSum(ws->scan_tmp, scan_bytes, item_cnt, item_off, (int)nbt + 1, st));
+                     nbt, bstart, bend, valid);
   H2G_PHASE(3);
-  hipLaunchKernelGGL(msm_acc_kernel, dim3((unsigned)((max_items + T - 1) / T)), dim3(T), 0, st, d_bases, vals_out,
-                     bstart, bend, item_off, nbt, L, (G1xyzz*)ws->partials);
+  hipLaunchKernelGGL(msm_acc_kernel, dim3((unsigned)((nchunks + T - 1) / T)), dim3(T), 0, st, d_bases, keys_out,
+                     vals_out, bstart, bend, (const uint32_t*)valid, L, buckets, bnd);
   H2G_PHASE(4);
-  uint32_t* big_list = (uint32_t*)ws->item_bucket;
-  uint32_t* big_count = (uint32_t*)ws->result;
-  H2G_TRY(hipMemsetAsync(big_count, 0, 4, st));
-  hipLaunchKernelGGL(msm_bucket_sum_kernel, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)ws->partials,
-                     item_off, nbt, (G1xyzz*)ws->buckets, big_list, big_count);
-  hipLaunchKernelGGL(msm_big_bucket_kernel, dim3(256), dim3(T), 0, st, (const G1xyzz*)ws->partials, item_off,
-                     (const uint32_t*)big_list, (const uint32_t*)big_count, (G1xyzz*)ws->buckets);
+  hipLaunchKernelGGL(msm_fixup_kernel, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend,
+                     nbt, L, buckets, big_list, big_count);
+  hipLaunchKernelGGL(msm_big_bucket_kernel, dim3(256), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend, L,
+                     (const uint32_t*)big_list, (const uint32_t*)big_count, buckets);
   H2G_PHASE(5);
   hipLaunchKernelGGL(msm_segment_kernel, dim3(((uint32_t)W * nseg + T - 1) / T), dim3(T), 0, st,
-                     (const G1xyzz*)ws->buckets, NB, W, (G1xyzz*)ws->segs);
+                     (const G1xyzz*)buckets, NB, W, (G1xyzz*)ws->segs);
   hipLaunchKernelGGL(msm_window_kernel, dim3(W), dim3(MSM_THREADS), 0, st, (const G1xyzz*)ws->segs, nseg,
                      (G1xyzz*)ws->windows);
-  hipLaunchKernelGGL(msm_final_kernel, dim3(1), dim3(64), 0, st, (const G1xyzz*)ws->windows, W, c, d_out);
+  if (d_out)
+    hipLaunchKernelGGL(msm_final_kernel, dim3(1), dim3(64), 0, st, (const G1xyzz*)ws->windows, W, c, d_out);
   H2G_TRY(hipGetLastError());
   H2G_PHASE(6);
 #undef H2G_PHASE

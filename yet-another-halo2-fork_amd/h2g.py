@@ -42,6 +42,7 @@ _SIGS = {
     "h2g_msm_with_cached_inputs": ([U64, U64, SZ, U64P, ctypes.POINTER(I32)], I32),
     "h2g_msm_dev": ([VP, VP, SZ, VP, VP], I32),
     "h2g_msm_dev_cfg": ([VP, VP, SZ, I32, VP, VP], I32),
+    "h2g_msm_dev_host": ([VP, VP, SZ, I32, U64P, ctypes.POINTER(I32), VP], I32),
     "h2g_descriptor_device_ptr": ([U64, ctypes.POINTER(VP), ctypes.POINTER(SZ)], I32),
     "h2g_srs_setup_dev": ([U64P, SZ, VP, VP], I32),
     "h2g_fft": ([U64P, U32, U64P], I32),
@@ -77,7 +78,7 @@ _SIGS = {
     "h2g_profile_msm_collect": ([ctypes.POINTER(ctypes.c_float), I32, ctypes.POINTER(I32), ctypes.POINTER(I32)], I32),
 }
 
-MSM_PHASES = ("digits", "sort", "bucket_bounds", "accumulate", "bucket_sum", "reduce")
+MSM_PHASES = ("digits", "sort", "bucket_bounds", "accumulate", "bucket_fixup", "reduce")
 
 _lib = None
 
@@ -233,6 +234,14 @@ class DevBuf:
 
 def msm_dev(d_scalars, d_bases, n, d_out, window_bits=0, stream=None):
     check(lib().h2g_msm_dev_cfg(VP(d_scalars), VP(d_bases), n, window_bits, VP(d_out), VP(stream) if stream else None))
+
+
+def msm_dev_host(d_scalars, d_bases, n, window_bits=0, stream=None):
+    out = np.zeros(8, dtype=np.uint64)
+    ident = I32(0)
+    check(lib().h2g_msm_dev_host(VP(d_scalars), VP(d_bases), n, window_bits, p64(out), ctypes.byref(ident),
+                                 VP(stream) if stream else None))
+    return out
 
 
 def srs_setup_dev(s, n, d_out, stream=None):
