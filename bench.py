@@ -183,6 +183,7 @@ def main():
             "phases_ms": {k: round(v / max(calls, 1), 4) for k, v in phases.items()},
             "msm_device_ms": round(total_phase_ms, 4),
         }
+        line["ntt"] = ntt_extras(h2g, torch, dev, stream)
         if not args.no_cpu_baseline and world == 1:
             cb = cpu_baseline()
             line["cpu_baseline"] = cb
@@ -192,6 +193,46 @@ def main():
     h2g.shutdown()
     if world > 1:
         dist.destroy_process_group()
+
+
+def ntt_extras(h2g, torch, dev, stream, reps=5):
+    """Side measurements (not the headline value): device-resident radix-2^m NTT
+    (best_fft) at 2^20 (BASELINE configs[1]) and 2^22, and coeff_to_extended
+    k=22 -> 2^23 (the quotient-domain coset NTT of configs[2..3]).
+    Algorithmic bytes: 64 B/element (read + write once)."""
+    out = {}
+    rng = np.random.default_rng(9)
+    for log_n in (20, 22):
+        n = 1 << log_n
+        a = torch.from_numpy(random_scalars(rng, n).view(np.int64)).to(dev)
+        d = h2g.Domain(2, log_n)
+        w = d.consts[0]
+        h2g.fft_dev(a.data_ptr(), log_n, w, stream)
+        torch.cuda.synchronize()
+        t = h2g.Timer(stream)
+        t.start()
+        for _ in range(reps):
+            h2g.fft_dev(a.data_ptr(), log_n, w, stream)
+        ms = t.stop_ms() / reps
+        d.close()
+        out[f"fft_2^{log_n}_ms"] = round(ms, 4)
+        out[f"fft_2^{log_n}_GBs"] = round(64 * n / (ms * 1e-3) / 1e9, 1)
+        out[f"fft_2^{log_n}_modmul_per_s"] = round((n // 2) * log_n / (ms * 1e-3), 1)
+    k = 22
+    d = h2g.Domain(3, k)
+    a = torch.from_numpy(random_scalars(rng, 1 << k).view(np.int64)).to(dev)
+    o = torch.empty((d.extended_len, 4), dtype=torch.int64, device=dev)
+    h2g.check(h2g.lib().h2g_coeff_to_extended_dev(d.h, h2g.VP(a.data_ptr()), h2g.VP(o.data_ptr()), h2g.VP(stream)))
+    torch.cuda.synchronize()
+    t = h2g.Timer(stream)
+    t.start()
+    for _ in range(reps):
+        h2g.check(h2g.lib().h2g_coeff_to_extended_dev(d.h, h2g.VP(a.data_ptr()), h2g.VP(o.data_ptr()),
+                                                      h2g.VP(stream)))
+    ms = t.stop_ms() / reps
+    d.close()
+    out["coeff_to_extended_k22_ms"] = round(ms, 4)
+    return out
 
 
 def h2g_choose_c(n):

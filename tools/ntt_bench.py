@@ -1,0 +1,27 @@
+"""Time device NTTs through the C ABI (for rocprofv3 --kernel-trace --stats)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "yet-another-halo2-fork_amd"))
+import h2g  # noqa: E402
+
+h2g.init([0])
+rng = np.random.default_rng(1)
+for log_n in [int(x) for x in (sys.argv[1:] or ["20", "22"])]:
+    n = 1 << log_n
+    a = rng.integers(0, 2**62, size=(n, 4), dtype=np.int64).astype(np.uint64)
+    d = h2g.DevBuf.from_array(a)
+    dom = h2g.Domain(2, log_n)
+    w = dom.consts[0]
+    h2g.fft_dev(d.ptr, log_n, w)
+    h2g.check(h2g.lib().h2g_synchronize())
+    t = h2g.Timer()
+    t.start()
+    for _ in range(10):
+        h2g.fft_dev(d.ptr, log_n, w)
+    ms = t.stop_ms() / 10
+    print(f"fft 2^{log_n}: {ms:.4f} ms  {(n // 2) * log_n / ms / 1e6:.1f} Mbfly/s")
+h2g.shutdown()

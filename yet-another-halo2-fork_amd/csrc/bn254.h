@@ -133,8 +133,11 @@ H2G_HD Fe<P> dbl(const Fe<P>& a) {
 // One inline-asm block per product: hipcc pads each block boundary with an
 // s_nop, but grouping a whole column per block measured
 // slower (118 vs 125 Gmodmul/s) -- the compiler interleaves small blocks better.
+// Not `volatile`: the scheduler may interleave the mac chains of independent
+// products (a volatile asm statement is a scheduling barrier, which serialises
+// e.g. the 4 independent butterflies of an NTT stage into one latency chain).
 __device__ __forceinline__ void h2g_mac(uint64_t& lo, uint32_t& hi, uint32_t a, uint32_t b) {
-  asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
                : "+v"(lo), "+v"(hi)
                : "v"(a), "v"(b)
                : "vcc");

@@ -5,7 +5,12 @@
 namespace h2g {
 
 static constexpr int NTT_SMALL_MAX_LOG = 10;  // whole transform in one block up to 2^10
-static constexpr int NTT_MAX_PASS_LOG = 8;    // LDS sub-transform size per HBM pass
+static constexpr int NTT_MAX_PASSES = 6;      // passes of 3..6 bits: N up to 2^28
+
+struct NttPlanLg {
+  int p = 0;
+  int lg[NTT_MAX_PASSES] = {0, 0, 0, 0, 0, 0};
+};
 
 struct NttTables {
   int L = 0;  // log2 N
@@ -33,7 +38,7 @@ struct NttArgs {
   Fr out_z1, out_z2;
 };
 
-void ntt_split(int L, int* P, int lg[4]);
+void ntt_split(int L, int* P, int lg[NTT_MAX_PASSES]);
 hipError_t ntt_build_tables(NttTables* t, const Fr& omega, int L, hipStream_t st);
 void ntt_free_tables(NttTables* t);
 hipError_t ntt_run(const NttArgs& a, hipStream_t st);

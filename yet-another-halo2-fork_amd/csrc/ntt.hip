@@ -1,4 +1,4 @@
-// ntt.hip -- radix-2^m LDS-tiled NTT over BN254 Fr for gfx950.
+// ntt.hip -- register-resident radix-2^m NTT over BN254 Fr for gfx950.
 //
 // Computes exactly what halo2curves' best_fft computes (natural order in,
 // natural order out, y_k = sum_i a_i w^(ik)), as called by
@@ -6,19 +6,28 @@
 // plus the fused pre/post maps of coeff_to_extended / extended_to_coeff /
 // lagrange_to_coeff (domain.rs:216-293).
 //
-// Algorithm: N = N_1 * ... * N_P (each N_p <= 2^8).  With i = i_low + (L_p/N_p) i_p
-// the pass-p DFT runs over i_p in LDS, then multiplies by w^{(N/L_p) i_low k_p}
-// (in place).  The last pass reads contiguous runs and writes natural order
-// (digit reversal folded into its store).  Every pass touches HBM once:
-// 64 B/element/pass of algorithmic traffic, reads and writes in >= 256 B runs
-// (G = 8 adjacent columns of 32-B elements).  Twiddles come from a 2-level
-// table w^E = lo[E mod 2^b] * hi[E >> b] (both L2-resident).
+// Decomposition: N = N_0 * N_1 * ... * N_{P-1}, every N_p = 2^m_p with
+// 3 <= m_p <= 6 and the last pass 2^6.  With i = i_low + (L_p/N_p) i_p, pass p
+// runs the size-N_p DFT over i_p, then multiplies by w^{(N/L_p) i_low k_p}, in
+// place; the last pass reads contiguous runs and writes natural order (digit
+// reversal folded into its store).  Each pass touches HBM once (64 B/element).
+//
+// One wavefront owns CPW = 64 / 2^(m-3) adjacent columns; every lane holds 8
+// elements of one column in registers.  A 2^m-point DIF = one in-register
+// radix-8 round on the top 3 index bits, (m-3) lane<->register bit swaps by
+// __shfl_xor (no LDS staging, no barriers), and a second in-register round on
+// the low m-3 bits.  Global accesses are runs of >= 8 x 32 B across the lanes
+// of one instruction.  Inter-pass twiddles come from a 2-level table
+// w^E = lo[E mod 2^b] * hi[E >> b] (both L2-resident).
 #include "ntt.h"
 
 namespace h2g {
 
-static constexpr int NTT_G = 8;        // columns per block (8 x 32 B = 256 B runs)
-static constexpr int NTT_THREADS = 256;
+static constexpr int NTT_WAVES = 4;  // waves per block (independent; no block barriers after the table)
+static constexpr int NTT_THREADS = 64 * NTT_WAVES;
+#ifndef NTT_MIN_WAVES
+#define NTT_MIN_WAVES 2  // waves per SIMD the register allocation must admit
+#endif
 
 __device__ __forceinline__ Fr ld_fr(const Fr* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
@@ -38,146 +47,204 @@ __device__ __forceinline__ Fr twiddle(const NttTables& t, uint64_t e) {
   return t.lo[e & ((1ull << t.b) - 1)] * t.hi[e >> t.b];
 }
 
-// In-LDS radix-2 DIF over `cols` columns of length 2^m (column c at s[c*len]).
-// Input natural order, output bit-reversed.  `w` holds w_len^j, j < len/2.
-__device__ __forceinline__ void lds_dif(Fr* s, const Fr* w, int m, int cols) {
-  const int len = 1 << m;
-  const int nbf = cols * (len >> 1);
-  for (int hlog = m - 1; hlog >= 0; hlog--) {
-    const int h = 1 << hlog;
-    for (int t = threadIdx.x; t < nbf; t += blockDim.x) {
-      const int c = t >> (m - 1);
-      const int r = t & ((len >> 1) - 1);
-      const int j = r & (h - 1);
-      const int i = ((r >> hlog) << (hlog + 1)) + j;
-      Fr* col = s + c * len;
-      const Fr u = col[i];
-      const Fr v = col[i + h];
-      col[i] = u + v;
-      const Fr d = u - v;
-      col[i + h] = (hlog == m - 1) ? d * w[j] : d * w[j << (m - 1 - hlog)];
-    }
-    __syncthreads();
-  }
+__device__ __forceinline__ Fr shfl_xor_fr(const Fr& v, int mask) {
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = (uint32_t)__shfl_xor((int)v.l[i], mask);
+  return r;
 }
 
-__device__ __forceinline__ int brev(int x, int m) { return (int)(__brev((unsigned)x) >> (32 - m)); }
+__device__ __forceinline__ Fr fr_select(int c, const Fr& a, const Fr& b) {
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = c ? a.l[i] : b.l[i];
+  return r;
+}
+
+// y mod 3 for 64-bit y with 32-bit arithmetic (2^32 = 1 mod 3)
+__device__ __forceinline__ uint32_t mod3(uint64_t y) {
+  return ((uint32_t)(y >> 32) % 3u + (uint32_t)y % 3u) % 3u;
+}
+
+__device__ __forceinline__ uint32_t brev_bits(uint32_t x, int m) { return __brev(x) >> (32 - m); }
+
+// In-register DIF of 2^M-point columns.  Lane = c + CPW * rg; register q of the
+// lane initially holds row r = rg + LPC * q.  `w[j] = w_{2^M}^j`, j < 2^(M-1).
+// After run(), register q holds DIF position rpos(q, rg) (output index
+// k = bitrev_M(rpos)).
+template <int M>
+struct WaveDif {
+  static constexpr int LPC = 1 << (M - 3);  // lanes per column
+  static constexpr int CPW = 64 / LPC;      // columns per wave
+
+  __device__ static __forceinline__ void run(Fr x[8], const Fr* w, int rg) {
+    // round A: row bits M-1..M-3 live in the register index
+#pragma unroll
+    for (int t = 2; t >= 0; t--) {
+      const int htlog = (M - 3) + t;
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        const int q = ((p >> t) << (t + 1)) | (p & ((1 << t) - 1));
+        const int j = rg + (p & ((1 << t) - 1)) * LPC;
+        const Fr a = x[q], b = x[q + (1 << t)];
+        x[q] = a + b;
+        x[q + (1 << t)] = (a - b) * w[j << (M - 1 - htlog)];
+      }
+    }
+    // swap register bit b <-> lane bit b (lane index bit log2(CPW) + b), b < M-3
+#pragma unroll
+    for (int b = 0; b < M - 3; b++) {
+      const int lb = (rg >> b) & 1;
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        const int q = ((p >> b) << (b + 1)) | (p & ((1 << b) - 1));
+        // value selects only (a data-dependent register index would spill x[] to scratch)
+        const Fr lo_v = x[q], hi_v = x[q | (1 << b)];
+        const Fr recv = shfl_xor_fr(fr_select(lb, lo_v, hi_v), CPW << b);
+        x[q] = fr_select(lb, recv, lo_v);
+        x[q | (1 << b)] = fr_select(lb, hi_v, recv);
+      }
+    }
+    // round B: row bits M-4..0 now live in register bits M-4..0
+#pragma unroll
+    for (int t = M - 4; t >= 0; t--) {
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        const int q = ((p >> t) << (t + 1)) | (p & ((1 << t) - 1));
+        const int j = q & ((1 << t) - 1);
+        const Fr a = x[q], b = x[q + (1 << t)];
+        x[q] = a + b;
+        x[q + (1 << t)] = (a - b) * w[j << (M - 1 - t)];
+      }
+    }
+  }
+
+  // DIF position held by register q of lane rg after run()
+  __device__ static __forceinline__ uint32_t rpos(int q, int rg) {
+    constexpr int LB = M - 3;
+    const uint32_t lowmask = (1u << LB) - 1;
+    const uint32_t lo = (uint32_t)q & lowmask;                              // row bits < LB
+    const uint32_t mid = (uint32_t)rg & lowmask;                            // row bits LB..2LB-1
+    const uint32_t hi = ((uint32_t)q >> LB) << LB;                          // untouched register bits
+    return lo + ((mid | hi) << LB);
+  }
+};
 
 // ---------------------------------------------------------------------------
-// Generic (non-last) pass, in place.  grid = N / (N_p * G) blocks.
-//   L_p = 2^lrem (remaining length including this pass), S = L_p / N_p.
-//   Optional input map on pass 0 (coset extend): read `in` (length n_in) with
-//   zero padding and multiply by zeta powers (domain.rs:325-341).
-__global__ void __launch_bounds__(NTT_THREADS)
-ntt_pass_kernel(Fr* data, const Fr* in, uint64_t n_in, NttTables tab, int L, int m, int lrem,
-                int distribute, Fr z1, Fr z2) {
-  extern __shared__ __align__(16) unsigned char smem_raw[];
-  Fr* s = reinterpret_cast<Fr*>(smem_raw);
-  const int Np = 1 << m;
-  Fr* w = s + NTT_G * Np;
-  const uint64_t S = 1ull << (lrem - m);
-  const uint64_t groups = S / NTT_G;
-  const uint64_t q = blockIdx.x / groups;
-  const uint64_t g = blockIdx.x % groups;
-  const uint64_t base = (q << lrem) + g * NTT_G;
-  // inner twiddles w_{Np}^j = w^{(N/Np) j}
-  for (int j = threadIdx.x; j < Np / 2; j += blockDim.x) w[j] = twiddle(tab, (uint64_t)j << (L - m));
-  for (int t = threadIdx.x; t < NTT_G * Np; t += blockDim.x) {
-    const int c = t % NTT_G, r = t / NTT_G;
-    const uint64_t pos = base + c + (uint64_t)r * S;
-    Fr v;
+// Generic (non-last) pass, 2^M-point sub-transforms, in place on `data`.
+//   L_p = 2^lrem (remaining length including this pass), S = L_p / 2^M.
+//   Pass 0 reads `in` (n_in valid elements, zero padding beyond) and, if
+//   `distribute`, multiplies element i by zeta^(i mod 3) (domain.rs:325-341).
+template <int M>
+__global__ void __launch_bounds__(NTT_THREADS, NTT_MIN_WAVES)
+ntt_pass_kernel(Fr* data, const Fr* in, uint64_t n_in, NttTables tab, int L, int lrem, int distribute, Fr z1,
+                Fr z2) {
+  using D = WaveDif<M>;
+  __shared__ Fr w[1 << (M - 1)];
+  for (int j = threadIdx.x; j < (1 << (M - 1)); j += blockDim.x) w[j] = twiddle(tab, (uint64_t)j << (L - M));
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * NTT_WAVES + (threadIdx.x >> 6);
+  if (wave >= (1ull << L) / ((1ull << M) * D::CPW)) return;
+  const uint64_t S = 1ull << (lrem - M);
+  const uint64_t groups = S / D::CPW;
+  const uint64_t q = wave / groups;
+  const uint64_t g = wave % groups;
+  const uint64_t base = (q << lrem) + g * D::CPW;
+  const int c = lane % D::CPW, rg = lane / D::CPW;
+  Fr x[8];
+#pragma unroll
+  for (int qq = 0; qq < 8; qq++) {
+    const uint64_t pos = base + c + (uint64_t)(rg + D::LPC * qq) * S;
     if (in) {
       if (pos < n_in) {
-        v = ld_fr(in + pos);
+        Fr v = ld_fr(in + pos);
         if (distribute) {
-          const uint32_t md = (uint32_t)(pos % 3);
-          if (md == 1) v = v * z1;
-          else if (md == 2) v = v * z2;
+          const uint32_t md = mod3(pos);
+          v = v * fr_select(md == 1, z1, fr_select(md == 2, z2, Fr::one()));
         }
+        x[qq] = v;
       } else {
-        v = Fr::zero();
+        x[qq] = Fr::zero();
       }
     } else {
-      v = ld_fr(data + pos);
+      x[qq] = ld_fr(data + pos);
     }
-    s[c * Np + r] = v;
   }
-  __syncthreads();
-  lds_dif(s, w, m, NTT_G);
-  const uint64_t stride_prefix = (uint64_t)1 << (L - lrem);  // N / L_p
-  for (int t = threadIdx.x; t < NTT_G * Np; t += blockDim.x) {
-    const int c = t % NTT_G, k = t / NTT_G;
-    Fr v = s[c * Np + brev(k, m)];
-    const uint64_t ilow = g * NTT_G + c;
-    const uint64_t e = (stride_prefix * ilow * (uint64_t)k) & ((1ull << L) - 1);
+  D::run(x, w, rg);
+  const uint64_t ilow_scaled = (g * D::CPW + c) << (L - lrem);  // (N / L_p) * i_low
+#pragma unroll
+  for (int qq = 0; qq < 8; qq++) {
+    const uint32_t k = brev_bits(D::rpos(qq, rg), M);
+    const uint64_t e = ilow_scaled * k;
+    Fr v = x[qq];
     if (e) v = v * twiddle(tab, e);
     st_fr(data + base + c + (uint64_t)k * S, v);
   }
 }
 
 // ---------------------------------------------------------------------------
-// Last pass: contiguous runs of N_P, output in natural order.
-//   pos = k1 (N/N1) + m_idx N_P + i_P ;  y = k1 + N1 * mid_nat(m_idx) + (N/N_P) k_P
-//   digits of m_idx (position order, least significant = k_{P-1}) are given by
-//   lg[1..P-2].  Epilogue: multiply by `scale` and, if `distribute`, by the
-//   zeta power of y mod 3; drop y >= out_len (truncation, domain.rs:288-290).
-__global__ void __launch_bounds__(NTT_THREADS)
-ntt_last_kernel(const Fr* data, Fr* out, uint64_t out_len, NttTables tab, int L, int P, int4 lg,
-                int has_scale, Fr scale, int distribute, Fr z1, Fr z2) {
-  extern __shared__ __align__(16) unsigned char smem_raw[];
-  Fr* s = reinterpret_cast<Fr*>(smem_raw);
-  const int lgs[4] = {lg.x, lg.y, lg.z, lg.w};
-  const int m = lgs[P - 1];
-  const int Np = 1 << m;
-  const int l1 = lgs[0];
-  Fr* w = s + NTT_G * Np;
-  const uint64_t N1 = 1ull << l1;
-  const uint64_t groups = N1 / NTT_G;
-  const uint64_t midx = blockIdx.x / groups;
-  const uint64_t g = blockIdx.x % groups;
-  // decode middle digits: m_idx = k2 * (N3..N_{P-1}) + ... + k_{P-1}
+// Last pass (2^6-point columns): contiguous runs, output in natural order.
+//   pos = k_0 (N/N_0) + m_idx 2^6 + i ;  y = k_0 + mid_nat(m_idx) + (N/2^6) k
+//   Epilogue: multiply by `scale` and, if `distribute`, by the zeta power of
+//   y mod 3; drop y >= out_len (truncation, domain.rs:288-290).
+__global__ void __launch_bounds__(NTT_THREADS, NTT_MIN_WAVES)
+ntt_last_kernel(const Fr* data, Fr* out, uint64_t out_len, NttTables tab, int L, NttPlanLg plan, int has_mul,
+                Fr mul0, Fr mul1, Fr mul2) {
+  constexpr int M = 6;
+  using D = WaveDif<M>;
+  __shared__ Fr w[1 << (M - 1)];
+  for (int j = threadIdx.x; j < (1 << (M - 1)); j += blockDim.x) w[j] = twiddle(tab, (uint64_t)j << (L - M));
+  __syncthreads();
+  const int* lgs = plan.lg;
+  const int P = plan.p;
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * NTT_WAVES + (threadIdx.x >> 6);
+  if (wave >= (1ull << L) / ((1ull << M) * D::CPW)) return;
+  const int l0 = lgs[0];
+  const uint64_t groups = (1ull << l0) / D::CPW;
+  const uint64_t midx = wave / groups;
+  const uint64_t g = wave % groups;
+  // m_idx = k_1 (N_2..N_{P-2}) + ... + k_{P-2}  ->  natural weight of k_p is N_0..N_{p-1}
   uint64_t mid_nat = 0;
   {
     uint64_t rem = midx;
-    int lsum_before = L - lgs[P - 1];  // bits of k1..k_{P-1}
-    // natural weight of k_p is N1*..*N_{p-1}
-    for (int p = P - 2; p >= 1; p--) {
-      const uint64_t dig = rem & ((1ull << lgs[p]) - 1);
-      rem >>= lgs[p];
-      int wbits = 0;
-      for (int qq = 0; qq < p; qq++) wbits += lgs[qq];
-      mid_nat |= dig << wbits;
+    int wbits_tail = L - M;  // bits of k_0..k_{P-2}
+#pragma unroll
+    for (int p = NTT_MAX_PASSES - 2; p >= 1; p--) {  // constant indices into plan.lg (no scratch copy)
+      if (p > P - 2) continue;
+      const int lgp = lgs[p];
+      const uint64_t dig = rem & ((1ull << lgp) - 1);
+      rem >>= lgp;
+      wbits_tail -= lgp;
+      mid_nat |= dig << wbits_tail;
     }
-    (void)lsum_before;
   }
-  for (int j = threadIdx.x; j < Np / 2; j += blockDim.x) w[j] = twiddle(tab, (uint64_t)j << (L - m));
-  const uint64_t colstride = 1ull << (L - l1);  // N / N1
-  for (int t = threadIdx.x; t < NTT_G * Np; t += blockDim.x) {
-    const int c = t / Np, i = t % Np;
-    const uint64_t pos = (g * NTT_G + c) * colstride + (midx << m) + i;
-    s[c * Np + i] = ld_fr(data + pos);
-  }
-  __syncthreads();
-  lds_dif(s, w, m, NTT_G);
-  const uint64_t kstride = 1ull << (L - m);  // N / N_P
-  for (int t = threadIdx.x; t < NTT_G * Np; t += blockDim.x) {
-    const int c = t % NTT_G, k = t / NTT_G;
-    const uint64_t y = (g * NTT_G + c) + mid_nat + (uint64_t)k * kstride;
+  const int c = lane % D::CPW, rg = lane / D::CPW;
+  const uint64_t k0 = g * D::CPW + c;
+  const uint64_t colbase = k0 * (1ull << (L - l0)) + (midx << M);
+  Fr x[8];
+#pragma unroll
+  for (int qq = 0; qq < 8; qq++) x[qq] = ld_fr(data + colbase + rg + D::LPC * qq);
+  D::run(x, w, rg);
+  const uint64_t kstride = 1ull << (L - M);
+#pragma unroll
+  for (int qq = 0; qq < 8; qq++) {
+    const uint32_t k = brev_bits(D::rpos(qq, rg), M);
+    const uint64_t y = k0 + mid_nat + (uint64_t)k * kstride;
     if (y >= out_len) continue;
-    Fr v = s[c * Np + brev(k, m)];
-    if (has_scale) v = v * scale;
-    if (distribute) {
-      const uint32_t md = (uint32_t)(y % 3);
-      if (md == 1) v = v * z1;
-      else if (md == 2) v = v * z2;
+    Fr v = x[qq];
+    if (has_mul) {  // ifft divisor and/or zeta power, one product (host folds them)
+      const uint32_t md = mod3(y);
+      v = v * fr_select(md == 1, mul1, fr_select(md == 2, mul2, mul0));
     }
     st_fr(out + y, v);
   }
 }
 
 // ---------------------------------------------------------------------------
-// Whole transform in one block (N <= 2^11): same maps as above.
-__global__ void __launch_bounds__(1024)
+// Whole transform in one block (N <= 2^NTT_SMALL_MAX_LOG), radix-2 DIF in LDS.
+__global__ void __launch_bounds__(256)
 ntt_small_kernel(const Fr* src, uint64_t n_in, Fr* out, uint64_t out_len, NttTables tab, int L,
                  int in_distribute, Fr iz1, Fr iz2, int has_scale, Fr scale, int out_distribute,
                  Fr oz1, Fr oz2) {
@@ -199,10 +266,20 @@ ntt_small_kernel(const Fr* src, uint64_t n_in, Fr* out, uint64_t out_len, NttTab
     s[i] = v;
   }
   __syncthreads();
-  if (L > 0) lds_dif(s, w, L, 1);
+  for (int hlog = L - 1; hlog >= 0; hlog--) {
+    const int h = 1 << hlog;
+    for (int t = threadIdx.x; t < N / 2; t += blockDim.x) {
+      const int j = t & (h - 1);
+      const int i = ((t >> hlog) << (hlog + 1)) + j;
+      const Fr a = s[i], b = s[i + h];
+      s[i] = a + b;
+      s[i + h] = (a - b) * w[j << (L - 1 - hlog)];
+    }
+    __syncthreads();
+  }
   for (int k = threadIdx.x; k < N; k += blockDim.x) {
     if ((uint64_t)k >= out_len) continue;
-    Fr v = s[L > 0 ? brev(k, L) : 0];
+    Fr v = s[L > 0 ? brev_bits((uint32_t)k, L) : 0];
     if (has_scale) v = v * scale;
     if (out_distribute) {
       const int md = k % 3;
@@ -229,12 +306,22 @@ __global__ void ntt_tables_kernel(Fr* lo, Fr* hi, Fr w, int b, int L) {
 // ---------------------------------------------------------------------------
 // Host side
 
-void ntt_split(int L, int* P, int lg[4]) {
-  if (L <= NTT_SMALL_MAX_LOG) { *P = 1; lg[0] = L; return; }
-  int p = (L + NTT_MAX_PASS_LOG - 1) / NTT_MAX_PASS_LOG;
-  if (p < 2) p = 2;
-  int base = L / p, extra = L % p;
-  for (int i = 0; i < p; i++) lg[i] = base + (i < extra ? 1 : 0);
+void ntt_split(int L, int* P, int lg[NTT_MAX_PASSES]) {
+  if (L <= NTT_SMALL_MAX_LOG) {
+    *P = 1;
+    lg[0] = L;
+    return;
+  }
+  int p = (L + 5) / 6;
+  const int R = L - 6 * (p - 1);
+  int i = 0;
+  if (R >= 3) {
+    lg[i++] = R;
+  } else {  // borrow 3 bits so every pass has 3..6 bits
+    lg[i++] = 3;
+    lg[i++] = R + 3;
+  }
+  while (i < p) lg[i++] = 6;
   *P = p;
 }
 
@@ -261,51 +348,67 @@ void ntt_free_tables(NttTables* t) {
 }
 
 hipError_t ntt_init_attributes() {
-  hipError_t e;
-  const int big = 160 * 1024;
-  e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ntt_pass_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, big);
-  if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ntt_last_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, big);
-  if (e != hipSuccess) return e;
   return hipFuncSetAttribute(reinterpret_cast<const void*>(&ntt_small_kernel),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, big);
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+template <int M>
+static void launch_pass(const NttArgs& a, Fr* data, const Fr* in, uint64_t n_in, int L, int lrem, int dist,
+                        hipStream_t st) {
+  const uint64_t N = 1ull << L;
+  const uint64_t waves = N / ((1ull << M) * WaveDif<M>::CPW);
+  const unsigned blocks = (unsigned)((waves + NTT_WAVES - 1) / NTT_WAVES);
+  hipLaunchKernelGGL(ntt_pass_kernel<M>, dim3(blocks), dim3(NTT_THREADS), 0, st, data, in, n_in, a.tab, L, lrem,
+                     dist, a.in_z1, a.in_z2);
 }
 
 hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
   const int L = a.tab.L;
   const uint64_t N = 1ull << L;
   const uint64_t out_len = a.out_len ? a.out_len : N;
-  int P, lg[4] = {0, 0, 0, 0};
-  ntt_split(L, &P, lg);
+  NttPlanLg plan;
+  ntt_split(L, &plan.p, plan.lg);
+  const int P = plan.p;
+  const int* lg = plan.lg;
   if (P == 1) {
     const size_t sm = (N + N / 2 + 1) * sizeof(Fr);
-    const int threads = N >= 1024 ? 1024 : (N >= 64 ? (int)N : 64);
-    hipLaunchKernelGGL(ntt_small_kernel, dim3(1), dim3(threads), sm, st, a.src, a.n_in, a.dst, out_len, a.tab,
-                       L, a.in_distribute, a.in_z1, a.in_z2, a.has_scale, a.scale, a.out_distribute, a.out_z1,
+    hipLaunchKernelGGL(ntt_small_kernel, dim3(1), dim3(256), sm, st, a.src, a.n_in, a.dst, out_len, a.tab, L,
+                       a.in_distribute, a.in_z1, a.in_z2, a.has_scale, a.scale, a.out_distribute, a.out_z1,
                        a.out_z2);
     return hipGetLastError();
   }
+  if (P > NTT_MAX_PASSES || lg[P - 1] != 6) return hipErrorInvalidValue;
+  // epilogue multiplier per (y mod 3): scale * zeta-power, folded on the host
+  const int has_mul = a.has_scale || a.out_distribute;
+  Fr mul[3];
+  for (int r = 0; r < 3; r++) {
+    Fr m = a.has_scale ? a.scale : Fr::one();
+    if (a.out_distribute && r == 1) m = m * a.out_z1;
+    if (a.out_distribute && r == 2) m = m * a.out_z2;
+    mul[r] = m;
+  }
+  // N / N_0 and every middle S are multiples of 64 >= CPW: waves divide evenly.
   // pass 0: src -> work (out of place), passes 1..P-2 in place on work,
   // last pass: work -> dst in natural order.
   int lrem = L;
   for (int p = 0; p < P - 1; p++) {
-    const int m = lg[p];
-    const uint64_t blocks = N / ((1ull << m) * NTT_G);
-    const size_t sm = (NTT_G * (1ull << m) + (1ull << m) / 2) * sizeof(Fr);
-    hipLaunchKernelGGL(ntt_pass_kernel, dim3((unsigned)blocks), dim3(NTT_THREADS), sm, st, a.work,
-                       p == 0 ? a.src : (const Fr*)nullptr, p == 0 ? a.n_in : 0, a.tab, L, m, lrem,
-                       p == 0 ? a.in_distribute : 0, a.in_z1, a.in_z2);
-    lrem -= m;
+    const Fr* in = p == 0 ? a.src : nullptr;
+    const uint64_t nin = p == 0 ? a.n_in : 0;
+    const int dist = p == 0 ? a.in_distribute : 0;
+    switch (lg[p]) {
+      case 3: launch_pass<3>(a, a.work, in, nin, L, lrem, dist, st); break;
+      case 4: launch_pass<4>(a, a.work, in, nin, L, lrem, dist, st); break;
+      case 5: launch_pass<5>(a, a.work, in, nin, L, lrem, dist, st); break;
+      case 6: launch_pass<6>(a, a.work, in, nin, L, lrem, dist, st); break;
+      default: return hipErrorInvalidValue;
+    }
+    lrem -= lg[p];
   }
   {
-    const int m = lg[P - 1];
-    const uint64_t blocks = N / ((1ull << m) * NTT_G);
-    const size_t sm = (NTT_G * (1ull << m) + (1ull << m) / 2) * sizeof(Fr);
-    hipLaunchKernelGGL(ntt_last_kernel, dim3((unsigned)blocks), dim3(NTT_THREADS), sm, st, (const Fr*)a.work,
-                       a.dst, out_len, a.tab, L, P, make_int4(lg[0], lg[1], lg[2], lg[3]), a.has_scale, a.scale,
-                       a.out_distribute, a.out_z1, a.out_z2);
+    const uint64_t waves = N / (64ull * WaveDif<6>::CPW);
+    const unsigned blocks = (unsigned)((waves + NTT_WAVES - 1) / NTT_WAVES);
+    hipLaunchKernelGGL(ntt_last_kernel, dim3(blocks), dim3(NTT_THREADS), 0, st, (const Fr*)a.work, a.dst, out_len,
+                       a.tab, L, plan, has_mul, mul[0], mul[1], mul[2]);
   }
   return hipGetLastError();
 }

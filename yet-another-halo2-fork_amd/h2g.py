@@ -14,7 +14,7 @@ import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "lib", "libh2g.so")
+LIB_PATH = os.environ.get("H2G_LIB") or os.path.join(PKG, "lib", "libh2g.so")  # H2G_LIB: A/B builds
 HEADER = os.path.join(REPO, "include", "h2g.h")
 
 U64P = ctypes.POINTER(ctypes.c_uint64)
