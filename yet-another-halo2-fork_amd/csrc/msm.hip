@@ -142,7 +142,11 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ 
   for (uint32_t p = lo; p < hi; p++) {
     const uint32_t k2 = keys[p];
     const uint32_t v = vals[p];
+#ifdef H2G_MSM_TIMING_GATHER_MASK  // timing-only A/B build: gather from a small (L2-resident) table
+    G1Affine pt = ld_aff(bases + (v & H2G_MSM_TIMING_GATHER_MASK));
+#else
     G1Affine pt = ld_aff(bases + (v & 0x7fffffffu));
+#endif
     if (k2 != key) {
       msm_emit(key, acc, first, lo, hi, t, start, end, buckets, bnd);
       first = false;
