@@ -1,0 +1,819 @@
+/*
+ * prover.c -- CPU restatement of halo2's create_proof over BN254 / KZG / SHPLONK
+ * with the Blake2b transcript.  TEST INFRASTRUCTURE ONLY (the parity checker for the
+ * device pipeline and the CPU baseline).  This translation unit includes oracle.c
+ * (field, G1, best_multiexp, best_fft, EvaluationDomain) and is the only file the
+ * oracle Makefile compiles.
+ *
+ * Restated reference code (paths relative to the reference root):
+ *   keygen_pk                          halo2_backend/src/plonk/keygen.rs:94-190
+ *   query collection / degree / bf     halo2_backend/src/plonk/keygen.rs:191-394, plonk/circuit.rs:95-180,292-320
+ *   permutation Assembly / build_pk    halo2_backend/src/plonk/permutation/keygen.rs:16-213
+ *   Prover::new_with_engine            halo2_backend/src/plonk/prover.rs:174-305
+ *   commit_phase                       halo2_backend/src/plonk/prover.rs:309-494
+ *   create_proof                       halo2_backend/src/plonk/prover.rs:512-899
+ *   permutation_commit / evaluate / open  halo2_backend/src/plonk/permutation/prover.rs:50-333
+ *   vanishing commit / construct / evaluate / open  halo2_backend/src/plonk/vanishing/prover.rs:40-205
+ *   evaluate_h (gates + permutation)   halo2_backend/src/plonk/evaluation.rs:317-483
+ *   SHPLONK create_proof               halo2_backend/src/poly/kzg/multiopen/shplonk/prover.rs:121-305
+ *   construct_intermediate_sets        halo2_backend/src/poly/kzg/multiopen/shplonk.rs:48-140
+ *   Blake2bWrite transcript            halo2_backend/src/transcript.rs:120-130,353-419,500-539
+ * Scope: advice (one phase), fixed, instance columns, custom gates (expression
+ * graphs with rotations), the permutation argument.  Lookups/shuffles/challenges are
+ * not restated yet.
+ * Unverifiable-here details (isolated): G1 compressed encoding (x LE, bit 7 of byte 31
+ * = y odd); vk.transcript_repr is taken as an input (plonk.rs:189-200 hashes the Rust
+ * Debug text of the pinned VK).
+ */
+#include "oracle.c"
+#include "hash.h"
+
+#include <stdio.h>
+
+/* ====================================================================== spec */
+enum { COL_ADVICE = 0, COL_FIXED = 1, COL_INSTANCE = 2 };
+enum { OP_CONST = 0, OP_QUERY = 1, OP_NEG = 2, OP_SUM = 3, OP_PROD = 4 };
+
+typedef struct {
+    uint32_t k, num_advice, num_fixed, num_instance;
+    uint32_t num_gates;
+    const int32_t *gate_roots;
+    uint32_t num_nodes;
+    const int32_t *nodes; /* 4 ints per node: op, a, b, c */
+    uint32_t num_constants;
+    const uint64_t *constants;
+    uint32_t num_perm_columns;
+    const int32_t *perm_columns; /* (type, index) pairs */
+    uint32_t num_copies;
+    const int32_t *copies; /* (ltype, lindex, lrow, rtype, rindex, rrow) */
+    const uint64_t *fixed_values;    /* num_fixed * n Fr */
+    const uint64_t *advice_values;   /* num_advice * n Fr */
+    const uint64_t *instance_values; /* num_instance * n Fr (zero padded) */
+    const uint32_t *instance_lens;
+    const uint64_t *transcript_repr; /* Fr */
+    const uint8_t *rng_seed;         /* 32 bytes: ChaCha20Rng::from_seed */
+    uint32_t vanishing_threads;
+    const uint64_t *srs_g;          /* n G1Affine */
+    const uint64_t *srs_g_lagrange; /* n G1Affine */
+    const uint8_t *unblinded;       /* num_advice flags (unblinded_advice_columns) or NULL */
+} or_spec;
+
+typedef struct { int type, index, rot; } query_t;
+
+/* ====================================================================== small helpers */
+static fe fe_from(const uint64_t *p) { fe r; memcpy(r.v, p, 32); return r; }
+
+static void fr_random(chacha_rng *rng, fe *out) {   /* Fr::random: LE512 mod r */
+    uint8_t b[64];
+    chacha_rng_fill(rng, b, 64);
+    uint64_t d[8];
+    for (int i = 0; i < 8; i++) d[i] = load64le(b + 8 * i);
+    static const fe R3 = {{0x5e94d8e1b4bf0040ULL, 0x2a489cbe1cfbb6b8ULL, 0x893cc664a19fcfedULL, 0x0cf8594b7fcc657cULL}};
+    fe lo = fe_from(d), hi = fe_from(d + 4), t1, t2;
+    fr_mul(&t1, &lo, &fr_R2);   /* d0 * R2 * R^-1 = mont(d0) */
+    fr_mul(&t2, &hi, &R3);      /* d1 * R3 * R^-1 = mont(d1 * 2^256) */
+    fr_add(out, &t1, &t2);
+}
+
+static fe fr_pow_u64(const fe *a, uint64_t e) {
+    uint64_t ee[4] = {e, 0, 0, 0};
+    fe r; fr_pow(&r, a, ee); return r;
+}
+
+/* ====================================================================== transcript */
+typedef struct {
+    blake2b_state st;
+    uint8_t *proof;
+    size_t len, cap;
+} transcript_t;
+
+static void tr_init(transcript_t *t, uint8_t *buf, size_t cap) {
+    blake2b_init(&t->st, 64, (const uint8_t *)"Halo2-Transcript");
+    t->proof = buf; t->len = 0; t->cap = cap;
+}
+static void fr_repr(const fe *a, uint8_t out[32]) {
+    uint64_t c[4]; fr_to_canonical(c, a);
+    for (int i = 0; i < 32; i++) out[i] = (uint8_t)(c[i / 8] >> (8 * (i % 8)));
+}
+static void fq_repr(const fe *a, uint8_t out[32]) {
+    uint64_t c[4]; fq_to_canonical(c, a);
+    for (int i = 0; i < 32; i++) out[i] = (uint8_t)(c[i / 8] >> (8 * (i % 8)));
+}
+static void tr_common_scalar(transcript_t *t, const fe *s) {
+    uint8_t b[33]; b[0] = 2; fr_repr(s, b + 1);
+    blake2b_update(&t->st, b, 33);
+}
+static void tr_write_scalar(transcript_t *t, const fe *s) {
+    tr_common_scalar(t, s);
+    uint8_t r[32]; fr_repr(s, r);
+    if (t->len + 32 <= t->cap) memcpy(t->proof + t->len, r, 32);
+    t->len += 32;
+}
+static int tr_write_point(transcript_t *t, const g1a *p) {
+    if (g1a_is_id(p)) return -1;  /* "cannot write points at infinity to the transcript" */
+    uint8_t b[65]; b[0] = 1; fq_repr(&p->x, b + 1); fq_repr(&p->y, b + 33);
+    blake2b_update(&t->st, b, 65);
+    uint8_t c[32]; memcpy(c, b + 1, 32);
+    if (b[33] & 1) c[31] |= 0x80;  /* compressed: x, sign of y in the top bit */
+    if (t->len + 32 <= t->cap) memcpy(t->proof + t->len, c, 32);
+    t->len += 32;
+    return 0;
+}
+static fe tr_squeeze(transcript_t *t) {
+    uint8_t z = 0; blake2b_update(&t->st, &z, 1);
+    uint8_t h[64]; blake2b_final_copy(&t->st, h);
+    uint64_t d[8];
+    for (int i = 0; i < 8; i++) d[i] = load64le(h + 8 * i);
+    static const fe R3 = {{0x5e94d8e1b4bf0040ULL, 0x2a489cbe1cfbb6b8ULL, 0x893cc664a19fcfedULL, 0x0cf8594b7fcc657cULL}};
+    fe lo = fe_from(d), hi = fe_from(d + 4), t1, t2, r;
+    fr_mul(&t1, &lo, &fr_R2); fr_mul(&t2, &hi, &R3); fr_add(&r, &t1, &t2);
+    return r;   /* Challenge255: from_uniform_bytes, stored as repr, re-read: same value */
+}
+
+/* ====================================================================== expressions */
+static int node_degree(const or_spec *s, int i) {
+    const int32_t *nd = s->nodes + 4 * i;
+    switch (nd[0]) {
+        case OP_CONST: return 0;
+        case OP_QUERY: return 1;
+        case OP_NEG: return node_degree(s, nd[1]);
+        case OP_SUM: { int a = node_degree(s, nd[1]), b = node_degree(s, nd[2]); return a > b ? a : b; }
+        default: return node_degree(s, nd[1]) + node_degree(s, nd[2]);
+    }
+}
+
+typedef struct { query_t *q; int n, cap; } qlist;
+static int qlist_add(qlist *l, int type, int index, int rot) {
+    for (int i = 0; i < l->n; i++)
+        if (l->q[i].type == type && l->q[i].index == index && l->q[i].rot == rot) return i;
+    if (l->n == l->cap) { l->cap = l->cap ? 2 * l->cap : 16; l->q = (query_t *)realloc(l->q, l->cap * sizeof(query_t)); }
+    l->q[l->n].type = type; l->q[l->n].index = index; l->q[l->n].rot = rot;
+    return l->n++;
+}
+/* QueriesMap::as_expression: depth first, lhs before rhs (keygen.rs:217-249) */
+static void collect_queries(const or_spec *s, int i, qlist *adv, qlist *fix, qlist *ins) {
+    const int32_t *nd = s->nodes + 4 * i;
+    switch (nd[0]) {
+        case OP_CONST: return;
+        case OP_QUERY:
+            if (nd[1] == COL_ADVICE) qlist_add(adv, nd[1], nd[2], nd[3]);
+            else if (nd[1] == COL_FIXED) qlist_add(fix, nd[1], nd[2], nd[3]);
+            else qlist_add(ins, nd[1], nd[2], nd[3]);
+            return;
+        case OP_NEG: collect_queries(s, nd[1], adv, fix, ins); return;
+        default: collect_queries(s, nd[1], adv, fix, ins); collect_queries(s, nd[2], adv, fix, ins); return;
+    }
+}
+
+/* evaluate expression i at extended row idx over coset arrays */
+static fe eval_node(const or_spec *s, int i, fe *const *adv, fe *const *fix, fe *const *ins, uint64_t idx,
+                    uint64_t rot_scale, uint64_t ext) {
+    const int32_t *nd = s->nodes + 4 * i;
+    fe r, a, b;
+    switch (nd[0]) {
+        case OP_CONST: return fe_from(s->constants + 4 * nd[1]);
+        case OP_QUERY: {
+            int64_t j = ((int64_t)idx + (int64_t)nd[3] * (int64_t)rot_scale) % (int64_t)ext;
+            if (j < 0) j += (int64_t)ext;
+            fe *const *cols = nd[1] == COL_ADVICE ? adv : (nd[1] == COL_FIXED ? fix : ins);
+            return cols[nd[2]][j];
+        }
+        case OP_NEG: a = eval_node(s, nd[1], adv, fix, ins, idx, rot_scale, ext); fr_neg(&r, &a); return r;
+        case OP_SUM:
+            a = eval_node(s, nd[1], adv, fix, ins, idx, rot_scale, ext);
+            b = eval_node(s, nd[2], adv, fix, ins, idx, rot_scale, ext);
+            fr_add(&r, &a, &b); return r;
+        default:
+            a = eval_node(s, nd[1], adv, fix, ins, idx, rot_scale, ext);
+            b = eval_node(s, nd[2], adv, fix, ins, idx, rot_scale, ext);
+            fr_mul(&r, &a, &b); return r;
+    }
+}
+
+/* ====================================================================== polynomial helpers */
+static fe *fr_alloc(uint64_t n) { return (fe *)calloc(n ? n : 1, sizeof(fe)); }
+static fe eval_poly(const fe *p, uint64_t n, const fe *x) {
+    fe r; or_fr_eval((const uint64_t *)p, n, x->v, r.v); return r;
+}
+static fe rotate_omega(const domain_t *d, const fe *x, int rot) {
+    fe w = rot >= 0 ? d->omega : d->omega_inv;
+    fe p = fr_pow_u64(&w, (uint64_t)(rot >= 0 ? rot : -rot)), r;
+    fr_mul(&r, x, &p); return r;
+}
+static void lagrange_to_coeff_d(const domain_t *d, fe *a, int threads) {
+    or_fft((uint64_t *)a, d->k, d->omega_inv.v, threads);
+    ifft_scale(a, d->n, &d->ifft_divisor);
+}
+static void coeff_to_extended_d(const domain_t *d, const fe *in, fe *out, int threads) {
+    uint64_t ext = 1ULL << d->extended_k;
+    memcpy(out, in, d->n * sizeof(fe));
+    distribute_powers_zeta(d, out, d->n, 1);
+    memset(out + d->n, 0, (ext - d->n) * sizeof(fe));
+    or_fft((uint64_t *)out, d->extended_k, d->extended_omega.v, threads);
+}
+static int commit_msm(const fe *scalars, uint64_t n, const uint64_t *bases, int threads, g1a *out) {
+    or_msm_best((const uint64_t *)scalars, bases, n, threads, (uint64_t *)out);
+    return 0;
+}
+/* lagrange_interpolate (arithmetic.rs:177-230): coefficients of the unique poly of
+ * degree < m through (points[i], evals[i]) */
+static void lagrange_interpolate(const fe *pts, const fe *ev, int m, fe *coeffs) {
+    for (int i = 0; i < m; i++) coeffs[i] = (fe){{0, 0, 0, 0}};
+    fe *basis = fr_alloc(m), *tmp = fr_alloc(m + 1);
+    for (int j = 0; j < m; j++) {
+        /* numerator prod_{k != j} (X - x_k), denominator prod (x_j - x_k) */
+        for (int i = 0; i <= m; i++) tmp[i] = (fe){{0, 0, 0, 0}};
+        tmp[0] = fr_ONE;
+        int deg = 0;
+        fe den = fr_ONE;
+        for (int kk = 0; kk < m; kk++) {
+            if (kk == j) continue;
+            fe nx; fr_neg(&nx, &pts[kk]);
+            for (int i = deg + 1; i >= 0; i--) {   /* tmp *= (X - x_k) */
+                fe a = i > 0 ? tmp[i - 1] : (fe){{0, 0, 0, 0}}, b, c;
+                fr_mul(&b, &tmp[i], &nx);
+                fr_add(&c, &a, &b);
+                tmp[i] = c;
+            }
+            deg++;
+            fe dd; fr_sub(&dd, &pts[j], &pts[kk]); fr_mul(&den, &den, &dd);
+        }
+        fe inv, sc; fr_inv(&inv, &den); fr_mul(&sc, &inv, &ev[j]);
+        for (int i = 0; i < m; i++) { fe t; fr_mul(&t, &tmp[i], &sc); fr_add(&coeffs[i], &coeffs[i], &t); }
+    }
+    free(basis); free(tmp);
+}
+static int fe_cmp_canon(const fe *a, const fe *b) {  /* Ord on Fr: canonical numeric order */
+    uint64_t ca[4], cb[4]; fr_to_canonical(ca, a); fr_to_canonical(cb, b);
+    for (int i = 3; i >= 0; i--) { if (ca[i] < cb[i]) return -1; if (ca[i] > cb[i]) return 1; }
+    return 0;
+}
+
+/* ====================================================================== permutation Assembly */
+typedef struct { int col, row; } cell_t;
+typedef struct { cell_t *mapping, *aux; uint64_t *sizes; int cols; uint64_t n; } assembly_t;
+static int perm_col_pos(const or_spec *s, int type, int index) {
+    for (uint32_t i = 0; i < s->num_perm_columns; i++)
+        if (s->perm_columns[2 * i] == type && s->perm_columns[2 * i + 1] == index) return (int)i;
+    return -1;
+}
+static void assembly_copy(assembly_t *A, int lc, int lr, int rc, int rr) {  /* permutation/keygen.rs:48-97 */
+    cell_t lcyc = A->aux[(uint64_t)lc * A->n + lr], rcyc = A->aux[(uint64_t)rc * A->n + rr];
+    if (lcyc.col == rcyc.col && lcyc.row == rcyc.row) return;
+    if (A->sizes[(uint64_t)lcyc.col * A->n + lcyc.row] < A->sizes[(uint64_t)rcyc.col * A->n + rcyc.row]) {
+        cell_t t = lcyc; lcyc = rcyc; rcyc = t;
+    }
+    A->sizes[(uint64_t)lcyc.col * A->n + lcyc.row] += A->sizes[(uint64_t)rcyc.col * A->n + rcyc.row];
+    cell_t i = rcyc;
+    for (;;) {
+        A->aux[(uint64_t)i.col * A->n + i.row] = lcyc;
+        i = A->mapping[(uint64_t)i.col * A->n + i.row];
+        if (i.col == rcyc.col && i.row == rcyc.row) break;
+    }
+    cell_t tmp = A->mapping[(uint64_t)lc * A->n + lr];
+    A->mapping[(uint64_t)lc * A->n + lr] = A->mapping[(uint64_t)rc * A->n + rr];
+    A->mapping[(uint64_t)rc * A->n + rr] = tmp;
+}
+
+/* ====================================================================== keygen */
+typedef struct { fe point; int poly_id; } query_ref;
+
+/* ProvingKey restated (plonk.rs ProvingKey + permutation::ProvingKey), plus the
+ * ConstraintSystem facts the prover needs.  Circuit arrays stay owned by the caller. */
+typedef struct {
+    uint32_t k;
+    uint64_t n, ext, rot_scale;
+    int degree, bf, P;
+    qlist adv_q, fix_q, ins_q;
+    domain_t D;
+    fe **fixed_polys, **fixed_cosets;
+    fe *l0, *l_last, *l_active;
+    fe **sigma_lag, **sigma_polys, **sigma_cosets;
+} or_pk;
+
+void or_pk_free(or_pk *pk);
+
+or_pk *or_keygen(const or_spec *s, int threads) {   /* keygen_vk + keygen_pk (keygen.rs:43-190) */
+    if (threads < 1) threads = 1;
+    const uint32_t k = s->k;
+    const uint64_t n = 1ULL << k;
+    int degree = 3;  /* permutation_argument_required_degree (circuit.rs:292-320) */
+    for (uint32_t g = 0; g < s->num_gates; g++) { int dg = node_degree(s, s->gate_roots[g]); if (dg > degree) degree = dg; }
+    qlist adv_q = {0}, fix_q = {0}, ins_q = {0};
+    for (uint32_t g = 0; g < s->num_gates; g++) collect_queries(s, s->gate_roots[g], &adv_q, &fix_q, &ins_q);
+    for (uint32_t i = 0; i < s->num_perm_columns; i++) {
+        int t = s->perm_columns[2 * i], idx = s->perm_columns[2 * i + 1];
+        qlist_add(t == COL_ADVICE ? &adv_q : (t == COL_FIXED ? &fix_q : &ins_q), t, idx, 0);
+    }
+    int max_q = 1;
+    {
+        int *cnt = (int *)calloc(s->num_advice + 1, sizeof(int));
+        for (int i = 0; i < adv_q.n; i++) cnt[adv_q.q[i].index]++;
+        if (s->num_advice) { max_q = 0; for (uint32_t i = 0; i < s->num_advice; i++) if (cnt[i] > max_q) max_q = cnt[i]; }
+        free(cnt);
+    }
+    const int bf = (max_q > 3 ? max_q : 3) + 2;   /* circuit.rs:143-170 */
+    if ((int64_t)n < bf + 3) return NULL;          /* minimum_rows */
+    or_pk *pk = (or_pk *)calloc(1, sizeof(or_pk));
+    pk->k = k; pk->n = n; pk->degree = degree; pk->bf = bf;
+    pk->adv_q = adv_q; pk->fix_q = fix_q; pk->ins_q = ins_q;
+    domain_new(&pk->D, (uint32_t)degree, k);
+    const domain_t *D = &pk->D;
+    const uint64_t ext = 1ULL << D->extended_k;
+    pk->ext = ext;
+    pk->rot_scale = 1ULL << (D->extended_k - k);
+
+    pk->fixed_polys = (fe **)calloc(s->num_fixed + 1, sizeof(fe *));
+    pk->fixed_cosets = (fe **)calloc(s->num_fixed + 1, sizeof(fe *));
+    for (uint32_t i = 0; i < s->num_fixed; i++) {
+        pk->fixed_polys[i] = fr_alloc(n);
+        memcpy(pk->fixed_polys[i], s->fixed_values + 4 * n * i, n * 32);
+        lagrange_to_coeff_d(D, pk->fixed_polys[i], threads);
+        pk->fixed_cosets[i] = fr_alloc(ext);
+        coeff_to_extended_d(D, pk->fixed_polys[i], pk->fixed_cosets[i], threads);
+    }
+    pk->l0 = fr_alloc(ext); pk->l_last = fr_alloc(ext); pk->l_active = fr_alloc(ext);
+    {
+        fe *t = fr_alloc(n);
+        t[0] = fr_ONE; lagrange_to_coeff_d(D, t, threads); coeff_to_extended_d(D, t, pk->l0, threads);
+        fe *lb = fr_alloc(ext);
+        memset(t, 0, n * 32);
+        for (int i = 0; i < bf; i++) t[n - 1 - i] = fr_ONE;
+        lagrange_to_coeff_d(D, t, threads); coeff_to_extended_d(D, t, lb, threads);
+        memset(t, 0, n * 32);
+        t[n - bf - 1] = fr_ONE;
+        lagrange_to_coeff_d(D, t, threads); coeff_to_extended_d(D, t, pk->l_last, threads);
+        for (uint64_t i = 0; i < ext; i++) { fe a; fr_add(&a, &pk->l_last[i], &lb[i]); fr_sub(&pk->l_active[i], &fr_ONE, &a); }
+        free(t); free(lb);
+    }
+    /* permutation keygen (permutation/keygen.rs:16-213) */
+    const int P = (int)s->num_perm_columns;
+    pk->P = P;
+    assembly_t A; A.cols = P; A.n = n;
+    A.mapping = (cell_t *)malloc((size_t)P * n * sizeof(cell_t) + 1);
+    A.aux = (cell_t *)malloc((size_t)P * n * sizeof(cell_t) + 1);
+    A.sizes = (uint64_t *)malloc((size_t)P * n * sizeof(uint64_t) + 1);
+    for (int c = 0; c < P; c++)
+        for (uint64_t r = 0; r < n; r++) {
+            A.mapping[c * n + r] = (cell_t){c, (int)r}; A.aux[c * n + r] = (cell_t){c, (int)r}; A.sizes[c * n + r] = 1;
+        }
+    for (uint32_t i = 0; i < s->num_copies; i++) {
+        const int32_t *cp = s->copies + 6 * i;
+        int lc = perm_col_pos(s, cp[0], cp[1]), rc = perm_col_pos(s, cp[3], cp[4]);
+        if (lc < 0 || rc < 0 || cp[2] < 0 || cp[5] < 0 || cp[2] >= (int)n || cp[5] >= (int)n) {
+            free(A.mapping); free(A.aux); free(A.sizes); or_pk_free(pk); return NULL;
+        }
+        assembly_copy(&A, lc, cp[2], rc, cp[5]);
+    }
+    pk->sigma_lag = (fe **)calloc(P + 1, sizeof(fe *));
+    pk->sigma_polys = (fe **)calloc(P + 1, sizeof(fe *));
+    pk->sigma_cosets = (fe **)calloc(P + 1, sizeof(fe *));
+    {
+        fe *omega_pow = fr_alloc(n);
+        omega_pow[0] = fr_ONE;
+        for (uint64_t j = 1; j < n; j++) fr_mul(&omega_pow[j], &omega_pow[j - 1], &D->omega);
+        fe *delta_pow = fr_alloc(P + 1);
+        delta_pow[0] = fr_ONE;
+        for (int i = 1; i <= P; i++) fr_mul(&delta_pow[i], &delta_pow[i - 1], &FR_DELTA);
+        for (int i = 0; i < P; i++) {
+            pk->sigma_lag[i] = fr_alloc(n);
+            for (uint64_t j = 0; j < n; j++) {
+                cell_t m = A.mapping[(uint64_t)i * n + j];
+                fr_mul(&pk->sigma_lag[i][j], &delta_pow[m.col], &omega_pow[m.row]);
+            }
+            pk->sigma_polys[i] = fr_alloc(n);
+            memcpy(pk->sigma_polys[i], pk->sigma_lag[i], n * 32);
+            lagrange_to_coeff_d(D, pk->sigma_polys[i], threads);
+            pk->sigma_cosets[i] = fr_alloc(ext);
+            coeff_to_extended_d(D, pk->sigma_polys[i], pk->sigma_cosets[i], threads);
+        }
+        free(omega_pow); free(delta_pow);
+    }
+    free(A.mapping); free(A.aux); free(A.sizes);
+    return pk;
+}
+
+void or_pk_free(or_pk *pk) {
+    if (!pk) return;
+    for (int i = 0; pk->fixed_polys && pk->fixed_polys[i]; i++) { free(pk->fixed_polys[i]); free(pk->fixed_cosets[i]); }
+    free(pk->fixed_polys); free(pk->fixed_cosets);
+    free(pk->l0); free(pk->l_last); free(pk->l_active);
+    for (int i = 0; i < pk->P && pk->sigma_lag; i++) { free(pk->sigma_lag[i]); free(pk->sigma_polys[i]); free(pk->sigma_cosets[i]); }
+    free(pk->sigma_lag); free(pk->sigma_polys); free(pk->sigma_cosets);
+    free(pk->adv_q.q); free(pk->fix_q.q); free(pk->ins_q.q);
+    domain_free(&pk->D);
+    free(pk);
+}
+
+/* sizes the verifier side needs */
+void or_pk_info(const or_pk *pk, int32_t *out8) {
+    out8[0] = pk->degree; out8[1] = pk->bf; out8[2] = (int32_t)pk->D.extended_k; out8[3] = pk->P;
+    out8[4] = pk->adv_q.n; out8[5] = pk->fix_q.n; out8[6] = pk->ins_q.n; out8[7] = (pk->P + pk->degree - 3) / (pk->degree - 2);
+}
+/* sigma values (Lagrange) of permutation column i: the vk commitments are commit_lagrange of these */
+void or_pk_sigma(const or_pk *pk, int i, uint64_t *out) { memcpy(out, pk->sigma_lag[i], pk->n * 32); }
+
+/* ====================================================================== create_proof */
+/* create_proof for one circuit (prover.rs:512-899).  The witness (advice, instance)
+ * and the prover inputs (rng seed, vanishing thread count, SRS) come from `s`. */
+int or_prove(const or_pk *pk, const or_spec *s, uint8_t *proof, uint64_t proof_cap, uint64_t *proof_len, int threads) {
+    if (threads < 1) threads = 1;
+    const uint32_t k = pk->k;
+    const uint64_t n = pk->n, ext = pk->ext, rot_scale = pk->rot_scale;
+    const int degree = pk->degree, bf = pk->bf, P = pk->P;
+    const domain_t D = pk->D;
+    const qlist adv_q = pk->adv_q, fix_q = pk->fix_q;
+    fe *const *fixed_polys = pk->fixed_polys, *const *fixed_cosets = pk->fixed_cosets;
+    fe *const *sigma_lag = pk->sigma_lag, *const *sigma_polys = pk->sigma_polys, *const *sigma_cosets = pk->sigma_cosets;
+    const fe *l0 = pk->l0, *l_last = pk->l_last, *l_active = pk->l_active;
+
+    chacha_rng rng; chacha_rng_init(&rng, s->rng_seed);
+    transcript_t T; tr_init(&T, proof, proof_cap);
+    { fe tr = fe_from(s->transcript_repr); tr_common_scalar(&T, &tr); }       /* vk.hash_into */
+    /* instances (prover.rs:196-271; KZG: QUERY_INSTANCE = false) */
+    fe **inst_vals = (fe **)calloc(s->num_instance + 1, sizeof(fe *)), **inst_polys = (fe **)calloc(s->num_instance + 1, sizeof(fe *));
+    for (uint32_t i = 0; i < s->num_instance; i++) {
+        if (s->instance_lens[i] > n - (bf + 1)) return -4;   /* InstanceTooLarge */
+        inst_vals[i] = fr_alloc(n);
+        memcpy(inst_vals[i], s->instance_values + 4 * n * i, n * 32);
+        for (uint32_t r = 0; r < s->instance_lens[i]; r++) tr_common_scalar(&T, &inst_vals[i][r]);
+        inst_polys[i] = fr_alloc(n);
+        memcpy(inst_polys[i], inst_vals[i], n * 32);
+        lagrange_to_coeff_d(&D, inst_polys[i], threads);
+    }
+    /* commit_phase, phase 0 (prover.rs:309-494) */
+    fe **adv = (fe **)calloc(s->num_advice + 1, sizeof(fe *));
+    const uint64_t unusable = n - (uint64_t)(bf + 1);
+    for (uint32_t c = 0; c < s->num_advice; c++) {
+        adv[c] = fr_alloc(n);
+        memcpy(adv[c], s->advice_values + 4 * n * c, n * 32);
+        if (s->unblinded && s->unblinded[c]) continue;
+        for (uint64_t r = unusable; r < n; r++) fr_random(&rng, &adv[c][r]);
+    }
+    for (uint32_t c = 0; c < s->num_advice; c++) {
+        if (s->unblinded && s->unblinded[c]) continue;
+        fe blind; fr_random(&rng, &blind);
+    }
+    for (uint32_t c = 0; c < s->num_advice; c++) {
+        g1a cm; commit_msm(adv[c], n, s->srs_g_lagrange, threads, &cm);
+        if (tr_write_point(&T, &cm)) return -5;
+    }
+    fe theta = tr_squeeze(&T); (void)theta;
+    fe beta = tr_squeeze(&T), gamma = tr_squeeze(&T);
+    /* permutation_commit (permutation/prover.rs:50-197) */
+    const int chunk_len = degree - 2;
+    const int nsets = (P + chunk_len - 1) / chunk_len;
+    fe **z_poly = (fe **)calloc(nsets + 1, sizeof(fe *)), **z_coset = (fe **)calloc(nsets + 1, sizeof(fe *));
+    {
+        fe deltaomega = fr_ONE, last_z = fr_ONE;
+        fe *mod = fr_alloc(n);
+        for (int st = 0; st < nsets; st++) {
+            int c0 = st * chunk_len, c1 = c0 + chunk_len < P ? c0 + chunk_len : P;
+            for (uint64_t r = 0; r < n; r++) mod[r] = fr_ONE;
+            for (int c = c0; c < c1; c++) {
+                int t = s->perm_columns[2 * c], idx = s->perm_columns[2 * c + 1];
+                fe *vals = t == COL_ADVICE ? adv[idx] : (t == COL_FIXED ? (fe *)(s->fixed_values + 4 * n * idx) : inst_vals[idx]);
+#pragma omp parallel for num_threads(threads) schedule(static)
+                for (uint64_t r = 0; r < n; r++) {
+                    fe a, b; fr_mul(&a, &beta, &sigma_lag[c][r]); fr_add(&a, &a, &gamma); fr_add(&b, &a, &vals[r]);
+                    fr_mul(&mod[r], &mod[r], &b);
+                }
+            }
+            or_fr_batch_invert((uint64_t *)mod, n);
+            for (int c = c0; c < c1; c++) {
+                int t = s->perm_columns[2 * c], idx = s->perm_columns[2 * c + 1];
+                fe *vals = t == COL_ADVICE ? adv[idx] : (t == COL_FIXED ? (fe *)(s->fixed_values + 4 * n * idx) : inst_vals[idx]);
+                fe dw = deltaomega;
+                for (uint64_t r = 0; r < n; r++) {
+                    fe a, b; fr_mul(&a, &dw, &beta); fr_add(&a, &a, &gamma); fr_add(&b, &a, &vals[r]);
+                    fr_mul(&mod[r], &mod[r], &b);
+                    fr_mul(&dw, &dw, &D.omega);
+                }
+                fr_mul(&deltaomega, &deltaomega, &FR_DELTA);
+            }
+            fe *z = fr_alloc(n);
+            z[0] = last_z;
+            for (uint64_t r = 1; r < n; r++) fr_mul(&z[r], &z[r - 1], &mod[r - 1]);
+            for (uint64_t r = n - bf; r < n; r++) fr_random(&rng, &z[r]);
+            last_z = z[n - (bf + 1)];
+            fe blind; fr_random(&rng, &blind);
+            g1a cm; commit_msm(z, n, s->srs_g_lagrange, threads, &cm);
+            lagrange_to_coeff_d(&D, z, threads);
+            z_poly[st] = z;
+            z_coset[st] = fr_alloc(ext);
+            coeff_to_extended_d(&D, z, z_coset[st], threads);
+            if (tr_write_point(&T, &cm)) return -5;
+        }
+        free(mod);
+    }
+    /* vanishing::Argument::commit (vanishing/prover.rs:40-98) */
+    fe *random_poly = fr_alloc(n);
+    {
+        uint64_t nt = s->vanishing_threads ? s->vanishing_threads : 1;
+        uint64_t chunk = n / nt, rem = n % nt;
+        uint64_t noff = 0, *off = (uint64_t *)calloc(nt + 1, sizeof(uint64_t));
+        for (uint64_t i = 0; i < rem && noff < nt; i++) off[noff++] = i * (chunk + 1);
+        if (chunk) for (uint64_t o = rem * (chunk + 1); noff < nt; o += chunk) off[noff++] = o;
+        uint8_t (*seeds)[32] = (uint8_t (*)[32])calloc(noff + 1, 32);
+        for (uint64_t i = 0; i < noff; i++) chacha_rng_fill(&rng, seeds[i], 32);
+        for (uint64_t i = 0; i < noff; i++) {
+            uint64_t lo = off[i], hi = i + 1 < noff ? off[i + 1] : n;
+            chacha_rng cr; chacha_rng_init(&cr, seeds[i]);
+            for (uint64_t r = lo; r < hi; r++) fr_random(&cr, &random_poly[r]);
+        }
+        free(off); free(seeds);
+    }
+    fe random_blind; fr_random(&rng, &random_blind); (void)random_blind;
+    {
+        g1a cm; commit_msm(random_poly, n, s->srs_g, threads, &cm);
+        if (tr_write_point(&T, &cm)) return -5;
+    }
+    /* advice to coefficient form */
+    for (uint32_t c = 0; c < s->num_advice; c++) lagrange_to_coeff_d(&D, adv[c], threads);
+    fe y = tr_squeeze(&T);
+    /* evaluate_h (evaluation.rs:317-483) */
+    fe *h = fr_alloc(ext);
+    {
+        fe **adv_c = (fe **)calloc(s->num_advice + 1, sizeof(fe *)), **ins_c = (fe **)calloc(s->num_instance + 1, sizeof(fe *));
+        for (uint32_t c = 0; c < s->num_advice; c++) { adv_c[c] = fr_alloc(ext); coeff_to_extended_d(&D, adv[c], adv_c[c], threads); }
+        for (uint32_t c = 0; c < s->num_instance; c++) { ins_c[c] = fr_alloc(ext); coeff_to_extended_d(&D, inst_polys[c], ins_c[c], threads); }
+        const fe delta_start_beta = beta;   /* delta_start = beta * ZETA */
+        fe delta_start; fr_mul(&delta_start, &delta_start_beta, &FR_ZETA);
+        const int last_rot = -(bf + 1);
+#pragma omp parallel for num_threads(threads) schedule(static)
+        for (uint64_t idx = 0; idx < ext; idx++) {
+            fe v = {{0, 0, 0, 0}};
+            for (uint32_t g = 0; g < s->num_gates; g++) {
+                fe gv = eval_node(s, s->gate_roots[g], adv_c, fixed_cosets, ins_c, idx, rot_scale, ext);
+                fr_mul(&v, &v, &y); fr_add(&v, &v, &gv);
+            }
+            if (nsets > 0) {
+                uint64_t r_next = (idx + rot_scale) % ext;
+                int64_t rl = ((int64_t)idx + (int64_t)last_rot * (int64_t)rot_scale) % (int64_t)ext;
+                uint64_t r_last = (uint64_t)(rl < 0 ? rl + (int64_t)ext : rl);
+                fe t, u;
+                /* l0 (1 - z_0) */
+                fr_sub(&t, &fr_ONE, &z_coset[0][idx]); fr_mul(&t, &t, &l0[idx]);
+                fr_mul(&v, &v, &y); fr_add(&v, &v, &t);
+                /* l_last (z_last^2 - z_last) */
+                fe *zl = z_coset[nsets - 1];
+                fr_mul(&t, &zl[idx], &zl[idx]); fr_sub(&t, &t, &zl[idx]); fr_mul(&t, &t, &l_last[idx]);
+                fr_mul(&v, &v, &y); fr_add(&v, &v, &t);
+                for (int st = 1; st < nsets; st++) {
+                    fr_sub(&t, &z_coset[st][idx], &z_coset[st - 1][r_last]); fr_mul(&t, &t, &l0[idx]);
+                    fr_mul(&v, &v, &y); fr_add(&v, &v, &t);
+                }
+                fe beta_term = fr_pow_u64(&D.extended_omega, idx), cur;
+                fr_mul(&cur, &delta_start, &beta_term);
+                for (int st = 0; st < nsets; st++) {
+                    int c0 = st * chunk_len, c1 = c0 + chunk_len < P ? c0 + chunk_len : P;
+                    fe left = z_coset[st][r_next], right = z_coset[st][idx];
+                    for (int c = c0; c < c1; c++) {
+                        int tt = s->perm_columns[2 * c], ix = s->perm_columns[2 * c + 1];
+                        fe *col = tt == COL_ADVICE ? adv_c[ix] : (tt == COL_FIXED ? fixed_cosets[ix] : ins_c[ix]);
+                        fr_mul(&t, &beta, &sigma_cosets[c][idx]); fr_add(&t, &t, &col[idx]); fr_add(&t, &t, &gamma);
+                        fr_mul(&left, &left, &t);
+                    }
+                    for (int c = c0; c < c1; c++) {
+                        int tt = s->perm_columns[2 * c], ix = s->perm_columns[2 * c + 1];
+                        fe *col = tt == COL_ADVICE ? adv_c[ix] : (tt == COL_FIXED ? fixed_cosets[ix] : ins_c[ix]);
+                        fr_add(&t, &col[idx], &cur); fr_add(&t, &t, &gamma);
+                        fr_mul(&right, &right, &t);
+                        fr_mul(&cur, &cur, &FR_DELTA);
+                    }
+                    fr_sub(&u, &left, &right); fr_mul(&u, &u, &l_active[idx]);
+                    fr_mul(&v, &v, &y); fr_add(&v, &v, &u);
+                }
+            }
+            h[idx] = v;
+        }
+        for (uint32_t c = 0; c < s->num_advice; c++) free(adv_c[c]);
+        for (uint32_t c = 0; c < s->num_instance; c++) free(ins_c[c]);
+        free(adv_c); free(ins_c);
+    }
+    /* vanishing.construct (vanishing/prover.rs:102-155) */
+    const int npieces = degree - 1;
+    fe **pieces = (fe **)calloc(npieces + 1, sizeof(fe *));
+    {
+        for (uint64_t i = 0; i < ext; i++) fr_mul(&h[i], &h[i], &D.t_evaluations[i % D.t_len]);
+        fe *hc = fr_alloc(n * npieces);
+        or_extended_to_coeff((uint64_t *)h, (uint64_t *)hc, (uint32_t)degree, k, threads);
+        for (int p = 0; p < npieces; p++) { pieces[p] = fr_alloc(n); memcpy(pieces[p], hc + n * p, n * 32); }
+        free(hc);
+        for (int p = 0; p < npieces; p++) { fe b; fr_random(&rng, &b); }
+        for (int p = 0; p < npieces; p++) {
+            g1a cm; commit_msm(pieces[p], n, s->srs_g, threads, &cm);
+            if (tr_write_point(&T, &cm)) return -5;
+        }
+    }
+    free(h);
+    fe x = tr_squeeze(&T);
+    fe xn = fr_pow_u64(&x, n);
+    /* evaluations (prover.rs:735-836) */
+    for (int i = 0; i < adv_q.n; i++) {
+        fe pt = rotate_omega(&D, &x, adv_q.q[i].rot), e = eval_poly(adv[adv_q.q[i].index], n, &pt);
+        tr_write_scalar(&T, &e);
+    }
+    for (int i = 0; i < fix_q.n; i++) {
+        fe pt = rotate_omega(&D, &x, fix_q.q[i].rot), e = eval_poly(fixed_polys[fix_q.q[i].index], n, &pt);
+        tr_write_scalar(&T, &e);
+    }
+    fe *h_poly = fr_alloc(n);   /* h(X) = sum_p x^{n p} piece_p (vanishing/prover.rs:166-170) */
+    for (int p = npieces - 1; p >= 0; p--)
+        for (uint64_t i = 0; i < n; i++) { fe t; fr_mul(&t, &h_poly[i], &xn); fr_add(&h_poly[i], &t, &pieces[p][i]); }
+    { fe e = eval_poly(random_poly, n, &x); tr_write_scalar(&T, &e); }
+    for (int c = 0; c < P; c++) { fe e = eval_poly(sigma_polys[c], n, &x); tr_write_scalar(&T, &e); }
+    const fe x_next = rotate_omega(&D, &x, 1), x_last = rotate_omega(&D, &x, -(bf + 1));
+    for (int st = 0; st < nsets; st++) {
+        fe e0 = eval_poly(z_poly[st], n, &x), e1 = eval_poly(z_poly[st], n, &x_next);
+        tr_write_scalar(&T, &e0); tr_write_scalar(&T, &e1);
+        if (st + 1 < nsets) { fe e2 = eval_poly(z_poly[st], n, &x_last); tr_write_scalar(&T, &e2); }
+    }
+    /* queries (prover.rs:840-889) -- poly ids: advice c -> c, fixed c -> A+c, sigma c -> A+F+c,
+       z st -> A+F+P+st, h -> ..+nsets, random -> ..+1 */
+    const int A_ = (int)s->num_advice, F_ = (int)s->num_fixed;
+    const int id_h = A_ + F_ + P + nsets, id_r = id_h + 1, npolys = id_r + 1;
+    fe **polys = (fe **)calloc(npolys, sizeof(fe *));
+    for (int c = 0; c < A_; c++) polys[c] = adv[c];
+    for (int c = 0; c < F_; c++) polys[A_ + c] = fixed_polys[c];
+    for (int c = 0; c < P; c++) polys[A_ + F_ + c] = sigma_polys[c];
+    for (int st = 0; st < nsets; st++) polys[A_ + F_ + P + st] = z_poly[st];
+    polys[id_h] = h_poly; polys[id_r] = random_poly;
+    int nq = 0, qcap = adv_q.n + fix_q.n + 3 * nsets + P + 2;
+    query_ref *Q = (query_ref *)calloc(qcap, sizeof(query_ref));
+    for (int i = 0; i < adv_q.n; i++) { Q[nq].point = rotate_omega(&D, &x, adv_q.q[i].rot); Q[nq++].poly_id = adv_q.q[i].index; }
+    for (int st = 0; st < nsets; st++) {
+        Q[nq].point = x; Q[nq++].poly_id = A_ + F_ + P + st;
+        Q[nq].point = x_next; Q[nq++].poly_id = A_ + F_ + P + st;
+    }
+    for (int st = nsets - 2; st >= 0; st--) { Q[nq].point = x_last; Q[nq++].poly_id = A_ + F_ + P + st; }
+    for (int i = 0; i < fix_q.n; i++) { Q[nq].point = rotate_omega(&D, &x, fix_q.q[i].rot); Q[nq++].poly_id = A_ + fix_q.q[i].index; }
+    for (int c = 0; c < P; c++) { Q[nq].point = x; Q[nq++].poly_id = A_ + F_ + c; }
+    Q[nq].point = x; Q[nq++].poly_id = id_h;
+    Q[nq].point = x; Q[nq++].poly_id = id_r;
+
+    /* ---- SHPLONK (shplonk/prover.rs:121-305, shplonk.rs:48-140) ---- */
+    fe sy = tr_squeeze(&T);
+    /* super point set (sorted, unique) */
+    fe *sps = fr_alloc(nq); int nsp = 0;
+    for (int i = 0; i < nq; i++) {
+        int found = 0; for (int j = 0; j < nsp; j++) if (fe_eq(&sps[j], &Q[i].point)) { found = 1; break; }
+        if (!found) sps[nsp++] = Q[i].point;
+    }
+    for (int i = 1; i < nsp; i++) for (int j = i; j > 0 && fe_cmp_canon(&sps[j - 1], &sps[j]) > 0; j--) { fe t = sps[j]; sps[j] = sps[j - 1]; sps[j - 1] = t; }
+    /* commitment -> sorted point set, in order of first appearance */
+    int *cm_id = (int *)calloc(nq, sizeof(int)), ncm = 0;
+    fe **cm_pts = (fe **)calloc(nq, sizeof(fe *)); int *cm_npts = (int *)calloc(nq, sizeof(int));
+    for (int i = 0; i < nq; i++) {
+        int f = -1; for (int j = 0; j < ncm; j++) if (cm_id[j] == Q[i].poly_id) { f = j; break; }
+        if (f < 0) { f = ncm++; cm_id[f] = Q[i].poly_id; cm_pts[f] = fr_alloc(nq); cm_npts[f] = 0; }
+        int dup = 0; for (int j = 0; j < cm_npts[f]; j++) if (fe_eq(&cm_pts[f][j], &Q[i].point)) dup = 1;
+        if (!dup) {
+            fe *pp = cm_pts[f]; int m = cm_npts[f]++; pp[m] = Q[i].point;
+            for (int j = m; j > 0 && fe_cmp_canon(&pp[j - 1], &pp[j]) > 0; j--) { fe t = pp[j]; pp[j] = pp[j - 1]; pp[j - 1] = t; }
+        }
+    }
+    /* rotation sets grouped by equal point sets, first appearance order */
+    int nrs = 0; int *rs_of = (int *)calloc(ncm, sizeof(int)); int *rs_rep = (int *)calloc(ncm, sizeof(int));
+    for (int c = 0; c < ncm; c++) {
+        int f = -1;
+        for (int r = 0; r < nrs; r++) {
+            int rep = rs_rep[r];
+            if (cm_npts[rep] != cm_npts[c]) continue;
+            int same = 1; for (int j = 0; j < cm_npts[c]; j++) if (!fe_eq(&cm_pts[rep][j], &cm_pts[c][j])) { same = 0; break; }
+            if (same) { f = r; break; }
+        }
+        if (f < 0) { f = nrs++; rs_rep[f] = c; }
+        rs_of[c] = f;
+    }
+    /* low degree equivalents r_i (lagrange_interpolate over each set's points) */
+    fe **low = (fe **)calloc(ncm, sizeof(fe *));
+    for (int c = 0; c < ncm; c++) {
+        int m = cm_npts[c];
+        fe *ev = fr_alloc(m);
+        for (int j = 0; j < m; j++) ev[j] = eval_poly(polys[cm_id[c]], n, &cm_pts[c][j]);
+        low[c] = fr_alloc(m);
+        lagrange_interpolate(cm_pts[c], ev, m, low[c]);
+        free(ev);
+    }
+    fe v = tr_squeeze(&T);
+    fe *hx = fr_alloc(n);
+    {
+        fe vpow = fr_ONE;
+        fe *nx = fr_alloc(n), *tmp = fr_alloc(n), *q = fr_alloc(n);
+        for (int r = 0; r < nrs; r++) {
+            memset(nx, 0, n * 32);
+            fe ypow = fr_ONE;
+            for (int c = 0; c < ncm; c++) {
+                if (rs_of[c] != r) continue;
+                memcpy(tmp, polys[cm_id[c]], n * 32);
+                for (int j = 0; j < cm_npts[c]; j++) fr_sub(&tmp[j], &tmp[j], &low[c][j]);
+                for (uint64_t i = 0; i < n; i++) { fe t; fr_mul(&t, &tmp[i], &ypow); fr_add(&nx[i], &nx[i], &t); }
+                fr_mul(&ypow, &ypow, &sy);
+            }
+            /* div_by_vanishing: successive kate_division by each point */
+            int rep = rs_rep[r]; uint64_t len = n;
+            memcpy(q, nx, n * 32);
+            for (int j = 0; j < cm_npts[rep]; j++) {
+                fe *qq = fr_alloc(len);
+                or_kate_division((uint64_t *)q, len, cm_pts[rep][j].v, (uint64_t *)qq);
+                len--; memset(q, 0, n * 32); memcpy(q, qq, len * 32); free(qq);
+            }
+            for (uint64_t i = 0; i < n; i++) { fe t; fr_mul(&t, &q[i], &vpow); fr_add(&hx[i], &hx[i], &t); }
+            fr_mul(&vpow, &vpow, &v);
+        }
+        free(nx); free(tmp); free(q);
+    }
+    { g1a cm; commit_msm(hx, n, s->srs_g, threads, &cm); if (tr_write_point(&T, &cm)) return -5; }
+    fe u = tr_squeeze(&T);
+    fe *lx = fr_alloc(n);
+    fe z0 = fr_ONE;
+    {
+        fe vpow = fr_ONE;
+        fe *ls = fr_alloc(n);
+        for (int r = 0; r < nrs; r++) {
+            int rep = rs_rep[r];
+            fe zi = fr_ONE;   /* prod over super points not in this set of (u - p) */
+            for (int j = 0; j < nsp; j++) {
+                int in = 0; for (int t = 0; t < cm_npts[rep]; t++) if (fe_eq(&cm_pts[rep][t], &sps[j])) in = 1;
+                if (in) continue;
+                fe d; fr_sub(&d, &u, &sps[j]); fr_mul(&zi, &d, &zi);
+            }
+            if (r == 0) z0 = zi;
+            memset(ls, 0, n * 32);
+            fe ypow = fr_ONE;
+            for (int c = 0; c < ncm; c++) {
+                if (rs_of[c] != r) continue;
+                fe reval = eval_poly(low[c], cm_npts[c], &u);
+                for (uint64_t i = 0; i < n; i++) {
+                    fe t = polys[cm_id[c]][i];
+                    if (i == 0) fr_sub(&t, &t, &reval);
+                    fr_mul(&t, &t, &ypow); fr_add(&ls[i], &ls[i], &t);
+                }
+                fr_mul(&ypow, &ypow, &sy);
+            }
+            for (uint64_t i = 0; i < n; i++) { fe t; fr_mul(&t, &ls[i], &zi); fr_mul(&t, &t, &vpow); fr_add(&lx[i], &lx[i], &t); }
+            fr_mul(&vpow, &vpow, &v);
+        }
+        free(ls);
+        fe zt = fr_ONE;
+        for (int j = 0; j < nsp; j++) { fe d; fr_sub(&d, &u, &sps[j]); fr_mul(&zt, &d, &zt); }
+        for (uint64_t i = 0; i < n; i++) { fe t; fr_mul(&t, &hx[i], &zt); fr_sub(&lx[i], &lx[i], &t); }
+    }
+    {
+        fe *q = fr_alloc(n);
+        or_kate_division((uint64_t *)lx, n, u.v, (uint64_t *)q);
+        fe zinv; fr_inv(&zinv, &z0);
+        for (uint64_t i = 0; i + 1 < n; i++) fr_mul(&q[i], &q[i], &zinv);
+        g1a cm; commit_msm(q, n - 1, s->srs_g, threads, &cm);
+        if (tr_write_point(&T, &cm)) return -5;
+        free(q);
+    }
+    *proof_len = T.len;
+    /* (small per-proof buffers of this test-infrastructure routine are not all
+       released; the large ones are) */
+    free(lx); free(hx); free(h_poly); free(random_poly);
+    return T.len <= proof_cap ? 0 : -6;
+}
+
+int or_create_proof(const or_spec *s, uint8_t *proof, uint64_t proof_cap, uint64_t *proof_len, int threads) {
+    or_pk *pk = or_keygen(s, threads);
+    if (!pk) return -2;
+    int rc = or_prove(pk, s, proof, proof_cap, proof_len, threads);
+    or_pk_free(pk);
+    return rc;
+}
+
+/* exported helpers for tests */
+void or_blake2b(const uint8_t *in, uint64_t len, const uint8_t *personal, uint8_t *out64) {
+    blake2b_state S; blake2b_init(&S, 64, personal);
+    blake2b_update(&S, in, len);
+    blake2b_final_copy(&S, out64);
+}
+void or_chacha20_block(const uint8_t *key, uint64_t counter, uint8_t *out64) { chacha20_block(key, counter, out64); }
+void or_fr_random_stream(const uint8_t *seed, uint64_t count, uint64_t *out) {
+    chacha_rng r; chacha_rng_init(&r, seed);
+    for (uint64_t i = 0; i < count; i++) fr_random(&r, (fe *)(out + 4 * i));
+}
+
+/* g_lagrange_i = [L_i(s)] G, L_i(s) = omega^i (s^n - 1) / (n (s - omega^i))
+ * (ParamsKZG::setup, halo2_backend/src/poly/kzg/commitment.rs:92-131) */
+void or_srs_lagrange(const uint64_t *s_, uint32_t k, uint64_t *out) {
+    static const uint64_t GEN[8] = {0xd35d438dc58f0d9dULL, 0x0a78eb28f5c70b3dULL, 0x666ea36f7879462cULL, 0x0e0a77c19a07df2fULL,
+                                    0xa6ba871b8b1e1b3aULL, 0x14f1d651eb8e167bULL, 0xccdd46def0f28c58ULL, 0x1c14ef83340fbe5eULL};
+    const uint64_t n = 1ULL << k;
+    const fe s = fe_from(s_);
+    fe root = FR_ROOT_OF_UNITY;
+    for (uint32_t i = k; i < FR_S; i++) fr_sqr(&root, &root);
+    fe ninv, mult; fr_from_u64(&ninv, n); fr_inv(&ninv, &ninv);
+    mult = fr_pow_u64(&s, n); fr_sub(&mult, &mult, &fr_ONE); fr_mul(&mult, &mult, &ninv);
+    g1j g; g1j_from_a(&g, (const g1a *)GEN);
+#pragma omp parallel for schedule(dynamic, 16)
+    for (uint64_t i = 0; i < n; i++) {
+        fe rp = fr_pow_u64(&root, i), d, sc;
+        fr_sub(&d, &s, &rp); fr_inv(&d, &d);
+        fr_mul(&sc, &mult, &rp); fr_mul(&sc, &sc, &d);
+        g1j r; g1j_mul(&r, &g, &sc);
+        g1j_to_a((g1a *)(out + 8 * i), &r);
+    }
+}

@@ -60,6 +60,16 @@ def lib():
             "or_fr_batch_invert": ([U64P, u64], None),
             "or_fr_prefix_product": ([U64P, U64P, u64], None),
             "or_num_threads": ([], i32),
+            "or_keygen": ([ctypes.c_void_p, i32], ctypes.c_void_p),
+            "or_prove": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p, u64, U64P, i32], i32),
+            "or_pk_free": ([ctypes.c_void_p], None),
+            "or_pk_info": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], None),
+            "or_pk_sigma": ([ctypes.c_void_p, i32, U64P], None),
+            "or_create_proof": ([ctypes.c_void_p, ctypes.c_char_p, u64, U64P, i32], i32),
+            "or_srs_lagrange": ([U64P, u32, U64P], None),
+            "or_blake2b": ([ctypes.c_char_p, u64, ctypes.c_char_p, ctypes.c_char_p], None),
+            "or_chacha20_block": ([ctypes.c_char_p, u64, ctypes.c_char_p], None),
+            "or_fr_random_stream": ([ctypes.c_char_p, u64, U64P], None),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -193,3 +203,119 @@ def random_fr(rng, n):
     c[:, 3] &= np.uint64((1 << 61) - 1)  # < 2^253 < r
     c[:, 0] = rng.integers(0, 2**63, size=n, dtype=np.int64).astype(np.uint64) * np.uint64(2) + (c[:, 0] & np.uint64(1))
     return fr_from_canonical(c)
+
+
+# ----------------------------------------------------------------------------- prover
+I32P = ctypes.POINTER(ctypes.c_int32)
+U8P = ctypes.POINTER(ctypes.c_uint8)
+U32P = ctypes.POINTER(ctypes.c_uint32)
+
+
+class OrSpec(ctypes.Structure):
+    """struct or_spec (oracle/c/prover.c)"""
+    _fields_ = [
+        ("k", ctypes.c_uint32), ("num_advice", ctypes.c_uint32), ("num_fixed", ctypes.c_uint32),
+        ("num_instance", ctypes.c_uint32),
+        ("num_gates", ctypes.c_uint32), ("gate_roots", I32P),
+        ("num_nodes", ctypes.c_uint32), ("nodes", I32P),
+        ("num_constants", ctypes.c_uint32), ("constants", U64P),
+        ("num_perm_columns", ctypes.c_uint32), ("perm_columns", I32P),
+        ("num_copies", ctypes.c_uint32), ("copies", I32P),
+        ("fixed_values", U64P), ("advice_values", U64P), ("instance_values", U64P),
+        ("instance_lens", U32P), ("transcript_repr", U64P), ("rng_seed", U8P),
+        ("vanishing_threads", ctypes.c_uint32), ("srs_g", U64P), ("srs_g_lagrange", U64P),
+        ("unblinded", U8P),
+    ]
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(t) if a is not None and a.size else None
+
+
+def make_spec(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=8):
+    """Builds the or_spec; returns (struct, keepalive list)."""
+    keep = [np.ascontiguousarray(x) for x in (
+        circ.gate_roots, circ.nodes, circ.constants, circ.perm_array, circ.copies, circ.fixed_values,
+        wit.advice, wit.instance, wit.instance_lens, circ.transcript_repr(),
+        np.frombuffer(bytes(seed), dtype=np.uint8).copy(), srs_g, srs_gl, circ.unblinded)]
+    (roots, nodes, consts, perm, copies, fixed, adv, ins, lens, tr, sd, g, gl, unb) = keep
+    s = OrSpec(circ.k, circ.num_advice, circ.num_fixed, circ.num_instance,
+               len(roots), _ptr(roots, I32P), len(nodes), _ptr(nodes, I32P),
+               circ.num_constants, _ptr(consts, U64P), len(perm), _ptr(perm, I32P),
+               len(copies), _ptr(copies, I32P), _ptr(fixed, U64P), _ptr(adv, U64P), _ptr(ins, U64P),
+               _ptr(lens, U32P), _ptr(tr, U64P), _ptr(sd, U8P), vanishing_threads,
+               _ptr(g, U64P), _ptr(gl, U64P), _ptr(unb, U8P))
+    return s, keep
+
+
+def srs_lagrange(s, k):
+    out = np.zeros((1 << k, 8), dtype=np.uint64)
+    lib().or_srs_lagrange(_p(np.ascontiguousarray(s)), k, _p(out))
+    return out
+
+
+_SRS_CACHE = {}
+
+
+def srs(k, s_int=None):
+    """(s (Montgomery limbs), g, g_lagrange) for a known toxic s (test setup)."""
+    import h2g_circuit as hc
+    if s_int is None:
+        s_int = 0x1234567890ABCDEF1122334455667788 * 3 + k
+    key = (k, s_int)
+    if key not in _SRS_CACHE:
+        s = np.asarray(hc.fr_to_limbs(s_int), dtype=np.uint64)
+        _SRS_CACHE[key] = (s_int, srs_powers(s, 1 << k), srs_lagrange(s, k))
+    return _SRS_CACHE[key]
+
+
+class Keygen:
+    def __init__(self, circ, wit, srs_g, srs_gl, threads=8):
+        self.spec, self.keep = make_spec(circ, wit, srs_g, srs_gl)
+        self.pk = lib().or_keygen(ctypes.byref(self.spec), threads)
+        if not self.pk:
+            raise ValueError("or_keygen failed")
+        info = (ctypes.c_int32 * 8)()
+        lib().or_pk_info(self.pk, info)
+        self.degree, self.bf, self.extended_k, self.P, self.n_adv_q, self.n_fix_q, self.n_ins_q, self.nsets = list(info)
+        self.n = 1 << circ.k
+
+    def sigma(self, i):
+        out = np.zeros((self.n, 4), dtype=np.uint64)
+        lib().or_pk_sigma(self.pk, i, _p(out))
+        return out
+
+    def close(self):
+        if self.pk:
+            lib().or_pk_free(self.pk)
+            self.pk = None
+
+    def __del__(self):
+        self.close()
+
+
+def create_proof(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=8, threads=8, keygen=None):
+    """Oracle create_proof -> proof bytes."""
+    spec, keep = make_spec(circ, wit, srs_g, srs_gl, seed, vanishing_threads)
+    cap = 1 << 20
+    buf = ctypes.create_string_buffer(cap)
+    ln = np.zeros(1, dtype=np.uint64)
+    if keygen is not None:
+        rc = lib().or_prove(keygen.pk, ctypes.byref(spec), buf, cap, _p(ln), threads)
+    else:
+        rc = lib().or_create_proof(ctypes.byref(spec), buf, cap, _p(ln), threads)
+    if rc != 0:
+        raise ValueError(f"oracle create_proof failed: {rc}")
+    return buf.raw[: int(ln[0])]
+
+
+class OracleOps:
+    """vectorised Montgomery arithmetic for witness generation (h2g_circuit.synthetic_c3)"""
+
+    @staticmethod
+    def mul(a, b):
+        return binop("or_fr_mul", np.ascontiguousarray(a), np.ascontiguousarray(b))
+
+    @staticmethod
+    def prefix_product(a):
+        return prefix_product(np.ascontiguousarray(a))

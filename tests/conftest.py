@@ -5,6 +5,7 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "oracle", "py"))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "yet-another-halo2-fork_amd"))
 

@@ -1,0 +1,157 @@
+"""CPU tests of the create_proof restatement (oracle/c/prover.c) and its pins:
+the transcript hash / RNG known answers, keygen's permutation vs an independent
+restatement, and prove -> verify with the independent Python verifier
+(oracle/py/verifier.py) -- the reference's own relational test
+(halo2_proofs/tests/plonk_api.rs: proofs must verify; corrupted ones must not)."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import h2g_circuit as hc
+import verifier as V
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _instances(circ, wit):
+    return [hc.mont_to_ints(wit.instance[i])[: int(wit.instance_lens[i])] for i in range(circ.num_instance)]
+
+
+def test_blake2b_personal_matches_hashlib():
+    import ctypes
+    rng = np.random.default_rng(0)
+    for ln in (0, 1, 33, 65, 127, 128, 129, 300):
+        d = rng.bytes(ln)
+        out = ctypes.create_string_buffer(64)
+        O.lib().or_blake2b(d, ln, b"Halo2-Transcript", out)
+        assert out.raw == hashlib.blake2b(d, digest_size=64, person=b"Halo2-Transcript").digest()
+
+
+def test_chacha20_known_answer():
+    """RFC 7539 zero-key keystream (= rand_chacha ChaCha20Rng::from_seed([0; 32]) test vector)"""
+    import ctypes
+    out = ctypes.create_string_buffer(64)
+    O.lib().or_chacha20_block(bytes(32), 0, out)
+    assert out.raw[:32].hex() == "76b8e0ada0f13d90405d6ae55386bd28bdd219b8a08ded1aa836efcc8b770dc7"
+    O.lib().or_chacha20_block(bytes(32), 1, out)
+    assert out.raw[:16].hex() == "9f07e7be5551387a98ba977c732d080d"
+
+
+def test_fr_random_is_le512_mod_r():
+    import ctypes
+    seed = bytes(range(32))
+    out = np.zeros((5, 4), dtype=np.uint64)
+    O.lib().or_fr_random_stream(seed, 5, O._p(out))
+    # keystream: blocks 0..4 of ChaCha20(seed)
+    ks = b""
+    buf = ctypes.create_string_buffer(64)
+    for c in range(5):
+        O.lib().or_chacha20_block(seed, c, buf)
+        ks += buf.raw
+    want = [int.from_bytes(ks[64 * i: 64 * i + 64], "little") % hc.R_MOD for i in range(5)]
+    assert hc.mont_to_ints(out) == want
+
+
+def test_one_rng_constant():
+    """with OneNg every Fr::random = LE512(0x01000000 x16) mod r"""
+    v = int.from_bytes(bytes([1, 0, 0, 0]) * 16, "little") % hc.R_MOD
+    assert v == 0x0FDD950C1DA3E00B1D2FB9CF61452B1EC0C9DFB910ECFB36B574601AEDF0313B
+
+
+CIRCUITS = {
+    "simple_k6": lambda: hc.simple_example(6),
+    "simple_k8": lambda: hc.simple_example(8),
+    "mixed_k7": lambda: hc.mixed_circuit(7),
+    "c3_k8": lambda: hc.synthetic_c3(8, O.OracleOps),
+}
+
+
+@pytest.mark.parametrize("name", list(CIRCUITS))
+def test_keygen_permutation_matches_restatement(name):
+    circ, wit = CIRCUITS[name]()
+    _, g, gl = O.srs(circ.k)
+    kg = O.Keygen(circ, wit, g, gl)
+    assert kg.degree == circ.degree() and kg.bf == circ.blinding_factors()
+    sig = V.sigma_lagrange(circ)
+    for i in range(len(circ.perm_columns)):
+        assert hc.mont_to_ints(kg.sigma(i)) == sig[i]
+
+
+@pytest.mark.parametrize("name", list(CIRCUITS))
+def test_prove_verify(name):
+    circ, wit = CIRCUITS[name]()
+    s, g, gl = O.srs(circ.k)
+    proof = O.create_proof(circ, wit, g, gl)
+    assert V.verify(circ, _instances(circ, wit), proof, s)
+
+
+def test_proof_deterministic_and_seed_dependent():
+    circ, wit = hc.simple_example(6)
+    s, g, gl = O.srs(circ.k)
+    p1 = O.create_proof(circ, wit, g, gl, seed=bytes([7] * 32), threads=1)
+    p2 = O.create_proof(circ, wit, g, gl, seed=bytes([7] * 32), threads=8)
+    p3 = O.create_proof(circ, wit, g, gl, seed=bytes([8] * 32))
+    p4 = O.create_proof(circ, wit, g, gl, vanishing_threads=3)
+    assert p1 == p2
+    assert p1 != p3 and p1 != p4
+    for p in (p3, p4):
+        assert V.verify(circ, _instances(circ, wit), p, s)
+
+
+def test_unsatisfied_gate_rejected():
+    circ, wit = hc.simple_example(6)
+    s, g, gl = O.srs(circ.k)
+    wit.advice[1, 0] = hc.fr_to_limbs(12345)   # a1[0] breaks s_mul * (a0 * a1 - a0[next])
+    proof = O.create_proof(circ, wit, g, gl)
+    assert not V.verify(circ, _instances(circ, wit), proof, s)
+
+
+def test_broken_copy_rejected():
+    circ, wit = hc.mixed_circuit(7)
+    s, g, gl = O.srs(circ.k)
+    lt, li, lr, rt, ri, rr = circ.copies[0]
+    assert lt == hc.ADVICE and rt == hc.ADVICE
+    wit.advice[ri, rr] = hc.fr_to_limbs(999)
+    proof = O.create_proof(circ, wit, g, gl)
+    assert not V.verify(circ, _instances(circ, wit), proof, s)
+
+
+def test_wrong_instance_rejected():
+    circ, wit = hc.simple_example(6)
+    s, g, gl = O.srs(circ.k)
+    proof = O.create_proof(circ, wit, g, gl)
+    ins = _instances(circ, wit)
+    ins[0][0] = (ins[0][0] + 1) % hc.R_MOD
+    assert not V.verify(circ, ins, proof, s)
+
+
+def test_tampered_proof_rejected():
+    circ, wit = hc.mixed_circuit(7)
+    s, g, gl = O.srs(circ.k)
+    proof = bytearray(O.create_proof(circ, wit, g, gl))
+    proof[-40] ^= 1
+    try:
+        assert not V.verify(circ, _instances(circ, wit), bytes(proof), s)
+    except V.VerifyError:
+        pass
+
+
+def test_instance_too_large_fails():
+    circ, wit = hc.simple_example(6)
+    _, g, gl = O.srs(circ.k)
+    wit.instance_lens[0] = circ.n - circ.blinding_factors()   # > n - (bf + 1)
+    with pytest.raises(ValueError):
+        O.create_proof(circ, wit, g, gl)
+
+
+def test_golden_proofs():
+    """committed fixtures (tests/golden/gen_proofs.py): the restatement reproduces them"""
+    d = np.load(os.path.join(GOLDEN, "proof_golden.npz"), allow_pickle=False)
+    for name in ("simple_k8", "mixed_k7"):
+        circ, wit = CIRCUITS[name]()
+        s, g, gl = O.srs(circ.k, int(d[f"{name}_s"].tobytes()[::-1].hex(), 16))
+        proof = O.create_proof(circ, wit, g, gl)
+        assert proof == d[f"{name}_proof"].tobytes()

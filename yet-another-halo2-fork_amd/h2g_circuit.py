@@ -1,0 +1,411 @@
+"""Backend circuit description consumed by keygen / create_proof, and the synthetic
+circuits the tests and the bench prove.
+
+This mirrors what the reference's backend receives from its frontend
+(`halo2_middleware/src/circuit.rs`): `ConstraintSystemMid` (column counts, gates as
+`ExpressionMid` trees, the permutation `ArgumentMid.columns`, unblinded advice
+columns) plus `Preprocessing` (fixed column values and `PermutationMid.copies`), and
+the witness of one proof (advice columns, instance columns).  Circuit authoring
+(chips, layouters, floor planners) is the frontend and out of scope; the generators
+below lay cells out directly.
+
+Expressions are flattened for the C ABI into nodes of 4 int32 `(op, a, b, c)`:
+  CONST (a = constant index) | QUERY (a = column type, b = column index, c = rotation)
+  | NEG (a = child) | SUM / PROD (a = lhs, b = rhs).
+Column types follow `halo2_middleware::circuit::Any` as used here: 0 advice,
+1 fixed, 2 instance.  Field elements travel as numpy uint64 arrays in halo2curves'
+layout (Montgomery form, 4 little-endian limbs).
+"""
+import hashlib
+
+import numpy as np
+
+ADVICE, FIXED, INSTANCE = 0, 1, 2
+OP_CONST, OP_QUERY, OP_NEG, OP_SUM, OP_PROD = 0, 1, 2, 3, 4
+
+R_MOD = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
+_MONT = (1 << 256) % R_MOD
+
+
+def fr_to_limbs(x: int) -> list:
+    """canonical int -> Montgomery limbs"""
+    m = (x % R_MOD) * _MONT % R_MOD
+    return [(m >> (64 * i)) & 0xFFFFFFFFFFFFFFFF for i in range(4)]
+
+
+def fr_from_limbs(l) -> int:
+    m = sum(int(l[i]) << (64 * i) for i in range(4))
+    return m * pow(_MONT, -1, R_MOD) % R_MOD
+
+
+def ints_to_mont(vals) -> np.ndarray:
+    out = np.zeros((len(vals), 4), dtype=np.uint64)
+    for i, v in enumerate(vals):
+        if v:
+            out[i] = fr_to_limbs(v)
+    return out
+
+
+def mont_to_ints(arr) -> list:
+    arr = np.asarray(arr, dtype=np.uint64).reshape(-1, 4)
+    return [fr_from_limbs(r) for r in arr]
+
+
+# ----------------------------------------------------------------------------- expressions
+class Expr:
+    """ExpressionMid (halo2_middleware/src/expression.rs) without challenges."""
+
+    __slots__ = ("op", "a", "b", "c")
+
+    def __init__(self, op, a=0, b=0, c=0):
+        self.op, self.a, self.b, self.c = op, a, b, c
+
+    def __add__(self, o):
+        return Expr(OP_SUM, self, _e(o))
+
+    def __radd__(self, o):
+        return Expr(OP_SUM, _e(o), self)
+
+    def __sub__(self, o):
+        return Expr(OP_SUM, self, Expr(OP_NEG, _e(o)))
+
+    def __rsub__(self, o):
+        return Expr(OP_SUM, _e(o), Expr(OP_NEG, self))
+
+    def __mul__(self, o):
+        return Expr(OP_PROD, self, _e(o))
+
+    def __rmul__(self, o):
+        return Expr(OP_PROD, _e(o), self)
+
+    def __neg__(self):
+        return Expr(OP_NEG, self)
+
+    def degree(self):
+        if self.op == OP_CONST:
+            return 0
+        if self.op == OP_QUERY:
+            return 1
+        if self.op == OP_NEG:
+            return self.a.degree()
+        if self.op == OP_SUM:
+            return max(self.a.degree(), self.b.degree())
+        return self.a.degree() + self.b.degree()
+
+    def evaluate(self, const, query, mod=R_MOD):
+        """Expression::evaluate with closures for constants and queries (ints mod r)."""
+        if self.op == OP_CONST:
+            return const(self.a) % mod
+        if self.op == OP_QUERY:
+            return query(self.a, self.b, self.c) % mod
+        if self.op == OP_NEG:
+            return (-self.a.evaluate(const, query, mod)) % mod
+        x = self.a.evaluate(const, query, mod)
+        y = self.b.evaluate(const, query, mod)
+        return (x + y) % mod if self.op == OP_SUM else (x * y) % mod
+
+
+def _e(x):
+    return x if isinstance(x, Expr) else const(int(x))
+
+
+def const(v: int) -> Expr:
+    return Expr(OP_CONST, int(v) % R_MOD)
+
+
+def advice(col, rot=0):
+    return Expr(OP_QUERY, ADVICE, col, rot)
+
+
+def fixed(col, rot=0):
+    return Expr(OP_QUERY, FIXED, col, rot)
+
+
+def instance(col, rot=0):
+    return Expr(OP_QUERY, INSTANCE, col, rot)
+
+
+# ----------------------------------------------------------------------------- circuit
+class Circuit:
+    """ConstraintSystemMid + Preprocessing (one compiled circuit)."""
+
+    def __init__(self, k, num_advice, num_fixed, num_instance, gates, perm_columns, copies,
+                 fixed_values, unblinded=None, name="circuit"):
+        self.k = int(k)
+        self.n = 1 << self.k
+        self.num_advice, self.num_fixed, self.num_instance = num_advice, num_fixed, num_instance
+        self.gates = list(gates)
+        self.perm_columns = [tuple(c) for c in perm_columns]
+        self.copies = np.asarray(copies, dtype=np.int32).reshape(-1, 6)
+        self.fixed_values = np.ascontiguousarray(fixed_values, dtype=np.uint64).reshape(num_fixed, self.n, 4)
+        self.unblinded = np.zeros(max(num_advice, 1), dtype=np.uint8)
+        for c in unblinded or []:
+            self.unblinded[c] = 1
+        self.name = name
+        self._flatten()
+
+    # -- ConstraintSystem facts (halo2_backend/src/plonk/circuit.rs, keygen.rs) --
+    def degree(self):
+        """required_degree with the permutation argument (degree 3) -- circuit.rs:292-320"""
+        return max([3] + [g.degree() for g in self.gates])
+
+    def queries(self):
+        """(advice, fixed, instance) query lists in first-appearance order: gate
+        expressions depth first (lhs before rhs), then permutation columns at
+        Rotation::cur() -- keygen.rs:191-260."""
+        lists = {ADVICE: [], FIXED: [], INSTANCE: []}
+
+        def add(t, i, r):
+            if (i, r) not in lists[t]:
+                lists[t].append((i, r))
+
+        def walk(e):
+            if e.op == OP_QUERY:
+                add(e.a, e.b, e.c)
+            elif e.op == OP_NEG:
+                walk(e.a)
+            elif e.op in (OP_SUM, OP_PROD):
+                walk(e.a)
+                walk(e.b)
+
+        for g in self.gates:
+            walk(g)
+        for t, i in self.perm_columns:
+            add(t, i, 0)
+        return lists[ADVICE], lists[FIXED], lists[INSTANCE]
+
+    def blinding_factors(self):
+        """max(3, max advice queries per column) + 2 -- circuit.rs:143-170"""
+        adv, _, _ = self.queries()
+        per_col = [sum(1 for (c, _) in adv if c == col) for col in range(self.num_advice)]
+        return max([3] + per_col) + 2 if self.num_advice else 5
+
+    def usable_rows(self):
+        return self.n - (self.blinding_factors() + 1)
+
+    def _flatten(self):
+        nodes, consts, const_idx = [], [], {}
+
+        def rec(e):
+            if e.op == OP_CONST:
+                if e.a not in const_idx:
+                    const_idx[e.a] = len(consts)
+                    consts.append(e.a)
+                nodes.append((OP_CONST, const_idx[e.a], 0, 0))
+            elif e.op == OP_QUERY:
+                nodes.append((OP_QUERY, e.a, e.b, e.c))
+            elif e.op == OP_NEG:
+                a = rec(e.a)
+                nodes.append((OP_NEG, a, 0, 0))
+            else:
+                a = rec(e.a)
+                b = rec(e.b)
+                nodes.append((e.op, a, b, 0))
+            return len(nodes) - 1
+
+        roots = [rec(g) for g in self.gates]
+        self.nodes = np.asarray(nodes, dtype=np.int32).reshape(-1, 4)
+        self.gate_roots = np.asarray(roots, dtype=np.int32)
+        self.constants = ints_to_mont(consts) if consts else np.zeros((1, 4), dtype=np.uint64)
+        self.num_constants = len(consts)
+        self.perm_array = np.asarray(self.perm_columns, dtype=np.int32).reshape(-1, 2)
+
+    def transcript_repr(self) -> np.ndarray:
+        """vk.transcript_repr.  The reference hashes the Debug text of the pinned VK
+        (plonk.rs:189-200: Blake2b-512, personal "Halo2-Verify-Key", length-prefixed,
+        from_uniform_bytes); that text cannot be reproduced outside Rust, so the same
+        construction is applied to this description's canonical bytes."""
+        h = hashlib.blake2b(digest_size=64, person=b"Halo2-Verify-Key")
+        desc = b"".join([
+            np.asarray([self.k, self.num_advice, self.num_fixed, self.num_instance], dtype=np.int64).tobytes(),
+            self.nodes.tobytes(), self.gate_roots.tobytes(), self.constants.tobytes(),
+            self.perm_array.tobytes(), self.copies.tobytes(), self.unblinded.tobytes(),
+            hashlib.blake2b(self.fixed_values.tobytes()).digest(),
+        ])
+        h.update(len(desc).to_bytes(8, "little"))
+        h.update(desc)
+        v = int.from_bytes(h.digest(), "little") % R_MOD
+        return np.asarray(fr_to_limbs(v), dtype=np.uint64)
+
+
+class Witness:
+    """One proof's advice and instance columns (Lagrange values, length n each)."""
+
+    def __init__(self, advice_values, instance_values, instance_lens):
+        self.advice = np.ascontiguousarray(advice_values, dtype=np.uint64)
+        self.instance = np.ascontiguousarray(instance_values, dtype=np.uint64)
+        self.instance_lens = np.ascontiguousarray(instance_lens, dtype=np.uint32)
+        if self.instance_lens.size == 0:
+            self.instance_lens = np.zeros(1, dtype=np.uint32)
+
+
+# ----------------------------------------------------------------------------- generators
+def _rand_ints(rng, count):
+    return [int.from_bytes(rng.bytes(32), "little") % R_MOD for _ in range(count)]
+
+
+def simple_example(k=8, seed=1, blocks=None):
+    """C1: the simple-example constraint system (halo2_proofs/examples/simple-example.rs:
+    98-117,266-277): advice a0, a1; instance i; fixed `constant` (enable_constant) and
+    the s_mul selector (as a fixed column); gate s_mul * (a0 * a1 - a0[next]);
+    equality on instance, constant, a0, a1.  Cells are laid out in 4-row blocks
+    computing c = constant * (a*b)^2 and exposing c in the instance column."""
+    n = 1 << k
+    rng = np.random.default_rng(seed)
+    a0, a1 = [0] * n, [0] * n
+    fconst, smul = [0] * n, [0] * n
+    inst = [0] * n
+    copies = []
+    gates = [fixed(1) * (advice(0) * advice(1) - advice(0, 1))]
+    perm = [(INSTANCE, 0), (FIXED, 0), (ADVICE, 0), (ADVICE, 1)]
+    # a0 has 2 queries (cur, next) -> bf = 5, usable = n - 6
+    usable = n - 6
+    nblocks = blocks if blocks is not None else max(1, (usable - 1) // 4)
+    for blk in range(nblocks):
+        r = 4 * blk
+        if r + 4 > usable:
+            break
+        a, b = _rand_ints(rng, 2)
+        cst = 7 + blk
+        ab = a * b % R_MOD
+        absq = ab * ab % R_MOD
+        c = cst * absq % R_MOD
+        a0[r], a1[r], smul[r] = a, b, 1          # ab = a * b
+        a0[r + 1], a1[r + 1], smul[r + 1] = ab, ab, 1   # absq = ab * ab
+        a0[r + 2], a1[r + 2], smul[r + 2] = absq, cst, 1  # c = absq * constant
+        a0[r + 3] = c
+        fconst[blk] = cst
+        inst[blk] = c
+        copies += [(ADVICE, 0, r + 1, ADVICE, 1, r + 1),
+                   (FIXED, 0, blk, ADVICE, 1, r + 2),
+                   (ADVICE, 0, r + 3, INSTANCE, 0, blk)]
+    fixed_vals = np.stack([ints_to_mont(fconst), ints_to_mont(smul)])
+    circ = Circuit(k, 2, 2, 1, gates, perm, copies, fixed_vals, name=f"simple-example k={k}")
+    wit = Witness(np.stack([ints_to_mont(a0), ints_to_mont(a1)]), ints_to_mont(inst)[None],
+                  [nblocks])
+    return circ, wit
+
+
+def mixed_circuit(k=7, seed=2):
+    """A circuit exercising every expression/argument feature the backend supports:
+    degree 5 (extended domain 4n), rotations -1/+1/+2, constants, negation, instance
+    queries inside gates, fixed and instance columns in the permutation, two
+    permutation sets (chunk_len 3), an unblinded advice column."""
+    n = 1 << k
+    rng = np.random.default_rng(seed)
+    A, B, C, D, E = range(5)
+    Q1, Q2, Q3, K = range(4)
+    gates = [
+        fixed(Q1) * (advice(A) * advice(B) * advice(C) - advice(D) + 7),
+        fixed(Q2) * (advice(A, 1) - advice(A) - advice(B, -1)),
+        fixed(Q3) * (advice(C) * advice(D) * advice(A, 2) * advice(B) - const(5) * instance(0)),
+        -(fixed(Q1) * (advice(D) - instance(1))),
+        fixed(Q2) * advice(E) * (advice(E) - 1),   # E boolean on q2 rows; E is unblinded
+    ]
+    perm = [(ADVICE, A), (FIXED, K), (INSTANCE, 0), (ADVICE, C), (ADVICE, B), (ADVICE, D)]
+    circ0 = Circuit(k, 5, 4, 2, gates, perm, [], np.zeros((4, n, 4), np.uint64))
+    u = circ0.usable_rows()
+    va = _rand_ints(rng, n)
+    vb = _rand_ints(rng, n)
+    vc = _rand_ints(rng, n)
+    vd = _rand_ints(rng, n)
+    ve = [0] * n
+    for r in range(n):
+        va[r] = va[r] if r < u else 0
+        vb[r] = vb[r] if r < u else 0
+        vc[r] = vc[r] if r < u else 0
+        vd[r] = vd[r] if r < u else 0
+    q1, q2, q3, kf = [0] * n, [0] * n, [0] * n, [0] * n
+    for r in range(u):
+        if r % 3 == 0:
+            q1[r] = 1
+        elif r % 3 == 1 and r + 1 < u:
+            q2[r] = 1
+            ve[r] = int(rng.integers(0, 2))
+        elif r % 3 == 2 and r + 2 < u:
+            q3[r] = 1
+    i0, i1 = [0] * n, [0] * n
+    copies = []
+    # copies between free cells (set before the constrained cells are derived)
+    used_b, used_a = set(), set()
+    for r in range(1, u - 3, 7):
+        r2 = (r * 5 + 3) % (u - 2)
+        if r2 % 3 == 0 or r2 in used_b:
+            continue
+        used_b.add(r2)
+        vb[r2] = vc[r]
+        copies.append((ADVICE, C, r, ADVICE, B, r2))
+    # c[r] == a[r3] for a few free a cells (r3 % 3 in {0,1}); joins the cycles above
+    for r in range(2, u - 3, 11):
+        r3 = (r * 3 + 1) % (u - 3)
+        if r3 % 3 == 2 or r3 in used_a:
+            continue
+        used_a.add(r3)
+        va[r3] = vc[r]
+        copies.append((ADVICE, A, r3, ADVICE, C, r))
+    # fixed constants copied into c cells
+    for j, r in enumerate(range(5, u, 13)):
+        kf[j] = vc[r]
+        copies.append((FIXED, K, j, ADVICE, C, r))
+    # constrained cells
+    for r in range(u):
+        if r % 3 == 2 and r >= 2:
+            va[r] = (va[r - 1] + vb[r - 2]) % R_MOD if q2[r - 1] else va[r]
+    for r in range(u):
+        if q1[r]:
+            vd[r] = (va[r] * vb[r] % R_MOD * vc[r] + 7) % R_MOD
+            i1[r] = vd[r]
+    inv5 = pow(5, -1, R_MOD)
+    for r in range(u):
+        if q3[r]:
+            i0[r] = vc[r] * vd[r] % R_MOD * va[r + 2] % R_MOD * vb[r] % R_MOD * inv5 % R_MOD
+        elif r % 3 == 0:
+            i0[r] = va[r]
+            copies.append((INSTANCE, 0, r, ADVICE, A, r))
+    fixed_vals = np.stack([ints_to_mont(q1), ints_to_mont(q2), ints_to_mont(q3), ints_to_mont(kf)])
+    circ = Circuit(k, 5, 4, 2, gates, perm, copies, fixed_vals, unblinded=[E], name=f"mixed k={k}")
+    wit = Witness(np.stack([ints_to_mont(v) for v in (va, vb, vc, vd, ve)]),
+                  np.stack([ints_to_mont(i0), ints_to_mont(i1)]), [u, u])
+    return circ, wit
+
+
+def synthetic_c3(k, ops, seed=3):
+    """C3: 3 advice a, b, c; 1 fixed f; gate f * (a * b - c); a, b, c in
+    the permutation (3 sets); copies c_i -> a_{i+1} chain every usable row.
+    Witness: random b, a_0; a_{i+1} = c_i = a_i * b_i (a prefix product), f = 1 on
+    usable rows.  `ops` supplies vectorised Montgomery arithmetic (mul, prefix_product)
+    so that k = 20..24 builds in seconds (GPU ops on the bench box, the C oracle in CPU
+    tests)."""
+    n = 1 << k
+    gates = [fixed(0) * (advice(0) * advice(1) - advice(2))]
+    perm = [(ADVICE, 0), (ADVICE, 1), (ADVICE, 2)]
+    bf = 5
+    u = n - (bf + 1)
+    rng = np.random.default_rng(seed)
+    b = random_mont(rng, n)
+    b[u:] = 0
+    a0 = random_mont(rng, 1)
+    # a_i = a0 * prod_{j<i} b_j  for i < u
+    pp = ops.prefix_product(b)              # pp_i = prod_{j<=i} b_j
+    a = np.empty_like(b)
+    a[0] = a0[0]
+    a[1:] = ops.mul(pp[:-1], np.broadcast_to(a0, (n - 1, 4)).copy())
+    a[u:] = 0
+    c = ops.mul(a, b)
+    f = np.zeros((1, n, 4), dtype=np.uint64)
+    one = np.asarray(fr_to_limbs(1), dtype=np.uint64)
+    f[0, :u] = one
+    rows = np.arange(u - 1, dtype=np.int32)
+    copies = np.stack([np.full(u - 1, ADVICE, np.int32), np.full(u - 1, 2, np.int32), rows,
+                       np.full(u - 1, ADVICE, np.int32), np.zeros(u - 1, np.int32), rows + 1], axis=1)
+    circ = Circuit(k, 3, 1, 0, gates, perm, copies, f, name=f"synthetic-c3 k={k}")
+    wit = Witness(np.stack([a, b, c]), np.zeros((0, n, 4), dtype=np.uint64), [])
+    return circ, wit
+
+
+def random_mont(rng, count):
+    """uniform-ish field elements already in Montgomery form (top limb < r's top limb)"""
+    x = rng.integers(0, 2**63, size=(count, 4), dtype=np.int64).astype(np.uint64) * np.uint64(2)
+    x += rng.integers(0, 2, size=(count, 4), dtype=np.int64).astype(np.uint64)
+    x[:, 3] %= np.uint64(0x30644E72E131A029)
+    return x
