@@ -141,6 +141,61 @@ int h2g_profile_msm_collect(float* ms, int max_phases, int* n_phases, int* calls
 /* ---- host-side point helpers (used to combine per-GPU MSM partials) -------- */
 int h2g_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);
 
+
+/* ---- create_proof (BN254 / KZG / SHPLONK, Blake2b transcript) -------------
+ * The backend entry points of halo2_backend/src/plonk/{keygen.rs, prover.rs}:
+ *   ParamsKZG::{setup, read}   poly/kzg/commitment.rs:64-131,167-267  -> h2g_params_*
+ *   keygen_vk + keygen_pk      plonk/keygen.rs:43-190                  -> h2g_keygen
+ *   create_proof(params, pk, circuits=[1], instances, rng, transcript)
+ *                              plonk/prover.rs:174-899 (ProverSingle)  -> h2g_create_proof
+ * The circuit is the backend's CompiledCircuit (halo2_middleware/src/circuit.rs):
+ * gates as flattened ExpressionMid nodes, permutation columns + copies, fixed values.
+ * Node = 4 x int32 (op, a, b, c): op 0 CONST (a = constant index), 1 QUERY (a = column
+ * type 0 advice / 1 fixed / 2 instance, b = column index, c = rotation), 2 NEG (a),
+ * 3 SUM (a, b), 4 PROD (a, b).  Copy = 6 x int32 (ltype, lindex, lrow, rtype, rindex, rrow).
+ * Supported: one advice phase, no challenges, no lookups/shuffles (H2G_ERR_ARG).
+ * rng: ChaCha20Rng::from_seed(rng_seed); vanishing_threads: the thread count that
+ * splits the vanishing argument's random polynomial into ChaCha streams
+ * (vanishing/prover.rs:57-81), part of the proof's determinism. */
+typedef struct {
+  uint32_t k, num_advice, num_fixed, num_instance;
+  uint32_t num_gates;
+  const int32_t* gate_roots;
+  uint32_t num_nodes;
+  const int32_t* nodes;
+  uint32_t num_constants;
+  const uint64_t* constants;      /* Fr */
+  uint32_t num_perm_columns;
+  const int32_t* perm_columns;    /* (type, index) pairs, permutation ArgumentMid.columns order */
+  uint32_t num_copies;
+  const int32_t* copies;
+  const uint64_t* fixed_values;   /* num_fixed x n Fr (Lagrange) */
+  const uint8_t* unblinded;       /* num_advice flags (unblinded_advice_columns) or NULL */
+  const uint64_t* transcript_repr; /* vk.transcript_repr (Fr) */
+} h2g_circuit;
+
+/* SRS resident on the current device: g[n] and g_lagrange[n] (G1Affine) from the host... */
+int h2g_params_create(uint32_t k, const uint64_t* g, const uint64_t* g_lagrange, uint64_t* handle);
+/* ...or generated on the device from the toxic secret s (ParamsKZG::setup; tests/bench) */
+int h2g_params_setup(uint32_t k, const uint64_t s[4], uint64_t* handle);
+int h2g_params_export(uint64_t params, uint64_t* g, uint64_t* g_lagrange); /* n x 8 u64 each, may be NULL */
+int h2g_params_free(uint64_t params);
+
+int h2g_keygen(uint64_t params, const h2g_circuit* circuit, uint64_t* pk);
+int h2g_pk_free(uint64_t pk);
+/* degree, blinding_factors, extended_k, #perm sets, #advice/#fixed/#instance queries */
+int h2g_pk_info(uint64_t pk, int32_t info[8]);
+
+/* advice: num_advice x n Fr; instance: num_instance x n Fr (zero padded), of which
+ * instance_lens[i] values enter the transcript.  Writes the proof bytes.
+ * advice_on_device != 0: `advice` is a device pointer (inputs resident in HBM). */
+int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int advice_on_device,
+                     const uint64_t* instance, const uint32_t* instance_lens, const uint8_t rng_seed[32],
+                     uint32_t vanishing_threads, uint8_t* proof, size_t proof_cap, size_t* proof_len);
+/* wall milliseconds of the stages of the last h2g_create_proof (names: h2g_prover_stage_name) */
+int h2g_prover_stages(double* ms, int max, int* count);
+const char* h2g_prover_stage_name(int i);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,120 @@
+"""GPU parity of the device create_proof pipeline (through the C ABI) against the
+C restatement prover (oracle/c/prover.c): proof bytes must be identical, and
+proofs must verify under the independent Python verifier (oracle/py/verifier.py)."""
+import numpy as np
+import pytest
+
+import _oracle as O
+import h2g
+import h2g_circuit as hc
+import verifier as V
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _init():
+    h2g.init()
+    yield
+
+
+def _instances(circ, wit):
+    return [hc.mont_to_ints(wit.instance[i])[: int(wit.instance_lens[i])] for i in range(circ.num_instance)]
+
+
+_PARAMS = {}
+
+
+def _params(k):
+    if k not in _PARAMS:
+        s, g, gl = O.srs(k)
+        _PARAMS[k] = (s, g, gl, h2g.Params(k, g, gl))
+    return _PARAMS[k]
+
+
+def test_params_setup_matches_oracle_srs():
+    for k in (4, 8):
+        s_int, g, gl = O.srs(k)
+        p = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(s_int), dtype=np.uint64))
+        dg, dgl = p.export()
+        assert np.array_equal(dg, g)
+        assert np.array_equal(dgl, gl)
+        p.close()
+
+
+CASES = {
+    "simple_k6": lambda: hc.simple_example(6),
+    "simple_k8": lambda: hc.simple_example(8),
+    "mixed_k7": lambda: hc.mixed_circuit(7),
+    "mixed_k10": lambda: hc.mixed_circuit(10, seed=5),
+    "c3_k8": lambda: hc.synthetic_c3(8, O.OracleOps),
+    "c3_k12": lambda: hc.synthetic_c3(12, O.OracleOps, seed=9),
+}
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_proof_bytes_match_oracle(name):
+    circ, wit = CASES[name]()
+    s, g, gl, params = _params(circ.k)
+    pk = h2g.ProvingKey(params, circ)
+    assert pk.degree == circ.degree() and pk.bf == circ.blinding_factors()
+    want = O.create_proof(circ, wit, g, gl)
+    got = pk.create_proof(wit)
+    assert len(got) == len(want)
+    assert got == want
+    # a second proof with the same key reuses the workspace and is identical
+    assert pk.create_proof(wit) == want
+    # another rng seed / vanishing split: still identical to the oracle
+    want2 = O.create_proof(circ, wit, g, gl, seed=bytes(range(32)), vanishing_threads=3)
+    assert pk.create_proof(wit, seed=bytes(range(32)), vanishing_threads=3) == want2
+    pk.close()
+
+
+def test_golden_proofs_on_device():
+    d = np.load(O.os.path.join(O.REPO, "tests", "golden", "proof_golden.npz"), allow_pickle=False)
+    for name in ("simple_k8", "mixed_k7"):
+        circ, wit = CASES[name]()
+        s = int(d[f"{name}_s"].tobytes()[::-1].hex(), 16)
+        _, g, gl = O.srs(circ.k, s)
+        params = h2g.Params(circ.k, g, gl)
+        pk = h2g.ProvingKey(params, circ)
+        assert pk.create_proof(wit) == d[f"{name}_proof"].tobytes()
+        pk.close()
+        params.close()
+
+
+def test_device_proof_verifies_and_rejects_bad_witness():
+    circ, wit = hc.mixed_circuit(8, seed=11)
+    s, g, gl, params = _params(8)
+    pk = h2g.ProvingKey(params, circ)
+    proof = pk.create_proof(wit)
+    assert V.verify(circ, _instances(circ, wit), proof, s)
+    bad = hc.Witness(wit.advice.copy(), wit.instance.copy(), wit.instance_lens.copy())
+    bad.advice[0, 3] = hc.fr_to_limbs(4242)
+    assert not V.verify(circ, _instances(circ, bad), pk.create_proof(bad), s)
+    pk.close()
+
+
+def test_advice_resident_on_device():
+    circ, wit = hc.synthetic_c3(10, O.OracleOps, seed=4)
+    s, g, gl, params = _params(10)
+    pk = h2g.ProvingKey(params, circ)
+    buf = h2g.DevBuf.from_array(np.ascontiguousarray(wit.advice))
+    got = pk.create_proof(advice_dev_ptr=buf.ptr, wit=wit)
+    assert got == O.create_proof(circ, wit, g, gl)
+    buf.close()
+    pk.close()
+
+
+def test_errors():
+    circ, wit = hc.simple_example(6)
+    s, g, gl, params = _params(6)
+    pk = h2g.ProvingKey(params, circ)
+    bad = hc.Witness(wit.advice, wit.instance, np.asarray([circ.n - circ.blinding_factors()], np.uint32))
+    with pytest.raises(h2g.H2GError, match="InstanceTooLarge"):
+        pk.create_proof(bad)
+    pk.close()
+    other = h2g.Params(7, *O.srs(7)[1:])
+    with pytest.raises(h2g.H2GError, match="params k"):
+        h2g.ProvingKey(other, circ)
+    other.close()

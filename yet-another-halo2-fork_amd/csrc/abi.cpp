@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/h2g.h"
+#include "runtime.h"
 #include "bn254.h"
 #include "msm.h"
 #include "ntt.h"
@@ -24,11 +25,23 @@
 #include "srs.h"
 
 using namespace h2g;
+using namespace h2g::rt;
 
-namespace {
+namespace h2g {
+namespace rt {
 
 thread_local std::string g_err;
 std::recursive_mutex g_mu;
+std::vector<std::unique_ptr<Device>> g_devs;
+bool g_profile = false;
+std::vector<MsmPhaseEvents> g_msm_prof;
+int g_cur = 0;
+std::map<uint64_t, Descriptor> g_desc;
+std::map<uint64_t, std::unique_ptr<Domain>> g_dom;
+uint64_t g_next_handle = 1;
+
+
+
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -38,77 +51,26 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(H2G_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define HIPCHK(expr)                                       \
-  do {                                                     \
-    hipError_t _e = (expr);                                \
-    if (_e != hipSuccess) return hip_fail(_e, #expr);      \
-  } while (0)
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-    hipError_t e = hipMalloc(&p, bytes);
-    if (e == hipSuccess) cap = bytes;
-    return e;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-};
 
-struct NttKey {
-  int L;
-  uint32_t w[8];
-  bool operator<(const NttKey& o) const {
-    if (L != o.L) return L < o.L;
-    return std::memcmp(w, o.w, sizeof(w)) < 0;
-  }
-};
 
-struct Domain {
-  uint32_t j, k, ek;
-  Fr omega, omega_inv, ext_omega, ext_omega_inv, g_coset, g_coset_inv, ifft_div, ext_ifft_div, bary;
-  std::vector<Fr> t_evals;
-  Fr* d_t = nullptr;
-};
 
-struct Descriptor {
-  int device;
-  void* d = nullptr;
-  size_t n = 0;
-  bool is_base = false;
-};
 
-struct Device {
-  int id = 0;
-  hipStream_t stream = nullptr;
-  MsmWorkspace msm;
-  DevBuf a, b, c, work, out;
-  std::map<NttKey, NttTables> ntt_tables;
-  void* h_windows = nullptr;  // pinned host copy of MSM window sums
-};
 
-std::vector<std::unique_ptr<Device>> g_devs;
-bool g_profile = false;
-std::vector<MsmPhaseEvents> g_msm_prof;
-int g_cur = 0;
-std::map<uint64_t, Descriptor> g_desc;
-std::map<uint64_t, std::unique_ptr<Domain>> g_dom;
-uint64_t g_next_handle = 1;
+
+
+
+
+
+
+
 
 Device* cur() {
   if (g_devs.empty()) return nullptr;
   return g_devs[g_cur].get();
 }
 
-hipStream_t pick_stream(Device* d, void* s) { return s ? reinterpret_cast<hipStream_t>(s) : d->stream; }
+
 
 Fr fr_from_limbs(const uint64_t* v) {
   Fr r;
@@ -131,7 +93,7 @@ Fr zeta() {
   const uint64_t v[4] = {0x93e7cede4a0329b3ULL, 0x7d4fdca77a96c167ULL, 0x8be4ba08b19a750aULL, 0x1cbd5653a5661c25ULL};
   return fr_from_limbs(v);
 }
-constexpr uint32_t FR_S = 28;
+
 
 int get_tables(Device* d, const Fr& omega, int L, hipStream_t st, NttTables* out) {
   NttKey key{L, {}};
@@ -227,7 +189,79 @@ Domain* get_dom(uint64_t h) {
   return it == g_dom.end() ? nullptr : it->second.get();
 }
 
-}  // namespace
+
+int domain_init(Domain* dm, uint32_t j, uint32_t k) {   // EvaluationDomain::new (domain.rs:38-144)
+  if (j < 2 || k > FR_S) return fail(H2G_ERR_ARG, "domain: bad j/k");
+  dm->j = j;
+  dm->k = k;
+  const uint64_t n = 1ull << k;
+  const uint64_t qdeg = j - 1;
+  uint32_t ek = k;
+  while ((1ull << ek) < n * qdeg) ek++;
+  if (ek > FR_S) return fail(H2G_ERR_ARG, "domain: extended_k > S");
+  dm->ek = ek;
+  Fr eo = root_of_unity();
+  for (uint32_t i = ek; i < FR_S; i++) eo = sqr(eo);
+  Fr o = eo;
+  for (uint32_t i = k; i < ek; i++) o = sqr(o);
+  dm->ext_omega = eo;
+  dm->omega = o;
+  dm->g_coset = zeta();
+  dm->g_coset_inv = sqr(dm->g_coset);
+  const uint64_t tlen = 1ull << (ek - k);
+  const Fr orig = pow_u64(dm->g_coset, n), step = pow_u64(eo, n);
+  Fr c = orig;
+  dm->t_evals.resize(tlen);
+  for (uint64_t i = 0; i < tlen; i++) {
+    dm->t_evals[i] = inv(c - Fr::one());
+    c = c * step;
+  }
+  dm->ifft_div = inv(from_u64<FrParams>(n));
+  dm->ext_ifft_div = inv(from_u64<FrParams>(1ull << ek));
+  dm->bary = inv(from_u64<FrParams>(n));
+  dm->ext_omega_inv = inv(eo);
+  dm->omega_inv = inv(o);
+  HIPCHK(hipMalloc(&dm->d_t, tlen * sizeof(Fr)));
+  HIPCHK(hipMemcpy(dm->d_t, dm->t_evals.data(), tlen * sizeof(Fr), hipMemcpyHostToDevice));
+  return H2G_OK;
+}
+
+void domain_release(Domain* dm) {
+  if (dm->d_t) (void)hipFree(dm->d_t);
+  dm->d_t = nullptr;
+}
+
+// lagrange_to_coeff (domain.rs:216-226): iFFT, * 1/n
+int lagrange_to_coeff(Device* d, const Domain& dm, const Fr* src, Fr* dst, hipStream_t st) {
+  const Fr one = Fr::one();
+  const uint64_t n = 1ull << dm.k;
+  return ntt_dev_impl(d, src, n, dst, n, (int)dm.k, dm.omega_inv, 0, one, one, 1, dm.ifft_div, 0, one, one, st);
+}
+
+// coeff_to_extended (domain.rs:230-244): distribute zeta powers, zero-pad, FFT over the extended domain
+int coeff_to_extended(Device* d, const Domain& dm, const Fr* src, Fr* dst, hipStream_t st) {
+  const Fr one = Fr::one();
+  const uint64_t n = 1ull << dm.k, ext = 1ull << dm.ek;
+  return ntt_dev_impl(d, src, n, dst, ext, (int)dm.ek, dm.ext_omega, 1, dm.g_coset, dm.g_coset_inv, 0, one, 0, one,
+                      one, st);
+}
+
+// extended_to_coeff (domain.rs:271-293): inverse FFT, * 1/2^ek, undistribute, truncate to n (j - 1)
+int extended_to_coeff(Device* d, const Domain& dm, const Fr* src, Fr* dst, hipStream_t st) {
+  const Fr one = Fr::one();
+  const uint64_t ext = 1ull << dm.ek;
+  const uint64_t out_len = (1ull << dm.k) * (dm.j - 1);
+  return ntt_dev_impl(d, src, ext, dst, out_len, (int)dm.ek, dm.ext_omega_inv, 0, one, one, 1, dm.ext_ifft_div, 1,
+                      dm.g_coset_inv, dm.g_coset, st);
+}
+
+Fr fr_delta() {
+  const uint64_t v[4] = {0x9a0c322befd78855ULL, 0x46e82d14249b563cULL, 0x5983a663e0b0b7a7ULL, 0x22ab452baaa111adULL};
+  return fr_from_limbs(v);
+}
+
+}  // namespace rt
+}  // namespace h2g
 
 #define NEED_DEV()                                                            \
   std::lock_guard<std::recursive_mutex> _lk(g_mu);                            \
@@ -441,39 +475,9 @@ int h2g_fft(uint64_t* a, uint32_t log_n, const uint64_t omega[4]) {
 // ---------------------------------------------------------------- EvaluationDomain
 int h2g_domain_create(uint32_t j, uint32_t k, uint64_t* handle) {
   NEED_DEV();
-  if (!handle || j < 2 || k > FR_S) return fail(H2G_ERR_ARG, "domain: bad j/k");
+  if (!handle) return fail(H2G_ERR_ARG, "domain: null handle");
   auto dm = std::make_unique<Domain>();
-  dm->j = j;
-  dm->k = k;
-  const uint64_t n = 1ull << k;
-  const uint64_t qdeg = j - 1;
-  uint32_t ek = k;
-  while ((1ull << ek) < n * qdeg) ek++;
-  if (ek > FR_S) return fail(H2G_ERR_ARG, "domain: extended_k > S");
-  dm->ek = ek;
-  Fr eo = root_of_unity();
-  for (uint32_t i = ek; i < FR_S; i++) eo = sqr(eo);
-  Fr o = eo;
-  for (uint32_t i = k; i < ek; i++) o = sqr(o);
-  dm->ext_omega = eo;
-  dm->omega = o;
-  dm->g_coset = zeta();
-  dm->g_coset_inv = sqr(dm->g_coset);
-  const uint64_t tlen = 1ull << (ek - k);
-  const Fr orig = pow_u64(dm->g_coset, n), step = pow_u64(eo, n);
-  Fr cur = orig;
-  dm->t_evals.resize(tlen);
-  for (uint64_t i = 0; i < tlen; i++) {
-    dm->t_evals[i] = inv(cur - Fr::one());
-    cur = cur * step;
-  }
-  dm->ifft_div = inv(from_u64<FrParams>(n));
-  dm->ext_ifft_div = inv(from_u64<FrParams>(1ull << ek));
-  dm->bary = inv(from_u64<FrParams>(n));
-  dm->ext_omega_inv = inv(eo);
-  dm->omega_inv = inv(o);
-  HIPCHK(hipMalloc(&dm->d_t, tlen * sizeof(Fr)));
-  HIPCHK(hipMemcpy(dm->d_t, dm->t_evals.data(), tlen * sizeof(Fr), hipMemcpyHostToDevice));
+  RCCHK(domain_init(dm.get(), j, k));
   *handle = g_next_handle++;
   g_dom[*handle] = std::move(dm);
   return H2G_OK;
@@ -507,10 +511,7 @@ int h2g_lagrange_to_coeff_dev(uint64_t dom, void* a, void* stream) {
   Domain* dm = get_dom(dom);
   if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
   if (!a) return fail(H2G_ERR_ARG, "null");
-  const Fr one = Fr::one();
-  const uint64_t n = 1ull << dm->k;
-  return ntt_dev_impl(d, (const Fr*)a, n, (Fr*)a, n, (int)dm->k, dm->omega_inv, 0, one, one, 1, dm->ifft_div, 0,
-                      one, one, pick_stream(d, stream));
+  return lagrange_to_coeff(d, *dm, (const Fr*)a, (Fr*)a, pick_stream(d, stream));
 }
 
 int h2g_coeff_to_extended_dev(uint64_t dom, const void* a, void* out, void* stream) {
@@ -519,10 +520,7 @@ int h2g_coeff_to_extended_dev(uint64_t dom, const void* a, void* out, void* stre
   if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
   if (!a || !out) return fail(H2G_ERR_ARG, "null");
   if (a == out) return fail(H2G_ERR_ARG, "coeff_to_extended: in and out must differ");
-  const Fr one = Fr::one();
-  const uint64_t n = 1ull << dm->k, ext = 1ull << dm->ek;
-  return ntt_dev_impl(d, (const Fr*)a, n, (Fr*)out, ext, (int)dm->ek, dm->ext_omega, 1, dm->g_coset,
-                      dm->g_coset_inv, 0, one, 0, one, one, pick_stream(d, stream));
+  return coeff_to_extended(d, *dm, (const Fr*)a, (Fr*)out, pick_stream(d, stream));
 }
 
 int h2g_extended_to_coeff_dev(uint64_t dom, const void* a, void* out, void* stream) {
@@ -530,12 +528,7 @@ int h2g_extended_to_coeff_dev(uint64_t dom, const void* a, void* out, void* stre
   Domain* dm = get_dom(dom);
   if (!dm) return fail(H2G_ERR_HANDLE, "unknown domain");
   if (!a || !out) return fail(H2G_ERR_ARG, "null");
-  const Fr one = Fr::one();
-  const uint64_t ext = 1ull << dm->ek;
-  const uint64_t out_len = (1ull << dm->k) * (dm->j - 1);
-  // inverse FFT, * 1/2^ek, then distribute_powers_zeta(into_coset = false): [zeta^2, zeta]
-  return ntt_dev_impl(d, (const Fr*)a, ext, (Fr*)out, out_len, (int)dm->ek, dm->ext_omega_inv, 0, one, one, 1,
-                      dm->ext_ifft_div, 1, dm->g_coset_inv, dm->g_coset, pick_stream(d, stream));
+  return extended_to_coeff(d, *dm, (const Fr*)a, (Fr*)out, pick_stream(d, stream));
 }
 
 int h2g_divide_by_vanishing_poly_dev(uint64_t dom, void* a, void* stream) {

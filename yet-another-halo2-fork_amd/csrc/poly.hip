@@ -7,24 +7,11 @@
 // shuffle/prover.rs:150) and the grand-product recurrences
 // (permutation/prover.rs:160-166, lookup/prover.rs:254-265, shuffle/prover.rs:161-172).
 #include "poly.h"
+#include "fr_io.h"
 
 namespace h2g {
 
 static constexpr int PT = 256;
-
-__device__ __forceinline__ Fr ldf(const Fr* p) {
-  const uint4* q = reinterpret_cast<const uint4*>(p);
-  uint4 a = q[0], b = q[1];
-  Fr r;
-  r.l[0] = a.x; r.l[1] = a.y; r.l[2] = a.z; r.l[3] = a.w;
-  r.l[4] = b.x; r.l[5] = b.y; r.l[6] = b.z; r.l[7] = b.w;
-  return r;
-}
-__device__ __forceinline__ void stf(Fr* p, const Fr& v) {
-  uint4* q = reinterpret_cast<uint4*>(p);
-  q[0] = make_uint4(v.l[0], v.l[1], v.l[2], v.l[3]);
-  q[1] = make_uint4(v.l[4], v.l[5], v.l[6], v.l[7]);
-}
 
 static unsigned grid_for(size_t n) {
   size_t g = (n + PT - 1) / PT;

@@ -1,0 +1,1174 @@
+// prover.cpp -- keygen and create_proof on the device (BN254 / KZG / SHPLONK).
+//
+// Host orchestration of halo2_backend's prover, all polynomial data resident in HBM:
+//   keygen_vk / keygen_pk          plonk/keygen.rs:43-190, circuit.rs:95-180,292-320
+//   permutation Assembly/build_pk  plonk/permutation/keygen.rs:16-213
+//   Prover::new_with_engine        plonk/prover.rs:174-305 (instances)
+//   commit_phase                   plonk/prover.rs:309-494 (one phase, no challenges)
+//   create_proof                   plonk/prover.rs:512-899
+//   permutation_commit/evaluate    plonk/permutation/prover.rs:50-333
+//   vanishing commit/construct     plonk/vanishing/prover.rs:40-205
+//   evaluate_h                     plonk/evaluation.rs:317-483
+//   SHPLONK                        poly/kzg/multiopen/shplonk/prover.rs:121-305, shplonk.rs:48-140
+// Host work is the transcript, the prover RNG's few hundred draws, query bookkeeping
+// and O(#queries^2) interpolation; every length-n or extended-length operation is a
+// kernel (MSM, NTT, prover_kernels.hip, poly.hip).  MSM results come back to the host
+// (they enter the transcript), which is the only per-step synchronisation.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <chrono>
+#include <functional>
+#include <set>
+
+#include "poly.h"
+#include "prover_kernels.h"
+#include "runtime.h"
+#include "srs.h"
+#include "transcript.h"
+
+using namespace h2g;
+using namespace h2g::rt;
+
+namespace {
+
+enum { COL_ADVICE = 0, COL_FIXED = 1, COL_INSTANCE = 2 };
+enum { OP_CONST = 0, OP_QUERY = 1, OP_NEG = 2, OP_SUM = 3, OP_PROD = 4 };
+
+struct Pool {  // owns device allocations of one params / pk object
+  std::vector<void*> ptrs;
+  hipError_t get(void** p, size_t bytes) {
+    hipError_t e = hipMalloc(p, bytes ? bytes : 16);
+    if (e == hipSuccess) ptrs.push_back(*p);
+    return e;
+  }
+  ~Pool() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+};
+#define PALLOC(pool, ptr, count) HIPCHK((pool).get((void**)&(ptr), (size_t)(count) * sizeof(*(ptr))))
+
+struct Params {
+  int device = 0;
+  uint32_t k = 0;
+  size_t n = 0;
+  G1Affine* g = nullptr;
+  G1Affine* gl = nullptr;
+  Pool pool;
+};
+
+struct Query {
+  int type, index, rot;
+  bool operator==(const Query& o) const { return type == o.type && index == o.index && rot == o.rot; }
+};
+
+struct ProvingKey {
+  int device = 0;
+  uint64_t params = 0;
+  uint32_t k = 0;
+  size_t n = 0, ext = 0;
+  uint64_t rot_scale = 0;
+  int degree = 0, bf = 0, P = 0, nsets = 0, chunk_len = 0;
+  int A = 0, F = 0, I = 0;
+  std::vector<Query> adv_q, fix_q, ins_q;
+  std::vector<std::pair<int, int>> perm_cols;
+  std::vector<uint8_t> unblinded;
+  Fr transcript_repr;
+  Domain dom;
+  Pool pool;
+  // proving key (device)
+  std::vector<Fr*> fixed_lag, fixed_poly, fixed_coset, sigma_lag, sigma_poly, sigma_coset;
+  Fr *l0 = nullptr, *l_last = nullptr, *l_active = nullptr;
+  PowTable om, eo;
+  int4* prog = nullptr;
+  int prog_len = 0, n_slots = 0;
+  Fr* consts = nullptr;
+  int n_loads = 0;
+  const Fr** d_load_col = nullptr;
+  int* d_load_rot = nullptr;
+  const Fr** d_z = nullptr;
+  const Fr** d_perm_v = nullptr;
+  const Fr** d_sigma = nullptr;
+  // per-proof workspace (device), reused across proofs
+  std::vector<Fr*> adv, adv_coset, inst_val, inst_poly, inst_coset, z, z_coset;
+  Fr *mod = nullptr, *pre = nullptr, *scr = nullptr, *random_poly = nullptr, *h_ext = nullptr, *h_coeff = nullptr;
+  Fr *h_poly = nullptr, *nx = nullptr, *q1 = nullptr, *q2 = nullptr, *hx = nullptr, *lx = nullptr;
+  Fr *small = nullptr, *last_z = nullptr, *evals = nullptr, *eval_scr = nullptr;
+  size_t scr_len = 0, eval_scr_len = 0;
+  EvalReq* d_reqs = nullptr;
+  int max_reqs = 0;
+  uint32_t* d_seeds = nullptr;
+  uint64_t* d_offsets = nullptr;
+  int max_chunks = 0;
+};
+
+std::map<uint64_t, std::unique_ptr<Params>> g_params;
+std::map<uint64_t, std::unique_ptr<ProvingKey>> g_pks;
+std::vector<std::pair<const char*, double>> g_stages;
+
+// ------------------------------------------------------------------ host field helpers
+int fr_cmp(const Fr& a, const Fr& b) {  // Ord on Fr: canonical numeric order
+  const Fr ca = to_canonical(a), cb = to_canonical(b);
+  for (int i = 7; i >= 0; i--) {
+    if (ca.l[i] < cb.l[i]) return -1;
+    if (ca.l[i] > cb.l[i]) return 1;
+  }
+  return 0;
+}
+Fr fr_neg_one() { return Fr::zero() - Fr::one(); }
+
+Fr rotate_omega(const Domain& d, const Fr& x, int rot) {
+  return x * pow_u64(rot >= 0 ? d.omega : d.omega_inv, (uint64_t)(rot >= 0 ? rot : -rot));
+}
+
+// coefficients of the unique polynomial of degree < m through (pts[i], ev[i])
+std::vector<Fr> lagrange_interpolate(const std::vector<Fr>& pts, const std::vector<Fr>& ev) {
+  const size_t m = pts.size();
+  std::vector<Fr> out(m, Fr::zero());
+  for (size_t j = 0; j < m; j++) {
+    std::vector<Fr> num(1, Fr::one());
+    Fr den = Fr::one();
+    for (size_t k = 0; k < m; k++) {
+      if (k == j) continue;
+      std::vector<Fr> nn(num.size() + 1, Fr::zero());
+      for (size_t i = 0; i < num.size(); i++) {
+        nn[i + 1] = nn[i + 1] + num[i];
+        nn[i] = nn[i] - pts[k] * num[i];
+      }
+      num.swap(nn);
+      den = den * (pts[j] - pts[k]);
+    }
+    const Fr sc = ev[j] * inv(den);
+    for (size_t i = 0; i < m; i++) out[i] = out[i] + num[i] * sc;
+  }
+  return out;
+}
+Fr eval_host(const std::vector<Fr>& p, const Fr& x) {
+  Fr acc = Fr::zero();
+  for (size_t i = p.size(); i-- > 0;) acc = acc * x + p[i];
+  return acc;
+}
+
+// two-level power table of w for exponents < 2^L
+int build_pow_table(Pool& pool, const Fr& w, int L, PowTable* t, hipStream_t st) {
+  const int bits = (L + 1) / 2;
+  const size_t nlo = (size_t)1 << bits, nhi = (size_t)1 << (L - bits > 0 ? L - bits : 0);
+  std::vector<Fr> lo(nlo), hi(nhi);
+  lo[0] = Fr::one();
+  for (size_t i = 1; i < nlo; i++) lo[i] = lo[i - 1] * w;
+  const Fr wb = lo[nlo - 1] * w;  // w^(2^bits)
+  hi[0] = Fr::one();
+  for (size_t i = 1; i < nhi; i++) hi[i] = hi[i - 1] * wb;
+  Fr *dlo, *dhi;
+  PALLOC(pool, dlo, nlo);
+  PALLOC(pool, dhi, nhi);
+  HIPCHK(hipMemcpyAsync(dlo, lo.data(), nlo * sizeof(Fr), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(dhi, hi.data(), nhi * sizeof(Fr), hipMemcpyHostToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
+  t->lo = dlo;
+  t->hi = dhi;
+  t->bits = bits;
+  return H2G_OK;
+}
+
+int commit(Device* d, const Fr* scalars, size_t n, const G1Affine* bases, G1Affine* out, hipStream_t st) {
+  int is_id = 0;
+  return msm_host_impl(d, scalars, bases, n, 0, reinterpret_cast<uint64_t*>(out), &is_id, st);
+}
+
+// Debug aid: H2G_DUMP=<dir> writes named intermediates (raw Fr arrays) of create_proof.
+void dump(const char* name, const Fr* dptr, size_t count, hipStream_t st, bool host = false) {
+  static const char* dir = std::getenv("H2G_DUMP");
+  if (!dir) return;
+  std::vector<Fr> h(count);
+  if (host) std::memcpy(h.data(), dptr, count * sizeof(Fr));
+  else {
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpy(h.data(), dptr, count * sizeof(Fr), hipMemcpyDeviceToHost);
+  }
+  const std::string path = std::string(dir) + "/" + name + ".bin";
+  if (FILE* f = std::fopen(path.c_str(), "wb")) {
+    std::fwrite(h.data(), sizeof(Fr), count, f);
+    std::fclose(f);
+  }
+}
+
+// ------------------------------------------------------------------ circuit analysis
+struct CircuitView {
+  const h2g_circuit* c;
+  const int32_t* node(int i) const { return c->nodes + 4 * i; }
+};
+
+int node_degree(const CircuitView& v, int i, std::vector<int>& memo) {
+  if (memo[i] >= 0) return memo[i];
+  const int32_t* nd = v.node(i);
+  int d = 0;
+  switch (nd[0]) {
+    case OP_CONST: d = 0; break;
+    case OP_QUERY: d = 1; break;
+    case OP_NEG: d = node_degree(v, nd[1], memo); break;
+    case OP_SUM: d = std::max(node_degree(v, nd[1], memo), node_degree(v, nd[2], memo)); break;
+    default: d = node_degree(v, nd[1], memo) + node_degree(v, nd[2], memo); break;
+  }
+  return memo[i] = d;
+}
+
+void add_query(std::vector<Query>& l, const Query& q) {
+  if (std::find(l.begin(), l.end(), q) == l.end()) l.push_back(q);
+}
+
+void collect(const CircuitView& v, int i, ProvingKey& pk) {  // keygen.rs:217-249, lhs before rhs
+  const int32_t* nd = v.node(i);
+  switch (nd[0]) {
+    case OP_CONST: return;
+    case OP_QUERY: {
+      const Query q{nd[1], nd[2], nd[3]};
+      add_query(nd[1] == COL_ADVICE ? pk.adv_q : (nd[1] == COL_FIXED ? pk.fix_q : pk.ins_q), q);
+      return;
+    }
+    case OP_NEG: collect(v, nd[1], pk); return;
+    default:
+      collect(v, nd[1], pk);
+      collect(v, nd[2], pk);
+      return;
+  }
+}
+
+// Gate expressions -> straight-line program over LDS value slots (tree code
+// generation, larger subtree first to bound live slots; a - b fused as SUB).
+struct GateCompiler {
+  const CircuitView& v;
+  std::vector<int4> prog;
+  std::vector<Query> loads;
+  std::vector<int> free_slots;
+  int n_slots = 0;
+  std::vector<int> need;
+  explicit GateCompiler(const CircuitView& cv) : v(cv), need(cv.c->num_nodes, -1) {}
+  int alloc() {
+    if (!free_slots.empty()) {
+      const int s = free_slots.back();
+      free_slots.pop_back();
+      return s;
+    }
+    return n_slots++;
+  }
+  void release(int s) { free_slots.push_back(s); }
+  int regs(int i) {  // Sethi-Ullman register need
+    if (need[i] >= 0) return need[i];
+    const int32_t* nd = v.node(i);
+    int r = 1;
+    if (nd[0] == OP_NEG) r = regs(nd[1]);
+    else if (nd[0] == OP_SUM || nd[0] == OP_PROD) {
+      const int a = regs(nd[1]), b = regs(nd[2]);
+      r = a == b ? a + 1 : std::max(a, b);
+    }
+    return need[i] = r;
+  }
+  int load_index(const Query& q) {
+    for (size_t i = 0; i < loads.size(); i++)
+      if (loads[i] == q) return (int)i;
+    loads.push_back(q);
+    return (int)loads.size() - 1;
+  }
+  int gen(int i) {
+    const int32_t* nd = v.node(i);
+    switch (nd[0]) {
+      case OP_CONST: {
+        const int s = alloc();
+        prog.push_back(make_int4(G_CONST, s, nd[1], 0));
+        return s;
+      }
+      case OP_QUERY: {
+        const int s = alloc();
+        prog.push_back(make_int4(G_LOAD, s, load_index(Query{nd[1], nd[2], nd[3]}), 0));
+        return s;
+      }
+      case OP_NEG: {
+        const int a = gen(nd[1]);
+        release(a);
+        const int s = alloc();
+        prog.push_back(make_int4(G_NEG, s, a, 0));
+        return s;
+      }
+      default: {
+        int lhs = nd[1], rhs = nd[2];
+        int op = nd[0] == OP_SUM ? G_ADD : G_MUL;
+        if (nd[0] == OP_SUM && v.node(rhs)[0] == OP_NEG) {  // a + (-b) -> a - b
+          op = G_SUB;
+          rhs = v.node(rhs)[1];
+        }
+        int a, b;
+        if (regs(rhs) > regs(lhs)) {
+          b = gen(rhs);
+          a = gen(lhs);
+        } else {
+          a = gen(lhs);
+          b = gen(rhs);
+        }
+        release(a);
+        release(b);
+        const int s = alloc();
+        prog.push_back(make_int4(op, s, a, b));
+        return s;
+      }
+    }
+  }
+};
+
+bool check_nodes(const h2g_circuit* c, std::string* why) {
+  const int64_t n = 1ll << c->k;
+  for (uint32_t i = 0; i < c->num_nodes; i++) {
+    const int32_t* nd = c->nodes + 4 * i;
+    switch (nd[0]) {
+      case OP_CONST:
+        if (nd[1] < 0 || (uint32_t)nd[1] >= c->num_constants) return *why = "constant index", false;
+        break;
+      case OP_QUERY: {
+        const uint32_t lim = nd[1] == COL_ADVICE ? c->num_advice : nd[1] == COL_FIXED ? c->num_fixed
+                                                                   : nd[1] == COL_INSTANCE ? c->num_instance : 0;
+        if (nd[2] < 0 || (uint32_t)nd[2] >= lim) return *why = "query column", false;
+        if (nd[3] <= -n || nd[3] >= n) return *why = "rotation", false;
+        break;
+      }
+      case OP_NEG:
+        if (nd[1] < 0 || (uint32_t)nd[1] >= i) return *why = "node child must precede its parent", false;
+        break;
+      case OP_SUM:
+      case OP_PROD:
+        if (nd[1] < 0 || nd[2] < 0 || (uint32_t)nd[1] >= i || (uint32_t)nd[2] >= i)
+          return *why = "node child must precede its parent", false;
+        break;
+      default: return *why = "node op", false;
+    }
+  }
+  for (uint32_t g = 0; g < c->num_gates; g++)
+    if (c->gate_roots[g] < 0 || (uint32_t)c->gate_roots[g] >= c->num_nodes) return *why = "gate root", false;
+  return true;
+}
+
+// ------------------------------------------------------------------ keygen
+int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk) {
+  hipStream_t st = d->stream;
+  std::string why;
+  if (c->k != prm.k) return fail(H2G_ERR_ARG, "keygen: circuit k != params k");
+  if (c->num_gates && (!c->gate_roots || !c->nodes)) return fail(H2G_ERR_ARG, "keygen: null gates");
+  if (!check_nodes(c, &why)) return fail(H2G_ERR_ARG, "keygen: bad expression graph: " + why);
+  if (c->num_fixed && !c->fixed_values) return fail(H2G_ERR_ARG, "keygen: null fixed values");
+  if (!c->transcript_repr) return fail(H2G_ERR_ARG, "keygen: null transcript_repr");
+  const CircuitView cv{c};
+  pk.device = d->id;
+  pk.k = c->k;
+  pk.n = (size_t)1 << c->k;
+  pk.A = (int)c->num_advice;
+  pk.F = (int)c->num_fixed;
+  pk.I = (int)c->num_instance;
+  pk.P = (int)c->num_perm_columns;
+  pk.transcript_repr = fr_from_limbs(c->transcript_repr);
+  pk.unblinded.assign(pk.A, 0);
+  if (c->unblinded)
+    for (int i = 0; i < pk.A; i++) pk.unblinded[i] = c->unblinded[i];
+  for (int i = 0; i < pk.P; i++) {
+    const int t = c->perm_columns[2 * i], ix = c->perm_columns[2 * i + 1];
+    const int lim = t == COL_ADVICE ? pk.A : t == COL_FIXED ? pk.F : t == COL_INSTANCE ? pk.I : 0;
+    if (ix < 0 || ix >= lim) return fail(H2G_ERR_ARG, "keygen: permutation column out of range");
+    pk.perm_cols.emplace_back(t, ix);
+  }
+  // degree, queries, blinding factors (circuit.rs:143-170,292-320; keygen.rs:191-260)
+  std::vector<int> memo(c->num_nodes, -1);
+  pk.degree = 3;
+  for (uint32_t g = 0; g < c->num_gates; g++) pk.degree = std::max(pk.degree, node_degree(cv, c->gate_roots[g], memo));
+  for (uint32_t g = 0; g < c->num_gates; g++) collect(cv, c->gate_roots[g], pk);
+  for (auto& pc : pk.perm_cols)
+    add_query(pc.first == COL_ADVICE ? pk.adv_q : (pc.first == COL_FIXED ? pk.fix_q : pk.ins_q),
+              Query{pc.first, pc.second, 0});
+  int maxq = 1;
+  if (pk.A) {
+    std::vector<int> cnt(pk.A, 0);
+    for (auto& q : pk.adv_q) cnt[q.index]++;
+    maxq = *std::max_element(cnt.begin(), cnt.end());
+  }
+  pk.bf = std::max(3, maxq) + 2;
+  if ((int64_t)pk.n < pk.bf + 3) return fail(H2G_ERR_ARG, "keygen: not enough rows available");
+  pk.chunk_len = pk.degree - 2;
+  pk.nsets = (pk.P + pk.chunk_len - 1) / pk.chunk_len;
+  RCCHK(domain_init(&pk.dom, (uint32_t)pk.degree, pk.k));
+  pk.ext = (size_t)1 << pk.dom.ek;
+  pk.rot_scale = 1ull << (pk.dom.ek - pk.k);
+  const size_t n = pk.n, ext = pk.ext;
+  Pool& pool = pk.pool;
+  RCCHK(build_pow_table(pool, pk.dom.omega, (int)pk.k, &pk.om, st));
+  RCCHK(build_pow_table(pool, pk.dom.ext_omega, (int)pk.dom.ek, &pk.eo, st));
+
+  // workspace first (keygen uses some of it as scratch)
+  auto falloc = [&](Fr** p, size_t cnt) { return pool.get((void**)p, cnt * sizeof(Fr)); };
+  pk.scr_len = std::max(n + 64, kate_scratch_len(n) + poly_prefix_scratch_len(n) + 64);
+  HIPCHK(falloc(&pk.mod, n));
+  HIPCHK(falloc(&pk.pre, n));
+  HIPCHK(falloc(&pk.scr, pk.scr_len));
+  HIPCHK(falloc(&pk.random_poly, n));
+  HIPCHK(falloc(&pk.h_ext, ext));
+  HIPCHK(falloc(&pk.h_coeff, ext));
+  HIPCHK(falloc(&pk.h_poly, n));
+  HIPCHK(falloc(&pk.nx, n));
+  HIPCHK(falloc(&pk.q1, n));
+  HIPCHK(falloc(&pk.q2, n));
+  HIPCHK(falloc(&pk.hx, n));
+  HIPCHK(falloc(&pk.lx, n));
+  HIPCHK(falloc(&pk.small, 4096));
+  HIPCHK(falloc(&pk.last_z, 1));
+  auto vec_alloc = [&](std::vector<Fr*>& v, int cnt, size_t len) -> hipError_t {
+    v.assign(cnt, nullptr);
+    for (int i = 0; i < cnt; i++) {
+      hipError_t e = falloc(&v[i], len);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  };
+  HIPCHK(vec_alloc(pk.adv, pk.A, n));
+  HIPCHK(vec_alloc(pk.adv_coset, pk.A, ext));
+  HIPCHK(vec_alloc(pk.inst_val, pk.I, n));
+  HIPCHK(vec_alloc(pk.inst_poly, pk.I, n));
+  HIPCHK(vec_alloc(pk.inst_coset, pk.I, ext));
+  HIPCHK(vec_alloc(pk.z, pk.nsets, n));
+  HIPCHK(vec_alloc(pk.z_coset, pk.nsets, ext));
+
+  // fixed columns
+  HIPCHK(vec_alloc(pk.fixed_lag, pk.F, n));
+  HIPCHK(vec_alloc(pk.fixed_poly, pk.F, n));
+  HIPCHK(vec_alloc(pk.fixed_coset, pk.F, ext));
+  for (int i = 0; i < pk.F; i++) {
+    HIPCHK(hipMemcpyAsync(pk.fixed_lag[i], c->fixed_values + 4 * n * i, n * sizeof(Fr), hipMemcpyHostToDevice, st));
+    RCCHK(lagrange_to_coeff(d, pk.dom, pk.fixed_lag[i], pk.fixed_poly[i], st));
+    RCCHK(coeff_to_extended(d, pk.dom, pk.fixed_poly[i], pk.fixed_coset[i], st));
+  }
+  // l_0, l_last, l_active (keygen.rs:147-175)
+  HIPCHK(falloc(&pk.l0, ext));
+  HIPCHK(falloc(&pk.l_last, ext));
+  HIPCHK(falloc(&pk.l_active, ext));
+  {
+    const Fr one = Fr::one();
+    std::vector<Fr> ones(pk.bf, one);
+    auto lagrange_unit = [&](size_t row0, int count, Fr* out) -> int {
+      HIPCHK(hipMemsetAsync(pk.pre, 0, n * sizeof(Fr), st));
+      HIPCHK(hipMemcpyAsync(pk.pre + row0, ones.data(), count * sizeof(Fr), hipMemcpyHostToDevice, st));
+      RCCHK(lagrange_to_coeff(d, pk.dom, pk.pre, pk.mod, st));
+      RCCHK(coeff_to_extended(d, pk.dom, pk.mod, out, st));
+      HIPCHK(hipStreamSynchronize(st));
+      return H2G_OK;
+    };
+    RCCHK(lagrange_unit(0, 1, pk.l0));
+    RCCHK(lagrange_unit(n - pk.bf, pk.bf, pk.h_ext));  // l_blind
+    RCCHK(lagrange_unit(n - pk.bf - 1, 1, pk.l_last));
+    HIPCHK(poly_binop(POLY_ADD, pk.l_last, pk.h_ext, one, pk.l_active, ext, st));
+    HIPCHK(poly_binop(POLY_SUB_CONST, pk.l_active, nullptr, one, pk.l_active, ext, st));
+    HIPCHK(poly_binop(POLY_SCALE, pk.l_active, nullptr, fr_neg_one(), pk.l_active, ext, st));
+  }
+  // permutation: Assembly on the host, sigma polynomials on the device
+  HIPCHK(vec_alloc(pk.sigma_lag, pk.P, n));
+  HIPCHK(vec_alloc(pk.sigma_poly, pk.P, n));
+  HIPCHK(vec_alloc(pk.sigma_coset, pk.P, ext));
+  if (pk.P) {
+    const size_t cells = (size_t)pk.P * n;
+    std::vector<uint32_t> mcol(cells), mrow(cells), acol(cells), arow(cells);
+    std::vector<uint64_t> sizes(cells, 1);
+    for (int cI = 0; cI < pk.P; cI++)
+      for (size_t r = 0; r < n; r++) {
+        mcol[cI * n + r] = acol[cI * n + r] = (uint32_t)cI;
+        mrow[cI * n + r] = arow[cI * n + r] = (uint32_t)r;
+      }
+    auto pos = [&](int t, int ix) -> int {
+      for (int i = 0; i < pk.P; i++)
+        if (pk.perm_cols[i].first == t && pk.perm_cols[i].second == ix) return i;
+      return -1;
+    };
+    for (uint32_t ci = 0; ci < c->num_copies; ci++) {  // Assembly::copy (permutation/keygen.rs:59-97)
+      const int32_t* cp = c->copies + 6 * ci;
+      const int lc = pos(cp[0], cp[1]), rc = pos(cp[3], cp[4]);
+      if (lc < 0 || rc < 0) return fail(H2G_ERR_ARG, "keygen: copy on a column not in the permutation");
+      if (cp[2] < 0 || cp[5] < 0 || (size_t)cp[2] >= n || (size_t)cp[5] >= n)
+        return fail(H2G_ERR_ARG, "keygen: copy row out of bounds");
+      const size_t li = lc * n + cp[2], ri = rc * n + cp[5];
+      size_t lcyc = acol[li] * n + arow[li], rcyc = acol[ri] * n + arow[ri];
+      if (lcyc == rcyc) continue;
+      if (sizes[lcyc] < sizes[rcyc]) std::swap(lcyc, rcyc);
+      sizes[lcyc] += sizes[rcyc];
+      size_t i = rcyc;
+      for (;;) {
+        acol[i] = (uint32_t)(lcyc / n);
+        arow[i] = (uint32_t)(lcyc % n);
+        i = (size_t)mcol[i] * n + mrow[i];
+        if (i == rcyc) break;
+      }
+      std::swap(mcol[li], mcol[ri]);
+      std::swap(mrow[li], mrow[ri]);
+    }
+    std::vector<Fr> dpow(pk.P + 1);
+    dpow[0] = Fr::one();
+    for (int i = 1; i <= pk.P; i++) dpow[i] = dpow[i - 1] * fr_delta();
+    uint32_t *dmc, *dmr;
+    Fr* ddp;
+    HIPCHK(hipMalloc(&dmc, cells * 4));
+    HIPCHK(hipMalloc(&dmr, cells * 4));
+    HIPCHK(hipMalloc(&ddp, dpow.size() * sizeof(Fr)));
+    HIPCHK(hipMemcpyAsync(dmc, mcol.data(), cells * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dmr, mrow.data(), cells * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(ddp, dpow.data(), dpow.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
+    for (int i = 0; i < pk.P; i++) {
+      HIPCHK(sigma_from_mapping(pk.sigma_lag[i], dmc + i * n, dmr + i * n, n, ddp, pk.om, st));
+      RCCHK(lagrange_to_coeff(d, pk.dom, pk.sigma_lag[i], pk.sigma_poly[i], st));
+      RCCHK(coeff_to_extended(d, pk.dom, pk.sigma_poly[i], pk.sigma_coset[i], st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    (void)hipFree(dmc);
+    (void)hipFree(dmr);
+    (void)hipFree(ddp);
+  }
+  // gate program
+  {
+    GateCompiler gc(cv);
+    for (uint32_t g = 0; g < c->num_gates; g++) {
+      const int s = gc.gen(c->gate_roots[g]);
+      gc.prog.push_back(make_int4(G_HORNER, 0, s, 0));
+      gc.release(s);
+    }
+    if (gc.n_slots > evaluate_h_max_slots())
+      return fail(H2G_ERR_ARG, "keygen: gate expressions need more than " + std::to_string(evaluate_h_max_slots()) +
+                                   " live values");
+    pk.prog_len = (int)gc.prog.size();
+    pk.n_slots = gc.n_slots;
+    PALLOC(pool, pk.prog, gc.prog.size() + 1);
+    HIPCHK(hipMemcpyAsync(pk.prog, gc.prog.data(), gc.prog.size() * sizeof(int4), hipMemcpyHostToDevice, st));
+    PALLOC(pool, pk.consts, c->num_constants + 1);
+    if (c->num_constants)
+      HIPCHK(hipMemcpyAsync(pk.consts, c->constants, c->num_constants * sizeof(Fr), hipMemcpyHostToDevice, st));
+    pk.n_loads = (int)gc.loads.size();
+    std::vector<const Fr*> lc(pk.n_loads + 1, nullptr);
+    std::vector<int> lr(pk.n_loads + 1, 0);
+    for (int i = 0; i < pk.n_loads; i++) {
+      const Query& q = gc.loads[i];
+      lc[i] = q.type == COL_ADVICE ? pk.adv_coset[q.index]
+                                   : (q.type == COL_FIXED ? pk.fixed_coset[q.index] : pk.inst_coset[q.index]);
+      lr[i] = q.rot;
+    }
+    PALLOC(pool, pk.d_load_col, lc.size());
+    PALLOC(pool, pk.d_load_rot, lr.size());
+    HIPCHK(hipMemcpyAsync(pk.d_load_col, lc.data(), lc.size() * sizeof(Fr*), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(pk.d_load_rot, lr.data(), lr.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    std::vector<const Fr*> zt(pk.nsets + 1), pv(pk.P + 1), sg(pk.P + 1);
+    for (int s = 0; s < pk.nsets; s++) zt[s] = pk.z_coset[s];
+    for (int i = 0; i < pk.P; i++) {
+      const auto& pc = pk.perm_cols[i];
+      pv[i] = pc.first == COL_ADVICE ? pk.adv_coset[pc.second]
+                                     : (pc.first == COL_FIXED ? pk.fixed_coset[pc.second] : pk.inst_coset[pc.second]);
+      sg[i] = pk.sigma_coset[i];
+    }
+    PALLOC(pool, pk.d_z, zt.size());
+    PALLOC(pool, pk.d_perm_v, pv.size());
+    PALLOC(pool, pk.d_sigma, sg.size());
+    HIPCHK(hipMemcpyAsync(pk.d_z, zt.data(), zt.size() * sizeof(Fr*), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(pk.d_perm_v, pv.data(), pv.size() * sizeof(Fr*), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(pk.d_sigma, sg.data(), sg.size() * sizeof(Fr*), hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  return H2G_OK;
+}
+
+// ------------------------------------------------------------------ create_proof
+struct StageClock {
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  hipStream_t st;
+  bool sync_each;
+  explicit StageClock(hipStream_t s, bool sync) : st(s), sync_each(sync) { g_stages.clear(); }
+  void mark(const char* name) {
+    if (sync_each) (void)hipStreamSynchronize(st);
+    const auto t = std::chrono::steady_clock::now();
+    g_stages.emplace_back(name, std::chrono::duration<double, std::milli>(t - t0).count());
+    t0 = t;
+  }
+};
+
+struct PolyRef {  // a committed polynomial in coefficient form (SHPLONK's "commitment identity")
+  const Fr* p;
+  uint64_t len;
+};
+
+int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, bool adv_dev,
+               const uint64_t* instance, const uint32_t* inst_lens, const uint8_t seed[32], uint32_t vthreads,
+               std::vector<uint8_t>* proof) {
+  hipStream_t st = d->stream;
+  const size_t n = pk.n, ext = pk.ext;
+  const int bf = pk.bf;
+  const Domain& D = pk.dom;
+  StageClock clk(st, false);
+  ChaChaRng rng(seed);
+  Transcript tr(proof);
+  auto write_point = [&](const G1Affine& p) -> int {
+    if (!tr.write_point(p)) return fail(H2G_ERR_ARG, "cannot write points at infinity to the transcript");
+    return H2G_OK;
+  };
+
+  // ---- vk.hash_into + instances (prover.rs:196-271; KZG: QUERY_INSTANCE = false)
+  tr.common_scalar(pk.transcript_repr);
+  for (int i = 0; i < pk.I; i++) {
+    const uint32_t len = inst_lens ? inst_lens[i] : 0;
+    if ((size_t)len > n - (size_t)(bf + 1)) return fail(H2G_ERR_ARG, "create_proof: InstanceTooLarge");
+    const uint64_t* col = instance + 4 * n * i;
+    for (uint32_t r = 0; r < len; r++) tr.common_scalar(fr_from_limbs(col + 4 * r));
+    HIPCHK(hipMemcpyAsync(pk.inst_val[i], col, n * sizeof(Fr), hipMemcpyHostToDevice, st));
+    RCCHK(lagrange_to_coeff(d, D, pk.inst_val[i], pk.inst_poly[i], st));
+  }
+  // ---- advice: blinding rows, commitments (prover.rs:405-455)
+  const size_t unusable = n - (size_t)(bf + 1);
+  for (int c = 0; c < pk.A; c++)
+    HIPCHK(hipMemcpyAsync(pk.adv[c], advice + 4 * n * c, n * sizeof(Fr),
+                          adv_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+  {
+    std::vector<Fr> rows((size_t)(bf + 1));
+    for (int c = 0; c < pk.A; c++) {
+      if (pk.unblinded[c]) continue;
+      for (auto& v : rows) v = rng.random_fr();
+      HIPCHK(hipMemcpyAsync(pk.adv[c] + unusable, rows.data(), rows.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));  // rows is reused
+    }
+    for (int c = 0; c < pk.A; c++)
+      if (!pk.unblinded[c]) (void)rng.random_fr();  // commitment blinds (unused by KZG)
+  }
+  clk.mark("upload+instances");
+  for (int c = 0; c < pk.A; c++) {
+    G1Affine cm;
+    RCCHK(commit(d, pk.adv[c], n, prm.gl, &cm, st));
+    RCCHK(write_point(cm));
+  }
+  clk.mark("advice commit");
+  (void)tr.squeeze();  // theta
+  const Fr beta = tr.squeeze(), gamma = tr.squeeze();
+  dump("beta", &beta, 1, st, true);
+  dump("gamma", &gamma, 1, st, true);
+
+  // ---- permutation_commit (permutation/prover.rs:50-197)
+  {
+    const Fr one = Fr::one();
+    HIPCHK(hipMemcpyAsync(pk.last_z, &one, sizeof(Fr), hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    Fr deltaomega = Fr::one();
+    std::vector<Fr> blind_rows(bf);
+    for (int s = 0; s < pk.nsets; s++) {
+      const int c0 = s * pk.chunk_len, c1 = std::min(c0 + pk.chunk_len, pk.P);
+      auto col_vals = [&](int c) -> const Fr* {
+        const auto& pc = pk.perm_cols[c];
+        return pc.first == COL_ADVICE ? pk.adv[pc.second]
+                                      : (pc.first == COL_FIXED ? pk.fixed_lag[pc.second] : pk.inst_val[pc.second]);
+      };
+      // denominators, batch inversion, numerators
+      for (int c = c0; c < c1; c += PERM_MAXC) {
+        PermCols pc;
+        pc.m = std::min(PERM_MAXC, c1 - c);
+        for (int j = 0; j < pc.m; j++) {
+          pc.v[j] = col_vals(c + j);
+          pc.sigma[j] = pk.sigma_lag[c + j];
+        }
+        HIPCHK(perm_denominators(pk.mod, n, pc, beta, gamma, c == c0, st));
+      }
+      if (s == 0) dump("den0", pk.mod, n, st);
+      HIPCHK(poly_batch_invert(pk.mod, n, pk.scr, st));
+      if (s == 0) dump("inv0", pk.mod, n, st);
+      for (int c = c0; c < c1; c += PERM_MAXC) {
+        PermCols pc;
+        pc.m = std::min(PERM_MAXC, c1 - c);
+        for (int j = 0; j < pc.m; j++) {
+          pc.v[j] = col_vals(c + j);
+          pc.beta_delta[j] = deltaomega * beta;
+          deltaomega = deltaomega * fr_delta();
+        }
+        HIPCHK(perm_numerators(pk.mod, n, pc, gamma, pk.om, st));
+      }
+      // z = last_z * running product, blinding rows from the rng
+      if (s == 0) dump("mod0", pk.mod, n, st);
+      HIPCHK(poly_prefix_product(pk.mod, pk.pre, n, pk.scr, pk.scr_len, st));
+      if (s == 0) dump("pre0", pk.pre, n, st);
+      for (auto& v : blind_rows) v = rng.random_fr();
+      (void)rng.random_fr();  // blind
+      HIPCHK(hipMemcpyAsync(pk.small, blind_rows.data(), bf * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(perm_z_assemble(pk.z[s], n, bf, pk.pre, pk.last_z, pk.small, st));
+      HIPCHK(hipMemcpyAsync(pk.last_z, pk.z[s] + (n - (size_t)(bf + 1)), sizeof(Fr), hipMemcpyDeviceToDevice, st));
+      if (s == 0) dump("z0", pk.z[s], n, st);
+      if (s == 0) dump("sigma0", pk.sigma_lag[0], n, st);
+      if (s == 0) dump("v0", col_vals(0), n, st);
+      G1Affine cm;
+      RCCHK(commit(d, pk.z[s], n, prm.gl, &cm, st));
+      RCCHK(lagrange_to_coeff(d, D, pk.z[s], pk.z[s], st));
+      RCCHK(coeff_to_extended(d, D, pk.z[s], pk.z_coset[s], st));
+      RCCHK(write_point(cm));
+    }
+  }
+  clk.mark("permutation commit");
+  // ---- vanishing commit (vanishing/prover.rs:40-98)
+  {
+    const uint64_t T = vthreads ? vthreads : 1;
+    const uint64_t chunk = n / T, rem = n % T;
+    std::vector<uint64_t> off;
+    for (uint64_t i = 0; i < rem && off.size() < T; i++) off.push_back(i * (chunk + 1));
+    if (chunk)
+      for (uint64_t o = rem * (chunk + 1); off.size() < T; o += chunk) off.push_back(o);
+    std::vector<uint32_t> seeds(off.size() * 8);
+    for (size_t i = 0; i < off.size(); i++) rng.fill(reinterpret_cast<uint8_t*>(&seeds[8 * i]), 32);
+    if ((int)off.size() > pk.max_chunks) {
+      PALLOC(pk.pool, pk.d_seeds, seeds.size());
+      PALLOC(pk.pool, pk.d_offsets, off.size());
+      pk.max_chunks = (int)off.size();
+    }
+    HIPCHK(hipMemcpyAsync(pk.d_seeds, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(pk.d_offsets, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)off.size(), st));
+    HIPCHK(hipStreamSynchronize(st));  // seeds/off are host temporaries
+    (void)rng.random_fr();             // random_blind
+    G1Affine cm;
+    RCCHK(commit(d, pk.random_poly, n, prm.g, &cm, st));
+    RCCHK(write_point(cm));
+  }
+  clk.mark("vanishing commit");
+  // ---- advice to coefficient form, y, evaluate_h
+  for (int c = 0; c < pk.A; c++) RCCHK(lagrange_to_coeff(d, D, pk.adv[c], pk.adv[c], st));
+  const Fr y = tr.squeeze();
+  for (int c = 0; c < pk.A; c++) RCCHK(coeff_to_extended(d, D, pk.adv[c], pk.adv_coset[c], st));
+  for (int c = 0; c < pk.I; c++) RCCHK(coeff_to_extended(d, D, pk.inst_poly[c], pk.inst_coset[c], st));
+  clk.mark("advice/instance cosets");
+  {
+    EvalHArgs a;
+    a.prog = pk.prog;
+    a.prog_len = pk.prog_len;
+    a.n_slots = pk.n_slots;
+    a.consts = pk.consts;
+    a.query_col = pk.d_load_col;
+    a.query_rot = pk.d_load_rot;
+    a.nsets = pk.nsets;
+    a.chunk_len = pk.chunk_len;
+    a.P = pk.P;
+    a.z = pk.d_z;
+    a.perm_v = pk.d_perm_v;
+    a.sigma = pk.d_sigma;
+    a.l0 = pk.l0;
+    a.l_last = pk.l_last;
+    a.l_active = pk.l_active;
+    a.beta = beta;
+    a.gamma = gamma;
+    a.y = y;
+    a.delta_start = beta * zeta();
+    a.delta = fr_delta();
+    a.ext_omega = pk.eo;
+    a.ext = ext;
+    a.rot_scale = pk.rot_scale;
+    a.last_rot = -(bf + 1);
+    a.t_evals = D.d_t;
+    a.t_mask = D.t_evals.size() - 1;
+    a.out = pk.h_ext;
+    HIPCHK(evaluate_h(a, st));
+  }
+  clk.mark("evaluate_h");
+  // ---- vanishing construct (vanishing/prover.rs:102-155): h(X) pieces of size n
+  RCCHK(extended_to_coeff(d, D, pk.h_ext, pk.h_coeff, st));
+  const int npieces = pk.degree - 1;
+  for (int p = 0; p < npieces; p++) (void)rng.random_fr();  // h blinds
+  for (int p = 0; p < npieces; p++) {
+    G1Affine cm;
+    RCCHK(commit(d, pk.h_coeff + (size_t)p * n, n, prm.g, &cm, st));
+    RCCHK(write_point(cm));
+  }
+  clk.mark("h commit");
+  const Fr x = tr.squeeze();
+  const Fr xn = pow_u64(x, n);
+  // h(X) = sum_p X^(n p) h_p(X)  (vanishing/prover.rs:166-170)
+  {
+    LinTerms t;
+    Fr c = Fr::one();
+    bool first = true;
+    for (int p = 0; p < npieces; p++) {
+      if (t.k == LIN_MAXT) {
+        HIPCHK(lincomb(pk.h_poly, n, t, !first, st));
+        first = false;
+        t.k = 0;
+      }
+      t.p[t.k] = pk.h_coeff + (size_t)p * n;
+      t.len[t.k] = n;
+      t.coef[t.k] = c;
+      t.k++;
+      c = c * xn;
+    }
+    HIPCHK(lincomb(pk.h_poly, n, t, !first, st));
+  }
+
+  // ---- the polynomial openings (prover.rs:840-889) and their evaluations
+  // poly ids: advice c, fixed A+c, sigma A+F+c, z A+F+P+s, h, random
+  std::vector<PolyRef> polys;
+  for (int c = 0; c < pk.A; c++) polys.push_back({pk.adv[c], n});
+  for (int c = 0; c < pk.F; c++) polys.push_back({pk.fixed_poly[c], n});
+  for (int c = 0; c < pk.P; c++) polys.push_back({pk.sigma_poly[c], n});
+  for (int s = 0; s < pk.nsets; s++) polys.push_back({pk.z[s], n});
+  const int id_h = (int)polys.size();
+  polys.push_back({pk.h_poly, n});
+  const int id_r = (int)polys.size();
+  polys.push_back({pk.random_poly, n});
+  const int id_adv = 0, id_fix = pk.A, id_sig = pk.A + pk.F, id_z = pk.A + pk.F + pk.P;
+  const Fr x_next = rotate_omega(D, x, 1), x_last = rotate_omega(D, x, -(bf + 1));
+  struct Q2 {
+    int poly;
+    Fr pt;
+  };
+  std::vector<Q2> queries;
+  for (auto& q : pk.adv_q) queries.push_back({id_adv + q.index, rotate_omega(D, x, q.rot)});
+  for (int s = 0; s < pk.nsets; s++) {
+    queries.push_back({id_z + s, x});
+    queries.push_back({id_z + s, x_next});
+  }
+  for (int s = pk.nsets - 2; s >= 0; s--) queries.push_back({id_z + s, x_last});
+  for (auto& q : pk.fix_q) queries.push_back({id_fix + q.index, rotate_omega(D, x, q.rot)});
+  for (int c = 0; c < pk.P; c++) queries.push_back({id_sig + c, x});
+  queries.push_back({id_h, x});
+  queries.push_back({id_r, x});
+  // unique (poly, point) evaluations, one batched launch
+  std::vector<Q2> ev_keys;
+  auto ev_index = [&](int poly, const Fr& pt) -> int {
+    for (size_t i = 0; i < ev_keys.size(); i++)
+      if (ev_keys[i].poly == poly && ev_keys[i].pt == pt) return (int)i;
+    ev_keys.push_back({poly, pt});
+    return (int)ev_keys.size() - 1;
+  };
+  for (auto& q : queries) ev_index(q.poly, q.pt);
+  std::vector<Fr> evals(ev_keys.size());
+  {
+    const int nreq = (int)ev_keys.size();
+    if (nreq > pk.max_reqs) {
+      PALLOC(pk.pool, pk.d_reqs, nreq);
+      PALLOC(pk.pool, pk.evals, nreq);
+      pk.max_reqs = nreq;
+    }
+    const size_t need = poly_eval_scratch_len(nreq, n);
+    if (need > pk.eval_scr_len) {
+      PALLOC(pk.pool, pk.eval_scr, need);
+      pk.eval_scr_len = need;
+    }
+    std::vector<EvalReq> reqs(nreq);
+    for (int i = 0; i < nreq; i++) reqs[i] = EvalReq{polys[ev_keys[i].poly].p, polys[ev_keys[i].poly].len, ev_keys[i].pt};
+    HIPCHK(hipMemcpyAsync(pk.d_reqs, reqs.data(), nreq * sizeof(EvalReq), hipMemcpyHostToDevice, st));
+    HIPCHK(poly_eval_batch(pk.d_reqs, nreq, n, pk.evals, pk.eval_scr, st));
+    HIPCHK(hipMemcpyAsync(evals.data(), pk.evals, nreq * sizeof(Fr), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  auto ev = [&](int poly, const Fr& pt) { return evals[ev_index(poly, pt)]; };
+  for (auto& q : pk.adv_q) tr.write_scalar(ev(id_adv + q.index, rotate_omega(D, x, q.rot)));
+  for (auto& q : pk.fix_q) tr.write_scalar(ev(id_fix + q.index, rotate_omega(D, x, q.rot)));
+  tr.write_scalar(ev(id_r, x));
+  for (int c = 0; c < pk.P; c++) tr.write_scalar(ev(id_sig + c, x));
+  for (int s = 0; s < pk.nsets; s++) {
+    tr.write_scalar(ev(id_z + s, x));
+    tr.write_scalar(ev(id_z + s, x_next));
+    if (s + 1 < pk.nsets) tr.write_scalar(ev(id_z + s, x_last));
+  }
+  clk.mark("evaluations");
+
+  // ---- SHPLONK (shplonk/prover.rs:121-305; construct_intermediate_sets shplonk.rs:48-140)
+  const Fr sy = tr.squeeze();
+  std::vector<Fr> super_pts;
+  for (auto& q : queries) {
+    bool f = false;
+    for (auto& p : super_pts) f = f || p == q.pt;
+    if (!f) super_pts.push_back(q.pt);
+  }
+  std::sort(super_pts.begin(), super_pts.end(), [](const Fr& a, const Fr& b) { return fr_cmp(a, b) < 0; });
+  std::vector<int> cm_ids;
+  std::vector<std::vector<Fr>> cm_pts;
+  for (auto& q : queries) {
+    int f = -1;
+    for (size_t i = 0; i < cm_ids.size(); i++)
+      if (cm_ids[i] == q.poly) f = (int)i;
+    if (f < 0) {
+      f = (int)cm_ids.size();
+      cm_ids.push_back(q.poly);
+      cm_pts.emplace_back();
+    }
+    auto& ps = cm_pts[f];
+    if (std::find(ps.begin(), ps.end(), q.pt) == ps.end()) ps.push_back(q.pt);
+  }
+  for (auto& ps : cm_pts) std::sort(ps.begin(), ps.end(), [](const Fr& a, const Fr& b) { return fr_cmp(a, b) < 0; });
+  std::vector<int> rs_of(cm_ids.size()), rs_rep;
+  for (size_t c = 0; c < cm_ids.size(); c++) {
+    int f = -1;
+    for (size_t r = 0; r < rs_rep.size(); r++)
+      if (cm_pts[rs_rep[r]] == cm_pts[c]) f = (int)r;
+    if (f < 0) {
+      f = (int)rs_rep.size();
+      rs_rep.push_back((int)c);
+    }
+    rs_of[c] = f;
+  }
+  std::vector<std::vector<Fr>> low(cm_ids.size());
+  for (size_t c = 0; c < cm_ids.size(); c++) {
+    std::vector<Fr> e;
+    for (auto& p : cm_pts[c]) e.push_back(ev(cm_ids[c], p));
+    low[c] = lagrange_interpolate(cm_pts[c], e);
+  }
+  const Fr v = tr.squeeze();
+  // h_x = sum_s v^s (sum_i y^i (p_i - r_i)) / Z_s
+  {
+    Fr vpow = Fr::one();
+    for (size_t r = 0; r < rs_rep.size(); r++) {
+      const std::vector<Fr>& pts = cm_pts[rs_rep[r]];
+      std::vector<Fr> corr(pts.size(), Fr::zero());
+      LinTerms t;
+      bool first = true;
+      Fr ypow = Fr::one();
+      for (size_t c = 0; c < cm_ids.size(); c++) {
+        if (rs_of[c] != (int)r) continue;
+        if (t.k == LIN_MAXT - 1) {
+          HIPCHK(lincomb(pk.nx, n, t, !first, st));
+          first = false;
+          t.k = 0;
+        }
+        t.p[t.k] = polys[cm_ids[c]].p;
+        t.len[t.k] = polys[cm_ids[c]].len;
+        t.coef[t.k] = ypow;
+        t.k++;
+        for (size_t j = 0; j < pts.size(); j++) corr[j] = corr[j] + ypow * low[c][j];
+        ypow = ypow * sy;
+      }
+      HIPCHK(hipMemcpyAsync(pk.small, corr.data(), corr.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
+      t.p[t.k] = pk.small;
+      t.len[t.k] = corr.size();
+      t.coef[t.k] = fr_neg_one();
+      t.k++;
+      HIPCHK(lincomb(pk.nx, n, t, !first, st));
+      // successive kate divisions by the set's points
+      const Fr* src = pk.nx;
+      uint64_t len = n;
+      Fr* bufs[2] = {pk.q1, pk.q2};
+      for (size_t j = 0; j < pts.size(); j++) {
+        Fr* dst = bufs[j & 1];
+        HIPCHK(kate_division(src, len, pts[j], dst, pk.scr, st));
+        src = dst;
+        len--;
+      }
+      LinTerms h;
+      h.k = 1;
+      h.p[0] = src;
+      h.len[0] = len;
+      h.coef[0] = vpow;
+      HIPCHK(lincomb(pk.hx, n, h, r > 0, st));
+      HIPCHK(hipStreamSynchronize(st));  // corr is a host temporary
+      vpow = vpow * v;
+    }
+  }
+  {
+    G1Affine cm;
+    RCCHK(commit(d, pk.hx, n, prm.g, &cm, st));
+    RCCHK(write_point(cm));
+  }
+  clk.mark("shplonk h");
+  const Fr u = tr.squeeze();
+  // linearisation: l_x = sum_s v^s Z_{T\S_s}(u) sum_i y^i (p_i - r_i(u)) - Z_T(u) h_x
+  Fr z0 = Fr::one();
+  {
+    Fr vpow = Fr::one(), c0 = Fr::zero();
+    LinTerms t;
+    bool first = true;
+    auto flush = [&]() -> int {
+      HIPCHK(lincomb(pk.lx, n, t, !first, st));
+      first = false;
+      t.k = 0;
+      return H2G_OK;
+    };
+    for (size_t r = 0; r < rs_rep.size(); r++) {
+      const std::vector<Fr>& pts = cm_pts[rs_rep[r]];
+      Fr zi = Fr::one();
+      for (auto& sp : super_pts)
+        if (std::find(pts.begin(), pts.end(), sp) == pts.end()) zi = (u - sp) * zi;
+      if (r == 0) z0 = zi;
+      Fr ypow = Fr::one();
+      for (size_t c = 0; c < cm_ids.size(); c++) {
+        if (rs_of[c] != (int)r) continue;
+        if (t.k == LIN_MAXT - 2) RCCHK(flush());
+        const Fr coef = ypow * zi * vpow;
+        t.p[t.k] = polys[cm_ids[c]].p;
+        t.len[t.k] = polys[cm_ids[c]].len;
+        t.coef[t.k] = coef;
+        t.k++;
+        c0 = c0 - coef * eval_host(low[c], u);
+        ypow = ypow * sy;
+      }
+      vpow = vpow * v;
+    }
+    Fr zt = Fr::one();
+    for (auto& sp : super_pts) zt = (u - sp) * zt;
+    HIPCHK(hipMemcpyAsync(pk.small, &c0, sizeof(Fr), hipMemcpyHostToDevice, st));
+    t.p[t.k] = pk.small;
+    t.len[t.k] = 1;
+    t.coef[t.k] = Fr::one();
+    t.k++;
+    t.p[t.k] = pk.hx;
+    t.len[t.k] = n;
+    t.coef[t.k] = Fr::zero() - zt;
+    t.k++;
+    RCCHK(flush());
+    HIPCHK(hipStreamSynchronize(st));  // c0 is a host temporary
+  }
+  HIPCHK(kate_division(pk.lx, n, u, pk.q1, pk.scr, st));
+  HIPCHK(poly_binop(POLY_SCALE, pk.q1, nullptr, inv(z0), pk.q1, n - 1, st));
+  {
+    G1Affine cm;
+    RCCHK(commit(d, pk.q1, n - 1, prm.g, &cm, st));
+    RCCHK(write_point(cm));
+  }
+  clk.mark("shplonk final");
+  return H2G_OK;
+}
+
+}  // namespace
+
+#define NEED_DEV_P()                                                          \
+  std::lock_guard<std::recursive_mutex> _lk(g_mu);                            \
+  Device* d = cur();                                                          \
+  if (!d) return fail(H2G_ERR_STATE, "h2g_init has not been called");         \
+  HIPCHK(hipSetDevice(d->id));
+
+extern "C" {
+
+int h2g_params_create(uint32_t k, const uint64_t* g, const uint64_t* g_lagrange, uint64_t* handle) {
+  NEED_DEV_P();
+  if (!g || !g_lagrange || !handle || k > 27) return fail(H2G_ERR_ARG, "params_create: bad arguments");
+  auto p = std::make_unique<Params>();
+  p->device = d->id;
+  p->k = k;
+  p->n = (size_t)1 << k;
+  PALLOC(p->pool, p->g, p->n);
+  PALLOC(p->pool, p->gl, p->n);
+  HIPCHK(hipMemcpy(p->g, g, p->n * sizeof(G1Affine), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(p->gl, g_lagrange, p->n * sizeof(G1Affine), hipMemcpyHostToDevice));
+  *handle = g_next_handle++;
+  g_params[*handle] = std::move(p);
+  return H2G_OK;
+}
+
+int h2g_params_setup(uint32_t k, const uint64_t s_limbs[4], uint64_t* handle) {
+  NEED_DEV_P();
+  if (!s_limbs || !handle || k > 27) return fail(H2G_ERR_ARG, "params_setup: bad arguments");
+  hipStream_t st = d->stream;
+  auto p = std::make_unique<Params>();
+  p->device = d->id;
+  p->k = k;
+  p->n = (size_t)1 << k;
+  const size_t n = p->n;
+  PALLOC(p->pool, p->g, n);
+  PALLOC(p->pool, p->gl, n);
+  const Fr s = fr_from_limbs(s_limbs);
+  HIPCHK(srs_setup(s, n, p->g, st));
+  Fr omega = root_of_unity();
+  for (uint32_t i = k; i < FR_S; i++) omega = sqr(omega);
+  Pool tmp;
+  PowTable om;
+  RCCHK(build_pow_table(tmp, omega, (int)k, &om, st));
+  Fr *sc, *scr;
+  HIPCHK(tmp.get((void**)&sc, n * sizeof(Fr)));
+  HIPCHK(tmp.get((void**)&scr, n * sizeof(Fr)));
+  const Fr mult = (pow_u64(s, n) - Fr::one()) * inv(from_u64<FrParams>(n));
+  HIPCHK(srs_lagrange_scalars(sc, n, s, mult, om, scr, st));
+  HIPCHK(g1_generator_mul(sc, n, p->gl, st));
+  HIPCHK(hipStreamSynchronize(st));
+  *handle = g_next_handle++;
+  g_params[*handle] = std::move(p);
+  return H2G_OK;
+}
+
+int h2g_params_export(uint64_t params, uint64_t* g, uint64_t* g_lagrange) {
+  NEED_DEV_P();
+  auto it = g_params.find(params);
+  if (it == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  if (g) HIPCHK(hipMemcpy(g, it->second->g, it->second->n * sizeof(G1Affine), hipMemcpyDeviceToHost));
+  if (g_lagrange) HIPCHK(hipMemcpy(g_lagrange, it->second->gl, it->second->n * sizeof(G1Affine), hipMemcpyDeviceToHost));
+  return H2G_OK;
+}
+
+int h2g_params_free(uint64_t params) {
+  NEED_DEV_P();
+  if (!g_params.erase(params)) return fail(H2G_ERR_HANDLE, "unknown params");
+  return H2G_OK;
+}
+
+int h2g_keygen(uint64_t params, const h2g_circuit* circuit, uint64_t* pk_out) {
+  NEED_DEV_P();
+  auto it = g_params.find(params);
+  if (it == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  if (!circuit || !pk_out) return fail(H2G_ERR_ARG, "keygen: null argument");
+  auto pk = std::make_unique<ProvingKey>();
+  pk->params = params;
+  int rc = keygen_impl(d, *it->second, circuit, *pk);
+  if (rc) {
+    domain_release(&pk->dom);
+    return rc;
+  }
+  *pk_out = g_next_handle++;
+  g_pks[*pk_out] = std::move(pk);
+  return H2G_OK;
+}
+
+int h2g_pk_free(uint64_t pk) {
+  NEED_DEV_P();
+  auto it = g_pks.find(pk);
+  if (it == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
+  (void)hipStreamSynchronize(d->stream);
+  domain_release(&it->second->dom);
+  g_pks.erase(it);
+  return H2G_OK;
+}
+
+int h2g_pk_info(uint64_t pk, int32_t info[8]) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  auto it = g_pks.find(pk);
+  if (it == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
+  const ProvingKey& p = *it->second;
+  const int32_t v[8] = {p.degree, p.bf, (int32_t)p.dom.ek, p.nsets, (int32_t)p.adv_q.size(),
+                        (int32_t)p.fix_q.size(), (int32_t)p.ins_q.size(), p.n_slots};
+  std::memcpy(info, v, sizeof(v));
+  return H2G_OK;
+}
+
+int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int advice_on_device,
+                     const uint64_t* instance, const uint32_t* instance_lens, const uint8_t rng_seed[32],
+                     uint32_t vanishing_threads, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
+  NEED_DEV_P();
+  auto ip = g_params.find(params);
+  if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  auto ik = g_pks.find(pk);
+  if (ik == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
+  ProvingKey& K = *ik->second;
+  if (ik->second->params != params) return fail(H2G_ERR_ARG, "create_proof: pk was generated with other params");
+  if (K.device != d->id) return fail(H2G_ERR_ARG, "create_proof: pk lives on another device");
+  if ((K.A && !advice) || (K.I && (!instance || !instance_lens)) || !rng_seed || !proof_len)
+    return fail(H2G_ERR_ARG, "create_proof: null argument");
+  std::vector<uint8_t> out;
+  out.reserve(32 * 256);
+  int rc = prove_impl(d, *ip->second, K, advice, advice_on_device != 0, instance, instance_lens, rng_seed,
+                      vanishing_threads, &out);
+  if (rc) {
+    (void)hipStreamSynchronize(d->stream);
+    return rc;
+  }
+  *proof_len = out.size();
+  if (out.size() > proof_cap) return fail(H2G_ERR_ARG, "create_proof: proof buffer too small");
+  if (proof) std::memcpy(proof, out.data(), out.size());
+  return H2G_OK;
+}
+
+int h2g_prover_stages(double* ms, int max, int* count) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  const int c = (int)g_stages.size();
+  for (int i = 0; i < c && i < max; i++) ms[i] = g_stages[i].second;
+  if (count) *count = c;
+  return H2G_OK;
+}
+
+const char* h2g_prover_stage_name(int i) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (i < 0 || i >= (int)g_stages.size()) return "";
+  return g_stages[i].first;
+}
+
+}  // extern "C"

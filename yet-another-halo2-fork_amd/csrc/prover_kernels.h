@@ -1,0 +1,104 @@
+// prover_kernels.h -- device kernels of the create_proof pipeline beyond MSM/NTT
+// (see prover_kernels.hip for the reference lines each one restates).
+#pragma once
+#include "bn254.h"
+
+namespace h2g {
+
+// Powers w^i of a fixed root for i < 2^L through two tables: w^i = lo[i & mask] * hi[i >> bits].
+struct PowTable {
+  const Fr* lo = nullptr;
+  const Fr* hi = nullptr;
+  int bits = 0;
+};
+
+// ---- permutation argument (permutation/prover.rs:103-171) ----
+static constexpr int PERM_MAXC = 8;  // columns per kernel launch (sets are split into launches)
+struct PermCols {
+  const Fr* v[PERM_MAXC];      // column values (Lagrange)
+  const Fr* sigma[PERM_MAXC];  // permutation polynomial values (Lagrange)
+  Fr beta_delta[PERM_MAXC];    // beta * delta^(global column index)
+  int m = 0;
+};
+// out[r] = (init ? 1 : out[r]) * prod_j (beta * sigma_j[r] + gamma + v_j[r])
+hipError_t perm_denominators(Fr* out, size_t n, const PermCols& c, const Fr& beta, const Fr& gamma, bool init,
+                             hipStream_t st);
+// mod[r] *= prod_j (beta * delta^j * omega^r + gamma + v_j[r])
+hipError_t perm_numerators(Fr* mod, size_t n, const PermCols& c, const Fr& gamma, const PowTable& omega,
+                           hipStream_t st);
+// z[0] = *last_z, z[i] = *last_z * prefix[i - 1] for 0 < i < n - bf; z[n-bf..n) = blind_rows[0..bf)
+hipError_t perm_z_assemble(Fr* z, size_t n, int bf, const Fr* prefix, const Fr* last_z, const Fr* blind_rows,
+                           hipStream_t st);
+
+// ---- vanishing argument: random polynomial (vanishing/prover.rs:57-81) ----
+// out[i] = Fr::random(ChaCha20Rng(seed_t)) for the i - off[t]'th draw of chunk t
+hipError_t chacha_random_poly(Fr* out, size_t n, const uint32_t* d_seeds, const uint64_t* d_offsets, int chunks,
+                              hipStream_t st);
+
+// ---- evaluate_h (evaluation.rs:317-483): gate program + permutation, fused / t(X) ----
+enum GateOp : int { G_LOAD = 0, G_CONST = 1, G_ADD = 2, G_SUB = 3, G_MUL = 4, G_NEG = 5, G_HORNER = 6 };
+// instruction: {op, dst slot, a, b}; G_LOAD: a = query index; G_CONST: a = constant index;
+// G_HORNER: acc = acc * y + slot[a]
+struct EvalHArgs {
+  const int4* prog = nullptr;
+  int prog_len = 0;
+  int n_slots = 0;
+  const Fr* consts = nullptr;
+  const Fr* const* query_col = nullptr;  // per query: column coset pointer
+  const int* query_rot = nullptr;        // per query: rotation
+  // permutation
+  int nsets = 0, chunk_len = 0, P = 0;
+  const Fr* const* z = nullptr;       // nsets
+  const Fr* const* perm_v = nullptr;  // P column cosets
+  const Fr* const* sigma = nullptr;   // P sigma cosets
+  const Fr* l0 = nullptr;
+  const Fr* l_last = nullptr;
+  const Fr* l_active = nullptr;
+  Fr beta, gamma, y, delta_start, delta;
+  PowTable ext_omega;
+  uint64_t ext = 0, rot_scale = 0;
+  int last_rot = 0;
+  const Fr* t_evals = nullptr;
+  uint64_t t_mask = 0;
+  Fr* out = nullptr;
+};
+hipError_t evaluate_h(const EvalHArgs& a, hipStream_t st);
+int evaluate_h_max_slots();
+
+// ---- polynomial evaluation (arithmetic.rs:57-82), batched ----
+struct EvalReq {
+  const Fr* poly;
+  uint64_t len;
+  Fr x;
+};
+// out[r] = sum_i reqs[r].poly[i] * reqs[r].x^i ; reqs/out in device memory; scratch >= eval_scratch_len
+hipError_t poly_eval_batch(const EvalReq* d_reqs, int nreq, uint64_t max_len, Fr* d_out, Fr* scratch,
+                           hipStream_t st);
+size_t poly_eval_scratch_len(int nreq, uint64_t max_len);
+
+// ---- kate_division (arithmetic.rs:101-120): q = (a - a(b)) / (X - b), len(q) = len(a) - 1 ----
+hipError_t kate_division(const Fr* a, uint64_t len, const Fr& b, Fr* q, Fr* scratch, hipStream_t st);
+size_t kate_scratch_len(uint64_t len);
+
+// ---- linear combinations: out[i] = (acc ? out[i] : 0) + sum_k coef_k * p_k[i] (i < len_k) ----
+static constexpr int LIN_MAXT = 12;
+struct LinTerms {
+  const Fr* p[LIN_MAXT];
+  uint64_t len[LIN_MAXT];
+  Fr coef[LIN_MAXT];
+  int k = 0;
+};
+hipError_t lincomb(Fr* out, uint64_t n, const LinTerms& t, bool accumulate, hipStream_t st);
+// out[i] = a[i] * (*scalar) (device scalar)
+hipError_t scale_by_dev(Fr* out, const Fr* a, uint64_t n, const Fr* scalar, hipStream_t st);
+
+// ---- keygen helpers ----
+// sigma[r] = delta^col[r] * omega^row[r]  (permutation/keygen.rs:139-170)
+hipError_t sigma_from_mapping(Fr* sigma, const uint32_t* map_col, const uint32_t* map_row, size_t n,
+                              const Fr* delta_pow, const PowTable& omega, hipStream_t st);
+// out[i] = [L_i(s)] G for the Lagrange SRS: L_i(s) = mult * w^i / (s - w^i) (kzg/commitment.rs:92-131)
+hipError_t srs_lagrange_scalars(Fr* out, size_t n, const Fr& s, const Fr& mult, const PowTable& omega, Fr* scratch,
+                                hipStream_t st);
+hipError_t g1_generator_mul(const Fr* scalars, size_t n, G1Affine* out, hipStream_t st);
+
+}  // namespace h2g

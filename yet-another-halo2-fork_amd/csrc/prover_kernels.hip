@@ -1,0 +1,465 @@
+// prover_kernels.hip -- the create_proof kernels beyond MSM / NTT, for gfx950.
+//
+//   perm_*               permutation_commit     halo2_backend/src/plonk/permutation/prover.rs:103-171
+//   chacha_random_poly   vanishing commit       halo2_backend/src/plonk/vanishing/prover.rs:57-81
+//   evaluate_h           Evaluator::evaluate_h  halo2_backend/src/plonk/evaluation.rs:317-483
+//                        (+ divide_by_vanishing_poly domain.rs:297-316, fused)
+//   poly_eval_batch      eval_polynomial        halo2_backend/src/arithmetic.rs:57-82
+//   kate_division        kate_division          halo2_backend/src/arithmetic.rs:101-120
+//   lincomb              Polynomial Add/Sub/Mul<F> folds (shplonk/prover.rs:157-276,
+//                        vanishing/prover.rs:166-176)
+//   sigma_from_mapping   permutation build_pk   halo2_backend/src/plonk/permutation/keygen.rs:139-170
+//   srs_lagrange_*       ParamsKZG::setup       halo2_backend/src/poly/kzg/commitment.rs:92-131
+//
+// Everything here is integer modular arithmetic on 32-byte Montgomery elements;
+// elementwise kernels are HBM-streaming grid-stride loops with 16-byte accesses.
+#include "fr_io.h"
+#include "poly.h"
+#include "prover_kernels.h"
+#include "transcript.h"
+
+namespace h2g {
+
+static constexpr int KT = 256;
+
+static unsigned grid_1d(size_t n, int per_block = KT) {
+  size_t g = (n + per_block - 1) / per_block;
+  const size_t cap = 256 * 16;
+  return (unsigned)(g < cap ? (g ? g : 1) : cap);
+}
+
+__device__ __forceinline__ Fr pw(const PowTable& t, uint64_t i) {
+  const uint64_t mask = (1ull << t.bits) - 1;
+  return ldf(t.lo + (i & mask)) * ldf(t.hi + (i >> t.bits));
+}
+
+// ------------------------------------------------------------------ permutation
+__global__ void __launch_bounds__(KT) perm_den_kernel(Fr* __restrict__ out, size_t n, PermCols c, Fr beta, Fr gamma,
+                                                      int init) {
+  for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
+    Fr acc = init ? Fr::one() : ldf(out + r);
+    for (int j = 0; j < c.m; j++) acc = acc * (beta * ldf(c.sigma[j] + r) + gamma + ldf(c.v[j] + r));
+    stf(out + r, acc);
+  }
+}
+
+hipError_t perm_denominators(Fr* out, size_t n, const PermCols& c, const Fr& beta, const Fr& gamma, bool init,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(perm_den_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, out, n, c, beta, gamma, init ? 1 : 0);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(KT) perm_num_kernel(Fr* __restrict__ mod, size_t n, PermCols c, Fr gamma,
+                                                      PowTable om) {
+  for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
+    const Fr w = pw(om, r);
+    Fr acc = ldf(mod + r);
+    for (int j = 0; j < c.m; j++) acc = acc * (c.beta_delta[j] * w + gamma + ldf(c.v[j] + r));
+    stf(mod + r, acc);
+  }
+}
+
+hipError_t perm_numerators(Fr* mod, size_t n, const PermCols& c, const Fr& gamma, const PowTable& omega,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(perm_num_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, mod, n, c, gamma, omega);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(KT) perm_z_kernel(Fr* __restrict__ z, size_t n, int bf, const Fr* __restrict__ pre,
+                                                    const Fr* __restrict__ last_z, const Fr* __restrict__ blind) {
+  const Fr lz = ldf(last_z);
+  const size_t u = n - (size_t)bf;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    Fr v;
+    if (i == 0) v = lz;
+    else if (i < u) v = lz * ldf(pre + i - 1);
+    else v = ldf(blind + (i - u));
+    stf(z + i, v);
+  }
+}
+
+hipError_t perm_z_assemble(Fr* z, size_t n, int bf, const Fr* prefix, const Fr* last_z, const Fr* blind_rows,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(perm_z_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, z, n, bf, prefix, last_z, blind_rows);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ vanishing random poly
+// Chunk t of the polynomial is filled by its own ChaCha20Rng(seed_t); each Fr::random
+// consumes exactly one 64-byte block, so element j of the chunk is block j.
+__global__ void __launch_bounds__(KT) chacha_poly_kernel(Fr* __restrict__ out, size_t n,
+                                                         const uint32_t* __restrict__ seeds,
+                                                         const uint64_t* __restrict__ off, int chunks) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    int lo = 0, hi = chunks - 1;  // last t with off[t] <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (off[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    uint32_t key[8], w[16];
+#pragma unroll
+    for (int k = 0; k < 8; k++) key[k] = seeds[8 * lo + k];
+    chacha20_block(key, (uint64_t)(i - off[lo]), w);
+    stf(out + i, fr_from_u512(w));
+  }
+}
+
+hipError_t chacha_random_poly(Fr* out, size_t n, const uint32_t* d_seeds, const uint64_t* d_offsets, int chunks,
+                              hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(chacha_poly_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, out, n, d_seeds, d_offsets, chunks);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ evaluate_h
+// One wave per block; the gate program's value slots live in LDS as
+// slot-major [slot][lane] 32-byte elements (conflict-free 16-byte accesses).
+static constexpr int EH_T = 64;
+static constexpr int EH_MAX_SLOTS = 24;
+int evaluate_h_max_slots() { return EH_MAX_SLOTS; }
+
+__global__ void __launch_bounds__(EH_T) evaluate_h_kernel(EvalHArgs a) {
+  extern __shared__ uint4 eh_lds[];
+  Fr* sl = reinterpret_cast<Fr*>(eh_lds);
+  const int lane = threadIdx.x;
+  const uint64_t emask = a.ext - 1;
+  for (uint64_t idx = blockIdx.x * (uint64_t)EH_T + lane; idx < a.ext; idx += (uint64_t)gridDim.x * EH_T) {
+    Fr acc = Fr::zero();
+    for (int pc = 0; pc < a.prog_len; pc++) {
+      const int4 in = a.prog[pc];
+      Fr v;
+      switch (in.x) {
+        case G_LOAD: {
+          const uint64_t j = (idx + (uint64_t)((int64_t)a.query_rot[in.z] * (int64_t)a.rot_scale)) & emask;
+          v = ldf(a.query_col[in.z] + j);
+          break;
+        }
+        case G_CONST: v = ldf(a.consts + in.z); break;
+        case G_ADD: v = sl[in.z * EH_T + lane] + sl[in.w * EH_T + lane]; break;
+        case G_SUB: v = sl[in.z * EH_T + lane] - sl[in.w * EH_T + lane]; break;
+        case G_MUL: v = sl[in.z * EH_T + lane] * sl[in.w * EH_T + lane]; break;
+        case G_NEG: v = neg(sl[in.z * EH_T + lane]); break;
+        default:  // G_HORNER
+          acc = acc * a.y + sl[in.z * EH_T + lane];
+          continue;
+      }
+      sl[in.y * EH_T + lane] = v;
+    }
+    if (a.nsets > 0) {
+      const uint64_t r_next = (idx + a.rot_scale) & emask;
+      const uint64_t r_last = (idx + (uint64_t)((int64_t)a.last_rot * (int64_t)a.rot_scale)) & emask;
+      const Fr l0 = ldf(a.l0 + idx);
+      // l_0(X) * (1 - z_0(X))
+      acc = acc * a.y + (Fr::one() - ldf(a.z[0] + idx)) * l0;
+      // l_last(X) * (z_l(X)^2 - z_l(X))
+      {
+        const Fr zl = ldf(a.z[a.nsets - 1] + idx);
+        acc = acc * a.y + (zl * zl - zl) * ldf(a.l_last + idx);
+      }
+      // l_0(X) * (z_i(X) - z_{i-1}(omega^(last) X))
+      for (int s = 1; s < a.nsets; s++) acc = acc * a.y + (ldf(a.z[s] + idx) - ldf(a.z[s - 1] + r_last)) * l0;
+      // l_active(X) * (z_i(omega X) prod(p + beta sigma + gamma) - z_i(X) prod(p + delta^j beta X + gamma))
+      const Fr la = ldf(a.l_active + idx);
+      Fr cur = a.delta_start * pw(a.ext_omega, idx);
+      for (int s = 0; s < a.nsets; s++) {
+        const int c0 = s * a.chunk_len;
+        const int c1 = c0 + a.chunk_len < a.P ? c0 + a.chunk_len : a.P;
+        Fr left = ldf(a.z[s] + r_next);
+        Fr right = ldf(a.z[s] + idx);
+        for (int c = c0; c < c1; c++) {
+          const Fr v = ldf(a.perm_v[c] + idx);
+          left = left * (v + a.beta * ldf(a.sigma[c] + idx) + a.gamma);
+          right = right * (v + cur + a.gamma);
+          cur = cur * a.delta;
+        }
+        acc = acc * a.y + (left - right) * la;
+      }
+    }
+    stf(a.out + idx, acc * ldf(a.t_evals + (idx & a.t_mask)));
+  }
+}
+
+hipError_t evaluate_h(const EvalHArgs& a, hipStream_t st) {
+  if (a.n_slots > EH_MAX_SLOTS) return hipErrorInvalidValue;
+  const size_t lds = (size_t)(a.n_slots > 0 ? a.n_slots : 1) * EH_T * sizeof(Fr);
+  size_t blocks = (a.ext + EH_T - 1) / EH_T;
+  if (blocks > 256 * 32) blocks = 256 * 32;
+  hipLaunchKernelGGL(evaluate_h_kernel, dim3((unsigned)blocks), dim3(EH_T), lds, st, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ block helpers
+// sum over this block's threads of v_t * X^(t) with X_t = xs^t, where each thread's
+// value already covers `per` consecutive elements: tree combine with xs^(per*2^l).
+template <int NT>
+__device__ Fr block_weighted_sum(Fr v, Fr step /* weight between consecutive threads */, Fr* sh) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  Fr X = step;
+  for (int s = 1; s < NT; s <<= 1) {
+    if ((t & (2 * s - 1)) == 0) sh[t] = sh[t] + X * sh[t + s];
+    X = X * X;
+    __syncthreads();
+  }
+  const Fr r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+// Suffix scan of affine maps f_t(c) = val_t + w_t * c over the block's threads.
+// Returns, for thread t, the map F_{t+1} = f_{t+1} o ... o f_{NT-1} as (val, w)
+// (identity (0, 1) for the last thread).
+template <int NT>
+__device__ void block_suffix_affine(Fr val, Fr w, Fr* shv, Fr* shw, Fr* out_val, Fr* out_w) {
+  const int t = threadIdx.x;
+  shv[t] = val;
+  shw[t] = w;
+  __syncthreads();
+  for (int s = 1; s < NT; s <<= 1) {
+    Fr v2 = shv[t], w2 = shw[t];
+    if (t + s < NT) {
+      // f_t..f_{t+s-1} composed with the next block of maps: (v, w) o (v', w') = (v + w v', w w')
+      const Fr vn = shv[t + s], wn = shw[t + s];
+      v2 = v2 + w2 * vn;
+      w2 = w2 * wn;
+    }
+    __syncthreads();
+    shv[t] = v2;
+    shw[t] = w2;
+    __syncthreads();
+  }
+  if (t + 1 < NT) {
+    *out_val = shv[t + 1];
+    *out_w = shw[t + 1];
+  } else {
+    *out_val = Fr::zero();
+    *out_w = Fr::one();
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------ polynomial evaluation
+static constexpr int EV_T = 256;
+static constexpr int EV_S = 16;                          // coefficients per thread
+static constexpr uint64_t EV_BLK = (uint64_t)EV_T * EV_S;  // per block
+
+__global__ void __launch_bounds__(EV_T) eval_level1(const EvalReq* __restrict__ reqs, Fr* __restrict__ part,
+                                                    uint64_t nbmax) {
+  __shared__ Fr sh[EV_T];
+  const EvalReq rq = reqs[blockIdx.y];
+  const uint64_t base = blockIdx.x * EV_BLK;
+  if (base >= rq.len) {
+    if (threadIdx.x == 0) part[blockIdx.y * nbmax + blockIdx.x] = Fr::zero();
+    return;
+  }
+  const uint64_t lo = base + (uint64_t)threadIdx.x * EV_S;
+  Fr acc = Fr::zero();
+  for (int i = EV_S - 1; i >= 0; i--) {
+    const uint64_t j = lo + i;
+    acc = acc * rq.x + (j < rq.len ? ldf(rq.poly + j) : Fr::zero());
+  }
+  Fr step = rq.x;
+#pragma unroll
+  for (int i = 0; i < 4; i++) step = step * step;  // x^16
+  const Fr r = block_weighted_sum<EV_T>(acc, step, sh);
+  if (threadIdx.x == 0) part[blockIdx.y * nbmax + blockIdx.x] = r;
+}
+
+__global__ void __launch_bounds__(EV_T) eval_level2(const EvalReq* __restrict__ reqs, const Fr* __restrict__ part,
+                                                    uint64_t nbmax, Fr* __restrict__ out) {
+  __shared__ Fr sh[EV_T];
+  const EvalReq rq = reqs[blockIdx.x];
+  const uint64_t nb = (rq.len + EV_BLK - 1) / EV_BLK;
+  const uint64_t per = (nb + EV_T - 1) / EV_T;
+  Fr xb = rq.x;
+  for (int i = 0; i < 12; i++) xb = xb * xb;  // x^4096 = x^EV_BLK
+  const Fr* p = part + blockIdx.x * nbmax;
+  const uint64_t lo = (uint64_t)threadIdx.x * per;
+  Fr acc = Fr::zero();
+  for (uint64_t i = per; i-- > 0;) {
+    const uint64_t j = lo + i;
+    acc = acc * xb + (j < nb ? p[j] : Fr::zero());
+  }
+  const Fr step = pow_u64(xb, per);
+  const Fr r = block_weighted_sum<EV_T>(acc, step, sh);
+  if (threadIdx.x == 0) out[blockIdx.x] = r;
+}
+
+size_t poly_eval_scratch_len(int nreq, uint64_t max_len) {
+  const uint64_t nb = (max_len + EV_BLK - 1) / EV_BLK;
+  return (size_t)nreq * (nb ? nb : 1);
+}
+
+hipError_t poly_eval_batch(const EvalReq* d_reqs, int nreq, uint64_t max_len, Fr* d_out, Fr* scratch,
+                           hipStream_t st) {
+  if (nreq == 0) return hipSuccess;
+  uint64_t nb = (max_len + EV_BLK - 1) / EV_BLK;
+  if (nb == 0) nb = 1;
+  hipLaunchKernelGGL(eval_level1, dim3((unsigned)nb, (unsigned)nreq), dim3(EV_T), 0, st, d_reqs, scratch, nb);
+  hipLaunchKernelGGL(eval_level2, dim3((unsigned)nreq), dim3(EV_T), 0, st, d_reqs, (const Fr*)scratch, nb, d_out);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ kate division
+// With a' = a[1..len) and M = len - 1: q[i] = sum_{j >= i} a'[j] b^(j - i), i.e. the
+// suffix Horner of a' at b.  Phase 1: per-tile sums; phase 2: tile carries (one block,
+// suffix scan of affine maps); phase 3: per-thread carries + the downward recurrence.
+static constexpr int KD_T = 256;
+static constexpr int KD_S = 8;
+static constexpr uint64_t KD_TILE = (uint64_t)KD_T * KD_S;
+
+__global__ void __launch_bounds__(KD_T) kate_phase1(const Fr* __restrict__ a1, uint64_t M, Fr b,
+                                                    Fr* __restrict__ tile_val) {
+  __shared__ Fr sh[KD_T];
+  const uint64_t lo = blockIdx.x * KD_TILE + (uint64_t)threadIdx.x * KD_S;
+  Fr acc = Fr::zero();
+  for (int i = KD_S - 1; i >= 0; i--) {
+    const uint64_t j = lo + i;
+    acc = acc * b + (j < M ? ldf(a1 + j) : Fr::zero());
+  }
+  Fr step = b;
+#pragma unroll
+  for (int i = 0; i < 3; i++) step = step * step;  // b^8
+  const Fr r = block_weighted_sum<KD_T>(acc, step, sh);
+  if (threadIdx.x == 0) tile_val[blockIdx.x] = r;
+}
+
+// one block: carry[c] = q[hi_c] = sum_{c' > c} V_c' B^(c' - c - 1), B = b^TILE
+__global__ void __launch_bounds__(KD_T) kate_phase2(Fr* __restrict__ tile_val, uint64_t ntiles, Fr b) {
+  __shared__ Fr shv[KD_T], shw[KD_T];
+  Fr B = b;
+  for (int i = 0; i < 11; i++) B = B * B;  // b^2048 = b^TILE
+  const uint64_t per = (ntiles + KD_T - 1) / KD_T;
+  const uint64_t lo = (uint64_t)threadIdx.x * per;
+  const uint64_t hi = lo + per < ntiles ? lo + per : ntiles;
+  // group map: f(c) = sum_{i in group} V_i B^(i - lo) + B^(cnt) c
+  Fr val = Fr::zero(), w = Fr::one();
+  for (uint64_t i = hi; i-- > lo;) {
+    val = val * B + tile_val[i];
+    w = w * B;
+  }
+  Fr cv, cw;
+  block_suffix_affine<KD_T>(val, w, shv, shw, &cv, &cw);
+  // carry above this group = F_{t+1}(0) = cv; walk down the group
+  Fr carry = cv;
+  for (uint64_t i = hi; i-- > lo;) {
+    const Fr v = tile_val[i];
+    tile_val[i] = carry;  // q at the top of tile i
+    carry = v + B * carry;
+  }
+}
+
+__global__ void __launch_bounds__(KD_T) kate_phase3(const Fr* __restrict__ a1, uint64_t M, Fr b,
+                                                    const Fr* __restrict__ tile_carry, Fr* __restrict__ q) {
+  __shared__ Fr shv[KD_T], shw[KD_T];
+  const uint64_t lo = blockIdx.x * KD_TILE + (uint64_t)threadIdx.x * KD_S;
+  Fr val = Fr::zero(), w = Fr::one();
+  for (int i = KD_S - 1; i >= 0; i--) {
+    const uint64_t j = lo + i;
+    val = val * b + (j < M ? ldf(a1 + j) : Fr::zero());
+    w = w * b;
+  }
+  Fr cv, cw;
+  block_suffix_affine<KD_T>(val, w, shv, shw, &cv, &cw);
+  Fr cur = cv + cw * tile_carry[blockIdx.x];
+  for (int i = KD_S - 1; i >= 0; i--) {
+    const uint64_t j = lo + i;
+    if (j < M) {
+      cur = ldf(a1 + j) + b * cur;
+      stf(q + j, cur);
+    }
+  }
+}
+
+size_t kate_scratch_len(uint64_t len) { return (size_t)((len + KD_TILE - 1) / KD_TILE + 1); }
+
+hipError_t kate_division(const Fr* a, uint64_t len, const Fr& b, Fr* q, Fr* scratch, hipStream_t st) {
+  if (len < 2) return hipSuccess;
+  const uint64_t M = len - 1;
+  const uint64_t nt = (M + KD_TILE - 1) / KD_TILE;
+  hipLaunchKernelGGL(kate_phase1, dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, scratch);
+  hipLaunchKernelGGL(kate_phase2, dim3(1), dim3(KD_T), 0, st, scratch, nt, b);
+  hipLaunchKernelGGL(kate_phase3, dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, (const Fr*)scratch, q);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ linear combinations
+__global__ void __launch_bounds__(KT) lincomb_kernel(Fr* __restrict__ out, uint64_t n, LinTerms t, int acc_in) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    Fr acc = acc_in ? ldf(out + i) : Fr::zero();
+    for (int k = 0; k < t.k; k++)
+      if (i < t.len[k]) acc = acc + t.coef[k] * ldf(t.p[k] + i);
+    stf(out + i, acc);
+  }
+}
+
+hipError_t lincomb(Fr* out, uint64_t n, const LinTerms& t, bool accumulate, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(lincomb_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, out, n, t, accumulate ? 1 : 0);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(KT) scale_dev_kernel(Fr* __restrict__ out, const Fr* __restrict__ a, uint64_t n,
+                                                       const Fr* __restrict__ s) {
+  const Fr c = ldf(s);
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    stf(out + i, ldf(a + i) * c);
+}
+
+hipError_t scale_by_dev(Fr* out, const Fr* a, uint64_t n, const Fr* scalar, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(scale_dev_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, out, a, n, scalar);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ keygen helpers
+__global__ void __launch_bounds__(KT) sigma_kernel(Fr* __restrict__ sigma, const uint32_t* __restrict__ mc,
+                                                   const uint32_t* __restrict__ mr, size_t n,
+                                                   const Fr* __restrict__ dp, PowTable om) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    stf(sigma + i, ldf(dp + mc[i]) * pw(om, mr[i]));
+}
+
+hipError_t sigma_from_mapping(Fr* sigma, const uint32_t* map_col, const uint32_t* map_row, size_t n,
+                              const Fr* delta_pow, const PowTable& omega, hipStream_t st) {
+  hipLaunchKernelGGL(sigma_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, sigma, map_col, map_row, n, delta_pow, omega);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(KT) lag_den_kernel(Fr* __restrict__ d, size_t n, Fr s, PowTable om) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    stf(d + i, s - pw(om, i));
+}
+__global__ void __launch_bounds__(KT) lag_num_kernel(Fr* __restrict__ d, size_t n, Fr mult, PowTable om) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    stf(d + i, ldf(d + i) * mult * pw(om, i));
+}
+
+hipError_t srs_lagrange_scalars(Fr* out, size_t n, const Fr& s, const Fr& mult, const PowTable& omega, Fr* scratch,
+                                hipStream_t st) {
+  hipLaunchKernelGGL(lag_den_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, out, n, s, omega);
+  hipError_t e = poly_batch_invert(out, n, scratch, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(lag_num_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, out, n, mult, omega);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(KT) gen_mul_kernel(const Fr* __restrict__ sc, size_t n, G1Affine* __restrict__ out) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Fr e = to_canonical(ldf(sc + i));
+  G1Affine g;
+  g.x = Fq::one();
+  g.y = from_u64<FqParams>(2);
+  out[i] = xyzz_to_affine(xyzz_mul_canonical(G1xyzz::from_affine(g), e.l));
+}
+
+hipError_t g1_generator_mul(const Fr* scalars, size_t n, G1Affine* out, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(gen_mul_kernel, dim3((unsigned)((n + KT - 1) / KT)), dim3(KT), 0, st, scalars, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace h2g

@@ -1,0 +1,131 @@
+// runtime.h -- host-side device runtime shared by the C ABI (abi.cpp) and the
+// prover orchestrator (prover.cpp): per-device state (stream, MSM workspace,
+// grow-only scratch buffers, NTT twiddle tables), evaluation domains, error
+// reporting.  Definitions live in abi.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/h2g.h"
+#include "bn254.h"
+#include "msm.h"
+#include "ntt.h"
+
+namespace h2g {
+namespace rt {
+
+extern thread_local std::string g_err;
+extern std::recursive_mutex g_mu;
+
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+#define HIPCHK(expr)                                                \
+  do {                                                              \
+    hipError_t _e = (expr);                                         \
+    if (_e != hipSuccess) return ::h2g::rt::hip_fail(_e, #expr);    \
+  } while (0)
+
+#define RCCHK(expr)         \
+  do {                      \
+    int _rc = (expr);       \
+    if (_rc) return _rc;    \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct NttKey {
+  int L;
+  uint32_t w[8];
+  bool operator<(const NttKey& o) const {
+    if (L != o.L) return L < o.L;
+    return std::memcmp(w, o.w, sizeof(w)) < 0;
+  }
+};
+
+// EvaluationDomain constants (halo2_backend/src/poly/domain.rs:38-144)
+struct Domain {
+  uint32_t j = 0, k = 0, ek = 0;
+  Fr omega, omega_inv, ext_omega, ext_omega_inv, g_coset, g_coset_inv, ifft_div, ext_ifft_div, bary;
+  std::vector<Fr> t_evals;
+  Fr* d_t = nullptr;
+};
+
+struct Descriptor {
+  int device;
+  void* d = nullptr;
+  size_t n = 0;
+  bool is_base = false;
+};
+
+struct Device {
+  int id = 0;
+  hipStream_t stream = nullptr;
+  MsmWorkspace msm;
+  DevBuf a, b, c, work, out;
+  std::map<NttKey, NttTables> ntt_tables;
+  void* h_windows = nullptr;  // pinned host copy of MSM window sums
+};
+
+extern std::vector<std::unique_ptr<Device>> g_devs;
+extern bool g_profile;
+extern std::vector<MsmPhaseEvents> g_msm_prof;
+extern int g_cur;
+extern std::map<uint64_t, Descriptor> g_desc;
+extern std::map<uint64_t, std::unique_ptr<Domain>> g_dom;
+extern uint64_t g_next_handle;
+
+Device* cur();
+inline hipStream_t pick_stream(Device* d, void* s) { return s ? reinterpret_cast<hipStream_t>(s) : d->stream; }
+
+Fr fr_from_limbs(const uint64_t* v);
+void fr_to_limbs(const Fr& a, uint64_t* v);
+Fr root_of_unity();
+Fr zeta();
+Fr fr_delta();
+constexpr uint32_t FR_S = 28;
+
+int domain_init(Domain* dm, uint32_t j, uint32_t k);  // host constants + device t-evaluations
+void domain_release(Domain* dm);
+Domain* get_dom(uint64_t h);
+
+int get_tables(Device* d, const Fr& omega, int L, hipStream_t st, NttTables* out);
+int msm_dev_impl(Device* d, const void* sc, const void* bs, size_t n, int c, void* out, hipStream_t st);
+int msm_host_impl(Device* d, const void* sc, const void* bs, size_t n, int c, uint64_t* out, int* is_id,
+                  hipStream_t st);
+int ntt_dev_impl(Device* d, const Fr* src, uint64_t n_in, Fr* dst, uint64_t out_len, int L, const Fr& omega,
+                 int in_dist, const Fr& iz1, const Fr& iz2, int has_scale, const Fr& scale, int out_dist,
+                 const Fr& oz1, const Fr& oz2, hipStream_t st);
+
+// EvaluationDomain maps on device pointers (domain.rs:216-316)
+int lagrange_to_coeff(Device* d, const Domain& dm, const Fr* src, Fr* dst, hipStream_t st);
+int coeff_to_extended(Device* d, const Domain& dm, const Fr* src, Fr* dst, hipStream_t st);
+int extended_to_coeff(Device* d, const Domain& dm, const Fr* src, Fr* dst, hipStream_t st);
+
+}  // namespace rt
+}  // namespace h2g

@@ -76,6 +76,17 @@ _SIGS = {
     "h2g_g1_add_affine": ([U64P, U64P, U64P], I32),
     "h2g_profile_enable": ([I32], I32),
     "h2g_profile_msm_collect": ([ctypes.POINTER(ctypes.c_float), I32, ctypes.POINTER(I32), ctypes.POINTER(I32)], I32),
+    "h2g_params_create": ([U32, U64P, U64P, ctypes.POINTER(U64)], I32),
+    "h2g_params_setup": ([U32, U64P, ctypes.POINTER(U64)], I32),
+    "h2g_params_export": ([U64, U64P, U64P], I32),
+    "h2g_params_free": ([U64], I32),
+    "h2g_keygen": ([U64, VP, ctypes.POINTER(U64)], I32),
+    "h2g_pk_free": ([U64], I32),
+    "h2g_pk_info": ([U64, ctypes.POINTER(ctypes.c_int32)], I32),
+    "h2g_create_proof": ([U64, U64, VP, I32, U64P, ctypes.POINTER(U32), ctypes.c_char_p, U32, ctypes.c_char_p, SZ,
+                          ctypes.POINTER(SZ)], I32),
+    "h2g_prover_stages": ([ctypes.POINTER(ctypes.c_double), I32, ctypes.POINTER(I32)], I32),
+    "h2g_prover_stage_name": ([I32], ctypes.c_char_p),
 }
 
 MSM_PHASES = ("digits", "sort", "bucket_bounds", "accumulate", "bucket_fixup", "reduce")
@@ -370,3 +381,110 @@ class Timer:
         ms = ctypes.c_float(0)
         check(lib().h2g_event_elapsed_ms(self.a, self.b, ctypes.byref(ms)))
         return ms.value
+
+
+# ----------------------------------------------------------------------------- prover
+I32P_ = ctypes.POINTER(ctypes.c_int32)
+
+
+class H2gCircuit(ctypes.Structure):
+    """struct h2g_circuit (include/h2g.h)"""
+    _fields_ = [
+        ("k", U32), ("num_advice", U32), ("num_fixed", U32), ("num_instance", U32),
+        ("num_gates", U32), ("gate_roots", I32P_),
+        ("num_nodes", U32), ("nodes", I32P_),
+        ("num_constants", U32), ("constants", U64P),
+        ("num_perm_columns", U32), ("perm_columns", I32P_),
+        ("num_copies", U32), ("copies", I32P_),
+        ("fixed_values", U64P), ("unblinded", ctypes.POINTER(ctypes.c_uint8)),
+        ("transcript_repr", U64P),
+    ]
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(t) if a is not None and a.size else None
+
+
+class Params:
+    """ParamsKZG resident on the device (g, g_lagrange)."""
+
+    def __init__(self, k, g=None, g_lagrange=None, s=None):
+        self.k = k
+        h = U64()
+        if s is not None:
+            s = np.ascontiguousarray(s, dtype=np.uint64)
+            check(lib().h2g_params_setup(k, p64(s), ctypes.byref(h)))
+        else:
+            g = np.ascontiguousarray(g, dtype=np.uint64)
+            gl = np.ascontiguousarray(g_lagrange, dtype=np.uint64)
+            check(lib().h2g_params_create(k, p64(g), p64(gl), ctypes.byref(h)))
+        self.handle = h.value
+
+    def export(self):
+        n = 1 << self.k
+        g = np.zeros((n, 8), dtype=np.uint64)
+        gl = np.zeros((n, 8), dtype=np.uint64)
+        check(lib().h2g_params_export(self.handle, p64(g), p64(gl)))
+        return g, gl
+
+    def close(self):
+        if self.handle:
+            lib().h2g_params_free(self.handle)
+            self.handle = 0
+
+
+class ProvingKey:
+    """keygen_vk + keygen_pk on the device for an h2g_circuit.Circuit."""
+
+    def __init__(self, params, circ):
+        self.params = params
+        self.circ = circ
+        keep = [np.ascontiguousarray(x) for x in (circ.gate_roots, circ.nodes, circ.constants, circ.perm_array,
+                                                  circ.copies, circ.fixed_values, circ.unblinded,
+                                                  circ.transcript_repr())]
+        roots, nodes, consts, perm, copies, fixed, unb, tr = keep
+        c = H2gCircuit(circ.k, circ.num_advice, circ.num_fixed, circ.num_instance,
+                       len(roots), _ptr(roots, I32P_), len(nodes), _ptr(nodes, I32P_),
+                       circ.num_constants, _ptr(consts, U64P), len(perm), _ptr(perm, I32P_),
+                       len(copies), _ptr(copies, I32P_), _ptr(fixed, U64P),
+                       _ptr(unb, ctypes.POINTER(ctypes.c_uint8)), _ptr(tr, U64P))
+        h = U64()
+        check(lib().h2g_keygen(params.handle, ctypes.byref(c), ctypes.byref(h)))
+        self.handle = h.value
+        info = (ctypes.c_int32 * 8)()
+        check(lib().h2g_pk_info(self.handle, info))
+        (self.degree, self.bf, self.extended_k, self.nsets, self.n_adv_q, self.n_fix_q, self.n_ins_q,
+         self.n_slots) = list(info)
+
+    def create_proof(self, wit=None, seed=bytes([7] * 32), vanishing_threads=8, advice_dev_ptr=None):
+        """-> proof bytes.  advice_dev_ptr: device pointer to num_advice x n Fr (resident inputs)."""
+        circ = self.circ
+        n = 1 << circ.k
+        if advice_dev_ptr is not None:
+            adv_p, on_dev = VP(advice_dev_ptr), 1
+            adv = None
+        else:
+            adv = np.ascontiguousarray(wit.advice, dtype=np.uint64)
+            adv_p, on_dev = VP(adv.ctypes.data) if adv.size else None, 0
+        ins = np.ascontiguousarray(wit.instance, dtype=np.uint64) if circ.num_instance else np.zeros(4, np.uint64)
+        lens = np.ascontiguousarray(wit.instance_lens if circ.num_instance else np.zeros(1), dtype=np.uint32)
+        cap = 32 * (64 + 8 * (circ.num_advice + circ.num_fixed + 4 * len(circ.perm_columns)) + 64 * 64)
+        buf = ctypes.create_string_buffer(cap)
+        ln = SZ()
+        check(lib().h2g_create_proof(self.params.handle, self.handle, adv_p, on_dev, p64(ins),
+                                     lens.ctypes.data_as(ctypes.POINTER(U32)), bytes(seed), vanishing_threads,
+                                     buf, cap, ctypes.byref(ln)))
+        del adv
+        return buf.raw[: ln.value]
+
+    def close(self):
+        if self.handle:
+            lib().h2g_pk_free(self.handle)
+            self.handle = 0
+
+
+def prover_stages():
+    ms = (ctypes.c_double * 64)()
+    cnt = I32()
+    check(lib().h2g_prover_stages(ms, 64, ctypes.byref(cnt)))
+    return [(lib().h2g_prover_stage_name(i).decode(), ms[i]) for i in range(min(cnt.value, 64))]
