@@ -1,22 +1,28 @@
 #!/usr/bin/env python3
-"""Benchmark: BN254 G1 MSM throughput (Mscalar-mul/s) at 2^24 points per GPU.
+"""Benchmark of the MI355X prover hot path (BASELINE.json metric:
+"create_proof wall-seconds at k=22 (BN254/KZG); MSM Mscalar-mul/s at 2^24").
 
-BASELINE.json metric: "create_proof wall-seconds at k=22 (BN254/KZG); MSM
-Mscalar-mul/s at 2^24".  This round the bench line reports the MSM half of it:
-one step = one MSM of 2^24 (scalar, SRS point) pairs resident in HBM, through
-the C ABI (h2g_msm_dev) on torch's current stream.
+Default workload (--workload prove): one step = one full create_proof
+(KZG + SHPLONK + Blake2b) of the C3 synthetic circuit at k=22 (BASELINE configs[2]/[3]:
+3 advice a,b,c + 1 fixed f, gate f*(a*b - c), a,b,c in the permutation, copies
+c_i -> a_{i+1}) through the C ABI (h2g_create_proof), witness resident in HBM when the
+timed region starts.  value = wall-seconds per proof (lower is better).  The proof
+bytes of this exact pipeline are tested identical to the CPU restatement prover
+(tests/test_gpu_prover.py).
+N > 1 (torchrun, one process per GPU): every rank proves its own instance (the path
+does not shard a single proof yet -- replicas); value = max-over-ranks wall time /
+(steps * N), "scaling": "weak".
 
-N > 1 (torchrun, one process per GPU): the MSM is sharded by point slabs
-(weak scaling: every rank owns its own 2^24-point slab of a 2^24*N MSM); the
-per-rank partial sums (64 B affine points) are exchanged with an RCCL
-all_gather and summed on the host -- the one real exchange step of a sharded
-MSM.
+--workload msm: one step = one MSM of 2^24 resident (scalar, SRS point) pairs
+(h2g_msm_dev_host); N > 1 shards point slabs and all_gathers the 64-B partials (RCCL).
 
-Also printed in the same JSON line:
-  roofline     : dominant kernel (bucket accumulation) from live HIP events;
-                 algorithmic bytes = 96 B/point
-  cpu_baseline : the CPU restatement oracle (halo2curves best_multiexp
-                 algorithm, oracle/) timed on a bounded sample on this host
+Also in the JSON line:
+  roofline     : dominant kernel = msm_acc_kernel (bucket accumulation), average
+                 launch time from HIP events on the library stream over the timed
+                 region; algorithmic bytes = 96 B/point x points per launch; PMC
+                 traffic from rocprofv3 --pmc child passes (MI355X guide recipe)
+  cpu_baseline : the CPU restatement (oracle/, halo2 algorithms) timed on a bounded
+                 sample on this host
 """
 import argparse
 import json
@@ -32,6 +38,8 @@ sys.path.insert(0, os.path.join(REPO, "yet-another-halo2-fork_amd"))
 HBM_PEAK_GBS = 8000.0
 MSM_BYTES_PER_POINT = 96  # 32 B scalar + 64 B affine base
 MADD_MODMUL = 10          # XYZZ mixed add: 8M + 2S
+PROVE_K = 22
+METRIC = "create_proof wall-seconds at k=22 (BN254/KZG); MSM Mscalar-mul/s at 2^24"
 
 
 def random_scalars(rng, n):
@@ -42,16 +50,53 @@ def random_scalars(rng, n):
     return c
 
 
-def cpu_baseline(log_n=20, reps=2):
-    """Oracle (CPU restatement, halo2curves best_multiexp algorithm) on a bounded
-    sample: one MSM of 2^log_n points with all host threads (<= 16)."""
+def h2g_choose_c(n):
+    # mirror of msm_choose_c (msm.hip) for reporting
+    best, bc = 1e300, 2
+    for c in range(2, 23):
+        W = (255 + c - 1) // c
+        cost = W * (n + 2.8 * (1 << (c - 1)))
+        if cost < best:
+            best, bc = cost, c
+    return bc
+
+
+# ----------------------------------------------------------------------------- CPU baselines
+def _oracle():
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle as O
+    return O
 
+
+def cpu_baseline_prove(k_sample=18, reps=1):
+    """The oracle's create_proof (C restatement of halo2's prover with best_multiexp /
+    best_fft, OpenMP) on the same C3 circuit at a bounded k, keygen excluded, scaled
+    linearly in n to k=22."""
+    O = _oracle()
+    import h2g_circuit as hc
+
+    threads = min(16, os.cpu_count() or 1)
+    circ, wit = hc.synthetic_c3(k_sample, O.OracleOps)
+    s, g, gl = O.srs(k_sample)
+    kg = O.Keygen(circ, wit, g, gl, threads=threads)
+    best = 1e30
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        O.create_proof(circ, wit, g, gl, threads=threads, keygen=kg)
+        best = min(best, time.perf_counter() - t0)
+    kg.close()
+    scale = 1 << (PROVE_K - k_sample)
+    return {"value": round(best * scale, 3), "unit": "s", "cores": threads, "kind": "port",
+            "sample": f"oracle create_proof (C restatement, OpenMP) of the C3 circuit at k={k_sample}: "
+                      f"{best:.3f} s measured, x{scale} (linear in n) to k={PROVE_K}; {threads} threads"}
+
+
+def cpu_baseline_msm(log_n=20, reps=2):
+    """Oracle best_multiexp (halo2curves algorithm) on one 2^log_n MSM."""
+    O = _oracle()
     threads = min(16, os.cpu_count() or 1)
     rng = np.random.default_rng(5)
     n = 1 << log_n
-    # bases: any valid points work for timing; reuse a small SRS tiled
     s = O.random_fr(rng, 1)[0]
     small = O.srs_powers(s, 1 << 10)
     bases = np.ascontiguousarray(np.tile(small, (n >> 10, 1)))
@@ -66,11 +111,12 @@ def cpu_baseline(log_n=20, reps=2):
                       f"{threads} threads, best of {reps}"}
 
 
-def pmc_traffic(log_n, window_bits):
+# ----------------------------------------------------------------------------- PMC traffic
+def pmc_traffic(args):
     """HBM traffic of the dominant kernel from PMC counters, per the MI355X guide:
     one rocprofv3 --pmc pass per counter (FETCH_SIZE and WRITE_SIZE cannot share a
     pass), values in KiB, FETCH_SIZE doubled (gfx950 reports half of a 16-B/lane
-    read stream).  Runs child processes BEFORE this process touches the GPU."""
+    read stream).  Child processes run BEFORE this process touches the GPU."""
     import csv
     import shutil
     import subprocess
@@ -84,11 +130,11 @@ def pmc_traffic(log_n, window_bits):
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix=f"h2g_pmc_{ctr}_", dir="/tmp")
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
-               sys.executable, os.path.abspath(__file__), "--pmc-child", "--log-n", str(log_n),
-               "--window-bits", str(window_bits)]
+               sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
+               "--log-n", str(args.log_n), "--k", str(args.k)]
         try:
             subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                           timeout=240, check=True)
+                           timeout=300, check=True)
             rows = []
             for root, _, files in os.walk(d):
                 for f in files:
@@ -103,65 +149,140 @@ def pmc_traffic(log_n, window_bits):
         finally:
             shutil.rmtree(d, ignore_errors=True)
     traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
-    return traffic, (f"rocprofv3 --pmc per launch of msm_acc_kernel: FETCH_SIZE {vals['FETCH_SIZE']:.0f} KiB (x2 gfx950 "
-                     f"correction), WRITE_SIZE {vals['WRITE_SIZE']:.0f} KiB")
+    return traffic, (f"rocprofv3 --pmc, mean per launch of msm_acc_kernel: FETCH_SIZE {vals['FETCH_SIZE']:.0f} KiB "
+                     f"(x2 gfx950 correction), WRITE_SIZE {vals['WRITE_SIZE']:.0f} KiB")
 
 
 def pmc_child(args):
-    """Minimal profiled workload: SRS + 2 MSMs (no torch)."""
+    """Minimal profiled workload (no torch): one proof, or SRS + 2 MSMs."""
     import h2g
 
     h2g.init([0])
-    n = 1 << args.log_n
-    rng = np.random.default_rng(1000)
-    bases = h2g.DevBuf(n * 64)
-    h2g.srs_setup_dev(random_scalars(rng, 1)[0], n, bases.ptr)
-    sc = h2g.DevBuf.from_array(random_scalars(rng, n))
-    for _ in range(2):
-        h2g.msm_dev_host(sc.ptr, bases.ptr, n, args.window_bits)
+    if args.workload == "prove":
+        import h2g_circuit as hc
+        circ, wit = hc.synthetic_c3(args.k, h2g.DeviceOps)
+        params = h2g.Params(args.k, s=np.asarray(hc.fr_to_limbs(0x1234567), dtype=np.uint64))
+        pk = h2g.ProvingKey(params, circ)
+        pk.create_proof(wit)
+        pk.close()
+        params.close()
+    else:
+        n = 1 << args.log_n
+        rng = np.random.default_rng(1000)
+        bases = h2g.DevBuf(n * 64)
+        h2g.srs_setup_dev(random_scalars(rng, 1)[0], n, bases.ptr)
+        sc = h2g.DevBuf.from_array(random_scalars(rng, n))
+        for _ in range(2):
+            h2g.msm_dev_host(sc.ptr, bases.ptr, n, 0)
     h2g.shutdown()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--log-n", type=int, default=24)
-    ap.add_argument("--window-bits", type=int, default=0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pmc", action="store_true", help="skip the PMC traffic passes")
-    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
-    args = ap.parse_args()
-    if args.pmc_child:
-        return pmc_child(args)
+# ----------------------------------------------------------------------------- roofline
+def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note):
+    acc_ms = phases.get("accumulate", 0.0) / max(calls, 1)
+    achieved = (points_per_launch * MSM_BYTES_PER_POINT) / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
+    c = h2g_choose_c(points_per_launch)
+    W = (255 + c - 1) // c
+    modmul_rate = (points_per_launch * W * MADD_MODMUL) / (acc_ms * 1e-3) if acc_ms > 0 else None
+    return {
+        "bound": "hbm",
+        "kernel": "msm_acc_kernel (Pippenger bucket accumulation)",
+        "achieved": round(achieved, 2) if achieved else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
+        "traffic": round(traffic) if traffic else None,
+        "traffic_note": traffic_note,
+        "kernel_ms": round(acc_ms, 4),
+        "launches": calls,
+        "bytes_per_launch": points_per_launch * MSM_BYTES_PER_POINT,
+        "note": "VALU-bound 256-bit modular arithmetic (no MFMA applies); the HBM fraction is low by "
+                "construction -- valu_modmul_per_s vs the measured 125 G/s Fq-modmul peak is the compute view",
+        "valu_modmul_per_s": round(modmul_rate, 1) if modmul_rate else None,
+        "window_bits": c,
+    }
 
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    traffic, traffic_note = (None, "skipped (--no-pmc)")
-    if not args.no_pmc and world_env == 1:
-        traffic, traffic_note = pmc_traffic(args.log_n, args.window_bits)
 
-    import torch
-    import torch.distributed as dist
+# ----------------------------------------------------------------------------- workloads
+def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
+    import h2g_circuit as hc
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    k = args.k
+    n = 1 << k
+    circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=3 + rank)
+    params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(0x1234567 + rank), dtype=np.uint64))
+    pk = h2g.ProvingKey(params, circ)
+    adv = torch.from_numpy(np.ascontiguousarray(wit.advice).view(np.int64)).to(dev)  # resident witness
+    torch.cuda.synchronize()
+    proofs = []
+
+    def step():
+        proofs.append(pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr()))
+
+    for _ in range(args.warmup):
+        step()
+    # PCIe-inclusive variant (advice handed over in host memory), reported beside value
+    t0 = time.perf_counter()
+    pk.create_proof(wit)
+    pcie_s = time.perf_counter() - t0
+    torch.cuda.synchronize()
     if world > 1:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        dist.barrier()
+    torch.cuda.synchronize()
+    h2g.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    h2g.profile_enable(False)
+    calls, phases = h2g.profile_msm_collect()
+    stages = h2g.prover_stages()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert all(p == proofs[0] for p in proofs), "non-deterministic proof bytes"
+    line = None
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        msm_ms = sum(phases.values()) / max(calls, 1)
+        line = {
+            "metric": METRIC,
+            "value": round(elapsed / (args.steps * world), 4),
+            "unit": "s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 limbs (BN254 Fr/Fq Montgomery, 256-bit modular integer)",
+            "data": "synthetic C3 witness (random b, a_0; a_{i+1} = c_i = a_i b_i), SRS from a fixed s generated "
+                    "on device, prover rng ChaCha20([7; 32])",
+            "config": {"workload": f"create_proof (KZG/SHPLONK/Blake2b) of the C3 synthetic circuit at k={k} "
+                                   "(BASELINE configs[2]/[3])",
+                       "k": k, "advice": 3, "fixed": 1, "permutation_columns": 3, "degree": pk.degree,
+                       "extended_k": pk.extended_k, "proof_bytes": len(proofs[0]),
+                       "parallelism": "single GPU per proof" if world == 1 else f"{world} independent provers"},
+            "roofline": roofline_from_phases(calls, phases, n, traffic, traffic_note),
+            "msm_in_prover": {"launches_per_proof": calls // max(args.steps, 1), "avg_ms": round(msm_ms, 4),
+                              "mscalar_mul_per_s": round(n / (msm_ms * 1e-3) / 1e6, 2) if msm_ms else None,
+                              "phases_ms": {kk: round(v / max(calls, 1), 4) for kk, v in phases.items()}},
+            "stages_ms_last_proof": {nm: round(ms, 3) for nm, ms in stages},
+            "pcie_inclusive_s": round(pcie_s, 4),
+        }
+    pk.close()
+    params.close()
+    return line
 
-    import h2g
 
-    h2g.init([torch.cuda.current_device()])
-    dev = torch.device("cuda", torch.cuda.current_device())
+def run_msm(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     stream = torch.cuda.current_stream().cuda_stream
     n = 1 << args.log_n
-
-    # inputs resident in HBM: SRS slab [s^i]G (generated on device) + random scalars
     rng = np.random.default_rng(1000 + rank)
     s = random_scalars(rng, 1)[0]
     bases = torch.empty((n, 8), dtype=torch.int64, device=dev)
@@ -171,8 +292,7 @@ def main():
     result = {}
 
     def step():
-        # MsmAccel::msm path: inputs resident in HBM, affine result returned to the host
-        result["p"] = h2g.msm_dev_host(scalars.data_ptr(), bases.data_ptr(), n, args.window_bits, stream)
+        result["p"] = h2g.msm_dev_host(scalars.data_ptr(), bases.data_ptr(), n, 0, stream)
 
     for _ in range(args.warmup):
         step()
@@ -194,122 +314,86 @@ def main():
     elapsed = time.perf_counter() - t0
     h2g.profile_enable(False)
     calls, phases = h2g.profile_msm_collect()
-
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        # combine the per-rank partial sums (host EC adds), once, outside timing
         total = np.zeros(8, dtype=np.uint64)
         for g in gathered:
             total = h2g.g1_add_affine(total, g.cpu().numpy().view(np.uint64))
+    if rank != 0:
+        return None
+    c = h2g_choose_c(n)
+    return {
+        "metric": METRIC,
+        "value": round(world * n * args.steps / elapsed / 1e6, 3),
+        "unit": "Mscalar-mul/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 limbs (BN254 Fr/Fq Montgomery, 256-bit modular integer)",
+        "data": "synthetic: uniform random Fr scalars, SRS bases [s^i]G generated on device",
+        "config": {"workload": f"BN254 G1 MSM, 2^{args.log_n} points per GPU (the metric's MSM half)",
+                   "points_per_gpu": n, "window_bits": c, "windows": (255 + c - 1) // c,
+                   "parallelism": f"point-slab shard x{world} + RCCL all_gather of partials"},
+        "roofline": roofline_from_phases(calls, phases, n, traffic, traffic_note),
+        "phases_ms": {kk: round(v / max(calls, 1), 4) for kk, v in phases.items()},
+    }
 
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=("prove", "msm"), default="prove")
+    ap.add_argument("--k", type=int, default=PROVE_K)
+    ap.add_argument("--log-n", type=int, default=24)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the PMC traffic passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.pmc_child:
+        return pmc_child(args)
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    traffic, traffic_note = (None, "skipped (--no-pmc)")
+    if not args.no_pmc and world_env == 1:
+        traffic, traffic_note = pmc_traffic(args)
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    import h2g
+
+    h2g.init([torch.cuda.current_device()])
+    dev = torch.device("cuda", torch.cuda.current_device())
+    run = run_prove if args.workload == "prove" else run_msm
+    line = run(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note)
     if rank == 0:
-        ms_per_step = elapsed / args.steps * 1e3
-        value = world * n * args.steps / elapsed / 1e6
-        acc_ms = phases.get("accumulate", 0.0) / max(calls, 1)
-        total_phase_ms = sum(phases.values()) / max(calls, 1)
-        achieved = (n * MSM_BYTES_PER_POINT) / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
-        W = None
-        try:
-            c = args.window_bits or h2g_choose_c(n)
-            W = (255 + c - 1) // c
-        except Exception:
-            c = None
-        modmul_rate = (n * W * MADD_MODMUL) / (acc_ms * 1e-3) if (acc_ms > 0 and W) else None
-        line = {
-            "metric": "MSM Mscalar-mul/s at 2^24 (BN254 G1)",
-            "value": round(value, 3),
-            "unit": "Mscalar-mul/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32 limbs (BN254 Fr/Fq Montgomery, 256-bit modular integer)",
-            "data": "synthetic: uniform random Fr scalars, SRS bases [s^i]G generated on device",
-            "config": {"workload": f"BN254 G1 MSM, 2^{args.log_n} points per GPU (BASELINE configs[1]/metric)",
-                       "points_per_gpu": n, "window_bits": c, "windows": W,
-                       "parallelism": f"point-slab shard x{world} + RCCL all_gather of partials"},
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "msm_acc_kernel (bucket accumulation)",
-                "achieved": round(achieved, 2) if achieved else None,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
-                "traffic": round(traffic) if traffic else None,
-                "traffic_note": traffic_note,
-                "kernel_ms": round(acc_ms, 4),
-                "note": "VALU-bound 256-bit modular arithmetic (no MFMA); HBM fraction is low by construction",
-                "valu_modmul_per_s": round(modmul_rate, 1) if modmul_rate else None,
-            },
-            "phases_ms": {k: round(v / max(calls, 1), 4) for k, v in phases.items()},
-            "msm_device_ms": round(total_phase_ms, 4),
-        }
-        line["ntt"] = ntt_extras(h2g, torch, dev, stream)
         if not args.no_cpu_baseline and world == 1:
-            cb = cpu_baseline()
+            cb = cpu_baseline_prove() if args.workload == "prove" else cpu_baseline_msm()
             line["cpu_baseline"] = cb
-            line["gpu_vs_cpu"] = round(value / cb["value"], 1)
+            ratio = cb["value"] / line["value"] if args.workload == "prove" else line["value"] / cb["value"]
+            line["gpu_vs_cpu"] = round(ratio, 1)
         print(json.dumps(line), flush=True)
-
     h2g.shutdown()
     if world > 1:
         dist.destroy_process_group()
-
-
-def ntt_extras(h2g, torch, dev, stream, reps=5):
-    """Side measurements (not the headline value): device-resident radix-2^m NTT
-    (best_fft) at 2^20 (BASELINE configs[1]) and 2^22, and coeff_to_extended
-    k=22 -> 2^23 (the quotient-domain coset NTT of configs[2..3]).
-    Algorithmic bytes: 64 B/element (read + write once)."""
-    out = {}
-    rng = np.random.default_rng(9)
-    for log_n in (20, 22):
-        n = 1 << log_n
-        a = torch.from_numpy(random_scalars(rng, n).view(np.int64)).to(dev)
-        d = h2g.Domain(2, log_n)
-        w = d.consts[0]
-        h2g.fft_dev(a.data_ptr(), log_n, w, stream)
-        torch.cuda.synchronize()
-        t = h2g.Timer(stream)
-        t.start()
-        for _ in range(reps):
-            h2g.fft_dev(a.data_ptr(), log_n, w, stream)
-        ms = t.stop_ms() / reps
-        d.close()
-        out[f"fft_2^{log_n}_ms"] = round(ms, 4)
-        out[f"fft_2^{log_n}_GBs"] = round(64 * n / (ms * 1e-3) / 1e9, 1)
-        out[f"fft_2^{log_n}_modmul_per_s"] = round((n // 2) * log_n / (ms * 1e-3), 1)
-    k = 22
-    d = h2g.Domain(3, k)
-    a = torch.from_numpy(random_scalars(rng, 1 << k).view(np.int64)).to(dev)
-    o = torch.empty((d.extended_len, 4), dtype=torch.int64, device=dev)
-    h2g.check(h2g.lib().h2g_coeff_to_extended_dev(d.h, h2g.VP(a.data_ptr()), h2g.VP(o.data_ptr()), h2g.VP(stream)))
-    torch.cuda.synchronize()
-    t = h2g.Timer(stream)
-    t.start()
-    for _ in range(reps):
-        h2g.check(h2g.lib().h2g_coeff_to_extended_dev(d.h, h2g.VP(a.data_ptr()), h2g.VP(o.data_ptr()),
-                                                      h2g.VP(stream)))
-    ms = t.stop_ms() / reps
-    d.close()
-    out["coeff_to_extended_k22_ms"] = round(ms, 4)
-    return out
-
-
-def h2g_choose_c(n):
-    # mirror of msm_choose_c (msm.hip) for reporting
-    best, bc = 1e300, 2
-    for c in range(2, 23):
-        W = (255 + c - 1) // c
-        cost = W * (n + 2.8 * (1 << (c - 1)))
-        if cost < best:
-            best, bc = cost, c
-    return bc
 
 
 if __name__ == "__main__":

@@ -1,0 +1,41 @@
+"""Time the device create_proof on the C3 synthetic circuit at the given
+k values; prints per-stage wall times.  usage: python tools/prove_bench.py 20 22"""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "yet-another-halo2-fork_amd")]
+import numpy as np  # noqa: E402
+
+import h2g  # noqa: E402
+import h2g_circuit as hc  # noqa: E402
+
+
+def main():
+    ks = [int(a) for a in sys.argv[1:]] or [20]
+    h2g.init()
+    for k in ks:
+        t0 = time.time()
+        circ, wit = hc.synthetic_c3(k, h2g.DeviceOps)
+        t1 = time.time()
+        params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(0x1234567 + k), dtype=np.uint64))
+        t2 = time.time()
+        pk = h2g.ProvingKey(params, circ)
+        t3 = time.time()
+        print(f"k={k}: witness {t1 - t0:.2f}s  srs {t2 - t1:.2f}s  keygen {t3 - t2:.2f}s", flush=True)
+        times = []
+        for it in range(4):
+            a = time.time()
+            proof = pk.create_proof(wit)
+            times.append(time.time() - a)
+            st = h2g.prover_stages()
+            print(f"  prove {times[-1] * 1e3:.1f} ms, {len(proof)} B: " +
+                  ", ".join(f"{nm} {ms:.1f}" for nm, ms in st), flush=True)
+        print(f"k={k} best {min(times) * 1e3:.1f} ms", flush=True)
+        pk.close()
+        params.close()
+
+
+if __name__ == "__main__":
+    main()

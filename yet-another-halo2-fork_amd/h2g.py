@@ -488,3 +488,16 @@ def prover_stages():
     cnt = I32()
     check(lib().h2g_prover_stages(ms, 64, ctypes.byref(cnt)))
     return [(lib().h2g_prover_stage_name(i).decode(), ms[i]) for i in range(min(cnt.value, 64))]
+
+
+class DeviceOps:
+    """vectorised Montgomery arithmetic on the device (witness generation for
+    h2g_circuit.synthetic_c3 at bench sizes)"""
+
+    @staticmethod
+    def mul(a, b):
+        return fr_op(OP_MUL, a, b)
+
+    @staticmethod
+    def prefix_product(a):
+        return prefix_product(a)
