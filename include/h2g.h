@@ -57,6 +57,12 @@ int h2g_msm(const uint64_t* coeffs, const uint64_t* bases, size_t n, uint64_t ou
 int h2g_msm_coeffs_descriptor(const uint64_t* coeffs, size_t n, uint64_t* handle);
 int h2g_msm_base_descriptor(const uint64_t* bases, size_t n, uint64_t* handle);
 int h2g_msm_descriptor_free(uint64_t handle); /* Drop of a descriptor (zal.rs:47) */
+/* Base descriptors keep fixed-base windows ([2^(c w)] P_i, W x n x 64 B of HBM) so the
+ * MSM runs one shared bucket set; the _dev variants take device-resident bases /
+ * scalars (window_bits 0 = choose). */
+int h2g_msm_base_descriptor_dev(const void* d_bases, size_t n, int window_bits, uint64_t* handle);
+int h2g_msm_with_cached_base_dev(const void* d_scalars, size_t n, uint64_t base, size_t base_offset,
+                                 uint64_t out_affine[8], int* out_is_identity, void* stream);
 /* msm_with_cached_scalars / _base / _inputs (zal.rs:86-102); base_offset selects the
  * prefix/sub-slice &bases[off..off+n] used by commit / commit_lagrange
  * (halo2_backend/src/poly/kzg/commitment.rs:316, 365) */

@@ -250,3 +250,63 @@ def test_poly_ops_vs_oracle(n):
     assert np.array_equal(h2g.batch_invert(a), O.batch_invert(a))
     b[:: 5] = O.fr_from_canonical(np.array([1, 0, 0, 0], dtype=np.uint64))[0]
     assert np.array_equal(h2g.prefix_product(b), O.prefix_product(b))
+
+
+# ---------------------------------------------------------------- fixed-base MSM (resident bases)
+def _skewed(dist, r, n):
+    if dist == "random":
+        return O.random_fr(r, n)
+    if dist == "ones":
+        return O.fr_from_canonical(np.tile(np.array([1, 0, 0, 0], dtype=np.uint64), (n, 1)))
+    if dist == "zeros":
+        return np.zeros((n, 4), dtype=np.uint64)
+    if dist == "rminus1":
+        rm1 = O.fr_from_canonical(np.array([0x43e1f593f0000000, 0x2833e84879b97091, 0xb85045b68181585d,
+                                            0x30644e72e131a029], dtype=np.uint64))
+        return np.tile(rm1, (n, 1))
+    sc = O.random_fr(r, n)   # sparse
+    sc[r.random(n) < 0.9] = 0
+    return sc
+
+
+@pytest.mark.parametrize("window_bits", [0, 3, 8, 13, 20])
+@pytest.mark.parametrize("dist", ["random", "ones", "zeros", "rminus1", "sparse"])
+def test_msm_fixed_base_vs_oracle(window_bits, dist):
+    """Fixed-base windows (h2g_msm_base_descriptor_dev) incl. offsets into the table."""
+    r = rng(window_bits * 7 + len(dist))
+    N = 5000
+    s = O.random_fr(r, 1)[0]
+    bases_dev = _srs(N, s)
+    bases = bases_dev.download((N, 8))
+    h = h2g.base_descriptor_dev(bases_dev.ptr, N, window_bits)
+    try:
+        for off, n in ((0, N), (0, 1024), (1234, 3000), (N - 2, 2), (7, 1)):
+            sc = _skewed(dist, r, n)
+            d_sc = h2g.DevBuf.from_array(sc)
+            got = h2g.msm_with_cached_base_dev(d_sc.ptr, n, h, off)
+            want = O.msm_best(sc, bases[off:off + n], 8)
+            assert np.array_equal(got, want), (dist, window_bits, off, n)
+            d_sc.close()
+        with pytest.raises(h2g.H2GError):
+            h2g.msm_with_cached_base_dev(0, 10, h, N - 5)
+    finally:
+        h2g.descriptor_free(h)
+        bases_dev.close()
+
+
+def test_msm_fixed_base_srs_identity_2_20():
+    """2^20 fixed-base MSM over the SRS: sum c_i [s^i]G == [c(s)]G."""
+    r = rng(20)
+    n = 1 << 20
+    s = O.random_fr(r, 1)[0]
+    bases_dev = _srs(n, s)
+    h = h2g.base_descriptor_dev(bases_dev.ptr, n, 0)
+    sc = O.random_fr(r, n)
+    d_sc = h2g.DevBuf.from_array(sc)
+    got = h2g.msm_with_cached_base_dev(d_sc.ptr, n, h, 0)
+    cs = O.eval_poly(sc, s)
+    want = O.g1_mul(GEN, cs)
+    assert np.array_equal(got, want)
+    h2g.descriptor_free(h)
+    d_sc.close()
+    bases_dev.close()

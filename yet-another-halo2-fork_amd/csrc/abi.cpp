@@ -156,6 +156,41 @@ int msm_host_impl(Device* d, const void* sc, const void* bs, size_t n, int c, ui
   return H2G_OK;
 }
 
+int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, uint64_t* out,
+                        int* is_id, hipStream_t st) {
+  if (n == 0) {
+    std::memset(out, 0, 64);
+    if (is_id) *is_id = 1;
+    return H2G_OK;
+  }
+  MsmPhaseEvents* pe = nullptr;
+  if (g_profile) {
+    MsmPhaseEvents ev;
+    for (auto& e : ev.ev) HIPCHK(hipEventCreate(&e));
+    g_msm_prof.push_back(ev);
+    pe = &g_msm_prof.back();
+  }
+  HIPCHK(msm_run_fixed(reinterpret_cast<const Fr*>(sc), fb, off, n, &d->msm, nullptr, st, pe));
+  if (!d->h_windows) HIPCHK(hipHostMalloc(&d->h_windows, 256 * sizeof(G1xyzz), hipHostMallocDefault));
+  HIPCHK(hipMemcpyAsync(d->h_windows, d->msm.windows, sizeof(G1xyzz), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const G1Affine r = msm_windows_host_finish(reinterpret_cast<const G1xyzz*>(d->h_windows), 1, d->msm.last_c);
+  std::memcpy(out, &r, 64);
+  if (is_id) {
+    uint64_t x = 0;
+    for (int i = 0; i < 8; i++) x |= out[i];
+    *is_id = x == 0;
+  }
+  return H2G_OK;
+}
+
+// MSM against a descriptor's bases [off, off + n): fixed-base tables when present
+int msm_desc_impl(Device* d, const void* sc, const Descriptor& ds, size_t off, size_t n, uint64_t* out, int* is_id,
+                  hipStream_t st) {
+  if (ds.fb.table) return msm_fixed_host_impl(d, sc, ds.fb, off, n, out, is_id, st);
+  return msm_host_impl(d, sc, (const char*)ds.d + off * 64, n, 0, out, is_id, st);
+}
+
 int ntt_dev_impl(Device* d, const Fr* src, uint64_t n_in, Fr* dst, uint64_t out_len, int L, const Fr& omega,
                  int in_dist, const Fr& iz1, const Fr& iz2, int has_scale, const Fr& scale, int out_dist,
                  const Fr& oz1, const Fr& oz2, hipStream_t st) {
@@ -359,6 +394,13 @@ static int make_desc(const uint64_t* data, size_t n, size_t elem_bytes, bool is_
   ds.is_base = is_base;
   HIPCHK(hipMalloc(&ds.d, n * elem_bytes + 64));
   HIPCHK(hipMemcpyAsync(ds.d, data, n * elem_bytes, hipMemcpyHostToDevice, d->stream));
+  if (is_base && n >= 2) {
+    // resident bases: precompute the fixed-base windows; the table's window 0 is the bases
+    HIPCHK(msm_fixed_base_build((const G1Affine*)ds.d, n, 0, &ds.fb, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    (void)hipFree(ds.d);
+    ds.d = ds.fb.table;
+  }
   HIPCHK(hipStreamSynchronize(d->stream));
   *handle = g_next_handle++;
   g_desc[*handle] = ds;
@@ -371,6 +413,31 @@ int h2g_msm_coeffs_descriptor(const uint64_t* coeffs, size_t n, uint64_t* handle
 int h2g_msm_base_descriptor(const uint64_t* bases, size_t n, uint64_t* handle) {
   return make_desc(bases, n, 64, true, handle);
 }
+int h2g_msm_base_descriptor_dev(const void* d_bases, size_t n, int window_bits, uint64_t* handle) {
+  NEED_DEV();
+  if (!handle || !d_bases || n < 2) return fail(H2G_ERR_ARG, "descriptor: bad argument");
+  Descriptor ds;
+  ds.device = g_cur;
+  ds.n = n;
+  ds.is_base = true;
+  HIPCHK(msm_fixed_base_build((const G1Affine*)d_bases, n, window_bits, &ds.fb, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  ds.d = ds.fb.table;
+  *handle = g_next_handle++;
+  g_desc[*handle] = ds;
+  return H2G_OK;
+}
+
+int h2g_msm_with_cached_base_dev(const void* d_scalars, size_t n, uint64_t base, size_t off, uint64_t out[8],
+                                 int* is_id, void* stream) {
+  NEED_DEV();
+  auto it = g_desc.find(base);
+  if (it == g_desc.end() || !it->second.is_base) return fail(H2G_ERR_HANDLE, "unknown base descriptor");
+  if (off + n > it->second.n) return fail(H2G_ERR_ARG, "msm: bases.len() < size");
+  if (n && !d_scalars) return fail(H2G_ERR_ARG, "msm: null scalars");
+  return msm_desc_impl(d, d_scalars, it->second, off, n, out, is_id, pick_stream(d, stream));
+}
+
 int h2g_msm_descriptor_free(uint64_t handle) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   auto it = g_desc.find(handle);
@@ -408,7 +475,7 @@ int h2g_msm_with_cached_base(const uint64_t* coeffs, size_t n, uint64_t base, si
   HIPCHK(d->a.ensure(n * 32 + 32));
   HIPCHK(d->out.ensure(64));
   HIPCHK(hipMemcpyAsync(d->a.p, coeffs, n * 32, hipMemcpyHostToDevice, d->stream));
-  return msm_host_impl(d, d->a.p, (const char*)it->second.d + off * 64, n, 0, out, is_id, d->stream);
+  return msm_desc_impl(d, d->a.p, it->second, off, n, out, is_id, d->stream);
 }
 
 int h2g_msm_with_cached_inputs(uint64_t coeffs, uint64_t base, size_t off, uint64_t out[8], int* is_id) {
@@ -419,8 +486,7 @@ int h2g_msm_with_cached_inputs(uint64_t coeffs, uint64_t base, size_t off, uint6
   if (ib == g_desc.end() || !ib->second.is_base) return fail(H2G_ERR_HANDLE, "unknown base descriptor");
   const size_t n = ic->second.n;
   if (off + n > ib->second.n) return fail(H2G_ERR_ARG, "msm: bases.len() < size");
-  HIPCHK(d->out.ensure(64));
-  return msm_host_impl(d, ic->second.d, (const char*)ib->second.d + off * 64, n, 0, out, is_id, d->stream);
+  return msm_desc_impl(d, ic->second.d, ib->second, off, n, out, is_id, d->stream);
 }
 
 int h2g_msm_dev(const void* sc, const void* bs, size_t n, void* out, void* stream) {

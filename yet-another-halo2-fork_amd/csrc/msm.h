@@ -13,6 +13,7 @@ struct MsmConfig {
 struct MsmWorkspace {
   size_t cap_n = 0;
   int cap_c = 0;
+  int cap_W = 0;
   uint32_t cap_L = 0;
   int last_c = 0, last_W = 0;    // window config of the most recent msm_run
   void* keys_in = nullptr;       // u32 [n*W]
@@ -25,7 +26,7 @@ struct MsmWorkspace {
   void* item_bucket = nullptr;   // u32 [W*NB] big-bucket list
   void* partials = nullptr;      // G1xyzz [2 * chunks] boundary slots
   void* buckets = nullptr;       // G1xyzz [W*NB]
-  void* segs = nullptr;          // G1xyzz [W*SEGS]
+  void* segs = nullptr;          // G1xyzz: reduction levels (2 ping-pong arrays + block sums)
   void* windows = nullptr;       // G1xyzz [W]
   void* result = nullptr;        // counters
   void* total_items = nullptr;   // (unused)
@@ -53,5 +54,21 @@ hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWo
                    const MsmConfig& cfg, G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof = nullptr);
 G1Affine msm_windows_host_finish(const G1xyzz* h_windows, int W, int c);
 void msm_free(MsmWorkspace* ws);
+
+// Fixed-base mode for resident bases (SRS, base descriptors): windows are
+// pre-multiplied, table[w * n + i] = [2^(c w)] bases[i], so all W windows share one
+// set of 2^(c-1) buckets (one reduction instead of W; larger c affordable).
+// W * n * 64 B of HBM per table (e.g. 3.5 GB for n = 2^22, c = 20).
+struct MsmFixedBase {
+  G1Affine* table = nullptr;
+  size_t n = 0;
+  int c = 0, W = 0;
+};
+int msm_choose_c_fixed(size_t n);
+hipError_t msm_fixed_base_build(const G1Affine* d_bases, size_t n, int c, MsmFixedBase* fb, hipStream_t st);
+void msm_fixed_base_free(MsmFixedBase* fb);
+// sum_{i < n} scalars[i] * bases[off + i]; leaves ws->windows[0] (ws->last_W = 1)
+hipError_t msm_run_fixed(const Fr* d_scalars, const MsmFixedBase& fb, size_t off, size_t n, MsmWorkspace* ws,
+                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof = nullptr);
 
 }  // namespace h2g

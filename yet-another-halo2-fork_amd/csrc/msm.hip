@@ -32,7 +32,6 @@
 
 namespace h2g {
 
-static constexpr int MSM_SEG = 64;  // buckets per reduction segment
 static constexpr int MSM_THREADS = 256;
 static constexpr uint32_t MSM_SMALL = 32;  // fixup: max chunk pieces summed by one thread
 
@@ -65,8 +64,11 @@ __device__ __forceinline__ G1Affine ld_aff(const G1Affine* p) {
 }
 
 // 1. signed digits ----------------------------------------------------------
+// Generic mode: key = window * NB + |d| - 1, value = point index.  Fixed-base mode
+// (bases pre-multiplied per window, table[w * stride + i] = [2^(c w)] P_i): every
+// window shares one set of NB buckets, key = |d| - 1, value = w * stride + i.
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_digits_kernel(const Fr* __restrict__ scalars, size_t n, int c, int W, uint32_t NB,
+msm_digits_kernel(const Fr* __restrict__ scalars, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride,
                   uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -78,7 +80,7 @@ msm_digits_kernel(const Fr* __restrict__ scalars, size_t n, int c, int W, uint32
   Fr v = to_canonical(s);
   const uint32_t mask = (1u << c) - 1;
   const uint32_t half = 1u << (c - 1);
-  const uint32_t sentinel = (uint32_t)W * NB;
+  const uint32_t sentinel = fixed ? NB : (uint32_t)W * NB;
   uint32_t carry = 0;
   for (int w = 0; w < W; w++) {
     uint32_t d = (v.l[0] & mask) + carry;
@@ -86,15 +88,16 @@ msm_digits_kernel(const Fr* __restrict__ scalars, size_t n, int c, int W, uint32
 #pragma unroll
     for (int k = 0; k < 7; k++) v.l[k] = (v.l[k] >> c) | (v.l[k + 1] << (32 - c));
     v.l[7] >>= c;
-    uint32_t key, val = (uint32_t)i;
+    const uint32_t koff = fixed ? 0u : (uint32_t)w * NB;
+    uint32_t key, val = fixed ? (uint32_t)((size_t)w * stride + i) : (uint32_t)i;
     if (d > half) {  // negative digit d - 2^c (d == 2^c gives digit 0, carry 1)
       const uint32_t mag = (1u << c) - d;
       carry = 1;
-      key = mag ? (uint32_t)w * NB + mag - 1 : sentinel;
+      key = mag ? koff + mag - 1 : sentinel;
       val |= 0x80000000u;
     } else {
       carry = 0;
-      key = d ? (uint32_t)w * NB + d - 1 : sentinel;
+      key = d ? koff + d - 1 : sentinel;
     }
     keys[(size_t)w * n + i] = key;
     vals[(size_t)w * n + i] = val;
@@ -209,33 +212,58 @@ msm_big_bucket_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict
   }
 }
 
-// 6. segment running sums: seg result = sum_{j in seg} (j+1) B_j ------------------
+// 6. bucket reduction: F = sum_j (j+1) B_j per window, shallow ---------------------
+// A serial chain of XYZZ additions costs ~12 us on the GPU at low occupancy, so the
+// reduction minimises dependent depth, not work:
+//   rgroup : groups of RG buckets: S_g = sum_t (t+1) B_{RG g+t}, R_g = sum_t B_{RG g+t}
+//   rscale : V_g = S_g + [RG g] R_g   (F = sum_g V_g), block sums of V
+//   rfinal : sum of the block sums
+// depth ~ 2 RG + (log2(RG m) dbl + adds) + 2 x 8 tree steps.
+static constexpr int RG = 8;
+
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_segment_kernel(const G1xyzz* __restrict__ buckets, uint32_t NB, int W, G1xyzz* __restrict__ segs) {
-  const uint32_t nseg = NB / MSM_SEG > 0 ? NB / MSM_SEG : 1;
-  const uint32_t seglen = NB / nseg;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (uint32_t)W * nseg) return;
-  const uint32_t w = t / nseg, sg = t % nseg;
-  const G1xyzz* B = buckets + (size_t)w * NB;
-  const uint32_t lo = sg * seglen;
-  G1xyzz R = G1xyzz::identity(), S = G1xyzz::identity();
-  for (int j = (int)(lo + seglen) - 1; j >= (int)lo; j--) {
-    R = xyzz_add(R, B[j]);
-    S = xyzz_add(S, R);
+msm_rgroup_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, G1xyzz* __restrict__ S,
+                  G1xyzz* __restrict__ R) {
+  const uint32_t w = blockIdx.y;
+  const uint32_t g = blockIdx.x * MSM_THREADS + threadIdx.x;
+  if (g >= m1) return;
+  const G1xyzz* b = B + (size_t)w * NB;
+  G1xyzz racc = G1xyzz::identity(), sacc = G1xyzz::identity();
+  for (int t = RG - 1; t >= 0; t--) {
+    const uint32_t j = g * RG + t;
+    if (j < NB) racc = xyzz_add(racc, b[j]);
+    sacc = xyzz_add(sacc, racc);
   }
-  // S = sum (j - lo + 1) B_j ; add lo * R
-  if (lo) S = xyzz_add(S, xyzz_mul_u32(R, lo));
-  segs[t] = S;
+  S[(size_t)w * m1 + g] = sacc;
+  R[(size_t)w * m1 + g] = racc;
 }
 
-// 7. per-window reduction ------------------------------------------------------------
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_window_kernel(const G1xyzz* __restrict__ segs, uint32_t nseg, G1xyzz* __restrict__ windows) {
+msm_rscale_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R, uint32_t m1,
+                  G1xyzz* __restrict__ part, uint32_t nblk) {
+  __shared__ G1xyzz sh[MSM_THREADS];
+  const uint32_t w = blockIdx.y;
+  const uint32_t g = blockIdx.x * MSM_THREADS + threadIdx.x;
+  G1xyzz v = G1xyzz::identity();
+  if (g < m1) {
+    v = S[(size_t)w * m1 + g];
+    if (g) v = xyzz_add(v, xyzz_mul_u32(R[(size_t)w * m1 + g], g * RG));
+  }
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[(size_t)w * nblk + blockIdx.x] = sh[0];
+}
+
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_rfinal_kernel(const G1xyzz* __restrict__ part, uint32_t nblk, G1xyzz* __restrict__ windows) {
   __shared__ G1xyzz sh[MSM_THREADS];
   const uint32_t w = blockIdx.x;
   G1xyzz acc = G1xyzz::identity();
-  for (uint32_t s = threadIdx.x; s < nseg; s += blockDim.x) acc = xyzz_add(acc, segs[(size_t)w * nseg + s]);
+  for (uint32_t i = threadIdx.x; i < nblk; i += MSM_THREADS) acc = xyzz_add(acc, part[(size_t)w * nblk + i]);
   sh[threadIdx.x] = acc;
   __syncthreads();
   for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
@@ -243,6 +271,21 @@ msm_window_kernel(const G1xyzz* __restrict__ segs, uint32_t nseg, G1xyzz* __rest
     __syncthreads();
   }
   if (threadIdx.x == 0) windows[w] = sh[0];
+}
+
+// fixed-base tables: table[w * stride + i] = [2^(c w)] bases[i] --------------------
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_precompute_kernel(const G1Affine* __restrict__ bases, size_t n, int c, int W, size_t stride,
+                      G1Affine* __restrict__ table) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const G1Affine p = bases[i];
+  table[i] = p;
+  G1xyzz x = G1xyzz::from_affine(p);
+  for (int w = 1; w < W; w++) {
+    for (int d = 0; d < c; d++) x = xyzz_dbl(x);
+    table[(size_t)w * stride + i] = xyzz_to_affine(x);
+  }
 }
 
 // 8. final Horner over windows -------------------------------------------------------
@@ -299,20 +342,22 @@ uint32_t msm_chunk_len(size_t total) {
   return (uint32_t)L;
 }
 
-hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWorkspace* ws,
-                   const MsmConfig& cfg, G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof) {
+static hipError_t msm_pipeline(const Fr* d_scalars, const G1Affine* d_bases, size_t n, int c, int W, int fixed,
+                               size_t stride, MsmWorkspace* ws, uint32_t item_len, G1Affine* d_out, hipStream_t st,
+                               MsmPhaseEvents* prof) {
 #define H2G_PHASE(i) \
   if (prof) H2G_TRY(hipEventRecord(prof->ev[i], st))
-  const int c = cfg.c > 0 ? cfg.c : msm_choose_c(n);
-  const int W = msm_windows_for(c);
   const uint32_t NB = 1u << (c - 1);
-  const uint32_t nbt = (uint32_t)W * NB;
+  const int WB = fixed ? 1 : W;  // bucket sets
+  const uint32_t nbt = (uint32_t)WB * NB;
   const size_t total = n * (size_t)W;
-  const uint32_t L = cfg.item_len > 0 ? (uint32_t)cfg.item_len : msm_chunk_len(total);
+  const uint32_t L = item_len > 0 ? item_len : msm_chunk_len(total);
   const size_t nchunks = (total + L - 1) / L;
-  const uint32_t nseg = NB / MSM_SEG > 0 ? NB / MSM_SEG : 1;
+  const uint32_t m1 = (NB + RG - 1) / RG;
+  const uint32_t nblk = (m1 + MSM_THREADS - 1) / MSM_THREADS;
+  const int cfg_key = c * 2 + fixed;
 
-  if (ws->cap_n < n || ws->cap_c != c || ws->cap_L != L) {
+  if (ws->cap_n < n || ws->cap_c != cfg_key || ws->cap_L != L || ws->cap_W != W) {
     H2G_TRY(grow(&ws->keys_in, total * 4));
     H2G_TRY(grow(&ws->keys_out, total * 4));
     H2G_TRY(grow(&ws->vals_in, total * 4));
@@ -322,15 +367,16 @@ hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWo
     H2G_TRY(grow(&ws->item_bucket, (size_t)nbt * 4));         // big-bucket list
     H2G_TRY(grow(&ws->partials, 2 * nchunks * sizeof(G1xyzz)));  // boundary slots
     H2G_TRY(grow(&ws->buckets, (size_t)nbt * sizeof(G1xyzz)));
-    H2G_TRY(grow(&ws->segs, (size_t)W * nseg * sizeof(G1xyzz)));
+    H2G_TRY(grow(&ws->segs, ((size_t)2 * m1 + nblk) * WB * sizeof(G1xyzz)));
     H2G_TRY(grow(&ws->windows, (size_t)W * sizeof(G1xyzz)));
     H2G_TRY(grow(&ws->result, 16));  // [0] big-bucket count, [1] valid count
     ws->cap_n = n;
-    ws->cap_c = c;
+    ws->cap_c = cfg_key;
     ws->cap_L = L;
+    ws->cap_W = W;
   }
   ws->last_c = c;
-  ws->last_W = W;
+  ws->last_W = WB;
   uint32_t* keys_in = (uint32_t*)ws->keys_in;
   uint32_t* keys_out = (uint32_t*)ws->keys_out;
   uint32_t* vals_in = (uint32_t*)ws->vals_in;
@@ -343,6 +389,9 @@ hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWo
   uint32_t* big_list = (uint32_t*)ws->item_bucket;
   G1xyzz* buckets = (G1xyzz*)ws->buckets;
   G1xyzz* bnd = (G1xyzz*)ws->partials;
+  G1xyzz* rS = (G1xyzz*)ws->segs;
+  G1xyzz* rR = rS + (size_t)WB * m1;
+  G1xyzz* rP = rR + (size_t)WB * m1;
 
   int key_bits = 1;
   while ((1ull << key_bits) <= (uint64_t)nbt) key_bits++;
@@ -358,7 +407,7 @@ hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWo
   const int T = MSM_THREADS;
   H2G_PHASE(0);
   hipLaunchKernelGGL(msm_digits_kernel, dim3((unsigned)((n + T - 1) / T)), dim3(T), 0, st, d_scalars, n, c, W, NB,
-                     keys_in, vals_in);
+                     fixed, stride, keys_in, vals_in);
   H2G_TRY(hipGetLastError());
   H2G_PHASE(1);
   H2G_TRY(hipcub::DeviceRadixSort::SortPairs(ws->sort_tmp, sort_bytes, keys_in, keys_out, vals_in, vals_out,
@@ -379,16 +428,66 @@ hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWo
   hipLaunchKernelGGL(msm_big_bucket_kernel, dim3(256), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend, L,
                      (const uint32_t*)big_list, (const uint32_t*)big_count, buckets);
   H2G_PHASE(5);
-  hipLaunchKernelGGL(msm_segment_kernel, dim3(((uint32_t)W * nseg + T - 1) / T), dim3(T), 0, st,
-                     (const G1xyzz*)buckets, NB, W, (G1xyzz*)ws->segs);
-  hipLaunchKernelGGL(msm_window_kernel, dim3(W), dim3(MSM_THREADS), 0, st, (const G1xyzz*)ws->segs, nseg,
+  hipLaunchKernelGGL(msm_rgroup_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1, rS,
+                     rR);
+  hipLaunchKernelGGL(msm_rscale_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
+                     (const G1xyzz*)rR, m1, rP, nblk);
+  hipLaunchKernelGGL(msm_rfinal_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rP, nblk,
                      (G1xyzz*)ws->windows);
   if (d_out)
-    hipLaunchKernelGGL(msm_final_kernel, dim3(1), dim3(64), 0, st, (const G1xyzz*)ws->windows, W, c, d_out);
+    hipLaunchKernelGGL(msm_final_kernel, dim3(1), dim3(64), 0, st, (const G1xyzz*)ws->windows, WB, c, d_out);
   H2G_TRY(hipGetLastError());
   H2G_PHASE(6);
 #undef H2G_PHASE
   return hipSuccess;
+}
+
+hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWorkspace* ws,
+                   const MsmConfig& cfg, G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof) {
+  const int c = cfg.c > 0 ? cfg.c : msm_choose_c(n);
+  return msm_pipeline(d_scalars, d_bases, n, c, msm_windows_for(c), 0, 0, ws, (uint32_t)cfg.item_len, d_out, st,
+                      prof);
+}
+
+int msm_choose_c_fixed(size_t n) {
+  // one shared bucket set: cost ~ n W (sort + accumulate) + a few adds per bucket
+  if (n < 4) return 2;
+  int best_c = 2;
+  double best = 1e300;
+  for (int c = 2; c <= 22; c++) {
+    const double cost = (double)msm_windows_for(c) * (double)n + 3.0 * (double)(1ull << (c - 1));
+    if (cost < best * 0.98) {  // prefer smaller tables unless clearly cheaper
+      best = cost;
+      best_c = c;
+    }
+  }
+  return best_c;
+}
+
+hipError_t msm_fixed_base_build(const G1Affine* d_bases, size_t n, int c, MsmFixedBase* fb, hipStream_t st) {
+  if (c <= 0) c = msm_choose_c_fixed(n);
+  const int W = msm_windows_for(c);
+  if ((size_t)W * n >= 0x80000000ull) return hipErrorInvalidValue;  // 31-bit table index
+  msm_fixed_base_free(fb);
+  H2G_TRY(hipMalloc(&fb->table, (size_t)W * n * sizeof(G1Affine)));
+  fb->n = n;
+  fb->c = c;
+  fb->W = W;
+  hipLaunchKernelGGL(msm_precompute_kernel, dim3((unsigned)((n + MSM_THREADS - 1) / MSM_THREADS)), dim3(MSM_THREADS),
+                     0, st, d_bases, n, c, W, n, fb->table);
+  return hipGetLastError();
+}
+
+void msm_fixed_base_free(MsmFixedBase* fb) {
+  if (fb->table) (void)hipFree(fb->table);
+  fb->table = nullptr;
+  fb->n = 0;
+}
+
+hipError_t msm_run_fixed(const Fr* d_scalars, const MsmFixedBase& fb, size_t off, size_t n, MsmWorkspace* ws,
+                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof) {
+  if (off + n > fb.n) return hipErrorInvalidValue;
+  return msm_pipeline(d_scalars, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, d_out, st, prof);
 }
 
 }  // namespace h2g

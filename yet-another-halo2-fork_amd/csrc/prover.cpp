@@ -54,8 +54,20 @@ struct Params {
   size_t n = 0;
   G1Affine* g = nullptr;
   G1Affine* gl = nullptr;
+  MsmFixedBase fg, fgl;  // fixed-base MSM windows of g and g_lagrange (commit / commit_lagrange)
   Pool pool;
+  ~Params() {
+    msm_fixed_base_free(&fg);
+    msm_fixed_base_free(&fgl);
+  }
 };
+
+int params_finish(Params& p, hipStream_t st) {
+  HIPCHK(msm_fixed_base_build(p.g, p.n, 0, &p.fg, st));
+  HIPCHK(msm_fixed_base_build(p.gl, p.n, 0, &p.fgl, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return H2G_OK;
+}
 
 struct Query {
   int type, index, rot;
@@ -171,9 +183,11 @@ int build_pow_table(Pool& pool, const Fr& w, int L, PowTable* t, hipStream_t st)
   return H2G_OK;
 }
 
-int commit(Device* d, const Fr* scalars, size_t n, const G1Affine* bases, G1Affine* out, hipStream_t st) {
+// ParamsKZG::commit / commit_lagrange (kzg/commitment.rs:305-317,354-366): MSM against a
+// prefix of the resident SRS, fixed-base windows
+int commit(Device* d, const Fr* scalars, size_t n, const MsmFixedBase& bases, G1Affine* out, hipStream_t st) {
   int is_id = 0;
-  return msm_host_impl(d, scalars, bases, n, 0, reinterpret_cast<uint64_t*>(out), &is_id, st);
+  return msm_fixed_host_impl(d, scalars, bases, 0, n, reinterpret_cast<uint64_t*>(out), &is_id, st);
 }
 
 // Debug aid: H2G_DUMP=<dir> writes named intermediates (raw Fr arrays) of create_proof.
@@ -636,7 +650,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   clk.mark("upload+instances");
   for (int c = 0; c < pk.A; c++) {
     G1Affine cm;
-    RCCHK(commit(d, pk.adv[c], n, prm.gl, &cm, st));
+    RCCHK(commit(d, pk.adv[c], n, prm.fgl, &cm, st));
     RCCHK(write_point(cm));
   }
   clk.mark("advice commit");
@@ -695,7 +709,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       if (s == 0) dump("sigma0", pk.sigma_lag[0], n, st);
       if (s == 0) dump("v0", col_vals(0), n, st);
       G1Affine cm;
-      RCCHK(commit(d, pk.z[s], n, prm.gl, &cm, st));
+      RCCHK(commit(d, pk.z[s], n, prm.fgl, &cm, st));
       RCCHK(lagrange_to_coeff(d, D, pk.z[s], pk.z[s], st));
       RCCHK(coeff_to_extended(d, D, pk.z[s], pk.z_coset[s], st));
       RCCHK(write_point(cm));
@@ -723,7 +737,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     HIPCHK(hipStreamSynchronize(st));  // seeds/off are host temporaries
     (void)rng.random_fr();             // random_blind
     G1Affine cm;
-    RCCHK(commit(d, pk.random_poly, n, prm.g, &cm, st));
+    RCCHK(commit(d, pk.random_poly, n, prm.fg, &cm, st));
     RCCHK(write_point(cm));
   }
   clk.mark("vanishing commit");
@@ -771,7 +785,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   for (int p = 0; p < npieces; p++) (void)rng.random_fr();  // h blinds
   for (int p = 0; p < npieces; p++) {
     G1Affine cm;
-    RCCHK(commit(d, pk.h_coeff + (size_t)p * n, n, prm.g, &cm, st));
+    RCCHK(commit(d, pk.h_coeff + (size_t)p * n, n, prm.fg, &cm, st));
     RCCHK(write_point(cm));
   }
   clk.mark("h commit");
@@ -959,7 +973,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   }
   {
     G1Affine cm;
-    RCCHK(commit(d, pk.hx, n, prm.g, &cm, st));
+    RCCHK(commit(d, pk.hx, n, prm.fg, &cm, st));
     RCCHK(write_point(cm));
   }
   clk.mark("shplonk h");
@@ -1014,7 +1028,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   HIPCHK(poly_binop(POLY_SCALE, pk.q1, nullptr, inv(z0), pk.q1, n - 1, st));
   {
     G1Affine cm;
-    RCCHK(commit(d, pk.q1, n - 1, prm.g, &cm, st));
+    RCCHK(commit(d, pk.q1, n - 1, prm.fg, &cm, st));
     RCCHK(write_point(cm));
   }
   clk.mark("shplonk final");
@@ -1042,6 +1056,7 @@ int h2g_params_create(uint32_t k, const uint64_t* g, const uint64_t* g_lagrange,
   PALLOC(p->pool, p->gl, p->n);
   HIPCHK(hipMemcpy(p->g, g, p->n * sizeof(G1Affine), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(p->gl, g_lagrange, p->n * sizeof(G1Affine), hipMemcpyHostToDevice));
+  RCCHK(params_finish(*p, d->stream));
   *handle = g_next_handle++;
   g_params[*handle] = std::move(p);
   return H2G_OK;
@@ -1072,6 +1087,7 @@ int h2g_params_setup(uint32_t k, const uint64_t s_limbs[4], uint64_t* handle) {
   HIPCHK(srs_lagrange_scalars(sc, n, s, mult, om, scr, st));
   HIPCHK(g1_generator_mul(sc, n, p->gl, st));
   HIPCHK(hipStreamSynchronize(st));
+  RCCHK(params_finish(*p, st));
   *handle = g_next_handle++;
   g_params[*handle] = std::move(p);
   return H2G_OK;

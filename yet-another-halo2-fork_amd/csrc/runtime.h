@@ -78,9 +78,10 @@ struct Domain {
 
 struct Descriptor {
   int device;
-  void* d = nullptr;
+  void* d = nullptr;  // scalars, or bases (= window 0 of fb.table when present)
   size_t n = 0;
   bool is_base = false;
+  MsmFixedBase fb;    // fixed-base windows of resident bases (owned: d aliases fb.table)
 };
 
 struct Device {
@@ -117,6 +118,10 @@ Domain* get_dom(uint64_t h);
 int get_tables(Device* d, const Fr& omega, int L, hipStream_t st, NttTables* out);
 int msm_dev_impl(Device* d, const void* sc, const void* bs, size_t n, int c, void* out, hipStream_t st);
 int msm_host_impl(Device* d, const void* sc, const void* bs, size_t n, int c, uint64_t* out, int* is_id,
+                  hipStream_t st);
+int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, uint64_t* out,
+                        int* is_id, hipStream_t st);
+int msm_desc_impl(Device* d, const void* sc, const Descriptor& ds, size_t off, size_t n, uint64_t* out, int* is_id,
                   hipStream_t st);
 int ntt_dev_impl(Device* d, const Fr* src, uint64_t n_in, Fr* dst, uint64_t out_len, int L, const Fr& omega,
                  int in_dist, const Fr& iz1, const Fr& iz2, int has_scale, const Fr& scale, int out_dist,

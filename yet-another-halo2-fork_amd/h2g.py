@@ -37,6 +37,8 @@ _SIGS = {
     "h2g_msm_coeffs_descriptor": ([U64P, SZ, ctypes.POINTER(U64)], I32),
     "h2g_msm_base_descriptor": ([U64P, SZ, ctypes.POINTER(U64)], I32),
     "h2g_msm_descriptor_free": ([U64], I32),
+    "h2g_msm_base_descriptor_dev": ([VP, SZ, I32, ctypes.POINTER(U64)], I32),
+    "h2g_msm_with_cached_base_dev": ([VP, SZ, U64, SZ, U64P, ctypes.POINTER(I32), VP], I32),
     "h2g_msm_with_cached_scalars": ([U64, U64P, SZ, U64P, ctypes.POINTER(I32)], I32),
     "h2g_msm_with_cached_base": ([U64P, SZ, U64, SZ, U64P, ctypes.POINTER(I32)], I32),
     "h2g_msm_with_cached_inputs": ([U64, U64, SZ, U64P, ctypes.POINTER(I32)], I32),
@@ -173,6 +175,21 @@ def coeffs_descriptor(scalars):
     sc = np.ascontiguousarray(scalars, dtype=np.uint64)
     check(lib().h2g_msm_coeffs_descriptor(p64(sc), sc.shape[0], ctypes.byref(h)))
     return h.value
+
+
+def base_descriptor_dev(d_bases, n, window_bits=0):
+    """fixed-base descriptor over device-resident bases (precomputed windows)"""
+    h = U64()
+    check(lib().h2g_msm_base_descriptor_dev(VP(d_bases), n, window_bits, ctypes.byref(h)))
+    return h.value
+
+
+def msm_with_cached_base_dev(d_scalars, n, base_handle, offset=0, stream=None):
+    out = np.zeros(8, dtype=np.uint64)
+    is_id = I32()
+    check(lib().h2g_msm_with_cached_base_dev(VP(d_scalars), n, base_handle, offset, p64(out), ctypes.byref(is_id),
+                                             VP(stream) if stream else None))
+    return out
 
 
 def descriptor_free(h):
