@@ -184,6 +184,75 @@ int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_
   return H2G_OK;
 }
 
+int msm_fixed_launch(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, hipStream_t producer,
+                     MsmTicket* t) {
+  if (!d->h_ring) {
+    HIPCHK(hipHostMalloc(&d->h_ring, MSM_RING * sizeof(G1xyzz), hipHostMallocDefault));
+    for (int i = 0; i < MSM_SLOTS; i++) HIPCHK(hipStreamCreateWithFlags(&d->mstream[i], hipStreamNonBlocking));
+    for (int i = 0; i < MSM_RING; i++) HIPCHK(hipEventCreateWithFlags(&d->ring_ev[i], hipEventDisableTiming));
+  }
+  int ring = -1;
+  for (int k = 0; k < MSM_RING; k++) {
+    const int r = (d->next_ring + k) % MSM_RING;
+    if (!d->ring_busy[r]) {
+      ring = r;
+      break;
+    }
+  }
+  if (ring < 0) return fail(H2G_ERR_STATE, "msm: too many outstanding asynchronous MSMs");
+  d->next_ring = (ring + 1) % MSM_RING;
+  const int slot = d->next_slot;
+  d->next_slot = (slot + 1) % MSM_SLOTS;
+  hipStream_t ms = d->mstream[slot];
+  // order after the producer's work (the scalars)
+  HIPCHK(hipEventRecord(d->ring_ev[ring], producer));
+  HIPCHK(hipStreamWaitEvent(ms, d->ring_ev[ring], 0));
+  MsmPhaseEvents* pe = nullptr;
+  if (g_profile && n > 0) {
+    MsmPhaseEvents ev;
+    for (auto& e : ev.ev) HIPCHK(hipEventCreate(&e));
+    g_msm_prof.push_back(ev);
+    pe = &g_msm_prof.back();
+  }
+  G1xyzz* host = reinterpret_cast<G1xyzz*>(d->h_ring) + ring;
+  if (n == 0) {
+    std::memset(host, 0, sizeof(G1xyzz));  // identity (ZZ = 0)
+  } else {
+    HIPCHK(msm_run_fixed(reinterpret_cast<const Fr*>(sc), fb, off, n, &d->mws[slot], nullptr, ms, pe));
+    HIPCHK(hipMemcpyAsync(host, d->mws[slot].windows, sizeof(G1xyzz), hipMemcpyDeviceToHost, ms));
+  }
+  HIPCHK(hipEventRecord(d->ring_ev[ring], ms));
+  d->ring_busy[ring] = true;
+  t->slot = slot;
+  t->ring = ring;
+  t->c = fb.c;
+  t->done = d->ring_ev[ring];
+  return H2G_OK;
+}
+
+int msm_collect(Device* d, MsmTicket* t, uint64_t* out) {
+  if (t->ring < 0) return fail(H2G_ERR_STATE, "msm: collect without launch");
+  HIPCHK(hipEventSynchronize(t->done));
+  const G1xyzz* host = reinterpret_cast<const G1xyzz*>(d->h_ring) + t->ring;
+  const G1Affine r = msm_windows_host_finish(host, 1, t->c);
+  std::memcpy(out, &r, 64);
+  d->ring_busy[t->ring] = false;
+  t->ring = -1;
+  return H2G_OK;
+}
+
+int msm_fence(Device* d, hipStream_t consumer) {
+  if (!d->h_ring) return H2G_OK;
+  for (int i = 0; i < MSM_SLOTS; i++) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(e, d->mstream[i]));
+    HIPCHK(hipStreamWaitEvent(consumer, e, 0));
+    HIPCHK(hipEventDestroy(e));
+  }
+  return H2G_OK;
+}
+
 // MSM against a descriptor's bases [off, off + n): fixed-base tables when present
 int msm_desc_impl(Device* d, const void* sc, const Descriptor& ds, size_t off, size_t n, uint64_t* out, int* is_id,
                   hipStream_t st) {
@@ -345,6 +414,16 @@ int h2g_shutdown(void) {
     (void)hipSetDevice(dev->id);
     (void)hipStreamSynchronize(dev->stream);
     msm_free(&dev->msm);
+    for (int i = 0; i < MSM_SLOTS; i++) {
+      msm_free(&dev->mws[i]);
+      if (dev->mstream[i]) {
+        (void)hipStreamSynchronize(dev->mstream[i]);
+        (void)hipStreamDestroy(dev->mstream[i]);
+      }
+    }
+    for (int i = 0; i < MSM_RING; i++)
+      if (dev->ring_ev[i]) (void)hipEventDestroy(dev->ring_ev[i]);
+    if (dev->h_ring) (void)hipHostFree(dev->h_ring);
     dev->a.release();
     dev->b.release();
     dev->c.release();

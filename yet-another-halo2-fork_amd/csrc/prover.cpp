@@ -102,7 +102,7 @@ struct ProvingKey {
   const Fr** d_perm_v = nullptr;
   const Fr** d_sigma = nullptr;
   // per-proof workspace (device), reused across proofs
-  std::vector<Fr*> adv, adv_coset, inst_val, inst_poly, inst_coset, z, z_coset;
+  std::vector<Fr*> adv, adv_coset, inst_val, inst_poly, inst_coset, z, z_lag, z_coset;
   Fr *mod = nullptr, *pre = nullptr, *scr = nullptr, *random_poly = nullptr, *h_ext = nullptr, *h_coeff = nullptr;
   Fr *h_poly = nullptr, *nx = nullptr, *q1 = nullptr, *q2 = nullptr, *hx = nullptr, *lx = nullptr;
   Fr *small = nullptr, *last_z = nullptr, *evals = nullptr, *eval_scr = nullptr;
@@ -183,13 +183,6 @@ int build_pow_table(Pool& pool, const Fr& w, int L, PowTable* t, hipStream_t st)
   return H2G_OK;
 }
 
-// ParamsKZG::commit / commit_lagrange (kzg/commitment.rs:305-317,354-366): MSM against a
-// prefix of the resident SRS, fixed-base windows
-int commit(Device* d, const Fr* scalars, size_t n, const MsmFixedBase& bases, G1Affine* out, hipStream_t st) {
-  int is_id = 0;
-  return msm_fixed_host_impl(d, scalars, bases, 0, n, reinterpret_cast<uint64_t*>(out), &is_id, st);
-}
-
 // Debug aid: H2G_DUMP=<dir> writes named intermediates (raw Fr arrays) of create_proof.
 void dump(const char* name, const Fr* dptr, size_t count, hipStream_t st, bool host = false) {
   static const char* dir = std::getenv("H2G_DUMP");
@@ -205,6 +198,21 @@ void dump(const char* name, const Fr* dptr, size_t count, hipStream_t st, bool h
     std::fwrite(h.data(), sizeof(Fr), count, f);
     std::fclose(f);
   }
+}
+
+// ParamsKZG::commit / commit_lagrange (kzg/commitment.rs:305-317,354-366): MSM against a
+// prefix of the resident SRS (fixed-base windows).  Launched asynchronously after the
+// work queued on `st`; the affine result is collected when it enters the transcript.
+int commit_launch(Device* d, const Fr* scalars, size_t n, const MsmFixedBase& bases, hipStream_t st, MsmTicket* t) {
+  return msm_fixed_launch(d, scalars, bases, 0, n, st, t);
+}
+int commit_collect(Device* d, MsmTicket* t, G1Affine* out) {
+  return msm_collect(d, t, reinterpret_cast<uint64_t*>(out));
+}
+int commit(Device* d, const Fr* scalars, size_t n, const MsmFixedBase& bases, G1Affine* out, hipStream_t st) {
+  MsmTicket t;
+  RCCHK(commit_launch(d, scalars, n, bases, st, &t));
+  return commit_collect(d, &t, out);
 }
 
 // ------------------------------------------------------------------ circuit analysis
@@ -444,6 +452,7 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk) {
   HIPCHK(vec_alloc(pk.inst_poly, pk.I, n));
   HIPCHK(vec_alloc(pk.inst_coset, pk.I, ext));
   HIPCHK(vec_alloc(pk.z, pk.nsets, n));
+  HIPCHK(vec_alloc(pk.z_lag, pk.nsets, n));
   HIPCHK(vec_alloc(pk.z_coset, pk.nsets, ext));
 
   // fixed columns
@@ -648,10 +657,14 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       if (!pk.unblinded[c]) (void)rng.random_fr();  // commitment blinds (unused by KZG)
   }
   clk.mark("upload+instances");
-  for (int c = 0; c < pk.A; c++) {
-    G1Affine cm;
-    RCCHK(commit(d, pk.adv[c], n, prm.fgl, &cm, st));
-    RCCHK(write_point(cm));
+  {
+    std::vector<MsmTicket> tk(pk.A);
+    for (int c = 0; c < pk.A; c++) RCCHK(commit_launch(d, pk.adv[c], n, prm.fgl, st, &tk[c]));
+    for (int c = 0; c < pk.A; c++) {
+      G1Affine cm;
+      RCCHK(commit_collect(d, &tk[c], &cm));
+      RCCHK(write_point(cm));
+    }
   }
   clk.mark("advice commit");
   (void)tr.squeeze();  // theta
@@ -659,7 +672,9 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   dump("beta", &beta, 1, st, true);
   dump("gamma", &gamma, 1, st, true);
 
-  // ---- permutation_commit (permutation/prover.rs:50-197)
+  // ---- permutation_commit (permutation/prover.rs:50-197); commitments are written
+  // after the loop (nothing is squeezed in between, so the transcript is unchanged)
+  std::vector<MsmTicket> perm_tk(pk.nsets);
   {
     const Fr one = Fr::one();
     HIPCHK(hipMemcpyAsync(pk.last_z, &one, sizeof(Fr), hipMemcpyHostToDevice, st));
@@ -703,20 +718,21 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       for (auto& v : blind_rows) v = rng.random_fr();
       (void)rng.random_fr();  // blind
       HIPCHK(hipMemcpyAsync(pk.small, blind_rows.data(), bf * sizeof(Fr), hipMemcpyHostToDevice, st));
-      HIPCHK(perm_z_assemble(pk.z[s], n, bf, pk.pre, pk.last_z, pk.small, st));
-      HIPCHK(hipMemcpyAsync(pk.last_z, pk.z[s] + (n - (size_t)(bf + 1)), sizeof(Fr), hipMemcpyDeviceToDevice, st));
-      if (s == 0) dump("z0", pk.z[s], n, st);
+      HIPCHK(perm_z_assemble(pk.z_lag[s], n, bf, pk.pre, pk.last_z, pk.small, st));
+      HIPCHK(hipMemcpyAsync(pk.last_z, pk.z_lag[s] + (n - (size_t)(bf + 1)), sizeof(Fr), hipMemcpyDeviceToDevice,
+                            st));
+      if (s == 0) dump("z0", pk.z_lag[s], n, st);
       if (s == 0) dump("sigma0", pk.sigma_lag[0], n, st);
       if (s == 0) dump("v0", col_vals(0), n, st);
-      G1Affine cm;
-      RCCHK(commit(d, pk.z[s], n, prm.fgl, &cm, st));
-      RCCHK(lagrange_to_coeff(d, D, pk.z[s], pk.z[s], st));
+      RCCHK(commit_launch(d, pk.z_lag[s], n, prm.fgl, st, &perm_tk[s]));
+      RCCHK(lagrange_to_coeff(d, D, pk.z_lag[s], pk.z[s], st));
       RCCHK(coeff_to_extended(d, D, pk.z[s], pk.z_coset[s], st));
-      RCCHK(write_point(cm));
+      HIPCHK(hipStreamSynchronize(st));  // blind_rows (host) is reused by the next set
     }
   }
-  clk.mark("permutation commit");
+  clk.mark("permutation products");
   // ---- vanishing commit (vanishing/prover.rs:40-98)
+  MsmTicket van_tk;
   {
     const uint64_t T = vthreads ? vthreads : 1;
     const uint64_t chunk = n / T, rem = n % T;
@@ -736,17 +752,25 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)off.size(), st));
     HIPCHK(hipStreamSynchronize(st));  // seeds/off are host temporaries
     (void)rng.random_fr();             // random_blind
-    G1Affine cm;
-    RCCHK(commit(d, pk.random_poly, n, prm.fg, &cm, st));
-    RCCHK(write_point(cm));
+    RCCHK(commit_launch(d, pk.random_poly, n, prm.fg, st, &van_tk));
   }
-  clk.mark("vanishing commit");
-  // ---- advice to coefficient form, y, evaluate_h
+  // advice to coefficient form and the extended-domain cosets do not depend on y:
+  // they overlap the permutation / vanishing MSMs
   for (int c = 0; c < pk.A; c++) RCCHK(lagrange_to_coeff(d, D, pk.adv[c], pk.adv[c], st));
-  const Fr y = tr.squeeze();
   for (int c = 0; c < pk.A; c++) RCCHK(coeff_to_extended(d, D, pk.adv[c], pk.adv_coset[c], st));
   for (int c = 0; c < pk.I; c++) RCCHK(coeff_to_extended(d, D, pk.inst_poly[c], pk.inst_coset[c], st));
-  clk.mark("advice/instance cosets");
+  for (int s = 0; s < pk.nsets; s++) {
+    G1Affine cm;
+    RCCHK(commit_collect(d, &perm_tk[s], &cm));
+    RCCHK(write_point(cm));
+  }
+  {
+    G1Affine cm;
+    RCCHK(commit_collect(d, &van_tk, &cm));
+    RCCHK(write_point(cm));
+  }
+  clk.mark("perm+vanishing commits, cosets");
+  const Fr y = tr.squeeze();
   {
     EvalHArgs a;
     a.prog = pk.prog;
@@ -783,10 +807,14 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   RCCHK(extended_to_coeff(d, D, pk.h_ext, pk.h_coeff, st));
   const int npieces = pk.degree - 1;
   for (int p = 0; p < npieces; p++) (void)rng.random_fr();  // h blinds
-  for (int p = 0; p < npieces; p++) {
-    G1Affine cm;
-    RCCHK(commit(d, pk.h_coeff + (size_t)p * n, n, prm.fg, &cm, st));
-    RCCHK(write_point(cm));
+  {
+    std::vector<MsmTicket> tk(npieces);
+    for (int p = 0; p < npieces; p++) RCCHK(commit_launch(d, pk.h_coeff + (size_t)p * n, n, prm.fg, st, &tk[p]));
+    for (int p = 0; p < npieces; p++) {
+      G1Affine cm;
+      RCCHK(commit_collect(d, &tk[p], &cm));
+      RCCHK(write_point(cm));
+    }
   }
   clk.mark("h commit");
   const Fr x = tr.squeeze();

@@ -84,6 +84,18 @@ struct Descriptor {
   MsmFixedBase fb;    // fixed-base windows of resident bases (owned: d aliases fb.table)
 };
 
+// Asynchronous fixed-base MSMs: two workspaces on two streams so that the
+// latency-bound phases (sort tail, fixup, reduction) of one MSM overlap the
+// accumulation of the next.  Results land in a pinned ring (one XYZZ point each).
+static constexpr int MSM_SLOTS = 2;
+static constexpr int MSM_RING = 64;
+struct MsmTicket {
+  int slot = -1;
+  int ring = -1;
+  int c = 0;
+  hipEvent_t done = nullptr;
+};
+
 struct Device {
   int id = 0;
   hipStream_t stream = nullptr;
@@ -91,6 +103,14 @@ struct Device {
   DevBuf a, b, c, work, out;
   std::map<NttKey, NttTables> ntt_tables;
   void* h_windows = nullptr;  // pinned host copy of MSM window sums
+  // async MSM slots
+  MsmWorkspace mws[MSM_SLOTS];
+  hipStream_t mstream[MSM_SLOTS] = {};
+  int next_slot = 0;
+  void* h_ring = nullptr;  // pinned G1xyzz[MSM_RING]
+  hipEvent_t ring_ev[MSM_RING] = {};
+  bool ring_busy[MSM_RING] = {};
+  int next_ring = 0;
 };
 
 extern std::vector<std::unique_ptr<Device>> g_devs;
@@ -121,6 +141,13 @@ int msm_host_impl(Device* d, const void* sc, const void* bs, size_t n, int c, ui
                   hipStream_t st);
 int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, uint64_t* out,
                         int* is_id, hipStream_t st);
+// launch sum_{i<n} sc[i] * bases[off+i] after the work already queued on `producer`
+int msm_fixed_launch(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, hipStream_t producer,
+                     MsmTicket* t);
+// wait for a launched MSM, affine result
+int msm_collect(Device* d, MsmTicket* t, uint64_t* out_affine);
+// make `consumer` wait until every launched MSM has finished reading its scalars
+int msm_fence(Device* d, hipStream_t consumer);
 int msm_desc_impl(Device* d, const void* sc, const Descriptor& ds, size_t off, size_t n, uint64_t* out, int* is_id,
                   hipStream_t st);
 int ntt_dev_impl(Device* d, const Fr* src, uint64_t n_in, Fr* dst, uint64_t out_len, int L, const Fr& omega,
