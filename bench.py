@@ -50,6 +50,16 @@ def random_scalars(rng, n):
     return c
 
 
+def fixed_c(n):
+    # mirror of msm_choose_c_fixed (msm.hip): one shared bucket set
+    best, bc = 1e300, 2
+    for c in range(2, 23):
+        cost = ((255 + c - 1) // c) * n + 3.0 * (1 << (c - 1))
+        if cost < best * 0.98:
+            best, bc = cost, c
+    return bc
+
+
 def h2g_choose_c(n):
     # mirror of msm_choose_c (msm.hip) for reporting
     best, bc = 1e300, 2
@@ -172,8 +182,10 @@ def pmc_child(args):
         bases = h2g.DevBuf(n * 64)
         h2g.srs_setup_dev(random_scalars(rng, 1)[0], n, bases.ptr)
         sc = h2g.DevBuf.from_array(random_scalars(rng, n))
+        base = h2g.base_descriptor_dev(bases.ptr, n, 0)
         for _ in range(2):
-            h2g.msm_dev_host(sc.ptr, bases.ptr, n, 0)
+            h2g.msm_with_cached_base_dev(sc.ptr, n, base, 0)
+        h2g.descriptor_free(base)
     h2g.shutdown()
 
 
@@ -181,7 +193,7 @@ def pmc_child(args):
 def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note):
     acc_ms = phases.get("accumulate", 0.0) / max(calls, 1)
     achieved = (points_per_launch * MSM_BYTES_PER_POINT) / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
-    c = h2g_choose_c(points_per_launch)
+    c = fixed_c(points_per_launch)
     W = (255 + c - 1) // c
     modmul_rate = (points_per_launch * W * MADD_MODMUL) / (acc_ms * 1e-3) if acc_ms > 0 else None
     return {
@@ -201,6 +213,35 @@ def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note
         "valu_modmul_per_s": round(modmul_rate, 1) if modmul_rate else None,
         "window_bits": c,
     }
+
+
+# ----------------------------------------------------------------------------- collectives
+def max_over_ranks(elapsed, dist, world, device):
+    """the job's time is the slowest rank's (contract: max over ranks)"""
+    if world == 1:
+        return elapsed
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_partials(part, dist, world, device):
+    """all_gather of the per-rank MSM partial sums (64-B affine points; RCCL has no
+    EC-add reduction) -> list of numpy uint64[8]"""
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(part, dtype=np.uint64).view(np.int64)).to(device)
+    gathered = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(gathered, t)
+    return [g.cpu().numpy().view(np.uint64) for g in gathered]
+
+
+def combine_partials(parts, add):
+    """sum of the gathered partials with a host EC add (h2g_g1_add_affine)"""
+    total = np.zeros(8, dtype=np.uint64)
+    for p in parts:
+        total = add(total, p)
+    return total
 
 
 # ----------------------------------------------------------------------------- workloads
@@ -240,10 +281,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     h2g.profile_enable(False)
     calls, phases = h2g.profile_msm_collect()
     stages = h2g.prover_stages()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dist, world, dev)
     assert all(p == proofs[0] for p in proofs), "non-deterministic proof bytes"
     line = None
     if rank == 0:
@@ -289,10 +327,12 @@ def run_msm(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     h2g.srs_setup_dev(s, n, bases.data_ptr(), stream)
     scalars = torch.from_numpy(random_scalars(rng, n).view(np.int64)).to(dev)
     torch.cuda.synchronize()
+    # resident bases registered once (MsmAccel base descriptor): fixed-base windows
+    base = h2g.base_descriptor_dev(bases.data_ptr(), n, args.window_bits)
     result = {}
 
     def step():
-        result["p"] = h2g.msm_dev_host(scalars.data_ptr(), bases.data_ptr(), n, 0, stream)
+        result["p"] = h2g.msm_with_cached_base_dev(scalars.data_ptr(), n, base, 0, stream)
 
     for _ in range(args.warmup):
         step()
@@ -305,25 +345,20 @@ def run_msm(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     for _ in range(args.steps):
         step()
         if world > 1:
-            part = torch.from_numpy(result["p"].view(np.int64)).to(dev)
-            gathered = [torch.empty_like(part) for _ in range(world)]
-            dist.all_gather(gathered, part)
+            result["parts"] = gather_partials(result["p"], dist, world, dev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     h2g.profile_enable(False)
     calls, phases = h2g.profile_msm_collect()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        total = np.zeros(8, dtype=np.uint64)
-        for g in gathered:
-            total = h2g.g1_add_affine(total, g.cpu().numpy().view(np.uint64))
+    elapsed = max_over_ranks(elapsed, dist, world, dev)
+    if world > 1:  # the job's MSM result (outside the timed region)
+        result["total"] = combine_partials(result["parts"], h2g.g1_add_affine)
     if rank != 0:
         return None
-    c = h2g_choose_c(n)
+    h2g.descriptor_free(base)
+    c = args.window_bits or fixed_c(n)
     return {
         "metric": METRIC,
         "value": round(world * n * args.steps / elapsed / 1e6, 3),
@@ -337,7 +372,8 @@ def run_msm(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         "vs_baseline": None,
         "dtype": "u32 limbs (BN254 Fr/Fq Montgomery, 256-bit modular integer)",
         "data": "synthetic: uniform random Fr scalars, SRS bases [s^i]G generated on device",
-        "config": {"workload": f"BN254 G1 MSM, 2^{args.log_n} points per GPU (the metric's MSM half)",
+        "config": {"workload": f"BN254 G1 MSM, 2^{args.log_n} resident points per GPU (the metric's MSM half), "
+                               "fixed-base windows via the base descriptor",
                    "points_per_gpu": n, "window_bits": c, "windows": (255 + c - 1) // c,
                    "parallelism": f"point-slab shard x{world} + RCCL all_gather of partials"},
         "roofline": roofline_from_phases(calls, phases, n, traffic, traffic_note),
@@ -353,6 +389,7 @@ def main():
     ap.add_argument("--workload", choices=("prove", "msm"), default="prove")
     ap.add_argument("--k", type=int, default=PROVE_K)
     ap.add_argument("--log-n", type=int, default=24)
+    ap.add_argument("--window-bits", type=int, default=0, help="MSM workload: fixed-base window bits (0: auto)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the PMC traffic passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
