@@ -18,9 +18,11 @@
  *   SHPLONK create_proof               halo2_backend/src/poly/kzg/multiopen/shplonk/prover.rs:121-305
  *   construct_intermediate_sets        halo2_backend/src/poly/kzg/multiopen/shplonk.rs:48-140
  *   Blake2bWrite transcript            halo2_backend/src/transcript.rs:120-130,353-419,500-539
+ *   lookup argument                    halo2_backend/src/plonk/lookup/prover.rs:64-494
+ *   shuffle argument                   halo2_backend/src/plonk/shuffle/prover.rs:36-255
  * Scope: advice (one phase), fixed, instance columns, custom gates (expression
- * graphs with rotations), the permutation argument.  Lookups/shuffles/challenges are
- * not restated yet.
+ * graphs with rotations), the permutation, lookup and shuffle arguments.
+ * Challenges (multi-phase advice) are not restated.
  * Unverifiable-here details (isolated): G1 compressed encoding (x LE, bit 7 of byte 31
  * = y odd); vk.transcript_repr is taken as an input (plonk.rs:189-200 hashes the Rust
  * Debug text of the pinned VK).
@@ -56,6 +58,12 @@ typedef struct {
     const uint64_t *srs_g;          /* n G1Affine */
     const uint64_t *srs_g_lagrange; /* n G1Affine */
     const uint8_t *unblinded;       /* num_advice flags (unblinded_advice_columns) or NULL */
+    uint32_t num_lookups;
+    const uint32_t *lookup_sizes;   /* m_l (input, table) expression pairs per lookup */
+    const int32_t *lookup_roots;    /* per lookup: m_l input roots, then m_l table roots */
+    uint32_t num_shuffles;
+    const uint32_t *shuffle_sizes;
+    const int32_t *shuffle_roots;   /* per shuffle: m input roots, then m shuffle roots */
 } or_spec;
 
 typedef struct { int type, index, rot; } query_t;
@@ -275,6 +283,84 @@ static void assembly_copy(assembly_t *A, int lc, int lr, int rc, int rr) {  /* p
     A->mapping[(uint64_t)rc * A->n + rr] = tmp;
 }
 
+/* ====================================================================== lookup / shuffle helpers */
+/* compress_expressions: fold_e (acc * theta + e(row)) over Lagrange columns (lookup/prover.rs:85-103;
+ * evaluate() evaluation.rs:838-872 with rot_scale 1 over n rows) */
+static void compress_lagrange(const or_spec *s, const int32_t *roots, int m, fe *const *adv, fe *const *fix,
+                              fe *const *ins, uint64_t n, const fe *theta, fe *out, int threads) {
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (uint64_t i = 0; i < n; i++) {
+        fe acc = {{0, 0, 0, 0}};
+        for (int e = 0; e < m; e++) {
+            fe v = eval_node(s, roots[e], adv, fix, ins, i, 1, n);
+            fr_mul(&acc, &acc, theta); fr_add(&acc, &acc, &v);
+        }
+        out[i] = acc;
+    }
+}
+/* the same fold on the extended coset (the lookup/shuffle GraphEvaluators, evaluation.rs:245-300) */
+static fe compress_coset(const or_spec *s, const int32_t *roots, int m, fe *const *adv, fe *const *fix,
+                         fe *const *ins, uint64_t idx, uint64_t rot_scale, uint64_t ext, const fe *theta) {
+    fe acc = {{0, 0, 0, 0}};
+    for (int e = 0; e < m; e++) {
+        fe v = eval_node(s, roots[e], adv, fix, ins, idx, rot_scale, ext);
+        fr_mul(&acc, &acc, theta); fr_add(&acc, &acc, &v);
+    }
+    return acc;
+}
+
+typedef struct { uint64_t c[4]; fe v; } keyed;
+static int keyed_cmp(const void *a_, const void *b_) {
+    const keyed *a = (const keyed *)a_, *b = (const keyed *)b_;
+    for (int i = 3; i >= 0; i--) { if (a->c[i] < b->c[i]) return -1; if (a->c[i] > b->c[i]) return 1; }
+    return 0;
+}
+/* permute_expression_pair (lookup/prover.rs:410-494): sorted input; table value = input at the
+ * first row of each run, leftover table values (ascending, BTreeMap order) fill the repeated
+ * rows from the last one backwards; then bf+1 random rows each (input first). */
+static int permute_pair(const fe *A, const fe *S, uint64_t n, int bf, chacha_rng *rng, fe *Ap, fe *Sp) {
+    const uint64_t u = n - (uint64_t)(bf + 1);
+    keyed *ia = (keyed *)malloc((u + 1) * sizeof(keyed)), *ta = (keyed *)malloc((u + 1) * sizeof(keyed));
+    for (uint64_t i = 0; i < u; i++) {
+        ia[i].v = A[i]; fr_to_canonical(ia[i].c, &A[i]);
+        ta[i].v = S[i]; fr_to_canonical(ta[i].c, &S[i]);
+    }
+    qsort(ia, u, sizeof(keyed), keyed_cmp);
+    qsort(ta, u, sizeof(keyed), keyed_cmp);
+    uint64_t *rep = (uint64_t *)malloc((u + 1) * sizeof(uint64_t)), nrep = 0;
+    uint8_t *used = (uint8_t *)calloc(u + 1, 1);
+    uint64_t tp = 0;
+    int ok = 1;
+    for (uint64_t r = 0; r < u; r++) {
+        Ap[r] = ia[r].v;
+        if (r == 0 || keyed_cmp(&ia[r], &ia[r - 1]) != 0) {
+            Sp[r] = ia[r].v;
+            while (tp < u && keyed_cmp(&ta[tp], &ia[r]) < 0) tp++;
+            if (tp < u && keyed_cmp(&ta[tp], &ia[r]) == 0) used[tp++] = 1;
+            else ok = 0;
+        } else {
+            rep[nrep++] = r;
+        }
+    }
+    if (ok) {
+        uint64_t li = 0;
+        for (uint64_t t = 0; t < u; t++)
+            if (!used[t]) Sp[rep[nrep - 1 - li++]] = ta[t].v;
+    }
+    free(ia); free(ta); free(rep); free(used);
+    if (!ok) return -7;   /* Error::ConstraintSystemFailure: an input value is not in the table */
+    for (uint64_t r = u; r < n; r++) fr_random(rng, &Ap[r]);
+    for (uint64_t r = u; r < n; r++) fr_random(rng, &Sp[r]);
+    return 0;
+}
+
+/* z = [1, prod_0, prod_0 prod_1, ...] over n - bf rows, then bf random rows */
+static void grand_product(const fe *prod, uint64_t n, int bf, chacha_rng *rng, fe *z) {
+    z[0] = fr_ONE;
+    for (uint64_t i = 1; i < n - (uint64_t)bf; i++) fr_mul(&z[i], &z[i - 1], &prod[i - 1]);
+    for (uint64_t i = n - (uint64_t)bf; i < n; i++) fr_random(rng, &z[i]);
+}
+
 /* ====================================================================== keygen */
 typedef struct { fe point; int poly_id; } query_ref;
 
@@ -298,9 +384,41 @@ or_pk *or_keygen(const or_spec *s, int threads) {   /* keygen_vk + keygen_pk (ke
     const uint32_t k = s->k;
     const uint64_t n = 1ULL << k;
     int degree = 3;  /* permutation_argument_required_degree (circuit.rs:292-320) */
+    {   /* lookup_argument_required_degree / shuffle_argument_required_degree (circuit.rs:327-389) */
+        const int32_t *r = s->lookup_roots;
+        for (uint32_t l = 0; l < s->num_lookups; l++) {
+            int m = (int)s->lookup_sizes[l], di = 1, dt = 1;
+            for (int i = 0; i < m; i++) { int d = node_degree(s, r[i]); if (d > di) di = d; }
+            for (int i = 0; i < m; i++) { int d = node_degree(s, r[m + i]); if (d > dt) dt = d; }
+            int need = 2 + di + dt > 4 ? 2 + di + dt : 4;
+            if (need > degree) degree = need;
+            r += 2 * m;
+        }
+        r = s->shuffle_roots;
+        for (uint32_t l = 0; l < s->num_shuffles; l++) {
+            int m = (int)s->shuffle_sizes[l], di = 1, ds = 1;
+            for (int i = 0; i < m; i++) { int d = node_degree(s, r[i]); if (d > di) di = d; }
+            for (int i = 0; i < m; i++) { int d = node_degree(s, r[m + i]); if (d > ds) ds = d; }
+            int need = 2 + (di > ds ? di : ds);
+            if (need > degree) degree = need;
+            r += 2 * m;
+        }
+    }
     for (uint32_t g = 0; g < s->num_gates; g++) { int dg = node_degree(s, s->gate_roots[g]); if (dg > degree) degree = dg; }
     qlist adv_q = {0}, fix_q = {0}, ins_q = {0};
     for (uint32_t g = 0; g < s->num_gates; g++) collect_queries(s, s->gate_roots[g], &adv_q, &fix_q, &ins_q);
+    {   /* lookups then shuffles (keygen.rs:266-321), each input expressions then tables */
+        const int32_t *r = s->lookup_roots;
+        for (uint32_t l = 0; l < s->num_lookups; l++) {
+            for (uint32_t i = 0; i < 2 * s->lookup_sizes[l]; i++) collect_queries(s, r[i], &adv_q, &fix_q, &ins_q);
+            r += 2 * s->lookup_sizes[l];
+        }
+        r = s->shuffle_roots;
+        for (uint32_t l = 0; l < s->num_shuffles; l++) {
+            for (uint32_t i = 0; i < 2 * s->shuffle_sizes[l]; i++) collect_queries(s, r[i], &adv_q, &fix_q, &ins_q);
+            r += 2 * s->shuffle_sizes[l];
+        }
+    }
     for (uint32_t i = 0; i < s->num_perm_columns; i++) {
         int t = s->perm_columns[2 * i], idx = s->perm_columns[2 * i + 1];
         qlist_add(t == COL_ADVICE ? &adv_q : (t == COL_FIXED ? &fix_q : &ins_q), t, idx, 0);
@@ -458,7 +576,33 @@ int or_prove(const or_pk *pk, const or_spec *s, uint8_t *proof, uint64_t proof_c
         g1a cm; commit_msm(adv[c], n, s->srs_g_lagrange, threads, &cm);
         if (tr_write_point(&T, &cm)) return -5;
     }
-    fe theta = tr_squeeze(&T); (void)theta;
+    fe theta = tr_squeeze(&T);
+    /* lookup_commit_permuted, per lookup (lookup/prover.rs:64-173) */
+    const int NL = (int)s->num_lookups, NS = (int)s->num_shuffles;
+    fe **fix_lag = (fe **)calloc(s->num_fixed + 1, sizeof(fe *));
+    for (uint32_t i = 0; i < s->num_fixed; i++) fix_lag[i] = (fe *)(s->fixed_values + 4 * n * i);
+    fe **lk_A = (fe **)calloc(NL + 1, sizeof(fe *)), **lk_S = (fe **)calloc(NL + 1, sizeof(fe *));
+    fe **lk_Ap = (fe **)calloc(NL + 1, sizeof(fe *)), **lk_Sp = (fe **)calloc(NL + 1, sizeof(fe *));
+    fe **lk_Ap_poly = (fe **)calloc(NL + 1, sizeof(fe *)), **lk_Sp_poly = (fe **)calloc(NL + 1, sizeof(fe *));
+    fe **lk_z_poly = (fe **)calloc(NL + 1, sizeof(fe *)), **sh_z_poly = (fe **)calloc(NS + 1, sizeof(fe *));
+    {
+        const int32_t *r = s->lookup_roots;
+        for (int l = 0; l < NL; l++) {
+            const int m = (int)s->lookup_sizes[l];
+            lk_A[l] = fr_alloc(n); lk_S[l] = fr_alloc(n); lk_Ap[l] = fr_alloc(n); lk_Sp[l] = fr_alloc(n);
+            compress_lagrange(s, r, m, adv, fix_lag, inst_vals, n, &theta, lk_A[l], threads);
+            compress_lagrange(s, r + m, m, adv, fix_lag, inst_vals, n, &theta, lk_S[l], threads);
+            if (permute_pair(lk_A[l], lk_S[l], n, bf, &rng, lk_Ap[l], lk_Sp[l])) return -7;
+            fe b1, b2; fr_random(&rng, &b1); fr_random(&rng, &b2);
+            g1a c1, c2;
+            commit_msm(lk_Ap[l], n, s->srs_g_lagrange, threads, &c1);
+            commit_msm(lk_Sp[l], n, s->srs_g_lagrange, threads, &c2);
+            lk_Ap_poly[l] = fr_alloc(n); memcpy(lk_Ap_poly[l], lk_Ap[l], n * 32); lagrange_to_coeff_d(&D, lk_Ap_poly[l], threads);
+            lk_Sp_poly[l] = fr_alloc(n); memcpy(lk_Sp_poly[l], lk_Sp[l], n * 32); lagrange_to_coeff_d(&D, lk_Sp_poly[l], threads);
+            if (tr_write_point(&T, &c1) || tr_write_point(&T, &c2)) return -5;
+            r += 2 * m;
+        }
+    }
     fe beta = tr_squeeze(&T), gamma = tr_squeeze(&T);
     /* permutation_commit (permutation/prover.rs:50-197) */
     const int chunk_len = degree - 2;
@@ -506,6 +650,48 @@ int or_prove(const or_pk *pk, const or_spec *s, uint8_t *proof, uint64_t proof_c
         }
         free(mod);
     }
+    /* lookup products (lookup/prover.rs:182-325), then shuffle products (shuffle/prover.rs:97-206) */
+    {
+        fe *prod = fr_alloc(n);
+        for (int l = 0; l < NL; l++) {
+#pragma omp parallel for num_threads(threads) schedule(static)
+            for (uint64_t i = 0; i < n; i++) {
+                fe a, b; fr_add(&a, &beta, &lk_Ap[l][i]); fr_add(&b, &gamma, &lk_Sp[l][i]); fr_mul(&prod[i], &a, &b);
+            }
+            or_fr_batch_invert((uint64_t *)prod, n);
+#pragma omp parallel for num_threads(threads) schedule(static)
+            for (uint64_t i = 0; i < n; i++) {
+                fe a, b; fr_add(&a, &lk_A[l][i], &beta); fr_add(&b, &lk_S[l][i], &gamma);
+                fr_mul(&prod[i], &prod[i], &a); fr_mul(&prod[i], &prod[i], &b);
+            }
+            fe *z = fr_alloc(n);
+            grand_product(prod, n, bf, &rng, z);
+            fe blind; fr_random(&rng, &blind);
+            g1a cm; commit_msm(z, n, s->srs_g_lagrange, threads, &cm);
+            lagrange_to_coeff_d(&D, z, threads);
+            lk_z_poly[l] = z;
+            if (tr_write_point(&T, &cm)) return -5;
+        }
+        const int32_t *r = s->shuffle_roots;
+        fe *ci = fr_alloc(n), *cs = fr_alloc(n);
+        for (int l = 0; l < NS; l++) {
+            const int m = (int)s->shuffle_sizes[l];
+            compress_lagrange(s, r, m, adv, fix_lag, inst_vals, n, &theta, ci, threads);
+            compress_lagrange(s, r + m, m, adv, fix_lag, inst_vals, n, &theta, cs, threads);
+            for (uint64_t i = 0; i < n; i++) fr_add(&prod[i], &gamma, &cs[i]);
+            or_fr_batch_invert((uint64_t *)prod, n);
+            for (uint64_t i = 0; i < n; i++) { fe a; fr_add(&a, &gamma, &ci[i]); fr_mul(&prod[i], &prod[i], &a); }
+            fe *z = fr_alloc(n);
+            grand_product(prod, n, bf, &rng, z);
+            fe blind; fr_random(&rng, &blind);
+            g1a cm; commit_msm(z, n, s->srs_g_lagrange, threads, &cm);
+            lagrange_to_coeff_d(&D, z, threads);
+            sh_z_poly[l] = z;
+            if (tr_write_point(&T, &cm)) return -5;
+            r += 2 * m;
+        }
+        free(prod); free(ci); free(cs);
+    }
     /* vanishing::Argument::commit (vanishing/prover.rs:40-98) */
     fe *random_poly = fr_alloc(n);
     {
@@ -537,6 +723,14 @@ int or_prove(const or_pk *pk, const or_spec *s, uint8_t *proof, uint64_t proof_c
         fe **adv_c = (fe **)calloc(s->num_advice + 1, sizeof(fe *)), **ins_c = (fe **)calloc(s->num_instance + 1, sizeof(fe *));
         for (uint32_t c = 0; c < s->num_advice; c++) { adv_c[c] = fr_alloc(ext); coeff_to_extended_d(&D, adv[c], adv_c[c], threads); }
         for (uint32_t c = 0; c < s->num_instance; c++) { ins_c[c] = fr_alloc(ext); coeff_to_extended_d(&D, inst_polys[c], ins_c[c], threads); }
+        fe **lk_zc = (fe **)calloc(NL + 1, sizeof(fe *)), **lk_Apc = (fe **)calloc(NL + 1, sizeof(fe *));
+        fe **lk_Spc = (fe **)calloc(NL + 1, sizeof(fe *)), **sh_zc = (fe **)calloc(NS + 1, sizeof(fe *));
+        for (int l = 0; l < NL; l++) {
+            lk_zc[l] = fr_alloc(ext); coeff_to_extended_d(&D, lk_z_poly[l], lk_zc[l], threads);
+            lk_Apc[l] = fr_alloc(ext); coeff_to_extended_d(&D, lk_Ap_poly[l], lk_Apc[l], threads);
+            lk_Spc[l] = fr_alloc(ext); coeff_to_extended_d(&D, lk_Sp_poly[l], lk_Spc[l], threads);
+        }
+        for (int l = 0; l < NS; l++) { sh_zc[l] = fr_alloc(ext); coeff_to_extended_d(&D, sh_z_poly[l], sh_zc[l], threads); }
         const fe delta_start_beta = beta;   /* delta_start = beta * ZETA */
         fe delta_start; fr_mul(&delta_start, &delta_start_beta, &FR_ZETA);
         const int last_rot = -(bf + 1);
@@ -585,8 +779,54 @@ int or_prove(const or_pk *pk, const or_spec *s, uint8_t *proof, uint64_t proof_c
                     fr_mul(&v, &v, &y); fr_add(&v, &v, &u);
                 }
             }
+            {   /* lookups (evaluation.rs:486-558), shuffles (:561-620) */
+                uint64_t r_next = (idx + rot_scale) % ext, r_prev = (idx + ext - rot_scale) % ext;
+                const int32_t *r = s->lookup_roots;
+                for (int l = 0; l < NL; l++) {
+                    const int m = (int)s->lookup_sizes[l];
+                    fe ci = compress_coset(s, r, m, adv_c, fixed_cosets, ins_c, idx, rot_scale, ext, &theta);
+                    fe ct = compress_coset(s, r + m, m, adv_c, fixed_cosets, ins_c, idx, rot_scale, ext, &theta);
+                    fe tv, t1, t2, t3;
+                    fr_add(&t1, &ci, &beta); fr_add(&t2, &ct, &gamma); fr_mul(&tv, &t1, &t2);
+                    const fe zc = lk_zc[l][idx], ap = lk_Apc[l][idx], sp = lk_Spc[l][idx];
+                    fe ams; fr_sub(&ams, &ap, &sp);
+                    fr_sub(&t1, &fr_ONE, &zc); fr_mul(&t1, &t1, &l0[idx]);
+                    fr_mul(&v, &v, &y); fr_add(&v, &v, &t1);
+                    fr_mul(&t1, &zc, &zc); fr_sub(&t1, &t1, &zc); fr_mul(&t1, &t1, &l_last[idx]);
+                    fr_mul(&v, &v, &y); fr_add(&v, &v, &t1);
+                    fr_add(&t2, &ap, &beta); fr_add(&t3, &sp, &gamma);
+                    fr_mul(&t1, &lk_zc[l][r_next], &t2); fr_mul(&t1, &t1, &t3);
+                    fr_mul(&t2, &zc, &tv); fr_sub(&t1, &t1, &t2); fr_mul(&t1, &t1, &l_active[idx]);
+                    fr_mul(&v, &v, &y); fr_add(&v, &v, &t1);
+                    fr_mul(&t1, &ams, &l0[idx]);
+                    fr_mul(&v, &v, &y); fr_add(&v, &v, &t1);
+                    fr_sub(&t2, &ap, &lk_Apc[l][r_prev]); fr_mul(&t1, &ams, &t2); fr_mul(&t1, &t1, &l_active[idx]);
+                    fr_mul(&v, &v, &y); fr_add(&v, &v, &t1);
+                    r += 2 * m;
+                }
+                r = s->shuffle_roots;
+                for (int l = 0; l < NS; l++) {
+                    const int m = (int)s->shuffle_sizes[l];
+                    fe ci = compress_coset(s, r, m, adv_c, fixed_cosets, ins_c, idx, rot_scale, ext, &theta);
+                    fe cs = compress_coset(s, r + m, m, adv_c, fixed_cosets, ins_c, idx, rot_scale, ext, &theta);
+                    fr_add(&ci, &ci, &gamma); fr_add(&cs, &cs, &gamma);
+                    const fe zc = sh_zc[l][idx];
+                    fe t1, t2;
+                    fr_sub(&t1, &fr_ONE, &zc); fr_mul(&t1, &t1, &l0[idx]);
+                    fr_mul(&v, &v, &y); fr_add(&v, &v, &t1);
+                    fr_mul(&t1, &zc, &zc); fr_sub(&t1, &t1, &zc); fr_mul(&t1, &t1, &l_last[idx]);
+                    fr_mul(&v, &v, &y); fr_add(&v, &v, &t1);
+                    fr_mul(&t1, &sh_zc[l][r_next], &cs); fr_mul(&t2, &zc, &ci); fr_sub(&t1, &t1, &t2);
+                    fr_mul(&t1, &t1, &l_active[idx]);
+                    fr_mul(&v, &v, &y); fr_add(&v, &v, &t1);
+                    r += 2 * m;
+                }
+            }
             h[idx] = v;
         }
+        for (int l = 0; l < NL; l++) { free(lk_zc[l]); free(lk_Apc[l]); free(lk_Spc[l]); }
+        for (int l = 0; l < NS; l++) free(sh_zc[l]);
+        free(lk_zc); free(lk_Apc); free(lk_Spc); free(sh_zc);
         for (uint32_t c = 0; c < s->num_advice; c++) free(adv_c[c]);
         for (uint32_t c = 0; c < s->num_instance; c++) free(ins_c[c]);
         free(adv_c); free(ins_c);
@@ -629,17 +869,30 @@ int or_prove(const or_pk *pk, const or_spec *s, uint8_t *proof, uint64_t proof_c
         tr_write_scalar(&T, &e0); tr_write_scalar(&T, &e1);
         if (st + 1 < nsets) { fe e2 = eval_poly(z_poly[st], n, &x_last); tr_write_scalar(&T, &e2); }
     }
+    const fe x_prev = rotate_omega(&D, &x, -1);
+    for (int l = 0; l < NL; l++) {   /* lookup/prover.rs:330-361 */
+        fe e[5] = {eval_poly(lk_z_poly[l], n, &x), eval_poly(lk_z_poly[l], n, &x_next), eval_poly(lk_Ap_poly[l], n, &x),
+                   eval_poly(lk_Ap_poly[l], n, &x_prev), eval_poly(lk_Sp_poly[l], n, &x)};
+        for (int i = 0; i < 5; i++) tr_write_scalar(&T, &e[i]);
+    }
+    for (int l = 0; l < NS; l++) {   /* shuffle/prover.rs:210-231 */
+        fe e0 = eval_poly(sh_z_poly[l], n, &x), e1 = eval_poly(sh_z_poly[l], n, &x_next);
+        tr_write_scalar(&T, &e0); tr_write_scalar(&T, &e1);
+    }
     /* queries (prover.rs:840-889) -- poly ids: advice c -> c, fixed c -> A+c, sigma c -> A+F+c,
        z st -> A+F+P+st, h -> ..+nsets, random -> ..+1 */
     const int A_ = (int)s->num_advice, F_ = (int)s->num_fixed;
-    const int id_h = A_ + F_ + P + nsets, id_r = id_h + 1, npolys = id_r + 1;
+    const int id_lk = A_ + F_ + P + nsets, id_sh = id_lk + 3 * NL;   /* lookup l: z, A', S' */
+    const int id_h = id_sh + NS, id_r = id_h + 1, npolys = id_r + 1;
     fe **polys = (fe **)calloc(npolys, sizeof(fe *));
     for (int c = 0; c < A_; c++) polys[c] = adv[c];
     for (int c = 0; c < F_; c++) polys[A_ + c] = fixed_polys[c];
     for (int c = 0; c < P; c++) polys[A_ + F_ + c] = sigma_polys[c];
     for (int st = 0; st < nsets; st++) polys[A_ + F_ + P + st] = z_poly[st];
+    for (int l = 0; l < NL; l++) { polys[id_lk + 3 * l] = lk_z_poly[l]; polys[id_lk + 3 * l + 1] = lk_Ap_poly[l]; polys[id_lk + 3 * l + 2] = lk_Sp_poly[l]; }
+    for (int l = 0; l < NS; l++) polys[id_sh + l] = sh_z_poly[l];
     polys[id_h] = h_poly; polys[id_r] = random_poly;
-    int nq = 0, qcap = adv_q.n + fix_q.n + 3 * nsets + P + 2;
+    int nq = 0, qcap = adv_q.n + fix_q.n + 3 * nsets + P + 2 + 5 * NL + 2 * NS;
     query_ref *Q = (query_ref *)calloc(qcap, sizeof(query_ref));
     for (int i = 0; i < adv_q.n; i++) { Q[nq].point = rotate_omega(&D, &x, adv_q.q[i].rot); Q[nq++].poly_id = adv_q.q[i].index; }
     for (int st = 0; st < nsets; st++) {
@@ -647,6 +900,18 @@ int or_prove(const or_pk *pk, const or_spec *s, uint8_t *proof, uint64_t proof_c
         Q[nq].point = x_next; Q[nq++].poly_id = A_ + F_ + P + st;
     }
     for (int st = nsets - 2; st >= 0; st--) { Q[nq].point = x_last; Q[nq++].poly_id = A_ + F_ + P + st; }
+    for (int l = 0; l < NL; l++) {   /* lookup/prover.rs:364-405 */
+        const int zi = id_lk + 3 * l;
+        Q[nq].point = x; Q[nq++].poly_id = zi;
+        Q[nq].point = x; Q[nq++].poly_id = zi + 1;
+        Q[nq].point = x; Q[nq++].poly_id = zi + 2;
+        Q[nq].point = x_prev; Q[nq++].poly_id = zi + 1;
+        Q[nq].point = x_next; Q[nq++].poly_id = zi;
+    }
+    for (int l = 0; l < NS; l++) {   /* shuffle/prover.rs:234-254 */
+        Q[nq].point = x; Q[nq++].poly_id = id_sh + l;
+        Q[nq].point = x_next; Q[nq++].poly_id = id_sh + l;
+    }
     for (int i = 0; i < fix_q.n; i++) { Q[nq].point = rotate_omega(&D, &x, fix_q.q[i].rot); Q[nq++].poly_id = A_ + fix_q.q[i].index; }
     for (int c = 0; c < P; c++) { Q[nq].point = x; Q[nq++].poly_id = A_ + F_ + c; }
     Q[nq].point = x; Q[nq++].poly_id = id_h;

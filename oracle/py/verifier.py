@@ -13,6 +13,7 @@ Restated reference code (paths relative to the reference root):
   l_i_range                        halo2_backend/src/poly/domain.rs:425-450
   DualMSM::check                   halo2_backend/src/poly/kzg/msm.rs:188-206
   permutation Assembly             halo2_backend/src/plonk/permutation/keygen.rs:16-213
+  lookup / shuffle verifiers       halo2_backend/src/plonk/lookup/verifier.rs, shuffle/verifier.rs
 
 Pairings: the test setup knows the SRS secret s, so the pairing equation
 e(left, [s]G2) = e(right, G2) of DualMSM::check is decided exactly as
@@ -231,10 +232,13 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None):
         for v in col:
             T.common_scalar(v)
     adv_cm = [T.read_point() for _ in range(circ.num_advice)]
-    T.squeeze()  # theta
+    theta = T.squeeze()
+    lk_perm_cm = [(T.read_point(), T.read_point()) for _ in circ.lookups]   # A', S'
     beta = T.squeeze()
     gamma = T.squeeze()
     perm_cm = [T.read_point() for _ in range(nsets)]
+    lk_z_cm = [T.read_point() for _ in circ.lookups]
+    sh_z_cm = [T.read_point() for _ in circ.shuffles]
     random_cm = T.read_point()
     y = T.squeeze()
     h_cm = [T.read_point() for _ in range(dom.quotient_poly_degree)]
@@ -260,6 +264,8 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None):
         e1 = T.read_scalar()
         e2 = T.read_scalar() if i + 1 < nsets else None
         sets.append((e0, e1, e2))
+    lk_ev = [tuple(T.read_scalar() for _ in range(5)) for _ in circ.lookups]   # z, z_next, A', A'_inv, S'
+    sh_ev = [tuple(T.read_scalar() for _ in range(2)) for _ in circ.shuffles]  # z, z_next
 
     # vanishing argument: expressions at x
     l_evals = l_i_range(dom, x, xn, range(-(bf + 1), 1))
@@ -290,6 +296,26 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None):
                 right = right * (qeval(t, i, 0) + cur + gamma) % R
                 cur = cur * DELTA % R
             exprs.append((left - right) * (1 - (l_last + l_blind)) % R)
+    active = (1 - (l_last + l_blind)) % R
+
+    def compress(es):
+        acc = 0
+        for e in es:
+            acc = (acc * theta + e.evaluate(lambda c: c, qeval)) % R
+        return acc
+
+    for (ins_e, tab_e), (z, zn, ap, api, sp) in zip(circ.lookups, lk_ev):   # lookup/verifier.rs:98-160
+        exprs.append(l_0 * (1 - z) % R)
+        exprs.append(l_last * (z * z - z) % R)
+        left = zn * (ap + beta) % R * (sp + gamma) % R
+        right = z * (compress(ins_e) + beta) % R * (compress(tab_e) + gamma) % R
+        exprs.append((left - right) * active % R)
+        exprs.append(l_0 * (ap - sp) % R)
+        exprs.append((ap - sp) * (ap - api) % R * active % R)
+    for (ins_e, sh_e), (z, zn) in zip(circ.shuffles, sh_ev):   # shuffle/verifier.rs
+        exprs.append(l_0 * (1 - z) % R)
+        exprs.append(l_last * (z * z - z) % R)
+        exprs.append(active * (zn * (compress(sh_e) + gamma) - z * (compress(ins_e) + gamma)) % R)
     h_eval = 0
     for v in exprs:
         h_eval = (h_eval * y + v) % R
@@ -310,6 +336,16 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None):
         queries.append((("z", i), perm_cm[i], x_next, sets[i][1]))
     for i in reversed(range(nsets - 1)):
         queries.append((("z", i), perm_cm[i], x_last, sets[i][2]))
+    x_prev = rotate_omega(dom, x, -1)
+    for l, (zc, (apc, spc), (z, zn, ap, api, sp)) in enumerate(zip(lk_z_cm, lk_perm_cm, lk_ev)):
+        queries.append((("lz", l), zc, x, z))
+        queries.append((("la", l), apc, x, ap))
+        queries.append((("ls", l), spc, x, sp))
+        queries.append((("la", l), apc, x_prev, api))
+        queries.append((("lz", l), zc, x_next, zn))
+    for l, (zc, (z, zn)) in enumerate(zip(sh_z_cm, sh_ev)):
+        queries.append((("sz", l), zc, x, z))
+        queries.append((("sz", l), zc, x_next, zn))
     for qi, (col, rot) in enumerate(fix_q):
         queries.append((("fix", col), fixed_cm[col], rotate_omega(dom, x, rot), fix_evals[qi]))
     for i in range(len(circ.perm_columns)):

@@ -225,6 +225,8 @@ class OrSpec(ctypes.Structure):
         ("instance_lens", U32P), ("transcript_repr", U64P), ("rng_seed", U8P),
         ("vanishing_threads", ctypes.c_uint32), ("srs_g", U64P), ("srs_g_lagrange", U64P),
         ("unblinded", U8P),
+        ("num_lookups", ctypes.c_uint32), ("lookup_sizes", U32P), ("lookup_roots", I32P),
+        ("num_shuffles", ctypes.c_uint32), ("shuffle_sizes", U32P), ("shuffle_roots", I32P),
     ]
 
 
@@ -237,14 +239,17 @@ def make_spec(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=
     keep = [np.ascontiguousarray(x) for x in (
         circ.gate_roots, circ.nodes, circ.constants, circ.perm_array, circ.copies, circ.fixed_values,
         wit.advice, wit.instance, wit.instance_lens, circ.transcript_repr(),
-        np.frombuffer(bytes(seed), dtype=np.uint8).copy(), srs_g, srs_gl, circ.unblinded)]
-    (roots, nodes, consts, perm, copies, fixed, adv, ins, lens, tr, sd, g, gl, unb) = keep
+        np.frombuffer(bytes(seed), dtype=np.uint8).copy(), srs_g, srs_gl, circ.unblinded,
+        circ.lookup_sizes, circ.lookup_roots, circ.shuffle_sizes, circ.shuffle_roots)]
+    (roots, nodes, consts, perm, copies, fixed, adv, ins, lens, tr, sd, g, gl, unb, lks, lkr, shs, shr) = keep
     s = OrSpec(circ.k, circ.num_advice, circ.num_fixed, circ.num_instance,
                len(roots), _ptr(roots, I32P), len(nodes), _ptr(nodes, I32P),
                circ.num_constants, _ptr(consts, U64P), len(perm), _ptr(perm, I32P),
                len(copies), _ptr(copies, I32P), _ptr(fixed, U64P), _ptr(adv, U64P), _ptr(ins, U64P),
                _ptr(lens, U32P), _ptr(tr, U64P), _ptr(sd, U8P), vanishing_threads,
-               _ptr(g, U64P), _ptr(gl, U64P), _ptr(unb, U8P))
+               _ptr(g, U64P), _ptr(gl, U64P), _ptr(unb, U8P),
+               len(circ.lookups), _ptr(lks, U32P), _ptr(lkr, I32P),
+               len(circ.shuffles), _ptr(shs, U32P), _ptr(shr, I32P))
     return s, keep
 
 

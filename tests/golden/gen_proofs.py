@@ -1,5 +1,6 @@
 """Generates tests/golden/proof_golden.npz: proofs of the C1 simple-example circuit
-(k=8) and the mixed-feature circuit (k=7) from the C restatement prover, each
+(k=8), the mixed-feature circuit (k=7) and the lookup/shuffle circuit (k=8) from the C
+restatement prover, each
 checked by the independent Python verifier before it is written.  Inputs are fully
 determined by the circuit generators' seeds, the SRS secret s (stored) and the
 prover RNG seed [7; 32] with vanishing thread count 8.
@@ -23,7 +24,8 @@ import verifier as V  # noqa: E402
 
 def main():
     out = {}
-    for name, make in (("simple_k8", lambda: hc.simple_example(8)), ("mixed_k7", lambda: hc.mixed_circuit(7))):
+    for name, make in (("simple_k8", lambda: hc.simple_example(8)), ("mixed_k7", lambda: hc.mixed_circuit(7)),
+                       ("lookup_k8", lambda: hc.lookup_circuit(8))):
         circ, wit = make()
         s, g, gl = O.srs(circ.k)
         proof = O.create_proof(circ, wit, g, gl)

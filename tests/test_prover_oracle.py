@@ -66,6 +66,8 @@ CIRCUITS = {
     "simple_k8": lambda: hc.simple_example(8),
     "mixed_k7": lambda: hc.mixed_circuit(7),
     "c3_k8": lambda: hc.synthetic_c3(8, O.OracleOps),
+    "lookup_k8": lambda: hc.lookup_circuit(8),
+    "lookup_k9": lambda: hc.lookup_circuit(9, seed=6),
 }
 
 
@@ -147,10 +149,33 @@ def test_instance_too_large_fails():
         O.create_proof(circ, wit, g, gl)
 
 
+def test_lookup_shuffle_negative_cases():
+    """a broken shuffle does not verify; an input missing from the table fails like the
+    reference (permute_expression_pair -> Error::ConstraintSystemFailure)"""
+    circ, wit = hc.lookup_circuit(8)
+    s, g, gl = O.srs(circ.k)
+    bad = hc.Witness(wit.advice.copy(), wit.instance, wit.instance_lens)
+    bad.advice[3, 5] = hc.fr_to_limbs(77)
+    assert not V.verify(circ, [], O.create_proof(circ, bad, g, gl), s)
+    bad = hc.Witness(wit.advice.copy(), wit.instance, wit.instance_lens)
+    bad.advice[0, 5] = hc.fr_to_limbs(300)
+    bad.advice[1, 5] = hc.fr_to_limbs(90000)
+    with pytest.raises(ValueError, match="-7"):
+        O.create_proof(circ, bad, g, gl)
+
+
+def test_lookup_degree_and_queries():
+    circ, _ = hc.lookup_circuit(8)
+    assert circ.degree() == 5   # 2 + deg(q a) + deg(t) = 5 (circuit.rs:327-373)
+    adv, fix, ins = circ.queries()
+    assert adv == [(1, 0), (0, 0), (0, 1), (2, 0), (3, 0)]   # gates, lookups, shuffles, permutation
+    assert fix == [(0, 0), (1, 0), (2, 0), (3, 0)]
+
+
 def test_golden_proofs():
     """committed fixtures (tests/golden/gen_proofs.py): the restatement reproduces them"""
     d = np.load(os.path.join(GOLDEN, "proof_golden.npz"), allow_pickle=False)
-    for name in ("simple_k8", "mixed_k7"):
+    for name in ("simple_k8", "mixed_k7", "lookup_k8"):
         circ, wit = CIRCUITS[name]()
         s, g, gl = O.srs(circ.k, int(d[f"{name}_s"].tobytes()[::-1].hex(), 16))
         proof = O.create_proof(circ, wit, g, gl)

@@ -130,7 +130,13 @@ class Circuit:
     """ConstraintSystemMid + Preprocessing (one compiled circuit)."""
 
     def __init__(self, k, num_advice, num_fixed, num_instance, gates, perm_columns, copies,
-                 fixed_values, unblinded=None, name="circuit"):
+                 fixed_values, unblinded=None, name="circuit", lookups=(), shuffles=()):
+        """lookups: [(input_exprs, table_exprs)], shuffles: [(input_exprs, shuffle_exprs)]
+        (halo2_middleware circuit.rs LookupArgument / ShuffleArgument)"""
+        self.lookups = [(list(a), list(b)) for a, b in lookups]
+        self.shuffles = [(list(a), list(b)) for a, b in shuffles]
+        for a, b in self.lookups + self.shuffles:
+            assert len(a) == len(b) and len(a) > 0
         self.k = int(k)
         self.n = 1 << self.k
         self.num_advice, self.num_fixed, self.num_instance = num_advice, num_fixed, num_instance
@@ -146,8 +152,14 @@ class Circuit:
 
     # -- ConstraintSystem facts (halo2_backend/src/plonk/circuit.rs, keygen.rs) --
     def degree(self):
-        """required_degree with the permutation argument (degree 3) -- circuit.rs:292-320"""
-        return max([3] + [g.degree() for g in self.gates])
+        """ConstraintSystem::degree: permutation (3), lookups max(4, 2 + deg(in) + deg(table)),
+        shuffles 2 + max(deg(in), deg(shuffle)), gates -- circuit.rs:100-139,292-389"""
+        d = [3] + [g.degree() for g in self.gates]
+        for a, b in self.lookups:
+            d.append(max(4, 2 + max([1] + [e.degree() for e in a]) + max([1] + [e.degree() for e in b])))
+        for a, b in self.shuffles:
+            d.append(2 + max([1] + [e.degree() for e in a] + [e.degree() for e in b]))
+        return max(d)
 
     def queries(self):
         """(advice, fixed, instance) query lists in first-appearance order: gate
@@ -170,6 +182,9 @@ class Circuit:
 
         for g in self.gates:
             walk(g)
+        for a, b in self.lookups + self.shuffles:
+            for e in a + b:
+                walk(e)
         for t, i in self.perm_columns:
             add(t, i, 0)
         return lists[ADVICE], lists[FIXED], lists[INSTANCE]
@@ -204,6 +219,10 @@ class Circuit:
             return len(nodes) - 1
 
         roots = [rec(g) for g in self.gates]
+        self.lookup_sizes = np.asarray([len(a) for a, _ in self.lookups] or [0], dtype=np.uint32)
+        self.lookup_roots = np.asarray([rec(e) for a, b in self.lookups for e in a + b] or [0], dtype=np.int32)
+        self.shuffle_sizes = np.asarray([len(a) for a, _ in self.shuffles] or [0], dtype=np.uint32)
+        self.shuffle_roots = np.asarray([rec(e) for a, b in self.shuffles for e in a + b] or [0], dtype=np.int32)
         self.nodes = np.asarray(nodes, dtype=np.int32).reshape(-1, 4)
         self.gate_roots = np.asarray(roots, dtype=np.int32)
         self.constants = ints_to_mont(consts) if consts else np.zeros((1, 4), dtype=np.uint64)
@@ -220,6 +239,8 @@ class Circuit:
             np.asarray([self.k, self.num_advice, self.num_fixed, self.num_instance], dtype=np.int64).tobytes(),
             self.nodes.tobytes(), self.gate_roots.tobytes(), self.constants.tobytes(),
             self.perm_array.tobytes(), self.copies.tobytes(), self.unblinded.tobytes(),
+            self.lookup_sizes.tobytes(), self.lookup_roots.tobytes(), self.shuffle_sizes.tobytes(),
+            self.shuffle_roots.tobytes(),
             hashlib.blake2b(self.fixed_values.tobytes()).digest(),
         ])
         h.update(len(desc).to_bytes(8, "little"))
@@ -366,6 +387,53 @@ def mixed_circuit(k=7, seed=2):
     circ = Circuit(k, 5, 4, 2, gates, perm, copies, fixed_vals, unblinded=[E], name=f"mixed k={k}")
     wit = Witness(np.stack([ints_to_mont(v) for v in (va, vb, vc, vd, ve)]),
                   np.stack([ints_to_mont(i0), ints_to_mont(i1)]), [u, u])
+    return circ, wit
+
+
+def lookup_circuit(k=8, seed=4, table_bits=None):
+    """Lookup + shuffle circuit (the argument shapes of BASELINE configs[4]): advice a (bytes),
+    b = a^2, c, d = a permutation of c; fixed q, t = range table 0..2^bits-1, t2 = t^2,
+    q2.  gate q (b - a a); lookup [q a] in [t]; lookup [q a, q b] in [t, t2] (two-column
+    table); lookup [q a[next]] in [t] (rotation inside a lookup); shuffle [q2 c] ~ [q2 d];
+    permutation over a, c with copies between equal cells."""
+    n = 1 << k
+    rng = np.random.default_rng(seed)
+    A, B, C, D = range(4)
+    Q, T, T2, Q2 = range(4)
+    gates = [fixed(Q) * (advice(B) - advice(A) * advice(A))]
+    lookups = [([fixed(Q) * advice(A)], [fixed(T)]),
+               ([fixed(Q) * advice(A), fixed(Q) * advice(B)], [fixed(T), fixed(T2)]),
+               ([fixed(Q) * advice(A, 1)], [fixed(T)])]
+    shuffles = [([fixed(Q2) * advice(C)], [fixed(Q2) * advice(D)])]
+    perm = [(ADVICE, A), (ADVICE, C)]
+    probe = Circuit(k, 4, 4, 0, gates, perm, [], np.zeros((4, n, 4), np.uint64), lookups=lookups,
+                    shuffles=shuffles)
+    u = probe.usable_rows()
+    tsize = 1 << (table_bits if table_bits is not None else min(8, k - 1))
+    assert tsize <= u, "the range table must fit in the usable rows"
+    va = [0] * n
+    vc = [0] * n
+    for r in range(u):
+        va[r] = int(rng.integers(0, tsize))
+        vc[r] = int.from_bytes(rng.bytes(32), "little") % R_MOD
+    vb = [v * v % R_MOD for v in va]
+    perm_idx = rng.permutation(u)
+    vd = [vc[int(perm_idx[r])] for r in range(u)] + [0] * (n - u)
+    q = [1 if r < u - 1 else 0 for r in range(n)]   # a[next] must stay inside the usable rows
+    q2 = [1 if r < u else 0 for r in range(n)]
+    t = [r % tsize if r < u else 0 for r in range(n)]
+    t2 = [v * v % R_MOD for v in t]
+    copies = []
+    seen = {}
+    for r in range(u):
+        if va[r] in seen and len(copies) < 20:
+            copies.append((ADVICE, A, seen[va[r]], ADVICE, A, r))
+        seen[va[r]] = r
+    copies.append((ADVICE, C, 3, ADVICE, C, 3))   # trivial self-copy (no-op in Assembly)
+    fixed_vals = np.stack([ints_to_mont(q), ints_to_mont(t), ints_to_mont(t2), ints_to_mont(q2)])
+    circ = Circuit(k, 4, 4, 0, gates, perm, copies, fixed_vals, name=f"lookup k={k}", lookups=lookups,
+                   shuffles=shuffles)
+    wit = Witness(np.stack([ints_to_mont(v) for v in (va, vb, vc, vd)]), np.zeros((0, n, 4), np.uint64), [])
     return circ, wit
 
 
