@@ -159,7 +159,7 @@ int h2g_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8])
  * Node = 4 x int32 (op, a, b, c): op 0 CONST (a = constant index), 1 QUERY (a = column
  * type 0 advice / 1 fixed / 2 instance, b = column index, c = rotation), 2 NEG (a),
  * 3 SUM (a, b), 4 PROD (a, b).  Copy = 6 x int32 (ltype, lindex, lrow, rtype, rindex, rrow).
- * Supported: one advice phase, no challenges, no lookups/shuffles (H2G_ERR_ARG).
+ * Supported: one advice phase (no challenges), gates, permutation, lookups, shuffles.
  * rng: ChaCha20Rng::from_seed(rng_seed); vanishing_threads: the thread count that
  * splits the vanishing argument's random polynomial into ChaCha streams
  * (vanishing/prover.rs:57-81), part of the proof's determinism. */
@@ -178,6 +178,15 @@ typedef struct {
   const uint64_t* fixed_values;   /* num_fixed x n Fr (Lagrange) */
   const uint8_t* unblinded;       /* num_advice flags (unblinded_advice_columns) or NULL */
   const uint64_t* transcript_repr; /* vk.transcript_repr (Fr) */
+  /* lookup arguments (lookup::Argument): per lookup m (input, table) expression pairs;
+   * roots: per lookup m input roots then m table roots */
+  uint32_t num_lookups;
+  const uint32_t* lookup_sizes;
+  const int32_t* lookup_roots;
+  /* shuffle arguments (shuffle::Argument): per shuffle m input roots then m shuffle roots */
+  uint32_t num_shuffles;
+  const uint32_t* shuffle_sizes;
+  const int32_t* shuffle_roots;
 } h2g_circuit;
 
 /* SRS resident on the current device: g[n] and g_lagrange[n] (G1Affine) from the host... */

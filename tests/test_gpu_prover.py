@@ -49,6 +49,8 @@ CASES = {
     "mixed_k10": lambda: hc.mixed_circuit(10, seed=5),
     "c3_k8": lambda: hc.synthetic_c3(8, O.OracleOps),
     "c3_k12": lambda: hc.synthetic_c3(12, O.OracleOps, seed=9),
+    "lookup_k8": lambda: hc.lookup_circuit(8),
+    "lookup_k11": lambda: hc.lookup_circuit(11, seed=8),
 }
 
 
@@ -72,7 +74,7 @@ def test_proof_bytes_match_oracle(name):
 
 def test_golden_proofs_on_device():
     d = np.load(O.os.path.join(O.REPO, "tests", "golden", "proof_golden.npz"), allow_pickle=False)
-    for name in ("simple_k8", "mixed_k7"):
+    for name in ("simple_k8", "mixed_k7", "lookup_k8"):
         circ, wit = CASES[name]()
         s = int(d[f"{name}_s"].tobytes()[::-1].hex(), 16)
         _, g, gl = O.srs(circ.k, s)
@@ -118,3 +120,18 @@ def test_errors():
     with pytest.raises(h2g.H2GError, match="params k"):
         h2g.ProvingKey(other, circ)
     other.close()
+
+
+def test_lookup_missing_table_value_fails():
+    """permute_expression_pair's ConstraintSystemFailure: reported as an argument error"""
+    circ, wit = hc.lookup_circuit(8)
+    s, g, gl, params = _params(8)
+    pk = h2g.ProvingKey(params, circ)
+    bad = hc.Witness(wit.advice.copy(), wit.instance, wit.instance_lens)
+    bad.advice[0, 5] = hc.fr_to_limbs(300)
+    bad.advice[1, 5] = hc.fr_to_limbs(90000)
+    with pytest.raises(h2g.H2GError, match="not in the table"):
+        pk.create_proof(bad)
+    # the key stays usable
+    assert pk.create_proof(wit) == O.create_proof(circ, wit, g, gl)
+    pk.close()

@@ -21,6 +21,8 @@
 #include <functional>
 #include <set>
 
+#include <hipcub/hipcub.hpp>
+
 #include "poly.h"
 #include "prover_kernels.h"
 #include "runtime.h"
@@ -94,13 +96,28 @@ struct ProvingKey {
   PowTable om, eo;
   int4* prog = nullptr;
   int prog_len = 0, n_slots = 0;
+  int2 seg_gates = {0, 0};
+  std::vector<int2> seg_lk_in, seg_lk_tab, seg_sh_in, seg_sh_sh;  // expression-list programs
   Fr* consts = nullptr;
   int n_loads = 0;
-  const Fr** d_load_col = nullptr;
+  const Fr** d_load_col = nullptr;      // extended-coset columns (evaluate_h)
+  const Fr** d_load_col_lag = nullptr;  // Lagrange columns (lookup / shuffle compression)
   int* d_load_rot = nullptr;
   const Fr** d_z = nullptr;
   const Fr** d_perm_v = nullptr;
   const Fr** d_sigma = nullptr;
+  // lookups (NL) and shuffles (NS): per-argument device buffers
+  int NL = 0, NS = 0;
+  std::vector<Fr*> lk_a, lk_s, lk_ap, lk_sp, lk_ap_poly, lk_sp_poly, lk_z, lk_z_poly, lk_zc, lk_apc, lk_spc;
+  std::vector<Fr*> sh_z, sh_z_poly, sh_zc;
+  EvalLookup* d_lookups = nullptr;
+  EvalShuffle* d_shuffles = nullptr;
+  Fr *tmp_a = nullptr, *tmp_b = nullptr, *one = nullptr;
+  CanonKey *ck_a = nullptr, *ck_t = nullptr, *ck_a2 = nullptr, *ck_t2 = nullptr, *ck_left = nullptr;
+  uint8_t *rep_flag = nullptr, *left_flag = nullptr;
+  uint32_t *rep_rows = nullptr, *counters = nullptr;
+  void* sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
   // per-proof workspace (device), reused across proofs
   std::vector<Fr*> adv, adv_coset, inst_val, inst_poly, inst_coset, z, z_lag, z_coset;
   Fr *mod = nullptr, *pre = nullptr, *scr = nullptr, *random_poly = nullptr, *h_ext = nullptr, *h_coeff = nullptr;
@@ -292,6 +309,16 @@ struct GateCompiler {
     loads.push_back(q);
     return (int)loads.size() - 1;
   }
+  // program segment: Horner (acc = acc * factor + e) over the expressions `roots`
+  int2 compile_list(const int32_t* roots, int m) {
+    const int off = (int)prog.size();
+    for (int i = 0; i < m; i++) {
+      const int s = gen(roots[i]);
+      prog.push_back(make_int4(G_HORNER, 0, s, 0));
+      release(s);
+    }
+    return make_int2(off, (int)prog.size() - off);
+  }
   int gen(int i) {
     const int32_t* nd = v.node(i);
     switch (nd[0]) {
@@ -365,7 +392,37 @@ bool check_nodes(const h2g_circuit* c, std::string* why) {
   }
   for (uint32_t g = 0; g < c->num_gates; g++)
     if (c->gate_roots[g] < 0 || (uint32_t)c->gate_roots[g] >= c->num_nodes) return *why = "gate root", false;
-  return true;
+  auto check_args = [&](uint32_t na, const uint32_t* sizes, const int32_t* roots, const char* what) -> bool {
+    if (na && (!sizes || !roots)) return *why = std::string("null ") + what, false;
+    size_t off = 0;
+    for (uint32_t l = 0; l < na; l++) {
+      if (sizes[l] == 0) return *why = std::string(what) + " without expressions", false;
+      for (uint32_t i = 0; i < 2 * sizes[l]; i++)
+        if (roots[off + i] < 0 || (uint32_t)roots[off + i] >= c->num_nodes)
+          return *why = std::string(what) + " root", false;
+      off += 2 * sizes[l];
+    }
+    return true;
+  };
+  return check_args(c->num_lookups, c->lookup_sizes, c->lookup_roots, "lookup") &&
+         check_args(c->num_shuffles, c->shuffle_sizes, c->shuffle_roots, "shuffle");
+}
+
+// per-argument root lists: (inputs, tables) of lookup l / (inputs, shuffles) of shuffle l
+struct ArgRoots {
+  const int32_t* in;
+  const int32_t* other;
+  int m;
+};
+std::vector<ArgRoots> arg_roots(uint32_t na, const uint32_t* sizes, const int32_t* roots) {
+  std::vector<ArgRoots> out;
+  size_t off = 0;
+  for (uint32_t l = 0; l < na; l++) {
+    const int m = (int)sizes[l];
+    out.push_back({roots + off, roots + off + m, m});
+    off += 2 * (size_t)m;
+  }
+  return out;
 }
 
 // ------------------------------------------------------------------ keygen
@@ -397,9 +454,38 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk) {
   }
   // degree, queries, blinding factors (circuit.rs:143-170,292-320; keygen.rs:191-260)
   std::vector<int> memo(c->num_nodes, -1);
+  const std::vector<ArgRoots> lks = arg_roots(c->num_lookups, c->lookup_sizes, c->lookup_roots);
+  const std::vector<ArgRoots> shs = arg_roots(c->num_shuffles, c->shuffle_sizes, c->shuffle_roots);
+  pk.NL = (int)lks.size();
+  pk.NS = (int)shs.size();
   pk.degree = 3;
   for (uint32_t g = 0; g < c->num_gates; g++) pk.degree = std::max(pk.degree, node_degree(cv, c->gate_roots[g], memo));
+  for (const auto& a : lks) {  // lookup_argument_required_degree (circuit.rs:327-373)
+    int di = 1, dt = 1;
+    for (int i = 0; i < a.m; i++) {
+      di = std::max(di, node_degree(cv, a.in[i], memo));
+      dt = std::max(dt, node_degree(cv, a.other[i], memo));
+    }
+    pk.degree = std::max(pk.degree, std::max(4, 2 + di + dt));
+  }
+  for (const auto& a : shs) {  // shuffle_argument_required_degree (circuit.rs:375-389)
+    int di = 1, ds = 1;
+    for (int i = 0; i < a.m; i++) {
+      di = std::max(di, node_degree(cv, a.in[i], memo));
+      ds = std::max(ds, node_degree(cv, a.other[i], memo));
+    }
+    pk.degree = std::max(pk.degree, 2 + std::max(di, ds));
+  }
+  // queries: gates, lookups (inputs then tables), shuffles, permutation (keygen.rs:320-345)
   for (uint32_t g = 0; g < c->num_gates; g++) collect(cv, c->gate_roots[g], pk);
+  for (const auto& a : lks) {
+    for (int i = 0; i < a.m; i++) collect(cv, a.in[i], pk);
+    for (int i = 0; i < a.m; i++) collect(cv, a.other[i], pk);
+  }
+  for (const auto& a : shs) {
+    for (int i = 0; i < a.m; i++) collect(cv, a.in[i], pk);
+    for (int i = 0; i < a.m; i++) collect(cv, a.other[i], pk);
+  }
   for (auto& pc : pk.perm_cols)
     add_query(pc.first == COL_ADVICE ? pk.adv_q : (pc.first == COL_FIXED ? pk.fix_q : pk.ins_q),
               Query{pc.first, pc.second, 0});
@@ -454,6 +540,48 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk) {
   HIPCHK(vec_alloc(pk.z, pk.nsets, n));
   HIPCHK(vec_alloc(pk.z_lag, pk.nsets, n));
   HIPCHK(vec_alloc(pk.z_coset, pk.nsets, ext));
+  // lookups / shuffles
+  HIPCHK(vec_alloc(pk.lk_a, pk.NL, n));
+  HIPCHK(vec_alloc(pk.lk_s, pk.NL, n));
+  HIPCHK(vec_alloc(pk.lk_ap, pk.NL, n));
+  HIPCHK(vec_alloc(pk.lk_sp, pk.NL, n));
+  HIPCHK(vec_alloc(pk.lk_ap_poly, pk.NL, n));
+  HIPCHK(vec_alloc(pk.lk_sp_poly, pk.NL, n));
+  HIPCHK(vec_alloc(pk.lk_z, pk.NL, n));
+  HIPCHK(vec_alloc(pk.lk_z_poly, pk.NL, n));
+  HIPCHK(vec_alloc(pk.lk_zc, pk.NL, ext));
+  HIPCHK(vec_alloc(pk.lk_apc, pk.NL, ext));
+  HIPCHK(vec_alloc(pk.lk_spc, pk.NL, ext));
+  HIPCHK(vec_alloc(pk.sh_z, pk.NS, n));
+  HIPCHK(vec_alloc(pk.sh_z_poly, pk.NS, n));
+  HIPCHK(vec_alloc(pk.sh_zc, pk.NS, ext));
+  HIPCHK(falloc(&pk.one, 1));
+  {
+    const Fr one = Fr::one();
+    HIPCHK(hipMemcpy(pk.one, &one, sizeof(Fr), hipMemcpyHostToDevice));
+  }
+  if (pk.NL + pk.NS) {
+    HIPCHK(falloc(&pk.tmp_a, n));
+    HIPCHK(falloc(&pk.tmp_b, n));
+  }
+  if (pk.NL) {  // permute_expression_pair scratch
+    PALLOC(pool, pk.ck_a, n);
+    PALLOC(pool, pk.ck_t, n);
+    PALLOC(pool, pk.ck_a2, n);
+    PALLOC(pool, pk.ck_t2, n);
+    PALLOC(pool, pk.ck_left, n);
+    PALLOC(pool, pk.rep_flag, n);
+    PALLOC(pool, pk.left_flag, n);
+    PALLOC(pool, pk.rep_rows, n);
+    PALLOC(pool, pk.counters, 8);
+    size_t b1 = 0, b2 = 0, b3 = 0;
+    HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(nullptr, b1, pk.ck_a, pk.ck_a2, (int)n, CanonLess(), st));
+    HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, b2, pk.ck_t2, pk.left_flag, pk.ck_left, pk.counters, (int)n, st));
+    HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, b3, hipcub::CountingInputIterator<uint32_t>(0), pk.rep_flag,
+                                         pk.rep_rows, pk.counters + 1, (int)n, st));
+    pk.sort_tmp_bytes = std::max(b1, std::max(b2, b3));
+    HIPCHK(pool.get(&pk.sort_tmp, pk.sort_tmp_bytes));
+  }
 
   // fixed columns
   HIPCHK(vec_alloc(pk.fixed_lag, pk.F, n));
@@ -546,37 +674,55 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk) {
     (void)hipFree(dmr);
     (void)hipFree(ddp);
   }
-  // gate program
+  // expression programs: gates (Horner in y), then each lookup's / shuffle's expression
+  // lists (Horner in theta), sharing one slot allocation and one load table
   {
     GateCompiler gc(cv);
-    for (uint32_t g = 0; g < c->num_gates; g++) {
-      const int s = gc.gen(c->gate_roots[g]);
-      gc.prog.push_back(make_int4(G_HORNER, 0, s, 0));
-      gc.release(s);
+    pk.seg_gates = gc.compile_list(c->gate_roots, (int)c->num_gates);
+    for (const auto& a : lks) {
+      pk.seg_lk_in.push_back(gc.compile_list(a.in, a.m));
+      pk.seg_lk_tab.push_back(gc.compile_list(a.other, a.m));
+    }
+    for (const auto& a : shs) {
+      pk.seg_sh_in.push_back(gc.compile_list(a.in, a.m));
+      pk.seg_sh_sh.push_back(gc.compile_list(a.other, a.m));
     }
     if (gc.n_slots > evaluate_h_max_slots())
-      return fail(H2G_ERR_ARG, "keygen: gate expressions need more than " + std::to_string(evaluate_h_max_slots()) +
+      return fail(H2G_ERR_ARG, "keygen: expressions need more than " + std::to_string(evaluate_h_max_slots()) +
                                    " live values");
     pk.prog_len = (int)gc.prog.size();
     pk.n_slots = gc.n_slots;
     PALLOC(pool, pk.prog, gc.prog.size() + 1);
-    HIPCHK(hipMemcpyAsync(pk.prog, gc.prog.data(), gc.prog.size() * sizeof(int4), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpy(pk.prog, gc.prog.data(), gc.prog.size() * sizeof(int4), hipMemcpyHostToDevice));
     PALLOC(pool, pk.consts, c->num_constants + 1);
     if (c->num_constants)
-      HIPCHK(hipMemcpyAsync(pk.consts, c->constants, c->num_constants * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpy(pk.consts, c->constants, c->num_constants * sizeof(Fr), hipMemcpyHostToDevice));
     pk.n_loads = (int)gc.loads.size();
-    std::vector<const Fr*> lc(pk.n_loads + 1, nullptr);
+    std::vector<const Fr*> lc(pk.n_loads + 1, nullptr), ll(pk.n_loads + 1, nullptr);
     std::vector<int> lr(pk.n_loads + 1, 0);
     for (int i = 0; i < pk.n_loads; i++) {
       const Query& q = gc.loads[i];
       lc[i] = q.type == COL_ADVICE ? pk.adv_coset[q.index]
                                    : (q.type == COL_FIXED ? pk.fixed_coset[q.index] : pk.inst_coset[q.index]);
+      ll[i] = q.type == COL_ADVICE ? pk.adv[q.index]
+                                   : (q.type == COL_FIXED ? pk.fixed_lag[q.index] : pk.inst_val[q.index]);
       lr[i] = q.rot;
     }
     PALLOC(pool, pk.d_load_col, lc.size());
+    PALLOC(pool, pk.d_load_col_lag, ll.size());
     PALLOC(pool, pk.d_load_rot, lr.size());
-    HIPCHK(hipMemcpyAsync(pk.d_load_col, lc.data(), lc.size() * sizeof(Fr*), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(pk.d_load_rot, lr.data(), lr.size() * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpy(pk.d_load_col, lc.data(), lc.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(pk.d_load_col_lag, ll.data(), ll.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(pk.d_load_rot, lr.data(), lr.size() * sizeof(int), hipMemcpyHostToDevice));
+    std::vector<EvalLookup> el(pk.NL + 1);
+    std::vector<EvalShuffle> es(pk.NS + 1);
+    for (int l = 0; l < pk.NL; l++)
+      el[l] = EvalLookup{pk.seg_lk_in[l], pk.seg_lk_tab[l], pk.lk_zc[l], pk.lk_apc[l], pk.lk_spc[l]};
+    for (int l = 0; l < pk.NS; l++) es[l] = EvalShuffle{pk.seg_sh_in[l], pk.seg_sh_sh[l], pk.sh_zc[l]};
+    PALLOC(pool, pk.d_lookups, el.size());
+    PALLOC(pool, pk.d_shuffles, es.size());
+    HIPCHK(hipMemcpy(pk.d_lookups, el.data(), el.size() * sizeof(EvalLookup), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(pk.d_shuffles, es.data(), es.size() * sizeof(EvalShuffle), hipMemcpyHostToDevice));
     std::vector<const Fr*> zt(pk.nsets + 1), pv(pk.P + 1), sg(pk.P + 1);
     for (int s = 0; s < pk.nsets; s++) zt[s] = pk.z_coset[s];
     for (int i = 0; i < pk.P; i++) {
@@ -588,9 +734,9 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk) {
     PALLOC(pool, pk.d_z, zt.size());
     PALLOC(pool, pk.d_perm_v, pv.size());
     PALLOC(pool, pk.d_sigma, sg.size());
-    HIPCHK(hipMemcpyAsync(pk.d_z, zt.data(), zt.size() * sizeof(Fr*), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(pk.d_perm_v, pv.data(), pv.size() * sizeof(Fr*), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(pk.d_sigma, sg.data(), sg.size() * sizeof(Fr*), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpy(pk.d_z, zt.data(), zt.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(pk.d_perm_v, pv.data(), pv.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(pk.d_sigma, sg.data(), sg.size() * sizeof(Fr*), hipMemcpyHostToDevice));
   }
   HIPCHK(hipStreamSynchronize(st));
   return H2G_OK;
@@ -667,7 +813,74 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     }
   }
   clk.mark("advice commit");
-  (void)tr.squeeze();  // theta
+  const Fr theta = tr.squeeze();
+  auto compress = [&](int2 seg, Fr* out) -> int {
+    CompressArgs ca;
+    ca.prog = pk.prog;
+    ca.seg = seg;
+    ca.n_slots = pk.n_slots;
+    ca.consts = pk.consts;
+    ca.load_col = pk.d_load_col_lag;
+    ca.load_rot = pk.d_load_rot;
+    ca.n = n;
+    ca.theta = theta;
+    ca.out = out;
+    HIPCHK(compress_lagrange(ca, st));
+    return H2G_OK;
+  };
+  // ---- lookup_commit_permuted, per lookup (lookup/prover.rs:64-173, 410-494)
+  {
+    std::vector<MsmTicket> tk(2 * pk.NL);
+    const size_t u = n - (size_t)(bf + 1);
+    std::vector<Fr> rows((size_t)(bf + 1));
+    for (int l = 0; l < pk.NL; l++) {
+      RCCHK(compress(pk.seg_lk_in[l], pk.lk_a[l]));
+      RCCHK(compress(pk.seg_lk_tab[l], pk.lk_s[l]));
+      // permute_expression_pair: sort by Ord (canonical value), match, fill leftovers
+      HIPCHK(fr_to_canon(pk.lk_a[l], pk.ck_a, u, st));
+      HIPCHK(fr_to_canon(pk.lk_s[l], pk.ck_t, u, st));
+      size_t tb = pk.sort_tmp_bytes;
+      HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(pk.sort_tmp, tb, pk.ck_a, pk.ck_a2, (int)u, CanonLess(), st));
+      tb = pk.sort_tmp_bytes;
+      HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(pk.sort_tmp, tb, pk.ck_t, pk.ck_t2, (int)u, CanonLess(), st));
+      HIPCHK(hipMemsetAsync(pk.left_flag, 1, u, st));
+      HIPCHK(hipMemsetAsync(pk.counters, 0, 8 * sizeof(uint32_t), st));
+      HIPCHK(lookup_mark(pk.ck_a2, pk.ck_t2, u, pk.rep_flag, pk.left_flag, pk.counters + 2, st));
+      tb = pk.sort_tmp_bytes;
+      HIPCHK(hipcub::DeviceSelect::Flagged(pk.sort_tmp, tb, pk.ck_t2, pk.left_flag, pk.ck_left, pk.counters, (int)u,
+                                           st));
+      tb = pk.sort_tmp_bytes;
+      HIPCHK(hipcub::DeviceSelect::Flagged(pk.sort_tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), pk.rep_flag,
+                                           pk.rep_rows, pk.counters + 1, (int)u, st));
+      HIPCHK(lookup_assign(pk.ck_a2, pk.rep_flag, u, pk.lk_ap[l], pk.lk_sp[l], st));
+      HIPCHK(lookup_scatter(pk.ck_left, pk.rep_rows, pk.counters + 1, u, pk.lk_sp[l], st));
+      uint32_t cnt[3];
+      HIPCHK(hipMemcpyAsync(cnt, pk.counters, sizeof(cnt), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (cnt[2] != 0 || cnt[0] != cnt[1])
+        return fail(H2G_ERR_ARG, "create_proof: lookup input value not in the table (ConstraintSystemFailure)");
+      for (int which = 0; which < 2; which++) {  // bf+1 random rows: input first, then table
+        for (auto& v : rows) v = rng.random_fr();
+        HIPCHK(hipMemcpyAsync((which ? pk.lk_sp[l] : pk.lk_ap[l]) + u, rows.data(), rows.size() * sizeof(Fr),
+                              hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+      }
+      (void)rng.random_fr();  // permuted input blind
+      (void)rng.random_fr();  // permuted table blind
+      RCCHK(commit_launch(d, pk.lk_ap[l], n, prm.fgl, st, &tk[2 * l]));
+      RCCHK(commit_launch(d, pk.lk_sp[l], n, prm.fgl, st, &tk[2 * l + 1]));
+      RCCHK(lagrange_to_coeff(d, D, pk.lk_ap[l], pk.lk_ap_poly[l], st));
+      RCCHK(lagrange_to_coeff(d, D, pk.lk_sp[l], pk.lk_sp_poly[l], st));
+      RCCHK(coeff_to_extended(d, D, pk.lk_ap_poly[l], pk.lk_apc[l], st));
+      RCCHK(coeff_to_extended(d, D, pk.lk_sp_poly[l], pk.lk_spc[l], st));
+    }
+    for (int i = 0; i < 2 * pk.NL; i++) {
+      G1Affine cm;
+      RCCHK(commit_collect(d, &tk[i], &cm));
+      RCCHK(write_point(cm));
+    }
+  }
+  if (pk.NL) clk.mark("lookup permuted");
   const Fr beta = tr.squeeze(), gamma = tr.squeeze();
   dump("beta", &beta, 1, st, true);
   dump("gamma", &gamma, 1, st, true);
@@ -731,6 +944,39 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     }
   }
   clk.mark("permutation products");
+  // ---- lookup products (lookup/prover.rs:182-325), then shuffle products
+  // (shuffle/prover.rs:97-206): z = [1, running product ...], bf random rows, blind
+  std::vector<MsmTicket> lkz_tk(pk.NL), shz_tk(pk.NS);
+  {
+    std::vector<Fr> rows((size_t)bf);
+    auto finish_z = [&](Fr* z_lag, Fr* z_poly, Fr* z_coset, MsmTicket* t) -> int {
+      HIPCHK(poly_prefix_product(pk.mod, pk.pre, n, pk.scr, pk.scr_len, st));
+      for (auto& v : rows) v = rng.random_fr();
+      (void)rng.random_fr();  // product blind
+      HIPCHK(hipMemcpyAsync(pk.small, rows.data(), rows.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(perm_z_assemble(z_lag, n, bf, pk.pre, pk.one, pk.small, st));
+      RCCHK(commit_launch(d, z_lag, n, prm.fgl, st, t));
+      RCCHK(lagrange_to_coeff(d, D, z_lag, z_poly, st));
+      RCCHK(coeff_to_extended(d, D, z_poly, z_coset, st));
+      HIPCHK(hipStreamSynchronize(st));  // rows (host) is reused
+      return H2G_OK;
+    };
+    for (int l = 0; l < pk.NL; l++) {
+      HIPCHK(lookup_prod_den(pk.lk_ap[l], pk.lk_sp[l], beta, gamma, pk.mod, n, st));
+      HIPCHK(poly_batch_invert(pk.mod, n, pk.scr, st));
+      HIPCHK(lookup_prod_num(pk.lk_a[l], pk.lk_s[l], beta, gamma, pk.mod, n, st));
+      RCCHK(finish_z(pk.lk_z[l], pk.lk_z_poly[l], pk.lk_zc[l], &lkz_tk[l]));
+    }
+    for (int s = 0; s < pk.NS; s++) {
+      RCCHK(compress(pk.seg_sh_in[s], pk.tmp_a));
+      RCCHK(compress(pk.seg_sh_sh[s], pk.tmp_b));
+      HIPCHK(shuffle_prod_den(pk.tmp_b, gamma, pk.mod, n, st));
+      HIPCHK(poly_batch_invert(pk.mod, n, pk.scr, st));
+      HIPCHK(shuffle_prod_num(pk.tmp_a, gamma, pk.mod, n, st));
+      RCCHK(finish_z(pk.sh_z[s], pk.sh_z_poly[s], pk.sh_zc[s], &shz_tk[s]));
+    }
+  }
+  if (pk.NL + pk.NS) clk.mark("lookup/shuffle products");
   // ---- vanishing commit (vanishing/prover.rs:40-98)
   MsmTicket van_tk;
   {
@@ -764,6 +1010,16 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     RCCHK(commit_collect(d, &perm_tk[s], &cm));
     RCCHK(write_point(cm));
   }
+  for (int l = 0; l < pk.NL; l++) {
+    G1Affine cm;
+    RCCHK(commit_collect(d, &lkz_tk[l], &cm));
+    RCCHK(write_point(cm));
+  }
+  for (int s = 0; s < pk.NS; s++) {
+    G1Affine cm;
+    RCCHK(commit_collect(d, &shz_tk[s], &cm));
+    RCCHK(write_point(cm));
+  }
   {
     G1Affine cm;
     RCCHK(commit_collect(d, &van_tk, &cm));
@@ -774,8 +1030,13 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   {
     EvalHArgs a;
     a.prog = pk.prog;
-    a.prog_len = pk.prog_len;
+    a.gates = pk.seg_gates;
     a.n_slots = pk.n_slots;
+    a.theta = theta;
+    a.nlookups = pk.NL;
+    a.nshuffles = pk.NS;
+    a.lookups = pk.d_lookups;
+    a.shuffles = pk.d_shuffles;
     a.consts = pk.consts;
     a.query_col = pk.d_load_col;
     a.query_rot = pk.d_load_rot;
@@ -846,6 +1107,14 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   for (int c = 0; c < pk.F; c++) polys.push_back({pk.fixed_poly[c], n});
   for (int c = 0; c < pk.P; c++) polys.push_back({pk.sigma_poly[c], n});
   for (int s = 0; s < pk.nsets; s++) polys.push_back({pk.z[s], n});
+  const int id_lk = (int)polys.size();  // lookup l: z, A', S' at id_lk + 3 l
+  for (int l = 0; l < pk.NL; l++) {
+    polys.push_back({pk.lk_z_poly[l], n});
+    polys.push_back({pk.lk_ap_poly[l], n});
+    polys.push_back({pk.lk_sp_poly[l], n});
+  }
+  const int id_sh = (int)polys.size();
+  for (int s = 0; s < pk.NS; s++) polys.push_back({pk.sh_z_poly[s], n});
   const int id_h = (int)polys.size();
   polys.push_back({pk.h_poly, n});
   const int id_r = (int)polys.size();
@@ -863,6 +1132,19 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     queries.push_back({id_z + s, x_next});
   }
   for (int s = pk.nsets - 2; s >= 0; s--) queries.push_back({id_z + s, x_last});
+  const Fr x_prev = rotate_omega(D, x, -1);
+  for (int l = 0; l < pk.NL; l++) {  // lookup/prover.rs:364-405
+    const int zi = id_lk + 3 * l;
+    queries.push_back({zi, x});
+    queries.push_back({zi + 1, x});
+    queries.push_back({zi + 2, x});
+    queries.push_back({zi + 1, x_prev});
+    queries.push_back({zi, x_next});
+  }
+  for (int s = 0; s < pk.NS; s++) {  // shuffle/prover.rs:234-254
+    queries.push_back({id_sh + s, x});
+    queries.push_back({id_sh + s, x_next});
+  }
   for (auto& q : pk.fix_q) queries.push_back({id_fix + q.index, rotate_omega(D, x, q.rot)});
   for (int c = 0; c < pk.P; c++) queries.push_back({id_sig + c, x});
   queries.push_back({id_h, x});
@@ -905,6 +1187,18 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     tr.write_scalar(ev(id_z + s, x));
     tr.write_scalar(ev(id_z + s, x_next));
     if (s + 1 < pk.nsets) tr.write_scalar(ev(id_z + s, x_last));
+  }
+  for (int l = 0; l < pk.NL; l++) {  // product, product_next, A', A'_inv, S' (lookup/prover.rs:330-361)
+    const int zi = id_lk + 3 * l;
+    tr.write_scalar(ev(zi, x));
+    tr.write_scalar(ev(zi, x_next));
+    tr.write_scalar(ev(zi + 1, x));
+    tr.write_scalar(ev(zi + 1, x_prev));
+    tr.write_scalar(ev(zi + 2, x));
+  }
+  for (int s = 0; s < pk.NS; s++) {
+    tr.write_scalar(ev(id_sh + s, x));
+    tr.write_scalar(ev(id_sh + s, x_next));
   }
   clk.mark("evaluations");
 

@@ -35,14 +35,30 @@ hipError_t perm_z_assemble(Fr* z, size_t n, int bf, const Fr* prefix, const Fr* 
 hipError_t chacha_random_poly(Fr* out, size_t n, const uint32_t* d_seeds, const uint64_t* d_offsets, int chunks,
                               hipStream_t st);
 
-// ---- evaluate_h (evaluation.rs:317-483): gate program + permutation, fused / t(X) ----
+// ---- evaluate_h (evaluation.rs:317-620): expression programs + permutation + lookup +
+// shuffle constraint blocks, fused with the division by t(X) ----
 enum GateOp : int { G_LOAD = 0, G_CONST = 1, G_ADD = 2, G_SUB = 3, G_MUL = 4, G_NEG = 5, G_HORNER = 6 };
-// instruction: {op, dst slot, a, b}; G_LOAD: a = query index; G_CONST: a = constant index;
-// G_HORNER: acc = acc * y + slot[a]
+// instruction: {op, dst slot, a, b}; G_LOAD: a = load index; G_CONST: a = constant index;
+// G_HORNER: acc = acc * factor + slot[a] (factor y for gates, theta for lookup/shuffle
+// expression lists).  A program segment is int2 {offset, length} into the program array.
+struct EvalLookup {
+  int2 in, tab;  // compressed input / table expression programs
+  const Fr* z;   // product coset
+  const Fr* ap;  // permuted input coset
+  const Fr* sp;  // permuted table coset
+};
+struct EvalShuffle {
+  int2 in, sh;
+  const Fr* z;
+};
 struct EvalHArgs {
   const int4* prog = nullptr;
-  int prog_len = 0;
+  int2 gates = {0, 0};
   int n_slots = 0;
+  Fr theta;
+  int nlookups = 0, nshuffles = 0;
+  const EvalLookup* lookups = nullptr;    // device arrays
+  const EvalShuffle* shuffles = nullptr;
   const Fr* consts = nullptr;
   const Fr* const* query_col = nullptr;  // per query: column coset pointer
   const int* query_rot = nullptr;        // per query: rotation
@@ -64,6 +80,51 @@ struct EvalHArgs {
 };
 hipError_t evaluate_h(const EvalHArgs& a, hipStream_t st);
 int evaluate_h_max_slots();
+
+// Lagrange-basis compression of an expression list (lookup/prover.rs:85-103,
+// shuffle/prover.rs:45-66): out[i] = fold_e (acc * theta + e(row i)), rotations mod n
+struct CompressArgs {
+  const int4* prog = nullptr;
+  int2 seg = {0, 0};
+  int n_slots = 0;
+  const Fr* consts = nullptr;
+  const Fr* const* load_col = nullptr;  // Lagrange columns
+  const int* load_rot = nullptr;
+  uint64_t n = 0;
+  Fr theta;
+  Fr* out = nullptr;
+};
+hipError_t compress_lagrange(const CompressArgs& a, hipStream_t st);
+
+// ---- permute_expression_pair (lookup/prover.rs:410-494) building blocks ----
+struct CanonKey {  // canonical (non-Montgomery) value: Ord on Fr
+  uint32_t l[8];
+};
+struct CanonLess {
+  __host__ __device__ bool operator()(const CanonKey& a, const CanonKey& b) const {
+    for (int i = 7; i >= 0; i--)
+      if (a.l[i] != b.l[i]) return a.l[i] < b.l[i];
+    return false;
+  }
+};
+hipError_t fr_to_canon(const Fr* in, CanonKey* out, size_t n, hipStream_t st);
+// run starts of the sorted input; each distinct input value marks its first occurrence in
+// the sorted table (lower_bound); *fail counts input values missing from the table
+hipError_t lookup_mark(const CanonKey* a, const CanonKey* t, size_t u, uint8_t* rep_flag, uint8_t* left_flag,
+                       uint32_t* fail, hipStream_t st);
+// Ap[r] = a[r]; Sp[r] = a[r] at run starts
+hipError_t lookup_assign(const CanonKey* a, const uint8_t* rep_flag, size_t u, Fr* ap, Fr* sp, hipStream_t st);
+// Sp[R[nrep - 1 - i]] = L[i]  (BTreeMap order, repeated rows popped from the end)
+hipError_t lookup_scatter(const CanonKey* L, const uint32_t* R, const uint32_t* d_nrep, size_t cap, Fr* sp,
+                          hipStream_t st);
+// prod[i] = (beta + ap[i]) (gamma + sp[i])   and   prod[i] *= (a[i] + beta) (s[i] + gamma)
+hipError_t lookup_prod_den(const Fr* ap, const Fr* sp, const Fr& beta, const Fr& gamma, Fr* prod, size_t n,
+                           hipStream_t st);
+hipError_t lookup_prod_num(const Fr* a, const Fr* s, const Fr& beta, const Fr& gamma, Fr* prod, size_t n,
+                           hipStream_t st);
+// shuffle: prod[i] = gamma + s[i]   and   prod[i] *= gamma + a[i]
+hipError_t shuffle_prod_den(const Fr* s, const Fr& gamma, Fr* prod, size_t n, hipStream_t st);
+hipError_t shuffle_prod_num(const Fr* a, const Fr& gamma, Fr* prod, size_t n, hipStream_t st);
 
 // ---- polynomial evaluation (arithmetic.rs:57-82), batched ----
 struct EvalReq {

@@ -2,7 +2,7 @@
 //
 //   perm_*               permutation_commit     halo2_backend/src/plonk/permutation/prover.rs:103-171
 //   chacha_random_poly   vanishing commit       halo2_backend/src/plonk/vanishing/prover.rs:57-81
-//   evaluate_h           Evaluator::evaluate_h  halo2_backend/src/plonk/evaluation.rs:317-483
+//   evaluate_h           Evaluator::evaluate_h  halo2_backend/src/plonk/evaluation.rs:317-620
 //                        (+ divide_by_vanishing_poly domain.rs:297-316, fused)
 //   poly_eval_batch      eval_polynomial        halo2_backend/src/arithmetic.rs:57-82
 //   kate_division        kate_division          halo2_backend/src/arithmetic.rs:101-120
@@ -10,6 +10,7 @@
 //                        vanishing/prover.rs:166-176)
 //   sigma_from_mapping   permutation build_pk   halo2_backend/src/plonk/permutation/keygen.rs:139-170
 //   srs_lagrange_*       ParamsKZG::setup       halo2_backend/src/poly/kzg/commitment.rs:92-131
+//   compress / lookup_* / shuffle_*   lookup/prover.rs:64-494, shuffle/prover.rs:36-206
 //
 // Everything here is integer modular arithmetic on 32-byte Montgomery elements;
 // elementwise kernels are HBM-streaming grid-stride loops with 16-byte accesses.
@@ -119,48 +120,57 @@ static constexpr int EH_T = 64;
 static constexpr int EH_MAX_SLOTS = 24;
 int evaluate_h_max_slots() { return EH_MAX_SLOTS; }
 
+// run one program segment for row idx: Horner of its expression values with `factor`
+__device__ __forceinline__ Fr run_prog(const int4* __restrict__ prog, int2 seg, const Fr* __restrict__ consts,
+                                       const Fr* const* __restrict__ cols, const int* __restrict__ rots, uint64_t idx,
+                                       uint64_t rot_scale, uint64_t mask, Fr factor, Fr* sl, int lane) {
+  Fr acc = Fr::zero();
+  for (int pc = seg.x; pc < seg.x + seg.y; pc++) {
+    const int4 in = prog[pc];
+    Fr v;
+    switch (in.x) {
+      case G_LOAD: {
+        const uint64_t j = (idx + (uint64_t)((int64_t)rots[in.z] * (int64_t)rot_scale)) & mask;
+        v = ldf(cols[in.z] + j);
+        break;
+      }
+      case G_CONST: v = ldf(consts + in.z); break;
+      case G_ADD: v = sl[in.z * EH_T + lane] + sl[in.w * EH_T + lane]; break;
+      case G_SUB: v = sl[in.z * EH_T + lane] - sl[in.w * EH_T + lane]; break;
+      case G_MUL: v = sl[in.z * EH_T + lane] * sl[in.w * EH_T + lane]; break;
+      case G_NEG: v = neg(sl[in.z * EH_T + lane]); break;
+      default:  // G_HORNER
+        acc = acc * factor + sl[in.z * EH_T + lane];
+        continue;
+    }
+    sl[in.y * EH_T + lane] = v;
+  }
+  return acc;
+}
+
 __global__ void __launch_bounds__(EH_T) evaluate_h_kernel(EvalHArgs a) {
   extern __shared__ uint4 eh_lds[];
   Fr* sl = reinterpret_cast<Fr*>(eh_lds);
   const int lane = threadIdx.x;
   const uint64_t emask = a.ext - 1;
   for (uint64_t idx = blockIdx.x * (uint64_t)EH_T + lane; idx < a.ext; idx += (uint64_t)gridDim.x * EH_T) {
-    Fr acc = Fr::zero();
-    for (int pc = 0; pc < a.prog_len; pc++) {
-      const int4 in = a.prog[pc];
-      Fr v;
-      switch (in.x) {
-        case G_LOAD: {
-          const uint64_t j = (idx + (uint64_t)((int64_t)a.query_rot[in.z] * (int64_t)a.rot_scale)) & emask;
-          v = ldf(a.query_col[in.z] + j);
-          break;
-        }
-        case G_CONST: v = ldf(a.consts + in.z); break;
-        case G_ADD: v = sl[in.z * EH_T + lane] + sl[in.w * EH_T + lane]; break;
-        case G_SUB: v = sl[in.z * EH_T + lane] - sl[in.w * EH_T + lane]; break;
-        case G_MUL: v = sl[in.z * EH_T + lane] * sl[in.w * EH_T + lane]; break;
-        case G_NEG: v = neg(sl[in.z * EH_T + lane]); break;
-        default:  // G_HORNER
-          acc = acc * a.y + sl[in.z * EH_T + lane];
-          continue;
-      }
-      sl[in.y * EH_T + lane] = v;
-    }
+    Fr acc = run_prog(a.prog, a.gates, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, a.y, sl, lane);
+    const Fr l0 = ldf(a.l0 + idx);
+    const Fr ll = ldf(a.l_last + idx);
+    const Fr la = ldf(a.l_active + idx);
+    const uint64_t r_next = (idx + a.rot_scale) & emask;
     if (a.nsets > 0) {
-      const uint64_t r_next = (idx + a.rot_scale) & emask;
       const uint64_t r_last = (idx + (uint64_t)((int64_t)a.last_rot * (int64_t)a.rot_scale)) & emask;
-      const Fr l0 = ldf(a.l0 + idx);
       // l_0(X) * (1 - z_0(X))
       acc = acc * a.y + (Fr::one() - ldf(a.z[0] + idx)) * l0;
       // l_last(X) * (z_l(X)^2 - z_l(X))
       {
         const Fr zl = ldf(a.z[a.nsets - 1] + idx);
-        acc = acc * a.y + (zl * zl - zl) * ldf(a.l_last + idx);
+        acc = acc * a.y + (zl * zl - zl) * ll;
       }
       // l_0(X) * (z_i(X) - z_{i-1}(omega^(last) X))
       for (int s = 1; s < a.nsets; s++) acc = acc * a.y + (ldf(a.z[s] + idx) - ldf(a.z[s - 1] + r_last)) * l0;
       // l_active(X) * (z_i(omega X) prod(p + beta sigma + gamma) - z_i(X) prod(p + delta^j beta X + gamma))
-      const Fr la = ldf(a.l_active + idx);
       Fr cur = a.delta_start * pw(a.ext_omega, idx);
       for (int s = 0; s < a.nsets; s++) {
         const int c0 = s * a.chunk_len;
@@ -176,6 +186,35 @@ __global__ void __launch_bounds__(EH_T) evaluate_h_kernel(EvalHArgs a) {
         acc = acc * a.y + (left - right) * la;
       }
     }
+    if (a.nlookups + a.nshuffles > 0) {
+      const uint64_t r_prev = (idx - a.rot_scale) & emask;
+      for (int l = 0; l < a.nlookups; l++) {  // evaluation.rs:486-558
+        const EvalLookup lk = a.lookups[l];
+        const Fr ci = run_prog(a.prog, lk.in, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, a.theta,
+                               sl, lane);
+        const Fr ct = run_prog(a.prog, lk.tab, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, a.theta,
+                               sl, lane);
+        const Fr table_value = (ci + a.beta) * (ct + a.gamma);
+        const Fr z = ldf(lk.z + idx), ap = ldf(lk.ap + idx), sp = ldf(lk.sp + idx);
+        const Fr ams = ap - sp;
+        acc = acc * a.y + (Fr::one() - z) * l0;
+        acc = acc * a.y + (z * z - z) * ll;
+        acc = acc * a.y + (ldf(lk.z + r_next) * (ap + a.beta) * (sp + a.gamma) - z * table_value) * la;
+        acc = acc * a.y + ams * l0;
+        acc = acc * a.y + ams * (ap - ldf(lk.ap + r_prev)) * la;
+      }
+      for (int s = 0; s < a.nshuffles; s++) {  // evaluation.rs:561-620
+        const EvalShuffle sh = a.shuffles[s];
+        const Fr ci = run_prog(a.prog, sh.in, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, a.theta,
+                               sl, lane) + a.gamma;
+        const Fr cs = run_prog(a.prog, sh.sh, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, a.theta,
+                               sl, lane) + a.gamma;
+        const Fr z = ldf(sh.z + idx);
+        acc = acc * a.y + (Fr::one() - z) * l0;
+        acc = acc * a.y + (z * z - z) * ll;
+        acc = acc * a.y + la * (ldf(sh.z + r_next) * cs - z * ci);
+      }
+    }
     stf(a.out + idx, acc * ldf(a.t_evals + (idx & a.t_mask)));
   }
 }
@@ -186,6 +225,151 @@ hipError_t evaluate_h(const EvalHArgs& a, hipStream_t st) {
   size_t blocks = (a.ext + EH_T - 1) / EH_T;
   if (blocks > 256 * 32) blocks = 256 * 32;
   hipLaunchKernelGGL(evaluate_h_kernel, dim3((unsigned)blocks), dim3(EH_T), lds, st, a);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(EH_T) compress_kernel(CompressArgs a) {
+  extern __shared__ uint4 eh_lds[];
+  Fr* sl = reinterpret_cast<Fr*>(eh_lds);
+  const int lane = threadIdx.x;
+  const uint64_t mask = a.n - 1;
+  for (uint64_t i = blockIdx.x * (uint64_t)EH_T + lane; i < a.n; i += (uint64_t)gridDim.x * EH_T)
+    stf(a.out + i, run_prog(a.prog, a.seg, a.consts, a.load_col, a.load_rot, i, 1, mask, a.theta, sl, lane));
+}
+
+hipError_t compress_lagrange(const CompressArgs& a, hipStream_t st) {
+  if (a.n_slots > EH_MAX_SLOTS) return hipErrorInvalidValue;
+  const size_t lds = (size_t)(a.n_slots > 0 ? a.n_slots : 1) * EH_T * sizeof(Fr);
+  size_t blocks = (a.n + EH_T - 1) / EH_T;
+  if (blocks > 256 * 32) blocks = 256 * 32;
+  hipLaunchKernelGGL(compress_kernel, dim3((unsigned)blocks), dim3(EH_T), lds, st, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ lookups / shuffles
+__global__ void __launch_bounds__(KT) canon_kernel(const Fr* __restrict__ in, CanonKey* __restrict__ out, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const Fr c = to_canonical(ldf(in + i));
+    CanonKey k;
+#pragma unroll
+    for (int j = 0; j < 8; j++) k.l[j] = c.l[j];
+    out[i] = k;
+  }
+}
+hipError_t fr_to_canon(const Fr* in, CanonKey* out, size_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(canon_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, in, out, n);
+  return hipGetLastError();
+}
+
+__device__ __forceinline__ bool ck_eq(const CanonKey& a, const CanonKey& b) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x |= a.l[i] ^ b.l[i];
+  return x == 0;
+}
+
+__global__ void __launch_bounds__(KT) lookup_mark_kernel(const CanonKey* __restrict__ a, const CanonKey* __restrict__ t,
+                                                         size_t u, uint8_t* __restrict__ rep_flag,
+                                                         uint8_t* __restrict__ left_flag, uint32_t* __restrict__ fail) {
+  for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < u; r += (size_t)gridDim.x * blockDim.x) {
+    const CanonKey v = a[r];
+    const bool start = r == 0 || !ck_eq(v, a[r - 1]);
+    rep_flag[r] = start ? 0 : 1;
+    if (!start) continue;
+    size_t lo = 0, hi = u;  // lower_bound
+    const CanonLess less;
+    while (lo < hi) {
+      const size_t mid = (lo + hi) >> 1;
+      if (less(t[mid], v)) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo < u && ck_eq(t[lo], v)) left_flag[lo] = 0;
+    else atomicAdd(fail, 1u);
+  }
+}
+hipError_t lookup_mark(const CanonKey* a, const CanonKey* t, size_t u, uint8_t* rep_flag, uint8_t* left_flag,
+                       uint32_t* fail, hipStream_t st) {
+  if (u == 0) return hipSuccess;
+  hipLaunchKernelGGL(lookup_mark_kernel, dim3(grid_1d(u)), dim3(KT), 0, st, a, t, u, rep_flag, left_flag, fail);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(KT) lookup_assign_kernel(const CanonKey* __restrict__ a,
+                                                           const uint8_t* __restrict__ rep_flag, size_t u,
+                                                           Fr* __restrict__ ap, Fr* __restrict__ sp) {
+  for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < u; r += (size_t)gridDim.x * blockDim.x) {
+    Fr c;
+#pragma unroll
+    for (int j = 0; j < 8; j++) c.l[j] = a[r].l[j];
+    const Fr m = from_canonical(c);
+    stf(ap + r, m);
+    if (!rep_flag[r]) stf(sp + r, m);
+  }
+}
+hipError_t lookup_assign(const CanonKey* a, const uint8_t* rep_flag, size_t u, Fr* ap, Fr* sp, hipStream_t st) {
+  if (u == 0) return hipSuccess;
+  hipLaunchKernelGGL(lookup_assign_kernel, dim3(grid_1d(u)), dim3(KT), 0, st, a, rep_flag, u, ap, sp);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(KT) lookup_scatter_kernel(const CanonKey* __restrict__ L,
+                                                            const uint32_t* __restrict__ R,
+                                                            const uint32_t* __restrict__ d_nrep, size_t cap,
+                                                            Fr* __restrict__ sp) {
+  const size_t nrep = *d_nrep;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nrep && i < cap;
+       i += (size_t)gridDim.x * blockDim.x) {
+    Fr c;
+#pragma unroll
+    for (int j = 0; j < 8; j++) c.l[j] = L[i].l[j];
+    stf(sp + R[nrep - 1 - i], from_canonical(c));
+  }
+}
+hipError_t lookup_scatter(const CanonKey* L, const uint32_t* R, const uint32_t* d_nrep, size_t cap, Fr* sp,
+                          hipStream_t st) {
+  if (cap == 0) return hipSuccess;
+  hipLaunchKernelGGL(lookup_scatter_kernel, dim3(grid_1d(cap)), dim3(KT), 0, st, L, R, d_nrep, cap, sp);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(KT) lk_den_kernel(const Fr* __restrict__ ap, const Fr* __restrict__ sp, Fr beta,
+                                                    Fr gamma, Fr* __restrict__ prod, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    stf(prod + i, (beta + ldf(ap + i)) * (gamma + ldf(sp + i)));
+}
+__global__ void __launch_bounds__(KT) lk_num_kernel(const Fr* __restrict__ a, const Fr* __restrict__ s, Fr beta,
+                                                    Fr gamma, Fr* __restrict__ prod, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    stf(prod + i, ldf(prod + i) * (ldf(a + i) + beta) * (ldf(s + i) + gamma));
+}
+hipError_t lookup_prod_den(const Fr* ap, const Fr* sp, const Fr& beta, const Fr& gamma, Fr* prod, size_t n,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(lk_den_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, ap, sp, beta, gamma, prod, n);
+  return hipGetLastError();
+}
+hipError_t lookup_prod_num(const Fr* a, const Fr* s, const Fr& beta, const Fr& gamma, Fr* prod, size_t n,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(lk_num_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, a, s, beta, gamma, prod, n);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(KT) sh_den_kernel(const Fr* __restrict__ s, Fr gamma, Fr* __restrict__ prod,
+                                                    size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    stf(prod + i, gamma + ldf(s + i));
+}
+__global__ void __launch_bounds__(KT) sh_num_kernel(const Fr* __restrict__ a, Fr gamma, Fr* __restrict__ prod,
+                                                    size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    stf(prod + i, ldf(prod + i) * (gamma + ldf(a + i)));
+}
+hipError_t shuffle_prod_den(const Fr* s, const Fr& gamma, Fr* prod, size_t n, hipStream_t st) {
+  hipLaunchKernelGGL(sh_den_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, s, gamma, prod, n);
+  return hipGetLastError();
+}
+hipError_t shuffle_prod_num(const Fr* a, const Fr& gamma, Fr* prod, size_t n, hipStream_t st) {
+  hipLaunchKernelGGL(sh_num_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, a, gamma, prod, n);
   return hipGetLastError();
 }
 

@@ -415,6 +415,8 @@ class H2gCircuit(ctypes.Structure):
         ("num_copies", U32), ("copies", I32P_),
         ("fixed_values", U64P), ("unblinded", ctypes.POINTER(ctypes.c_uint8)),
         ("transcript_repr", U64P),
+        ("num_lookups", U32), ("lookup_sizes", ctypes.POINTER(U32)), ("lookup_roots", I32P_),
+        ("num_shuffles", U32), ("shuffle_sizes", ctypes.POINTER(U32)), ("shuffle_roots", I32P_),
     ]
 
 
@@ -458,13 +460,16 @@ class ProvingKey:
         self.circ = circ
         keep = [np.ascontiguousarray(x) for x in (circ.gate_roots, circ.nodes, circ.constants, circ.perm_array,
                                                   circ.copies, circ.fixed_values, circ.unblinded,
-                                                  circ.transcript_repr())]
-        roots, nodes, consts, perm, copies, fixed, unb, tr = keep
+                                                  circ.transcript_repr(), circ.lookup_sizes, circ.lookup_roots,
+                                                  circ.shuffle_sizes, circ.shuffle_roots)]
+        roots, nodes, consts, perm, copies, fixed, unb, tr, lks, lkr, shs, shr = keep
         c = H2gCircuit(circ.k, circ.num_advice, circ.num_fixed, circ.num_instance,
                        len(roots), _ptr(roots, I32P_), len(nodes), _ptr(nodes, I32P_),
                        circ.num_constants, _ptr(consts, U64P), len(perm), _ptr(perm, I32P_),
                        len(copies), _ptr(copies, I32P_), _ptr(fixed, U64P),
-                       _ptr(unb, ctypes.POINTER(ctypes.c_uint8)), _ptr(tr, U64P))
+                       _ptr(unb, ctypes.POINTER(ctypes.c_uint8)), _ptr(tr, U64P),
+                       len(circ.lookups), _ptr(lks, ctypes.POINTER(U32)), _ptr(lkr, I32P_),
+                       len(circ.shuffles), _ptr(shs, ctypes.POINTER(U32)), _ptr(shr, I32P_))
         h = U64()
         check(lib().h2g_keygen(params.handle, ctypes.byref(c), ctypes.byref(h)))
         self.handle = h.value
@@ -485,7 +490,8 @@ class ProvingKey:
             adv_p, on_dev = VP(adv.ctypes.data) if adv.size else None, 0
         ins = np.ascontiguousarray(wit.instance, dtype=np.uint64) if circ.num_instance else np.zeros(4, np.uint64)
         lens = np.ascontiguousarray(wit.instance_lens if circ.num_instance else np.zeros(1), dtype=np.uint32)
-        cap = 32 * (64 + 8 * (circ.num_advice + circ.num_fixed + 4 * len(circ.perm_columns)) + 64 * 64)
+        cap = 32 * (64 + 8 * (circ.num_advice + circ.num_fixed + 4 * len(circ.perm_columns)) + 64 * 64
+                    + 16 * (len(circ.lookups) + len(circ.shuffles)))
         buf = ctypes.create_string_buffer(cap)
         ln = SZ()
         check(lib().h2g_create_proof(self.params.handle, self.handle, adv_p, on_dev, p64(ins),
