@@ -51,6 +51,8 @@ CASES = {
     "c3_k12": lambda: hc.synthetic_c3(12, O.OracleOps, seed=9),
     "lookup_k8": lambda: hc.lookup_circuit(8),
     "lookup_k11": lambda: hc.lookup_circuit(11, seed=8),
+    "keccak_k9": lambda: hc.keccak_style(9, words=8),
+    "keccak_k12": lambda: hc.keccak_style(12, words=16, seed=9),
 }
 
 

@@ -68,6 +68,7 @@ CIRCUITS = {
     "c3_k8": lambda: hc.synthetic_c3(8, O.OracleOps),
     "lookup_k8": lambda: hc.lookup_circuit(8),
     "lookup_k9": lambda: hc.lookup_circuit(9, seed=6),
+    "keccak_k9": lambda: hc.keccak_style(9, words=5),
 }
 
 

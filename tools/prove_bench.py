@@ -1,5 +1,6 @@
-"""Time the device create_proof on the C3 synthetic circuit at the given
-k values; prints per-stage wall times.  usage: python tools/prove_bench.py 20 22"""
+"""Time the device create_proof on the C3 synthetic circuit or the C5-shaped
+keccak-style circuit at the given k values; prints per-stage wall times.
+usage: python tools/prove_bench.py [c3|keccak] 20 22"""
 import os
 import sys
 import time
@@ -13,11 +14,15 @@ import h2g_circuit as hc  # noqa: E402
 
 
 def main():
-    ks = [int(a) for a in sys.argv[1:]] or [20]
+    args = sys.argv[1:]
+    kind = "c3"
+    if args and not args[0].isdigit():
+        kind = args.pop(0)
+    ks = [int(a) for a in args] or [20]
     h2g.init()
     for k in ks:
         t0 = time.time()
-        circ, wit = hc.synthetic_c3(k, h2g.DeviceOps)
+        circ, wit = hc.synthetic_c3(k, h2g.DeviceOps) if kind == "c3" else hc.keccak_style(k)
         t1 = time.time()
         params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(0x1234567 + k), dtype=np.uint64))
         t2 = time.time()

@@ -477,3 +477,59 @@ def random_mont(rng, count):
     x += rng.integers(0, 2, size=(count, 4), dtype=np.int64).astype(np.uint64)
     x[:, 3] %= np.uint64(0x30644E72E131A029)
     return x
+
+
+def keccak_style(k, words=16, seed=5):
+    """C5-shaped circuit (BASELINE configs[4]: many advice columns + lookup arguments, the
+    shape of keccak's nibble-xor tables): advice x_0..x_{W-1}, y_0..y_{W-1}; fixed q, qc,
+    Ta, Tb, Tc with (Ta, Tb, Tc) = (a, b, a ^ b) over 4-bit nibbles; W lookups
+    [q x_i, q x_{i+1 mod W}, q y_i] in [Ta, Tb, Tc] (y_i = x_i ^ x_{i+1}, degree 5 ->
+    extended domain 4n); gate qc (x_0[next] - y_0) (a xor chain down x_0); permutation
+    over y_0, x_4 with copies y_0[r] = x_4[r] every 5th row.  Witness generation is
+    vectorised (numpy), so k = 18 builds in seconds."""
+    n = 1 << k
+    W = words
+    assert W >= 5
+    X = list(range(W))
+    Y = list(range(W, 2 * W))
+    Q, QC, TA, TB, TC = range(5)
+    lookups = [([fixed(Q) * advice(X[i]), fixed(Q) * advice(X[(i + 1) % W]), fixed(Q) * advice(Y[i])],
+                [fixed(TA), fixed(TB), fixed(TC)]) for i in range(W)]
+    gates = [fixed(QC) * (advice(X[0], 1) - advice(Y[0]))]
+    perm = [(ADVICE, Y[0]), (ADVICE, X[4])]
+    probe = Circuit(k, 2 * W, 5, 0, gates, perm, [], np.zeros((5, n, 4), np.uint64), lookups=lookups)
+    u = probe.usable_rows()
+    assert u >= 256, "the nibble-xor table needs 256 usable rows"
+    rng = np.random.default_rng(seed)
+    x = rng.integers(0, 16, size=(W, n), dtype=np.int64)
+    x[:, u:] = 0
+    # x_0 chain: x0[r+1] = x0[r] ^ x1[r] for r < u - 1
+    acc = np.bitwise_xor.accumulate(x[1, : u - 1])
+    x[0, 1:u] = x[0, 0] ^ acc
+    y = np.zeros_like(x)
+    rows_c = np.arange(0, u, 5)
+    for i in range(W):
+        if i == 4:  # copies: x_4 = y_0 on the copy rows (y_0 is final by now)
+            x[4, rows_c] = y[0, rows_c]
+        if i < W - 1:
+            y[i, :u] = x[i, :u] ^ x[i + 1, :u]
+    y[3, :u] = x[3, :u] ^ x[4, :u]
+    y[W - 1, :u] = x[W - 1, :u] ^ x[0, :u]
+    small = ints_to_mont(list(range(16)))
+    adv = np.concatenate([small[x], small[y]], axis=0)
+    q = np.zeros(n, np.int64)
+    q[:u] = 1
+    qc = np.zeros(n, np.int64)
+    qc[: u - 1] = 1
+    r = np.arange(n)
+    ta = np.where(r < u, r % 16, 0)
+    tb = np.where(r < u, (r // 16) % 16, 0)
+    tc = ta ^ tb
+    fixed_vals = np.stack([small[q], small[qc], small[ta], small[tb], small[tc]])
+    copies = np.stack([np.full(len(rows_c), ADVICE, np.int32), np.full(len(rows_c), Y[0], np.int32),
+                       rows_c.astype(np.int32), np.full(len(rows_c), ADVICE, np.int32),
+                       np.full(len(rows_c), X[4], np.int32), rows_c.astype(np.int32)], axis=1)
+    circ = Circuit(k, 2 * W, 5, 0, gates, perm, copies, fixed_vals, name=f"keccak-style k={k} W={W}",
+                   lookups=lookups)
+    wit = Witness(adv, np.zeros((0, n, 4), np.uint64), [])
+    return circ, wit
