@@ -17,6 +17,10 @@ struct NttTables {
   int b = 0;  // split of the 2-level table
   Fr* lo = nullptr;
   Fr* hi = nullptr;
+  // precomputed inter-pass twiddles of the non-last passes: pass p's table holds
+  // w^((N/L_p) i_low k) at [k * S_p + i_low] (L_p entries; sum over passes ~ 1.1 N)
+  Fr* pass_tw = nullptr;
+  uint64_t pass_off[NTT_MAX_PASSES] = {0, 0, 0, 0, 0, 0};
 };
 
 // One transform y = DFT_w(x) of size N = 2^tab.L with fused maps:

@@ -137,8 +137,8 @@ struct WaveDif {
 //   `distribute`, multiplies element i by zeta^(i mod 3) (domain.rs:325-341).
 template <int M>
 __global__ void __launch_bounds__(NTT_THREADS, NTT_MIN_WAVES)
-ntt_pass_kernel(Fr* data, const Fr* in, uint64_t n_in, NttTables tab, int L, int lrem, int distribute, Fr z1,
-                Fr z2) {
+ntt_pass_kernel(Fr* data, const Fr* in, uint64_t n_in, NttTables tab, const Fr* __restrict__ ptw, int L, int lrem,
+                int distribute, Fr z1, Fr z2) {
   using D = WaveDif<M>;
   __shared__ Fr w[1 << (M - 1)];
   for (int j = threadIdx.x; j < (1 << (M - 1)); j += blockDim.x) w[j] = twiddle(tab, (uint64_t)j << (L - M));
@@ -172,13 +172,13 @@ ntt_pass_kernel(Fr* data, const Fr* in, uint64_t n_in, NttTables tab, int L, int
     }
   }
   D::run(x, w, rg);
-  const uint64_t ilow_scaled = (g * D::CPW + c) << (L - lrem);  // (N / L_p) * i_low
+  const uint64_t ilow = g * D::CPW + c;
 #pragma unroll
   for (int qq = 0; qq < 8; qq++) {
     const uint32_t k = brev_bits(D::rpos(qq, rg), M);
-    const uint64_t e = ilow_scaled * k;
-    Fr v = x[qq];
-    if (e) v = v * twiddle(tab, e);
+    // w^((N / L_p) i_low k) from the precomputed pass table (one load instead of a
+    // table product + multiplication)
+    const Fr v = x[qq] * ld_fr(ptw + (uint64_t)k * S + ilow);
     st_fr(data + base + c + (uint64_t)k * S, v);
   }
 }
@@ -303,6 +303,15 @@ __global__ void ntt_tables_kernel(Fr* lo, Fr* hi, Fr w, int b, int L) {
   }
 }
 
+// pass table: t = k * S + i_low over [0, 2^lrem): w^(i_low k 2^(L - lrem))
+__global__ void ntt_pass_tw_kernel(Fr* out, NttTables tab, int L, int lrem, int M) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t >= (1ull << lrem)) return;
+  const uint64_t S = 1ull << (lrem - M);
+  const uint64_t k = t / S, ilow = t % S;
+  out[t] = twiddle(tab, (ilow * k) << (L - lrem));
+}
+
 // ---------------------------------------------------------------------------
 // Host side
 
@@ -338,13 +347,34 @@ hipError_t ntt_build_tables(NttTables* t, const Fr& omega, int L, hipStream_t st
   const int bs = 256;
   hipLaunchKernelGGL(ntt_tables_kernel, dim3((unsigned)((mx + bs - 1) / bs)), dim3(bs), 0, st, t->lo, t->hi,
                      omega, t->b, L < t->b ? t->b : L);
+  e = hipGetLastError();
+  if (e != hipSuccess || L <= NTT_SMALL_MAX_LOG) return e;
+  int P, lg[NTT_MAX_PASSES];
+  ntt_split(L, &P, lg);
+  uint64_t total = 0;
+  int lrem = L;
+  for (int p = 0; p < P - 1; p++) {
+    t->pass_off[p] = total;
+    total += 1ull << lrem;
+    lrem -= lg[p];
+  }
+  e = hipMalloc(&t->pass_tw, (total ? total : 1) * sizeof(Fr));
+  if (e != hipSuccess) return e;
+  lrem = L;
+  for (int p = 0; p < P - 1; p++) {
+    const uint64_t cnt = 1ull << lrem;
+    hipLaunchKernelGGL(ntt_pass_tw_kernel, dim3((unsigned)((cnt + bs - 1) / bs)), dim3(bs), 0, st,
+                       t->pass_tw + t->pass_off[p], *t, L, lrem, lg[p]);
+    lrem -= lg[p];
+  }
   return hipGetLastError();
 }
 
 void ntt_free_tables(NttTables* t) {
   if (t->lo) (void)hipFree(t->lo);
   if (t->hi) (void)hipFree(t->hi);
-  t->lo = t->hi = nullptr;
+  if (t->pass_tw) (void)hipFree(t->pass_tw);
+  t->lo = t->hi = t->pass_tw = nullptr;
 }
 
 hipError_t ntt_init_attributes() {
@@ -353,13 +383,13 @@ hipError_t ntt_init_attributes() {
 }
 
 template <int M>
-static void launch_pass(const NttArgs& a, Fr* data, const Fr* in, uint64_t n_in, int L, int lrem, int dist,
+static void launch_pass(const NttArgs& a, int p, Fr* data, const Fr* in, uint64_t n_in, int L, int lrem, int dist,
                         hipStream_t st) {
   const uint64_t N = 1ull << L;
   const uint64_t waves = N / ((1ull << M) * WaveDif<M>::CPW);
   const unsigned blocks = (unsigned)((waves + NTT_WAVES - 1) / NTT_WAVES);
-  hipLaunchKernelGGL(ntt_pass_kernel<M>, dim3(blocks), dim3(NTT_THREADS), 0, st, data, in, n_in, a.tab, L, lrem,
-                     dist, a.in_z1, a.in_z2);
+  hipLaunchKernelGGL(ntt_pass_kernel<M>, dim3(blocks), dim3(NTT_THREADS), 0, st, data, in, n_in, a.tab,
+                     (const Fr*)(a.tab.pass_tw + a.tab.pass_off[p]), L, lrem, dist, a.in_z1, a.in_z2);
 }
 
 hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
@@ -377,7 +407,7 @@ hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
                        a.out_z2);
     return hipGetLastError();
   }
-  if (P > NTT_MAX_PASSES || lg[P - 1] != 6) return hipErrorInvalidValue;
+  if (P > NTT_MAX_PASSES || lg[P - 1] != 6 || !a.tab.pass_tw) return hipErrorInvalidValue;
   // epilogue multiplier per (y mod 3): scale * zeta-power, folded on the host
   const int has_mul = a.has_scale || a.out_distribute;
   Fr mul[3];
@@ -396,10 +426,10 @@ hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
     const uint64_t nin = p == 0 ? a.n_in : 0;
     const int dist = p == 0 ? a.in_distribute : 0;
     switch (lg[p]) {
-      case 3: launch_pass<3>(a, a.work, in, nin, L, lrem, dist, st); break;
-      case 4: launch_pass<4>(a, a.work, in, nin, L, lrem, dist, st); break;
-      case 5: launch_pass<5>(a, a.work, in, nin, L, lrem, dist, st); break;
-      case 6: launch_pass<6>(a, a.work, in, nin, L, lrem, dist, st); break;
+      case 3: launch_pass<3>(a, p, a.work, in, nin, L, lrem, dist, st); break;
+      case 4: launch_pass<4>(a, p, a.work, in, nin, L, lrem, dist, st); break;
+      case 5: launch_pass<5>(a, p, a.work, in, nin, L, lrem, dist, st); break;
+      case 6: launch_pass<6>(a, p, a.work, in, nin, L, lrem, dist, st); break;
       default: return hipErrorInvalidValue;
     }
     lrem -= lg[p];
