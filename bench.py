@@ -9,9 +9,11 @@ c_i -> a_{i+1}) through the C ABI (h2g_create_proof), witness resident in HBM wh
 timed region starts.  value = wall-seconds per proof (lower is better).  The proof
 bytes of this exact pipeline are tested identical to the CPU restatement prover
 (tests/test_gpu_prover.py).
-N > 1 (torchrun, one process per GPU): every rank proves its own instance (the path
-does not shard a single proof yet -- replicas); value = max-over-ranks wall time /
-(steps * N), "scaling": "weak".
+N > 1 (torchrun, one process per GPU), --mode shard (default): ONE proof at a time
+over all ranks -- rank 0 runs the prover, every commitment MSM is split into point
+slabs and ranks 1.. compute theirs (h2g_dist: RCCL p2p slabs + partials, SURVEY 8e);
+value = max-over-ranks wall time / steps, "scaling": "strong".  --mode replicas:
+every rank proves its own instance; value = max-over-ranks time / (steps * N), "weak".
 
 --workload msm: one step = one MSM of 2^24 resident (scalar, SRS point) pairs
 (h2g_msm_dev_host); N > 1 shards point slabs and all_gathers the 64-B partials (RCCL).
@@ -190,10 +192,10 @@ def pmc_child(args):
 
 
 # ----------------------------------------------------------------------------- roofline
-def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note):
+def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note, window_bits=0):
     acc_ms = phases.get("accumulate", 0.0) / max(calls, 1)
     achieved = (points_per_launch * MSM_BYTES_PER_POINT) / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
-    c = fixed_c(points_per_launch)
+    c = window_bits or fixed_c(points_per_launch)
     W = (255 + c - 1) // c
     modmul_rate = (points_per_launch * W * MADD_MODMUL) / (acc_ms * 1e-3) if acc_ms > 0 else None
     return {
@@ -221,6 +223,8 @@ def max_over_ranks(elapsed, dist, world, device):
     if world == 1:
         return elapsed
     import torch
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
@@ -230,6 +234,8 @@ def gather_partials(part, dist, world, device):
     """all_gather of the per-rank MSM partial sums (64-B affine points; RCCL has no
     EC-add reduction) -> list of numpy uint64[8]"""
     import torch
+    if dist.get_backend() == "gloo":
+        device = "cpu"
     t = torch.from_numpy(np.ascontiguousarray(part, dtype=np.uint64).view(np.int64)).to(device)
     gathered = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(gathered, t)
@@ -247,33 +253,65 @@ def combine_partials(parts, add):
 # ----------------------------------------------------------------------------- workloads
 def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     import h2g_circuit as hc
+    import h2g_dist
 
     k = args.k
     n = 1 << k
-    circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=3 + rank)
-    params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(0x1234567 + rank), dtype=np.uint64))
-    pk = h2g.ProvingKey(params, circ)
-    adv = torch.from_numpy(np.ascontiguousarray(wit.advice).view(np.int64)).to(dev)  # resident witness
+    shard = world > 1 and args.mode == "shard"
+    worker = shard and rank != 0
+    seed_off = 0 if shard else rank  # sharded ranks hold the same SRS
+    params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(0x1234567 + seed_off), dtype=np.uint64))
+    if shard:  # fixed-base windows sized for this rank's point slab
+        params.set_slab(*h2g_dist.slab(n, world, rank))
+    if worker:
+        slabs = h2g_dist.SlabWorker(dist, params=params)
+    else:
+        circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=3 + seed_off)
+        pk = h2g.ProvingKey(params, circ)
+        adv = torch.from_numpy(np.ascontiguousarray(wit.advice).view(np.int64)).to(dev)  # resident witness
+        client = h2g_dist.SlabClient(dist, points=n) if shard else None
     torch.cuda.synchronize()
     proofs = []
 
     def step():
         proofs.append(pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr()))
 
-    for _ in range(args.warmup):
-        step()
-    # PCIe-inclusive variant (advice handed over in host memory), reported beside value
-    t0 = time.perf_counter()
-    pk.create_proof(wit)
-    pcie_s = time.perf_counter() - t0
+    def session(body):
+        """rank 0 proves with the slab transport installed; peers serve until it stops"""
+        if worker:
+            slabs.serve()
+            return
+        if client:
+            client.install()
+        try:
+            body()
+        finally:
+            if client:
+                client.uninstall()
+                client.stop()
+
+    pcie = {}
+
+    def warm():
+        for _ in range(args.warmup):
+            step()
+        # PCIe-inclusive variant (advice handed over in host memory), reported beside value
+        t0 = time.perf_counter()
+        pk.create_proof(wit)
+        pcie["s"] = time.perf_counter() - t0
+
+    def timed():
+        for _ in range(args.steps):
+            step()
+
+    session(warm)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     h2g.profile_enable(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    session(timed)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -282,21 +320,22 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     calls, phases = h2g.profile_msm_collect()
     stages = h2g.prover_stages()
     elapsed = max_over_ranks(elapsed, dist, world, dev)
-    assert all(p == proofs[0] for p in proofs), "non-deterministic proof bytes"
     line = None
     if rank == 0:
+        assert all(p == proofs[0] for p in proofs), "non-deterministic proof bytes"
         ms_per_step = elapsed / args.steps * 1e3
         msm_ms = sum(phases.values()) / max(calls, 1)
+        n_local = h2g_dist.slab(n, world, 1)[0] if shard else n  # rank 0's points per MSM
         line = {
             "metric": METRIC,
-            "value": round(elapsed / (args.steps * world), 4),
+            "value": round(elapsed / (args.steps * (1 if shard else world)), 4),
             "unit": "s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": False,
-            "scaling": "weak",
+            "scaling": "strong" if shard else "weak",
             "vs_baseline": None,
             "dtype": "u32 limbs (BN254 Fr/Fq Montgomery, 256-bit modular integer)",
             "data": "synthetic C3 witness (random b, a_0; a_{i+1} = c_i = a_i b_i), SRS from a fixed s generated "
@@ -305,15 +344,20 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                                    "(BASELINE configs[2]/[3])",
                        "k": k, "advice": 3, "fixed": 1, "permutation_columns": 3, "degree": pk.degree,
                        "extended_k": pk.extended_k, "proof_bytes": len(proofs[0]),
-                       "parallelism": "single GPU per proof" if world == 1 else f"{world} independent provers"},
-            "roofline": roofline_from_phases(calls, phases, n, traffic, traffic_note),
+                       "parallelism": ("single GPU per proof" if world == 1 else
+                                       f"one proof over {world} GPUs: commitment MSMs in point slabs (RCCL p2p "
+                                       "slabs + partials), NTT/evaluate_h/SHPLONK on rank 0" if shard else
+                                       f"{world} independent provers")},
+            "roofline": roofline_from_phases(calls, phases, n_local, traffic, traffic_note),
             "msm_in_prover": {"launches_per_proof": calls // max(args.steps, 1), "avg_ms": round(msm_ms, 4),
-                              "mscalar_mul_per_s": round(n / (msm_ms * 1e-3) / 1e6, 2) if msm_ms else None,
+                              "points_per_launch": n_local,
+                              "mscalar_mul_per_s": round(n_local / (msm_ms * 1e-3) / 1e6, 2) if msm_ms else None,
                               "phases_ms": {kk: round(v / max(calls, 1), 4) for kk, v in phases.items()}},
             "stages_ms_last_proof": {nm: round(ms, 3) for nm, ms in stages},
-            "pcie_inclusive_s": round(pcie_s, 4),
+            "pcie_inclusive_s": round(pcie["s"], 4),
         }
-    pk.close()
+    if not worker:
+        pk.close()
     params.close()
     return line
 
@@ -390,9 +434,12 @@ def main():
     ap.add_argument("--k", type=int, default=PROVE_K)
     ap.add_argument("--log-n", type=int, default=24)
     ap.add_argument("--window-bits", type=int, default=0, help="MSM workload: fixed-base window bits (0: auto)")
+    ap.add_argument("--mode", choices=("shard", "replicas"), default="shard",
+                    help="prove workload, N > 1: one proof over all GPUs (shard) or one per GPU (replicas)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the PMC traffic passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
         return pmc_child(args)
@@ -410,8 +457,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "gloo":  # rehearsal: ranks may share GPUs, host-staged exchanges
+            local %= torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
 

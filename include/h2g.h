@@ -211,6 +211,38 @@ int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int a
 int h2g_prover_stages(double* ms, int max, int* count);
 const char* h2g_prover_stage_name(int i);
 
+/* ---- one proof across several GPUs: MSM point slabs ------------
+ * Every commitment MSM of create_proof (the MsmAccel::msm call sites of SURVEY 8a-1)
+ * is split into `world` contiguous point slabs [P r / world, P (r + 1) / world) (P = 2^k
+ * of the params, clipped to the MSM length n); rank 0 (the
+ * prover) computes slab 0 and the transport hands slabs 1.. to the peer ranks, each of
+ * which holds the same SRS (h2g_params_setup / _create) and answers with the affine
+ * partial sum of its slab (h2g_params_msm_dev).  Rank 0 adds the partials (the group sum
+ * is exact, so the proof bytes do not depend on `world`).  The transport is the host's
+ * (one process per GPU over RCCL in yet-another-halo2-fork_amd/h2g_dist.py).
+ *   launch : called once per MSM, in transcript order, after the scalars (n Fr,
+ *            device pointer, valid until the matching collect) are complete;
+ *            base_set 0 = params.g (commit), 1 = params.g_lagrange (commit_lagrange)
+ *   collect: the world - 1 partials of MSM `seq` (8 u64 affine each, is_identity flags)
+ * Both return 0 on success; nonzero fails the proof with H2G_ERR_STATE. */
+typedef struct {
+  void* ctx;
+  int32_t world;
+  int (*launch)(void* ctx, uint64_t seq, int32_t base_set, uint64_t n, const void* d_scalars);
+  int (*collect)(void* ctx, uint64_t seq, uint64_t* partials, int32_t* is_identity);
+} h2g_shard_transport;
+/* install (world >= 2) or remove (NULL or world <= 1) the transport of h2g_create_proof */
+int h2g_set_shard_transport(const h2g_shard_transport* t);
+/* this rank's slab [lo, hi) of the params' points: builds fixed-base windows sized for
+ * the slab (used by h2g_params_msm_dev and, on rank 0, by create_proof's own slab);
+ * lo == hi removes them */
+int h2g_params_set_slab(uint64_t params, uint64_t lo, uint64_t hi);
+/* peer side: MSM of n device scalars against params' base set [offset, offset + n) */
+int h2g_params_msm_dev(uint64_t params, int32_t base_set, uint64_t offset, uint64_t n, const void* d_scalars,
+                       uint64_t out_affine[8], int32_t* out_is_identity);
+/* synchronous device-to-device copy (staging slabs for the transport) */
+int h2g_memcpy_dtod(void* d_dst, const void* d_src, size_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,90 @@
+"""One create_proof split over WORLD_SIZE ranks (h2g_dist slab transport) must give the
+same proof bytes as the single-device prover.  Launched by tests/test_gpu_sharded.py:
+  python -m torch.distributed.run --nproc-per-node W --master-addr 127.0.0.1 \
+      --master-port P tests/_shard_prove.py --backend gloo case...
+With --backend gloo every rank may share one GPU (host-staged slabs); with nccl each
+rank needs its own GPU (RCCL)."""
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path[:0] = [os.path.join(REPO, "yet-another-halo2-fork_amd"), HERE, os.path.join(REPO, "oracle", "py")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import h2g  # noqa: E402
+import h2g_circuit as hc  # noqa: E402
+import h2g_dist as D  # noqa: E402
+
+CASES = {
+    "simple_k6": lambda: hc.simple_example(6),
+    "mixed_k10": lambda: hc.mixed_circuit(10, seed=5),
+    "lookup_k11": lambda: hc.lookup_circuit(11, seed=8),
+    "keccak_k12": lambda: hc.keccak_style(12, words=16, seed=9),
+    "c3_k14": lambda: hc.synthetic_c3(14, h2g.DeviceOps, seed=4),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--backend", default="gloo")
+    ap.add_argument("cases", nargs="+")
+    args = ap.parse_args()
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = local if args.backend == "nccl" else 0
+    torch.cuda.set_device(dev)
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    else:
+        dist.init_process_group("gloo")
+    h2g.init([dev])
+    results = {}
+    for name in args.cases:
+        circ, wit = CASES[name]()
+        params = h2g.Params(circ.k, s=np.asarray(hc.fr_to_limbs(0x5eed + circ.k), dtype=np.uint64))
+        P = 1 << circ.k
+        if rank == 0:
+            pk = h2g.ProvingKey(params, circ)
+            want = [pk.create_proof(wit), pk.create_proof(wit, seed=bytes(range(32)), vanishing_threads=3)]
+            params.set_slab(*D.slab(P, world, 0))
+            cl = D.SlabClient(dist, points=P)
+            cl.install()
+            try:
+                got = [pk.create_proof(wit), pk.create_proof(wit, seed=bytes(range(32)), vanishing_threads=3)]
+            finally:
+                D.SlabClient.uninstall()
+                cl.stop()
+            results[name] = {"same": got == want, "bytes": len(got[0]), "msms": None}
+            pk.close()
+        else:
+            params.set_slab(*D.slab(P, world, rank))
+            served = D.SlabWorker(dist, params=params).serve()
+            results[name] = {"served": served}
+        params.close()
+        dist.barrier()
+    if rank != 0:  # peers report how many slabs they served
+        counts = [results[nm]["served"] for nm in args.cases]
+    else:
+        counts = [0] * len(args.cases)
+    t = torch.tensor(counts, dtype=torch.int64)
+    if args.backend == "nccl":
+        t = t.cuda()
+    gathered = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(gathered, t)
+    if rank == 0:
+        for i, nm in enumerate(args.cases):
+            results[nm]["msms"] = [int(g[i]) for g in gathered[1:]]
+        print("SHARD_RESULT " + json.dumps(results), flush=True)
+    h2g.shutdown()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -835,6 +835,13 @@ int h2g_memcpy_dtoh(void* dst, const void* src, size_t bytes) {
   HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
   return H2G_OK;
 }
+int h2g_memcpy_dtod(void* dst, const void* src, size_t bytes) {
+  NEED_DEV();
+  if (bytes && (!dst || !src)) return fail(H2G_ERR_ARG, "memcpy_dtod: null pointer");
+  HIPCHK(hipStreamSynchronize(d->stream));
+  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
+  return H2G_OK;
+}
 int h2g_synchronize(void) {
   NEED_DEV();
   HIPCHK(hipStreamSynchronize(d->stream));

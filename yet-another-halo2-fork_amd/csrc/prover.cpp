@@ -57,10 +57,25 @@ struct Params {
   G1Affine* g = nullptr;
   G1Affine* gl = nullptr;
   MsmFixedBase fg, fgl;  // fixed-base MSM windows of g and g_lagrange (commit / commit_lagrange)
+  // this rank's point slab [slab_lo, slab_hi) when one proof spans several GPUs: windows
+  // sized for the slab length (h2g_params_set_slab)
+  size_t slab_lo = 0, slab_hi = 0;
+  MsmFixedBase sg, sgl;
   Pool pool;
   ~Params() {
     msm_fixed_base_free(&fg);
     msm_fixed_base_free(&fgl);
+    msm_fixed_base_free(&sg);
+    msm_fixed_base_free(&sgl);
+  }
+  // windows and table offset serving the base range [off, off + n) of set 0 (g) / 1 (g_lagrange)
+  const MsmFixedBase& tables(int set, size_t off, size_t n, size_t* table_off) const {
+    if (sg.table && off >= slab_lo && off + n <= slab_hi) {
+      *table_off = off - slab_lo;
+      return set == 0 ? sg : sgl;
+    }
+    *table_off = off;
+    return set == 0 ? fg : fgl;
   }
 };
 
@@ -220,15 +235,53 @@ void dump(const char* name, const Fr* dptr, size_t count, hipStream_t st, bool h
 // ParamsKZG::commit / commit_lagrange (kzg/commitment.rs:305-317,354-366): MSM against a
 // prefix of the resident SRS (fixed-base windows).  Launched asynchronously after the
 // work queued on `st`; the affine result is collected when it enters the transcript.
-int commit_launch(Device* d, const Fr* scalars, size_t n, const MsmFixedBase& bases, hipStream_t st, MsmTicket* t) {
-  return msm_fixed_launch(d, scalars, bases, 0, n, st, t);
+// With a shard transport installed (h2g_set_shard_transport) the MSM is split into point
+// slabs: this device takes slab 0, the peers the rest.
+enum { SRS_G = 0, SRS_LAGRANGE = 1 };
+h2g_shard_transport g_shard{nullptr, 1, nullptr, nullptr};
+uint64_t g_shard_seq = 0;
+
+// slab r of an MSM of length n: the points [P r / world, P (r + 1) / world) of the
+// params' P = 2^k, clipped to n (one partition for every MSM length, so each rank's
+// slab windows cover all of its MSMs)
+size_t shard_lo(size_t P, size_t n, int world, int r) {
+  const size_t b = (size_t)((unsigned __int128)P * (unsigned)r / (unsigned)world);
+  return b < n ? b : n;
+}
+
+int commit_launch(Device* d, const Params& prm, const Fr* scalars, size_t n, int set, hipStream_t st, MsmTicket* t) {
+  t->shard_seq = -1;
+  size_t toff = 0;
+  if (g_shard.world <= 1) return msm_fixed_launch(d, scalars, prm.tables(set, 0, n, &toff), 0, n, st, t);
+  const size_t n0 = shard_lo(prm.n, n, g_shard.world, 1);
+  const MsmFixedBase& tb = prm.tables(set, 0, n0, &toff);
+  RCCHK(msm_fixed_launch(d, scalars, tb, toff, n0, st, t));
+  HIPCHK(hipStreamSynchronize(st));  // the transport reads the scalars right away
+  const uint64_t seq = g_shard_seq++;
+  if (g_shard.launch(g_shard.ctx, seq, set, n, scalars) != 0)
+    return fail(H2G_ERR_STATE, "shard transport: launch of MSM " + std::to_string(seq) + " failed");
+  t->shard_seq = (int64_t)seq;
+  return H2G_OK;
 }
 int commit_collect(Device* d, MsmTicket* t, G1Affine* out) {
-  return msm_collect(d, t, reinterpret_cast<uint64_t*>(out));
+  RCCHK(msm_collect(d, t, reinterpret_cast<uint64_t*>(out)));
+  if (t->shard_seq < 0) return H2G_OK;
+  const int peers = g_shard.world - 1;
+  std::vector<G1Affine> part(peers);
+  std::vector<int32_t> ids(peers, 0);
+  if (g_shard.collect(g_shard.ctx, (uint64_t)t->shard_seq, reinterpret_cast<uint64_t*>(part.data()), ids.data()) != 0)
+    return fail(H2G_ERR_STATE, "shard transport: collect of MSM " + std::to_string(t->shard_seq) + " failed");
+  t->shard_seq = -1;
+  G1xyzz acc = G1xyzz::identity();
+  if (!out->is_identity()) acc = G1xyzz::from_affine(*out);
+  for (int i = 0; i < peers; i++)
+    if (!ids[i]) acc = xyzz_madd(acc, part[i]);
+  *out = xyzz_to_affine(acc);
+  return H2G_OK;
 }
-int commit(Device* d, const Fr* scalars, size_t n, const MsmFixedBase& bases, G1Affine* out, hipStream_t st) {
+int commit(Device* d, const Params& prm, const Fr* scalars, size_t n, int set, G1Affine* out, hipStream_t st) {
   MsmTicket t;
-  RCCHK(commit_launch(d, scalars, n, bases, st, &t));
+  RCCHK(commit_launch(d, prm, scalars, n, set, st, &t));
   return commit_collect(d, &t, out);
 }
 
@@ -805,7 +858,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   clk.mark("upload+instances");
   {
     std::vector<MsmTicket> tk(pk.A);
-    for (int c = 0; c < pk.A; c++) RCCHK(commit_launch(d, pk.adv[c], n, prm.fgl, st, &tk[c]));
+    for (int c = 0; c < pk.A; c++) RCCHK(commit_launch(d, prm, pk.adv[c], n, SRS_LAGRANGE, st, &tk[c]));
     for (int c = 0; c < pk.A; c++) {
       G1Affine cm;
       RCCHK(commit_collect(d, &tk[c], &cm));
@@ -867,8 +920,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       }
       (void)rng.random_fr();  // permuted input blind
       (void)rng.random_fr();  // permuted table blind
-      RCCHK(commit_launch(d, pk.lk_ap[l], n, prm.fgl, st, &tk[2 * l]));
-      RCCHK(commit_launch(d, pk.lk_sp[l], n, prm.fgl, st, &tk[2 * l + 1]));
+      RCCHK(commit_launch(d, prm, pk.lk_ap[l], n, SRS_LAGRANGE, st, &tk[2 * l]));
+      RCCHK(commit_launch(d, prm, pk.lk_sp[l], n, SRS_LAGRANGE, st, &tk[2 * l + 1]));
       RCCHK(lagrange_to_coeff(d, D, pk.lk_ap[l], pk.lk_ap_poly[l], st));
       RCCHK(lagrange_to_coeff(d, D, pk.lk_sp[l], pk.lk_sp_poly[l], st));
       RCCHK(coeff_to_extended(d, D, pk.lk_ap_poly[l], pk.lk_apc[l], st));
@@ -937,7 +990,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       if (s == 0) dump("z0", pk.z_lag[s], n, st);
       if (s == 0) dump("sigma0", pk.sigma_lag[0], n, st);
       if (s == 0) dump("v0", col_vals(0), n, st);
-      RCCHK(commit_launch(d, pk.z_lag[s], n, prm.fgl, st, &perm_tk[s]));
+      RCCHK(commit_launch(d, prm, pk.z_lag[s], n, SRS_LAGRANGE, st, &perm_tk[s]));
       RCCHK(lagrange_to_coeff(d, D, pk.z_lag[s], pk.z[s], st));
       RCCHK(coeff_to_extended(d, D, pk.z[s], pk.z_coset[s], st));
       HIPCHK(hipStreamSynchronize(st));  // blind_rows (host) is reused by the next set
@@ -955,7 +1008,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       (void)rng.random_fr();  // product blind
       HIPCHK(hipMemcpyAsync(pk.small, rows.data(), rows.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
       HIPCHK(perm_z_assemble(z_lag, n, bf, pk.pre, pk.one, pk.small, st));
-      RCCHK(commit_launch(d, z_lag, n, prm.fgl, st, t));
+      RCCHK(commit_launch(d, prm, z_lag, n, SRS_LAGRANGE, st, t));
       RCCHK(lagrange_to_coeff(d, D, z_lag, z_poly, st));
       RCCHK(coeff_to_extended(d, D, z_poly, z_coset, st));
       HIPCHK(hipStreamSynchronize(st));  // rows (host) is reused
@@ -998,7 +1051,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)off.size(), st));
     HIPCHK(hipStreamSynchronize(st));  // seeds/off are host temporaries
     (void)rng.random_fr();             // random_blind
-    RCCHK(commit_launch(d, pk.random_poly, n, prm.fg, st, &van_tk));
+    RCCHK(commit_launch(d, prm, pk.random_poly, n, SRS_G, st, &van_tk));
   }
   // advice to coefficient form and the extended-domain cosets do not depend on y:
   // they overlap the permutation / vanishing MSMs
@@ -1070,7 +1123,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   for (int p = 0; p < npieces; p++) (void)rng.random_fr();  // h blinds
   {
     std::vector<MsmTicket> tk(npieces);
-    for (int p = 0; p < npieces; p++) RCCHK(commit_launch(d, pk.h_coeff + (size_t)p * n, n, prm.fg, st, &tk[p]));
+    for (int p = 0; p < npieces; p++) RCCHK(commit_launch(d, prm, pk.h_coeff + (size_t)p * n, n, SRS_G, st, &tk[p]));
     for (int p = 0; p < npieces; p++) {
       G1Affine cm;
       RCCHK(commit_collect(d, &tk[p], &cm));
@@ -1295,7 +1348,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   }
   {
     G1Affine cm;
-    RCCHK(commit(d, pk.hx, n, prm.fg, &cm, st));
+    RCCHK(commit(d, prm, pk.hx, n, SRS_G, &cm, st));
     RCCHK(write_point(cm));
   }
   clk.mark("shplonk h");
@@ -1350,7 +1403,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   HIPCHK(poly_binop(POLY_SCALE, pk.q1, nullptr, inv(z0), pk.q1, n - 1, st));
   {
     G1Affine cm;
-    RCCHK(commit(d, pk.q1, n - 1, prm.fg, &cm, st));
+    RCCHK(commit(d, prm, pk.q1, n - 1, SRS_G, &cm, st));
     RCCHK(write_point(cm));
   }
   clk.mark("shplonk final");
@@ -1492,6 +1545,54 @@ int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int a
   *proof_len = out.size();
   if (out.size() > proof_cap) return fail(H2G_ERR_ARG, "create_proof: proof buffer too small");
   if (proof) std::memcpy(proof, out.data(), out.size());
+  return H2G_OK;
+}
+
+int h2g_set_shard_transport(const h2g_shard_transport* t) {
+  if (t && t->world > 1) {
+    if (!t->launch || !t->collect || t->world > 4096) return fail(H2G_ERR_ARG, "set_shard_transport: bad transport");
+    g_shard = *t;
+  } else {
+    g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
+  }
+  g_shard_seq = 0;
+  return H2G_OK;
+}
+
+int h2g_params_set_slab(uint64_t params, uint64_t lo, uint64_t hi) {
+  NEED_DEV_P();
+  auto ip = g_params.find(params);
+  if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  Params& prm = *ip->second;
+  if (prm.device != d->id) return fail(H2G_ERR_ARG, "params_set_slab: params live on another device");
+  if (lo > hi || hi > prm.n) return fail(H2G_ERR_ARG, "params_set_slab: bad range");
+  msm_fixed_base_free(&prm.sg);
+  msm_fixed_base_free(&prm.sgl);
+  prm.slab_lo = prm.slab_hi = 0;
+  if (hi == lo || (lo == 0 && hi == prm.n)) return H2G_OK;  // none / the full tables
+  HIPCHK(msm_fixed_base_build(prm.g + lo, hi - lo, 0, &prm.sg, d->stream));
+  HIPCHK(msm_fixed_base_build(prm.gl + lo, hi - lo, 0, &prm.sgl, d->stream));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  prm.slab_lo = lo;
+  prm.slab_hi = hi;
+  return H2G_OK;
+}
+
+int h2g_params_msm_dev(uint64_t params, int32_t base_set, uint64_t offset, uint64_t n, const void* d_scalars,
+                       uint64_t out_affine[8], int32_t* out_is_identity) {
+  NEED_DEV_P();
+  auto ip = g_params.find(params);
+  if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  const Params& prm = *ip->second;
+  if (prm.device != d->id) return fail(H2G_ERR_ARG, "params_msm_dev: params live on another device");
+  if ((base_set != SRS_G && base_set != SRS_LAGRANGE) || offset > prm.n || n > prm.n - offset || !out_affine ||
+      (n && !d_scalars))
+    return fail(H2G_ERR_ARG, "params_msm_dev: bad arguments");
+  int id = 0;
+  size_t toff = 0;
+  const MsmFixedBase& tb = prm.tables(base_set, offset, n, &toff);
+  RCCHK(msm_fixed_host_impl(d, d_scalars, tb, toff, n, out_affine, &id, d->stream));
+  if (out_is_identity) *out_is_identity = id;
   return H2G_OK;
 }
 

@@ -94,6 +94,7 @@ struct MsmTicket {
   int ring = -1;
   int c = 0;
   hipEvent_t done = nullptr;
+  int64_t shard_seq = -1;  // >= 0: the peers' slabs of this MSM are pending (h2g_shard_transport)
 };
 
 struct Device {

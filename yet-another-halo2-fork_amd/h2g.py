@@ -89,6 +89,10 @@ _SIGS = {
                           ctypes.POINTER(SZ)], I32),
     "h2g_prover_stages": ([ctypes.POINTER(ctypes.c_double), I32, ctypes.POINTER(I32)], I32),
     "h2g_prover_stage_name": ([I32], ctypes.c_char_p),
+    "h2g_set_shard_transport": ([VP], I32),
+    "h2g_params_set_slab": ([U64, U64, U64], I32),
+    "h2g_params_msm_dev": ([U64, ctypes.c_int32, U64, U64, VP, U64P, ctypes.POINTER(ctypes.c_int32)], I32),
+    "h2g_memcpy_dtod": ([VP, VP, SZ], I32),
 }
 
 MSM_PHASES = ("digits", "sort", "bucket_bounds", "accumulate", "bucket_fixup", "reduce")
@@ -439,6 +443,10 @@ class Params:
             check(lib().h2g_params_create(k, p64(g), p64(gl), ctypes.byref(h)))
         self.handle = h.value
 
+    def set_slab(self, lo, hi):
+        """fixed-base windows for this rank's point slab [lo, hi) (one proof over several GPUs)"""
+        check(lib().h2g_params_set_slab(self.handle, lo, hi))
+
     def export(self):
         n = 1 << self.k
         g = np.zeros((n, 8), dtype=np.uint64)
@@ -504,6 +512,88 @@ class ProvingKey:
         if self.handle:
             lib().h2g_pk_free(self.handle)
             self.handle = 0
+
+
+# ----------------------------------------------------------- multi-GPU MSM slabs
+SHARD_LAUNCH = ctypes.CFUNCTYPE(ctypes.c_int, VP, U64, ctypes.c_int32, U64, VP)
+SHARD_COLLECT = ctypes.CFUNCTYPE(ctypes.c_int, VP, U64, U64P, ctypes.POINTER(ctypes.c_int32))
+
+
+class ShardTransport(ctypes.Structure):
+    """struct h2g_shard_transport (include/h2g.h)"""
+    _fields_ = [("ctx", VP), ("world", ctypes.c_int32), ("launch", SHARD_LAUNCH), ("collect", SHARD_COLLECT)]
+
+
+_transport_keep = None
+
+
+def set_shard_transport(world, launch=None, collect=None):
+    """Install the MSM slab transport of create_proof: launch(seq, base_set, n, d_scalars)
+    and collect(seq) -> [(affine uint64[8], is_identity)] * (world - 1).  world <= 1
+    removes it.  Exceptions inside the callbacks fail the proof (nonzero status)."""
+    global _transport_keep
+    if world <= 1:
+        check(lib().h2g_set_shard_transport(None))
+        _transport_keep = None
+        return
+
+    def _launch(ctx, seq, base_set, n, d_scalars):
+        try:
+            launch(int(seq), int(base_set), int(n), int(d_scalars or 0))
+            return 0
+        except Exception as e:  # noqa: BLE001 -- reported through the C status
+            _transport_keep[3].append(e)
+            return 1
+
+    def _collect(ctx, seq, partials, ids):
+        try:
+            parts = collect(int(seq))
+            assert len(parts) == world - 1
+            for i, (pt, is_id) in enumerate(parts):
+                pt = np.ascontiguousarray(pt, dtype=np.uint64).reshape(8)
+                for j in range(8):
+                    partials[8 * i + j] = int(pt[j])
+                ids[i] = 1 if is_id else 0
+            return 0
+        except Exception as e:  # noqa: BLE001
+            _transport_keep[3].append(e)
+            return 1
+
+    cl, cc = SHARD_LAUNCH(_launch), SHARD_COLLECT(_collect)
+    t = ShardTransport(None, world, cl, cc)
+    _transport_keep = (t, cl, cc, [])
+    check(lib().h2g_set_shard_transport(ctypes.byref(t)))
+
+
+def transport_errors():
+    """exceptions raised inside the installed transport's callbacks (cleared)"""
+    if _transport_keep is None:
+        return []
+    errs = list(_transport_keep[3])
+    _transport_keep[3].clear()
+    return errs
+
+
+def params_msm_dev(params, base_set, offset, n, d_scalars):
+    """peer side of the slab transport: MSM of n device scalars against params'
+    base set (0 = g, 1 = g_lagrange) at [offset, offset + n) -> (affine, is_identity)"""
+    out = np.zeros(8, dtype=np.uint64)
+    is_id = ctypes.c_int32()
+    check(lib().h2g_params_msm_dev(params.handle, base_set, offset, n, VP(d_scalars) if n else None, p64(out),
+                                   ctypes.byref(is_id)))
+    return out, bool(is_id.value)
+
+
+def memcpy_dtod(d_dst, d_src, nbytes):
+    check(lib().h2g_memcpy_dtod(VP(d_dst), VP(d_src), nbytes))
+
+
+def memcpy_dtoh(h_dst, d_src, nbytes):
+    check(lib().h2g_memcpy_dtoh(VP(h_dst), VP(d_src), nbytes))
+
+
+def memcpy_htod(d_dst, h_src, nbytes):
+    check(lib().h2g_memcpy_htod(VP(d_dst), VP(h_src), nbytes))
 
 
 def prover_stages():

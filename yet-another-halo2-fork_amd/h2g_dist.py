@@ -1,0 +1,183 @@
+"""One create_proof across several GPUs: the proof's commitment MSMs are
+split into contiguous point slabs, one per rank, over torch.distributed -- backend
+"nccl" (RCCL over xGMI) with one process per GPU, or "gloo" with host staging (CPU
+tests; several ranks sharing one GPU).
+
+Rank 0 runs h2g_create_proof with a slab transport installed
+(h2g_set_shard_transport, include/h2g.h); ranks 1.. run SlabWorker.serve(), which
+answers each MSM with the affine partial sum of its slab.  The reference's MSM call
+sites (MsmAccel::msm, halo2_middleware/src/zal.rs:58, via ParamsKZG::commit /
+commit_lagrange, poly/kzg/commitment.rs:305-317,354-366) are unchanged in meaning: the
+group sum of the slabs is the MSM, so the proof bytes do not depend on the rank count.
+
+Messages rank 0 -> rank r per MSM: header int64[5] = (op, seq, base_set, lo, count), then
+the `count` scalars of slab r = points [lo, lo + count) (int64 view of the Fr limbs).  Reply r -> 0: int64[9] = the
+affine partial (8 limbs) and its identity flag.  op 0 ends a serve() session.
+"""
+import numpy as np
+
+OP_STOP, OP_MSM = 0, 1
+
+
+def slab(n, world, r, P=None):
+    """[lo, hi) of rank r's points in an MSM of length n: the slab of the params' P = 2^k
+    points, clipped to n (the C prover's shard_lo, csrc/prover.cpp)"""
+    P = n if P is None else P
+    return min(n, P * r // world), min(n, P * (r + 1) // world)
+
+
+def _staging(dist, group):
+    """device tensors for RCCL, host tensors for gloo"""
+    import torch
+    backend = dist.get_backend(group)
+    if backend == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+class SlabClient:
+    """rank 0: sends each MSM's slabs to the peers and collects their partials"""
+
+    def __init__(self, dist, points=None, group=None):
+        """points: the params' P = 2^k (slab partition); None = each MSM's own length"""
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.device = _staging(dist, group)
+        self.points = points
+        self.pending = {}
+
+    def _send(self, seq, base_set, n, fill):
+        import torch
+        dist, dev = self.dist, self.device
+        works, keep, replies = [], [], []
+        for r in range(1, self.world):
+            lo, hi = slab(n, self.world, r, self.points)
+            hdr = torch.tensor([OP_MSM, seq, base_set, lo, hi - lo], dtype=torch.int64, device=dev)
+            keep.append(hdr)
+            works.append(dist.isend(hdr, r, group=self.group))
+            if hi > lo:
+                buf = torch.empty((hi - lo) * 4, dtype=torch.int64, device=dev)
+                fill(buf, lo, hi)
+                keep.append(buf)
+                works.append(dist.isend(buf, r, group=self.group))
+            rep = torch.empty(9, dtype=torch.int64, device=dev)
+            replies.append(rep)
+            works.append(dist.irecv(rep, r, group=self.group))
+        self.pending[seq] = (works, keep, replies)
+
+    def launch(self, seq, base_set, n, d_scalars):
+        """transport launch: d_scalars = device pointer to n Fr (the prover's buffer)"""
+        import h2g
+
+        def fill(buf, lo, hi):
+            src = d_scalars + lo * 32
+            if buf.is_cuda:
+                h2g.memcpy_dtod(buf.data_ptr(), src, (hi - lo) * 32)
+            else:
+                h2g.memcpy_dtoh(buf.data_ptr(), src, (hi - lo) * 32)
+
+        self._send(seq, base_set, n, fill)
+
+    def launch_host(self, seq, base_set, scalars):
+        """the same from host scalars (numpy (n, 4) uint64): CPU tests / host callers"""
+        import torch
+        sc = np.ascontiguousarray(scalars, dtype=np.uint64)
+
+        def fill(buf, lo, hi):
+            buf.copy_(torch.from_numpy(sc[lo:hi].reshape(-1).view(np.int64)))
+
+        self._send(seq, base_set, len(sc), fill)
+
+    def collect(self, seq):
+        """transport collect: [(affine uint64[8], is_identity)] for ranks 1.."""
+        works, _keep, replies = self.pending.pop(seq)
+        for w in works:
+            w.wait()
+        out = []
+        for rep in replies:
+            a = rep.cpu().numpy().view(np.uint64)
+            out.append((a[:8].copy(), bool(a[8])))
+        return out
+
+    def drain(self):
+        """complete every outstanding exchange (after a failed proof) so the peers stay
+        in step"""
+        for seq in sorted(self.pending):
+            self.collect(seq)
+
+    def stop(self):
+        """end the peers' serve() session"""
+        import torch
+        self.drain()
+        works = []
+        for r in range(1, self.world):
+            hdr = torch.tensor([OP_STOP, 0, 0, 0, 0], dtype=torch.int64, device=self.device)
+            works.append((hdr, self.dist.isend(hdr, r, group=self.group)))
+        for _, w in works:
+            w.wait()
+
+    def install(self):
+        """make this client h2g_create_proof's slab transport"""
+        import h2g
+        h2g.set_shard_transport(self.world, self.launch, self.collect)
+
+    @staticmethod
+    def uninstall():
+        import h2g
+        h2g.set_shard_transport(1)
+
+
+class SlabWorker:
+    """ranks 1..: serve MSM slabs until rank 0 stops the session.  engine(base_set, lo,
+    n, buf) -> (affine uint64[8], is_identity), buf = the slab's int64 tensor; the default
+    engine is the device MSM against the params' resident fixed-base windows."""
+
+    def __init__(self, dist, params=None, engine=None, group=None):
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = _staging(dist, group)
+        self.params = params
+        self.engine = engine or self._device_engine
+        self._stage = None
+
+    def _device_engine(self, base_set, lo, n, buf):
+        import h2g
+        import torch
+        if buf.is_cuda:
+            torch.cuda.current_stream().synchronize()  # the received slab is complete
+            ptr = buf.data_ptr()
+        else:  # gloo: stage the host slab into a reusable device buffer
+            if self._stage is None or self._stage.nbytes < n * 32:
+                self._stage = h2g.DevBuf(n * 32)
+            h2g.memcpy_htod(self._stage.ptr, buf.data_ptr(), n * 32)
+            ptr = self._stage.ptr
+        return h2g.params_msm_dev(self.params, base_set, lo, n, ptr)
+
+    def serve(self):
+        """-> number of MSM slabs served in this session"""
+        import torch
+        dist, dev = self.dist, self.device
+        count = 0
+        while True:
+            hdr = torch.empty(5, dtype=torch.int64, device=dev)
+            dist.recv(hdr, 0, group=self.group)
+            op, seq, base_set, lo, cnt = hdr.cpu().tolist()
+            if op == OP_STOP:
+                return count
+            if op != OP_MSM:
+                raise RuntimeError(f"slab worker: unknown op {op}")
+            hi = lo + cnt
+            if hi > lo:
+                buf = torch.empty((hi - lo) * 4, dtype=torch.int64, device=dev)
+                dist.recv(buf, 0, group=self.group)
+                pt, is_id = self.engine(base_set, lo, hi - lo, buf)
+            else:
+                pt, is_id = np.zeros(8, dtype=np.uint64), True
+            rep = np.zeros(9, dtype=np.uint64)
+            rep[:8] = pt
+            rep[8] = 1 if is_id else 0
+            dist.send(torch.from_numpy(rep.view(np.int64)).to(dev), 0, group=self.group)
+            count += 1
