@@ -73,45 +73,47 @@ using Fr = Fe<FrParams>;
 using Fq = Fe<FqParams>;
 
 // ---------------------------------------------------------------- add / sub
+// Carry chains through clang's __builtin_addc / __builtin_subc: on gfx950 each
+// limb is one v_add_co/v_addc_co (v_sub_co/v_subb_co) and the reduction one
+// v_cndmask -- 24 VALU ops per add or sub (a 64-bit signed emulation of the
+// borrow compiled to ~5 ops per limb).
 template <class P>
 H2G_HD Fe<P> operator+(const Fe<P>& a, const Fe<P>& b) {
   Fe<P> s, d;
-  uint64_t c = 0;
+  unsigned c = 0, br = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    c += (uint64_t)a.l[i] + b.l[i];
-    s.l[i] = (uint32_t)c;
-    c >>= 32;
-  }
+  for (int i = 0; i < 8; i++) s.l[i] = __builtin_addc(a.l[i], b.l[i], c, &c);
   // a + b < 2M < 2^255: no carry out; subtract M, keep if no borrow
-  int64_t br = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    int64_t t = (int64_t)s.l[i] - P::M[i] + br;
-    d.l[i] = (uint32_t)t;
-    br = t >> 32;
-  }
-  return br ? s : d;
+  for (int i = 0; i < 8; i++) d.l[i] = __builtin_subc(s.l[i], P::M[i], br, &br);
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.l[i] = br ? s.l[i] : d.l[i];
+  return d;
 }
 
 template <class P>
 H2G_HD Fe<P> operator-(const Fe<P>& a, const Fe<P>& b) {
   Fe<P> d, s;
-  int64_t br = 0;
+  unsigned br = 0, c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    int64_t t = (int64_t)a.l[i] - b.l[i] + br;
-    d.l[i] = (uint32_t)t;
-    br = t >> 32;
-  }
-  uint64_t c = 0;
+  for (int i = 0; i < 8; i++) d.l[i] = __builtin_subc(a.l[i], b.l[i], br, &br);
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    c += (uint64_t)d.l[i] + P::M[i];
-    s.l[i] = (uint32_t)c;
-    c >>= 32;
-  }
-  return br ? s : d;
+  for (int i = 0; i < 8; i++) s.l[i] = __builtin_addc(d.l[i], P::M[i], c, &c);
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.l[i] = br ? s.l[i] : d.l[i];
+  return d;
+}
+
+// r - M if r >= M (r < 2M)
+template <class P>
+H2G_HD Fe<P> reduce_once(const Fe<P>& r) {
+  Fe<P> d;
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.l[i] = __builtin_subc(r.l[i], P::M[i], br, &br);
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.l[i] = br ? r.l[i] : d.l[i];
+  return d;
 }
 
 template <class P>
@@ -143,12 +145,15 @@ __device__ __forceinline__ void h2g_mac(uint64_t& lo, uint32_t& hi, uint32_t a, 
                : "vcc");
 }
 
+// Montgomery product without the final conditional subtraction: for inputs
+// a, b < 2M the result is < (4M^2 + 2^256 M) / 2^256 < 2M (both BN254 moduli are
+// < 2^254, so 4M < 2^256).  Used by the "lazy" [0, 2M) arithmetic below.
 template <class P>
-__device__ __forceinline__ Fe<P> operator*(const Fe<P>& A, const Fe<P>& B) {
+__device__ __forceinline__ Fe<P> mont_mul_lazy(const Fe<P>& A, const Fe<P>& B) {
   const uint32_t* a = A.l;
   const uint32_t* b = B.l;
   uint32_t m[8];
-  Fe<P> r, d;
+  Fe<P> r;
   uint64_t lo = 0;
   uint32_t hi = 0;
 #pragma unroll
@@ -175,15 +180,13 @@ __device__ __forceinline__ Fe<P> operator*(const Fe<P>& A, const Fe<P>& B) {
     lo = (lo >> 32) | ((uint64_t)hi << 32);
     hi = 0;
   }
-  r.l[7] = (uint32_t)lo;  // result < 2M < 2^255
-  int64_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    int64_t u = (int64_t)r.l[i] - P::M[i] + br;
-    d.l[i] = (uint32_t)u;
-    br = u >> 32;
-  }
-  return br ? r : d;
+  r.l[7] = (uint32_t)lo;
+  return r;
+}
+
+template <class P>
+__device__ __forceinline__ Fe<P> operator*(const Fe<P>& A, const Fe<P>& B) {
+  return reduce_once(mont_mul_lazy(A, B));  // fully reduced inputs: result < 2M
 }
 // Host: CIOS with the "no final carry" shortcut (top modulus limb < 2^31 - 1 for
 // both BN254 moduli), 32-bit limbs.  Returns a*b*2^-256 mod M, fully reduced.
@@ -211,17 +214,10 @@ __host__ inline Fe<P> operator*(const Fe<P>& a, const Fe<P>& b) {
     }
     t[7] = C + A;
   }
-  Fe<P> r, d;
+  Fe<P> r;
 #pragma unroll
   for (int i = 0; i < 8; i++) r.l[i] = t[i];
-  int64_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    int64_t u = (int64_t)r.l[i] - P::M[i] + br;
-    d.l[i] = (uint32_t)u;
-    br = u >> 32;
-  }
-  return br ? r : d;
+  return reduce_once(r);
 }
 
 template <class P>
@@ -416,6 +412,87 @@ H2G_HD G1Affine xyzz_to_affine(const G1xyzz& p) {
   const Fq izzz = i * p.ZZ;        // 1/ZZZ
   r.x = p.X * izz;
   r.y = p.Y * izzz;
+  return r;
+}
+
+// ---------------------------------------------------------------- lazy [0, 2M) arithmetic (device)
+// For long chains of group additions that never leave the device (the MSM bucket
+// accumulation): values live in [0, 2M), so a Montgomery product skips its final
+// conditional subtraction (mont_mul_lazy); add/sub reduce modulo 2M; zero tests
+// accept both representatives 0 and M.  canon2 maps back to [0, M) before a value
+// is stored for code that assumes fully reduced limbs.
+template <class P>
+__device__ __forceinline__ uint32_t two_m_limb(int i) {
+  return (P::M[i] << 1) | (i ? P::M[i - 1] >> 31 : 0u);
+}
+template <class P>
+__device__ __forceinline__ Fe<P> add2(const Fe<P>& a, const Fe<P>& b) {
+  Fe<P> s, d;
+  unsigned c = 0, br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) s.l[i] = __builtin_addc(a.l[i], b.l[i], c, &c);  // < 4M < 2^256
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.l[i] = __builtin_subc(s.l[i], two_m_limb<P>(i), br, &br);
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.l[i] = br ? s.l[i] : d.l[i];
+  return d;
+}
+template <class P>
+__device__ __forceinline__ Fe<P> sub2(const Fe<P>& a, const Fe<P>& b) {
+  Fe<P> d, s;
+  unsigned br = 0, c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.l[i] = __builtin_subc(a.l[i], b.l[i], br, &br);
+  // a - b in (-2M, 2M): add 2M back on borrow (mod 2^256)
+#pragma unroll
+  for (int i = 0; i < 8; i++) s.l[i] = __builtin_addc(d.l[i], two_m_limb<P>(i), c, &c);
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.l[i] = br ? s.l[i] : d.l[i];
+  return d;
+}
+template <class P>
+__device__ __forceinline__ bool is_zero2(const Fe<P>& a) {
+  uint32_t z = 0, m = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    z |= a.l[i];
+    m |= a.l[i] ^ P::M[i];
+  }
+  return z == 0 || m == 0;
+}
+template <class P>
+__device__ __forceinline__ Fe<P> canon2(const Fe<P>& a) {
+  return reduce_once(a);
+}
+__device__ __forceinline__ G1xyzz xyzz_canon2(const G1xyzz& p) {
+  G1xyzz r;
+  r.X = canon2(p.X);
+  r.Y = canon2(p.Y);
+  r.ZZ = canon2(p.ZZ);
+  r.ZZZ = canon2(p.ZZZ);
+  return r;
+}
+// madd-2008-s on [0, 2M) coordinates (p lazy or the identity, q canonical affine);
+// the same formula and special cases as xyzz_madd.
+__device__ __forceinline__ G1xyzz xyzz_madd_lazy(const G1xyzz& p, const G1Affine& q) {
+  if (q.is_identity()) return p;
+  if (is_zero2(p.ZZ)) return G1xyzz::from_affine(q);
+  const Fq U2 = mont_mul_lazy(q.x, p.ZZ);
+  const Fq S2 = mont_mul_lazy(q.y, p.ZZZ);
+  const Fq Pp = sub2(U2, p.X);
+  const Fq R = sub2(S2, p.Y);
+  if (is_zero2(Pp)) {
+    if (is_zero2(R)) return xyzz_mdbl(q);
+    return G1xyzz::identity();
+  }
+  const Fq PP = mont_mul_lazy(Pp, Pp);
+  const Fq PPP = mont_mul_lazy(Pp, PP);
+  const Fq Q = mont_mul_lazy(p.X, PP);
+  G1xyzz r;
+  r.X = sub2(sub2(mont_mul_lazy(R, R), PPP), add2(Q, Q));
+  r.Y = sub2(mont_mul_lazy(R, sub2(Q, r.X)), mont_mul_lazy(p.Y, PPP));
+  r.ZZ = mont_mul_lazy(p.ZZ, PP);
+  r.ZZZ = mont_mul_lazy(p.ZZZ, PPP);
   return r;
 }
 

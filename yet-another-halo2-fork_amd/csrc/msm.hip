@@ -12,8 +12,8 @@
 //   4. accumulate : the sorted array is cut into fixed chunks of L entries, one
 //                   thread per chunk (every thread does exactly L mixed additions,
 //                   whatever the bucket sizes -> no load imbalance, also for skewed
-//                   scalars).  XYZZ += affine (madd-2008-s), bases gathered by
-//                   sorted index.  Buckets wholly inside a chunk are written
+//                   scalars).  XYZZ += affine (madd-2008-s) on lazily reduced
+//                   [0, 2p) coordinates, bases gathered by sorted index.  Buckets wholly inside a chunk are written
 //                   directly; a chunk's first/last run that crosses a chunk
 //                   boundary is written to a boundary slot.
 //   5. fixup      : buckets spanning chunks sum their boundary slots (one thread,
@@ -125,8 +125,9 @@ __device__ __forceinline__ void msm_emit(uint32_t key, const G1xyzz& acc, bool f
                                          uint32_t t, const uint32_t* __restrict__ start,
                                          const uint32_t* __restrict__ end, G1xyzz* __restrict__ buckets,
                                          G1xyzz* __restrict__ bnd) {
-  if (start[key] >= lo && end[key] <= hi) buckets[key] = acc;
-  else bnd[2 * (size_t)t + (first ? 0 : 1)] = acc;
+  const G1xyzz v = xyzz_canon2(acc);  // lazy [0, 2M) -> fully reduced for the later kernels
+  if (start[key] >= lo && end[key] <= hi) buckets[key] = v;
+  else bnd[2 * (size_t)t + (first ? 0 : 1)] = v;
 }
 
 __global__ void __launch_bounds__(MSM_THREADS)
@@ -157,7 +158,7 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ 
       acc = G1xyzz::identity();
     }
     if (v >> 31) pt = affine_neg(pt);
-    acc = xyzz_madd(acc, pt);
+    acc = xyzz_madd_lazy(acc, pt);
   }
   msm_emit(key, acc, first, lo, hi, t, start, end, buckets, bnd);
 }

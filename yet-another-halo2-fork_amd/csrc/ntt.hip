@@ -28,6 +28,12 @@ static constexpr int NTT_THREADS = 64 * NTT_WAVES;
 #ifndef NTT_MIN_WAVES
 #define NTT_MIN_WAVES 2  // waves per SIMD the register allocation must admit
 #endif
+// 2^6 passes fit 168 VGPRs without spilling -> 3 waves per SIMD (512 / 168);
+// the smaller passes would spill at 168 and stay at 2.
+template <int M>
+struct NttPassWaves {
+  static constexpr int value = M == 6 ? 3 : NTT_MIN_WAVES;
+};
 
 __device__ __forceinline__ Fr ld_fr(const Fr* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
@@ -111,10 +117,12 @@ struct WaveDif {
 #pragma unroll
       for (int p = 0; p < 4; p++) {
         const int q = ((p >> t) << (t + 1)) | (p & ((1 << t) - 1));
-        const int j = q & ((1 << t) - 1);
+        const int j = q & ((1 << t) - 1);  // compile-time after unrolling
         const Fr a = x[q], b = x[q + (1 << t)];
         x[q] = a + b;
-        x[q + (1 << t)] = (a - b) * w[j << (M - 1 - t)];
+        // w^0 = 1 exactly (Montgomery one, fully reduced): skip the product --
+        // every butterfly of the t = 0 stage, half of t = 1, a quarter of t = 2
+        x[q + (1 << t)] = j == 0 ? a - b : (a - b) * w[j << (M - 1 - t)];
       }
     }
   }
@@ -136,7 +144,7 @@ struct WaveDif {
 //   Pass 0 reads `in` (n_in valid elements, zero padding beyond) and, if
 //   `distribute`, multiplies element i by zeta^(i mod 3) (domain.rs:325-341).
 template <int M>
-__global__ void __launch_bounds__(NTT_THREADS, NTT_MIN_WAVES)
+__global__ void __launch_bounds__(NTT_THREADS, NttPassWaves<M>::value)
 ntt_pass_kernel(Fr* data, const Fr* in, uint64_t n_in, NttTables tab, const Fr* __restrict__ ptw, int L, int lrem,
                 int distribute, Fr z1, Fr z2) {
   using D = WaveDif<M>;
