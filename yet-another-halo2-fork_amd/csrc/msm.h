@@ -16,10 +16,8 @@ struct MsmWorkspace {
   int cap_W = 0;
   uint32_t cap_L = 0;
   int last_c = 0, last_W = 0;    // window config of the most recent msm_run
-  void* keys_in = nullptr;       // u32 [n*W]
-  void* keys_out = nullptr;      // u32 [n*W]
-  void* vals_in = nullptr;       // u32 [n*W]
-  void* vals_out = nullptr;      // u32 [n*W]
+  void* keys_in = nullptr;       // u64 [n*W] entries (key << 32 | value)
+  void* keys_out = nullptr;      // u64 [n*W] sorted entries
   void* bucket_start = nullptr;  // u32 [W*NB]
   void* bucket_end = nullptr;    // u32 [W*NB]
   void* item_off = nullptr;      // (unused)
