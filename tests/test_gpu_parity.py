@@ -110,7 +110,14 @@ def test_msm_skewed_distributions(dist):
         for i, b in enumerate(bit):
             c[i, b // 64] = np.uint64(1) << np.uint64(b % 64)
         sc = O.fr_from_canonical(c)
-    assert np.array_equal(h2g.msm(sc, bases), O.msm_best(sc, bases, 8)), dist
+    want = O.msm_best(sc, bases, 8)
+    assert np.array_equal(h2g.msm(sc, bases), want), dist
+    # fixed-base windows (one shared bucket set): the same skew through the descriptor path
+    hb = h2g.base_descriptor(bases)
+    try:
+        assert np.array_equal(h2g.msm_with_cached_base(sc, hb), want), dist
+    finally:
+        h2g.descriptor_free(hb)
 
 
 @pytest.mark.parametrize("window_bits", [4, 9, 13, 17])

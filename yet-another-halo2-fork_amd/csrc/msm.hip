@@ -11,20 +11,21 @@
 //   2. sort       : LSD radix sort of the entries over the key bits only (rocprim,
 //                   keys-only: 1.07 vs 1.29 ms for separate key/value arrays at
 //                   13 x 2^22 entries, tools/microbench/radix_cfg.hip)
-//   3. bounds     : bucket [start, end) from the sorted keys, count of valid entries
-//   4. accumulate : the sorted array is cut into fixed chunks of L entries, one
+//   3. accumulate : the sorted array is cut into fixed chunks of L entries, one
 //                   thread per chunk (every thread does exactly L mixed additions,
 //                   whatever the bucket sizes -> no load imbalance, also for skewed
 //                   scalars).  XYZZ += affine (madd-2008-s) on lazily reduced
-//                   [0, 2p) coordinates, bases gathered by sorted index.  Buckets wholly inside a chunk are written
-//                   directly; a chunk's first/last run that crosses a chunk
-//                   boundary is written to a boundary slot.
-//   5. fixup      : buckets spanning chunks sum their boundary slots (one thread,
+//                   [0, 2p) coordinates, bases gathered by sorted index.  A run that
+//                   neither continues from the previous chunk nor into the next (two
+//                   neighbour reads) is a whole bucket and is written directly;
+//                   otherwise it goes to the chunk's boundary slot.  The runs also
+//                   record each bucket's [start, end) in the sorted array.
+//   4. fixup      : buckets spanning chunks sum their boundary slots (one thread,
 //                   or a whole workgroup for buckets spanning > 32 chunks)
-//   6. segments   : per (window, segment of SEG buckets) running sums
+//   5. segments   : per (window, segment of SEG buckets) running sums
 //                   sum_j (j+1) B_j = S_local + offset * R
-//   7. windows    : per window tree reduction of segment results in LDS
-//   8. final      : Horner over windows (c doublings each), to affine -- on the
+//   6. windows    : per window tree reduction of segment results in LDS
+//   7. final      : Horner over windows (c doublings each), to affine -- on the
 //                   host for host-returning entry points (a single-lane chain of
 //                   ~250 doublings is latency-bound on the GPU), else one device lane.
 // The result is the unique affine point, so it is bit-identical to any other
@@ -108,31 +109,24 @@ msm_digits_kernel(const Fr* __restrict__ scalars, size_t n, int c, int W, uint32
   }
 }
 
-// 3. bucket bounds + valid count -------------------------------------------------
+// 3-4. accumulation straight from the sorted entries -------------------------------
+// The sorted array is cut into chunks of L entries, one thread per chunk.  A chunk's
+// run of one bucket is the whole bucket iff it neither continues from the previous
+// chunk nor into the next (two neighbour reads; no separate bounds pass): such
+// buckets are written directly, a run that crosses a chunk boundary goes to the
+// chunk's boundary slot (slot 0 = its first run, slot 1 = its last run).  The run
+// that begins a bucket records its start, the run that ends it its end (for the
+// fixup).  The sentinel entries (zero digits) sort last and end a chunk.
 __device__ __forceinline__ uint32_t ent_key(uint64_t e) { return (uint32_t)(e >> 32); }
 
-__global__ void msm_bounds_kernel(const uint64_t* __restrict__ ent, size_t total, uint32_t sentinel,
-                                  uint32_t* __restrict__ start, uint32_t* __restrict__ end,
-                                  uint32_t* __restrict__ valid) {
-  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const uint32_t k = ent_key(ent[i]);
-  if (k == sentinel) return;
-  const uint32_t next = i == total - 1 ? sentinel + 1 : ent_key(ent[i + 1]);
-  if (i == 0 || ent_key(ent[i - 1]) != k) start[k] = (uint32_t)i;
-  if (next != k) {
-    end[k] = (uint32_t)(i + 1);
-    if (i == total - 1 || next == sentinel) *valid = (uint32_t)(i + 1);
-  }
-}
-
-// 4. chunked accumulation ----------------------------------------------------------
-__device__ __forceinline__ void msm_emit(uint32_t key, const G1xyzz& acc, bool first, uint32_t lo, uint32_t hi,
-                                         uint32_t t, const uint32_t* __restrict__ start,
-                                         const uint32_t* __restrict__ end, G1xyzz* __restrict__ buckets,
-                                         G1xyzz* __restrict__ bnd) {
+__device__ __forceinline__ void msm_emit(uint32_t key, const G1xyzz& acc, bool first, bool from_prev, bool to_next,
+                                         uint32_t a, uint32_t b, uint32_t t, G1xyzz* __restrict__ buckets,
+                                         G1xyzz* __restrict__ bnd, uint32_t* __restrict__ start,
+                                         uint32_t* __restrict__ end) {
   const G1xyzz v = xyzz_canon2(acc);  // lazy [0, 2M) -> fully reduced for the later kernels
-  if (start[key] >= lo && end[key] <= hi) buckets[key] = v;
+  if (!from_prev) start[key] = a;
+  if (!to_next) end[key] = b;
+  if (!from_prev && !to_next) buckets[key] = v;
   else bnd[2 * (size_t)t + (first ? 0 : 1)] = v;
 }
 
@@ -141,22 +135,24 @@ __device__ __forceinline__ void msm_emit(uint32_t key, const G1xyzz& acc, bool f
 // 16 VGPRs).
 template <bool PF>
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_acc_kernel(const G1Affine* __restrict__ bases, const uint64_t* __restrict__ ent,
-               const uint32_t* __restrict__ start,
-               const uint32_t* __restrict__ end, const uint32_t* __restrict__ valid_p, uint32_t L,
-               G1xyzz* __restrict__ buckets, G1xyzz* __restrict__ bnd) {
+msm_acc_kernel(const G1Affine* __restrict__ bases, const uint64_t* __restrict__ ent, uint32_t total,
+               uint32_t sentinel, uint32_t L, G1xyzz* __restrict__ buckets, G1xyzz* __restrict__ bnd,
+               uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t valid = *valid_p;
   const uint32_t lo = t * L;
-  if (lo >= valid) return;
-  const uint32_t hi = lo + L < valid ? lo + L : valid;
+  if (lo >= total) return;
+  const uint32_t hi = lo + L < total ? lo + L : total;
   uint64_t e = ent[lo];
   uint32_t key = ent_key(e);
+  if (key == sentinel) return;
+  const bool prev_same = lo > 0 && ent_key(ent[lo - 1]) == key;
   bool first = true;
+  uint32_t run_lo = lo;
   G1xyzz acc = G1xyzz::identity();
   G1Affine pt;
   if (PF) pt = ld_aff(bases + ((uint32_t)e & 0x7fffffffu));
-  for (uint32_t p = lo; p < hi; p++) {
+  uint32_t p = lo;
+  for (; p < hi; p++) {
     uint64_t e_next = 0;
     G1Affine pt_next;
     if (PF) {
@@ -171,10 +167,12 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint64_t* __restrict__ 
 #endif
     }
     const uint32_t k2 = ent_key(e);
+    if (k2 == sentinel) break;
     const uint32_t v = (uint32_t)e;
     if (k2 != key) {
-      msm_emit(key, acc, first, lo, hi, t, start, end, buckets, bnd);
+      msm_emit(key, acc, first, first && prev_same, false, run_lo, p, t, buckets, bnd, start, end);
       first = false;
+      run_lo = p;
       key = k2;
       acc = G1xyzz::identity();
     }
@@ -185,14 +183,16 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint64_t* __restrict__ 
       pt = pt_next;
     }
   }
-  msm_emit(key, acc, first, lo, hi, t, start, end, buckets, bnd);
+  const bool to_next = p == hi && hi < total && ent_key(ent[hi]) == key;
+  msm_emit(key, acc, first, first && prev_same, to_next, run_lo, p, t, buckets, bnd, start, end);
 }
 
-// 5. buckets spanning chunks -----------------------------------------------------
+// Buckets spanning chunks, one thread per bucket: the piece in its first chunk t0 is
+// that chunk's last run (slot 1) unless the bucket starts the chunk (slot 0); every
+// later chunk holds it as its first run (slot 0).  Buckets over more than MSM_SMALL
+// chunks are summed by whole workgroups.
 __device__ __forceinline__ const G1xyzz& msm_piece(const G1xyzz* bnd, uint32_t t, uint32_t t0, uint32_t bs,
                                                    uint32_t L) {
-  // chunk t0: the bucket is its last run (slot 1) unless it also starts the chunk
-  // (slot 0); every later chunk sees it as its first run (slot 0).
   return bnd[2 * (size_t)t + ((t == t0 && bs != t0 * L) ? 1 : 0)];
 }
 
@@ -388,12 +388,12 @@ static hipError_t msm_pipeline(const Fr* d_scalars, const G1Affine* d_bases, siz
     H2G_TRY(grow(&ws->keys_out, total * 8));
     H2G_TRY(grow(&ws->bucket_start, (size_t)nbt * 4));
     H2G_TRY(grow(&ws->bucket_end, (size_t)nbt * 4));
-    H2G_TRY(grow(&ws->item_bucket, (size_t)nbt * 4));         // big-bucket list
+    H2G_TRY(grow(&ws->item_bucket, (size_t)nbt * 4));  // big-bucket list
     H2G_TRY(grow(&ws->partials, 2 * nchunks * sizeof(G1xyzz)));  // boundary slots
     H2G_TRY(grow(&ws->buckets, (size_t)nbt * sizeof(G1xyzz)));
     H2G_TRY(grow(&ws->segs, ((size_t)2 * m1 + nblk) * WB * sizeof(G1xyzz)));
     H2G_TRY(grow(&ws->windows, (size_t)W * sizeof(G1xyzz)));
-    H2G_TRY(grow(&ws->result, 16));  // [0] big-bucket count, [1] valid count
+    H2G_TRY(grow(&ws->result, 16));  // [0] big-bucket count
     ws->cap_n = n;
     ws->cap_c = cfg_key;
     ws->cap_L = L;
@@ -407,7 +407,7 @@ static hipError_t msm_pipeline(const Fr* d_scalars, const G1Affine* d_bases, siz
   uint32_t* bend = (uint32_t*)ws->bucket_end;
   uint32_t* counters = (uint32_t*)ws->result;
   uint32_t* big_count = counters;
-  uint32_t* valid = counters + 1;
+  const uint32_t sentinel = nbt;  // key of zero digits (msm_digits_kernel)
   uint32_t* big_list = (uint32_t*)ws->item_bucket;
   G1xyzz* buckets = (G1xyzz*)ws->buckets;
   G1xyzz* bnd = (G1xyzz*)ws->partials;
@@ -435,27 +435,26 @@ static hipError_t msm_pipeline(const Fr* d_scalars, const G1Affine* d_bases, siz
   H2G_TRY(hipcub::DeviceRadixSort::SortKeys(ws->sort_tmp, sort_bytes, keys_in, keys_out, (int)total, 32,
                                             32 + key_bits, st));
   H2G_PHASE(2);
-  H2G_TRY(hipMemsetAsync(bstart, 0, (size_t)nbt * 4, st));
-  H2G_TRY(hipMemsetAsync(bend, 0, (size_t)nbt * 4, st));
   H2G_TRY(hipMemsetAsync(counters, 0, 8, st));
+  H2G_TRY(hipMemsetAsync(bstart, 0, (size_t)nbt * 4, st));  // empty buckets: start = end = 0
+  H2G_TRY(hipMemsetAsync(bend, 0, (size_t)nbt * 4, st));
   H2G_TRY(hipMemsetAsync(buckets, 0, (size_t)nbt * sizeof(G1xyzz), st));
-  hipLaunchKernelGGL(msm_bounds_kernel, dim3((unsigned)((total + T - 1) / T)), dim3(T), 0, st, keys_out, total,
-                     nbt, bstart, bend, valid);
   H2G_PHASE(3);
   static const bool prefetch = [] {
     const char* e = getenv("H2G_MSM_PREFETCH");
     return e ? atoi(e) != 0 : true;
   }();
+  const unsigned cgrid = (unsigned)((nchunks + T - 1) / T);
   if (prefetch)
-    hipLaunchKernelGGL(msm_acc_kernel<true>, dim3((unsigned)((nchunks + T - 1) / T)), dim3(T), 0, st, d_bases,
-                       keys_out, bstart, bend, (const uint32_t*)valid, L, buckets, bnd);
+    hipLaunchKernelGGL(msm_acc_kernel<true>, dim3(cgrid), dim3(T), 0, st, d_bases, (const uint64_t*)keys_out,
+                       (uint32_t)total, sentinel, L, buckets, bnd, bstart, bend);
   else
-    hipLaunchKernelGGL(msm_acc_kernel<false>, dim3((unsigned)((nchunks + T - 1) / T)), dim3(T), 0, st, d_bases,
-                       keys_out, bstart, bend, (const uint32_t*)valid, L, buckets, bnd);
+    hipLaunchKernelGGL(msm_acc_kernel<false>, dim3(cgrid), dim3(T), 0, st, d_bases, (const uint64_t*)keys_out,
+                       (uint32_t)total, sentinel, L, buckets, bnd, bstart, bend);
   H2G_PHASE(4);
   hipLaunchKernelGGL(msm_fixup_kernel, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend,
                      nbt, L, buckets, big_list, big_count);
-  hipLaunchKernelGGL(msm_big_bucket_kernel, dim3(256), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend, L,
+  hipLaunchKernelGGL(msm_big_bucket_kernel, dim3(32), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend, L,
                      (const uint32_t*)big_list, (const uint32_t*)big_count, buckets);
   H2G_PHASE(5);
   hipLaunchKernelGGL(msm_rgroup_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1, rS,
