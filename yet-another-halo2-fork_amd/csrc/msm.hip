@@ -21,7 +21,7 @@
 //                   otherwise it goes to the chunk's boundary slot.  The runs also
 //                   record each bucket's [start, end) in the sorted array.
 //   4. fixup      : buckets spanning chunks sum their boundary slots (one thread,
-//                   or a whole workgroup for buckets spanning > 32 chunks)
+//                   or one wavefront for buckets spanning > 32 chunks)
 //   5. segments   : per (window, segment of SEG buckets) running sums
 //                   sum_j (j+1) B_j = S_local + offset * R
 //   6. windows    : per window tree reduction of segment results in LDS
@@ -190,7 +190,7 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint64_t* __restrict__ 
 // Buckets spanning chunks, one thread per bucket: the piece in its first chunk t0 is
 // that chunk's last run (slot 1) unless the bucket starts the chunk (slot 0); every
 // later chunk holds it as its first run (slot 0).  Buckets over more than MSM_SMALL
-// chunks are summed by whole workgroups.
+// chunks are summed by one wavefront each (msm_big_bucket_kernel).
 __device__ __forceinline__ const G1xyzz& msm_piece(const G1xyzz* bnd, uint32_t t, uint32_t t0, uint32_t bs,
                                                    uint32_t L) {
   return bnd[2 * (size_t)t + ((t == t0 && bs != t0 * L) ? 1 : 0)];
@@ -215,26 +215,37 @@ msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ st
   buckets[b] = acc;
 }
 
+// One wavefront per big bucket (persistent grid): lanes sum strided pieces, then a
+// 6-level tree in the wave's LDS slice.  (Fixed-base windows make big buckets
+// common: the top window holds only the scalars' last few bits, e.g. 12 bits at
+// c = 22, so its 2^12 buckets take n / 2^12 entries each.)
+static constexpr unsigned MSM_BIG_BLOCKS = 512;
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_big_bucket_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ start,
                       const uint32_t* __restrict__ end, uint32_t L, const uint32_t* __restrict__ big_list,
                       const uint32_t* __restrict__ big_count, G1xyzz* __restrict__ buckets) {
   __shared__ G1xyzz sh[MSM_THREADS];
   const uint32_t nbig = *big_count;
-  for (uint32_t q = blockIdx.x; q < nbig; q += gridDim.x) {
+  const uint32_t lane = threadIdx.x & 63;
+  G1xyzz* w = sh + (threadIdx.x & ~63u);
+  const uint32_t nwaves = gridDim.x * (MSM_THREADS / 64);
+  for (uint32_t q = blockIdx.x * (MSM_THREADS / 64) + (threadIdx.x >> 6); q < nbig; q += nwaves) {
     const uint32_t b = big_list[q];
     const uint32_t bs = start[b], be = end[b];
     const uint32_t t0 = bs / L, t1 = (be - 1) / L;
     G1xyzz acc = G1xyzz::identity();
-    for (uint32_t t = t0 + threadIdx.x; t <= t1; t += blockDim.x) acc = xyzz_add(acc, msm_piece(bnd, t, t0, bs, L));
-    sh[threadIdx.x] = acc;
-    __syncthreads();
-    for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
-      if ((int)threadIdx.x < h) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + h]);
-      __syncthreads();
+    for (uint32_t t = t0 + lane; t <= t1; t += 64) acc = xyzz_add(acc, msm_piece(bnd, t, t0, bs, L));
+    w[lane] = acc;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+    for (uint32_t h = 32; h > 0; h >>= 1) {
+      if (lane < h) w[lane] = xyzz_add(w[lane], w[lane + h]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (threadIdx.x == 0) buckets[b] = sh[0];
-    __syncthreads();
+    if (lane == 0) buckets[b] = w[0];
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -454,7 +465,7 @@ static hipError_t msm_pipeline(const Fr* d_scalars, const G1Affine* d_bases, siz
   H2G_PHASE(4);
   hipLaunchKernelGGL(msm_fixup_kernel, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend,
                      nbt, L, buckets, big_list, big_count);
-  hipLaunchKernelGGL(msm_big_bucket_kernel, dim3(32), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend, L,
+  hipLaunchKernelGGL(msm_big_bucket_kernel, dim3(MSM_BIG_BLOCKS), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend, L,
                      (const uint32_t*)big_list, (const uint32_t*)big_count, buckets);
   H2G_PHASE(5);
   hipLaunchKernelGGL(msm_rgroup_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1, rS,
