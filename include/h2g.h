@@ -195,9 +195,29 @@ int h2g_params_create(uint32_t k, const uint64_t* g, const uint64_t* g_lagrange,
 int h2g_params_setup(uint32_t k, const uint64_t s[4], uint64_t* handle);
 int h2g_params_export(uint64_t params, uint64_t* g, uint64_t* g_lagrange); /* n x 8 u64 each, may be NULL */
 int h2g_params_free(uint64_t params);
+/* the G2 points of ParamsKZG (kzg/commitment.rs:26-27): g2 and s_g2, 16 u64 each
+ * (x.c0, x.c1, y.c0, y.c1 in Montgomery form); setup computes them, create needs set_g2
+ * before the params can be written */
+int h2g_params_g2(uint64_t params, uint64_t g2[16], uint64_t s_g2[16]);
+int h2g_params_set_g2(uint64_t params, const uint64_t g2[16], const uint64_t s_g2[16]);
+
+/* ---- serialisation: SerdeFormat (halo2_backend/src/helpers.rs:8-21) -----------------
+ * format 1 RawBytes (uncompressed points, Montgomery limbs; reads check that field
+ * elements are below the modulus and points lie on the curve), 2 RawBytesUnchecked
+ * (no checks).  0 Processed (compressed points) is refused with H2G_ERR_ARG.
+ * Writers: out == NULL returns the byte length in *len.
+ *   ParamsKZG::write_custom / read_custom  kzg/commitment.rs:166-267
+ *   ProvingKey::write / read               plonk.rs:311-359 (+ VerifyingKey::write/read :73-129)
+ * h2g_pk_read takes the constraint system from `circuit` (as the reference takes `cs`)
+ * and every array of the key from the bytes; circuit->fixed_values / ->copies unused. */
+int h2g_params_write(uint64_t params, int format, uint8_t* out, size_t cap, size_t* len);
+int h2g_params_read(const uint8_t* buf, size_t len, int format, uint64_t* handle);
 
 int h2g_keygen(uint64_t params, const h2g_circuit* circuit, uint64_t* pk);
 int h2g_pk_free(uint64_t pk);
+int h2g_pk_write(uint64_t pk, int format, uint8_t* out, size_t cap, size_t* len);
+int h2g_pk_read(uint64_t params, const h2g_circuit* circuit, const uint8_t* buf, size_t len, int format,
+                uint64_t* pk);
 /* degree, blinding_factors, extended_k, #perm sets, #advice/#fixed/#instance queries */
 int h2g_pk_info(uint64_t pk, int32_t info[8]);
 

@@ -254,3 +254,74 @@ def kate_division(a, b: int):
         q[idx - 1] = lead
         tmp = lead * b % R
     return q
+
+
+# ---------------------------------------------------------------- G2 (twist over Fq2 = Fq[u]/(u^2 + 1))
+# ParamsKZG keeps g2 and s_g2 = [s] g2 (halo2_backend/src/poly/kzg/commitment.rs:122-123).
+# Elements of Fq2 are (c0, c1) = c0 + c1 u; the twist is y^2 = x^3 + 3 / (9 + u).
+
+
+def fq2_mul(a, b):
+    return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+
+def fq2_inv(a):
+    t = pow(a[0] * a[0] + a[1] * a[1], P - 2, P)
+    return (a[0] * t % P, (-a[1]) * t % P)
+
+
+def fq2_add(a, b):
+    return ((a[0] + b[0]) % P, (a[1] + b[1]) % P)
+
+
+def fq2_sub(a, b):
+    return ((a[0] - b[0]) % P, (a[1] - b[1]) % P)
+
+
+G2_B = fq2_mul((3, 0), fq2_inv((9, 1)))
+# the standard BN254 G2 generator (EIP-197; halo2curves G2_GENERATOR_X / _Y)
+G2_GEN = ((10857046999023057135944570762232829481370756359578518086990519993285655852781,
+           11559732032986387107991004021392285783925812861821192530917403151452391805634),
+          (8495653923123431417604973247489272438418190587263600148770280649306958101930,
+           4082367875863433681332203403145435568316851327593401208105741076214120093531))
+
+
+def g2_on_curve(pt) -> bool:
+    if pt is None:
+        return True
+    x, y = pt
+    return fq2_mul(y, y) == fq2_add(fq2_mul(fq2_mul(x, x), x), G2_B)
+
+
+def g2_add(a, b):
+    if a is None:
+        return b
+    if b is None:
+        return a
+    (x1, y1), (x2, y2) = a, b
+    if x1 == x2:
+        if fq2_add(y1, y2) == (0, 0):
+            return None
+        lam = fq2_mul(fq2_mul((3, 0), fq2_mul(x1, x1)), fq2_inv(fq2_add(y1, y1)))
+    else:
+        lam = fq2_mul(fq2_sub(y2, y1), fq2_inv(fq2_sub(x2, x1)))
+    x3 = fq2_sub(fq2_sub(fq2_mul(lam, lam), x1), x2)
+    return (x3, fq2_sub(fq2_mul(lam, fq2_sub(x1, x3)), y1))
+
+
+def g2_mul(pt, k: int):
+    k %= R
+    acc, add = None, pt
+    while k:
+        if k & 1:
+            acc = g2_add(acc, add)
+        add = g2_add(add, add)
+        k >>= 1
+    return acc
+
+
+def g2_affine_mont_limbs(pt) -> list[int]:
+    """halo2curves G2Affine raw layout: x.c0, x.c1, y.c0, y.c1 Montgomery (4 u64 each)."""
+    if pt is None:
+        return [0] * 16
+    return fq_mont_limbs(pt[0][0]) + fq_mont_limbs(pt[0][1]) + fq_mont_limbs(pt[1][0]) + fq_mont_limbs(pt[1][1])

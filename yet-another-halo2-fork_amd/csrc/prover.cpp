@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <chrono>
 #include <functional>
 #include <set>
@@ -24,6 +25,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "poly.h"
+#include "g2.h"
 #include "prover_kernels.h"
 #include "runtime.h"
 #include "srs.h"
@@ -61,6 +63,9 @@ struct Params {
   // sized for the slab length (h2g_params_set_slab)
   size_t slab_lo = 0, slab_hi = 0;
   MsmFixedBase sg, sgl;
+  // the G2 half of ParamsKZG (g2, s_g2 = [s] g2; verifier side, serialised with the params)
+  bool has_g2 = false;
+  G2Affine g2, s_g2;
   Pool pool;
   ~Params() {
     msm_fixed_base_free(&fg);
@@ -103,6 +108,9 @@ struct ProvingKey {
   std::vector<std::pair<int, int>> perm_cols;
   std::vector<uint8_t> unblinded;
   Fr transcript_repr;
+  // verifying-key commitments (fixed, permutation) of a key read from bytes; a key made
+  // by keygen computes them when it is written (h2g_pk_write)
+  std::vector<G1Affine> vk_fixed, vk_perm;
   Domain dom;
   Pool pool;
   // proving key (device)
@@ -479,13 +487,21 @@ std::vector<ArgRoots> arg_roots(uint32_t na, const uint32_t* sizes, const int32_
 }
 
 // ------------------------------------------------------------------ keygen
-int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk) {
+// Proving-key arrays taken from a serialised ProvingKey (h2g_pk_read, plonk.rs:311-359)
+// instead of being computed: host pointers into the file buffer, raw Montgomery Fr
+// (SerdeFormat::RawBytes layout = the device layout).
+struct PkImage {
+  std::vector<const uint8_t*> fixed_lag, fixed_poly, fixed_coset, sigma_lag, sigma_poly, sigma_coset;
+  const uint8_t *l0 = nullptr, *l_last = nullptr, *l_active = nullptr;
+};
+
+int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, const PkImage* img = nullptr) {
   hipStream_t st = d->stream;
   std::string why;
   if (c->k != prm.k) return fail(H2G_ERR_ARG, "keygen: circuit k != params k");
   if (c->num_gates && (!c->gate_roots || !c->nodes)) return fail(H2G_ERR_ARG, "keygen: null gates");
   if (!check_nodes(c, &why)) return fail(H2G_ERR_ARG, "keygen: bad expression graph: " + why);
-  if (c->num_fixed && !c->fixed_values) return fail(H2G_ERR_ARG, "keygen: null fixed values");
+  if (!img && c->num_fixed && !c->fixed_values) return fail(H2G_ERR_ARG, "keygen: null fixed values");
   if (!c->transcript_repr) return fail(H2G_ERR_ARG, "keygen: null transcript_repr");
   const CircuitView cv{c};
   pk.device = d->id;
@@ -641,6 +657,12 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk) {
   HIPCHK(vec_alloc(pk.fixed_poly, pk.F, n));
   HIPCHK(vec_alloc(pk.fixed_coset, pk.F, ext));
   for (int i = 0; i < pk.F; i++) {
+    if (img) {
+      HIPCHK(hipMemcpyAsync(pk.fixed_lag[i], img->fixed_lag[i], n * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(pk.fixed_poly[i], img->fixed_poly[i], n * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(pk.fixed_coset[i], img->fixed_coset[i], ext * sizeof(Fr), hipMemcpyHostToDevice, st));
+      continue;
+    }
     HIPCHK(hipMemcpyAsync(pk.fixed_lag[i], c->fixed_values + 4 * n * i, n * sizeof(Fr), hipMemcpyHostToDevice, st));
     RCCHK(lagrange_to_coeff(d, pk.dom, pk.fixed_lag[i], pk.fixed_poly[i], st));
     RCCHK(coeff_to_extended(d, pk.dom, pk.fixed_poly[i], pk.fixed_coset[i], st));
@@ -649,7 +671,11 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk) {
   HIPCHK(falloc(&pk.l0, ext));
   HIPCHK(falloc(&pk.l_last, ext));
   HIPCHK(falloc(&pk.l_active, ext));
-  {
+  if (img) {
+    HIPCHK(hipMemcpyAsync(pk.l0, img->l0, ext * sizeof(Fr), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(pk.l_last, img->l_last, ext * sizeof(Fr), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(pk.l_active, img->l_active, ext * sizeof(Fr), hipMemcpyHostToDevice, st));
+  } else {
     const Fr one = Fr::one();
     std::vector<Fr> ones(pk.bf, one);
     auto lagrange_unit = [&](size_t row0, int count, Fr* out) -> int {
@@ -671,7 +697,14 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk) {
   HIPCHK(vec_alloc(pk.sigma_lag, pk.P, n));
   HIPCHK(vec_alloc(pk.sigma_poly, pk.P, n));
   HIPCHK(vec_alloc(pk.sigma_coset, pk.P, ext));
-  if (pk.P) {
+  if (pk.P && img) {
+    for (int i = 0; i < pk.P; i++) {
+      HIPCHK(hipMemcpyAsync(pk.sigma_lag[i], img->sigma_lag[i], n * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(pk.sigma_poly[i], img->sigma_poly[i], n * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(pk.sigma_coset[i], img->sigma_coset[i], ext * sizeof(Fr), hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+  } else if (pk.P) {
     const size_t cells = (size_t)pk.P * n;
     std::vector<uint32_t> mcol(cells), mrow(cells), acol(cells), arow(cells);
     std::vector<uint64_t> sizes(cells, 1);
@@ -1463,6 +1496,11 @@ int h2g_params_setup(uint32_t k, const uint64_t s_limbs[4], uint64_t* handle) {
   HIPCHK(g1_generator_mul(sc, n, p->gl, st));
   HIPCHK(hipStreamSynchronize(st));
   RCCHK(params_finish(*p, st));
+  // g2 = generator, s_g2 = [s] g2 (kzg/commitment.rs:122-123)
+  p->g2 = g2_generator();
+  const Fr s_can = to_canonical(s);
+  p->s_g2 = g2_mul(p->g2, s_can.l);
+  p->has_g2 = true;
   *handle = g_next_handle++;
   g_params[*handle] = std::move(p);
   return H2G_OK;
@@ -1495,6 +1533,330 @@ int h2g_keygen(uint64_t params, const h2g_circuit* circuit, uint64_t* pk_out) {
     domain_release(&pk->dom);
     return rc;
   }
+  *pk_out = g_next_handle++;
+  g_pks[*pk_out] = std::move(pk);
+  return H2G_OK;
+}
+
+// ------------------------------------------------------------------ serialisation
+// SerdeFormat (halo2_backend/src/helpers.rs:8-21): 0 Processed, 1 RawBytes,
+// 2 RawBytesUnchecked.  RawBytes writes points uncompressed and field elements as their
+// Montgomery limbs -- the device layout, so arrays move with one copy -- and on read
+// checks that every element is below its modulus and every point is on its curve (on
+// the device for the n-sized arrays).  Processed (compressed points, canonical field
+// elements) is refused: halo2curves' compressed-point flag bits cannot be pinned here.
+}  // extern "C"
+
+namespace {
+enum { SERDE_PROCESSED = 0, SERDE_RAW = 1, SERDE_RAW_UNCHECKED = 2 };
+constexpr uint8_t PK_VERSION = 0x04;  // plonk.rs:58
+
+struct ByteWriter {  // out == NULL: count only
+  uint8_t* out;
+  size_t cap, len = 0;
+  bool fits(size_t k) const { return out && len + k <= cap; }
+  void put(const void* p, size_t k) {
+    if (fits(k)) std::memcpy(out + len, p, k);
+    len += k;
+  }
+  void u8(uint8_t v) { put(&v, 1); }
+  void u32le(uint32_t v) { put(&v, 4); }
+  void u32be(uint32_t v) {
+    const uint8_t b[4] = {(uint8_t)(v >> 24), (uint8_t)(v >> 16), (uint8_t)(v >> 8), (uint8_t)v};
+    put(b, 4);
+  }
+  int dev(const void* d, size_t k) {  // device bytes
+    if (fits(k)) HIPCHK(hipMemcpy(out + len, d, k, hipMemcpyDeviceToHost));
+    len += k;
+    return H2G_OK;
+  }
+  void g1(const G1Affine& a) { put(&a, sizeof(G1Affine)); }
+  void g2(const G2Affine& a) { put(&a, sizeof(G2Affine)); }
+  int poly(const Fr* d, size_t cnt) {  // Polynomial::write (poly.rs:187-197)
+    u32be((uint32_t)cnt);
+    return dev(d, cnt * sizeof(Fr));
+  }
+  int polys(const std::vector<Fr*>& v, size_t cnt) {  // write_polynomial_slice (helpers.rs:119-129)
+    u32be((uint32_t)v.size());
+    for (const Fr* p : v) RCCHK(poly(p, cnt));
+    return H2G_OK;
+  }
+};
+
+struct ByteReader {
+  const uint8_t* p;
+  size_t len, pos = 0;
+  bool ok = true;
+  const uint8_t* take(size_t k) {
+    if (!ok || pos + k > len) {
+      ok = false;
+      return nullptr;
+    }
+    const uint8_t* r = p + pos;
+    pos += k;
+    return r;
+  }
+  uint8_t u8() {
+    const uint8_t* b = take(1);
+    return b ? b[0] : 0;
+  }
+  uint32_t u32le() {
+    const uint8_t* b = take(4);
+    return b ? (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24 : 0;
+  }
+  uint32_t u32be() {
+    const uint8_t* b = take(4);
+    return b ? (uint32_t)b[3] | (uint32_t)b[2] << 8 | (uint32_t)b[1] << 16 | (uint32_t)b[0] << 24 : 0;
+  }
+  // one polynomial of exactly `cnt` elements (read_polynomial_vec / Polynomial::read)
+  const uint8_t* poly(size_t cnt) {
+    if (u32be() != cnt) ok = false;
+    return take(cnt * sizeof(Fr));
+  }
+  bool polys(std::vector<const uint8_t*>& v, size_t count, size_t cnt) {
+    if (u32be() != count) return ok = false;
+    v.resize(count);
+    for (auto& q : v) q = poly(cnt);
+    return ok;
+  }
+};
+
+bool fq_below(const Fq& a) {
+  unsigned br = 0;
+  for (int i = 0; i < 8; i++) (void)__builtin_subc(a.l[i], FqParams::M[i], br, &br);
+  return br != 0;
+}
+bool g2_valid(const G2Affine& a) {
+  return fq_below(a.x.c0) && fq_below(a.x.c1) && fq_below(a.y.c0) && fq_below(a.y.c1) && g2_on_curve(a);
+}
+bool g1_valid_host(const G1Affine& a) {
+  if (!fq_below(a.x) || !fq_below(a.y)) return false;
+  return a.is_identity() || sqr(a.y) == sqr(a.x) * a.x + from_u64<FqParams>(3);
+}
+
+// device RawBytes checks of uploaded arrays: number of bad elements
+int count_bad_fr(const std::vector<std::pair<const Fr*, size_t>>& arrays, hipStream_t st, uint32_t* bad_out) {
+  uint32_t* bad;
+  HIPCHK(hipMalloc(&bad, 4));
+  HIPCHK(hipMemsetAsync(bad, 0, 4, st));
+  for (const auto& a : arrays) HIPCHK(fr_count_unreduced(a.first, a.second, bad, st));
+  HIPCHK(hipMemcpyAsync(bad_out, bad, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  (void)hipFree(bad);
+  return H2G_OK;
+}
+}  // namespace
+
+extern "C" {
+
+/* ParamsKZG::write_custom (kzg/commitment.rs:166-181): k (u32 LE), g, g_lagrange, g2, s_g2 */
+int h2g_params_write(uint64_t params, int format, uint8_t* out, size_t cap, size_t* len) {
+  NEED_DEV_P();
+  auto it = g_params.find(params);
+  if (it == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  if (!len) return fail(H2G_ERR_ARG, "params_write: null length");
+  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED)
+    return fail(H2G_ERR_ARG, "params_write: only SerdeFormat::RawBytes / RawBytesUnchecked are supported");
+  const Params& p = *it->second;
+  if (!p.has_g2) return fail(H2G_ERR_STATE, "params_write: the params have no G2 points (h2g_params_set_g2)");
+  ByteWriter w{out, out ? cap : 0};
+  w.u32le(p.k);
+  RCCHK(w.dev(p.g, p.n * sizeof(G1Affine)));
+  RCCHK(w.dev(p.gl, p.n * sizeof(G1Affine)));
+  w.g2(p.g2);
+  w.g2(p.s_g2);
+  *len = w.len;
+  if (out && w.len > cap) return fail(H2G_ERR_ARG, "params_write: buffer too small");
+  return H2G_OK;
+}
+
+/* ParamsKZG::read_custom (kzg/commitment.rs:183-267) */
+int h2g_params_read(const uint8_t* buf, size_t len, int format, uint64_t* handle) {
+  NEED_DEV_P();
+  if (!buf || !handle) return fail(H2G_ERR_ARG, "params_read: null argument");
+  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED)
+    return fail(H2G_ERR_ARG, "params_read: only SerdeFormat::RawBytes / RawBytesUnchecked are supported");
+  ByteReader r{buf, len};
+  const uint32_t k = r.u32le();
+  if (!r.ok || k > 27) return fail(H2G_ERR_ARG, "params_read: bad k");
+  const size_t n = (size_t)1 << k;
+  const uint8_t* g = r.take(n * sizeof(G1Affine));
+  const uint8_t* gl = r.take(n * sizeof(G1Affine));
+  const uint8_t* g2 = r.take(sizeof(G2Affine));
+  const uint8_t* sg2 = r.take(sizeof(G2Affine));
+  if (!r.ok) return fail(H2G_ERR_ARG, "params_read: truncated input");
+  hipStream_t st = d->stream;
+  auto p = std::make_unique<Params>();
+  p->device = d->id;
+  p->k = k;
+  p->n = n;
+  PALLOC(p->pool, p->g, n);
+  PALLOC(p->pool, p->gl, n);
+  HIPCHK(hipMemcpyAsync(p->g, g, n * sizeof(G1Affine), hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(p->gl, gl, n * sizeof(G1Affine), hipMemcpyHostToDevice, st));
+  std::memcpy(&p->g2, g2, sizeof(G2Affine));
+  std::memcpy(&p->s_g2, sg2, sizeof(G2Affine));
+  p->has_g2 = true;
+  if (format == SERDE_RAW) {
+    uint32_t* bad;
+    uint32_t nbad = 0;
+    HIPCHK(hipMalloc(&bad, 4));
+    HIPCHK(hipMemsetAsync(bad, 0, 4, st));
+    HIPCHK(g1_count_invalid(p->g, n, bad, st));
+    HIPCHK(g1_count_invalid(p->gl, n, bad, st));
+    HIPCHK(hipMemcpyAsync(&nbad, bad, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    (void)hipFree(bad);
+    if (nbad) return fail(H2G_ERR_ARG, "params_read: " + std::to_string(nbad) + " G1 points off the curve or unreduced");
+    if (!g2_valid(p->g2) || !g2_valid(p->s_g2)) return fail(H2G_ERR_ARG, "params_read: invalid G2 point");
+  }
+  RCCHK(params_finish(*p, st));
+  *handle = g_next_handle++;
+  g_params[*handle] = std::move(p);
+  return H2G_OK;
+}
+
+/* the G2 points of the params: 16 u64 each (x.c0, x.c1, y.c0, y.c1, Montgomery) */
+int h2g_params_g2(uint64_t params, uint64_t g2[16], uint64_t s_g2[16]) {
+  NEED_DEV_P();
+  auto it = g_params.find(params);
+  if (it == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  if (!it->second->has_g2) return fail(H2G_ERR_STATE, "params have no G2 points");
+  if (g2) std::memcpy(g2, &it->second->g2, sizeof(G2Affine));
+  if (s_g2) std::memcpy(s_g2, &it->second->s_g2, sizeof(G2Affine));
+  return H2G_OK;
+}
+int h2g_params_set_g2(uint64_t params, const uint64_t g2[16], const uint64_t s_g2[16]) {
+  NEED_DEV_P();
+  auto it = g_params.find(params);
+  if (it == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  if (!g2 || !s_g2) return fail(H2G_ERR_ARG, "params_set_g2: null argument");
+  G2Affine a, b;
+  std::memcpy(&a, g2, sizeof(G2Affine));
+  std::memcpy(&b, s_g2, sizeof(G2Affine));
+  if (!g2_valid(a) || !g2_valid(b)) return fail(H2G_ERR_ARG, "params_set_g2: invalid G2 point");
+  it->second->g2 = a;
+  it->second->s_g2 = b;
+  it->second->has_g2 = true;
+  return H2G_OK;
+}
+
+/* ProvingKey::write (plonk.rs:311-321) with VerifyingKey::write (plonk.rs:73-86) */
+int h2g_pk_write(uint64_t pk_h, int format, uint8_t* out, size_t cap, size_t* len) {
+  NEED_DEV_P();
+  auto it = g_pks.find(pk_h);
+  if (it == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
+  if (!len) return fail(H2G_ERR_ARG, "pk_write: null length");
+  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED)
+    return fail(H2G_ERR_ARG, "pk_write: only SerdeFormat::RawBytes / RawBytesUnchecked are supported");
+  ProvingKey& pk = *it->second;
+  auto pit = g_params.find(pk.params);
+  if (pit == g_params.end()) return fail(H2G_ERR_HANDLE, "pk_write: the key's params were freed");
+  if (pk.vk_fixed.size() != (size_t)pk.F || pk.vk_perm.size() != (size_t)pk.P) {  // commit_lagrange
+    std::vector<G1Affine> f(pk.F), q(pk.P);
+    for (int i = 0; i < pk.F; i++) RCCHK(commit(d, *pit->second, pk.fixed_lag[i], pk.n, SRS_LAGRANGE, &f[i], d->stream));
+    for (int i = 0; i < pk.P; i++) RCCHK(commit(d, *pit->second, pk.sigma_lag[i], pk.n, SRS_LAGRANGE, &q[i], d->stream));
+    pk.vk_fixed = f;
+    pk.vk_perm = q;
+  }
+  HIPCHK(hipStreamSynchronize(d->stream));
+  ByteWriter w{out, out ? cap : 0};
+  w.u8(PK_VERSION);
+  w.u8((uint8_t)pk.k);
+  w.u32le((uint32_t)pk.F);
+  for (const auto& c : pk.vk_fixed) w.g1(c);
+  for (const auto& c : pk.vk_perm) w.g1(c);  // permutation::VerifyingKey::write
+  RCCHK(w.poly(pk.l0, pk.ext));
+  RCCHK(w.poly(pk.l_last, pk.ext));
+  RCCHK(w.poly(pk.l_active, pk.ext));
+  RCCHK(w.polys(pk.fixed_lag, pk.n));
+  RCCHK(w.polys(pk.fixed_poly, pk.n));
+  RCCHK(w.polys(pk.fixed_coset, pk.ext));
+  RCCHK(w.polys(pk.sigma_lag, pk.n));  // permutation::ProvingKey::write (permutation.rs:82-91)
+  RCCHK(w.polys(pk.sigma_poly, pk.n));
+  RCCHK(w.polys(pk.sigma_coset, pk.ext));
+  *len = w.len;
+  if (out && w.len > cap) return fail(H2G_ERR_ARG, "pk_write: buffer too small");
+  return H2G_OK;
+}
+
+/* ProvingKey::read (plonk.rs:334-359): like the reference, the circuit (its constraint
+ * system) comes from the caller; the key's arrays and commitments come from the bytes
+ * (circuit->fixed_values and ->copies are not used and may be NULL). */
+int h2g_pk_read(uint64_t params, const h2g_circuit* circuit, const uint8_t* buf, size_t len, int format,
+                uint64_t* pk_out) {
+  NEED_DEV_P();
+  auto it = g_params.find(params);
+  if (it == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  if (!circuit || !buf || !pk_out) return fail(H2G_ERR_ARG, "pk_read: null argument");
+  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED)
+    return fail(H2G_ERR_ARG, "pk_read: only SerdeFormat::RawBytes / RawBytesUnchecked are supported");
+  ByteReader r{buf, len};
+  if (r.u8() != PK_VERSION) return fail(H2G_ERR_ARG, "pk_read: unexpected version byte");
+  const uint32_t k = r.u8();
+  if (!r.ok || k != circuit->k || k != it->second->k) return fail(H2G_ERR_ARG, "pk_read: k does not match");
+  const uint32_t F = r.u32le();
+  if (!r.ok || F != circuit->num_fixed) return fail(H2G_ERR_ARG, "pk_read: fixed column count does not match");
+  const uint32_t P = circuit->num_perm_columns;
+  std::vector<G1Affine> vf(F), vp(P);
+  for (auto& c : vf)
+    if (const uint8_t* b = r.take(sizeof(G1Affine))) std::memcpy(&c, b, sizeof(G1Affine));
+  for (auto& c : vp)
+    if (const uint8_t* b = r.take(sizeof(G1Affine))) std::memcpy(&c, b, sizeof(G1Affine));
+  if (!r.ok) return fail(H2G_ERR_ARG, "pk_read: truncated verifying key");
+  if (format == SERDE_RAW) {
+    for (const auto& c : vf)
+      if (!g1_valid_host(c)) return fail(H2G_ERR_ARG, "pk_read: invalid fixed commitment");
+    for (const auto& c : vp)
+      if (!g1_valid_host(c)) return fail(H2G_ERR_ARG, "pk_read: invalid permutation commitment");
+  }
+  // the extended domain size follows from the constraint system (keygen::create_domain):
+  // taken from the first polynomial here and checked against the keygen's below
+  const size_t n = (size_t)1 << k;
+  PkImage img;
+  const uint8_t *l0, *ll, *la;
+  const uint32_t ext_len = r.u32be();
+  if (!r.ok || ext_len < n || (ext_len & (ext_len - 1))) return fail(H2G_ERR_ARG, "pk_read: bad l0 length");
+  l0 = r.take((size_t)ext_len * sizeof(Fr));
+  ll = r.poly(ext_len);
+  la = r.poly(ext_len);
+  img.l0 = l0;
+  img.l_last = ll;
+  img.l_active = la;
+  r.polys(img.fixed_lag, F, n);
+  r.polys(img.fixed_poly, F, n);
+  r.polys(img.fixed_coset, F, ext_len);
+  r.polys(img.sigma_lag, P, n);
+  r.polys(img.sigma_poly, P, n);
+  r.polys(img.sigma_coset, P, ext_len);
+  if (!r.ok) return fail(H2G_ERR_ARG, "pk_read: truncated or mis-sized proving key");
+  if (r.pos != len) return fail(H2G_ERR_ARG, "pk_read: trailing bytes");
+  auto pk = std::make_unique<ProvingKey>();
+  pk->params = params;
+  int rc = keygen_impl(d, *it->second, circuit, *pk, &img);
+  if (rc == H2G_OK && pk->ext != ext_len) rc = fail(H2G_ERR_ARG, "pk_read: extended domain size does not match the circuit");
+  if (rc == H2G_OK && format == SERDE_RAW) {
+    std::vector<std::pair<const Fr*, size_t>> arrays = {{pk->l0, pk->ext}, {pk->l_last, pk->ext}, {pk->l_active, pk->ext}};
+    for (int i = 0; i < pk->F; i++) {
+      arrays.push_back({pk->fixed_lag[i], n});
+      arrays.push_back({pk->fixed_poly[i], n});
+      arrays.push_back({pk->fixed_coset[i], pk->ext});
+    }
+    for (int i = 0; i < pk->P; i++) {
+      arrays.push_back({pk->sigma_lag[i], n});
+      arrays.push_back({pk->sigma_poly[i], n});
+      arrays.push_back({pk->sigma_coset[i], pk->ext});
+    }
+    uint32_t nbad = 0;
+    rc = count_bad_fr(arrays, d->stream, &nbad);
+    if (rc == H2G_OK && nbad) rc = fail(H2G_ERR_ARG, "pk_read: " + std::to_string(nbad) + " field elements not below the modulus");
+  }
+  if (rc) {
+    domain_release(&pk->dom);
+    return rc;
+  }
+  pk->vk_fixed = vf;
+  pk->vk_perm = vp;
   *pk_out = g_next_handle++;
   g_pks[*pk_out] = std::move(pk);
   return H2G_OK;

@@ -162,4 +162,10 @@ hipError_t srs_lagrange_scalars(Fr* out, size_t n, const Fr& s, const Fr& mult, 
                                 hipStream_t st);
 hipError_t g1_generator_mul(const Fr* scalars, size_t n, G1Affine* out, hipStream_t st);
 
+// ---- SerdeFormat::RawBytes checks (helpers.rs:40-48): *bad += count of elements not
+// below the modulus (Fr arrays) / points with a coordinate >= p or off y^2 = x^3 + 3
+// (identity (0, 0) allowed).  *bad must be zeroed by the caller.
+hipError_t fr_count_unreduced(const Fr* a, size_t n, uint32_t* bad, hipStream_t st);
+hipError_t g1_count_invalid(const G1Affine* p, size_t n, uint32_t* bad, hipStream_t st);
+
 }  // namespace h2g

@@ -646,4 +646,42 @@ hipError_t g1_generator_mul(const Fr* scalars, size_t n, G1Affine* out, hipStrea
   return hipGetLastError();
 }
 
+// ---- RawBytes checks ---------------------------------------------------------
+template <class P>
+__device__ __forceinline__ bool below_modulus(const Fe<P>& a) {
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) (void)__builtin_subc(a.l[i], P::M[i], br, &br);
+  return br != 0;  // a - M borrows <=> a < M
+}
+// one no-return atomic per wave that saw a bad element (bad inputs are the rare case)
+__device__ __forceinline__ void count_bad(bool bad, uint32_t* out) {
+  const uint64_t m = __ballot(bad);
+  if (m && __lane_id() == (uint32_t)__builtin_ctzll(m)) atomicAdd(out, (uint32_t)__popcll(m));
+}
+__global__ void __launch_bounds__(KT) fr_unreduced_kernel(const Fr* __restrict__ a, size_t n, uint32_t* bad) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  count_bad(i < n && !below_modulus(a[i]), bad);
+}
+__global__ void __launch_bounds__(KT) g1_invalid_kernel(const G1Affine* __restrict__ p, size_t n, uint32_t* bad) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  bool b = false;
+  if (i < n) {
+    const G1Affine q = p[i];
+    if (!below_modulus(q.x) || !below_modulus(q.y)) b = true;
+    else if (!q.is_identity()) b = sqr(q.y) != sqr(q.x) * q.x + from_u64<FqParams>(3);
+  }
+  count_bad(b, bad);
+}
+hipError_t fr_count_unreduced(const Fr* a, size_t n, uint32_t* bad, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(fr_unreduced_kernel, dim3((unsigned)((n + KT - 1) / KT)), dim3(KT), 0, st, a, n, bad);
+  return hipGetLastError();
+}
+hipError_t g1_count_invalid(const G1Affine* p, size_t n, uint32_t* bad, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(g1_invalid_kernel, dim3((unsigned)((n + KT - 1) / KT)), dim3(KT), 0, st, p, n, bad);
+  return hipGetLastError();
+}
+
 }  // namespace h2g

@@ -82,6 +82,12 @@ _SIGS = {
     "h2g_params_setup": ([U32, U64P, ctypes.POINTER(U64)], I32),
     "h2g_params_export": ([U64, U64P, U64P], I32),
     "h2g_params_free": ([U64], I32),
+    "h2g_params_g2": ([U64, U64P, U64P], I32),
+    "h2g_params_set_g2": ([U64, U64P, U64P], I32),
+    "h2g_params_write": ([U64, I32, VP, SZ, ctypes.POINTER(SZ)], I32),
+    "h2g_params_read": ([ctypes.c_char_p, SZ, I32, ctypes.POINTER(U64)], I32),
+    "h2g_pk_write": ([U64, I32, VP, SZ, ctypes.POINTER(SZ)], I32),
+    "h2g_pk_read": ([U64, VP, ctypes.c_char_p, SZ, I32, ctypes.POINTER(U64)], I32),
     "h2g_keygen": ([U64, VP, ctypes.POINTER(U64)], I32),
     "h2g_pk_free": ([U64], I32),
     "h2g_pk_info": ([U64, ctypes.POINTER(ctypes.c_int32)], I32),
@@ -428,13 +434,27 @@ def _ptr(a, t):
     return a.ctypes.data_as(t) if a is not None and a.size else None
 
 
-class Params:
-    """ParamsKZG resident on the device (g, g_lagrange)."""
+# SerdeFormat (halo2_backend/src/helpers.rs:8-21)
+PROCESSED, RAW_BYTES, RAW_BYTES_UNCHECKED = 0, 1, 2
 
-    def __init__(self, k, g=None, g_lagrange=None, s=None):
+
+def _write_bytes(fn, handle, fmt):
+    ln = SZ()
+    check(fn(handle, fmt, None, 0, ctypes.byref(ln)))
+    buf = ctypes.create_string_buffer(max(ln.value, 1))
+    check(fn(handle, fmt, ctypes.cast(buf, VP), ln.value, ctypes.byref(ln)))
+    return buf.raw[: ln.value]
+
+
+class Params:
+    """ParamsKZG resident on the device (g, g_lagrange; g2, s_g2 on the host)."""
+
+    def __init__(self, k, g=None, g_lagrange=None, s=None, _handle=None):
         self.k = k
         h = U64()
-        if s is not None:
+        if _handle is not None:
+            h.value = _handle
+        elif s is not None:
             s = np.ascontiguousarray(s, dtype=np.uint64)
             check(lib().h2g_params_setup(k, p64(s), ctypes.byref(h)))
         else:
@@ -442,6 +462,30 @@ class Params:
             gl = np.ascontiguousarray(g_lagrange, dtype=np.uint64)
             check(lib().h2g_params_create(k, p64(g), p64(gl), ctypes.byref(h)))
         self.handle = h.value
+
+    @classmethod
+    def read(cls, data, fmt=RAW_BYTES):
+        """ParamsKZG::read_custom (kzg/commitment.rs:183-267)"""
+        h = U64()
+        check(lib().h2g_params_read(bytes(data), len(data), fmt, ctypes.byref(h)))
+        k = int.from_bytes(bytes(data[:4]), "little")
+        return cls(k, _handle=h.value)
+
+    def write(self, fmt=RAW_BYTES):
+        """ParamsKZG::write_custom (kzg/commitment.rs:166-181) -> bytes"""
+        return _write_bytes(lib().h2g_params_write, self.handle, fmt)
+
+    def g2(self):
+        """(g2, s_g2) as 16 u64 each (x.c0, x.c1, y.c0, y.c1 Montgomery)"""
+        a = np.zeros(16, dtype=np.uint64)
+        b = np.zeros(16, dtype=np.uint64)
+        check(lib().h2g_params_g2(self.handle, p64(a), p64(b)))
+        return a, b
+
+    def set_g2(self, g2, s_g2):
+        a = np.ascontiguousarray(g2, dtype=np.uint64)
+        b = np.ascontiguousarray(s_g2, dtype=np.uint64)
+        check(lib().h2g_params_set_g2(self.handle, p64(a), p64(b)))
 
     def set_slab(self, lo, hi):
         """fixed-base windows for this rank's point slab [lo, hi) (one proof over several GPUs)"""
@@ -463,7 +507,8 @@ class Params:
 class ProvingKey:
     """keygen_vk + keygen_pk on the device for an h2g_circuit.Circuit."""
 
-    def __init__(self, params, circ):
+    def __init__(self, params, circ, data=None, fmt=RAW_BYTES):
+        """keygen, or -- with `data` -- ProvingKey::read of serialised bytes (plonk.rs:334-359)"""
         self.params = params
         self.circ = circ
         keep = [np.ascontiguousarray(x) for x in (circ.gate_roots, circ.nodes, circ.constants, circ.perm_array,
@@ -479,12 +524,19 @@ class ProvingKey:
                        len(circ.lookups), _ptr(lks, ctypes.POINTER(U32)), _ptr(lkr, I32P_),
                        len(circ.shuffles), _ptr(shs, ctypes.POINTER(U32)), _ptr(shr, I32P_))
         h = U64()
-        check(lib().h2g_keygen(params.handle, ctypes.byref(c), ctypes.byref(h)))
+        if data is None:
+            check(lib().h2g_keygen(params.handle, ctypes.byref(c), ctypes.byref(h)))
+        else:
+            check(lib().h2g_pk_read(params.handle, ctypes.byref(c), bytes(data), len(data), fmt, ctypes.byref(h)))
         self.handle = h.value
         info = (ctypes.c_int32 * 8)()
         check(lib().h2g_pk_info(self.handle, info))
         (self.degree, self.bf, self.extended_k, self.nsets, self.n_adv_q, self.n_fix_q, self.n_ins_q,
          self.n_slots) = list(info)
+
+    def write(self, fmt=RAW_BYTES):
+        """ProvingKey::write (plonk.rs:311-321) -> bytes"""
+        return _write_bytes(lib().h2g_pk_write, self.handle, fmt)
 
     def create_proof(self, wit=None, seed=bytes([7] * 32), vanishing_threads=8, advice_dev_ptr=None):
         """-> proof bytes.  advice_dev_ptr: device pointer to num_advice x n Fr (resident inputs)."""
