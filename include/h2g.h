@@ -220,6 +220,11 @@ int h2g_pk_read(uint64_t params, const h2g_circuit* circuit, const uint8_t* buf,
                 uint64_t* pk);
 /* degree, blinding_factors, extended_k, #perm sets, #advice/#fixed/#instance queries */
 int h2g_pk_info(uint64_t pk, int32_t info[8]);
+/* the multi-open argument h2g_create_proof ends with -- the reference's Prover type
+ * parameter of create_proof (halo2_proofs/src/plonk/prover.rs:19-36): 0 ProverSHPLONK
+ * (default; poly/kzg/multiopen/shplonk/prover.rs:121-305), 1 ProverGWC
+ * (poly/kzg/multiopen/gwc/prover.rs:40-90) */
+int h2g_pk_set_multiopen(uint64_t pk, int scheme);
 
 /* advice: num_advice x n Fr; instance: num_instance x n Fr (zero padded), of which
  * instance_lens[i] values enter the transcript.  Writes the proof bytes.

@@ -16,6 +16,7 @@
  *   vanishing commit / construct / evaluate / open  halo2_backend/src/plonk/vanishing/prover.rs:40-205
  *   evaluate_h (gates + permutation)   halo2_backend/src/plonk/evaluation.rs:317-483
  *   SHPLONK create_proof               halo2_backend/src/poly/kzg/multiopen/shplonk/prover.rs:121-305
+ *   GWC create_proof                   halo2_backend/src/poly/kzg/multiopen/gwc/prover.rs:40-90, gwc.rs:25-50
  *   construct_intermediate_sets        halo2_backend/src/poly/kzg/multiopen/shplonk.rs:48-140
  *   Blake2bWrite transcript            halo2_backend/src/transcript.rs:120-130,353-419,500-539
  *   lookup argument                    halo2_backend/src/plonk/lookup/prover.rs:64-494
@@ -64,6 +65,7 @@ typedef struct {
     uint32_t num_shuffles;
     const uint32_t *shuffle_sizes;
     const int32_t *shuffle_roots;   /* per shuffle: m input roots, then m shuffle roots */
+    uint32_t multiopen;             /* 0 ProverSHPLONK, 1 ProverGWC (poly/kzg/multiopen) */
 } or_spec;
 
 typedef struct { int type, index, rot; } query_t;
@@ -916,6 +918,39 @@ int or_prove(const or_pk *pk, const or_spec *s, uint8_t *proof, uint64_t proof_c
     for (int c = 0; c < P; c++) { Q[nq].point = x; Q[nq++].poly_id = A_ + F_ + c; }
     Q[nq].point = x; Q[nq++].poly_id = id_h;
     Q[nq].point = x; Q[nq++].poly_id = id_r;
+
+    if (s->multiopen == 1) {
+        /* ---- ProverGWC::create_proof_with_engine (gwc/prover.rs:40-90): queries grouped by
+           point in first-appearance order (construct_intermediate_sets, gwc.rs:25-50); per
+           point sum_i v^i (p_i - e_i), divided by (X - z), committed against g ---- */
+        fe v = tr_squeeze(&T);
+        int *done = (int *)calloc(nq, sizeof(int));
+        fe *batch = fr_alloc(n), *q = fr_alloc(n);
+        for (int i = 0; i < nq; i++) {
+            if (done[i]) continue;
+            const fe z = Q[i].point;
+            fe evb, vp = fr_ONE;
+            memset(&evb, 0, sizeof(evb));
+            memset(batch, 0, n * 32);
+            for (int j = i; j < nq; j++) {
+                if (done[j] || !fe_eq(&Q[j].point, &z)) continue;
+                done[j] = 1;
+                const fe *pj = polys[Q[j].poly_id];
+                fe e = eval_poly(pj, n, &z), t;
+                for (uint64_t r = 0; r < n; r++) { fr_mul(&t, &pj[r], &vp); fr_add(&batch[r], &batch[r], &t); }
+                fr_mul(&t, &e, &vp); fr_add(&evb, &evb, &t);
+                fr_mul(&vp, &vp, &v);
+            }
+            fr_sub(&batch[0], &batch[0], &evb);   /* poly_batch - eval_batch (Sub<F>, poly.rs:268-276) */
+            or_kate_division((uint64_t *)batch, n, z.v, (uint64_t *)q);
+            g1a cm; commit_msm(q, n - 1, s->srs_g, threads, &cm);
+            if (tr_write_point(&T, &cm)) return -5;
+        }
+        free(done); free(batch); free(q);
+        *proof_len = T.len;
+        free(h_poly); free(random_poly);
+        return T.len <= proof_cap ? 0 : -6;
+    }
 
     /* ---- SHPLONK (shplonk/prover.rs:121-305, shplonk.rs:48-140) ---- */
     fe sy = tr_squeeze(&T);

@@ -9,6 +9,7 @@ Restated reference code (paths relative to the reference root):
   vanishing verifier               halo2_backend/src/plonk/vanishing/verifier.rs:40-137
   permutation verifier             halo2_backend/src/plonk/permutation/verifier.rs:33-253
   VerifierSHPLONK::verify_proof    halo2_backend/src/poly/kzg/multiopen/shplonk/verifier.rs:45-140
+  VerifierGWC::verify_proof        halo2_backend/src/poly/kzg/multiopen/gwc/verifier.rs:42-123, gwc.rs:25-50
   construct_intermediate_sets      halo2_backend/src/poly/kzg/multiopen/shplonk.rs:48-140
   l_i_range                        halo2_backend/src/poly/domain.rs:425-450
   DualMSM::check                   halo2_backend/src/poly/kzg/msm.rs:188-206
@@ -200,8 +201,9 @@ class Msm:
 
 
 # ----------------------------------------------------------------------------- verify
-def verify(circ, instances, proof: bytes, s: int, instance_lens=None):
-    """Returns True iff the proof verifies (raises VerifyError on malformed input)."""
+def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen="shplonk"):
+    """Returns True iff the proof verifies (raises VerifyError on malformed input).
+    multiopen: "shplonk" (VerifierSHPLONK) or "gwc" (VerifierGWC)."""
     from h2g_circuit import fr_from_limbs
     adv_q, fix_q, ins_q = circ.queries()
     degree = circ.degree()
@@ -353,6 +355,9 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None):
     queries.append((("h",), h_msm, x, expected_h_eval))
     queries.append((("random",), random_cm, x, random_eval))
 
+    if multiopen == "gwc":
+        return _verify_gwc(T, queries, proof, s)
+
     # SHPLONK (construct_intermediate_sets + VerifierSHPLONK::verify_proof)
     super_points = sorted({q[2] for q in queries})
     order, cm_points, cm_obj, evals = [], {}, {}, {}
@@ -417,6 +422,49 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None):
     right = outer.eval()
     left_s = g1_mul(h2, s)
     return left_s == right
+
+
+def _verify_gwc(T, queries, proof, s):
+    """VerifierGWC::verify_proof (gwc/verifier.rs:42-123): queries grouped by point in
+    first-appearance order (gwc.rs:25-50); one witness point per group; then
+    DualMSM::check, decided as [s]·left == right."""
+    v = T.squeeze()
+    groups = []  # [(point, [(commitment-or-msm, eval)])]
+    for _key, obj, pt, ev in queries:
+        for g in groups:
+            if g[0] == pt:
+                g[1].append((obj, ev))
+                break
+        else:
+            groups.append((pt, [(obj, ev)]))
+    ws = [T.read_point() for _ in groups]
+    u = T.squeeze()
+    if T.pos != len(proof):
+        raise VerifyError(f"trailing proof bytes: read {T.pos} of {len(proof)}")
+    commitment_multi, eval_multi = Msm(), 0
+    left, right = Msm(), Msm()
+    upow = 1
+    for (z, items), wi in zip(groups, ws):
+        batch, evb, vpow = Msm(), 0, 1
+        for obj, ev in items:
+            m = Msm()
+            if isinstance(obj, Msm):
+                m.add_msm(obj)
+            else:
+                m.add(1, obj)
+            m.scale(vpow)
+            batch.add_msm(m)
+            evb = (evb + vpow * ev) % R
+            vpow = vpow * v % R
+        batch.scale(upow)
+        commitment_multi.add_msm(batch)
+        eval_multi = (eval_multi + upow * evb) % R
+        right.add(upow * z, wi)   # witness_with_aux
+        left.add(upow, wi)        # witness
+        upow = upow * u % R
+    right.add_msm(commitment_multi)
+    right.add(-eval_multi, G1_GEN)
+    return g1_mul(left.eval(), s) == right.eval()
 
 
 def sigma_lagrange(circ):

@@ -227,14 +227,18 @@ class OrSpec(ctypes.Structure):
         ("unblinded", U8P),
         ("num_lookups", ctypes.c_uint32), ("lookup_sizes", U32P), ("lookup_roots", I32P),
         ("num_shuffles", ctypes.c_uint32), ("shuffle_sizes", U32P), ("shuffle_roots", I32P),
+        ("multiopen", ctypes.c_uint32),
     ]
+
+
+MULTIOPEN = {"shplonk": 0, "gwc": 1}
 
 
 def _ptr(a, t):
     return a.ctypes.data_as(t) if a is not None and a.size else None
 
 
-def make_spec(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=8):
+def make_spec(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=8, multiopen="shplonk"):
     """Builds the or_spec; returns (struct, keepalive list)."""
     keep = [np.ascontiguousarray(x) for x in (
         circ.gate_roots, circ.nodes, circ.constants, circ.perm_array, circ.copies, circ.fixed_values,
@@ -249,7 +253,7 @@ def make_spec(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=
                _ptr(lens, U32P), _ptr(tr, U64P), _ptr(sd, U8P), vanishing_threads,
                _ptr(g, U64P), _ptr(gl, U64P), _ptr(unb, U8P),
                len(circ.lookups), _ptr(lks, U32P), _ptr(lkr, I32P),
-               len(circ.shuffles), _ptr(shs, U32P), _ptr(shr, I32P))
+               len(circ.shuffles), _ptr(shs, U32P), _ptr(shr, I32P), MULTIOPEN[multiopen])
     return s, keep
 
 
@@ -299,9 +303,10 @@ class Keygen:
         self.close()
 
 
-def create_proof(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=8, threads=8, keygen=None):
-    """Oracle create_proof -> proof bytes."""
-    spec, keep = make_spec(circ, wit, srs_g, srs_gl, seed, vanishing_threads)
+def create_proof(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=8, threads=8, keygen=None,
+                 multiopen="shplonk"):
+    """Oracle create_proof -> proof bytes (multiopen: "shplonk" = ProverSHPLONK, "gwc" = ProverGWC)."""
+    spec, keep = make_spec(circ, wit, srs_g, srs_gl, seed, vanishing_threads, multiopen)
     cap = 1 << 20
     buf = ctypes.create_string_buffer(cap)
     ln = np.zeros(1, dtype=np.uint64)

@@ -137,3 +137,23 @@ def test_lookup_missing_table_value_fails():
     # the key stays usable
     assert pk.create_proof(wit) == O.create_proof(circ, wit, g, gl)
     pk.close()
+
+
+GWC_CASES = ["simple_k6", "mixed_k10", "c3_k8", "lookup_k11", "keccak_k9"]
+
+
+@pytest.mark.parametrize("name", GWC_CASES)
+def test_gwc_proof_bytes_match_oracle(name):
+    """ProverGWC on the device (h2g_pk_set_multiopen 1): bytes identical to the oracle's
+    GWC proof, which the independent GWC verifier accepts; the same key still proves
+    SHPLONK afterwards."""
+    circ, wit = CASES[name]()
+    s, g, gl, params = _params(circ.k)
+    pk = h2g.ProvingKey(params, circ)
+    want = O.create_proof(circ, wit, g, gl, multiopen="gwc")
+    got = pk.create_proof(wit, multiopen="gwc")
+    assert got == want
+    assert pk.create_proof(wit, multiopen="gwc") == want
+    assert V.verify(circ, _instances(circ, wit), got, s, multiopen="gwc")
+    assert pk.create_proof(wit) == O.create_proof(circ, wit, g, gl)
+    pk.close()

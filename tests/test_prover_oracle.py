@@ -181,3 +181,33 @@ def test_golden_proofs():
         s, g, gl = O.srs(circ.k, int(d[f"{name}_s"].tobytes()[::-1].hex(), 16))
         proof = O.create_proof(circ, wit, g, gl)
         assert proof == d[f"{name}_proof"].tobytes()
+
+
+@pytest.mark.parametrize("name", ["simple_k6", "mixed_k7", "c3_k8", "lookup_k8", "keccak_k9"])
+def test_prove_verify_gwc(name):
+    """ProverGWC / VerifierGWC (poly/kzg/multiopen/gwc): the multi-open the reference's
+    serialization test uses (halo2_proofs/tests/serialization.rs:158-175)"""
+    circ, wit = CIRCUITS[name]()
+    s, g, gl = O.srs(circ.k)
+    proof = O.create_proof(circ, wit, g, gl, multiopen="gwc")
+    ins = _instances(circ, wit)
+    assert V.verify(circ, ins, proof, s, multiopen="gwc")
+    # the two multi-opens share everything up to the opening: same prefix, different tail
+    shplonk = O.create_proof(circ, wit, g, gl)
+    npts = len(proof) - (len(shplonk) - 64)
+    assert npts > 0 and npts % 32 == 0 and proof[: len(shplonk) - 64] == shplonk[:-64]
+
+
+def test_gwc_negative_cases():
+    circ, wit = hc.mixed_circuit(7)
+    s, g, gl = O.srs(circ.k)
+    proof = bytearray(O.create_proof(circ, wit, g, gl, multiopen="gwc"))
+    proof[-40] ^= 1
+    try:
+        assert not V.verify(circ, _instances(circ, wit), bytes(proof), s, multiopen="gwc")
+    except V.VerifyError:
+        pass
+    bad = hc.Witness(wit.advice.copy(), wit.instance, wit.instance_lens)
+    bad.advice[0, 3] = hc.fr_to_limbs(4242)
+    assert not V.verify(circ, _instances(circ, bad), O.create_proof(circ, bad, g, gl, multiopen="gwc"), s,
+                        multiopen="gwc")

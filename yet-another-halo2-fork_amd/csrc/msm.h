@@ -11,10 +11,7 @@ struct MsmConfig {
 
 // Device workspace, grown on demand and reused across calls.
 struct MsmWorkspace {
-  size_t cap_n = 0;
-  int cap_c = 0;
-  int cap_W = 0;
-  uint32_t cap_L = 0;
+  size_t cap[10] = {};  // byte capacity of each buffer below (grown on demand, never shrunk)
   int last_c = 0, last_W = 0;    // window config of the most recent msm_run
   void* keys_in = nullptr;       // u64 [n*W] entries (key << 32 | value)
   void* keys_out = nullptr;      // u64 [n*W] sorted entries

@@ -359,9 +359,7 @@ void msm_free(MsmWorkspace* ws) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
   }
-  ws->cap_n = 0;
-  ws->cap_c = 0;
-  ws->cap_L = 0;
+  for (auto& c : ws->cap) c = 0;
   ws->sort_tmp_bytes = ws->scan_tmp_bytes = 0;
 }
 
@@ -392,24 +390,27 @@ static hipError_t msm_pipeline(const Fr* d_scalars, const G1Affine* d_bases, siz
   const size_t nchunks = (total + L - 1) / L;
   const uint32_t m1 = (NB + RG - 1) / RG;
   const uint32_t nblk = (m1 + MSM_THREADS - 1) / MSM_THREADS;
-  const int cfg_key = c * 2 + fixed;
-
-  if (ws->cap_n < n || ws->cap_c != cfg_key || ws->cap_L != L || ws->cap_W != W) {
-    H2G_TRY(grow(&ws->keys_in, total * 8));
-    H2G_TRY(grow(&ws->keys_out, total * 8));
-    H2G_TRY(grow(&ws->bucket_start, (size_t)nbt * 4));
-    H2G_TRY(grow(&ws->bucket_end, (size_t)nbt * 4));
-    H2G_TRY(grow(&ws->item_bucket, (size_t)nbt * 4));  // big-bucket list
-    H2G_TRY(grow(&ws->partials, 2 * nchunks * sizeof(G1xyzz)));  // boundary slots
-    H2G_TRY(grow(&ws->buckets, (size_t)nbt * sizeof(G1xyzz)));
-    H2G_TRY(grow(&ws->segs, ((size_t)2 * m1 + nblk) * WB * sizeof(G1xyzz)));
-    H2G_TRY(grow(&ws->windows, (size_t)W * sizeof(G1xyzz)));
-    H2G_TRY(grow(&ws->result, 16));  // [0] big-bucket count
-    ws->cap_n = n;
-    ws->cap_c = cfg_key;
-    ws->cap_L = L;
-    ws->cap_W = W;
-  }
+  // grow-only workspace: MSMs of slightly different shapes (e.g. n and n - 1 points, so
+  // another chunk length) reuse it instead of reallocating (~2 ms of host stall each)
+  struct Need {
+    void** p;
+    size_t bytes;
+  };
+  const Need need[10] = {{&ws->keys_in, total * 8},
+                         {&ws->keys_out, total * 8},
+                         {&ws->bucket_start, (size_t)nbt * 4},
+                         {&ws->bucket_end, (size_t)nbt * 4},
+                         {&ws->item_bucket, (size_t)nbt * 4},            // big-bucket list
+                         {&ws->partials, 2 * nchunks * sizeof(G1xyzz)},  // boundary slots
+                         {&ws->buckets, (size_t)nbt * sizeof(G1xyzz)},
+                         {&ws->segs, ((size_t)2 * m1 + nblk) * WB * sizeof(G1xyzz)},
+                         {&ws->windows, (size_t)W * sizeof(G1xyzz)},
+                         {&ws->result, 16}};  // [0] big-bucket count
+  for (int b = 0; b < 10; b++)
+    if (need[b].bytes > ws->cap[b]) {
+      H2G_TRY(grow(need[b].p, need[b].bytes));
+      ws->cap[b] = need[b].bytes;
+    }
   ws->last_c = c;
   ws->last_W = WB;
   uint64_t* keys_in = (uint64_t*)ws->keys_in;

@@ -111,6 +111,10 @@ struct ProvingKey {
   // verifying-key commitments (fixed, permutation) of a key read from bytes; a key made
   // by keygen computes them when it is written (h2g_pk_write)
   std::vector<G1Affine> vk_fixed, vk_perm;
+  // multi-open scheme of create_proof (the Prover type parameter, prover.rs:19-36):
+  // 0 ProverSHPLONK, 1 ProverGWC; GWC witness polynomials, one per opening point
+  int multiopen = 0;
+  std::vector<Fr*> gwc_q;
   Domain dom;
   Pool pool;
   // proving key (device)
@@ -1288,6 +1292,64 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   }
   clk.mark("evaluations");
 
+  if (pk.multiopen == 1) {
+    // ---- ProverGWC::create_proof_with_engine (gwc/prover.rs:40-90): the queries grouped
+    // by point in first-appearance order (construct_intermediate_sets, gwc.rs:25-50); per
+    // point W(X) = (sum_i v^i p_i(X) - sum_i v^i p_i(z)) / (X - z), committed against g.
+    // The points' MSMs are independent, so all are launched before the first is collected.
+    const Fr v = tr.squeeze();
+    std::vector<char> done(queries.size(), 0);
+    std::vector<MsmTicket> tk;
+    std::vector<Fr> neg_evb;
+    neg_evb.reserve(queries.size());
+    for (size_t i = 0; i < queries.size(); i++) {
+      if (done[i]) continue;
+      const Fr z = queries[i].pt;
+      const size_t g = tk.size();
+      if (g >= pk.gwc_q.size()) {
+        Fr* q;
+        PALLOC(pk.pool, q, n);
+        pk.gwc_q.push_back(q);
+      }
+      LinTerms t;
+      bool first = true;
+      Fr vp = Fr::one(), evb = Fr::zero();
+      for (size_t j = i; j < queries.size(); j++) {
+        if (done[j] || queries[j].pt != z) continue;
+        done[j] = 1;
+        if (t.k == LIN_MAXT - 1) {
+          HIPCHK(lincomb(pk.nx, n, t, !first, st));
+          first = false;
+          t.k = 0;
+        }
+        t.p[t.k] = polys[queries[j].poly].p;
+        t.len[t.k] = polys[queries[j].poly].len;
+        t.coef[t.k] = vp;
+        t.k++;
+        evb = evb + vp * ev(queries[j].poly, z);
+        vp = vp * v;
+      }
+      neg_evb.push_back(Fr::zero() - evb);  // poly_batch - eval_batch (poly.rs:268-276)
+      HIPCHK(hipMemcpyAsync(pk.small + g, &neg_evb.back(), sizeof(Fr), hipMemcpyHostToDevice, st));
+      t.p[t.k] = pk.small + g;
+      t.len[t.k] = 1;
+      t.coef[t.k] = Fr::one();
+      t.k++;
+      HIPCHK(lincomb(pk.nx, n, t, !first, st));
+      HIPCHK(kate_division(pk.nx, n, z, pk.gwc_q[g], pk.scr, st));
+      tk.emplace_back();
+      RCCHK(commit_launch(d, prm, pk.gwc_q[g], n - 1, SRS_G, st, &tk.back()));  // commit (kzg/commitment.rs:354-366)
+    }
+    for (auto& t : tk) {
+      G1Affine cm;
+      RCCHK(commit_collect(d, &t, &cm));
+      RCCHK(write_point(cm));
+    }
+    HIPCHK(hipStreamSynchronize(st));  // neg_evb (host) is read by the copies above
+    clk.mark("gwc");
+    return H2G_OK;
+  }
+
   // ---- SHPLONK (shplonk/prover.rs:121-305; construct_intermediate_sets shplonk.rs:48-140)
   const Fr sy = tr.squeeze();
   std::vector<Fr> super_pts;
@@ -1869,6 +1931,15 @@ int h2g_pk_free(uint64_t pk) {
   (void)hipStreamSynchronize(d->stream);
   domain_release(&it->second->dom);
   g_pks.erase(it);
+  return H2G_OK;
+}
+
+int h2g_pk_set_multiopen(uint64_t pk, int scheme) {
+  NEED_DEV_P();
+  auto it = g_pks.find(pk);
+  if (it == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
+  if (scheme != 0 && scheme != 1) return fail(H2G_ERR_ARG, "pk_set_multiopen: scheme must be 0 (SHPLONK) or 1 (GWC)");
+  it->second->multiopen = scheme;
   return H2G_OK;
 }
 

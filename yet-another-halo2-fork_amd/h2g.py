@@ -91,6 +91,7 @@ _SIGS = {
     "h2g_keygen": ([U64, VP, ctypes.POINTER(U64)], I32),
     "h2g_pk_free": ([U64], I32),
     "h2g_pk_info": ([U64, ctypes.POINTER(ctypes.c_int32)], I32),
+    "h2g_pk_set_multiopen": ([U64, I32], I32),
     "h2g_create_proof": ([U64, U64, VP, I32, U64P, ctypes.POINTER(U32), ctypes.c_char_p, U32, ctypes.c_char_p, SZ,
                           ctypes.POINTER(SZ)], I32),
     "h2g_prover_stages": ([ctypes.POINTER(ctypes.c_double), I32, ctypes.POINTER(I32)], I32),
@@ -124,6 +125,8 @@ def lib():
                            "(yet-another-halo2-fork_amd/build_lib.py)")
         L = ctypes.CDLL(LIB_PATH)
         for name, (args, res) in _SIGS.items():
+            if os.environ.get("H2G_LIB") and not hasattr(L, name):
+                continue  # an older A/B build lacks newer entry points
             f = getattr(L, name)
             f.argtypes = args
             f.restype = res
@@ -538,8 +541,12 @@ class ProvingKey:
         """ProvingKey::write (plonk.rs:311-321) -> bytes"""
         return _write_bytes(lib().h2g_pk_write, self.handle, fmt)
 
-    def create_proof(self, wit=None, seed=bytes([7] * 32), vanishing_threads=8, advice_dev_ptr=None):
-        """-> proof bytes.  advice_dev_ptr: device pointer to num_advice x n Fr (resident inputs)."""
+    def create_proof(self, wit=None, seed=bytes([7] * 32), vanishing_threads=8, advice_dev_ptr=None,
+                     multiopen="shplonk"):
+        """-> proof bytes.  advice_dev_ptr: device pointer to num_advice x n Fr (resident inputs).
+        multiopen: "shplonk" (ProverSHPLONK) or "gwc" (ProverGWC)."""
+        if multiopen != "shplonk" or hasattr(lib(), "h2g_pk_set_multiopen"):
+            check(lib().h2g_pk_set_multiopen(self.handle, {"shplonk": 0, "gwc": 1}[multiopen]))
         circ = self.circ
         n = 1 << circ.k
         if advice_dev_ptr is not None:
