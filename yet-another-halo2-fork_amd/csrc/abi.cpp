@@ -184,50 +184,64 @@ int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_
   return H2G_OK;
 }
 
-int msm_fixed_launch(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, hipStream_t producer,
-                     MsmTicket* t) {
+// nb MSMs of n scalars each against the same fixed-base windows, launched as one batched
+// pipeline (msm_run_fixed_batch) on the next MSM stream; ticket b collects MSM b.
+int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFixedBase& fb, size_t off, size_t n,
+                           hipStream_t producer, MsmTicket* t) {
+  if (nb < 1 || nb > MSM_MAX_BATCH) return fail(H2G_ERR_ARG, "msm: bad batch size");
   if (!d->h_ring) {
     HIPCHK(hipHostMalloc(&d->h_ring, MSM_RING * sizeof(G1xyzz), hipHostMallocDefault));
     for (int i = 0; i < MSM_SLOTS; i++) HIPCHK(hipStreamCreateWithFlags(&d->mstream[i], hipStreamNonBlocking));
     for (int i = 0; i < MSM_RING; i++) HIPCHK(hipEventCreateWithFlags(&d->ring_ev[i], hipEventDisableTiming));
   }
-  int ring = -1;
-  for (int k = 0; k < MSM_RING; k++) {
+  int rings[MSM_MAX_BATCH];
+  int got = 0;
+  for (int k = 0; k < MSM_RING && got < nb; k++) {
     const int r = (d->next_ring + k) % MSM_RING;
-    if (!d->ring_busy[r]) {
-      ring = r;
-      break;
-    }
+    if (!d->ring_busy[r]) rings[got++] = r;
   }
-  if (ring < 0) return fail(H2G_ERR_STATE, "msm: too many outstanding asynchronous MSMs");
-  d->next_ring = (ring + 1) % MSM_RING;
+  if (got < nb) return fail(H2G_ERR_STATE, "msm: too many outstanding asynchronous MSMs");
+  d->next_ring = (rings[nb - 1] + 1) % MSM_RING;
   const int slot = d->next_slot;
   d->next_slot = (slot + 1) % MSM_SLOTS;
   hipStream_t ms = d->mstream[slot];
   // order after the producer's work (the scalars)
-  HIPCHK(hipEventRecord(d->ring_ev[ring], producer));
-  HIPCHK(hipStreamWaitEvent(ms, d->ring_ev[ring], 0));
+  HIPCHK(hipEventRecord(d->ring_ev[rings[0]], producer));
+  HIPCHK(hipStreamWaitEvent(ms, d->ring_ev[rings[0]], 0));
   MsmPhaseEvents* pe = nullptr;
   if (g_profile && n > 0) {
     MsmPhaseEvents ev;
     for (auto& e : ev.ev) HIPCHK(hipEventCreate(&e));
+    ev.msms = nb;
     g_msm_prof.push_back(ev);
     pe = &g_msm_prof.back();
   }
-  G1xyzz* host = reinterpret_cast<G1xyzz*>(d->h_ring) + ring;
+  G1xyzz* host = reinterpret_cast<G1xyzz*>(d->h_ring);
   if (n == 0) {
-    std::memset(host, 0, sizeof(G1xyzz));  // identity (ZZ = 0)
+    for (int b = 0; b < nb; b++) std::memset(host + rings[b], 0, sizeof(G1xyzz));  // identity (ZZ = 0)
   } else {
-    HIPCHK(msm_run_fixed(reinterpret_cast<const Fr*>(sc), fb, off, n, &d->mws[slot], nullptr, ms, pe));
-    HIPCHK(hipMemcpyAsync(host, d->mws[slot].windows, sizeof(G1xyzz), hipMemcpyDeviceToHost, ms));
+    MsmScalarList list;
+    for (int b = 0; b < nb; b++) list.p[b] = reinterpret_cast<const Fr*>(sc[b]);
+    if (nb == 1) HIPCHK(msm_run_fixed(list.p[0], fb, off, n, &d->mws[slot], nullptr, ms, pe));
+    else HIPCHK(msm_run_fixed_batch(list, nb, fb, off, n, &d->mws[slot], ms, pe));
+    const G1xyzz* win = reinterpret_cast<const G1xyzz*>(d->mws[slot].windows);
+    for (int b = 0; b < nb; b++)
+      HIPCHK(hipMemcpyAsync(host + rings[b], win + b, sizeof(G1xyzz), hipMemcpyDeviceToHost, ms));
   }
-  HIPCHK(hipEventRecord(d->ring_ev[ring], ms));
-  d->ring_busy[ring] = true;
-  t->slot = slot;
-  t->ring = ring;
-  t->c = fb.c;
-  t->done = d->ring_ev[ring];
+  for (int b = 0; b < nb; b++) {
+    HIPCHK(hipEventRecord(d->ring_ev[rings[b]], ms));
+    d->ring_busy[rings[b]] = true;
+    t[b].slot = slot;
+    t[b].ring = rings[b];
+    t[b].c = fb.c;
+    t[b].done = d->ring_ev[rings[b]];
+  }
   return H2G_OK;
+}
+
+int msm_fixed_launch(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, hipStream_t producer,
+                     MsmTicket* t) {
+  return msm_fixed_launch_batch(d, &sc, 1, fb, off, n, producer, t);
 }
 
 int msm_collect(Device* d, MsmTicket* t, uint64_t* out) {
@@ -891,7 +905,11 @@ int h2g_profile_msm_collect(float* ms, int max_phases, int* n_phases, int* calls
       ms[i] += t;
     }
   }
-  if (calls) *calls = (int)g_msm_prof.size();
+  if (calls) {
+    int c = 0;
+    for (auto& pe : g_msm_prof) c += pe.msms;
+    *calls = c;
+  }
   if (n_phases) *n_phases = np;
   for (auto& pe : g_msm_prof)
     for (auto& e : pe.ev) (void)hipEventDestroy(e);

@@ -39,6 +39,13 @@ int msm_windows_for(int c);
 static constexpr int MSM_NPHASES = 6;
 struct MsmPhaseEvents {
   hipEvent_t ev[MSM_NPHASES + 1];
+  int msms = 1;  // MSMs the timed pipeline served (a batch counts each)
+};
+
+// Scalar vectors of a batch of MSMs (kernel argument by value).
+static constexpr int MSM_MAX_BATCH = 64;
+struct MsmScalarList {
+  const Fr* p[MSM_MAX_BATCH];
 };
 
 // sum_i scalars[i] * bases[i]; scalars Montgomery Fr, bases affine Montgomery Fq
@@ -65,5 +72,11 @@ void msm_fixed_base_free(MsmFixedBase* fb);
 // sum_{i < n} scalars[i] * bases[off + i]; leaves ws->windows[0] (ws->last_W = 1)
 hipError_t msm_run_fixed(const Fr* d_scalars, const MsmFixedBase& fb, size_t off, size_t n, MsmWorkspace* ws,
                          G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof = nullptr);
+// nbatch MSMs sum_i list.p[b][i] * bases[off + i] (b < nbatch <= MSM_MAX_BATCH) as one
+// pipeline -- one digits launch, one sort, one accumulation, one reduction with a bucket
+// set per MSM -- so the latency-bound reduction is paid once.  Leaves MSM b's sum in
+// ws->windows[b] (ws->last_W = nbatch).  nbatch * W * n must stay below 2^31.
+hipError_t msm_run_fixed_batch(const MsmScalarList& list, int nbatch, const MsmFixedBase& fb, size_t off, size_t n,
+                               MsmWorkspace* ws, hipStream_t st, MsmPhaseEvents* prof = nullptr);
 
 }  // namespace h2g

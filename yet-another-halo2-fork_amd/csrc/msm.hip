@@ -73,12 +73,16 @@ __device__ __forceinline__ G1Affine ld_aff(const G1Affine* p) {
 // Generic mode: key = window * NB + |d| - 1, value = point index.  Fixed-base mode
 // (bases pre-multiplied per window, table[w * stride + i] = [2^(c w)] P_i): every
 // window shares one set of NB buckets, key = |d| - 1, value = w * stride + i.
+// Batched fixed-base mode (blockIdx.y = b of nbatch MSMs over the same windows): MSM b
+// owns bucket set b, key = b * NB + |d| - 1, so one sort / accumulation / reduction
+// serves them all.
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_digits_kernel(const Fr* __restrict__ scalars, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride,
+msm_digits_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride,
                   uint64_t* __restrict__ ent) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint4* q = reinterpret_cast<const uint4*>(scalars + i);
+  const uint32_t bi = blockIdx.y;  // which MSM of the batch
+  const uint4* q = reinterpret_cast<const uint4*>(list.p[bi] + i);
   uint4 a = q[0], b = q[1];
   Fr s;
   s.l[0] = a.x; s.l[1] = a.y; s.l[2] = a.z; s.l[3] = a.w;
@@ -86,7 +90,8 @@ msm_digits_kernel(const Fr* __restrict__ scalars, size_t n, int c, int W, uint32
   Fr v = to_canonical(s);
   const uint32_t mask = (1u << c) - 1;
   const uint32_t half = 1u << (c - 1);
-  const uint32_t sentinel = fixed ? NB : (uint32_t)W * NB;
+  const uint32_t sentinel = fixed ? gridDim.y * NB : (uint32_t)W * NB;
+  uint64_t* out = ent + (size_t)bi * W * n;
   uint32_t carry = 0;
   for (int w = 0; w < W; w++) {
     uint32_t d = (v.l[0] & mask) + carry;
@@ -94,7 +99,7 @@ msm_digits_kernel(const Fr* __restrict__ scalars, size_t n, int c, int W, uint32
 #pragma unroll
     for (int k = 0; k < 7; k++) v.l[k] = (v.l[k] >> c) | (v.l[k + 1] << (32 - c));
     v.l[7] >>= c;
-    const uint32_t koff = fixed ? 0u : (uint32_t)w * NB;
+    const uint32_t koff = fixed ? bi * NB : (uint32_t)w * NB;
     uint32_t key, val = fixed ? (uint32_t)((size_t)w * stride + i) : (uint32_t)i;
     if (d > half) {  // negative digit d - 2^c (d == 2^c gives digit 0, carry 1)
       const uint32_t mag = (1u << c) - d;
@@ -105,7 +110,7 @@ msm_digits_kernel(const Fr* __restrict__ scalars, size_t n, int c, int W, uint32
       carry = 0;
       key = d ? koff + d - 1 : sentinel;
     }
-    ent[(size_t)w * n + i] = ((uint64_t)key << 32) | val;
+    out[(size_t)w * n + i] = ((uint64_t)key << 32) | val;
   }
 }
 
@@ -377,15 +382,17 @@ uint32_t msm_chunk_len(size_t total) {
   return (uint32_t)L;
 }
 
-static hipError_t msm_pipeline(const Fr* d_scalars, const G1Affine* d_bases, size_t n, int c, int W, int fixed,
-                               size_t stride, MsmWorkspace* ws, uint32_t item_len, G1Affine* d_out, hipStream_t st,
-                               MsmPhaseEvents* prof) {
+static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Affine* d_bases, size_t n, int c,
+                               int W, int fixed, size_t stride, MsmWorkspace* ws, uint32_t item_len, G1Affine* d_out,
+                               hipStream_t st, MsmPhaseEvents* prof) {
 #define H2G_PHASE(i) \
   if (prof) H2G_TRY(hipEventRecord(prof->ev[i], st))
   const uint32_t NB = 1u << (c - 1);
-  const int WB = fixed ? 1 : W;  // bucket sets
+  if (nbatch < 1 || nbatch > MSM_MAX_BATCH || (!fixed && nbatch != 1)) return hipErrorInvalidValue;
+  const int WB = fixed ? nbatch : W;  // bucket sets
   const uint32_t nbt = (uint32_t)WB * NB;
-  const size_t total = n * (size_t)W;
+  const size_t total = n * (size_t)W * nbatch;
+  if (total >= 0x80000000ull) return hipErrorInvalidValue;  // u32 positions in the sorted array
   const uint32_t L = item_len > 0 ? item_len : msm_chunk_len(total);
   const size_t nchunks = (total + L - 1) / L;
   const uint32_t m1 = (NB + RG - 1) / RG;
@@ -404,7 +411,7 @@ static hipError_t msm_pipeline(const Fr* d_scalars, const G1Affine* d_bases, siz
                          {&ws->partials, 2 * nchunks * sizeof(G1xyzz)},  // boundary slots
                          {&ws->buckets, (size_t)nbt * sizeof(G1xyzz)},
                          {&ws->segs, ((size_t)2 * m1 + nblk) * WB * sizeof(G1xyzz)},
-                         {&ws->windows, (size_t)W * sizeof(G1xyzz)},
+                         {&ws->windows, (size_t)(W > WB ? W : WB) * sizeof(G1xyzz)},
                          {&ws->result, 16}};  // [0] big-bucket count
   for (int b = 0; b < 10; b++)
     if (need[b].bytes > ws->cap[b]) {
@@ -440,8 +447,8 @@ static hipError_t msm_pipeline(const Fr* d_scalars, const G1Affine* d_bases, siz
 
   const int T = MSM_THREADS;
   H2G_PHASE(0);
-  hipLaunchKernelGGL(msm_digits_kernel, dim3((unsigned)((n + T - 1) / T)), dim3(T), 0, st, d_scalars, n, c, W, NB,
-                     fixed, stride, keys_in);
+  hipLaunchKernelGGL(msm_digits_kernel, dim3((unsigned)((n + T - 1) / T), (unsigned)nbatch), dim3(T), 0, st, list,
+                     n, c, W, NB, fixed, stride, keys_in);
   H2G_TRY(hipGetLastError());
   H2G_PHASE(1);
   H2G_TRY(hipcub::DeviceRadixSort::SortKeys(ws->sort_tmp, sort_bytes, keys_in, keys_out, (int)total, 32,
@@ -475,7 +482,7 @@ static hipError_t msm_pipeline(const Fr* d_scalars, const G1Affine* d_bases, siz
                      (const G1xyzz*)rR, m1, rP, nblk);
   hipLaunchKernelGGL(msm_rfinal_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rP, nblk,
                      (G1xyzz*)ws->windows);
-  if (d_out)
+  if (d_out && nbatch == 1)
     hipLaunchKernelGGL(msm_final_kernel, dim3(1), dim3(64), 0, st, (const G1xyzz*)ws->windows, WB, c, d_out);
   H2G_TRY(hipGetLastError());
   H2G_PHASE(6);
@@ -486,8 +493,9 @@ static hipError_t msm_pipeline(const Fr* d_scalars, const G1Affine* d_bases, siz
 hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWorkspace* ws,
                    const MsmConfig& cfg, G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof) {
   const int c = cfg.c > 0 ? cfg.c : msm_choose_c(n);
-  return msm_pipeline(d_scalars, d_bases, n, c, msm_windows_for(c), 0, 0, ws, (uint32_t)cfg.item_len, d_out, st,
-                      prof);
+  MsmScalarList list;
+  list.p[0] = d_scalars;
+  return msm_pipeline(list, 1, d_bases, n, c, msm_windows_for(c), 0, 0, ws, (uint32_t)cfg.item_len, d_out, st, prof);
 }
 
 int msm_choose_c_fixed(size_t n) {
@@ -528,7 +536,15 @@ void msm_fixed_base_free(MsmFixedBase* fb) {
 hipError_t msm_run_fixed(const Fr* d_scalars, const MsmFixedBase& fb, size_t off, size_t n, MsmWorkspace* ws,
                          G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof) {
   if (off + n > fb.n) return hipErrorInvalidValue;
-  return msm_pipeline(d_scalars, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, d_out, st, prof);
+  MsmScalarList list;
+  list.p[0] = d_scalars;
+  return msm_pipeline(list, 1, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, d_out, st, prof);
+}
+
+hipError_t msm_run_fixed_batch(const MsmScalarList& list, int nbatch, const MsmFixedBase& fb, size_t off, size_t n,
+                               MsmWorkspace* ws, hipStream_t st, MsmPhaseEvents* prof) {
+  if (off + n > fb.n) return hipErrorInvalidValue;
+  return msm_pipeline(list, nbatch, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, nullptr, st, prof);
 }
 
 }  // namespace h2g

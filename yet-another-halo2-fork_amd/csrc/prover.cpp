@@ -291,6 +291,45 @@ int commit_collect(Device* d, MsmTicket* t, G1Affine* out) {
   *out = xyzz_to_affine(acc);
   return H2G_OK;
 }
+// Several commitments against one base set as batched MSMs (msm_run_fixed_batch): one
+// sort, accumulation and reduction serve a group, so the latency-bound reduction is paid
+// once per group instead of once per commitment -- what circuits with many columns at
+// small k (C5) are dominated by (commit_batch_chunk); with a shard transport every MSM
+// goes alone (point slabs).
+// MSMs per batch for commitments of length n (1: no batching).  Batching pays where
+// the reduction's latency is comparable to the accumulation: measured on MI355X, a
+// keccak-style k = 18 proof (80 MSMs of 2^18) 127 -> 101 ms, while C3 at k = 22 (MSMs
+// of 2^22, 13 x 2^22 entries each) is 0.6 ms better without -- so only MSMs of at most
+// 2^25 sorted entries are batched, up to 2^27 entries per batch.
+int commit_batch_chunk(const Params& prm, size_t n, int set) {
+  static const uint64_t max_entries = [] {
+    const char* e = std::getenv("H2G_MSM_BATCH_ENTRIES");
+    return e ? std::strtoull(e, nullptr, 0) : (1ull << 27);
+  }();
+  if (g_shard.world > 1) return 1;
+  size_t toff = 0;
+  const uint64_t per = (uint64_t)prm.tables(set, 0, n, &toff).W * (n ? n : 1);
+  if (per > (1ull << 25)) return 1;
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>(MSM_MAX_BATCH, max_entries / per));
+}
+
+int commit_launch_batch(Device* d, const Params& prm, const Fr* const* scalars, int nb, size_t n, int set,
+                        hipStream_t st, MsmTicket* t) {
+  size_t toff = 0;
+  const MsmFixedBase& tb = prm.tables(set, 0, n, &toff);
+  const int chunk = commit_batch_chunk(prm, n, set);
+  if (chunk < 2) {
+    for (int b = 0; b < nb; b++) RCCHK(commit_launch(d, prm, scalars[b], n, set, st, &t[b]));
+    return H2G_OK;
+  }
+  for (int b0 = 0; b0 < nb; b0 += chunk) {
+    const int m = std::min(chunk, nb - b0);
+    for (int b = 0; b < m; b++) t[b0 + b].shard_seq = -1;
+    RCCHK(msm_fixed_launch_batch(d, reinterpret_cast<const void* const*>(scalars + b0), m, tb, toff, n, st, t + b0));
+  }
+  return H2G_OK;
+}
+
 int commit(Device* d, const Params& prm, const Fr* scalars, size_t n, int set, G1Affine* out, hipStream_t st) {
   MsmTicket t;
   RCCHK(commit_launch(d, prm, scalars, n, set, st, &t));
@@ -895,7 +934,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   clk.mark("upload+instances");
   {
     std::vector<MsmTicket> tk(pk.A);
-    for (int c = 0; c < pk.A; c++) RCCHK(commit_launch(d, prm, pk.adv[c], n, SRS_LAGRANGE, st, &tk[c]));
+    RCCHK(commit_launch_batch(d, prm, pk.adv.data(), pk.A, n, SRS_LAGRANGE, st, tk.data()));
     for (int c = 0; c < pk.A; c++) {
       G1Affine cm;
       RCCHK(commit_collect(d, &tk[c], &cm));
@@ -957,13 +996,17 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       }
       (void)rng.random_fr();  // permuted input blind
       (void)rng.random_fr();  // permuted table blind
-      RCCHK(commit_launch(d, prm, pk.lk_ap[l], n, SRS_LAGRANGE, st, &tk[2 * l]));
-      RCCHK(commit_launch(d, prm, pk.lk_sp[l], n, SRS_LAGRANGE, st, &tk[2 * l + 1]));
       RCCHK(lagrange_to_coeff(d, D, pk.lk_ap[l], pk.lk_ap_poly[l], st));
       RCCHK(lagrange_to_coeff(d, D, pk.lk_sp[l], pk.lk_sp_poly[l], st));
       RCCHK(coeff_to_extended(d, D, pk.lk_ap_poly[l], pk.lk_apc[l], st));
       RCCHK(coeff_to_extended(d, D, pk.lk_sp_poly[l], pk.lk_spc[l], st));
     }
+    std::vector<const Fr*> perm_cols;  // (A'_l, S'_l) in transcript order
+    for (int l = 0; l < pk.NL; l++) {
+      perm_cols.push_back(pk.lk_ap[l]);
+      perm_cols.push_back(pk.lk_sp[l]);
+    }
+    RCCHK(commit_launch_batch(d, prm, perm_cols.data(), 2 * pk.NL, n, SRS_LAGRANGE, st, tk.data()));
     for (int i = 0; i < 2 * pk.NL; i++) {
       G1Affine cm;
       RCCHK(commit_collect(d, &tk[i], &cm));
@@ -978,6 +1021,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   // ---- permutation_commit (permutation/prover.rs:50-197); commitments are written
   // after the loop (nothing is squeezed in between, so the transcript is unchanged)
   std::vector<MsmTicket> perm_tk(pk.nsets);
+  // large MSMs start as soon as their set's z is ready; small ones wait and go as a batch
+  const bool perm_batched = commit_batch_chunk(prm, n, SRS_LAGRANGE) > 1;
   {
     const Fr one = Fr::one();
     HIPCHK(hipMemcpyAsync(pk.last_z, &one, sizeof(Fr), hipMemcpyHostToDevice, st));
@@ -1027,25 +1072,25 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       if (s == 0) dump("z0", pk.z_lag[s], n, st);
       if (s == 0) dump("sigma0", pk.sigma_lag[0], n, st);
       if (s == 0) dump("v0", col_vals(0), n, st);
-      RCCHK(commit_launch(d, prm, pk.z_lag[s], n, SRS_LAGRANGE, st, &perm_tk[s]));
       RCCHK(lagrange_to_coeff(d, D, pk.z_lag[s], pk.z[s], st));
       RCCHK(coeff_to_extended(d, D, pk.z[s], pk.z_coset[s], st));
+      if (!perm_batched) RCCHK(commit_launch(d, prm, pk.z_lag[s], n, SRS_LAGRANGE, st, &perm_tk[s]));
       HIPCHK(hipStreamSynchronize(st));  // blind_rows (host) is reused by the next set
     }
   }
+  if (perm_batched) RCCHK(commit_launch_batch(d, prm, pk.z_lag.data(), pk.nsets, n, SRS_LAGRANGE, st, perm_tk.data()));
   clk.mark("permutation products");
   // ---- lookup products (lookup/prover.rs:182-325), then shuffle products
   // (shuffle/prover.rs:97-206): z = [1, running product ...], bf random rows, blind
   std::vector<MsmTicket> lkz_tk(pk.NL), shz_tk(pk.NS);
   {
     std::vector<Fr> rows((size_t)bf);
-    auto finish_z = [&](Fr* z_lag, Fr* z_poly, Fr* z_coset, MsmTicket* t) -> int {
+    auto finish_z = [&](Fr* z_lag, Fr* z_poly, Fr* z_coset, MsmTicket*) -> int {
       HIPCHK(poly_prefix_product(pk.mod, pk.pre, n, pk.scr, pk.scr_len, st));
       for (auto& v : rows) v = rng.random_fr();
       (void)rng.random_fr();  // product blind
       HIPCHK(hipMemcpyAsync(pk.small, rows.data(), rows.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
       HIPCHK(perm_z_assemble(z_lag, n, bf, pk.pre, pk.one, pk.small, st));
-      RCCHK(commit_launch(d, prm, z_lag, n, SRS_LAGRANGE, st, t));
       RCCHK(lagrange_to_coeff(d, D, z_lag, z_poly, st));
       RCCHK(coeff_to_extended(d, D, z_poly, z_coset, st));
       HIPCHK(hipStreamSynchronize(st));  // rows (host) is reused
@@ -1065,6 +1110,14 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       HIPCHK(shuffle_prod_num(pk.tmp_a, gamma, pk.mod, n, st));
       RCCHK(finish_z(pk.sh_z[s], pk.sh_z_poly[s], pk.sh_zc[s], &shz_tk[s]));
     }
+  }
+  {  // product commitments: lookups then shuffles, one batch
+    std::vector<const Fr*> zs(pk.lk_z.begin(), pk.lk_z.end());
+    zs.insert(zs.end(), pk.sh_z.begin(), pk.sh_z.end());
+    std::vector<MsmTicket> zt(zs.size());
+    RCCHK(commit_launch_batch(d, prm, zs.data(), (int)zs.size(), n, SRS_LAGRANGE, st, zt.data()));
+    for (int l = 0; l < pk.NL; l++) lkz_tk[l] = zt[l];
+    for (int s = 0; s < pk.NS; s++) shz_tk[s] = zt[pk.NL + s];
   }
   if (pk.NL + pk.NS) clk.mark("lookup/shuffle products");
   // ---- vanishing commit (vanishing/prover.rs:40-98)
@@ -1160,7 +1213,9 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   for (int p = 0; p < npieces; p++) (void)rng.random_fr();  // h blinds
   {
     std::vector<MsmTicket> tk(npieces);
-    for (int p = 0; p < npieces; p++) RCCHK(commit_launch(d, prm, pk.h_coeff + (size_t)p * n, n, SRS_G, st, &tk[p]));
+    std::vector<const Fr*> pieces(npieces);
+    for (int p = 0; p < npieces; p++) pieces[p] = pk.h_coeff + (size_t)p * n;
+    RCCHK(commit_launch_batch(d, prm, pieces.data(), npieces, n, SRS_G, st, tk.data()));
     for (int p = 0; p < npieces; p++) {
       G1Affine cm;
       RCCHK(commit_collect(d, &tk[p], &cm));

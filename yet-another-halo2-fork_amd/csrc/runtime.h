@@ -145,6 +145,9 @@ int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_
 // launch sum_{i<n} sc[i] * bases[off+i] after the work already queued on `producer`
 int msm_fixed_launch(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, hipStream_t producer,
                      MsmTicket* t);
+// nb (<= MSM_MAX_BATCH) MSMs against the same windows as one batched pipeline; t[nb]
+int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFixedBase& fb, size_t off, size_t n,
+                           hipStream_t producer, MsmTicket* t);
 // wait for a launched MSM, affine result
 int msm_collect(Device* d, MsmTicket* t, uint64_t* out_affine);
 // make `consumer` wait until every launched MSM has finished reading its scalars
