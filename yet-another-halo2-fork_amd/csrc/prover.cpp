@@ -115,6 +115,8 @@ struct ProvingKey {
   // 0 ProverSHPLONK, 1 ProverGWC; GWC witness polynomials, one per opening point
   int multiopen = 0;
   std::vector<Fr*> gwc_q;
+  uint32_t* lk_cnt = nullptr;  // pinned per-lookup match counters (3 per lookup)
+  size_t lk_cnt_len = 0;
   Domain dom;
   Pool pool;
   // proving key (device)
@@ -961,7 +963,15 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   {
     std::vector<MsmTicket> tk(2 * pk.NL);
     const size_t u = n - (size_t)(bf + 1);
-    std::vector<Fr> rows((size_t)(bf + 1));
+    // per-lookup host staging (random rows, match counters): no host synchronisation
+    // between lookups, so their device pipelines queue back to back; the counters are
+    // checked once all lookups are queued
+    std::vector<Fr> rows((size_t)pk.NL * 2 * (bf + 1));
+    if ((size_t)pk.NL * 3 > pk.lk_cnt_len) {
+      if (pk.lk_cnt) (void)hipHostFree(pk.lk_cnt);
+      HIPCHK(hipHostMalloc((void**)&pk.lk_cnt, (size_t)pk.NL * 3 * sizeof(uint32_t), hipHostMallocDefault));
+      pk.lk_cnt_len = (size_t)pk.NL * 3;
+    }
     for (int l = 0; l < pk.NL; l++) {
       RCCHK(compress(pk.seg_lk_in[l], pk.lk_a[l]));
       RCCHK(compress(pk.seg_lk_tab[l], pk.lk_s[l]));
@@ -983,16 +993,12 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
                                            pk.rep_rows, pk.counters + 1, (int)u, st));
       HIPCHK(lookup_assign(pk.ck_a2, pk.rep_flag, u, pk.lk_ap[l], pk.lk_sp[l], st));
       HIPCHK(lookup_scatter(pk.ck_left, pk.rep_rows, pk.counters + 1, u, pk.lk_sp[l], st));
-      uint32_t cnt[3];
-      HIPCHK(hipMemcpyAsync(cnt, pk.counters, sizeof(cnt), hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      if (cnt[2] != 0 || cnt[0] != cnt[1])
-        return fail(H2G_ERR_ARG, "create_proof: lookup input value not in the table (ConstraintSystemFailure)");
+      HIPCHK(hipMemcpyAsync(pk.lk_cnt + 3 * l, pk.counters, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       for (int which = 0; which < 2; which++) {  // bf+1 random rows: input first, then table
-        for (auto& v : rows) v = rng.random_fr();
-        HIPCHK(hipMemcpyAsync((which ? pk.lk_sp[l] : pk.lk_ap[l]) + u, rows.data(), rows.size() * sizeof(Fr),
+        Fr* r = rows.data() + ((size_t)2 * l + which) * (bf + 1);
+        for (int i = 0; i <= bf; i++) r[i] = rng.random_fr();
+        HIPCHK(hipMemcpyAsync((which ? pk.lk_sp[l] : pk.lk_ap[l]) + u, r, (size_t)(bf + 1) * sizeof(Fr),
                               hipMemcpyHostToDevice, st));
-        HIPCHK(hipStreamSynchronize(st));
       }
       (void)rng.random_fr();  // permuted input blind
       (void)rng.random_fr();  // permuted table blind
@@ -1000,6 +1006,12 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       RCCHK(lagrange_to_coeff(d, D, pk.lk_sp[l], pk.lk_sp_poly[l], st));
       RCCHK(coeff_to_extended(d, D, pk.lk_ap_poly[l], pk.lk_apc[l], st));
       RCCHK(coeff_to_extended(d, D, pk.lk_sp_poly[l], pk.lk_spc[l], st));
+    }
+    HIPCHK(hipStreamSynchronize(st));  // counters landed; rows (host) read
+    for (int l = 0; l < pk.NL; l++) {
+      const uint32_t* cnt = pk.lk_cnt + 3 * l;
+      if (cnt[2] != 0 || cnt[0] != cnt[1])
+        return fail(H2G_ERR_ARG, "create_proof: lookup input value not in the table (ConstraintSystemFailure)");
     }
     std::vector<const Fr*> perm_cols;  // (A'_l, S'_l) in transcript order
     for (int l = 0; l < pk.NL; l++) {
@@ -1985,6 +1997,7 @@ int h2g_pk_free(uint64_t pk) {
   if (it == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
   (void)hipStreamSynchronize(d->stream);
   domain_release(&it->second->dom);
+  if (it->second->lk_cnt) (void)hipHostFree(it->second->lk_cnt);
   g_pks.erase(it);
   return H2G_OK;
 }
