@@ -27,6 +27,8 @@ struct FrParams {
                                       0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
   static constexpr uint32_t R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
                                      0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+  static constexpr uint32_t R3[8] = {0xb4bf0040u, 0x5e94d8e1u, 0x1cfbb6b8u, 0x2a489cbeu,
+                                     0xa19fcfedu, 0x893cc664u, 0x7fcc657cu, 0x0cf8594bu};
 };
 struct FqParams {
   static constexpr uint32_t M[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
@@ -36,6 +38,8 @@ struct FqParams {
                                       0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
   static constexpr uint32_t R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
                                      0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
+  static constexpr uint32_t R3[8] = {0xda1530dfu, 0xb1cd6dafu, 0xa7283db6u, 0x62f210e6u,
+                                     0x0ada0afbu, 0xef7f0b0cu, 0x2d592544u, 0x20fd6e90u};
 };
 
 template <class P>
@@ -267,14 +271,99 @@ H2G_HD Fe<P> pow_u64(const Fe<P>& a, uint64_t e) {
   }
   return acc;
 }
-// Fermat inversion; inv(0) = 0 (matches ff's invert().unwrap_or(ZERO) use in batch_invert).
+// Fermat inversion a^(M-2); inv_fermat(0) = 0.
 template <class P>
-H2G_HD Fe<P> inv(const Fe<P>& a) {
+H2G_HD Fe<P> inv_fermat(const Fe<P>& a) {
   uint32_t e[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) e[i] = P::M[i];
   e[0] -= 2;
   return pow_limbs(a, e);
+}
+
+// Inversion by the binary extended Euclidean algorithm; inv(0) = 0 (matches ff's
+// invert().unwrap_or(ZERO) use in batch_invert).  Variable time -- nothing the prover
+// inverts is secret from the device.  ~500 halvings and ~350 subtractions of 8-limb
+// integers (add/sub/shift only, no multiplies): on a lone wave its dependent chain is
+// ~4x shorter than Fermat's 380 Montgomery products, which is what bounds a batch
+// inversion (one inversion per thread at the end of a serial prefix product).
+// The Montgomery limbs x = aR are inverted as an integer, y = (aR)^-1, and one
+// Montgomery product by R^3 gives a^-1 R.
+template <class P>
+H2G_HD void bgcd_half_mod(uint32_t x[8]) {  // x / 2 mod M, x < M
+  uint32_t s[8];
+  unsigned c = 0;
+  const uint32_t odd = 0u - (x[0] & 1u);
+#pragma unroll
+  for (int i = 0; i < 8; i++) s[i] = __builtin_addc(x[i], P::M[i] & odd, c, &c);  // < 2^255
+#pragma unroll
+  for (int i = 0; i < 7; i++) x[i] = (s[i] >> 1) | (s[i + 1] << 31);
+  x[7] = s[7] >> 1;
+}
+H2G_HD void bgcd_shr1(uint32_t u[8]) {
+#pragma unroll
+  for (int i = 0; i < 7; i++) u[i] = (u[i] >> 1) | (u[i + 1] << 31);
+  u[7] >>= 1;
+}
+template <class P>
+H2G_HD void bgcd_sub_mod(uint32_t x[8], const uint32_t y[8]) {  // x - y mod M
+  unsigned br = 0, c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[i] = __builtin_subc(x[i], y[i], br, &br);
+  const uint32_t mask = 0u - br;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[i] = __builtin_addc(x[i], P::M[i] & mask, c, &c);
+}
+H2G_HD bool bgcd_is_one(const uint32_t u[8]) {
+  uint32_t o = u[0] ^ 1u;
+#pragma unroll
+  for (int i = 1; i < 8; i++) o |= u[i];
+  return o == 0;
+}
+template <class P>
+H2G_HD Fe<P> inv(const Fe<P>& a) {
+  if (a.is_zero()) return a;
+  uint32_t u[8], v[8], x1[8], x2[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u[i] = a.l[i];
+    v[i] = P::M[i];
+    x1[i] = 0;
+    x2[i] = 0;
+  }
+  x1[0] = 1;  // invariants: x1 * a = u, x2 * a = v (mod M)
+  while (!bgcd_is_one(u) && !bgcd_is_one(v)) {
+    while (!(u[0] & 1u)) {
+      bgcd_shr1(u);
+      bgcd_half_mod<P>(x1);
+    }
+    while (!(v[0] & 1u)) {
+      bgcd_shr1(v);
+      bgcd_half_mod<P>(x2);
+    }
+    uint32_t d[8];
+    unsigned br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) d[i] = __builtin_subc(u[i], v[i], br, &br);
+    if (!br) {  // u >= v
+#pragma unroll
+      for (int i = 0; i < 8; i++) u[i] = d[i];
+      bgcd_sub_mod<P>(x1, x2);
+    } else {
+      unsigned b2 = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) v[i] = __builtin_subc(v[i], u[i], b2, &b2);
+      bgcd_sub_mod<P>(x2, x1);
+    }
+  }
+  Fe<P> y, r3;
+  const bool uo = bgcd_is_one(u);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    y.l[i] = uo ? x1[i] : x2[i];
+    r3.l[i] = P::R3[i];  // R^3 mod M
+  }
+  return y * r3;
 }
 
 // ---------------------------------------------------------------- G1 (y^2 = x^3 + 3 over Fq)

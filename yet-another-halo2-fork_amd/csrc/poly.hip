@@ -9,6 +9,8 @@
 #include "poly.h"
 #include "fr_io.h"
 
+#include <stdlib.h>
+
 namespace h2g {
 
 static constexpr int PT = 256;
@@ -67,7 +69,8 @@ hipError_t poly_mul_cyclic(Fr* a, size_t n, const Fr* t, size_t t_len, hipStream
 
 // ---------------------------------------------------------------- batch inversion
 // Montgomery's trick over the strided subset {i = t (mod T)} of each thread:
-// 3 multiplications per element + one Fermat inversion per thread.
+// 3 multiplications per element + one inversion per thread (bn254.h inv: binary
+// extended Euclid, whose short dependent chain bounds the kernel's latency).
 __global__ void __launch_bounds__(PT) batch_invert_kernel(Fr* __restrict__ a, size_t n, Fr* __restrict__ pref) {
   const size_t T = (size_t)gridDim.x * blockDim.x;
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -94,7 +97,12 @@ __global__ void __launch_bounds__(PT) batch_invert_kernel(Fr* __restrict__ a, si
 
 hipError_t poly_batch_invert(Fr* a, size_t n, Fr* scratch, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  size_t threads = (n + 63) / 64;  // ~64 elements per thread amortise the Fermat inversion
+  static const size_t per = [] {
+    const char* e = getenv("H2G_BINV_PER");
+    const long v = e ? atol(e) : 32;
+    return (size_t)(v > 0 ? v : 32);
+  }();
+  size_t threads = (n + per - 1) / per;  // elements per thread amortise the inversion
   if (threads < 1) threads = 1;
   const unsigned blocks = (unsigned)((threads + PT - 1) / PT);
   hipLaunchKernelGGL(batch_invert_kernel, dim3(blocks), dim3(PT), 0, st, a, n, scratch);
