@@ -317,3 +317,25 @@ def test_msm_fixed_base_srs_identity_2_20():
     h2g.descriptor_free(h)
     d_sc.close()
     bases_dev.close()
+
+
+@pytest.mark.parametrize("k", [18, 20])
+def test_msm_equal_scalars_srs_identity(k):
+    """One scalar value for every point (a constant column): each window's digits all
+    land in one bucket of n entries, cut into items and combined (msm_big_item_kernel,
+    msm_big_combine_kernel).  sum_i c [s^i]G == [c sum_i s^i]G."""
+    r = rng(300 + k)
+    n = 1 << k
+    s = O.random_fr(r, 1)[0]
+    bases_dev = _srs(n, s)
+    sc = np.tile(O.random_fr(r, 1), (n, 1))
+    want = O.g1_mul(GEN, O.eval_poly(sc, s))
+    d_sc = h2g.DevBuf.from_array(sc)
+    assert np.array_equal(h2g.msm_dev_host(d_sc.ptr, bases_dev.ptr, n), want)
+    h = h2g.base_descriptor_dev(bases_dev.ptr, n, 0)
+    try:
+        assert np.array_equal(h2g.msm_with_cached_base_dev(d_sc.ptr, n, h, 0), want)
+    finally:
+        h2g.descriptor_free(h)
+        d_sc.close()
+        bases_dev.close()

@@ -11,20 +11,20 @@ struct MsmConfig {
 
 // Device workspace, grown on demand and reused across calls.
 struct MsmWorkspace {
-  size_t cap[10] = {};  // byte capacity of each buffer below (grown on demand, never shrunk)
+  size_t cap[12] = {};  // byte capacity of each buffer below (grown on demand, never shrunk)
   int last_c = 0, last_W = 0;    // window config of the most recent msm_run
   void* keys_in = nullptr;       // u64 [n*W] entries (key << 32 | value)
   void* keys_out = nullptr;      // u64 [n*W] sorted entries
   void* bucket_start = nullptr;  // u32 [W*NB]
   void* bucket_end = nullptr;    // u32 [W*NB]
-  void* item_off = nullptr;      // (unused)
-  void* item_bucket = nullptr;   // u32 [W*NB] big-bucket list
+  void* item_off = nullptr;      // uint4 multi-item big buckets (bucket, first item, items)
+  void* item_bucket = nullptr;   // big-bucket work items
   void* partials = nullptr;      // G1xyzz [2 * chunks] boundary slots
   void* buckets = nullptr;       // G1xyzz [W*NB]
   void* segs = nullptr;          // G1xyzz: reduction levels (2 ping-pong arrays + block sums)
   void* windows = nullptr;       // G1xyzz [W]
-  void* result = nullptr;        // counters
-  void* total_items = nullptr;   // (unused)
+  void* result = nullptr;        // counters: [0] items, [1] multi-item buckets
+  void* total_items = nullptr;   // G1xyzz partial sums of big-bucket items
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   void* scan_tmp = nullptr;

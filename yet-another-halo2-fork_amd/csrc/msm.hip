@@ -39,7 +39,7 @@
 namespace h2g {
 
 static constexpr int MSM_THREADS = 256;
-static constexpr uint32_t MSM_SMALL = 32;  // fixup: max chunk pieces summed by one thread
+static constexpr uint32_t MSM_SMALL = 8;  // fixup: max chunk pieces summed by one thread
 
 int msm_windows_for(int c) { return (255 + c - 1) / c; }
 
@@ -195,24 +195,53 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint64_t* __restrict__ 
 // Buckets spanning chunks, one thread per bucket: the piece in its first chunk t0 is
 // that chunk's last run (slot 1) unless the bucket starts the chunk (slot 0); every
 // later chunk holds it as its first run (slot 0).  Buckets over more than MSM_SMALL
-// chunks are summed by one wavefront each (msm_big_bucket_kernel).
+// chunks are cut into items of at most MSM_ITEM pieces (msm_big_item_kernel), whose
+// partial sums a second pass combines per bucket (msm_big_combine_kernel): the depth
+// stays logarithmic however the scalars concentrate (fixed-base top windows: n / 2^12
+// entries per bucket at c = 22; a column of equal values: n entries per bucket).
 __device__ __forceinline__ const G1xyzz& msm_piece(const G1xyzz* bnd, uint32_t t, uint32_t t0, uint32_t bs,
                                                    uint32_t L) {
   return bnd[2 * (size_t)t + ((t == t0 && bs != t0 * L) ? 1 : 0)];
 }
 
+static constexpr uint32_t MSM_GROUP = 16;            // lanes per item
+static constexpr uint32_t MSM_ITEM = MSM_GROUP * 4;  // pieces per item (4 per lane)
+static constexpr unsigned MSM_BIG_BLOCKS = 512;      // persistent grids below
+
+// big-bucket work item: pieces [tb, te) of bucket b; slot = the item's index into the
+// partial sums when the bucket has several items, ~0u when it is the bucket's only one
+struct MsmBigItem {
+  uint32_t b, tb, te, slot;
+};
+
+// upper bounds of the item lists (sizing): a bucket over np > MSM_SMALL chunks takes
+// ceil(np / MSM_ITEM) items, and the buckets' piece counts sum to < 2 nchunks
+static size_t msm_big_items_cap(size_t nchunks) { return 2 * nchunks / MSM_ITEM + 2 * nchunks / MSM_SMALL + 2; }
+static size_t msm_big_multi_cap(size_t nchunks) { return 2 * nchunks / MSM_ITEM + 2; }
+
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ start,
                  const uint32_t* __restrict__ end, uint32_t nbt, uint32_t L, G1xyzz* __restrict__ buckets,
-                 uint32_t* __restrict__ big_list, uint32_t* __restrict__ big_count) {
+                 MsmBigItem* __restrict__ items, uint4* __restrict__ multi, uint32_t* __restrict__ counters) {
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nbt) return;
   const uint32_t bs = start[b], be = end[b];
   if (be <= bs) return;  // empty (buckets[] is zero = identity)
   const uint32_t t0 = bs / L, t1 = (be - 1) / L;
   if (t0 == t1) return;  // written by the accumulation kernel
-  if (t1 - t0 + 1 > MSM_SMALL) {
-    big_list[atomicAdd(big_count, 1u)] = b;
+  const uint32_t np = t1 - t0 + 1;
+  if (np > MSM_SMALL) {
+    const uint32_t cnt = (np + MSM_ITEM - 1) / MSM_ITEM;
+    const uint32_t base = atomicAdd(&counters[0], cnt);
+    for (uint32_t i = 0; i < cnt; i++) {
+      MsmBigItem it;
+      it.b = b;
+      it.tb = t0 + i * MSM_ITEM;
+      it.te = min(t0 + (i + 1) * MSM_ITEM, t1 + 1);
+      it.slot = cnt > 1 ? base + i : ~0u;
+      items[base + i] = it;
+    }
+    if (cnt > 1) multi[atomicAdd(&counters[1], 1u)] = make_uint4(b, base, cnt, 0);
     return;
   }
   G1xyzz acc = msm_piece(bnd, t0, t0, bs, L);
@@ -220,28 +249,65 @@ msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ st
   buckets[b] = acc;
 }
 
-// One wavefront per big bucket (persistent grid): lanes sum strided pieces, then a
-// 6-level tree in the wave's LDS slice.  (Fixed-base windows make big buckets
-// common: the top window holds only the scalars' last few bits, e.g. 12 bits at
-// c = 22, so its 2^12 buckets take n / 2^12 entries each.)
-static constexpr unsigned MSM_BIG_BLOCKS = 512;
+// MSM_GROUP lanes per item (4 items per wave, persistent grid): each lane sums up to
+// 4 strided pieces, then a log2(MSM_GROUP)-level tree in the wave's LDS slice.
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_big_bucket_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ start,
-                      const uint32_t* __restrict__ end, uint32_t L, const uint32_t* __restrict__ big_list,
-                      const uint32_t* __restrict__ big_count, G1xyzz* __restrict__ buckets) {
+msm_big_item_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ start, uint32_t L,
+                    const MsmBigItem* __restrict__ items, const uint32_t* __restrict__ counters,
+                    G1xyzz* __restrict__ partial, G1xyzz* __restrict__ buckets) {
   __shared__ G1xyzz sh[MSM_THREADS];
-  const uint32_t nbig = *big_count;
+  const uint32_t nitems = counters[0];
+  const uint32_t lane = threadIdx.x & 63, g = lane & (MSM_GROUP - 1);
+  G1xyzz* w = sh + (threadIdx.x & ~(MSM_GROUP - 1));
+  constexpr uint32_t per_wave = 64 / MSM_GROUP;
+  const uint32_t stride = gridDim.x * (MSM_THREADS / 64) * per_wave;
+  // uniform trip count per wave (all lanes reach the wave barriers)
+  for (uint32_t q0 = (blockIdx.x * (MSM_THREADS / 64) + (threadIdx.x >> 6)) * per_wave; q0 < nitems;
+       q0 += stride) {
+    const uint32_t q = q0 + lane / MSM_GROUP;
+    G1xyzz acc = G1xyzz::identity();
+    MsmBigItem it = {0, 0, 0, 0};
+    if (q < nitems) {
+      it = items[q];
+      const uint32_t bs = start[it.b], t0 = bs / L;
+      for (uint32_t t = it.tb + g; t < it.te; t += MSM_GROUP) acc = xyzz_add(acc, msm_piece(bnd, t, t0, bs, L));
+    }
+    w[g] = acc;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+    for (uint32_t h = MSM_GROUP / 2; h > 0; h >>= 1) {
+      if (g < h) w[g] = xyzz_add(w[g], w[g + h]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (g == 0 && q < nitems) {
+      if (it.slot == ~0u) buckets[it.b] = w[0];
+      else partial[it.slot] = w[0];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// one wavefront per bucket with several items: sum of its items' partial sums
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_big_combine_kernel(const uint4* __restrict__ multi, const uint32_t* __restrict__ counters,
+                       const G1xyzz* __restrict__ partial, G1xyzz* __restrict__ buckets) {
+  __shared__ G1xyzz sh[MSM_THREADS];
+  const uint32_t nm = counters[1];
   const uint32_t lane = threadIdx.x & 63;
   G1xyzz* w = sh + (threadIdx.x & ~63u);
   const uint32_t nwaves = gridDim.x * (MSM_THREADS / 64);
-  for (uint32_t q = blockIdx.x * (MSM_THREADS / 64) + (threadIdx.x >> 6); q < nbig; q += nwaves) {
-    const uint32_t b = big_list[q];
-    const uint32_t bs = start[b], be = end[b];
-    const uint32_t t0 = bs / L, t1 = (be - 1) / L;
+  for (uint32_t q = blockIdx.x * (MSM_THREADS / 64) + (threadIdx.x >> 6); q < nm; q += nwaves) {
+    const uint4 m = multi[q];  // (bucket, first item, items)
     G1xyzz acc = G1xyzz::identity();
-    for (uint32_t t = t0 + lane; t <= t1; t += 64) acc = xyzz_add(acc, msm_piece(bnd, t, t0, bs, L));
+    for (uint32_t i = lane; i < m.z; i += 64) acc = xyzz_add(acc, partial[m.y + i]);
     w[lane] = acc;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll 1
     for (uint32_t h = 32; h > 0; h >>= 1) {
       if (lane < h) w[lane] = xyzz_add(w[lane], w[lane + h]);
@@ -249,7 +315,7 @@ msm_big_bucket_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (lane == 0) buckets[b] = w[0];
+    if (lane == 0) buckets[m.x] = w[0];
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -403,17 +469,20 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     void** p;
     size_t bytes;
   };
-  const Need need[10] = {{&ws->keys_in, total * 8},
+  const size_t icap = msm_big_items_cap(nchunks), mcap = msm_big_multi_cap(nchunks);
+  const Need need[12] = {{&ws->keys_in, total * 8},
                          {&ws->keys_out, total * 8},
                          {&ws->bucket_start, (size_t)nbt * 4},
                          {&ws->bucket_end, (size_t)nbt * 4},
-                         {&ws->item_bucket, (size_t)nbt * 4},            // big-bucket list
+                         {&ws->item_bucket, icap * sizeof(MsmBigItem)},  // big-bucket items
                          {&ws->partials, 2 * nchunks * sizeof(G1xyzz)},  // boundary slots
                          {&ws->buckets, (size_t)nbt * sizeof(G1xyzz)},
                          {&ws->segs, ((size_t)2 * m1 + nblk) * WB * sizeof(G1xyzz)},
                          {&ws->windows, (size_t)(W > WB ? W : WB) * sizeof(G1xyzz)},
-                         {&ws->result, 16}};  // [0] big-bucket count
-  for (int b = 0; b < 10; b++)
+                         {&ws->result, 16},                              // [0] items, [1] multi-item buckets
+                         {&ws->item_off, mcap * sizeof(uint4)},          // multi-item buckets
+                         {&ws->total_items, icap * sizeof(G1xyzz)}};     // items' partial sums
+  for (int b = 0; b < 12; b++)
     if (need[b].bytes > ws->cap[b]) {
       H2G_TRY(grow(need[b].p, need[b].bytes));
       ws->cap[b] = need[b].bytes;
@@ -425,9 +494,10 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   uint32_t* bstart = (uint32_t*)ws->bucket_start;
   uint32_t* bend = (uint32_t*)ws->bucket_end;
   uint32_t* counters = (uint32_t*)ws->result;
-  uint32_t* big_count = counters;
   const uint32_t sentinel = nbt;  // key of zero digits (msm_digits_kernel)
-  uint32_t* big_list = (uint32_t*)ws->item_bucket;
+  MsmBigItem* items = (MsmBigItem*)ws->item_bucket;
+  uint4* multi = (uint4*)ws->item_off;
+  G1xyzz* ipart = (G1xyzz*)ws->total_items;
   G1xyzz* buckets = (G1xyzz*)ws->buckets;
   G1xyzz* bnd = (G1xyzz*)ws->partials;
   G1xyzz* rS = (G1xyzz*)ws->segs;
@@ -472,9 +542,11 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
                        (uint32_t)total, sentinel, L, buckets, bnd, bstart, bend);
   H2G_PHASE(4);
   hipLaunchKernelGGL(msm_fixup_kernel, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend,
-                     nbt, L, buckets, big_list, big_count);
-  hipLaunchKernelGGL(msm_big_bucket_kernel, dim3(MSM_BIG_BLOCKS), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend, L,
-                     (const uint32_t*)big_list, (const uint32_t*)big_count, buckets);
+                     nbt, L, buckets, items, multi, counters);
+  hipLaunchKernelGGL(msm_big_item_kernel, dim3(MSM_BIG_BLOCKS), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, L,
+                     (const MsmBigItem*)items, (const uint32_t*)counters, ipart, buckets);
+  hipLaunchKernelGGL(msm_big_combine_kernel, dim3(MSM_BIG_BLOCKS / 4), dim3(T), 0, st, (const uint4*)multi,
+                     (const uint32_t*)counters, (const G1xyzz*)ipart, buckets);
   H2G_PHASE(5);
   hipLaunchKernelGGL(msm_rgroup_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1, rS,
                      rR);
