@@ -11,6 +11,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 namespace h2g {
 
 static constexpr int PT = 256;
@@ -97,11 +99,14 @@ __global__ void __launch_bounds__(PT) batch_invert_kernel(Fr* __restrict__ a, si
 
 hipError_t poly_batch_invert(Fr* a, size_t n, Fr* scratch, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  static const size_t per = [] {
+  // elements per thread: the serial chain is ~3 per products + one inversion, the
+  // inversions' total work n / per of them -- measured on MI355X, 4 at 2^18 (keccak-style
+  // proof) and 32 at 2^22 (C3) are best: about 2^16 threads
+  static const long env_per = [] {
     const char* e = getenv("H2G_BINV_PER");
-    const long v = e ? atol(e) : 32;
-    return (size_t)(v > 0 ? v : 32);
+    return e ? atol(e) : 0L;
   }();
+  size_t per = env_per > 0 ? (size_t)env_per : std::min<size_t>(32, std::max<size_t>(4, n >> 16));
   size_t threads = (n + per - 1) / per;  // elements per thread amortise the inversion
   if (threads < 1) threads = 1;
   const unsigned blocks = (unsigned)((threads + PT - 1) / PT);

@@ -117,6 +117,14 @@ struct ProvingKey {
   std::vector<Fr*> gwc_q;
   uint32_t* lk_cnt = nullptr;  // pinned per-lookup match counters (3 per lookup)
   size_t lk_cnt_len = 0;
+  // permute_expression_pair's sort, chosen per lookup from the value width lk_hb[l] (bit
+  // length of the largest canonical value) seen by the previous proof: <= 64 bits: radix
+  // sort of the values themselves; wider: radix sort of a 48-bit window of the top bits
+  // with the row index, gather, and a sortedness check; 0: merge sort of the 256-bit
+  // values.  lk_or_* (device / pinned, LKF per lookup): the limbs' OR and the check flag.
+  static constexpr int LKF = 5;
+  std::vector<int> lk_hb;
+  unsigned long long *lk_or_d = nullptr, *lk_or_h = nullptr;
   Domain dom;
   Pool pool;
   // proving key (device)
@@ -693,7 +701,13 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
     HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, b2, pk.ck_t2, pk.left_flag, pk.ck_left, pk.counters, (int)n, st));
     HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, b3, hipcub::CountingInputIterator<uint32_t>(0), pk.rep_flag,
                                          pk.rep_rows, pk.counters + 1, (int)n, st));
-    pk.sort_tmp_bytes = std::max(b1, std::max(b2, b3));
+    size_t b4 = 0, b5 = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, b4, (uint64_t*)pk.ck_a, (uint64_t*)pk.ck_a + n, (int)n, 0, 64,
+                                             st));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, b5, (uint64_t*)pk.ck_left, (uint64_t*)pk.ck_left + n,
+                                              (uint32_t*)pk.ck_a, (uint32_t*)pk.ck_a + n, (int)n, 0, 48, st));
+    pk.sort_tmp_bytes = std::max(std::max(std::max(b1, b4), b5), std::max(b2, b3));
+    pk.lk_hb.assign(pk.NL, 64);
     HIPCHK(pool.get(&pk.sort_tmp, pk.sort_tmp_bytes));
   }
 
@@ -972,16 +986,50 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       HIPCHK(hipHostMalloc((void**)&pk.lk_cnt, (size_t)pk.NL * 3 * sizeof(uint32_t), hipHostMallocDefault));
       pk.lk_cnt_len = (size_t)pk.NL * 3;
     }
-    for (int l = 0; l < pk.NL; l++) {
-      RCCHK(compress(pk.seg_lk_in[l], pk.lk_a[l]));
-      RCCHK(compress(pk.seg_lk_tab[l], pk.lk_s[l]));
-      // permute_expression_pair: sort by Ord (canonical value), match, fill leftovers
-      HIPCHK(fr_to_canon(pk.lk_a[l], pk.ck_a, u, st));
-      HIPCHK(fr_to_canon(pk.lk_s[l], pk.ck_t, u, st));
+    constexpr int LKF = ProvingKey::LKF;
+    if (!pk.lk_or_d) {
+      HIPCHK(hipMalloc((void**)&pk.lk_or_d, (size_t)pk.NL * LKF * sizeof(unsigned long long)));
+      HIPCHK(hipHostMalloc((void**)&pk.lk_or_h, (size_t)pk.NL * LKF * sizeof(unsigned long long),
+                           hipHostMallocDefault));
+    }
+    HIPCHK(hipMemsetAsync(pk.lk_or_d, 0, (size_t)pk.NL * LKF * sizeof(unsigned long long), st));
+    // permute_expression_pair: sort by Ord (canonical value), match, fill leftovers;
+    // then the bf + 1 random rows (input first, then table) and the two cosets.
+    // hb: value width the sort assumes (1..64 narrow, 65..254 key window, 0 full sort)
+    auto permute = [&](int l, int hb) -> int {
       size_t tb = pk.sort_tmp_bytes;
-      HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(pk.sort_tmp, tb, pk.ck_a, pk.ck_a2, (int)u, CanonLess(), st));
-      tb = pk.sort_tmp_bytes;
-      HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(pk.sort_tmp, tb, pk.ck_t, pk.ck_t2, (int)u, CanonLess(), st));
+      unsigned long long* flags = pk.lk_or_d + (size_t)LKF * l;
+      if (hb > 0 && hb <= 64) {  // the values themselves are the keys
+        uint64_t* ka = (uint64_t*)pk.ck_a;  // [0, n): keys, [n, 2n): sorted
+        uint64_t* kt = (uint64_t*)pk.ck_t;
+        HIPCHK(lookup_keys(pk.lk_a[l], u, 0, nullptr, ka, nullptr, flags, st));
+        HIPCHK(lookup_keys(pk.lk_s[l], u, 0, nullptr, kt, nullptr, flags, st));
+        HIPCHK(hipcub::DeviceRadixSort::SortKeys(pk.sort_tmp, tb, ka, ka + n, (int)u, 0, hb, st));
+        tb = pk.sort_tmp_bytes;
+        HIPCHK(hipcub::DeviceRadixSort::SortKeys(pk.sort_tmp, tb, kt, kt + n, (int)u, 0, hb, st));
+        HIPCHK(key64_expand(ka + n, pk.ck_a2, u, st));
+        HIPCHK(key64_expand(kt + n, pk.ck_t2, u, st));
+      } else if (hb > 64) {  // 48-bit window [hb - 48, hb) with the row index, then gather
+        uint64_t* kin = (uint64_t*)pk.ck_left;  // scratch: keys in/out, indices in/out
+        uint64_t* kout = kin + n;
+        uint32_t* iin = (uint32_t*)(kout + n);
+        uint32_t* iout = iin + n;
+        const Fr* src[2] = {pk.lk_a[l], pk.lk_s[l]};
+        CanonKey* canon[2] = {pk.ck_a, pk.ck_t};
+        CanonKey* sorted[2] = {pk.ck_a2, pk.ck_t2};
+        for (int w = 0; w < 2; w++) {
+          HIPCHK(lookup_keys(src[w], u, hb - 48, canon[w], kin, iin, flags, st));
+          tb = pk.sort_tmp_bytes;
+          HIPCHK(hipcub::DeviceRadixSort::SortPairs(pk.sort_tmp, tb, kin, kout, iin, iout, (int)u, 0, 48, st));
+          HIPCHK(lookup_gather(canon[w], iout, u, sorted[w], flags + 4, st));
+        }
+      } else {
+        HIPCHK(fr_to_canon(pk.lk_a[l], pk.ck_a, u, st));
+        HIPCHK(fr_to_canon(pk.lk_s[l], pk.ck_t, u, st));
+        HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(pk.sort_tmp, tb, pk.ck_a, pk.ck_a2, (int)u, CanonLess(), st));
+        tb = pk.sort_tmp_bytes;
+        HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(pk.sort_tmp, tb, pk.ck_t, pk.ck_t2, (int)u, CanonLess(), st));
+      }
       HIPCHK(hipMemsetAsync(pk.left_flag, 1, u, st));
       HIPCHK(hipMemsetAsync(pk.counters, 0, 8 * sizeof(uint32_t), st));
       HIPCHK(lookup_mark(pk.ck_a2, pk.ck_t2, u, pk.rep_flag, pk.left_flag, pk.counters + 2, st));
@@ -994,20 +1042,52 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       HIPCHK(lookup_assign(pk.ck_a2, pk.rep_flag, u, pk.lk_ap[l], pk.lk_sp[l], st));
       HIPCHK(lookup_scatter(pk.ck_left, pk.rep_rows, pk.counters + 1, u, pk.lk_sp[l], st));
       HIPCHK(hipMemcpyAsync(pk.lk_cnt + 3 * l, pk.counters, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      for (int which = 0; which < 2; which++) {  // bf+1 random rows: input first, then table
-        Fr* r = rows.data() + ((size_t)2 * l + which) * (bf + 1);
-        for (int i = 0; i <= bf; i++) r[i] = rng.random_fr();
+      for (int which = 0; which < 2; which++) {
+        const Fr* r = rows.data() + ((size_t)2 * l + which) * (bf + 1);
         HIPCHK(hipMemcpyAsync((which ? pk.lk_sp[l] : pk.lk_ap[l]) + u, r, (size_t)(bf + 1) * sizeof(Fr),
                               hipMemcpyHostToDevice, st));
       }
-      (void)rng.random_fr();  // permuted input blind
-      (void)rng.random_fr();  // permuted table blind
       RCCHK(lagrange_to_coeff(d, D, pk.lk_ap[l], pk.lk_ap_poly[l], st));
       RCCHK(lagrange_to_coeff(d, D, pk.lk_sp[l], pk.lk_sp_poly[l], st));
       RCCHK(coeff_to_extended(d, D, pk.lk_ap_poly[l], pk.lk_apc[l], st));
       RCCHK(coeff_to_extended(d, D, pk.lk_sp_poly[l], pk.lk_spc[l], st));
+      return H2G_OK;
+    };
+    std::vector<int> used(pk.NL);
+    for (int l = 0; l < pk.NL; l++) {
+      RCCHK(compress(pk.seg_lk_in[l], pk.lk_a[l]));
+      RCCHK(compress(pk.seg_lk_tab[l], pk.lk_s[l]));
+      for (int which = 0; which < 2; which++) {
+        Fr* r = rows.data() + ((size_t)2 * l + which) * (bf + 1);
+        for (int i = 0; i <= bf; i++) r[i] = rng.random_fr();
+      }
+      (void)rng.random_fr();  // permuted input blind
+      (void)rng.random_fr();  // permuted table blind
+      used[l] = pk.lk_hb[l];
+      RCCHK(permute(l, used[l]));
     }
-    HIPCHK(hipStreamSynchronize(st));  // counters landed; rows (host) read
+    HIPCHK(hipMemcpyAsync(pk.lk_or_h, pk.lk_or_d, (size_t)pk.NL * LKF * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));  // counters and value masks landed; rows (host) read
+    // a sort whose assumption failed (values wider than its keys, or a key window that
+    // tied different values out of order) is redone with the full sort; the width is
+    // remembered for the next proof
+    bool redo = false;
+    for (int l = 0; l < pk.NL; l++) {
+      if (used[l] == 0) continue;
+      const unsigned long long* f = pk.lk_or_h + (size_t)LKF * l;
+      int hb = 0;
+      for (int j = 3; j >= 0 && !hb; j--)
+        if (f[j]) hb = 64 * j + 64 - __builtin_clzll(f[j]);
+      if (hb == 0) hb = 1;
+      const bool tie = f[4] != 0;
+      pk.lk_hb[l] = tie && hb == used[l] ? 0 : hb;  // ties at the right width: full sort from now on
+      if (tie || hb > used[l]) {
+        RCCHK(permute(l, 0));
+        redo = true;
+      }
+    }
+    if (redo) HIPCHK(hipStreamSynchronize(st));
     for (int l = 0; l < pk.NL; l++) {
       const uint32_t* cnt = pk.lk_cnt + 3 * l;
       if (cnt[2] != 0 || cnt[0] != cnt[1])
@@ -1998,6 +2078,8 @@ int h2g_pk_free(uint64_t pk) {
   (void)hipStreamSynchronize(d->stream);
   domain_release(&it->second->dom);
   if (it->second->lk_cnt) (void)hipHostFree(it->second->lk_cnt);
+  if (it->second->lk_or_h) (void)hipHostFree(it->second->lk_or_h);
+  if (it->second->lk_or_d) (void)hipFree(it->second->lk_or_d);
   g_pks.erase(it);
   return H2G_OK;
 }

@@ -108,6 +108,15 @@ struct CanonLess {
   }
 };
 hipError_t fr_to_canon(const Fr* in, CanonKey* out, size_t n, hipStream_t st);
+// radix-sort keys key[i] = bits [s, s + 64) of canonical(in[i]) (s < 256); canon / idx
+// (optional) receive the canonical values and i; d_or[0..3] |= the values' 64-bit limbs
+hipError_t lookup_keys(const Fr* in, size_t n, int s, CanonKey* canon, uint64_t* key, uint32_t* idx,
+                       unsigned long long* d_or, hipStream_t st);
+// out[i] = canon[idx[i]]; *unsorted |= 1 if out is not non-decreasing
+hipError_t lookup_gather(const CanonKey* canon, const uint32_t* idx, size_t u, CanonKey* out,
+                         unsigned long long* unsorted, hipStream_t st);
+// canonical values below 2^64 from their low limbs
+hipError_t key64_expand(const uint64_t* in, CanonKey* out, size_t n, hipStream_t st);
 // run starts of the sorted input; each distinct input value marks its first occurrence in
 // the sorted table (lower_bound); *fail counts input values missing from the table
 hipError_t lookup_mark(const CanonKey* a, const CanonKey* t, size_t u, uint8_t* rep_flag, uint8_t* left_flag,

@@ -262,6 +262,90 @@ hipError_t fr_to_canon(const Fr* in, CanonKey* out, size_t n, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Radix keys: bits [s, s + 64) of the canonical value (bits past 255 read as zero) (monotone in the value while every
+// value is below 2^(s + 64)); optionally the canonical values and the identity index;
+// d_or[0..3] |= the values' 64-bit limbs (one atomic per limb per wave), from which the
+// caller checks afterwards that the values fit the key window it chose.
+__global__ void __launch_bounds__(KT) lookup_keys_kernel(const Fr* __restrict__ in, size_t n, int s,
+                                                         CanonKey* __restrict__ canon, uint64_t* __restrict__ key,
+                                                         uint32_t* __restrict__ idx,
+                                                         unsigned long long* __restrict__ d_or) {
+  uint64_t m[4] = {0, 0, 0, 0};
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const Fr c = to_canonical(ldf(in + i));
+    uint64_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      v[j] = (uint64_t)c.l[2 * j] | ((uint64_t)c.l[2 * j + 1] << 32);
+      m[j] |= v[j];
+    }
+    const int w = s >> 6, b = s & 63;
+    const uint64_t lo = w < 4 ? v[w] : 0, hi = w + 1 < 4 ? v[w + 1] : 0;
+    key[i] = b ? (lo >> b) | (hi << (64 - b)) : lo;
+    if (idx) idx[i] = (uint32_t)i;
+    if (canon) {
+      CanonKey k;
+#pragma unroll
+      for (int j = 0; j < 8; j++) k.l[j] = c.l[j];
+      canon[i] = k;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m[j] |= __shfl_xor(m[j], o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (m[j]) atomicOr(&d_or[j], (unsigned long long)m[j]);
+  }
+}
+hipError_t lookup_keys(const Fr* in, size_t n, int s, CanonKey* canon, uint64_t* key, uint32_t* idx,
+                       unsigned long long* d_or, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (s < 0 || s > 255) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(lookup_keys_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, in, n, s, canon, key, idx, d_or);
+  return hipGetLastError();
+}
+
+// out[i] = canon[idx[i]]; *unsorted |= 1 where out[i + 1] < out[i] (the key window
+// tied two different values out of order: the caller falls back to the full sort)
+__global__ void __launch_bounds__(KT) lookup_gather_kernel(const CanonKey* __restrict__ canon,
+                                                           const uint32_t* __restrict__ idx, size_t u,
+                                                           CanonKey* __restrict__ out,
+                                                           unsigned long long* __restrict__ unsorted) {
+  const CanonLess less;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < u; i += (size_t)gridDim.x * blockDim.x) {
+    const CanonKey v = canon[idx[i]];
+    out[i] = v;
+    if (i + 1 < u && less(canon[idx[i + 1]], v)) atomicOr(unsorted, 1ull);
+  }
+}
+hipError_t lookup_gather(const CanonKey* canon, const uint32_t* idx, size_t u, CanonKey* out,
+                         unsigned long long* unsorted, hipStream_t st) {
+  if (u == 0) return hipSuccess;
+  hipLaunchKernelGGL(lookup_gather_kernel, dim3(grid_1d(u)), dim3(KT), 0, st, canon, idx, u, out, unsorted);
+  return hipGetLastError();
+}
+__global__ void __launch_bounds__(KT) key64_expand_kernel(const uint64_t* __restrict__ in, CanonKey* __restrict__ out,
+                                                          size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const uint64_t k = in[i];
+    CanonKey c;
+    c.l[0] = (uint32_t)k;
+    c.l[1] = (uint32_t)(k >> 32);
+#pragma unroll
+    for (int j = 2; j < 8; j++) c.l[j] = 0;
+    out[i] = c;
+  }
+}
+hipError_t key64_expand(const uint64_t* in, CanonKey* out, size_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(key64_expand_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, in, out, n);
+  return hipGetLastError();
+}
+
 __device__ __forceinline__ bool ck_eq(const CanonKey& a, const CanonKey& b) {
   uint32_t x = 0;
 #pragma unroll
