@@ -274,21 +274,27 @@ int msm_desc_impl(Device* d, const void* sc, const Descriptor& ds, size_t off, s
   return msm_host_impl(d, sc, (const char*)ds.d + off * 64, n, 0, out, is_id, st);
 }
 
-int ntt_dev_impl(Device* d, const Fr* src, uint64_t n_in, Fr* dst, uint64_t out_len, int L, const Fr& omega,
-                 int in_dist, const Fr& iz1, const Fr& iz2, int has_scale, const Fr& scale, int out_dist,
-                 const Fr& oz1, const Fr& oz2, hipStream_t st) {
+int ntt_dev_impl_batch(Device* d, const Fr* const* src, uint64_t n_in, Fr* const* dst, int count, uint64_t out_len,
+                       int L, const Fr& omega, int in_dist, const Fr& iz1, const Fr& iz2, int has_scale,
+                       const Fr& scale, int out_dist, const Fr& oz1, const Fr& oz2, hipStream_t st) {
+  if (count < 1 || count > NTT_MAX_BATCH) return fail(H2G_ERR_ARG, "ntt: batch size");
   NttArgs a;
   int rc = get_tables(d, omega, L, st, &a.tab);
   if (rc) return rc;
   const size_t N = (size_t)1 << L;
   if (L > NTT_SMALL_MAX_LOG) {
-    hipError_t e = d->work.ensure(N * sizeof(Fr));
+    hipError_t e = d->work.ensure((size_t)count * N * sizeof(Fr));
     if (e != hipSuccess) return hip_fail(e, "ntt work buffer");
   }
-  a.src = src;
+  a.src = src[0];
   a.n_in = n_in;
   a.work = reinterpret_cast<Fr*>(d->work.p);
-  a.dst = dst;
+  a.dst = dst[0];
+  a.count = count;
+  for (int b = 0; b < count; b++) {
+    a.srcs[b] = src[b];
+    a.dsts[b] = dst[b];
+  }
   a.out_len = out_len;
   a.in_distribute = in_dist;
   a.in_z1 = iz1;
@@ -300,6 +306,13 @@ int ntt_dev_impl(Device* d, const Fr* src, uint64_t n_in, Fr* dst, uint64_t out_
   a.out_z2 = oz2;
   HIPCHK(ntt_run(a, st));
   return H2G_OK;
+}
+
+int ntt_dev_impl(Device* d, const Fr* src, uint64_t n_in, Fr* dst, uint64_t out_len, int L, const Fr& omega,
+                 int in_dist, const Fr& iz1, const Fr& iz2, int has_scale, const Fr& scale, int out_dist,
+                 const Fr& oz1, const Fr& oz2, hipStream_t st) {
+  return ntt_dev_impl_batch(d, &src, n_in, &dst, 1, out_len, L, omega, in_dist, iz1, iz2, has_scale, scale, out_dist,
+                            oz1, oz2, st);
 }
 
 Domain* get_dom(uint64_t h) {
@@ -351,17 +364,30 @@ void domain_release(Domain* dm) {
 
 // lagrange_to_coeff (domain.rs:216-226): iFFT, * 1/n
 int lagrange_to_coeff(Device* d, const Domain& dm, const Fr* src, Fr* dst, hipStream_t st) {
+  return lagrange_to_coeff_batch(d, dm, &src, &dst, 1, st);
+}
+int lagrange_to_coeff_batch(Device* d, const Domain& dm, const Fr* const* src, Fr* const* dst, int count,
+                            hipStream_t st) {
   const Fr one = Fr::one();
   const uint64_t n = 1ull << dm.k;
-  return ntt_dev_impl(d, src, n, dst, n, (int)dm.k, dm.omega_inv, 0, one, one, 1, dm.ifft_div, 0, one, one, st);
+  for (int b0 = 0; b0 < count; b0 += NTT_MAX_BATCH)
+    RCCHK(ntt_dev_impl_batch(d, src + b0, n, dst + b0, std::min(NTT_MAX_BATCH, count - b0), n, (int)dm.k,
+                             dm.omega_inv, 0, one, one, 1, dm.ifft_div, 0, one, one, st));
+  return H2G_OK;
 }
 
 // coeff_to_extended (domain.rs:230-244): distribute zeta powers, zero-pad, FFT over the extended domain
 int coeff_to_extended(Device* d, const Domain& dm, const Fr* src, Fr* dst, hipStream_t st) {
+  return coeff_to_extended_batch(d, dm, &src, &dst, 1, st);
+}
+int coeff_to_extended_batch(Device* d, const Domain& dm, const Fr* const* src, Fr* const* dst, int count,
+                            hipStream_t st) {
   const Fr one = Fr::one();
   const uint64_t n = 1ull << dm.k, ext = 1ull << dm.ek;
-  return ntt_dev_impl(d, src, n, dst, ext, (int)dm.ek, dm.ext_omega, 1, dm.g_coset, dm.g_coset_inv, 0, one, 0, one,
-                      one, st);
+  for (int b0 = 0; b0 < count; b0 += NTT_MAX_BATCH)
+    RCCHK(ntt_dev_impl_batch(d, src + b0, n, dst + b0, std::min(NTT_MAX_BATCH, count - b0), ext, (int)dm.ek,
+                             dm.ext_omega, 1, dm.g_coset, dm.g_coset_inv, 0, one, 0, one, one, st));
+  return H2G_OK;
 }
 
 // extended_to_coeff (domain.rs:271-293): inverse FFT, * 1/2^ek, undistribute, truncate to n (j - 1)

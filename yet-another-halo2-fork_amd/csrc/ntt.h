@@ -6,6 +6,13 @@ namespace h2g {
 
 static constexpr int NTT_SMALL_MAX_LOG = 10;  // whole transform in one block up to 2^10
 static constexpr int NTT_MAX_PASSES = 6;      // passes of 3..6 bits: N up to 2^28
+static constexpr int NTT_MAX_BATCH = 8;       // transforms per batched launch (blockIdx.y)
+
+// per-transform source / destination of a batched launch
+struct NttIo {
+  const Fr* src[NTT_MAX_BATCH];
+  Fr* dst[NTT_MAX_BATCH];
+};
 
 struct NttPlanLg {
   int p = 0;
@@ -27,11 +34,17 @@ struct NttTables {
 //   x_i = src[i] * (in_distribute ? zeta-power(i mod 3) : 1) for i < n_in, 0 beyond
 //   dst[k] = y_k * (has_scale ? scale : 1) * (out_distribute ? zeta-power(k mod 3) : 1), k < out_len
 // `work` is an N-element scratch buffer distinct from src and dst (src may alias dst).
+// Batched: `count` > 1 independent transforms with the same maps, src / dst from
+// `srcs` / `dsts`, `work` of count * N elements; one launch per pass serves them all
+// (more waves in flight for the small transforms of many-column circuits).
 struct NttArgs {
   const Fr* src = nullptr;
   uint64_t n_in = 0;
   Fr* work = nullptr;
   Fr* dst = nullptr;
+  int count = 1;
+  const Fr* srcs[NTT_MAX_BATCH] = {};
+  Fr* dsts[NTT_MAX_BATCH] = {};
   uint64_t out_len = 0;
   NttTables tab;
   int in_distribute = 0;

@@ -145,9 +145,11 @@ struct WaveDif {
 //   `distribute`, multiplies element i by zeta^(i mod 3) (domain.rs:325-341).
 template <int M>
 __global__ void __launch_bounds__(NTT_THREADS, NttPassWaves<M>::value)
-ntt_pass_kernel(Fr* data, const Fr* in, uint64_t n_in, NttTables tab, const Fr* __restrict__ ptw, int L, int lrem,
-                int distribute, Fr z1, Fr z2) {
+ntt_pass_kernel(Fr* data, NttIo io, int first, uint64_t n_in, NttTables tab, const Fr* __restrict__ ptw, int L,
+                int lrem, int distribute, Fr z1, Fr z2) {
   using D = WaveDif<M>;
+  data += (uint64_t)blockIdx.y << L;  // transform blockIdx.y of a batch
+  const Fr* in = first ? io.src[blockIdx.y] : nullptr;
   __shared__ Fr w[1 << (M - 1)];
   for (int j = threadIdx.x; j < (1 << (M - 1)); j += blockDim.x) w[j] = twiddle(tab, (uint64_t)j << (L - M));
   __syncthreads();
@@ -197,9 +199,11 @@ ntt_pass_kernel(Fr* data, const Fr* in, uint64_t n_in, NttTables tab, const Fr* 
 //   Epilogue: multiply by `scale` and, if `distribute`, by the zeta power of
 //   y mod 3; drop y >= out_len (truncation, domain.rs:288-290).
 __global__ void __launch_bounds__(NTT_THREADS, NTT_MIN_WAVES)
-ntt_last_kernel(const Fr* data, Fr* out, uint64_t out_len, NttTables tab, int L, NttPlanLg plan, int has_mul,
+ntt_last_kernel(const Fr* data, NttIo io, uint64_t out_len, NttTables tab, int L, NttPlanLg plan, int has_mul,
                 Fr mul0, Fr mul1, Fr mul2) {
   constexpr int M = 6;
+  data += (uint64_t)blockIdx.y << L;
+  Fr* out = io.dst[blockIdx.y];
   using D = WaveDif<M>;
   __shared__ Fr w[1 << (M - 1)];
   for (int j = threadIdx.x; j < (1 << (M - 1)); j += blockDim.x) w[j] = twiddle(tab, (uint64_t)j << (L - M));
@@ -253,9 +257,11 @@ ntt_last_kernel(const Fr* data, Fr* out, uint64_t out_len, NttTables tab, int L,
 // ---------------------------------------------------------------------------
 // Whole transform in one block (N <= 2^NTT_SMALL_MAX_LOG), radix-2 DIF in LDS.
 __global__ void __launch_bounds__(256)
-ntt_small_kernel(const Fr* src, uint64_t n_in, Fr* out, uint64_t out_len, NttTables tab, int L,
+ntt_small_kernel(NttIo io, uint64_t n_in, uint64_t out_len, NttTables tab, int L,
                  int in_distribute, Fr iz1, Fr iz2, int has_scale, Fr scale, int out_distribute,
                  Fr oz1, Fr oz2) {
+  const Fr* src = io.src[blockIdx.x];
+  Fr* out = io.dst[blockIdx.x];
   extern __shared__ __align__(16) unsigned char smem_raw[];
   Fr* s = reinterpret_cast<Fr*>(smem_raw);
   const int N = 1 << L;
@@ -391,26 +397,33 @@ hipError_t ntt_init_attributes() {
 }
 
 template <int M>
-static void launch_pass(const NttArgs& a, int p, Fr* data, const Fr* in, uint64_t n_in, int L, int lrem, int dist,
-                        hipStream_t st) {
+static void launch_pass(const NttArgs& a, const NttIo& io, int B, int p, int first, uint64_t n_in, int L, int lrem,
+                        int dist, hipStream_t st) {
   const uint64_t N = 1ull << L;
   const uint64_t waves = N / ((1ull << M) * WaveDif<M>::CPW);
   const unsigned blocks = (unsigned)((waves + NTT_WAVES - 1) / NTT_WAVES);
-  hipLaunchKernelGGL(ntt_pass_kernel<M>, dim3(blocks), dim3(NTT_THREADS), 0, st, data, in, n_in, a.tab,
-                     (const Fr*)(a.tab.pass_tw + a.tab.pass_off[p]), L, lrem, dist, a.in_z1, a.in_z2);
+  hipLaunchKernelGGL(ntt_pass_kernel<M>, dim3(blocks, (unsigned)B), dim3(NTT_THREADS), 0, st, a.work, io, first, n_in,
+                     a.tab, (const Fr*)(a.tab.pass_tw + a.tab.pass_off[p]), L, lrem, dist, a.in_z1, a.in_z2);
 }
 
 hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
   const int L = a.tab.L;
   const uint64_t N = 1ull << L;
   const uint64_t out_len = a.out_len ? a.out_len : N;
+  const int B = a.count < 1 ? 1 : a.count;
+  if (B > NTT_MAX_BATCH) return hipErrorInvalidValue;
+  NttIo io = {};
+  for (int b = 0; b < B; b++) {
+    io.src[b] = B == 1 ? a.src : a.srcs[b];
+    io.dst[b] = B == 1 ? a.dst : a.dsts[b];
+  }
   NttPlanLg plan;
   ntt_split(L, &plan.p, plan.lg);
   const int P = plan.p;
   const int* lg = plan.lg;
   if (P == 1) {
     const size_t sm = (N + N / 2 + 1) * sizeof(Fr);
-    hipLaunchKernelGGL(ntt_small_kernel, dim3(1), dim3(256), sm, st, a.src, a.n_in, a.dst, out_len, a.tab, L,
+    hipLaunchKernelGGL(ntt_small_kernel, dim3((unsigned)B), dim3(256), sm, st, io, a.n_in, out_len, a.tab, L,
                        a.in_distribute, a.in_z1, a.in_z2, a.has_scale, a.scale, a.out_distribute, a.out_z1,
                        a.out_z2);
     return hipGetLastError();
@@ -430,14 +443,14 @@ hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
   // last pass: work -> dst in natural order.
   int lrem = L;
   for (int p = 0; p < P - 1; p++) {
-    const Fr* in = p == 0 ? a.src : nullptr;
-    const uint64_t nin = p == 0 ? a.n_in : 0;
-    const int dist = p == 0 ? a.in_distribute : 0;
+    const int first = p == 0;
+    const uint64_t nin = first ? a.n_in : 0;
+    const int dist = first ? a.in_distribute : 0;
     switch (lg[p]) {
-      case 3: launch_pass<3>(a, p, a.work, in, nin, L, lrem, dist, st); break;
-      case 4: launch_pass<4>(a, p, a.work, in, nin, L, lrem, dist, st); break;
-      case 5: launch_pass<5>(a, p, a.work, in, nin, L, lrem, dist, st); break;
-      case 6: launch_pass<6>(a, p, a.work, in, nin, L, lrem, dist, st); break;
+      case 3: launch_pass<3>(a, io, B, p, first, nin, L, lrem, dist, st); break;
+      case 4: launch_pass<4>(a, io, B, p, first, nin, L, lrem, dist, st); break;
+      case 5: launch_pass<5>(a, io, B, p, first, nin, L, lrem, dist, st); break;
+      case 6: launch_pass<6>(a, io, B, p, first, nin, L, lrem, dist, st); break;
       default: return hipErrorInvalidValue;
     }
     lrem -= lg[p];
@@ -445,8 +458,8 @@ hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
   {
     const uint64_t waves = N / (64ull * WaveDif<6>::CPW);
     const unsigned blocks = (unsigned)((waves + NTT_WAVES - 1) / NTT_WAVES);
-    hipLaunchKernelGGL(ntt_last_kernel, dim3(blocks), dim3(NTT_THREADS), 0, st, (const Fr*)a.work, a.dst, out_len,
-                       a.tab, L, plan, has_mul, mul[0], mul[1], mul[2]);
+    hipLaunchKernelGGL(ntt_last_kernel, dim3(blocks, (unsigned)B), dim3(NTT_THREADS), 0, st, (const Fr*)a.work, io,
+                       out_len, a.tab, L, plan, has_mul, mul[0], mul[1], mul[2]);
   }
   return hipGetLastError();
 }

@@ -888,6 +888,13 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
 }
 
 // ------------------------------------------------------------------ create_proof
+// Synchronises a stream when it goes out of scope: declared after host staging buffers
+// that asynchronous copies read, so that an early return cannot free them under a copy.
+struct StreamSyncGuard {
+  hipStream_t s;
+  ~StreamSyncGuard() { (void)hipStreamSynchronize(s); }
+};
+
 struct StageClock {
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
   hipStream_t st;
@@ -936,13 +943,16 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   for (int c = 0; c < pk.A; c++)
     HIPCHK(hipMemcpyAsync(pk.adv[c], advice + 4 * n * c, n * sizeof(Fr),
                           adv_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+  // host staging that device copies read asynchronously: lives until the proof returns
+  // (every copy has completed by then: the final commitment is collected after it)
+  std::vector<Fr> adv_blind((size_t)pk.A * (bf + 1));
+  StreamSyncGuard adv_guard{st};
   {
-    std::vector<Fr> rows((size_t)(bf + 1));
     for (int c = 0; c < pk.A; c++) {
       if (pk.unblinded[c]) continue;
-      for (auto& v : rows) v = rng.random_fr();
-      HIPCHK(hipMemcpyAsync(pk.adv[c] + unusable, rows.data(), rows.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
-      HIPCHK(hipStreamSynchronize(st));  // rows is reused
+      Fr* rows = adv_blind.data() + (size_t)c * (bf + 1);
+      for (int i = 0; i <= bf; i++) rows[i] = rng.random_fr();
+      HIPCHK(hipMemcpyAsync(pk.adv[c] + unusable, rows, (size_t)(bf + 1) * sizeof(Fr), hipMemcpyHostToDevice, st));
     }
     for (int c = 0; c < pk.A; c++)
       if (!pk.unblinded[c]) (void)rng.random_fr();  // commitment blinds (unused by KZG)
@@ -1047,10 +1057,6 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
         HIPCHK(hipMemcpyAsync((which ? pk.lk_sp[l] : pk.lk_ap[l]) + u, r, (size_t)(bf + 1) * sizeof(Fr),
                               hipMemcpyHostToDevice, st));
       }
-      RCCHK(lagrange_to_coeff(d, D, pk.lk_ap[l], pk.lk_ap_poly[l], st));
-      RCCHK(lagrange_to_coeff(d, D, pk.lk_sp[l], pk.lk_sp_poly[l], st));
-      RCCHK(coeff_to_extended(d, D, pk.lk_ap_poly[l], pk.lk_apc[l], st));
-      RCCHK(coeff_to_extended(d, D, pk.lk_sp_poly[l], pk.lk_spc[l], st));
       return H2G_OK;
     };
     std::vector<int> used(pk.NL);
@@ -1094,11 +1100,19 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
         return fail(H2G_ERR_ARG, "create_proof: lookup input value not in the table (ConstraintSystemFailure)");
     }
     std::vector<const Fr*> perm_cols;  // (A'_l, S'_l) in transcript order
+    std::vector<Fr*> perm_polys, perm_cosets;
     for (int l = 0; l < pk.NL; l++) {
       perm_cols.push_back(pk.lk_ap[l]);
       perm_cols.push_back(pk.lk_sp[l]);
+      perm_polys.push_back(pk.lk_ap_poly[l]);
+      perm_polys.push_back(pk.lk_sp_poly[l]);
+      perm_cosets.push_back(pk.lk_apc[l]);
+      perm_cosets.push_back(pk.lk_spc[l]);
     }
     RCCHK(commit_launch_batch(d, prm, perm_cols.data(), 2 * pk.NL, n, SRS_LAGRANGE, st, tk.data()));
+    // coefficient forms and cosets, batched transforms (they overlap the commitments)
+    RCCHK(lagrange_to_coeff_batch(d, D, perm_cols.data(), perm_polys.data(), 2 * pk.NL, st));
+    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)perm_polys.data(), perm_cosets.data(), 2 * pk.NL, st));
     for (int i = 0; i < 2 * pk.NL; i++) {
       G1Affine cm;
       RCCHK(commit_collect(d, &tk[i], &cm));
@@ -1115,13 +1129,17 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   std::vector<MsmTicket> perm_tk(pk.nsets);
   // large MSMs start as soon as their set's z is ready; small ones wait and go as a batch
   const bool perm_batched = commit_batch_chunk(prm, n, SRS_LAGRANGE) > 1;
+  // host staging of every set's / product's blinding rows: no host synchronisation per
+  // set, the transforms of all sets go as batches after the loop
+  std::vector<Fr> perm_blind((size_t)pk.nsets * bf), prod_blind((size_t)(pk.NL + pk.NS) * bf);
+  StreamSyncGuard blind_guard{st};
   {
     const Fr one = Fr::one();
     HIPCHK(hipMemcpyAsync(pk.last_z, &one, sizeof(Fr), hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
     Fr deltaomega = Fr::one();
-    std::vector<Fr> blind_rows(bf);
     for (int s = 0; s < pk.nsets; s++) {
+      Fr* blind_rows = perm_blind.data() + (size_t)s * bf;
       const int c0 = s * pk.chunk_len, c1 = std::min(c0 + pk.chunk_len, pk.P);
       auto col_vals = [&](int c) -> const Fr* {
         const auto& pc = pk.perm_cols[c];
@@ -1155,20 +1173,19 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       if (s == 0) dump("mod0", pk.mod, n, st);
       HIPCHK(poly_prefix_product(pk.mod, pk.pre, n, pk.scr, pk.scr_len, st));
       if (s == 0) dump("pre0", pk.pre, n, st);
-      for (auto& v : blind_rows) v = rng.random_fr();
+      for (int i = 0; i < bf; i++) blind_rows[i] = rng.random_fr();
       (void)rng.random_fr();  // blind
-      HIPCHK(hipMemcpyAsync(pk.small, blind_rows.data(), bf * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(pk.small, blind_rows, bf * sizeof(Fr), hipMemcpyHostToDevice, st));
       HIPCHK(perm_z_assemble(pk.z_lag[s], n, bf, pk.pre, pk.last_z, pk.small, st));
       HIPCHK(hipMemcpyAsync(pk.last_z, pk.z_lag[s] + (n - (size_t)(bf + 1)), sizeof(Fr), hipMemcpyDeviceToDevice,
                             st));
       if (s == 0) dump("z0", pk.z_lag[s], n, st);
       if (s == 0) dump("sigma0", pk.sigma_lag[0], n, st);
       if (s == 0) dump("v0", col_vals(0), n, st);
-      RCCHK(lagrange_to_coeff(d, D, pk.z_lag[s], pk.z[s], st));
-      RCCHK(coeff_to_extended(d, D, pk.z[s], pk.z_coset[s], st));
       if (!perm_batched) RCCHK(commit_launch(d, prm, pk.z_lag[s], n, SRS_LAGRANGE, st, &perm_tk[s]));
-      HIPCHK(hipStreamSynchronize(st));  // blind_rows (host) is reused by the next set
     }
+    RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)pk.z_lag.data(), pk.z.data(), pk.nsets, st));
+    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)pk.z.data(), pk.z_coset.data(), pk.nsets, st));
   }
   if (perm_batched) RCCHK(commit_launch_batch(d, prm, pk.z_lag.data(), pk.nsets, n, SRS_LAGRANGE, st, perm_tk.data()));
   clk.mark("permutation products");
@@ -1176,16 +1193,18 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   // (shuffle/prover.rs:97-206): z = [1, running product ...], bf random rows, blind
   std::vector<MsmTicket> lkz_tk(pk.NL), shz_tk(pk.NS);
   {
-    std::vector<Fr> rows((size_t)bf);
+    std::vector<const Fr*> z_lags;
+    std::vector<Fr*> z_polys, z_cosets;
     auto finish_z = [&](Fr* z_lag, Fr* z_poly, Fr* z_coset, MsmTicket*) -> int {
       HIPCHK(poly_prefix_product(pk.mod, pk.pre, n, pk.scr, pk.scr_len, st));
-      for (auto& v : rows) v = rng.random_fr();
+      Fr* rows = prod_blind.data() + z_lags.size() * (size_t)bf;
+      for (int i = 0; i < bf; i++) rows[i] = rng.random_fr();
       (void)rng.random_fr();  // product blind
-      HIPCHK(hipMemcpyAsync(pk.small, rows.data(), rows.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(pk.small, rows, (size_t)bf * sizeof(Fr), hipMemcpyHostToDevice, st));
       HIPCHK(perm_z_assemble(z_lag, n, bf, pk.pre, pk.one, pk.small, st));
-      RCCHK(lagrange_to_coeff(d, D, z_lag, z_poly, st));
-      RCCHK(coeff_to_extended(d, D, z_poly, z_coset, st));
-      HIPCHK(hipStreamSynchronize(st));  // rows (host) is reused
+      z_lags.push_back(z_lag);
+      z_polys.push_back(z_poly);
+      z_cosets.push_back(z_coset);
       return H2G_OK;
     };
     for (int l = 0; l < pk.NL; l++) {
@@ -1202,6 +1221,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       HIPCHK(shuffle_prod_num(pk.tmp_a, gamma, pk.mod, n, st));
       RCCHK(finish_z(pk.sh_z[s], pk.sh_z_poly[s], pk.sh_zc[s], &shz_tk[s]));
     }
+    RCCHK(lagrange_to_coeff_batch(d, D, z_lags.data(), z_polys.data(), (int)z_lags.size(), st));
+    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)z_polys.data(), z_cosets.data(), (int)z_lags.size(), st));
   }
   {  // product commitments: lookups then shuffles, one batch
     std::vector<const Fr*> zs(pk.lk_z.begin(), pk.lk_z.end());
@@ -1214,14 +1235,17 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   if (pk.NL + pk.NS) clk.mark("lookup/shuffle products");
   // ---- vanishing commit (vanishing/prover.rs:40-98)
   MsmTicket van_tk;
+  std::vector<uint64_t> off;  // staging read by async copies (lives until the proof returns)
+  std::vector<uint32_t> seeds;
+  StreamSyncGuard seed_guard{st};
   {
     const uint64_t T = vthreads ? vthreads : 1;
     const uint64_t chunk = n / T, rem = n % T;
-    std::vector<uint64_t> off;
+    off.clear();
     for (uint64_t i = 0; i < rem && off.size() < T; i++) off.push_back(i * (chunk + 1));
     if (chunk)
       for (uint64_t o = rem * (chunk + 1); off.size() < T; o += chunk) off.push_back(o);
-    std::vector<uint32_t> seeds(off.size() * 8);
+    seeds.assign(off.size() * 8, 0);
     for (size_t i = 0; i < off.size(); i++) rng.fill(reinterpret_cast<uint8_t*>(&seeds[8 * i]), 32);
     if ((int)off.size() > pk.max_chunks) {
       PALLOC(pk.pool, pk.d_seeds, seeds.size());
@@ -1231,15 +1255,14 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     HIPCHK(hipMemcpyAsync(pk.d_seeds, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(pk.d_offsets, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
     HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)off.size(), st));
-    HIPCHK(hipStreamSynchronize(st));  // seeds/off are host temporaries
     (void)rng.random_fr();             // random_blind
     RCCHK(commit_launch(d, prm, pk.random_poly, n, SRS_G, st, &van_tk));
   }
   // advice to coefficient form and the extended-domain cosets do not depend on y:
   // they overlap the permutation / vanishing MSMs
-  for (int c = 0; c < pk.A; c++) RCCHK(lagrange_to_coeff(d, D, pk.adv[c], pk.adv[c], st));
-  for (int c = 0; c < pk.A; c++) RCCHK(coeff_to_extended(d, D, pk.adv[c], pk.adv_coset[c], st));
-  for (int c = 0; c < pk.I; c++) RCCHK(coeff_to_extended(d, D, pk.inst_poly[c], pk.inst_coset[c], st));
+  RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)pk.adv.data(), pk.adv.data(), pk.A, st));
+  RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)pk.adv.data(), pk.adv_coset.data(), pk.A, st));
+  RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)pk.inst_poly.data(), pk.inst_coset.data(), pk.I, st));
   for (int s = 0; s < pk.nsets; s++) {
     G1Affine cm;
     RCCHK(commit_collect(d, &perm_tk[s], &cm));
@@ -1498,6 +1521,10 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   }
 
   // ---- SHPLONK (shplonk/prover.rs:121-305; construct_intermediate_sets shplonk.rs:48-140)
+  // host values the device copies read asynchronously (live until the proof returns)
+  std::vector<std::vector<Fr>> corr_stage;
+  Fr c0_stage;
+  StreamSyncGuard corr_guard{st};
   const Fr sy = tr.squeeze();
   std::vector<Fr> super_pts;
   for (auto& q : queries) {
@@ -1544,7 +1571,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     Fr vpow = Fr::one();
     for (size_t r = 0; r < rs_rep.size(); r++) {
       const std::vector<Fr>& pts = cm_pts[rs_rep[r]];
-      std::vector<Fr> corr(pts.size(), Fr::zero());
+      corr_stage.emplace_back(pts.size(), Fr::zero());  // read by an async copy
+      std::vector<Fr>& corr = corr_stage.back();
       LinTerms t;
       bool first = true;
       Fr ypow = Fr::one();
@@ -1584,7 +1612,6 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       h.len[0] = len;
       h.coef[0] = vpow;
       HIPCHK(lincomb(pk.hx, n, h, r > 0, st));
-      HIPCHK(hipStreamSynchronize(st));  // corr is a host temporary
       vpow = vpow * v;
     }
   }
@@ -1629,7 +1656,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     }
     Fr zt = Fr::one();
     for (auto& sp : super_pts) zt = (u - sp) * zt;
-    HIPCHK(hipMemcpyAsync(pk.small, &c0, sizeof(Fr), hipMemcpyHostToDevice, st));
+    c0_stage = c0;
+    HIPCHK(hipMemcpyAsync(pk.small, &c0_stage, sizeof(Fr), hipMemcpyHostToDevice, st));
     t.p[t.k] = pk.small;
     t.len[t.k] = 1;
     t.coef[t.k] = Fr::one();
@@ -1639,7 +1667,6 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     t.coef[t.k] = Fr::zero() - zt;
     t.k++;
     RCCHK(flush());
-    HIPCHK(hipStreamSynchronize(st));  // c0 is a host temporary
   }
   HIPCHK(kate_division(pk.lx, n, u, pk.q1, pk.scr, st));
   HIPCHK(poly_binop(POLY_SCALE, pk.q1, nullptr, inv(z0), pk.q1, n - 1, st));

@@ -154,6 +154,9 @@ int msm_collect(Device* d, MsmTicket* t, uint64_t* out_affine);
 int msm_fence(Device* d, hipStream_t consumer);
 int msm_desc_impl(Device* d, const void* sc, const Descriptor& ds, size_t off, size_t n, uint64_t* out, int* is_id,
                   hipStream_t st);
+int ntt_dev_impl_batch(Device* d, const Fr* const* src, uint64_t n_in, Fr* const* dst, int count, uint64_t out_len,
+                       int L, const Fr& omega, int in_dist, const Fr& iz1, const Fr& iz2, int has_scale,
+                       const Fr& scale, int out_dist, const Fr& oz1, const Fr& oz2, hipStream_t st);
 int ntt_dev_impl(Device* d, const Fr* src, uint64_t n_in, Fr* dst, uint64_t out_len, int L, const Fr& omega,
                  int in_dist, const Fr& iz1, const Fr& iz2, int has_scale, const Fr& scale, int out_dist,
                  const Fr& oz1, const Fr& oz2, hipStream_t st);
@@ -161,6 +164,11 @@ int ntt_dev_impl(Device* d, const Fr* src, uint64_t n_in, Fr* dst, uint64_t out_
 // EvaluationDomain maps on device pointers (domain.rs:216-316)
 int lagrange_to_coeff(Device* d, const Domain& dm, const Fr* src, Fr* dst, hipStream_t st);
 int coeff_to_extended(Device* d, const Domain& dm, const Fr* src, Fr* dst, hipStream_t st);
+// `count` independent transforms, NTT_MAX_BATCH per launch (work buffer grows to match)
+int lagrange_to_coeff_batch(Device* d, const Domain& dm, const Fr* const* src, Fr* const* dst, int count,
+                            hipStream_t st);
+int coeff_to_extended_batch(Device* d, const Domain& dm, const Fr* const* src, Fr* const* dst, int count,
+                            hipStream_t st);
 int extended_to_coeff(Device* d, const Domain& dm, const Fr* src, Fr* dst, hipStream_t st);
 
 }  // namespace rt
