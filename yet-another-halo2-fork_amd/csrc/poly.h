@@ -19,6 +19,10 @@ hipError_t poly_binop(int op, const Fr* a, const Fr* b, const Fr& c, Fr* out, si
 hipError_t poly_mul_cyclic(Fr* a, size_t n, const Fr* t, size_t t_len, hipStream_t st);
 // ff BatchInvert semantics (zeros stay zero), in place; scratch >= n Fr
 hipError_t poly_batch_invert(Fr* a, size_t n, Fr* scratch, hipStream_t st);
+// count independent batch inversions of n elements (a[i] in place, scratch[i] >= n Fr),
+// POLY_INV_MAX_BATCH arrays per launch
+static constexpr int POLY_INV_MAX_BATCH = 16;
+hipError_t poly_batch_invert_multi(Fr* const* a, Fr* const* scratch, int count, size_t n, hipStream_t st);
 // out[i] = prod_{j<=i} a[j]; scratch >= 2 * ceil(n / 2^?) Fr (see poly.hip)
 hipError_t poly_prefix_product(const Fr* a, Fr* out, size_t n, Fr* scratch, size_t scratch_len, hipStream_t st);
 size_t poly_prefix_scratch_len(size_t n);

@@ -73,7 +73,16 @@ hipError_t poly_mul_cyclic(Fr* a, size_t n, const Fr* t, size_t t_len, hipStream
 // Montgomery's trick over the strided subset {i = t (mod T)} of each thread:
 // 3 multiplications per element + one inversion per thread (bn254.h inv: binary
 // extended Euclid, whose short dependent chain bounds the kernel's latency).
-__global__ void __launch_bounds__(PT) batch_invert_kernel(Fr* __restrict__ a, size_t n, Fr* __restrict__ pref) {
+// Arrays of one launch (blockIdx.y): independent batch inversions share the latency of
+// the per-thread inversion (e.g. every lookup's product denominators at once).
+struct InvBatch {
+  Fr* a[POLY_INV_MAX_BATCH];
+  Fr* pref[POLY_INV_MAX_BATCH];
+};
+
+__global__ void __launch_bounds__(PT) batch_invert_kernel(InvBatch bt, size_t n) {
+  Fr* __restrict__ a = bt.a[blockIdx.y];
+  Fr* __restrict__ pref = bt.pref[blockIdx.y];
   const size_t T = (size_t)gridDim.x * blockDim.x;
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (t >= n) return;
@@ -97,11 +106,11 @@ __global__ void __launch_bounds__(PT) batch_invert_kernel(Fr* __restrict__ a, si
   }
 }
 
-hipError_t poly_batch_invert(Fr* a, size_t n, Fr* scratch, hipStream_t st) {
-  if (n == 0) return hipSuccess;
+hipError_t poly_batch_invert_multi(Fr* const* a, Fr* const* scratch, int count, size_t n, hipStream_t st) {
+  if (n == 0 || count <= 0) return hipSuccess;
   // elements per thread: the serial chain is ~3 per products + one inversion, the
   // inversions' total work n / per of them -- measured on MI355X, 4 at 2^18 (keccak-style
-  // proof) and 32 at 2^22 (C3) are best: about 2^16 threads
+  // proof) and 32 at 2^22 (C3) are best: about 2^16 threads per array
   static const long env_per = [] {
     const char* e = getenv("H2G_BINV_PER");
     return e ? atol(e) : 0L;
@@ -110,8 +119,20 @@ hipError_t poly_batch_invert(Fr* a, size_t n, Fr* scratch, hipStream_t st) {
   size_t threads = (n + per - 1) / per;  // elements per thread amortise the inversion
   if (threads < 1) threads = 1;
   const unsigned blocks = (unsigned)((threads + PT - 1) / PT);
-  hipLaunchKernelGGL(batch_invert_kernel, dim3(blocks), dim3(PT), 0, st, a, n, scratch);
+  for (int b0 = 0; b0 < count; b0 += POLY_INV_MAX_BATCH) {
+    const int m = std::min(POLY_INV_MAX_BATCH, count - b0);
+    InvBatch bt = {};
+    for (int i = 0; i < m; i++) {
+      bt.a[i] = a[b0 + i];
+      bt.pref[i] = scratch[b0 + i];
+    }
+    hipLaunchKernelGGL(batch_invert_kernel, dim3(blocks, (unsigned)m), dim3(PT), 0, st, bt, n);
+  }
   return hipGetLastError();
+}
+
+hipError_t poly_batch_invert(Fr* a, size_t n, Fr* scratch, hipStream_t st) {
+  return poly_batch_invert_multi(&a, &scratch, 1, n, st);
 }
 
 // ---------------------------------------------------------------- prefix product

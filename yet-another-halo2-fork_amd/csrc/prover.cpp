@@ -1137,16 +1137,15 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     const Fr one = Fr::one();
     HIPCHK(hipMemcpyAsync(pk.last_z, &one, sizeof(Fr), hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
-    Fr deltaomega = Fr::one();
+    auto col_vals = [&](int c) -> const Fr* {
+      const auto& pc = pk.perm_cols[c];
+      return pc.first == COL_ADVICE ? pk.adv[pc.second]
+                                    : (pc.first == COL_FIXED ? pk.fixed_lag[pc.second] : pk.inst_val[pc.second]);
+    };
+    // every set's denominators (into z_lag[s]), one batched inversion (z[s] as its
+    // scratch until the iNTT fills it), then per set numerators, scan and z
     for (int s = 0; s < pk.nsets; s++) {
-      Fr* blind_rows = perm_blind.data() + (size_t)s * bf;
       const int c0 = s * pk.chunk_len, c1 = std::min(c0 + pk.chunk_len, pk.P);
-      auto col_vals = [&](int c) -> const Fr* {
-        const auto& pc = pk.perm_cols[c];
-        return pc.first == COL_ADVICE ? pk.adv[pc.second]
-                                      : (pc.first == COL_FIXED ? pk.fixed_lag[pc.second] : pk.inst_val[pc.second]);
-      };
-      // denominators, batch inversion, numerators
       for (int c = c0; c < c1; c += PERM_MAXC) {
         PermCols pc;
         pc.m = std::min(PERM_MAXC, c1 - c);
@@ -1154,11 +1153,17 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
           pc.v[j] = col_vals(c + j);
           pc.sigma[j] = pk.sigma_lag[c + j];
         }
-        HIPCHK(perm_denominators(pk.mod, n, pc, beta, gamma, c == c0, st));
+        HIPCHK(perm_denominators(pk.z_lag[s], n, pc, beta, gamma, c == c0, st));
       }
-      if (s == 0) dump("den0", pk.mod, n, st);
-      HIPCHK(poly_batch_invert(pk.mod, n, pk.scr, st));
-      if (s == 0) dump("inv0", pk.mod, n, st);
+    }
+    dump("den0", pk.z_lag[0], n, st);
+    HIPCHK(poly_batch_invert_multi(pk.z_lag.data(), pk.z.data(), pk.nsets, n, st));
+    dump("inv0", pk.z_lag[0], n, st);
+    Fr deltaomega = Fr::one();
+    for (int s = 0; s < pk.nsets; s++) {
+      Fr* blind_rows = perm_blind.data() + (size_t)s * bf;
+      const int c0 = s * pk.chunk_len, c1 = std::min(c0 + pk.chunk_len, pk.P);
+      Fr* prod = pk.z_lag[s];
       for (int c = c0; c < c1; c += PERM_MAXC) {
         PermCols pc;
         pc.m = std::min(PERM_MAXC, c1 - c);
@@ -1167,11 +1172,11 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
           pc.beta_delta[j] = deltaomega * beta;
           deltaomega = deltaomega * fr_delta();
         }
-        HIPCHK(perm_numerators(pk.mod, n, pc, gamma, pk.om, st));
+        HIPCHK(perm_numerators(prod, n, pc, gamma, pk.om, st));
       }
       // z = last_z * running product, blinding rows from the rng
-      if (s == 0) dump("mod0", pk.mod, n, st);
-      HIPCHK(poly_prefix_product(pk.mod, pk.pre, n, pk.scr, pk.scr_len, st));
+      if (s == 0) dump("mod0", prod, n, st);
+      HIPCHK(poly_prefix_product(prod, pk.pre, n, pk.scr, pk.scr_len, st));
       if (s == 0) dump("pre0", pk.pre, n, st);
       for (int i = 0; i < bf; i++) blind_rows[i] = rng.random_fr();
       (void)rng.random_fr();  // blind
@@ -1195,8 +1200,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   {
     std::vector<const Fr*> z_lags;
     std::vector<Fr*> z_polys, z_cosets;
-    auto finish_z = [&](Fr* z_lag, Fr* z_poly, Fr* z_coset, MsmTicket*) -> int {
-      HIPCHK(poly_prefix_product(pk.mod, pk.pre, n, pk.scr, pk.scr_len, st));
+    auto finish_z = [&](const Fr* prod, Fr* z_lag, Fr* z_poly, Fr* z_coset, MsmTicket*) -> int {
+      HIPCHK(poly_prefix_product(prod, pk.pre, n, pk.scr, pk.scr_len, st));
       Fr* rows = prod_blind.data() + z_lags.size() * (size_t)bf;
       for (int i = 0; i < bf; i++) rows[i] = rng.random_fr();
       (void)rng.random_fr();  // product blind
@@ -1207,11 +1212,15 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       z_cosets.push_back(z_coset);
       return H2G_OK;
     };
+    // every lookup's denominators go through one batched inversion (the per-thread
+    // inversion's latency is paid once); z_poly holds the product until its iNTT,
+    // z_lag serves as the inversion's scratch until z is assembled into it
+    for (int l = 0; l < pk.NL; l++)
+      HIPCHK(lookup_prod_den(pk.lk_ap[l], pk.lk_sp[l], beta, gamma, pk.lk_z_poly[l], n, st));
+    HIPCHK(poly_batch_invert_multi(pk.lk_z_poly.data(), pk.lk_z.data(), pk.NL, n, st));
     for (int l = 0; l < pk.NL; l++) {
-      HIPCHK(lookup_prod_den(pk.lk_ap[l], pk.lk_sp[l], beta, gamma, pk.mod, n, st));
-      HIPCHK(poly_batch_invert(pk.mod, n, pk.scr, st));
-      HIPCHK(lookup_prod_num(pk.lk_a[l], pk.lk_s[l], beta, gamma, pk.mod, n, st));
-      RCCHK(finish_z(pk.lk_z[l], pk.lk_z_poly[l], pk.lk_zc[l], &lkz_tk[l]));
+      HIPCHK(lookup_prod_num(pk.lk_a[l], pk.lk_s[l], beta, gamma, pk.lk_z_poly[l], n, st));
+      RCCHK(finish_z(pk.lk_z_poly[l], pk.lk_z[l], pk.lk_z_poly[l], pk.lk_zc[l], &lkz_tk[l]));
     }
     for (int s = 0; s < pk.NS; s++) {
       RCCHK(compress(pk.seg_sh_in[s], pk.tmp_a));
@@ -1219,7 +1228,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       HIPCHK(shuffle_prod_den(pk.tmp_b, gamma, pk.mod, n, st));
       HIPCHK(poly_batch_invert(pk.mod, n, pk.scr, st));
       HIPCHK(shuffle_prod_num(pk.tmp_a, gamma, pk.mod, n, st));
-      RCCHK(finish_z(pk.sh_z[s], pk.sh_z_poly[s], pk.sh_zc[s], &shz_tk[s]));
+      RCCHK(finish_z(pk.mod, pk.sh_z[s], pk.sh_z_poly[s], pk.sh_zc[s], &shz_tk[s]));
     }
     RCCHK(lagrange_to_coeff_batch(d, D, z_lags.data(), z_polys.data(), (int)z_lags.size(), st));
     RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)z_polys.data(), z_cosets.data(), (int)z_lags.size(), st));

@@ -290,22 +290,32 @@ __global__ void __launch_bounds__(KT) lookup_keys_kernel(const Fr* __restrict__ 
       canon[i] = k;
     }
   }
+  // wave, then block reduction: one atomic per limb per block (same-address atomics
+  // serialise at the memory side -- one per wave cost ~0.15 ms at 2^18)
+  __shared__ uint64_t sm[KT / 64][4];
 #pragma unroll
   for (int j = 0; j < 4; j++) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m[j] |= __shfl_xor(m[j], o);
   }
-  if ((threadIdx.x & 63) == 0) {
+  if ((threadIdx.x & 63) == 0)
 #pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (m[j]) atomicOr(&d_or[j], (unsigned long long)m[j]);
+    for (int j = 0; j < 4; j++) sm[threadIdx.x >> 6][j] = m[j];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int w = 0; w < KT / 64; w++) v |= sm[w][threadIdx.x];
+    if (v) atomicOr(&d_or[threadIdx.x], (unsigned long long)v);
   }
 }
 hipError_t lookup_keys(const Fr* in, size_t n, int s, CanonKey* canon, uint64_t* key, uint32_t* idx,
                        unsigned long long* d_or, hipStream_t st) {
   if (n == 0) return hipSuccess;
   if (s < 0 || s > 255) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(lookup_keys_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, in, n, s, canon, key, idx, d_or);
+  // at most 512 blocks (grid-stride): 512 x 4 atomics
+  const unsigned g = grid_1d(n) < 512 ? grid_1d(n) : 512;
+  hipLaunchKernelGGL(lookup_keys_kernel, dim3(g), dim3(KT), 0, st, in, n, s, canon, key, idx, d_or);
   return hipGetLastError();
 }
 
