@@ -158,8 +158,10 @@ int h2g_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8])
  * gates as flattened ExpressionMid nodes, permutation columns + copies, fixed values.
  * Node = 4 x int32 (op, a, b, c): op 0 CONST (a = constant index), 1 QUERY (a = column
  * type 0 advice / 1 fixed / 2 instance, b = column index, c = rotation), 2 NEG (a),
- * 3 SUM (a, b), 4 PROD (a, b).  Copy = 6 x int32 (ltype, lindex, lrow, rtype, rindex, rrow).
- * Supported: one advice phase (no challenges), gates, permutation, lookups, shuffles.
+ * 3 SUM (a, b), 4 PROD (a, b), 5 CHALLENGE (a = challenge index; ExpressionMid::Challenge).
+ * Copy = 6 x int32 (ltype, lindex, lrow, rtype, rindex, rrow).
+ * Supported: advice phases and challenges (advice_column_phase / challenge_phase of
+ * ConstraintSystemMid, circuit.rs), gates, permutation, lookups, shuffles.
  * rng: ChaCha20Rng::from_seed(rng_seed); vanishing_threads: the thread count that
  * splits the vanishing argument's random polynomial into ChaCha streams
  * (vanishing/prover.rs:57-81), part of the proof's determinism. */
@@ -187,6 +189,11 @@ typedef struct {
   uint32_t num_shuffles;
   const uint32_t* shuffle_sizes;
   const int32_t* shuffle_roots;
+  /* phases (appended; NULL / 0 = one phase, no challenges): advice_phase[num_advice]
+   * (advice_column_phase), challenge_phase[num_challenges] (challenge_phase) */
+  const uint8_t* advice_phase;
+  uint32_t num_challenges;
+  const uint8_t* challenge_phase;
 } h2g_circuit;
 
 /* SRS resident on the current device: g[n] and g_lagrange[n] (G1Affine) from the host... */
@@ -232,6 +239,24 @@ int h2g_pk_set_multiopen(uint64_t pk, int scheme);
 int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int advice_on_device,
                      const uint64_t* instance, const uint32_t* instance_lens, const uint8_t rng_seed[32],
                      uint32_t vanishing_threads, uint8_t* proof, size_t proof_cap, size_t* proof_len);
+/* Prover::commit_phase driven by the caller's witness generator (plonk/prover.rs:309-494):
+ * before committing phase p (0..max advice phase) the prover calls
+ *   fill(ctx, p, challenges, advice)
+ * with the challenges squeezed so far (num_challenges x 4 u64 Montgomery limbs; those of
+ * phases >= p are zero) and the host advice buffer (num_advice x n Fr), in which the
+ * callback writes the columns of phase p (the columns of earlier phases hold what it wrote
+ * before; the prover overwrites their blinding rows).  Nonzero from fill fails the proof
+ * with H2G_ERR_ARG.  h2g_create_proof is the same prover with every phase read from
+ * `advice` (a witness that was computed with the challenges already known). */
+typedef struct {
+  void* ctx;
+  int (*fill)(void* ctx, uint32_t phase, const uint64_t* challenges, uint64_t* advice);
+} h2g_witness_source;
+int h2g_create_proof_phased(uint64_t params, uint64_t pk, const h2g_witness_source* witness,
+                            const uint64_t* instance, const uint32_t* instance_lens, const uint8_t rng_seed[32],
+                            uint32_t vanishing_threads, uint8_t* proof, size_t proof_cap, size_t* proof_len);
+/* the challenges of the last proof (num_challenges x 4 u64), *count = num_challenges */
+int h2g_last_challenges(uint64_t* out, int max, int* count);
 /* wall milliseconds of the stages of the last h2g_create_proof (names: h2g_prover_stage_name) */
 int h2g_prover_stages(double* ms, int max, int* count);
 const char* h2g_prover_stage_name(int i);

@@ -35,7 +35,7 @@
 
 /* ====================================================================== spec */
 enum { COL_ADVICE = 0, COL_FIXED = 1, COL_INSTANCE = 2 };
-enum { OP_CONST = 0, OP_QUERY = 1, OP_NEG = 2, OP_SUM = 3, OP_PROD = 4 };
+enum { OP_CONST = 0, OP_QUERY = 1, OP_NEG = 2, OP_SUM = 3, OP_PROD = 4, OP_CHALLENGE = 5 };
 
 typedef struct {
     uint32_t k, num_advice, num_fixed, num_instance;
@@ -66,6 +66,17 @@ typedef struct {
     const uint32_t *shuffle_sizes;
     const int32_t *shuffle_roots;   /* per shuffle: m input roots, then m shuffle roots */
     uint32_t multiopen;             /* 0 ProverSHPLONK, 1 ProverGWC (poly/kzg/multiopen) */
+    /* phases (ConstraintSystemMid advice_column_phase / challenge_phase; NULL / 0 = one
+     * phase, no challenges) and the witness source of Prover::commit_phase
+     * (prover.rs:309-494): fill(ctx, phase, challenges so far, advice num_advice x n) writes
+     * the phase's columns; NULL fill = every phase read from advice_values */
+    const uint8_t *advice_phase;
+    uint32_t num_challenges;
+    const uint8_t *challenge_phase;
+    int (*fill)(void *ctx, uint32_t phase, const uint64_t *challenges, uint64_t *advice);
+    void *fill_ctx;
+    uint64_t *challenges_out;       /* num_challenges x 4 (may be NULL) */
+    const uint64_t *challenge_values; /* set by or_prove: the squeezed challenges */
 } or_spec;
 
 typedef struct { int type, index, rot; } query_t;
@@ -144,7 +155,7 @@ static fe tr_squeeze(transcript_t *t) {
 static int node_degree(const or_spec *s, int i) {
     const int32_t *nd = s->nodes + 4 * i;
     switch (nd[0]) {
-        case OP_CONST: return 0;
+        case OP_CONST: case OP_CHALLENGE: return 0;
         case OP_QUERY: return 1;
         case OP_NEG: return node_degree(s, nd[1]);
         case OP_SUM: { int a = node_degree(s, nd[1]), b = node_degree(s, nd[2]); return a > b ? a : b; }
@@ -164,7 +175,7 @@ static int qlist_add(qlist *l, int type, int index, int rot) {
 static void collect_queries(const or_spec *s, int i, qlist *adv, qlist *fix, qlist *ins) {
     const int32_t *nd = s->nodes + 4 * i;
     switch (nd[0]) {
-        case OP_CONST: return;
+        case OP_CONST: case OP_CHALLENGE: return;
         case OP_QUERY:
             if (nd[1] == COL_ADVICE) qlist_add(adv, nd[1], nd[2], nd[3]);
             else if (nd[1] == COL_FIXED) qlist_add(fix, nd[1], nd[2], nd[3]);
@@ -182,6 +193,7 @@ static fe eval_node(const or_spec *s, int i, fe *const *adv, fe *const *fix, fe 
     fe r, a, b;
     switch (nd[0]) {
         case OP_CONST: return fe_from(s->constants + 4 * nd[1]);
+        case OP_CHALLENGE: return fe_from(s->challenge_values + 4 * nd[1]);
         case OP_QUERY: {
             int64_t j = ((int64_t)idx + (int64_t)nd[3] * (int64_t)rot_scale) % (int64_t)ext;
             if (j < 0) j += (int64_t)ext;
@@ -536,8 +548,10 @@ void or_pk_sigma(const or_pk *pk, int i, uint64_t *out) { memcpy(out, pk->sigma_
 /* ====================================================================== create_proof */
 /* create_proof for one circuit (prover.rs:512-899).  The witness (advice, instance)
  * and the prover inputs (rng seed, vanishing thread count, SRS) come from `s`. */
-int or_prove(const or_pk *pk, const or_spec *s, uint8_t *proof, uint64_t proof_cap, uint64_t *proof_len, int threads) {
+int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proof_cap, uint64_t *proof_len, int threads) {
     if (threads < 1) threads = 1;
+    or_spec s_local = *s_in;   /* + the challenge values, once squeezed */
+    const or_spec *s = &s_local;
     const uint32_t k = pk->k;
     const uint64_t n = pk->n, ext = pk->ext, rot_scale = pk->rot_scale;
     const int degree = pk->degree, bf = pk->bf, P = pk->P;
@@ -561,23 +575,45 @@ int or_prove(const or_pk *pk, const or_spec *s, uint8_t *proof, uint64_t proof_c
         memcpy(inst_polys[i], inst_vals[i], n * 32);
         lagrange_to_coeff_d(&D, inst_polys[i], threads);
     }
-    /* commit_phase, phase 0 (prover.rs:309-494) */
+    /* commit_phase per advice phase (prover.rs:309-494): the phase's blinding rows, its
+     * blinds, its commitments, then the challenges of the phase */
     fe **adv = (fe **)calloc(s->num_advice + 1, sizeof(fe *));
     const uint64_t unusable = n - (uint64_t)(bf + 1);
-    for (uint32_t c = 0; c < s->num_advice; c++) {
-        adv[c] = fr_alloc(n);
-        memcpy(adv[c], s->advice_values + 4 * n * c, n * 32);
-        if (s->unblinded && s->unblinded[c]) continue;
-        for (uint64_t r = unusable; r < n; r++) fr_random(&rng, &adv[c][r]);
+    int max_phase = 0;
+    for (uint32_t c = 0; c < s->num_advice; c++)
+        if (s->advice_phase && s->advice_phase[c] > max_phase) max_phase = s->advice_phase[c];
+    uint64_t *ch = (uint64_t *)calloc(4 * (s->num_challenges + 1), sizeof(uint64_t));
+    uint64_t *src = s->fill ? (uint64_t *)calloc(4 * n * (s->num_advice + 1), sizeof(uint64_t)) : NULL;
+    for (int ph = 0; ph <= max_phase; ph++) {
+#define IN_PHASE(c) ((s->advice_phase ? s->advice_phase[c] : 0) == ph)
+        const uint64_t *from = s->advice_values;
+        if (s->fill) {
+            if (s->fill(s->fill_ctx, (uint32_t)ph, ch, src)) return -7;
+            from = src;
+        }
+        for (uint32_t c = 0; c < s->num_advice; c++) {
+            if (!IN_PHASE(c)) continue;
+            adv[c] = fr_alloc(n);
+            memcpy(adv[c], from + 4 * n * c, n * 32);
+            if (s->unblinded && s->unblinded[c]) continue;
+            for (uint64_t r = unusable; r < n; r++) fr_random(&rng, &adv[c][r]);
+        }
+        for (uint32_t c = 0; c < s->num_advice; c++) {
+            if (!IN_PHASE(c) || (s->unblinded && s->unblinded[c])) continue;
+            fe blind; fr_random(&rng, &blind);
+        }
+        for (uint32_t c = 0; c < s->num_advice; c++) {
+            if (!IN_PHASE(c)) continue;
+            g1a cm; commit_msm(adv[c], n, s->srs_g_lagrange, threads, &cm);
+            if (tr_write_point(&T, &cm)) return -5;
+        }
+        for (uint32_t i = 0; i < s->num_challenges; i++)
+            if (s->challenge_phase[i] == ph) { fe v = tr_squeeze(&T); memcpy(ch + 4 * i, &v, 32); }
+#undef IN_PHASE
     }
-    for (uint32_t c = 0; c < s->num_advice; c++) {
-        if (s->unblinded && s->unblinded[c]) continue;
-        fe blind; fr_random(&rng, &blind);
-    }
-    for (uint32_t c = 0; c < s->num_advice; c++) {
-        g1a cm; commit_msm(adv[c], n, s->srs_g_lagrange, threads, &cm);
-        if (tr_write_point(&T, &cm)) return -5;
-    }
+    free(src);
+    s_local.challenge_values = ch;
+    if (s->challenges_out) memcpy(s->challenges_out, ch, 32 * s->num_challenges);
     fe theta = tr_squeeze(&T);
     /* lookup_commit_permuted, per lookup (lookup/prover.rs:64-173) */
     const int NL = (int)s->num_lookups, NS = (int)s->num_shuffles;
@@ -1072,7 +1108,7 @@ int or_prove(const or_pk *pk, const or_spec *s, uint8_t *proof, uint64_t proof_c
     *proof_len = T.len;
     /* (small per-proof buffers of this test-infrastructure routine are not all
        released; the large ones are) */
-    free(lx); free(hx); free(h_poly); free(random_poly);
+    free(lx); free(hx); free(h_poly); free(random_poly); free(ch);
     return T.len <= proof_cap ? 0 : -6;
 }
 

@@ -233,7 +233,16 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen=
     for col in instances:
         for v in col:
             T.common_scalar(v)
-    adv_cm = [T.read_point() for _ in range(circ.num_advice)]
+    # advice commitments per phase, each phase followed by its challenges (verifier.rs:104-140)
+    adv_cm = [None] * circ.num_advice
+    chal = [0] * circ.num_challenges
+    for ph in range(circ.max_phase + 1):
+        for col in range(circ.num_advice):
+            if int(circ.advice_phase[col]) == ph:
+                adv_cm[col] = T.read_point()
+        for i in range(circ.num_challenges):
+            if int(circ.challenge_phase[i]) == ph:
+                chal[i] = T.squeeze()
     theta = T.squeeze()
     lk_perm_cm = [(T.read_point(), T.read_point()) for _ in circ.lookups]   # A', S'
     beta = T.squeeze()
@@ -280,7 +289,7 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen=
             return fix_evals[fix_q.index((i, r))]
         return ins_evals[ins_q.index((i, r))]
 
-    exprs = [g.evaluate(lambda c: c, qeval) for g in circ.gates]
+    exprs = [g.evaluate(lambda c: c, qeval, challenge=lambda i: chal[i]) for g in circ.gates]
     if nsets:
         exprs.append(l_0 * (1 - sets[0][0]) % R)
         exprs.append((sets[-1][0] * sets[-1][0] - sets[-1][0]) * l_last % R)
@@ -303,7 +312,7 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen=
     def compress(es):
         acc = 0
         for e in es:
-            acc = (acc * theta + e.evaluate(lambda c: c, qeval)) % R
+            acc = (acc * theta + e.evaluate(lambda c: c, qeval, challenge=lambda i: chal[i])) % R
         return acc
 
     for (ins_e, tab_e), (z, zn, ap, api, sp) in zip(circ.lookups, lk_ev):   # lookup/verifier.rs:98-160

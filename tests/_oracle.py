@@ -228,6 +228,9 @@ class OrSpec(ctypes.Structure):
         ("num_lookups", ctypes.c_uint32), ("lookup_sizes", U32P), ("lookup_roots", I32P),
         ("num_shuffles", ctypes.c_uint32), ("shuffle_sizes", U32P), ("shuffle_roots", I32P),
         ("multiopen", ctypes.c_uint32),
+        ("advice_phase", U8P), ("num_challenges", ctypes.c_uint32), ("challenge_phase", U8P),
+        ("fill", ctypes.c_void_p), ("fill_ctx", ctypes.c_void_p), ("challenges_out", U64P),
+        ("challenge_values", U64P),
     ]
 
 
@@ -244,8 +247,10 @@ def make_spec(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=
         circ.gate_roots, circ.nodes, circ.constants, circ.perm_array, circ.copies, circ.fixed_values,
         wit.advice, wit.instance, wit.instance_lens, circ.transcript_repr(),
         np.frombuffer(bytes(seed), dtype=np.uint8).copy(), srs_g, srs_gl, circ.unblinded,
-        circ.lookup_sizes, circ.lookup_roots, circ.shuffle_sizes, circ.shuffle_roots)]
-    (roots, nodes, consts, perm, copies, fixed, adv, ins, lens, tr, sd, g, gl, unb, lks, lkr, shs, shr) = keep
+        circ.lookup_sizes, circ.lookup_roots, circ.shuffle_sizes, circ.shuffle_roots, circ.advice_phase,
+        circ.challenge_phase)]
+    (roots, nodes, consts, perm, copies, fixed, adv, ins, lens, tr, sd, g, gl, unb, lks, lkr, shs, shr, aph,
+     chph) = keep
     s = OrSpec(circ.k, circ.num_advice, circ.num_fixed, circ.num_instance,
                len(roots), _ptr(roots, I32P), len(nodes), _ptr(nodes, I32P),
                circ.num_constants, _ptr(consts, U64P), len(perm), _ptr(perm, I32P),
@@ -253,7 +258,8 @@ def make_spec(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=
                _ptr(lens, U32P), _ptr(tr, U64P), _ptr(sd, U8P), vanishing_threads,
                _ptr(g, U64P), _ptr(gl, U64P), _ptr(unb, U8P),
                len(circ.lookups), _ptr(lks, U32P), _ptr(lkr, I32P),
-               len(circ.shuffles), _ptr(shs, U32P), _ptr(shr, I32P), MULTIOPEN[multiopen])
+               len(circ.shuffles), _ptr(shs, U32P), _ptr(shr, I32P), MULTIOPEN[multiopen],
+               _ptr(aph, U8P), circ.num_challenges, _ptr(chph, U8P), None, None, None, None)
     return s, keep
 
 
@@ -304,9 +310,20 @@ class Keygen:
 
 
 def create_proof(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=8, threads=8, keygen=None,
-                 multiopen="shplonk"):
-    """Oracle create_proof -> proof bytes (multiopen: "shplonk" = ProverSHPLONK, "gwc" = ProverGWC)."""
+                 multiopen="shplonk", fill=None, challenges_out=None):
+    """Oracle create_proof -> proof bytes (multiopen: "shplonk" = ProverSHPLONK, "gwc" = ProverGWC).
+    fill: the per-phase witness source fill(phase, challenges) -> {column: values}
+    (h2g.witness_fill); challenges_out: a list that receives the squeezed challenges."""
     spec, keep = make_spec(circ, wit, srs_g, srs_gl, seed, vanishing_threads, multiopen)
+    ch = np.zeros((max(circ.num_challenges, 1), 4), dtype=np.uint64)
+    spec.challenges_out = _ptr(ch, U64P)
+    if fill is not None:
+        import h2g
+        cb = h2g.witness_fill(circ.num_advice, circ.n, fill)
+        cb.num_challenges = circ.num_challenges
+        cfn = h2g.WITNESS_FILL(cb)
+        keep.append(cfn)
+        spec.fill = ctypes.cast(cfn, ctypes.c_void_p)
     cap = 1 << 20
     buf = ctypes.create_string_buffer(cap)
     ln = np.zeros(1, dtype=np.uint64)
@@ -316,6 +333,9 @@ def create_proof(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threa
         rc = lib().or_create_proof(ctypes.byref(spec), buf, cap, _p(ln), threads)
     if rc != 0:
         raise ValueError(f"oracle create_proof failed: {rc}")
+    if challenges_out is not None:
+        import h2g_circuit as hc
+        challenges_out[:] = hc.mont_to_ints(ch[: circ.num_challenges])
     return buf.raw[: int(ln[0])]
 
 

@@ -157,3 +157,21 @@ def test_gwc_proof_bytes_match_oracle(name):
     assert V.verify(circ, _instances(circ, wit), got, s, multiopen="gwc")
     assert pk.create_proof(wit) == O.create_proof(circ, wit, g, gl)
     pk.close()
+
+
+def test_phased_proof_matches_oracle():
+    """h2g_create_proof_phased (Prover::commit_phase per phase with the caller's witness
+    source) produces the oracle's bytes and challenges; h2g_create_proof with the complete
+    witness (challenges known) produces the same proof."""
+    circ, wit, fill = hc.challenge_circuit(6)
+    s, g, gl, params = _params(circ.k)
+    ch = []
+    want = O.create_proof(circ, wit, g, gl, fill=fill, challenges_out=ch)
+    pk = h2g.ProvingKey(params, circ)
+    got, got_ch = pk.create_proof_phased(fill, wit)
+    assert got_ch == ch
+    assert got == want
+    full = hc.Witness(np.stack([hc.ints_to_mont(fill.a), hc.ints_to_mont(fill.z_values(ch))]), wit.instance, [])
+    assert pk.create_proof(full) == want
+    assert V.verify(circ, [], got, s)
+    pk.close()

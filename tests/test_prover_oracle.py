@@ -211,3 +211,30 @@ def test_gwc_negative_cases():
     bad.advice[0, 3] = hc.fr_to_limbs(4242)
     assert not V.verify(circ, _instances(circ, bad), O.create_proof(circ, bad, g, gl, multiopen="gwc"), s,
                         multiopen="gwc")
+
+
+def test_phases_and_challenges():
+    """Prover::commit_phase over two advice phases (prover.rs:309-494): the phase-1 witness
+    is computed from the phase-0 challenge the prover hands back; challenges enter gates and
+    compressed lookup expressions.  The proof verifies, equals the proof from the complete
+    witness computed with the same challenges, and a witness that ignores the challenge is
+    rejected.  (Phases are my restatement's; parity with the Rust prover is unpinned here:
+    the reference holds no multi-phase golden proof.)"""
+    circ, wit, fill = hc.challenge_circuit(6)
+    s, g, gl = O.srs(circ.k)
+    ch = []
+    proof = O.create_proof(circ, wit, g, gl, fill=fill, challenges_out=ch)
+    assert len(ch) == 2 and all(0 < c < hc.R_MOD for c in ch)
+    assert V.verify(circ, [], proof, s)
+    full = hc.Witness(np.stack([hc.ints_to_mont(fill.a), hc.ints_to_mont(fill.z_values(ch))]), wit.instance, [])
+    assert O.create_proof(circ, full, g, gl) == proof
+    bad = hc.Witness(np.stack([hc.ints_to_mont(fill.a), hc.ints_to_mont(fill.z_values([5, 0]))]), wit.instance, [])
+    assert not V.verify(circ, [], O.create_proof(circ, bad, g, gl), s)
+
+
+def test_single_phase_transcript_repr_unchanged():
+    """circuits without phases keep their description hash (no phase bytes appended)"""
+    circ, _ = hc.simple_example(6)
+    assert circ.max_phase == 0 and circ.num_challenges == 0
+    c2, _, _ = hc.challenge_circuit(6)
+    assert c2.max_phase == 1 and c2.num_challenges == 2

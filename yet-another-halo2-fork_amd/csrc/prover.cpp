@@ -37,7 +37,7 @@ using namespace h2g::rt;
 namespace {
 
 enum { COL_ADVICE = 0, COL_FIXED = 1, COL_INSTANCE = 2 };
-enum { OP_CONST = 0, OP_QUERY = 1, OP_NEG = 2, OP_SUM = 3, OP_PROD = 4 };
+enum { OP_CONST = 0, OP_QUERY = 1, OP_NEG = 2, OP_SUM = 3, OP_PROD = 4, OP_CHALLENGE = 5 };
 
 struct Pool {  // owns device allocations of one params / pk object
   std::vector<void*> ptrs;
@@ -107,6 +107,10 @@ struct ProvingKey {
   std::vector<Query> adv_q, fix_q, ins_q;
   std::vector<std::pair<int, int>> perm_cols;
   std::vector<uint8_t> unblinded;
+  // advice_column_phase, challenge_phase (ConstraintSystemMid); challenge values live in
+  // consts[num_consts ..]
+  std::vector<uint8_t> adv_phase, ch_phase;
+  int num_consts = 0, max_phase = 0;
   Fr transcript_repr;
   // verifying-key commitments (fixed, permutation) of a key read from bytes; a key made
   // by keygen computes them when it is written (h2g_pk_write)
@@ -357,7 +361,8 @@ int node_degree(const CircuitView& v, int i, std::vector<int>& memo) {
   const int32_t* nd = v.node(i);
   int d = 0;
   switch (nd[0]) {
-    case OP_CONST: d = 0; break;
+    case OP_CONST:
+    case OP_CHALLENGE: d = 0; break;
     case OP_QUERY: d = 1; break;
     case OP_NEG: d = node_degree(v, nd[1], memo); break;
     case OP_SUM: d = std::max(node_degree(v, nd[1], memo), node_degree(v, nd[2], memo)); break;
@@ -373,7 +378,8 @@ void add_query(std::vector<Query>& l, const Query& q) {
 void collect(const CircuitView& v, int i, ProvingKey& pk) {  // keygen.rs:217-249, lhs before rhs
   const int32_t* nd = v.node(i);
   switch (nd[0]) {
-    case OP_CONST: return;
+    case OP_CONST:
+    case OP_CHALLENGE: return;
     case OP_QUERY: {
       const Query q{nd[1], nd[2], nd[3]};
       add_query(nd[1] == COL_ADVICE ? pk.adv_q : (nd[1] == COL_FIXED ? pk.fix_q : pk.ins_q), q);
@@ -441,6 +447,11 @@ struct GateCompiler {
         prog.push_back(make_int4(G_CONST, s, nd[1], 0));
         return s;
       }
+      case OP_CHALLENGE: {  // challenge values follow the constants in pk.consts
+        const int s = alloc();
+        prog.push_back(make_int4(G_CONST, s, (int)v.c->num_constants + nd[1], 0));
+        return s;
+      }
       case OP_QUERY: {
         const int s = alloc();
         prog.push_back(make_int4(G_LOAD, s, load_index(Query{nd[1], nd[2], nd[3]}), 0));
@@ -500,6 +511,9 @@ bool check_nodes(const h2g_circuit* c, std::string* why) {
       case OP_PROD:
         if (nd[1] < 0 || nd[2] < 0 || (uint32_t)nd[1] >= i || (uint32_t)nd[2] >= i)
           return *why = "node child must precede its parent", false;
+        break;
+      case OP_CHALLENGE:
+        if (nd[1] < 0 || (uint32_t)nd[1] >= c->num_challenges) return *why = "challenge index", false;
         break;
       default: return *why = "node op", false;
     }
@@ -568,6 +582,17 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
   pk.unblinded.assign(pk.A, 0);
   if (c->unblinded)
     for (int i = 0; i < pk.A; i++) pk.unblinded[i] = c->unblinded[i];
+  pk.adv_phase.assign(pk.A, 0);
+  if (c->advice_phase)
+    for (int i = 0; i < pk.A; i++) pk.adv_phase[i] = c->advice_phase[i];
+  pk.ch_phase.assign(c->num_challenges, 0);
+  if (c->num_challenges && !c->challenge_phase) return fail(H2G_ERR_ARG, "keygen: null challenge_phase");
+  for (uint32_t i = 0; i < c->num_challenges; i++) pk.ch_phase[i] = c->challenge_phase[i];
+  pk.max_phase = 0;
+  for (int i = 0; i < pk.A; i++) pk.max_phase = std::max(pk.max_phase, (int)pk.adv_phase[i]);
+  for (uint8_t ph : pk.ch_phase)
+    if ((int)ph > pk.max_phase) return fail(H2G_ERR_ARG, "keygen: challenge phase after the last advice phase");
+  pk.num_consts = (int)c->num_constants;
   for (int i = 0; i < pk.P; i++) {
     const int t = c->perm_columns[2 * i], ix = c->perm_columns[2 * i + 1];
     const int lim = t == COL_ADVICE ? pk.A : t == COL_FIXED ? pk.F : t == COL_INSTANCE ? pk.I : 0;
@@ -839,7 +864,7 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
     pk.n_slots = gc.n_slots;
     PALLOC(pool, pk.prog, gc.prog.size() + 1);
     HIPCHK(hipMemcpy(pk.prog, gc.prog.data(), gc.prog.size() * sizeof(int4), hipMemcpyHostToDevice));
-    PALLOC(pool, pk.consts, c->num_constants + 1);
+    PALLOC(pool, pk.consts, c->num_constants + c->num_challenges + 1);
     if (c->num_constants)
       HIPCHK(hipMemcpy(pk.consts, c->constants, c->num_constants * sizeof(Fr), hipMemcpyHostToDevice));
     pk.n_loads = (int)gc.loads.size();
@@ -913,8 +938,10 @@ struct PolyRef {  // a committed polynomial in coefficient form (SHPLONK's "comm
   uint64_t len;
 };
 
+std::vector<Fr> g_last_challenges;  // the challenges of the last proof (h2g_last_challenges)
+
 int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, bool adv_dev,
-               const uint64_t* instance, const uint32_t* inst_lens, const uint8_t seed[32], uint32_t vthreads,
+               const h2g_witness_source* src, const uint64_t* instance, const uint32_t* inst_lens, const uint8_t seed[32], uint32_t vthreads,
                std::vector<uint8_t>* proof) {
   hipStream_t st = d->stream;
   const size_t n = pk.n, ext = pk.ext;
@@ -938,35 +965,61 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     HIPCHK(hipMemcpyAsync(pk.inst_val[i], col, n * sizeof(Fr), hipMemcpyHostToDevice, st));
     RCCHK(lagrange_to_coeff(d, D, pk.inst_val[i], pk.inst_poly[i], st));
   }
-  // ---- advice: blinding rows, commitments (prover.rs:405-455)
+  // ---- commit_phase per advice phase: blinding rows, commitments, then the phase's
+  // challenges (prover.rs:309-494; A.3 draw order: the phase's blinding rows, then its blinds)
   const size_t unusable = n - (size_t)(bf + 1);
-  for (int c = 0; c < pk.A; c++)
-    HIPCHK(hipMemcpyAsync(pk.adv[c], advice + 4 * n * c, n * sizeof(Fr),
-                          adv_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
   // host staging that device copies read asynchronously: lives until the proof returns
   // (every copy has completed by then: the final commitment is collected after it)
   std::vector<Fr> adv_blind((size_t)pk.A * (bf + 1));
+  std::vector<uint64_t> src_buf;  // the witness source's advice columns (host)
+  if (src) src_buf.assign((size_t)pk.A * n * 4, 0);
+  const int NC = (int)pk.ch_phase.size();
+  std::vector<Fr> challenges(NC);
+  std::memset(challenges.data(), 0, challenges.size() * sizeof(Fr));
   StreamSyncGuard adv_guard{st};
-  {
-    for (int c = 0; c < pk.A; c++) {
+  for (int ph = 0; ph <= pk.max_phase; ph++) {
+    std::vector<int> cols;
+    for (int c = 0; c < pk.A; c++)
+      if (pk.adv_phase[c] == ph) cols.push_back(c);
+    const uint64_t* from = advice;
+    bool from_dev = adv_dev;
+    if (src) {
+      if (ph > 0) HIPCHK(hipStreamSynchronize(st));  // the previous phase's uploads read src_buf
+      if (src->fill(src->ctx, (uint32_t)ph, reinterpret_cast<const uint64_t*>(challenges.data()), src_buf.data()))
+        return fail(H2G_ERR_ARG, "create_proof: witness source failed at phase " + std::to_string(ph));
+      from = src_buf.data();
+      from_dev = false;
+    }
+    for (int c : cols)
+      HIPCHK(hipMemcpyAsync(pk.adv[c], from + 4 * n * c, n * sizeof(Fr),
+                            from_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    for (int c : cols) {
       if (pk.unblinded[c]) continue;
       Fr* rows = adv_blind.data() + (size_t)c * (bf + 1);
       for (int i = 0; i <= bf; i++) rows[i] = rng.random_fr();
       HIPCHK(hipMemcpyAsync(pk.adv[c] + unusable, rows, (size_t)(bf + 1) * sizeof(Fr), hipMemcpyHostToDevice, st));
+      if (src) std::memcpy(src_buf.data() + 4 * (n * c + unusable), rows, (size_t)(bf + 1) * sizeof(Fr));
     }
-    for (int c = 0; c < pk.A; c++)
+    for (int c : cols)
       if (!pk.unblinded[c]) (void)rng.random_fr();  // commitment blinds (unused by KZG)
-  }
-  clk.mark("upload+instances");
-  {
-    std::vector<MsmTicket> tk(pk.A);
-    RCCHK(commit_launch_batch(d, prm, pk.adv.data(), pk.A, n, SRS_LAGRANGE, st, tk.data()));
-    for (int c = 0; c < pk.A; c++) {
-      G1Affine cm;
-      RCCHK(commit_collect(d, &tk[c], &cm));
-      RCCHK(write_point(cm));
+    if (ph == 0) clk.mark("upload+instances");
+    if (!cols.empty()) {
+      std::vector<MsmTicket> tk(cols.size());
+      std::vector<Fr*> polys(cols.size());
+      for (size_t i = 0; i < cols.size(); i++) polys[i] = pk.adv[cols[i]];
+      RCCHK(commit_launch_batch(d, prm, polys.data(), (int)cols.size(), n, SRS_LAGRANGE, st, tk.data()));
+      for (size_t i = 0; i < cols.size(); i++) {
+        G1Affine cm;
+        RCCHK(commit_collect(d, &tk[i], &cm));
+        RCCHK(write_point(cm));
+      }
     }
+    for (int i = 0; i < NC; i++)
+      if (pk.ch_phase[i] == ph) challenges[i] = tr.squeeze();
   }
+  if (NC)
+    HIPCHK(hipMemcpyAsync(pk.consts + pk.num_consts, challenges.data(), NC * sizeof(Fr), hipMemcpyHostToDevice, st));
+  g_last_challenges = challenges;
   clk.mark("advice commit");
   const Fr theta = tr.squeeze();
   auto compress = [&](int2 seg, Fr* out) -> int {
@@ -2155,7 +2208,34 @@ int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int a
     return fail(H2G_ERR_ARG, "create_proof: null argument");
   std::vector<uint8_t> out;
   out.reserve(32 * 256);
-  int rc = prove_impl(d, *ip->second, K, advice, advice_on_device != 0, instance, instance_lens, rng_seed,
+  int rc = prove_impl(d, *ip->second, K, advice, advice_on_device != 0, nullptr, instance, instance_lens,
+                      rng_seed, vanishing_threads, &out);
+  if (rc) {
+    (void)hipStreamSynchronize(d->stream);
+    return rc;
+  }
+  *proof_len = out.size();
+  if (out.size() > proof_cap) return fail(H2G_ERR_ARG, "create_proof: proof buffer too small");
+  if (proof) std::memcpy(proof, out.data(), out.size());
+  return H2G_OK;
+}
+
+int h2g_create_proof_phased(uint64_t params, uint64_t pk, const h2g_witness_source* witness,
+                            const uint64_t* instance, const uint32_t* instance_lens, const uint8_t rng_seed[32],
+                            uint32_t vanishing_threads, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
+  NEED_DEV_P();
+  auto ip = g_params.find(params);
+  if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  auto ik = g_pks.find(pk);
+  if (ik == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
+  ProvingKey& K = *ik->second;
+  if (ik->second->params != params) return fail(H2G_ERR_ARG, "create_proof: pk was generated with other params");
+  if (K.device != d->id) return fail(H2G_ERR_ARG, "create_proof: pk lives on another device");
+  if (!witness || !witness->fill || (K.I && (!instance || !instance_lens)) || !rng_seed || !proof_len)
+    return fail(H2G_ERR_ARG, "create_proof: null argument");
+  std::vector<uint8_t> out;
+  out.reserve(32 * 256);
+  int rc = prove_impl(d, *ip->second, K, nullptr, false, witness, instance, instance_lens, rng_seed,
                       vanishing_threads, &out);
   if (rc) {
     (void)hipStreamSynchronize(d->stream);
@@ -2164,6 +2244,14 @@ int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int a
   *proof_len = out.size();
   if (out.size() > proof_cap) return fail(H2G_ERR_ARG, "create_proof: proof buffer too small");
   if (proof) std::memcpy(proof, out.data(), out.size());
+  return H2G_OK;
+}
+
+int h2g_last_challenges(uint64_t* out, int max, int* count) {
+  if (!count) return fail(H2G_ERR_ARG, "last_challenges: null count");
+  *count = (int)g_last_challenges.size();
+  if (out)
+    for (int i = 0; i < *count && i < max; i++) std::memcpy(out + 4 * i, &g_last_challenges[i], sizeof(Fr));
   return H2G_OK;
 }
 

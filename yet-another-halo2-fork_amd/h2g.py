@@ -94,6 +94,9 @@ _SIGS = {
     "h2g_pk_set_multiopen": ([U64, I32], I32),
     "h2g_create_proof": ([U64, U64, VP, I32, U64P, ctypes.POINTER(U32), ctypes.c_char_p, U32, ctypes.c_char_p, SZ,
                           ctypes.POINTER(SZ)], I32),
+    "h2g_create_proof_phased": ([U64, U64, VP, U64P, ctypes.POINTER(U32), ctypes.c_char_p, U32, ctypes.c_char_p,
+                                 SZ, ctypes.POINTER(SZ)], I32),
+    "h2g_last_challenges": ([U64P, I32, ctypes.POINTER(I32)], I32),
     "h2g_prover_stages": ([ctypes.POINTER(ctypes.c_double), I32, ctypes.POINTER(I32)], I32),
     "h2g_prover_stage_name": ([I32], ctypes.c_char_p),
     "h2g_set_shard_transport": ([VP], I32),
@@ -430,7 +433,40 @@ class H2gCircuit(ctypes.Structure):
         ("transcript_repr", U64P),
         ("num_lookups", U32), ("lookup_sizes", ctypes.POINTER(U32)), ("lookup_roots", I32P_),
         ("num_shuffles", U32), ("shuffle_sizes", ctypes.POINTER(U32)), ("shuffle_roots", I32P_),
+        ("advice_phase", ctypes.POINTER(ctypes.c_uint8)), ("num_challenges", U32),
+        ("challenge_phase", ctypes.POINTER(ctypes.c_uint8)),
     ]
+
+
+# h2g_witness_source.fill(ctx, phase, challenges, advice)
+WITNESS_FILL = ctypes.CFUNCTYPE(ctypes.c_int, VP, U32, U64P, U64P)
+
+
+class WitnessSource(ctypes.Structure):
+    """struct h2g_witness_source (include/h2g.h)"""
+    _fields_ = [("ctx", VP), ("fill", WITNESS_FILL)]
+
+
+def witness_fill(num_advice, n, fn):
+    """Wraps fn(phase, challenges: list[int] (canonical, 0 for later phases)) -> {column:
+    n x 4 Montgomery array} as a WITNESS_FILL callback (Prover::commit_phase's witness)."""
+    import h2g_circuit as hc
+
+    def cb(_ctx, phase, ch_p, adv_p):
+        try:
+            nch = cb.num_challenges
+            ch = np.ctypeslib.as_array(ch_p, shape=(max(nch, 1), 4))[:nch] if nch else np.zeros((0, 4), np.uint64)
+            adv = np.ctypeslib.as_array(adv_p, shape=(num_advice, n, 4))
+            for col, vals in fn(int(phase), hc.mont_to_ints(ch)).items():
+                adv[col] = vals
+            return 0
+        except Exception:  # noqa: BLE001 -- reported to the prover as a failed witness
+            import traceback
+            traceback.print_exc()
+            return 1
+
+    cb.num_challenges = 0
+    return cb
 
 
 def _ptr(a, t):
@@ -517,15 +553,18 @@ class ProvingKey:
         keep = [np.ascontiguousarray(x) for x in (circ.gate_roots, circ.nodes, circ.constants, circ.perm_array,
                                                   circ.copies, circ.fixed_values, circ.unblinded,
                                                   circ.transcript_repr(), circ.lookup_sizes, circ.lookup_roots,
-                                                  circ.shuffle_sizes, circ.shuffle_roots)]
-        roots, nodes, consts, perm, copies, fixed, unb, tr, lks, lkr, shs, shr = keep
+                                                  circ.shuffle_sizes, circ.shuffle_roots, circ.advice_phase,
+                                                  circ.challenge_phase)]
+        roots, nodes, consts, perm, copies, fixed, unb, tr, lks, lkr, shs, shr, aph, chph = keep
         c = H2gCircuit(circ.k, circ.num_advice, circ.num_fixed, circ.num_instance,
                        len(roots), _ptr(roots, I32P_), len(nodes), _ptr(nodes, I32P_),
                        circ.num_constants, _ptr(consts, U64P), len(perm), _ptr(perm, I32P_),
                        len(copies), _ptr(copies, I32P_), _ptr(fixed, U64P),
                        _ptr(unb, ctypes.POINTER(ctypes.c_uint8)), _ptr(tr, U64P),
                        len(circ.lookups), _ptr(lks, ctypes.POINTER(U32)), _ptr(lkr, I32P_),
-                       len(circ.shuffles), _ptr(shs, ctypes.POINTER(U32)), _ptr(shr, I32P_))
+                       len(circ.shuffles), _ptr(shs, ctypes.POINTER(U32)), _ptr(shr, I32P_),
+                       _ptr(aph, ctypes.POINTER(ctypes.c_uint8)), circ.num_challenges,
+                       _ptr(chph, ctypes.POINTER(ctypes.c_uint8)))
         h = U64()
         if data is None:
             check(lib().h2g_keygen(params.handle, ctypes.byref(c), ctypes.byref(h)))
@@ -566,6 +605,31 @@ class ProvingKey:
                                      buf, cap, ctypes.byref(ln)))
         del adv
         return buf.raw[: ln.value]
+
+    def create_proof_phased(self, fill, wit, seed=bytes([7] * 32), vanishing_threads=8):
+        """Prover::commit_phase per phase with the witness from fill(phase, challenges) ->
+        {column: values} (see witness_fill); wit supplies the instance columns.
+        -> (proof bytes, challenges as ints)"""
+        check(lib().h2g_pk_set_multiopen(self.handle, 0))
+        circ = self.circ
+        ins = np.ascontiguousarray(wit.instance, dtype=np.uint64) if circ.num_instance else np.zeros(4, np.uint64)
+        lens = np.ascontiguousarray(wit.instance_lens if circ.num_instance else np.zeros(1), dtype=np.uint32)
+        cb = witness_fill(circ.num_advice, circ.n, fill)
+        cb.num_challenges = circ.num_challenges
+        cfn = WITNESS_FILL(cb)
+        src = WitnessSource(None, cfn)
+        cap = 32 * (64 + 8 * (circ.num_advice + circ.num_fixed + 4 * len(circ.perm_columns)) + 64 * 64
+                    + 16 * (len(circ.lookups) + len(circ.shuffles)))
+        buf = ctypes.create_string_buffer(cap)
+        ln = SZ()
+        check(lib().h2g_create_proof_phased(self.params.handle, self.handle, ctypes.byref(src), p64(ins),
+                                            lens.ctypes.data_as(ctypes.POINTER(U32)), bytes(seed),
+                                            vanishing_threads, buf, cap, ctypes.byref(ln)))
+        ch = np.zeros((max(circ.num_challenges, 1), 4), dtype=np.uint64)
+        cnt = ctypes.c_int()
+        check(lib().h2g_last_challenges(p64(ch), circ.num_challenges, ctypes.byref(cnt)))
+        import h2g_circuit as hc
+        return buf.raw[: ln.value], hc.mont_to_ints(ch[: cnt.value])
 
     def close(self):
         if self.handle:

@@ -11,7 +11,7 @@ below lay cells out directly.
 
 Expressions are flattened for the C ABI into nodes of 4 int32 `(op, a, b, c)`:
   CONST (a = constant index) | QUERY (a = column type, b = column index, c = rotation)
-  | NEG (a = child) | SUM / PROD (a = lhs, b = rhs).
+  | NEG (a = child) | SUM / PROD (a = lhs, b = rhs) | CHALLENGE (a = challenge index).
 Column types follow `halo2_middleware::circuit::Any` as used here: 0 advice,
 1 fixed, 2 instance.  Field elements travel as numpy uint64 arrays in halo2curves'
 layout (Montgomery form, 4 little-endian limbs).
@@ -21,7 +21,7 @@ import hashlib
 import numpy as np
 
 ADVICE, FIXED, INSTANCE = 0, 1, 2
-OP_CONST, OP_QUERY, OP_NEG, OP_SUM, OP_PROD = 0, 1, 2, 3, 4
+OP_CONST, OP_QUERY, OP_NEG, OP_SUM, OP_PROD, OP_CHALLENGE = 0, 1, 2, 3, 4, 5
 
 R_MOD = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
 _MONT = (1 << 256) % R_MOD
@@ -53,7 +53,7 @@ def mont_to_ints(arr) -> list:
 
 # ----------------------------------------------------------------------------- expressions
 class Expr:
-    """ExpressionMid (halo2_middleware/src/expression.rs) without challenges."""
+    """ExpressionMid (halo2_middleware/src/expression.rs), challenges included."""
 
     __slots__ = ("op", "a", "b", "c")
 
@@ -82,7 +82,7 @@ class Expr:
         return Expr(OP_NEG, self)
 
     def degree(self):
-        if self.op == OP_CONST:
+        if self.op in (OP_CONST, OP_CHALLENGE):
             return 0
         if self.op == OP_QUERY:
             return 1
@@ -92,16 +92,18 @@ class Expr:
             return max(self.a.degree(), self.b.degree())
         return self.a.degree() + self.b.degree()
 
-    def evaluate(self, const, query, mod=R_MOD):
-        """Expression::evaluate with closures for constants and queries (ints mod r)."""
+    def evaluate(self, const, query, mod=R_MOD, challenge=None):
+        """Expression::evaluate with closures for constants, queries and challenges (ints mod r)."""
         if self.op == OP_CONST:
             return const(self.a) % mod
+        if self.op == OP_CHALLENGE:
+            return challenge(self.a) % mod
         if self.op == OP_QUERY:
             return query(self.a, self.b, self.c) % mod
         if self.op == OP_NEG:
-            return (-self.a.evaluate(const, query, mod)) % mod
-        x = self.a.evaluate(const, query, mod)
-        y = self.b.evaluate(const, query, mod)
+            return (-self.a.evaluate(const, query, mod, challenge)) % mod
+        x = self.a.evaluate(const, query, mod, challenge)
+        y = self.b.evaluate(const, query, mod, challenge)
         return (x + y) % mod if self.op == OP_SUM else (x * y) % mod
 
 
@@ -111,6 +113,11 @@ def _e(x):
 
 def const(v: int) -> Expr:
     return Expr(OP_CONST, int(v) % R_MOD)
+
+
+def challenge(index):
+    """ExpressionMid::Challenge (the value squeezed after its phase's advice commitments)"""
+    return Expr(OP_CHALLENGE, int(index))
 
 
 def advice(col, rot=0):
@@ -130,9 +137,11 @@ class Circuit:
     """ConstraintSystemMid + Preprocessing (one compiled circuit)."""
 
     def __init__(self, k, num_advice, num_fixed, num_instance, gates, perm_columns, copies,
-                 fixed_values, unblinded=None, name="circuit", lookups=(), shuffles=()):
+                 fixed_values, unblinded=None, name="circuit", lookups=(), shuffles=(), advice_phase=None,
+                 challenge_phase=None):
         """lookups: [(input_exprs, table_exprs)], shuffles: [(input_exprs, shuffle_exprs)]
-        (halo2_middleware circuit.rs LookupArgument / ShuffleArgument)"""
+        (halo2_middleware circuit.rs LookupArgument / ShuffleArgument); advice_phase /
+        challenge_phase: ConstraintSystemMid advice_column_phase / challenge_phase"""
         self.lookups = [(list(a), list(b)) for a, b in lookups]
         self.shuffles = [(list(a), list(b)) for a, b in shuffles]
         for a, b in self.lookups + self.shuffles:
@@ -148,6 +157,13 @@ class Circuit:
         for c in unblinded or []:
             self.unblinded[c] = 1
         self.name = name
+        self.advice_phase = np.zeros(max(num_advice, 1), dtype=np.uint8)
+        if advice_phase is not None:
+            self.advice_phase[:num_advice] = advice_phase
+        self.challenge_phase = np.asarray(list(challenge_phase or []) or [0], dtype=np.uint8)
+        self.num_challenges = len(challenge_phase or [])
+        self.max_phase = int(self.advice_phase[:num_advice].max()) if num_advice else 0
+        assert all(int(p) <= self.max_phase for p in self.challenge_phase[:self.num_challenges])
         self._flatten()
 
     # -- ConstraintSystem facts (halo2_backend/src/plonk/circuit.rs, keygen.rs) --
@@ -209,6 +225,8 @@ class Circuit:
                 nodes.append((OP_CONST, const_idx[e.a], 0, 0))
             elif e.op == OP_QUERY:
                 nodes.append((OP_QUERY, e.a, e.b, e.c))
+            elif e.op == OP_CHALLENGE:
+                nodes.append((OP_CHALLENGE, e.a, 0, 0))
             elif e.op == OP_NEG:
                 a = rec(e.a)
                 nodes.append((OP_NEG, a, 0, 0))
@@ -242,7 +260,8 @@ class Circuit:
             self.lookup_sizes.tobytes(), self.lookup_roots.tobytes(), self.shuffle_sizes.tobytes(),
             self.shuffle_roots.tobytes(),
             hashlib.blake2b(self.fixed_values.tobytes()).digest(),
-        ])
+        ] + ([self.advice_phase.tobytes(), self.challenge_phase[:self.num_challenges].tobytes()]
+             if self.max_phase or self.num_challenges else []))
         h.update(len(desc).to_bytes(8, "little"))
         h.update(desc)
         v = int.from_bytes(h.digest(), "little") % R_MOD
@@ -533,3 +552,45 @@ def keccak_style(k, words=16, seed=5):
                    lookups=lookups)
     wit = Witness(adv, np.zeros((0, n, 4), np.uint64), [])
     return circ, wit
+
+
+def challenge_circuit(k=6, seed=6):
+    """C6: two advice phases and two challenges (ConstraintSystemMid advice_column_phase /
+    challenge_phase; Prover::commit_phase, halo2_backend/src/plonk/prover.rs:309-494).
+    Phase 0: advice a (values 0..15); challenge c0 squeezed after it.  Phase 1: advice
+    z, the running random linear combination z[i+1] = z[i] c0 + a[i] (z[0] = 0 by a copy
+    from a cell holding 0); challenge c1 squeezed after it.  Gates: q (z[next] - z c0 - a)
+    c1 and q0 z; lookup (a c0) in (t c0) over a fixed table t = 0..15, so challenges
+    also enter the compressed lookup expressions.
+    -> (circuit, phase-0 witness (instance only), fill(phase, challenges) -> {column: values})"""
+    n = 1 << k
+    rng = np.random.default_rng(seed)
+    c0, c1 = challenge(0), challenge(1)
+    gates = [fixed(0) * (advice(1, 1) - advice(1) * c0 - advice(0)) * c1, fixed(1) * advice(1)]
+    lookups = [([advice(0) * c0], [fixed(2) * c0])]
+    # z has 2 queries (cur, next) -> bf = 5, usable = n - 6
+    usable = n - 6
+    a = [int(v) for v in rng.integers(0, 16, size=n)]
+    a[4] = 0
+    q = [1 if i < usable - 1 else 0 for i in range(n)]
+    q0 = [1 if i == 0 else 0 for i in range(n)]
+    t = [i % 16 for i in range(n)]
+    copies = [(ADVICE, 1, 0, ADVICE, 0, 4), (ADVICE, 0, 2, ADVICE, 0, 6)]
+    a[6] = a[2]
+    fixed_vals = np.stack([ints_to_mont(q), ints_to_mont(q0), ints_to_mont(t)])
+    circ = Circuit(k, 2, 3, 0, gates, [(ADVICE, 0), (ADVICE, 1)], copies, fixed_vals,
+                   name=f"challenge k={k}", lookups=lookups, advice_phase=[0, 1], challenge_phase=[0, 1])
+
+    def z_values(ch):
+        z = [0] * n
+        for i in range(usable - 1):
+            z[i + 1] = (z[i] * ch[0] + a[i]) % R_MOD
+        return z
+
+    def fill(phase, ch):
+        return {0: ints_to_mont(a)} if phase == 0 else {1: ints_to_mont(z_values(ch))}
+
+    fill.z_values = z_values
+    fill.a = a
+    wit = Witness(np.zeros((2, n, 4), dtype=np.uint64), np.zeros((0, n, 4), dtype=np.uint64), [])
+    return circ, wit, fill
