@@ -175,3 +175,18 @@ def test_phased_proof_matches_oracle():
     assert pk.create_proof(full) == want
     assert V.verify(circ, [], got, s)
     pk.close()
+
+
+@pytest.mark.parametrize("k,multiopen", [(7, "shplonk"), (11, "shplonk"), (7, "gwc")])
+def test_three_phase_proof_matches_oracle(k, multiopen):
+    circ, wit, fill = hc.challenge_circuit(k, seed=k, extended=True)
+    s, g, gl, params = _params(circ.k)
+    ch = []
+    want = O.create_proof(circ, wit, g, gl, fill=fill, challenges_out=ch, multiopen=multiopen)
+    pk = h2g.ProvingKey(params, circ)
+    got, got_ch = pk.create_proof_phased(fill, wit, multiopen=multiopen)
+    assert got_ch == ch
+    assert got == want
+    assert pk.create_proof(fill.full(ch), multiopen=multiopen) == want
+    assert V.verify(circ, _instances(circ, wit), got, s, multiopen=multiopen)
+    pk.close()

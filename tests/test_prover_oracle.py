@@ -238,3 +238,20 @@ def test_single_phase_transcript_repr_unchanged():
     assert circ.max_phase == 0 and circ.num_challenges == 0
     c2, _, _ = hc.challenge_circuit(6)
     assert c2.max_phase == 1 and c2.num_challenges == 2
+
+
+@pytest.mark.parametrize("multiopen", ["shplonk", "gwc"])
+def test_three_phases_shuffle_unblinded(multiopen):
+    """three advice phases, an unblinded phase-1 column shuffled against a phase-0 column,
+    an instance column, a phase-1 challenge used by a phase-2 column"""
+    circ, wit, fill = hc.challenge_circuit(7, extended=True)
+    s, g, gl = O.srs(circ.k)
+    ch = []
+    proof = O.create_proof(circ, wit, g, gl, fill=fill, challenges_out=ch, multiopen=multiopen)
+    inst = _instances(circ, wit)
+    assert V.verify(circ, inst, proof, s, multiopen=multiopen)
+    assert O.create_proof(circ, fill.full(ch), g, gl, multiopen=multiopen) == proof
+    # a w that is not a permutation of a's active rows breaks the shuffle
+    bad = fill.full(ch)
+    bad.advice[2, 0] = hc.ints_to_mont([(fill.a[1] + 1) % 16])[0]
+    assert not V.verify(circ, inst, O.create_proof(circ, bad, g, gl, multiopen=multiopen), s, multiopen=multiopen)

@@ -606,11 +606,11 @@ class ProvingKey:
         del adv
         return buf.raw[: ln.value]
 
-    def create_proof_phased(self, fill, wit, seed=bytes([7] * 32), vanishing_threads=8):
+    def create_proof_phased(self, fill, wit, seed=bytes([7] * 32), vanishing_threads=8, multiopen="shplonk"):
         """Prover::commit_phase per phase with the witness from fill(phase, challenges) ->
         {column: values} (see witness_fill); wit supplies the instance columns.
         -> (proof bytes, challenges as ints)"""
-        check(lib().h2g_pk_set_multiopen(self.handle, 0))
+        check(lib().h2g_pk_set_multiopen(self.handle, {"shplonk": 0, "gwc": 1}[multiopen]))
         circ = self.circ
         ins = np.ascontiguousarray(wit.instance, dtype=np.uint64) if circ.num_instance else np.zeros(4, np.uint64)
         lens = np.ascontiguousarray(wit.instance_lens if circ.num_instance else np.zeros(1), dtype=np.uint32)

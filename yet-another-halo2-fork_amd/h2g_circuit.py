@@ -554,7 +554,7 @@ def keccak_style(k, words=16, seed=5):
     return circ, wit
 
 
-def challenge_circuit(k=6, seed=6):
+def challenge_circuit(k=6, seed=6, extended=False):
     """C6: two advice phases and two challenges (ConstraintSystemMid advice_column_phase /
     challenge_phase; Prover::commit_phase, halo2_backend/src/plonk/prover.rs:309-494).
     Phase 0: advice a (values 0..15); challenge c0 squeezed after it.  Phase 1: advice
@@ -562,6 +562,9 @@ def challenge_circuit(k=6, seed=6):
     from a cell holding 0); challenge c1 squeezed after it.  Gates: q (z[next] - z c0 - a)
     c1 and q0 z; lookup (a c0) in (t c0) over a fixed table t = 0..15, so challenges
     also enter the compressed lookup expressions.
+    extended: adds an unblinded phase-1 column w = a c1-free copy of a shifted (w[i] = a[i+1])
+    whose rows are shuffled against a (shuffle (w) ~ (a) over the usable rows), an instance
+    column, and a third phase with a column holding z scaled by the phase-1 challenge.
     -> (circuit, phase-0 witness (instance only), fill(phase, challenges) -> {column: values})"""
     n = 1 << k
     rng = np.random.default_rng(seed)
@@ -578,8 +581,19 @@ def challenge_circuit(k=6, seed=6):
     copies = [(ADVICE, 1, 0, ADVICE, 0, 4), (ADVICE, 0, 2, ADVICE, 0, 6)]
     a[6] = a[2]
     fixed_vals = np.stack([ints_to_mont(q), ints_to_mont(q0), ints_to_mont(t)])
-    circ = Circuit(k, 2, 3, 0, gates, [(ADVICE, 0), (ADVICE, 1)], copies, fixed_vals,
-                   name=f"challenge k={k}", lookups=lookups, advice_phase=[0, 1], challenge_phase=[0, 1])
+    if not extended:
+        circ = Circuit(k, 2, 3, 0, gates, [(ADVICE, 0), (ADVICE, 1)], copies, fixed_vals,
+                       name=f"challenge k={k}", lookups=lookups, advice_phase=[0, 1], challenge_phase=[0, 1])
+    else:
+        # w (col 2, phase 1, unblinded): a permutation of a's active rows (rotated by one);
+        # y (col 3, phase 2): y = z c1 on the q rows; instance 0 = a[0..4)
+        gates.append(fixed(0) * (advice(3) - advice(1) * c1))
+        shuffles = [([fixed(3) * advice(2)], [fixed(3) * advice(0)])]
+        fixed_vals = np.concatenate([fixed_vals, ints_to_mont([1 if i < usable else 0 for i in range(n)])[None]])
+        copies = copies + [(ADVICE, 0, i, INSTANCE, 0, i) for i in range(4)]
+        circ = Circuit(k, 4, 4, 1, gates, [(ADVICE, 0), (ADVICE, 1), (INSTANCE, 0)], copies, fixed_vals,
+                       unblinded=[2], name=f"challenge+ k={k}", lookups=lookups, shuffles=shuffles,
+                       advice_phase=[0, 1, 1, 2], challenge_phase=[0, 1])
 
     def z_values(ch):
         z = [0] * n
@@ -587,10 +601,33 @@ def challenge_circuit(k=6, seed=6):
             z[i + 1] = (z[i] * ch[0] + a[i]) % R_MOD
         return z
 
+    w = [a[(i + 1) % usable] if i < usable else 0 for i in range(n)]
+
+    def y_values(ch):
+        z = z_values(ch)
+        return [z[i] * ch[1] % R_MOD if q[i] else 0 for i in range(n)]
+
     def fill(phase, ch):
-        return {0: ints_to_mont(a)} if phase == 0 else {1: ints_to_mont(z_values(ch))}
+        if phase == 0:
+            return {0: ints_to_mont(a)}
+        if phase == 1:
+            out = {1: ints_to_mont(z_values(ch))}
+            if extended:
+                out[2] = ints_to_mont(w)
+            return out
+        return {3: ints_to_mont(y_values(ch))}
+
+    def full(ch):
+        """the complete witness once the challenges are known"""
+        cols = [a, z_values(ch)] + ([w, y_values(ch)] if extended else [])
+        return Witness(np.stack([ints_to_mont(c) for c in cols]), wit.instance, wit.instance_lens)
 
     fill.z_values = z_values
     fill.a = a
-    wit = Witness(np.zeros((2, n, 4), dtype=np.uint64), np.zeros((0, n, 4), dtype=np.uint64), [])
+    fill.full = full
+    if extended:
+        inst = ints_to_mont(a[:4] + [0] * (n - 4))[None]
+        wit = Witness(np.zeros((4, n, 4), dtype=np.uint64), inst, [4])
+    else:
+        wit = Witness(np.zeros((2, n, 4), dtype=np.uint64), np.zeros((0, n, 4), dtype=np.uint64), [])
     return circ, wit, fill
