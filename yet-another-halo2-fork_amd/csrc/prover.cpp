@@ -4,7 +4,7 @@
 //   keygen_vk / keygen_pk          plonk/keygen.rs:43-190, circuit.rs:95-180,292-320
 //   permutation Assembly/build_pk  plonk/permutation/keygen.rs:16-213
 //   Prover::new_with_engine        plonk/prover.rs:174-305 (instances)
-//   commit_phase                   plonk/prover.rs:309-494 (one phase, no challenges)
+//   commit_phase                   plonk/prover.rs:309-494 (every advice phase, challenges after each)
 //   create_proof                   plonk/prover.rs:512-899
 //   permutation_commit/evaluate    plonk/permutation/prover.rs:50-333
 //   vanishing commit/construct     plonk/vanishing/prover.rs:40-205
