@@ -190,3 +190,22 @@ def test_three_phase_proof_matches_oracle(k, multiopen):
     assert pk.create_proof(fill.full(ch), multiopen=multiopen) == want
     assert V.verify(circ, _instances(circ, wit), got, s, multiopen=multiopen)
     pk.close()
+
+
+def test_phased_witness_failure_is_an_error():
+    circ, wit, fill = hc.challenge_circuit(6)
+    _, _, _, params = _params(circ.k)
+    pk = h2g.ProvingKey(params, circ)
+
+    def broken(phase, ch):
+        if phase == 1:
+            raise RuntimeError("witness generator failed")
+        return fill(phase, ch)
+
+    with pytest.raises(h2g.H2GError, match="witness source failed at phase 1"):
+        pk.create_proof_phased(broken, wit)
+    # the key still proves afterwards
+    ch = []
+    s, g, gl, _ = _params(circ.k)
+    assert pk.create_proof_phased(fill, wit)[0] == O.create_proof(circ, wit, g, gl, fill=fill, challenges_out=ch)
+    pk.close()

@@ -255,3 +255,16 @@ def test_three_phases_shuffle_unblinded(multiopen):
     bad = fill.full(ch)
     bad.advice[2, 0] = hc.ints_to_mont([(fill.a[1] + 1) % 16])[0]
     assert not V.verify(circ, inst, O.create_proof(circ, bad, g, gl, multiopen=multiopen), s, multiopen=multiopen)
+
+
+def test_witness_source_failure_fails_the_proof():
+    circ, wit, fill = hc.challenge_circuit(6)
+    _, g, gl = O.srs(circ.k)
+
+    def broken(phase, ch):
+        if phase == 1:
+            raise RuntimeError("witness generator failed")
+        return fill(phase, ch)
+
+    with pytest.raises(ValueError):
+        O.create_proof(circ, wit, g, gl, fill=broken)
