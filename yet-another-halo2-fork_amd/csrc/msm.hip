@@ -327,7 +327,10 @@ msm_big_combine_kernel(const uint4* __restrict__ multi, const uint32_t* __restri
 //   rscale : V_g = S_g + [RG g] R_g   (F = sum_g V_g), block sums of V
 //   rfinal : sum of the block sums
 // depth ~ 2 RG + (log2(RG m) dbl + adds) + 2 x 8 tree steps.
-static constexpr int RG = 8;
+#ifndef H2G_MSM_RG
+#define H2G_MSM_RG 8
+#endif
+static constexpr int RG = H2G_MSM_RG;
 
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_rgroup_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, G1xyzz* __restrict__ S,
