@@ -244,9 +244,9 @@ int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int a
  *   fill(ctx, p, challenges, advice)
  * with the challenges squeezed so far (num_challenges x 4 u64 Montgomery limbs; those of
  * phases >= p are zero) and the host advice buffer (num_advice x n Fr), in which the
- * callback writes the columns of phase p (the columns of earlier phases hold what it wrote
- * before; the prover overwrites their blinding rows).  Nonzero from fill fails the proof
- * with H2G_ERR_ARG.  h2g_create_proof is the same prover with every phase read from
+ * callback writes the columns of phase p (pinned staging owned by the key; the prover reads
+ * only phase p's columns from it, other rows/columns may hold anything).  Nonzero from fill
+ * fails the proof with H2G_ERR_ARG.  h2g_create_proof is the same prover with every phase read from
  * `advice` (a witness that was computed with the challenges already known). */
 typedef struct {
   void* ctx;

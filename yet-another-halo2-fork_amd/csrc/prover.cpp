@@ -120,6 +120,7 @@ struct ProvingKey {
   int multiopen = 0;
   std::vector<Fr*> gwc_q;
   uint32_t* lk_cnt = nullptr;  // pinned per-lookup match counters (3 per lookup)
+  uint64_t* wit_pin = nullptr;  // pinned advice staging of the witness source (num_advice x n Fr)
   size_t lk_cnt_len = 0;
   // permute_expression_pair's sort, chosen per lookup from the value width lk_hb[l] (bit
   // length of the largest canonical value) seen by the previous proof: <= 64 bits: radix
@@ -971,8 +972,14 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   // host staging that device copies read asynchronously: lives until the proof returns
   // (every copy has completed by then: the final commitment is collected after it)
   std::vector<Fr> adv_blind((size_t)pk.A * (bf + 1));
-  std::vector<uint64_t> src_buf;  // the witness source's advice columns (host)
-  if (src) src_buf.assign((size_t)pk.A * n * 4, 0);
+  // the witness source writes straight into pinned staging (allocated once per key: a
+  // pinned allocation of this size costs far more than the copies it speeds up)
+  uint64_t* src_buf = nullptr;
+  if (src) {
+    if (!pk.wit_pin)
+      HIPCHK(hipHostMalloc((void**)&pk.wit_pin, (size_t)std::max(pk.A, 1) * n * sizeof(Fr), hipHostMallocDefault));
+    src_buf = pk.wit_pin;  // only the committed phase's columns are read from it
+  }
   const int NC = (int)pk.ch_phase.size();
   std::vector<Fr> challenges(NC);
   std::memset(challenges.data(), 0, challenges.size() * sizeof(Fr));
@@ -985,9 +992,9 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     bool from_dev = adv_dev;
     if (src) {
       if (ph > 0) HIPCHK(hipStreamSynchronize(st));  // the previous phase's uploads read src_buf
-      if (src->fill(src->ctx, (uint32_t)ph, reinterpret_cast<const uint64_t*>(challenges.data()), src_buf.data()))
+      if (src->fill(src->ctx, (uint32_t)ph, reinterpret_cast<const uint64_t*>(challenges.data()), src_buf))
         return fail(H2G_ERR_ARG, "create_proof: witness source failed at phase " + std::to_string(ph));
-      from = src_buf.data();
+      from = src_buf;
       from_dev = false;
     }
     for (int c : cols)
@@ -998,7 +1005,6 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       Fr* rows = adv_blind.data() + (size_t)c * (bf + 1);
       for (int i = 0; i <= bf; i++) rows[i] = rng.random_fr();
       HIPCHK(hipMemcpyAsync(pk.adv[c] + unusable, rows, (size_t)(bf + 1) * sizeof(Fr), hipMemcpyHostToDevice, st));
-      if (src) std::memcpy(src_buf.data() + 4 * (n * c + unusable), rows, (size_t)(bf + 1) * sizeof(Fr));
     }
     for (int c : cols)
       if (!pk.unblinded[c]) (void)rng.random_fr();  // commitment blinds (unused by KZG)
@@ -2167,6 +2173,7 @@ int h2g_pk_free(uint64_t pk) {
   (void)hipStreamSynchronize(d->stream);
   domain_release(&it->second->dom);
   if (it->second->lk_cnt) (void)hipHostFree(it->second->lk_cnt);
+  if (it->second->wit_pin) (void)hipHostFree(it->second->wit_pin);
   if (it->second->lk_or_h) (void)hipHostFree(it->second->lk_or_h);
   if (it->second->lk_or_d) (void)hipFree(it->second->lk_or_d);
   g_pks.erase(it);
