@@ -27,7 +27,14 @@ CASES = {
     "lookup_k11": lambda: hc.lookup_circuit(11, seed=8),
     "keccak_k12": lambda: hc.keccak_style(12, words=16, seed=9),
     "c3_k14": lambda: hc.synthetic_c3(14, h2g.DeviceOps, seed=4),
+    "challenge_k9": lambda: hc.challenge_circuit(9, seed=9, extended=True),  # phases: witness source
 }
+
+
+def _prove(pk, case, **kw):
+    if len(case) == 3:  # (circuit, instance witness, fill): Prover::commit_phase per phase
+        return pk.create_proof_phased(case[2], case[1], **kw)[0]
+    return pk.create_proof(case[1], **kw)
 
 
 def main():
@@ -47,17 +54,18 @@ def main():
     h2g.init([dev])
     results = {}
     for name in args.cases:
-        circ, wit = CASES[name]()
+        case = CASES[name]()
+        circ = case[0]
         params = h2g.Params(circ.k, s=np.asarray(hc.fr_to_limbs(0x5eed + circ.k), dtype=np.uint64))
         P = 1 << circ.k
         if rank == 0:
             pk = h2g.ProvingKey(params, circ)
-            want = [pk.create_proof(wit), pk.create_proof(wit, seed=bytes(range(32)), vanishing_threads=3)]
+            want = [_prove(pk, case), _prove(pk, case, seed=bytes(range(32)), vanishing_threads=3)]
             params.set_slab(*D.slab(P, world, 0))
             cl = D.SlabClient(dist, points=P)
             cl.install()
             try:
-                got = [pk.create_proof(wit), pk.create_proof(wit, seed=bytes(range(32)), vanishing_threads=3)]
+                got = [_prove(pk, case), _prove(pk, case, seed=bytes(range(32)), vanishing_threads=3)]
             finally:
                 D.SlabClient.uninstall()
                 cl.stop()

@@ -35,7 +35,7 @@ def _run(world, cases):
 
 
 def test_sharded_proof_two_ranks():
-    cases = ["simple_k6", "mixed_k10", "lookup_k11", "keccak_k12", "c3_k14"]
+    cases = ["simple_k6", "mixed_k10", "lookup_k11", "keccak_k12", "c3_k14", "challenge_k9"]
     res = _run(2, cases)
     for nm in cases:
         assert res[nm]["same"], nm
