@@ -227,6 +227,10 @@ int h2g_pk_read(uint64_t params, const h2g_circuit* circuit, const uint8_t* buf,
                 uint64_t* pk);
 /* degree, blinding_factors, extended_k, #perm sets, #advice/#fixed/#instance queries */
 int h2g_pk_info(uint64_t pk, int32_t info[8]);
+/* the verifying key's commitments: VerifyingKey::fixed_commitments() (plonk.rs:228-231) and
+ * the permutation VerifyingKey's commitments (plonk/permutation.rs:18-47), G1Affine (8 u64 each):
+ * fixed[num_fixed], perm[num_perm_columns]; either may be NULL */
+int h2g_pk_vk_commitments(uint64_t pk, uint64_t* fixed, uint64_t* perm);
 /* the multi-open argument h2g_create_proof ends with -- the reference's Prover type
  * parameter of create_proof (halo2_proofs/src/plonk/prover.rs:19-36): 0 ProverSHPLONK
  * (default; poly/kzg/multiopen/shplonk/prover.rs:121-305), 1 ProverGWC
@@ -244,9 +248,14 @@ int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int a
  *   fill(ctx, p, challenges, advice)
  * with the challenges squeezed so far (num_challenges x 4 u64 Montgomery limbs; those of
  * phases >= p are zero) and the host advice buffer (num_advice x n Fr), in which the
- * callback writes the columns of phase p (pinned staging owned by the key; the prover reads
- * only phase p's columns from it, other rows/columns may hold anything).  Nonzero from fill
- * fails the proof with H2G_ERR_ARG.  h2g_create_proof is the same prover with every phase read from
+ * callback writes the columns of phase p (staging owned by the key, pinned when the host
+ * allows: num_advice x n x 32 B for the key's lifetime; the prover reads only phase p's
+ * columns from it, other columns may hold anything).  fill must write rows
+ * [0, n - blinding_factors - 1) of every phase-p column; the prover zeroes the unusable rows
+ * of unblinded columns before calling it (blinded ones receive randomness).  Nonzero from
+ * fill fails the proof with H2G_ERR_ARG.  Callbacks (fill, and the shard transport's
+ * launch / collect) run on the calling thread with the library lock held: they must not
+ * wait on h2g calls made from other threads.  h2g_create_proof is the same prover with every phase read from
  * `advice` (a witness that was computed with the challenges already known). */
 typedef struct {
   void* ctx;
@@ -257,7 +266,11 @@ int h2g_create_proof_phased(uint64_t params, uint64_t pk, const h2g_witness_sour
                             uint32_t vanishing_threads, uint8_t* proof, size_t proof_cap, size_t* proof_len);
 /* the challenges of the last proof (num_challenges x 4 u64), *count = num_challenges */
 int h2g_last_challenges(uint64_t* out, int max, int* count);
-/* wall milliseconds of the stages of the last h2g_create_proof (names: h2g_prover_stage_name) */
+/* wall milliseconds of the stages of the last h2g_create_proof (names: h2g_prover_stage_name).
+ * Stages end when their work is queued, unless h2g_prover_stage_sync(1) is set: then each
+ * stage boundary synchronises the prover stream and the times are GPU completion times
+ * (diagnostics only -- it serialises the pipeline) */
+int h2g_prover_stage_sync(int on);
 int h2g_prover_stages(double* ms, int max, int* count);
 const char* h2g_prover_stage_name(int i);
 

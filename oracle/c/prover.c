@@ -222,8 +222,15 @@ static fe rotate_omega(const domain_t *d, const fe *x, int rot) {
     fe p = fr_pow_u64(&w, (uint64_t)(rot >= 0 ? rot : -rot)), r;
     fr_mul(&r, x, &p); return r;
 }
+/* CPU-baseline mode: 0 = MSM/FFT use the prover's thread count ("all cores");
+ * t > 0 = MSM/FFT on t threads while parallelize-style loops keep the prover's count -- 1
+ * is the "faithful" mode of a halo2curves build without its multicore feature */
+static int g_kernel_threads = 0;
+void or_set_kernel_threads(int t) { g_kernel_threads = t > 0 ? t : 0; }
+static int kt(int threads) { return g_kernel_threads ? g_kernel_threads : threads; }
+
 static void lagrange_to_coeff_d(const domain_t *d, fe *a, int threads) {
-    or_fft((uint64_t *)a, d->k, d->omega_inv.v, threads);
+    or_fft((uint64_t *)a, d->k, d->omega_inv.v, kt(threads));
     ifft_scale(a, d->n, &d->ifft_divisor);
 }
 static void coeff_to_extended_d(const domain_t *d, const fe *in, fe *out, int threads) {
@@ -231,10 +238,10 @@ static void coeff_to_extended_d(const domain_t *d, const fe *in, fe *out, int th
     memcpy(out, in, d->n * sizeof(fe));
     distribute_powers_zeta(d, out, d->n, 1);
     memset(out + d->n, 0, (ext - d->n) * sizeof(fe));
-    or_fft((uint64_t *)out, d->extended_k, d->extended_omega.v, threads);
+    or_fft((uint64_t *)out, d->extended_k, d->extended_omega.v, kt(threads));
 }
 static int commit_msm(const fe *scalars, uint64_t n, const uint64_t *bases, int threads, g1a *out) {
-    or_msm_best((const uint64_t *)scalars, bases, n, threads, (uint64_t *)out);
+    or_msm_best((const uint64_t *)scalars, bases, n, kt(threads), (uint64_t *)out);
     return 0;
 }
 /* lagrange_interpolate (arithmetic.rs:177-230): coefficients of the unique poly of
@@ -875,7 +882,7 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
     {
         for (uint64_t i = 0; i < ext; i++) fr_mul(&h[i], &h[i], &D.t_evaluations[i % D.t_len]);
         fe *hc = fr_alloc(n * npieces);
-        or_extended_to_coeff((uint64_t *)h, (uint64_t *)hc, (uint32_t)degree, k, threads);
+        or_extended_to_coeff((uint64_t *)h, (uint64_t *)hc, (uint32_t)degree, k, kt(threads));
         for (int p = 0; p < npieces; p++) { pieces[p] = fr_alloc(n); memcpy(pieces[p], hc + n * p, n * 32); }
         free(hc);
         for (int p = 0; p < npieces; p++) { fe b; fr_random(&rng, &b); }

@@ -201,9 +201,21 @@ class Msm:
 
 
 # ----------------------------------------------------------------------------- verify
-def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen="shplonk"):
+def affine_from_limbs(a):
+    """G1Affine in the halo2curves layout (8 u64 Montgomery limbs; identity = zeros) ->
+    (x, y) ints or None"""
+    from bn254_ref import from_limbs, from_mont
+    a = [int(v) for v in a]
+    if not any(a):
+        return None
+    return (from_mont(from_limbs(a[:4]), P), from_mont(from_limbs(a[4:8]), P))
+
+
+def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen="shplonk", vk=None):
     """Returns True iff the proof verifies (raises VerifyError on malformed input).
-    multiopen: "shplonk" (VerifierSHPLONK) or "gwc" (VerifierGWC)."""
+    multiopen: "shplonk" (VerifierSHPLONK) or "gwc" (VerifierGWC).
+    vk: optional (fixed commitments, permutation commitments) -- each a list of (x, y) ints
+    or 8-limb affine arrays -- taken instead of recomputing [f(s)]G here (large k)."""
     from h2g_circuit import fr_from_limbs
     adv_q, fix_q, ins_q = circ.queries()
     degree = circ.degree()
@@ -214,19 +226,27 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen=
     nsets = (len(circ.perm_columns) + chunk_len - 1) // chunk_len
 
     # vk: fixed and permutation commitments, [f(s)]G
-    L = lagrange_at(dom, s)
+    if vk is not None:
+        def pt(c):
+            return c if c is None or isinstance(c, tuple) else affine_from_limbs(c)
+        fixed_cm = [pt(c) for c in vk[0]]
+        sigma_cm = [pt(c) for c in vk[1]]
+        if len(fixed_cm) != circ.num_fixed or len(sigma_cm) != len(circ.perm_columns):
+            raise VerifyError("verifying key does not match the circuit")
+    else:
+        L = lagrange_at(dom, s)
 
-    def commit_lagrange(vals):
-        acc = 0
-        for v, l in zip(vals, L):
-            if v:
-                acc = (acc + v * l) % R
-        return g1_mul(G1_GEN, acc)
+        def commit_lagrange(vals):
+            acc = 0
+            for v, l in zip(vals, L):
+                if v:
+                    acc = (acc + v * l) % R
+            return g1_mul(G1_GEN, acc)
 
-    fixed_vals = [[fr_from_limbs(r) for r in col] for col in circ.fixed_values]
-    fixed_cm = [commit_lagrange(v) for v in fixed_vals]
-    sig = sigma_values(circ, dom)
-    sigma_cm = [commit_lagrange(v) for v in sig]
+        fixed_vals = [[fr_from_limbs(r) for r in col] for col in circ.fixed_values]
+        fixed_cm = [commit_lagrange(v) for v in fixed_vals]
+        sig = sigma_values(circ, dom)
+        sigma_cm = [commit_lagrange(v) for v in sig]
 
     T = Blake2bRead(proof)
     T.common_scalar(fr_from_limbs(circ.transcript_repr()))

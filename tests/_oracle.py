@@ -70,6 +70,7 @@ def lib():
             "or_blake2b": ([ctypes.c_char_p, u64, ctypes.c_char_p, ctypes.c_char_p], None),
             "or_chacha20_block": ([ctypes.c_char_p, u64, ctypes.c_char_p], None),
             "or_fr_random_stream": ([ctypes.c_char_p, u64, U64P], None),
+            "or_set_kernel_threads": ([i32], None),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -349,3 +350,29 @@ class OracleOps:
     @staticmethod
     def prefix_product(a):
         return prefix_product(np.ascontiguousarray(a))
+
+
+def commit_lagrange_at_s(values, s_int, degree, k, threads=8):
+    """[f(s)]G for a Lagrange-form column f (ParamsKZG::commit_lagrange against an SRS whose
+    secret s is known): the column's coefficients by the oracle's iNTT, Horner at s, one
+    scalar multiplication -- independent of any SRS array.  -> (x, y) ints or None."""
+    import h2g_circuit as hc
+    from bn254_ref import G1_GEN, g1_mul
+
+    coeff = lagrange_to_coeff(np.ascontiguousarray(values, dtype=np.uint64), degree, k, threads)
+    e = eval_poly(coeff, np.asarray(hc.fr_to_limbs(s_int), dtype=np.uint64))
+    return g1_mul(G1_GEN, hc.fr_from_limbs(e))
+
+
+def vk_commitments(circ, wit, s_int, srs_g, srs_gl, threads=8):
+    """The verifying key's (fixed, permutation) commitments computed on the CPU: sigma
+    columns from the oracle keygen (C restatement of permutation/keygen.rs), fixed
+    columns from the circuit, each committed as [f(s)]G."""
+    kg = Keygen(circ, wit, srs_g, srs_gl, threads=threads)
+    try:
+        d, k = circ.degree(), circ.k
+        fixed = [commit_lagrange_at_s(circ.fixed_values[i], s_int, d, k, threads) for i in range(circ.num_fixed)]
+        sigma = [commit_lagrange_at_s(kg.sigma(i), s_int, d, k, threads) for i in range(len(circ.perm_columns))]
+    finally:
+        kg.close()
+    return fixed, sigma

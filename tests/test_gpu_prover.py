@@ -209,3 +209,31 @@ def test_phased_witness_failure_is_an_error():
     s, g, gl, _ = _params(circ.k)
     assert pk.create_proof_phased(fill, wit)[0] == O.create_proof(circ, wit, g, gl, fill=fill, challenges_out=ch)
     pk.close()
+
+
+def test_witness_source_writing_usable_rows_only():
+    """h2g_create_proof_phased's staging outlives proofs: a witness source that writes only
+    the usable rows gets the reference's zero tail in its unblinded column (prover.rs:
+    417-421), not what an earlier proof left there."""
+    k = 7
+    circ, wit, fill = hc.challenge_circuit(k, seed=3, extended=True)
+    s, g, gl, params = _params(circ.k)
+    usable = circ.usable_rows()
+    rng = np.random.default_rng(0)
+
+    def poison(phase, ch):  # full-length columns with garbage in the unusable rows
+        out = {c: v.copy() for c, v in fill(phase, ch).items()}
+        for v in out.values():
+            v[usable:] = hc.random_mont(rng, circ.n - usable)
+        return out
+
+    def usable_only(phase, ch):
+        return {c: v[:usable] for c, v in fill(phase, ch).items()}
+
+    ch = []
+    want = O.create_proof(circ, wit, g, gl, fill=fill, challenges_out=ch)
+    pk = h2g.ProvingKey(params, circ)
+    pk.create_proof_phased(poison, wit)
+    assert pk.create_proof_phased(usable_only, wit)[0] == want
+    assert pk.create_proof_phased(usable_only, wit)[0] == want
+    pk.close()

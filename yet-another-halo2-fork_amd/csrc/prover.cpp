@@ -120,7 +120,8 @@ struct ProvingKey {
   int multiopen = 0;
   std::vector<Fr*> gwc_q;
   uint32_t* lk_cnt = nullptr;  // pinned per-lookup match counters (3 per lookup)
-  uint64_t* wit_pin = nullptr;  // pinned advice staging of the witness source (num_advice x n Fr)
+  uint64_t* wit_pin = nullptr;  // advice staging of the witness source (num_advice x n Fr), pinned if possible
+  bool wit_pin_pinned = false;
   size_t lk_cnt_len = 0;
   // permute_expression_pair's sort, chosen per lookup from the value width lk_hb[l] (bit
   // length of the largest canonical value) seen by the previous proof: <= 64 bits: radix
@@ -176,6 +177,7 @@ struct ProvingKey {
 std::map<uint64_t, std::unique_ptr<Params>> g_params;
 std::map<uint64_t, std::unique_ptr<ProvingKey>> g_pks;
 std::vector<std::pair<const char*, double>> g_stages;
+bool g_stage_sync = false;  // h2g_prover_stage_sync: stage times = GPU completion times
 
 // ------------------------------------------------------------------ host field helpers
 int fr_cmp(const Fr& a, const Fr& b) {  // Ord on Fr: canonical numeric order
@@ -948,7 +950,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   const size_t n = pk.n, ext = pk.ext;
   const int bf = pk.bf;
   const Domain& D = pk.dom;
-  StageClock clk(st, false);
+  StageClock clk(st, g_stage_sync);
   ChaChaRng rng(seed);
   Transcript tr(proof);
   auto write_point = [&](const G1Affine& p) -> int {
@@ -976,8 +978,17 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   // pinned allocation of this size costs far more than the copies it speeds up)
   uint64_t* src_buf = nullptr;
   if (src) {
-    if (!pk.wit_pin)
-      HIPCHK(hipHostMalloc((void**)&pk.wit_pin, (size_t)std::max(pk.A, 1) * n * sizeof(Fr), hipHostMallocDefault));
+    if (!pk.wit_pin) {
+      const size_t bytes = (size_t)std::max(pk.A, 1) * n * sizeof(Fr);
+      if (hipHostMalloc((void**)&pk.wit_pin, bytes, hipHostMallocDefault) == hipSuccess) {
+        pk.wit_pin_pinned = true;
+      } else {  // pageable fallback: slower uploads, same bytes
+        (void)hipGetLastError();
+        pk.wit_pin = static_cast<uint64_t*>(std::malloc(bytes));
+        pk.wit_pin_pinned = false;
+        if (!pk.wit_pin) return fail(H2G_ERR_NOMEM, "create_proof: witness staging allocation failed");
+      }
+    }
     src_buf = pk.wit_pin;  // only the committed phase's columns are read from it
   }
   const int NC = (int)pk.ch_phase.size();
@@ -992,6 +1003,10 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     bool from_dev = adv_dev;
     if (src) {
       if (ph > 0) HIPCHK(hipStreamSynchronize(st));  // the previous phase's uploads read src_buf
+      // the staging outlives proofs: the unusable rows of unblinded columns start at zero
+      // as the reference requires (prover.rs:417-421), whatever an earlier proof left there
+      for (int c : cols)
+        if (pk.unblinded[c]) std::memset(src_buf + 4 * (n * c + unusable), 0, (n - unusable) * sizeof(Fr));
       if (src->fill(src->ctx, (uint32_t)ph, reinterpret_cast<const uint64_t*>(challenges.data()), src_buf))
         return fail(H2G_ERR_ARG, "create_proof: witness source failed at phase " + std::to_string(ph));
       from = src_buf;
@@ -2056,13 +2071,7 @@ int h2g_pk_write(uint64_t pk_h, int format, uint8_t* out, size_t cap, size_t* le
   ProvingKey& pk = *it->second;
   auto pit = g_params.find(pk.params);
   if (pit == g_params.end()) return fail(H2G_ERR_HANDLE, "pk_write: the key's params were freed");
-  if (pk.vk_fixed.size() != (size_t)pk.F || pk.vk_perm.size() != (size_t)pk.P) {  // commit_lagrange
-    std::vector<G1Affine> f(pk.F), q(pk.P);
-    for (int i = 0; i < pk.F; i++) RCCHK(commit(d, *pit->second, pk.fixed_lag[i], pk.n, SRS_LAGRANGE, &f[i], d->stream));
-    for (int i = 0; i < pk.P; i++) RCCHK(commit(d, *pit->second, pk.sigma_lag[i], pk.n, SRS_LAGRANGE, &q[i], d->stream));
-    pk.vk_fixed = f;
-    pk.vk_perm = q;
-  }
+  RCCHK(h2g_pk_vk_commitments(pk_h, nullptr, nullptr));  // commit_lagrange, once
   HIPCHK(hipStreamSynchronize(d->stream));
   ByteWriter w{out, out ? cap : 0};
   w.u8(PK_VERSION);
@@ -2173,10 +2182,35 @@ int h2g_pk_free(uint64_t pk) {
   (void)hipStreamSynchronize(d->stream);
   domain_release(&it->second->dom);
   if (it->second->lk_cnt) (void)hipHostFree(it->second->lk_cnt);
-  if (it->second->wit_pin) (void)hipHostFree(it->second->wit_pin);
+  if (it->second->wit_pin) {
+    if (it->second->wit_pin_pinned) (void)hipHostFree(it->second->wit_pin);
+    else std::free(it->second->wit_pin);
+  }
   if (it->second->lk_or_h) (void)hipHostFree(it->second->lk_or_h);
   if (it->second->lk_or_d) (void)hipFree(it->second->lk_or_d);
   g_pks.erase(it);
+  return H2G_OK;
+}
+
+/* VerifyingKey::fixed_commitments() (plonk.rs:228-231) and the permutation VerifyingKey's
+ * commitments (plonk/permutation.rs:18-47): commit_lagrange of the fixed and sigma columns
+ * (keygen.rs, permutation/keygen.rs:269), computed once */
+int h2g_pk_vk_commitments(uint64_t pk_h, uint64_t* fixed, uint64_t* perm) {
+  NEED_DEV_P();
+  auto it = g_pks.find(pk_h);
+  if (it == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
+  ProvingKey& pk = *it->second;
+  auto pit = g_params.find(pk.params);
+  if (pit == g_params.end()) return fail(H2G_ERR_HANDLE, "pk_vk_commitments: the key's params were freed");
+  if (pk.vk_fixed.size() != (size_t)pk.F || pk.vk_perm.size() != (size_t)pk.P) {
+    std::vector<G1Affine> f(pk.F), q(pk.P);
+    for (int i = 0; i < pk.F; i++) RCCHK(commit(d, *pit->second, pk.fixed_lag[i], pk.n, SRS_LAGRANGE, &f[i], d->stream));
+    for (int i = 0; i < pk.P; i++) RCCHK(commit(d, *pit->second, pk.sigma_lag[i], pk.n, SRS_LAGRANGE, &q[i], d->stream));
+    pk.vk_fixed = f;
+    pk.vk_perm = q;
+  }
+  if (fixed && pk.F) std::memcpy(fixed, pk.vk_fixed.data(), pk.vk_fixed.size() * sizeof(G1Affine));
+  if (perm && pk.P) std::memcpy(perm, pk.vk_perm.data(), pk.vk_perm.size() * sizeof(G1Affine));
   return H2G_OK;
 }
 
@@ -2255,6 +2289,7 @@ int h2g_create_proof_phased(uint64_t params, uint64_t pk, const h2g_witness_sour
 }
 
 int h2g_last_challenges(uint64_t* out, int max, int* count) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (!count) return fail(H2G_ERR_ARG, "last_challenges: null count");
   *count = (int)g_last_challenges.size();
   if (out)
@@ -2263,6 +2298,7 @@ int h2g_last_challenges(uint64_t* out, int max, int* count) {
 }
 
 int h2g_set_shard_transport(const h2g_shard_transport* t) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (t && t->world > 1) {
     if (!t->launch || !t->collect || t->world > 4096) return fail(H2G_ERR_ARG, "set_shard_transport: bad transport");
     g_shard = *t;
@@ -2307,6 +2343,12 @@ int h2g_params_msm_dev(uint64_t params, int32_t base_set, uint64_t offset, uint6
   const MsmFixedBase& tb = prm.tables(base_set, offset, n, &toff);
   RCCHK(msm_fixed_host_impl(d, d_scalars, tb, toff, n, out_affine, &id, d->stream));
   if (out_is_identity) *out_is_identity = id;
+  return H2G_OK;
+}
+
+int h2g_prover_stage_sync(int on) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  g_stage_sync = on != 0;
   return H2G_OK;
 }
 

@@ -91,6 +91,7 @@ _SIGS = {
     "h2g_keygen": ([U64, VP, ctypes.POINTER(U64)], I32),
     "h2g_pk_free": ([U64], I32),
     "h2g_pk_info": ([U64, ctypes.POINTER(ctypes.c_int32)], I32),
+    "h2g_pk_vk_commitments": ([U64, U64P, U64P], I32),
     "h2g_pk_set_multiopen": ([U64, I32], I32),
     "h2g_create_proof": ([U64, U64, VP, I32, U64P, ctypes.POINTER(U32), ctypes.c_char_p, U32, ctypes.c_char_p, SZ,
                           ctypes.POINTER(SZ)], I32),
@@ -99,6 +100,7 @@ _SIGS = {
     "h2g_last_challenges": ([U64P, I32, ctypes.POINTER(I32)], I32),
     "h2g_prover_stages": ([ctypes.POINTER(ctypes.c_double), I32, ctypes.POINTER(I32)], I32),
     "h2g_prover_stage_name": ([I32], ctypes.c_char_p),
+    "h2g_prover_stage_sync": ([I32], I32),
     "h2g_set_shard_transport": ([VP], I32),
     "h2g_params_set_slab": ([U64, U64, U64], I32),
     "h2g_params_msm_dev": ([U64, ctypes.c_int32, U64, U64, VP, U64P, ctypes.POINTER(ctypes.c_int32)], I32),
@@ -449,7 +451,8 @@ class WitnessSource(ctypes.Structure):
 
 def witness_fill(num_advice, n, fn):
     """Wraps fn(phase, challenges: list[int] (canonical, 0 for later phases)) -> {column:
-    n x 4 Montgomery array} as a WITNESS_FILL callback (Prover::commit_phase's witness)."""
+    m x 4 Montgomery array, m <= n (rows [0, m) are written: at least the usable rows)} as a
+    WITNESS_FILL callback (Prover::commit_phase's witness)."""
     import h2g_circuit as hc
 
     def cb(_ctx, phase, ch_p, adv_p):
@@ -458,7 +461,7 @@ def witness_fill(num_advice, n, fn):
             ch = np.ctypeslib.as_array(ch_p, shape=(max(nch, 1), 4))[:nch] if nch else np.zeros((0, 4), np.uint64)
             adv = np.ctypeslib.as_array(adv_p, shape=(num_advice, n, 4))
             for col, vals in fn(int(phase), hc.mont_to_ints(ch)).items():
-                adv[col] = vals
+                adv[col, : len(vals)] = vals  # a prefix of rows: the usable ones at least
             return 0
         except Exception:  # noqa: BLE001 -- reported to the prover as a failed witness
             import traceback
@@ -575,6 +578,14 @@ class ProvingKey:
         check(lib().h2g_pk_info(self.handle, info))
         (self.degree, self.bf, self.extended_k, self.nsets, self.n_adv_q, self.n_fix_q, self.n_ins_q,
          self.n_slots) = list(info)
+
+    def vk_commitments(self):
+        """(fixed commitments, permutation commitments): uint64 arrays (F, 8), (P, 8) affine
+        Montgomery (VerifyingKey::fixed_commitments, the permutation VerifyingKey)"""
+        f = np.zeros((max(self.circ.num_fixed, 1), 8), dtype=np.uint64)
+        p = np.zeros((max(len(self.circ.perm_columns), 1), 8), dtype=np.uint64)
+        check(lib().h2g_pk_vk_commitments(self.handle, p64(f), p64(p)))
+        return f[: self.circ.num_fixed], p[: len(self.circ.perm_columns)]
 
     def write(self, fmt=RAW_BYTES):
         """ProvingKey::write (plonk.rs:311-321) -> bytes"""
@@ -717,6 +728,11 @@ def memcpy_dtoh(h_dst, d_src, nbytes):
 
 def memcpy_htod(d_dst, h_src, nbytes):
     check(lib().h2g_memcpy_htod(VP(d_dst), VP(h_src), nbytes))
+
+
+def prover_stage_sync(on=True):
+    """stage boundaries synchronise the prover stream (GPU completion times; diagnostics)"""
+    check(lib().h2g_prover_stage_sync(1 if on else 0))
 
 
 def prover_stages():
