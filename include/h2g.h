@@ -264,6 +264,46 @@ typedef struct {
 int h2g_create_proof_phased(uint64_t params, uint64_t pk, const h2g_witness_source* witness,
                             const uint64_t* instance, const uint32_t* instance_lens, const uint8_t rng_seed[32],
                             uint32_t vanishing_threads, uint8_t* proof, size_t proof_cap, size_t* proof_len);
+/* ---- create_proof with the reference's full argument list ------------------------
+ * create_proof(params, pk, circuits: &[C], instances: &[&[&[F]]], rng: R: RngCore,
+ * transcript) (halo2_proofs/src/plonk/prover.rs:19-36; Prover::new_with_engine /
+ * commit_phase / create_proof, halo2_backend/src/plonk/prover.rs:174-899): several
+ * circuits of one key in one proof, in the reference's interleaving -- instances per
+ * circuit, each phase's advice commitments circuit by circuit, then per circuit its
+ * lookups, permutation sets, lookup products and shuffles, one vanishing argument and one
+ * h(X) over all circuits (evaluation.rs:365-620), evaluations and queries circuit by
+ * circuit before the fixed and common ones.
+ * rng: the caller's `R: RngCore`, drawn in the reference's order.  Two kinds
+ * of draw exist: F::random(&mut rng) (blinding rows and blinds) and rng.fill_bytes(&mut
+ * [u8; 32]) (the vanishing argument's ChaCha20 seeds, vanishing/prover.rs:69-73).
+ *   random_fr : F::random(&mut rng) as 4 Montgomery limbs (the Rust shim calls
+ *               Fr::random itself, so the proof does not depend on how halo2curves
+ *               consumes the RNG); NULL = fill_bytes(64) read as from_uniform_bytes
+ *   fill_bytes: RngCore::fill_bytes(out[0..len])
+ * Nonzero from either fails the proof with H2G_ERR_ARG. */
+typedef struct {
+  void* ctx;
+  int (*fill_bytes)(void* ctx, uint8_t* out, size_t len);
+  int (*random_fr)(void* ctx, uint64_t out[4]);
+} h2g_rng;
+/* Prover::commit_phase's witness per circuit: like h2g_witness_source.fill, for circuit c */
+typedef struct {
+  void* ctx;
+  int (*fill)(void* ctx, uint32_t circuit, uint32_t phase, const uint64_t* challenges, uint64_t* advice);
+} h2g_witness_source_multi;
+typedef struct {
+  uint32_t num_circuits;                /* >= 1 */
+  const uint64_t* const* advice;        /* [num_circuits] num_advice x n Fr, or NULL with `witness` */
+  int advice_on_device;                 /* advice[c] are device pointers */
+  const h2g_witness_source_multi* witness;
+  const uint64_t* const* instance;      /* [num_circuits] num_instance x n Fr (zero padded) */
+  const uint32_t* const* instance_lens; /* [num_circuits] num_instance values each */
+  const h2g_rng* rng;                   /* NULL: ChaCha20Rng::from_seed(rng_seed) */
+  const uint8_t* rng_seed;
+  uint32_t vanishing_threads;
+} h2g_prove_inputs;
+int h2g_create_proof_multi(uint64_t params, uint64_t pk, const h2g_prove_inputs* in, uint8_t* proof,
+                           size_t proof_cap, size_t* proof_len);
 /* the challenges of the last proof (num_challenges x 4 u64), *count = num_challenges */
 int h2g_last_challenges(uint64_t* out, int max, int* count);
 /* wall milliseconds of the stages of the last h2g_create_proof (names: h2g_prover_stage_name).

@@ -21,9 +21,9 @@
  *   Blake2bWrite transcript            halo2_backend/src/transcript.rs:120-130,353-419,500-539
  *   lookup argument                    halo2_backend/src/plonk/lookup/prover.rs:64-494
  *   shuffle argument                   halo2_backend/src/plonk/shuffle/prover.rs:36-255
- * Scope: advice (one phase), fixed, instance columns, custom gates (expression
- * graphs with rotations), the permutation, lookup and shuffle arguments.
- * Challenges (multi-phase advice) are not restated.
+ * Scope: several circuits per proof, advice phases and challenges, fixed and instance
+ * columns, custom gates (expression graphs with rotations), the permutation, lookup and
+ * shuffle arguments; the prover rng is ChaCha20Rng::from_seed or the caller's RngCore.
  * Unverifiable-here details (isolated): G1 compressed encoding (x LE, bit 7 of byte 31
  * = y odd); vk.transcript_repr is taken as an input (plonk.rs:189-200 hashes the Rust
  * Debug text of the pinned VK).
@@ -77,6 +77,20 @@ typedef struct {
     void *fill_ctx;
     uint64_t *challenges_out;       /* num_challenges x 4 (may be NULL) */
     const uint64_t *challenge_values; /* set by or_prove: the squeezed challenges */
+    /* several circuits of one key in one proof (create_proof's circuits: &[C] and
+     * instances: &[&[&[F]]], halo2_proofs/src/plonk/prover.rs:19-36); num_circuits 0 = one
+     * circuit from advice_values / instance_values / instance_lens / fill above */
+    uint32_t num_circuits;
+    const uint64_t *const *advice_c;       /* [num_circuits] num_advice x n Fr */
+    const uint64_t *const *instance_c;     /* [num_circuits] num_instance x n Fr */
+    const uint32_t *const *instance_lens_c;
+    int (*fill_multi)(void *ctx, uint32_t circuit, uint32_t phase, const uint64_t *challenges, uint64_t *advice);
+    /* the caller's `rng: R: RngCore` (NULL both = ChaCha20Rng::from_seed(rng_seed)):
+     * random_fr = F::random(rng) (Montgomery limbs; NULL = 64 fill_bytes, from_uniform_bytes),
+     * fill_bytes = RngCore::fill_bytes (the vanishing seeds) */
+    int (*rng_fill_bytes)(void *ctx, uint8_t *out, size_t len);
+    int (*rng_random_fr)(void *ctx, uint64_t *out);
+    void *rng_ctx;
 } or_spec;
 
 typedef struct { int type, index, rot; } query_t;
@@ -94,6 +108,37 @@ static void fr_random(chacha_rng *rng, fe *out) {   /* Fr::random: LE512 mod r *
     fr_mul(&t1, &lo, &fr_R2);   /* d0 * R2 * R^-1 = mont(d0) */
     fr_mul(&t2, &hi, &R3);      /* d1 * R3 * R^-1 = mont(d1 * 2^256) */
     fr_add(out, &t1, &t2);
+}
+
+/* the prover's rng: ChaCha20Rng::from_seed, or the caller's RngCore (or_spec rng_*) */
+typedef struct {
+    chacha_rng cc;
+    int (*fb)(void *, uint8_t *, size_t);
+    int (*fr)(void *, uint64_t *);
+    void *ctx;
+    int failed;
+} prng_t;
+static void prng_fill(prng_t *r, uint8_t *out, size_t len) {
+    if (!r->fb && !r->fr) { chacha_rng_fill(&r->cc, out, len); return; }
+    if (r->failed || !r->fb || r->fb(r->ctx, out, len)) { r->failed = 1; memset(out, 0, len); }
+}
+static void prng_random(prng_t *r, fe *out) {   /* F::random(&mut rng) */
+    if (r->fr) {
+        uint64_t v[4] = {0, 0, 0, 0};
+        if (r->failed || r->fr(r->ctx, v)) { r->failed = 1; memset(out, 0, sizeof(fe)); return; }
+        int below = 0;   /* an Fr must be below r */
+        for (int i = 3; i >= 0; i--) if (v[i] != fr_MOD[i]) { below = v[i] < fr_MOD[i]; break; }
+        if (!below) { r->failed = 1; memset(out, 0, sizeof(fe)); return; }
+        *out = fe_from(v);
+        return;
+    }
+    uint8_t b[64];
+    prng_fill(r, b, 64);
+    uint64_t d[8];
+    for (int i = 0; i < 8; i++) d[i] = load64le(b + 8 * i);
+    static const fe R3 = {{0x5e94d8e1b4bf0040ULL, 0x2a489cbe1cfbb6b8ULL, 0x893cc664a19fcfedULL, 0x0cf8594b7fcc657cULL}};
+    fe lo = fe_from(d), hi = fe_from(d + 4), t1, t2;
+    fr_mul(&t1, &lo, &fr_R2); fr_mul(&t2, &hi, &R3); fr_add(out, &t1, &t2);
 }
 
 static fe fr_pow_u64(const fe *a, uint64_t e) {
@@ -339,7 +384,7 @@ static int keyed_cmp(const void *a_, const void *b_) {
 /* permute_expression_pair (lookup/prover.rs:410-494): sorted input; table value = input at the
  * first row of each run, leftover table values (ascending, BTreeMap order) fill the repeated
  * rows from the last one backwards; then bf+1 random rows each (input first). */
-static int permute_pair(const fe *A, const fe *S, uint64_t n, int bf, chacha_rng *rng, fe *Ap, fe *Sp) {
+static int permute_pair(const fe *A, const fe *S, uint64_t n, int bf, prng_t *rng, fe *Ap, fe *Sp) {
     const uint64_t u = n - (uint64_t)(bf + 1);
     keyed *ia = (keyed *)malloc((u + 1) * sizeof(keyed)), *ta = (keyed *)malloc((u + 1) * sizeof(keyed));
     for (uint64_t i = 0; i < u; i++) {
@@ -370,16 +415,16 @@ static int permute_pair(const fe *A, const fe *S, uint64_t n, int bf, chacha_rng
     }
     free(ia); free(ta); free(rep); free(used);
     if (!ok) return -7;   /* Error::ConstraintSystemFailure: an input value is not in the table */
-    for (uint64_t r = u; r < n; r++) fr_random(rng, &Ap[r]);
-    for (uint64_t r = u; r < n; r++) fr_random(rng, &Sp[r]);
+    for (uint64_t r = u; r < n; r++) prng_random(rng, &Ap[r]);
+    for (uint64_t r = u; r < n; r++) prng_random(rng, &Sp[r]);
     return 0;
 }
 
 /* z = [1, prod_0, prod_0 prod_1, ...] over n - bf rows, then bf random rows */
-static void grand_product(const fe *prod, uint64_t n, int bf, chacha_rng *rng, fe *z) {
+static void grand_product(const fe *prod, uint64_t n, int bf, prng_t *rng, fe *z) {
     z[0] = fr_ONE;
     for (uint64_t i = 1; i < n - (uint64_t)bf; i++) fr_mul(&z[i], &z[i - 1], &prod[i - 1]);
-    for (uint64_t i = n - (uint64_t)bf; i < n; i++) fr_random(rng, &z[i]);
+    for (uint64_t i = n - (uint64_t)bf; i < n; i++) prng_random(rng, &z[i]);
 }
 
 /* ====================================================================== keygen */
@@ -553,8 +598,18 @@ void or_pk_info(const or_pk *pk, int32_t *out8) {
 void or_pk_sigma(const or_pk *pk, int i, uint64_t *out) { memcpy(out, pk->sigma_lag[i], pk->n * 32); }
 
 /* ====================================================================== create_proof */
-/* create_proof for one circuit (prover.rs:512-899).  The witness (advice, instance)
- * and the prover inputs (rng seed, vanishing thread count, SRS) come from `s`. */
+/* one circuit's state through create_proof (prover.rs:187-899 keep one of each per circuit:
+ * InstanceSingle, AdviceSingle, the permutation / lookup / shuffle arguments) */
+typedef struct {
+    const uint64_t *advice, *instance;
+    const uint32_t *inst_lens;
+    fe **inst_vals, **inst_polys, **adv;
+    fe **lk_A, **lk_S, **lk_Ap, **lk_Sp, **lk_Ap_poly, **lk_Sp_poly, **lk_z_poly, **sh_z_poly;
+    fe **z_poly;
+} circ_t;
+
+/* create_proof (prover.rs:174-899) over the spec's circuits.  The witnesses (advice,
+ * instance) and the prover inputs (rng, vanishing thread count, SRS) come from `s`. */
 int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proof_cap, uint64_t *proof_len, int threads) {
     if (threads < 1) threads = 1;
     or_spec s_local = *s_in;   /* + the challenge values, once squeezed */
@@ -567,52 +622,73 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
     fe *const *fixed_polys = pk->fixed_polys, *const *fixed_cosets = pk->fixed_cosets;
     fe *const *sigma_lag = pk->sigma_lag, *const *sigma_polys = pk->sigma_polys, *const *sigma_cosets = pk->sigma_cosets;
     const fe *l0 = pk->l0, *l_last = pk->l_last, *l_active = pk->l_active;
+    const int NL = (int)s->num_lookups, NS = (int)s->num_shuffles;
+    const int NC = s->num_circuits ? (int)s->num_circuits : 1;
+    circ_t *C = (circ_t *)calloc(NC, sizeof(circ_t));
+    for (int ci = 0; ci < NC; ci++) {
+        C[ci].advice = s->num_circuits ? s->advice_c[ci] : s->advice_values;
+        C[ci].instance = s->num_circuits ? (s->instance_c ? s->instance_c[ci] : NULL) : s->instance_values;
+        C[ci].inst_lens = s->num_circuits ? (s->instance_lens_c ? s->instance_lens_c[ci] : NULL) : s->instance_lens;
+    }
 
-    chacha_rng rng; chacha_rng_init(&rng, s->rng_seed);
+    prng_t rng = {0};
+    chacha_rng_init(&rng.cc, s->rng_seed ? s->rng_seed : (const uint8_t *)"\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0");
+    rng.fb = s->rng_fill_bytes; rng.fr = s->rng_random_fr; rng.ctx = s->rng_ctx;
     transcript_t T; tr_init(&T, proof, proof_cap);
     { fe tr = fe_from(s->transcript_repr); tr_common_scalar(&T, &tr); }       /* vk.hash_into */
-    /* instances (prover.rs:196-271; KZG: QUERY_INSTANCE = false) */
-    fe **inst_vals = (fe **)calloc(s->num_instance + 1, sizeof(fe *)), **inst_polys = (fe **)calloc(s->num_instance + 1, sizeof(fe *));
-    for (uint32_t i = 0; i < s->num_instance; i++) {
-        if (s->instance_lens[i] > n - (bf + 1)) return -4;   /* InstanceTooLarge */
-        inst_vals[i] = fr_alloc(n);
-        memcpy(inst_vals[i], s->instance_values + 4 * n * i, n * 32);
-        for (uint32_t r = 0; r < s->instance_lens[i]; r++) tr_common_scalar(&T, &inst_vals[i][r]);
-        inst_polys[i] = fr_alloc(n);
-        memcpy(inst_polys[i], inst_vals[i], n * 32);
-        lagrange_to_coeff_d(&D, inst_polys[i], threads);
+    /* every circuit's instances (prover.rs:187-271; KZG: QUERY_INSTANCE = false) */
+    for (int ci = 0; ci < NC; ci++) {
+        circ_t *c = &C[ci];
+        c->inst_vals = (fe **)calloc(s->num_instance + 1, sizeof(fe *));
+        c->inst_polys = (fe **)calloc(s->num_instance + 1, sizeof(fe *));
+        for (uint32_t i = 0; i < s->num_instance; i++) {
+            if (c->inst_lens[i] > n - (bf + 1)) return -4;   /* InstanceTooLarge */
+            c->inst_vals[i] = fr_alloc(n);
+            memcpy(c->inst_vals[i], c->instance + 4 * n * i, n * 32);
+            for (uint32_t r = 0; r < c->inst_lens[i]; r++) tr_common_scalar(&T, &c->inst_vals[i][r]);
+            c->inst_polys[i] = fr_alloc(n);
+            memcpy(c->inst_polys[i], c->inst_vals[i], n * 32);
+            lagrange_to_coeff_d(&D, c->inst_polys[i], threads);
+        }
     }
-    /* commit_phase per advice phase (prover.rs:309-494): the phase's blinding rows, its
-     * blinds, its commitments, then the challenges of the phase */
-    fe **adv = (fe **)calloc(s->num_advice + 1, sizeof(fe *));
+    /* commit_phase per advice phase (prover.rs:309-494), circuit by circuit: the phase's
+     * blinding rows, its blinds, its commitments; then the challenges of the phase */
     const uint64_t unusable = n - (uint64_t)(bf + 1);
     int max_phase = 0;
     for (uint32_t c = 0; c < s->num_advice; c++)
         if (s->advice_phase && s->advice_phase[c] > max_phase) max_phase = s->advice_phase[c];
     uint64_t *ch = (uint64_t *)calloc(4 * (s->num_challenges + 1), sizeof(uint64_t));
-    uint64_t *src = s->fill ? (uint64_t *)calloc(4 * n * (s->num_advice + 1), sizeof(uint64_t)) : NULL;
+    const int has_fill = s->fill || s->fill_multi;
+    uint64_t *src = has_fill ? (uint64_t *)calloc(4 * n * (s->num_advice + 1), sizeof(uint64_t)) : NULL;
+    for (int ci = 0; ci < NC; ci++) C[ci].adv = (fe **)calloc(s->num_advice + 1, sizeof(fe *));
     for (int ph = 0; ph <= max_phase; ph++) {
 #define IN_PHASE(c) ((s->advice_phase ? s->advice_phase[c] : 0) == ph)
-        const uint64_t *from = s->advice_values;
-        if (s->fill) {
-            if (s->fill(s->fill_ctx, (uint32_t)ph, ch, src)) return -7;
-            from = src;
-        }
-        for (uint32_t c = 0; c < s->num_advice; c++) {
-            if (!IN_PHASE(c)) continue;
-            adv[c] = fr_alloc(n);
-            memcpy(adv[c], from + 4 * n * c, n * 32);
-            if (s->unblinded && s->unblinded[c]) continue;
-            for (uint64_t r = unusable; r < n; r++) fr_random(&rng, &adv[c][r]);
-        }
-        for (uint32_t c = 0; c < s->num_advice; c++) {
-            if (!IN_PHASE(c) || (s->unblinded && s->unblinded[c])) continue;
-            fe blind; fr_random(&rng, &blind);
-        }
-        for (uint32_t c = 0; c < s->num_advice; c++) {
-            if (!IN_PHASE(c)) continue;
-            g1a cm; commit_msm(adv[c], n, s->srs_g_lagrange, threads, &cm);
-            if (tr_write_point(&T, &cm)) return -5;
+        for (int ci = 0; ci < NC; ci++) {
+            fe **adv = C[ci].adv;
+            const uint64_t *from = C[ci].advice;
+            if (has_fill) {
+                memset(src, 0, 4 * n * (s->num_advice + 1) * sizeof(uint64_t));
+                int rc = s->fill_multi ? s->fill_multi(s->fill_ctx, (uint32_t)ci, (uint32_t)ph, ch, src)
+                                       : s->fill(s->fill_ctx, (uint32_t)ph, ch, src);
+                if (rc) return -7;
+                from = src;
+            }
+            for (uint32_t c = 0; c < s->num_advice; c++) {
+                if (!IN_PHASE(c)) continue;
+                adv[c] = fr_alloc(n);
+                memcpy(adv[c], from + 4 * n * c, n * 32);
+                if (s->unblinded && s->unblinded[c]) continue;
+                for (uint64_t r = unusable; r < n; r++) prng_random(&rng, &adv[c][r]);
+            }
+            for (uint32_t c = 0; c < s->num_advice; c++) {
+                if (!IN_PHASE(c) || (s->unblinded && s->unblinded[c])) continue;
+                fe blind; prng_random(&rng, &blind);
+            }
+            for (uint32_t c = 0; c < s->num_advice; c++) {
+                if (!IN_PHASE(c)) continue;
+                g1a cm; commit_msm(adv[c], n, s->srs_g_lagrange, threads, &cm);
+                if (tr_write_point(&T, &cm)) return -5;
+            }
         }
         for (uint32_t i = 0; i < s->num_challenges; i++)
             if (s->challenge_phase[i] == ph) { fe v = tr_squeeze(&T); memcpy(ch + 4 * i, &v, 32); }
@@ -622,38 +698,40 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
     s_local.challenge_values = ch;
     if (s->challenges_out) memcpy(s->challenges_out, ch, 32 * s->num_challenges);
     fe theta = tr_squeeze(&T);
-    /* lookup_commit_permuted, per lookup (lookup/prover.rs:64-173) */
-    const int NL = (int)s->num_lookups, NS = (int)s->num_shuffles;
+    /* lookup_commit_permuted, per circuit, per lookup (lookup/prover.rs:64-173) */
     fe **fix_lag = (fe **)calloc(s->num_fixed + 1, sizeof(fe *));
     for (uint32_t i = 0; i < s->num_fixed; i++) fix_lag[i] = (fe *)(s->fixed_values + 4 * n * i);
-    fe **lk_A = (fe **)calloc(NL + 1, sizeof(fe *)), **lk_S = (fe **)calloc(NL + 1, sizeof(fe *));
-    fe **lk_Ap = (fe **)calloc(NL + 1, sizeof(fe *)), **lk_Sp = (fe **)calloc(NL + 1, sizeof(fe *));
-    fe **lk_Ap_poly = (fe **)calloc(NL + 1, sizeof(fe *)), **lk_Sp_poly = (fe **)calloc(NL + 1, sizeof(fe *));
-    fe **lk_z_poly = (fe **)calloc(NL + 1, sizeof(fe *)), **sh_z_poly = (fe **)calloc(NS + 1, sizeof(fe *));
-    {
+    for (int ci = 0; ci < NC; ci++) {
+        circ_t *c = &C[ci];
+        c->lk_A = (fe **)calloc(NL + 1, sizeof(fe *)); c->lk_S = (fe **)calloc(NL + 1, sizeof(fe *));
+        c->lk_Ap = (fe **)calloc(NL + 1, sizeof(fe *)); c->lk_Sp = (fe **)calloc(NL + 1, sizeof(fe *));
+        c->lk_Ap_poly = (fe **)calloc(NL + 1, sizeof(fe *)); c->lk_Sp_poly = (fe **)calloc(NL + 1, sizeof(fe *));
+        c->lk_z_poly = (fe **)calloc(NL + 1, sizeof(fe *)); c->sh_z_poly = (fe **)calloc(NS + 1, sizeof(fe *));
         const int32_t *r = s->lookup_roots;
         for (int l = 0; l < NL; l++) {
             const int m = (int)s->lookup_sizes[l];
-            lk_A[l] = fr_alloc(n); lk_S[l] = fr_alloc(n); lk_Ap[l] = fr_alloc(n); lk_Sp[l] = fr_alloc(n);
-            compress_lagrange(s, r, m, adv, fix_lag, inst_vals, n, &theta, lk_A[l], threads);
-            compress_lagrange(s, r + m, m, adv, fix_lag, inst_vals, n, &theta, lk_S[l], threads);
-            if (permute_pair(lk_A[l], lk_S[l], n, bf, &rng, lk_Ap[l], lk_Sp[l])) return -7;
-            fe b1, b2; fr_random(&rng, &b1); fr_random(&rng, &b2);
+            c->lk_A[l] = fr_alloc(n); c->lk_S[l] = fr_alloc(n); c->lk_Ap[l] = fr_alloc(n); c->lk_Sp[l] = fr_alloc(n);
+            compress_lagrange(s, r, m, c->adv, fix_lag, c->inst_vals, n, &theta, c->lk_A[l], threads);
+            compress_lagrange(s, r + m, m, c->adv, fix_lag, c->inst_vals, n, &theta, c->lk_S[l], threads);
+            if (permute_pair(c->lk_A[l], c->lk_S[l], n, bf, &rng, c->lk_Ap[l], c->lk_Sp[l])) return -7;
+            fe b1, b2; prng_random(&rng, &b1); prng_random(&rng, &b2);
             g1a c1, c2;
-            commit_msm(lk_Ap[l], n, s->srs_g_lagrange, threads, &c1);
-            commit_msm(lk_Sp[l], n, s->srs_g_lagrange, threads, &c2);
-            lk_Ap_poly[l] = fr_alloc(n); memcpy(lk_Ap_poly[l], lk_Ap[l], n * 32); lagrange_to_coeff_d(&D, lk_Ap_poly[l], threads);
-            lk_Sp_poly[l] = fr_alloc(n); memcpy(lk_Sp_poly[l], lk_Sp[l], n * 32); lagrange_to_coeff_d(&D, lk_Sp_poly[l], threads);
+            commit_msm(c->lk_Ap[l], n, s->srs_g_lagrange, threads, &c1);
+            commit_msm(c->lk_Sp[l], n, s->srs_g_lagrange, threads, &c2);
+            c->lk_Ap_poly[l] = fr_alloc(n); memcpy(c->lk_Ap_poly[l], c->lk_Ap[l], n * 32); lagrange_to_coeff_d(&D, c->lk_Ap_poly[l], threads);
+            c->lk_Sp_poly[l] = fr_alloc(n); memcpy(c->lk_Sp_poly[l], c->lk_Sp[l], n * 32); lagrange_to_coeff_d(&D, c->lk_Sp_poly[l], threads);
             if (tr_write_point(&T, &c1) || tr_write_point(&T, &c2)) return -5;
             r += 2 * m;
         }
     }
     fe beta = tr_squeeze(&T), gamma = tr_squeeze(&T);
-    /* permutation_commit (permutation/prover.rs:50-197) */
+    /* permutation_commit per circuit (permutation/prover.rs:50-197) */
     const int chunk_len = degree - 2;
     const int nsets = (P + chunk_len - 1) / chunk_len;
-    fe **z_poly = (fe **)calloc(nsets + 1, sizeof(fe *)), **z_coset = (fe **)calloc(nsets + 1, sizeof(fe *));
-    {
+    for (int ci = 0; ci < NC; ci++) {
+        circ_t *cc = &C[ci];
+        fe **adv = cc->adv;
+        cc->z_poly = (fe **)calloc(nsets + 1, sizeof(fe *));
         fe deltaomega = fr_ONE, last_z = fr_ONE;
         fe *mod = fr_alloc(n);
         for (int st = 0; st < nsets; st++) {
@@ -661,7 +739,7 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
             for (uint64_t r = 0; r < n; r++) mod[r] = fr_ONE;
             for (int c = c0; c < c1; c++) {
                 int t = s->perm_columns[2 * c], idx = s->perm_columns[2 * c + 1];
-                fe *vals = t == COL_ADVICE ? adv[idx] : (t == COL_FIXED ? (fe *)(s->fixed_values + 4 * n * idx) : inst_vals[idx]);
+                fe *vals = t == COL_ADVICE ? adv[idx] : (t == COL_FIXED ? (fe *)(s->fixed_values + 4 * n * idx) : cc->inst_vals[idx]);
 #pragma omp parallel for num_threads(threads) schedule(static)
                 for (uint64_t r = 0; r < n; r++) {
                     fe a, b; fr_mul(&a, &beta, &sigma_lag[c][r]); fr_add(&a, &a, &gamma); fr_add(&b, &a, &vals[r]);
@@ -671,7 +749,7 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
             or_fr_batch_invert((uint64_t *)mod, n);
             for (int c = c0; c < c1; c++) {
                 int t = s->perm_columns[2 * c], idx = s->perm_columns[2 * c + 1];
-                fe *vals = t == COL_ADVICE ? adv[idx] : (t == COL_FIXED ? (fe *)(s->fixed_values + 4 * n * idx) : inst_vals[idx]);
+                fe *vals = t == COL_ADVICE ? adv[idx] : (t == COL_FIXED ? (fe *)(s->fixed_values + 4 * n * idx) : cc->inst_vals[idx]);
                 fe dw = deltaomega;
                 for (uint64_t r = 0; r < n; r++) {
                     fe a, b; fr_mul(&a, &dw, &beta); fr_add(&a, &a, &gamma); fr_add(&b, &a, &vals[r]);
@@ -683,59 +761,64 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
             fe *z = fr_alloc(n);
             z[0] = last_z;
             for (uint64_t r = 1; r < n; r++) fr_mul(&z[r], &z[r - 1], &mod[r - 1]);
-            for (uint64_t r = n - bf; r < n; r++) fr_random(&rng, &z[r]);
+            for (uint64_t r = n - bf; r < n; r++) prng_random(&rng, &z[r]);
             last_z = z[n - (bf + 1)];
-            fe blind; fr_random(&rng, &blind);
+            fe blind; prng_random(&rng, &blind);
             g1a cm; commit_msm(z, n, s->srs_g_lagrange, threads, &cm);
             lagrange_to_coeff_d(&D, z, threads);
-            z_poly[st] = z;
-            z_coset[st] = fr_alloc(ext);
-            coeff_to_extended_d(&D, z, z_coset[st], threads);
+            cc->z_poly[st] = z;
             if (tr_write_point(&T, &cm)) return -5;
         }
         free(mod);
     }
-    /* lookup products (lookup/prover.rs:182-325), then shuffle products (shuffle/prover.rs:97-206) */
+    /* lookup products, every circuit's (lookup/prover.rs:182-325), then shuffle products
+     * (shuffle/prover.rs:97-206) */
     {
         fe *prod = fr_alloc(n);
-        for (int l = 0; l < NL; l++) {
+        for (int ci = 0; ci < NC; ci++) {
+            circ_t *c = &C[ci];
+            for (int l = 0; l < NL; l++) {
 #pragma omp parallel for num_threads(threads) schedule(static)
-            for (uint64_t i = 0; i < n; i++) {
-                fe a, b; fr_add(&a, &beta, &lk_Ap[l][i]); fr_add(&b, &gamma, &lk_Sp[l][i]); fr_mul(&prod[i], &a, &b);
-            }
-            or_fr_batch_invert((uint64_t *)prod, n);
+                for (uint64_t i = 0; i < n; i++) {
+                    fe a, b; fr_add(&a, &beta, &c->lk_Ap[l][i]); fr_add(&b, &gamma, &c->lk_Sp[l][i]); fr_mul(&prod[i], &a, &b);
+                }
+                or_fr_batch_invert((uint64_t *)prod, n);
 #pragma omp parallel for num_threads(threads) schedule(static)
-            for (uint64_t i = 0; i < n; i++) {
-                fe a, b; fr_add(&a, &lk_A[l][i], &beta); fr_add(&b, &lk_S[l][i], &gamma);
-                fr_mul(&prod[i], &prod[i], &a); fr_mul(&prod[i], &prod[i], &b);
+                for (uint64_t i = 0; i < n; i++) {
+                    fe a, b; fr_add(&a, &c->lk_A[l][i], &beta); fr_add(&b, &c->lk_S[l][i], &gamma);
+                    fr_mul(&prod[i], &prod[i], &a); fr_mul(&prod[i], &prod[i], &b);
+                }
+                fe *z = fr_alloc(n);
+                grand_product(prod, n, bf, &rng, z);
+                fe blind; prng_random(&rng, &blind);
+                g1a cm; commit_msm(z, n, s->srs_g_lagrange, threads, &cm);
+                lagrange_to_coeff_d(&D, z, threads);
+                c->lk_z_poly[l] = z;
+                if (tr_write_point(&T, &cm)) return -5;
             }
-            fe *z = fr_alloc(n);
-            grand_product(prod, n, bf, &rng, z);
-            fe blind; fr_random(&rng, &blind);
-            g1a cm; commit_msm(z, n, s->srs_g_lagrange, threads, &cm);
-            lagrange_to_coeff_d(&D, z, threads);
-            lk_z_poly[l] = z;
-            if (tr_write_point(&T, &cm)) return -5;
         }
-        const int32_t *r = s->shuffle_roots;
-        fe *ci = fr_alloc(n), *cs = fr_alloc(n);
-        for (int l = 0; l < NS; l++) {
-            const int m = (int)s->shuffle_sizes[l];
-            compress_lagrange(s, r, m, adv, fix_lag, inst_vals, n, &theta, ci, threads);
-            compress_lagrange(s, r + m, m, adv, fix_lag, inst_vals, n, &theta, cs, threads);
-            for (uint64_t i = 0; i < n; i++) fr_add(&prod[i], &gamma, &cs[i]);
-            or_fr_batch_invert((uint64_t *)prod, n);
-            for (uint64_t i = 0; i < n; i++) { fe a; fr_add(&a, &gamma, &ci[i]); fr_mul(&prod[i], &prod[i], &a); }
-            fe *z = fr_alloc(n);
-            grand_product(prod, n, bf, &rng, z);
-            fe blind; fr_random(&rng, &blind);
-            g1a cm; commit_msm(z, n, s->srs_g_lagrange, threads, &cm);
-            lagrange_to_coeff_d(&D, z, threads);
-            sh_z_poly[l] = z;
-            if (tr_write_point(&T, &cm)) return -5;
-            r += 2 * m;
+        fe *ci_ = fr_alloc(n), *cs_ = fr_alloc(n);
+        for (int ci = 0; ci < NC; ci++) {
+            circ_t *c = &C[ci];
+            const int32_t *r = s->shuffle_roots;
+            for (int l = 0; l < NS; l++) {
+                const int m = (int)s->shuffle_sizes[l];
+                compress_lagrange(s, r, m, c->adv, fix_lag, c->inst_vals, n, &theta, ci_, threads);
+                compress_lagrange(s, r + m, m, c->adv, fix_lag, c->inst_vals, n, &theta, cs_, threads);
+                for (uint64_t i = 0; i < n; i++) fr_add(&prod[i], &gamma, &cs_[i]);
+                or_fr_batch_invert((uint64_t *)prod, n);
+                for (uint64_t i = 0; i < n; i++) { fe a; fr_add(&a, &gamma, &ci_[i]); fr_mul(&prod[i], &prod[i], &a); }
+                fe *z = fr_alloc(n);
+                grand_product(prod, n, bf, &rng, z);
+                fe blind; prng_random(&rng, &blind);
+                g1a cm; commit_msm(z, n, s->srs_g_lagrange, threads, &cm);
+                lagrange_to_coeff_d(&D, z, threads);
+                c->sh_z_poly[l] = z;
+                if (tr_write_point(&T, &cm)) return -5;
+                r += 2 * m;
+            }
         }
-        free(prod); free(ci); free(cs);
+        free(prod); free(ci_); free(cs_);
     }
     /* vanishing::Argument::commit (vanishing/prover.rs:40-98) */
     fe *random_poly = fr_alloc(n);
@@ -746,7 +829,7 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
         for (uint64_t i = 0; i < rem && noff < nt; i++) off[noff++] = i * (chunk + 1);
         if (chunk) for (uint64_t o = rem * (chunk + 1); noff < nt; o += chunk) off[noff++] = o;
         uint8_t (*seeds)[32] = (uint8_t (*)[32])calloc(noff + 1, 32);
-        for (uint64_t i = 0; i < noff; i++) chacha_rng_fill(&rng, seeds[i], 32);
+        for (uint64_t i = 0; i < noff; i++) prng_fill(&rng, seeds[i], 32);
         for (uint64_t i = 0; i < noff; i++) {
             uint64_t lo = off[i], hi = i + 1 < noff ? off[i + 1] : n;
             chacha_rng cr; chacha_rng_init(&cr, seeds[i]);
@@ -754,34 +837,39 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
         }
         free(off); free(seeds);
     }
-    fe random_blind; fr_random(&rng, &random_blind); (void)random_blind;
+    fe random_blind; prng_random(&rng, &random_blind); (void)random_blind;
     {
         g1a cm; commit_msm(random_poly, n, s->srs_g, threads, &cm);
         if (tr_write_point(&T, &cm)) return -5;
     }
     /* advice to coefficient form */
-    for (uint32_t c = 0; c < s->num_advice; c++) lagrange_to_coeff_d(&D, adv[c], threads);
+    for (int ci = 0; ci < NC; ci++)
+        for (uint32_t c = 0; c < s->num_advice; c++) lagrange_to_coeff_d(&D, C[ci].adv[c], threads);
     fe y = tr_squeeze(&T);
-    /* evaluate_h (evaluation.rs:317-483) */
+    /* evaluate_h (evaluation.rs:317-620): circuit by circuit, each continuing the Horner
+     * chain in y of the circuits before it (evaluation.rs:367-373) */
     fe *h = fr_alloc(ext);
-    {
+    for (int ci = 0; ci < NC; ci++) {
+        circ_t *cc = &C[ci];
         fe **adv_c = (fe **)calloc(s->num_advice + 1, sizeof(fe *)), **ins_c = (fe **)calloc(s->num_instance + 1, sizeof(fe *));
-        for (uint32_t c = 0; c < s->num_advice; c++) { adv_c[c] = fr_alloc(ext); coeff_to_extended_d(&D, adv[c], adv_c[c], threads); }
-        for (uint32_t c = 0; c < s->num_instance; c++) { ins_c[c] = fr_alloc(ext); coeff_to_extended_d(&D, inst_polys[c], ins_c[c], threads); }
+        for (uint32_t c = 0; c < s->num_advice; c++) { adv_c[c] = fr_alloc(ext); coeff_to_extended_d(&D, cc->adv[c], adv_c[c], threads); }
+        for (uint32_t c = 0; c < s->num_instance; c++) { ins_c[c] = fr_alloc(ext); coeff_to_extended_d(&D, cc->inst_polys[c], ins_c[c], threads); }
+        fe **z_coset = (fe **)calloc(nsets + 1, sizeof(fe *));
+        for (int st = 0; st < nsets; st++) { z_coset[st] = fr_alloc(ext); coeff_to_extended_d(&D, cc->z_poly[st], z_coset[st], threads); }
         fe **lk_zc = (fe **)calloc(NL + 1, sizeof(fe *)), **lk_Apc = (fe **)calloc(NL + 1, sizeof(fe *));
         fe **lk_Spc = (fe **)calloc(NL + 1, sizeof(fe *)), **sh_zc = (fe **)calloc(NS + 1, sizeof(fe *));
         for (int l = 0; l < NL; l++) {
-            lk_zc[l] = fr_alloc(ext); coeff_to_extended_d(&D, lk_z_poly[l], lk_zc[l], threads);
-            lk_Apc[l] = fr_alloc(ext); coeff_to_extended_d(&D, lk_Ap_poly[l], lk_Apc[l], threads);
-            lk_Spc[l] = fr_alloc(ext); coeff_to_extended_d(&D, lk_Sp_poly[l], lk_Spc[l], threads);
+            lk_zc[l] = fr_alloc(ext); coeff_to_extended_d(&D, cc->lk_z_poly[l], lk_zc[l], threads);
+            lk_Apc[l] = fr_alloc(ext); coeff_to_extended_d(&D, cc->lk_Ap_poly[l], lk_Apc[l], threads);
+            lk_Spc[l] = fr_alloc(ext); coeff_to_extended_d(&D, cc->lk_Sp_poly[l], lk_Spc[l], threads);
         }
-        for (int l = 0; l < NS; l++) { sh_zc[l] = fr_alloc(ext); coeff_to_extended_d(&D, sh_z_poly[l], sh_zc[l], threads); }
+        for (int l = 0; l < NS; l++) { sh_zc[l] = fr_alloc(ext); coeff_to_extended_d(&D, cc->sh_z_poly[l], sh_zc[l], threads); }
         const fe delta_start_beta = beta;   /* delta_start = beta * ZETA */
         fe delta_start; fr_mul(&delta_start, &delta_start_beta, &FR_ZETA);
         const int last_rot = -(bf + 1);
 #pragma omp parallel for num_threads(threads) schedule(static)
         for (uint64_t idx = 0; idx < ext; idx++) {
-            fe v = {{0, 0, 0, 0}};
+            fe v = h[idx];
             for (uint32_t g = 0; g < s->num_gates; g++) {
                 fe gv = eval_node(s, s->gate_roots[g], adv_c, fixed_cosets, ins_c, idx, rot_scale, ext);
                 fr_mul(&v, &v, &y); fr_add(&v, &v, &gv);
@@ -871,7 +959,8 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
         }
         for (int l = 0; l < NL; l++) { free(lk_zc[l]); free(lk_Apc[l]); free(lk_Spc[l]); }
         for (int l = 0; l < NS; l++) free(sh_zc[l]);
-        free(lk_zc); free(lk_Apc); free(lk_Spc); free(sh_zc);
+        for (int st = 0; st < nsets; st++) free(z_coset[st]);
+        free(lk_zc); free(lk_Apc); free(lk_Spc); free(sh_zc); free(z_coset);
         for (uint32_t c = 0; c < s->num_advice; c++) free(adv_c[c]);
         for (uint32_t c = 0; c < s->num_instance; c++) free(ins_c[c]);
         free(adv_c); free(ins_c);
@@ -885,20 +974,25 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
         or_extended_to_coeff((uint64_t *)h, (uint64_t *)hc, (uint32_t)degree, k, kt(threads));
         for (int p = 0; p < npieces; p++) { pieces[p] = fr_alloc(n); memcpy(pieces[p], hc + n * p, n * 32); }
         free(hc);
-        for (int p = 0; p < npieces; p++) { fe b; fr_random(&rng, &b); }
+        for (int p = 0; p < npieces; p++) { fe b; prng_random(&rng, &b); }
         for (int p = 0; p < npieces; p++) {
             g1a cm; commit_msm(pieces[p], n, s->srs_g, threads, &cm);
             if (tr_write_point(&T, &cm)) return -5;
         }
     }
     free(h);
+    if (rng.failed) return -8;   /* the caller's RNG failed */
     fe x = tr_squeeze(&T);
     fe xn = fr_pow_u64(&x, n);
-    /* evaluations (prover.rs:735-836) */
-    for (int i = 0; i < adv_q.n; i++) {
-        fe pt = rotate_omega(&D, &x, adv_q.q[i].rot), e = eval_poly(adv[adv_q.q[i].index], n, &pt);
-        tr_write_scalar(&T, &e);
-    }
+    const fe x_next = rotate_omega(&D, &x, 1), x_last = rotate_omega(&D, &x, -(bf + 1));
+    const fe x_prev = rotate_omega(&D, &x, -1);
+    /* evaluations (prover.rs:735-836): every circuit's advice, fixed, vanishing, common
+     * permutation, then every circuit's permutation, lookups, shuffles */
+    for (int ci = 0; ci < NC; ci++)
+        for (int i = 0; i < adv_q.n; i++) {
+            fe pt = rotate_omega(&D, &x, adv_q.q[i].rot), e = eval_poly(C[ci].adv[adv_q.q[i].index], n, &pt);
+            tr_write_scalar(&T, &e);
+        }
     for (int i = 0; i < fix_q.n; i++) {
         fe pt = rotate_omega(&D, &x, fix_q.q[i].rot), e = eval_poly(fixed_polys[fix_q.q[i].index], n, &pt);
         tr_write_scalar(&T, &e);
@@ -908,57 +1002,70 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
         for (uint64_t i = 0; i < n; i++) { fe t; fr_mul(&t, &h_poly[i], &xn); fr_add(&h_poly[i], &t, &pieces[p][i]); }
     { fe e = eval_poly(random_poly, n, &x); tr_write_scalar(&T, &e); }
     for (int c = 0; c < P; c++) { fe e = eval_poly(sigma_polys[c], n, &x); tr_write_scalar(&T, &e); }
-    const fe x_next = rotate_omega(&D, &x, 1), x_last = rotate_omega(&D, &x, -(bf + 1));
-    for (int st = 0; st < nsets; st++) {
-        fe e0 = eval_poly(z_poly[st], n, &x), e1 = eval_poly(z_poly[st], n, &x_next);
-        tr_write_scalar(&T, &e0); tr_write_scalar(&T, &e1);
-        if (st + 1 < nsets) { fe e2 = eval_poly(z_poly[st], n, &x_last); tr_write_scalar(&T, &e2); }
-    }
-    const fe x_prev = rotate_omega(&D, &x, -1);
-    for (int l = 0; l < NL; l++) {   /* lookup/prover.rs:330-361 */
-        fe e[5] = {eval_poly(lk_z_poly[l], n, &x), eval_poly(lk_z_poly[l], n, &x_next), eval_poly(lk_Ap_poly[l], n, &x),
-                   eval_poly(lk_Ap_poly[l], n, &x_prev), eval_poly(lk_Sp_poly[l], n, &x)};
-        for (int i = 0; i < 5; i++) tr_write_scalar(&T, &e[i]);
-    }
-    for (int l = 0; l < NS; l++) {   /* shuffle/prover.rs:210-231 */
-        fe e0 = eval_poly(sh_z_poly[l], n, &x), e1 = eval_poly(sh_z_poly[l], n, &x_next);
-        tr_write_scalar(&T, &e0); tr_write_scalar(&T, &e1);
-    }
-    /* queries (prover.rs:840-889) -- poly ids: advice c -> c, fixed c -> A+c, sigma c -> A+F+c,
-       z st -> A+F+P+st, h -> ..+nsets, random -> ..+1 */
+    for (int ci = 0; ci < NC; ci++)
+        for (int st = 0; st < nsets; st++) {
+            fe *zp = C[ci].z_poly[st];
+            fe e0 = eval_poly(zp, n, &x), e1 = eval_poly(zp, n, &x_next);
+            tr_write_scalar(&T, &e0); tr_write_scalar(&T, &e1);
+            if (st + 1 < nsets) { fe e2 = eval_poly(zp, n, &x_last); tr_write_scalar(&T, &e2); }
+        }
+    for (int ci = 0; ci < NC; ci++)
+        for (int l = 0; l < NL; l++) {   /* lookup/prover.rs:330-361 */
+            circ_t *c = &C[ci];
+            fe e[5] = {eval_poly(c->lk_z_poly[l], n, &x), eval_poly(c->lk_z_poly[l], n, &x_next), eval_poly(c->lk_Ap_poly[l], n, &x),
+                       eval_poly(c->lk_Ap_poly[l], n, &x_prev), eval_poly(c->lk_Sp_poly[l], n, &x)};
+            for (int i = 0; i < 5; i++) tr_write_scalar(&T, &e[i]);
+        }
+    for (int ci = 0; ci < NC; ci++)
+        for (int l = 0; l < NS; l++) {   /* shuffle/prover.rs:210-231 */
+            fe e0 = eval_poly(C[ci].sh_z_poly[l], n, &x), e1 = eval_poly(C[ci].sh_z_poly[l], n, &x_next);
+            tr_write_scalar(&T, &e0); tr_write_scalar(&T, &e1);
+        }
+    /* queries (prover.rs:840-889) -- poly ids: per circuit ci (base ci * per_c) advice c,
+       z st, lookup l (z, A', S'), shuffle l; then fixed, sigma, h, random */
     const int A_ = (int)s->num_advice, F_ = (int)s->num_fixed;
-    const int id_lk = A_ + F_ + P + nsets, id_sh = id_lk + 3 * NL;   /* lookup l: z, A', S' */
-    const int id_h = id_sh + NS, id_r = id_h + 1, npolys = id_r + 1;
+    const int per_c = A_ + nsets + 3 * NL + NS;
+    const int id_fix = NC * per_c, id_sig = id_fix + F_, id_h = id_sig + P, id_r = id_h + 1, npolys = id_r + 1;
     fe **polys = (fe **)calloc(npolys, sizeof(fe *));
-    for (int c = 0; c < A_; c++) polys[c] = adv[c];
-    for (int c = 0; c < F_; c++) polys[A_ + c] = fixed_polys[c];
-    for (int c = 0; c < P; c++) polys[A_ + F_ + c] = sigma_polys[c];
-    for (int st = 0; st < nsets; st++) polys[A_ + F_ + P + st] = z_poly[st];
-    for (int l = 0; l < NL; l++) { polys[id_lk + 3 * l] = lk_z_poly[l]; polys[id_lk + 3 * l + 1] = lk_Ap_poly[l]; polys[id_lk + 3 * l + 2] = lk_Sp_poly[l]; }
-    for (int l = 0; l < NS; l++) polys[id_sh + l] = sh_z_poly[l];
+    for (int ci = 0; ci < NC; ci++) {
+        const int b = ci * per_c;
+        for (int c = 0; c < A_; c++) polys[b + c] = C[ci].adv[c];
+        for (int st = 0; st < nsets; st++) polys[b + A_ + st] = C[ci].z_poly[st];
+        for (int l = 0; l < NL; l++) {
+            polys[b + A_ + nsets + 3 * l] = C[ci].lk_z_poly[l];
+            polys[b + A_ + nsets + 3 * l + 1] = C[ci].lk_Ap_poly[l];
+            polys[b + A_ + nsets + 3 * l + 2] = C[ci].lk_Sp_poly[l];
+        }
+        for (int l = 0; l < NS; l++) polys[b + A_ + nsets + 3 * NL + l] = C[ci].sh_z_poly[l];
+    }
+    for (int c = 0; c < F_; c++) polys[id_fix + c] = fixed_polys[c];
+    for (int c = 0; c < P; c++) polys[id_sig + c] = sigma_polys[c];
     polys[id_h] = h_poly; polys[id_r] = random_poly;
-    int nq = 0, qcap = adv_q.n + fix_q.n + 3 * nsets + P + 2 + 5 * NL + 2 * NS;
+    int nq = 0, qcap = NC * (adv_q.n + 3 * nsets + 5 * NL + 2 * NS) + fix_q.n + P + 2;
     query_ref *Q = (query_ref *)calloc(qcap, sizeof(query_ref));
-    for (int i = 0; i < adv_q.n; i++) { Q[nq].point = rotate_omega(&D, &x, adv_q.q[i].rot); Q[nq++].poly_id = adv_q.q[i].index; }
-    for (int st = 0; st < nsets; st++) {
-        Q[nq].point = x; Q[nq++].poly_id = A_ + F_ + P + st;
-        Q[nq].point = x_next; Q[nq++].poly_id = A_ + F_ + P + st;
+    for (int ci = 0; ci < NC; ci++) {
+        const int b = ci * per_c, id_z = b + A_, id_lk = b + A_ + nsets, id_sh = id_lk + 3 * NL;
+        for (int i = 0; i < adv_q.n; i++) { Q[nq].point = rotate_omega(&D, &x, adv_q.q[i].rot); Q[nq++].poly_id = b + adv_q.q[i].index; }
+        for (int st = 0; st < nsets; st++) {
+            Q[nq].point = x; Q[nq++].poly_id = id_z + st;
+            Q[nq].point = x_next; Q[nq++].poly_id = id_z + st;
+        }
+        for (int st = nsets - 2; st >= 0; st--) { Q[nq].point = x_last; Q[nq++].poly_id = id_z + st; }
+        for (int l = 0; l < NL; l++) {   /* lookup/prover.rs:364-405 */
+            const int zi = id_lk + 3 * l;
+            Q[nq].point = x; Q[nq++].poly_id = zi;
+            Q[nq].point = x; Q[nq++].poly_id = zi + 1;
+            Q[nq].point = x; Q[nq++].poly_id = zi + 2;
+            Q[nq].point = x_prev; Q[nq++].poly_id = zi + 1;
+            Q[nq].point = x_next; Q[nq++].poly_id = zi;
+        }
+        for (int l = 0; l < NS; l++) {   /* shuffle/prover.rs:234-254 */
+            Q[nq].point = x; Q[nq++].poly_id = id_sh + l;
+            Q[nq].point = x_next; Q[nq++].poly_id = id_sh + l;
+        }
     }
-    for (int st = nsets - 2; st >= 0; st--) { Q[nq].point = x_last; Q[nq++].poly_id = A_ + F_ + P + st; }
-    for (int l = 0; l < NL; l++) {   /* lookup/prover.rs:364-405 */
-        const int zi = id_lk + 3 * l;
-        Q[nq].point = x; Q[nq++].poly_id = zi;
-        Q[nq].point = x; Q[nq++].poly_id = zi + 1;
-        Q[nq].point = x; Q[nq++].poly_id = zi + 2;
-        Q[nq].point = x_prev; Q[nq++].poly_id = zi + 1;
-        Q[nq].point = x_next; Q[nq++].poly_id = zi;
-    }
-    for (int l = 0; l < NS; l++) {   /* shuffle/prover.rs:234-254 */
-        Q[nq].point = x; Q[nq++].poly_id = id_sh + l;
-        Q[nq].point = x_next; Q[nq++].poly_id = id_sh + l;
-    }
-    for (int i = 0; i < fix_q.n; i++) { Q[nq].point = rotate_omega(&D, &x, fix_q.q[i].rot); Q[nq++].poly_id = A_ + fix_q.q[i].index; }
-    for (int c = 0; c < P; c++) { Q[nq].point = x; Q[nq++].poly_id = A_ + F_ + c; }
+    for (int i = 0; i < fix_q.n; i++) { Q[nq].point = rotate_omega(&D, &x, fix_q.q[i].rot); Q[nq++].poly_id = id_fix + fix_q.q[i].index; }
+    for (int c = 0; c < P; c++) { Q[nq].point = x; Q[nq++].poly_id = id_sig + c; }
     Q[nq].point = x; Q[nq++].poly_id = id_h;
     Q[nq].point = x; Q[nq++].poly_id = id_r;
 

@@ -211,11 +211,14 @@ def affine_from_limbs(a):
     return (from_mont(from_limbs(a[:4]), P), from_mont(from_limbs(a[4:8]), P))
 
 
-def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen="shplonk", vk=None):
+def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen="shplonk", vk=None,
+           instances_multi=None):
     """Returns True iff the proof verifies (raises VerifyError on malformed input).
     multiopen: "shplonk" (VerifierSHPLONK) or "gwc" (VerifierGWC).
     vk: optional (fixed commitments, permutation commitments) -- each a list of (x, y) ints
-    or 8-limb affine arrays -- taken instead of recomputing [f(s)]G here (large k)."""
+    or 8-limb affine arrays -- taken instead of recomputing [f(s)]G here (large k).
+    instances_multi: per-circuit instance columns of a proof over several circuits
+    (verify_proof's instances: &[&[&[F]]], verifier.rs:58-140); `instances` is then unused."""
     from h2g_circuit import fr_from_limbs
     adv_q, fix_q, ins_q = circ.queries()
     degree = circ.degree()
@@ -224,6 +227,8 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen=
     n = circ.n
     chunk_len = degree - 2
     nsets = (len(circ.perm_columns) + chunk_len - 1) // chunk_len
+    insts = instances_multi if instances_multi is not None else [instances]
+    NC = len(insts)
 
     # vk: fixed and permutation commitments, [f(s)]G
     if vk is not None:
@@ -250,26 +255,29 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen=
 
     T = Blake2bRead(proof)
     T.common_scalar(fr_from_limbs(circ.transcript_repr()))
-    for col in instances:
-        for v in col:
-            T.common_scalar(v)
-    # advice commitments per phase, each phase followed by its challenges (verifier.rs:104-140)
-    adv_cm = [None] * circ.num_advice
+    for inst in insts:
+        for col in inst:
+            for v in col:
+                T.common_scalar(v)
+    # advice commitments per phase, circuit by circuit, each phase followed by its
+    # challenges (verifier.rs:104-140)
+    adv_cm = [[None] * circ.num_advice for _ in range(NC)]
     chal = [0] * circ.num_challenges
     for ph in range(circ.max_phase + 1):
-        for col in range(circ.num_advice):
-            if int(circ.advice_phase[col]) == ph:
-                adv_cm[col] = T.read_point()
+        for c in range(NC):
+            for col in range(circ.num_advice):
+                if int(circ.advice_phase[col]) == ph:
+                    adv_cm[c][col] = T.read_point()
         for i in range(circ.num_challenges):
             if int(circ.challenge_phase[i]) == ph:
                 chal[i] = T.squeeze()
     theta = T.squeeze()
-    lk_perm_cm = [(T.read_point(), T.read_point()) for _ in circ.lookups]   # A', S'
+    lk_perm_cm = [[(T.read_point(), T.read_point()) for _ in circ.lookups] for _ in range(NC)]   # A', S'
     beta = T.squeeze()
     gamma = T.squeeze()
-    perm_cm = [T.read_point() for _ in range(nsets)]
-    lk_z_cm = [T.read_point() for _ in circ.lookups]
-    sh_z_cm = [T.read_point() for _ in circ.shuffles]
+    perm_cm = [[T.read_point() for _ in range(nsets)] for _ in range(NC)]
+    lk_z_cm = [[T.read_point() for _ in circ.lookups] for _ in range(NC)]
+    sh_z_cm = [[T.read_point() for _ in circ.shuffles] for _ in range(NC)]
     random_cm = T.read_point()
     y = T.squeeze()
     h_cm = [T.read_point() for _ in range(dom.quotient_poly_degree)]
@@ -278,75 +286,83 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen=
     # instance evals (QUERY_INSTANCE = false): inner product with l_i_range
     rots = [r for (_, r) in ins_q] or [0]
     min_rot, max_rot = min(0, min(rots)), max(0, max(rots))
-    max_len = max([len(c) for c in instances] or [0])
+    max_len = max([len(c) for inst in insts for c in inst] or [0])
     l_is = l_i_range(dom, x, xn, range(-max_rot, max_len + abs(min_rot)))
     ins_evals = []
-    for (col, rot) in ins_q:
-        off = max_rot - rot
-        vals = instances[col]
-        ins_evals.append(sum(v * l for v, l in zip(vals, l_is[off:off + len(vals)])) % R)
-    adv_evals = [T.read_scalar() for _ in adv_q]
+    for inst in insts:
+        ev_c = []
+        for (col, rot) in ins_q:
+            off = max_rot - rot
+            vals = inst[col]
+            ev_c.append(sum(v * l for v, l in zip(vals, l_is[off:off + len(vals)])) % R)
+        ins_evals.append(ev_c)
+    adv_evals = [[T.read_scalar() for _ in adv_q] for _ in range(NC)]
     fix_evals = [T.read_scalar() for _ in fix_q]
     random_eval = T.read_scalar()
     perm_evals = [T.read_scalar() for _ in circ.perm_columns]
     sets = []
-    for i in range(nsets):
-        e0 = T.read_scalar()
-        e1 = T.read_scalar()
-        e2 = T.read_scalar() if i + 1 < nsets else None
-        sets.append((e0, e1, e2))
-    lk_ev = [tuple(T.read_scalar() for _ in range(5)) for _ in circ.lookups]   # z, z_next, A', A'_inv, S'
-    sh_ev = [tuple(T.read_scalar() for _ in range(2)) for _ in circ.shuffles]  # z, z_next
+    for _ in range(NC):
+        sc = []
+        for i in range(nsets):
+            e0 = T.read_scalar()
+            e1 = T.read_scalar()
+            e2 = T.read_scalar() if i + 1 < nsets else None
+            sc.append((e0, e1, e2))
+        sets.append(sc)
+    lk_ev = [[tuple(T.read_scalar() for _ in range(5)) for _ in circ.lookups] for _ in range(NC)]   # z, z_next, A', A'_inv, S'
+    sh_ev = [[tuple(T.read_scalar() for _ in range(2)) for _ in circ.shuffles] for _ in range(NC)]  # z, z_next
 
-    # vanishing argument: expressions at x
+    # vanishing argument: every circuit's expressions at x, one Horner chain in y
     l_evals = l_i_range(dom, x, xn, range(-(bf + 1), 1))
     l_last, l_blind, l_0 = l_evals[0], sum(l_evals[1:1 + bf]) % R, l_evals[1 + bf]
-
-    def qeval(t, i, r):
-        if t == ADVICE:
-            return adv_evals[adv_q.index((i, r))]
-        if t == FIXED:
-            return fix_evals[fix_q.index((i, r))]
-        return ins_evals[ins_q.index((i, r))]
-
-    exprs = [g.evaluate(lambda c: c, qeval, challenge=lambda i: chal[i]) for g in circ.gates]
-    if nsets:
-        exprs.append(l_0 * (1 - sets[0][0]) % R)
-        exprs.append((sets[-1][0] * sets[-1][0] - sets[-1][0]) * l_last % R)
-        for i in range(1, nsets):
-            exprs.append((sets[i][0] - sets[i - 1][2]) * l_0 % R)
-        for ci in range(nsets):
-            cols = circ.perm_columns[ci * chunk_len:(ci + 1) * chunk_len]
-            pev = perm_evals[ci * chunk_len:(ci + 1) * chunk_len]
-            left = sets[ci][1]
-            for (t, i), pe in zip(cols, pev):
-                left = left * (qeval(t, i, 0) + beta * pe + gamma) % R
-            right = sets[ci][0]
-            cur = beta * x % R * pow(DELTA, ci * chunk_len, R) % R
-            for (t, i) in cols:
-                right = right * (qeval(t, i, 0) + cur + gamma) % R
-                cur = cur * DELTA % R
-            exprs.append((left - right) * (1 - (l_last + l_blind)) % R)
     active = (1 - (l_last + l_blind)) % R
+    exprs = []
+    for c in range(NC):
+        def qeval(t, i, r, c=c):
+            if t == ADVICE:
+                return adv_evals[c][adv_q.index((i, r))]
+            if t == FIXED:
+                return fix_evals[fix_q.index((i, r))]
+            return ins_evals[c][ins_q.index((i, r))]
 
-    def compress(es):
-        acc = 0
-        for e in es:
-            acc = (acc * theta + e.evaluate(lambda c: c, qeval, challenge=lambda i: chal[i])) % R
-        return acc
+        exprs += [g.evaluate(lambda v: v, qeval, challenge=lambda i: chal[i]) for g in circ.gates]
+        st = sets[c]
+        if nsets:
+            exprs.append(l_0 * (1 - st[0][0]) % R)
+            exprs.append((st[-1][0] * st[-1][0] - st[-1][0]) * l_last % R)
+            for i in range(1, nsets):
+                exprs.append((st[i][0] - st[i - 1][2]) * l_0 % R)
+            for ci in range(nsets):
+                cols = circ.perm_columns[ci * chunk_len:(ci + 1) * chunk_len]
+                pev = perm_evals[ci * chunk_len:(ci + 1) * chunk_len]
+                left = st[ci][1]
+                for (t, i), pe in zip(cols, pev):
+                    left = left * (qeval(t, i, 0) + beta * pe + gamma) % R
+                right = st[ci][0]
+                cur = beta * x % R * pow(DELTA, ci * chunk_len, R) % R
+                for (t, i) in cols:
+                    right = right * (qeval(t, i, 0) + cur + gamma) % R
+                    cur = cur * DELTA % R
+                exprs.append((left - right) * active % R)
 
-    for (ins_e, tab_e), (z, zn, ap, api, sp) in zip(circ.lookups, lk_ev):   # lookup/verifier.rs:98-160
-        exprs.append(l_0 * (1 - z) % R)
-        exprs.append(l_last * (z * z - z) % R)
-        left = zn * (ap + beta) % R * (sp + gamma) % R
-        right = z * (compress(ins_e) + beta) % R * (compress(tab_e) + gamma) % R
-        exprs.append((left - right) * active % R)
-        exprs.append(l_0 * (ap - sp) % R)
-        exprs.append((ap - sp) * (ap - api) % R * active % R)
-    for (ins_e, sh_e), (z, zn) in zip(circ.shuffles, sh_ev):   # shuffle/verifier.rs
-        exprs.append(l_0 * (1 - z) % R)
-        exprs.append(l_last * (z * z - z) % R)
-        exprs.append(active * (zn * (compress(sh_e) + gamma) - z * (compress(ins_e) + gamma)) % R)
+        def compress(es, qeval=qeval):
+            acc = 0
+            for e in es:
+                acc = (acc * theta + e.evaluate(lambda v: v, qeval, challenge=lambda i: chal[i])) % R
+            return acc
+
+        for (ins_e, tab_e), (z, zn, ap, api, sp) in zip(circ.lookups, lk_ev[c]):   # lookup/verifier.rs:98-160
+            exprs.append(l_0 * (1 - z) % R)
+            exprs.append(l_last * (z * z - z) % R)
+            left = zn * (ap + beta) % R * (sp + gamma) % R
+            right = z * (compress(ins_e) + beta) % R * (compress(tab_e) + gamma) % R
+            exprs.append((left - right) * active % R)
+            exprs.append(l_0 * (ap - sp) % R)
+            exprs.append((ap - sp) * (ap - api) % R * active % R)
+        for (ins_e, sh_e), (z, zn) in zip(circ.shuffles, sh_ev[c]):   # shuffle/verifier.rs
+            exprs.append(l_0 * (1 - z) % R)
+            exprs.append(l_last * (z * z - z) % R)
+            exprs.append(active * (zn * (compress(sh_e) + gamma) - z * (compress(ins_e) + gamma)) % R)
     h_eval = 0
     for v in exprs:
         h_eval = (h_eval * y + v) % R
@@ -356,27 +372,28 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen=
         h_msm.scale(xn)
         h_msm.add(1, c)
 
-    # queries: (key, commitment-or-msm, point, eval)
+    # queries: (key, commitment-or-msm, point, eval), circuit by circuit then the common ones
     x_next = rotate_omega(dom, x, 1)
     x_last = rotate_omega(dom, x, -(bf + 1))
-    queries = []
-    for qi, (col, rot) in enumerate(adv_q):
-        queries.append((("adv", col), adv_cm[col], rotate_omega(dom, x, rot), adv_evals[qi]))
-    for i in range(nsets):
-        queries.append((("z", i), perm_cm[i], x, sets[i][0]))
-        queries.append((("z", i), perm_cm[i], x_next, sets[i][1]))
-    for i in reversed(range(nsets - 1)):
-        queries.append((("z", i), perm_cm[i], x_last, sets[i][2]))
     x_prev = rotate_omega(dom, x, -1)
-    for l, (zc, (apc, spc), (z, zn, ap, api, sp)) in enumerate(zip(lk_z_cm, lk_perm_cm, lk_ev)):
-        queries.append((("lz", l), zc, x, z))
-        queries.append((("la", l), apc, x, ap))
-        queries.append((("ls", l), spc, x, sp))
-        queries.append((("la", l), apc, x_prev, api))
-        queries.append((("lz", l), zc, x_next, zn))
-    for l, (zc, (z, zn)) in enumerate(zip(sh_z_cm, sh_ev)):
-        queries.append((("sz", l), zc, x, z))
-        queries.append((("sz", l), zc, x_next, zn))
+    queries = []
+    for c in range(NC):
+        for qi, (col, rot) in enumerate(adv_q):
+            queries.append((("adv", c, col), adv_cm[c][col], rotate_omega(dom, x, rot), adv_evals[c][qi]))
+        for i in range(nsets):
+            queries.append((("z", c, i), perm_cm[c][i], x, sets[c][i][0]))
+            queries.append((("z", c, i), perm_cm[c][i], x_next, sets[c][i][1]))
+        for i in reversed(range(nsets - 1)):
+            queries.append((("z", c, i), perm_cm[c][i], x_last, sets[c][i][2]))
+        for l, (zc, (apc, spc), (z, zn, ap, api, sp)) in enumerate(zip(lk_z_cm[c], lk_perm_cm[c], lk_ev[c])):
+            queries.append((("lz", c, l), zc, x, z))
+            queries.append((("la", c, l), apc, x, ap))
+            queries.append((("ls", c, l), spc, x, sp))
+            queries.append((("la", c, l), apc, x_prev, api))
+            queries.append((("lz", c, l), zc, x_next, zn))
+        for l, (zc, (z, zn)) in enumerate(zip(sh_z_cm[c], sh_ev[c])):
+            queries.append((("sz", c, l), zc, x, z))
+            queries.append((("sz", c, l), zc, x_next, zn))
     for qi, (col, rot) in enumerate(fix_q):
         queries.append((("fix", col), fixed_cm[col], rotate_omega(dom, x, rot), fix_evals[qi]))
     for i in range(len(circ.perm_columns)):

@@ -232,6 +232,10 @@ class OrSpec(ctypes.Structure):
         ("advice_phase", U8P), ("num_challenges", ctypes.c_uint32), ("challenge_phase", U8P),
         ("fill", ctypes.c_void_p), ("fill_ctx", ctypes.c_void_p), ("challenges_out", U64P),
         ("challenge_values", U64P),
+        ("num_circuits", ctypes.c_uint32), ("advice_c", ctypes.POINTER(ctypes.c_void_p)),
+        ("instance_c", ctypes.POINTER(ctypes.c_void_p)), ("instance_lens_c", ctypes.POINTER(ctypes.c_void_p)),
+        ("fill_multi", ctypes.c_void_p),
+        ("rng_fill_bytes", ctypes.c_void_p), ("rng_random_fr", ctypes.c_void_p), ("rng_ctx", ctypes.c_void_p),
     ]
 
 
@@ -260,7 +264,8 @@ def make_spec(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=
                _ptr(g, U64P), _ptr(gl, U64P), _ptr(unb, U8P),
                len(circ.lookups), _ptr(lks, U32P), _ptr(lkr, I32P),
                len(circ.shuffles), _ptr(shs, U32P), _ptr(shr, I32P), MULTIOPEN[multiopen],
-               _ptr(aph, U8P), circ.num_challenges, _ptr(chph, U8P), None, None, None, None)
+               _ptr(aph, U8P), circ.num_challenges, _ptr(chph, U8P), None, None, None, None,
+               0, None, None, None, None, None, None, None)
     return s, keep
 
 
@@ -311,20 +316,47 @@ class Keygen:
 
 
 def create_proof(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=8, threads=8, keygen=None,
-                 multiopen="shplonk", fill=None, challenges_out=None):
+                 multiopen="shplonk", fill=None, challenges_out=None, wits=None, rng=None, fills=None):
     """Oracle create_proof -> proof bytes (multiopen: "shplonk" = ProverSHPLONK, "gwc" = ProverGWC).
     fill: the per-phase witness source fill(phase, challenges) -> {column: values}
-    (h2g.witness_fill); challenges_out: a list that receives the squeezed challenges."""
+    (h2g.witness_fill); challenges_out: a list that receives the squeezed challenges.
+    wits: several circuits' witnesses in one proof (create_proof's circuits: &[C]; `wit`
+    is then only used for the spec's shapes), fills: their per-circuit witness sources;
+    rng: the caller's RngCore (fill_bytes(n), optionally random_fr()) instead of the seed."""
     spec, keep = make_spec(circ, wit, srs_g, srs_gl, seed, vanishing_threads, multiopen)
     ch = np.zeros((max(circ.num_challenges, 1), 4), dtype=np.uint64)
     spec.challenges_out = _ptr(ch, U64P)
+    import h2g
     if fill is not None:
-        import h2g
         cb = h2g.witness_fill(circ.num_advice, circ.n, fill)
         cb.num_challenges = circ.num_challenges
         cfn = h2g.WITNESS_FILL(cb)
         keep.append(cfn)
         spec.fill = ctypes.cast(cfn, ctypes.c_void_p)
+    if wits is not None:
+        nc = len(wits)
+        arrs = [(ctypes.c_void_p * nc)() for _ in range(3)]
+        for c, w in enumerate(wits):
+            a = np.ascontiguousarray(w.advice, dtype=np.uint64)
+            ins = np.ascontiguousarray(w.instance, dtype=np.uint64) if circ.num_instance else np.zeros(4, np.uint64)
+            ln_ = np.ascontiguousarray(w.instance_lens if circ.num_instance else np.zeros(1), dtype=np.uint32)
+            keep += [a, ins, ln_]
+            arrs[0][c], arrs[1][c], arrs[2][c] = a.ctypes.data, ins.ctypes.data, ln_.ctypes.data
+        keep += arrs
+        spec.num_circuits = nc
+        spec.advice_c, spec.instance_c, spec.instance_lens_c = (ctypes.cast(x, ctypes.POINTER(ctypes.c_void_p))
+                                                               for x in arrs)
+    if fills is not None:
+        cbm = h2g.witness_fill_multi(circ.num_advice, circ.n, fills)
+        cbm.num_challenges = circ.num_challenges
+        cfm = h2g.WITNESS_FILL_MULTI(cbm)
+        keep += [cbm, cfm]
+        spec.fill_multi = ctypes.cast(cfm, ctypes.c_void_p)
+    if rng is not None:
+        fb, fr = h2g.rng_callbacks(rng)
+        keep += [fb, fr]
+        spec.rng_fill_bytes = ctypes.cast(fb, ctypes.c_void_p)
+        spec.rng_random_fr = ctypes.cast(fr, ctypes.c_void_p) if fr else None
     cap = 1 << 20
     buf = ctypes.create_string_buffer(cap)
     ln = np.zeros(1, dtype=np.uint64)

@@ -54,6 +54,7 @@ def main():
                 t0 = time.perf_counter()
                 O.create_proof(circ, wit, g, gl, threads=T, keygen=kg)
                 ts.append(time.perf_counter() - t0)
+                print(f"  k={k} {mode}: {ts[-1]:.3f} s", flush=True)
             run = {"k": k, "mode": mode, "median_s": round(sorted(ts)[len(ts) // 2], 3),
                    "runs_s": [round(t, 3) for t in ts]}
             res["runs"].append(run)

@@ -96,6 +96,30 @@ struct Query {
   bool operator==(const Query& o) const { return type == o.type && index == o.index && rot == o.rot; }
 };
 
+// Per-circuit workspace of create_proof (one per circuit of a proof over several
+// circuits, grown on demand and reused across proofs): the advice / instance columns,
+// permutation, lookup and shuffle polynomials, and the device pointer tables that
+// evaluate_h and the expression compressions read for this circuit.
+struct CircuitWs {
+  Pool pool;
+  std::vector<Fr*> adv, adv_coset, inst_val, inst_poly, inst_coset, z, z_lag, z_coset;
+  std::vector<Fr*> lk_a, lk_s, lk_ap, lk_sp, lk_ap_poly, lk_sp_poly, lk_z, lk_z_poly, lk_zc, lk_apc, lk_spc;
+  std::vector<Fr*> sh_z, sh_z_poly, sh_zc;
+  const Fr** d_load_col = nullptr;      // extended-coset columns (evaluate_h)
+  const Fr** d_load_col_lag = nullptr;  // Lagrange columns (lookup / shuffle compression)
+  const Fr** d_z = nullptr;
+  const Fr** d_perm_v = nullptr;
+  EvalLookup* d_lookups = nullptr;
+  EvalShuffle* d_shuffles = nullptr;
+  uint64_t* wit_pin = nullptr;  // advice staging of the witness source (num_advice x n Fr), pinned if possible
+  bool wit_pin_pinned = false;
+  ~CircuitWs() {
+    if (!wit_pin) return;
+    if (wit_pin_pinned) (void)hipHostFree(wit_pin);
+    else std::free(wit_pin);
+  }
+};
+
 struct ProvingKey {
   int device = 0;
   uint64_t params = 0;
@@ -119,9 +143,7 @@ struct ProvingKey {
   // 0 ProverSHPLONK, 1 ProverGWC; GWC witness polynomials, one per opening point
   int multiopen = 0;
   std::vector<Fr*> gwc_q;
-  uint32_t* lk_cnt = nullptr;  // pinned per-lookup match counters (3 per lookup)
-  uint64_t* wit_pin = nullptr;  // advice staging of the witness source (num_advice x n Fr), pinned if possible
-  bool wit_pin_pinned = false;
+  uint32_t* lk_cnt = nullptr;  // pinned per-(circuit, lookup) match counters (3 each)
   size_t lk_cnt_len = 0;
   // permute_expression_pair's sort, chosen per lookup from the value width lk_hb[l] (bit
   // length of the largest canonical value) seen by the previous proof: <= 64 bits: radix
@@ -131,6 +153,7 @@ struct ProvingKey {
   static constexpr int LKF = 5;
   std::vector<int> lk_hb;
   unsigned long long *lk_or_d = nullptr, *lk_or_h = nullptr;
+  size_t lk_or_len = 0;  // (circuit, lookup) entries of lk_or_*
   Domain dom;
   Pool pool;
   // proving key (device)
@@ -143,26 +166,18 @@ struct ProvingKey {
   std::vector<int2> seg_lk_in, seg_lk_tab, seg_sh_in, seg_sh_sh;  // expression-list programs
   Fr* consts = nullptr;
   int n_loads = 0;
-  const Fr** d_load_col = nullptr;      // extended-coset columns (evaluate_h)
-  const Fr** d_load_col_lag = nullptr;  // Lagrange columns (lookup / shuffle compression)
+  std::vector<Query> loads;  // the programs' load table (column, rotation)
   int* d_load_rot = nullptr;
-  const Fr** d_z = nullptr;
-  const Fr** d_perm_v = nullptr;
   const Fr** d_sigma = nullptr;
-  // lookups (NL) and shuffles (NS): per-argument device buffers
-  int NL = 0, NS = 0;
-  std::vector<Fr*> lk_a, lk_s, lk_ap, lk_sp, lk_ap_poly, lk_sp_poly, lk_z, lk_z_poly, lk_zc, lk_apc, lk_spc;
-  std::vector<Fr*> sh_z, sh_z_poly, sh_zc;
-  EvalLookup* d_lookups = nullptr;
-  EvalShuffle* d_shuffles = nullptr;
+  int NL = 0, NS = 0;  // lookups, shuffles
   Fr *tmp_a = nullptr, *tmp_b = nullptr, *one = nullptr;
   CanonKey *ck_a = nullptr, *ck_t = nullptr, *ck_a2 = nullptr, *ck_t2 = nullptr, *ck_left = nullptr;
   uint8_t *rep_flag = nullptr, *left_flag = nullptr;
   uint32_t *rep_rows = nullptr, *counters = nullptr;
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
-  // per-proof workspace (device), reused across proofs
-  std::vector<Fr*> adv, adv_coset, inst_val, inst_poly, inst_coset, z, z_lag, z_coset;
+  // per-proof workspace (device), reused across proofs: per circuit, and shared
+  std::vector<std::unique_ptr<CircuitWs>> cws;
   Fr *mod = nullptr, *pre = nullptr, *scr = nullptr, *random_poly = nullptr, *h_ext = nullptr, *h_coeff = nullptr;
   Fr *h_poly = nullptr, *nx = nullptr, *q1 = nullptr, *q2 = nullptr, *hx = nullptr, *lx = nullptr;
   Fr *small = nullptr, *last_z = nullptr, *evals = nullptr, *eval_scr = nullptr;
@@ -565,6 +580,74 @@ struct PkImage {
   const uint8_t *l0 = nullptr, *l_last = nullptr, *l_active = nullptr;
 };
 
+// one more circuit workspace (create_proof over pk.cws.size() + 1 circuits)
+int circuit_ws_add(ProvingKey& pk) {
+  auto w = std::make_unique<CircuitWs>();
+  const size_t n = pk.n, ext = pk.ext;
+  auto vec_alloc = [&](std::vector<Fr*>& v, int cnt, size_t len) -> hipError_t {
+    v.assign(cnt, nullptr);
+    for (int i = 0; i < cnt; i++) {
+      hipError_t e = w->pool.get((void**)&v[i], len * sizeof(Fr));
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  };
+  HIPCHK(vec_alloc(w->adv, pk.A, n));
+  HIPCHK(vec_alloc(w->adv_coset, pk.A, ext));
+  HIPCHK(vec_alloc(w->inst_val, pk.I, n));
+  HIPCHK(vec_alloc(w->inst_poly, pk.I, n));
+  HIPCHK(vec_alloc(w->inst_coset, pk.I, ext));
+  HIPCHK(vec_alloc(w->z, pk.nsets, n));
+  HIPCHK(vec_alloc(w->z_lag, pk.nsets, n));
+  HIPCHK(vec_alloc(w->z_coset, pk.nsets, ext));
+  HIPCHK(vec_alloc(w->lk_a, pk.NL, n));
+  HIPCHK(vec_alloc(w->lk_s, pk.NL, n));
+  HIPCHK(vec_alloc(w->lk_ap, pk.NL, n));
+  HIPCHK(vec_alloc(w->lk_sp, pk.NL, n));
+  HIPCHK(vec_alloc(w->lk_ap_poly, pk.NL, n));
+  HIPCHK(vec_alloc(w->lk_sp_poly, pk.NL, n));
+  HIPCHK(vec_alloc(w->lk_z, pk.NL, n));
+  HIPCHK(vec_alloc(w->lk_z_poly, pk.NL, n));
+  HIPCHK(vec_alloc(w->lk_zc, pk.NL, ext));
+  HIPCHK(vec_alloc(w->lk_apc, pk.NL, ext));
+  HIPCHK(vec_alloc(w->lk_spc, pk.NL, ext));
+  HIPCHK(vec_alloc(w->sh_z, pk.NS, n));
+  HIPCHK(vec_alloc(w->sh_z_poly, pk.NS, n));
+  HIPCHK(vec_alloc(w->sh_zc, pk.NS, ext));
+  // pointer tables: the load table's columns for this circuit (fixed columns are shared)
+  auto col = [&](const Query& q, bool coset) -> const Fr* {
+    if (q.type == COL_ADVICE) return coset ? w->adv_coset[q.index] : w->adv[q.index];
+    if (q.type == COL_FIXED) return coset ? pk.fixed_coset[q.index] : pk.fixed_lag[q.index];
+    return coset ? w->inst_coset[q.index] : w->inst_val[q.index];
+  };
+  std::vector<const Fr*> lc(pk.n_loads + 1, nullptr), ll(pk.n_loads + 1, nullptr);
+  for (int i = 0; i < pk.n_loads; i++) {
+    lc[i] = col(pk.loads[i], true);
+    ll[i] = col(pk.loads[i], false);
+  }
+  std::vector<EvalLookup> el(pk.NL + 1);
+  std::vector<EvalShuffle> es(pk.NS + 1);
+  for (int l = 0; l < pk.NL; l++) el[l] = EvalLookup{pk.seg_lk_in[l], pk.seg_lk_tab[l], w->lk_zc[l], w->lk_apc[l], w->lk_spc[l]};
+  for (int l = 0; l < pk.NS; l++) es[l] = EvalShuffle{pk.seg_sh_in[l], pk.seg_sh_sh[l], w->sh_zc[l]};
+  std::vector<const Fr*> zt(pk.nsets + 1), pv(pk.P + 1);
+  for (int s = 0; s < pk.nsets; s++) zt[s] = w->z_coset[s];
+  for (int i = 0; i < pk.P; i++) pv[i] = col(Query{pk.perm_cols[i].first, pk.perm_cols[i].second, 0}, true);
+  PALLOC(w->pool, w->d_load_col, lc.size());
+  PALLOC(w->pool, w->d_load_col_lag, ll.size());
+  PALLOC(w->pool, w->d_lookups, el.size());
+  PALLOC(w->pool, w->d_shuffles, es.size());
+  PALLOC(w->pool, w->d_z, zt.size());
+  PALLOC(w->pool, w->d_perm_v, pv.size());
+  HIPCHK(hipMemcpy(w->d_load_col, lc.data(), lc.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(w->d_load_col_lag, ll.data(), ll.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(w->d_lookups, el.data(), el.size() * sizeof(EvalLookup), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(w->d_shuffles, es.data(), es.size() * sizeof(EvalShuffle), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(w->d_z, zt.data(), zt.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(w->d_perm_v, pv.data(), pv.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+  pk.cws.push_back(std::move(w));
+  return H2G_OK;
+}
+
 int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, const PkImage* img = nullptr) {
   hipStream_t st = d->stream;
   std::string why;
@@ -682,29 +765,6 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
     }
     return hipSuccess;
   };
-  HIPCHK(vec_alloc(pk.adv, pk.A, n));
-  HIPCHK(vec_alloc(pk.adv_coset, pk.A, ext));
-  HIPCHK(vec_alloc(pk.inst_val, pk.I, n));
-  HIPCHK(vec_alloc(pk.inst_poly, pk.I, n));
-  HIPCHK(vec_alloc(pk.inst_coset, pk.I, ext));
-  HIPCHK(vec_alloc(pk.z, pk.nsets, n));
-  HIPCHK(vec_alloc(pk.z_lag, pk.nsets, n));
-  HIPCHK(vec_alloc(pk.z_coset, pk.nsets, ext));
-  // lookups / shuffles
-  HIPCHK(vec_alloc(pk.lk_a, pk.NL, n));
-  HIPCHK(vec_alloc(pk.lk_s, pk.NL, n));
-  HIPCHK(vec_alloc(pk.lk_ap, pk.NL, n));
-  HIPCHK(vec_alloc(pk.lk_sp, pk.NL, n));
-  HIPCHK(vec_alloc(pk.lk_ap_poly, pk.NL, n));
-  HIPCHK(vec_alloc(pk.lk_sp_poly, pk.NL, n));
-  HIPCHK(vec_alloc(pk.lk_z, pk.NL, n));
-  HIPCHK(vec_alloc(pk.lk_z_poly, pk.NL, n));
-  HIPCHK(vec_alloc(pk.lk_zc, pk.NL, ext));
-  HIPCHK(vec_alloc(pk.lk_apc, pk.NL, ext));
-  HIPCHK(vec_alloc(pk.lk_spc, pk.NL, ext));
-  HIPCHK(vec_alloc(pk.sh_z, pk.NS, n));
-  HIPCHK(vec_alloc(pk.sh_z_poly, pk.NS, n));
-  HIPCHK(vec_alloc(pk.sh_zc, pk.NS, ext));
   HIPCHK(falloc(&pk.one, 1));
   {
     const Fr one = Fr::one();
@@ -871,46 +931,17 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
     if (c->num_constants)
       HIPCHK(hipMemcpy(pk.consts, c->constants, c->num_constants * sizeof(Fr), hipMemcpyHostToDevice));
     pk.n_loads = (int)gc.loads.size();
-    std::vector<const Fr*> lc(pk.n_loads + 1, nullptr), ll(pk.n_loads + 1, nullptr);
+    pk.loads = gc.loads;
     std::vector<int> lr(pk.n_loads + 1, 0);
-    for (int i = 0; i < pk.n_loads; i++) {
-      const Query& q = gc.loads[i];
-      lc[i] = q.type == COL_ADVICE ? pk.adv_coset[q.index]
-                                   : (q.type == COL_FIXED ? pk.fixed_coset[q.index] : pk.inst_coset[q.index]);
-      ll[i] = q.type == COL_ADVICE ? pk.adv[q.index]
-                                   : (q.type == COL_FIXED ? pk.fixed_lag[q.index] : pk.inst_val[q.index]);
-      lr[i] = q.rot;
-    }
-    PALLOC(pool, pk.d_load_col, lc.size());
-    PALLOC(pool, pk.d_load_col_lag, ll.size());
+    for (int i = 0; i < pk.n_loads; i++) lr[i] = gc.loads[i].rot;
     PALLOC(pool, pk.d_load_rot, lr.size());
-    HIPCHK(hipMemcpy(pk.d_load_col, lc.data(), lc.size() * sizeof(Fr*), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(pk.d_load_col_lag, ll.data(), ll.size() * sizeof(Fr*), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(pk.d_load_rot, lr.data(), lr.size() * sizeof(int), hipMemcpyHostToDevice));
-    std::vector<EvalLookup> el(pk.NL + 1);
-    std::vector<EvalShuffle> es(pk.NS + 1);
-    for (int l = 0; l < pk.NL; l++)
-      el[l] = EvalLookup{pk.seg_lk_in[l], pk.seg_lk_tab[l], pk.lk_zc[l], pk.lk_apc[l], pk.lk_spc[l]};
-    for (int l = 0; l < pk.NS; l++) es[l] = EvalShuffle{pk.seg_sh_in[l], pk.seg_sh_sh[l], pk.sh_zc[l]};
-    PALLOC(pool, pk.d_lookups, el.size());
-    PALLOC(pool, pk.d_shuffles, es.size());
-    HIPCHK(hipMemcpy(pk.d_lookups, el.data(), el.size() * sizeof(EvalLookup), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(pk.d_shuffles, es.data(), es.size() * sizeof(EvalShuffle), hipMemcpyHostToDevice));
-    std::vector<const Fr*> zt(pk.nsets + 1), pv(pk.P + 1), sg(pk.P + 1);
-    for (int s = 0; s < pk.nsets; s++) zt[s] = pk.z_coset[s];
-    for (int i = 0; i < pk.P; i++) {
-      const auto& pc = pk.perm_cols[i];
-      pv[i] = pc.first == COL_ADVICE ? pk.adv_coset[pc.second]
-                                     : (pc.first == COL_FIXED ? pk.fixed_coset[pc.second] : pk.inst_coset[pc.second]);
-      sg[i] = pk.sigma_coset[i];
-    }
-    PALLOC(pool, pk.d_z, zt.size());
-    PALLOC(pool, pk.d_perm_v, pv.size());
+    std::vector<const Fr*> sg(pk.P + 1);
+    for (int i = 0; i < pk.P; i++) sg[i] = pk.sigma_coset[i];
     PALLOC(pool, pk.d_sigma, sg.size());
-    HIPCHK(hipMemcpy(pk.d_z, zt.data(), zt.size() * sizeof(Fr*), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(pk.d_perm_v, pv.data(), pv.size() * sizeof(Fr*), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(pk.d_sigma, sg.data(), sg.size() * sizeof(Fr*), hipMemcpyHostToDevice));
   }
+  RCCHK(circuit_ws_add(pk));  // circuit 0's workspace
   HIPCHK(hipStreamSynchronize(st));
   return H2G_OK;
 }
@@ -943,113 +974,137 @@ struct PolyRef {  // a committed polynomial in coefficient form (SHPLONK's "comm
 
 std::vector<Fr> g_last_challenges;  // the challenges of the last proof (h2g_last_challenges)
 
-int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, bool adv_dev,
-               const h2g_witness_source* src, const uint64_t* instance, const uint32_t* inst_lens, const uint8_t seed[32], uint32_t vthreads,
-               std::vector<uint8_t>* proof) {
+// create_proof's inputs (halo2_proofs/src/plonk/prover.rs:19-36): per circuit the witness
+// and the instances, the RNG, and the vanishing argument's thread count
+struct ProveIn {
+  int nc = 1;                                     // circuits
+  const uint64_t* const* advice = nullptr;        // [nc] num_advice x n Fr (host, or device)
+  bool adv_dev = false;
+  const h2g_witness_source* src1 = nullptr;       // one circuit's per-phase witness source
+  const h2g_witness_source_multi* src = nullptr;  // per-circuit per-phase witness source
+  const uint64_t* const* instance = nullptr;      // [nc] num_instance x n Fr (zero padded)
+  const uint32_t* const* inst_lens = nullptr;     // [nc] num_instance lengths
+  ProverRng* rng = nullptr;
+  uint32_t vthreads = 1;
+};
+
+int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::vector<uint8_t>* proof) {
   hipStream_t st = d->stream;
   const size_t n = pk.n, ext = pk.ext;
   const int bf = pk.bf;
   const Domain& D = pk.dom;
+  const int ncirc = in.nc;
+  while ((int)pk.cws.size() < ncirc) RCCHK(circuit_ws_add(pk));  // workspaces grow once
+  std::vector<CircuitWs*> W(ncirc);
+  for (int c = 0; c < ncirc; c++) W[c] = pk.cws[c].get();
   StageClock clk(st, g_stage_sync);
-  ChaChaRng rng(seed);
+  ProverRng& rng = *in.rng;
   Transcript tr(proof);
   auto write_point = [&](const G1Affine& p) -> int {
     if (!tr.write_point(p)) return fail(H2G_ERR_ARG, "cannot write points at infinity to the transcript");
     return H2G_OK;
   };
+  auto rng_ok = [&]() -> int { return rng.failed() ? fail(H2G_ERR_ARG, "create_proof: the caller's RNG failed") : H2G_OK; };
 
-  // ---- vk.hash_into + instances (prover.rs:196-271; KZG: QUERY_INSTANCE = false)
+  // ---- vk.hash_into + every circuit's instances (prover.rs:187-271; KZG: QUERY_INSTANCE = false)
   tr.common_scalar(pk.transcript_repr);
-  for (int i = 0; i < pk.I; i++) {
-    const uint32_t len = inst_lens ? inst_lens[i] : 0;
-    if ((size_t)len > n - (size_t)(bf + 1)) return fail(H2G_ERR_ARG, "create_proof: InstanceTooLarge");
-    const uint64_t* col = instance + 4 * n * i;
-    for (uint32_t r = 0; r < len; r++) tr.common_scalar(fr_from_limbs(col + 4 * r));
-    HIPCHK(hipMemcpyAsync(pk.inst_val[i], col, n * sizeof(Fr), hipMemcpyHostToDevice, st));
-    RCCHK(lagrange_to_coeff(d, D, pk.inst_val[i], pk.inst_poly[i], st));
-  }
-  // ---- commit_phase per advice phase: blinding rows, commitments, then the phase's
-  // challenges (prover.rs:309-494; A.3 draw order: the phase's blinding rows, then its blinds)
+  for (int ci = 0; ci < ncirc; ci++)
+    for (int i = 0; i < pk.I; i++) {
+      const uint32_t len = in.inst_lens[ci][i];
+      if ((size_t)len > n - (size_t)(bf + 1)) return fail(H2G_ERR_ARG, "create_proof: InstanceTooLarge");
+      const uint64_t* col = in.instance[ci] + 4 * n * i;
+      for (uint32_t r = 0; r < len; r++) tr.common_scalar(fr_from_limbs(col + 4 * r));
+      HIPCHK(hipMemcpyAsync(W[ci]->inst_val[i], col, n * sizeof(Fr), hipMemcpyHostToDevice, st));
+      RCCHK(lagrange_to_coeff(d, D, W[ci]->inst_val[i], W[ci]->inst_poly[i], st));
+    }
+  // ---- commit_phase per advice phase (prover.rs:309-494), circuit by circuit: the
+  // phase's blinding rows, its blinds, its commitments; then the phase's challenges
   const size_t unusable = n - (size_t)(bf + 1);
   // host staging that device copies read asynchronously: lives until the proof returns
   // (every copy has completed by then: the final commitment is collected after it)
-  std::vector<Fr> adv_blind((size_t)pk.A * (bf + 1));
-  // the witness source writes straight into pinned staging (allocated once per key: a
-  // pinned allocation of this size costs far more than the copies it speeds up)
-  uint64_t* src_buf = nullptr;
-  if (src) {
-    if (!pk.wit_pin) {
+  std::vector<Fr> adv_blind((size_t)ncirc * pk.A * (bf + 1));
+  const bool from_src = in.src || in.src1;
+  if (from_src)  // a witness source writes straight into pinned staging, one per circuit,
+    for (CircuitWs* w : W) {  // allocated once (a pinned allocation costs more than the copies it speeds up)
+      if (w->wit_pin) continue;
       const size_t bytes = (size_t)std::max(pk.A, 1) * n * sizeof(Fr);
-      if (hipHostMalloc((void**)&pk.wit_pin, bytes, hipHostMallocDefault) == hipSuccess) {
-        pk.wit_pin_pinned = true;
+      if (hipHostMalloc((void**)&w->wit_pin, bytes, hipHostMallocDefault) == hipSuccess) {
+        w->wit_pin_pinned = true;
       } else {  // pageable fallback: slower uploads, same bytes
         (void)hipGetLastError();
-        pk.wit_pin = static_cast<uint64_t*>(std::malloc(bytes));
-        pk.wit_pin_pinned = false;
-        if (!pk.wit_pin) return fail(H2G_ERR_NOMEM, "create_proof: witness staging allocation failed");
+        w->wit_pin = static_cast<uint64_t*>(std::malloc(bytes));
+        w->wit_pin_pinned = false;
+        if (!w->wit_pin) return fail(H2G_ERR_NOMEM, "create_proof: witness staging allocation failed");
       }
     }
-    src_buf = pk.wit_pin;  // only the committed phase's columns are read from it
-  }
-  const int NC = (int)pk.ch_phase.size();
-  std::vector<Fr> challenges(NC);
+  const int NCH = (int)pk.ch_phase.size();
+  std::vector<Fr> challenges(NCH);
   std::memset(challenges.data(), 0, challenges.size() * sizeof(Fr));
   StreamSyncGuard adv_guard{st};
   for (int ph = 0; ph <= pk.max_phase; ph++) {
     std::vector<int> cols;
     for (int c = 0; c < pk.A; c++)
       if (pk.adv_phase[c] == ph) cols.push_back(c);
-    const uint64_t* from = advice;
-    bool from_dev = adv_dev;
-    if (src) {
-      if (ph > 0) HIPCHK(hipStreamSynchronize(st));  // the previous phase's uploads read src_buf
-      // the staging outlives proofs: the unusable rows of unblinded columns start at zero
-      // as the reference requires (prover.rs:417-421), whatever an earlier proof left there
+    if (from_src && ph > 0) HIPCHK(hipStreamSynchronize(st));  // the previous phase's uploads read the staging
+    std::vector<MsmTicket> tk(cols.size() * ncirc);
+    for (int ci = 0; ci < ncirc; ci++) {
+      CircuitWs& w = *W[ci];
+      const uint64_t* from = in.advice ? in.advice[ci] : nullptr;
+      bool from_dev = in.adv_dev;
+      if (from_src) {
+        // the staging outlives proofs: the unusable rows of unblinded columns start at zero
+        // as the reference requires (prover.rs:417-421), whatever an earlier proof left there
+        for (int c : cols)
+          if (pk.unblinded[c]) std::memset(w.wit_pin + 4 * (n * c + unusable), 0, (n - unusable) * sizeof(Fr));
+        const uint64_t* chp = reinterpret_cast<const uint64_t*>(challenges.data());
+        const int frc = in.src ? in.src->fill(in.src->ctx, (uint32_t)ci, (uint32_t)ph, chp, w.wit_pin)
+                               : in.src1->fill(in.src1->ctx, (uint32_t)ph, chp, w.wit_pin);
+        if (frc)
+          return fail(H2G_ERR_ARG, "create_proof: witness source failed at circuit " + std::to_string(ci) + " phase " +
+                                       std::to_string(ph));
+        from = w.wit_pin;
+        from_dev = false;
+      }
       for (int c : cols)
-        if (pk.unblinded[c]) std::memset(src_buf + 4 * (n * c + unusable), 0, (n - unusable) * sizeof(Fr));
-      if (src->fill(src->ctx, (uint32_t)ph, reinterpret_cast<const uint64_t*>(challenges.data()), src_buf))
-        return fail(H2G_ERR_ARG, "create_proof: witness source failed at phase " + std::to_string(ph));
-      from = src_buf;
-      from_dev = false;
-    }
-    for (int c : cols)
-      HIPCHK(hipMemcpyAsync(pk.adv[c], from + 4 * n * c, n * sizeof(Fr),
-                            from_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
-    for (int c : cols) {
-      if (pk.unblinded[c]) continue;
-      Fr* rows = adv_blind.data() + (size_t)c * (bf + 1);
-      for (int i = 0; i <= bf; i++) rows[i] = rng.random_fr();
-      HIPCHK(hipMemcpyAsync(pk.adv[c] + unusable, rows, (size_t)(bf + 1) * sizeof(Fr), hipMemcpyHostToDevice, st));
-    }
-    for (int c : cols)
-      if (!pk.unblinded[c]) (void)rng.random_fr();  // commitment blinds (unused by KZG)
-    if (ph == 0) clk.mark("upload+instances");
-    if (!cols.empty()) {
-      std::vector<MsmTicket> tk(cols.size());
-      std::vector<Fr*> polys(cols.size());
-      for (size_t i = 0; i < cols.size(); i++) polys[i] = pk.adv[cols[i]];
-      RCCHK(commit_launch_batch(d, prm, polys.data(), (int)cols.size(), n, SRS_LAGRANGE, st, tk.data()));
-      for (size_t i = 0; i < cols.size(); i++) {
-        G1Affine cm;
-        RCCHK(commit_collect(d, &tk[i], &cm));
-        RCCHK(write_point(cm));
+        HIPCHK(hipMemcpyAsync(w.adv[c], from + 4 * n * c, n * sizeof(Fr),
+                              from_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+      for (int c : cols) {
+        if (pk.unblinded[c]) continue;
+        Fr* rows = adv_blind.data() + ((size_t)ci * pk.A + c) * (bf + 1);
+        for (int i = 0; i <= bf; i++) rows[i] = rng.random_fr();
+        HIPCHK(hipMemcpyAsync(w.adv[c] + unusable, rows, (size_t)(bf + 1) * sizeof(Fr), hipMemcpyHostToDevice, st));
+      }
+      for (int c : cols)
+        if (!pk.unblinded[c]) (void)rng.random_fr();  // commitment blinds (unused by KZG)
+      if (!cols.empty()) {
+        std::vector<const Fr*> polys(cols.size());
+        for (size_t i = 0; i < cols.size(); i++) polys[i] = w.adv[cols[i]];
+        RCCHK(commit_launch_batch(d, prm, polys.data(), (int)cols.size(), n, SRS_LAGRANGE, st,
+                                  tk.data() + (size_t)ci * cols.size()));
       }
     }
-    for (int i = 0; i < NC; i++)
+    if (ph == 0) clk.mark("upload+instances");
+    for (auto& t : tk) {  // circuit by circuit, column by column
+      G1Affine cm;
+      RCCHK(commit_collect(d, &t, &cm));
+      RCCHK(write_point(cm));
+    }
+    RCCHK(rng_ok());
+    for (int i = 0; i < NCH; i++)
       if (pk.ch_phase[i] == ph) challenges[i] = tr.squeeze();
   }
-  if (NC)
-    HIPCHK(hipMemcpyAsync(pk.consts + pk.num_consts, challenges.data(), NC * sizeof(Fr), hipMemcpyHostToDevice, st));
+  if (NCH)
+    HIPCHK(hipMemcpyAsync(pk.consts + pk.num_consts, challenges.data(), NCH * sizeof(Fr), hipMemcpyHostToDevice, st));
   g_last_challenges = challenges;
   clk.mark("advice commit");
   const Fr theta = tr.squeeze();
-  auto compress = [&](int2 seg, Fr* out) -> int {
+  auto compress = [&](const CircuitWs& w, int2 seg, Fr* out) -> int {
     CompressArgs ca;
     ca.prog = pk.prog;
     ca.seg = seg;
     ca.n_slots = pk.n_slots;
     ca.consts = pk.consts;
-    ca.load_col = pk.d_load_col_lag;
+    ca.load_col = w.d_load_col_lag;
     ca.load_rot = pk.d_load_rot;
     ca.n = n;
     ca.theta = theta;
@@ -1057,37 +1112,47 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     HIPCHK(compress_lagrange(ca, st));
     return H2G_OK;
   };
-  // ---- lookup_commit_permuted, per lookup (lookup/prover.rs:64-173, 410-494)
+  // ---- lookup_commit_permuted, per circuit, per lookup (lookup/prover.rs:64-173, 410-494)
+  const int NLT = ncirc * pk.NL;  // (circuit, lookup) pairs, circuit-major: j = ci * NL + l
   {
-    std::vector<MsmTicket> tk(2 * pk.NL);
-    const size_t u = n - (size_t)(bf + 1);
+    std::vector<MsmTicket> tk(2 * NLT);
+    const size_t u = unusable;
     // per-lookup host staging (random rows, match counters): no host synchronisation
     // between lookups, so their device pipelines queue back to back; the counters are
     // checked once all lookups are queued
-    std::vector<Fr> rows((size_t)pk.NL * 2 * (bf + 1));
-    if ((size_t)pk.NL * 3 > pk.lk_cnt_len) {
+    std::vector<Fr> rows((size_t)NLT * 2 * (bf + 1));
+    if ((size_t)NLT * 3 > pk.lk_cnt_len) {
       if (pk.lk_cnt) (void)hipHostFree(pk.lk_cnt);
-      HIPCHK(hipHostMalloc((void**)&pk.lk_cnt, (size_t)pk.NL * 3 * sizeof(uint32_t), hipHostMallocDefault));
-      pk.lk_cnt_len = (size_t)pk.NL * 3;
+      pk.lk_cnt = nullptr;
+      pk.lk_cnt_len = 0;
+      HIPCHK(hipHostMalloc((void**)&pk.lk_cnt, (size_t)NLT * 3 * sizeof(uint32_t), hipHostMallocDefault));
+      pk.lk_cnt_len = (size_t)NLT * 3;
     }
     constexpr int LKF = ProvingKey::LKF;
-    if (!pk.lk_or_d) {
-      HIPCHK(hipMalloc((void**)&pk.lk_or_d, (size_t)pk.NL * LKF * sizeof(unsigned long long)));
-      HIPCHK(hipHostMalloc((void**)&pk.lk_or_h, (size_t)pk.NL * LKF * sizeof(unsigned long long),
-                           hipHostMallocDefault));
+    if ((size_t)NLT > pk.lk_or_len) {
+      if (pk.lk_or_d) (void)hipFree(pk.lk_or_d);
+      if (pk.lk_or_h) (void)hipHostFree(pk.lk_or_h);
+      pk.lk_or_d = pk.lk_or_h = nullptr;
+      pk.lk_or_len = 0;
+      HIPCHK(hipMalloc((void**)&pk.lk_or_d, (size_t)NLT * LKF * sizeof(unsigned long long)));
+      HIPCHK(hipHostMalloc((void**)&pk.lk_or_h, (size_t)NLT * LKF * sizeof(unsigned long long), hipHostMallocDefault));
+      pk.lk_or_len = (size_t)NLT;
     }
-    HIPCHK(hipMemsetAsync(pk.lk_or_d, 0, (size_t)pk.NL * LKF * sizeof(unsigned long long), st));
+    if ((int)pk.lk_hb.size() < NLT) pk.lk_hb.resize(NLT, 64);
+    if (NLT) HIPCHK(hipMemsetAsync(pk.lk_or_d, 0, (size_t)NLT * LKF * sizeof(unsigned long long), st));
     // permute_expression_pair: sort by Ord (canonical value), match, fill leftovers;
     // then the bf + 1 random rows (input first, then table) and the two cosets.
     // hb: value width the sort assumes (1..64 narrow, 65..254 key window, 0 full sort)
-    auto permute = [&](int l, int hb) -> int {
+    auto permute = [&](int ci, int l, int hb) -> int {
+      const int j = ci * pk.NL + l;
+      CircuitWs& w = *W[ci];
       size_t tb = pk.sort_tmp_bytes;
-      unsigned long long* flags = pk.lk_or_d + (size_t)LKF * l;
+      unsigned long long* flags = pk.lk_or_d + (size_t)LKF * j;
       if (hb > 0 && hb <= 64) {  // the values themselves are the keys
         uint64_t* ka = (uint64_t*)pk.ck_a;  // [0, n): keys, [n, 2n): sorted
         uint64_t* kt = (uint64_t*)pk.ck_t;
-        HIPCHK(lookup_keys(pk.lk_a[l], u, 0, nullptr, ka, nullptr, flags, st));
-        HIPCHK(lookup_keys(pk.lk_s[l], u, 0, nullptr, kt, nullptr, flags, st));
+        HIPCHK(lookup_keys(w.lk_a[l], u, 0, nullptr, ka, nullptr, flags, st));
+        HIPCHK(lookup_keys(w.lk_s[l], u, 0, nullptr, kt, nullptr, flags, st));
         HIPCHK(hipcub::DeviceRadixSort::SortKeys(pk.sort_tmp, tb, ka, ka + n, (int)u, 0, hb, st));
         tb = pk.sort_tmp_bytes;
         HIPCHK(hipcub::DeviceRadixSort::SortKeys(pk.sort_tmp, tb, kt, kt + n, (int)u, 0, hb, st));
@@ -1098,18 +1163,18 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
         uint64_t* kout = kin + n;
         uint32_t* iin = (uint32_t*)(kout + n);
         uint32_t* iout = iin + n;
-        const Fr* src[2] = {pk.lk_a[l], pk.lk_s[l]};
+        const Fr* srcs[2] = {w.lk_a[l], w.lk_s[l]};
         CanonKey* canon[2] = {pk.ck_a, pk.ck_t};
         CanonKey* sorted[2] = {pk.ck_a2, pk.ck_t2};
-        for (int w = 0; w < 2; w++) {
-          HIPCHK(lookup_keys(src[w], u, hb - 48, canon[w], kin, iin, flags, st));
+        for (int s = 0; s < 2; s++) {
+          HIPCHK(lookup_keys(srcs[s], u, hb - 48, canon[s], kin, iin, flags, st));
           tb = pk.sort_tmp_bytes;
           HIPCHK(hipcub::DeviceRadixSort::SortPairs(pk.sort_tmp, tb, kin, kout, iin, iout, (int)u, 0, 48, st));
-          HIPCHK(lookup_gather(canon[w], iout, u, sorted[w], flags + 4, st));
+          HIPCHK(lookup_gather(canon[s], iout, u, sorted[s], flags + 4, st));
         }
       } else {
-        HIPCHK(fr_to_canon(pk.lk_a[l], pk.ck_a, u, st));
-        HIPCHK(fr_to_canon(pk.lk_s[l], pk.ck_t, u, st));
+        HIPCHK(fr_to_canon(w.lk_a[l], pk.ck_a, u, st));
+        HIPCHK(fr_to_canon(w.lk_s[l], pk.ck_t, u, st));
         HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(pk.sort_tmp, tb, pk.ck_a, pk.ck_a2, (int)u, CanonLess(), st));
         tb = pk.sort_tmp_bytes;
         HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(pk.sort_tmp, tb, pk.ck_t, pk.ck_t2, (int)u, CanonLess(), st));
@@ -1123,158 +1188,180 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
       tb = pk.sort_tmp_bytes;
       HIPCHK(hipcub::DeviceSelect::Flagged(pk.sort_tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), pk.rep_flag,
                                            pk.rep_rows, pk.counters + 1, (int)u, st));
-      HIPCHK(lookup_assign(pk.ck_a2, pk.rep_flag, u, pk.lk_ap[l], pk.lk_sp[l], st));
-      HIPCHK(lookup_scatter(pk.ck_left, pk.rep_rows, pk.counters + 1, u, pk.lk_sp[l], st));
-      HIPCHK(hipMemcpyAsync(pk.lk_cnt + 3 * l, pk.counters, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      HIPCHK(lookup_assign(pk.ck_a2, pk.rep_flag, u, w.lk_ap[l], w.lk_sp[l], st));
+      HIPCHK(lookup_scatter(pk.ck_left, pk.rep_rows, pk.counters + 1, u, w.lk_sp[l], st));
+      HIPCHK(hipMemcpyAsync(pk.lk_cnt + 3 * j, pk.counters, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       for (int which = 0; which < 2; which++) {
-        const Fr* r = rows.data() + ((size_t)2 * l + which) * (bf + 1);
-        HIPCHK(hipMemcpyAsync((which ? pk.lk_sp[l] : pk.lk_ap[l]) + u, r, (size_t)(bf + 1) * sizeof(Fr),
+        const Fr* r = rows.data() + ((size_t)2 * j + which) * (bf + 1);
+        HIPCHK(hipMemcpyAsync((which ? w.lk_sp[l] : w.lk_ap[l]) + u, r, (size_t)(bf + 1) * sizeof(Fr),
                               hipMemcpyHostToDevice, st));
       }
       return H2G_OK;
     };
-    std::vector<int> used(pk.NL);
-    for (int l = 0; l < pk.NL; l++) {
-      RCCHK(compress(pk.seg_lk_in[l], pk.lk_a[l]));
-      RCCHK(compress(pk.seg_lk_tab[l], pk.lk_s[l]));
-      for (int which = 0; which < 2; which++) {
-        Fr* r = rows.data() + ((size_t)2 * l + which) * (bf + 1);
-        for (int i = 0; i <= bf; i++) r[i] = rng.random_fr();
+    std::vector<int> used(NLT);
+    for (int ci = 0; ci < ncirc; ci++)
+      for (int l = 0; l < pk.NL; l++) {
+        const int j = ci * pk.NL + l;
+        RCCHK(compress(*W[ci], pk.seg_lk_in[l], W[ci]->lk_a[l]));
+        RCCHK(compress(*W[ci], pk.seg_lk_tab[l], W[ci]->lk_s[l]));
+        for (int which = 0; which < 2; which++) {
+          Fr* r = rows.data() + ((size_t)2 * j + which) * (bf + 1);
+          for (int i = 0; i <= bf; i++) r[i] = rng.random_fr();
+        }
+        (void)rng.random_fr();  // permuted input blind
+        (void)rng.random_fr();  // permuted table blind
+        used[j] = pk.lk_hb[j];
+        RCCHK(permute(ci, l, used[j]));
       }
-      (void)rng.random_fr();  // permuted input blind
-      (void)rng.random_fr();  // permuted table blind
-      used[l] = pk.lk_hb[l];
-      RCCHK(permute(l, used[l]));
+    if (NLT) {
+      HIPCHK(hipMemcpyAsync(pk.lk_or_h, pk.lk_or_d, (size_t)NLT * LKF * sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));  // counters and value masks landed; rows (host) read
     }
-    HIPCHK(hipMemcpyAsync(pk.lk_or_h, pk.lk_or_d, (size_t)pk.NL * LKF * sizeof(unsigned long long),
-                          hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));  // counters and value masks landed; rows (host) read
     // a sort whose assumption failed (values wider than its keys, or a key window that
     // tied different values out of order) is redone with the full sort; the width is
     // remembered for the next proof
     bool redo = false;
-    for (int l = 0; l < pk.NL; l++) {
-      if (used[l] == 0) continue;
-      const unsigned long long* f = pk.lk_or_h + (size_t)LKF * l;
+    for (int j = 0; j < NLT; j++) {
+      if (used[j] == 0) continue;
+      const unsigned long long* f = pk.lk_or_h + (size_t)LKF * j;
       int hb = 0;
-      for (int j = 3; j >= 0 && !hb; j--)
-        if (f[j]) hb = 64 * j + 64 - __builtin_clzll(f[j]);
+      for (int q = 3; q >= 0 && !hb; q--)
+        if (f[q]) hb = 64 * q + 64 - __builtin_clzll(f[q]);
       if (hb == 0) hb = 1;
       const bool tie = f[4] != 0;
-      pk.lk_hb[l] = tie && hb == used[l] ? 0 : hb;  // ties at the right width: full sort from now on
-      if (tie || hb > used[l]) {
-        RCCHK(permute(l, 0));
+      pk.lk_hb[j] = tie && hb == used[j] ? 0 : hb;  // ties at the right width: full sort from now on
+      if (tie || hb > used[j]) {
+        RCCHK(permute(j / pk.NL, j % pk.NL, 0));
         redo = true;
       }
     }
     if (redo) HIPCHK(hipStreamSynchronize(st));
-    for (int l = 0; l < pk.NL; l++) {
-      const uint32_t* cnt = pk.lk_cnt + 3 * l;
+    for (int j = 0; j < NLT; j++) {
+      const uint32_t* cnt = pk.lk_cnt + 3 * j;
       if (cnt[2] != 0 || cnt[0] != cnt[1])
         return fail(H2G_ERR_ARG, "create_proof: lookup input value not in the table (ConstraintSystemFailure)");
     }
     std::vector<const Fr*> perm_cols;  // (A'_l, S'_l) in transcript order
     std::vector<Fr*> perm_polys, perm_cosets;
-    for (int l = 0; l < pk.NL; l++) {
-      perm_cols.push_back(pk.lk_ap[l]);
-      perm_cols.push_back(pk.lk_sp[l]);
-      perm_polys.push_back(pk.lk_ap_poly[l]);
-      perm_polys.push_back(pk.lk_sp_poly[l]);
-      perm_cosets.push_back(pk.lk_apc[l]);
-      perm_cosets.push_back(pk.lk_spc[l]);
-    }
-    RCCHK(commit_launch_batch(d, prm, perm_cols.data(), 2 * pk.NL, n, SRS_LAGRANGE, st, tk.data()));
+    for (int ci = 0; ci < ncirc; ci++)
+      for (int l = 0; l < pk.NL; l++) {
+        CircuitWs& w = *W[ci];
+        perm_cols.push_back(w.lk_ap[l]);
+        perm_cols.push_back(w.lk_sp[l]);
+        perm_polys.push_back(w.lk_ap_poly[l]);
+        perm_polys.push_back(w.lk_sp_poly[l]);
+        perm_cosets.push_back(w.lk_apc[l]);
+        perm_cosets.push_back(w.lk_spc[l]);
+      }
+    RCCHK(commit_launch_batch(d, prm, perm_cols.data(), 2 * NLT, n, SRS_LAGRANGE, st, tk.data()));
     // coefficient forms and cosets, batched transforms (they overlap the commitments)
-    RCCHK(lagrange_to_coeff_batch(d, D, perm_cols.data(), perm_polys.data(), 2 * pk.NL, st));
-    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)perm_polys.data(), perm_cosets.data(), 2 * pk.NL, st));
-    for (int i = 0; i < 2 * pk.NL; i++) {
+    RCCHK(lagrange_to_coeff_batch(d, D, perm_cols.data(), perm_polys.data(), 2 * NLT, st));
+    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)perm_polys.data(), perm_cosets.data(), 2 * NLT, st));
+    for (int i = 0; i < 2 * NLT; i++) {
       G1Affine cm;
       RCCHK(commit_collect(d, &tk[i], &cm));
       RCCHK(write_point(cm));
     }
+    RCCHK(rng_ok());
   }
   if (pk.NL) clk.mark("lookup permuted");
   const Fr beta = tr.squeeze(), gamma = tr.squeeze();
   dump("beta", &beta, 1, st, true);
   dump("gamma", &gamma, 1, st, true);
 
-  // ---- permutation_commit (permutation/prover.rs:50-197); commitments are written
-  // after the loop (nothing is squeezed in between, so the transcript is unchanged)
-  std::vector<MsmTicket> perm_tk(pk.nsets);
+  // ---- permutation_commit per circuit (permutation/prover.rs:50-197); commitments are
+  // written after the loop (nothing is squeezed in between, so the transcript is unchanged)
+  const int NST = ncirc * pk.nsets;  // (circuit, set), circuit-major
+  std::vector<MsmTicket> perm_tk(NST);
   // large MSMs start as soon as their set's z is ready; small ones wait and go as a batch
   const bool perm_batched = commit_batch_chunk(prm, n, SRS_LAGRANGE) > 1;
   // host staging of every set's / product's blinding rows: no host synchronisation per
   // set, the transforms of all sets go as batches after the loop
-  std::vector<Fr> perm_blind((size_t)pk.nsets * bf), prod_blind((size_t)(pk.NL + pk.NS) * bf);
+  std::vector<Fr> perm_blind((size_t)NST * bf), prod_blind((size_t)ncirc * (pk.NL + pk.NS) * bf);
   StreamSyncGuard blind_guard{st};
+  std::vector<Fr*> all_z_lag, all_z, all_z_coset;
+  for (CircuitWs* w : W)
+    for (int s = 0; s < pk.nsets; s++) {
+      all_z_lag.push_back(w->z_lag[s]);
+      all_z.push_back(w->z[s]);
+      all_z_coset.push_back(w->z_coset[s]);
+    }
   {
-    const Fr one = Fr::one();
-    HIPCHK(hipMemcpyAsync(pk.last_z, &one, sizeof(Fr), hipMemcpyHostToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));
-    auto col_vals = [&](int c) -> const Fr* {
+    auto col_vals = [&](const CircuitWs& w, int c) -> const Fr* {
       const auto& pc = pk.perm_cols[c];
-      return pc.first == COL_ADVICE ? pk.adv[pc.second]
-                                    : (pc.first == COL_FIXED ? pk.fixed_lag[pc.second] : pk.inst_val[pc.second]);
+      return pc.first == COL_ADVICE ? w.adv[pc.second]
+                                    : (pc.first == COL_FIXED ? pk.fixed_lag[pc.second] : w.inst_val[pc.second]);
     };
-    // every set's denominators (into z_lag[s]), one batched inversion (z[s] as its
-    // scratch until the iNTT fills it), then per set numerators, scan and z
-    for (int s = 0; s < pk.nsets; s++) {
-      const int c0 = s * pk.chunk_len, c1 = std::min(c0 + pk.chunk_len, pk.P);
-      for (int c = c0; c < c1; c += PERM_MAXC) {
-        PermCols pc;
-        pc.m = std::min(PERM_MAXC, c1 - c);
-        for (int j = 0; j < pc.m; j++) {
-          pc.v[j] = col_vals(c + j);
-          pc.sigma[j] = pk.sigma_lag[c + j];
+    // every set's denominators (into z_lag), one batched inversion over all circuits'
+    // sets (z as its scratch until the iNTT fills it), then per set numerators, scan and z
+    for (int ci = 0; ci < ncirc; ci++)
+      for (int s = 0; s < pk.nsets; s++) {
+        const int c0 = s * pk.chunk_len, c1 = std::min(c0 + pk.chunk_len, pk.P);
+        for (int c = c0; c < c1; c += PERM_MAXC) {
+          PermCols pc;
+          pc.m = std::min(PERM_MAXC, c1 - c);
+          for (int j = 0; j < pc.m; j++) {
+            pc.v[j] = col_vals(*W[ci], c + j);
+            pc.sigma[j] = pk.sigma_lag[c + j];
+          }
+          HIPCHK(perm_denominators(W[ci]->z_lag[s], n, pc, beta, gamma, c == c0, st));
         }
-        HIPCHK(perm_denominators(pk.z_lag[s], n, pc, beta, gamma, c == c0, st));
+      }
+    if (NST) dump("den0", W[0]->z_lag[0], n, st);
+    HIPCHK(poly_batch_invert_multi(all_z_lag.data(), all_z.data(), NST, n, st));
+    if (NST) dump("inv0", W[0]->z_lag[0], n, st);
+    for (int ci = 0; ci < ncirc; ci++) {
+      CircuitWs& w = *W[ci];
+      HIPCHK(hipMemcpyAsync(pk.last_z, pk.one, sizeof(Fr), hipMemcpyDeviceToDevice, st));  // z_0 starts at one
+      Fr deltaomega = Fr::one();
+      for (int s = 0; s < pk.nsets; s++) {
+        Fr* blind_rows = perm_blind.data() + ((size_t)ci * pk.nsets + s) * bf;
+        const int c0 = s * pk.chunk_len, c1 = std::min(c0 + pk.chunk_len, pk.P);
+        Fr* prod = w.z_lag[s];
+        for (int c = c0; c < c1; c += PERM_MAXC) {
+          PermCols pc;
+          pc.m = std::min(PERM_MAXC, c1 - c);
+          for (int j = 0; j < pc.m; j++) {
+            pc.v[j] = col_vals(w, c + j);
+            pc.beta_delta[j] = deltaomega * beta;
+            deltaomega = deltaomega * fr_delta();
+          }
+          HIPCHK(perm_numerators(prod, n, pc, gamma, pk.om, st));
+        }
+        // z = last_z * running product, blinding rows from the rng
+        if (ci == 0 && s == 0) dump("mod0", prod, n, st);
+        HIPCHK(poly_prefix_product(prod, pk.pre, n, pk.scr, pk.scr_len, st));
+        if (ci == 0 && s == 0) dump("pre0", pk.pre, n, st);
+        for (int i = 0; i < bf; i++) blind_rows[i] = rng.random_fr();
+        (void)rng.random_fr();  // blind
+        HIPCHK(hipMemcpyAsync(pk.small, blind_rows, bf * sizeof(Fr), hipMemcpyHostToDevice, st));
+        HIPCHK(perm_z_assemble(w.z_lag[s], n, bf, pk.pre, pk.last_z, pk.small, st));
+        HIPCHK(hipMemcpyAsync(pk.last_z, w.z_lag[s] + (n - (size_t)(bf + 1)), sizeof(Fr), hipMemcpyDeviceToDevice,
+                              st));
+        if (ci == 0 && s == 0) {
+          dump("z0", w.z_lag[s], n, st);
+          dump("sigma0", pk.sigma_lag[0], n, st);
+          dump("v0", col_vals(w, 0), n, st);
+        }
+        if (!perm_batched)
+          RCCHK(commit_launch(d, prm, w.z_lag[s], n, SRS_LAGRANGE, st, &perm_tk[(size_t)ci * pk.nsets + s]));
       }
     }
-    dump("den0", pk.z_lag[0], n, st);
-    HIPCHK(poly_batch_invert_multi(pk.z_lag.data(), pk.z.data(), pk.nsets, n, st));
-    dump("inv0", pk.z_lag[0], n, st);
-    Fr deltaomega = Fr::one();
-    for (int s = 0; s < pk.nsets; s++) {
-      Fr* blind_rows = perm_blind.data() + (size_t)s * bf;
-      const int c0 = s * pk.chunk_len, c1 = std::min(c0 + pk.chunk_len, pk.P);
-      Fr* prod = pk.z_lag[s];
-      for (int c = c0; c < c1; c += PERM_MAXC) {
-        PermCols pc;
-        pc.m = std::min(PERM_MAXC, c1 - c);
-        for (int j = 0; j < pc.m; j++) {
-          pc.v[j] = col_vals(c + j);
-          pc.beta_delta[j] = deltaomega * beta;
-          deltaomega = deltaomega * fr_delta();
-        }
-        HIPCHK(perm_numerators(prod, n, pc, gamma, pk.om, st));
-      }
-      // z = last_z * running product, blinding rows from the rng
-      if (s == 0) dump("mod0", prod, n, st);
-      HIPCHK(poly_prefix_product(prod, pk.pre, n, pk.scr, pk.scr_len, st));
-      if (s == 0) dump("pre0", pk.pre, n, st);
-      for (int i = 0; i < bf; i++) blind_rows[i] = rng.random_fr();
-      (void)rng.random_fr();  // blind
-      HIPCHK(hipMemcpyAsync(pk.small, blind_rows, bf * sizeof(Fr), hipMemcpyHostToDevice, st));
-      HIPCHK(perm_z_assemble(pk.z_lag[s], n, bf, pk.pre, pk.last_z, pk.small, st));
-      HIPCHK(hipMemcpyAsync(pk.last_z, pk.z_lag[s] + (n - (size_t)(bf + 1)), sizeof(Fr), hipMemcpyDeviceToDevice,
-                            st));
-      if (s == 0) dump("z0", pk.z_lag[s], n, st);
-      if (s == 0) dump("sigma0", pk.sigma_lag[0], n, st);
-      if (s == 0) dump("v0", col_vals(0), n, st);
-      if (!perm_batched) RCCHK(commit_launch(d, prm, pk.z_lag[s], n, SRS_LAGRANGE, st, &perm_tk[s]));
-    }
-    RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)pk.z_lag.data(), pk.z.data(), pk.nsets, st));
-    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)pk.z.data(), pk.z_coset.data(), pk.nsets, st));
+    RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)all_z_lag.data(), all_z.data(), NST, st));
+    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)all_z.data(), all_z_coset.data(), NST, st));
   }
-  if (perm_batched) RCCHK(commit_launch_batch(d, prm, pk.z_lag.data(), pk.nsets, n, SRS_LAGRANGE, st, perm_tk.data()));
+  if (perm_batched)
+    RCCHK(commit_launch_batch(d, prm, (const Fr* const*)all_z_lag.data(), NST, n, SRS_LAGRANGE, st, perm_tk.data()));
   clk.mark("permutation products");
-  // ---- lookup products (lookup/prover.rs:182-325), then shuffle products
-  // (shuffle/prover.rs:97-206): z = [1, running product ...], bf random rows, blind
-  std::vector<MsmTicket> lkz_tk(pk.NL), shz_tk(pk.NS);
+  // ---- lookup products (lookup/prover.rs:182-325), every circuit's, then shuffle
+  // products (shuffle/prover.rs:97-206): z = [1, running product ...], bf random rows, blind
+  const int NSH = ncirc * pk.NS;
+  std::vector<MsmTicket> lkz_tk(NLT), shz_tk(NSH);
   {
     std::vector<const Fr*> z_lags;
     std::vector<Fr*> z_polys, z_cosets;
-    auto finish_z = [&](const Fr* prod, Fr* z_lag, Fr* z_poly, Fr* z_coset, MsmTicket*) -> int {
+    auto finish_z = [&](const Fr* prod, Fr* z_lag, Fr* z_poly, Fr* z_coset) -> int {
       HIPCHK(poly_prefix_product(prod, pk.pre, n, pk.scr, pk.scr_len, st));
       Fr* rows = prod_blind.data() + z_lags.size() * (size_t)bf;
       for (int i = 0; i < bf; i++) rows[i] = rng.random_fr();
@@ -1289,31 +1376,39 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     // every lookup's denominators go through one batched inversion (the per-thread
     // inversion's latency is paid once); z_poly holds the product until its iNTT,
     // z_lag serves as the inversion's scratch until z is assembled into it
-    for (int l = 0; l < pk.NL; l++)
-      HIPCHK(lookup_prod_den(pk.lk_ap[l], pk.lk_sp[l], beta, gamma, pk.lk_z_poly[l], n, st));
-    HIPCHK(poly_batch_invert_multi(pk.lk_z_poly.data(), pk.lk_z.data(), pk.NL, n, st));
-    for (int l = 0; l < pk.NL; l++) {
-      HIPCHK(lookup_prod_num(pk.lk_a[l], pk.lk_s[l], beta, gamma, pk.lk_z_poly[l], n, st));
-      RCCHK(finish_z(pk.lk_z_poly[l], pk.lk_z[l], pk.lk_z_poly[l], pk.lk_zc[l], &lkz_tk[l]));
-    }
-    for (int s = 0; s < pk.NS; s++) {
-      RCCHK(compress(pk.seg_sh_in[s], pk.tmp_a));
-      RCCHK(compress(pk.seg_sh_sh[s], pk.tmp_b));
-      HIPCHK(shuffle_prod_den(pk.tmp_b, gamma, pk.mod, n, st));
-      HIPCHK(poly_batch_invert(pk.mod, n, pk.scr, st));
-      HIPCHK(shuffle_prod_num(pk.tmp_a, gamma, pk.mod, n, st));
-      RCCHK(finish_z(pk.mod, pk.sh_z[s], pk.sh_z_poly[s], pk.sh_zc[s], &shz_tk[s]));
-    }
+    std::vector<Fr*> dens, dens_scr;
+    for (CircuitWs* w : W)
+      for (int l = 0; l < pk.NL; l++) {
+        HIPCHK(lookup_prod_den(w->lk_ap[l], w->lk_sp[l], beta, gamma, w->lk_z_poly[l], n, st));
+        dens.push_back(w->lk_z_poly[l]);
+        dens_scr.push_back(w->lk_z[l]);
+      }
+    HIPCHK(poly_batch_invert_multi(dens.data(), dens_scr.data(), NLT, n, st));
+    for (CircuitWs* w : W)
+      for (int l = 0; l < pk.NL; l++) {
+        HIPCHK(lookup_prod_num(w->lk_a[l], w->lk_s[l], beta, gamma, w->lk_z_poly[l], n, st));
+        RCCHK(finish_z(w->lk_z_poly[l], w->lk_z[l], w->lk_z_poly[l], w->lk_zc[l]));
+      }
+    for (CircuitWs* w : W)
+      for (int s = 0; s < pk.NS; s++) {
+        RCCHK(compress(*w, pk.seg_sh_in[s], pk.tmp_a));
+        RCCHK(compress(*w, pk.seg_sh_sh[s], pk.tmp_b));
+        HIPCHK(shuffle_prod_den(pk.tmp_b, gamma, pk.mod, n, st));
+        HIPCHK(poly_batch_invert(pk.mod, n, pk.scr, st));
+        HIPCHK(shuffle_prod_num(pk.tmp_a, gamma, pk.mod, n, st));
+        RCCHK(finish_z(pk.mod, w->sh_z[s], w->sh_z_poly[s], w->sh_zc[s]));
+      }
     RCCHK(lagrange_to_coeff_batch(d, D, z_lags.data(), z_polys.data(), (int)z_lags.size(), st));
     RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)z_polys.data(), z_cosets.data(), (int)z_lags.size(), st));
   }
-  {  // product commitments: lookups then shuffles, one batch
-    std::vector<const Fr*> zs(pk.lk_z.begin(), pk.lk_z.end());
-    zs.insert(zs.end(), pk.sh_z.begin(), pk.sh_z.end());
+  {  // product commitments: every circuit's lookups, then every circuit's shuffles, one batch
+    std::vector<const Fr*> zs;
+    for (CircuitWs* w : W) zs.insert(zs.end(), w->lk_z.begin(), w->lk_z.end());
+    for (CircuitWs* w : W) zs.insert(zs.end(), w->sh_z.begin(), w->sh_z.end());
     std::vector<MsmTicket> zt(zs.size());
     RCCHK(commit_launch_batch(d, prm, zs.data(), (int)zs.size(), n, SRS_LAGRANGE, st, zt.data()));
-    for (int l = 0; l < pk.NL; l++) lkz_tk[l] = zt[l];
-    for (int s = 0; s < pk.NS; s++) shz_tk[s] = zt[pk.NL + s];
+    for (int j = 0; j < NLT; j++) lkz_tk[j] = zt[j];
+    for (int j = 0; j < NSH; j++) shz_tk[j] = zt[NLT + j];
   }
   if (pk.NL + pk.NS) clk.mark("lookup/shuffle products");
   // ---- vanishing commit (vanishing/prover.rs:40-98)
@@ -1322,7 +1417,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   std::vector<uint32_t> seeds;
   StreamSyncGuard seed_guard{st};
   {
-    const uint64_t T = vthreads ? vthreads : 1;
+    const uint64_t T = in.vthreads ? in.vthreads : 1;
     const uint64_t chunk = n / T, rem = n % T;
     off.clear();
     for (uint64_t i = 0; i < rem && off.size() < T; i++) off.push_back(i * (chunk + 1));
@@ -1339,28 +1434,22 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     HIPCHK(hipMemcpyAsync(pk.d_offsets, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
     HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)off.size(), st));
     (void)rng.random_fr();             // random_blind
+    RCCHK(rng_ok());
     RCCHK(commit_launch(d, prm, pk.random_poly, n, SRS_G, st, &van_tk));
   }
   // advice to coefficient form and the extended-domain cosets do not depend on y:
   // they overlap the permutation / vanishing MSMs
-  RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)pk.adv.data(), pk.adv.data(), pk.A, st));
-  RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)pk.adv.data(), pk.adv_coset.data(), pk.A, st));
-  RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)pk.inst_poly.data(), pk.inst_coset.data(), pk.I, st));
-  for (int s = 0; s < pk.nsets; s++) {
-    G1Affine cm;
-    RCCHK(commit_collect(d, &perm_tk[s], &cm));
-    RCCHK(write_point(cm));
+  for (CircuitWs* w : W) {
+    RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)w->adv.data(), w->adv.data(), pk.A, st));
+    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)w->adv.data(), w->adv_coset.data(), pk.A, st));
+    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)w->inst_poly.data(), w->inst_coset.data(), pk.I, st));
   }
-  for (int l = 0; l < pk.NL; l++) {
-    G1Affine cm;
-    RCCHK(commit_collect(d, &lkz_tk[l], &cm));
-    RCCHK(write_point(cm));
-  }
-  for (int s = 0; s < pk.NS; s++) {
-    G1Affine cm;
-    RCCHK(commit_collect(d, &shz_tk[s], &cm));
-    RCCHK(write_point(cm));
-  }
+  for (auto* tks : {&perm_tk, &lkz_tk, &shz_tk})
+    for (auto& t : *tks) {
+      G1Affine cm;
+      RCCHK(commit_collect(d, &t, &cm));
+      RCCHK(write_point(cm));
+    }
   {
     G1Affine cm;
     RCCHK(commit_collect(d, &van_tk, &cm));
@@ -1368,7 +1457,10 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   }
   clk.mark("perm+vanishing commits, cosets");
   const Fr y = tr.squeeze();
-  {
+  // ---- evaluate_h (evaluation.rs:317-620): one launch per circuit, each continuing the
+  // previous circuit's Horner chain in y; the last one divides by t(X)
+  for (int ci = 0; ci < ncirc; ci++) {
+    const CircuitWs& w = *W[ci];
     EvalHArgs a;
     a.prog = pk.prog;
     a.gates = pk.seg_gates;
@@ -1376,16 +1468,16 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     a.theta = theta;
     a.nlookups = pk.NL;
     a.nshuffles = pk.NS;
-    a.lookups = pk.d_lookups;
-    a.shuffles = pk.d_shuffles;
+    a.lookups = w.d_lookups;
+    a.shuffles = w.d_shuffles;
     a.consts = pk.consts;
-    a.query_col = pk.d_load_col;
+    a.query_col = w.d_load_col;
     a.query_rot = pk.d_load_rot;
     a.nsets = pk.nsets;
     a.chunk_len = pk.chunk_len;
     a.P = pk.P;
-    a.z = pk.d_z;
-    a.perm_v = pk.d_perm_v;
+    a.z = w.d_z;
+    a.perm_v = w.d_perm_v;
     a.sigma = pk.d_sigma;
     a.l0 = pk.l0;
     a.l_last = pk.l_last;
@@ -1401,6 +1493,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     a.last_rot = -(bf + 1);
     a.t_evals = D.d_t;
     a.t_mask = D.t_evals.size() - 1;
+    a.acc_in = ci > 0 ? pk.h_ext : nullptr;
+    a.divide = ci + 1 == ncirc;
     a.out = pk.h_ext;
     HIPCHK(evaluate_h(a, st));
   }
@@ -1409,6 +1503,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   RCCHK(extended_to_coeff(d, D, pk.h_ext, pk.h_coeff, st));
   const int npieces = pk.degree - 1;
   for (int p = 0; p < npieces; p++) (void)rng.random_fr();  // h blinds
+  RCCHK(rng_ok());
   {
     std::vector<MsmTicket> tk(npieces);
     std::vector<const Fr*> pieces(npieces);
@@ -1444,49 +1539,58 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
   }
 
   // ---- the polynomial openings (prover.rs:840-889) and their evaluations
-  // poly ids: advice c, fixed A+c, sigma A+F+c, z A+F+P+s, h, random
+  // poly ids: per circuit ci (base ci * per_c): advice c, z s, lookup l (z, A', S'),
+  // shuffle s; then fixed, sigma, h, random
+  const int per_c = pk.A + pk.nsets + 3 * pk.NL + pk.NS;
+  auto id_adv = [&](int ci) { return ci * per_c; };
+  auto id_z = [&](int ci) { return ci * per_c + pk.A; };
+  auto id_lk = [&](int ci) { return ci * per_c + pk.A + pk.nsets; };  // lookup l: z, A', S' at + 3 l
+  auto id_sh = [&](int ci) { return ci * per_c + pk.A + pk.nsets + 3 * pk.NL; };
   std::vector<PolyRef> polys;
-  for (int c = 0; c < pk.A; c++) polys.push_back({pk.adv[c], n});
-  for (int c = 0; c < pk.F; c++) polys.push_back({pk.fixed_poly[c], n});
-  for (int c = 0; c < pk.P; c++) polys.push_back({pk.sigma_poly[c], n});
-  for (int s = 0; s < pk.nsets; s++) polys.push_back({pk.z[s], n});
-  const int id_lk = (int)polys.size();  // lookup l: z, A', S' at id_lk + 3 l
-  for (int l = 0; l < pk.NL; l++) {
-    polys.push_back({pk.lk_z_poly[l], n});
-    polys.push_back({pk.lk_ap_poly[l], n});
-    polys.push_back({pk.lk_sp_poly[l], n});
+  for (const CircuitWs* w : W) {
+    for (int c = 0; c < pk.A; c++) polys.push_back({w->adv[c], n});
+    for (int s = 0; s < pk.nsets; s++) polys.push_back({w->z[s], n});
+    for (int l = 0; l < pk.NL; l++) {
+      polys.push_back({w->lk_z_poly[l], n});
+      polys.push_back({w->lk_ap_poly[l], n});
+      polys.push_back({w->lk_sp_poly[l], n});
+    }
+    for (int s = 0; s < pk.NS; s++) polys.push_back({w->sh_z_poly[s], n});
   }
-  const int id_sh = (int)polys.size();
-  for (int s = 0; s < pk.NS; s++) polys.push_back({pk.sh_z_poly[s], n});
+  const int id_fix = (int)polys.size();
+  for (int c = 0; c < pk.F; c++) polys.push_back({pk.fixed_poly[c], n});
+  const int id_sig = (int)polys.size();
+  for (int c = 0; c < pk.P; c++) polys.push_back({pk.sigma_poly[c], n});
   const int id_h = (int)polys.size();
   polys.push_back({pk.h_poly, n});
   const int id_r = (int)polys.size();
   polys.push_back({pk.random_poly, n});
-  const int id_adv = 0, id_fix = pk.A, id_sig = pk.A + pk.F, id_z = pk.A + pk.F + pk.P;
   const Fr x_next = rotate_omega(D, x, 1), x_last = rotate_omega(D, x, -(bf + 1));
+  const Fr x_prev = rotate_omega(D, x, -1);
   struct Q2 {
     int poly;
     Fr pt;
   };
   std::vector<Q2> queries;
-  for (auto& q : pk.adv_q) queries.push_back({id_adv + q.index, rotate_omega(D, x, q.rot)});
-  for (int s = 0; s < pk.nsets; s++) {
-    queries.push_back({id_z + s, x});
-    queries.push_back({id_z + s, x_next});
-  }
-  for (int s = pk.nsets - 2; s >= 0; s--) queries.push_back({id_z + s, x_last});
-  const Fr x_prev = rotate_omega(D, x, -1);
-  for (int l = 0; l < pk.NL; l++) {  // lookup/prover.rs:364-405
-    const int zi = id_lk + 3 * l;
-    queries.push_back({zi, x});
-    queries.push_back({zi + 1, x});
-    queries.push_back({zi + 2, x});
-    queries.push_back({zi + 1, x_prev});
-    queries.push_back({zi, x_next});
-  }
-  for (int s = 0; s < pk.NS; s++) {  // shuffle/prover.rs:234-254
-    queries.push_back({id_sh + s, x});
-    queries.push_back({id_sh + s, x_next});
+  for (int ci = 0; ci < ncirc; ci++) {  // per circuit: advice, permutation, lookups, shuffles
+    for (auto& q : pk.adv_q) queries.push_back({id_adv(ci) + q.index, rotate_omega(D, x, q.rot)});
+    for (int s = 0; s < pk.nsets; s++) {  // permutation/prover.rs:300-333
+      queries.push_back({id_z(ci) + s, x});
+      queries.push_back({id_z(ci) + s, x_next});
+    }
+    for (int s = pk.nsets - 2; s >= 0; s--) queries.push_back({id_z(ci) + s, x_last});
+    for (int l = 0; l < pk.NL; l++) {  // lookup/prover.rs:364-405
+      const int zi = id_lk(ci) + 3 * l;
+      queries.push_back({zi, x});
+      queries.push_back({zi + 1, x});
+      queries.push_back({zi + 2, x});
+      queries.push_back({zi + 1, x_prev});
+      queries.push_back({zi, x_next});
+    }
+    for (int s = 0; s < pk.NS; s++) {  // shuffle/prover.rs:234-254
+      queries.push_back({id_sh(ci) + s, x});
+      queries.push_back({id_sh(ci) + s, x_next});
+    }
   }
   for (auto& q : pk.fix_q) queries.push_back({id_fix + q.index, rotate_omega(D, x, q.rot)});
   for (int c = 0; c < pk.P; c++) queries.push_back({id_sig + c, x});
@@ -1522,27 +1626,31 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const uint64_t* advice, b
     HIPCHK(hipStreamSynchronize(st));
   }
   auto ev = [&](int poly, const Fr& pt) { return evals[ev_index(poly, pt)]; };
-  for (auto& q : pk.adv_q) tr.write_scalar(ev(id_adv + q.index, rotate_omega(D, x, q.rot)));
+  for (int ci = 0; ci < ncirc; ci++)  // [TRANSCRIPT-17] every circuit's advice evaluations
+    for (auto& q : pk.adv_q) tr.write_scalar(ev(id_adv(ci) + q.index, rotate_omega(D, x, q.rot)));
   for (auto& q : pk.fix_q) tr.write_scalar(ev(id_fix + q.index, rotate_omega(D, x, q.rot)));
   tr.write_scalar(ev(id_r, x));
   for (int c = 0; c < pk.P; c++) tr.write_scalar(ev(id_sig + c, x));
-  for (int s = 0; s < pk.nsets; s++) {
-    tr.write_scalar(ev(id_z + s, x));
-    tr.write_scalar(ev(id_z + s, x_next));
-    if (s + 1 < pk.nsets) tr.write_scalar(ev(id_z + s, x_last));
-  }
-  for (int l = 0; l < pk.NL; l++) {  // product, product_next, A', A'_inv, S' (lookup/prover.rs:330-361)
-    const int zi = id_lk + 3 * l;
-    tr.write_scalar(ev(zi, x));
-    tr.write_scalar(ev(zi, x_next));
-    tr.write_scalar(ev(zi + 1, x));
-    tr.write_scalar(ev(zi + 1, x_prev));
-    tr.write_scalar(ev(zi + 2, x));
-  }
-  for (int s = 0; s < pk.NS; s++) {
-    tr.write_scalar(ev(id_sh + s, x));
-    tr.write_scalar(ev(id_sh + s, x_next));
-  }
+  for (int ci = 0; ci < ncirc; ci++)
+    for (int s = 0; s < pk.nsets; s++) {
+      tr.write_scalar(ev(id_z(ci) + s, x));
+      tr.write_scalar(ev(id_z(ci) + s, x_next));
+      if (s + 1 < pk.nsets) tr.write_scalar(ev(id_z(ci) + s, x_last));
+    }
+  for (int ci = 0; ci < ncirc; ci++)
+    for (int l = 0; l < pk.NL; l++) {  // product, product_next, A', A'_inv, S' (lookup/prover.rs:330-361)
+      const int zi = id_lk(ci) + 3 * l;
+      tr.write_scalar(ev(zi, x));
+      tr.write_scalar(ev(zi, x_next));
+      tr.write_scalar(ev(zi + 1, x));
+      tr.write_scalar(ev(zi + 1, x_prev));
+      tr.write_scalar(ev(zi + 2, x));
+    }
+  for (int ci = 0; ci < ncirc; ci++)
+    for (int s = 0; s < pk.NS; s++) {
+      tr.write_scalar(ev(id_sh(ci) + s, x));
+      tr.write_scalar(ev(id_sh(ci) + s, x_next));
+    }
   clk.mark("evaluations");
 
   if (pk.multiopen == 1) {
@@ -2182,10 +2290,6 @@ int h2g_pk_free(uint64_t pk) {
   (void)hipStreamSynchronize(d->stream);
   domain_release(&it->second->dom);
   if (it->second->lk_cnt) (void)hipHostFree(it->second->lk_cnt);
-  if (it->second->wit_pin) {
-    if (it->second->wit_pin_pinned) (void)hipHostFree(it->second->wit_pin);
-    else std::free(it->second->wit_pin);
-  }
   if (it->second->lk_or_h) (void)hipHostFree(it->second->lk_or_h);
   if (it->second->lk_or_d) (void)hipFree(it->second->lk_or_d);
   g_pks.erase(it);
@@ -2234,23 +2338,28 @@ int h2g_pk_info(uint64_t pk, int32_t info[8]) {
   return H2G_OK;
 }
 
-int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int advice_on_device,
-                     const uint64_t* instance, const uint32_t* instance_lens, const uint8_t rng_seed[32],
-                     uint32_t vanishing_threads, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
-  NEED_DEV_P();
+}  // extern "C"
+
+namespace {
+// the checks and output handling every create_proof entry point shares
+int create_proof_entry(Device* d, uint64_t params, uint64_t pk, ProveIn& in, uint8_t* proof, size_t proof_cap,
+                       size_t* proof_len) {
   auto ip = g_params.find(params);
   if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
   auto ik = g_pks.find(pk);
   if (ik == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
   ProvingKey& K = *ik->second;
-  if (ik->second->params != params) return fail(H2G_ERR_ARG, "create_proof: pk was generated with other params");
+  if (K.params != params) return fail(H2G_ERR_ARG, "create_proof: pk was generated with other params");
   if (K.device != d->id) return fail(H2G_ERR_ARG, "create_proof: pk lives on another device");
-  if ((K.A && !advice) || (K.I && (!instance || !instance_lens)) || !rng_seed || !proof_len)
-    return fail(H2G_ERR_ARG, "create_proof: null argument");
+  if (!proof_len || in.nc < 1 || in.nc > 1024) return fail(H2G_ERR_ARG, "create_proof: bad arguments");
+  for (int c = 0; c < in.nc; c++) {
+    if (K.A && !in.src && !in.src1 && (!in.advice || !in.advice[c])) return fail(H2G_ERR_ARG, "create_proof: null advice");
+    if (K.I && (!in.instance || !in.inst_lens || !in.instance[c] || !in.inst_lens[c]))
+      return fail(H2G_ERR_ARG, "create_proof: null instance");  // InvalidInstances
+  }
   std::vector<uint8_t> out;
   out.reserve(32 * 256);
-  int rc = prove_impl(d, *ip->second, K, advice, advice_on_device != 0, nullptr, instance, instance_lens,
-                      rng_seed, vanishing_threads, &out);
+  int rc = prove_impl(d, *ip->second, K, in, &out);
   if (rc) {
     (void)hipStreamSynchronize(d->stream);
     return rc;
@@ -2260,32 +2369,60 @@ int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int a
   if (proof) std::memcpy(proof, out.data(), out.size());
   return H2G_OK;
 }
+}  // namespace
+
+extern "C" {
+
+int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int advice_on_device,
+                     const uint64_t* instance, const uint32_t* instance_lens, const uint8_t rng_seed[32],
+                     uint32_t vanishing_threads, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
+  NEED_DEV_P();
+  if (!rng_seed) return fail(H2G_ERR_ARG, "create_proof: null rng seed");
+  ProverRng rng(rng_seed);
+  ProveIn in;
+  in.advice = &advice;
+  in.adv_dev = advice_on_device != 0;
+  in.instance = &instance;
+  in.inst_lens = &instance_lens;
+  in.rng = &rng;
+  in.vthreads = vanishing_threads;
+  return create_proof_entry(d, params, pk, in, proof, proof_cap, proof_len);
+}
 
 int h2g_create_proof_phased(uint64_t params, uint64_t pk, const h2g_witness_source* witness,
                             const uint64_t* instance, const uint32_t* instance_lens, const uint8_t rng_seed[32],
                             uint32_t vanishing_threads, uint8_t* proof, size_t proof_cap, size_t* proof_len) {
   NEED_DEV_P();
-  auto ip = g_params.find(params);
-  if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
-  auto ik = g_pks.find(pk);
-  if (ik == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
-  ProvingKey& K = *ik->second;
-  if (ik->second->params != params) return fail(H2G_ERR_ARG, "create_proof: pk was generated with other params");
-  if (K.device != d->id) return fail(H2G_ERR_ARG, "create_proof: pk lives on another device");
-  if (!witness || !witness->fill || (K.I && (!instance || !instance_lens)) || !rng_seed || !proof_len)
-    return fail(H2G_ERR_ARG, "create_proof: null argument");
-  std::vector<uint8_t> out;
-  out.reserve(32 * 256);
-  int rc = prove_impl(d, *ip->second, K, nullptr, false, witness, instance, instance_lens, rng_seed,
-                      vanishing_threads, &out);
-  if (rc) {
-    (void)hipStreamSynchronize(d->stream);
-    return rc;
-  }
-  *proof_len = out.size();
-  if (out.size() > proof_cap) return fail(H2G_ERR_ARG, "create_proof: proof buffer too small");
-  if (proof) std::memcpy(proof, out.data(), out.size());
-  return H2G_OK;
+  if (!rng_seed || !witness || !witness->fill) return fail(H2G_ERR_ARG, "create_proof: null argument");
+  ProverRng rng(rng_seed);
+  ProveIn in;
+  in.src1 = witness;
+  in.instance = &instance;
+  in.inst_lens = &instance_lens;
+  in.rng = &rng;
+  in.vthreads = vanishing_threads;
+  return create_proof_entry(d, params, pk, in, proof, proof_cap, proof_len);
+}
+
+int h2g_create_proof_multi(uint64_t params, uint64_t pk, const h2g_prove_inputs* p, uint8_t* proof,
+                           size_t proof_cap, size_t* proof_len) {
+  NEED_DEV_P();
+  if (!p || p->num_circuits < 1) return fail(H2G_ERR_ARG, "create_proof: no circuits");
+  if (p->witness && !p->witness->fill) return fail(H2G_ERR_ARG, "create_proof: null witness fill");
+  if (!p->rng && !p->rng_seed) return fail(H2G_ERR_ARG, "create_proof: neither an rng nor a seed");
+  if (p->rng && !p->rng->fill_bytes && !p->rng->random_fr) return fail(H2G_ERR_ARG, "create_proof: rng without draws");
+  std::unique_ptr<ProverRng> rng = p->rng ? std::make_unique<ProverRng>(p->rng->fill_bytes, p->rng->random_fr, p->rng->ctx)
+                                          : std::make_unique<ProverRng>(p->rng_seed);
+  ProveIn in;
+  in.nc = (int)std::min<uint32_t>(p->num_circuits, 1u << 20);
+  in.advice = p->advice;
+  in.adv_dev = p->advice_on_device != 0;
+  in.src = p->witness;
+  in.instance = p->instance;
+  in.inst_lens = p->instance_lens;
+  in.rng = rng.get();
+  in.vthreads = p->vanishing_threads;
+  return create_proof_entry(d, params, pk, in, proof, proof_cap, proof_len);
 }
 
 int h2g_last_challenges(uint64_t* out, int max, int* count) {

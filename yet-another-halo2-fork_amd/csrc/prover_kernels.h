@@ -76,6 +76,11 @@ struct EvalHArgs {
   int last_rot = 0;
   const Fr* t_evals = nullptr;
   uint64_t t_mask = 0;
+  // several circuits in one proof (evaluation.rs:367-620): circuit c > 0 continues the
+  // Horner chain of the circuits before it from acc_in (the previous launch's output,
+  // may alias out); only the last circuit's launch divides by t(X)
+  const Fr* acc_in = nullptr;
+  int divide = 1;
   Fr* out = nullptr;
 };
 hipError_t evaluate_h(const EvalHArgs& a, hipStream_t st);

@@ -120,11 +120,12 @@ static constexpr int EH_T = 64;
 static constexpr int EH_MAX_SLOTS = 24;
 int evaluate_h_max_slots() { return EH_MAX_SLOTS; }
 
-// run one program segment for row idx: Horner of its expression values with `factor`
+// run one program segment for row idx: Horner of its expression values with `factor`,
+// starting from `acc`
 __device__ __forceinline__ Fr run_prog(const int4* __restrict__ prog, int2 seg, const Fr* __restrict__ consts,
                                        const Fr* const* __restrict__ cols, const int* __restrict__ rots, uint64_t idx,
-                                       uint64_t rot_scale, uint64_t mask, Fr factor, Fr* sl, int lane) {
-  Fr acc = Fr::zero();
+                                       uint64_t rot_scale, uint64_t mask, Fr factor, Fr* sl, int lane,
+                                       Fr acc = Fr::zero()) {
   for (int pc = seg.x; pc < seg.x + seg.y; pc++) {
     const int4 in = prog[pc];
     Fr v;
@@ -154,7 +155,8 @@ __global__ void __launch_bounds__(EH_T) evaluate_h_kernel(EvalHArgs a) {
   const int lane = threadIdx.x;
   const uint64_t emask = a.ext - 1;
   for (uint64_t idx = blockIdx.x * (uint64_t)EH_T + lane; idx < a.ext; idx += (uint64_t)gridDim.x * EH_T) {
-    Fr acc = run_prog(a.prog, a.gates, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, a.y, sl, lane);
+    Fr acc = run_prog(a.prog, a.gates, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, a.y, sl, lane,
+                      a.acc_in ? ldf(a.acc_in + idx) : Fr::zero());
     const Fr l0 = ldf(a.l0 + idx);
     const Fr ll = ldf(a.l_last + idx);
     const Fr la = ldf(a.l_active + idx);
@@ -215,7 +217,7 @@ __global__ void __launch_bounds__(EH_T) evaluate_h_kernel(EvalHArgs a) {
         acc = acc * a.y + la * (ldf(sh.z + r_next) * cs - z * ci);
       }
     }
-    stf(a.out + idx, acc * ldf(a.t_evals + (idx & a.t_mask)));
+    stf(a.out + idx, a.divide ? acc * ldf(a.t_evals + (idx & a.t_mask)) : acc);
   }
 }
 

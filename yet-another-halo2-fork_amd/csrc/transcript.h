@@ -206,6 +206,56 @@ class ChaChaRng {
   size_t pos_ = 64;
 };
 
+// The prover's `rng: R: RngCore` (halo2_proofs/src/plonk/prover.rs:27,34): either
+// ChaCha20Rng::from_seed, or the caller's RNG (h2g_rng): F::random draws through its
+// random_fr (or 64 bytes of fill_bytes), seed draws through fill_bytes, in the
+// reference's order.  A failed callback latches: later draws return zeros
+// and the prover fails the proof once it checks failed().
+class ProverRng {
+ public:
+  using FillFn = int (*)(void*, uint8_t*, size_t);
+  using FrFn = int (*)(void*, uint64_t*);
+  explicit ProverRng(const uint8_t seed[32]) : cc_(seed) {}
+  ProverRng(FillFn fill_bytes, FrFn random, void* ctx) : cc_(kZeroSeed), fb_(fill_bytes), fr_(random), ctx_(ctx) {}
+  void fill(uint8_t* out, size_t len) {
+    if (!fb_ && !fr_) return cc_.fill(out, len);
+    if (failed_ || !fb_ || fb_(ctx_, out, len) != 0) {
+      failed_ = true;
+      std::memset(out, 0, len);
+    }
+  }
+  Fr random_fr() {
+    if (fr_) {  // the caller's F::random, Montgomery limbs
+      uint64_t v[4] = {0, 0, 0, 0};
+      if (failed_ || fr_(ctx_, v) != 0) {
+        failed_ = true;
+        return Fr::zero();
+      }
+      Fr r;
+      std::memcpy(r.l, v, 32);
+      unsigned br = 0;  // an Fr must be below r
+      for (int i = 0; i < 8; i++) (void)__builtin_subc(r.l[i], FrParams::M[i], br, &br);
+      if (!br) {
+        failed_ = true;
+        return Fr::zero();
+      }
+      return r;
+    }
+    uint32_t w[16];  // from_uniform_bytes of 64 bytes: LE512 mod r
+    fill(reinterpret_cast<uint8_t*>(w), 64);
+    return fr_from_u512(w);
+  }
+  bool failed() const { return failed_; }
+
+ private:
+  static constexpr uint8_t kZeroSeed[32] = {};
+  ChaChaRng cc_;
+  FillFn fb_ = nullptr;
+  FrFn fr_ = nullptr;
+  void* ctx_ = nullptr;
+  bool failed_ = false;
+};
+
 class Transcript {
  public:
   explicit Transcript(std::vector<uint8_t>* proof) : h_("Halo2-Transcript"), proof_(proof) {}

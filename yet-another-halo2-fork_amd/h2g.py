@@ -97,6 +97,7 @@ _SIGS = {
                           ctypes.POINTER(SZ)], I32),
     "h2g_create_proof_phased": ([U64, U64, VP, U64P, ctypes.POINTER(U32), ctypes.c_char_p, U32, ctypes.c_char_p,
                                  SZ, ctypes.POINTER(SZ)], I32),
+    "h2g_create_proof_multi": ([U64, U64, VP, ctypes.c_char_p, SZ, ctypes.POINTER(SZ)], I32),
     "h2g_last_challenges": ([U64P, I32, ctypes.POINTER(I32)], I32),
     "h2g_prover_stages": ([ctypes.POINTER(ctypes.c_double), I32, ctypes.POINTER(I32)], I32),
     "h2g_prover_stage_name": ([I32], ctypes.c_char_p),
@@ -472,6 +473,72 @@ def witness_fill(num_advice, n, fn):
     return cb
 
 
+# h2g_witness_source_multi.fill(ctx, circuit, phase, challenges, advice)
+WITNESS_FILL_MULTI = ctypes.CFUNCTYPE(ctypes.c_int, VP, U32, U32, U64P, U64P)
+
+
+class WitnessSourceMulti(ctypes.Structure):
+    """struct h2g_witness_source_multi (include/h2g.h)"""
+    _fields_ = [("ctx", VP), ("fill", WITNESS_FILL_MULTI)]
+
+
+def witness_fill_multi(num_advice, n, fns):
+    """fns[c](phase, challenges) -> {column: values} per circuit c (see witness_fill) as a
+    WITNESS_FILL_MULTI callback"""
+    single = [witness_fill(num_advice, n, f) for f in fns]
+
+    def cb(ctx, circuit, phase, ch_p, adv_p):
+        if circuit >= len(single):
+            return 1
+        single[circuit].num_challenges = cb.num_challenges
+        return single[circuit](ctx, phase, ch_p, adv_p)
+
+    cb.num_challenges = 0
+    return cb
+
+
+# h2g_rng: RngCore::fill_bytes and F::random of the caller's RNG
+RNG_FILL = ctypes.CFUNCTYPE(ctypes.c_int, VP, ctypes.POINTER(ctypes.c_uint8), SZ)
+RNG_FR = ctypes.CFUNCTYPE(ctypes.c_int, VP, U64P)
+
+
+class Rng(ctypes.Structure):
+    """struct h2g_rng (include/h2g.h)"""
+    _fields_ = [("ctx", VP), ("fill_bytes", RNG_FILL), ("random_fr", RNG_FR)]
+
+
+def rng_callbacks(rng):
+    """(RNG_FILL, RNG_FR or None) of a Python RNG object: rng.fill_bytes(n) -> bytes, and
+    optionally rng.random_fr() -> 4 Montgomery limbs (F::random)"""
+    def fill(_ctx, out, n):
+        try:
+            b = bytes(rng.fill_bytes(int(n)))
+            if len(b) != n:
+                return 1
+            ctypes.memmove(out, b, n)
+            return 0
+        except Exception:  # noqa: BLE001 -- reported to the prover as a failed draw
+            return 1
+
+    def fr(_ctx, out):
+        try:
+            v = np.ascontiguousarray(rng.random_fr(), dtype=np.uint64)
+            ctypes.memmove(out, v.ctypes.data, 32)
+            return 0
+        except Exception:  # noqa: BLE001
+            return 1
+
+    return RNG_FILL(fill), (RNG_FR(fr) if hasattr(rng, "random_fr") else RNG_FR())
+
+
+class ProveInputs(ctypes.Structure):
+    """struct h2g_prove_inputs (include/h2g.h)"""
+    _fields_ = [("num_circuits", U32), ("advice", ctypes.POINTER(VP)), ("advice_on_device", I32),
+                ("witness", ctypes.POINTER(WitnessSourceMulti)), ("instance", ctypes.POINTER(VP)),
+                ("instance_lens", ctypes.POINTER(VP)), ("rng", ctypes.POINTER(Rng)),
+                ("rng_seed", ctypes.POINTER(ctypes.c_uint8)), ("vanishing_threads", U32)]
+
+
 def _ptr(a, t):
     return a.ctypes.data_as(t) if a is not None and a.size else None
 
@@ -641,6 +708,63 @@ class ProvingKey:
         check(lib().h2g_last_challenges(p64(ch), circ.num_challenges, ctypes.byref(cnt)))
         import h2g_circuit as hc
         return buf.raw[: ln.value], hc.mont_to_ints(ch[: cnt.value])
+
+    def create_proof_multi(self, wits, seed=bytes([7] * 32), rng=None, fills=None, vanishing_threads=8,
+                           multiopen="shplonk", advice_dev_ptrs=None):
+        """create_proof(params, pk, circuits, instances, rng, transcript) over several circuits
+        (halo2_proofs/src/plonk/prover.rs:19-36) -> proof bytes.  wits: one witness per circuit
+        (advice, or -- with fills -- only the instance columns); rng: None = ChaCha20Rng::from_seed(
+        seed), else an object with fill_bytes(n) (and optionally random_fr()); fills: per-circuit
+        fill(phase, challenges) -> {column: values} witness sources."""
+        check(lib().h2g_pk_set_multiopen(self.handle, {"shplonk": 0, "gwc": 1}[multiopen]))
+        circ = self.circ
+        nc = len(wits)
+        keep = []
+        adv_arr = (VP * nc)()
+        ins_arr = (VP * nc)()
+        lens_arr = (VP * nc)()
+        for c, wit in enumerate(wits):
+            if advice_dev_ptrs is not None:
+                adv_arr[c] = advice_dev_ptrs[c]
+            elif fills is None:
+                a = np.ascontiguousarray(wit.advice, dtype=np.uint64)
+                keep.append(a)
+                adv_arr[c] = a.ctypes.data if a.size else None
+            ins = np.ascontiguousarray(wit.instance, dtype=np.uint64) if circ.num_instance else np.zeros(4, np.uint64)
+            lens = np.ascontiguousarray(wit.instance_lens if circ.num_instance else np.zeros(1), dtype=np.uint32)
+            keep += [ins, lens]
+            ins_arr[c] = ins.ctypes.data
+            lens_arr[c] = lens.ctypes.data
+        inp = ProveInputs()
+        inp.num_circuits = nc
+        inp.advice = ctypes.cast(adv_arr, ctypes.POINTER(VP))
+        inp.advice_on_device = 1 if advice_dev_ptrs is not None else 0
+        inp.instance = ctypes.cast(ins_arr, ctypes.POINTER(VP))
+        inp.instance_lens = ctypes.cast(lens_arr, ctypes.POINTER(VP))
+        inp.vanishing_threads = vanishing_threads
+        if fills is not None:
+            cb = witness_fill_multi(circ.num_advice, circ.n, fills)
+            cb.num_challenges = circ.num_challenges
+            cfn = WITNESS_FILL_MULTI(cb)
+            src = WitnessSourceMulti(None, cfn)
+            keep += [cb, cfn, src]
+            inp.witness = ctypes.pointer(src)
+        if rng is not None:
+            fb, fr = rng_callbacks(rng)
+            r = Rng(None, fb, fr)
+            keep += [fb, fr, r]
+            inp.rng = ctypes.pointer(r)
+        sd = (ctypes.c_uint8 * 32)(*bytes(seed))
+        keep.append(sd)
+        inp.rng_seed = ctypes.cast(sd, ctypes.POINTER(ctypes.c_uint8))
+        cap = nc * 32 * (64 + 8 * (circ.num_advice + 4 * len(circ.perm_columns)) + 64 * 64
+                         + 16 * (len(circ.lookups) + len(circ.shuffles))) + 32 * 8 * circ.num_fixed
+        buf = ctypes.create_string_buffer(cap)
+        ln = SZ()
+        check(lib().h2g_create_proof_multi(self.params.handle, self.handle, ctypes.byref(inp), buf, cap,
+                                           ctypes.byref(ln)))
+        del keep
+        return buf.raw[: ln.value]
 
     def close(self):
         if self.handle:

@@ -631,3 +631,140 @@ def challenge_circuit(k=6, seed=6, extended=False):
     else:
         wit = Witness(np.zeros((2, n, 4), dtype=np.uint64), np.zeros((0, n, 4), dtype=np.uint64), [])
     return circ, wit, fill
+
+
+def my_circuit(k=6, input_value=42):
+    """The MyCircuit shape of halo2_proofs/tests/frontend_backend_split.rs:33-465 (WIDTH_FACTOR
+    1, one synthesize_unit), compiled by hand: advice a, b, c (first phase), e (second phase);
+    fixed d, s_lookup, s_ltable, s_shuffle, s_stable and the selectors s_gate, s_rlc as fixed
+    columns (the frontend's selector compression is not restated); one instance column.
+      gate_a   s_gate (a + b c d - a[next])
+      lookup   [s_lookup, s_lookup a, s_lookup b] in [s_ltable, s_ltable d, s_ltable c]
+      shuffle  [s_shuffle, s_shuffle a] ~ [s_stable, s_stable b]
+      gate_rlc s_rlc (a + ch b - e), s_rlc (c + ch d - e)   (ch: a FirstPhase challenge)
+    equality on a, b, d, instance; the unit's cells and copies as synthesize_unit assigns them
+    (:236-409); the instance column is MyCircuit::instance() (:114-131).
+    -> (circuit, instance-only witness, fill(phase, challenges) -> {column: values})"""
+    n = 1 << k
+    A, B, C, E = range(4)
+    D, SL, ST, SS, SSt, SG, SR = range(7)
+    ch = challenge(0)
+    one = const(1)
+    gates = [fixed(SG) * (advice(A) + advice(B) * advice(C) * fixed(D) - advice(A, 1)),
+             fixed(SR) * (advice(A) + ch * advice(B) - advice(E)),
+             fixed(SR) * (advice(C) + ch * fixed(D) - advice(E))]
+    lookups = [([one * fixed(SL), advice(A) * fixed(SL), advice(B) * fixed(SL)],
+                [one * fixed(ST), fixed(D) * fixed(ST), advice(C) * fixed(ST)])]
+    shuffles = [([one * fixed(SS), advice(A) * fixed(SS)], [one * fixed(SSt), advice(B) * fixed(SSt)])]
+    perm = [(ADVICE, A), (ADVICE, B), (FIXED, D), (INSTANCE, 0)]
+    a, b, c = [0] * n, [0] * n, [0] * n
+    fx = [[0] * n for _ in range(7)]
+    rlc_rows = []
+    copies = [(INSTANCE, 0, 0, ADVICE, A, 0)]   # assign_advice_from_instance(instance, 0, a, 0)
+    off = 0
+
+    def gate(av, bv, cv, dv):
+        nonlocal off
+        fx[SG][off] = 1
+        if av is not None:
+            a[off] = av
+        b[off], c[off], fx[D][off] = bv, cv, dv
+        a[off + 1] = (a[off] + bv * cv * dv) % R_MOD
+        cells = (off, off)
+        off += 1
+        return cells
+
+    a[0] = input_value
+    inst_rows = []
+    for bcd in ((3, 4, 1), (6, 7, 1), (8, 9, 1)):
+        gate(None, *bcd)
+        inst_rows.append((ADVICE, A, off))
+    gate(None, 0xffffffff, 0xdeadbeef, 1)
+    gate(None, 0xabad1d3a, 0x12345678, 0x42424242)
+    off += 1
+    r1 = off
+    gate(5, 2, 1, 1)
+    off += 1
+    r2 = off
+    gate(2, 3, 1, 1)
+    off += 1
+    r3 = off
+    gate(4, 2, 1, 1)
+    off += 1
+    copies += [(ADVICE, B, r1, ADVICE, A, r2), (ADVICE, A, r2, ADVICE, B, r3)]
+    inst_rows += [(ADVICE, B, r1), (ADVICE, A, r2)]
+    r1 = off
+    gate(5, 9, 1, 9)
+    off += 1
+    r2 = off
+    gate(2, 9, 1, 1)
+    off += 1
+    r3 = off
+    gate(9, 2, 1, 1)
+    off += 1
+    copies += [(ADVICE, B, r1, FIXED, D, r1), (ADVICE, B, r2, FIXED, D, r1), (ADVICE, A, r3, FIXED, D, r1)]
+    lk = [(2, 4), (2, 4), (10, 1024), (0, 1), (2, 4)]
+    for i in range(11):
+        fx[SL][off] = fx[ST][off] = 1
+        a[off], b[off] = lk[i] if i < len(lk) else (0, 1)
+        fx[D][off], c[off] = i, 2 ** i
+        off += 1
+    for abcd in ((3, 5, 3, 5), (8, 9, 8, 9), (111, 222, 111, 222)):
+        fx[SR][off] = 1
+        rlc_rows.append((off, abcd[0], abcd[1]))
+        gate(*abcd)
+        off += 1
+    shuf = [0, 2, 4, 6, 8, 10, 12, 14, 1, 3, 5, 7, 9, 11, 13, 15]
+    for i in range(16):
+        fx[SS][off] = fx[SSt][off] = 1
+        a[off], b[off] = shuf[i], i
+        off += 1
+    # layouter.constrain_instance(instance_copy[i], instance, 1 + i)
+    copies += [(t, col, r, INSTANCE, 0, 1 + i) for i, (t, col, r) in enumerate(inst_rows)]
+    inst = [input_value]
+    for bcd in ((3, 4, 1), (6, 7, 1), (8, 9, 1)):
+        inst.append((inst[-1] + bcd[0] * bcd[1] * bcd[2]) % R_MOD)
+    inst += [2, 2]
+    circ = Circuit(k, 4, 7, 1, gates, perm, copies, np.stack([ints_to_mont(v) for v in fx]),
+                   name=f"MyCircuit shape k={k}", lookups=lookups, shuffles=shuffles,
+                   advice_phase=[0, 0, 0, 1], challenge_phase=[0])
+    assert off <= circ.usable_rows(), "the unit must fit in the usable rows"
+    wit = Witness(np.zeros((4, n, 4), dtype=np.uint64), ints_to_mont(inst + [0] * (n - len(inst)))[None],
+                  [len(inst)])
+
+    def e_values(chs):
+        e = [0] * n
+        for r, av, bv in rlc_rows:
+            e[r] = (av + chs[0] * bv) % R_MOD
+        return e
+
+    def fill(phase, chs):
+        if phase == 0:
+            return {A: ints_to_mont(a), B: ints_to_mont(b), C: ints_to_mont(c)}
+        return {E: ints_to_mont(e_values(chs))}
+
+    def full(chs):
+        return Witness(np.stack([ints_to_mont(v) for v in (a, b, c, e_values(chs))]), wit.instance,
+                       wit.instance_lens)
+
+    fill.full = full
+    return circ, wit, fill
+
+
+# OneNg (halo2_proofs/tests/frontend_backend_split.rs:477-489): a BlockRng whose every u32
+# is 1, so every Fr::random is LE512(01 00 00 00 x 16) mod r
+ONE_NG_FR = 0x0fdd950c1da3e00b1d2fb9cf61452b1ec0c9dfb910ecfb36b574601aedf0313b
+
+
+class OneNg:
+    """the reference's deterministic test RNG as an h2g_rng source (fill_bytes only)"""
+
+    def fill_bytes(self, n):
+        return (b"\x01\x00\x00\x00" * ((n + 3) // 4))[:n]
+
+
+class OneNgFr(OneNg):
+    """OneNg with F::random answered directly (the shim's random_fr path)"""
+
+    def random_fr(self):
+        return np.asarray(fr_to_limbs(ONE_NG_FR), dtype=np.uint64)
