@@ -17,7 +17,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(REPO, "yet-another-halo2-fork_amd"), os.path.join(REPO, "tests")]
+sys.path[:0] = [REPO, os.path.join(REPO, "yet-another-halo2-fork_amd"), os.path.join(REPO, "tests")]
 import numpy as np  # noqa: E402
 
 
@@ -28,12 +28,22 @@ def main():
     ap.add_argument("--modes", default="all,faithful")
     ap.add_argument("--faithful-max-k", type=int, default=20)
     ap.add_argument("--out", default="")
+    ap.add_argument("--no-warmup", action="store_true")
     a = ap.parse_args()
     import _oracle as O  # the checker's CPU restatement, timed here as the baseline
     import bench
     import h2g
     import h2g_circuit as hc
 
+    import threading
+
+    def heartbeat():  # a progress line every minute (long faithful-mode runs)
+        t0 = time.time()
+        while True:
+            time.sleep(60)
+            print(f"  ... {time.time() - t0:.0f} s", flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     h2g.init()
     model, ncpu = bench.cpu_info()
     T = min(16, ncpu)
@@ -48,7 +58,8 @@ def main():
             if mode == "faithful" and k > a.faithful_max_k:
                 continue
             O.lib().or_set_kernel_threads(1 if mode == "faithful" else 0)
-            O.create_proof(circ, wit, g, gl, threads=T, keygen=kg)  # warm-up
+            if not a.no_warmup:
+                O.create_proof(circ, wit, g, gl, threads=T, keygen=kg)  # warm-up
             ts = []
             for _ in range(a.reps):
                 t0 = time.perf_counter()

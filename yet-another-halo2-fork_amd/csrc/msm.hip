@@ -7,10 +7,10 @@
 // Pipeline (one stream, no host round trips):
 //   1. digits     : Montgomery -> canonical, signed c-bit windows (|d| <= 2^(c-1)),
 //                   key = window*NB + |d|-1, value = point index | sign << 31,
-//                   packed as one u64 entry (key << 32 | value)
-//   2. sort       : LSD radix sort of the entries over the key bits only (rocprim,
-//                   keys-only: 1.07 vs 1.29 ms for separate key/value arrays at
-//                   13 x 2^22 entries, tools/microbench/radix_cfg.hip)
+//                   packed as one u64 entry (key << 32 | value); zero digits dropped
+//   2. partition  : two counting rounds group the entries by key (coarse bins from the
+//                   scalars directly, then keys inside each bin) -- the accumulation
+//                   needs buckets contiguous, not sorted
 //   3. accumulate : the sorted array is cut into fixed chunks of L entries, one
 //                   thread per chunk (every thread does exactly L mixed additions,
 //                   whatever the bucket sizes -> no load imbalance, also for skewed
@@ -30,8 +30,6 @@
 //                   ~250 doublings is latency-bound on the GPU), else one device lane.
 // The result is the unique affine point, so it is bit-identical to any other
 // correct MSM (e.g. the CPU restatement in oracle/) regardless of summation order.
-#include <hipcub/hipcub.hpp>
-
 #include <stdlib.h>
 
 #include "msm.h"
@@ -69,19 +67,31 @@ __device__ __forceinline__ G1Affine ld_aff(const G1Affine* p) {
   return r;
 }
 
-// 1. signed digits ----------------------------------------------------------
-// Generic mode: key = window * NB + |d| - 1, value = point index.  Fixed-base mode
-// (bases pre-multiplied per window, table[w * stride + i] = [2^(c w)] P_i): every
-// window shares one set of NB buckets, key = |d| - 1, value = w * stride + i.
+// 1. signed digits: key = window * NB + |d| - 1 (generic mode), value = point index.
+// Fixed-base mode (bases pre-multiplied per window, table[w * stride + i] = [2^(c w)] P_i):
+// every window shares one set of NB buckets, key = |d| - 1, value = w * stride + i.
 // Batched fixed-base mode (blockIdx.y = b of nbatch MSMs over the same windows): MSM b
-// owns bucket set b, key = b * NB + |d| - 1, so one sort / accumulation / reduction
-// serves them all.
-__global__ void __launch_bounds__(MSM_THREADS)
-msm_digits_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride,
-                  uint64_t* __restrict__ ent) {
-  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t bi = blockIdx.y;  // which MSM of the batch
+// owns bucket set b, key = b * NB + |d| - 1, so one partition / accumulation / reduction
+// serves them all.  Negative digits set bit 31 of the value.
+// 2. bucket partition of the entries ------------------------------------------------
+// The accumulation needs each bucket's entries contiguous, not sorted: a two-round
+// counting partition replaces the radix sort.  Round 1 splits by the key's high bits
+// (coarse bins) straight from the scalars, round 2 by the low FB bits inside each coarse
+// bin (a bin's region is a few hundred KB, so its scattered writes stay in L2).  Zero
+// digits produce no entry at all.  Order inside a bucket is arbitrary (the sum is exact).
+static constexpr int PT = 512;          // threads of the coarse kernels (one scalar each)
+static constexpr int PWG = 16;          // windows per coarse-kernel thread (grid.z groups)
+static constexpr int FT = 256;          // threads of the fine kernels
+static constexpr int FPER = 16;         // entries per fine-kernel thread
+static constexpr uint32_t FTILE = (uint32_t)FT * FPER;
+static constexpr int FB_MAX = 11;       // fine bits
+static constexpr int COARSE_MAX = 2048;  // coarse bins (keys < 2^22)
+
+// the signed digits of scalar i (batch bi) for windows [w0, w0 + PWG): fn(slot, key, val)
+// for each nonzero digit (same key / value encoding as msm_digits_kernel)
+template <class Fn>
+__device__ __forceinline__ void scalar_digits(const MsmScalarList& list, size_t n, int c, int W, uint32_t NB,
+                                              int fixed, size_t stride, uint32_t bi, size_t i, int w0, Fn fn) {
   const uint4* q = reinterpret_cast<const uint4*>(list.p[bi] + i);
   uint4 a = q[0], b = q[1];
   Fr s;
@@ -90,28 +100,193 @@ msm_digits_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, int f
   Fr v = to_canonical(s);
   const uint32_t mask = (1u << c) - 1;
   const uint32_t half = 1u << (c - 1);
-  const uint32_t sentinel = fixed ? gridDim.y * NB : (uint32_t)W * NB;
-  uint64_t* out = ent + (size_t)bi * W * n;
   uint32_t carry = 0;
-  for (int w = 0; w < W; w++) {
-    uint32_t d = (v.l[0] & mask) + carry;
-    // shift the 256-bit value right by c (c < 32)
+  const int wend = w0 + PWG < W ? w0 + PWG : W;
+  for (int w = 0; w < wend; w++) {
+    const uint32_t d = (v.l[0] & mask) + carry;
 #pragma unroll
     for (int k = 0; k < 7; k++) v.l[k] = (v.l[k] >> c) | (v.l[k + 1] << (32 - c));
     v.l[7] >>= c;
-    const uint32_t koff = fixed ? bi * NB : (uint32_t)w * NB;
-    uint32_t key, val = fixed ? (uint32_t)((size_t)w * stride + i) : (uint32_t)i;
+    uint32_t mag, sign;
     if (d > half) {  // negative digit d - 2^c (d == 2^c gives digit 0, carry 1)
-      const uint32_t mag = (1u << c) - d;
+      mag = (1u << c) - d;
       carry = 1;
-      key = mag ? koff + mag - 1 : sentinel;
-      val |= 0x80000000u;
+      sign = 0x80000000u;
     } else {
+      mag = d;
       carry = 0;
-      key = d ? koff + d - 1 : sentinel;
+      sign = 0;
     }
-    out[(size_t)w * n + i] = ((uint64_t)key << 32) | val;
+    if (w < w0 || mag == 0) continue;
+    const uint32_t koff = fixed ? bi * NB : (uint32_t)w * NB;
+    const uint32_t val = (fixed ? (uint32_t)((size_t)w * stride + i) : (uint32_t)i) | sign;
+    fn(w - w0, koff + mag - 1, val);
   }
+}
+
+// round 1a: coarse histogram (LDS per block, one global atomic per bin and block)
+__global__ void __launch_bounds__(PT)
+msm_coarse_hist_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride, int fb,
+                       uint32_t ncoarse, uint32_t* __restrict__ ccount) {
+  __shared__ uint32_t h[COARSE_MAX];
+  for (uint32_t t = threadIdx.x; t < ncoarse; t += PT) h[t] = 0;
+  __syncthreads();
+  const size_t i = blockIdx.x * (size_t)PT + threadIdx.x;
+  if (i < n)
+    scalar_digits(list, n, c, W, NB, fixed, stride, blockIdx.y, i, blockIdx.z * PWG,
+                  [&](int, uint32_t key, uint32_t) { atomicAdd(&h[key >> fb], 1u); });
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < ncoarse; t += PT)
+    if (h[t]) atomicAdd(&ccount[t], h[t]);
+}
+
+// exclusive scan of cnt[0, len) (one block, len <= 1024 * 64): off[] = cursor[] =
+// prefix; *total = sum
+__global__ void __launch_bounds__(1024)
+msm_scan_kernel(const uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__ off,
+                uint32_t* __restrict__ cursor, uint32_t* __restrict__ total) {
+  __shared__ uint32_t part[1024];
+  const uint32_t per = (len + 1023) / 1024;
+  const uint32_t lo = threadIdx.x * per, hi = lo + per < len ? lo + per : len;
+  uint32_t s = 0;
+  for (uint32_t i = lo; i < hi; i++) s += cnt[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
+    const uint32_t v = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+  for (uint32_t i = lo; i < hi; i++) {
+    off[i] = run;
+    if (cursor) cursor[i] = run;
+    run += cnt[i];
+  }
+  if (threadIdx.x == 1023 && total) *total = part[1023];
+}
+
+// large scans (the per-key counts): 1024-element blocks scanned locally, block sums
+// scanned by msm_scan_kernel, then added back
+__global__ void __launch_bounds__(1024)
+msm_scan_block_kernel(const uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__ off,
+                      uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t part[1024];
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  const uint32_t v0 = i < len ? cnt[i] : 0;
+  part[threadIdx.x] = v0;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const uint32_t v = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  if (i < len) off[i] = part[threadIdx.x] - v0;
+  if (threadIdx.x == 1023) bsum[blockIdx.x] = part[1023];
+}
+__global__ void __launch_bounds__(1024)
+msm_scan_add_kernel(uint32_t* __restrict__ off, uint32_t len, const uint32_t* __restrict__ boff,
+                    uint32_t* __restrict__ cursor) {
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  if (i >= len) return;
+  const uint32_t v = off[i] + boff[blockIdx.x];
+  off[i] = v;
+  cursor[i] = v;
+}
+
+// round 1b: entries written into their coarse bins (ranks from LDS atomics, one global
+// reservation per bin and block)
+__global__ void __launch_bounds__(PT)
+msm_coarse_scatter_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride, int fb,
+                          uint32_t ncoarse, uint32_t* __restrict__ ccursor, uint64_t* __restrict__ out) {
+  __shared__ uint32_t cnt[COARSE_MAX], base[COARSE_MAX];
+  for (uint32_t t = threadIdx.x; t < ncoarse; t += PT) cnt[t] = 0;
+  __syncthreads();
+  uint64_t ent[PWG];
+  uint32_t rk[PWG];
+#pragma unroll
+  for (int k = 0; k < PWG; k++) rk[k] = ~0u;
+  const size_t i = blockIdx.x * (size_t)PT + threadIdx.x;
+  if (i < n)
+    scalar_digits(list, n, c, W, NB, fixed, stride, blockIdx.y, i, blockIdx.z * PWG,
+                  [&](int slot, uint32_t key, uint32_t val) {
+#pragma unroll
+                    for (int k = 0; k < PWG; k++)
+                      if (k == slot) {
+                        ent[k] = ((uint64_t)key << 32) | val;
+                        rk[k] = atomicAdd(&cnt[key >> fb], 1u);
+                      }
+                  });
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < ncoarse; t += PT)
+    if (cnt[t]) base[t] = atomicAdd(&ccursor[t], cnt[t]);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < PWG; k++)
+    if (rk[k] != ~0u) out[base[(uint32_t)(ent[k] >> 32) >> fb] + rk[k]] = ent[k];
+}
+
+// round 2a: per-key counts inside coarse bins: tiles of FTILE entries; entries of the
+// tile's first bin go through an LDS histogram, others (tiles straddling bins) directly
+__global__ void __launch_bounds__(FT)
+msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
+                     uint32_t* __restrict__ kcount) {
+  __shared__ uint32_t h[1 << FB_MAX];
+  const uint32_t total = *d_total;
+  const uint32_t lo = blockIdx.x * FTILE;
+  if (lo >= total) return;
+  const uint32_t nf = 1u << fb;
+  for (uint32_t t = threadIdx.x; t < nf; t += FT) h[t] = 0;
+  const uint32_t bin0 = (uint32_t)(in[lo] >> 32) >> fb;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < FPER; k++) {
+    const uint32_t p = lo + k * FT + threadIdx.x;
+    if (p >= total) break;
+    const uint32_t key = (uint32_t)(in[p] >> 32);
+    if ((key >> fb) == bin0) atomicAdd(&h[key & (nf - 1)], 1u);
+    else atomicAdd(&kcount[key], 1u);
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < nf; t += FT)
+    if (h[t]) atomicAdd(&kcount[(bin0 << fb) + t], h[t]);
+}
+
+// round 2b: the same tiles scattered to their keys' positions
+__global__ void __launch_bounds__(FT)
+msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
+                        uint32_t* __restrict__ kcursor, uint64_t* __restrict__ out) {
+  __shared__ uint32_t cnt[1 << FB_MAX], base[1 << FB_MAX];
+  const uint32_t total = *d_total;
+  const uint32_t lo = blockIdx.x * FTILE;
+  if (lo >= total) return;
+  const uint32_t nf = 1u << fb;
+  for (uint32_t t = threadIdx.x; t < nf; t += FT) cnt[t] = 0;
+  const uint32_t bin0 = (uint32_t)(in[lo] >> 32) >> fb;
+  __syncthreads();
+  uint64_t ent[FPER];
+  uint32_t rk[FPER];
+#pragma unroll
+  for (int k = 0; k < FPER; k++) {
+    const uint32_t p = lo + k * FT + threadIdx.x;
+    rk[k] = ~0u;
+    ent[k] = 0;
+    if (p < total) {
+      ent[k] = in[p];
+      const uint32_t key = (uint32_t)(ent[k] >> 32);
+      if ((key >> fb) == bin0) rk[k] = atomicAdd(&cnt[key & (nf - 1)], 1u);
+      else out[atomicAdd(&kcursor[key], 1u)] = ent[k];
+    }
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < nf; t += FT)
+    if (cnt[t]) base[t] = atomicAdd(&kcursor[(bin0 << fb) + t], cnt[t]);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < FPER; k++)
+    if (rk[k] != ~0u) out[base[(uint32_t)(ent[k] >> 32) & (nf - 1)] + rk[k]] = ent[k];
 }
 
 // 3-4. accumulation straight from the sorted entries -------------------------------
@@ -140,9 +315,10 @@ __device__ __forceinline__ void msm_emit(uint32_t key, const G1xyzz& acc, bool f
 // 16 VGPRs).
 template <bool PF>
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_acc_kernel(const G1Affine* __restrict__ bases, const uint64_t* __restrict__ ent, uint32_t total,
-               uint32_t sentinel, uint32_t L, G1xyzz* __restrict__ buckets, G1xyzz* __restrict__ bnd,
-               uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
+msm_acc_kernel(const G1Affine* __restrict__ bases, const uint64_t* __restrict__ ent,
+               const uint32_t* __restrict__ d_total, uint32_t sentinel, uint32_t L, G1xyzz* __restrict__ buckets,
+               G1xyzz* __restrict__ bnd, uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
+  const uint32_t total = *d_total;  // entries (nonzero digits) of the partition
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lo = t * L;
   if (lo >= total) return;
@@ -320,68 +496,119 @@ msm_big_combine_kernel(const uint4* __restrict__ multi, const uint32_t* __restri
   }
 }
 
-// 6. bucket reduction: F = sum_j (j+1) B_j per window, shallow ---------------------
-// A serial chain of XYZZ additions costs ~12 us on the GPU at low occupancy, so the
-// reduction minimises dependent depth, not work:
-//   rgroup : groups of RG buckets: S_g = sum_t (t+1) B_{RG g+t}, R_g = sum_t B_{RG g+t}
-//   rscale : V_g = S_g + [RG g] R_g   (F = sum_g V_g), block sums of V
-//   rfinal : sum of the block sums
-// depth ~ 2 RG + (log2(RG m) dbl + adds) + 2 x 8 tree steps.
-#ifndef H2G_MSM_RG
-#define H2G_MSM_RG 8
-#endif
-static constexpr int RG = H2G_MSM_RG;
-
-__global__ void __launch_bounds__(MSM_THREADS)
-msm_rgroup_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, G1xyzz* __restrict__ S,
-                  G1xyzz* __restrict__ R) {
-  const uint32_t w = blockIdx.y;
-  const uint32_t g = blockIdx.x * MSM_THREADS + threadIdx.x;
-  if (g >= m1) return;
-  const G1xyzz* b = B + (size_t)w * NB;
-  G1xyzz racc = G1xyzz::identity(), sacc = G1xyzz::identity();
-  for (int t = RG - 1; t >= 0; t--) {
-    const uint32_t j = g * RG + t;
-    if (j < NB) racc = xyzz_add(racc, b[j]);
-    sacc = xyzz_add(sacc, racc);
-  }
-  S[(size_t)w * m1 + g] = sacc;
-  R[(size_t)w * m1 + g] = racc;
+// 6. bucket reduction F = sum_{m=1}^{NB} m B_{m-1} per bucket set -----------------------
+// As a weighted sum WS(Y) = sum_t t Y_t (Y_t = B_{t-1}, Y_0 = 0) split by the low s bits
+// of t: WS(Y) = WS(V) + 2^s WS(U) with V_b = sum_{t mod 2^s = b} Y_t, U_a = sum_{t >> s = a} Y_t
+// -- plain sums, work ~2 NB additions at full occupancy, no per-group scalar
+// multiplications.  Two levels of splits leave four weighted sums of <= 64 points, each
+// done by one wave as the sum of its suffix sums (sum_t t Y_t = sum_{t >= 1} sum_{u >= t}
+// Y_u), scaled by doublings and added.  Latency-bound depth: ~11 (split 1) + ~7 (split 2)
+// + 12 (suffix scan + sum) + <= 21 doublings, against ~62 dependent point operations for
+// the previous group / scalar-multiplication / tree scheme.
+struct WsPlan {
+  uint32_t len0;         // NB + 1 (weights 0..NB)
+  int s1;                // first split
+  uint32_t nv1, nu1;     // V1, U1 lengths
+  int s2v, s2u;          // second splits of V1, U1
+  uint32_t nv2v, nu2v;   // V1 -> (V, U)
+  uint32_t nv2u, nu2u;   // U1 -> (V, U)
+  uint32_t per_set;      // points of level-1 + level-2 outputs per set
+};
+static int ceil_log2(uint64_t x) {
+  int b = 0;
+  while ((1ull << b) < x) b++;
+  return b;
+}
+static WsPlan ws_plan(uint32_t NB) {
+  WsPlan p;
+  p.len0 = NB + 1;
+  p.s1 = (ceil_log2(p.len0) + 1) / 2;
+  p.nv1 = 1u << p.s1;
+  p.nu1 = (p.len0 + p.nv1 - 1) >> p.s1;
+  p.s2v = (ceil_log2(p.nv1) + 1) / 2;
+  p.s2u = (ceil_log2(p.nu1) + 1) / 2;
+  p.nv2v = 1u << p.s2v;
+  p.nu2v = (p.nv1 + p.nv2v - 1) >> p.s2v;
+  p.nv2u = 1u << p.s2u;
+  p.nu2u = (p.nu1 + p.nv2u - 1) >> p.s2u;
+  p.per_set = p.nv1 + p.nu1 + p.nv2v + p.nu2v + p.nv2u + p.nu2u;
+  return p;
 }
 
-__global__ void __launch_bounds__(MSM_THREADS)
-msm_rscale_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R, uint32_t m1,
-                  G1xyzz* __restrict__ part, uint32_t nblk) {
-  __shared__ G1xyzz sh[MSM_THREADS];
-  const uint32_t w = blockIdx.y;
-  const uint32_t g = blockIdx.x * MSM_THREADS + threadIdx.x;
-  G1xyzz v = G1xyzz::identity();
-  if (g < m1) {
-    v = S[(size_t)w * m1 + g];
-    if (g) v = xyzz_add(v, xyzz_mul_u32(R[(size_t)w * m1 + g], g * RG));
-  }
-  sh[threadIdx.x] = v;
-  __syncthreads();
-  for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + h]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) part[(size_t)w * nblk + blockIdx.x] = sh[0];
-}
-
-__global__ void __launch_bounds__(MSM_THREADS)
-msm_rfinal_kernel(const G1xyzz* __restrict__ part, uint32_t nblk, G1xyzz* __restrict__ windows) {
-  __shared__ G1xyzz sh[MSM_THREADS];
-  const uint32_t w = blockIdx.x;
+// one block per output: o < nV -> V_o = sum_a Y_{a 2^s + o}; else U_{o - nV} = sum_b Y_{(o - nV) 2^s + b};
+// Y_t = in[set * in_stride + t - yoff] for t >= yoff (identity below), t < len
+template <int BT>
+__global__ void __launch_bounds__(BT)
+msm_wsplit_kernel(const G1xyzz* __restrict__ in, uint32_t in_stride, uint32_t yoff, uint32_t len, int s,
+                  uint32_t nV, G1xyzz* __restrict__ out, uint32_t out_stride) {
+  __shared__ G1xyzz sh[BT];
+  const uint32_t o = blockIdx.x;
+  const G1xyzz* y = in + (size_t)blockIdx.y * in_stride;
   G1xyzz acc = G1xyzz::identity();
-  for (uint32_t i = threadIdx.x; i < nblk; i += MSM_THREADS) acc = xyzz_add(acc, part[(size_t)w * nblk + i]);
+  if (o < nV) {
+    for (uint32_t t = ((uint32_t)threadIdx.x << s) + o; t < len; t += (uint32_t)BT << s)
+      if (t >= yoff) acc = xyzz_add(acc, y[t - yoff]);
+  } else {
+    const uint32_t lo = (o - nV) << s, hi = min(lo + (1u << s), len);
+    for (uint32_t t = lo + threadIdx.x; t < hi; t += BT)
+      if (t >= yoff) acc = xyzz_add(acc, y[t - yoff]);
+  }
   sh[threadIdx.x] = acc;
   __syncthreads();
-  for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
+#pragma unroll 1
+  for (int h = BT / 2; h > 0; h >>= 1) {
     if ((int)threadIdx.x < h) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + h]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) windows[w] = sh[0];
+  if (threadIdx.x == 0) out[(size_t)blockIdx.y * out_stride + o] = sh[0];
+}
+
+// per set: wave q < 4 computes X_q = sum_t t Y^q_t over its array (<= 64 points) and scales
+// it by 2^{e_q}; F = X_0 + X_1 + X_2 + X_3
+struct WsFinal {
+  uint32_t off[4], len[4];  // arrays inside the set's level-2 outputs
+  int e[4];                 // doublings
+};
+__global__ void __launch_bounds__(256)
+msm_wfinal_kernel(const G1xyzz* __restrict__ lv2, uint32_t stride, WsFinal f, G1xyzz* __restrict__ windows) {
+  __shared__ G1xyzz sh[256];
+  __shared__ G1xyzz res[4];
+  const int q = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const G1xyzz* y = lv2 + (size_t)blockIdx.x * stride + f.off[q];
+  G1xyzz* w = sh + 64 * q;
+  w[lane] = (uint32_t)lane < f.len[q] ? y[lane] : G1xyzz::identity();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+  for (int d = 1; d < 64; d <<= 1) {  // inclusive suffix scan S_t = sum_{u >= t} Y_u
+    const G1xyzz v = lane + d < 64 ? xyzz_add(w[lane], w[lane + d]) : w[lane];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    w[lane] = v;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (lane == 0) w[0] = G1xyzz::identity();  // sum_{t >= 1} S_t
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+  for (int h = 32; h > 0; h >>= 1) {
+    if (lane < h) w[lane] = xyzz_add(w[lane], w[lane + h]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (lane == 0) {
+    G1xyzz x = w[0];
+    for (int i = 0; i < f.e[q]; i++) x = xyzz_dbl(x);
+    res[q] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) windows[blockIdx.x] = xyzz_add(xyzz_add(res[0], res[1]), xyzz_add(res[2], res[3]));
 }
 
 // fixed-base tables: table[w * stride + i] = [2^(c w)] bases[i] --------------------
@@ -464,8 +691,8 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   if (total >= 0x80000000ull) return hipErrorInvalidValue;  // u32 positions in the sorted array
   const uint32_t L = item_len > 0 ? item_len : msm_chunk_len(total);
   const size_t nchunks = (total + L - 1) / L;
-  const uint32_t m1 = (NB + RG - 1) / RG;
-  const uint32_t nblk = (m1 + MSM_THREADS - 1) / MSM_THREADS;
+  const WsPlan wp = ws_plan(NB);
+  if (wp.nv2v > 64 || wp.nu2v > 64 || wp.nv2u > 64 || wp.nu2u > 64) return hipErrorInvalidValue;  // c <= 22
   // grow-only workspace: MSMs of slightly different shapes (e.g. n and n - 1 points, so
   // another chunk length) reuse it instead of reallocating (~2 ms of host stall each)
   struct Need {
@@ -480,7 +707,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
                          {&ws->item_bucket, icap * sizeof(MsmBigItem)},  // big-bucket items
                          {&ws->partials, 2 * nchunks * sizeof(G1xyzz)},  // boundary slots
                          {&ws->buckets, (size_t)nbt * sizeof(G1xyzz)},
-                         {&ws->segs, ((size_t)2 * m1 + nblk) * WB * sizeof(G1xyzz)},
+                         {&ws->segs, (size_t)wp.per_set * WB * sizeof(G1xyzz)},
                          {&ws->windows, (size_t)(W > WB ? W : WB) * sizeof(G1xyzz)},
                          {&ws->result, 16},                              // [0] items, [1] multi-item buckets
                          {&ws->item_off, mcap * sizeof(uint4)},          // multi-item buckets
@@ -503,29 +730,63 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   G1xyzz* ipart = (G1xyzz*)ws->total_items;
   G1xyzz* buckets = (G1xyzz*)ws->buckets;
   G1xyzz* bnd = (G1xyzz*)ws->partials;
-  G1xyzz* rS = (G1xyzz*)ws->segs;
-  G1xyzz* rR = rS + (size_t)WB * m1;
-  G1xyzz* rP = rR + (size_t)WB * m1;
+  G1xyzz* lv1 = (G1xyzz*)ws->segs;                    // per set: V1 | U1
+  G1xyzz* lv2 = lv1 + (size_t)WB * (wp.nv1 + wp.nu1);  // per set: V1 -> (V, U) | U1 -> (V, U)
 
+  // bucket partition geometry: keys < nbt, fine bits fb, coarse bins nbt >> fb
   int key_bits = 1;
-  while ((1ull << key_bits) <= (uint64_t)nbt) key_bits++;
-
-  size_t sort_bytes = 0;
-  H2G_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, keys_in, keys_out, (int)total, 32, 32 + key_bits,
-                                            st));
-  if (sort_bytes > ws->sort_tmp_bytes) {
-    H2G_TRY(grow(&ws->sort_tmp, sort_bytes));
-    ws->sort_tmp_bytes = sort_bytes;
+  while ((1ull << key_bits) < (uint64_t)nbt) key_bits++;
+  int fb = key_bits < FB_MAX ? key_bits : FB_MAX;
+  while (fb < 13 && (((uint64_t)nbt + (1ull << fb) - 1) >> fb) > COARSE_MAX) fb++;
+  const uint32_t nf = 1u << fb;
+  const uint32_t ncoarse = (uint32_t)((nbt + nf - 1) >> fb);
+  if (ncoarse > COARSE_MAX || fb > FB_MAX) return hipErrorInvalidValue;
+  const uint32_t kblocks = (nbt + 1023) / 1024;
+  // scratch (u32): ccount | coff | ccursor | total | kcount | koff | kcursor | block sums | block offsets
+  const size_t sort_words = 3 * (size_t)COARSE_MAX + 16 + 3 * (size_t)nbt + 2 * (size_t)kblocks + 16;
+  if (sort_words * 4 > ws->sort_tmp_bytes) {
+    H2G_TRY(grow(&ws->sort_tmp, sort_words * 4));
+    ws->sort_tmp_bytes = sort_words * 4;
   }
+  uint32_t* ccount = (uint32_t*)ws->sort_tmp;
+  uint32_t* coff = ccount + COARSE_MAX;
+  uint32_t* ccursor = coff + COARSE_MAX;
+  uint32_t* d_total = ccursor + COARSE_MAX;
+  uint32_t* kcount = d_total + 16;
+  uint32_t* koff = kcount + nbt;
+  uint32_t* kcursor = koff + nbt;
+  uint32_t* kbsum = kcursor + nbt;
+  uint32_t* kboff = kbsum + kblocks;
 
   const int T = MSM_THREADS;
   H2G_PHASE(0);
-  hipLaunchKernelGGL(msm_digits_kernel, dim3((unsigned)((n + T - 1) / T), (unsigned)nbatch), dim3(T), 0, st, list,
-                     n, c, W, NB, fixed, stride, keys_in);
-  H2G_TRY(hipGetLastError());
+  {  // round 1: coarse bins straight from the scalars
+    const dim3 g((unsigned)((n + PT - 1) / PT), (unsigned)nbatch, (unsigned)((W + PWG - 1) / PWG));
+    H2G_TRY(hipMemsetAsync(ccount, 0, (size_t)COARSE_MAX * 4, st));
+    hipLaunchKernelGGL(msm_coarse_hist_kernel, g, dim3(PT), 0, st, list, n, c, W, NB, fixed, stride, fb, ncoarse,
+                       ccount);
+    hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)ccount, ncoarse, coff, ccursor,
+                       d_total);
+    hipLaunchKernelGGL(msm_coarse_scatter_kernel, g, dim3(PT), 0, st, list, n, c, W, NB, fixed, stride, fb, ncoarse,
+                       ccursor, keys_in);
+    H2G_TRY(hipGetLastError());
+  }
   H2G_PHASE(1);
-  H2G_TRY(hipcub::DeviceRadixSort::SortKeys(ws->sort_tmp, sort_bytes, keys_in, keys_out, (int)total, 32,
-                                            32 + key_bits, st));
+  {  // round 2: keys inside the coarse bins
+    const unsigned tiles = (unsigned)((total + FTILE - 1) / FTILE);
+    H2G_TRY(hipMemsetAsync(kcount, 0, (size_t)nbt * 4, st));
+    hipLaunchKernelGGL(msm_fine_hist_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)keys_in,
+                       (const uint32_t*)d_total, fb, kcount);
+    hipLaunchKernelGGL(msm_scan_block_kernel, dim3(kblocks), dim3(1024), 0, st, (const uint32_t*)kcount, nbt, koff,
+                       kbsum);
+    hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)kbsum, kblocks, kboff,
+                       (uint32_t*)nullptr, (uint32_t*)nullptr);
+    hipLaunchKernelGGL(msm_scan_add_kernel, dim3(kblocks), dim3(1024), 0, st, koff, nbt, (const uint32_t*)kboff,
+                       kcursor);
+    hipLaunchKernelGGL(msm_fine_scatter_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)keys_in,
+                       (const uint32_t*)d_total, fb, kcursor, keys_out);
+    H2G_TRY(hipGetLastError());
+  }
   H2G_PHASE(2);
   H2G_TRY(hipMemsetAsync(counters, 0, 8, st));
   H2G_TRY(hipMemsetAsync(bstart, 0, (size_t)nbt * 4, st));  // empty buckets: start = end = 0
@@ -539,10 +800,10 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   const unsigned cgrid = (unsigned)((nchunks + T - 1) / T);
   if (prefetch)
     hipLaunchKernelGGL(msm_acc_kernel<true>, dim3(cgrid), dim3(T), 0, st, d_bases, (const uint64_t*)keys_out,
-                       (uint32_t)total, sentinel, L, buckets, bnd, bstart, bend);
+                       (const uint32_t*)d_total, sentinel, L, buckets, bnd, bstart, bend);
   else
     hipLaunchKernelGGL(msm_acc_kernel<false>, dim3(cgrid), dim3(T), 0, st, d_bases, (const uint64_t*)keys_out,
-                       (uint32_t)total, sentinel, L, buckets, bnd, bstart, bend);
+                       (const uint32_t*)d_total, sentinel, L, buckets, bnd, bstart, bend);
   H2G_PHASE(4);
   hipLaunchKernelGGL(msm_fixup_kernel, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend,
                      nbt, L, buckets, items, multi, counters);
@@ -551,12 +812,30 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   hipLaunchKernelGGL(msm_big_combine_kernel, dim3(MSM_BIG_BLOCKS / 4), dim3(T), 0, st, (const uint4*)multi,
                      (const uint32_t*)counters, (const G1xyzz*)ipart, buckets);
   H2G_PHASE(5);
-  hipLaunchKernelGGL(msm_rgroup_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1, rS,
-                     rR);
-  hipLaunchKernelGGL(msm_rscale_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
-                     (const G1xyzz*)rR, m1, rP, nblk);
-  hipLaunchKernelGGL(msm_rfinal_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rP, nblk,
-                     (G1xyzz*)ws->windows);
+  {
+    const uint32_t s1n = wp.nv1 + wp.nu1, s2n = wp.nv2v + wp.nu2v + wp.nv2u + wp.nu2u;
+    hipLaunchKernelGGL(msm_wsplit_kernel<256>, dim3(s1n, (unsigned)WB), dim3(256), 0, st, (const G1xyzz*)buckets, NB,
+                       1u, wp.len0, wp.s1, wp.nv1, lv1, s1n);
+    hipLaunchKernelGGL(msm_wsplit_kernel<64>, dim3(wp.nv2v + wp.nu2v, (unsigned)WB), dim3(64), 0, st,
+                       (const G1xyzz*)lv1, s1n, 0u, wp.nv1, wp.s2v, wp.nv2v, lv2, s2n);
+    hipLaunchKernelGGL(msm_wsplit_kernel<64>, dim3(wp.nv2u + wp.nu2u, (unsigned)WB), dim3(64), 0, st,
+                       (const G1xyzz*)(lv1 + wp.nv1), s1n, 0u, wp.nu1, wp.s2u, wp.nv2u, lv2 + wp.nv2v + wp.nu2v, s2n);
+    WsFinal f;  // F = X(V1.V) + 2^s2v X(V1.U) + 2^s1 (X(U1.V) + 2^s2u X(U1.U))
+    f.off[0] = 0;
+    f.len[0] = wp.nv2v;
+    f.e[0] = 0;
+    f.off[1] = wp.nv2v;
+    f.len[1] = wp.nu2v;
+    f.e[1] = wp.s2v;
+    f.off[2] = wp.nv2v + wp.nu2v;
+    f.len[2] = wp.nv2u;
+    f.e[2] = wp.s1;
+    f.off[3] = wp.nv2v + wp.nu2v + wp.nv2u;
+    f.len[3] = wp.nu2u;
+    f.e[3] = wp.s1 + wp.s2u;
+    hipLaunchKernelGGL(msm_wfinal_kernel, dim3((unsigned)WB), dim3(256), 0, st, (const G1xyzz*)lv2, s2n, f,
+                       (G1xyzz*)ws->windows);
+  }
   if (d_out && nbatch == 1)
     hipLaunchKernelGGL(msm_final_kernel, dim3(1), dim3(64), 0, st, (const G1xyzz*)ws->windows, WB, c, d_out);
   H2G_TRY(hipGetLastError());

@@ -1060,7 +1060,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         const int frc = in.src ? in.src->fill(in.src->ctx, (uint32_t)ci, (uint32_t)ph, chp, w.wit_pin)
                                : in.src1->fill(in.src1->ctx, (uint32_t)ph, chp, w.wit_pin);
         if (frc)
-          return fail(H2G_ERR_ARG, "create_proof: witness source failed at circuit " + std::to_string(ci) + " phase " +
+          return fail(H2G_ERR_ARG, "create_proof: witness source failed at " +
+                                       (ncirc > 1 ? "circuit " + std::to_string(ci) + " " : std::string()) + "phase " +
                                        std::to_string(ph));
         from = w.wit_pin;
         from_dev = false;
