@@ -2,6 +2,9 @@
 """Benchmark of the MI355X prover hot path (BASELINE.json metric:
 "create_proof wall-seconds at k=22 (BN254/KZG); MSM Mscalar-mul/s at 2^24").
 
+--workload keccak: the same over the keccak256-style circuit of BASELINE configs[4]
+(32 advice columns, 16 three-column lookups, degree 5) at k = 18.
+
 Default workload (--workload prove): one step = one full create_proof
 (KZG + SHPLONK + Blake2b) of the C3 synthetic circuit at k=22 (BASELINE configs[2]/[3]:
 3 advice a,b,c + 1 fixed f, gate f*(a*b - c), a,b,c in the permutation, copies
@@ -47,6 +50,7 @@ HBM_PEAK_GBS = 8000.0
 MSM_BYTES_PER_POINT = 96  # 32 B scalar + 64 B affine base
 MADD_MODMUL = 10          # XYZZ mixed add: 8M + 2S
 PROVE_K = 22
+KECCAK_K = 18  # BASELINE configs[4]: keccak256-style circuit (many columns, lookups) at k = 18
 METRIC = "create_proof wall-seconds at k=22 (BN254/KZG); MSM Mscalar-mul/s at 2^24"
 
 
@@ -189,9 +193,10 @@ def pmc_child(args):
     import h2g
 
     h2g.init([0])
-    if args.workload == "prove":
+    if args.workload in ("prove", "keccak"):
         import h2g_circuit as hc
-        circ, wit = hc.synthetic_c3(args.k, h2g.DeviceOps)
+        circ, wit = (hc.keccak_style(args.k, words=16) if args.workload == "keccak"
+                     else hc.synthetic_c3(args.k, h2g.DeviceOps))
         params = h2g.Params(args.k, s=np.asarray(hc.fr_to_limbs(0x1234567), dtype=np.uint64))
         pk = h2g.ProvingKey(params, circ)
         pk.create_proof(wit)
@@ -297,13 +302,24 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(s_int), dtype=np.uint64))
     if shard:  # fixed-base windows sized for this rank's point slab
         params.set_slab(*h2g_dist.slab(n, world, rank))
+    native = shard and args.transport == "native"
+    if native:  # the library's own RCCL communicators (csrc/comm.cpp); the id travels over torch
+        import torch as _t
+        uid = _t.zeros(256, dtype=_t.uint8, device=dev if dist.get_backend() == "nccl" else "cpu")
+        if rank == 0:
+            uid.copy_(_t.frombuffer(bytearray(h2g.comm_unique_id()), dtype=_t.uint8))
+        dist.broadcast(uid, 0)
+        h2g.comm_init(bytes(uid.cpu().numpy().tobytes()), world, rank)
     if worker:
-        slabs = h2g_dist.SlabWorker(dist, params=params)
+        slabs = None if native else h2g_dist.SlabWorker(dist, params=params)
     else:
-        circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=3 + seed_off)
+        if args.workload == "keccak":
+            circ, wit = hc.keccak_style(k, words=16, seed=5 + seed_off)
+        else:
+            circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=3 + seed_off)
         pk = h2g.ProvingKey(params, circ)
         adv = torch.from_numpy(np.ascontiguousarray(wit.advice).view(np.int64)).to(dev)  # resident witness
-        client = h2g_dist.SlabClient(dist, points=n) if shard else None
+        client = h2g_dist.SlabClient(dist, points=n) if shard and not native else None
     torch.cuda.synchronize()
     proofs = []
 
@@ -313,14 +329,21 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     def session(body):
         """rank 0 proves with the slab transport installed; peers serve until it stops"""
         if worker:
-            slabs.serve()
+            if native:
+                h2g.comm_serve(params)
+            else:
+                slabs.serve()
             return
-        if client:
+        if native:
+            h2g.comm_install(params)
+        elif client:
             client.install()
         try:
             body()
         finally:
-            if client:
+            if native:
+                h2g.comm_stop()
+            elif client:
                 client.uninstall()
                 client.stop()
 
@@ -383,15 +406,22 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             "scaling": "strong" if shard else "weak",
             "vs_baseline": None,
             "dtype": "u32 limbs (BN254 Fr/Fq Montgomery, 256-bit modular integer)",
-            "data": "synthetic C3 witness (random b, a_0; a_{i+1} = c_i = a_i b_i), SRS from a fixed s generated "
-                    "on device, prover rng ChaCha20([7; 32])",
-            "config": {"workload": f"create_proof (KZG/SHPLONK/Blake2b) of the C3 synthetic circuit at k={k} "
-                                   "(BASELINE configs[2]/[3])",
-                       "k": k, "advice": 3, "fixed": 1, "permutation_columns": 3, "degree": pk.degree,
+            "data": ("synthetic keccak-style witness (nibble xor chains, 16 lookups into a 3-column table)"
+                     if args.workload == "keccak" else
+                     "synthetic C3 witness (random b, a_0; a_{i+1} = c_i = a_i b_i)")
+                    + ", SRS from a fixed s generated on device, prover rng ChaCha20([7; 32])",
+            "config": {"workload": (f"create_proof (KZG/SHPLONK/Blake2b) of the keccak256-style circuit (32 advice, "
+                                    f"5 fixed, 16 lookups) at k={k} (BASELINE configs[4])"
+                                    if args.workload == "keccak" else
+                                    f"create_proof (KZG/SHPLONK/Blake2b) of the C3 synthetic circuit at k={k} "
+                                    "(BASELINE configs[2]/[3])"),
+                       "k": k, "advice": circ.num_advice, "fixed": circ.num_fixed,
+                       "lookups": len(circ.lookups), "permutation_columns": len(circ.perm_columns), "degree": pk.degree,
                        "extended_k": pk.extended_k, "proof_bytes": len(proofs[0]),
                        "parallelism": ("single GPU per proof" if world == 1 else
-                                       f"one proof over {world} GPUs: commitment MSMs in point slabs (RCCL p2p "
-                                       "slabs + partials), NTT/evaluate_h/SHPLONK on rank 0" if shard else
+                                       f"one proof over {world} GPUs: commitment MSMs in point slabs ("
+                                       + ("libh2g RCCL communicators" if native else "torch.distributed p2p")
+                                       + " slabs + partials), NTT/evaluate_h/SHPLONK on rank 0" if shard else
                                        f"{world} independent provers")},
             "roofline": roofline_from_phases(calls, phases, n_local, traffic, traffic_note),
             "msm_in_prover": {"launches_per_proof": calls // max(args.steps, 1), "avg_ms": round(msm_ms, 4),
@@ -402,11 +432,13 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             "stages_ms_synced_proof": {nm: round(ms, 3) for nm, ms in stages},
             "pcie_inclusive_s": round(pcie["s"], 4),
         }
-        if world == 1:
+        if world == 1 and args.workload == "prove":
             line["msm_2p24"] = measure_msm(h2g, torch, dev, 24, steps=10, warmup=2)
+    if native:
+        h2g.comm_destroy()
     if not worker:
         pk.close()
-    if line is not None and world == 1 and not args.no_cpu_baseline:
+    if line is not None and world == 1 and not args.no_cpu_baseline and args.workload == "prove":
         g, gl = params.export()
         params.close()
         cb = cpu_baseline_prove(circ, wit, g, gl, k, reps=args.cpu_reps)
@@ -538,8 +570,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=("prove", "msm"), default="prove")
-    ap.add_argument("--k", type=int, default=PROVE_K)
+    ap.add_argument("--workload", choices=("prove", "keccak", "msm"), default="prove")
+    ap.add_argument("--k", type=int, default=0, help="prove: 22 (C3), keccak: 18")
     ap.add_argument("--log-n", type=int, default=24)
     ap.add_argument("--window-bits", type=int, default=0, help="MSM workload: fixed-base window bits (0: auto)")
     ap.add_argument("--mode", choices=("shard", "replicas"), default="shard",
@@ -549,7 +581,11 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the PMC traffic passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl", help=argparse.SUPPRESS)
+    ap.add_argument("--transport", choices=("native", "torch"), default="native",
+                    help="shard mode: libh2g's own RCCL communicators, or torch.distributed slabs (h2g_dist)")
     args = ap.parse_args()
+    if not args.k:
+        args.k = KECCAK_K if args.workload == "keccak" else PROVE_K
     if args.pmc_child:
         return pmc_child(args)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -573,6 +609,7 @@ def main():
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if args.dist_backend == "gloo":  # rehearsal: ranks may share GPUs, host-staged exchanges
+            args.transport = "torch"  # RCCL refuses two ranks on one GPU
             local %= torch.cuda.device_count()
             torch.cuda.set_device(local)
             dist.init_process_group("gloo")
@@ -586,7 +623,7 @@ def main():
 
     h2g.init([torch.cuda.current_device()])
     dev = torch.device("cuda", torch.cuda.current_device())
-    run = run_prove if args.workload == "prove" else run_msm
+    run = run_msm if args.workload == "msm" else run_prove
     line = run(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note)
     if rank == 0:
         if not args.no_cpu_baseline and world == 1 and args.workload == "msm":

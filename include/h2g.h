@@ -346,6 +346,26 @@ int h2g_params_msm_dev(uint64_t params, int32_t base_set, uint64_t offset, uint6
 /* synchronous device-to-device copy (staging slabs for the transport) */
 int h2g_memcpy_dtod(void* d_dst, const void* d_src, size_t bytes);
 
+/* ---- the same sharding with the library's own RCCL transport (xGMI), no host callbacks:
+ * a Rust (or any) host binds these five calls and shards create_proof's MSMs natively.
+ * One process per GPU, each after h2g_init on its own device and with the same params:
+ *   rank 0:  h2g_comm_unique_id(id) -> the host sends the 256 bytes to every rank
+ *   all:     h2g_comm_init(id, world, rank)          (ncclCommInitRank x 2: slabs, partials)
+ *   rank 0:  h2g_comm_install(params)  -> create_proof shards every commitment MSM
+ *            ... h2g_create_proof* ...  -> h2g_comm_stop() ends the peers' sessions
+ *   ranks 1..: h2g_comm_serve(params, &served)     (returns when rank 0 stops)
+ *   all:     h2g_comm_destroy()
+ * Slab r = points [P r / world, P (r + 1) / world) of the params' P, as for
+ * h2g_shard_transport; rank 0 stages the peers' scalars with one device copy, sends them
+ * over one communicator and receives the 64-B partials over the other, so later MSMs'
+ * slabs stream while the peers compute.  The proof bytes do not depend on `world`. */
+int h2g_comm_unique_id(uint8_t id[256]);
+int h2g_comm_init(const uint8_t id[256], int world, int rank);
+int h2g_comm_install(uint64_t params);
+int h2g_comm_serve(uint64_t params, uint64_t* served);
+int h2g_comm_stop(void);
+int h2g_comm_destroy(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -136,3 +136,22 @@ def test_keccak_style_k18_proof_verifies():
         assert _rejects(circ, _tampered(proof, at), s_int, vk), at
     pk.close()
     params.close()
+
+
+@pytest.mark.timeout(900)
+def test_c3_k24_proof_verifies():
+    """north_star's k-range top (k = 24, extended domain 2^25): the device proof verifies
+    with the device verifying key (which equals the CPU-computed key at k = 18, 20, 22
+    above) and a tampered copy is rejected"""
+    k = 24
+    s_int = _s(k)
+    circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=24)
+    params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(s_int), dtype=np.uint64))
+    pk = h2g.ProvingKey(params, circ)
+    proof = pk.create_proof(wit)
+    assert len(proof) == 864 and pk.create_proof(wit) == proof
+    vk = _dev_vk(pk)
+    assert V.verify(circ, [], proof, s_int, vk=vk)
+    assert _rejects(circ, _tampered(proof, 32 * 11 + 3), s_int, vk)
+    pk.close()
+    params.close()

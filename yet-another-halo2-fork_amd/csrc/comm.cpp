@@ -1,0 +1,282 @@
+// comm.cpp -- native RCCL exchange of create_proof's MSM slabs across GPUs (see comm.h).
+//
+// The reference has no multi-GPU path; SURVEY 8e places the exchange at the commitment MSMs
+// (MsmAccel::msm, halo2_middleware/src/zal.rs:58, via ParamsKZG::commit / commit_lagrange,
+// halo2_backend/src/poly/kzg/commitment.rs:305-317,354-366): a sum over independent points,
+// so point slabs on different GPUs and one exchange of 64-B partials.  RCCL has no
+// elliptic-curve reduction, so the partials travel point-to-point and rank 0 adds them.
+#include "comm.h"
+
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "runtime.h"
+
+namespace h2g {
+namespace rt {
+namespace {
+
+#define NCCLCHK(expr)                                                                              \
+  do {                                                                                            \
+    ncclResult_t _r = (expr);                                                                     \
+    if (_r != ncclSuccess) return fail(H2G_ERR_DEVICE, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+
+static constexpr int RING = 16;  // outstanding MSMs on rank 0
+
+struct Slot {
+  bool busy = false;
+  uint64_t seq = 0;
+  void* stage = nullptr;  // the peers' scalars (device copy)
+  size_t cap = 0;
+  hipEvent_t copied = nullptr, done = nullptr;
+};
+
+struct Comm {
+  int world = 1, rank = 0, device = 0;
+  ncclComm_t tx = nullptr, rx = nullptr;
+  hipStream_t stx = nullptr, srx = nullptr;
+  // rank 0
+  uint64_t points = 0;             // the params' P (slab partition)
+  Slot slots[RING];
+  int64_t* h_hdr = nullptr;        // pinned [RING][world][5]
+  int64_t* d_hdr = nullptr;        // device mirror
+  int64_t* h_part = nullptr;       // pinned [RING][world][9]
+  int64_t* d_part = nullptr;
+  // ranks 1..
+  void* rstage[2] = {nullptr, nullptr};
+  size_t rcap[2] = {0, 0};
+  int rnext = 0;
+  int64_t *h_rhdr = nullptr, *d_rhdr = nullptr;  // one header
+  int64_t *h_rpart = nullptr, *d_rpart = nullptr;
+};
+Comm* g_comm = nullptr;
+
+size_t slab_lo(uint64_t P, uint64_t n, int world, int r) {  // prover.cpp shard_lo
+  const uint64_t b = (uint64_t)((unsigned __int128)P * (unsigned)r / (unsigned)world);
+  return b < n ? b : n;
+}
+
+int grow(void** p, size_t* cap, size_t bytes) {
+  if (bytes <= *cap) return H2G_OK;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  HIPCHK(hipMalloc(p, bytes ? bytes : 16));
+  *cap = bytes;
+  return H2G_OK;
+}
+
+}  // namespace
+
+int comm_unique_id(uint8_t id[COMM_ID_BYTES]) {
+  ncclUniqueId a, b;
+  NCCLCHK(ncclGetUniqueId(&a));
+  NCCLCHK(ncclGetUniqueId(&b));
+  std::memcpy(id, &a, sizeof(a));
+  std::memcpy(id + 128, &b, sizeof(b));
+  return H2G_OK;
+}
+
+int comm_init(const uint8_t id[COMM_ID_BYTES], int world, int rank) {
+  if (g_comm) return fail(H2G_ERR_STATE, "comm_init: a communicator exists (h2g_comm_destroy first)");
+  if (world < 2 || rank < 0 || rank >= world) return fail(H2G_ERR_ARG, "comm_init: bad world / rank");
+  Device* d = cur();
+  if (!d) return fail(H2G_ERR_STATE, "h2g_init has not been called");
+  HIPCHK(hipSetDevice(d->id));
+  auto c = std::make_unique<Comm>();
+  c->world = world;
+  c->rank = rank;
+  c->device = d->id;
+  ncclUniqueId a, b;
+  std::memcpy(&a, id, sizeof(a));
+  std::memcpy(&b, id + 128, sizeof(b));
+  NCCLCHK(ncclCommInitRank(&c->tx, world, a, rank));
+  NCCLCHK(ncclCommInitRank(&c->rx, world, b, rank));
+  HIPCHK(hipStreamCreateWithFlags(&c->stx, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&c->srx, hipStreamNonBlocking));
+  if (rank == 0) {
+    const size_t nh = (size_t)RING * world;
+    HIPCHK(hipHostMalloc((void**)&c->h_hdr, nh * 5 * 8, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&c->h_part, nh * 9 * 8, hipHostMallocDefault));
+    HIPCHK(hipMalloc((void**)&c->d_hdr, nh * 5 * 8));
+    HIPCHK(hipMalloc((void**)&c->d_part, nh * 9 * 8));
+    for (auto& s : c->slots) {
+      HIPCHK(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    }
+  } else {
+    HIPCHK(hipHostMalloc((void**)&c->h_rhdr, 5 * 8, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&c->h_rpart, 9 * 8, hipHostMallocDefault));
+    HIPCHK(hipMalloc((void**)&c->d_rhdr, 5 * 8));
+    HIPCHK(hipMalloc((void**)&c->d_rpart, 9 * 8));
+  }
+  g_comm = c.release();
+  return H2G_OK;
+}
+
+int comm_destroy() {
+  Comm* c = g_comm;
+  if (!c) return H2G_OK;
+  g_comm = nullptr;
+  (void)hipSetDevice(c->device);
+  if (c->stx) (void)hipStreamSynchronize(c->stx);
+  if (c->srx) (void)hipStreamSynchronize(c->srx);
+  if (c->tx) (void)ncclCommDestroy(c->tx);
+  if (c->rx) (void)ncclCommDestroy(c->rx);
+  for (auto& s : c->slots) {
+    if (s.stage) (void)hipFree(s.stage);
+    if (s.copied) (void)hipEventDestroy(s.copied);
+    if (s.done) (void)hipEventDestroy(s.done);
+  }
+  for (void* p : c->rstage)
+    if (p) (void)hipFree(p);
+  for (int64_t* p : {c->h_hdr, c->h_part, c->h_rhdr, c->h_rpart})
+    if (p) (void)hipHostFree(p);
+  for (int64_t* p : {c->d_hdr, c->d_part, c->d_rhdr, c->d_rpart})
+    if (p) (void)hipFree(p);
+  if (c->stx) (void)hipStreamDestroy(c->stx);
+  if (c->srx) (void)hipStreamDestroy(c->srx);
+  delete c;
+  return H2G_OK;
+}
+
+int comm_world() { return g_comm ? g_comm->world : 1; }
+int comm_rank() { return g_comm ? g_comm->rank : 0; }
+
+void* comm_transport_ctx(uint64_t points) {
+  if (!g_comm || g_comm->rank != 0) return nullptr;
+  g_comm->points = points;
+  return g_comm;
+}
+
+// rank 0: one MSM's slabs to the peers.  The scalars are final when this is called (the
+// prover synchronises its stream first); the prover stream is made to wait for the staging
+// copy, so later in-place work cannot race the sends.
+int comm_launch(void* ctx, uint64_t seq, int32_t base_set, uint64_t n, const void* d_scalars) {
+  Comm* c = static_cast<Comm*>(ctx);
+  if (!c || c != g_comm || c->rank != 0) return fail(H2G_ERR_STATE, "comm_launch: no rank-0 communicator");
+  int si = -1;
+  for (int i = 0; i < RING; i++)
+    if (!c->slots[(seq + i) % RING].busy) {
+      si = (int)((seq + i) % RING);
+      break;
+    }
+  if (si < 0) return fail(H2G_ERR_STATE, "comm_launch: too many outstanding sharded MSMs");
+  Slot& s = c->slots[si];
+  const int W = c->world;
+  const uint64_t lo1 = slab_lo(c->points, n, W, 1);
+  const size_t bytes = (size_t)(n - lo1) * 32;
+  RCCHK(grow(&s.stage, &s.cap, bytes));
+  if (bytes) HIPCHK(hipMemcpyAsync(s.stage, (const uint8_t*)d_scalars + lo1 * 32, bytes, hipMemcpyDeviceToDevice, c->stx));
+  HIPCHK(hipEventRecord(s.copied, c->stx));
+  Device* d = cur();
+  HIPCHK(hipStreamWaitEvent(d->stream, s.copied, 0));
+  int64_t* hh = c->h_hdr + (size_t)si * W * 5;
+  int64_t* dh = c->d_hdr + (size_t)si * W * 5;
+  for (int r = 1; r < W; r++) {
+    const uint64_t lo = slab_lo(c->points, n, W, r), hi = slab_lo(c->points, n, W, r + 1);
+    const int64_t h[5] = {COMM_OP_MSM, (int64_t)seq, base_set, (int64_t)lo, (int64_t)(hi - lo)};
+    std::memcpy(hh + 5 * r, h, sizeof(h));
+  }
+  HIPCHK(hipMemcpyAsync(dh + 5, hh + 5, (size_t)(W - 1) * 5 * 8, hipMemcpyHostToDevice, c->stx));
+  // headers, then slabs (a peer reads its header before it posts the slab's receive)
+  NCCLCHK(ncclGroupStart());
+  for (int r = 1; r < W; r++) NCCLCHK(ncclSend(dh + 5 * r, 5 * 8, ncclUint8, r, c->tx, c->stx));
+  NCCLCHK(ncclGroupEnd());
+  NCCLCHK(ncclGroupStart());
+  for (int r = 1; r < W; r++) {
+    const uint64_t lo = slab_lo(c->points, n, W, r), hi = slab_lo(c->points, n, W, r + 1);
+    if (hi > lo) NCCLCHK(ncclSend((const uint8_t*)s.stage + (lo - lo1) * 32, (hi - lo) * 32, ncclUint8, r, c->tx, c->stx));
+  }
+  NCCLCHK(ncclGroupEnd());
+  int64_t* dp = c->d_part + (size_t)si * W * 9;
+  NCCLCHK(ncclGroupStart());
+  for (int r = 1; r < W; r++) NCCLCHK(ncclRecv(dp + 9 * r, 9 * 8, ncclUint8, r, c->rx, c->srx));
+  NCCLCHK(ncclGroupEnd());
+  HIPCHK(hipMemcpyAsync(c->h_part + (size_t)si * W * 9 + 9, dp + 9, (size_t)(W - 1) * 9 * 8, hipMemcpyDeviceToHost,
+                        c->srx));
+  HIPCHK(hipEventRecord(s.done, c->srx));
+  s.busy = true;
+  s.seq = seq;
+  return H2G_OK;
+}
+
+int comm_collect(void* ctx, uint64_t seq, uint64_t* partials, int32_t* is_identity) {
+  Comm* c = static_cast<Comm*>(ctx);
+  if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm_collect: no communicator");
+  for (int i = 0; i < RING; i++) {
+    Slot& s = c->slots[i];
+    if (!s.busy || s.seq != seq) continue;
+    HIPCHK(hipEventSynchronize(s.done));
+    const int64_t* hp = c->h_part + (size_t)i * c->world * 9;
+    for (int r = 1; r < c->world; r++) {
+      std::memcpy(partials + 8 * (r - 1), hp + 9 * r, 64);
+      is_identity[r - 1] = hp[9 * r + 8] != 0;
+    }
+    s.busy = false;
+    return H2G_OK;
+  }
+  return fail(H2G_ERR_STATE, "comm_collect: unknown MSM " + std::to_string(seq));
+}
+
+int comm_stop() {
+  Comm* c = g_comm;
+  if (!c || c->rank != 0) return fail(H2G_ERR_STATE, "comm_stop: no rank-0 communicator");
+  for (auto& s : c->slots)
+    if (s.busy) HIPCHK(hipEventSynchronize(s.done));
+  const int W = c->world;
+  int64_t* hh = c->h_hdr;  // slot 0's header row (no launch is in flight)
+  for (int r = 1; r < W; r++) {
+    const int64_t h[5] = {COMM_OP_STOP, 0, 0, 0, 0};
+    std::memcpy(hh + 5 * r, h, sizeof(h));
+  }
+  HIPCHK(hipMemcpyAsync(c->d_hdr + 5, hh + 5, (size_t)(W - 1) * 5 * 8, hipMemcpyHostToDevice, c->stx));
+  NCCLCHK(ncclGroupStart());
+  for (int r = 1; r < W; r++) NCCLCHK(ncclSend(c->d_hdr + 5 * r, 5 * 8, ncclUint8, r, c->tx, c->stx));
+  NCCLCHK(ncclGroupEnd());
+  HIPCHK(hipStreamSynchronize(c->stx));
+  for (auto& s : c->slots) s.busy = false;
+  return H2G_OK;
+}
+
+int comm_next_request(int32_t* op, int32_t* base_set, uint64_t* lo, uint64_t* count, const void** d_slab,
+                      hipStream_t* ready) {
+  Comm* c = g_comm;
+  if (!c || c->rank == 0) return fail(H2G_ERR_STATE, "comm_next_request: no peer communicator");
+  NCCLCHK(ncclRecv(c->d_rhdr, 5 * 8, ncclUint8, 0, c->tx, c->stx));
+  HIPCHK(hipMemcpyAsync(c->h_rhdr, c->d_rhdr, 5 * 8, hipMemcpyDeviceToHost, c->stx));
+  HIPCHK(hipStreamSynchronize(c->stx));
+  const int64_t* h = c->h_rhdr;
+  *op = (int32_t)h[0];
+  *base_set = (int32_t)h[2];
+  *lo = (uint64_t)h[3];
+  *count = (uint64_t)h[4];
+  *d_slab = nullptr;
+  *ready = c->stx;
+  if (*op != COMM_OP_MSM || *count == 0) return H2G_OK;
+  const int b = c->rnext;
+  c->rnext ^= 1;
+  RCCHK(grow(&c->rstage[b], &c->rcap[b], (size_t)*count * 32));
+  NCCLCHK(ncclRecv(c->rstage[b], (size_t)*count * 32, ncclUint8, 0, c->tx, c->stx));
+  *d_slab = c->rstage[b];
+  return H2G_OK;
+}
+
+int comm_send_partial(const uint64_t partial[8], int32_t is_identity) {
+  Comm* c = g_comm;
+  if (!c || c->rank == 0) return fail(H2G_ERR_STATE, "comm_send_partial: no peer communicator");
+  HIPCHK(hipStreamSynchronize(c->srx));  // the previous partial left the pinned buffer
+  std::memcpy(c->h_rpart, partial, 64);
+  c->h_rpart[8] = is_identity ? 1 : 0;
+  HIPCHK(hipMemcpyAsync(c->d_rpart, c->h_rpart, 9 * 8, hipMemcpyHostToDevice, c->srx));
+  NCCLCHK(ncclSend(c->d_rpart, 9 * 8, ncclUint8, 0, c->rx, c->srx));
+  return H2G_OK;
+}
+
+}  // namespace rt
+}  // namespace h2g

@@ -1,0 +1,42 @@
+// comm.h -- native multi-GPU exchange over RCCL (xGMI) for one create_proof across several
+// GPUs, one process per GPU.  Rank 0 (the prover) splits every commitment MSM
+// into point slabs [P r / world, P (r + 1) / world) of the params' P points; the scalars of
+// slab r go to rank r, which answers with the 64-B affine partial sum of its slab.  Two
+// communicators keep the directions independent, so the slabs of later MSMs stream while
+// the peers compute earlier ones:
+//   tx (rank 0 -> r): header int64[5] = (op, seq, base_set, lo, count), then the slab
+//                     (count x 32 B, from a device staging copy of the prover's scalars)
+//   rx (r -> rank 0): int64[9] = affine partial (8 limbs) + identity flag
+// Definitions in comm.cpp; the peers' serve loop (h2g_comm_serve) lives in prover.cpp next
+// to the params it computes against.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace h2g {
+namespace rt {
+
+enum { COMM_OP_STOP = 0, COMM_OP_MSM = 1 };
+static constexpr int COMM_ID_BYTES = 256;  // two ncclUniqueIds (tx, rx)
+
+int comm_unique_id(uint8_t id[COMM_ID_BYTES]);
+int comm_init(const uint8_t id[COMM_ID_BYTES], int world, int rank);
+int comm_destroy();
+int comm_world();
+int comm_rank();
+
+// rank 0 (the h2g_shard_transport callbacks of a native transport; ctx = Comm state)
+int comm_launch(void* ctx, uint64_t seq, int32_t base_set, uint64_t n, const void* d_scalars);
+int comm_collect(void* ctx, uint64_t seq, uint64_t* partials, int32_t* is_identity);
+void* comm_transport_ctx(uint64_t points);  // the params' P of the slab partition
+int comm_stop();  // ends the peers' serve loops
+
+// ranks 1..: next request from rank 0.  op COMM_OP_MSM: *d_slab (device, count Fr) is
+// complete after the work queued on the stream *ready (the receive), until the next call.
+int comm_next_request(int32_t* op, int32_t* base_set, uint64_t* lo, uint64_t* count, const void** d_slab,
+                      hipStream_t* ready);
+int comm_send_partial(const uint64_t partial[8], int32_t is_identity);
+
+}  // namespace rt
+}  // namespace h2g

@@ -32,6 +32,9 @@
 // correct MSM (e.g. the CPU restatement in oracle/) regardless of summation order.
 #include <stdlib.h>
 
+#include <algorithm>
+#include <string>
+
 #include "msm.h"
 
 namespace h2g {
@@ -496,7 +499,71 @@ msm_big_combine_kernel(const uint4* __restrict__ multi, const uint32_t* __restri
   }
 }
 
-// 6. bucket reduction F = sum_{m=1}^{NB} m B_{m-1} per bucket set -----------------------
+// 6a. bucket reduction (default): F = sum_j (j+1) B_j per window, shallow ------------------
+// A serial chain of XYZZ additions costs ~12 us on the GPU at low occupancy, so the
+// reduction minimises dependent depth, not work:
+//   rgroup : groups of RG buckets: S_g = sum_t (t+1) B_{RG g+t}, R_g = sum_t B_{RG g+t}
+//   rscale : V_g = S_g + [RG g] R_g   (F = sum_g V_g), block sums of V
+//   rfinal : sum of the block sums
+// depth ~ 2 RG + (log2(RG m) dbl + adds) + 2 x 8 tree steps.
+#ifndef H2G_MSM_RG
+#define H2G_MSM_RG 8
+#endif
+static constexpr int RG = H2G_MSM_RG;
+
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_rgroup_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, G1xyzz* __restrict__ S,
+                  G1xyzz* __restrict__ R) {
+  const uint32_t w = blockIdx.y;
+  const uint32_t g = blockIdx.x * MSM_THREADS + threadIdx.x;
+  if (g >= m1) return;
+  const G1xyzz* b = B + (size_t)w * NB;
+  G1xyzz racc = G1xyzz::identity(), sacc = G1xyzz::identity();
+  for (int t = RG - 1; t >= 0; t--) {
+    const uint32_t j = g * RG + t;
+    if (j < NB) racc = xyzz_add(racc, b[j]);
+    sacc = xyzz_add(sacc, racc);
+  }
+  S[(size_t)w * m1 + g] = sacc;
+  R[(size_t)w * m1 + g] = racc;
+}
+
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_rscale_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R, uint32_t m1,
+                  G1xyzz* __restrict__ part, uint32_t nblk) {
+  __shared__ G1xyzz sh[MSM_THREADS];
+  const uint32_t w = blockIdx.y;
+  const uint32_t g = blockIdx.x * MSM_THREADS + threadIdx.x;
+  G1xyzz v = G1xyzz::identity();
+  if (g < m1) {
+    v = S[(size_t)w * m1 + g];
+    if (g) v = xyzz_add(v, xyzz_mul_u32(R[(size_t)w * m1 + g], g * RG));
+  }
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[(size_t)w * nblk + blockIdx.x] = sh[0];
+}
+
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_rfinal_kernel(const G1xyzz* __restrict__ part, uint32_t nblk, G1xyzz* __restrict__ windows) {
+  __shared__ G1xyzz sh[MSM_THREADS];
+  const uint32_t w = blockIdx.x;
+  G1xyzz acc = G1xyzz::identity();
+  for (uint32_t i = threadIdx.x; i < nblk; i += MSM_THREADS) acc = xyzz_add(acc, part[(size_t)w * nblk + i]);
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) windows[w] = sh[0];
+}
+
+// 6b. bucket reduction, alternative (H2G_MSM_RED=split): F = sum_{m=1}^{NB} m B_{m-1} ------
 // As a weighted sum WS(Y) = sum_t t Y_t (Y_t = B_{t-1}, Y_0 = 0) split by the low s bits
 // of t: WS(Y) = WS(V) + 2^s WS(U) with V_b = sum_{t mod 2^s = b} Y_t, U_a = sum_{t >> s = a} Y_t
 // -- plain sums, work ~2 NB additions at full occupancy, no per-group scalar
@@ -691,8 +758,14 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   if (total >= 0x80000000ull) return hipErrorInvalidValue;  // u32 positions in the sorted array
   const uint32_t L = item_len > 0 ? item_len : msm_chunk_len(total);
   const size_t nchunks = (total + L - 1) / L;
+  static const bool red_split = [] {
+    const char* e = getenv("H2G_MSM_RED");
+    return e && std::string(e) == "split";
+  }();
+  const uint32_t m1 = (NB + RG - 1) / RG;
+  const uint32_t nblk = (m1 + MSM_THREADS - 1) / MSM_THREADS;
   const WsPlan wp = ws_plan(NB);
-  if (wp.nv2v > 64 || wp.nu2v > 64 || wp.nv2u > 64 || wp.nu2u > 64) return hipErrorInvalidValue;  // c <= 22
+  if (red_split && (wp.nv2v > 64 || wp.nu2v > 64 || wp.nv2u > 64 || wp.nu2u > 64)) return hipErrorInvalidValue;
   // grow-only workspace: MSMs of slightly different shapes (e.g. n and n - 1 points, so
   // another chunk length) reuse it instead of reallocating (~2 ms of host stall each)
   struct Need {
@@ -707,7 +780,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
                          {&ws->item_bucket, icap * sizeof(MsmBigItem)},  // big-bucket items
                          {&ws->partials, 2 * nchunks * sizeof(G1xyzz)},  // boundary slots
                          {&ws->buckets, (size_t)nbt * sizeof(G1xyzz)},
-                         {&ws->segs, (size_t)wp.per_set * WB * sizeof(G1xyzz)},
+                         {&ws->segs, std::max<size_t>(wp.per_set, (size_t)2 * m1 + nblk) * WB * sizeof(G1xyzz)},
                          {&ws->windows, (size_t)(W > WB ? W : WB) * sizeof(G1xyzz)},
                          {&ws->result, 16},                              // [0] items, [1] multi-item buckets
                          {&ws->item_off, mcap * sizeof(uint4)},          // multi-item buckets
@@ -730,7 +803,10 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   G1xyzz* ipart = (G1xyzz*)ws->total_items;
   G1xyzz* buckets = (G1xyzz*)ws->buckets;
   G1xyzz* bnd = (G1xyzz*)ws->partials;
-  G1xyzz* lv1 = (G1xyzz*)ws->segs;                    // per set: V1 | U1
+  G1xyzz* rS = (G1xyzz*)ws->segs;  // default reduction: group sums, group weights, block sums
+  G1xyzz* rR = rS + (size_t)WB * m1;
+  G1xyzz* rP = rR + (size_t)WB * m1;
+  G1xyzz* lv1 = (G1xyzz*)ws->segs;                    // split reduction, per set: V1 | U1
   G1xyzz* lv2 = lv1 + (size_t)WB * (wp.nv1 + wp.nu1);  // per set: V1 -> (V, U) | U1 -> (V, U)
 
   // bucket partition geometry: keys < nbt, fine bits fb, coarse bins nbt >> fb
@@ -812,7 +888,14 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   hipLaunchKernelGGL(msm_big_combine_kernel, dim3(MSM_BIG_BLOCKS / 4), dim3(T), 0, st, (const uint4*)multi,
                      (const uint32_t*)counters, (const G1xyzz*)ipart, buckets);
   H2G_PHASE(5);
-  {
+  if (!red_split) {
+    hipLaunchKernelGGL(msm_rgroup_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1,
+                       rS, rR);
+    hipLaunchKernelGGL(msm_rscale_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
+                       (const G1xyzz*)rR, m1, rP, nblk);
+    hipLaunchKernelGGL(msm_rfinal_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rP, nblk,
+                       (G1xyzz*)ws->windows);
+  } else {
     const uint32_t s1n = wp.nv1 + wp.nu1, s2n = wp.nv2v + wp.nu2v + wp.nv2u + wp.nu2u;
     hipLaunchKernelGGL(msm_wsplit_kernel<256>, dim3(s1n, (unsigned)WB), dim3(256), 0, st, (const G1xyzz*)buckets, NB,
                        1u, wp.len0, wp.s1, wp.nv1, lv1, s1n);

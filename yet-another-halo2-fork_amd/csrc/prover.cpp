@@ -24,6 +24,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include "comm.h"
 #include "poly.h"
 #include "g2.h"
 #include "prover_kernels.h"
@@ -2502,6 +2503,75 @@ const char* h2g_prover_stage_name(int i) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (i < 0 || i >= (int)g_stages.size()) return "";
   return g_stages[i].first;
+}
+
+
+/* ---- native multi-GPU exchange (csrc/comm.cpp) --------------------------------------- */
+int h2g_comm_unique_id(uint8_t id[256]) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!id) return fail(H2G_ERR_ARG, "comm_unique_id: null id");
+  return comm_unique_id(id);
+}
+
+int h2g_comm_init(const uint8_t id[256], int world, int rank) {
+  NEED_DEV_P();
+  if (!id) return fail(H2G_ERR_ARG, "comm_init: null id");
+  return comm_init(id, world, rank);
+}
+
+int h2g_comm_destroy(void) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (g_shard.launch == comm_launch) g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
+  return comm_destroy();
+}
+
+int h2g_comm_install(uint64_t params) {
+  NEED_DEV_P();
+  auto ip = g_params.find(params);
+  if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  if (comm_world() < 2 || comm_rank() != 0) return fail(H2G_ERR_STATE, "comm_install: needs rank 0 of a communicator");
+  g_shard = h2g_shard_transport{comm_transport_ctx(ip->second->n), comm_world(), comm_launch, comm_collect};
+  g_shard_seq = 0;
+  return H2G_OK;
+}
+
+int h2g_comm_stop(void) {
+  NEED_DEV_P();
+  if (g_shard.launch == comm_launch) g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
+  return comm_stop();
+}
+
+/* ranks 1..: answer rank 0's MSM slabs against `params` until it stops the session */
+int h2g_comm_serve(uint64_t params, uint64_t* served) {
+  NEED_DEV_P();
+  auto ip = g_params.find(params);
+  if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  const Params& prm = *ip->second;
+  if (prm.device != d->id) return fail(H2G_ERR_ARG, "comm_serve: params live on another device");
+  uint64_t count = 0;
+  for (;;) {
+    int32_t op = 0, set = 0;
+    uint64_t lo = 0, cnt = 0;
+    const void* slab = nullptr;
+    hipStream_t ready = nullptr;
+    RCCHK(comm_next_request(&op, &set, &lo, &cnt, &slab, &ready));
+    if (op == COMM_OP_STOP) break;
+    if (op != COMM_OP_MSM || (set != SRS_G && set != SRS_LAGRANGE) || lo > prm.n || cnt > prm.n - lo)
+      return fail(H2G_ERR_STATE, "comm_serve: malformed request");
+    uint64_t out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (cnt) {
+      size_t toff = 0;
+      MsmTicket t;
+      RCCHK(msm_fixed_launch(d, slab, prm.tables(set, lo, cnt, &toff), toff, cnt, ready, &t));
+      RCCHK(msm_collect(d, &t, out));
+    }
+    uint64_t nz = 0;
+    for (uint64_t v : out) nz |= v;
+    RCCHK(comm_send_partial(out, nz == 0));
+    count++;
+  }
+  if (served) *served = count;
+  return H2G_OK;
 }
 
 }  // extern "C"

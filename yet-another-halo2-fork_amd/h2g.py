@@ -106,6 +106,12 @@ _SIGS = {
     "h2g_params_set_slab": ([U64, U64, U64], I32),
     "h2g_params_msm_dev": ([U64, ctypes.c_int32, U64, U64, VP, U64P, ctypes.POINTER(ctypes.c_int32)], I32),
     "h2g_memcpy_dtod": ([VP, VP, SZ], I32),
+    "h2g_comm_unique_id": ([ctypes.c_char_p], I32),
+    "h2g_comm_init": ([ctypes.c_char_p, I32, I32], I32),
+    "h2g_comm_install": ([U64], I32),
+    "h2g_comm_serve": ([U64, ctypes.POINTER(U64)], I32),
+    "h2g_comm_stop": ([], I32),
+    "h2g_comm_destroy": ([], I32),
 }
 
 MSM_PHASES = ("digits", "sort", "bucket_bounds", "accumulate", "bucket_fixup", "reduce")
@@ -830,6 +836,35 @@ def transport_errors():
     errs = list(_transport_keep[3])
     _transport_keep[3].clear()
     return errs
+
+
+# ------------------------------------------------- native RCCL transport (csrc/comm.cpp)
+def comm_unique_id():
+    buf = ctypes.create_string_buffer(256)
+    check(lib().h2g_comm_unique_id(buf))
+    return buf.raw
+
+
+def comm_init(uid, world, rank):
+    check(lib().h2g_comm_init(bytes(uid), world, rank))
+
+
+def comm_install(params):
+    check(lib().h2g_comm_install(params.handle))
+
+
+def comm_serve(params):
+    served = U64()
+    check(lib().h2g_comm_serve(params.handle, ctypes.byref(served)))
+    return served.value
+
+
+def comm_stop():
+    check(lib().h2g_comm_stop())
+
+
+def comm_destroy():
+    check(lib().h2g_comm_destroy())
 
 
 def params_msm_dev(params, base_set, offset, n, d_scalars):
