@@ -40,6 +40,8 @@ def _prove(pk, case, **kw):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", default="gloo")
+    ap.add_argument("--transport", default="torch", choices=("torch", "native"),
+                    help="h2g_dist over torch.distributed, or libh2g's RCCL communicators (nccl only)")
     ap.add_argument("cases", nargs="+")
     args = ap.parse_args()
     rank = int(os.environ["RANK"])
@@ -52,6 +54,13 @@ def main():
     else:
         dist.init_process_group("gloo")
     h2g.init([dev])
+    native = args.transport == "native"
+    if native:  # the library's communicators; the id travels over torch.distributed
+        uid = torch.zeros(256, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(h2g.comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        h2g.comm_init(bytes(uid.cpu().numpy().tobytes()), world, rank)
     results = {}
     for name in args.cases:
         case = CASES[name]()
@@ -62,18 +71,24 @@ def main():
             pk = h2g.ProvingKey(params, circ)
             want = [_prove(pk, case), _prove(pk, case, seed=bytes(range(32)), vanishing_threads=3)]
             params.set_slab(*D.slab(P, world, 0))
-            cl = D.SlabClient(dist, points=P)
-            cl.install()
+            if native:
+                h2g.comm_install(params)
+            else:
+                cl = D.SlabClient(dist, points=P)
+                cl.install()
             try:
                 got = [_prove(pk, case), _prove(pk, case, seed=bytes(range(32)), vanishing_threads=3)]
             finally:
-                D.SlabClient.uninstall()
-                cl.stop()
+                if native:
+                    h2g.comm_stop()
+                else:
+                    D.SlabClient.uninstall()
+                    cl.stop()
             results[name] = {"same": got == want, "bytes": len(got[0]), "msms": None}
             pk.close()
         else:
             params.set_slab(*D.slab(P, world, rank))
-            served = D.SlabWorker(dist, params=params).serve()
+            served = h2g.comm_serve(params) if native else D.SlabWorker(dist, params=params).serve()
             results[name] = {"served": served}
         params.close()
         dist.barrier()
@@ -90,6 +105,8 @@ def main():
         for i, nm in enumerate(args.cases):
             results[nm]["msms"] = [int(g[i]) for g in gathered[1:]]
         print("SHARD_RESULT " + json.dumps(results), flush=True)
+    if native:
+        h2g.comm_destroy()
     h2g.shutdown()
     dist.destroy_process_group()
 

@@ -22,10 +22,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(world, cases):
+def _gpus():
+    import torch
+    return torch.cuda.device_count()
+
+
+def _run(world, cases, backend="gloo", transport="torch"):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(HERE, "_shard_prove.py"), "--backend", "gloo"] + cases
+           os.path.join(HERE, "_shard_prove.py"), "--backend", backend, "--transport", transport] + cases
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
@@ -48,3 +53,16 @@ def test_sharded_proof_three_ranks():
     for nm in cases:
         assert res[nm]["same"], nm
         assert len(res[nm]["msms"]) == 2 and all(m > 0 for m in res[nm]["msms"]), (nm, res[nm])
+
+
+@pytest.mark.parametrize("transport", ["torch", "native"])
+def test_sharded_proof_rccl_two_gpus(transport):
+    """the RCCL paths (one GPU per rank): torch.distributed slabs, and libh2g's own
+    communicators (h2g_comm_*); needs >= 2 GPUs (RCCL refuses two ranks on one GPU)"""
+    if _gpus() < 2:
+        pytest.skip("needs two GPUs")
+    cases = ["simple_k6", "lookup_k11", "c3_k14", "challenge_k9"]
+    res = _run(2, cases, backend="nccl", transport=transport)
+    for nm in cases:
+        assert res[nm]["same"], nm
+        assert all(m > 0 for m in res[nm]["msms"]), (nm, res[nm])

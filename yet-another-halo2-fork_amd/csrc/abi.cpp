@@ -17,6 +17,8 @@
 #include <vector>
 
 #include "../../include/h2g.h"
+#include <hip/hip_ext.h>
+
 #include "runtime.h"
 #include "bn254.h"
 #include "msm.h"
@@ -184,6 +186,25 @@ int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_
   return H2G_OK;
 }
 
+// Optional CU masks (diagnostics / A/B): H2G_CU_MASK_MAIN / H2G_CU_MASK_MSM = 8 hex words
+// (CU 0 = bit 0 of the first), restricting the prover's main stream (NTTs, evaluate_h,
+// grand products) or the MSM streams to a subset of the 256 CUs.
+static hipError_t make_stream(hipStream_t* s, const char* env) {
+  const char* e = std::getenv(env);
+  if (!e || !*e) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  std::vector<uint32_t> mask;
+  std::string str(e);
+  size_t pos = 0;
+  while (pos < str.size() && mask.size() < 8) {
+    size_t nxt = str.find(',', pos);
+    if (nxt == std::string::npos) nxt = str.size();
+    mask.push_back((uint32_t)std::strtoul(str.substr(pos, nxt - pos).c_str(), nullptr, 16));
+    pos = nxt + 1;
+  }
+  while (mask.size() < 8) mask.push_back(mask.empty() ? 0xffffffffu : mask.back());
+  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+}
+
 // nb MSMs of n scalars each against the same fixed-base windows, launched as one batched
 // pipeline (msm_run_fixed_batch) on the next MSM stream; ticket b collects MSM b.
 int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFixedBase& fb, size_t off, size_t n,
@@ -191,7 +212,7 @@ int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFi
   if (nb < 1 || nb > MSM_MAX_BATCH) return fail(H2G_ERR_ARG, "msm: bad batch size");
   if (!d->h_ring) {
     HIPCHK(hipHostMalloc(&d->h_ring, MSM_RING * sizeof(G1xyzz), hipHostMallocDefault));
-    for (int i = 0; i < MSM_SLOTS; i++) HIPCHK(hipStreamCreateWithFlags(&d->mstream[i], hipStreamNonBlocking));
+    for (int i = 0; i < MSM_SLOTS; i++) HIPCHK(make_stream(&d->mstream[i], "H2G_CU_MASK_MSM"));
     for (int i = 0; i < MSM_RING; i++) HIPCHK(hipEventCreateWithFlags(&d->ring_ev[i], hipEventDisableTiming));
   }
   int rings[MSM_MAX_BATCH];
@@ -432,7 +453,7 @@ int h2g_init(const int* devices, int ndev) {
     auto dev = std::make_unique<Device>();
     dev->id = id;
     HIPCHK(hipSetDevice(id));
-    HIPCHK(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
+    HIPCHK(make_stream(&dev->stream, "H2G_CU_MASK_MAIN"));
     HIPCHK(ntt_init_attributes());
     g_devs.push_back(std::move(dev));
   }
