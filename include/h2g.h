@@ -139,8 +139,11 @@ int h2g_event_record(void* ev, void* stream);
 int h2g_event_elapsed_ms(void* start, void* stop, float* ms);
 
 /* ---- profiling: per-phase HIP-event times of MSM calls made while enabled.
- * Phases (in order): digits, sort, bucket_bounds, accumulate, bucket_sum, reduce.
- * collect() synchronises, returns the per-phase sums (ms) over `calls` MSMs and resets. */
+ * Phases (in order): partition_coarse (digits -> coarse bins), partition_fine (bins -> bucket
+ * order), bucket_bounds, accumulate, bucket_fixup, reduce.  collect() synchronises, returns the
+ * per-phase sums (ms) over `calls` MSMs and resets.  With max_phases >= 8, ms[6] and ms[7] are
+ * the busy time (union of the intervals) of the accumulate phases and of the whole MSMs:
+ * MSMs on the two MSM streams overlap, so work / union is the aggregate rate. */
 int h2g_profile_enable(int on);
 int h2g_profile_msm_collect(float* ms, int max_phases, int* n_phases, int* calls);
 

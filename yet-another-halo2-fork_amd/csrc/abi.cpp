@@ -6,8 +6,10 @@
 // lengths, commit's `bases.len() >= size`, EvaluationDomain's length asserts).
 // All arithmetic runs in the HIP kernels (msm.hip, ntt.hip, poly.hip, srs.hip);
 // there is no CPU fallback: without a usable device every call fails loudly.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -17,8 +19,6 @@
 #include <vector>
 
 #include "../../include/h2g.h"
-#include <hip/hip_ext.h>
-
 #include "runtime.h"
 #include "bn254.h"
 #include "msm.h"
@@ -958,6 +958,35 @@ int h2g_profile_msm_collect(float* ms, int max_phases, int* n_phases, int* calls
     *calls = c;
   }
   if (n_phases) *n_phases = np;
+  // ms[NPHASES], ms[NPHASES + 1] (when asked for): the union of the accumulate intervals and
+  // of the whole-MSM intervals over every recorded MSM -- the busy time of overlapping MSMs
+  // (two MSM streams), so that work / union is the aggregate rate, not the per-launch one
+  if (max_phases >= MSM_NPHASES + 2 && !g_msm_prof.empty()) {
+    const hipEvent_t ref = g_msm_prof.front().ev[0];
+    auto union_ms = [&](int a, int b) -> float {
+      std::vector<std::pair<float, float>> iv;
+      for (auto& pe : g_msm_prof) {
+        float s = 0.f, e = 0.f;
+        if (hipEventElapsedTime(&s, ref, pe.ev[a]) != hipSuccess) return -1.f;
+        if (hipEventElapsedTime(&e, ref, pe.ev[b]) != hipSuccess) return -1.f;
+        iv.emplace_back(s, e);
+      }
+      std::sort(iv.begin(), iv.end());
+      float tot = 0.f, cs = iv[0].first, ce = iv[0].second;
+      for (size_t i = 1; i < iv.size(); i++) {
+        if (iv[i].first > ce) {
+          tot += ce - cs;
+          cs = iv[i].first;
+          ce = iv[i].second;
+        } else if (iv[i].second > ce) {
+          ce = iv[i].second;
+        }
+      }
+      return tot + (ce - cs);
+    };
+    ms[MSM_NPHASES] = union_ms(3, 4);
+    ms[MSM_NPHASES + 1] = union_ms(0, MSM_NPHASES);
+  }
   for (auto& pe : g_msm_prof)
     for (auto& e : pe.ev) (void)hipEventDestroy(e);
   g_msm_prof.clear();

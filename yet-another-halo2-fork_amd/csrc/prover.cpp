@@ -22,7 +22,7 @@
 #include <functional>
 #include <set>
 
-#include <hipcub/hipcub.hpp>
+#include <rocprim/rocprim.hpp>
 
 #include "comm.h"
 #include "poly.h"
@@ -786,14 +786,14 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
     PALLOC(pool, pk.rep_rows, n);
     PALLOC(pool, pk.counters, 8);
     size_t b1 = 0, b2 = 0, b3 = 0;
-    HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(nullptr, b1, pk.ck_a, pk.ck_a2, (int)n, CanonLess(), st));
-    HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, b2, pk.ck_t2, pk.left_flag, pk.ck_left, pk.counters, (int)n, st));
-    HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, b3, hipcub::CountingInputIterator<uint32_t>(0), pk.rep_flag,
+    HIPCHK(rocprim::merge_sort(nullptr, b1, pk.ck_a, pk.ck_a2, (int)n, CanonLess(), st));
+    HIPCHK(rocprim::select(nullptr, b2, pk.ck_t2, pk.left_flag, pk.ck_left, pk.counters, (int)n, st));
+    HIPCHK(rocprim::select(nullptr, b3, rocprim::counting_iterator<uint32_t>(0), pk.rep_flag,
                                          pk.rep_rows, pk.counters + 1, (int)n, st));
     size_t b4 = 0, b5 = 0;
-    HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, b4, (uint64_t*)pk.ck_a, (uint64_t*)pk.ck_a + n, (int)n, 0, 64,
+    HIPCHK(rocprim::radix_sort_keys(nullptr, b4, (uint64_t*)pk.ck_a, (uint64_t*)pk.ck_a + n, (int)n, 0, 64,
                                              st));
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, b5, (uint64_t*)pk.ck_left, (uint64_t*)pk.ck_left + n,
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, b5, (uint64_t*)pk.ck_left, (uint64_t*)pk.ck_left + n,
                                               (uint32_t*)pk.ck_a, (uint32_t*)pk.ck_a + n, (int)n, 0, 48, st));
     pk.sort_tmp_bytes = std::max(std::max(std::max(b1, b4), b5), std::max(b2, b3));
     pk.lk_hb.assign(pk.NL, 64);
@@ -1155,9 +1155,9 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         uint64_t* kt = (uint64_t*)pk.ck_t;
         HIPCHK(lookup_keys(w.lk_a[l], u, 0, nullptr, ka, nullptr, flags, st));
         HIPCHK(lookup_keys(w.lk_s[l], u, 0, nullptr, kt, nullptr, flags, st));
-        HIPCHK(hipcub::DeviceRadixSort::SortKeys(pk.sort_tmp, tb, ka, ka + n, (int)u, 0, hb, st));
+        HIPCHK(rocprim::radix_sort_keys(pk.sort_tmp, tb, ka, ka + n, (int)u, 0, hb, st));
         tb = pk.sort_tmp_bytes;
-        HIPCHK(hipcub::DeviceRadixSort::SortKeys(pk.sort_tmp, tb, kt, kt + n, (int)u, 0, hb, st));
+        HIPCHK(rocprim::radix_sort_keys(pk.sort_tmp, tb, kt, kt + n, (int)u, 0, hb, st));
         HIPCHK(key64_expand(ka + n, pk.ck_a2, u, st));
         HIPCHK(key64_expand(kt + n, pk.ck_t2, u, st));
       } else if (hb > 64) {  // 48-bit window [hb - 48, hb) with the row index, then gather
@@ -1171,24 +1171,24 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         for (int s = 0; s < 2; s++) {
           HIPCHK(lookup_keys(srcs[s], u, hb - 48, canon[s], kin, iin, flags, st));
           tb = pk.sort_tmp_bytes;
-          HIPCHK(hipcub::DeviceRadixSort::SortPairs(pk.sort_tmp, tb, kin, kout, iin, iout, (int)u, 0, 48, st));
+          HIPCHK(rocprim::radix_sort_pairs(pk.sort_tmp, tb, kin, kout, iin, iout, (int)u, 0, 48, st));
           HIPCHK(lookup_gather(canon[s], iout, u, sorted[s], flags + 4, st));
         }
       } else {
         HIPCHK(fr_to_canon(w.lk_a[l], pk.ck_a, u, st));
         HIPCHK(fr_to_canon(w.lk_s[l], pk.ck_t, u, st));
-        HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(pk.sort_tmp, tb, pk.ck_a, pk.ck_a2, (int)u, CanonLess(), st));
+        HIPCHK(rocprim::merge_sort(pk.sort_tmp, tb, pk.ck_a, pk.ck_a2, (int)u, CanonLess(), st));
         tb = pk.sort_tmp_bytes;
-        HIPCHK(hipcub::DeviceMergeSort::SortKeysCopy(pk.sort_tmp, tb, pk.ck_t, pk.ck_t2, (int)u, CanonLess(), st));
+        HIPCHK(rocprim::merge_sort(pk.sort_tmp, tb, pk.ck_t, pk.ck_t2, (int)u, CanonLess(), st));
       }
       HIPCHK(hipMemsetAsync(pk.left_flag, 1, u, st));
       HIPCHK(hipMemsetAsync(pk.counters, 0, 8 * sizeof(uint32_t), st));
       HIPCHK(lookup_mark(pk.ck_a2, pk.ck_t2, u, pk.rep_flag, pk.left_flag, pk.counters + 2, st));
       tb = pk.sort_tmp_bytes;
-      HIPCHK(hipcub::DeviceSelect::Flagged(pk.sort_tmp, tb, pk.ck_t2, pk.left_flag, pk.ck_left, pk.counters, (int)u,
+      HIPCHK(rocprim::select(pk.sort_tmp, tb, pk.ck_t2, pk.left_flag, pk.ck_left, pk.counters, (int)u,
                                            st));
       tb = pk.sort_tmp_bytes;
-      HIPCHK(hipcub::DeviceSelect::Flagged(pk.sort_tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), pk.rep_flag,
+      HIPCHK(rocprim::select(pk.sort_tmp, tb, rocprim::counting_iterator<uint32_t>(0), pk.rep_flag,
                                            pk.rep_rows, pk.counters + 1, (int)u, st));
       HIPCHK(lookup_assign(pk.ck_a2, pk.rep_flag, u, w.lk_ap[l], w.lk_sp[l], st));
       HIPCHK(lookup_scatter(pk.ck_left, pk.rep_rows, pk.counters + 1, u, w.lk_sp[l], st));

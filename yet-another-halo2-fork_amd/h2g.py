@@ -114,7 +114,7 @@ _SIGS = {
     "h2g_comm_destroy": ([], I32),
 }
 
-MSM_PHASES = ("digits", "sort", "bucket_bounds", "accumulate", "bucket_fixup", "reduce")
+MSM_PHASES = ("partition_coarse", "partition_fine", "bucket_bounds", "accumulate", "bucket_fixup", "reduce")
 
 _lib = None
 
@@ -397,12 +397,17 @@ def profile_enable(on=True):
     check(lib().h2g_profile_enable(1 if on else 0))
 
 
-def profile_msm_collect():
-    """-> (calls, {phase: total_ms}) for MSMs run since profiling was enabled."""
+def profile_msm_collect(with_union=False):
+    """-> (calls, {phase: total_ms}) for MSMs run since profiling was enabled; with_union:
+    (calls, phases, {"accumulate": ms, "msm": ms}) adding the busy time (union of the
+    intervals) of the overlapping MSMs' accumulate phases and of the whole MSMs."""
     ms = (ctypes.c_float * 8)()
     npz, calls = I32(0), I32(0)
     check(lib().h2g_profile_msm_collect(ms, 8, ctypes.byref(npz), ctypes.byref(calls)))
-    return calls.value, {MSM_PHASES[i]: ms[i] for i in range(npz.value)}
+    phases = {MSM_PHASES[i]: ms[i] for i in range(npz.value)}
+    if not with_union:
+        return calls.value, phases
+    return calls.value, phases, {"accumulate": ms[npz.value], "msm": ms[npz.value + 1]}
 
 
 class Timer:
