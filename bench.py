@@ -443,8 +443,11 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             "stages_ms_synced_proof": {nm: round(ms, 3) for nm, ms in stages},
             "pcie_inclusive_s": round(pcie["s"], 4),
         }
-        if world == 1 and args.workload == "prove":
-            line["msm_2p24"] = measure_msm(h2g, torch, dev, 24, steps=10, warmup=2)
+    if args.workload == "prove" and (world == 1 or dist.get_backend() == "nccl"):
+        # every rank takes part when sharded (collectives inside)
+        m = measure_msm(h2g, torch, dev, 24, steps=10, warmup=2, dist=dist, world=world, rank=rank)
+        if line is not None:
+            line["msm_2p24"] = m
     if native:
         h2g.comm_destroy()
     if not worker:
@@ -471,33 +474,54 @@ def verify_proof(h2g, circ, pk, proof, s_int):
     return bool(V.verify(circ, [], proof, s_int, vk=vk))
 
 
-def measure_msm(h2g, torch, dev, log_n, steps, warmup):
+def measure_msm(h2g, torch, dev, log_n, steps, warmup, dist=None, world=1, rank=0):
     """the metric's MSM half: one MSM of 2^log_n resident (scalar, SRS point) pairs through
-    the base-descriptor path (fixed-base windows), HIP-event timed on the MSM stream"""
+    the base-descriptor path (fixed-base windows), HIP-event timed on the MSM stream.
+    world > 1: the same MSM strong-scaled over the ranks -- rank r holds point slab
+    [n r / world, n (r + 1) / world) and its scalars, and each step ends with the RCCL
+    all_gather of the 64-B partials and their host sum ("MSM sharded ... final
+    bucket-sum reduce"); the time is the slowest rank's"""
     stream = torch.cuda.current_stream().cuda_stream
     n = 1 << log_n
-    rng = np.random.default_rng(1000)
-    bases = torch.empty((n, 8), dtype=torch.int64, device=dev)
-    h2g.srs_setup_dev(random_scalars(rng, 1)[0], n, bases.data_ptr(), stream)
-    scalars = torch.from_numpy(random_scalars(rng, n).view(np.int64)).to(dev)
+    n_loc = n // world
+    rng = np.random.default_rng(1000 + rank)
+    bases = torch.empty((n_loc, 8), dtype=torch.int64, device=dev)
+    h2g.srs_setup_dev(random_scalars(rng, 1)[0], n_loc, bases.data_ptr(), stream)
+    scalars = torch.from_numpy(random_scalars(rng, n_loc).view(np.int64)).to(dev)
     torch.cuda.synchronize()
-    base = h2g.base_descriptor_dev(bases.data_ptr(), n, 0)
+    base = h2g.base_descriptor_dev(bases.data_ptr(), n_loc, 0)
+    out = {}
+
+    def step():
+        out["p"] = h2g.msm_with_cached_base_dev(scalars.data_ptr(), n_loc, base, 0, stream)
+        if world > 1:
+            out["total"] = combine_partials(gather_partials(out["p"], dist, world, dev), h2g.g1_add_affine)
+
     for _ in range(warmup):
-        h2g.msm_with_cached_base_dev(scalars.data_ptr(), n, base, 0, stream)
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     h2g.profile_enable(True)
     t0 = time.perf_counter()
     for _ in range(steps):
-        h2g.msm_with_cached_base_dev(scalars.data_ptr(), n, base, 0, stream)
+        step()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     el = time.perf_counter() - t0
     h2g.profile_enable(False)
     calls, phases = h2g.profile_msm_collect()
+    el = max_over_ranks(el, dist, world, dev)
     h2g.descriptor_free(base)
     del bases, scalars
     torch.cuda.empty_cache()
     return {"value": round(n * steps / el / 1e6, 2), "unit": "Mscalar-mul/s", "points": n, "steps": steps,
-            "ms_per_msm": round(el / steps * 1e3, 3), "window_bits": fixed_c(n),
+            "ms_per_msm": round(el / steps * 1e3, 3), "window_bits": fixed_c(n_loc), "n_gpus": world,
+            "points_per_gpu": n_loc,
+            "scaling": "strong (one 2^%d MSM split into %d point slabs, RCCL all_gather of partials)" % (log_n, world)
+                       if world > 1 else "single GPU",
             "phases_ms": {kk: round(v / max(calls, 1), 4) for kk, v in phases.items()}}
 
 

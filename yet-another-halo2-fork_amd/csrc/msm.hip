@@ -257,15 +257,20 @@ msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict
     if (h[t]) atomicAdd(&kcount[(bin0 << fb) + t], h[t]);
 }
 
-// round 2b: the same tiles scattered to their keys' positions
+// round 2b: the same tiles scattered to their keys' positions.  The tile's first-bin
+// entries are counting-sorted in LDS first, so that consecutive lanes store consecutive
+// addresses of a key's run (~FTILE / 2^fb entries): scattered 8-B stores wrote ~3.6x the
+// entry bytes to HBM (PMC WRITE_SIZE), the staged runs write them about once.
 __global__ void __launch_bounds__(FT)
 msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
                         uint32_t* __restrict__ kcursor, uint64_t* __restrict__ out) {
-  __shared__ uint32_t cnt[1 << FB_MAX], base[1 << FB_MAX];
+  __shared__ uint32_t cnt[1 << FB_MAX], adj[1 << FB_MAX];
+  __shared__ uint32_t part[FT];
+  __shared__ uint64_t stage[FTILE];
   const uint32_t total = *d_total;
   const uint32_t lo = blockIdx.x * FTILE;
   if (lo >= total) return;
-  const uint32_t nf = 1u << fb;
+  const uint32_t nf = 1u << fb, mask = nf - 1;
   for (uint32_t t = threadIdx.x; t < nf; t += FT) cnt[t] = 0;
   const uint32_t bin0 = (uint32_t)(in[lo] >> 32) >> fb;
   __syncthreads();
@@ -279,17 +284,42 @@ msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restr
     if (p < total) {
       ent[k] = in[p];
       const uint32_t key = (uint32_t)(ent[k] >> 32);
-      if ((key >> fb) == bin0) rk[k] = atomicAdd(&cnt[key & (nf - 1)], 1u);
-      else out[atomicAdd(&kcursor[key], 1u)] = ent[k];
+      if ((key >> fb) == bin0) rk[k] = atomicAdd(&cnt[key & mask], 1u);
+      else out[atomicAdd(&kcursor[key], 1u)] = ent[k];  // tiles straddling bins: few entries
     }
   }
   __syncthreads();
-  for (uint32_t t = threadIdx.x; t < nf; t += FT)
-    if (cnt[t]) base[t] = atomicAdd(&kcursor[(bin0 << fb) + t], cnt[t]);
+  // exclusive scan of cnt (each thread a contiguous run of per <= 8 counters), and the
+  // global reservation per key: adj[key] = global base - local offset
+  const uint32_t per = (nf + FT - 1) / FT, a = threadIdx.x * per;
+  uint32_t sum = 0;
+  for (uint32_t i = 0; i < per && a + i < nf; i++) sum += cnt[a + i];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int d = 1; d < FT; d <<= 1) {
+    const uint32_t v = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const uint32_t nb0 = part[FT - 1];  // first-bin entries of the tile
+  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+  for (uint32_t i = 0; i < per && a + i < nf; i++) {
+    const uint32_t c = cnt[a + i];
+    const uint32_t g = c ? atomicAdd(&kcursor[(bin0 << fb) + a + i], c) : 0;
+    cnt[a + i] = run;  // local offset
+    adj[a + i] = g - run;
+    run += c;
+  }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < FPER; k++)
-    if (rk[k] != ~0u) out[base[(uint32_t)(ent[k] >> 32) & (nf - 1)] + rk[k]] = ent[k];
+    if (rk[k] != ~0u) stage[cnt[(uint32_t)(ent[k] >> 32) & mask] + rk[k]] = ent[k];
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < nb0; j += FT) {
+    const uint64_t e = stage[j];
+    out[adj[(uint32_t)(e >> 32) & mask] + j] = e;
+  }
 }
 
 // 3-4. accumulation straight from the sorted entries -------------------------------
