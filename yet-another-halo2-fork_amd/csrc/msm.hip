@@ -90,8 +90,15 @@ static constexpr uint32_t FTILE = (uint32_t)FT * FPER;
 static constexpr int FB_MAX = 11;       // fine bits
 static constexpr int COARSE_MAX = 2048;  // coarse bins (keys < 2^22)
 
+// Fixed-base windows have balanced widths: W = ceil(255 / c) windows covering the 255
+// bits signed digits need, the first 255 % W of them one bit wider (<= c).  Uniform
+// c-bit windows leave a short top window (255 - c (W - 1) bits: 7 at c = 19, W = 14)
+// whose digits pile n entries into a few buckets -- the big-bucket path, ~0.2-0.5 ms.
+__host__ __device__ __forceinline__ int fb_width(int W, int w) { return 255 / W + (w < 255 % W ? 1 : 0); }
+
 // the signed digits of scalar i (batch bi) for windows [w0, w0 + PWG): fn(slot, key, val)
-// for each nonzero digit (same key / value encoding as msm_digits_kernel)
+// for each nonzero digit (same key / value encoding as msm_digits_kernel); fixed-base
+// windows take their balanced widths (fb_width), generic ones c bits each
 template <class Fn>
 __device__ __forceinline__ void scalar_digits(const MsmScalarList& list, size_t n, int c, int W, uint32_t NB,
                                               int fixed, size_t stride, uint32_t bi, size_t i, int w0, Fn fn) {
@@ -101,18 +108,19 @@ __device__ __forceinline__ void scalar_digits(const MsmScalarList& list, size_t 
   s.l[0] = a.x; s.l[1] = a.y; s.l[2] = a.z; s.l[3] = a.w;
   s.l[4] = b.x; s.l[5] = b.y; s.l[6] = b.z; s.l[7] = b.w;
   Fr v = to_canonical(s);
-  const uint32_t mask = (1u << c) - 1;
-  const uint32_t half = 1u << (c - 1);
   uint32_t carry = 0;
   const int wend = w0 + PWG < W ? w0 + PWG : W;
   for (int w = 0; w < wend; w++) {
+    const int cw = fixed ? fb_width(W, w) : c;
+    const uint32_t mask = (1u << cw) - 1;
+    const uint32_t half = 1u << (cw - 1);
     const uint32_t d = (v.l[0] & mask) + carry;
 #pragma unroll
-    for (int k = 0; k < 7; k++) v.l[k] = (v.l[k] >> c) | (v.l[k + 1] << (32 - c));
-    v.l[7] >>= c;
+    for (int k = 0; k < 7; k++) v.l[k] = (v.l[k] >> cw) | (v.l[k + 1] << (32 - cw));
+    v.l[7] >>= cw;
     uint32_t mag, sign;
-    if (d > half) {  // negative digit d - 2^c (d == 2^c gives digit 0, carry 1)
-      mag = (1u << c) - d;
+    if (d > half) {  // negative digit d - 2^cw (d == 2^cw gives digit 0, carry 1)
+      mag = (1u << cw) - d;
       carry = 1;
       sign = 0x80000000u;
     } else {
@@ -257,20 +265,15 @@ msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict
     if (h[t]) atomicAdd(&kcount[(bin0 << fb) + t], h[t]);
 }
 
-// round 2b: the same tiles scattered to their keys' positions.  The tile's first-bin
-// entries are counting-sorted in LDS first, so that consecutive lanes store consecutive
-// addresses of a key's run (~FTILE / 2^fb entries): scattered 8-B stores wrote ~3.6x the
-// entry bytes to HBM (PMC WRITE_SIZE), the staged runs write them about once.
+// round 2b: the same tiles scattered to their keys' positions
 __global__ void __launch_bounds__(FT)
 msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
                         uint32_t* __restrict__ kcursor, uint64_t* __restrict__ out) {
-  __shared__ uint32_t cnt[1 << FB_MAX], adj[1 << FB_MAX];
-  __shared__ uint32_t part[FT];
-  __shared__ uint64_t stage[FTILE];
+  __shared__ uint32_t cnt[1 << FB_MAX], base[1 << FB_MAX];
   const uint32_t total = *d_total;
   const uint32_t lo = blockIdx.x * FTILE;
   if (lo >= total) return;
-  const uint32_t nf = 1u << fb, mask = nf - 1;
+  const uint32_t nf = 1u << fb;
   for (uint32_t t = threadIdx.x; t < nf; t += FT) cnt[t] = 0;
   const uint32_t bin0 = (uint32_t)(in[lo] >> 32) >> fb;
   __syncthreads();
@@ -284,42 +287,17 @@ msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restr
     if (p < total) {
       ent[k] = in[p];
       const uint32_t key = (uint32_t)(ent[k] >> 32);
-      if ((key >> fb) == bin0) rk[k] = atomicAdd(&cnt[key & mask], 1u);
-      else out[atomicAdd(&kcursor[key], 1u)] = ent[k];  // tiles straddling bins: few entries
+      if ((key >> fb) == bin0) rk[k] = atomicAdd(&cnt[key & (nf - 1)], 1u);
+      else out[atomicAdd(&kcursor[key], 1u)] = ent[k];
     }
   }
   __syncthreads();
-  // exclusive scan of cnt (each thread a contiguous run of per <= 8 counters), and the
-  // global reservation per key: adj[key] = global base - local offset
-  const uint32_t per = (nf + FT - 1) / FT, a = threadIdx.x * per;
-  uint32_t sum = 0;
-  for (uint32_t i = 0; i < per && a + i < nf; i++) sum += cnt[a + i];
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  for (int d = 1; d < FT; d <<= 1) {
-    const uint32_t v = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  const uint32_t nb0 = part[FT - 1];  // first-bin entries of the tile
-  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-  for (uint32_t i = 0; i < per && a + i < nf; i++) {
-    const uint32_t c = cnt[a + i];
-    const uint32_t g = c ? atomicAdd(&kcursor[(bin0 << fb) + a + i], c) : 0;
-    cnt[a + i] = run;  // local offset
-    adj[a + i] = g - run;
-    run += c;
-  }
+  for (uint32_t t = threadIdx.x; t < nf; t += FT)
+    if (cnt[t]) base[t] = atomicAdd(&kcursor[(bin0 << fb) + t], cnt[t]);
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < FPER; k++)
-    if (rk[k] != ~0u) stage[cnt[(uint32_t)(ent[k] >> 32) & mask] + rk[k]] = ent[k];
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < nb0; j += FT) {
-    const uint64_t e = stage[j];
-    out[adj[(uint32_t)(e >> 32) & mask] + j] = e;
-  }
+    if (rk[k] != ~0u) out[base[(uint32_t)(ent[k] >> 32) & (nf - 1)] + rk[k]] = ent[k];
 }
 
 // 3-4. accumulation straight from the sorted entries -------------------------------
@@ -529,6 +507,87 @@ msm_big_combine_kernel(const uint4* __restrict__ multi, const uint32_t* __restri
   }
 }
 
+// Quad-cooperative XYZZ arithmetic for the latency-bound reduction kernels ----------
+// With one wave per SIMD an XYZZ addition is issue-bound at ~13 us (14 Montgomery
+// products in sequence).  Its products fall into 4 dependent levels (a doubling's 10
+// into 3): the 4 lanes of a quad hold the same operands, each lane computes one product
+// of a level, and DPP quad_perm broadcasts hand the results to the quad.  ~3x less
+// latency per operation for 1.3x the issue slots -- used where a kernel has too few
+// threads to fill the SIMDs.  Every lane of a quad must be active with equal operands.
+template <int K>
+__device__ __forceinline__ Fq quad_bcast(const Fq& a) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], K | (K << 2) | (K << 4) | (K << 6), 0xf, 0xf, false);
+  return r;
+}
+__device__ __forceinline__ Fq quad_sel(int s, const Fq& a, const Fq& b, const Fq& c, const Fq& d) {
+  Fq r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.l[i] = s == 0 ? a.l[i] : (s == 1 ? b.l[i] : (s == 2 ? c.l[i] : d.l[i]));
+  return r;
+}
+
+// dbl-2008-s-1 (= xyzz_dbl): levels {V, X^2}, {W, S, ZZ', M^2}, {ZZZ', W Y, M (S - X')}
+__device__ G1xyzz xyzz_dbl_q4(const G1xyzz& p) {
+  if (p.is_identity()) return p;
+  const int s = threadIdx.x & 3;
+  const Fq U = dbl(p.Y);
+  const Fq a1 = (s & 1) ? p.X : U;
+  Fq m = a1 * a1;
+  const Fq V = quad_bcast<0>(m), X2 = quad_bcast<1>(m);
+  const Fq M = X2 + dbl(X2);
+  m = quad_sel(s, U, p.X, V, M) * quad_sel(s, V, V, p.ZZ, M);
+  const Fq W = quad_bcast<0>(m), S = quad_bcast<1>(m), ZZ3 = quad_bcast<2>(m), MM = quad_bcast<3>(m);
+  G1xyzz r;
+  r.X = MM - dbl(S);
+  m = quad_sel(s, W, W, M, W) * quad_sel(s, p.ZZZ, p.Y, S - r.X, p.ZZZ);
+  r.Y = quad_bcast<2>(m) - quad_bcast<1>(m);
+  r.ZZ = ZZ3;
+  r.ZZZ = quad_bcast<0>(m);
+  return r;
+}
+
+// add-2008-s (= xyzz_add): levels {U1, U2, S1, S2}, {P^2, R^2, ZZ1 ZZ2, ZZZ1 ZZZ2},
+// {PPP, Q, ZZ'}, {R (Q - X'), S1 PPP, ZZZ'}
+__device__ G1xyzz xyzz_add_q4(const G1xyzz& p, const G1xyzz& q) {
+  if (q.is_identity()) return p;
+  if (p.is_identity()) return q;
+  const int s = threadIdx.x & 3;
+  Fq m = quad_sel(s, p.X, q.X, p.Y, q.Y) * quad_sel(s, q.ZZ, p.ZZ, q.ZZZ, p.ZZZ);
+  const Fq U1 = quad_bcast<0>(m), U2 = quad_bcast<1>(m), S1 = quad_bcast<2>(m), S2 = quad_bcast<3>(m);
+  const Fq Pp = U2 - U1;
+  const Fq R = S2 - S1;
+  if (Pp.is_zero()) {
+    if (R.is_zero()) return xyzz_dbl_q4(p);
+    return G1xyzz::identity();
+  }
+  m = quad_sel(s, Pp, R, p.ZZ, p.ZZZ) * quad_sel(s, Pp, R, q.ZZ, q.ZZZ);
+  const Fq PP = quad_bcast<0>(m), RR = quad_bcast<1>(m), ZZ12 = quad_bcast<2>(m), ZZZ12 = quad_bcast<3>(m);
+  m = quad_sel(s, Pp, U1, ZZ12, Pp) * PP;
+  const Fq PPP = quad_bcast<0>(m), Q = quad_bcast<1>(m);
+  G1xyzz r;
+  r.ZZ = quad_bcast<2>(m);
+  r.X = RR - PPP - dbl(Q);
+  m = quad_sel(s, R, S1, ZZZ12, R) * quad_sel(s, Q - r.X, PPP, PPP, PPP);
+  r.Y = quad_bcast<0>(m) - quad_bcast<1>(m);
+  r.ZZZ = quad_bcast<2>(m);
+  return r;
+}
+
+__device__ G1xyzz xyzz_mul_u32_q4(const G1xyzz& p, uint32_t k) {
+  if (k == 0) return G1xyzz::identity();
+  int top = 31;
+  while (!((k >> top) & 1)) top--;
+  G1xyzz acc = p;
+  for (int b = top - 1; b >= 0; b--) {
+    acc = xyzz_dbl_q4(acc);
+    if ((k >> b) & 1) acc = xyzz_add_q4(acc, p);
+  }
+  return acc;
+}
+
 // 6a. bucket reduction (default): F = sum_j (j+1) B_j per window, shallow ------------------
 // A serial chain of XYZZ additions costs ~12 us on the GPU at low occupancy, so the
 // reduction minimises dependent depth, not work:
@@ -578,16 +637,66 @@ msm_rscale_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R, ui
   if (threadIdx.x == 0) part[(size_t)w * nblk + blockIdx.x] = sh[0];
 }
 
+// the same three kernels with one quad per thread above (xyzz_*_q4): a quad per group,
+// 64 groups per block; taken when the groups cannot fill the SIMDs (small MSMs, e.g. the
+// 2^19-2^20-point slabs of a sharded proof), and always for the final tree
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_rfinal_kernel(const G1xyzz* __restrict__ part, uint32_t nblk, G1xyzz* __restrict__ windows) {
-  __shared__ G1xyzz sh[MSM_THREADS];
-  const uint32_t w = blockIdx.x;
-  G1xyzz acc = G1xyzz::identity();
-  for (uint32_t i = threadIdx.x; i < nblk; i += MSM_THREADS) acc = xyzz_add(acc, part[(size_t)w * nblk + i]);
-  sh[threadIdx.x] = acc;
+msm_rgroup_q4_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, G1xyzz* __restrict__ S,
+                     G1xyzz* __restrict__ R) {
+  const uint32_t w = blockIdx.y;
+  const uint32_t g = (blockIdx.x * MSM_THREADS + threadIdx.x) >> 2;
+  if (g >= m1) return;  // the whole quad
+  const G1xyzz* b = B + (size_t)w * NB;
+  G1xyzz racc = G1xyzz::identity(), sacc = G1xyzz::identity();
+  for (int t = RG - 1; t >= 0; t--) {
+    const uint32_t j = g * RG + t;
+    if (j < NB) racc = xyzz_add_q4(racc, b[j]);
+    sacc = xyzz_add_q4(sacc, racc);
+  }
+  if ((threadIdx.x & 3) == 0) {
+    S[(size_t)w * m1 + g] = sacc;
+    R[(size_t)w * m1 + g] = racc;
+  }
+}
+
+static constexpr uint32_t Q4_GROUPS = MSM_THREADS / 4;  // quads per block
+
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_rscale_q4_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R, uint32_t m1,
+                     G1xyzz* __restrict__ part, uint32_t nblk) {
+  __shared__ G1xyzz sh[Q4_GROUPS];
+  const uint32_t w = blockIdx.y, qi = threadIdx.x >> 2;
+  const uint32_t g = blockIdx.x * Q4_GROUPS + qi;
+  G1xyzz v = G1xyzz::identity();
+  if (g < m1) {
+    v = S[(size_t)w * m1 + g];
+    if (g) v = xyzz_add_q4(v, xyzz_mul_u32_q4(R[(size_t)w * m1 + g], g * RG));
+  }
+  if ((threadIdx.x & 3) == 0) sh[qi] = v;
   __syncthreads();
-  for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + h]);
+  for (uint32_t h = Q4_GROUPS / 2; h > 0; h >>= 1) {
+    if (qi < h) {  // sh[qi + h] is not written at this level
+      const G1xyzz t = xyzz_add_q4(sh[qi], sh[qi + h]);
+      if ((threadIdx.x & 3) == 0) sh[qi] = t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[(size_t)w * nblk + blockIdx.x] = sh[0];
+}
+
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_rfinal_q4_kernel(const G1xyzz* __restrict__ part, uint32_t nblk, G1xyzz* __restrict__ windows) {
+  __shared__ G1xyzz sh[Q4_GROUPS];
+  const uint32_t w = blockIdx.x, qi = threadIdx.x >> 2;
+  G1xyzz acc = G1xyzz::identity();
+  for (uint32_t i = qi; i < nblk; i += Q4_GROUPS) acc = xyzz_add_q4(acc, part[(size_t)w * nblk + i]);
+  if ((threadIdx.x & 3) == 0) sh[qi] = acc;
+  __syncthreads();
+  for (uint32_t h = Q4_GROUPS / 2; h > 0; h >>= 1) {
+    if (qi < h) {
+      const G1xyzz t = xyzz_add_q4(sh[qi], sh[qi + h]);
+      if ((threadIdx.x & 3) == 0) sh[qi] = t;
+    }
     __syncthreads();
   }
   if (threadIdx.x == 0) windows[w] = sh[0];
@@ -708,9 +817,9 @@ msm_wfinal_kernel(const G1xyzz* __restrict__ lv2, uint32_t stride, WsFinal f, G1
   if (threadIdx.x == 0) windows[blockIdx.x] = xyzz_add(xyzz_add(res[0], res[1]), xyzz_add(res[2], res[3]));
 }
 
-// fixed-base tables: table[w * stride + i] = [2^(c w)] bases[i] --------------------
+// fixed-base tables: table[w * stride + i] = [2^(offset of window w)] bases[i] -------
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_precompute_kernel(const G1Affine* __restrict__ bases, size_t n, int c, int W, size_t stride,
+msm_precompute_kernel(const G1Affine* __restrict__ bases, size_t n, int W, size_t stride,
                       G1Affine* __restrict__ table) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -718,7 +827,7 @@ msm_precompute_kernel(const G1Affine* __restrict__ bases, size_t n, int c, int W
   table[i] = p;
   G1xyzz x = G1xyzz::from_affine(p);
   for (int w = 1; w < W; w++) {
-    for (int d = 0; d < c; d++) x = xyzz_dbl(x);
+    for (int d = 0; d < fb_width(W, w - 1); d++) x = xyzz_dbl(x);
     table[(size_t)w * stride + i] = xyzz_to_affine(x);
   }
 }
@@ -767,9 +876,16 @@ void msm_free(MsmWorkspace* ws) {
     if (_e != hipSuccess) return _e;    \
   } while (0)
 
-uint32_t msm_chunk_len(size_t total) {
-  // ~4 resident waves per SIMD x 256 CUs x 64 lanes, several rounds deep
+uint32_t msm_chunk_len(size_t total, size_t nbt) {
+  // ~4 resident waves per SIMD x 256 CUs x 64 lanes, several rounds deep ...
   uint64_t L = total / (256ull * 4 * 4 * 64 * 4);
+  // ... but at least a quarter of the mean bucket, so that a bucket spans few chunks and
+  // the fixup sums it in one thread (small MSMs: 2^19 points at c = 17 put ~120 entries
+  // in each of 2^16 buckets; L = 8 sent every bucket through the big-item path, 0.74 ms),
+  // while >= 2^17 threads remain
+  const uint64_t quarter = nbt ? total / (4 * nbt) : 0;
+  const uint64_t cap = total >> 17;
+  if (L < quarter) L = quarter < cap ? quarter : (cap > L ? cap : L);
   if (L < 8) L = 8;
   if (L > 128) L = 128;
   return (uint32_t)L;
@@ -786,14 +902,19 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   const uint32_t nbt = (uint32_t)WB * NB;
   const size_t total = n * (size_t)W * nbatch;
   if (total >= 0x80000000ull) return hipErrorInvalidValue;  // u32 positions in the sorted array
-  const uint32_t L = item_len > 0 ? item_len : msm_chunk_len(total);
+  // buckets most windows can reach (fixed-base: 2^(base width - 1) of the balanced widths)
+  const size_t nb_eff = (size_t)WB << ((fixed ? 255 / W : c) - 1);
+  const uint32_t L = item_len > 0 ? item_len : msm_chunk_len(total, nb_eff);
   const size_t nchunks = (total + L - 1) / L;
   static const bool red_split = [] {
     const char* e = getenv("H2G_MSM_RED");
     return e && std::string(e) == "split";
   }();
   const uint32_t m1 = (NB + RG - 1) / RG;
-  const uint32_t nblk = (m1 + MSM_THREADS - 1) / MSM_THREADS;
+  // quad-cooperative group kernels when the groups leave SIMDs idle (<= 512 waves of one
+  // lane per group); the block sums then cover Q4_GROUPS groups each
+  const bool red_q4 = (size_t)m1 * WB <= 32768;
+  const uint32_t nblk = red_q4 ? (m1 + Q4_GROUPS - 1) / Q4_GROUPS : (m1 + MSM_THREADS - 1) / MSM_THREADS;
   const WsPlan wp = ws_plan(NB);
   if (red_split && (wp.nv2v > 64 || wp.nu2v > 64 || wp.nv2u > 64 || wp.nu2u > 64)) return hipErrorInvalidValue;
   // grow-only workspace: MSMs of slightly different shapes (e.g. n and n - 1 points, so
@@ -919,11 +1040,18 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
                      (const uint32_t*)counters, (const G1xyzz*)ipart, buckets);
   H2G_PHASE(5);
   if (!red_split) {
-    hipLaunchKernelGGL(msm_rgroup_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1,
-                       rS, rR);
-    hipLaunchKernelGGL(msm_rscale_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
-                       (const G1xyzz*)rR, m1, rP, nblk);
-    hipLaunchKernelGGL(msm_rfinal_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rP, nblk,
+    if (red_q4) {
+      hipLaunchKernelGGL(msm_rgroup_q4_kernel, dim3((unsigned)(((size_t)m1 * 4 + T - 1) / T), (unsigned)WB), dim3(T),
+                         0, st, (const G1xyzz*)buckets, NB, m1, rS, rR);
+      hipLaunchKernelGGL(msm_rscale_q4_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
+                         (const G1xyzz*)rR, m1, rP, nblk);
+    } else {
+      hipLaunchKernelGGL(msm_rgroup_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1,
+                         rS, rR);
+      hipLaunchKernelGGL(msm_rscale_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
+                         (const G1xyzz*)rR, m1, rP, nblk);
+    }
+    hipLaunchKernelGGL(msm_rfinal_q4_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rP, nblk,
                        (G1xyzz*)ws->windows);
   } else {
     const uint32_t s1n = wp.nv1 + wp.nu1, s2n = wp.nv2v + wp.nu2v + wp.nv2u + wp.nu2u;
@@ -990,7 +1118,7 @@ hipError_t msm_fixed_base_build(const G1Affine* d_bases, size_t n, int c, MsmFix
   fb->c = c;
   fb->W = W;
   hipLaunchKernelGGL(msm_precompute_kernel, dim3((unsigned)((n + MSM_THREADS - 1) / MSM_THREADS)), dim3(MSM_THREADS),
-                     0, st, d_bases, n, c, W, n, fb->table);
+                     0, st, d_bases, n, W, n, fb->table);
   return hipGetLastError();
 }
 
