@@ -12,11 +12,13 @@ c_i -> a_{i+1}) through the C ABI (h2g_create_proof), witness resident in HBM wh
 timed region starts.  value = wall-seconds per proof (lower is better).  The proof
 bytes of this exact pipeline are tested identical to the CPU restatement prover
 (tests/test_gpu_prover.py).
-N > 1 (torchrun, one process per GPU), --mode shard (default): ONE proof at a time
-over all ranks -- rank 0 runs the prover, every commitment MSM is split into point
-slabs and ranks 1.. compute theirs (h2g_dist: RCCL p2p slabs + partials, SURVEY 8e);
-value = max-over-ranks wall time / steps, "scaling": "strong".  --mode replicas:
-every rank proves its own instance; value = max-over-ranks time / (steps * N), "weak".
+N > 1 (torchrun, one process per GPU), --mode spmd (default): ONE proof at a time over
+all ranks -- every rank runs the same prover (same key, witness and seed) and computes
+point slab `rank` of each commitment MSM; the 64-B partials are all-gathered (libh2g's
+RCCL communicator, --transport native, or torch.distributed) so every rank writes the
+same proof; value = max-over-ranks wall time / steps, "scaling": "strong".  --mode shard:
+rank 0 proves and sends each MSM's scalar slabs to the peers.  --mode
+replicas: every rank proves its own instance; value = max-over-ranks time / (steps * N).
 
 --workload msm: one step = one MSM of 2^24 resident (scalar, SRS point) pairs
 (h2g_msm_dev_host); N > 1 shards point slabs and all_gathers the 64-B partials (RCCL).
@@ -304,14 +306,16 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
 
     k = args.k
     n = 1 << k
-    shard = world > 1 and args.mode == "shard"
+    shard = world > 1 and args.mode == "shard"  # rank 0 proves, peers serve slabs
+    spmd = world > 1 and args.mode == "spmd"    # every rank proves its slab of each MSM
+    one_proof = shard or spmd
     worker = shard and rank != 0
-    seed_off = 0 if shard else rank  # sharded ranks hold the same SRS
+    seed_off = 0 if one_proof else rank  # ranks of one proof hold the same SRS and witness
     s_int = 0x1234567 + seed_off
     params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(s_int), dtype=np.uint64))
-    if shard:  # fixed-base windows sized for this rank's point slab
+    if one_proof:  # fixed-base windows sized for this rank's point slab
         params.set_slab(*h2g_dist.slab(n, world, rank))
-    native = shard and args.transport == "native"
+    native = one_proof and args.transport == "native"
     if native:  # the library's own RCCL communicators (csrc/comm.cpp); the id travels over torch
         import torch as _t
         uid = _t.zeros(256, dtype=_t.uint8, device=dev if dist.get_backend() == "nccl" else "cpu")
@@ -329,6 +333,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         pk = h2g.ProvingKey(params, circ)
         adv = torch.from_numpy(np.ascontiguousarray(wit.advice).view(np.int64)).to(dev)  # resident witness
         client = h2g_dist.SlabClient(dist, points=n) if shard and not native else None
+        gather = h2g_dist.SpmdGather(dist) if spmd and not native else None
     torch.cuda.synchronize()
     proofs = []
 
@@ -336,7 +341,21 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         proofs.append(pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr()))
 
     def session(body):
-        """rank 0 proves with the slab transport installed; peers serve until it stops"""
+        """shard: rank 0 proves with the slab transport installed, peers serve until it
+        stops; spmd: every rank proves with the all-gather installed"""
+        if spmd:
+            if native:
+                h2g.comm_spmd_install()
+            else:
+                gather.install()
+            try:
+                body()
+            finally:
+                if native:
+                    h2g.comm_spmd_uninstall()
+                else:
+                    gather.uninstall()
+            return
         if worker:
             if native:
                 h2g.comm_serve(params)
@@ -387,6 +406,13 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     elapsed = max_over_ranks(elapsed, dist, world, dev)
     line = None
     extra = {}
+    if spmd:  # every rank wrote the proof: the same bytes on all ranks
+        import hashlib
+        hd = torch.frombuffer(bytearray(hashlib.sha256(proofs[0]).digest()), dtype=torch.uint8).to(torch.int64)
+        hd = hd.to(dev) if dist.get_backend() == "nccl" else hd
+        allh = [torch.empty_like(hd) for _ in range(world)]
+        dist.all_gather(allh, hd)
+        extra["ranks_equal"] = all(bool(torch.equal(a.cpu(), allh[0].cpu())) for a in allh)
     if rank == 0:
         assert all(p == proofs[0] for p in proofs), "non-deterministic proof bytes"
         # outside the timed region: the proof checked by the independent verifier
@@ -394,7 +420,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         # boundaries for a per-stage GPU time breakdown
         extra["verified"] = verify_proof(h2g, circ, pk, proofs[0], s_int)
         stages = []
-        if not shard:
+        if not one_proof:
             h2g.prover_stage_sync(True)
             step()
             h2g.prover_stage_sync(False)
@@ -402,17 +428,17 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             assert proofs[-1] == proofs[0]
         ms_per_step = elapsed / args.steps * 1e3
         msm_ms = sum(phases.values()) / max(calls, 1)
-        n_local = h2g_dist.slab(n, world, 1)[0] if shard else n  # rank 0's points per MSM
+        n_local = h2g_dist.slab(n, world, 1)[0] if one_proof else n  # rank 0's points per MSM
         line = {
             "metric": METRIC,
-            "value": round(elapsed / (args.steps * (1 if shard else world)), 4),
+            "value": round(elapsed / (args.steps * (1 if one_proof else world)), 4),
             "unit": "s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": False,
-            "scaling": "strong" if shard else "weak",
+            "scaling": "strong" if one_proof else "weak",
             "vs_baseline": None,
             "dtype": "u32 limbs (BN254 Fr/Fq Montgomery, 256-bit modular integer)",
             "data": ("synthetic keccak-style witness (nibble xor chains, 16 lookups into a 3-column table)"
@@ -428,6 +454,10 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                        "lookups": len(circ.lookups), "permutation_columns": len(circ.perm_columns), "degree": pk.degree,
                        "extended_k": pk.extended_k, "proof_bytes": len(proofs[0]),
                        "parallelism": ("single GPU per proof" if world == 1 else
+                                       f"one proof over {world} GPUs, SPMD: every rank runs the prover and "
+                                       "computes its point slab of each commitment MSM, partials all-gathered ("
+                                       + ("libh2g RCCL all-gather" if native else "torch.distributed all_gather")
+                                       + "); NTT/evaluate_h/SHPLONK replicated" if spmd else
                                        f"one proof over {world} GPUs: commitment MSMs in point slabs ("
                                        + ("libh2g RCCL communicators" if native else "torch.distributed p2p")
                                        + " slabs + partials), NTT/evaluate_h/SHPLONK on rank 0" if shard else
@@ -443,6 +473,8 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             "stages_ms_synced_proof": {nm: round(ms, 3) for nm, ms in stages},
             "pcie_inclusive_s": round(pcie["s"], 4),
         }
+        if spmd:
+            line["proof_bytes_equal_across_ranks"] = extra["ranks_equal"]
     if args.workload == "prove" and (world == 1 or dist.get_backend() == "nccl"):
         # every rank takes part when sharded (collectives inside)
         m = measure_msm(h2g, torch, dev, 24, steps=10, warmup=2, dist=dist, world=world, rank=rank)
@@ -609,8 +641,9 @@ def main():
     ap.add_argument("--k", type=int, default=0, help="prove: 22 (C3), keccak: 18")
     ap.add_argument("--log-n", type=int, default=24)
     ap.add_argument("--window-bits", type=int, default=0, help="MSM workload: fixed-base window bits (0: auto)")
-    ap.add_argument("--mode", choices=("shard", "replicas"), default="shard",
-                    help="prove workload, N > 1: one proof over all GPUs (shard) or one per GPU (replicas)")
+    ap.add_argument("--mode", choices=("spmd", "shard", "replicas"), default="spmd",
+                    help="prove workload, N > 1: one proof over all GPUs -- every rank proves its MSM slabs "
+                         "(spmd) or rank 0 proves and peers serve slabs (shard) -- or one proof per GPU (replicas)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=1, help="CPU baseline runs (median)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the PMC traffic passes")

@@ -369,6 +369,27 @@ int h2g_comm_serve(uint64_t params, uint64_t* served);
 int h2g_comm_stop(void);
 int h2g_comm_destroy(void);
 
+/* ---- one proof across several GPUs, SPMD: every rank runs the same create_proof (same
+ * key, witness, instances and RNG stream -- a seed, or draws the host replicates -- hence
+ * the same transcript).  Rank r computes point slab r ([P r / world, P (r + 1) / world),
+ * h2g_params_set_slab) of every commitment MSM from its own copy of the scalars, and the
+ * 64-B partials are all-gathered and summed in rank order, so every rank writes the same
+ * proof bytes as one GPU would and no scalars cross the links.
+ *   allgather: in = this rank's partial (8 u64 affine limbs, then 1 if the identity),
+ *              out = world x 9 u64 in rank order; 0 on success
+ * The host transport (callbacks) or the library's RCCL all-gather (h2g_comm_spmd_install,
+ * after h2g_comm_init on every rank).  Installing one sharding mode removes the other. */
+typedef struct {
+  void* ctx;
+  int32_t world;
+  int32_t rank;
+  int (*allgather)(void* ctx, uint64_t seq, const uint64_t in[9], uint64_t* out);
+} h2g_spmd_transport;
+/* install (world >= 2) or remove (NULL or world <= 1) */
+int h2g_set_spmd_transport(const h2g_spmd_transport* t);
+int h2g_comm_spmd_install(void);
+int h2g_comm_spmd_uninstall(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,5 +1,7 @@
-"""One create_proof split over WORLD_SIZE ranks (h2g_dist slab transport) must give the
-same proof bytes as the single-device prover.  Launched by tests/test_gpu_sharded.py:
+"""One create_proof split over WORLD_SIZE ranks must give the same proof bytes as the
+single-device prover: --mode slab (rank 0 proves, h2g_dist slab transport or libh2g's
+RCCL communicators) or --mode spmd (every rank proves its point slab of each MSM,
+partials all-gathered).  Launched by tests/test_gpu_sharded.py:
   python -m torch.distributed.run --nproc-per-node W --master-addr 127.0.0.1 \
       --master-port P tests/_shard_prove.py --backend gloo case...
 With --backend gloo every rank may share one GPU (host-staged slabs); with nccl each
@@ -42,6 +44,8 @@ def main():
     ap.add_argument("--backend", default="gloo")
     ap.add_argument("--transport", default="torch", choices=("torch", "native"),
                     help="h2g_dist over torch.distributed, or libh2g's RCCL communicators (nccl only)")
+    ap.add_argument("--mode", default="slab", choices=("slab", "spmd"),
+                    help="slab: rank 0 proves, peers serve slabs; spmd: every rank proves its slab")
     ap.add_argument("cases", nargs="+")
     args = ap.parse_args()
     rank = int(os.environ["RANK"])
@@ -61,6 +65,9 @@ def main():
             uid.copy_(torch.frombuffer(bytearray(h2g.comm_unique_id()), dtype=torch.uint8))
         dist.broadcast(uid, 0)
         h2g.comm_init(bytes(uid.cpu().numpy().tobytes()), world, rank)
+    if args.mode == "spmd":
+        spmd_main(args, rank, world, native)
+        return
     results = {}
     for name in args.cases:
         case = CASES[name]()
@@ -104,6 +111,57 @@ def main():
     if rank == 0:
         for i, nm in enumerate(args.cases):
             results[nm]["msms"] = [int(g[i]) for g in gathered[1:]]
+        print("SHARD_RESULT " + json.dumps(results), flush=True)
+    if native:
+        h2g.comm_destroy()
+    h2g.shutdown()
+    dist.destroy_process_group()
+
+
+def spmd_main(args, rank, world, native):
+    """every rank: the single-device proofs first, then the same proofs with its slab of
+    every MSM and the all-gathered partials; all ranks must print identical bytes"""
+    import hashlib
+    results = {}
+    for name in args.cases:
+        case = CASES[name]()
+        circ = case[0]
+        params = h2g.Params(circ.k, s=np.asarray(hc.fr_to_limbs(0x5eed + circ.k), dtype=np.uint64))
+        P = 1 << circ.k
+        params.set_slab(*D.slab(P, world, rank))
+        pk = h2g.ProvingKey(params, circ)
+        want = [_prove(pk, case), _prove(pk, case, seed=bytes(range(32)), vanishing_threads=3)]
+        g = None
+        if native:
+            h2g.comm_spmd_install()
+        else:
+            g = D.SpmdGather(dist)
+            g.install()
+        try:
+            got = [_prove(pk, case), _prove(pk, case, seed=bytes(range(32)), vanishing_threads=3)]
+        finally:
+            if native:
+                h2g.comm_spmd_uninstall()
+            else:
+                D.SpmdGather.uninstall()
+        digest = hashlib.sha256(b"".join(got)).digest()
+        t = torch.frombuffer(bytearray(digest), dtype=torch.uint8).to(torch.int64)
+        if args.backend == "nccl":
+            t = t.cuda()
+        allh = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allh, t)
+        same_ranks = all(bool(torch.equal(a.cpu(), allh[0].cpu())) for a in allh)
+        ok = torch.tensor([1 if got == want else 0], dtype=torch.int64)
+        if args.backend == "nccl":
+            ok = ok.cuda()
+        allok = [torch.empty_like(ok) for _ in range(world)]
+        dist.all_gather(allok, ok)
+        results[name] = {"same": all(int(a.item()) == 1 for a in allok), "same_ranks": same_ranks,
+                         "bytes": len(got[0]), "gathers": None if g is None else g.calls}
+        pk.close()
+        params.close()
+        dist.barrier()
+    if rank == 0:
         print("SHARD_RESULT " + json.dumps(results), flush=True)
     if native:
         h2g.comm_destroy()

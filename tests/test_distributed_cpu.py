@@ -121,3 +121,58 @@ def test_slab_protocol_gloo(world):
     assert out[0] == want
     for rk in range(1, world):
         assert out[rk] == len(jobs)   # every MSM reached every peer (empty slabs answer identity)
+
+
+# ---------------------------------------------------------------- SPMD: every rank proves
+def _spmd_worker(rank, world, port, jobs, bases, q):
+    """h2g_dist.SpmdGather over gloo with the prover's slab rule (h2g_dist.slab of the
+    params' P) and its rank-order sum (csrc/prover.cpp commit_collect), the oracle MSM as
+    each rank's slab engine (no GPU here): every rank must hold the unsharded MSM"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import h2g
+        import h2g_dist as D
+
+        g = D.SpmdGather(dist)
+        P = len(bases[0])
+        totals = []
+        for seq, (base_set, sc) in enumerate(jobs):
+            lo, hi = D.slab(len(sc), world, rank, P)
+            own = O.msm_best(sc[lo:hi], bases[base_set][lo:hi], 1) if hi > lo else np.zeros(8, np.uint64)
+            mine = np.concatenate([own, np.array([0 if own.any() else 1], np.uint64)])
+            allp = g.allgather(seq, mine)
+            assert allp.shape == (world, 9)
+            assert np.array_equal(allp[rank], mine)
+            total = np.zeros(8, np.uint64)
+            for r in range(world):
+                if not allp[r, 8]:
+                    total = allp[r, :8].copy() if not total.any() else h2g.g1_add_affine(total, allp[r, :8])
+            totals.append(total.tobytes())
+        q.put((rank, totals, g.calls))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_spmd_gather_gloo(world):
+    r = np.random.default_rng(29 + world)
+    n = 256
+    s = O.random_fr(r, 1)[0]
+    bases = [O.srs_powers(s, n), O.srs_powers(O.random_fr(r, 1)[0], n)]
+    jobs = [(0, O.random_fr(r, n)), (1, O.random_fr(r, n - 1)), (1, O.random_fr(r, 2)),
+            (0, np.zeros((n, 4), np.uint64))]
+    want = [O.msm_best(sc, bases[b][:len(sc)], 2).tobytes() for b, sc in jobs]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spmd_worker, args=(i, world, port, jobs, bases, q)) for i in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, totals, calls in out:
+        assert totals == want, rank
+        assert calls == len(jobs)

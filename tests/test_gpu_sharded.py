@@ -27,10 +27,11 @@ def _gpus():
     return torch.cuda.device_count()
 
 
-def _run(world, cases, backend="gloo", transport="torch"):
+def _run(world, cases, backend="gloo", transport="torch", mode="slab"):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(HERE, "_shard_prove.py"), "--backend", backend, "--transport", transport] + cases
+           os.path.join(HERE, "_shard_prove.py"), "--backend", backend, "--transport", transport,
+           "--mode", mode] + cases
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
@@ -55,14 +56,31 @@ def test_sharded_proof_three_ranks():
         assert len(res[nm]["msms"]) == 2 and all(m > 0 for m in res[nm]["msms"]), (nm, res[nm])
 
 
+def test_spmd_proof_two_and_three_ranks():
+    """SPMD: every rank proves with its slab of each MSM and the all-gathered partials;
+    every rank's bytes == the single-device proof"""
+    cases = ["simple_k6", "mixed_k10", "lookup_k11", "keccak_k12", "c3_k14", "challenge_k9"]
+    res = _run(2, cases, mode="spmd")
+    for nm in cases:
+        assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
+        assert res[nm]["gathers"] > 0, (nm, res[nm])
+    res = _run(3, ["simple_k6", "lookup_k11"], mode="spmd")
+    for nm in ("simple_k6", "lookup_k11"):
+        assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
+
+
+@pytest.mark.parametrize("mode", ["slab", "spmd"])
 @pytest.mark.parametrize("transport", ["torch", "native"])
-def test_sharded_proof_rccl_two_gpus(transport):
+def test_sharded_proof_rccl_two_gpus(transport, mode):
     """the RCCL paths (one GPU per rank): torch.distributed slabs, and libh2g's own
     communicators (h2g_comm_*); needs >= 2 GPUs (RCCL refuses two ranks on one GPU)"""
     if _gpus() < 2:
         pytest.skip("needs two GPUs")
     cases = ["simple_k6", "lookup_k11", "c3_k14", "challenge_k9"]
-    res = _run(2, cases, backend="nccl", transport=transport)
+    res = _run(2, cases, backend="nccl", transport=transport, mode=mode)
     for nm in cases:
         assert res[nm]["same"], nm
-        assert all(m > 0 for m in res[nm]["msms"]), (nm, res[nm])
+        if mode == "spmd":
+            assert res[nm]["same_ranks"], nm
+        else:
+            assert all(m > 0 for m in res[nm]["msms"]), (nm, res[nm])

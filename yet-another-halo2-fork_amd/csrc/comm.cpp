@@ -53,6 +53,9 @@ struct Comm {
   int rnext = 0;
   int64_t *h_rhdr = nullptr, *d_rhdr = nullptr;  // one header
   int64_t *h_rpart = nullptr, *d_rpart = nullptr;
+  // SPMD all-gather of partials: pinned [world][9], device in [9] / out [world][9]
+  uint64_t* h_ag = nullptr;
+  uint64_t *d_ag_in = nullptr, *d_ag_out = nullptr;
 };
 Comm* g_comm = nullptr;
 
@@ -139,6 +142,9 @@ int comm_destroy() {
     if (p) (void)hipHostFree(p);
   for (int64_t* p : {c->d_hdr, c->d_part, c->d_rhdr, c->d_rpart})
     if (p) (void)hipFree(p);
+  if (c->h_ag) (void)hipHostFree(c->h_ag);
+  for (uint64_t* p : {c->d_ag_in, c->d_ag_out})
+    if (p) (void)hipFree(p);
   if (c->stx) (void)hipStreamDestroy(c->stx);
   if (c->srx) (void)hipStreamDestroy(c->srx);
   delete c;
@@ -147,6 +153,30 @@ int comm_destroy() {
 
 int comm_world() { return g_comm ? g_comm->world : 1; }
 int comm_rank() { return g_comm ? g_comm->rank : 0; }
+
+void* comm_spmd_ctx() { return g_comm; }
+
+// SPMD: every rank's partial of MSM `seq`, in rank order (one ncclAllGather of 9 words per
+// rank on the slab communicator; every rank calls it for the same MSMs in the same order)
+int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[9], uint64_t* out) {
+  (void)seq;
+  Comm* c = static_cast<Comm*>(ctx);
+  if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm: no communicator for the SPMD all-gather");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t W = (size_t)c->world;
+  if (!c->h_ag) {
+    HIPCHK(hipHostMalloc((void**)&c->h_ag, W * 9 * 8, hipHostMallocDefault));
+    HIPCHK(hipMalloc((void**)&c->d_ag_in, 9 * 8));
+    HIPCHK(hipMalloc((void**)&c->d_ag_out, W * 9 * 8));
+  }
+  std::memcpy(c->h_ag, in, 9 * 8);
+  HIPCHK(hipMemcpyAsync(c->d_ag_in, c->h_ag, 9 * 8, hipMemcpyHostToDevice, c->stx));
+  NCCLCHK(ncclAllGather(c->d_ag_in, c->d_ag_out, 9, ncclUint64, c->tx, c->stx));
+  HIPCHK(hipMemcpyAsync(c->h_ag, c->d_ag_out, W * 9 * 8, hipMemcpyDeviceToHost, c->stx));
+  HIPCHK(hipStreamSynchronize(c->stx));
+  std::memcpy(out, c->h_ag, W * 9 * 8);
+  return H2G_OK;
+}
 
 void* comm_transport_ctx(uint64_t points) {
   if (!g_comm || g_comm->rank != 0) return nullptr;

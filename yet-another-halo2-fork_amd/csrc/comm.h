@@ -38,5 +38,10 @@ int comm_next_request(int32_t* op, int32_t* base_set, uint64_t* lo, uint64_t* co
                       hipStream_t* ready);
 int comm_send_partial(const uint64_t partial[8], int32_t is_identity);
 
+// SPMD (every rank proves): all-gather of the ranks' 9-word partials in rank order
+// (h2g_spmd_transport.allgather; ctx = Comm state from comm_spmd_ctx)
+void* comm_spmd_ctx();
+int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[9], uint64_t* out);
+
 }  // namespace rt
 }  // namespace h2g

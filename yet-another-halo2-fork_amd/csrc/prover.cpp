@@ -285,6 +285,9 @@ void dump(const char* name, const Fr* dptr, size_t count, hipStream_t st, bool h
 enum { SRS_G = 0, SRS_LAGRANGE = 1 };
 h2g_shard_transport g_shard{nullptr, 1, nullptr, nullptr};
 uint64_t g_shard_seq = 0;
+// SPMD sharding (h2g_set_spmd_transport): every rank proves, rank r computes slab r
+h2g_spmd_transport g_spmd{nullptr, 1, 0, nullptr};
+uint64_t g_spmd_seq = 0;
 
 // slab r of an MSM of length n: the points [P r / world, P (r + 1) / world) of the
 // params' P = 2^k, clipped to n (one partition for every MSM length, so each rank's
@@ -297,6 +300,14 @@ size_t shard_lo(size_t P, size_t n, int world, int r) {
 int commit_launch(Device* d, const Params& prm, const Fr* scalars, size_t n, int set, hipStream_t st, MsmTicket* t) {
   t->shard_seq = -1;
   size_t toff = 0;
+  if (g_spmd.world > 1) {  // this rank's slab of its own copy of the scalars
+    const size_t lo = shard_lo(prm.n, n, g_spmd.world, g_spmd.rank);
+    const size_t hi = shard_lo(prm.n, n, g_spmd.world, g_spmd.rank + 1);
+    const MsmFixedBase& tb = prm.tables(set, lo, hi - lo, &toff);
+    RCCHK(msm_fixed_launch(d, scalars + lo, tb, toff, hi - lo, st, t));
+    t->shard_seq = (int64_t)g_spmd_seq++;
+    return H2G_OK;
+  }
   if (g_shard.world <= 1) return msm_fixed_launch(d, scalars, prm.tables(set, 0, n, &toff), 0, n, st, t);
   const size_t n0 = shard_lo(prm.n, n, g_shard.world, 1);
   const MsmFixedBase& tb = prm.tables(set, 0, n0, &toff);
@@ -311,6 +322,25 @@ int commit_launch(Device* d, const Params& prm, const Fr* scalars, size_t n, int
 int commit_collect(Device* d, MsmTicket* t, G1Affine* out) {
   RCCHK(msm_collect(d, t, reinterpret_cast<uint64_t*>(out)));
   if (t->shard_seq < 0) return H2G_OK;
+  if (g_spmd.world > 1) {  // every rank's partial, summed in rank order (the same on every rank)
+    const int W = g_spmd.world;
+    uint64_t mine[9];
+    std::memcpy(mine, out, 64);
+    mine[8] = out->is_identity() ? 1 : 0;
+    std::vector<uint64_t> all((size_t)W * 9);
+    if (g_spmd.allgather(g_spmd.ctx, (uint64_t)t->shard_seq, mine, all.data()) != 0)
+      return fail(H2G_ERR_STATE, "spmd transport: all-gather of MSM " + std::to_string(t->shard_seq) + " failed");
+    t->shard_seq = -1;
+    G1xyzz acc = G1xyzz::identity();
+    for (int r = 0; r < W; r++) {
+      if (all[(size_t)r * 9 + 8]) continue;
+      G1Affine p;
+      std::memcpy(&p, &all[(size_t)r * 9], 64);
+      acc = xyzz_madd(acc, p);
+    }
+    *out = xyzz_to_affine(acc);
+    return H2G_OK;
+  }
   const int peers = g_shard.world - 1;
   std::vector<G1Affine> part(peers);
   std::vector<int32_t> ids(peers, 0);
@@ -339,7 +369,7 @@ int commit_batch_chunk(const Params& prm, size_t n, int set) {
     const char* e = std::getenv("H2G_MSM_BATCH_ENTRIES");
     return e ? std::strtoull(e, nullptr, 0) : (1ull << 27);
   }();
-  if (g_shard.world > 1) return 1;
+  if (g_shard.world > 1 || g_spmd.world > 1) return 1;
   size_t toff = 0;
   const uint64_t per = (uint64_t)prm.tables(set, 0, n, &toff).W * (n ? n : 1);
   if (per > (1ull << 25)) return 1;
@@ -2441,10 +2471,25 @@ int h2g_set_shard_transport(const h2g_shard_transport* t) {
   if (t && t->world > 1) {
     if (!t->launch || !t->collect || t->world > 4096) return fail(H2G_ERR_ARG, "set_shard_transport: bad transport");
     g_shard = *t;
+    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr};
   } else {
     g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   }
   g_shard_seq = 0;
+  return H2G_OK;
+}
+
+int h2g_set_spmd_transport(const h2g_spmd_transport* t) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (t && t->world > 1) {
+    if (!t->allgather || t->world > 4096 || t->rank < 0 || t->rank >= t->world)
+      return fail(H2G_ERR_ARG, "set_spmd_transport: bad transport");
+    g_spmd = *t;
+    g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
+  } else {
+    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr};
+  }
+  g_spmd_seq = 0;
   return H2G_OK;
 }
 
@@ -2522,7 +2567,24 @@ int h2g_comm_init(const uint8_t id[256], int world, int rank) {
 int h2g_comm_destroy(void) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (g_shard.launch == comm_launch) g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
+  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr};
   return comm_destroy();
+}
+
+int h2g_comm_spmd_install(void) {
+  NEED_DEV_P();
+  if (comm_world() < 2) return fail(H2G_ERR_STATE, "comm_spmd_install: needs a communicator (h2g_comm_init)");
+  g_spmd = h2g_spmd_transport{comm_spmd_ctx(), comm_world(), comm_rank(), comm_allgather_partial};
+  g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
+  g_spmd_seq = 0;
+  return H2G_OK;
+}
+
+int h2g_comm_spmd_uninstall(void) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr};
+  g_spmd_seq = 0;
+  return H2G_OK;
 }
 
 int h2g_comm_install(uint64_t params) {

@@ -112,6 +112,9 @@ _SIGS = {
     "h2g_comm_serve": ([U64, ctypes.POINTER(U64)], I32),
     "h2g_comm_stop": ([], I32),
     "h2g_comm_destroy": ([], I32),
+    "h2g_set_spmd_transport": ([VP], I32),
+    "h2g_comm_spmd_install": ([], I32),
+    "h2g_comm_spmd_uninstall": ([], I32),
 }
 
 MSM_PHASES = ("partition_coarse", "partition_fine", "bucket_bounds", "accumulate", "bucket_fixup", "reduce")
@@ -811,7 +814,7 @@ def set_shard_transport(world, launch=None, collect=None):
             launch(int(seq), int(base_set), int(n), int(d_scalars or 0))
             return 0
         except Exception as e:  # noqa: BLE001 -- reported through the C status
-            _transport_keep[3].append(e)
+            _transport_keep[-1].append(e)
             return 1
 
     def _collect(ctx, seq, partials, ids):
@@ -825,7 +828,7 @@ def set_shard_transport(world, launch=None, collect=None):
                 ids[i] = 1 if is_id else 0
             return 0
         except Exception as e:  # noqa: BLE001
-            _transport_keep[3].append(e)
+            _transport_keep[-1].append(e)
             return 1
 
     cl, cc = SHARD_LAUNCH(_launch), SHARD_COLLECT(_collect)
@@ -838,9 +841,43 @@ def transport_errors():
     """exceptions raised inside the installed transport's callbacks (cleared)"""
     if _transport_keep is None:
         return []
-    errs = list(_transport_keep[3])
-    _transport_keep[3].clear()
+    errs = list(_transport_keep[-1])
+    _transport_keep[-1].clear()
     return errs
+
+
+SPMD_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, VP, U64, U64P, U64P)
+
+
+class SpmdTransport(ctypes.Structure):
+    """struct h2g_spmd_transport (include/h2g.h)"""
+    _fields_ = [("ctx", VP), ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("allgather", SPMD_ALLGATHER)]
+
+
+def set_spmd_transport(world, rank=0, allgather=None):
+    """SPMD sharding: every rank runs the same create_proof and computes its point slab of
+    each commitment MSM; allgather(seq, mine: uint64[9]) -> uint64[world, 9] (rank order)
+    collects the partials.  world <= 1 removes it.  Exceptions fail the proof."""
+    global _transport_keep
+    if world <= 1:
+        check(lib().h2g_set_spmd_transport(None))
+        _transport_keep = None
+        return
+
+    def _ag(ctx, seq, mine, out):
+        try:
+            got = np.ascontiguousarray(allgather(int(seq), np.ctypeslib.as_array(mine, shape=(9,)).copy()),
+                                       dtype=np.uint64).reshape(world * 9)
+            ctypes.memmove(out, got.ctypes.data, world * 9 * 8)
+            return 0
+        except Exception as e:  # noqa: BLE001 -- reported through the C status
+            _transport_keep[2].append(e)
+            return 1
+
+    cb = SPMD_ALLGATHER(_ag)
+    t = SpmdTransport(None, world, rank, cb)
+    _transport_keep = (t, cb, [])
+    check(lib().h2g_set_spmd_transport(ctypes.byref(t)))
 
 
 # ------------------------------------------------- native RCCL transport (csrc/comm.cpp)
@@ -870,6 +907,15 @@ def comm_stop():
 
 def comm_destroy():
     check(lib().h2g_comm_destroy())
+
+
+def comm_spmd_install():
+    """SPMD sharding over the library's communicator (RCCL all-gather of the partials)"""
+    check(lib().h2g_comm_spmd_install())
+
+
+def comm_spmd_uninstall():
+    check(lib().h2g_comm_spmd_uninstall())
 
 
 def params_msm_dev(params, base_set, offset, n, d_scalars):

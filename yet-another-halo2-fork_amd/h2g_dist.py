@@ -181,3 +181,36 @@ class SlabWorker:
             rep[8] = 1 if is_id else 0
             dist.send(torch.from_numpy(rep.view(np.int64)).to(dev), 0, group=self.group)
             count += 1
+
+
+class SpmdGather:
+    """SPMD sharding over torch.distributed (h2g_set_spmd_transport): every rank runs the
+    same create_proof and computes point slab `rank` of each commitment MSM; the 9-word
+    partials (affine limbs + identity flag) are all-gathered in rank order and every rank
+    sums them, so no scalars travel.  h2g_comm_spmd_install is the same over the library's
+    own RCCL communicator."""
+
+    def __init__(self, dist, group=None):
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.device = _staging(dist, group)
+        self.calls = 0
+
+    def allgather(self, seq, mine):
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(mine, dtype=np.uint64).view(np.int64)).to(self.device)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.group)
+        self.calls += 1
+        return np.stack([o.cpu().numpy().view(np.uint64) for o in out])
+
+    def install(self):
+        import h2g
+        h2g.set_spmd_transport(self.world, self.rank, self.allgather)
+
+    @staticmethod
+    def uninstall():
+        import h2g
+        h2g.set_spmd_transport(1)
