@@ -57,8 +57,8 @@ int h2g_msm(const uint64_t* coeffs, const uint64_t* bases, size_t n, uint64_t ou
 int h2g_msm_coeffs_descriptor(const uint64_t* coeffs, size_t n, uint64_t* handle);
 int h2g_msm_base_descriptor(const uint64_t* bases, size_t n, uint64_t* handle);
 int h2g_msm_descriptor_free(uint64_t handle); /* Drop of a descriptor (zal.rs:47) */
-/* Base descriptors keep fixed-base windows ([2^(c w)] P_i, W x n x 64 B of HBM) so the
- * MSM runs one shared bucket set; the _dev variants take device-resident bases /
+/* Base descriptors keep fixed-base windows ([2^(o_w)] P_i at each window's bit offset o_w,
+ * W x n x 64 B of HBM) so the MSM runs one shared bucket set; the _dev variants take device-resident bases /
  * scalars (window_bits 0 = choose). */
 int h2g_msm_base_descriptor_dev(const void* d_bases, size_t n, int window_bits, uint64_t* handle);
 int h2g_msm_with_cached_base_dev(const void* d_scalars, size_t n, uint64_t base, size_t base_offset,
@@ -239,6 +239,10 @@ int h2g_pk_vk_commitments(uint64_t pk, uint64_t* fixed, uint64_t* perm);
  * (default; poly/kzg/multiopen/shplonk/prover.rs:121-305), 1 ProverGWC
  * (poly/kzg/multiopen/gwc/prover.rs:40-90) */
 int h2g_pk_set_multiopen(uint64_t pk, int scheme);
+/* the transcript the proof is written with -- create_proof's TranscriptWrite type
+ * parameter: 0 Blake2bWrite (default; halo2_backend/src/transcript.rs:291-419),
+ * 1 Keccak256Write (EVM-verifiable; transcript.rs:299-463) */
+int h2g_pk_set_transcript(uint64_t pk, int kind);
 
 /* advice: num_advice x n Fr; instance: num_instance x n Fr (zero padded), of which
  * instance_lens[i] values enter the transcript.  Writes the proof bytes.

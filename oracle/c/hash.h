@@ -173,4 +173,64 @@ static void chacha_rng_fill(chacha_rng *r, uint8_t *out, size_t len) {
     }
 }
 
+/* Keccak-256 (the original Keccak padding 0x01 .. 0x80, as the `sha3` crate's Keccak256 used
+ * by Keccak256Write, halo2_backend/src/transcript.rs:299-463): Keccak-f[1600], rate 136 bytes.
+ * pad = 0x06 gives SHA3-256 (the permutation is pinned against hashlib.sha3_256). */
+typedef struct {
+    uint64_t a[25];
+    uint8_t buf[136];
+    size_t fill;
+} keccak_state;
+
+static void keccak_f1600(uint64_t a[25]) {
+    static const uint64_t RC[24] = {
+        0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808aULL, 0x8000000080008000ULL,
+        0x000000000000808bULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+        0x000000000000008aULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000aULL,
+        0x000000008000808bULL, 0x800000000000008bULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+        0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800aULL, 0x800000008000000aULL,
+        0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+    static const int ROT[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+    for (int round = 0; round < 24; round++) {
+        uint64_t c[5], d[5], b[25];
+        for (int x = 0; x < 5; x++) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+        for (int x = 0; x < 5; x++) d[x] = c[(x + 4) % 5] ^ ((c[(x + 1) % 5] << 1) | (c[(x + 1) % 5] >> 63));
+        for (int i = 0; i < 25; i++) a[i] ^= d[i % 5];
+        /* rho + pi: B[y, 2x + 3y] = rot(A[x, y], r[x, y]) (lane index x + 5 y) */
+        for (int x = 0; x < 5; x++)
+            for (int y = 0; y < 5; y++) {
+                const int r = ROT[x + 5 * y];
+                const uint64_t v = a[x + 5 * y];
+                b[y + 5 * ((2 * x + 3 * y) % 5)] = r ? (v << r) | (v >> (64 - r)) : v;
+            }
+        for (int y = 0; y < 5; y++)
+            for (int x = 0; x < 5; x++) a[x + 5 * y] = b[x + 5 * y] ^ (~b[(x + 1) % 5 + 5 * y] & b[(x + 2) % 5 + 5 * y]);
+        a[0] ^= RC[round];
+    }
+}
+static void keccak_absorb_block(keccak_state *S, const uint8_t *blk) {
+    for (int i = 0; i < 17; i++) S->a[i] ^= load64le(blk + 8 * i);
+    keccak_f1600(S->a);
+}
+static void keccak_init(keccak_state *S) { memset(S, 0, sizeof(*S)); }
+static void keccak_update(keccak_state *S, const void *in_, size_t len) {
+    const uint8_t *in = (const uint8_t *)in_;
+    while (len) {
+        size_t take = 136 - S->fill;
+        if (take > len) take = len;
+        memcpy(S->buf + S->fill, in, take);
+        S->fill += take; in += take; len -= take;
+        if (S->fill == 136) { keccak_absorb_block(S, S->buf); S->fill = 0; }
+    }
+}
+/* finalize a COPY (Keccak256::clone().finalize()) */
+static void keccak_final_copy(const keccak_state *S0, uint8_t pad, uint8_t out[32]) {
+    keccak_state S = *S0;
+    memset(S.buf + S.fill, 0, 136 - S.fill);
+    S.buf[S.fill] ^= pad;
+    S.buf[135] ^= 0x80;
+    keccak_absorb_block(&S, S.buf);
+    for (int i = 0; i < 32; i++) out[i] = (uint8_t)(S.a[i / 8] >> (8 * (i % 8)));
+}
+
 #endif

@@ -91,6 +91,8 @@ typedef struct {
     int (*rng_fill_bytes)(void *ctx, uint8_t *out, size_t len);
     int (*rng_random_fr)(void *ctx, uint64_t *out);
     void *rng_ctx;
+    /* 0 Blake2bWrite, 1 Keccak256Write (halo2_backend/src/transcript.rs:299-463) */
+    uint32_t transcript;
 } or_spec;
 
 typedef struct { int type, index, rot; } query_t;
@@ -147,15 +149,31 @@ static fe fr_pow_u64(const fe *a, uint64_t e) {
 }
 
 /* ====================================================================== transcript */
+/* Blake2bWrite (transcript.rs:120-130,353-419) or Keccak256Write (transcript.rs:299-463):
+ * the same prefixes (challenge 0, point 1, scalar 2) absorbed into the growing state;
+ * Keccak256 squeezes [0] into the state, then hashes two copies with the extra bytes 10
+ * and 11 (not kept in the state) for the low and high 32 bytes of the 64 uniform bytes */
 typedef struct {
+    int kind;
     blake2b_state st;
+    keccak_state ks;
     uint8_t *proof;
     size_t len, cap;
 } transcript_t;
 
-static void tr_init(transcript_t *t, uint8_t *buf, size_t cap) {
-    blake2b_init(&t->st, 64, (const uint8_t *)"Halo2-Transcript");
+static void tr_init(transcript_t *t, int kind, uint8_t *buf, size_t cap) {
+    t->kind = kind;
+    if (kind == 1) {
+        keccak_init(&t->ks);
+        keccak_update(&t->ks, "Halo2-Transcript", 16);
+    } else {
+        blake2b_init(&t->st, 64, (const uint8_t *)"Halo2-Transcript");
+    }
     t->proof = buf; t->len = 0; t->cap = cap;
+}
+static void tr_absorb(transcript_t *t, const uint8_t *b, size_t len) {
+    if (t->kind == 1) keccak_update(&t->ks, b, len);
+    else blake2b_update(&t->st, b, len);
 }
 static void fr_repr(const fe *a, uint8_t out[32]) {
     uint64_t c[4]; fr_to_canonical(c, a);
@@ -167,7 +185,7 @@ static void fq_repr(const fe *a, uint8_t out[32]) {
 }
 static void tr_common_scalar(transcript_t *t, const fe *s) {
     uint8_t b[33]; b[0] = 2; fr_repr(s, b + 1);
-    blake2b_update(&t->st, b, 33);
+    tr_absorb(t, b, 33);
 }
 static void tr_write_scalar(transcript_t *t, const fe *s) {
     tr_common_scalar(t, s);
@@ -178,7 +196,7 @@ static void tr_write_scalar(transcript_t *t, const fe *s) {
 static int tr_write_point(transcript_t *t, const g1a *p) {
     if (g1a_is_id(p)) return -1;  /* "cannot write points at infinity to the transcript" */
     uint8_t b[65]; b[0] = 1; fq_repr(&p->x, b + 1); fq_repr(&p->y, b + 33);
-    blake2b_update(&t->st, b, 65);
+    tr_absorb(t, b, 65);
     uint8_t c[32]; memcpy(c, b + 1, 32);
     if (b[33] & 1) c[31] |= 0x80;  /* compressed: x, sign of y in the top bit */
     if (t->len + 32 <= t->cap) memcpy(t->proof + t->len, c, 32);
@@ -186,8 +204,18 @@ static int tr_write_point(transcript_t *t, const g1a *p) {
     return 0;
 }
 static fe tr_squeeze(transcript_t *t) {
-    uint8_t z = 0; blake2b_update(&t->st, &z, 1);
-    uint8_t h[64]; blake2b_final_copy(&t->st, h);
+    uint8_t z = 0; tr_absorb(t, &z, 1);
+    uint8_t h[64];
+    if (t->kind == 1) {
+        keccak_state lo = t->ks, hi = t->ks;
+        const uint8_t plo = 10, phi = 11;
+        keccak_update(&lo, &plo, 1);
+        keccak_update(&hi, &phi, 1);
+        keccak_final_copy(&lo, 0x01, h);
+        keccak_final_copy(&hi, 0x01, h + 32);
+    } else {
+        blake2b_final_copy(&t->st, h);
+    }
     uint64_t d[8];
     for (int i = 0; i < 8; i++) d[i] = load64le(h + 8 * i);
     static const fe R3 = {{0x5e94d8e1b4bf0040ULL, 0x2a489cbe1cfbb6b8ULL, 0x893cc664a19fcfedULL, 0x0cf8594b7fcc657cULL}};
@@ -634,7 +662,7 @@ int or_prove(const or_pk *pk, const or_spec *s_in, uint8_t *proof, uint64_t proo
     prng_t rng = {0};
     chacha_rng_init(&rng.cc, s->rng_seed ? s->rng_seed : (const uint8_t *)"\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0");
     rng.fb = s->rng_fill_bytes; rng.fr = s->rng_random_fr; rng.ctx = s->rng_ctx;
-    transcript_t T; tr_init(&T, proof, proof_cap);
+    transcript_t T; tr_init(&T, (int)s->transcript, proof, proof_cap);
     { fe tr = fe_from(s->transcript_repr); tr_common_scalar(&T, &tr); }       /* vk.hash_into */
     /* every circuit's instances (prover.rs:187-271; KZG: QUERY_INSTANCE = false) */
     for (int ci = 0; ci < NC; ci++) {
@@ -1239,6 +1267,12 @@ void or_blake2b(const uint8_t *in, uint64_t len, const uint8_t *personal, uint8_
     blake2b_state S; blake2b_init(&S, 64, personal);
     blake2b_update(&S, in, len);
     blake2b_final_copy(&S, out64);
+}
+/* pad 0x01: Keccak-256 (Keccak256Write); 0x06: SHA3-256 (pins the permutation) */
+void or_keccak(const uint8_t *in, uint64_t len, uint8_t pad, uint8_t *out32) {
+    keccak_state S; keccak_init(&S);
+    keccak_update(&S, in, len);
+    keccak_final_copy(&S, pad, out32);
 }
 void or_chacha20_block(const uint8_t *key, uint64_t counter, uint8_t *out64) { chacha20_block(key, counter, out64); }
 void or_fr_random_stream(const uint8_t *seed, uint64_t count, uint64_t *out) {

@@ -89,6 +89,28 @@ class Blake2bRead:
         return v
 
 
+class Keccak256Read(Blake2bRead):
+    """Keccak256Read (transcript.rs:109-150,248-288): the state starts with
+    "Halo2-Transcript"; the same prefixes; squeeze = update([0]), then two clones
+    finalized after the extra bytes 10 and 11 (not kept in the state) give the low and
+    high 32 of the 64 uniform bytes.  Keccak-256 from keccak_ref (Python ints)."""
+
+    def __init__(self, proof: bytes):
+        from keccak_ref import Keccak
+        self.h = Keccak(0x01).update(b"Halo2-Transcript")
+        self.buf = proof
+        self.pos = 0
+
+    def squeeze(self) -> int:
+        self.h.update(b"\x00")
+        lo = self.h.copy().update(b"\x0a").digest()
+        hi = self.h.copy().update(b"\x0b").digest()
+        return int.from_bytes(lo + hi, "little") % R
+
+
+TRANSCRIPTS = {"blake2b": Blake2bRead, "keccak256": Keccak256Read}
+
+
 # ----------------------------------------------------------------------------- keygen restated
 def permutation_mapping(circ):
     """Assembly::copy over the copies in order (permutation/keygen.rs:48-97);
@@ -212,9 +234,10 @@ def affine_from_limbs(a):
 
 
 def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen="shplonk", vk=None,
-           instances_multi=None):
+           instances_multi=None, transcript="blake2b"):
     """Returns True iff the proof verifies (raises VerifyError on malformed input).
     multiopen: "shplonk" (VerifierSHPLONK) or "gwc" (VerifierGWC).
+    transcript: "blake2b" (Blake2bRead) or "keccak256" (Keccak256Read).
     vk: optional (fixed commitments, permutation commitments) -- each a list of (x, y) ints
     or 8-limb affine arrays -- taken instead of recomputing [f(s)]G here (large k).
     instances_multi: per-circuit instance columns of a proof over several circuits
@@ -253,7 +276,7 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen=
         sig = sigma_values(circ, dom)
         sigma_cm = [commit_lagrange(v) for v in sig]
 
-    T = Blake2bRead(proof)
+    T = TRANSCRIPTS[transcript](proof)
     T.common_scalar(fr_from_limbs(circ.transcript_repr()))
     for inst in insts:
         for col in inst:

@@ -69,6 +69,7 @@ def lib():
             "or_srs_lagrange": ([U64P, u32, U64P], None),
             "or_blake2b": ([ctypes.c_char_p, u64, ctypes.c_char_p, ctypes.c_char_p], None),
             "or_chacha20_block": ([ctypes.c_char_p, u64, ctypes.c_char_p], None),
+            "or_keccak": ([ctypes.c_char_p, u64, ctypes.c_uint8, ctypes.c_char_p], None),
             "or_fr_random_stream": ([ctypes.c_char_p, u64, U64P], None),
             "or_set_kernel_threads": ([i32], None),
         }
@@ -78,6 +79,13 @@ def lib():
             f.restype = res
         _lib = L
     return _lib
+
+
+def keccak(data, pad=0x01):
+    """the oracle's Keccak sponge: pad 0x01 = Keccak-256, 0x06 = SHA3-256"""
+    out = ctypes.create_string_buffer(32)
+    lib().or_keccak(bytes(data), len(data), pad, out)
+    return out.raw
 
 
 def fr_arr(n):
@@ -236,6 +244,7 @@ class OrSpec(ctypes.Structure):
         ("instance_c", ctypes.POINTER(ctypes.c_void_p)), ("instance_lens_c", ctypes.POINTER(ctypes.c_void_p)),
         ("fill_multi", ctypes.c_void_p),
         ("rng_fill_bytes", ctypes.c_void_p), ("rng_random_fr", ctypes.c_void_p), ("rng_ctx", ctypes.c_void_p),
+        ("transcript", ctypes.c_uint32),
     ]
 
 
@@ -316,14 +325,17 @@ class Keygen:
 
 
 def create_proof(circ, wit, srs_g, srs_gl, seed=bytes([7] * 32), vanishing_threads=8, threads=8, keygen=None,
-                 multiopen="shplonk", fill=None, challenges_out=None, wits=None, rng=None, fills=None):
+                 multiopen="shplonk", fill=None, challenges_out=None, wits=None, rng=None, fills=None,
+                 transcript="blake2b"):
     """Oracle create_proof -> proof bytes (multiopen: "shplonk" = ProverSHPLONK, "gwc" = ProverGWC).
     fill: the per-phase witness source fill(phase, challenges) -> {column: values}
     (h2g.witness_fill); challenges_out: a list that receives the squeezed challenges.
     wits: several circuits' witnesses in one proof (create_proof's circuits: &[C]; `wit`
     is then only used for the spec's shapes), fills: their per-circuit witness sources;
-    rng: the caller's RngCore (fill_bytes(n), optionally random_fr()) instead of the seed."""
+    rng: the caller's RngCore (fill_bytes(n), optionally random_fr()) instead of the seed.
+    transcript: "blake2b" (Blake2bWrite) or "keccak256" (Keccak256Write)."""
     spec, keep = make_spec(circ, wit, srs_g, srs_gl, seed, vanishing_threads, multiopen)
+    spec.transcript = {"blake2b": 0, "keccak256": 1}[transcript]
     ch = np.zeros((max(circ.num_challenges, 1), 4), dtype=np.uint64)
     spec.challenges_out = _ptr(ch, U64P)
     import h2g

@@ -143,6 +143,7 @@ struct ProvingKey {
   // multi-open scheme of create_proof (the Prover type parameter, prover.rs:19-36):
   // 0 ProverSHPLONK, 1 ProverGWC; GWC witness polynomials, one per opening point
   int multiopen = 0;
+  int transcript = 0;  // TRANSCRIPT_BLAKE2B / TRANSCRIPT_KECCAK256 (transcript.h)
   std::vector<Fr*> gwc_q;
   uint32_t* lk_cnt = nullptr;  // pinned per-(circuit, lookup) match counters (3 each)
   size_t lk_cnt_len = 0;
@@ -1030,7 +1031,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   for (int c = 0; c < ncirc; c++) W[c] = pk.cws[c].get();
   StageClock clk(st, g_stage_sync);
   ProverRng& rng = *in.rng;
-  Transcript tr(proof);
+  Transcript tr(proof, pk.transcript);
   auto write_point = [&](const G1Affine& p) -> int {
     if (!tr.write_point(p)) return fail(H2G_ERR_ARG, "cannot write points at infinity to the transcript");
     return H2G_OK;
@@ -2356,6 +2357,16 @@ int h2g_pk_set_multiopen(uint64_t pk, int scheme) {
   if (it == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
   if (scheme != 0 && scheme != 1) return fail(H2G_ERR_ARG, "pk_set_multiopen: scheme must be 0 (SHPLONK) or 1 (GWC)");
   it->second->multiopen = scheme;
+  return H2G_OK;
+}
+
+int h2g_pk_set_transcript(uint64_t pk, int kind) {
+  NEED_DEV_P();
+  auto it = g_pks.find(pk);
+  if (it == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
+  if (kind != TRANSCRIPT_BLAKE2B && kind != TRANSCRIPT_KECCAK256)
+    return fail(H2G_ERR_ARG, "pk_set_transcript: kind must be 0 (Blake2bWrite) or 1 (Keccak256Write)");
+  it->second->transcript = kind;
   return H2G_OK;
 }
 

@@ -1,6 +1,7 @@
 // transcript.h -- host-side Fiat-Shamir transcript and prover RNG.
 //
 //   Blake2bWrite<_, G1Affine, Challenge255>  halo2_backend/src/transcript.rs:120-130,353-419
+//   Keccak256Write<_, G1Affine, Challenge255> halo2_backend/src/transcript.rs:299-351,370-463
 //     personal "Halo2-Transcript"; absorb prefixes: challenge 0, point 1, scalar 2;
 //     squeeze = absorb [0] then finalize a copy of the state -> 64 bytes ->
 //     from_uniform_bytes (LE512 mod r).  Points: x, y canonical LE absorbed; the
@@ -256,14 +257,90 @@ class ProverRng {
   bool failed_ = false;
 };
 
+// Keccak-256 (the `sha3` crate's Keccak256: Keccak-f[1600], rate 136, padding 0x01..0x80)
+class Keccak256 {
+ public:
+  Keccak256() { std::memset(a_, 0, sizeof(a_)); }
+  void update(const void* data, size_t len) {
+    const uint8_t* p = static_cast<const uint8_t*>(data);
+    while (len) {
+      size_t take = 136 - fill_ < len ? 136 - fill_ : len;
+      std::memcpy(buf_ + fill_, p, take);
+      fill_ += take;
+      p += take;
+      len -= take;
+      if (fill_ == 136) {
+        absorb(buf_);
+        fill_ = 0;
+      }
+    }
+  }
+  // digest of a copy (the state stays usable: Keccak256::clone().finalize())
+  void digest(uint8_t out[32]) const {
+    Keccak256 k = *this;
+    std::memset(k.buf_ + k.fill_, 0, 136 - k.fill_);
+    k.buf_[k.fill_] ^= 0x01;
+    k.buf_[135] ^= 0x80;
+    k.absorb(k.buf_);
+    for (int i = 0; i < 32; i++) out[i] = (uint8_t)(k.a_[i / 8] >> (8 * (i % 8)));
+  }
+
+ private:
+  static uint64_t rotl(uint64_t v, int r) { return r ? (v << r) | (v >> (64 - r)) : v; }
+  void absorb(const uint8_t* blk) {
+    for (int i = 0; i < 17; i++) {
+      uint64_t w;
+      std::memcpy(&w, blk + 8 * i, 8);
+      a_[i] ^= w;
+    }
+    permute();
+  }
+  void permute() {
+    static const uint64_t RC[24] = {
+        0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808aULL, 0x8000000080008000ULL,
+        0x000000000000808bULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+        0x000000000000008aULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000aULL,
+        0x000000008000808bULL, 0x800000000000008bULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+        0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800aULL, 0x800000008000000aULL,
+        0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+    // rotation of lane x + 5 y (FIPS 202 rho)
+    static const int ROT[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+    for (int round = 0; round < 24; round++) {
+      uint64_t c[5], b[25];
+      for (int x = 0; x < 5; x++) c[x] = a_[x] ^ a_[x + 5] ^ a_[x + 10] ^ a_[x + 15] ^ a_[x + 20];
+      for (int x = 0; x < 5; x++) {
+        const uint64_t d = c[(x + 4) % 5] ^ rotl(c[(x + 1) % 5], 1);
+        for (int y = 0; y < 25; y += 5) a_[x + y] ^= d;
+      }
+      for (int x = 0; x < 5; x++)
+        for (int y = 0; y < 5; y++) b[y + 5 * ((2 * x + 3 * y) % 5)] = rotl(a_[x + 5 * y], ROT[x + 5 * y]);
+      for (int y = 0; y < 25; y += 5)
+        for (int x = 0; x < 5; x++) a_[x + y] = b[x + y] ^ (~b[(x + 1) % 5 + y] & b[(x + 2) % 5 + y]);
+      a_[0] ^= RC[round];
+    }
+  }
+  uint64_t a_[25];
+  uint8_t buf_[136] = {};
+  size_t fill_ = 0;
+};
+
+// Blake2bWrite (transcript.rs:120-130,353-419) or Keccak256Write (transcript.rs:299-463):
+// the same prefixes absorbed into the growing state; a Keccak256 squeeze absorbs [0], then
+// hashes two copies with the extra bytes 10 and 11 (not kept) for the low and high 32 of
+// the 64 uniform bytes
+enum { TRANSCRIPT_BLAKE2B = 0, TRANSCRIPT_KECCAK256 = 1 };
+
 class Transcript {
  public:
-  explicit Transcript(std::vector<uint8_t>* proof) : h_("Halo2-Transcript"), proof_(proof) {}
+  explicit Transcript(std::vector<uint8_t>* proof, int kind = TRANSCRIPT_BLAKE2B)
+      : h_("Halo2-Transcript"), kind_(kind), proof_(proof) {
+    if (kind_ == TRANSCRIPT_KECCAK256) k_.update("Halo2-Transcript", 16);
+  }
   void common_scalar(const Fr& s) {
     uint8_t b[33];
     b[0] = 2;
     repr(to_canonical(s), b + 1);
-    h_.update(b, 33);
+    absorb(b, 33);
   }
   void write_scalar(const Fr& s) {
     common_scalar(s);
@@ -278,7 +355,7 @@ class Transcript {
     b[0] = 1;
     repr(to_canonical(p.x), b + 1);
     repr(to_canonical(p.y), b + 33);
-    h_.update(b, 65);
+    absorb(b, 65);
     uint8_t c[32];
     std::memcpy(c, b + 1, 32);
     if (b[33] & 1) c[31] |= 0x80;
@@ -287,9 +364,18 @@ class Transcript {
   }
   Fr squeeze() {
     const uint8_t z = 0;
-    h_.update(&z, 1);
+    absorb(&z, 1);
     uint8_t d[64];
-    h_.digest(d);
+    if (kind_ == TRANSCRIPT_KECCAK256) {
+      Keccak256 lo = k_, hi = k_;
+      const uint8_t plo = 10, phi = 11;
+      lo.update(&plo, 1);
+      hi.update(&phi, 1);
+      lo.digest(d);
+      hi.digest(d + 32);
+    } else {
+      h_.digest(d);
+    }
     uint32_t w[16];
     std::memcpy(w, d, 64);
     return fr_from_u512(w);
@@ -300,7 +386,13 @@ class Transcript {
   static void repr(const F& c, uint8_t out[32]) {
     std::memcpy(out, c.l, 32);  // canonical limbs, little-endian
   }
+  void absorb(const uint8_t* b, size_t len) {
+    if (kind_ == TRANSCRIPT_KECCAK256) k_.update(b, len);
+    else h_.update(b, len);
+  }
   Blake2b h_;
+  Keccak256 k_;
+  int kind_;
   std::vector<uint8_t>* proof_;
 };
 

@@ -93,6 +93,7 @@ _SIGS = {
     "h2g_pk_info": ([U64, ctypes.POINTER(ctypes.c_int32)], I32),
     "h2g_pk_vk_commitments": ([U64, U64P, U64P], I32),
     "h2g_pk_set_multiopen": ([U64, I32], I32),
+    "h2g_pk_set_transcript": ([U64, I32], I32),
     "h2g_create_proof": ([U64, U64, VP, I32, U64P, ctypes.POINTER(U32), ctypes.c_char_p, U32, ctypes.c_char_p, SZ,
                           ctypes.POINTER(SZ)], I32),
     "h2g_create_proof_phased": ([U64, U64, VP, U64P, ctypes.POINTER(U32), ctypes.c_char_p, U32, ctypes.c_char_p,
@@ -117,6 +118,7 @@ _SIGS = {
     "h2g_comm_spmd_uninstall": ([], I32),
 }
 
+TRANSCRIPTS = {"blake2b": 0, "keccak256": 1}  # Blake2bWrite / Keccak256Write (h2g_pk_set_transcript)
 MSM_PHASES = ("partition_coarse", "partition_fine", "bucket_bounds", "accumulate", "bucket_fixup", "reduce")
 
 _lib = None
@@ -673,11 +675,12 @@ class ProvingKey:
         return _write_bytes(lib().h2g_pk_write, self.handle, fmt)
 
     def create_proof(self, wit=None, seed=bytes([7] * 32), vanishing_threads=8, advice_dev_ptr=None,
-                     multiopen="shplonk"):
+                     multiopen="shplonk", transcript="blake2b"):
         """-> proof bytes.  advice_dev_ptr: device pointer to num_advice x n Fr (resident inputs).
         multiopen: "shplonk" (ProverSHPLONK) or "gwc" (ProverGWC)."""
         if multiopen != "shplonk" or hasattr(lib(), "h2g_pk_set_multiopen"):
             check(lib().h2g_pk_set_multiopen(self.handle, {"shplonk": 0, "gwc": 1}[multiopen]))
+        check(lib().h2g_pk_set_transcript(self.handle, TRANSCRIPTS[transcript]))
         circ = self.circ
         n = 1 << circ.k
         if advice_dev_ptr is not None:
@@ -698,11 +701,13 @@ class ProvingKey:
         del adv
         return buf.raw[: ln.value]
 
-    def create_proof_phased(self, fill, wit, seed=bytes([7] * 32), vanishing_threads=8, multiopen="shplonk"):
+    def create_proof_phased(self, fill, wit, seed=bytes([7] * 32), vanishing_threads=8, multiopen="shplonk",
+                            transcript="blake2b"):
         """Prover::commit_phase per phase with the witness from fill(phase, challenges) ->
         {column: values} (see witness_fill); wit supplies the instance columns.
         -> (proof bytes, challenges as ints)"""
         check(lib().h2g_pk_set_multiopen(self.handle, {"shplonk": 0, "gwc": 1}[multiopen]))
+        check(lib().h2g_pk_set_transcript(self.handle, TRANSCRIPTS[transcript]))
         circ = self.circ
         ins = np.ascontiguousarray(wit.instance, dtype=np.uint64) if circ.num_instance else np.zeros(4, np.uint64)
         lens = np.ascontiguousarray(wit.instance_lens if circ.num_instance else np.zeros(1), dtype=np.uint32)
@@ -724,13 +729,14 @@ class ProvingKey:
         return buf.raw[: ln.value], hc.mont_to_ints(ch[: cnt.value])
 
     def create_proof_multi(self, wits, seed=bytes([7] * 32), rng=None, fills=None, vanishing_threads=8,
-                           multiopen="shplonk", advice_dev_ptrs=None):
+                           multiopen="shplonk", advice_dev_ptrs=None, transcript="blake2b"):
         """create_proof(params, pk, circuits, instances, rng, transcript) over several circuits
         (halo2_proofs/src/plonk/prover.rs:19-36) -> proof bytes.  wits: one witness per circuit
         (advice, or -- with fills -- only the instance columns); rng: None = ChaCha20Rng::from_seed(
         seed), else an object with fill_bytes(n) (and optionally random_fr()); fills: per-circuit
         fill(phase, challenges) -> {column: values} witness sources."""
         check(lib().h2g_pk_set_multiopen(self.handle, {"shplonk": 0, "gwc": 1}[multiopen]))
+        check(lib().h2g_pk_set_transcript(self.handle, TRANSCRIPTS[transcript]))
         circ = self.circ
         nc = len(wits)
         keep = []
