@@ -316,13 +316,26 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     if one_proof:  # fixed-base windows sized for this rank's point slab
         params.set_slab(*h2g_dist.slab(n, world, rank))
     native = one_proof and args.transport == "native"
+    transport_note = None
     if native:  # the library's own RCCL communicators (csrc/comm.cpp); the id travels over torch
         import torch as _t
-        uid = _t.zeros(256, dtype=_t.uint8, device=dev if dist.get_backend() == "nccl" else "cpu")
+        tdev = dev if dist.get_backend() == "nccl" else "cpu"
+        uid = _t.zeros(256, dtype=_t.uint8, device=tdev)
         if rank == 0:
             uid.copy_(_t.frombuffer(bytearray(h2g.comm_unique_id()), dtype=_t.uint8))
         dist.broadcast(uid, 0)
-        h2g.comm_init(bytes(uid.cpu().numpy().tobytes()), world, rank)
+        ok = 1
+        try:
+            h2g.comm_init(bytes(uid.cpu().numpy().tobytes()), world, rank)
+        except h2g.H2GError as e:  # every rank learns of any failure and falls back together
+            ok, transport_note = 0, f"native communicator failed ({e}); torch.distributed transport used"
+        flag = _t.tensor([ok], dtype=_t.int64, device=tdev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not int(flag.item()):
+            if ok:
+                h2g.comm_destroy()
+            native = False
+            transport_note = transport_note or "a peer's native communicator failed; torch.distributed transport used"
     if worker:
         slabs = None if native else h2g_dist.SlabWorker(dist, params=params)
     else:
@@ -418,7 +431,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         # outside the timed region: the proof checked by the independent verifier
         # (oracle/py/verifier.py, the checker), and one proof with synchronised stage
         # boundaries for a per-stage GPU time breakdown
-        extra["verified"] = verify_proof(h2g, circ, pk, proofs[0], s_int)
+        extra["verified"] = verify_proof(h2g, circ, pk, params, proofs[0])
         stages = []
         if not one_proof:
             h2g.prover_stage_sync(True)
@@ -475,6 +488,8 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         }
         if spmd:
             line["proof_bytes_equal_across_ranks"] = extra["ranks_equal"]
+        if transport_note:
+            line["transport_note"] = transport_note
     if args.workload == "prove" and (world == 1 or dist.get_backend() == "nccl"):
         # every rank takes part when sharded (collectives inside)
         m = measure_msm(h2g, torch, dev, 24, steps=10, warmup=2, dist=dist, world=world, rank=rank)
@@ -495,15 +510,17 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     return line
 
 
-def verify_proof(h2g, circ, pk, proof, s_int):
+def verify_proof(h2g, circ, pk, params, proof):
     """prove -> verify (halo2_proofs/tests/plonk_api.rs): the checker's verifier with the
     device key's VK commitments (the device VK equals the CPU-computed one in
-    tests/test_gpu_baseline_sizes.py)"""
+    tests/test_gpu_baseline_sizes.py) and the params' G2 elements -- DualMSM::check by the
+    pairing (oracle/py/pairing_ref.py), no SRS secret involved"""
     sys.path.insert(0, os.path.join(REPO, "oracle", "py"))
     import verifier as V
     f, p = pk.vk_commitments()
     vk = ([V.affine_from_limbs(c) for c in f], [V.affine_from_limbs(c) for c in p])
-    return bool(V.verify(circ, [], proof, s_int, vk=vk))
+    g2, s_g2 = params.g2()
+    return bool(V.verify(circ, [], proof, None, vk=vk, g2=(V.g2_from_limbs(g2), V.g2_from_limbs(s_g2))))
 
 
 def measure_msm(h2g, torch, dev, log_n, steps, warmup, dist=None, world=1, rank=0):

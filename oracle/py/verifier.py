@@ -17,8 +17,9 @@ Restated reference code (paths relative to the reference root):
   lookup / shuffle verifiers       halo2_backend/src/plonk/lookup/verifier.rs, shuffle/verifier.rs
 
 Pairings: the test setup knows the SRS secret s, so the pairing equation
-e(left, [s]G2) = e(right, G2) of DualMSM::check is decided exactly as
-[s]·left == right in G1.  VK commitments are computed as [f(s)]G the same way.
+e(left, [s]G2) = e(right, G2) of DualMSM::check is decided by the BN254 optimal ate
+pairing (pairing_ref.py) from the params' G2 elements when they are passed (`g2=`),
+else exactly as [s]·left == right in G1 with the secret.  VK commitments are computed as [f(s)]G the same way.
 
 Independent of the C code: field/curve arithmetic (Python ints), Blake2b (hashlib),
 the permutation Assembly and the query collection are restated again here.
@@ -234,10 +235,13 @@ def affine_from_limbs(a):
 
 
 def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen="shplonk", vk=None,
-           instances_multi=None, transcript="blake2b"):
+           instances_multi=None, transcript="blake2b", g2=None):
     """Returns True iff the proof verifies (raises VerifyError on malformed input).
     multiopen: "shplonk" (VerifierSHPLONK) or "gwc" (VerifierGWC).
     transcript: "blake2b" (Blake2bRead) or "keccak256" (Keccak256Read).
+    g2: the params' (g2, s_g2) as G2 affine int pairs: DualMSM::check is then decided by
+    the pairing equation e(left, s_g2) == e(right, g2) (pairing_ref) as the reference
+    does, and s is needed only to compute the VK when `vk` is not given.
     vk: optional (fixed commitments, permutation commitments) -- each a list of (x, y) ints
     or 8-limb affine arrays -- taken instead of recomputing [f(s)]G here (large k).
     instances_multi: per-circuit instance columns of a proof over several circuits
@@ -425,7 +429,7 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen=
     queries.append((("random",), random_cm, x, random_eval))
 
     if multiopen == "gwc":
-        return _verify_gwc(T, queries, proof, s)
+        return _verify_gwc(T, queries, proof, s, g2)
 
     # SHPLONK (construct_intermediate_sets + VerifierSHPLONK::verify_proof)
     super_points = sorted({q[2] for q in queries})
@@ -489,11 +493,28 @@ def verify(circ, instances, proof: bytes, s: int, instance_lens=None, multiopen=
     if T.pos != len(proof):
         raise VerifyError(f"trailing proof bytes: read {T.pos} of {len(proof)}")
     right = outer.eval()
-    left_s = g1_mul(h2, s)
-    return left_s == right
+    return _dual_msm_check(h2, right, s, g2)
 
 
-def _verify_gwc(T, queries, proof, s):
+def g2_from_limbs(a):
+    """a G2 affine point from 16 u64 (x.c0, x.c1, y.c0, y.c1, Montgomery limbs; the layout of
+    h2g_params_g2 and of halo2curves' G2Affine)"""
+    from bn254_ref import from_limbs, from_mont
+    v = [from_mont(from_limbs([int(t) for t in a[4 * i:4 * i + 4]]), P) for i in range(4)]
+    return (v[0], v[1]), (v[2], v[3])
+
+
+def _dual_msm_check(left, right, s, g2):
+    """DualMSM::check: e(left, [s]G2) == e(right, G2) -- by the pairing when the params'
+    G2 elements are given, else exactly as [s] left == right with the secret"""
+    if g2 is None:
+        return g1_mul(left, s) == right
+    from pairing_ref import pairing_check
+    g2_gen, s_g2 = g2
+    return pairing_check([(left, s_g2), (g1_neg(right) if right is not None else None, g2_gen)])
+
+
+def _verify_gwc(T, queries, proof, s, g2=None):
     """VerifierGWC::verify_proof (gwc/verifier.rs:42-123): queries grouped by point in
     first-appearance order (gwc.rs:25-50); one witness point per group; then
     DualMSM::check, decided as [s]·left == right."""
@@ -533,7 +554,7 @@ def _verify_gwc(T, queries, proof, s):
         upow = upow * u % R
     right.add_msm(commitment_multi)
     right.add(-eval_multi, G1_GEN)
-    return g1_mul(left.eval(), s) == right.eval()
+    return _dual_msm_check(left.eval(), right.eval(), s, g2)
 
 
 def sigma_lagrange(circ):
