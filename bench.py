@@ -346,7 +346,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         pk = h2g.ProvingKey(params, circ)
         adv = torch.from_numpy(np.ascontiguousarray(wit.advice).view(np.int64)).to(dev)  # resident witness
         client = h2g_dist.SlabClient(dist, points=n) if shard and not native else None
-        gather = h2g_dist.SpmdGather(dist) if spmd and not native else None
+        gather = h2g_dist.SpmdGather(dist, subcosets=not args.no_subcosets) if spmd and not native else None
     torch.cuda.synchronize()
     proofs = []
 
@@ -358,7 +358,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         stops; spmd: every rank proves with the all-gather installed"""
         if spmd:
             if native:
-                h2g.comm_spmd_install()
+                h2g.comm_spmd_install(not args.no_subcosets)
             else:
                 gather.install()
             try:
@@ -470,7 +470,9 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                                        f"one proof over {world} GPUs, SPMD: every rank runs the prover and "
                                        "computes its point slab of each commitment MSM, partials all-gathered ("
                                        + ("libh2g RCCL all-gather" if native else "torch.distributed all_gather")
-                                       + "); NTT/evaluate_h/SHPLONK replicated" if spmd else
+                                       + ("); extended-domain cosets + evaluate_h replicated" if args.no_subcosets else
+                                          "); extended-domain sub-cosets + evaluate_h divided over the ranks, h "
+                                          "broadcast; other transforms and SHPLONK replicated") if spmd else
                                        f"one proof over {world} GPUs: commitment MSMs in point slabs ("
                                        + ("libh2g RCCL communicators" if native else "torch.distributed p2p")
                                        + " slabs + partials), NTT/evaluate_h/SHPLONK on rank 0" if shard else
@@ -661,6 +663,8 @@ def main():
     ap.add_argument("--mode", choices=("spmd", "shard", "replicas"), default="spmd",
                     help="prove workload, N > 1: one proof over all GPUs -- every rank proves its MSM slabs "
                          "(spmd) or rank 0 proves and peers serve slabs (shard) -- or one proof per GPU (replicas)")
+    ap.add_argument("--no-subcosets", action="store_true",
+                    help="spmd: replicate the extended-domain work instead of splitting its sub-cosets")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=1, help="CPU baseline runs (median)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the PMC traffic passes")

@@ -388,10 +388,19 @@ typedef struct {
   int32_t world;
   int32_t rank;
   int (*allgather)(void* ctx, uint64_t seq, const uint64_t in[9], uint64_t* out);
+  /* optional -- NULL replicates the extended-domain work on every rank.  Otherwise the
+   * 2^e sub-cosets of the extended domain (e = extended_k - k; row t + 2^e m is point
+   * zeta w_ext^t w^m) are divided over the ranks: rank r computes the sub-cosets
+   * t = r, r + world, ... of every column and h(X) on those rows, and each sub-coset's
+   * h evaluations (n Fr, device memory) are broadcast from their owner t mod world:
+   * bcast(ctx, d_buf, bytes, root) in place, complete on return */
+  int (*bcast)(void* ctx, void* d_buf, size_t bytes, int root);
 } h2g_spmd_transport;
 /* install (world >= 2) or remove (NULL or world <= 1) */
 int h2g_set_spmd_transport(const h2g_spmd_transport* t);
-int h2g_comm_spmd_install(void);
+/* split_subcosets: 1 divides the extended domain's sub-cosets over the ranks (bcast over
+ * the communicator), 0 replicates that work */
+int h2g_comm_spmd_install(int split_subcosets);
 int h2g_comm_spmd_uninstall(void);
 
 #ifdef __cplusplus

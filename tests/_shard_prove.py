@@ -46,6 +46,8 @@ def main():
                     help="h2g_dist over torch.distributed, or libh2g's RCCL communicators (nccl only)")
     ap.add_argument("--mode", default="slab", choices=("slab", "spmd"),
                     help="slab: rank 0 proves, peers serve slabs; spmd: every rank proves its slab")
+    ap.add_argument("--no-subcosets", action="store_true",
+                    help="spmd: replicate the extended-domain work instead of splitting the sub-cosets")
     ap.add_argument("cases", nargs="+")
     args = ap.parse_args()
     rank = int(os.environ["RANK"])
@@ -119,6 +121,9 @@ def main():
 
 
 def spmd_main(args, rank, world, native):
+    if os.environ.get("H2G_DUMP_BASE"):  # debugging: one dump directory per rank
+        os.environ["H2G_DUMP"] = os.path.join(os.environ["H2G_DUMP_BASE"], f"r{rank}")
+        os.makedirs(os.environ["H2G_DUMP"], exist_ok=True)
     """every rank: the single-device proofs first, then the same proofs with its slab of
     every MSM and the all-gathered partials; all ranks must print identical bytes"""
     import hashlib
@@ -133,9 +138,9 @@ def spmd_main(args, rank, world, native):
         want = [_prove(pk, case), _prove(pk, case, seed=bytes(range(32)), vanishing_threads=3)]
         g = None
         if native:
-            h2g.comm_spmd_install()
+            h2g.comm_spmd_install(not args.no_subcosets)
         else:
-            g = D.SpmdGather(dist)
+            g = D.SpmdGather(dist, subcosets=not args.no_subcosets)
             g.install()
         try:
             got = [_prove(pk, case), _prove(pk, case, seed=bytes(range(32)), vanishing_threads=3)]
@@ -157,7 +162,8 @@ def spmd_main(args, rank, world, native):
         allok = [torch.empty_like(ok) for _ in range(world)]
         dist.all_gather(allok, ok)
         results[name] = {"same": all(int(a.item()) == 1 for a in allok), "same_ranks": same_ranks,
-                         "bytes": len(got[0]), "gathers": None if g is None else g.calls}
+                         "bytes": len(got[0]), "gathers": None if g is None else g.calls,
+                         "bcasts": None if g is None else g.bcasts}
         pk.close()
         params.close()
         dist.barrier()

@@ -27,11 +27,11 @@ def _gpus():
     return torch.cuda.device_count()
 
 
-def _run(world, cases, backend="gloo", transport="torch", mode="slab"):
+def _run(world, cases, backend="gloo", transport="torch", mode="slab", extra=()):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(HERE, "_shard_prove.py"), "--backend", backend, "--transport", transport,
-           "--mode", mode] + cases
+           "--mode", mode] + list(extra) + cases
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
@@ -57,16 +57,23 @@ def test_sharded_proof_three_ranks():
 
 
 def test_spmd_proof_two_and_three_ranks():
-    """SPMD: every rank proves with its slab of each MSM and the all-gathered partials;
-    every rank's bytes == the single-device proof"""
+    """SPMD: every rank proves with its slab of each MSM and the all-gathered partials, and
+    the extended domain's sub-cosets divided over the ranks (h broadcast from each owner);
+    every rank's bytes == the single-device proof.  Three ranks leave a rank without a
+    sub-coset for the degree-3 circuits (2 sub-cosets) and give one rank two of the
+    keccak-style circuit's four."""
     cases = ["simple_k6", "mixed_k10", "lookup_k11", "keccak_k12", "c3_k14", "challenge_k9"]
     res = _run(2, cases, mode="spmd")
     for nm in cases:
         assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
-        assert res[nm]["gathers"] > 0, (nm, res[nm])
-    res = _run(3, ["simple_k6", "lookup_k11"], mode="spmd")
-    for nm in ("simple_k6", "lookup_k11"):
+        assert res[nm]["gathers"] > 0 and res[nm]["bcasts"] > 0, (nm, res[nm])
+    res = _run(3, ["simple_k6", "lookup_k11", "keccak_k12", "c3_k14"], mode="spmd")
+    for nm in ("simple_k6", "lookup_k11", "keccak_k12", "c3_k14"):
         assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
+    # the MSM-only split (extended domain replicated)
+    res = _run(2, ["lookup_k11", "c3_k14"], mode="spmd", extra=["--no-subcosets"])
+    for nm in ("lookup_k11", "c3_k14"):
+        assert res[nm]["same"] and res[nm]["same_ranks"] and res[nm]["bcasts"] == 0, (nm, res[nm])
 
 
 @pytest.mark.parametrize("mode", ["slab", "spmd"])

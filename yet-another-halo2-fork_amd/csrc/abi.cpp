@@ -899,8 +899,10 @@ int h2g_memcpy_dtoh(void* dst, const void* src, size_t bytes) {
 int h2g_memcpy_dtod(void* dst, const void* src, size_t bytes) {
   NEED_DEV();
   if (bytes && (!dst || !src)) return fail(H2G_ERR_ARG, "memcpy_dtod: null pointer");
+  // on the library stream and waited for: a device-to-device hipMemcpy may return before
+  // the copy is done, and the prover's non-blocking streams would not order after it
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, d->stream));
   HIPCHK(hipStreamSynchronize(d->stream));
-  HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
   return H2G_OK;
 }
 int h2g_synchronize(void) {

@@ -178,6 +178,15 @@ int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[9], uint64
   return H2G_OK;
 }
 
+int comm_bcast(void* ctx, void* d_buf, size_t bytes, int root) {
+  Comm* c = static_cast<Comm*>(ctx);
+  if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm: no communicator for the SPMD broadcast");
+  HIPCHK(hipSetDevice(c->device));
+  NCCLCHK(ncclBroadcast(d_buf, d_buf, bytes, ncclUint8, root, c->tx, c->stx));
+  HIPCHK(hipStreamSynchronize(c->stx));
+  return H2G_OK;
+}
+
 void* comm_transport_ctx(uint64_t points) {
   if (!g_comm || g_comm->rank != 0) return nullptr;
   g_comm->points = points;

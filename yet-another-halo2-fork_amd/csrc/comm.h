@@ -42,6 +42,8 @@ int comm_send_partial(const uint64_t partial[8], int32_t is_identity);
 // (h2g_spmd_transport.allgather; ctx = Comm state from comm_spmd_ctx)
 void* comm_spmd_ctx();
 int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[9], uint64_t* out);
+// in-place broadcast of device memory from `root` (the sub-coset h evaluations)
+int comm_bcast(void* ctx, void* d_buf, size_t bytes, int root);
 
 }  // namespace rt
 }  // namespace h2g

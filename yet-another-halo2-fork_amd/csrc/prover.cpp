@@ -114,6 +114,17 @@ struct CircuitWs {
   EvalShuffle* d_shuffles = nullptr;
   uint64_t* wit_pin = nullptr;  // advice staging of the witness source (num_advice x n Fr), pinned if possible
   bool wit_pin_pinned = false;
+  // SPMD sub-coset split: per owned sub-coset i, the evaluate_h pointer tables with every
+  // extended-coset column replaced by its sub-coset i (built for ProvingKey::sub_key)
+  struct SubTables {
+    const Fr** load_col = nullptr;
+    const Fr** z = nullptr;
+    const Fr** perm_v = nullptr;
+    EvalLookup* lookups = nullptr;
+    EvalShuffle* shuffles = nullptr;
+  };
+  std::vector<SubTables> sub;
+  int64_t sub_key = -1;
   ~CircuitWs() {
     if (!wit_pin) return;
     if (wit_pin_pinned) (void)hipHostFree(wit_pin);
@@ -183,6 +194,16 @@ struct ProvingKey {
   Fr *mod = nullptr, *pre = nullptr, *scr = nullptr, *random_poly = nullptr, *h_ext = nullptr, *h_coeff = nullptr;
   Fr *h_poly = nullptr, *nx = nullptr, *q1 = nullptr, *q2 = nullptr, *hx = nullptr, *lx = nullptr;
   Fr *small = nullptr, *last_z = nullptr, *evals = nullptr, *eval_scr = nullptr;
+  // SPMD sub-coset split (h2g_spmd_transport.bcast): this rank's sub-cosets t = rank,
+  // rank + world, ... < 2^e of the extended domain; the key's cosets cut to them (slot i
+  // of each buffer = sub-coset sub_ts[i]), per-slot sigma tables, and the 2^e x n slots
+  // the h evaluations are broadcast through
+  int64_t sub_key = -1;  // world * 65536 + rank the cache holds
+  std::vector<uint64_t> sub_ts;
+  std::vector<Fr*> sub_fixed, sub_sigma;
+  Fr *sub_l0 = nullptr, *sub_ll = nullptr, *sub_la = nullptr;
+  std::vector<const Fr**> d_sigma_sub;
+  Fr* h_gather = nullptr;
   size_t scr_len = 0, eval_scr_len = 0;
   EvalReq* d_reqs = nullptr;
   int max_reqs = 0;
@@ -287,7 +308,7 @@ enum { SRS_G = 0, SRS_LAGRANGE = 1 };
 h2g_shard_transport g_shard{nullptr, 1, nullptr, nullptr};
 uint64_t g_shard_seq = 0;
 // SPMD sharding (h2g_set_spmd_transport): every rank proves, rank r computes slab r
-h2g_spmd_transport g_spmd{nullptr, 1, 0, nullptr};
+h2g_spmd_transport g_spmd{nullptr, 1, 0, nullptr, nullptr};
 uint64_t g_spmd_seq = 0;
 
 // slab r of an MSM of length n: the points [P r / world, P (r + 1) / world) of the
@@ -680,6 +701,110 @@ int circuit_ws_add(ProvingKey& pk) {
   return H2G_OK;
 }
 
+// ------------------------------------------------------------------ SPMD sub-cosets
+// Row y = t + 2^e m of the extended coset (e = extended_k - k) is the point
+// zeta w_ext^t w^m, so sub-coset t of a column is an n-point NTT of its coefficients
+// twisted by w_ext^(t j), and evaluate_h on rows of one sub-coset reads only sub-coset t of
+// every column: rotations move rows by multiples of 2^e (evaluation.rs:317-620 evaluates
+// the same expressions row by row; the row split does not change any value).
+bool spmd_subcosets() { return g_spmd.world > 1 && g_spmd.bcast != nullptr; }
+
+// the key's cosets cut to this rank's sub-cosets, once per (world, rank)
+int sub_prepare(ProvingKey& pk, hipStream_t st) {
+  const int64_t key = (int64_t)g_spmd.world * 65536 + g_spmd.rank;
+  if (pk.sub_key == key) return H2G_OK;
+  const int e = (int)(pk.dom.ek - pk.dom.k);
+  const uint64_t E = 1ull << e;
+  const size_t n = pk.n;
+  pk.sub_ts.clear();
+  for (uint64_t t = (uint64_t)g_spmd.rank; t < E; t += (uint64_t)g_spmd.world) pk.sub_ts.push_back(t);
+  const size_t nt = pk.sub_ts.size();
+  auto cut = [&](const Fr* full, Fr** out) -> int {
+    if (!*out) HIPCHK(pk.pool.get((void**)out, pk.ext * sizeof(Fr)));  // room for any rank's slots
+    for (size_t i = 0; i < nt; i++) HIPCHK(subcoset_gather(full, *out + i * n, n, pk.sub_ts[i], e, st));
+    return H2G_OK;
+  };
+  pk.sub_fixed.resize(pk.F, nullptr);
+  pk.sub_sigma.resize(pk.P, nullptr);
+  for (int f = 0; f < pk.F; f++) RCCHK(cut(pk.fixed_coset[f], &pk.sub_fixed[f]));
+  for (int c = 0; c < pk.P; c++) RCCHK(cut(pk.sigma_coset[c], &pk.sub_sigma[c]));
+  RCCHK(cut(pk.l0, &pk.sub_l0));
+  RCCHK(cut(pk.l_last, &pk.sub_ll));
+  RCCHK(cut(pk.l_active, &pk.sub_la));
+  pk.d_sigma_sub.assign(nt, nullptr);
+  for (size_t i = 0; i < nt; i++) {
+    std::vector<const Fr*> sg(pk.P + 1, nullptr);
+    for (int c = 0; c < pk.P; c++) sg[c] = pk.sub_sigma[c] + i * n;
+    PALLOC(pk.pool, pk.d_sigma_sub[i], sg.size());
+    HIPCHK(hipMemcpy(pk.d_sigma_sub[i], sg.data(), sg.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+  }
+  if (!pk.h_gather) PALLOC(pk.pool, pk.h_gather, pk.ext);
+  HIPCHK(hipStreamSynchronize(st));
+  pk.sub_key = key;
+  return H2G_OK;
+}
+
+// a circuit workspace's evaluate_h tables for each owned sub-coset (cf. circuit_ws_add)
+int sub_ws_tables(const ProvingKey& pk, CircuitWs& w) {
+  if (w.sub_key == pk.sub_key) return H2G_OK;
+  const size_t n = pk.n, nt = pk.sub_ts.size();
+  w.sub.assign(nt, CircuitWs::SubTables{});
+  for (size_t i = 0; i < nt; i++) {
+    const size_t off = i * n;
+    auto col = [&](const Query& q) -> const Fr* {
+      if (q.type == COL_ADVICE) return w.adv_coset[q.index] + off;
+      if (q.type == COL_FIXED) return pk.sub_fixed[q.index] + off;
+      return w.inst_coset[q.index] + off;
+    };
+    std::vector<const Fr*> lc(pk.n_loads + 1, nullptr);
+    for (int j = 0; j < pk.n_loads; j++) lc[j] = col(pk.loads[j]);
+    std::vector<EvalLookup> el(pk.NL + 1);
+    std::vector<EvalShuffle> es(pk.NS + 1);
+    for (int l = 0; l < pk.NL; l++)
+      el[l] = EvalLookup{pk.seg_lk_in[l], pk.seg_lk_tab[l], w.lk_zc[l] + off, w.lk_apc[l] + off, w.lk_spc[l] + off};
+    for (int l = 0; l < pk.NS; l++) es[l] = EvalShuffle{pk.seg_sh_in[l], pk.seg_sh_sh[l], w.sh_zc[l] + off};
+    std::vector<const Fr*> zt(pk.nsets + 1, nullptr), pv(pk.P + 1, nullptr);
+    for (int q = 0; q < pk.nsets; q++) zt[q] = w.z_coset[q] + off;
+    for (int c = 0; c < pk.P; c++) pv[c] = col(Query{pk.perm_cols[c].first, pk.perm_cols[c].second, 0});
+    CircuitWs::SubTables& S = w.sub[i];
+    PALLOC(w.pool, S.load_col, lc.size());
+    PALLOC(w.pool, S.lookups, el.size());
+    PALLOC(w.pool, S.shuffles, es.size());
+    PALLOC(w.pool, S.z, zt.size());
+    PALLOC(w.pool, S.perm_v, pv.size());
+    HIPCHK(hipMemcpy(S.load_col, lc.data(), lc.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(S.lookups, el.data(), el.size() * sizeof(EvalLookup), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(S.shuffles, es.data(), es.size() * sizeof(EvalShuffle), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(S.z, zt.data(), zt.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(S.perm_v, pv.data(), pv.size() * sizeof(Fr*), hipMemcpyHostToDevice));
+  }
+  w.sub_key = pk.sub_key;
+  return H2G_OK;
+}
+
+// the extended-coset columns evaluate_h reads (coeff_to_extended, domain.rs:230-244):
+// whole cosets, or under the SPMD sub-coset split this rank's sub-cosets (slot i of dst =
+// sub-coset sub_ts[i]; a rank past 2^e owns none and computes nothing)
+int ext_cosets(Device* d, const ProvingKey& pk, const Fr* const* src, Fr* const* dst, int count, hipStream_t st) {
+  if (!spmd_subcosets()) return coeff_to_extended_batch(d, pk.dom, src, dst, count, st);
+  const size_t n = pk.n, nt = pk.sub_ts.size();
+  std::vector<const Fr*> s2;
+  std::vector<Fr*> d2;
+  for (int c = 0; c < count; c++)
+    for (size_t i = 0; i < nt; i++) {
+      Fr* o = dst[c] + i * n;
+      HIPCHK(subcoset_twist(src[c], o, n, pk.eo, pk.sub_ts[i], pk.ext - 1, st));
+      s2.push_back(o);
+      d2.push_back(o);
+    }
+  const Fr one = Fr::one();
+  for (size_t b0 = 0; b0 < s2.size(); b0 += NTT_MAX_BATCH)
+    RCCHK(ntt_dev_impl_batch(d, s2.data() + b0, n, d2.data() + b0, (int)std::min<size_t>(NTT_MAX_BATCH, s2.size() - b0),
+                             n, (int)pk.dom.k, pk.dom.omega, 1, pk.dom.g_coset, pk.dom.g_coset_inv, 0, one, 0, one,
+                             one, st));
+  return H2G_OK;
+}
+
 int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, const PkImage* img = nullptr) {
   hipStream_t st = d->stream;
   std::string why;
@@ -1029,6 +1154,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   while ((int)pk.cws.size() < ncirc) RCCHK(circuit_ws_add(pk));  // workspaces grow once
   std::vector<CircuitWs*> W(ncirc);
   for (int c = 0; c < ncirc; c++) W[c] = pk.cws[c].get();
+  if (spmd_subcosets()) RCCHK(sub_prepare(pk, st));  // this rank's sub-cosets of the key's cosets
   StageClock clk(st, g_stage_sync);
   ProverRng& rng = *in.rng;
   Transcript tr(proof, pk.transcript);
@@ -1290,7 +1416,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     RCCHK(commit_launch_batch(d, prm, perm_cols.data(), 2 * NLT, n, SRS_LAGRANGE, st, tk.data()));
     // coefficient forms and cosets, batched transforms (they overlap the commitments)
     RCCHK(lagrange_to_coeff_batch(d, D, perm_cols.data(), perm_polys.data(), 2 * NLT, st));
-    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)perm_polys.data(), perm_cosets.data(), 2 * NLT, st));
+    RCCHK(ext_cosets(d, pk, (const Fr* const*)perm_polys.data(), perm_cosets.data(), 2 * NLT, st));
     for (int i = 0; i < 2 * NLT; i++) {
       G1Affine cm;
       RCCHK(commit_collect(d, &tk[i], &cm));
@@ -1382,7 +1508,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       }
     }
     RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)all_z_lag.data(), all_z.data(), NST, st));
-    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)all_z.data(), all_z_coset.data(), NST, st));
+    RCCHK(ext_cosets(d, pk, (const Fr* const*)all_z.data(), all_z_coset.data(), NST, st));
   }
   if (perm_batched)
     RCCHK(commit_launch_batch(d, prm, (const Fr* const*)all_z_lag.data(), NST, n, SRS_LAGRANGE, st, perm_tk.data()));
@@ -1432,7 +1558,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         RCCHK(finish_z(pk.mod, w->sh_z[s], w->sh_z_poly[s], w->sh_zc[s]));
       }
     RCCHK(lagrange_to_coeff_batch(d, D, z_lags.data(), z_polys.data(), (int)z_lags.size(), st));
-    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)z_polys.data(), z_cosets.data(), (int)z_lags.size(), st));
+    RCCHK(ext_cosets(d, pk, (const Fr* const*)z_polys.data(), z_cosets.data(), (int)z_lags.size(), st));
   }
   {  // product commitments: every circuit's lookups, then every circuit's shuffles, one batch
     std::vector<const Fr*> zs;
@@ -1474,8 +1600,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   // they overlap the permutation / vanishing MSMs
   for (CircuitWs* w : W) {
     RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)w->adv.data(), w->adv.data(), pk.A, st));
-    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)w->adv.data(), w->adv_coset.data(), pk.A, st));
-    RCCHK(coeff_to_extended_batch(d, D, (const Fr* const*)w->inst_poly.data(), w->inst_coset.data(), pk.I, st));
+    RCCHK(ext_cosets(d, pk, (const Fr* const*)w->adv.data(), w->adv_coset.data(), pk.A, st));
+    RCCHK(ext_cosets(d, pk, (const Fr* const*)w->inst_poly.data(), w->inst_coset.data(), pk.I, st));
   }
   for (auto* tks : {&perm_tk, &lkz_tk, &shz_tk})
     for (auto& t : *tks) {
@@ -1492,7 +1618,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   const Fr y = tr.squeeze();
   // ---- evaluate_h (evaluation.rs:317-620): one launch per circuit, each continuing the
   // previous circuit's Horner chain in y; the last one divides by t(X)
-  for (int ci = 0; ci < ncirc; ci++) {
+  const bool subc = spmd_subcosets();
+  for (int ci = 0; ci < ncirc && !subc; ci++) {
     const CircuitWs& w = *W[ci];
     EvalHArgs a;
     a.prog = pk.prog;
@@ -1531,6 +1658,59 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     a.out = pk.h_ext;
     HIPCHK(evaluate_h(a, st));
   }
+  if (subc) {  // rows of this rank's sub-cosets, then every sub-coset's h from its owner
+    const int e = (int)(D.ek - D.k);
+    for (CircuitWs* w : W) RCCHK(sub_ws_tables(pk, *w));
+    for (size_t i = 0; i < pk.sub_ts.size(); i++) {
+      const uint64_t t = pk.sub_ts[i];
+      Fr* slot = pk.h_gather + t * n;
+      for (int ci = 0; ci < ncirc; ci++) {
+        const CircuitWs& w = *W[ci];
+        EvalHArgs a;
+        a.prog = pk.prog;
+        a.gates = pk.seg_gates;
+        a.n_slots = pk.n_slots;
+        a.theta = theta;
+        a.nlookups = pk.NL;
+        a.nshuffles = pk.NS;
+        a.lookups = w.sub[i].lookups;
+        a.shuffles = w.sub[i].shuffles;
+        a.consts = pk.consts;
+        a.query_col = w.sub[i].load_col;
+        a.query_rot = pk.d_load_rot;
+        a.nsets = pk.nsets;
+        a.chunk_len = pk.chunk_len;
+        a.P = pk.P;
+        a.z = w.sub[i].z;
+        a.perm_v = w.sub[i].perm_v;
+        a.sigma = pk.d_sigma_sub[i];
+        a.l0 = pk.sub_l0 + i * n;
+        a.l_last = pk.sub_ll + i * n;
+        a.l_active = pk.sub_la + i * n;
+        a.beta = beta;
+        a.gamma = gamma;
+        a.y = y;
+        a.delta_start = beta * zeta() * pow_u64(D.ext_omega, t);  // X = zeta w_ext^t w^m
+        a.delta = fr_delta();
+        a.ext_omega = pk.om;
+        a.ext = n;
+        a.rot_scale = 1;
+        a.last_rot = -(bf + 1);
+        a.t_evals = D.d_t + t;  // t(X) is constant on a sub-coset
+        a.t_mask = 0;
+        a.acc_in = ci > 0 ? slot : nullptr;
+        a.divide = ci + 1 == ncirc;
+        a.out = slot;
+        HIPCHK(evaluate_h(a, st));
+      }
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    for (uint64_t t = 0; t < (1ull << e); t++)
+      if (g_spmd.bcast(g_spmd.ctx, pk.h_gather + t * n, n * sizeof(Fr), (int)(t % (uint64_t)g_spmd.world)) != 0)
+        return fail(H2G_ERR_STATE, "spmd transport: broadcast of sub-coset " + std::to_string(t) + " failed");
+    HIPCHK(subcoset_scatter(pk.h_gather, pk.h_ext, n, e, st));
+  }
+  dump("h_ext", pk.h_ext, ext, st);
   clk.mark("evaluate_h");
   // ---- vanishing construct (vanishing/prover.rs:102-155): h(X) pieces of size n
   RCCHK(extended_to_coeff(d, D, pk.h_ext, pk.h_coeff, st));
@@ -2482,7 +2662,7 @@ int h2g_set_shard_transport(const h2g_shard_transport* t) {
   if (t && t->world > 1) {
     if (!t->launch || !t->collect || t->world > 4096) return fail(H2G_ERR_ARG, "set_shard_transport: bad transport");
     g_shard = *t;
-    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr};
+    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr};
   } else {
     g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   }
@@ -2498,7 +2678,7 @@ int h2g_set_spmd_transport(const h2g_spmd_transport* t) {
     g_spmd = *t;
     g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   } else {
-    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr};
+    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr};
   }
   g_spmd_seq = 0;
   return H2G_OK;
@@ -2578,14 +2758,15 @@ int h2g_comm_init(const uint8_t id[256], int world, int rank) {
 int h2g_comm_destroy(void) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (g_shard.launch == comm_launch) g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
-  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr};
+  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr};
   return comm_destroy();
 }
 
-int h2g_comm_spmd_install(void) {
+int h2g_comm_spmd_install(int split_subcosets) {
   NEED_DEV_P();
   if (comm_world() < 2) return fail(H2G_ERR_STATE, "comm_spmd_install: needs a communicator (h2g_comm_init)");
-  g_spmd = h2g_spmd_transport{comm_spmd_ctx(), comm_world(), comm_rank(), comm_allgather_partial};
+  g_spmd = h2g_spmd_transport{comm_spmd_ctx(), comm_world(), comm_rank(), comm_allgather_partial,
+                              split_subcosets ? comm_bcast : nullptr};
   g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   g_spmd_seq = 0;
   return H2G_OK;
@@ -2593,7 +2774,7 @@ int h2g_comm_spmd_install(void) {
 
 int h2g_comm_spmd_uninstall(void) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
-  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr};
+  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr};
   g_spmd_seq = 0;
   return H2G_OK;
 }

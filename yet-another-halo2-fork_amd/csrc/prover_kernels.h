@@ -84,6 +84,12 @@ struct EvalHArgs {
   Fr* out = nullptr;
 };
 hipError_t evaluate_h(const EvalHArgs& a, hipStream_t st);
+
+// SPMD sub-coset split of the extended domain (prover_kernels.hip)
+hipError_t subcoset_twist(const Fr* src, Fr* dst, size_t n, const PowTable& eo, uint64_t t, uint64_t ext_mask,
+                          hipStream_t st);
+hipError_t subcoset_gather(const Fr* full, Fr* out, size_t n, uint64_t t, int e, hipStream_t st);
+hipError_t subcoset_scatter(const Fr* subs, Fr* ext, size_t n, int e, hipStream_t st);
 int evaluate_h_max_slots();
 
 // Lagrange-basis compression of an expression list (lookup/prover.rs:85-103,

@@ -694,6 +694,45 @@ hipError_t scale_by_dev(Fr* out, const Fr* a, uint64_t n, const Fr* scalar, hipS
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ sub-cosets (SPMD)
+// The extended domain is 2^e cosets of the n-point subgroup: row y = t + 2^e m of the
+// extended coset is point zeta w_ext^t w^m, so sub-coset t of a polynomial is an n-point
+// NTT of c_j zeta^(j mod 3) w_ext^(t j) (the zeta powers are the NTT's input distribution)
+__global__ void __launch_bounds__(KT) subcoset_twist_kernel(const Fr* __restrict__ src, Fr* __restrict__ dst,
+                                                            size_t n, PowTable eo, uint64_t t, uint64_t ext_mask) {
+  for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < n; j += (size_t)gridDim.x * blockDim.x)
+    stf(dst + j, ldf(src + j) * pw(eo, (t * j) & ext_mask));
+}
+hipError_t subcoset_twist(const Fr* src, Fr* dst, size_t n, const PowTable& eo, uint64_t t, uint64_t ext_mask,
+                          hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(subcoset_twist_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, src, dst, n, eo, t, ext_mask);
+  return hipGetLastError();
+}
+// out[m] = full[t + (m << e)]: sub-coset t of a full extended-coset array (the key's cosets)
+__global__ void __launch_bounds__(KT) subcoset_gather_kernel(const Fr* __restrict__ full, Fr* __restrict__ out,
+                                                             size_t n, uint64_t t, int e) {
+  for (size_t m = blockIdx.x * (size_t)blockDim.x + threadIdx.x; m < n; m += (size_t)gridDim.x * blockDim.x)
+    stf(out + m, ldf(full + t + ((uint64_t)m << e)));
+}
+hipError_t subcoset_gather(const Fr* full, Fr* out, size_t n, uint64_t t, int e, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(subcoset_gather_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, full, out, n, t, e);
+  return hipGetLastError();
+}
+// ext[t + (m << e)] = subs[t n + m] for every t < 2^e: sub-coset slots back to row order
+__global__ void __launch_bounds__(KT) subcoset_scatter_kernel(const Fr* __restrict__ subs, Fr* __restrict__ ext,
+                                                              size_t n, int e) {
+  const uint64_t total = (uint64_t)n << e, tmask = (1ull << e) - 1;
+  for (uint64_t y = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; y < total; y += (uint64_t)gridDim.x * blockDim.x)
+    stf(ext + y, ldf(subs + (y & tmask) * n + (y >> e)));
+}
+hipError_t subcoset_scatter(const Fr* subs, Fr* ext, size_t n, int e, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(subcoset_scatter_kernel, dim3(grid_1d((size_t)n << e)), dim3(KT), 0, st, subs, ext, n, e);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ keygen helpers
 __global__ void __launch_bounds__(KT) sigma_kernel(Fr* __restrict__ sigma, const uint32_t* __restrict__ mc,
                                                    const uint32_t* __restrict__ mr, size_t n,

@@ -114,7 +114,7 @@ _SIGS = {
     "h2g_comm_stop": ([], I32),
     "h2g_comm_destroy": ([], I32),
     "h2g_set_spmd_transport": ([VP], I32),
-    "h2g_comm_spmd_install": ([], I32),
+    "h2g_comm_spmd_install": ([I32], I32),
     "h2g_comm_spmd_uninstall": ([], I32),
 }
 
@@ -853,17 +853,21 @@ def transport_errors():
 
 
 SPMD_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, VP, U64, U64P, U64P)
+SPMD_BCAST = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, SZ, ctypes.c_int)
 
 
 class SpmdTransport(ctypes.Structure):
     """struct h2g_spmd_transport (include/h2g.h)"""
-    _fields_ = [("ctx", VP), ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("allgather", SPMD_ALLGATHER)]
+    _fields_ = [("ctx", VP), ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("allgather", SPMD_ALLGATHER),
+                ("bcast", SPMD_BCAST)]
 
 
-def set_spmd_transport(world, rank=0, allgather=None):
+def set_spmd_transport(world, rank=0, allgather=None, bcast=None):
     """SPMD sharding: every rank runs the same create_proof and computes its point slab of
     each commitment MSM; allgather(seq, mine: uint64[9]) -> uint64[world, 9] (rank order)
-    collects the partials.  world <= 1 removes it.  Exceptions fail the proof."""
+    collects the partials.  bcast(d_ptr, nbytes, root) (optional) divides the extended
+    domain's sub-cosets over the ranks and broadcasts each one's h evaluations (device
+    memory, in place).  world <= 1 removes it.  Exceptions fail the proof."""
     global _transport_keep
     if world <= 1:
         check(lib().h2g_set_spmd_transport(None))
@@ -877,12 +881,21 @@ def set_spmd_transport(world, rank=0, allgather=None):
             ctypes.memmove(out, got.ctypes.data, world * 9 * 8)
             return 0
         except Exception as e:  # noqa: BLE001 -- reported through the C status
-            _transport_keep[2].append(e)
+            _transport_keep[-1].append(e)
+            return 1
+
+    def _bc(ctx, d_ptr, nbytes, root):
+        try:
+            bcast(int(d_ptr or 0), int(nbytes), int(root))
+            return 0
+        except Exception as e:  # noqa: BLE001
+            _transport_keep[-1].append(e)
             return 1
 
     cb = SPMD_ALLGATHER(_ag)
-    t = SpmdTransport(None, world, rank, cb)
-    _transport_keep = (t, cb, [])
+    cbb = SPMD_BCAST(_bc) if bcast is not None else ctypes.cast(None, SPMD_BCAST)
+    t = SpmdTransport(None, world, rank, cb, cbb)
+    _transport_keep = (t, cb, cbb, [])
     check(lib().h2g_set_spmd_transport(ctypes.byref(t)))
 
 
@@ -915,9 +928,10 @@ def comm_destroy():
     check(lib().h2g_comm_destroy())
 
 
-def comm_spmd_install():
-    """SPMD sharding over the library's communicator (RCCL all-gather of the partials)"""
-    check(lib().h2g_comm_spmd_install())
+def comm_spmd_install(subcosets=True):
+    """SPMD sharding over the library's communicator (RCCL all-gather of the partials;
+    subcosets: the extended domain's sub-cosets divided over the ranks, h broadcast)"""
+    check(lib().h2g_comm_spmd_install(1 if subcosets else 0))
 
 
 def comm_spmd_uninstall():

@@ -190,13 +190,15 @@ class SpmdGather:
     sums them, so no scalars travel.  h2g_comm_spmd_install is the same over the library's
     own RCCL communicator."""
 
-    def __init__(self, dist, group=None):
+    def __init__(self, dist, group=None, subcosets=True):
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.device = _staging(dist, group)
+        self.subcosets = subcosets
         self.calls = 0
+        self.bcasts = 0
 
     def allgather(self, seq, mine):
         import torch
@@ -206,9 +208,28 @@ class SpmdGather:
         self.calls += 1
         return np.stack([o.cpu().numpy().view(np.uint64) for o in out])
 
+    def bcast(self, d_ptr, nbytes, root):
+        """in-place broadcast of device memory from `root` (a sub-coset's h evaluations):
+        staged through a torch tensor (RCCL) or host memory (gloo)"""
+        import h2g
+        import torch
+        t = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        if self.rank == root:
+            h2g.memcpy_dtod(t.data_ptr(), d_ptr, nbytes)
+        if self.device.type == "cuda":
+            self.dist.broadcast(t, root, group=self.group)
+        else:
+            h = t.cpu()
+            self.dist.broadcast(h, root, group=self.group)
+            t.copy_(h)
+        torch.cuda.synchronize()
+        if self.rank != root:
+            h2g.memcpy_dtod(d_ptr, t.data_ptr(), nbytes)
+        self.bcasts += 1
+
     def install(self):
         import h2g
-        h2g.set_spmd_transport(self.world, self.rank, self.allgather)
+        h2g.set_spmd_transport(self.world, self.rank, self.allgather, self.bcast if self.subcosets else None)
 
     @staticmethod
     def uninstall():
