@@ -1224,18 +1224,25 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         from = w.wit_pin;
         from_dev = false;
       }
-      for (int c : cols)
+      // column by column: upload, blinding rows, and (when the MSMs go one by one) the
+      // commitment at once, so that a column's MSM overlaps the next column's upload
+      // from host memory; the RNG draws keep the reference's order (every column's rows,
+      // then every column's blind)
+      const bool early = commit_batch_chunk(prm, n, SRS_LAGRANGE) < 2;
+      for (size_t k = 0; k < cols.size(); k++) {
+        const int c = cols[k];
         HIPCHK(hipMemcpyAsync(w.adv[c], from + 4 * n * c, n * sizeof(Fr),
                               from_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
-      for (int c : cols) {
-        if (pk.unblinded[c]) continue;
-        Fr* rows = adv_blind.data() + ((size_t)ci * pk.A + c) * (bf + 1);
-        for (int i = 0; i <= bf; i++) rows[i] = rng.random_fr();
-        HIPCHK(hipMemcpyAsync(w.adv[c] + unusable, rows, (size_t)(bf + 1) * sizeof(Fr), hipMemcpyHostToDevice, st));
+        if (!pk.unblinded[c]) {
+          Fr* rows = adv_blind.data() + ((size_t)ci * pk.A + c) * (bf + 1);
+          for (int i = 0; i <= bf; i++) rows[i] = rng.random_fr();
+          HIPCHK(hipMemcpyAsync(w.adv[c] + unusable, rows, (size_t)(bf + 1) * sizeof(Fr), hipMemcpyHostToDevice, st));
+        }
+        if (early) RCCHK(commit_launch(d, prm, w.adv[c], n, SRS_LAGRANGE, st, &tk[(size_t)ci * cols.size() + k]));
       }
       for (int c : cols)
         if (!pk.unblinded[c]) (void)rng.random_fr();  // commitment blinds (unused by KZG)
-      if (!cols.empty()) {
+      if (!cols.empty() && !early) {
         std::vector<const Fr*> polys(cols.size());
         for (size_t i = 0; i < cols.size(); i++) polys[i] = w.adv[cols[i]];
         RCCHK(commit_launch_batch(d, prm, polys.data(), (int)cols.size(), n, SRS_LAGRANGE, st,
