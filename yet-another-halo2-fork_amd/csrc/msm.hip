@@ -82,10 +82,16 @@ __device__ __forceinline__ G1Affine ld_aff(const G1Affine* p) {
 // (coarse bins) straight from the scalars, round 2 by the low FB bits inside each coarse
 // bin (a bin's region is a few hundred KB, so its scattered writes stay in L2).  Zero
 // digits produce no entry at all.  Order inside a bucket is arbitrary (the sum is exact).
-static constexpr int PT = 512;          // threads of the coarse kernels (one scalar each)
-static constexpr int PWG = 16;          // windows per coarse-kernel thread (grid.z groups)
-static constexpr int FT = 256;          // threads of the fine kernels
-static constexpr int FPER = 16;         // entries per fine-kernel thread
+#ifndef H2G_MSM_PT
+#define H2G_MSM_PT 512
+#endif
+#ifndef H2G_MSM_FPER
+#define H2G_MSM_FPER 16
+#endif
+static constexpr int PT = H2G_MSM_PT;      // threads of the coarse kernels (one scalar each)
+static constexpr int PWG = 16;             // windows per coarse-kernel thread (grid.z groups)
+static constexpr int FT = 256;             // threads of the fine kernels
+static constexpr int FPER = H2G_MSM_FPER;  // entries per fine-kernel thread
 static constexpr uint32_t FTILE = (uint32_t)FT * FPER;
 static constexpr int FB_MAX = 11;       // fine bits
 static constexpr int COARSE_MAX = 2048;  // coarse bins (keys < 2^22)
