@@ -192,7 +192,7 @@ struct ProvingKey {
   // per-proof workspace (device), reused across proofs: per circuit, and shared
   std::vector<std::unique_ptr<CircuitWs>> cws;
   Fr *mod = nullptr, *pre = nullptr, *scr = nullptr, *random_poly = nullptr, *h_ext = nullptr, *h_coeff = nullptr;
-  Fr *h_poly = nullptr, *nx = nullptr, *q1 = nullptr, *q2 = nullptr, *hx = nullptr, *lx = nullptr;
+  Fr *h_poly = nullptr, *nx = nullptr, *q1 = nullptr, *hx = nullptr, *lx = nullptr;
   Fr *small = nullptr, *last_z = nullptr, *evals = nullptr, *eval_scr = nullptr;
   // SPMD sub-coset split (h2g_spmd_transport.bcast): this rank's sub-cosets t = rank,
   // rank + world, ... < 2^e of the extended domain; the key's cosets cut to them (slot i
@@ -909,7 +909,6 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
   HIPCHK(falloc(&pk.h_poly, n));
   HIPCHK(falloc(&pk.nx, n));
   HIPCHK(falloc(&pk.q1, n));
-  HIPCHK(falloc(&pk.q2, n));
   HIPCHK(falloc(&pk.hx, n));
   HIPCHK(falloc(&pk.lx, n));
   HIPCHK(falloc(&pk.small, 4096));
@@ -1977,29 +1976,62 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     low[c] = lagrange_interpolate(cm_pts[c], e);
   }
   const Fr v = tr.squeeze();
-  // h_x = sum_s v^s (sum_i y^i (p_i - r_i)) / Z_s
+  // h_x = sum_s v^s (sum_i y^i (p_i - r_i)) / Z_s (the reference divides by Z_s with one
+  // kate division per point of S_s, shplonk/prover.rs:142-176).  Partial fractions instead:
+  // 1 / Z_s = sum_{p in S_s} c_{s,p} / (X - p) with c_{s,p} = prod_{p' in S_s \ p} (p - p')^-1,
+  // and (g_s - r_s) / (X - p) is exact for every p in S_s, so with
+  // G_p = sum_{s : p in S_s} v^s c_{s,p} (g_s - r_s), h_x = sum_p G_p / (X - p): one kate
+  // division per distinct point (accumulated into h_x) instead of one per (set, point).
+  // Exact field arithmetic, so h_x is the same polynomial.
   {
-    Fr vpow = Fr::one();
-    for (size_t r = 0; r < rs_rep.size(); r++) {
-      const std::vector<Fr>& pts = cm_pts[rs_rep[r]];
-      corr_stage.emplace_back(pts.size(), Fr::zero());  // read by an async copy
+    std::vector<Fr> vpow(rs_rep.size()), ypow(cm_ids.size());
+    {
+      Fr vp = Fr::one();
+      for (size_t r = 0; r < rs_rep.size(); r++) {
+        vpow[r] = vp;
+        vp = vp * v;
+        Fr yp = Fr::one();
+        for (size_t c = 0; c < cm_ids.size(); c++)
+          if (rs_of[c] == (int)r) {
+            ypow[c] = yp;
+            yp = yp * sy;
+          }
+      }
+    }
+    HIPCHK(hipMemsetAsync(pk.hx, 0, n * sizeof(Fr), st));
+    for (const Fr& p : super_pts) {
+      // alpha_s = v^s c_{s,p} for the sets containing p
+      std::vector<Fr> alpha(rs_rep.size(), Fr::zero());
+      std::vector<char> has(rs_rep.size(), 0);
+      size_t ncorr = 0;
+      for (size_t r = 0; r < rs_rep.size(); r++) {
+        const std::vector<Fr>& pts = cm_pts[rs_rep[r]];
+        if (std::find(pts.begin(), pts.end(), p) == pts.end()) continue;
+        Fr den = Fr::one();
+        for (const Fr& q : pts)
+          if (!(q == p)) den = den * (p - q);
+        alpha[r] = vpow[r] * inv(den);
+        has[r] = 1;
+        ncorr = std::max(ncorr, pts.size());
+      }
+      corr_stage.emplace_back(ncorr, Fr::zero());  // read by an async copy
       std::vector<Fr>& corr = corr_stage.back();
       LinTerms t;
       bool first = true;
-      Fr ypow = Fr::one();
       for (size_t c = 0; c < cm_ids.size(); c++) {
-        if (rs_of[c] != (int)r) continue;
+        const int r = rs_of[c];
+        if (!has[r]) continue;
         if (t.k == LIN_MAXT - 1) {
           HIPCHK(lincomb(pk.nx, n, t, !first, st));
           first = false;
           t.k = 0;
         }
+        const Fr coef = alpha[r] * ypow[c];
         t.p[t.k] = polys[cm_ids[c]].p;
         t.len[t.k] = polys[cm_ids[c]].len;
-        t.coef[t.k] = ypow;
+        t.coef[t.k] = coef;
         t.k++;
-        for (size_t j = 0; j < pts.size(); j++) corr[j] = corr[j] + ypow * low[c][j];
-        ypow = ypow * sy;
+        for (size_t j = 0; j < low[c].size(); j++) corr[j] = corr[j] + coef * low[c][j];
       }
       HIPCHK(hipMemcpyAsync(pk.small, corr.data(), corr.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
       t.p[t.k] = pk.small;
@@ -2007,23 +2039,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       t.coef[t.k] = fr_neg_one();
       t.k++;
       HIPCHK(lincomb(pk.nx, n, t, !first, st));
-      // successive kate divisions by the set's points
-      const Fr* src = pk.nx;
-      uint64_t len = n;
-      Fr* bufs[2] = {pk.q1, pk.q2};
-      for (size_t j = 0; j < pts.size(); j++) {
-        Fr* dst = bufs[j & 1];
-        HIPCHK(kate_division(src, len, pts[j], dst, pk.scr, st));
-        src = dst;
-        len--;
-      }
-      LinTerms h;
-      h.k = 1;
-      h.p[0] = src;
-      h.len[0] = len;
-      h.coef[0] = vpow;
-      HIPCHK(lincomb(pk.hx, n, h, r > 0, st));
-      vpow = vpow * v;
+      HIPCHK(kate_division(pk.nx, n, p, pk.hx, pk.scr, st, true));
     }
   }
   {

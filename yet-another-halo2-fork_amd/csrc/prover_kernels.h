@@ -158,7 +158,9 @@ hipError_t poly_eval_batch(const EvalReq* d_reqs, int nreq, uint64_t max_len, Fr
 size_t poly_eval_scratch_len(int nreq, uint64_t max_len);
 
 // ---- kate_division (arithmetic.rs:101-120): q = (a - a(b)) / (X - b), len(q) = len(a) - 1 ----
-hipError_t kate_division(const Fr* a, uint64_t len, const Fr& b, Fr* q, Fr* scratch, hipStream_t st);
+// accumulate: q[0..len-1) += the quotient instead of =; scratch: kate_scratch_len(len)
+hipError_t kate_division(const Fr* a, uint64_t len, const Fr& b, Fr* q, Fr* scratch, hipStream_t st,
+                         bool accumulate = false);
 size_t kate_scratch_len(uint64_t len);
 
 // ---- linear combinations: out[i] = (acc ? out[i] : 0) + sum_k coef_k * p_k[i] (i < len_k) ----

@@ -584,33 +584,52 @@ hipError_t poly_eval_batch(const EvalReq* d_reqs, int nreq, uint64_t max_len, Fr
 
 // ------------------------------------------------------------------ kate division
 // With a' = a[1..len) and M = len - 1: q[i] = sum_{j >= i} a'[j] b^(j - i), i.e. the
-// suffix Horner of a' at b.  Phase 1: per-tile sums; phase 2: tile carries (one block,
-// suffix scan of affine maps); phase 3: per-thread carries + the downward recurrence.
+// suffix Horner of a' at b.  Phase 1: per-thread suffix sums over KD_S elements (kept for
+// phase 3) and per-tile sums; phase 2: tile carries (one block, suffix scan of affine
+// maps); phase 3: a weighted suffix scan of the kept per-thread sums (seeded with the
+// tile's carry) gives each thread its carry, then the downward recurrence.  Every
+// thread's map has the same slope b^KD_S, so both block scans need one product per level,
+// with the level weights b^(KD_S 2^l) computed once on the host (KatePow).
+#ifndef H2G_KD_S
+#define H2G_KD_S 8
+#endif
 static constexpr int KD_T = 256;
-static constexpr int KD_S = 8;
+static constexpr int KD_S = H2G_KD_S;
+static constexpr int KD_L = 8;  // log2(KD_T)
 static constexpr uint64_t KD_TILE = (uint64_t)KD_T * KD_S;
+static_assert((1 << KD_L) == KD_T, "KD_L");
 
-__global__ void __launch_bounds__(KD_T) kate_phase1(const Fr* __restrict__ a1, uint64_t M, Fr b,
-                                                    Fr* __restrict__ tile_val) {
+struct KatePow {
+  Fr p[KD_L + 1];  // p[l] = b^(KD_S 2^l); p[KD_L] = b^KD_TILE
+};
+
+__global__ void __launch_bounds__(KD_T) kate_phase1(const Fr* __restrict__ a1, uint64_t M, Fr b, KatePow pw,
+                                                    Fr* __restrict__ tile_val, Fr* __restrict__ thr_val) {
   __shared__ Fr sh[KD_T];
-  const uint64_t lo = blockIdx.x * KD_TILE + (uint64_t)threadIdx.x * KD_S;
+  const int t = threadIdx.x;
+  const uint64_t lo = blockIdx.x * KD_TILE + (uint64_t)t * KD_S;
   Fr acc = Fr::zero();
+#pragma unroll
   for (int i = KD_S - 1; i >= 0; i--) {
     const uint64_t j = lo + i;
     acc = acc * b + (j < M ? ldf(a1 + j) : Fr::zero());
   }
-  Fr step = b;
+  stf(thr_val + blockIdx.x * (uint64_t)KD_T + t, acc);
+  // sum_t acc_t b^(KD_S t): tree with the level weights
+  sh[t] = acc;
+  __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 3; i++) step = step * step;  // b^8
-  const Fr r = block_weighted_sum<KD_T>(acc, step, sh);
-  if (threadIdx.x == 0) tile_val[blockIdx.x] = r;
+  for (int l = 0; l < KD_L; l++) {
+    const int s = 1 << l;
+    if ((t & (2 * s - 1)) == 0) sh[t] = sh[t] + pw.p[l] * sh[t + s];
+    __syncthreads();
+  }
+  if (t == 0) tile_val[blockIdx.x] = sh[0];
 }
 
 // one block: carry[c] = q[hi_c] = sum_{c' > c} V_c' B^(c' - c - 1), B = b^TILE
-__global__ void __launch_bounds__(KD_T) kate_phase2(Fr* __restrict__ tile_val, uint64_t ntiles, Fr b) {
+__global__ void __launch_bounds__(KD_T) kate_phase2(Fr* __restrict__ tile_val, uint64_t ntiles, Fr B) {
   __shared__ Fr shv[KD_T], shw[KD_T];
-  Fr B = b;
-  for (int i = 0; i < 11; i++) B = B * B;  // b^2048 = b^TILE
   const uint64_t per = (ntiles + KD_T - 1) / KD_T;
   const uint64_t lo = (uint64_t)threadIdx.x * per;
   const uint64_t hi = lo + per < ntiles ? lo + per : ntiles;
@@ -631,37 +650,62 @@ __global__ void __launch_bounds__(KD_T) kate_phase2(Fr* __restrict__ tile_val, u
   }
 }
 
-__global__ void __launch_bounds__(KD_T) kate_phase3(const Fr* __restrict__ a1, uint64_t M, Fr b,
-                                                    const Fr* __restrict__ tile_carry, Fr* __restrict__ q) {
-  __shared__ Fr shv[KD_T], shw[KD_T];
-  const uint64_t lo = blockIdx.x * KD_TILE + (uint64_t)threadIdx.x * KD_S;
-  Fr val = Fr::zero(), w = Fr::one();
-  for (int i = KD_S - 1; i >= 0; i--) {
-    const uint64_t j = lo + i;
-    val = val * b + (j < M ? ldf(a1 + j) : Fr::zero());
-    w = w * b;
+// q[j] (+)= the quotient; thread t's carry is the inclusive weighted suffix sum of
+// x_t = (thread t+1's sum, or the tile's carry for the last thread)
+template <bool ACC>
+__global__ void __launch_bounds__(KD_T) kate_phase3(const Fr* __restrict__ a1, uint64_t M, Fr b, KatePow pw,
+                                                    const Fr* __restrict__ tile_carry,
+                                                    const Fr* __restrict__ thr_val, Fr* __restrict__ q) {
+  __shared__ Fr sh[KD_T];
+  const int t = threadIdx.x;
+  const uint64_t g = blockIdx.x * (uint64_t)KD_T + t;
+  Fr x = t + 1 < KD_T ? ldf(thr_val + g + 1) : tile_carry[blockIdx.x];
+#pragma unroll
+  for (int l = 0; l < KD_L; l++) {
+    const int s = 1 << l;
+    sh[t] = x;
+    __syncthreads();
+    if (t + s < KD_T) x = x + pw.p[l] * sh[t + s];
+    __syncthreads();
   }
-  Fr cv, cw;
-  block_suffix_affine<KD_T>(val, w, shv, shw, &cv, &cw);
-  Fr cur = cv + cw * tile_carry[blockIdx.x];
+  const uint64_t lo = blockIdx.x * KD_TILE + (uint64_t)t * KD_S;
+  Fr cur = x;
   for (int i = KD_S - 1; i >= 0; i--) {
     const uint64_t j = lo + i;
     if (j < M) {
       cur = ldf(a1 + j) + b * cur;
-      stf(q + j, cur);
+      stf(q + j, ACC ? ldf(q + j) + cur : cur);
     }
   }
 }
 
-size_t kate_scratch_len(uint64_t len) { return (size_t)((len + KD_TILE - 1) / KD_TILE + 1); }
+size_t kate_scratch_len(uint64_t len) {
+  const uint64_t nt = (len + KD_TILE - 1) / KD_TILE;
+  return (size_t)(nt + 1 + nt * KD_T);
+}
 
-hipError_t kate_division(const Fr* a, uint64_t len, const Fr& b, Fr* q, Fr* scratch, hipStream_t st) {
+hipError_t kate_division(const Fr* a, uint64_t len, const Fr& b, Fr* q, Fr* scratch, hipStream_t st,
+                         bool accumulate) {
   if (len < 2) return hipSuccess;
   const uint64_t M = len - 1;
   const uint64_t nt = (M + KD_TILE - 1) / KD_TILE;
-  hipLaunchKernelGGL(kate_phase1, dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, scratch);
-  hipLaunchKernelGGL(kate_phase2, dim3(1), dim3(KD_T), 0, st, scratch, nt, b);
-  hipLaunchKernelGGL(kate_phase3, dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, (const Fr*)scratch, q);
+  KatePow pw;
+  Fr x = b;
+  for (int i = 1; i < KD_S; i <<= 1) x = x * x;
+  for (int l = 0; l <= KD_L; l++) {
+    pw.p[l] = x;
+    x = x * x;
+  }
+  Fr* tile = scratch;
+  Fr* thr = scratch + nt + 1;
+  hipLaunchKernelGGL(kate_phase1, dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, pw, tile, thr);
+  hipLaunchKernelGGL(kate_phase2, dim3(1), dim3(KD_T), 0, st, tile, nt, pw.p[KD_L]);
+  if (accumulate)
+    hipLaunchKernelGGL(kate_phase3<true>, dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, pw, (const Fr*)tile,
+                       (const Fr*)thr, q);
+  else
+    hipLaunchKernelGGL(kate_phase3<false>, dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, pw, (const Fr*)tile,
+                       (const Fr*)thr, q);
   return hipGetLastError();
 }
 
