@@ -26,5 +26,9 @@ hipError_t poly_batch_invert_multi(Fr* const* a, Fr* const* scratch, int count, 
 // out[i] = prod_{j<=i} a[j]; scratch >= 2 * ceil(n / 2^?) Fr (see poly.hip)
 hipError_t poly_prefix_product(const Fr* a, Fr* out, size_t n, Fr* scratch, size_t scratch_len, hipStream_t st);
 size_t poly_prefix_scratch_len(size_t n);
+// count independent prefix products (out[i] may alias a[i]); scratch >= min(count, 16) *
+// poly_prefix_scratch_len(n) Fr
+hipError_t poly_prefix_product_multi(const Fr* const* a, Fr* const* out, int count, size_t n, Fr* scratch,
+                                     size_t scratch_len, hipStream_t st);
 
 }  // namespace h2g

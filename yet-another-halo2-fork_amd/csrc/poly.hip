@@ -70,55 +70,95 @@ hipError_t poly_mul_cyclic(Fr* a, size_t n, const Fr* t, size_t t_len, hipStream
 }
 
 // ---------------------------------------------------------------- batch inversion
-// Montgomery's trick over the strided subset {i = t (mod T)} of each thread:
-// 3 multiplications per element + one inversion per thread (bn254.h inv: binary
-// extended Euclid, whose short dependent chain bounds the kernel's latency).
-// Arrays of one launch (blockIdx.y): independent batch inversions share the latency of
-// the per-thread inversion (e.g. every lookup's product denominators at once).
+// Montgomery's trick in three levels, so the inversion (binary extended Euclid in bn254.h:
+// ≈ 300 Montgomery products of issue time on gfx950) is paid once per ≈ 256 elements while
+// the element passes keep 2^18+ threads in flight:
+//   1. inv_fwd: thread t walks its strided subset {t + kT}, storing the running product
+//      before each element (the prefix; 1 for k = 0, so slot t of the scratch is free and
+//      takes the thread's total P_t);
+//   2. inv_regs: the totals P_t (scratch[0..T)) inverted in place, INV_REG per thread with
+//      the prefixes in registers and one inversion per thread;
+//   3. inv_bwd: from 1/P_t back down the subset: 1/x_i = (1/P) * prefix_i, 1/P *= x_i.
+// Zeros are skipped and stay zero (ff's invert().unwrap_or(ZERO)).  3 products per element
+// plus 3 per INV_PER1 elements for level 2.  Arrays of one launch (blockIdx.y) are
+// independent inversions (e.g. every lookup's product denominators at once).
 struct InvBatch {
   Fr* a[POLY_INV_MAX_BATCH];
   Fr* pref[POLY_INV_MAX_BATCH];
 };
+static constexpr int INV_REG = 16;
 
-__global__ void __launch_bounds__(PT) batch_invert_kernel(InvBatch bt, size_t n) {
-  Fr* __restrict__ a = bt.a[blockIdx.y];
+__global__ void __launch_bounds__(PT) inv_fwd_kernel(InvBatch bt, size_t n, size_t T) {
+  const Fr* __restrict__ a = bt.a[blockIdx.y];
   Fr* __restrict__ pref = bt.pref[blockIdx.y];
-  const size_t T = (size_t)gridDim.x * blockDim.x;
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (t >= n) return;
+  if (t >= T) return;
   Fr acc = Fr::one();
-  size_t last = t;
-  for (size_t i = t; i < n; i += T) {
+  {
+    const Fr x = ldf(a + t);
+    if (!x.is_zero()) acc = x;
+  }
+  for (size_t i = t + T; i < n; i += T) {
     stf(pref + i, acc);
     const Fr x = ldf(a + i);
     if (!x.is_zero()) acc = acc * x;
-    last = i;
+  }
+  stf(pref + t, acc);
+}
+
+// in place over a[0..m) of each array (nonzero entries), no scratch
+__global__ void __launch_bounds__(PT) inv_regs_kernel(InvBatch bt, size_t m) {
+  Fr* __restrict__ a = bt.pref[blockIdx.y];
+  const size_t T = (size_t)gridDim.x * blockDim.x;
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  Fr v[INV_REG], pre[INV_REG];
+  Fr acc = Fr::one();
+#pragma unroll
+  for (int k = 0; k < INV_REG; k++) {
+    const size_t i = t + k * T;
+    v[k] = i < m ? ldf(a + i) : Fr::zero();
+    pre[k] = acc;
+    if (!v[k].is_zero()) acc = acc * v[k];
   }
   Fr iv = inv(acc);
-  for (size_t i = last;; i -= T) {
+#pragma unroll
+  for (int k = INV_REG - 1; k >= 0; k--) {
+    const size_t i = t + k * T;
+    if (!v[k].is_zero()) {
+      stf(a + i, iv * pre[k]);
+      iv = iv * v[k];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(PT) inv_bwd_kernel(InvBatch bt, size_t n, size_t T) {
+  Fr* __restrict__ a = bt.a[blockIdx.y];
+  const Fr* __restrict__ pref = bt.pref[blockIdx.y];
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  Fr iv = ldf(pref + t);
+  size_t last = t;
+  while (last + T < n) last += T;
+  for (size_t i = last; i > t; i -= T) {
     const Fr x = ldf(a + i);
     if (!x.is_zero()) {
       const Fr r = iv * ldf(pref + i);
       iv = iv * x;
       stf(a + i, r);
     }
-    if (i < T) break;
   }
+  if (!ldf(a + t).is_zero()) stf(a + t, iv);
 }
 
 hipError_t poly_batch_invert_multi(Fr* const* a, Fr* const* scratch, int count, size_t n, hipStream_t st) {
   if (n == 0 || count <= 0) return hipSuccess;
-  // elements per thread: the serial chain is ~3 per products + one inversion, the
-  // inversions' total work n / per of them -- measured on MI355X, 4 at 2^18 (keccak-style
-  // proof) and 32 at 2^22 (C3) are best: about 2^16 threads per array
-  static const long env_per = [] {
-    const char* e = getenv("H2G_BINV_PER");
-    return e ? atol(e) : 0L;
-  }();
-  size_t per = env_per > 0 ? (size_t)env_per : std::min<size_t>(32, std::max<size_t>(4, n >> 16));
-  size_t threads = (n + per - 1) / per;  // elements per thread amortise the inversion
-  if (threads < 1) threads = 1;
-  const unsigned blocks = (unsigned)((threads + PT - 1) / PT);
+  // level-1 elements per thread: 16 once the arrays give 2^18 threads, fewer below
+  size_t per = 16;
+  while (per > 2 && (n * (size_t)count) / per < ((size_t)1 << 18)) per >>= 1;
+  const size_t T = (n + per - 1) / per;
+  const unsigned blk1 = (unsigned)((T + PT - 1) / PT);
+  const size_t T2 = (T + INV_REG - 1) / INV_REG;
+  const unsigned blk2 = (unsigned)((T2 + PT - 1) / PT);
   for (int b0 = 0; b0 < count; b0 += POLY_INV_MAX_BATCH) {
     const int m = std::min(POLY_INV_MAX_BATCH, count - b0);
     InvBatch bt = {};
@@ -126,7 +166,9 @@ hipError_t poly_batch_invert_multi(Fr* const* a, Fr* const* scratch, int count, 
       bt.a[i] = a[b0 + i];
       bt.pref[i] = scratch[b0 + i];
     }
-    hipLaunchKernelGGL(batch_invert_kernel, dim3(blocks, (unsigned)m), dim3(PT), 0, st, bt, n);
+    hipLaunchKernelGGL(inv_fwd_kernel, dim3(blk1, (unsigned)m), dim3(PT), 0, st, bt, n, T);
+    hipLaunchKernelGGL(inv_regs_kernel, dim3(blk2, (unsigned)m), dim3(PT), 0, st, bt, T);
+    hipLaunchKernelGGL(inv_bwd_kernel, dim3(blk1, (unsigned)m), dim3(PT), 0, st, bt, n, T);
   }
   return hipGetLastError();
 }
@@ -161,20 +203,29 @@ __device__ Fr block_exclusive_scan_mul(Fr v, Fr* sh, Fr* total) {
   return excl;
 }
 
-__global__ void __launch_bounds__(PT) prefix_phase1(const Fr* __restrict__ a, size_t n, Fr* __restrict__ tile_prod) {
+// Arrays of one launch (blockIdx.y) are independent scans (every lookup's product at once);
+// array y's tile products live at scratch[y * (m + 1)].
+struct PrefBatch {
+  const Fr* a[POLY_INV_MAX_BATCH];
+  Fr* out[POLY_INV_MAX_BATCH];
+};
+
+__global__ void __launch_bounds__(PT) prefix_phase1(PrefBatch pb, size_t n, Fr* __restrict__ tile_prod, size_t m) {
   __shared__ Fr sh[PT];
+  const Fr* __restrict__ a = pb.a[blockIdx.y];
   const size_t base = blockIdx.x * PTILE + (size_t)threadIdx.x * PK;
   Fr p = Fr::one();
   for (int k = 0; k < PK; k++)
     if (base + k < n) p = p * ldf(a + base + k);
   Fr total;
   block_exclusive_scan_mul(p, sh, &total);
-  if (threadIdx.x == 0) tile_prod[blockIdx.x] = total;
+  if (threadIdx.x == 0) tile_prod[blockIdx.y * (m + 1) + blockIdx.x] = total;
 }
 
-// single block: exclusive scan of m tile products, in place
-__global__ void __launch_bounds__(PT) prefix_phase2(Fr* __restrict__ tp, size_t m) {
+// one block per array: exclusive scan of its m tile products, in place
+__global__ void __launch_bounds__(PT) prefix_phase2(Fr* __restrict__ tile_prod, size_t m) {
   __shared__ Fr sh[PT];
+  Fr* __restrict__ tp = tile_prod + blockIdx.x * (m + 1);
   const size_t per = (m + PT - 1) / PT;
   const size_t lo = threadIdx.x * per;
   Fr p = Fr::one();
@@ -187,32 +238,53 @@ __global__ void __launch_bounds__(PT) prefix_phase2(Fr* __restrict__ tp, size_t 
   }
 }
 
-__global__ void __launch_bounds__(PT) prefix_phase3(const Fr* __restrict__ a, Fr* __restrict__ out, size_t n,
-                                                    const Fr* __restrict__ tile_excl) {
+// out may alias a (each thread reads its own elements before writing them)
+__global__ void __launch_bounds__(PT) prefix_phase3(PrefBatch pb, size_t n, const Fr* __restrict__ tile_excl,
+                                                    size_t m) {
   __shared__ Fr sh[PT];
+  const Fr* a = pb.a[blockIdx.y];
+  Fr* out = pb.out[blockIdx.y];
   const size_t base = blockIdx.x * PTILE + (size_t)threadIdx.x * PK;
+  Fr x[PK];
   Fr p = Fr::one();
-  for (int k = 0; k < PK; k++)
-    if (base + k < n) p = p * ldf(a + base + k);
+#pragma unroll
+  for (int k = 0; k < PK; k++) {
+    x[k] = base + k < n ? ldf(a + base + k) : Fr::one();
+    p = p * x[k];
+  }
   Fr run = block_exclusive_scan_mul(p, sh, nullptr);
-  run = tile_excl[blockIdx.x] * run;
+  run = tile_excl[blockIdx.y * (m + 1) + blockIdx.x] * run;
+#pragma unroll
   for (int k = 0; k < PK; k++)
     if (base + k < n) {
-      run = run * ldf(a + base + k);
+      run = run * x[k];
       stf(out + base + k, run);
     }
 }
 
 size_t poly_prefix_scratch_len(size_t n) { return (n + PTILE - 1) / PTILE + 1; }
 
-hipError_t poly_prefix_product(const Fr* a, Fr* out, size_t n, Fr* scratch, size_t scratch_len, hipStream_t st) {
-  if (n == 0) return hipSuccess;
+hipError_t poly_prefix_product_multi(const Fr* const* a, Fr* const* out, int count, size_t n, Fr* scratch,
+                                     size_t scratch_len, hipStream_t st) {
+  if (n == 0 || count <= 0) return hipSuccess;
   const size_t m = (n + PTILE - 1) / PTILE;
-  if (scratch_len < m) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(prefix_phase1, dim3((unsigned)m), dim3(PT), 0, st, a, n, scratch);
-  hipLaunchKernelGGL(prefix_phase2, dim3(1), dim3(PT), 0, st, scratch, m);
-  hipLaunchKernelGGL(prefix_phase3, dim3((unsigned)m), dim3(PT), 0, st, a, out, n, (const Fr*)scratch);
+  for (int b0 = 0; b0 < count; b0 += POLY_INV_MAX_BATCH) {
+    const int c = std::min(POLY_INV_MAX_BATCH, count - b0);
+    if (scratch_len < (size_t)c * (m + 1)) return hipErrorInvalidValue;
+    PrefBatch pb = {};
+    for (int i = 0; i < c; i++) {
+      pb.a[i] = a[b0 + i];
+      pb.out[i] = out[b0 + i];
+    }
+    hipLaunchKernelGGL(prefix_phase1, dim3((unsigned)m, (unsigned)c), dim3(PT), 0, st, pb, n, scratch, m);
+    hipLaunchKernelGGL(prefix_phase2, dim3((unsigned)c), dim3(PT), 0, st, scratch, m);
+    hipLaunchKernelGGL(prefix_phase3, dim3((unsigned)m, (unsigned)c), dim3(PT), 0, st, pb, n, (const Fr*)scratch, m);
+  }
   return hipGetLastError();
+}
+
+hipError_t poly_prefix_product(const Fr* a, Fr* out, size_t n, Fr* scratch, size_t scratch_len, hipStream_t st) {
+  return poly_prefix_product_multi(&a, &out, 1, n, scratch, scratch_len, st);
 }
 
 }  // namespace h2g

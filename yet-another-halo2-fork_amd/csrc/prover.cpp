@@ -1526,13 +1526,18 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   {
     std::vector<const Fr*> z_lags;
     std::vector<Fr*> z_polys, z_cosets;
-    auto finish_z = [&](const Fr* prod, Fr* z_lag, Fr* z_poly, Fr* z_coset) -> int {
-      HIPCHK(poly_prefix_product(prod, pk.pre, n, pk.scr, pk.scr_len, st));
+    // prod: the running product's factors, or (scanned) already its prefix products
+    auto finish_z = [&](const Fr* prod, Fr* z_lag, Fr* z_poly, Fr* z_coset, bool scanned) -> int {
+      const Fr* pre = prod;
+      if (!scanned) {
+        HIPCHK(poly_prefix_product(prod, pk.pre, n, pk.scr, pk.scr_len, st));
+        pre = pk.pre;
+      }
       Fr* rows = prod_blind.data() + z_lags.size() * (size_t)bf;
       for (int i = 0; i < bf; i++) rows[i] = rng.random_fr();
       (void)rng.random_fr();  // product blind
       HIPCHK(hipMemcpyAsync(pk.small, rows, (size_t)bf * sizeof(Fr), hipMemcpyHostToDevice, st));
-      HIPCHK(perm_z_assemble(z_lag, n, bf, pk.pre, pk.one, pk.small, st));
+      HIPCHK(perm_z_assemble(z_lag, n, bf, pre, pk.one, pk.small, st));
       z_lags.push_back(z_lag);
       z_polys.push_back(z_poly);
       z_cosets.push_back(z_coset);
@@ -1549,11 +1554,14 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         dens_scr.push_back(w->lk_z[l]);
       }
     HIPCHK(poly_batch_invert_multi(dens.data(), dens_scr.data(), NLT, n, st));
+    // numerators, then every lookup's running product in one batched scan (in place)
     for (CircuitWs* w : W)
-      for (int l = 0; l < pk.NL; l++) {
+      for (int l = 0; l < pk.NL; l++)
         HIPCHK(lookup_prod_num(w->lk_a[l], w->lk_s[l], beta, gamma, w->lk_z_poly[l], n, st));
-        RCCHK(finish_z(w->lk_z_poly[l], w->lk_z[l], w->lk_z_poly[l], w->lk_zc[l]));
-      }
+    HIPCHK(poly_prefix_product_multi((const Fr* const*)dens.data(), dens.data(), NLT, n, pk.scr, pk.scr_len, st));
+    for (CircuitWs* w : W)
+      for (int l = 0; l < pk.NL; l++)
+        RCCHK(finish_z(w->lk_z_poly[l], w->lk_z[l], w->lk_z_poly[l], w->lk_zc[l], true));
     for (CircuitWs* w : W)
       for (int s = 0; s < pk.NS; s++) {
         RCCHK(compress(*w, pk.seg_sh_in[s], pk.tmp_a));
@@ -1561,7 +1569,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         HIPCHK(shuffle_prod_den(pk.tmp_b, gamma, pk.mod, n, st));
         HIPCHK(poly_batch_invert(pk.mod, n, pk.scr, st));
         HIPCHK(shuffle_prod_num(pk.tmp_a, gamma, pk.mod, n, st));
-        RCCHK(finish_z(pk.mod, w->sh_z[s], w->sh_z_poly[s], w->sh_zc[s]));
+        RCCHK(finish_z(pk.mod, w->sh_z[s], w->sh_z_poly[s], w->sh_zc[s], false));
       }
     RCCHK(lagrange_to_coeff_batch(d, D, z_lags.data(), z_polys.data(), (int)z_lags.size(), st));
     RCCHK(ext_cosets(d, pk, (const Fr* const*)z_polys.data(), z_cosets.data(), (int)z_lags.size(), st));
