@@ -919,7 +919,11 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   const uint32_t m1 = (NB + RG - 1) / RG;
   // quad-cooperative group kernels when the groups leave SIMDs idle (<= 512 waves of one
   // lane per group); the block sums then cover Q4_GROUPS groups each
-  const bool red_q4 = (size_t)m1 * WB <= 32768;
+  static const size_t q4_max = [] {
+    const char* e = getenv("H2G_MSM_Q4_MAX");
+    return e ? (size_t)atol(e) : (size_t)32768;
+  }();
+  const bool red_q4 = (size_t)m1 * WB <= q4_max;
   const uint32_t nblk = red_q4 ? (m1 + Q4_GROUPS - 1) / Q4_GROUPS : (m1 + MSM_THREADS - 1) / MSM_THREADS;
   const WsPlan wp = ws_plan(NB);
   if (red_split && (wp.nv2v > 64 || wp.nu2v > 64 || wp.nv2u > 64 || wp.nu2u > 64)) return hipErrorInvalidValue;

@@ -524,6 +524,8 @@ __device__ void block_suffix_affine(Fr val, Fr w, Fr* shv, Fr* shw, Fr* out_val,
 static constexpr int EV_T = 256;
 static constexpr int EV_S = 16;                          // coefficients per thread
 static constexpr uint64_t EV_BLK = (uint64_t)EV_T * EV_S;  // per block
+static constexpr int EV_L = 8;                           // log2(EV_T)
+static_assert((1 << EV_L) == EV_T && EV_BLK == 4096, "eval_level2 raises x to EV_BLK = 2^12");
 
 __global__ void __launch_bounds__(EV_T) eval_level1(const EvalReq* __restrict__ reqs, Fr* __restrict__ part,
                                                     uint64_t nbmax) {
@@ -534,17 +536,33 @@ __global__ void __launch_bounds__(EV_T) eval_level1(const EvalReq* __restrict__ 
     if (threadIdx.x == 0) part[blockIdx.y * nbmax + blockIdx.x] = Fr::zero();
     return;
   }
-  const uint64_t lo = base + (uint64_t)threadIdx.x * EV_S;
+  __shared__ Fr pw[EV_L];  // pw[l] = x^(EV_S 2^l): one thread's squaring chain overlaps the Horner
+  const int t = threadIdx.x;
+  if (t == 0) {
+    Fr step = rq.x;
+#pragma unroll
+    for (int i = 1; i < EV_S; i <<= 1) step = step * step;
+    for (int l = 0; l < EV_L; l++) {
+      pw[l] = step;
+      step = step * step;
+    }
+  }
+  const uint64_t lo = base + (uint64_t)t * EV_S;
   Fr acc = Fr::zero();
   for (int i = EV_S - 1; i >= 0; i--) {
     const uint64_t j = lo + i;
     acc = acc * rq.x + (j < rq.len ? ldf(rq.poly + j) : Fr::zero());
   }
-  Fr step = rq.x;
+  // sum_t acc_t x^(EV_S t): tree with the level weights (255 products per block)
+  sh[t] = acc;
+  __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 4; i++) step = step * step;  // x^16
-  const Fr r = block_weighted_sum<EV_T>(acc, step, sh);
-  if (threadIdx.x == 0) part[blockIdx.y * nbmax + blockIdx.x] = r;
+  for (int l = 0; l < EV_L; l++) {
+    const int s = 1 << l;
+    if ((t & (2 * s - 1)) == 0) sh[t] = sh[t] + pw[l] * sh[t + s];
+    __syncthreads();
+  }
+  if (t == 0) part[blockIdx.y * nbmax + blockIdx.x] = sh[0];
 }
 
 __global__ void __launch_bounds__(EV_T) eval_level2(const EvalReq* __restrict__ reqs, const Fr* __restrict__ part,
