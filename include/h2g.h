@@ -214,7 +214,10 @@ int h2g_params_set_g2(uint64_t params, const uint64_t g2[16], const uint64_t s_g
 /* ---- serialisation: SerdeFormat (halo2_backend/src/helpers.rs:8-21) -----------------
  * format 1 RawBytes (uncompressed points, Montgomery limbs; reads check that field
  * elements are below the modulus and points lie on the curve), 2 RawBytesUnchecked
- * (no checks).  0 Processed (compressed points) is refused with H2G_ERR_ARG.
+ * (no checks), 0 Processed (helpers.rs:36-100: G1 points as 32-B GroupEncoding -- x
+ * canonical LE, bit 7 of the last byte = y odd, identity all zero --, G2 points as 64 B
+ * (x.c0 || x.c1, sign from y.c0), field elements canonical LE (to_repr); reads decompress
+ * on the device and refuse x >= p, x without a curve point and field elements >= r).
  * Writers: out == NULL returns the byte length in *len.
  *   ParamsKZG::write_custom / read_custom  kzg/commitment.rs:166-267
  *   ProvingKey::write / read               plonk.rs:311-359 (+ VerifyingKey::write/read :73-129)

@@ -325,3 +325,93 @@ def g2_affine_mont_limbs(pt) -> list[int]:
     if pt is None:
         return [0] * 16
     return fq_mont_limbs(pt[0][0]) + fq_mont_limbs(pt[0][1]) + fq_mont_limbs(pt[1][0]) + fq_mont_limbs(pt[1][1])
+
+
+# ---------------------------------------------------------------- SerdeFormat::Processed
+# halo2_backend/src/helpers.rs:36-100: curve points as GroupEncoding::to_bytes (halo2curves
+# 0.6 bn256, the encoding the transcript's write_point also uses: x canonical LE, bit 7 of
+# the last byte = parity of canonical y -- of y.c0 for G2 --, identity all zero), field
+# elements as PrimeField::to_repr (canonical LE).  halo2curves is not vendored in the
+# reference, so the flag convention is restated, not pinned by a reference vector.
+
+
+def fq_sqrt(a: int):
+    """a^((p+1)/4) (p = 3 mod 4), None for a non-residue"""
+    y = pow(a % P, (P + 1) // 4, P)
+    return y if y * y % P == a % P else None
+
+
+def fq2_pow(a, e: int):
+    acc = (1, 0)
+    for bit in bin(e)[2:]:
+        acc = fq2_mul(acc, acc)
+        if bit == "1":
+            acc = fq2_mul(acc, a)
+    return acc
+
+
+def fq2_sqrt(a):
+    """a square root in Fq2 (eprint 2012/685 Algorithm 9), None for a non-residue"""
+    if a == (0, 0):
+        return (0, 0)
+    a1 = fq2_pow(a, (P - 3) // 4)
+    alpha = fq2_mul(fq2_mul(a1, a1), a)
+    x0 = fq2_mul(a1, a)
+    if alpha == (P - 1, 0):
+        x = ((-x0[1]) % P, x0[0])
+    else:
+        x = fq2_mul(fq2_pow(fq2_add(alpha, (1, 0)), (P - 1) // 2), x0)
+    return x if fq2_mul(x, x) == a else None
+
+
+def g1_to_bytes(pt) -> bytes:
+    if pt is None:
+        return bytes(32)
+    b = bytearray(pt[0].to_bytes(32, "little"))
+    b[31] |= (pt[1] & 1) << 7
+    return bytes(b)
+
+
+def g1_from_bytes(b: bytes):
+    """(ok, point): GroupEncoding::from_bytes"""
+    ysign = b[31] >> 7
+    x = int.from_bytes(bytes(b[:31]) + bytes([b[31] & 0x7F]), "little")
+    if x >= P:
+        return False, None
+    if x == 0 and not ysign:
+        return True, None
+    y = fq_sqrt(x * x * x + G1_B)
+    if y is None:
+        return False, None
+    if (y & 1) != ysign:
+        y = (-y) % P
+    return True, (x, y)
+
+
+def g2_to_bytes(pt) -> bytes:
+    if pt is None:
+        return bytes(64)
+    b = bytearray(pt[0][0].to_bytes(32, "little") + pt[0][1].to_bytes(32, "little"))
+    b[63] |= (pt[1][0] & 1) << 7
+    return bytes(b)
+
+
+def g2_from_bytes(b: bytes):
+    ysign = b[63] >> 7
+    x0 = int.from_bytes(b[:32], "little")
+    x1 = int.from_bytes(bytes(b[32:63]) + bytes([b[63] & 0x7F]), "little")
+    if x0 >= P or x1 >= P:
+        return False, None
+    if x0 == 0 and x1 == 0 and not ysign:
+        return True, None
+    x = (x0, x1)
+    y = fq2_sqrt(fq2_add(fq2_mul(fq2_mul(x, x), x), G2_B))
+    if y is None:
+        return False, None
+    if (y[0] & 1) != ysign:
+        y = ((-y[0]) % P, (-y[1]) % P)
+    return True, (x, y)
+
+
+def fr_to_repr(x: int) -> bytes:
+    return (x % R).to_bytes(32, "little")

@@ -276,7 +276,7 @@ def _skewed(dist, r, n):
     return sc
 
 
-@pytest.mark.parametrize("window_bits", [0, 3, 8, 13, 20])
+@pytest.mark.parametrize("window_bits", [0, 3, 8, 13, 20, 22])
 @pytest.mark.parametrize("dist", ["random", "ones", "zeros", "rminus1", "sparse"])
 def test_msm_fixed_base_vs_oracle(window_bits, dist):
     """Fixed-base windows (h2g_msm_base_descriptor_dev) incl. offsets into the table."""

@@ -1,4 +1,4 @@
-"""SerdeFormat::RawBytes serialisation of ParamsKZG and ProvingKey on the device path
+"""SerdeFormat::RawBytes and ::Processed serialisation of ParamsKZG and ProvingKey on the device path
 (h2g_params_write/read, h2g_pk_write/read; helpers.rs:8-21, kzg/commitment.rs:166-267,
 plonk.rs:73-129,311-359).  The byte layout is checked field by field against the
 reference's writers (lengths, endianness, section order) and against the oracle
@@ -78,8 +78,6 @@ def test_params_read_checks():
         h2g.Params.read(bytes(bad_g2))
     with pytest.raises(h2g.H2GError):
         h2g.Params.read(bytes(data[:-5]))  # truncated
-    with pytest.raises(h2g.H2GError):
-        h2g.Params.read(bytes(data), h2g.PROCESSED)
     # created params have no G2 half until it is supplied
     q = h2g.Params(k, g, gl)
     with pytest.raises(h2g.H2GError):
@@ -189,6 +187,136 @@ def test_pk_read_checks():
     with pytest.raises(h2g.H2GError):
         h2g.ProvingKey(params, circ, data=bytes(unreduced))
     h2g.ProvingKey(params, circ, data=bytes(unreduced), fmt=h2g.RAW_BYTES_UNCHECKED).close()
-    with pytest.raises(h2g.H2GError):
-        h2g.ProvingKey(params, circ, data=data, fmt=h2g.PROCESSED)
+    params.close()
+
+
+# ---- SerdeFormat::Processed (helpers.rs:36-100): compressed points, canonical scalars ----
+
+
+def _g1_int(limbs):
+    """G1Affine raw limbs (8 u64, Montgomery) -> affine ints, None = identity"""
+    limbs = [int(v) for v in limbs]
+    if not any(limbs):
+        return None
+    return B.from_mont(B.from_limbs(limbs[:4]), B.P), B.from_mont(B.from_limbs(limbs[4:]), B.P)
+
+
+def _g2_int(limbs):
+    limbs = [int(v) for v in limbs]
+    if not any(limbs):
+        return None
+    f = [B.from_mont(B.from_limbs(limbs[4 * i:4 * i + 4]), B.P) for i in range(4)]
+    return (f[0], f[1]), (f[2], f[3])
+
+
+def _fr_repr_bytes(arr):
+    return b"".join(B.fr_to_repr(B.from_mont(B.from_limbs(row), B.R)) for row in arr)
+
+
+def test_params_processed_layout_and_roundtrip():
+    k = 6
+    n = 1 << k
+    s_int, g, gl = O.srs(k)
+    p = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(s_int), dtype=np.uint64))
+    raw = p.write()
+    data = p.write(h2g.PROCESSED)
+    want = (k.to_bytes(4, "little") + b"".join(B.g1_to_bytes(_g1_int(r)) for r in g)
+            + b"".join(B.g1_to_bytes(_g1_int(r)) for r in gl)
+            + B.g2_to_bytes(B.G2_GEN) + B.g2_to_bytes(B.g2_mul(B.G2_GEN, s_int)))
+    assert len(data) == 4 + 2 * n * 32 + 2 * 64
+    assert data == want
+    q = h2g.Params.read(data, h2g.PROCESSED)
+    dg, dgl = q.export()
+    assert np.array_equal(dg, g) and np.array_equal(dgl, gl)
+    assert q.write() == raw and q.write(h2g.PROCESSED) == data
+    circ, wit = hc.simple_example(k)
+    pk = h2g.ProvingKey(q, circ)
+    assert pk.create_proof(wit) == O.create_proof(circ, wit, g, gl)
+    for o in (pk, p, q):
+        o.close()
+
+
+def test_params_processed_read_checks():
+    k = 4
+    n = 1 << k
+    s_int, g, gl = O.srs(k)
+    p = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(s_int), dtype=np.uint64))
+    data = p.write(h2g.PROCESSED)
+    p.close()
+    x = 1
+    while B.fq_sqrt(x ** 3 + 3) is not None:
+        x += 1
+    cases = []
+    for off in (4 + 3 * 32, 4 + n * 32 + 7 * 32):  # a point of g, a point of g_lagrange
+        for enc in (B.P.to_bytes(32, "little"), x.to_bytes(32, "little"), bytes(31) + b"\x80"):
+            bad = bytearray(data)
+            bad[off:off + 32] = enc
+            cases.append(bytes(bad))
+    bad_g2 = bytearray(data)
+    bad_g2[-64:-32] = B.P.to_bytes(32, "little")  # s_g2.x.c0 >= p
+    cases.append(bytes(bad_g2))
+    cases.append(data[:-3])
+    for bad in cases:
+        with pytest.raises(h2g.H2GError):
+            h2g.Params.read(bad, h2g.PROCESSED)
+    # a sign flip is a valid encoding of the negated point
+    flip = bytearray(data)
+    flip[4 + 2 * 32 + 31] ^= 0x80
+    q = h2g.Params.read(bytes(flip), h2g.PROCESSED)
+    dg, _ = q.export()
+    assert _g1_int(dg[2]) == B.g1_neg(_g1_int(g[2]))
+    q.close()
+
+
+@pytest.mark.parametrize("name", ["simple_k6", "lookup_k8", "c3_k9"])
+def test_pk_processed_layout_and_roundtrip(name):
+    circ, wit = PK_CASES[name]()
+    k, n = circ.k, 1 << circ.k
+    s_int, g, gl = O.srs(k)
+    params = h2g.Params(k, g, gl)
+    pk = h2g.ProvingKey(params, circ)
+    raw = pk.write()
+    ext = 1 << pk.extended_k
+    sec = _parse_pk(raw, circ, ext)
+    F, P = circ.num_fixed, len(circ.perm_columns)
+    want = bytearray([4, k]) + F.to_bytes(4, "little")
+    want += b"".join(B.g1_to_bytes(_g1_int(c)) for c in sec["fixed_com"])
+    want += b"".join(B.g1_to_bytes(_g1_int(c)) for c in sec["perm_com"])
+
+    def poly(a):
+        return len(a).to_bytes(4, "big") + _fr_repr_bytes(a)
+
+    def polys(v):
+        return len(v).to_bytes(4, "big") + b"".join(poly(a) for a in v)
+
+    want += poly(sec["l0"]) + poly(sec["l_last"]) + poly(sec["l_active"])
+    want += polys(sec["fixed_values"]) + polys(sec["fixed_polys"]) + polys(sec["fixed_cosets"])
+    want += polys(sec["sigma"]) + polys(sec["sigma_polys"]) + polys(sec["sigma_cosets"])
+    data = pk.write(h2g.PROCESSED)
+    assert data == bytes(want)
+    pk2 = h2g.ProvingKey(params, circ, data=data, fmt=h2g.PROCESSED)
+    assert pk2.write() == raw
+    want_proof = O.create_proof(circ, wit, g, gl)
+    assert pk2.create_proof(wit) == want_proof
+    for o in (pk, pk2, params):
+        o.close()
+
+
+def test_pk_processed_read_checks():
+    circ, wit = hc.simple_example(5)
+    s_int, g, gl = O.srs(5)
+    params = h2g.Params(5, g, gl)
+    pk = h2g.ProvingKey(params, circ)
+    data = pk.write(h2g.PROCESSED)
+    pk.close()
+    unreduced = bytearray(data)
+    unreduced[-32:] = B.R.to_bytes(32, "little")  # last sigma coset element = r
+    bad_com = bytearray(data)
+    bad_com[6:38] = B.P.to_bytes(32, "little")  # the first fixed commitment's x = p
+    for bad in (bytes(unreduced), bytes(bad_com), data[:-1], data + b"\x00"):
+        with pytest.raises(h2g.H2GError):
+            h2g.ProvingKey(params, circ, data=bad, fmt=h2g.PROCESSED)
+    ok = bytearray(data)
+    ok[-32:] = (B.R - 1).to_bytes(32, "little")  # r - 1 is a valid repr
+    h2g.ProvingKey(params, circ, data=bytes(ok), fmt=h2g.PROCESSED).close()
     params.close()

@@ -5,6 +5,8 @@
 // Layout = halo2curves' G2Affine: x = (c0, c1), y = (c0, c1), each an Fq in Montgomery
 // form (4 x u64 LE) -> 16 u64 / 128 raw bytes; identity = all zero.
 #pragma once
+#include <cstring>
+
 #include "bn254.h"
 
 namespace h2g {
@@ -108,6 +110,76 @@ inline G2Affine g2_mul(const G2Affine& p, const uint32_t s[8]) {
       if ((s[i] >> b) & 1) acc = g2_add_affine(acc, p);
     }
   return g2_to_affine(acc);
+}
+
+// ---- SerdeFormat::Processed for G2 (GroupEncoding over Fq2: x = c0 || c1 canonical LE,
+// bit 7 of byte 63 = parity of canonical y.c0, identity = 64 zero bytes)
+inline Fq2 fq2_pow(const Fq2& a, const uint32_t e[8]) {
+  Fq2 acc{Fq::one(), Fq::zero()};
+  for (int i = 7; i >= 0; i--)
+    for (int b = 31; b >= 0; b--) {
+      acc = fq2_sqr(acc);
+      if ((e[i] >> b) & 1) acc = fq2_mul(acc, a);
+    }
+  return acc;
+}
+// a square root in Fq2 for p = 3 mod 4 (Adj & Rodriguez-Henriquez, eprint 2012/685,
+// Algorithm 9); false if a is a non-residue.  Which of the two roots comes back does not
+// matter: the decoder picks the one whose parity matches the sign bit.
+inline bool fq2_sqrt(const Fq2& a, Fq2* out) {
+  static constexpr uint32_t P34[8] = {0xb61f3f51u, 0x4f082305u, 0x5a1c72a3u, 0x65e05aa4u,
+                                      0xa0605617u, 0x6e14116du, 0xb84c680au, 0x0c19139cu};  // (p-3)/4
+  static constexpr uint32_t P12[8] = {0x6c3e7ea3u, 0x9e10460bu, 0xb438e546u, 0xcbc0b548u,
+                                      0x40c0ac2eu, 0xdc2822dbu, 0x7098d014u, 0x18322739u};  // (p-1)/2
+  if (fq2_is_zero(a)) {
+    *out = a;
+    return true;
+  }
+  const Fq2 a1 = fq2_pow(a, P34);
+  const Fq2 alpha = fq2_mul(fq2_sqr(a1), a);
+  const Fq2 x0 = fq2_mul(a1, a);
+  const Fq2 minus_one{Fq::zero() - Fq::one(), Fq::zero()};
+  Fq2 x;
+  if (fq2_eq(alpha, minus_one)) {
+    x = {Fq::zero() - x0.c1, x0.c0};  // u * x0
+  } else {
+    const Fq2 b = fq2_pow(fq2_add(alpha, {Fq::one(), Fq::zero()}), P12);
+    x = fq2_mul(b, x0);
+  }
+  if (!fq2_eq(fq2_sqr(x), a)) return false;
+  *out = x;
+  return true;
+}
+inline void g2_compress(const G2Affine& p, uint8_t out[64]) {
+  std::memset(out, 0, 64);
+  if (p.is_identity()) return;
+  const Fq x0 = to_canonical(p.x.c0), x1 = to_canonical(p.x.c1);
+  std::memcpy(out, x0.l, 32);
+  std::memcpy(out + 32, x1.l, 32);
+  out[63] |= (uint8_t)((to_canonical(p.y.c0).l[0] & 1u) << 7);
+}
+inline bool g2_decompress(const uint8_t in[64], G2Affine* out) {
+  Fq x0, x1;
+  std::memcpy(x0.l, in, 32);
+  std::memcpy(x1.l, in + 32, 32);
+  const uint32_t ysign = x1.l[7] >> 31;
+  x1.l[7] &= 0x7fffffffu;
+  auto below = [](const Fq& v) {
+    unsigned br = 0;
+    for (int i = 0; i < 8; i++) (void)__builtin_subc(v.l[i], FqParams::M[i], br, &br);
+    return br != 0;
+  };
+  if (!below(x0) || !below(x1)) return false;
+  if (x0.is_zero() && x1.is_zero() && !ysign) {
+    *out = G2Affine{{Fq::zero(), Fq::zero()}, {Fq::zero(), Fq::zero()}};
+    return true;
+  }
+  const Fq2 x{from_canonical(x0), from_canonical(x1)};
+  Fq2 y;
+  if (!fq2_sqrt(fq2_add(fq2_mul(fq2_sqr(x), x), g2_b()), &y)) return false;
+  if ((to_canonical(y.c0).l[0] & 1u) != ysign) y = {Fq::zero() - y.c0, Fq::zero() - y.c1};
+  *out = G2Affine{x, y};
+  return true;
 }
 
 }  // namespace h2g

@@ -627,10 +627,19 @@ std::vector<ArgRoots> arg_roots(uint32_t na, const uint32_t* sizes, const int32_
 // ------------------------------------------------------------------ keygen
 // Proving-key arrays taken from a serialised ProvingKey (h2g_pk_read, plonk.rs:311-359)
 // instead of being computed: host pointers into the file buffer, raw Montgomery Fr
-// (SerdeFormat::RawBytes layout = the device layout).
+// (SerdeFormat::RawBytes layout = the device layout), or canonical Fr (Processed: each
+// array is converted with from_repr on the device right after its upload, elements >= r
+// counted into *bad).
 struct PkImage {
   std::vector<const uint8_t*> fixed_lag, fixed_poly, fixed_coset, sigma_lag, sigma_poly, sigma_coset;
   const uint8_t *l0 = nullptr, *l_last = nullptr, *l_active = nullptr;
+  bool canonical = false;
+  uint32_t* bad = nullptr;  // device counter, Processed only
+  hipError_t upload(Fr* dst, const uint8_t* src, size_t cnt, hipStream_t st) const {
+    hipError_t e = hipMemcpyAsync(dst, src, cnt * sizeof(Fr), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess && canonical) e = fr_from_repr(dst, cnt, bad, st);
+    return e;
+  }
 };
 
 // one more circuit workspace (create_proof over pk.cws.size() + 1 circuits)
@@ -961,9 +970,9 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
   HIPCHK(vec_alloc(pk.fixed_coset, pk.F, ext));
   for (int i = 0; i < pk.F; i++) {
     if (img) {
-      HIPCHK(hipMemcpyAsync(pk.fixed_lag[i], img->fixed_lag[i], n * sizeof(Fr), hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(pk.fixed_poly[i], img->fixed_poly[i], n * sizeof(Fr), hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(pk.fixed_coset[i], img->fixed_coset[i], ext * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(img->upload(pk.fixed_lag[i], img->fixed_lag[i], n, st));
+      HIPCHK(img->upload(pk.fixed_poly[i], img->fixed_poly[i], n, st));
+      HIPCHK(img->upload(pk.fixed_coset[i], img->fixed_coset[i], ext, st));
       continue;
     }
     HIPCHK(hipMemcpyAsync(pk.fixed_lag[i], c->fixed_values + 4 * n * i, n * sizeof(Fr), hipMemcpyHostToDevice, st));
@@ -975,9 +984,9 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
   HIPCHK(falloc(&pk.l_last, ext));
   HIPCHK(falloc(&pk.l_active, ext));
   if (img) {
-    HIPCHK(hipMemcpyAsync(pk.l0, img->l0, ext * sizeof(Fr), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(pk.l_last, img->l_last, ext * sizeof(Fr), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(pk.l_active, img->l_active, ext * sizeof(Fr), hipMemcpyHostToDevice, st));
+    HIPCHK(img->upload(pk.l0, img->l0, ext, st));
+    HIPCHK(img->upload(pk.l_last, img->l_last, ext, st));
+    HIPCHK(img->upload(pk.l_active, img->l_active, ext, st));
   } else {
     const Fr one = Fr::one();
     std::vector<Fr> ones(pk.bf, one);
@@ -1002,9 +1011,9 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
   HIPCHK(vec_alloc(pk.sigma_coset, pk.P, ext));
   if (pk.P && img) {
     for (int i = 0; i < pk.P; i++) {
-      HIPCHK(hipMemcpyAsync(pk.sigma_lag[i], img->sigma_lag[i], n * sizeof(Fr), hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(pk.sigma_poly[i], img->sigma_poly[i], n * sizeof(Fr), hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(pk.sigma_coset[i], img->sigma_coset[i], ext * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(img->upload(pk.sigma_lag[i], img->sigma_lag[i], n, st));
+      HIPCHK(img->upload(pk.sigma_poly[i], img->sigma_poly[i], n, st));
+      HIPCHK(img->upload(pk.sigma_coset[i], img->sigma_coset[i], ext, st));
     }
     HIPCHK(hipStreamSynchronize(st));
   } else if (pk.P) {
@@ -2222,6 +2231,44 @@ namespace {
 enum { SERDE_PROCESSED = 0, SERDE_RAW = 1, SERDE_RAW_UNCHECKED = 2 };
 constexpr uint8_t PK_VERSION = 0x04;  // plonk.rs:58
 
+struct DevScratch {
+  void* p = nullptr;
+  ~DevScratch() {
+    if (p) (void)hipFree(p);
+  }
+};
+// GroupEncoding::to_bytes / from_bytes of one G1 point on the host (the VK's commitments);
+// the device form for whole arrays is g1_compress / g1_decompress (serde.hip)
+void g1_compress_host(const G1Affine& a, uint8_t c[32]) {
+  Fq x = Fq::zero();
+  if (!a.is_identity()) {
+    x = to_canonical(a.x);
+    x.l[7] |= (to_canonical(a.y).l[0] & 1u) << 31;
+  }
+  std::memcpy(c, x.l, 32);
+}
+bool g1_decompress_host(const uint8_t c[32], G1Affine* out) {
+  static constexpr uint32_t SQRT_EXP[8] = {0xb61f3f52u, 0x4f082305u, 0x5a1c72a3u, 0x65e05aa4u,
+                                           0xa0605617u, 0x6e14116du, 0xb84c680au, 0x0c19139cu};  // (p+1)/4
+  Fq x;
+  std::memcpy(x.l, c, 32);
+  const uint32_t ysign = x.l[7] >> 31;
+  x.l[7] &= 0x7fffffffu;
+  unsigned br = 0;
+  for (int i = 0; i < 8; i++) (void)__builtin_subc(x.l[i], FqParams::M[i], br, &br);
+  if (!br) return false;  // x >= p
+  out->x = out->y = Fq::zero();
+  if (x.is_zero() && !ysign) return true;  // identity
+  const Fq xm = from_canonical(x);
+  const Fq y2 = sqr(xm) * xm + from_u64<FqParams>(3);
+  Fq y = pow_limbs(y2, SQRT_EXP);
+  if (sqr(y) != y2) return false;
+  if ((to_canonical(y).l[0] & 1u) != ysign) y = neg(y);
+  out->x = xm;
+  out->y = y;
+  return true;
+}
+
 struct ByteWriter {  // out == NULL: count only
   uint8_t* out;
   size_t cap, len = 0;
@@ -2236,16 +2283,44 @@ struct ByteWriter {  // out == NULL: count only
     const uint8_t b[4] = {(uint8_t)(v >> 24), (uint8_t)(v >> 16), (uint8_t)(v >> 8), (uint8_t)v};
     put(b, 4);
   }
+  bool proc = false;  // SerdeFormat::Processed: compressed points, canonical field elements
   int dev(const void* d, size_t k) {  // device bytes
     if (fits(k)) HIPCHK(hipMemcpy(out + len, d, k, hipMemcpyDeviceToHost));
     len += k;
     return H2G_OK;
   }
-  void g1(const G1Affine& a) { put(&a, sizeof(G1Affine)); }
-  void g2(const G2Affine& a) { put(&a, sizeof(G2Affine)); }
+  // `cnt` elements converted on the device into a scratch array of `k` bytes, then copied
+  template <class Conv>
+  int dev_conv(size_t k, Conv conv) {
+    if (fits(k)) {
+      DevScratch t;
+      HIPCHK(hipMalloc(&t.p, k));
+      HIPCHK(conv(t.p));
+      HIPCHK(hipMemcpy(out + len, t.p, k, hipMemcpyDeviceToHost));
+    }
+    len += k;
+    return H2G_OK;
+  }
+  int g1s(const G1Affine* d, size_t cnt) {  // SerdeCurveAffine::write of cnt device points
+    if (!proc) return dev(d, cnt * sizeof(G1Affine));
+    return dev_conv(cnt * 32, [&](void* t) { return g1_compress(d, cnt, (uint8_t*)t, nullptr); });
+  }
+  void g1(const G1Affine& a) {
+    if (!proc) return put(&a, sizeof(G1Affine));
+    uint8_t c[32];
+    g1_compress_host(a, c);
+    put(c, 32);
+  }
+  void g2(const G2Affine& a) {
+    if (!proc) return put(&a, sizeof(G2Affine));
+    uint8_t c[64];
+    g2_compress(a, c);
+    put(c, 64);
+  }
   int poly(const Fr* d, size_t cnt) {  // Polynomial::write (poly.rs:187-197)
     u32be((uint32_t)cnt);
-    return dev(d, cnt * sizeof(Fr));
+    if (!proc) return dev(d, cnt * sizeof(Fr));
+    return dev_conv(cnt * sizeof(Fr), [&](void* t) { return fr_to_repr(d, cnt, (Fr*)t, nullptr); });
   }
   int polys(const std::vector<Fr*>& v, size_t cnt) {  // write_polynomial_slice (helpers.rs:119-129)
     u32be((uint32_t)v.size());
@@ -2326,14 +2401,15 @@ int h2g_params_write(uint64_t params, int format, uint8_t* out, size_t cap, size
   auto it = g_params.find(params);
   if (it == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
   if (!len) return fail(H2G_ERR_ARG, "params_write: null length");
-  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED)
-    return fail(H2G_ERR_ARG, "params_write: only SerdeFormat::RawBytes / RawBytesUnchecked are supported");
+  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED && format != SERDE_PROCESSED)
+    return fail(H2G_ERR_ARG, "params_write: unknown SerdeFormat");
   const Params& p = *it->second;
   if (!p.has_g2) return fail(H2G_ERR_STATE, "params_write: the params have no G2 points (h2g_params_set_g2)");
   ByteWriter w{out, out ? cap : 0};
+  w.proc = format == SERDE_PROCESSED;
   w.u32le(p.k);
-  RCCHK(w.dev(p.g, p.n * sizeof(G1Affine)));
-  RCCHK(w.dev(p.gl, p.n * sizeof(G1Affine)));
+  RCCHK(w.g1s(p.g, p.n));
+  RCCHK(w.g1s(p.gl, p.n));
   w.g2(p.g2);
   w.g2(p.s_g2);
   *len = w.len;
@@ -2345,16 +2421,18 @@ int h2g_params_write(uint64_t params, int format, uint8_t* out, size_t cap, size
 int h2g_params_read(const uint8_t* buf, size_t len, int format, uint64_t* handle) {
   NEED_DEV_P();
   if (!buf || !handle) return fail(H2G_ERR_ARG, "params_read: null argument");
-  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED)
-    return fail(H2G_ERR_ARG, "params_read: only SerdeFormat::RawBytes / RawBytesUnchecked are supported");
+  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED && format != SERDE_PROCESSED)
+    return fail(H2G_ERR_ARG, "params_read: unknown SerdeFormat");
+  const bool proc = format == SERDE_PROCESSED;
+  const size_t g1b = proc ? 32 : sizeof(G1Affine), g2b = proc ? 64 : sizeof(G2Affine);
   ByteReader r{buf, len};
   const uint32_t k = r.u32le();
   if (!r.ok || k > 27) return fail(H2G_ERR_ARG, "params_read: bad k");
   const size_t n = (size_t)1 << k;
-  const uint8_t* g = r.take(n * sizeof(G1Affine));
-  const uint8_t* gl = r.take(n * sizeof(G1Affine));
-  const uint8_t* g2 = r.take(sizeof(G2Affine));
-  const uint8_t* sg2 = r.take(sizeof(G2Affine));
+  const uint8_t* g = r.take(n * g1b);
+  const uint8_t* gl = r.take(n * g1b);
+  const uint8_t* g2 = r.take(g2b);
+  const uint8_t* sg2 = r.take(g2b);
   if (!r.ok) return fail(H2G_ERR_ARG, "params_read: truncated input");
   hipStream_t st = d->stream;
   auto p = std::make_unique<Params>();
@@ -2363,10 +2441,27 @@ int h2g_params_read(const uint8_t* buf, size_t len, int format, uint64_t* handle
   p->n = n;
   PALLOC(p->pool, p->g, n);
   PALLOC(p->pool, p->gl, n);
-  HIPCHK(hipMemcpyAsync(p->g, g, n * sizeof(G1Affine), hipMemcpyHostToDevice, st));
-  HIPCHK(hipMemcpyAsync(p->gl, gl, n * sizeof(G1Affine), hipMemcpyHostToDevice, st));
-  std::memcpy(&p->g2, g2, sizeof(G2Affine));
-  std::memcpy(&p->s_g2, sg2, sizeof(G2Affine));
+  if (proc) {  // load_points_from_file_parallelly (kzg/commitment.rs:195-213), on the device
+    DevScratch t, bad;
+    uint32_t nbad = 0;
+    HIPCHK(hipMalloc(&t.p, 2 * n * 32));
+    HIPCHK(hipMalloc(&bad.p, 4));
+    HIPCHK(hipMemsetAsync(bad.p, 0, 4, st));
+    HIPCHK(hipMemcpyAsync(t.p, g, n * 32, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync((uint8_t*)t.p + n * 32, gl, n * 32, hipMemcpyHostToDevice, st));
+    HIPCHK(g1_decompress((const uint8_t*)t.p, n, p->g, (uint32_t*)bad.p, st));
+    HIPCHK(g1_decompress((const uint8_t*)t.p + n * 32, n, p->gl, (uint32_t*)bad.p, st));
+    HIPCHK(hipMemcpyAsync(&nbad, bad.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (nbad) return fail(H2G_ERR_ARG, "params_read: " + std::to_string(nbad) + " invalid point encodings");
+    if (!g2_decompress(g2, &p->g2) || !g2_decompress(sg2, &p->s_g2))
+      return fail(H2G_ERR_ARG, "params_read: invalid G2 point encoding");
+  } else {
+    HIPCHK(hipMemcpyAsync(p->g, g, n * sizeof(G1Affine), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(p->gl, gl, n * sizeof(G1Affine), hipMemcpyHostToDevice, st));
+    std::memcpy(&p->g2, g2, sizeof(G2Affine));
+    std::memcpy(&p->s_g2, sg2, sizeof(G2Affine));
+  }
   p->has_g2 = true;
   if (format == SERDE_RAW) {
     uint32_t* bad;
@@ -2418,14 +2513,15 @@ int h2g_pk_write(uint64_t pk_h, int format, uint8_t* out, size_t cap, size_t* le
   auto it = g_pks.find(pk_h);
   if (it == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
   if (!len) return fail(H2G_ERR_ARG, "pk_write: null length");
-  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED)
-    return fail(H2G_ERR_ARG, "pk_write: only SerdeFormat::RawBytes / RawBytesUnchecked are supported");
+  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED && format != SERDE_PROCESSED)
+    return fail(H2G_ERR_ARG, "pk_write: unknown SerdeFormat");
   ProvingKey& pk = *it->second;
   auto pit = g_params.find(pk.params);
   if (pit == g_params.end()) return fail(H2G_ERR_HANDLE, "pk_write: the key's params were freed");
   RCCHK(h2g_pk_vk_commitments(pk_h, nullptr, nullptr));  // commit_lagrange, once
   HIPCHK(hipStreamSynchronize(d->stream));
   ByteWriter w{out, out ? cap : 0};
+  w.proc = format == SERDE_PROCESSED;
   w.u8(PK_VERSION);
   w.u8((uint8_t)pk.k);
   w.u32le((uint32_t)pk.F);
@@ -2454,8 +2550,9 @@ int h2g_pk_read(uint64_t params, const h2g_circuit* circuit, const uint8_t* buf,
   auto it = g_params.find(params);
   if (it == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
   if (!circuit || !buf || !pk_out) return fail(H2G_ERR_ARG, "pk_read: null argument");
-  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED)
-    return fail(H2G_ERR_ARG, "pk_read: only SerdeFormat::RawBytes / RawBytesUnchecked are supported");
+  if (format != SERDE_RAW && format != SERDE_RAW_UNCHECKED && format != SERDE_PROCESSED)
+    return fail(H2G_ERR_ARG, "pk_read: unknown SerdeFormat");
+  const bool proc = format == SERDE_PROCESSED;
   ByteReader r{buf, len};
   if (r.u8() != PK_VERSION) return fail(H2G_ERR_ARG, "pk_read: unexpected version byte");
   const uint32_t k = r.u8();
@@ -2464,11 +2561,17 @@ int h2g_pk_read(uint64_t params, const h2g_circuit* circuit, const uint8_t* buf,
   if (!r.ok || F != circuit->num_fixed) return fail(H2G_ERR_ARG, "pk_read: fixed column count does not match");
   const uint32_t P = circuit->num_perm_columns;
   std::vector<G1Affine> vf(F), vp(P);
-  for (auto& c : vf)
-    if (const uint8_t* b = r.take(sizeof(G1Affine))) std::memcpy(&c, b, sizeof(G1Affine));
-  for (auto& c : vp)
-    if (const uint8_t* b = r.take(sizeof(G1Affine))) std::memcpy(&c, b, sizeof(G1Affine));
+  bool enc_ok = true;
+  for (auto* v : {&vf, &vp})
+    for (auto& c : *v) {
+      if (proc) {
+        if (const uint8_t* b = r.take(32)) enc_ok = g1_decompress_host(b, &c) && enc_ok;
+      } else if (const uint8_t* b = r.take(sizeof(G1Affine))) {
+        std::memcpy(&c, b, sizeof(G1Affine));
+      }
+    }
   if (!r.ok) return fail(H2G_ERR_ARG, "pk_read: truncated verifying key");
+  if (!enc_ok) return fail(H2G_ERR_ARG, "pk_read: invalid point encoding in the verifying key");
   if (format == SERDE_RAW) {
     for (const auto& c : vf)
       if (!g1_valid_host(c)) return fail(H2G_ERR_ARG, "pk_read: invalid fixed commitment");
@@ -2496,9 +2599,23 @@ int h2g_pk_read(uint64_t params, const h2g_circuit* circuit, const uint8_t* buf,
   r.polys(img.sigma_coset, P, ext_len);
   if (!r.ok) return fail(H2G_ERR_ARG, "pk_read: truncated or mis-sized proving key");
   if (r.pos != len) return fail(H2G_ERR_ARG, "pk_read: trailing bytes");
+  DevScratch bad;
+  if (proc) {
+    img.canonical = true;
+    HIPCHK(hipMalloc(&bad.p, 4));
+    HIPCHK(hipMemsetAsync(bad.p, 0, 4, d->stream));
+    img.bad = (uint32_t*)bad.p;
+  }
   auto pk = std::make_unique<ProvingKey>();
   pk->params = params;
   int rc = keygen_impl(d, *it->second, circuit, *pk, &img);
+  if (rc == H2G_OK && proc) {
+    uint32_t nbad = 0;
+    if (hipMemcpyAsync(&nbad, bad.p, 4, hipMemcpyDeviceToHost, d->stream) != hipSuccess ||
+        hipStreamSynchronize(d->stream) != hipSuccess)
+      rc = fail(H2G_ERR_DEVICE, "pk_read: counter copy");
+    else if (nbad) rc = fail(H2G_ERR_ARG, "pk_read: " + std::to_string(nbad) + " field elements not below the modulus");
+  }
   if (rc == H2G_OK && pk->ext != ext_len) rc = fail(H2G_ERR_ARG, "pk_read: extended domain size does not match the circuit");
   if (rc == H2G_OK && format == SERDE_RAW) {
     std::vector<std::pair<const Fr*, size_t>> arrays = {{pk->l0, pk->ext}, {pk->l_last, pk->ext}, {pk->l_active, pk->ext}};

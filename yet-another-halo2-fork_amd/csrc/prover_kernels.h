@@ -190,4 +190,12 @@ hipError_t g1_generator_mul(const Fr* scalars, size_t n, G1Affine* out, hipStrea
 hipError_t fr_count_unreduced(const Fr* a, size_t n, uint32_t* bad, hipStream_t st);
 hipError_t g1_count_invalid(const G1Affine* p, size_t n, uint32_t* bad, hipStream_t st);
 
+// ---- SerdeFormat::Processed (helpers.rs:36-100; serde.hip): 32-B compressed G1 points
+// (GroupEncoding) and canonical field elements (to_repr / from_repr).  Decompression and
+// from_repr add the number of invalid encodings to *bad (zeroed by the caller).
+hipError_t g1_compress(const G1Affine* p, size_t n, uint8_t* out, hipStream_t st);
+hipError_t g1_decompress(const uint8_t* in, size_t n, G1Affine* out, uint32_t* bad, hipStream_t st);
+hipError_t fr_to_repr(const Fr* a, size_t n, Fr* out, hipStream_t st);
+hipError_t fr_from_repr(Fr* a, size_t n, uint32_t* bad, hipStream_t st);
+
 }  // namespace h2g
