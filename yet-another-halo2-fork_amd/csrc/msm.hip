@@ -596,11 +596,12 @@ __device__ G1xyzz xyzz_mul_u32_q4(const G1xyzz& p, uint32_t k) {
 
 // 6a. bucket reduction (default): F = sum_j (j+1) B_j per window, shallow ------------------
 // A serial chain of XYZZ additions costs ~12 us on the GPU at low occupancy, so the
-// reduction minimises dependent depth, not work:
+// reduction minimises dependent depth, not only work:
 //   rgroup : groups of RG buckets: S_g = sum_t (t+1) B_{RG g+t}, R_g = sum_t B_{RG g+t}
-//   rscale : V_g = S_g + [RG g] R_g   (F = sum_g V_g), block sums of V
+//   then F = sum_g (S_g + [RG g] R_g) by bit planes (6a', up to 2^16 groups), or
+//   rscale : V_g = S_g + [RG g] R_g (one scalar multiplication per group), block sums of V
 //   rfinal : sum of the block sums
-// depth ~ 2 RG + (log2(RG m) dbl + adds) + 2 x 8 tree steps.
+// (rscale's depth ~ 2 RG + (log2(RG m) dbl + adds) + 2 x 8 tree steps).
 #ifndef H2G_MSM_RG
 #define H2G_MSM_RG 8
 #endif
@@ -702,6 +703,154 @@ msm_rfinal_q4_kernel(const G1xyzz* __restrict__ part, uint32_t nblk, G1xyzz* __r
     if (qi < h) {
       const G1xyzz t = xyzz_add_q4(sh[qi], sh[qi + h]);
       if ((threadIdx.x & 3) == 0) sh[qi] = t;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) windows[w] = sh[0];
+}
+
+// 6a'. group weights by bit planes (default when the groups fit 2^16) ----------------------
+// F = sum_g (S_g + 2^e g R_g) = sum_g S_g + sum_b 2^(b+e) U_b,  U_b = sum_{g : bit b of g} R_g.
+// The plane sums need no scalar multiplication: a block of 256 groups folds its R_t in
+// a binary tree whose nodes keep (T, L_0 .. L_{k-1}) -- the subtree total and the sums of
+// the elements with bit b of t set; merging halves A | C of size 2^k costs k + 1 additions
+// (T += T_C, L_b += L_b^C) and C's total becomes L_k in place.  ~2.5 point operations per
+// group against ~30 for rscale's 19-bit double-and-add, depth 8.  The blocks' L_b are
+// plain-summed across blocks (plane b < 8) and their totals folded once more by block
+// index (planes 8..15); the last block to finish scales the 16 planes and adds them to
+// sum S.  Two launches (rgroup fused into the first), lane-per-group (Q = 1) or
+// quad-cooperative (Q = 4) like the group kernels above.
+static constexpr uint32_t BP = 256;  // groups per block of the plane kernels
+
+template <int Q>
+__device__ __forceinline__ G1xyzz padd(const G1xyzz& a, const G1xyzz& b) {
+  if constexpr (Q == 4) return xyzz_add_q4(a, b);
+  else return xyzz_add(a, b);
+}
+template <int Q>
+__device__ __forceinline__ G1xyzz pdbl(const G1xyzz& a) {
+  if constexpr (Q == 4) return xyzz_dbl_q4(a);
+  else return xyzz_dbl(a);
+}
+
+// in LDS: T[0..len) holds one value per element, len = 2^K <= BP.  Afterwards T[0] is the
+// total and T[2^b] (b < K) the sum over the elements with bit b of their index set.
+template <int Q>
+__device__ __forceinline__ void plane_fold(G1xyzz* T, int K, uint32_t e, bool lead) {
+  for (int k = 0; k < K; k++) {
+    const uint32_t per = (uint32_t)k + 1, pairs = (1u << (K - 1 - k));
+    if (e < pairs * per) {
+      const uint32_t j = e / per, i = e % per;
+      const uint32_t dst = (j << (k + 1)) + (i == 0 ? 0u : (1u << (i - 1))), src = dst + (1u << k);
+      const G1xyzz v = padd<Q>(T[dst], T[src]);
+      if (lead) T[dst] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// level A, fused with rgroup: block b takes groups g = 256 b + t, forms S_t, R_t like
+// msm_rgroup_kernel, and writes planes[0][b] = sum S, planes[1 + p][b] = L_p (p < 8),
+// planes[9][b] = T (the block's R total); planes[q] is (WB x nblk)
+template <int Q>
+__global__ void __launch_bounds__(BP * Q)
+msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, uint32_t nblk,
+                        G1xyzz* __restrict__ planes) {
+  __shared__ G1xyzz shT[BP], shS[BP];
+  const uint32_t w = blockIdx.y, e = threadIdx.x / Q;
+  const bool lead = (threadIdx.x % Q) == 0;
+  const uint32_t g = blockIdx.x * BP + e;
+  const size_t ps = (size_t)gridDim.y * nblk;  // stride between planes
+  const G1xyzz* b = B + (size_t)w * NB;
+  G1xyzz racc = G1xyzz::identity(), sacc = G1xyzz::identity();
+  if (g < m1) {
+    for (int t = RG - 1; t >= 0; t--) {
+      const uint32_t j = g * RG + t;
+      if (j < NB) racc = padd<Q>(racc, b[j]);
+      sacc = padd<Q>(sacc, racc);
+    }
+  }
+  if (lead) {
+    shT[e] = racc;
+    shS[e] = sacc;
+  }
+  __syncthreads();
+  // the R tree and a plain S tree side by side: elements [0, 2^(7-k)(k+1)) fold R at level
+  // k, the next 2^(7-k) fold S
+  for (int k = 0; k < 8; k++) {
+    const uint32_t per = (uint32_t)k + 1, pairs = 1u << (7 - k);
+    if (e < pairs * per) {
+      const uint32_t j = e / per, i = e % per;
+      const uint32_t dst = (j << (k + 1)) + (i == 0 ? 0u : (1u << (i - 1))), src = dst + (1u << k);
+      const G1xyzz v = padd<Q>(shT[dst], shT[src]);
+      if (lead) shT[dst] = v;
+    } else if (e < pairs * (per + 1)) {
+      const uint32_t j = e - pairs * per, dst = j << (k + 1);
+      const G1xyzz v = padd<Q>(shS[dst], shS[dst + (1u << k)]);
+      if (lead) shS[dst] = v;
+    }
+    __syncthreads();
+  }
+  if (lead && e < 10) {
+    const G1xyzz v = e == 0 ? shS[0] : (e < 9 ? shT[1u << (e - 1)] : shT[0]);
+    planes[e * ps + (size_t)w * nblk + blockIdx.x] = v;
+  }
+}
+
+// levels B and C, one launch: block q < 9 sums plane q over the nblk blocks; block 9
+// folds the totals T by block index (nblk <= BP) -- mid[q' * WB + w], q' < 17: 0 = sum S,
+// 1 + b = U_b (b < 16).  The last of a set's 10 blocks to finish (device-scope counter,
+// zeroed by the host) then scales U_b by 2^(b + e0), one quad per plane, and sums.
+__global__ void __launch_bounds__(4 * BP)
+msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int e0, G1xyzz* __restrict__ mid,
+                      uint32_t* __restrict__ done, G1xyzz* __restrict__ windows) {
+  __shared__ G1xyzz sh[BP];
+  __shared__ uint32_t last;
+  const uint32_t q = blockIdx.x, w = blockIdx.y, e = threadIdx.x >> 2, WB = gridDim.y;
+  const bool lead = (threadIdx.x & 3) == 0;
+  const G1xyzz* in = planes + (size_t)q * WB * nblk + (size_t)w * nblk;
+  if (q < 9) {
+    G1xyzz acc = G1xyzz::identity();
+    for (uint32_t i = e; i < nblk; i += BP) acc = xyzz_add_q4(acc, in[i]);
+    if (lead) sh[e] = acc;
+    __syncthreads();
+    for (uint32_t h = BP / 2; h > 0; h >>= 1) {
+      if (e < h) {
+        const G1xyzz v = xyzz_add_q4(sh[e], sh[e + h]);
+        if (lead) sh[e] = v;
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) mid[(size_t)q * WB + w] = sh[0];
+  } else {
+    int K = 0;
+    while ((1u << K) < nblk) K++;
+    if (lead) sh[e] = e < nblk ? in[e] : G1xyzz::identity();
+    __syncthreads();
+    plane_fold<4>(sh, K, e, lead);
+    if (lead && e < 8) mid[(size_t)(9 + e) * WB + w] = e < (uint32_t)K ? sh[1u << e] : G1xyzz::identity();
+  }
+  __syncthreads();  // this block's outputs are written
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(&done[w], 1u) == 9u;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  G1xyzz x = G1xyzz::identity();
+  if (e < 16) {
+    x = mid[(size_t)(1 + e) * WB + w];
+    for (int i = 0; i < (int)e + e0; i++) x = xyzz_dbl_q4(x);
+  } else if (e == 16) {
+    x = mid[w];
+  }
+  if (lead && e < 32) sh[e] = x;
+  __syncthreads();
+  for (uint32_t h = 16; h > 0; h >>= 1) {
+    if (e < h) {
+      const G1xyzz v = xyzz_add_q4(sh[e], sh[e + h]);
+      if (lead) sh[e] = v;
     }
     __syncthreads();
   }
@@ -916,6 +1065,10 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     const char* e = getenv("H2G_MSM_RED");
     return e && std::string(e) == "split";
   }();
+  static const bool red_group = [] {  // rscale / rfinal for every size (A/B runs)
+    const char* e = getenv("H2G_MSM_RED");
+    return e && std::string(e) == "group";
+  }();
   const uint32_t m1 = (NB + RG - 1) / RG;
   // quad-cooperative group kernels when the groups leave SIMDs idle (<= 512 waves of one
   // lane per group); the block sums then cover Q4_GROUPS groups each
@@ -925,6 +1078,11 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   }();
   const bool red_q4 = (size_t)m1 * WB <= q4_max;
   const uint32_t nblk = red_q4 ? (m1 + Q4_GROUPS - 1) / Q4_GROUPS : (m1 + MSM_THREADS - 1) / MSM_THREADS;
+  const uint32_t nblk_p = (m1 + BP - 1) / BP;  // plane kernels' blocks
+  // planes where the groups fill the SIMDs (2^21-2^22-point MSMs at c = 20); small MSMs
+  // keep the quad-cooperative rscale scheme, whose 64-group blocks spread over more CUs
+  // (2^19 points: reduction 0.40 vs 0.54 ms with 256-group plane blocks)
+  const bool red_plane = !red_group && !red_q4 && nblk_p <= BP;
   const WsPlan wp = ws_plan(NB);
   if (red_split && (wp.nv2v > 64 || wp.nu2v > 64 || wp.nv2u > 64 || wp.nu2u > 64)) return hipErrorInvalidValue;
   // grow-only workspace: MSMs of slightly different shapes (e.g. n and n - 1 points, so
@@ -941,7 +1099,8 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
                          {&ws->item_bucket, icap * sizeof(MsmBigItem)},  // big-bucket items
                          {&ws->partials, 2 * nchunks * sizeof(G1xyzz)},  // boundary slots
                          {&ws->buckets, (size_t)nbt * sizeof(G1xyzz)},
-                         {&ws->segs, std::max<size_t>(wp.per_set, (size_t)2 * m1 + nblk) * WB * sizeof(G1xyzz)},
+                         {&ws->segs, std::max<size_t>(wp.per_set, (size_t)2 * m1 + nblk + 10 * (size_t)nblk_p + 17) *
+                                         WB * sizeof(G1xyzz)},
                          {&ws->windows, (size_t)(W > WB ? W : WB) * sizeof(G1xyzz)},
                          {&ws->result, 16},                              // [0] items, [1] multi-item buckets
                          {&ws->item_off, mcap * sizeof(uint4)},          // multi-item buckets
@@ -980,7 +1139,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   if (ncoarse > COARSE_MAX || fb > FB_MAX) return hipErrorInvalidValue;
   const uint32_t kblocks = (nbt + 1023) / 1024;
   // scratch (u32): ccount | coff | ccursor | total | kcount | koff | kcursor | block sums | block offsets
-  const size_t sort_words = 3 * (size_t)COARSE_MAX + 16 + 3 * (size_t)nbt + 2 * (size_t)kblocks + 16;
+  const size_t sort_words = 3 * (size_t)COARSE_MAX + 16 + 3 * (size_t)nbt + 2 * (size_t)kblocks + 16 + (size_t)WB;
   if (sort_words * 4 > ws->sort_tmp_bytes) {
     H2G_TRY(grow(&ws->sort_tmp, sort_words * 4));
     ws->sort_tmp_bytes = sort_words * 4;
@@ -994,6 +1153,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   uint32_t* kcursor = koff + nbt;
   uint32_t* kbsum = kcursor + nbt;
   uint32_t* kboff = kbsum + kblocks;
+  uint32_t* rdone = kboff + kblocks;  // plane reduction: finished blocks per set
 
   const int T = MSM_THREADS;
   H2G_PHASE(0);
@@ -1050,19 +1210,36 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
                      (const uint32_t*)counters, (const G1xyzz*)ipart, buckets);
   H2G_PHASE(5);
   if (!red_split) {
-    if (red_q4) {
-      hipLaunchKernelGGL(msm_rgroup_q4_kernel, dim3((unsigned)(((size_t)m1 * 4 + T - 1) / T), (unsigned)WB), dim3(T),
-                         0, st, (const G1xyzz*)buckets, NB, m1, rS, rR);
-      hipLaunchKernelGGL(msm_rscale_q4_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
-                         (const G1xyzz*)rR, m1, rP, nblk);
+    if (red_plane) {  // bit planes (6a')
+      G1xyzz* planes = rP;
+      G1xyzz* mid = planes + (size_t)10 * WB * nblk_p;
+      int e0 = 0;
+      while ((1 << e0) < RG) e0++;
+      H2G_TRY(hipMemsetAsync(rdone, 0, (size_t)WB * 4, st));
+      if (red_q4)
+        hipLaunchKernelGGL(msm_rgroup_plane_kernel<4>, dim3(nblk_p, (unsigned)WB), dim3(4 * BP), 0, st,
+                           (const G1xyzz*)buckets, NB, m1, nblk_p, planes);
+      else
+        hipLaunchKernelGGL(msm_rgroup_plane_kernel<1>, dim3(nblk_p, (unsigned)WB), dim3(BP), 0, st,
+                           (const G1xyzz*)buckets, NB, m1, nblk_p, planes);
+      hipLaunchKernelGGL(msm_rplane_mid_kernel, dim3(10, (unsigned)WB), dim3(4 * BP), 0, st, (const G1xyzz*)planes,
+                         nblk_p, e0, mid, rdone, (G1xyzz*)ws->windows);
     } else {
-      hipLaunchKernelGGL(msm_rgroup_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1,
-                         rS, rR);
-      hipLaunchKernelGGL(msm_rscale_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
-                         (const G1xyzz*)rR, m1, rP, nblk);
+      if (red_q4)
+        hipLaunchKernelGGL(msm_rgroup_q4_kernel, dim3((unsigned)(((size_t)m1 * 4 + T - 1) / T), (unsigned)WB),
+                           dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1, rS, rR);
+      else
+        hipLaunchKernelGGL(msm_rgroup_kernel, dim3((m1 + T - 1) / T, (unsigned)WB), dim3(T), 0, st,
+                           (const G1xyzz*)buckets, NB, m1, rS, rR);
+      if (red_q4)
+        hipLaunchKernelGGL(msm_rscale_q4_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
+                           (const G1xyzz*)rR, m1, rP, nblk);
+      else
+        hipLaunchKernelGGL(msm_rscale_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
+                           (const G1xyzz*)rR, m1, rP, nblk);
+      hipLaunchKernelGGL(msm_rfinal_q4_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rP, nblk,
+                         (G1xyzz*)ws->windows);
     }
-    hipLaunchKernelGGL(msm_rfinal_q4_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rP, nblk,
-                       (G1xyzz*)ws->windows);
   } else {
     const uint32_t s1n = wp.nv1 + wp.nu1, s2n = wp.nv2v + wp.nu2v + wp.nv2u + wp.nu2u;
     hipLaunchKernelGGL(msm_wsplit_kernel<256>, dim3(s1n, (unsigned)WB), dim3(256), 0, st, (const G1xyzz*)buckets, NB,
