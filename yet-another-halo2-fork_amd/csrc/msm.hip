@@ -718,9 +718,8 @@ msm_rfinal_q4_kernel(const G1xyzz* __restrict__ part, uint32_t nblk, G1xyzz* __r
 // group against ~30 for rscale's 19-bit double-and-add, depth 8.  The blocks' L_b are
 // plain-summed across blocks (plane b < 8) and their totals folded once more by block
 // index (planes 8..15); the last block to finish scales the 16 planes and adds them to
-// sum S.  Two launches (rgroup fused into the first), lane-per-group (Q = 1) or
-// quad-cooperative (Q = 4) like the group kernels above.
-static constexpr uint32_t BP = 256;  // groups per block of the plane kernels
+// sum S.  Two launches (rgroup fused into the first), lane-per-group (Q = 1, 256-group
+// blocks) or quad-cooperative (Q = 4, 64-group blocks) like the group kernels above.
 
 template <int Q>
 __device__ __forceinline__ G1xyzz padd(const G1xyzz& a, const G1xyzz& b) {
@@ -733,7 +732,7 @@ __device__ __forceinline__ G1xyzz pdbl(const G1xyzz& a) {
   else return xyzz_dbl(a);
 }
 
-// in LDS: T[0..len) holds one value per element, len = 2^K <= BP.  Afterwards T[0] is the
+// in LDS: T[0..len) holds one value per element, len = 2^K <= 512.  Afterwards T[0] is the
 // total and T[2^b] (b < K) the sum over the elements with bit b of their index set.
 template <int Q>
 __device__ __forceinline__ void plane_fold(G1xyzz* T, int K, uint32_t e, bool lead) {
@@ -749,17 +748,20 @@ __device__ __forceinline__ void plane_fold(G1xyzz* T, int K, uint32_t e, bool le
   }
 }
 
-// level A, fused with rgroup: block b takes groups g = 256 b + t, forms S_t, R_t like
-// msm_rgroup_kernel, and writes planes[0][b] = sum S, planes[1 + p][b] = L_p (p < 8),
-// planes[9][b] = T (the block's R total); planes[q] is (WB x nblk)
-template <int Q>
-__global__ void __launch_bounds__(BP * Q)
+// level A, fused with rgroup: block b takes 2^LB groups g = 2^LB b + t, forms S_t, R_t like
+// msm_rgroup_kernel, and writes planes[0][b] = sum S, planes[1 + p][b] = L_p (p < LB),
+// planes[LB + 1][b] = T (the block's R total); planes[q] is (WB x nblk).  LB = 8 with a
+// lane per group (full-size sets), LB = 6 with a quad per group (small sets: 4x the
+// blocks, so the CUs fill)
+template <int Q, int LB>
+__global__ void __launch_bounds__((1 << LB) * Q)
 msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, uint32_t nblk,
                         G1xyzz* __restrict__ planes) {
-  __shared__ G1xyzz shT[BP], shS[BP];
+  constexpr uint32_t BPL = 1u << LB;
+  __shared__ G1xyzz shT[BPL], shS[BPL];
   const uint32_t w = blockIdx.y, e = threadIdx.x / Q;
   const bool lead = (threadIdx.x % Q) == 0;
-  const uint32_t g = blockIdx.x * BP + e;
+  const uint32_t g = blockIdx.x * BPL + e;
   const size_t ps = (size_t)gridDim.y * nblk;  // stride between planes
   const G1xyzz* b = B + (size_t)w * NB;
   G1xyzz racc = G1xyzz::identity(), sacc = G1xyzz::identity();
@@ -775,10 +777,10 @@ msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, 
     shS[e] = sacc;
   }
   __syncthreads();
-  // the R tree and a plain S tree side by side: elements [0, 2^(7-k)(k+1)) fold R at level
-  // k, the next 2^(7-k) fold S
-  for (int k = 0; k < 8; k++) {
-    const uint32_t per = (uint32_t)k + 1, pairs = 1u << (7 - k);
+  // the R tree and a plain S tree side by side: elements [0, 2^(LB-1-k)(k+1)) fold R at
+  // level k, the next 2^(LB-1-k) fold S
+  for (int k = 0; k < LB; k++) {
+    const uint32_t per = (uint32_t)k + 1, pairs = 1u << (LB - 1 - k);
     if (e < pairs * per) {
       const uint32_t j = e / per, i = e % per;
       const uint32_t dst = (j << (k + 1)) + (i == 0 ? 0u : (1u << (i - 1))), src = dst + (1u << k);
@@ -791,30 +793,34 @@ msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, 
     }
     __syncthreads();
   }
-  if (lead && e < 10) {
-    const G1xyzz v = e == 0 ? shS[0] : (e < 9 ? shT[1u << (e - 1)] : shT[0]);
+  if (lead && e < LB + 2) {
+    const G1xyzz v = e == 0 ? shS[0] : (e <= LB ? shT[1u << (e - 1)] : shT[0]);
     planes[e * ps + (size_t)w * nblk + blockIdx.x] = v;
   }
 }
 
-// levels B and C, one launch: block q < 9 sums plane q over the nblk blocks; block 9
-// folds the totals T by block index (nblk <= BP) -- mid[q' * WB + w], q' < 17: 0 = sum S,
-// 1 + b = U_b (b < 16).  The last of a set's 10 blocks to finish (device-scope counter,
-// zeroed by the host) then scales U_b by 2^(b + e0), one quad per plane, and sums.
-__global__ void __launch_bounds__(4 * BP)
-msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int e0, G1xyzz* __restrict__ mid,
+// levels B and C, one launch (LB + 2 blocks per set): block q <= LB sums plane q over the
+// nblk blocks; block LB + 1 folds the totals T by block index (nblk <= 2^RPK_MAX) --
+// mid[q' * WB + w]: 0 = sum S, 1 + b = U_b (b < LB + K).  The last of a set's blocks to
+// finish (device-scope counter, zeroed by the host) then scales U_b by 2^(b + e0), one
+// quad per plane, and sums.
+static constexpr int RPK_MAX = 9;  // block-index planes
+__global__ void __launch_bounds__(1024)
+msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, int e0, G1xyzz* __restrict__ mid,
                       uint32_t* __restrict__ done, G1xyzz* __restrict__ windows) {
-  __shared__ G1xyzz sh[BP];
+  __shared__ G1xyzz sh[1 << RPK_MAX];
   __shared__ uint32_t last;
   const uint32_t q = blockIdx.x, w = blockIdx.y, e = threadIdx.x >> 2, WB = gridDim.y;
   const bool lead = (threadIdx.x & 3) == 0;
   const G1xyzz* in = planes + (size_t)q * WB * nblk + (size_t)w * nblk;
-  if (q < 9) {
+  int K = 0;
+  while ((1u << K) < nblk) K++;
+  if (q <= (uint32_t)LB) {
     G1xyzz acc = G1xyzz::identity();
-    for (uint32_t i = e; i < nblk; i += BP) acc = xyzz_add_q4(acc, in[i]);
+    for (uint32_t i = e; i < nblk; i += 256) acc = xyzz_add_q4(acc, in[i]);
     if (lead) sh[e] = acc;
     __syncthreads();
-    for (uint32_t h = BP / 2; h > 0; h >>= 1) {
+    for (uint32_t h = 128; h > 0; h >>= 1) {
       if (e < h) {
         const G1xyzz v = xyzz_add_q4(sh[e], sh[e + h]);
         if (lead) sh[e] = v;
@@ -823,26 +829,26 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int e0, 
     }
     if (threadIdx.x == 0) mid[(size_t)q * WB + w] = sh[0];
   } else {
-    int K = 0;
-    while ((1u << K) < nblk) K++;
-    if (lead) sh[e] = e < nblk ? in[e] : G1xyzz::identity();
+    for (uint32_t i = e; i < (1u << K); i += 256)
+      if (lead) sh[i] = i < nblk ? in[i] : G1xyzz::identity();
     __syncthreads();
     plane_fold<4>(sh, K, e, lead);
-    if (lead && e < 8) mid[(size_t)(9 + e) * WB + w] = e < (uint32_t)K ? sh[1u << e] : G1xyzz::identity();
+    if (lead && e < (uint32_t)K) mid[(size_t)(1 + LB + e) * WB + w] = sh[1u << e];
   }
   __syncthreads();  // this block's outputs are written
   if (threadIdx.x == 0) {
     __threadfence();
-    last = atomicAdd(&done[w], 1u) == 9u;
+    last = atomicAdd(&done[w], 1u) == (uint32_t)LB + 1u;
   }
   __syncthreads();
   if (!last) return;
   __threadfence();
+  const uint32_t np = (uint32_t)(LB + K);  // planes (<= 17)
   G1xyzz x = G1xyzz::identity();
-  if (e < 16) {
+  if (e < np) {
     x = mid[(size_t)(1 + e) * WB + w];
     for (int i = 0; i < (int)e + e0; i++) x = xyzz_dbl_q4(x);
-  } else if (e == 16) {
+  } else if (e == np) {
     x = mid[w];
   }
   if (lead && e < 32) sh[e] = x;
@@ -1078,11 +1084,11 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   }();
   const bool red_q4 = (size_t)m1 * WB <= q4_max;
   const uint32_t nblk = red_q4 ? (m1 + Q4_GROUPS - 1) / Q4_GROUPS : (m1 + MSM_THREADS - 1) / MSM_THREADS;
-  const uint32_t nblk_p = (m1 + BP - 1) / BP;  // plane kernels' blocks
-  // planes where the groups fill the SIMDs (2^21-2^22-point MSMs at c = 20); small MSMs
-  // keep the quad-cooperative rscale scheme, whose 64-group blocks spread over more CUs
-  // (2^19 points: reduction 0.40 vs 0.54 ms with 256-group plane blocks)
-  const bool red_plane = !red_group && !red_q4 && nblk_p <= BP;
+  const int plane_lb = red_q4 ? 6 : 8;  // log2 groups per plane block
+  const uint32_t nblk_p = (m1 + (1u << plane_lb) - 1) >> plane_lb;  // plane kernels' blocks
+  // bit planes unless the block index needs more than RPK_MAX bits (sets of > 2^17
+  // groups, e.g. c = 22): those keep the rscale scheme
+  const bool red_plane = !red_group && nblk_p <= (1u << RPK_MAX);
   const WsPlan wp = ws_plan(NB);
   if (red_split && (wp.nv2v > 64 || wp.nu2v > 64 || wp.nv2u > 64 || wp.nu2u > 64)) return hipErrorInvalidValue;
   // grow-only workspace: MSMs of slightly different shapes (e.g. n and n - 1 points, so
@@ -1099,7 +1105,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
                          {&ws->item_bucket, icap * sizeof(MsmBigItem)},  // big-bucket items
                          {&ws->partials, 2 * nchunks * sizeof(G1xyzz)},  // boundary slots
                          {&ws->buckets, (size_t)nbt * sizeof(G1xyzz)},
-                         {&ws->segs, std::max<size_t>(wp.per_set, (size_t)2 * m1 + nblk + 10 * (size_t)nblk_p + 17) *
+                         {&ws->segs, std::max<size_t>(wp.per_set, (size_t)2 * m1 + nblk + 10 * (size_t)nblk_p + 32) *
                                          WB * sizeof(G1xyzz)},
                          {&ws->windows, (size_t)(W > WB ? W : WB) * sizeof(G1xyzz)},
                          {&ws->result, 16},                              // [0] items, [1] multi-item buckets
@@ -1212,18 +1218,18 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   if (!red_split) {
     if (red_plane) {  // bit planes (6a')
       G1xyzz* planes = rP;
-      G1xyzz* mid = planes + (size_t)10 * WB * nblk_p;
+      G1xyzz* mid = planes + (size_t)(plane_lb + 2) * WB * nblk_p;
       int e0 = 0;
       while ((1 << e0) < RG) e0++;
       H2G_TRY(hipMemsetAsync(rdone, 0, (size_t)WB * 4, st));
       if (red_q4)
-        hipLaunchKernelGGL(msm_rgroup_plane_kernel<4>, dim3(nblk_p, (unsigned)WB), dim3(4 * BP), 0, st,
+        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 6>), dim3(nblk_p, (unsigned)WB), dim3(4 << 6), 0, st,
                            (const G1xyzz*)buckets, NB, m1, nblk_p, planes);
       else
-        hipLaunchKernelGGL(msm_rgroup_plane_kernel<1>, dim3(nblk_p, (unsigned)WB), dim3(BP), 0, st,
+        hipLaunchKernelGGL((msm_rgroup_plane_kernel<1, 8>), dim3(nblk_p, (unsigned)WB), dim3(1 << 8), 0, st,
                            (const G1xyzz*)buckets, NB, m1, nblk_p, planes);
-      hipLaunchKernelGGL(msm_rplane_mid_kernel, dim3(10, (unsigned)WB), dim3(4 * BP), 0, st, (const G1xyzz*)planes,
-                         nblk_p, e0, mid, rdone, (G1xyzz*)ws->windows);
+      hipLaunchKernelGGL(msm_rplane_mid_kernel, dim3((unsigned)plane_lb + 2, (unsigned)WB), dim3(1024), 0, st,
+                         (const G1xyzz*)planes, nblk_p, plane_lb, e0, mid, rdone, (G1xyzz*)ws->windows);
     } else {
       if (red_q4)
         hipLaunchKernelGGL(msm_rgroup_q4_kernel, dim3((unsigned)(((size_t)m1 * 4 + T - 1) / T), (unsigned)WB),
