@@ -232,7 +232,13 @@ def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note
     achieved = (points_per_launch * MSM_BYTES_PER_POINT) / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
     c = window_bits or fixed_c(points_per_launch)
     W = (255 + c - 1) // c
-    modmul_rate = (points_per_launch * W * MADD_MODMUL) / (acc_ms * 1e-3) if acc_ms > 0 else None
+    # mixed additions per MSM: the device's count of sorted entries (nonzero signed digits)
+    # when recorded -- W x n overstates it for scalars with zero digits (small witness
+    # values, e.g. the keccak-style circuit's nibbles)
+    entries = (union or {}).get("entries")
+    madds = entries / max(calls, 1) if entries else points_per_launch * W
+    madd_source = "counted (sorted entries)" if entries else f"{W} windows x n"
+    modmul_rate = (madds * MADD_MODMUL) / (acc_ms * 1e-3) if acc_ms > 0 else None
     out = {
         "bound": "valu",
         "kernel": "msm_acc_kernel (Pippenger bucket accumulation)",
@@ -252,13 +258,14 @@ def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note
                  "peak_microbench": MODMUL_PEAK_MICROBENCH / 1e9, "peak_issue_model": round(MODMUL_PEAK_ISSUE / 1e9, 1),
                  "frac_microbench": round(modmul_rate / MODMUL_PEAK_MICROBENCH, 4) if modmul_rate else None,
                  "frac_issue_model": round(modmul_rate / MODMUL_PEAK_ISSUE, 4) if modmul_rate else None,
-                 "per_point": f"{W} windows x 1 XYZZ mixed add (8M + 2S = {MADD_MODMUL} modmul)"},
+                 "per_point": f"{W} windows x 1 XYZZ mixed add (8M + 2S = {MADD_MODMUL} modmul)",
+                 "madds_per_launch": round(madds), "madds": madd_source},
         "window_bits": c,
     }
     if union and union.get("accumulate", 0) > 0:
         # MSMs on the two MSM streams overlap each other, so a launch's duration counts the
         # chip's time twice while they do: the chip-level rate is the work over the busy time
-        agg = calls * points_per_launch * W * MADD_MODMUL / (union["accumulate"] * 1e-3)
+        agg = calls * madds * MADD_MODMUL / (union["accumulate"] * 1e-3)
         out["valu"].update({"aggregate": round(agg / 1e9, 2), "aggregate_frac_microbench":
                             round(agg / MODMUL_PEAK_MICROBENCH, 4),
                             "aggregate_note": "all launches' modmuls / union of their accumulate intervals"})
@@ -634,7 +641,8 @@ def run_msm(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                                "fixed-base windows via the base descriptor",
                    "points_per_gpu": n, "window_bits": c, "windows": (255 + c - 1) // c,
                    "parallelism": f"point-slab shard x{world} + RCCL all_gather of partials"},
-        "roofline": roofline_from_phases(calls, phases, n, traffic, traffic_note),
+        "roofline": roofline_from_phases(calls, phases, n, traffic, traffic_note,
+                                         union={"entries": union.get("entries")}),
         "phases_ms": {kk: round(v / max(calls, 1), 4) for kk, v in phases.items()},
     }
 

@@ -146,6 +146,10 @@ int h2g_event_elapsed_ms(void* start, void* stop, float* ms);
  * MSMs on the two MSM streams overlap, so work / union is the aggregate rate. */
 int h2g_profile_enable(int on);
 int h2g_profile_msm_collect(float* ms, int max_phases, int* n_phases, int* calls);
+/* the profiled MSMs' sorted entries (nonzero signed digits = mixed additions in the
+ * accumulation) summed, before collect() resets them; *uncounted = MSMs past the
+ * recorder's capacity (may be NULL) */
+int h2g_profile_msm_entries(uint64_t* total, int* uncounted);
 
 /* ---- host-side point helpers (used to combine per-GPU MSM partials) -------- */
 int h2g_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);

@@ -339,3 +339,29 @@ def test_msm_equal_scalars_srs_identity(k):
         h2g.descriptor_free(h)
         d_sc.close()
         bases_dev.close()
+
+
+def test_msm_profile_counts_sorted_entries():
+    """h2g_profile_msm_entries: the accumulation's mixed additions are the nonzero signed
+    digits -- n for scalars equal to 1 (one digit each), 0 for zeros, W n for random
+    scalars up to the rare zero digit (what the bench's modmul rates divide by)."""
+    r = rng(77)
+    n = 4096
+    s = O.random_fr(r, 1)[0]
+    bases_dev = _srs(n, s)
+    h = h2g.base_descriptor_dev(bases_dev.ptr, n, 0)
+    try:
+        import bn254_ref as B
+        one = np.tile(np.asarray(B.fr_mont_limbs(1), dtype=np.uint64), (n, 1))
+        cases = ((one, lambda e: e == n), (np.zeros((n, 4), dtype=np.uint64), lambda e: e == 0))
+        for sc, ok in cases:
+            d_sc = h2g.DevBuf.from_array(sc)
+            h2g.profile_enable(True)
+            h2g.msm_with_cached_base_dev(d_sc.ptr, n, h, 0)
+            h2g.profile_enable(False)
+            calls, _, union = h2g.profile_msm_collect(with_union=True)
+            assert calls == 1 and ok(union["entries"]), union
+            d_sc.close()
+    finally:
+        h2g.descriptor_free(h)
+        bases_dev.close()

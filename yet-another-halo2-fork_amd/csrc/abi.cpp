@@ -37,6 +37,16 @@ std::recursive_mutex g_mu;
 std::vector<std::unique_ptr<Device>> g_devs;
 bool g_profile = false;
 std::vector<MsmPhaseEvents> g_msm_prof;
+// pinned words receiving each profiled MSM's sorted-entry count (nonzero digits); beyond
+// the capacity an MSM goes uncounted and h2g_profile_msm_entries reports it
+static constexpr size_t PROF_ENTRY_CAP = 1 << 16;
+uint32_t* g_prof_entries = nullptr;
+int prof_entries_slot(MsmPhaseEvents* ev) {
+  if (!g_prof_entries) HIPCHK(hipHostMalloc((void**)&g_prof_entries, PROF_ENTRY_CAP * 4, hipHostMallocDefault));
+  ev->entries = g_msm_prof.size() < PROF_ENTRY_CAP ? g_prof_entries + g_msm_prof.size() : nullptr;
+  if (ev->entries) *ev->entries = 0;
+  return H2G_OK;
+}
 int g_cur = 0;
 std::map<uint64_t, Descriptor> g_desc;
 std::map<uint64_t, std::unique_ptr<Domain>> g_dom;
@@ -125,6 +135,7 @@ int msm_dev_impl(Device* d, const void* sc, const void* bs, size_t n, int c, voi
   if (g_profile) {
     MsmPhaseEvents ev;
     for (auto& e : ev.ev) HIPCHK(hipEventCreate(&e));
+    RCCHK(prof_entries_slot(&ev));
     g_msm_prof.push_back(ev);
     pe = &g_msm_prof.back();
   }
@@ -169,6 +180,7 @@ int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_
   if (g_profile) {
     MsmPhaseEvents ev;
     for (auto& e : ev.ev) HIPCHK(hipEventCreate(&e));
+    RCCHK(prof_entries_slot(&ev));
     g_msm_prof.push_back(ev);
     pe = &g_msm_prof.back();
   }
@@ -233,6 +245,7 @@ int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFi
   if (g_profile && n > 0) {
     MsmPhaseEvents ev;
     for (auto& e : ev.ev) HIPCHK(hipEventCreate(&e));
+    RCCHK(prof_entries_slot(&ev));
     ev.msms = nb;
     g_msm_prof.push_back(ev);
     pe = &g_msm_prof.back();
@@ -939,6 +952,21 @@ int h2g_event_elapsed_ms(void* a, void* b, float* ms) {
 int h2g_profile_enable(int on) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   g_profile = on != 0;
+  return H2G_OK;
+}
+
+int h2g_profile_msm_entries(uint64_t* total, int* uncounted) {
+  NEED_DEV();
+  if (!total) return fail(H2G_ERR_ARG, "profile_msm_entries: null total");
+  uint64_t t = 0;
+  int un = 0;
+  for (auto& pe : g_msm_prof) {
+    HIPCHK(hipEventSynchronize(pe.ev[MSM_NPHASES]));
+    if (pe.entries) t += *pe.entries;
+    else un++;
+  }
+  *total = t;
+  if (uncounted) *uncounted = un;
   return H2G_OK;
 }
 

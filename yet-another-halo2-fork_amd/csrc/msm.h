@@ -40,6 +40,7 @@ static constexpr int MSM_NPHASES = 6;
 struct MsmPhaseEvents {
   hipEvent_t ev[MSM_NPHASES + 1];
   int msms = 1;  // MSMs the timed pipeline served (a batch counts each)
+  uint32_t* entries = nullptr;  // pinned: receives the sorted-entry (nonzero digit) count
 };
 
 // Scalar vectors of a batch of MSMs (kernel argument by value).

@@ -1175,6 +1175,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     H2G_TRY(hipGetLastError());
   }
   H2G_PHASE(1);
+  if (prof && prof->entries) H2G_TRY(hipMemcpyAsync(prof->entries, d_total, 4, hipMemcpyDeviceToHost, st));
   {  // round 2: keys inside the coarse bins
     const unsigned tiles = (unsigned)((total + FTILE - 1) / FTILE);
     H2G_TRY(hipMemsetAsync(kcount, 0, (size_t)nbt * 4, st));

@@ -78,6 +78,7 @@ _SIGS = {
     "h2g_g1_add_affine": ([U64P, U64P, U64P], I32),
     "h2g_profile_enable": ([I32], I32),
     "h2g_profile_msm_collect": ([ctypes.POINTER(ctypes.c_float), I32, ctypes.POINTER(I32), ctypes.POINTER(I32)], I32),
+    "h2g_profile_msm_entries": ([ctypes.POINTER(U64), ctypes.POINTER(I32)], I32),
     "h2g_params_create": ([U32, U64P, U64P, ctypes.POINTER(U64)], I32),
     "h2g_params_setup": ([U32, U64P, ctypes.POINTER(U64)], I32),
     "h2g_params_export": ([U64, U64P, U64P], I32),
@@ -408,11 +409,14 @@ def profile_msm_collect(with_union=False):
     intervals) of the overlapping MSMs' accumulate phases and of the whole MSMs."""
     ms = (ctypes.c_float * 8)()
     npz, calls = I32(0), I32(0)
+    ent, unc = U64(0), I32(0)
+    check(lib().h2g_profile_msm_entries(ctypes.byref(ent), ctypes.byref(unc)))
     check(lib().h2g_profile_msm_collect(ms, 8, ctypes.byref(npz), ctypes.byref(calls)))
     phases = {MSM_PHASES[i]: ms[i] for i in range(npz.value)}
     if not with_union:
         return calls.value, phases
-    return calls.value, phases, {"accumulate": ms[npz.value], "msm": ms[npz.value + 1]}
+    return calls.value, phases, {"accumulate": ms[npz.value], "msm": ms[npz.value + 1],
+                                 "entries": ent.value if unc.value == 0 else None}
 
 
 class Timer:
