@@ -1138,7 +1138,16 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   // bucket partition geometry: keys < nbt, fine bits fb, coarse bins nbt >> fb
   int key_bits = 1;
   while ((1ull << key_bits) < (uint64_t)nbt) key_bits++;
-  int fb = key_bits < FB_MAX ? key_bits : FB_MAX;
+  // fine bits (the fine pass's fan-out per 4096-entry tile; H2G_MSM_FB for A/B runs): 10
+  // -- 2x the coarse bins of 11 but half the per-tile key runs and global cursor atomics
+  // of the fine scatter; interleaved on one box the k = 22 proof took 86.5-86.8 ms vs
+  // 86.8-87.3 ms at 11, the 2^22 MSM 6.94-6.97 vs 6.98-6.99 ms (8, 9: slower coarse pass)
+  static const int fb_max = [] {
+    const char* e = getenv("H2G_MSM_FB");
+    const int v = e ? atoi(e) : 10;
+    return v >= 4 && v <= FB_MAX ? v : 10;
+  }();
+  int fb = key_bits < fb_max ? key_bits : fb_max;
   while (fb < 13 && (((uint64_t)nbt + (1ull << fb) - 1) >> fb) > COARSE_MAX) fb++;
   const uint32_t nf = 1u << fb;
   const uint32_t ncoarse = (uint32_t)((nbt + nf - 1) >> fb);
