@@ -1065,7 +1065,11 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   if (total >= 0x80000000ull) return hipErrorInvalidValue;  // u32 positions in the sorted array
   // buckets most windows can reach (fixed-base: 2^(base width - 1) of the balanced widths)
   const size_t nb_eff = (size_t)WB << ((fixed ? 255 / W : c) - 1);
-  const uint32_t L = item_len > 0 ? item_len : msm_chunk_len(total, nb_eff);
+  static const uint32_t chunk_env = [] {  // H2G_MSM_CHUNK: fixed chunk length (A/B runs)
+    const char* e = getenv("H2G_MSM_CHUNK");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
+  const uint32_t L = item_len > 0 ? item_len : (chunk_env ? chunk_env : msm_chunk_len(total, nb_eff));
   const size_t nchunks = (total + L - 1) / L;
   static const bool red_split = [] {
     const char* e = getenv("H2G_MSM_RED");
