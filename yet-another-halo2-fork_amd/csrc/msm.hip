@@ -85,8 +85,8 @@ __device__ __forceinline__ G1Affine ld_aff(const G1Affine* p) {
 #ifndef H2G_MSM_PT
 #define H2G_MSM_PT 512
 #endif
-#ifndef H2G_MSM_FPER
-#define H2G_MSM_FPER 16
+#ifndef H2G_MSM_FPER  // entries per fine-kernel thread: 8 (2048-entry tiles) measured best at 10 fine bits
+#define H2G_MSM_FPER 8
 #endif
 static constexpr int PT = H2G_MSM_PT;      // threads of the coarse kernels (one scalar each)
 static constexpr int PWG = 16;             // windows per coarse-kernel thread (grid.z groups)
