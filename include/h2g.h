@@ -293,7 +293,8 @@ int h2g_create_proof_phased(uint64_t params, uint64_t pk, const h2g_witness_sour
  *   random_fr : F::random(&mut rng) as 4 Montgomery limbs (the Rust shim calls
  *               Fr::random itself, so the proof does not depend on how halo2curves
  *               consumes the RNG); NULL = fill_bytes(64) read as from_uniform_bytes
- *   fill_bytes: RngCore::fill_bytes(out[0..len])
+ *   fill_bytes: RngCore::fill_bytes(out[0..len]); required, even with random_fr (the
+ *               vanishing seeds are fill_bytes draws) -- NULL fails the call up front
  * Nonzero from either fails the proof with H2G_ERR_ARG. */
 typedef struct {
   void* ctx;
@@ -386,8 +387,17 @@ int h2g_comm_destroy(void);
  * h2g_params_set_slab) of every commitment MSM from its own copy of the scalars, and the
  * 64-B partials are all-gathered and summed in rank order, so every rank writes the same
  * proof bytes as one GPU would and no scalars cross the links.
- *   allgather: in = this rank's partial (8 u64 affine limbs, then 1 if the identity),
- *              out = world x 9 u64 in rank order; 0 on success
+ *   allgather: in = this rank's H2G_SPMD_WORDS words: its partial (8 u64 affine limbs,
+ *              then 1 if the identity) and 4 words of consistency digest (a Blake2b of
+ *              the transcript state and of every RNG draw so far); out = world x
+ *              H2G_SPMD_WORDS u64 in rank order; 0 on success.  Every rank compares the
+ *              digests and fails the proof (H2G_ERR_STATE) if any rank's differ: ranks
+ *              fed different witnesses, instances or RNG draws would otherwise sum slabs
+ *              of different polynomials into one invalid proof without an error (a
+ *              diverged witness shows up at the latest when the evaluations enter the
+ *              transcript, before the multi-open commitments are gathered). */
+#define H2G_SPMD_WORDS 13
+/*
  * The host transport (callbacks) or the library's RCCL all-gather (h2g_comm_spmd_install,
  * after h2g_comm_init on every rank).  Installing one sharding mode removes the other. */
 typedef struct {
@@ -402,11 +412,20 @@ typedef struct {
    * h evaluations (n Fr, device memory) are broadcast from their owner t mod world:
    * bcast(ctx, d_buf, bytes, root) in place, complete on return */
   int (*bcast)(void* ctx, void* d_buf, size_t bytes, int root);
+  /* optional -- NULL replicates the multi-open tail.  Otherwise the evaluations and the
+   * SHPLONK multi-open (poly/kzg/multiopen/shplonk/prover.rs:121-305) run on coefficient
+   * slabs: rank r evaluates, combines and divides only coefficients [P r / world,
+   * P (r + 1) / world) of each polynomial -- the points its MSM slabs cover -- and the
+   * few scalars that join the slabs (partial evaluations, the kate divisions' carries
+   * between slabs) are all-gathered: allgather_host(ctx, in, bytes, out) with `bytes`
+   * host bytes from this rank, out = world x bytes in rank order, complete on return */
+  int (*allgather_host)(void* ctx, const void* in, size_t bytes, void* out);
 } h2g_spmd_transport;
 /* install (world >= 2) or remove (NULL or world <= 1) */
 int h2g_set_spmd_transport(const h2g_spmd_transport* t);
 /* split_subcosets: 1 divides the extended domain's sub-cosets over the ranks (bcast over
- * the communicator), 0 replicates that work */
+ * the communicator), 0 replicates that work; the multi-open tail always runs on
+ * coefficient slabs (allgather_host over the communicator) */
 int h2g_comm_spmd_install(int split_subcosets);
 int h2g_comm_spmd_uninstall(void);
 

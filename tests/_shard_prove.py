@@ -30,10 +30,23 @@ CASES = {
     "keccak_k12": lambda: hc.keccak_style(12, words=16, seed=9),
     "c3_k14": lambda: hc.synthetic_c3(14, h2g.DeviceOps, seed=4),
     "challenge_k9": lambda: hc.challenge_circuit(9, seed=9, extended=True),  # phases: witness source
+    # BASELINE sizes: configs[3] (C3 at k = 22) and configs[4] (the keccak-style circuit at k = 18)
+    "c3_k22": lambda: hc.synthetic_c3(22, h2g.DeviceOps, seed=22),
+    "keccak_k18": lambda: hc.keccak_style(18, words=16),
+    # two MyCircuit instances with different inputs (witnesses, instances) in one proof
+    "multi_my_k6": lambda: _multi_my(),
 }
 
 
+def _multi_my():
+    circ, w0, f0 = hc.my_circuit(6, input_value=42)
+    _, w1, f1 = hc.my_circuit(6, input_value=1000)
+    return circ, [w0, w1], [f0, f1], "multi"
+
+
 def _prove(pk, case, **kw):
+    if len(case) == 4:  # (circuit, witnesses, fills, "multi"): several circuits in one proof
+        return pk.create_proof_multi(case[1], fills=case[2], **kw)
     if len(case) == 3:  # (circuit, instance witness, fill): Prover::commit_phase per phase
         return pk.create_proof_phased(case[2], case[1], **kw)[0]
     return pk.create_proof(case[1], **kw)
@@ -48,6 +61,10 @@ def main():
                     help="slab: rank 0 proves, peers serve slabs; spmd: every rank proves its slab")
     ap.add_argument("--no-subcosets", action="store_true",
                     help="spmd: replicate the extended-domain work instead of splitting the sub-cosets")
+    ap.add_argument("--diverge", action="store_true",
+                    help="spmd: the last rank proves with another RNG seed; every rank must refuse the proof")
+    ap.add_argument("--one-variant", action="store_true",
+                    help="prove each case once (default seed) instead of twice (large cases)")
     ap.add_argument("cases", nargs="+")
     args = ap.parse_args()
     rank = int(os.environ["RANK"])
@@ -128,6 +145,7 @@ def spmd_main(args, rank, world, native):
     every MSM and the all-gathered partials; all ranks must print identical bytes"""
     import hashlib
     results = {}
+    variants = [{}] if args.one_variant else [{}, {"seed": bytes(range(32)), "vanishing_threads": 3}]
     for name in args.cases:
         case = CASES[name]()
         circ = case[0]
@@ -135,15 +153,37 @@ def spmd_main(args, rank, world, native):
         P = 1 << circ.k
         params.set_slab(*D.slab(P, world, rank))
         pk = h2g.ProvingKey(params, circ)
-        want = [_prove(pk, case), _prove(pk, case, seed=bytes(range(32)), vanishing_threads=3)]
+        want = [_prove(pk, case, **kw) for kw in variants]
         g = None
         if native:
             h2g.comm_spmd_install(not args.no_subcosets)
         else:
             g = D.SpmdGather(dist, subcosets=not args.no_subcosets)
             g.install()
+        if args.diverge:  # the last rank draws other randomness: the digest check must catch it
+            try:
+                seed = bytes([9] * 32) if rank == world - 1 else bytes([7] * 32)
+                _prove(pk, case, seed=seed)
+                err = ""
+            except h2g.H2GError as e:
+                err = str(e)
+            finally:
+                if native:
+                    h2g.comm_spmd_uninstall()
+                else:
+                    D.SpmdGather.uninstall()
+            ok = torch.tensor([1 if "diverged" in err else 0], dtype=torch.int64)
+            if args.backend == "nccl":
+                ok = ok.cuda()
+            allok = [torch.empty_like(ok) for _ in range(world)]
+            dist.all_gather(allok, ok)
+            results[name] = {"refused_all": all(int(a.item()) == 1 for a in allok), "error": err[:200]}
+            pk.close()
+            params.close()
+            dist.barrier()
+            continue
         try:
-            got = [_prove(pk, case), _prove(pk, case, seed=bytes(range(32)), vanishing_threads=3)]
+            got = [_prove(pk, case, **kw) for kw in variants]
         finally:
             if native:
                 h2g.comm_spmd_uninstall()

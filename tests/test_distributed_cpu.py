@@ -140,9 +140,13 @@ def _spmd_worker(rank, world, port, jobs, bases, q):
         for seq, (base_set, sc) in enumerate(jobs):
             lo, hi = D.slab(len(sc), world, rank, P)
             own = O.msm_best(sc[lo:hi], bases[base_set][lo:hi], 1) if hi > lo else np.zeros(8, np.uint64)
-            mine = np.concatenate([own, np.array([0 if own.any() else 1], np.uint64)])
+            # payload = partial, identity flag, 4 digest words (h2g.SPMD_WORDS, H2G_SPMD_WORDS)
+            digest = np.array([seq, 1, 2, 3], np.uint64)
+            mine = np.concatenate([own, np.array([0 if own.any() else 1], np.uint64), digest])
+            assert len(mine) == h2g.SPMD_WORDS
             allp = g.allgather(seq, mine)
-            assert allp.shape == (world, 9)
+            assert allp.shape == (world, h2g.SPMD_WORDS)
+            assert all(np.array_equal(allp[r, 9:], digest) for r in range(world))
             assert np.array_equal(allp[rank], mine)
             total = np.zeros(8, np.uint64)
             for r in range(world):

@@ -3,9 +3,10 @@
   * C3 at k = 20 (configs[2]): device proof bytes == the oracle's create_proof bytes (C
     restatement of halo2_backend/src/plonk/prover.rs), on the device-generated SRS, whose
     entries are spot-checked against [s^i]G and [L_i(s)]G computed here.
-  * C3 at k = 22 (the bench proof, configs[3]) and the keccak-style circuit (32 advice
-    columns, 16 lookups) at k = 18 (configs[4]): the device proof is accepted by the
-    independent Python verifier (oracle/py/verifier.py, halo2_backend/src/plonk/verifier.rs)
+  * C3 at k = 22 (the bench proof, configs[3]), C3 at k = 24 (north_star's k-range top) and
+    the keccak-style circuit (32 advice columns, 16 lookups) at k = 18 (configs[4]): device
+    proof bytes == the oracle's, and the device proof is accepted by the independent Python
+    verifier (oracle/py/verifier.py, halo2_backend/src/plonk/verifier.rs)
     and a tampered proof is rejected -- the prove -> verify relation of
     halo2_proofs/tests/plonk_api.rs:580-640.  The verifying key is computed twice: by the
     device keygen (h2g_pk_vk_commitments) and on the CPU from the oracle keygen's sigma
@@ -25,7 +26,7 @@ from bn254_ref import G1_GEN, R, g1_mul
 
 pytestmark = pytest.mark.gpu
 
-THREADS = max(1, min(16, os.cpu_count() or 1))
+THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -90,9 +91,10 @@ def test_c3_k20_bytes_match_oracle():
 
 
 @pytest.mark.timeout(900)
-def test_c3_k22_proof_verifies():
-    """the bench proof (C3, k = 22): accepted by the verifier, tampered copies rejected,
-    identical across repeated proofs with the same key"""
+def test_c3_k22_proof_bytes_match_oracle_and_verify():
+    """the bench proof (C3, k = 22, BASELINE configs[3]): device proof bytes == the oracle's
+    create_proof bytes (same circuit, witness, SRS and RNG seed), accepted by the verifier,
+    tampered copies rejected, identical across repeated proofs with the same key"""
     k = 22
     s_int = _s(k)
     circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=22)
@@ -102,6 +104,7 @@ def test_c3_k22_proof_verifies():
     assert pk.create_proof(wit) == proof
     vk = _dev_vk(pk)
     g, gl = params.export()
+    assert proof == O.create_proof(circ, wit, g, gl, threads=THREADS)
     assert vk == O.vk_commitments(circ, wit, s_int, g, gl, threads=THREADS)
     del g, gl
     assert V.verify(circ, [], proof, s_int, vk=vk)
@@ -117,9 +120,9 @@ def test_c3_k22_proof_verifies():
 
 
 @pytest.mark.timeout(900)
-def test_keccak_style_k18_proof_verifies():
+def test_keccak_style_k18_proof_bytes_match_oracle_and_verify():
     """BASELINE configs[4]'s circuit shape at its size: 32 advice columns, 16 three-column
-    lookups, degree 5 (extended domain 4n), at k = 18"""
+    lookups, degree 5 (extended domain 4n), at k = 18; device bytes == oracle bytes"""
     k = 18
     s_int = _s(k)
     circ, wit = hc.keccak_style(k, words=16)
@@ -130,6 +133,7 @@ def test_keccak_style_k18_proof_verifies():
     assert pk.create_proof(wit) == proof
     vk = _dev_vk(pk)
     g, gl = params.export()
+    assert proof == O.create_proof(circ, wit, g, gl, threads=THREADS)
     assert vk == O.vk_commitments(circ, wit, s_int, g, gl, threads=THREADS)
     assert V.verify(circ, [], proof, s_int, vk=vk)
     for at in (5, 32 * 40 + 7, len(proof) - 40):
@@ -138,11 +142,11 @@ def test_keccak_style_k18_proof_verifies():
     params.close()
 
 
-@pytest.mark.timeout(900)
-def test_c3_k24_proof_verifies():
-    """north_star's k-range top (k = 24, extended domain 2^25): the device proof verifies
-    with the device verifying key (which equals the CPU-computed key at k = 18, 20, 22
-    above) and a tampered copy is rejected"""
+@pytest.mark.timeout(1200)
+def test_c3_k24_proof_bytes_match_oracle_and_verify():
+    """north_star's k-range top (k = 24, extended domain 2^25): device bytes == oracle
+    bytes, the proof verifies with the device verifying key (which equals the CPU-computed
+    key at k = 18, 20, 22 above) and a tampered copy is rejected"""
     k = 24
     s_int = _s(k)
     circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=24)
@@ -150,6 +154,9 @@ def test_c3_k24_proof_verifies():
     pk = h2g.ProvingKey(params, circ)
     proof = pk.create_proof(wit)
     assert len(proof) == 864 and pk.create_proof(wit) == proof
+    g, gl = params.export()
+    assert proof == O.create_proof(circ, wit, g, gl, threads=THREADS)
+    del g, gl
     vk = _dev_vk(pk)
     assert V.verify(circ, [], proof, s_int, vk=vk)
     assert _rejects(circ, _tampered(proof, 32 * 11 + 3), s_int, vk)

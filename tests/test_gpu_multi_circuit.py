@@ -61,6 +61,32 @@ def test_two_my_circuits_phases_lookups_shuffles(multiopen):
     params.close()
 
 
+@pytest.mark.parametrize("multiopen", ["shplonk", "gwc"])
+def test_two_my_circuits_distinct_inputs(multiopen):
+    """two circuits with different witnesses and instances (MyCircuit with input 42 and
+    1000): a swapped circuit index -- the instance hashing order, fill(circuit, phase), the
+    lookup index ci * NL + l, the shuffle products' order -- changes the bytes"""
+    circ, w0, f0 = hc.my_circuit(6, input_value=42)
+    _, w1, f1 = hc.my_circuit(6, input_value=1000)
+    assert not np.array_equal(w0.instance, w1.instance)
+    s, g, gl = O.srs(circ.k)
+    params = h2g.Params(circ.k, g, gl)
+    pk = h2g.ProvingKey(params, circ)
+    want = O.create_proof(circ, w0, g, gl, wits=[w0, w1], fills=[f0, f1], multiopen=multiopen)
+    got = pk.create_proof_multi([w0, w1], fills=[f0, f1], multiopen=multiopen)
+    assert got == want
+    assert got != pk.create_proof_multi([w1, w0], fills=[f1, f0], multiopen=multiopen)
+    inst = [_instances(circ, w0), _instances(circ, w1)]
+    assert V.verify(circ, None, got, s, instances_multi=inst, multiopen=multiopen)
+    try:
+        swapped = V.verify(circ, None, got, s, instances_multi=inst[::-1], multiopen=multiopen)
+    except V.VerifyError:
+        swapped = False
+    assert not swapped
+    pk.close()
+    params.close()
+
+
 def test_one_ng_my_circuit_matches_oracle():
     """frontend_backend_split.rs:513-560: OneNg sets up the SRS (s = Fr::random(OneNg)) and
     drives create_proof; device bytes == oracle bytes, with F::random drawn through

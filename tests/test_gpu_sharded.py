@@ -27,13 +27,13 @@ def _gpus():
     return torch.cuda.device_count()
 
 
-def _run(world, cases, backend="gloo", transport="torch", mode="slab", extra=()):
+def _run(world, cases, backend="gloo", transport="torch", mode="slab", extra=(), timeout=900):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(HERE, "_shard_prove.py"), "--backend", backend, "--transport", transport,
            "--mode", mode] + list(extra) + cases
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("SHARD_RESULT ")]
     assert line, p.stdout[-3000:] + p.stderr[-3000:]
@@ -74,6 +74,40 @@ def test_spmd_proof_two_and_three_ranks():
     res = _run(2, ["lookup_k11", "c3_k14"], mode="spmd", extra=["--no-subcosets"])
     for nm in ("lookup_k11", "c3_k14"):
         assert res[nm]["same"] and res[nm]["same_ranks"] and res[nm]["bcasts"] == 0, (nm, res[nm])
+
+
+def test_spmd_two_circuits_distinct_witnesses():
+    """two MyCircuit instances with different inputs (witnesses and instances), a lookup,
+    a shuffle and a second phase each, in one SPMD proof: every rank == one GPU"""
+    res = _run(2, ["multi_my_k6"], mode="spmd")
+    assert res["multi_my_k6"]["same"] and res["multi_my_k6"]["same_ranks"], res
+
+
+def test_spmd_diverged_ranks_refuse_the_proof():
+    """a rank with other RNG draws: the digest in every all-gather payload makes every rank
+    fail the proof (H2G_ERR_STATE) instead of summing slabs of different polynomials"""
+    res = _run(2, ["simple_k6", "lookup_k11"], mode="spmd", extra=["--diverge"])
+    for nm in ("simple_k6", "lookup_k11"):
+        assert res[nm]["refused_all"], (nm, res[nm])
+
+
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("world", [2, 4])
+def test_spmd_c3_k22_at_size(world):
+    """BASELINE configs[3] at its size: the C3 k = 22 proof with every commitment MSM split
+    into `world` point slabs and the extended domain's sub-cosets divided over the ranks
+    (gloo ranks sharing this box's GPU); every rank's bytes == the single-GPU proof"""
+    res = _run(world, ["c3_k22"], mode="spmd", extra=["--one-variant"], timeout=1100)
+    assert res["c3_k22"]["same"] and res["c3_k22"]["same_ranks"], res
+    assert res["c3_k22"]["gathers"] == 11 and res["c3_k22"]["bcasts"] == 2, res
+
+
+@pytest.mark.timeout(1200)
+def test_spmd_keccak_k18_eight_ranks():
+    """BASELINE configs[4] at its size and GPU count: the keccak-style circuit at k = 18
+    over 8 SPMD ranks (MSM slabs, 4 sub-cosets over the first 4 ranks); bytes == one GPU"""
+    res = _run(8, ["keccak_k18"], mode="spmd", extra=["--one-variant"], timeout=1100)
+    assert res["keccak_k18"]["same"] and res["keccak_k18"]["same_ranks"], res
 
 
 @pytest.mark.parametrize("mode", ["slab", "spmd"])

@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""Per-rank cost of one SPMD proof at world N, measured on ONE GPU.
+
+The driver's 8-GPU node is the only place the SPMD prover runs at N > 1 on RCCL.  This
+tool measures what one rank of an N-rank proof computes: it installs an SPMD transport
+with (world = N, rank = r) whose collectives return at once -- the all-gather hands back
+this rank's own partial and digest for itself and the generator for the peers, broadcasts
+and exchanges are no-ops -- so the rank runs exactly its share of the kernels (its MSM
+slabs, its sub-cosets, its coefficient slabs) and the proof bytes are meaningless.  The
+time per proof of the slowest rank plus a communication model (comm_model below) is the
+predicted N-GPU proof time.
+
+    python tools/spmd_emulate.py --k 22 --world 8 [--ranks 0,1,2] [--workload c3|keccak]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "yet-another-halo2-fork_amd"))
+
+import h2g  # noqa: E402
+import h2g_circuit as hc  # noqa: E402
+import h2g_dist as D  # noqa: E402
+
+FQ_P = 0x30644e72e131a029b85045b68181585d97816a916871ca8d3c208c16d87cfd47
+
+
+def _fq_mont_limbs(v):
+    m = (v << 256) % FQ_P
+    return [(m >> (64 * i)) & (2**64 - 1) for i in range(4)]
+
+
+G1_GEN_MONT = np.array(_fq_mont_limbs(1) + _fq_mont_limbs(2), dtype=np.uint64)  # (1, 2), Montgomery form
+
+
+class FakeCollectives:
+    """world x the rank's own payload; the peers' partials are a fixed nonzero point so
+    the sum never degenerates to the identity (which the transcript refuses)"""
+
+    def __init__(self, world, rank, gen):
+        self.world, self.rank, self.gen = world, rank, gen
+        self.calls = self.bcasts = self.exchanges = 0
+
+    def allgather(self, seq, mine):
+        out = np.tile(mine, (self.world, 1))
+        for r in range(self.world):
+            if r != self.rank:
+                out[r, :8] = self.gen
+                out[r, 8] = 0
+        self.calls += 1
+        return out
+
+    def bcast(self, d_ptr, nbytes, root):
+        self.bcasts += 1
+
+    def allgather_host(self, data):
+        self.exchanges += 1
+        return [data] * self.world
+
+
+def run(args):
+    h2g.init([0])
+    k = args.k
+    if args.workload == "keccak":
+        circ, wit = hc.keccak_style(k, words=16, seed=5)
+    else:
+        circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=3)
+    params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(0x1234567), dtype=np.uint64))
+    gen = G1_GEN_MONT
+    pk = h2g.ProvingKey(params, circ)
+    import torch
+    adv = torch.from_numpy(np.ascontiguousarray(wit.advice).view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    n = 1 << k
+    ranks = [int(r) for r in args.ranks.split(",")] if args.ranks else list(range(args.world))
+    out = {"k": k, "workload": args.workload, "world": args.world, "ranks": {}}
+    single = []
+    for _ in range(args.warmup):
+        pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())
+        single.append(time.perf_counter() - t0)
+    out["single_gpu_ms"] = round(1e3 * sorted(single)[len(single) // 2], 3)
+    for r in ranks:
+        if args.world > 1:
+            params.set_slab(*D.slab(n, args.world, r))
+        fc = FakeCollectives(args.world, r, gen)
+        h2g.set_spmd_transport(args.world, r, fc.allgather, None if args.no_subcosets else fc.bcast,
+                               None if args.no_slabs else fc.allgather_host)
+        try:
+            for _ in range(args.warmup):
+                pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())
+            ts = []
+            for _ in range(args.steps):
+                t0 = time.perf_counter()
+                pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())
+                ts.append(time.perf_counter() - t0)
+            h2g.prover_stage_sync(True)
+            pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())
+            h2g.prover_stage_sync(False)
+            stages = h2g.prover_stages()
+        finally:
+            h2g.set_spmd_transport(1)
+        ts.sort()
+        out["ranks"][r] = {"median_ms": round(1e3 * ts[len(ts) // 2], 3), "min_ms": round(1e3 * ts[0], 3),
+                           "gathers_per_proof": fc.calls // (args.warmup + args.steps + 1),
+                           "bcasts_per_proof": fc.bcasts // (args.warmup + args.steps + 1),
+                           "host_gathers_per_proof": fc.exchanges // (args.warmup + args.steps + 1),
+                           "stages_ms_synced": {nm: round(ms, 3) for nm, ms in stages}}
+        print(json.dumps({"rank": r, **out["ranks"][r]}), flush=True)
+    if args.world > 1:
+        params.set_slab(0, 0)
+    worst = max(v["median_ms"] for v in out["ranks"].values())
+    out["slowest_rank_ms"] = worst
+    pk.close()
+    params.close()
+    h2g.shutdown()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--k", type=int, default=22)
+    ap.add_argument("--workload", choices=("c3", "keccak"), default="c3")
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--ranks", default="")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-subcosets", action="store_true")
+    ap.add_argument("--no-slabs", action="store_true", help="replicate the multi-open tail")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    res = run(args)
+    print("EMULATE " + json.dumps(res), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

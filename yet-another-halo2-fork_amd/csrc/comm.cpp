@@ -53,9 +53,12 @@ struct Comm {
   int rnext = 0;
   int64_t *h_rhdr = nullptr, *d_rhdr = nullptr;  // one header
   int64_t *h_rpart = nullptr, *d_rpart = nullptr;
-  // SPMD all-gather of partials: pinned [world][9], device in [9] / out [world][9]
+  // SPMD all-gather of partials: pinned [world][H2G_SPMD_WORDS], device in / out
   uint64_t* h_ag = nullptr;
   uint64_t *d_ag_in = nullptr, *d_ag_out = nullptr;
+  // SPMD host all-gather (multi-open tail): pinned / device staging, world x bytes + bytes
+  void *h_hg = nullptr, *d_hg = nullptr;
+  size_t hg_cap = 0;
 };
 Comm* g_comm = nullptr;
 
@@ -143,6 +146,8 @@ int comm_destroy() {
   for (int64_t* p : {c->d_hdr, c->d_part, c->d_rhdr, c->d_rpart})
     if (p) (void)hipFree(p);
   if (c->h_ag) (void)hipHostFree(c->h_ag);
+  if (c->h_hg) (void)hipHostFree(c->h_hg);
+  if (c->d_hg) (void)hipFree(c->d_hg);
   for (uint64_t* p : {c->d_ag_in, c->d_ag_out})
     if (p) (void)hipFree(p);
   if (c->stx) (void)hipStreamDestroy(c->stx);
@@ -156,25 +161,56 @@ int comm_rank() { return g_comm ? g_comm->rank : 0; }
 
 void* comm_spmd_ctx() { return g_comm; }
 
-// SPMD: every rank's partial of MSM `seq`, in rank order (one ncclAllGather of 9 words per
-// rank on the slab communicator; every rank calls it for the same MSMs in the same order)
-int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[9], uint64_t* out) {
+// SPMD: every rank's partial of MSM `seq` and its consistency digest, in rank order (one
+// ncclAllGather of H2G_SPMD_WORDS words per rank on the slab communicator; every rank calls
+// it for the same MSMs in the same order)
+int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[H2G_SPMD_WORDS], uint64_t* out) {
   (void)seq;
   Comm* c = static_cast<Comm*>(ctx);
   if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm: no communicator for the SPMD all-gather");
   HIPCHK(hipSetDevice(c->device));
   const size_t W = (size_t)c->world;
+  constexpr size_t SW = H2G_SPMD_WORDS;
   if (!c->h_ag) {
-    HIPCHK(hipHostMalloc((void**)&c->h_ag, W * 9 * 8, hipHostMallocDefault));
-    HIPCHK(hipMalloc((void**)&c->d_ag_in, 9 * 8));
-    HIPCHK(hipMalloc((void**)&c->d_ag_out, W * 9 * 8));
+    HIPCHK(hipHostMalloc((void**)&c->h_ag, W * SW * 8, hipHostMallocDefault));
+    HIPCHK(hipMalloc((void**)&c->d_ag_in, SW * 8));
+    HIPCHK(hipMalloc((void**)&c->d_ag_out, W * SW * 8));
   }
-  std::memcpy(c->h_ag, in, 9 * 8);
-  HIPCHK(hipMemcpyAsync(c->d_ag_in, c->h_ag, 9 * 8, hipMemcpyHostToDevice, c->stx));
-  NCCLCHK(ncclAllGather(c->d_ag_in, c->d_ag_out, 9, ncclUint64, c->tx, c->stx));
-  HIPCHK(hipMemcpyAsync(c->h_ag, c->d_ag_out, W * 9 * 8, hipMemcpyDeviceToHost, c->stx));
+  std::memcpy(c->h_ag, in, SW * 8);
+  HIPCHK(hipMemcpyAsync(c->d_ag_in, c->h_ag, SW * 8, hipMemcpyHostToDevice, c->stx));
+  NCCLCHK(ncclAllGather(c->d_ag_in, c->d_ag_out, SW, ncclUint64, c->tx, c->stx));
+  HIPCHK(hipMemcpyAsync(c->h_ag, c->d_ag_out, W * SW * 8, hipMemcpyDeviceToHost, c->stx));
   HIPCHK(hipStreamSynchronize(c->stx));
-  std::memcpy(out, c->h_ag, W * 9 * 8);
+  std::memcpy(out, c->h_ag, W * SW * 8);
+  return H2G_OK;
+}
+
+// the multi-open tail's scalars (partial evaluations, kate carries): staged through
+// grow-only pinned / device buffers, one ncclAllGather of bytes
+int comm_allgather_host(void* ctx, const void* in, size_t bytes, void* out) {
+  Comm* c = static_cast<Comm*>(ctx);
+  if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm: no communicator for the SPMD host all-gather");
+  if (bytes == 0) return H2G_OK;
+  HIPCHK(hipSetDevice(c->device));
+  const size_t W = (size_t)c->world, total = W * bytes;
+  if (total > c->hg_cap) {
+    if (c->h_hg) (void)hipHostFree(c->h_hg);
+    if (c->d_hg) (void)hipFree(c->d_hg);
+    c->h_hg = nullptr;
+    c->d_hg = nullptr;
+    c->hg_cap = 0;
+    HIPCHK(hipHostMalloc(&c->h_hg, total + bytes, hipHostMallocDefault));
+    HIPCHK(hipMalloc(&c->d_hg, total + bytes));
+    c->hg_cap = total;
+  }
+  uint8_t* hin = static_cast<uint8_t*>(c->h_hg) + total;  // the send staging follows the receive buffer
+  uint8_t* din = static_cast<uint8_t*>(c->d_hg) + total;
+  std::memcpy(hin, in, bytes);
+  HIPCHK(hipMemcpyAsync(din, hin, bytes, hipMemcpyHostToDevice, c->stx));
+  NCCLCHK(ncclAllGather(din, c->d_hg, bytes, ncclUint8, c->tx, c->stx));
+  HIPCHK(hipMemcpyAsync(c->h_hg, c->d_hg, total, hipMemcpyDeviceToHost, c->stx));
+  HIPCHK(hipStreamSynchronize(c->stx));
+  std::memcpy(out, c->h_hg, total);
   return H2G_OK;
 }
 

@@ -7,12 +7,15 @@
 //   tx (rank 0 -> r): header int64[5] = (op, seq, base_set, lo, count), then the slab
 //                     (count x 32 B, from a device staging copy of the prover's scalars)
 //   rx (r -> rank 0): int64[9] = affine partial (8 limbs) + identity flag
+// SPMD mode all-gathers H2G_SPMD_WORDS words per rank instead (partial, flag, digest).
 // Definitions in comm.cpp; the peers' serve loop (h2g_comm_serve) lives in prover.cpp next
 // to the params it computes against.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+
+#include "h2g.h"
 
 namespace h2g {
 namespace rt {
@@ -41,7 +44,9 @@ int comm_send_partial(const uint64_t partial[8], int32_t is_identity);
 // SPMD (every rank proves): all-gather of the ranks' 9-word partials in rank order
 // (h2g_spmd_transport.allgather; ctx = Comm state from comm_spmd_ctx)
 void* comm_spmd_ctx();
-int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[9], uint64_t* out);
+int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[H2G_SPMD_WORDS], uint64_t* out);
+// SPMD: `bytes` host bytes from every rank, out = world x bytes in rank order
+int comm_allgather_host(void* ctx, const void* in, size_t bytes, void* out);
 // in-place broadcast of device memory from `root` (the sub-coset h evaluations)
 int comm_bcast(void* ctx, void* d_buf, size_t bytes, int root);
 

@@ -207,6 +207,9 @@ struct ProvingKey {
   size_t scr_len = 0, eval_scr_len = 0;
   EvalReq* d_reqs = nullptr;
   int max_reqs = 0;
+  // SPMD coefficient slabs: per SHPLONK point a (slab + halo) combination buffer
+  Fr* slab_buf = nullptr;
+  size_t slab_buf_len = 0;
   uint32_t* d_seeds = nullptr;
   uint64_t* d_offsets = nullptr;
   int max_chunks = 0;
@@ -310,6 +313,28 @@ uint64_t g_shard_seq = 0;
 // SPMD sharding (h2g_set_spmd_transport): every rank proves, rank r computes slab r
 h2g_spmd_transport g_spmd{nullptr, 1, 0, nullptr, nullptr};
 uint64_t g_spmd_seq = 0;
+// the running proof's transcript and RNG, whose digest travels with every SPMD partial
+// (H2G_SPMD_WORDS): ranks that diverged fail the proof instead of summing slabs of
+// different polynomials
+struct SpmdCheck {
+  const Transcript* tr = nullptr;
+  const ProverRng* rng = nullptr;
+};
+SpmdCheck g_spmd_check;
+struct SpmdCheckScope {
+  SpmdCheckScope(const Transcript* tr, const ProverRng* rng) { g_spmd_check = SpmdCheck{tr, rng}; }
+  ~SpmdCheckScope() { g_spmd_check = SpmdCheck{}; }
+};
+void spmd_digest(uint64_t out[4]) {
+  uint8_t a[64] = {}, b[64] = {}, d[64];
+  if (g_spmd_check.tr) g_spmd_check.tr->state_digest(a);
+  if (g_spmd_check.rng) g_spmd_check.rng->draws_digest(b);
+  Blake2b h("h2g-spmd-check\0\0");
+  h.update(a, 64);
+  h.update(b, 64);
+  h.digest(d);
+  std::memcpy(out, d, 32);
+}
 
 // slab r of an MSM of length n: the points [P r / world, P (r + 1) / world) of the
 // params' P = 2^k, clipped to n (one partition for every MSM length, so each rank's
@@ -346,18 +371,26 @@ int commit_collect(Device* d, MsmTicket* t, G1Affine* out) {
   if (t->shard_seq < 0) return H2G_OK;
   if (g_spmd.world > 1) {  // every rank's partial, summed in rank order (the same on every rank)
     const int W = g_spmd.world;
-    uint64_t mine[9];
+    constexpr int SW = H2G_SPMD_WORDS;
+    uint64_t mine[SW];
     std::memcpy(mine, out, 64);
     mine[8] = out->is_identity() ? 1 : 0;
-    std::vector<uint64_t> all((size_t)W * 9);
-    if (g_spmd.allgather(g_spmd.ctx, (uint64_t)t->shard_seq, mine, all.data()) != 0)
-      return fail(H2G_ERR_STATE, "spmd transport: all-gather of MSM " + std::to_string(t->shard_seq) + " failed");
+    spmd_digest(mine + 9);
+    std::vector<uint64_t> all((size_t)W * SW);
+    const int64_t seq = t->shard_seq;
+    if (g_spmd.allgather(g_spmd.ctx, (uint64_t)seq, mine, all.data()) != 0)
+      return fail(H2G_ERR_STATE, "spmd transport: all-gather of MSM " + std::to_string(seq) + " failed");
     t->shard_seq = -1;
+    for (int r = 0; r < W; r++)
+      if (std::memcmp(&all[(size_t)r * SW + 9], mine + 9, 32) != 0)
+        return fail(H2G_ERR_STATE, "spmd: rank " + std::to_string(r) + " diverged from rank " +
+                                       std::to_string(g_spmd.rank) + " before MSM " + std::to_string(seq) +
+                                       " (different witness, instances, key or RNG draws on the ranks)");
     G1xyzz acc = G1xyzz::identity();
     for (int r = 0; r < W; r++) {
-      if (all[(size_t)r * 9 + 8]) continue;
+      if (all[(size_t)r * SW + 8]) continue;
       G1Affine p;
-      std::memcpy(&p, &all[(size_t)r * 9], 64);
+      std::memcpy(&p, &all[(size_t)r * SW], 64);
       acc = xyzz_madd(acc, p);
     }
     *out = xyzz_to_affine(acc);
@@ -717,6 +750,85 @@ int circuit_ws_add(ProvingKey& pk) {
 // every column: rotations move rows by multiples of 2^e (evaluation.rs:317-620 evaluates
 // the same expressions row by row; the row split does not change any value).
 bool spmd_subcosets() { return g_spmd.world > 1 && g_spmd.bcast != nullptr; }
+
+// ------------------------------------------------------------------ SPMD coefficient slabs
+// With h2g_spmd_transport.allgather_host the evaluations and the SHPLONK multi-open run on
+// coefficient slabs: rank r owns coefficients [lo, hi) of every length-n polynomial (the
+// points of its MSM slabs, shard_lo) and computes one more (hi, the halo) where a kate
+// division reads a[i + 1].  Partial evaluations and the divisions' carries between slabs
+// are the only values that cross ranks (a few Fr per proof).
+struct Slab {
+  size_t lo = 0, hi = 0;  // owned coefficients
+  size_t hi1 = 0;         // hi + 1 (the halo coefficient), clipped to n
+};
+Slab spmd_slab(size_t n, int r) {
+  Slab s;
+  s.lo = shard_lo(n, n, g_spmd.world, r);
+  s.hi = shard_lo(n, n, g_spmd.world, r + 1);
+  s.hi1 = std::min(s.hi + 1, n);
+  return s;
+}
+// every rank's `mine` (same count on each), rank order
+int spmd_allgather_fr(const std::vector<Fr>& mine, std::vector<Fr>* all) {
+  const size_t W = (size_t)g_spmd.world, cnt = mine.size();
+  all->assign(W * cnt, Fr::zero());
+  if (!cnt) return H2G_OK;
+  if (g_spmd.allgather_host(g_spmd.ctx, mine.data(), cnt * sizeof(Fr), all->data()) != 0)
+    return fail(H2G_ERR_STATE, "spmd transport: host all-gather failed");
+  return H2G_OK;
+}
+// out[i] (+)= sum_k coef_k p_k[i] for i in [lo, hi) only (global indices; out, p_k full-length)
+int lincomb_range(Fr* out, size_t lo, size_t hi, LinTerms t, bool accumulate, hipStream_t st) {
+  if (hi <= lo) return H2G_OK;
+  for (int k = 0; k < t.k; k++) {
+    t.len[k] = t.len[k] > lo ? std::min<uint64_t>(t.len[k], hi) - lo : 0;
+    t.p[k] = t.len[k] ? t.p[k] + lo : t.p[k];
+  }
+  HIPCHK(lincomb(out + lo, hi - lo, t, accumulate, st));
+  return H2G_OK;
+}
+// The kate divisions' carries: for a_i (global indexing, valid on [lo, hi1)) and point b_i,
+// carry[i] = q_i[hi'] = sum_{j >= hi'} a_i[j + 1] b_i^(j - hi') (hi' = min(hi, n - 1)), from
+// every slab's partial Horner value E_s = sum_{j in [lo_s, hi'_s)} a_i[j + 1] b_i^(j - lo_s):
+// C_{W-1} = 0, C_r = E_{r+1} + b^(hi'_{r+1} - lo_{r+1}) C_{r+1}.  One all-gather for all points.
+template <class Buf>
+int slab_carries(ProvingKey& pk, const Slab& sl, size_t n, const std::vector<Fr>& pts, Buf a, std::vector<Fr>* carry,
+                 hipStream_t st) {
+  const size_t np = pts.size();
+  const size_t hq = std::min(sl.hi, n - 1);
+  const uint64_t m = hq > sl.lo ? hq - sl.lo : 0;
+  std::vector<EvalReq> reqs(np);
+  for (size_t i = 0; i < np; i++) reqs[i] = EvalReq{a(i) + sl.lo + 1, m, pts[i]};
+  if ((int)np > pk.max_reqs) {
+    PALLOC(pk.pool, pk.d_reqs, np);
+    PALLOC(pk.pool, pk.evals, np);
+    pk.max_reqs = (int)np;
+  }
+  const size_t need = poly_eval_scratch_len((int)np, m ? m : 1);
+  if (need > pk.eval_scr_len) {
+    PALLOC(pk.pool, pk.eval_scr, need);
+    pk.eval_scr_len = need;
+  }
+  HIPCHK(hipMemcpyAsync(pk.d_reqs, reqs.data(), np * sizeof(EvalReq), hipMemcpyHostToDevice, st));
+  HIPCHK(poly_eval_batch(pk.d_reqs, (int)np, m ? m : 1, pk.evals, pk.eval_scr, st));
+  std::vector<Fr> mine(np);
+  HIPCHK(hipMemcpyAsync(mine.data(), pk.evals, np * sizeof(Fr), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::vector<Fr> all;
+  RCCHK(spmd_allgather_fr(mine, &all));
+  carry->assign(np, Fr::zero());
+  for (size_t i = 0; i < np; i++) {
+    Fr c = Fr::zero();
+    for (int s = g_spmd.world - 1; s > g_spmd.rank; s--) {
+      const Slab ss = spmd_slab(n, s);
+      const size_t hs = std::min(ss.hi, n - 1);
+      const uint64_t ms = hs > ss.lo ? hs - ss.lo : 0;
+      c = all[(size_t)s * np + i] + pow_u64(pts[i], ms) * c;
+    }
+    (*carry)[i] = c;
+  }
+  return H2G_OK;
+}
 
 // the key's cosets cut to this rank's sub-cosets, once per (world, rank)
 int sub_prepare(ProvingKey& pk, hipStream_t st) {
@@ -1119,6 +1231,21 @@ struct StreamSyncGuard {
   ~StreamSyncGuard() { (void)hipStreamSynchronize(s); }
 };
 
+// A proof that fails part-way leaves launched MSMs uncollected: their result ring entries
+// would stay reserved.  Proofs run one at a time under the library lock and collect every
+// MSM they launch, so on the way out the MSM streams are drained and the ring freed.
+struct MsmRingGuard {
+  Device* d;
+  ~MsmRingGuard() {
+    bool any = false;
+    for (bool b : d->ring_busy) any = any || b;
+    if (!any) return;
+    for (hipStream_t s : d->mstream)
+      if (s) (void)hipStreamSynchronize(s);
+    for (bool& b : d->ring_busy) b = false;
+  }
+};
+
 struct StageClock {
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
   hipStream_t st;
@@ -1163,9 +1290,16 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   std::vector<CircuitWs*> W(ncirc);
   for (int c = 0; c < ncirc; c++) W[c] = pk.cws[c].get();
   if (spmd_subcosets()) RCCHK(sub_prepare(pk, st));  // this rank's sub-cosets of the key's cosets
+  MsmRingGuard ring_guard{d};
   StageClock clk(st, g_stage_sync);
+  // SPMD coefficient slabs for the multi-open tail (SHPLONK only; GWC stays replicated)
+  const bool slabs = g_spmd.world > 1 && g_spmd.allgather_host != nullptr && pk.multiopen == 0;
+  Slab sl;
+  sl.hi = sl.hi1 = n;
+  if (slabs) sl = spmd_slab(n, g_spmd.rank);
   ProverRng& rng = *in.rng;
   Transcript tr(proof, pk.transcript);
+  SpmdCheckScope spmd_check(&tr, &rng);
   auto write_point = [&](const G1Affine& p) -> int {
     if (!tr.write_point(p)) return fail(H2G_ERR_ARG, "cannot write points at infinity to the transcript");
     return H2G_OK;
@@ -1614,7 +1748,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     }
     HIPCHK(hipMemcpyAsync(pk.d_seeds, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(pk.d_offsets, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)off.size(), st));
+    // a slab-mode rank draws only its coefficients (and the halo) of the random polynomial
+    HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)off.size(), st, sl.lo, sl.hi1));
     (void)rng.random_fr();             // random_blind
     RCCHK(rng_ok());
     RCCHK(commit_launch(d, prm, pk.random_poly, n, SRS_G, st, &van_tk));
@@ -1761,7 +1896,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     bool first = true;
     for (int p = 0; p < npieces; p++) {
       if (t.k == LIN_MAXT) {
-        HIPCHK(lincomb(pk.h_poly, n, t, !first, st));
+        RCCHK(lincomb_range(pk.h_poly, sl.lo, sl.hi1, t, !first, st));  // a slab rank: its slab + halo
         first = false;
         t.k = 0;
       }
@@ -1771,7 +1906,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       t.k++;
       c = c * xn;
     }
-    HIPCHK(lincomb(pk.h_poly, n, t, !first, st));
+    RCCHK(lincomb_range(pk.h_poly, sl.lo, sl.hi1, t, !first, st));
   }
 
   // ---- the polynomial openings (prover.rs:840-889) and their evaluations
@@ -1855,11 +1990,25 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       pk.eval_scr_len = need;
     }
     std::vector<EvalReq> reqs(nreq);
-    for (int i = 0; i < nreq; i++) reqs[i] = EvalReq{polys[ev_keys[i].poly].p, polys[ev_keys[i].poly].len, ev_keys[i].pt};
+    for (int i = 0; i < nreq; i++) {  // a slab rank evaluates its coefficients [lo, hi) only
+      const PolyRef& pr = polys[ev_keys[i].poly];
+      const uint64_t len = pr.len > sl.lo ? std::min<uint64_t>(pr.len, sl.hi) - sl.lo : 0;
+      reqs[i] = EvalReq{pr.p + (len ? sl.lo : 0), len, ev_keys[i].pt};
+    }
     HIPCHK(hipMemcpyAsync(pk.d_reqs, reqs.data(), nreq * sizeof(EvalReq), hipMemcpyHostToDevice, st));
-    HIPCHK(poly_eval_batch(pk.d_reqs, nreq, n, pk.evals, pk.eval_scr, st));
+    HIPCHK(poly_eval_batch(pk.d_reqs, nreq, sl.hi - sl.lo, pk.evals, pk.eval_scr, st));
     HIPCHK(hipMemcpyAsync(evals.data(), pk.evals, nreq * sizeof(Fr), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (slabs) {  // p(x) = sum_r x^lo_r (slab r's partial evaluation), summed in rank order
+      for (int i = 0; i < nreq; i++) evals[i] = evals[i] * pow_u64(ev_keys[i].pt, sl.lo);
+      std::vector<Fr> all;
+      RCCHK(spmd_allgather_fr(evals, &all));
+      for (int i = 0; i < nreq; i++) {
+        Fr acc = Fr::zero();
+        for (int r = 0; r < g_spmd.world; r++) acc = acc + all[(size_t)r * nreq + i];
+        evals[i] = acc;
+      }
+    }
   }
   auto ev = [&](int poly, const Fr& pt) { return evals[ev_index(poly, pt)]; };
   for (int ci = 0; ci < ncirc; ci++)  // [TRANSCRIPT-17] every circuit's advice evaluations
@@ -2015,8 +2164,18 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
           }
       }
     }
-    HIPCHK(hipMemsetAsync(pk.hx, 0, n * sizeof(Fr), st));
-    for (const Fr& p : super_pts) {
+    // slab mode: per point a (slab + halo) buffer; gbuf(i) indexes it globally
+    const size_t np = super_pts.size(), cap = sl.hi1 - sl.lo + 1;
+    if (slabs && np * cap > pk.slab_buf_len) {
+      PALLOC(pk.pool, pk.slab_buf, np * cap);
+      pk.slab_buf_len = np * cap;
+    }
+    auto gbuf = [&](size_t i) { return pk.slab_buf + i * cap - sl.lo; };
+    if (slabs) HIPCHK(hipMemsetAsync(pk.hx + sl.lo, 0, (sl.hi1 - sl.lo) * sizeof(Fr), st));
+    else HIPCHK(hipMemsetAsync(pk.hx, 0, n * sizeof(Fr), st));
+    for (size_t pi = 0; pi < np; pi++) {
+      const Fr& p = super_pts[pi];
+      Fr* gp = slabs ? gbuf(pi) : pk.nx;
       // alpha_s = v^s c_{s,p} for the sets containing p
       std::vector<Fr> alpha(rs_rep.size(), Fr::zero());
       std::vector<char> has(rs_rep.size(), 0);
@@ -2039,7 +2198,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         const int r = rs_of[c];
         if (!has[r]) continue;
         if (t.k == LIN_MAXT - 1) {
-          HIPCHK(lincomb(pk.nx, n, t, !first, st));
+          RCCHK(lincomb_range(gp, sl.lo, sl.hi1, t, !first, st));
           first = false;
           t.k = 0;
         }
@@ -2055,8 +2214,28 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       t.len[t.k] = corr.size();
       t.coef[t.k] = fr_neg_one();
       t.k++;
-      HIPCHK(lincomb(pk.nx, n, t, !first, st));
-      HIPCHK(kate_division(pk.nx, n, p, pk.hx, pk.scr, st, true));
+      RCCHK(lincomb_range(gp, sl.lo, sl.hi1, t, !first, st));
+      if (!slabs) HIPCHK(kate_division(pk.nx, n, p, pk.hx, pk.scr, st, true));
+    }
+    if (slabs) {
+      // G_p / (X - p) on slabs: q[i] = sum_{j >= i} a[j + 1] p^(j - i).  The slab's own part
+      // plus p^(hi' - i) C, with C = q[hi'] the quotient just above the slab = sum over the
+      // higher slabs of their partial Horner values E_s (one all-gather for every point);
+      // C enters as p C added to a[hi'], so the division runs unchanged on the slab.
+      std::vector<Fr> carry;
+      RCCHK(slab_carries(pk, sl, n, super_pts, [&](size_t i) { return gbuf(i); }, &carry, st));
+      Fr halo = Fr::zero();
+      for (size_t pi = 0; pi < np; pi++) {
+        const size_t hq = std::min(sl.hi, n - 1);
+        if (hq <= sl.lo) continue;
+        HIPCHK(poly_binop(POLY_ADD_CONST, gbuf(pi) + hq, nullptr, super_pts[pi] * carry[pi], gbuf(pi) + hq, 1, st));
+        HIPCHK(kate_division(gbuf(pi) + sl.lo, hq - sl.lo + 1, super_pts[pi], pk.hx + sl.lo, pk.scr, st, true));
+        halo = halo + carry[pi];
+      }
+      if (sl.hi < n) {  // h_x's halo coefficient (read by the linearisation): q[hi] = sum of the carries
+        corr_stage.emplace_back(1, halo);
+        HIPCHK(hipMemcpyAsync(pk.hx + sl.hi, corr_stage.back().data(), sizeof(Fr), hipMemcpyHostToDevice, st));
+      }
     }
   }
   {
@@ -2073,7 +2252,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     LinTerms t;
     bool first = true;
     auto flush = [&]() -> int {
-      HIPCHK(lincomb(pk.lx, n, t, !first, st));
+      RCCHK(lincomb_range(pk.lx, sl.lo, sl.hi1, t, !first, st));  // a slab rank: slab + halo
       first = false;
       t.k = 0;
       return H2G_OK;
@@ -2112,8 +2291,20 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     t.k++;
     RCCHK(flush());
   }
-  HIPCHK(kate_division(pk.lx, n, u, pk.q1, pk.scr, st));
-  HIPCHK(poly_binop(POLY_SCALE, pk.q1, nullptr, inv(z0), pk.q1, n - 1, st));
+  if (slabs) {  // the same slab division by (X - u), one carry
+    std::vector<Fr> carry;
+    const std::vector<Fr> pts{u};
+    RCCHK(slab_carries(pk, sl, n, pts, [&](size_t) { return pk.lx; }, &carry, st));
+    const size_t hq = std::min(sl.hi, n - 1);
+    if (hq > sl.lo) {
+      HIPCHK(poly_binop(POLY_ADD_CONST, pk.lx + hq, nullptr, u * carry[0], pk.lx + hq, 1, st));
+      HIPCHK(kate_division(pk.lx + sl.lo, hq - sl.lo + 1, u, pk.q1 + sl.lo, pk.scr, st));
+      HIPCHK(poly_binop(POLY_SCALE, pk.q1 + sl.lo, nullptr, inv(z0), pk.q1 + sl.lo, hq - sl.lo, st));
+    }
+  } else {
+    HIPCHK(kate_division(pk.lx, n, u, pk.q1, pk.scr, st));
+    HIPCHK(poly_binop(POLY_SCALE, pk.q1, nullptr, inv(z0), pk.q1, n - 1, st));
+  }
   {
     G1Affine cm;
     RCCHK(commit(d, prm, pk.q1, n - 1, SRS_G, &cm, st));
@@ -2271,7 +2462,11 @@ bool g1_decompress_host(const uint8_t c[32], G1Affine* out) {
 
 struct ByteWriter {  // out == NULL: count only
   uint8_t* out;
-  size_t cap, len = 0;
+  size_t cap;
+  // the library stream the arrays were produced on: copies and conversions queue behind
+  // its work (it is non-blocking, so the NULL stream would not order with it)
+  hipStream_t st;
+  size_t len = 0;
   bool fits(size_t k) const { return out && len + k <= cap; }
   void put(const void* p, size_t k) {
     if (fits(k)) std::memcpy(out + len, p, k);
@@ -2285,7 +2480,10 @@ struct ByteWriter {  // out == NULL: count only
   }
   bool proc = false;  // SerdeFormat::Processed: compressed points, canonical field elements
   int dev(const void* d, size_t k) {  // device bytes
-    if (fits(k)) HIPCHK(hipMemcpy(out + len, d, k, hipMemcpyDeviceToHost));
+    if (fits(k)) {
+      HIPCHK(hipMemcpyAsync(out + len, d, k, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+    }
     len += k;
     return H2G_OK;
   }
@@ -2296,14 +2494,15 @@ struct ByteWriter {  // out == NULL: count only
       DevScratch t;
       HIPCHK(hipMalloc(&t.p, k));
       HIPCHK(conv(t.p));
-      HIPCHK(hipMemcpy(out + len, t.p, k, hipMemcpyDeviceToHost));
+      HIPCHK(hipMemcpyAsync(out + len, t.p, k, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
     }
     len += k;
     return H2G_OK;
   }
   int g1s(const G1Affine* d, size_t cnt) {  // SerdeCurveAffine::write of cnt device points
     if (!proc) return dev(d, cnt * sizeof(G1Affine));
-    return dev_conv(cnt * 32, [&](void* t) { return g1_compress(d, cnt, (uint8_t*)t, nullptr); });
+    return dev_conv(cnt * 32, [&](void* t) { return g1_compress(d, cnt, (uint8_t*)t, st); });
   }
   void g1(const G1Affine& a) {
     if (!proc) return put(&a, sizeof(G1Affine));
@@ -2320,7 +2519,7 @@ struct ByteWriter {  // out == NULL: count only
   int poly(const Fr* d, size_t cnt) {  // Polynomial::write (poly.rs:187-197)
     u32be((uint32_t)cnt);
     if (!proc) return dev(d, cnt * sizeof(Fr));
-    return dev_conv(cnt * sizeof(Fr), [&](void* t) { return fr_to_repr(d, cnt, (Fr*)t, nullptr); });
+    return dev_conv(cnt * sizeof(Fr), [&](void* t) { return fr_to_repr(d, cnt, (Fr*)t, st); });
   }
   int polys(const std::vector<Fr*>& v, size_t cnt) {  // write_polynomial_slice (helpers.rs:119-129)
     u32be((uint32_t)v.size());
@@ -2405,7 +2604,7 @@ int h2g_params_write(uint64_t params, int format, uint8_t* out, size_t cap, size
     return fail(H2G_ERR_ARG, "params_write: unknown SerdeFormat");
   const Params& p = *it->second;
   if (!p.has_g2) return fail(H2G_ERR_STATE, "params_write: the params have no G2 points (h2g_params_set_g2)");
-  ByteWriter w{out, out ? cap : 0};
+  ByteWriter w{out, out ? cap : 0, d->stream};
   w.proc = format == SERDE_PROCESSED;
   w.u32le(p.k);
   RCCHK(w.g1s(p.g, p.n));
@@ -2520,7 +2719,7 @@ int h2g_pk_write(uint64_t pk_h, int format, uint8_t* out, size_t cap, size_t* le
   if (pit == g_params.end()) return fail(H2G_ERR_HANDLE, "pk_write: the key's params were freed");
   RCCHK(h2g_pk_vk_commitments(pk_h, nullptr, nullptr));  // commit_lagrange, once
   HIPCHK(hipStreamSynchronize(d->stream));
-  ByteWriter w{out, out ? cap : 0};
+  ByteWriter w{out, out ? cap : 0, d->stream};
   w.proc = format == SERDE_PROCESSED;
   w.u8(PK_VERSION);
   w.u8((uint8_t)pk.k);
@@ -2781,7 +2980,9 @@ int h2g_create_proof_multi(uint64_t params, uint64_t pk, const h2g_prove_inputs*
   if (!p || p->num_circuits < 1) return fail(H2G_ERR_ARG, "create_proof: no circuits");
   if (p->witness && !p->witness->fill) return fail(H2G_ERR_ARG, "create_proof: null witness fill");
   if (!p->rng && !p->rng_seed) return fail(H2G_ERR_ARG, "create_proof: neither an rng nor a seed");
-  if (p->rng && !p->rng->fill_bytes && !p->rng->random_fr) return fail(H2G_ERR_ARG, "create_proof: rng without draws");
+  // fill_bytes is required: the vanishing argument's ChaCha seeds are fill_bytes draws
+  // (vanishing/prover.rs:69-73) whatever F::random uses
+  if (p->rng && !p->rng->fill_bytes) return fail(H2G_ERR_ARG, "create_proof: the caller's rng needs fill_bytes");
   std::unique_ptr<ProverRng> rng = p->rng ? std::make_unique<ProverRng>(p->rng->fill_bytes, p->rng->random_fr, p->rng->ctx)
                                           : std::make_unique<ProverRng>(p->rng_seed);
   ProveIn in;
@@ -2810,7 +3011,7 @@ int h2g_set_shard_transport(const h2g_shard_transport* t) {
   if (t && t->world > 1) {
     if (!t->launch || !t->collect || t->world > 4096) return fail(H2G_ERR_ARG, "set_shard_transport: bad transport");
     g_shard = *t;
-    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr};
+    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr};
   } else {
     g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   }
@@ -2826,7 +3027,7 @@ int h2g_set_spmd_transport(const h2g_spmd_transport* t) {
     g_spmd = *t;
     g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   } else {
-    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr};
+    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr};
   }
   g_spmd_seq = 0;
   return H2G_OK;
@@ -2906,7 +3107,7 @@ int h2g_comm_init(const uint8_t id[256], int world, int rank) {
 int h2g_comm_destroy(void) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (g_shard.launch == comm_launch) g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
-  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr};
+  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr};
   return comm_destroy();
 }
 
@@ -2914,7 +3115,7 @@ int h2g_comm_spmd_install(int split_subcosets) {
   NEED_DEV_P();
   if (comm_world() < 2) return fail(H2G_ERR_STATE, "comm_spmd_install: needs a communicator (h2g_comm_init)");
   g_spmd = h2g_spmd_transport{comm_spmd_ctx(), comm_world(), comm_rank(), comm_allgather_partial,
-                              split_subcosets ? comm_bcast : nullptr};
+                              split_subcosets ? comm_bcast : nullptr, comm_allgather_host};
   g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   g_spmd_seq = 0;
   return H2G_OK;
@@ -2922,7 +3123,7 @@ int h2g_comm_spmd_install(int split_subcosets) {
 
 int h2g_comm_spmd_uninstall(void) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
-  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr};
+  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr};
   g_spmd_seq = 0;
   return H2G_OK;
 }

@@ -31,9 +31,9 @@ hipError_t perm_z_assemble(Fr* z, size_t n, int bf, const Fr* prefix, const Fr* 
                            hipStream_t st);
 
 // ---- vanishing argument: random polynomial (vanishing/prover.rs:57-81) ----
-// out[i] = Fr::random(ChaCha20Rng(seed_t)) for the i - off[t]'th draw of chunk t
+// out[i] = Fr::random(ChaCha20Rng(seed_t)) for the i - off[t]'th draw of chunk t, i in [lo, hi)
 hipError_t chacha_random_poly(Fr* out, size_t n, const uint32_t* d_seeds, const uint64_t* d_offsets, int chunks,
-                              hipStream_t st);
+                              hipStream_t st, size_t lo = 0, size_t hi = ~(size_t)0);
 
 // ---- evaluate_h (evaluation.rs:317-620): expression programs + permutation + lookup +
 // shuffle constraint blocks, fused with the division by t(X) ----

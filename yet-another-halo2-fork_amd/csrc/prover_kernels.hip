@@ -88,10 +88,12 @@ hipError_t perm_z_assemble(Fr* z, size_t n, int bf, const Fr* prefix, const Fr* 
 // ------------------------------------------------------------------ vanishing random poly
 // Chunk t of the polynomial is filled by its own ChaCha20Rng(seed_t); each Fr::random
 // consumes exactly one 64-byte block, so element j of the chunk is block j.
-__global__ void __launch_bounds__(KT) chacha_poly_kernel(Fr* __restrict__ out, size_t n,
+// Elements [lo, hi) only: the SPMD multi-open tail draws a rank's coefficient slab.
+__global__ void __launch_bounds__(KT) chacha_poly_kernel(Fr* __restrict__ out, size_t lo_i, size_t hi_i,
                                                          const uint32_t* __restrict__ seeds,
                                                          const uint64_t* __restrict__ off, int chunks) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+  for (size_t i = lo_i + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < hi_i;
+       i += (size_t)gridDim.x * blockDim.x) {
     int lo = 0, hi = chunks - 1;  // last t with off[t] <= i
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
@@ -107,9 +109,11 @@ __global__ void __launch_bounds__(KT) chacha_poly_kernel(Fr* __restrict__ out, s
 }
 
 hipError_t chacha_random_poly(Fr* out, size_t n, const uint32_t* d_seeds, const uint64_t* d_offsets, int chunks,
-                              hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(chacha_poly_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, out, n, d_seeds, d_offsets, chunks);
+                              hipStream_t st, size_t lo, size_t hi) {
+  if (hi > n) hi = n;
+  if (lo >= hi) return hipSuccess;
+  hipLaunchKernelGGL(chacha_poly_kernel, dim3(grid_1d(hi - lo)), dim3(KT), 0, st, out, lo, hi, d_seeds, d_offsets,
+                     chunks);
   return hipGetLastError();
 }
 

@@ -219,11 +219,13 @@ class ProverRng {
   explicit ProverRng(const uint8_t seed[32]) : cc_(seed) {}
   ProverRng(FillFn fill_bytes, FrFn random, void* ctx) : cc_(kZeroSeed), fb_(fill_bytes), fr_(random), ctx_(ctx) {}
   void fill(uint8_t* out, size_t len) {
-    if (!fb_ && !fr_) return cc_.fill(out, len);
-    if (failed_ || !fb_ || fb_(ctx_, out, len) != 0) {
+    if (!fb_ && !fr_) {
+      cc_.fill(out, len);
+    } else if (failed_ || !fb_ || fb_(ctx_, out, len) != 0) {
       failed_ = true;
       std::memset(out, 0, len);
     }
+    draws_.update(out, len);
   }
   Fr random_fr() {
     if (fr_) {  // the caller's F::random, Montgomery limbs
@@ -234,6 +236,7 @@ class ProverRng {
       }
       Fr r;
       std::memcpy(r.l, v, 32);
+      draws_.update(v, 32);
       unsigned br = 0;  // an Fr must be below r
       for (int i = 0; i < 8; i++) (void)__builtin_subc(r.l[i], FrParams::M[i], br, &br);
       if (!br) {
@@ -247,10 +250,13 @@ class ProverRng {
     return fr_from_u512(w);
   }
   bool failed() const { return failed_; }
+  // digest of every draw so far (SPMD ranks must draw the same values)
+  void draws_digest(uint8_t out[64]) const { draws_.digest(out); }
 
  private:
   static constexpr uint8_t kZeroSeed[32] = {};
   ChaChaRng cc_;
+  Blake2b draws_{"h2g-rng-draws\0\0\0"};
   FillFn fb_ = nullptr;
   FrFn fr_ = nullptr;
   void* ctx_ = nullptr;
@@ -361,6 +367,12 @@ class Transcript {
     if (b[33] & 1) c[31] |= 0x80;
     proof_->insert(proof_->end(), c, c + 32);
     return true;
+  }
+  // digest of everything absorbed so far (SPMD consistency check; the state is unchanged)
+  void state_digest(uint8_t out[64]) const {
+    std::memset(out, 0, 64);
+    if (kind_ == TRANSCRIPT_KECCAK256) k_.digest(out);
+    else h_.digest(out);
   }
   Fr squeeze() {
     const uint8_t z = 0;

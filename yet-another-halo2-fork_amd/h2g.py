@@ -856,22 +856,27 @@ def transport_errors():
     return errs
 
 
+SPMD_WORDS = 13  # H2G_SPMD_WORDS (include/h2g.h)
 SPMD_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, VP, U64, U64P, U64P)
 SPMD_BCAST = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, SZ, ctypes.c_int)
+SPMD_ALLGATHER_HOST = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, SZ, VP)
 
 
 class SpmdTransport(ctypes.Structure):
     """struct h2g_spmd_transport (include/h2g.h)"""
     _fields_ = [("ctx", VP), ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("allgather", SPMD_ALLGATHER),
-                ("bcast", SPMD_BCAST)]
+                ("bcast", SPMD_BCAST), ("allgather_host", SPMD_ALLGATHER_HOST)]
 
 
-def set_spmd_transport(world, rank=0, allgather=None, bcast=None):
+def set_spmd_transport(world, rank=0, allgather=None, bcast=None, allgather_host=None):
     """SPMD sharding: every rank runs the same create_proof and computes its point slab of
-    each commitment MSM; allgather(seq, mine: uint64[9]) -> uint64[world, 9] (rank order)
-    collects the partials.  bcast(d_ptr, nbytes, root) (optional) divides the extended
+    each commitment MSM; allgather(seq, mine: uint64[SPMD_WORDS]) -> uint64[world, SPMD_WORDS]
+    (rank order) collects the partials (8 affine limbs, identity flag, 4 words of the
+    rank's transcript / RNG digest, which the library compares across ranks).  bcast(d_ptr, nbytes, root) (optional) divides the extended
     domain's sub-cosets over the ranks and broadcasts each one's h evaluations (device
-    memory, in place).  world <= 1 removes it.  Exceptions fail the proof."""
+    memory, in place).  allgather_host(data: bytes) -> world byte strings in rank order
+    (optional) runs the evaluations and the SHPLONK multi-open on coefficient slabs.
+    world <= 1 removes it.  Exceptions fail the proof."""
     global _transport_keep
     if world <= 1:
         check(lib().h2g_set_spmd_transport(None))
@@ -880,9 +885,9 @@ def set_spmd_transport(world, rank=0, allgather=None, bcast=None):
 
     def _ag(ctx, seq, mine, out):
         try:
-            got = np.ascontiguousarray(allgather(int(seq), np.ctypeslib.as_array(mine, shape=(9,)).copy()),
-                                       dtype=np.uint64).reshape(world * 9)
-            ctypes.memmove(out, got.ctypes.data, world * 9 * 8)
+            got = np.ascontiguousarray(allgather(int(seq), np.ctypeslib.as_array(mine, shape=(SPMD_WORDS,)).copy()),
+                                       dtype=np.uint64).reshape(world * SPMD_WORDS)
+            ctypes.memmove(out, got.ctypes.data, world * SPMD_WORDS * 8)
             return 0
         except Exception as e:  # noqa: BLE001 -- reported through the C status
             _transport_keep[-1].append(e)
@@ -896,10 +901,22 @@ def set_spmd_transport(world, rank=0, allgather=None, bcast=None):
             _transport_keep[-1].append(e)
             return 1
 
+    def _agh(ctx, d_in, nbytes, d_out):
+        try:
+            parts = allgather_host(ctypes.string_at(d_in, nbytes))
+            if len(parts) != world or any(len(p) != nbytes for p in parts):
+                raise ValueError("allgather_host: world x bytes expected")
+            ctypes.memmove(d_out, b"".join(bytes(p) for p in parts), world * nbytes)
+            return 0
+        except Exception as e:  # noqa: BLE001
+            _transport_keep[-1].append(e)
+            return 1
+
     cb = SPMD_ALLGATHER(_ag)
     cbb = SPMD_BCAST(_bc) if bcast is not None else ctypes.cast(None, SPMD_BCAST)
-    t = SpmdTransport(None, world, rank, cb, cbb)
-    _transport_keep = (t, cb, cbb, [])
+    cbh = SPMD_ALLGATHER_HOST(_agh) if allgather_host is not None else ctypes.cast(None, SPMD_ALLGATHER_HOST)
+    t = SpmdTransport(None, world, rank, cb, cbb, cbh)
+    _transport_keep = (t, cb, cbb, cbh, [])
     check(lib().h2g_set_spmd_transport(ctypes.byref(t)))
 
 

@@ -187,18 +187,30 @@ class SpmdGather:
     """SPMD sharding over torch.distributed (h2g_set_spmd_transport): every rank runs the
     same create_proof and computes point slab `rank` of each commitment MSM; the 9-word
     partials (affine limbs + identity flag) are all-gathered in rank order and every rank
-    sums them, so no scalars travel.  h2g_comm_spmd_install is the same over the library's
-    own RCCL communicator."""
+    sums them, so no scalars travel; with `slabs` the evaluations and SHPLONK run on
+    coefficient slabs joined by small host all-gathers (allgather_host).
+    h2g_comm_spmd_install is the same over the library's own RCCL communicator."""
 
-    def __init__(self, dist, group=None, subcosets=True):
+    def __init__(self, dist, group=None, subcosets=True, slabs=True):
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.device = _staging(dist, group)
         self.subcosets = subcosets
+        self.slabs = slabs
         self.calls = 0
         self.bcasts = 0
+        self.host_gathers = 0
+
+    def allgather_host(self, data):
+        """the multi-open tail's scalars: `data` (bytes) from every rank, rank order"""
+        import torch
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(self.device)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.group)
+        self.host_gathers += 1
+        return [o.cpu().numpy().tobytes() for o in out]
 
     def allgather(self, seq, mine):
         import torch
@@ -229,7 +241,8 @@ class SpmdGather:
 
     def install(self):
         import h2g
-        h2g.set_spmd_transport(self.world, self.rank, self.allgather, self.bcast if self.subcosets else None)
+        h2g.set_spmd_transport(self.world, self.rank, self.allgather, self.bcast if self.subcosets else None,
+                               self.allgather_host if self.slabs else None)
 
     @staticmethod
     def uninstall():
