@@ -197,8 +197,13 @@ def pmc_traffic(args):
         finally:
             shutil.rmtree(d, ignore_errors=True)
     traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+    low = (vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
     return traffic, (f"rocprofv3 --pmc, mean per launch of msm_acc_kernel: FETCH_SIZE {vals['FETCH_SIZE']:.0f} KiB "
-                     f"(x2 gfx950 correction), WRITE_SIZE {vals['WRITE_SIZE']:.0f} KiB")
+                     f"(x2 gfx950 correction), WRITE_SIZE {vals['WRITE_SIZE']:.0f} KiB.  Calibration "
+                     f"(tools/microbench/pmc_calib.hip, profiles/r03/pmc_calibration.json): FETCH_SIZE counts 0.50 of "
+                     f"a coalesced 16-B or 8-B per lane stream and 1.01 of random 64-B point gathers, i.e. one 64-B "
+                     f"unit per read request; x2 prices every request as the 128-B line it moves (upper bound), "
+                     f"{low / 1e9:.2f} GB per launch if the point gathers move 64 B (lower bound)")
 
 
 def pmc_child(args):

@@ -420,6 +420,15 @@ typedef struct {
    * between slabs) are all-gathered: allgather_host(ctx, in, bytes, out) with `bytes`
    * host bytes from this rank, out = world x bytes in rank order, complete on return */
   int (*allgather_host)(void* ctx, const void* in, size_t bytes, void* out);
+  /* optional, with bcast and allgather_host -- h(X) reaches the ranks as coefficient
+   * slabs instead of broadcast evaluations: the owner of sub-coset t interpolates its h
+   * evaluations (an n-point inverse NTT instead of everyone's 2^e n-point one) and every
+   * rank receives slab r of each sub-coset's folded coefficients, from which it forms
+   * its slab of the h pieces (vanishing/prover.rs:102-155).  exchange(ctx, d_send,
+   * send_bytes, d_recv, recv_bytes): device buffers, all-to-all with per-peer byte counts
+   * (world entries each; peer p's data contiguous, in peer order; the rank's own entry
+   * is a local copy), complete on return */
+  int (*exchange)(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv, const size_t* recv_bytes);
 } h2g_spmd_transport;
 /* install (world >= 2) or remove (NULL or world <= 1) */
 int h2g_set_spmd_transport(const h2g_spmd_transport* t);

@@ -61,6 +61,10 @@ def main():
                     help="slab: rank 0 proves, peers serve slabs; spmd: every rank proves its slab")
     ap.add_argument("--no-subcosets", action="store_true",
                     help="spmd: replicate the extended-domain work instead of splitting the sub-cosets")
+    ap.add_argument("--no-slabs", action="store_true",
+                    help="spmd: replicate the evaluations / SHPLONK tail (no host all-gather)")
+    ap.add_argument("--bcast-h", action="store_true",
+                    help="spmd: broadcast the sub-cosets' h evaluations instead of exchanging coefficient slabs")
     ap.add_argument("--diverge", action="store_true",
                     help="spmd: the last rank proves with another RNG seed; every rank must refuse the proof")
     ap.add_argument("--one-variant", action="store_true",
@@ -158,7 +162,8 @@ def spmd_main(args, rank, world, native):
         if native:
             h2g.comm_spmd_install(not args.no_subcosets)
         else:
-            g = D.SpmdGather(dist, subcosets=not args.no_subcosets)
+            g = D.SpmdGather(dist, subcosets=not args.no_subcosets, slabs=not args.no_slabs,
+                             h_exchange=not args.bcast_h)
             g.install()
         if args.diverge:  # the last rank draws other randomness: the digest check must catch it
             try:
@@ -203,7 +208,9 @@ def spmd_main(args, rank, world, native):
         dist.all_gather(allok, ok)
         results[name] = {"same": all(int(a.item()) == 1 for a in allok), "same_ranks": same_ranks,
                          "bytes": len(got[0]), "gathers": None if g is None else g.calls,
-                         "bcasts": None if g is None else g.bcasts}
+                         "bcasts": None if g is None else g.bcasts,
+                         "host_gathers": None if g is None else g.host_gathers,
+                         "exchanges": None if g is None else g.exchanges}
         pk.close()
         params.close()
         dist.barrier()

@@ -341,6 +341,31 @@ def test_msm_equal_scalars_srs_identity(k):
         bases_dev.close()
 
 
+@pytest.mark.parametrize("frac", [0.5, 0.97])
+def test_msm_mixed_big_and_small_bins_srs_identity(frac):
+    """A constant run of scalars among random ones at 2^20 points: the constant's digits
+    fill a few coarse bins past the per-bin kernel's capacity (tile path, cursors rebased
+    onto their bins) while the random ones fill every bin below it (per-bin kernel) --
+    both partition paths in one MSM, generic and fixed-base windows."""
+    r = rng(400 + int(frac * 100))
+    n = 1 << 20
+    s = O.random_fr(r, 1)[0]
+    bases_dev = _srs(n, s)
+    sc = O.random_fr(r, n)
+    m = int(n * frac)
+    sc[:m] = O.random_fr(r, 1)[0]
+    want = O.g1_mul(GEN, O.eval_poly(sc, s))
+    d_sc = h2g.DevBuf.from_array(sc)
+    assert np.array_equal(h2g.msm_dev_host(d_sc.ptr, bases_dev.ptr, n), want)
+    h = h2g.base_descriptor_dev(bases_dev.ptr, n, 0)
+    try:
+        assert np.array_equal(h2g.msm_with_cached_base_dev(d_sc.ptr, n, h, 0), want)
+    finally:
+        h2g.descriptor_free(h)
+        d_sc.close()
+        bases_dev.close()
+
+
 def test_msm_profile_counts_sorted_entries():
     """h2g_profile_msm_entries: the accumulation's mixed additions are the nonzero signed
     digits -- n for scalars equal to 1 (one digit each), 0 for zeros, W n for random

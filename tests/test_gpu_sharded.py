@@ -57,23 +57,36 @@ def test_sharded_proof_three_ranks():
 
 
 def test_spmd_proof_two_and_three_ranks():
-    """SPMD: every rank proves with its slab of each MSM and the all-gathered partials, and
-    the extended domain's sub-cosets divided over the ranks (h broadcast from each owner);
-    every rank's bytes == the single-device proof.  Three ranks leave a rank without a
-    sub-coset for the degree-3 circuits (2 sub-cosets) and give one rank two of the
-    keccak-style circuit's four."""
+    """SPMD: every rank proves with its slab of each MSM and the all-gathered partials, the
+    extended domain's sub-cosets divided over the ranks (each owner interpolates its h
+    evaluations and every rank receives its coefficient slab of them), and the
+    evaluations / SHPLONK on coefficient slabs; every rank's bytes == the single-device
+    proof.  Three ranks leave a rank without a sub-coset for the degree-3 circuits (2
+    sub-cosets) and give one rank two of the keccak-style circuit's four."""
     cases = ["simple_k6", "mixed_k10", "lookup_k11", "keccak_k12", "c3_k14", "challenge_k9"]
     res = _run(2, cases, mode="spmd")
     for nm in cases:
         assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
-        assert res[nm]["gathers"] > 0 and res[nm]["bcasts"] > 0, (nm, res[nm])
+        assert res[nm]["gathers"] > 0 and res[nm]["exchanges"] > 0 and res[nm]["host_gathers"] > 0, (nm, res[nm])
+        assert res[nm]["bcasts"] == 0, (nm, res[nm])
     res = _run(3, ["simple_k6", "lookup_k11", "keccak_k12", "c3_k14"], mode="spmd")
     for nm in ("simple_k6", "lookup_k11", "keccak_k12", "c3_k14"):
         assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
-    # the MSM-only split (extended domain replicated)
+    # h broadcast as evaluations, tail on slabs; and everything but the MSMs and sub-cosets
+    # replicated (the round-2 split)
+    res = _run(2, ["lookup_k11", "c3_k14"], mode="spmd", extra=["--bcast-h"])
+    for nm in ("lookup_k11", "c3_k14"):
+        assert res[nm]["same"] and res[nm]["same_ranks"] and res[nm]["bcasts"] > 0, (nm, res[nm])
+        assert res[nm]["exchanges"] == 0 and res[nm]["host_gathers"] > 0, (nm, res[nm])
+    res = _run(3, ["keccak_k12", "c3_k14"], mode="spmd", extra=["--no-slabs"])
+    for nm in ("keccak_k12", "c3_k14"):
+        assert res[nm]["same"] and res[nm]["same_ranks"] and res[nm]["bcasts"] > 0, (nm, res[nm])
+        assert res[nm]["host_gathers"] == 0, (nm, res[nm])
+    # the MSM-only split (extended domain replicated), tail on slabs
     res = _run(2, ["lookup_k11", "c3_k14"], mode="spmd", extra=["--no-subcosets"])
     for nm in ("lookup_k11", "c3_k14"):
         assert res[nm]["same"] and res[nm]["same_ranks"] and res[nm]["bcasts"] == 0, (nm, res[nm])
+        assert res[nm]["exchanges"] == 0, (nm, res[nm])
 
 
 def test_spmd_two_circuits_distinct_witnesses():
@@ -99,7 +112,7 @@ def test_spmd_c3_k22_at_size(world):
     (gloo ranks sharing this box's GPU); every rank's bytes == the single-GPU proof"""
     res = _run(world, ["c3_k22"], mode="spmd", extra=["--one-variant"], timeout=1100)
     assert res["c3_k22"]["same"] and res["c3_k22"]["same_ranks"], res
-    assert res["c3_k22"]["gathers"] == 11 and res["c3_k22"]["bcasts"] == 2, res
+    assert res["c3_k22"]["gathers"] == 11 and res["c3_k22"]["exchanges"] == 1, res
 
 
 @pytest.mark.timeout(1200)

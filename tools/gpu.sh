@@ -5,6 +5,7 @@
 #   tools/gpu.sh bench TAG [bench args...]    bench.py line                    -> gpurun_out/TAG/bench.json
 #   tools/gpu.sh prof  TAG [bench args...]    rocprofv3 --kernel-trace --stats of bench.py
 #   tools/gpu.sh pmc   TAG [bench args...]    one rocprofv3 --pmc pass per counter (FETCH_SIZE, WRITE_SIZE)
+#   tools/gpu.sh pmcbin TAG binary [args]    a standalone binary under the two --pmc passes
 #   tools/gpu.sh py    TAG script.py [args]   any python script (A/B runs, microbenchmarks)
 set -o pipefail
 CMD=$1; TAG=$2; shift 2
@@ -32,6 +33,13 @@ case "$CMD" in
         python3 "$R/bench.py" --no-cpu-baseline --no-pmc --no-krange "$@" > "$O/pmc_$C.log" 2>&1 || { echo "pmc $C failed"; exit 1; }
     done
     echo pmc ok ;;
+  pmcbin)  # a standalone binary under one --pmc pass per counter (tools/microbench/pmc_calib)
+    B=$1; shift
+    cd /tmp
+    for C in FETCH_SIZE WRITE_SIZE; do
+      timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$O/pmc_$C" -o pmc -- "$R/$B" "$@" > "$O/pmc_$C.log" 2>&1 || { echo "pmc $C failed"; exit 1; }
+    done
+    cat "$O/pmc_FETCH_SIZE.log"; echo pmc ok ;;
   py)
     S=$1; shift
     timeout -k 10 900 python3 -u "$S" "$@" > "$O/out.txt" 2> "$O/err.txt"

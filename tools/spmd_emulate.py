@@ -44,7 +44,7 @@ class FakeCollectives:
 
     def __init__(self, world, rank, gen):
         self.world, self.rank, self.gen = world, rank, gen
-        self.calls = self.bcasts = self.exchanges = 0
+        self.calls = self.bcasts = self.exchanges = self.xchg = self.xchg_bytes = 0
 
     def allgather(self, seq, mine):
         out = np.tile(mine, (self.world, 1))
@@ -62,8 +62,14 @@ class FakeCollectives:
         self.exchanges += 1
         return [data] * self.world
 
+    def exchange(self, d_send, send_bytes, d_recv, recv_bytes):
+        self.xchg += 1
+        self.xchg_bytes += sum(recv_bytes)
+
 
 def run(args):
+    import torch
+    torch.cuda.set_device(0)  # torch's HIP context first (as bench.py), then the library's
     h2g.init([0])
     k = args.k
     if args.workload == "keccak":
@@ -73,7 +79,6 @@ def run(args):
     params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(0x1234567), dtype=np.uint64))
     gen = G1_GEN_MONT
     pk = h2g.ProvingKey(params, circ)
-    import torch
     adv = torch.from_numpy(np.ascontiguousarray(wit.advice).view(np.int64)).cuda()
     torch.cuda.synchronize()
     n = 1 << k
@@ -92,7 +97,8 @@ def run(args):
             params.set_slab(*D.slab(n, args.world, r))
         fc = FakeCollectives(args.world, r, gen)
         h2g.set_spmd_transport(args.world, r, fc.allgather, None if args.no_subcosets else fc.bcast,
-                               None if args.no_slabs else fc.allgather_host)
+                               None if args.no_slabs else fc.allgather_host,
+                               None if (args.no_slabs or args.no_subcosets or args.bcast_h) else fc.exchange)
         try:
             for _ in range(args.warmup):
                 pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())
@@ -112,6 +118,8 @@ def run(args):
                            "gathers_per_proof": fc.calls // (args.warmup + args.steps + 1),
                            "bcasts_per_proof": fc.bcasts // (args.warmup + args.steps + 1),
                            "host_gathers_per_proof": fc.exchanges // (args.warmup + args.steps + 1),
+                           "h_exchanges_per_proof": fc.xchg // (args.warmup + args.steps + 1),
+                           "h_exchange_recv_bytes": fc.xchg_bytes // max(fc.xchg, 1),
                            "stages_ms_synced": {nm: round(ms, 3) for nm, ms in stages}}
         print(json.dumps({"rank": r, **out["ranks"][r]}), flush=True)
     if args.world > 1:
@@ -134,6 +142,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-subcosets", action="store_true")
     ap.add_argument("--no-slabs", action="store_true", help="replicate the multi-open tail")
+    ap.add_argument("--bcast-h", action="store_true", help="broadcast h evaluations (no slab exchange)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     res = run(args)

@@ -214,6 +214,36 @@ int comm_allgather_host(void* ctx, const void* in, size_t bytes, void* out) {
   return H2G_OK;
 }
 
+// h(X)'s coefficient slabs from the sub-coset owners: one group of sends and receives on
+// the slab communicator, the rank's own block a device copy
+int comm_exchange(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv, const size_t* recv_bytes) {
+  Comm* c = static_cast<Comm*>(ctx);
+  if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm: no communicator for the SPMD exchange");
+  HIPCHK(hipSetDevice(c->device));
+  const int W = c->world;
+  size_t so = 0, ro = 0;
+  NCCLCHK(ncclGroupStart());
+  for (int p = 0; p < W; p++) {
+    const uint8_t* sp = static_cast<const uint8_t*>(d_send) + so;
+    uint8_t* rp = static_cast<uint8_t*>(d_recv) + ro;
+    if (p == c->rank) {
+      if (send_bytes[p] != recv_bytes[p]) {
+        (void)ncclGroupEnd();
+        return fail(H2G_ERR_ARG, "comm_exchange: own block sizes differ");
+      }
+      if (send_bytes[p]) HIPCHK(hipMemcpyAsync(rp, sp, send_bytes[p], hipMemcpyDeviceToDevice, c->stx));
+    } else {
+      if (send_bytes[p]) NCCLCHK(ncclSend(sp, send_bytes[p], ncclUint8, p, c->tx, c->stx));
+      if (recv_bytes[p]) NCCLCHK(ncclRecv(rp, recv_bytes[p], ncclUint8, p, c->tx, c->stx));
+    }
+    so += send_bytes[p];
+    ro += recv_bytes[p];
+  }
+  NCCLCHK(ncclGroupEnd());
+  HIPCHK(hipStreamSynchronize(c->stx));
+  return H2G_OK;
+}
+
 int comm_bcast(void* ctx, void* d_buf, size_t bytes, int root) {
   Comm* c = static_cast<Comm*>(ctx);
   if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm: no communicator for the SPMD broadcast");

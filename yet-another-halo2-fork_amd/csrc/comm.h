@@ -47,6 +47,8 @@ void* comm_spmd_ctx();
 int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[H2G_SPMD_WORDS], uint64_t* out);
 // SPMD: `bytes` host bytes from every rank, out = world x bytes in rank order
 int comm_allgather_host(void* ctx, const void* in, size_t bytes, void* out);
+// SPMD: all-to-all of device bytes with per-peer counts (grouped send / receive)
+int comm_exchange(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv, const size_t* recv_bytes);
 // in-place broadcast of device memory from `root` (the sub-coset h evaluations)
 int comm_bcast(void* ctx, void* d_buf, size_t bytes, int root);
 

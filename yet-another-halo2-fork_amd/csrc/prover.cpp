@@ -210,6 +210,9 @@ struct ProvingKey {
   // SPMD coefficient slabs: per SHPLONK point a (slab + halo) combination buffer
   Fr* slab_buf = nullptr;
   size_t slab_buf_len = 0;
+  // SPMD h(X) by slabs (h2g_spmd_transport.exchange): send / receive staging
+  Fr *x_send = nullptr, *x_recv = nullptr;
+  size_t x_send_len = 0, x_recv_len = 0;
   uint32_t* d_seeds = nullptr;
   uint64_t* d_offsets = nullptr;
   int max_chunks = 0;
@@ -923,6 +926,97 @@ int ext_cosets(Device* d, const ProvingKey& pk, const Fr* const* src, Fr* const*
     RCCHK(ntt_dev_impl_batch(d, s2.data() + b0, n, d2.data() + b0, (int)std::min<size_t>(NTT_MAX_BATCH, s2.size() - b0),
                              n, (int)pk.dom.k, pk.dom.omega, 1, pk.dom.g_coset, pk.dom.g_coset_inv, 0, one, 0, one,
                              one, st));
+  return H2G_OK;
+}
+
+// SPMD h(X) by coefficient slabs (h2g_spmd_transport.exchange): the owner of sub-coset t
+// holds h's evaluations H(zeta w_ext^t w^m) in h_gather slot t.  An n-point inverse NTT
+// (1/n, times zeta^-j) and the twist w_ext^(-t j) give the folded coefficients
+// F_t[j] = sum_p h_{j+np} zeta^(np) rho^(t p) (rho = w_ext^n); slab r of every F_t goes
+// to rank r, which inverts the E-point transform over t for its coefficients:
+// h_{j+np} = zeta^(-np) E^-1 sum_t rho^(-t p) F_t[j] (extended_to_coeff, domain.rs:271-293,
+// split into pieces of n, vanishing/prover.rs:122-128).  Exact, so the pieces equal the
+// single-GPU ones.
+int h_by_slabs(Device* d, ProvingKey& pk, const Slab& sl, hipStream_t st) {
+  const Domain& D = pk.dom;
+  const size_t n = pk.n, ext = pk.ext;
+  const int W = g_spmd.world, me = g_spmd.rank;
+  const int e = (int)(D.ek - D.k);
+  const int E = 1 << e;
+  const int np = pk.degree - 1;
+  if (E > HSLAB_MAX_E || np > E) return fail(H2G_ERR_ARG, "create_proof: too many sub-cosets for the h slab exchange");
+  const size_t nt = pk.sub_ts.size();
+  // sizes: slab r of each owned sub-coset to rank r; every owner's blocks to me
+  std::vector<size_t> sb(W), rb(W), soff(W + 1, 0);
+  std::vector<Slab> slabs(W);
+  for (int r = 0; r < W; r++) {
+    slabs[r] = spmd_slab(n, r);
+    sb[r] = nt * (slabs[r].hi1 - slabs[r].lo) * sizeof(Fr);
+    soff[r + 1] = soff[r] + sb[r] / sizeof(Fr);
+    int own = 0;
+    for (int t = r; t < E; t += W) own++;
+    rb[r] = (size_t)own * (sl.hi1 - sl.lo) * sizeof(Fr);
+  }
+  size_t rtot = 0;
+  for (int r = 0; r < W; r++) rtot += rb[r] / sizeof(Fr);
+  if (soff[W] > pk.x_send_len) {
+    PALLOC(pk.pool, pk.x_send, soff[W]);
+    pk.x_send_len = soff[W];
+  }
+  if (rtot > pk.x_recv_len) {
+    PALLOC(pk.pool, pk.x_recv, rtot);
+    pk.x_recv_len = rtot;
+  }
+  const Fr one = Fr::one();
+  for (size_t i = 0; i < nt; i++) {
+    const uint64_t t = pk.sub_ts[i];
+    Fr* f = pk.h_coeff + i * n;  // scratch until the combine
+    RCCHK(ntt_dev_impl(d, pk.h_gather + t * n, n, f, n, (int)D.k, D.omega_inv, 0, one, one, 1, D.ifft_div, 1,
+                       D.g_coset_inv, D.g_coset, st));
+    HIPCHK(subcoset_twist(f, f, n, pk.eo, (ext - t) & (ext - 1), ext - 1, st));
+    for (int r = 0; r < W; r++) {
+      const size_t cnt = slabs[r].hi1 - slabs[r].lo;
+      if (cnt)
+        HIPCHK(hipMemcpyAsync(pk.x_send + soff[r] + i * cnt, f + slabs[r].lo, cnt * sizeof(Fr), hipMemcpyDeviceToDevice,
+                              st));
+    }
+  }
+  // combine coefficients coef[p E + t] = zeta^(-n p) rho^(-t p) / E
+  std::vector<Fr> coef((size_t)np * E);
+  {
+    Fr ef = Fr::zero();
+    for (int i = 0; i < E; i++) ef = ef + one;
+    const Fr einv = inv(ef);
+    const Fr rho_inv = inv(pow_u64(D.ext_omega, n));
+    const Fr zinv_n = pow_u64(inv(zeta()), n);
+    Fr zp = einv;
+    for (int p = 0; p < np; p++) {
+      Fr w = zp;
+      const Fr step = pow_u64(rho_inv, (uint64_t)p);
+      for (int t = 0; t < E; t++) {
+        coef[(size_t)p * E + t] = w;
+        w = w * step;
+      }
+      zp = zp * zinv_n;
+    }
+  }
+  HIPCHK(hipMemcpyAsync(pk.small, coef.data(), coef.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));  // the send staging is complete; coef (host) was read
+  if (g_spmd.exchange(g_spmd.ctx, pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
+    return fail(H2G_ERR_STATE, "spmd transport: exchange of h slabs failed");
+  HSlabArgs a;
+  a.recv = pk.x_recv;
+  int pos = 0;
+  for (int o = 0; o < W; o++)
+    for (int t = o; t < E; t += W) a.idx[t] = pos++;
+  a.E = E;
+  a.np = np;
+  a.cnt = sl.hi1 - sl.lo;
+  a.n = n;
+  a.lo = sl.lo;
+  a.coef = pk.small;
+  a.out = pk.h_coeff;
+  HIPCHK(h_slab_combine(a, st));
   return H2G_OK;
 }
 
@@ -1777,6 +1871,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   // ---- evaluate_h (evaluation.rs:317-620): one launch per circuit, each continuing the
   // previous circuit's Horner chain in y; the last one divides by t(X)
   const bool subc = spmd_subcosets();
+  const bool h_slabs = subc && slabs && g_spmd.exchange != nullptr;
   for (int ci = 0; ci < ncirc && !subc; ci++) {
     const CircuitWs& w = *W[ci];
     EvalHArgs a;
@@ -1862,16 +1957,21 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         HIPCHK(evaluate_h(a, st));
       }
     }
-    HIPCHK(hipStreamSynchronize(st));
-    for (uint64_t t = 0; t < (1ull << e); t++)
-      if (g_spmd.bcast(g_spmd.ctx, pk.h_gather + t * n, n * sizeof(Fr), (int)(t % (uint64_t)g_spmd.world)) != 0)
-        return fail(H2G_ERR_STATE, "spmd transport: broadcast of sub-coset " + std::to_string(t) + " failed");
-    HIPCHK(subcoset_scatter(pk.h_gather, pk.h_ext, n, e, st));
+    if (h_slabs) {
+      RCCHK(h_by_slabs(d, pk, sl, st));
+    } else {
+      HIPCHK(hipStreamSynchronize(st));
+      for (uint64_t t = 0; t < (1ull << e); t++)
+        if (g_spmd.bcast(g_spmd.ctx, pk.h_gather + t * n, n * sizeof(Fr), (int)(t % (uint64_t)g_spmd.world)) != 0)
+          return fail(H2G_ERR_STATE, "spmd transport: broadcast of sub-coset " + std::to_string(t) + " failed");
+      HIPCHK(subcoset_scatter(pk.h_gather, pk.h_ext, n, e, st));
+    }
   }
-  dump("h_ext", pk.h_ext, ext, st);
+  if (!h_slabs) dump("h_ext", pk.h_ext, ext, st);
   clk.mark("evaluate_h");
-  // ---- vanishing construct (vanishing/prover.rs:102-155): h(X) pieces of size n
-  RCCHK(extended_to_coeff(d, D, pk.h_ext, pk.h_coeff, st));
+  // ---- vanishing construct (vanishing/prover.rs:102-155): h(X) pieces of size n (a rank
+  // that received h by slabs holds its slab of each piece already)
+  if (!h_slabs) RCCHK(extended_to_coeff(d, D, pk.h_ext, pk.h_coeff, st));
   const int npieces = pk.degree - 1;
   for (int p = 0; p < npieces; p++) (void)rng.random_fr();  // h blinds
   RCCHK(rng_ok());
@@ -3011,7 +3111,7 @@ int h2g_set_shard_transport(const h2g_shard_transport* t) {
   if (t && t->world > 1) {
     if (!t->launch || !t->collect || t->world > 4096) return fail(H2G_ERR_ARG, "set_shard_transport: bad transport");
     g_shard = *t;
-    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr};
+    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr, nullptr};
   } else {
     g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   }
@@ -3027,7 +3127,7 @@ int h2g_set_spmd_transport(const h2g_spmd_transport* t) {
     g_spmd = *t;
     g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   } else {
-    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr};
+    g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr, nullptr};
   }
   g_spmd_seq = 0;
   return H2G_OK;
@@ -3107,7 +3207,7 @@ int h2g_comm_init(const uint8_t id[256], int world, int rank) {
 int h2g_comm_destroy(void) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (g_shard.launch == comm_launch) g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
-  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr};
+  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr, nullptr};
   return comm_destroy();
 }
 
@@ -3115,7 +3215,8 @@ int h2g_comm_spmd_install(int split_subcosets) {
   NEED_DEV_P();
   if (comm_world() < 2) return fail(H2G_ERR_STATE, "comm_spmd_install: needs a communicator (h2g_comm_init)");
   g_spmd = h2g_spmd_transport{comm_spmd_ctx(), comm_world(), comm_rank(), comm_allgather_partial,
-                              split_subcosets ? comm_bcast : nullptr, comm_allgather_host};
+                              split_subcosets ? comm_bcast : nullptr, comm_allgather_host,
+                              split_subcosets ? comm_exchange : nullptr};
   g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   g_spmd_seq = 0;
   return H2G_OK;
@@ -3123,7 +3224,7 @@ int h2g_comm_spmd_install(int split_subcosets) {
 
 int h2g_comm_spmd_uninstall(void) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
-  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr};
+  if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr, nullptr};
   g_spmd_seq = 0;
   return H2G_OK;
 }

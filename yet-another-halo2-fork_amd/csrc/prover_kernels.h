@@ -91,6 +91,18 @@ hipError_t subcoset_twist(const Fr* src, Fr* dst, size_t n, const PowTable& eo, 
 hipError_t subcoset_gather(const Fr* full, Fr* out, size_t n, uint64_t t, int e, hipStream_t st);
 hipError_t subcoset_scatter(const Fr* subs, Fr* ext, size_t n, int e, hipStream_t st);
 int evaluate_h_max_slots();
+// SPMD: this rank's slab [lo, lo + cnt) of the h pieces (out[p n + j], p < np) from the E
+// sub-cosets' folded coefficients F_t (recv + idx[t] cnt); coef: np x E device matrix
+static constexpr int HSLAB_MAX_E = 16;
+struct HSlabArgs {
+  const Fr* recv = nullptr;
+  int idx[HSLAB_MAX_E] = {};
+  int E = 0, np = 0;
+  uint64_t cnt = 0, n = 0, lo = 0;
+  const Fr* coef = nullptr;
+  Fr* out = nullptr;
+};
+hipError_t h_slab_combine(const HSlabArgs& a, hipStream_t st);
 
 // Lagrange-basis compression of an expression list (lookup/prover.rs:85-103,
 // shuffle/prover.rs:45-66): out[i] = fold_e (acc * theta + e(row i)), rotations mod n

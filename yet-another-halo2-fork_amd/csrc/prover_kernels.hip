@@ -799,6 +799,26 @@ hipError_t subcoset_scatter(const Fr* subs, Fr* ext, size_t n, int e, hipStream_
   return hipGetLastError();
 }
 
+// h(X)'s slab from the sub-coset owners' folded coefficients (SPMD, h2g_spmd_transport
+// exchange): F_t[j] = sum_p h_{j+np} zeta^(np) rho^(t p) (rho = w_ext^n, t < E) for j in
+// this rank's slab; h_{j+np} = sum_t coef[p E + t] F_t[j] with coef = zeta^(-np) rho^(-tp) / E
+__global__ void __launch_bounds__(KT) h_slab_combine_kernel(HSlabArgs a) {
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < a.cnt; j += (uint64_t)gridDim.x * blockDim.x) {
+    Fr f[HSLAB_MAX_E];
+    for (int t = 0; t < a.E; t++) f[t] = ldf(a.recv + (uint64_t)a.idx[t] * a.cnt + j);
+    for (int p = 0; p < a.np; p++) {
+      Fr acc = Fr::zero();
+      for (int t = 0; t < a.E; t++) acc = acc + ldf(a.coef + p * a.E + t) * f[t];
+      stf(a.out + (uint64_t)p * a.n + a.lo + j, acc);
+    }
+  }
+}
+hipError_t h_slab_combine(const HSlabArgs& a, hipStream_t st) {
+  if (a.cnt == 0 || a.np == 0) return hipSuccess;
+  hipLaunchKernelGGL(h_slab_combine_kernel, dim3(grid_1d(a.cnt)), dim3(KT), 0, st, a);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ keygen helpers
 __global__ void __launch_bounds__(KT) sigma_kernel(Fr* __restrict__ sigma, const uint32_t* __restrict__ mc,
                                                    const uint32_t* __restrict__ mr, size_t n,

@@ -860,15 +860,16 @@ SPMD_WORDS = 13  # H2G_SPMD_WORDS (include/h2g.h)
 SPMD_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, VP, U64, U64P, U64P)
 SPMD_BCAST = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, SZ, ctypes.c_int)
 SPMD_ALLGATHER_HOST = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, SZ, VP)
+SPMD_EXCHANGE = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, ctypes.POINTER(SZ), VP, ctypes.POINTER(SZ))
 
 
 class SpmdTransport(ctypes.Structure):
     """struct h2g_spmd_transport (include/h2g.h)"""
     _fields_ = [("ctx", VP), ("world", ctypes.c_int32), ("rank", ctypes.c_int32), ("allgather", SPMD_ALLGATHER),
-                ("bcast", SPMD_BCAST), ("allgather_host", SPMD_ALLGATHER_HOST)]
+                ("bcast", SPMD_BCAST), ("allgather_host", SPMD_ALLGATHER_HOST), ("exchange", SPMD_EXCHANGE)]
 
 
-def set_spmd_transport(world, rank=0, allgather=None, bcast=None, allgather_host=None):
+def set_spmd_transport(world, rank=0, allgather=None, bcast=None, allgather_host=None, exchange=None):
     """SPMD sharding: every rank runs the same create_proof and computes its point slab of
     each commitment MSM; allgather(seq, mine: uint64[SPMD_WORDS]) -> uint64[world, SPMD_WORDS]
     (rank order) collects the partials (8 affine limbs, identity flag, 4 words of the
@@ -876,6 +877,8 @@ def set_spmd_transport(world, rank=0, allgather=None, bcast=None, allgather_host
     domain's sub-cosets over the ranks and broadcasts each one's h evaluations (device
     memory, in place).  allgather_host(data: bytes) -> world byte strings in rank order
     (optional) runs the evaluations and the SHPLONK multi-open on coefficient slabs.
+    exchange(d_send, send_bytes, d_recv, recv_bytes) (optional, with both): all-to-all of
+    device memory with per-peer byte lists -- h(X) then travels as coefficient slabs.
     world <= 1 removes it.  Exceptions fail the proof."""
     global _transport_keep
     if world <= 1:
@@ -912,11 +915,21 @@ def set_spmd_transport(world, rank=0, allgather=None, bcast=None, allgather_host
             _transport_keep[-1].append(e)
             return 1
 
+    def _ex(ctx, d_send, sbytes, d_recv, rbytes):
+        try:
+            exchange(int(d_send or 0), [int(sbytes[i]) for i in range(world)], int(d_recv or 0),
+                     [int(rbytes[i]) for i in range(world)])
+            return 0
+        except Exception as e:  # noqa: BLE001
+            _transport_keep[-1].append(e)
+            return 1
+
     cb = SPMD_ALLGATHER(_ag)
     cbb = SPMD_BCAST(_bc) if bcast is not None else ctypes.cast(None, SPMD_BCAST)
     cbh = SPMD_ALLGATHER_HOST(_agh) if allgather_host is not None else ctypes.cast(None, SPMD_ALLGATHER_HOST)
-    t = SpmdTransport(None, world, rank, cb, cbb, cbh)
-    _transport_keep = (t, cb, cbb, cbh, [])
+    cbx = SPMD_EXCHANGE(_ex) if exchange is not None else ctypes.cast(None, SPMD_EXCHANGE)
+    t = SpmdTransport(None, world, rank, cb, cbb, cbh, cbx)
+    _transport_keep = (t, cb, cbb, cbh, cbx, [])
     check(lib().h2g_set_spmd_transport(ctypes.byref(t)))
 
 

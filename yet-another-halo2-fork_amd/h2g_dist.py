@@ -191,7 +191,7 @@ class SpmdGather:
     coefficient slabs joined by small host all-gathers (allgather_host).
     h2g_comm_spmd_install is the same over the library's own RCCL communicator."""
 
-    def __init__(self, dist, group=None, subcosets=True, slabs=True):
+    def __init__(self, dist, group=None, subcosets=True, slabs=True, h_exchange=True):
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
@@ -199,9 +199,11 @@ class SpmdGather:
         self.device = _staging(dist, group)
         self.subcosets = subcosets
         self.slabs = slabs
+        self.h_exchange = h_exchange
         self.calls = 0
         self.bcasts = 0
         self.host_gathers = 0
+        self.exchanges = 0
 
     def allgather_host(self, data):
         """the multi-open tail's scalars: `data` (bytes) from every rank, rank order"""
@@ -239,10 +241,51 @@ class SpmdGather:
             h2g.memcpy_dtod(d_ptr, t.data_ptr(), nbytes)
         self.bcasts += 1
 
+    def exchange(self, d_send, send_bytes, d_recv, recv_bytes):
+        """all-to-all of device bytes (h(X)'s coefficient slabs from the sub-coset owners):
+        torch device tensors over RCCL (all_to_all_single), host tensors and point-to-point
+        messages over gloo"""
+        import h2g
+        import torch
+        W = self.world
+        so = [sum(send_bytes[:p]) for p in range(W)]
+        ro = [sum(recv_bytes[:p]) for p in range(W)]
+        tot_s, tot_r = sum(send_bytes), sum(recv_bytes)
+        if self.device.type == "cuda":
+            sb = torch.empty(max(tot_s, 1), dtype=torch.uint8, device="cuda")
+            rb = torch.empty(max(tot_r, 1), dtype=torch.uint8, device="cuda")
+            if tot_s:
+                h2g.memcpy_dtod(sb.data_ptr(), d_send, tot_s)
+            self.dist.all_to_all_single(rb[:tot_r], sb[:tot_s], list(recv_bytes), list(send_bytes), group=self.group)
+            torch.cuda.synchronize()
+            if tot_r:
+                h2g.memcpy_dtod(d_recv, rb.data_ptr(), tot_r)
+        else:
+            sb = torch.empty(max(tot_s, 1), dtype=torch.uint8)
+            rb = torch.empty(max(tot_r, 1), dtype=torch.uint8)
+            if tot_s:
+                h2g.memcpy_dtoh(sb.data_ptr(), d_send, tot_s)
+            ops = []
+            for p in range(W):
+                if p == self.rank:
+                    rb[ro[p]:ro[p] + recv_bytes[p]] = sb[so[p]:so[p] + send_bytes[p]]
+                    continue
+                if send_bytes[p]:
+                    ops.append(self.dist.P2POp(self.dist.isend, sb[so[p]:so[p] + send_bytes[p]], p, self.group))
+                if recv_bytes[p]:
+                    ops.append(self.dist.P2POp(self.dist.irecv, rb[ro[p]:ro[p] + recv_bytes[p]], p, self.group))
+            if ops:
+                for w in self.dist.batch_isend_irecv(ops):
+                    w.wait()
+            if tot_r:
+                h2g.memcpy_htod(d_recv, rb.data_ptr(), tot_r)
+        self.exchanges += 1
+
     def install(self):
         import h2g
         h2g.set_spmd_transport(self.world, self.rank, self.allgather, self.bcast if self.subcosets else None,
-                               self.allgather_host if self.slabs else None)
+                               self.allgather_host if self.slabs else None,
+                               self.exchange if (self.subcosets and self.slabs and self.h_exchange) else None)
 
     @staticmethod
     def uninstall():
