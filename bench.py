@@ -334,9 +334,10 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     one_proof = shard or spmd
     worker = shard and rank != 0
     seed_off = 0 if one_proof else rank  # ranks of one proof hold the same SRS and witness
+    spmd_weights = {"w": None}
     s_int = 0x1234567 + seed_off
     params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(s_int), dtype=np.uint64))
-    if one_proof:  # fixed-base windows sized for this rank's point slab
+    if shard:  # fixed-base windows sized for this rank's point slab (spmd: after keygen, weighted)
         params.set_slab(*h2g_dist.slab(n, world, rank))
     native = one_proof and args.transport == "native"
     transport_note = None
@@ -367,6 +368,12 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         else:
             circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=3 + seed_off)
         pk = h2g.ProvingKey(params, circ)
+        if spmd:  # lighter slabs for the ranks that own extended-domain sub-cosets
+            weights = h2g_dist.owner_weights(world, pk.extended_k, k, args.spmd_owner_weight) \
+                if args.spmd_owner_weight > 0 else None
+            h2g.spmd_set_weights(weights)
+            params.set_slab(*h2g_dist.slab(n, world, rank, weights=weights))
+            spmd_weights["w"] = weights
         adv = torch.from_numpy(np.ascontiguousarray(wit.advice).view(np.int64)).to(dev)  # resident witness
         client = h2g_dist.SlabClient(dist, points=n) if shard and not native else None
         gather = h2g_dist.SpmdGather(dist, subcosets=not args.no_subcosets) if spmd and not native else None
@@ -523,6 +530,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             line["pcie_inclusive_s"] = pcie["median_s"]
         if spmd:
             line["proof_bytes_equal_across_ranks"] = extra["ranks_equal"]
+            line["config"]["spmd_slab_weights"] = spmd_weights["w"]
         if transport_note:
             line["transport_note"] = transport_note
     if args.workload == "prove" and (world == 1 or dist.get_backend() == "nccl"):
@@ -741,6 +749,8 @@ def main():
                          "(spmd) or rank 0 proves and peers serve slabs (shard) -- or one proof per GPU (replicas)")
     ap.add_argument("--no-subcosets", action="store_true",
                     help="spmd: replicate the extended-domain work instead of splitting its sub-cosets")
+    ap.add_argument("--spmd-owner-weight", type=float, default=0.5,
+                    help="spmd: slab weight of the sub-coset owners against 1 for the other ranks (0: uniform)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3, help="CPU baseline runs (median)")
     ap.add_argument("--no-krange", action="store_true",

@@ -432,6 +432,13 @@ typedef struct {
 } h2g_spmd_transport;
 /* install (world >= 2) or remove (NULL or world <= 1) */
 int h2g_set_spmd_transport(const h2g_spmd_transport* t);
+/* SPMD slab partition (optional): rank r's slab -- of every commitment MSM and of the
+ * multi-open tail's coefficients -- is [P S_r / S, P S_{r+1} / S) with S_r = weights[0] +
+ * ... + weights[r - 1] and S their total, instead of [P r / world, P (r + 1) / world).
+ * Every rank must pass the same weights, and its h2g_params_set_slab the same slab.  The
+ * ranks that own extended-domain sub-cosets carry that extra work; smaller slabs balance
+ * them against the others.  NULL (or world <= 1) restores the uniform partition. */
+int h2g_spmd_set_weights(const uint32_t* weights, int world);
 /* split_subcosets: 1 divides the extended domain's sub-cosets over the ranks (bcast over
  * the communicator), 0 replicates that work; the multi-open tail always runs on
  * coefficient slabs (allgather_host over the communicator) */

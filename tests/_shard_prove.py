@@ -65,6 +65,7 @@ def main():
                     help="spmd: replicate the evaluations / SHPLONK tail (no host all-gather)")
     ap.add_argument("--bcast-h", action="store_true",
                     help="spmd: broadcast the sub-cosets' h evaluations instead of exchanging coefficient slabs")
+    ap.add_argument("--weights", default="", help="spmd: slab weights (h2g.spmd_set_weights), comma separated")
     ap.add_argument("--diverge", action="store_true",
                     help="spmd: the last rank proves with another RNG seed; every rank must refuse the proof")
     ap.add_argument("--one-variant", action="store_true",
@@ -150,12 +151,14 @@ def spmd_main(args, rank, world, native):
     import hashlib
     results = {}
     variants = [{}] if args.one_variant else [{}, {"seed": bytes(range(32)), "vanishing_threads": 3}]
+    weights = [int(x) for x in args.weights.split(",")] if args.weights else None
+    h2g.spmd_set_weights(weights)
     for name in args.cases:
         case = CASES[name]()
         circ = case[0]
         params = h2g.Params(circ.k, s=np.asarray(hc.fr_to_limbs(0x5eed + circ.k), dtype=np.uint64))
         P = 1 << circ.k
-        params.set_slab(*D.slab(P, world, rank))
+        params.set_slab(*D.slab(P, world, rank, weights=weights))
         pk = h2g.ProvingKey(params, circ)
         want = [_prove(pk, case, **kw) for kw in variants]
         g = None

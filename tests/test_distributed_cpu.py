@@ -180,3 +180,54 @@ def test_spmd_gather_gloo(world):
     for rank, totals, calls in out:
         assert totals == want, rank
         assert calls == len(jobs)
+
+
+# ---------------------------------------------------------------- SPMD slab partition
+def test_weighted_slabs_partition_the_points():
+    """h2g_dist.slab with SPMD weights (h2g_spmd_set_weights): contiguous, disjoint,
+    covering, proportional to the weights; owner_weights lightens the sub-coset owners"""
+    import h2g_dist as D
+    P = 1 << 22
+    for world, w in [(8, D.owner_weights(8, 23, 22)), (3, [3, 1, 2]), (4, None)]:
+        sl = [D.slab(P, world, r, weights=w) for r in range(world)]
+        assert sl[0][0] == 0 and sl[-1][1] == P
+        assert all(sl[r][1] == sl[r + 1][0] for r in range(world - 1))
+        ws = w or [1] * world
+        for r in range(world):
+            assert abs((sl[r][1] - sl[r][0]) - P * ws[r] / sum(ws)) <= 1
+        # an MSM shorter than P: the same boundaries clipped to its length
+        assert [D.slab(P - 1, world, r, P, w) for r in range(world)][-1][1] == P - 1
+    assert D.owner_weights(8, 23, 22) == [50, 50] + [100] * 6
+    assert D.owner_weights(2, 23, 22) is None  # every rank owns a sub-coset
+    assert D.owner_weights(8, 20, 18) == [50] * 4 + [100] * 4
+
+
+def _host_gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import h2g_dist as D
+        g = D.SpmdGather(dist)
+        parts = g.allgather_host(bytes([rank]) * (5 + rank % 1))
+        q.put((rank, parts, g.host_gathers))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_spmd_host_allgather_gloo():
+    """the multi-open tail's scalar all-gather (h2g_spmd_transport.allgather_host) over gloo:
+    every rank receives every rank's bytes in rank order"""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_host_gather_worker, args=(i, world, port, q)) for i in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, parts, calls in out:
+        assert parts == [bytes([r]) * 5 for r in range(world)], rank
+        assert calls == 1

@@ -82,6 +82,11 @@ def test_spmd_proof_two_and_three_ranks():
     for nm in ("keccak_k12", "c3_k14"):
         assert res[nm]["same"] and res[nm]["same_ranks"] and res[nm]["bcasts"] > 0, (nm, res[nm])
         assert res[nm]["host_gathers"] == 0, (nm, res[nm])
+    # uneven slab weights (h2g_spmd_set_weights): the MSM slabs, the tail's coefficient
+    # slabs and the h slab exchange all follow the weighted partition
+    res = _run(3, ["lookup_k11", "keccak_k12", "c3_k14"], mode="spmd", extra=["--weights", "3,1,2"])
+    for nm in ("lookup_k11", "keccak_k12", "c3_k14"):
+        assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
     # the MSM-only split (extended domain replicated), tail on slabs
     res = _run(2, ["lookup_k11", "c3_k14"], mode="spmd", extra=["--no-subcosets"])
     for nm in ("lookup_k11", "c3_k14"):

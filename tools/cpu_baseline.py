@@ -46,8 +46,8 @@ def main():
     threading.Thread(target=heartbeat, daemon=True).start()
     h2g.init()
     model, ncpu = bench.cpu_info()
-    T = min(16, ncpu)
-    res = {"cpu_model": model, "nproc": ncpu, "threads": T, "reps": a.reps, "runs": []}
+    T, how = bench.cpu_threads()
+    res = {"cpu_model": model, "nproc": ncpu, "threads": T, "threads_from": how, "reps": a.reps, "runs": []}
     for k in [int(x) for x in a.ks.split(",")]:
         circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=3)
         params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(0x1234567), dtype=np.uint64))

@@ -92,9 +92,16 @@ def run(args):
         pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())
         single.append(time.perf_counter() - t0)
     out["single_gpu_ms"] = round(1e3 * sorted(single)[len(single) // 2], 3)
+    weights = None
+    if args.weights:
+        weights = [int(x) for x in args.weights.split(",")]
+    elif args.owner_weight:
+        weights = D.owner_weights(args.world, pk.extended_k, k, args.owner_weight)
+    out["weights"] = weights
+    h2g.spmd_set_weights(weights)
     for r in ranks:
         if args.world > 1:
-            params.set_slab(*D.slab(n, args.world, r))
+            params.set_slab(*D.slab(n, args.world, r, weights=weights))
         fc = FakeCollectives(args.world, r, gen)
         h2g.set_spmd_transport(args.world, r, fc.allgather, None if args.no_subcosets else fc.bcast,
                                None if args.no_slabs else fc.allgather_host,
@@ -143,6 +150,9 @@ def main():
     ap.add_argument("--no-subcosets", action="store_true")
     ap.add_argument("--no-slabs", action="store_true", help="replicate the multi-open tail")
     ap.add_argument("--bcast-h", action="store_true", help="broadcast h evaluations (no slab exchange)")
+    ap.add_argument("--weights", default="", help="SPMD slab weights, comma separated")
+    ap.add_argument("--owner-weight", type=float, default=0.0,
+                    help="slab weight of the sub-coset owners (h2g_dist.owner_weights), others 1")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     res = run(args)

@@ -245,41 +245,15 @@ msm_coarse_scatter_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t N
     if (rk[k] != ~0u) out[base[(uint32_t)(ent[k] >> 32) >> fb] + rk[k]] = ent[k];
 }
 
-// Round 2 has two paths.  Per-bin (default): one block per coarse bin of at most FBIN_MAX
-// entries sorts the bin by its fine key in one kernel (LDS histogram, scan, scatter of
-// the bin's entries to their keys' runs; the second read of the bin's few hundred KB
-// comes from the caches) -- no global per-key counts, no global atomics.  Tiles (the
-// round-2 path, H2G_MSM_FINE=tile, and the bins above FBIN_MAX that concentrated scalars
-// produce): tiles of FTILE entries with global per-key counts and cursors.  With
-// `only_big` the tile kernels leave the per-bin path's bins alone: a tile whose position
-// range meets no big bin returns before reading an entry.
-static constexpr int FBT = 1024;                  // threads of the per-bin kernel
-static constexpr uint32_t FBIN_MAX = 1u << 18;    // entries of a bin the per-bin kernel takes
-
-__device__ __forceinline__ bool tile_has_big_bin(uint32_t lo, uint32_t hi, const uint32_t* __restrict__ coff,
-                                                 const uint32_t* __restrict__ ccount, uint32_t ncoarse) {
-  uint32_t a = 0, b = ncoarse - 1;  // last bin with coff <= lo
-  while (a < b) {
-    const uint32_t m = (a + b + 1) >> 1;
-    if (coff[m] <= lo) a = m;
-    else b = m - 1;
-  }
-  for (uint32_t k = a; k < ncoarse && coff[k] < hi; k++)
-    if (ccount[k] > FBIN_MAX) return true;
-  return false;
-}
-
 // round 2a: per-key counts inside coarse bins: tiles of FTILE entries; entries of the
 // tile's first bin go through an LDS histogram, others (tiles straddling bins) directly
 __global__ void __launch_bounds__(FT)
 msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
-                     uint32_t* __restrict__ kcount, const uint32_t* __restrict__ coff,
-                     const uint32_t* __restrict__ ccount, uint32_t ncoarse, int only_big) {
+                     uint32_t* __restrict__ kcount) {
   __shared__ uint32_t h[1 << FB_MAX];
   const uint32_t total = *d_total;
   const uint32_t lo = blockIdx.x * FTILE;
   if (lo >= total) return;
-  if (only_big && !tile_has_big_bin(lo, min(lo + FTILE, total), coff, ccount, ncoarse)) return;
   const uint32_t nf = 1u << fb;
   for (uint32_t t = threadIdx.x; t < nf; t += FT) h[t] = 0;
   const uint32_t bin0 = (uint32_t)(in[lo] >> 32) >> fb;
@@ -289,7 +263,6 @@ msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict
     const uint32_t p = lo + k * FT + threadIdx.x;
     if (p >= total) break;
     const uint32_t key = (uint32_t)(in[p] >> 32);
-    if (only_big && ccount[key >> fb] <= FBIN_MAX) continue;  // the per-bin kernel's
     if ((key >> fb) == bin0) atomicAdd(&h[key & (nf - 1)], 1u);
     else atomicAdd(&kcount[key], 1u);
   }
@@ -298,24 +271,15 @@ msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict
     if (h[t]) atomicAdd(&kcount[(bin0 << fb) + t], h[t]);
 }
 
-// round 2b: the same tiles scattered to their keys' positions.  With only_big the cursors
-// count within the big bins only (the global scan skips the per-bin path's keys), so a
-// position is rebased onto its bin: coff[bin] + cursor - koff[first key of the bin].
+// round 2b: the same tiles scattered to their keys' positions
 __global__ void __launch_bounds__(FT)
 msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
-                        uint32_t* __restrict__ kcursor, uint64_t* __restrict__ out, const uint32_t* __restrict__ coff,
-                        const uint32_t* __restrict__ ccount, uint32_t ncoarse, const uint32_t* __restrict__ koff,
-                        int only_big) {
+                        uint32_t* __restrict__ kcursor, uint64_t* __restrict__ out) {
   __shared__ uint32_t cnt[1 << FB_MAX], base[1 << FB_MAX];
   const uint32_t total = *d_total;
   const uint32_t lo = blockIdx.x * FTILE;
   if (lo >= total) return;
-  if (only_big && !tile_has_big_bin(lo, min(lo + FTILE, total), coff, ccount, ncoarse)) return;
   const uint32_t nf = 1u << fb;
-  auto rebase = [&](uint32_t key) -> uint32_t {
-    const uint32_t b = key >> fb;
-    return only_big ? coff[b] - koff[b << fb] : 0u;
-  };
   for (uint32_t t = threadIdx.x; t < nf; t += FT) cnt[t] = 0;
   const uint32_t bin0 = (uint32_t)(in[lo] >> 32) >> fb;
   __syncthreads();
@@ -329,63 +293,17 @@ msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restr
     if (p < total) {
       ent[k] = in[p];
       const uint32_t key = (uint32_t)(ent[k] >> 32);
-      if (only_big && ccount[key >> fb] <= FBIN_MAX) continue;  // the per-bin kernel's
       if ((key >> fb) == bin0) rk[k] = atomicAdd(&cnt[key & (nf - 1)], 1u);
-      else out[rebase(key) + atomicAdd(&kcursor[key], 1u)] = ent[k];
+      else out[atomicAdd(&kcursor[key], 1u)] = ent[k];
     }
   }
   __syncthreads();
   for (uint32_t t = threadIdx.x; t < nf; t += FT)
-    if (cnt[t]) base[t] = rebase(bin0 << fb) + atomicAdd(&kcursor[(bin0 << fb) + t], cnt[t]);
+    if (cnt[t]) base[t] = atomicAdd(&kcursor[(bin0 << fb) + t], cnt[t]);
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < FPER; k++)
     if (rk[k] != ~0u) out[base[(uint32_t)(ent[k] >> 32) & (nf - 1)] + rk[k]] = ent[k];
-}
-
-// round 2, per-bin path: block b sorts coarse bin b (at most FBIN_MAX entries) by fine key
-__global__ void __launch_bounds__(FBT)
-msm_fine_bin_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ coff,
-                    const uint32_t* __restrict__ ccount, int fb, uint64_t* __restrict__ out) {
-  __shared__ uint32_t cur[1 << FB_MAX];
-  __shared__ uint32_t part[FBT];
-  const uint32_t cnt = ccount[blockIdx.x];
-  if (cnt == 0 || cnt > FBIN_MAX) return;
-  const uint32_t base = coff[blockIdx.x], nf = 1u << fb, t = threadIdx.x;
-  for (uint32_t i = t; i < nf; i += FBT) cur[i] = 0;
-  __syncthreads();
-  const uint64_t* src = in + base;
-  for (uint32_t p = t; p < cnt; p += FBT) atomicAdd(&cur[(uint32_t)(src[p] >> 32) & (nf - 1)], 1u);
-  __syncthreads();
-  // exclusive scan of cur[0, nf): thread t owns keys [t per, (t + 1) per)
-  const uint32_t per = (nf + FBT - 1) / FBT;
-  uint32_t s = 0;
-  for (uint32_t i = 0; i < per; i++) {
-    const uint32_t k = t * per + i;
-    if (k < nf) s += cur[k];
-  }
-  part[t] = s;
-  __syncthreads();
-  for (uint32_t d = 1; d < FBT; d <<= 1) {
-    const uint32_t v = t >= d ? part[t - d] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint32_t run = base + part[t] - s;
-  for (uint32_t i = 0; i < per; i++) {
-    const uint32_t k = t * per + i;
-    if (k < nf) {
-      const uint32_t c = cur[k];
-      cur[k] = run;
-      run += c;
-    }
-  }
-  __syncthreads();
-  for (uint32_t p = t; p < cnt; p += FBT) {
-    const uint64_t e = src[p];
-    out[atomicAdd(&cur[(uint32_t)(e >> 32) & (nf - 1)], 1u)] = e;
-  }
 }
 
 // 3-4. accumulation straight from the sorted entries -------------------------------
@@ -1233,13 +1151,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     const int v = e ? atoi(e) : 10;
     return v >= 4 && v <= FB_MAX ? v : 10;
   }();
-  static const bool fine_tile = [] {  // H2G_MSM_FINE=tile: the round-2 tile path for every bin (A/B)
-    const char* e = getenv("H2G_MSM_FINE");
-    return e && std::string(e) == "tile";
-  }();
   int fb = key_bits < fb_max ? key_bits : fb_max;
-  if (!fine_tile && key_bits - 8 < fb)  // the per-bin path wants >= 256 coarse bins (one block each)
-    fb = key_bits - 8 >= 4 ? key_bits - 8 : (key_bits < 4 ? key_bits : 4);
   while (fb < 13 && (((uint64_t)nbt + (1ull << fb) - 1) >> fb) > COARSE_MAX) fb++;
   const uint32_t nf = 1u << fb;
   const uint32_t ncoarse = (uint32_t)((nbt + nf - 1) >> fb);
@@ -1278,15 +1190,10 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   H2G_PHASE(1);
   if (prof && prof->entries) H2G_TRY(hipMemcpyAsync(prof->entries, d_total, 4, hipMemcpyDeviceToHost, st));
   {  // round 2: keys inside the coarse bins
-    const int only_big = fine_tile ? 0 : 1;
-    if (!fine_tile)
-      hipLaunchKernelGGL(msm_fine_bin_kernel, dim3(ncoarse), dim3(FBT), 0, st, (const uint64_t*)keys_in,
-                         (const uint32_t*)coff, (const uint32_t*)ccount, fb, keys_out);
     const unsigned tiles = (unsigned)((total + FTILE - 1) / FTILE);
     H2G_TRY(hipMemsetAsync(kcount, 0, (size_t)nbt * 4, st));
     hipLaunchKernelGGL(msm_fine_hist_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)keys_in,
-                       (const uint32_t*)d_total, fb, kcount, (const uint32_t*)coff, (const uint32_t*)ccount, ncoarse,
-                       only_big);
+                       (const uint32_t*)d_total, fb, kcount);
     hipLaunchKernelGGL(msm_scan_block_kernel, dim3(kblocks), dim3(1024), 0, st, (const uint32_t*)kcount, nbt, koff,
                        kbsum);
     hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)kbsum, kblocks, kboff,
@@ -1294,8 +1201,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     hipLaunchKernelGGL(msm_scan_add_kernel, dim3(kblocks), dim3(1024), 0, st, koff, nbt, (const uint32_t*)kboff,
                        kcursor);
     hipLaunchKernelGGL(msm_fine_scatter_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)keys_in,
-                       (const uint32_t*)d_total, fb, kcursor, keys_out, (const uint32_t*)coff, (const uint32_t*)ccount,
-                       ncoarse, (const uint32_t*)koff, only_big);
+                       (const uint32_t*)d_total, fb, kcursor, keys_out);
     H2G_TRY(hipGetLastError());
   }
   H2G_PHASE(2);

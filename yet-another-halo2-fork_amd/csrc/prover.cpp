@@ -22,10 +22,9 @@
 #include <functional>
 #include <set>
 
-#include <rocprim/rocprim.hpp>
-
 #include "comm.h"
 #include "poly.h"
+#include "radix.h"
 #include "g2.h"
 #include "prover_kernels.h"
 #include "runtime.h"
@@ -103,7 +102,7 @@ struct Query {
 // evaluate_h and the expression compressions read for this circuit.
 struct CircuitWs {
   Pool pool;
-  std::vector<Fr*> adv, adv_coset, inst_val, inst_poly, inst_coset, z, z_lag, z_coset;
+  std::vector<Fr*> adv, adv_poly, adv_coset, inst_val, inst_poly, inst_coset, z, z_lag, z_coset;
   std::vector<Fr*> lk_a, lk_s, lk_ap, lk_sp, lk_ap_poly, lk_sp_poly, lk_z, lk_z_poly, lk_zc, lk_apc, lk_spc;
   std::vector<Fr*> sh_z, sh_z_poly, sh_zc;
   const Fr** d_load_col = nullptr;      // extended-coset columns (evaluate_h)
@@ -184,11 +183,9 @@ struct ProvingKey {
   const Fr** d_sigma = nullptr;
   int NL = 0, NS = 0;  // lookups, shuffles
   Fr *tmp_a = nullptr, *tmp_b = nullptr, *one = nullptr;
-  CanonKey *ck_a = nullptr, *ck_t = nullptr, *ck_a2 = nullptr, *ck_t2 = nullptr, *ck_left = nullptr;
+  CanonKey *ck_a2 = nullptr, *ck_t2 = nullptr, *ck_left = nullptr;
   uint8_t *rep_flag = nullptr, *left_flag = nullptr;
   uint32_t *rep_rows = nullptr, *counters = nullptr;
-  void* sort_tmp = nullptr;
-  size_t sort_tmp_bytes = 0;
   // per-proof workspace (device), reused across proofs: per circuit, and shared
   std::vector<std::unique_ptr<CircuitWs>> cws;
   Fr *mod = nullptr, *pre = nullptr, *scr = nullptr, *random_poly = nullptr, *h_ext = nullptr, *h_coeff = nullptr;
@@ -207,6 +204,13 @@ struct ProvingKey {
   size_t scr_len = 0, eval_scr_len = 0;
   EvalReq* d_reqs = nullptr;
   int max_reqs = 0;
+  // permute_expression_pair's batched sort: every lookup column's canonical values, keys
+  // and row indices (ping-pong pairs), radix / compaction scratch
+  CanonKey* lkb_canon = nullptr;
+  uint64_t* lkb_key[2] = {nullptr, nullptr};
+  uint32_t* lkb_idx[2] = {nullptr, nullptr};
+  void* lkb_scr = nullptr;
+  size_t lkb_len = 0;
   // SPMD coefficient slabs: per SHPLONK point a (slab + halo) combination buffer
   Fr* slab_buf = nullptr;
   size_t slab_buf_len = 0;
@@ -339,11 +343,18 @@ void spmd_digest(uint64_t out[4]) {
   std::memcpy(out, d, 32);
 }
 
+// SPMD slab weights (h2g_spmd_set_weights): prefix sums, world + 1 entries; empty = uniform
+std::vector<uint64_t> g_spmd_wprefix;
+
 // slab r of an MSM of length n: the points [P r / world, P (r + 1) / world) of the
 // params' P = 2^k, clipped to n (one partition for every MSM length, so each rank's
-// slab windows cover all of its MSMs)
+// slab windows cover all of its MSMs); SPMD with weights: [P S_r / S, P S_{r+1} / S)
 size_t shard_lo(size_t P, size_t n, int world, int r) {
-  const size_t b = (size_t)((unsigned __int128)P * (unsigned)r / (unsigned)world);
+  size_t b;
+  if (world > 1 && world == g_spmd.world && g_spmd_wprefix.size() == (size_t)world + 1)
+    b = (size_t)((unsigned __int128)P * g_spmd_wprefix[(size_t)r] / g_spmd_wprefix[(size_t)world]);
+  else
+    b = (size_t)((unsigned __int128)P * (unsigned)r / (unsigned)world);
   return b < n ? b : n;
 }
 
@@ -691,6 +702,7 @@ int circuit_ws_add(ProvingKey& pk) {
     return hipSuccess;
   };
   HIPCHK(vec_alloc(w->adv, pk.A, n));
+  HIPCHK(vec_alloc(w->adv_poly, pk.A, n));
   HIPCHK(vec_alloc(w->adv_coset, pk.A, ext));
   HIPCHK(vec_alloc(w->inst_val, pk.I, n));
   HIPCHK(vec_alloc(w->inst_poly, pk.I, n));
@@ -1145,9 +1157,7 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
     HIPCHK(falloc(&pk.tmp_a, n));
     HIPCHK(falloc(&pk.tmp_b, n));
   }
-  if (pk.NL) {  // permute_expression_pair scratch
-    PALLOC(pool, pk.ck_a, n);
-    PALLOC(pool, pk.ck_t, n);
+  if (pk.NL) {  // permute_expression_pair scratch (the batched sort's buffers grow per proof)
     PALLOC(pool, pk.ck_a2, n);
     PALLOC(pool, pk.ck_t2, n);
     PALLOC(pool, pk.ck_left, n);
@@ -1155,19 +1165,7 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
     PALLOC(pool, pk.left_flag, n);
     PALLOC(pool, pk.rep_rows, n);
     PALLOC(pool, pk.counters, 8);
-    size_t b1 = 0, b2 = 0, b3 = 0;
-    HIPCHK(rocprim::merge_sort(nullptr, b1, pk.ck_a, pk.ck_a2, (int)n, CanonLess(), st));
-    HIPCHK(rocprim::select(nullptr, b2, pk.ck_t2, pk.left_flag, pk.ck_left, pk.counters, (int)n, st));
-    HIPCHK(rocprim::select(nullptr, b3, rocprim::counting_iterator<uint32_t>(0), pk.rep_flag,
-                                         pk.rep_rows, pk.counters + 1, (int)n, st));
-    size_t b4 = 0, b5 = 0;
-    HIPCHK(rocprim::radix_sort_keys(nullptr, b4, (uint64_t*)pk.ck_a, (uint64_t*)pk.ck_a + n, (int)n, 0, 64,
-                                             st));
-    HIPCHK(rocprim::radix_sort_pairs(nullptr, b5, (uint64_t*)pk.ck_left, (uint64_t*)pk.ck_left + n,
-                                              (uint32_t*)pk.ck_a, (uint32_t*)pk.ck_a + n, (int)n, 0, 48, st));
-    pk.sort_tmp_bytes = std::max(std::max(std::max(b1, b4), b5), std::max(b2, b3));
     pk.lk_hb.assign(pk.NL, 64);
-    HIPCHK(pool.get(&pk.sort_tmp, pk.sort_tmp_bytes));
   }
 
   // fixed columns
@@ -1485,6 +1483,22 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
                                   tk.data() + (size_t)ci * cols.size()));
       }
     }
+    // the phase's advice to coefficient form and its extended-domain cosets do not depend
+    // on any challenge: queued behind the uploads, they run while the commitment MSMs
+    // (their own streams) are in flight (lagrange_to_coeff, prover.rs:673-689; the
+    // cosets of evaluation.rs:344-361)
+    for (int ci = 0; ci < ncirc && !cols.empty(); ci++) {
+      CircuitWs& w = *W[ci];
+      std::vector<const Fr*> src;
+      std::vector<Fr*> dst, cst;
+      for (int c : cols) {
+        src.push_back(w.adv[c]);
+        dst.push_back(w.adv_poly[c]);
+        cst.push_back(w.adv_coset[c]);
+      }
+      RCCHK(lagrange_to_coeff_batch(d, D, src.data(), dst.data(), (int)cols.size(), st));
+      RCCHK(ext_cosets(d, pk, (const Fr* const*)dst.data(), cst.data(), (int)cols.size(), st));
+    }
     if (ph == 0) clk.mark("upload+instances");
     for (auto& t : tk) {  // circuit by circuit, column by column
       G1Affine cm;
@@ -1542,54 +1556,39 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     }
     if ((int)pk.lk_hb.size() < NLT) pk.lk_hb.resize(NLT, 64);
     if (NLT) HIPCHK(hipMemsetAsync(pk.lk_or_d, 0, (size_t)NLT * LKF * sizeof(unsigned long long), st));
-    // permute_expression_pair: sort by Ord (canonical value), match, fill leftovers;
-    // then the bf + 1 random rows (input first, then table) and the two cosets.
-    // hb: value width the sort assumes (1..64 narrow, 65..254 key window, 0 full sort)
-    auto permute = [&](int ci, int l, int hb) -> int {
-      const int j = ci * pk.NL + l;
-      CircuitWs& w = *W[ci];
-      size_t tb = pk.sort_tmp_bytes;
-      unsigned long long* flags = pk.lk_or_d + (size_t)LKF * j;
-      if (hb > 0 && hb <= 64) {  // the values themselves are the keys
-        uint64_t* ka = (uint64_t*)pk.ck_a;  // [0, n): keys, [n, 2n): sorted
-        uint64_t* kt = (uint64_t*)pk.ck_t;
-        HIPCHK(lookup_keys(w.lk_a[l], u, 0, nullptr, ka, nullptr, flags, st));
-        HIPCHK(lookup_keys(w.lk_s[l], u, 0, nullptr, kt, nullptr, flags, st));
-        HIPCHK(rocprim::radix_sort_keys(pk.sort_tmp, tb, ka, ka + n, (int)u, 0, hb, st));
-        tb = pk.sort_tmp_bytes;
-        HIPCHK(rocprim::radix_sort_keys(pk.sort_tmp, tb, kt, kt + n, (int)u, 0, hb, st));
-        HIPCHK(key64_expand(ka + n, pk.ck_a2, u, st));
-        HIPCHK(key64_expand(kt + n, pk.ck_t2, u, st));
-      } else if (hb > 64) {  // 48-bit window [hb - 48, hb) with the row index, then gather
-        uint64_t* kin = (uint64_t*)pk.ck_left;  // scratch: keys in/out, indices in/out
-        uint64_t* kout = kin + n;
-        uint32_t* iin = (uint32_t*)(kout + n);
-        uint32_t* iout = iin + n;
-        const Fr* srcs[2] = {w.lk_a[l], w.lk_s[l]};
-        CanonKey* canon[2] = {pk.ck_a, pk.ck_t};
-        CanonKey* sorted[2] = {pk.ck_a2, pk.ck_t2};
-        for (int s = 0; s < 2; s++) {
-          HIPCHK(lookup_keys(srcs[s], u, hb - 48, canon[s], kin, iin, flags, st));
-          tb = pk.sort_tmp_bytes;
-          HIPCHK(rocprim::radix_sort_pairs(pk.sort_tmp, tb, kin, kout, iin, iout, (int)u, 0, 48, st));
-          HIPCHK(lookup_gather(canon[s], iout, u, sorted[s], flags + 4, st));
-        }
-      } else {
-        HIPCHK(fr_to_canon(w.lk_a[l], pk.ck_a, u, st));
-        HIPCHK(fr_to_canon(w.lk_s[l], pk.ck_t, u, st));
-        HIPCHK(rocprim::merge_sort(pk.sort_tmp, tb, pk.ck_a, pk.ck_a2, (int)u, CanonLess(), st));
-        tb = pk.sort_tmp_bytes;
-        HIPCHK(rocprim::merge_sort(pk.sort_tmp, tb, pk.ck_t, pk.ck_t2, (int)u, CanonLess(), st));
+    // permute_expression_pair (lookup/prover.rs:410-494): sort by Ord (canonical value),
+    // match, fill leftovers; then the bf + 1 random rows (input first, then table).
+    // Every lookup's two columns go through ONE radix sort (radix.hip): column g = 2 j + side
+    // keys on a 48-bit window of its canonical values -- bits [hb - 48, hb) below the value
+    // width hb the previous proof measured for that lookup (lk_hb) -- with g above the
+    // window, so each column's rows come out contiguous and sorted.  The gather of the
+    // canonical values checks the order (a window that tied different values); a lookup
+    // whose check or width failed, or whose width is unknown (hb 0), is sorted in full
+    // (four stable 64-bit limb sorts, least significant first).
+    const int G = 2 * NLT;
+    int gbits = 0;
+    while ((1 << gbits) < G) gbits++;
+    if (NLT && (size_t)G * u > pk.lkb_len) {  // grow-only batch buffers
+      const size_t m = (size_t)G * u;
+      PALLOC(pk.pool, pk.lkb_canon, m);
+      for (int q = 0; q < 2; q++) {
+        PALLOC(pk.pool, pk.lkb_key[q], m);
+        PALLOC(pk.pool, pk.lkb_idx[q], m);
       }
+      const size_t sb = std::max(std::max(radix_sort_scratch_bytes(m), radix_sort_scratch_bytes(n)),
+                                 compact_scratch_bytes(n));
+      HIPCHK(pk.pool.get(&pk.lkb_scr, sb));
+      pk.lkb_len = m;
+    }
+    // the match and fill of lookup j from its sorted columns (pk.ck_a2 input, pk.ck_t2 table)
+    auto match_fill = [&](int j) -> int {
+      const int ci = j / pk.NL, l = j % pk.NL;
+      CircuitWs& w = *W[ci];
       HIPCHK(hipMemsetAsync(pk.left_flag, 1, u, st));
       HIPCHK(hipMemsetAsync(pk.counters, 0, 8 * sizeof(uint32_t), st));
       HIPCHK(lookup_mark(pk.ck_a2, pk.ck_t2, u, pk.rep_flag, pk.left_flag, pk.counters + 2, st));
-      tb = pk.sort_tmp_bytes;
-      HIPCHK(rocprim::select(pk.sort_tmp, tb, pk.ck_t2, pk.left_flag, pk.ck_left, pk.counters, (int)u,
-                                           st));
-      tb = pk.sort_tmp_bytes;
-      HIPCHK(rocprim::select(pk.sort_tmp, tb, rocprim::counting_iterator<uint32_t>(0), pk.rep_flag,
-                                           pk.rep_rows, pk.counters + 1, (int)u, st));
+      HIPCHK(compact_canon(pk.ck_t2, pk.left_flag, u, pk.ck_left, pk.counters, pk.lkb_scr, st));
+      HIPCHK(compact_index(pk.rep_flag, u, pk.rep_rows, pk.counters + 1, pk.lkb_scr, st));
       HIPCHK(lookup_assign(pk.ck_a2, pk.rep_flag, u, w.lk_ap[l], w.lk_sp[l], st));
       HIPCHK(lookup_scatter(pk.ck_left, pk.rep_rows, pk.counters + 1, u, w.lk_sp[l], st));
       HIPCHK(hipMemcpyAsync(pk.lk_cnt + 3 * j, pk.counters, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -1597,6 +1596,30 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         const Fr* r = rows.data() + ((size_t)2 * j + which) * (bf + 1);
         HIPCHK(hipMemcpyAsync((which ? w.lk_sp[l] : w.lk_ap[l]) + u, r, (size_t)(bf + 1) * sizeof(Fr),
                               hipMemcpyHostToDevice, st));
+      }
+      return H2G_OK;
+    };
+    // the full sort of lookup j's columns into pk.ck_a2 / ck_t2 (radix sorts on the limbs,
+    // in lookup j's own regions of the batch's key / index buffers)
+    auto full_sort = [&](int j) -> int {
+      const int ci = j / pk.NL, l = j % pk.NL;
+      CircuitWs& w = *W[ci];
+      const Fr* srcs[2] = {w.lk_a[l], w.lk_s[l]};
+      CanonKey* sorted[2] = {pk.ck_a2, pk.ck_t2};
+      for (int side = 0; side < 2; side++) {
+        CanonKey* canon = pk.lkb_canon + (size_t)(2 * j + side) * u;
+        HIPCHK(lookup_keys(srcs[side], u, 0, canon, nullptr, nullptr, pk.lk_or_d + (size_t)LKF * j, st));
+        const size_t o = (size_t)2 * j * u;
+        uint64_t *k0 = pk.lkb_key[0] + o, *k1 = pk.lkb_key[1] + o;
+        uint32_t *i0 = pk.lkb_idx[0] + o, *i1 = pk.lkb_idx[1] + o;
+        HIPCHK(iota_u32(i0, u, st));
+        for (int limb = 0; limb < 4; limb++) {  // least significant first; 8 passes end where they began
+          HIPCHK(canon_limb_keys(canon, i0, u, limb, k0, st));
+          bool alt = false;
+          HIPCHK(radix_sort_pairs(k0, i0, k1, i1, u, 0, 64, pk.lkb_scr, st, &alt));
+          if (alt) return fail(H2G_ERR_STATE, "lookup full sort: unexpected pass parity");
+        }
+        HIPCHK(lookup_gather(canon, i0, u, sorted[side], pk.lk_or_d + (size_t)LKF * j + 4, st));
       }
       return H2G_OK;
     };
@@ -1613,15 +1636,39 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         (void)rng.random_fr();  // permuted input blind
         (void)rng.random_fr();  // permuted table blind
         used[j] = pk.lk_hb[j];
-        RCCHK(permute(ci, l, used[j]));
+        const int shift = used[j] > 48 ? used[j] - 48 : 0;
+        const Fr* srcs[2] = {W[ci]->lk_a[l], W[ci]->lk_s[l]};
+        for (int side = 0; side < 2; side++) {  // every column keys (a full-sort lookup's are ignored)
+          const size_t g = (size_t)2 * j + side;
+          HIPCHK(lookup_keys(srcs[side], u, shift, pk.lkb_canon + g * u, pk.lkb_key[0] + g * u, pk.lkb_idx[0] + g * u,
+                             pk.lk_or_d + (size_t)LKF * j, st, 48, (uint64_t)g << 48));
+        }
       }
+    if (NLT) {
+      bool alt = false;
+      HIPCHK(radix_sort_pairs(pk.lkb_key[0], pk.lkb_idx[0], pk.lkb_key[1], pk.lkb_idx[1], (size_t)G * u, 0,
+                              48 + gbits, pk.lkb_scr, st, &alt));
+      const uint32_t* sidx = pk.lkb_idx[alt ? 1 : 0];
+      for (int j = 0; j < NLT; j++) {
+        if (used[j] == 0) {
+          RCCHK(full_sort(j));
+        } else {
+          for (int side = 0; side < 2; side++) {
+            const size_t g = (size_t)2 * j + side;
+            HIPCHK(lookup_gather(pk.lkb_canon + g * u, sidx + g * u, u, side ? pk.ck_t2 : pk.ck_a2,
+                                 pk.lk_or_d + (size_t)LKF * j + 4, st));
+          }
+        }
+        RCCHK(match_fill(j));
+      }
+    }
     if (NLT) {
       HIPCHK(hipMemcpyAsync(pk.lk_or_h, pk.lk_or_d, (size_t)NLT * LKF * sizeof(unsigned long long),
                             hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));  // counters and value masks landed; rows (host) read
     }
-    // a sort whose assumption failed (values wider than its keys, or a key window that
-    // tied different values out of order) is redone with the full sort; the width is
+    // a sort whose assumption failed (values wider than its window, or a window that tied
+    // different values out of order) is redone with the full sort; the width is
     // remembered for the next proof
     bool redo = false;
     for (int j = 0; j < NLT; j++) {
@@ -1634,7 +1681,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       const bool tie = f[4] != 0;
       pk.lk_hb[j] = tie && hb == used[j] ? 0 : hb;  // ties at the right width: full sort from now on
       if (tie || hb > used[j]) {
-        RCCHK(permute(j / pk.NL, j % pk.NL, 0));
+        RCCHK(full_sort(j));
+        RCCHK(match_fill(j));
         redo = true;
       }
     }
@@ -1848,13 +1896,10 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     RCCHK(rng_ok());
     RCCHK(commit_launch(d, prm, pk.random_poly, n, SRS_G, st, &van_tk));
   }
-  // advice to coefficient form and the extended-domain cosets do not depend on y:
-  // they overlap the permutation / vanishing MSMs
-  for (CircuitWs* w : W) {
-    RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)w->adv.data(), w->adv.data(), pk.A, st));
-    RCCHK(ext_cosets(d, pk, (const Fr* const*)w->adv.data(), w->adv_coset.data(), pk.A, st));
+  // the instance columns' cosets do not depend on y: they overlap the permutation /
+  // vanishing MSMs (the advice went to coefficients and cosets under its own MSMs)
+  for (CircuitWs* w : W)
     RCCHK(ext_cosets(d, pk, (const Fr* const*)w->inst_poly.data(), w->inst_coset.data(), pk.I, st));
-  }
   for (auto* tks : {&perm_tk, &lkz_tk, &shz_tk})
     for (auto& t : *tks) {
       G1Affine cm;
@@ -2019,7 +2064,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   auto id_sh = [&](int ci) { return ci * per_c + pk.A + pk.nsets + 3 * pk.NL; };
   std::vector<PolyRef> polys;
   for (const CircuitWs* w : W) {
-    for (int c = 0; c < pk.A; c++) polys.push_back({w->adv[c], n});
+    for (int c = 0; c < pk.A; c++) polys.push_back({w->adv_poly[c], n});
     for (int s = 0; s < pk.nsets; s++) polys.push_back({w->z[s], n});
     for (int l = 0; l < pk.NL; l++) {
       polys.push_back({w->lk_z_poly[l], n});
@@ -3116,6 +3161,20 @@ int h2g_set_shard_transport(const h2g_shard_transport* t) {
     g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   }
   g_shard_seq = 0;
+  return H2G_OK;
+}
+
+int h2g_spmd_set_weights(const uint32_t* weights, int world) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  g_spmd_wprefix.clear();
+  if (!weights || world <= 1) return H2G_OK;
+  if (world > 4096) return fail(H2G_ERR_ARG, "spmd_set_weights: bad world");
+  std::vector<uint64_t> pre(1, 0);
+  for (int r = 0; r < world; r++) {
+    if (weights[r] == 0) return fail(H2G_ERR_ARG, "spmd_set_weights: every rank needs a nonzero weight");
+    pre.push_back(pre.back() + weights[r]);
+  }
+  g_spmd_wprefix = pre;
   return H2G_OK;
 }
 

@@ -131,10 +131,11 @@ struct CanonLess {
   }
 };
 hipError_t fr_to_canon(const Fr* in, CanonKey* out, size_t n, hipStream_t st);
-// radix-sort keys key[i] = bits [s, s + 64) of canonical(in[i]) (s < 256); canon / idx
-// (optional) receive the canonical values and i; d_or[0..3] |= the values' 64-bit limbs
+// radix-sort keys key[i] = (bits [s, s + kbits) of canonical(in[i])) | tag (s < 256); key /
+// canon / idx (optional) receive the keys, the canonical values and i; d_or[0..3] |= the
+// values' 64-bit limbs
 hipError_t lookup_keys(const Fr* in, size_t n, int s, CanonKey* canon, uint64_t* key, uint32_t* idx,
-                       unsigned long long* d_or, hipStream_t st);
+                       unsigned long long* d_or, hipStream_t st, int kbits = 64, uint64_t tag = 0);
 // out[i] = canon[idx[i]]; *unsorted |= 1 if out is not non-decreasing
 hipError_t lookup_gather(const CanonKey* canon, const uint32_t* idx, size_t u, CanonKey* out,
                          unsigned long long* unsorted, hipStream_t st);

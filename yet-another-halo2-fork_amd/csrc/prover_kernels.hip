@@ -275,7 +275,8 @@ hipError_t fr_to_canon(const Fr* in, CanonKey* out, size_t n, hipStream_t st) {
 __global__ void __launch_bounds__(KT) lookup_keys_kernel(const Fr* __restrict__ in, size_t n, int s,
                                                          CanonKey* __restrict__ canon, uint64_t* __restrict__ key,
                                                          uint32_t* __restrict__ idx,
-                                                         unsigned long long* __restrict__ d_or) {
+                                                         unsigned long long* __restrict__ d_or, uint64_t kmask,
+                                                         uint64_t tag) {
   uint64_t m[4] = {0, 0, 0, 0};
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const Fr c = to_canonical(ldf(in + i));
@@ -287,7 +288,7 @@ __global__ void __launch_bounds__(KT) lookup_keys_kernel(const Fr* __restrict__ 
     }
     const int w = s >> 6, b = s & 63;
     const uint64_t lo = w < 4 ? v[w] : 0, hi = w + 1 < 4 ? v[w + 1] : 0;
-    key[i] = b ? (lo >> b) | (hi << (64 - b)) : lo;
+    if (key) key[i] = ((b ? (lo >> b) | (hi << (64 - b)) : lo) & kmask) | tag;
     if (idx) idx[i] = (uint32_t)i;
     if (canon) {
       CanonKey k;
@@ -316,12 +317,13 @@ __global__ void __launch_bounds__(KT) lookup_keys_kernel(const Fr* __restrict__ 
   }
 }
 hipError_t lookup_keys(const Fr* in, size_t n, int s, CanonKey* canon, uint64_t* key, uint32_t* idx,
-                       unsigned long long* d_or, hipStream_t st) {
+                       unsigned long long* d_or, hipStream_t st, int kbits, uint64_t tag) {
   if (n == 0) return hipSuccess;
-  if (s < 0 || s > 255) return hipErrorInvalidValue;
+  if (s < 0 || s > 255 || kbits < 1 || kbits > 64) return hipErrorInvalidValue;
+  const uint64_t kmask = kbits == 64 ? ~0ull : (1ull << kbits) - 1;
   // at most 512 blocks (grid-stride): 512 x 4 atomics
   const unsigned g = grid_1d(n) < 512 ? grid_1d(n) : 512;
-  hipLaunchKernelGGL(lookup_keys_kernel, dim3(g), dim3(KT), 0, st, in, n, s, canon, key, idx, d_or);
+  hipLaunchKernelGGL(lookup_keys_kernel, dim3(g), dim3(KT), 0, st, in, n, s, canon, key, idx, d_or, kmask, tag);
   return hipGetLastError();
 }
 

@@ -115,6 +115,7 @@ _SIGS = {
     "h2g_comm_stop": ([], I32),
     "h2g_comm_destroy": ([], I32),
     "h2g_set_spmd_transport": ([VP], I32),
+    "h2g_spmd_set_weights": ([VP, I32], I32),
     "h2g_comm_spmd_install": ([I32], I32),
     "h2g_comm_spmd_uninstall": ([], I32),
 }
@@ -931,6 +932,17 @@ def set_spmd_transport(world, rank=0, allgather=None, bcast=None, allgather_host
     t = SpmdTransport(None, world, rank, cb, cbb, cbh, cbx)
     _transport_keep = (t, cb, cbb, cbh, cbx, [])
     check(lib().h2g_set_spmd_transport(ctypes.byref(t)))
+
+
+def spmd_set_weights(weights):
+    """SPMD slab weights (h2g_spmd_set_weights): rank r's slab is [P S_r / S, P S_{r+1} / S);
+    None restores the uniform partition.  Every rank passes the same list, and sets its
+    params slab to h2g_dist.slab(P, world, rank, weights=...)."""
+    if not weights:
+        check(lib().h2g_spmd_set_weights(None, 0))
+        return
+    w = np.ascontiguousarray(weights, dtype=np.uint32)
+    check(lib().h2g_spmd_set_weights(VP(w.ctypes.data), len(w)))
 
 
 # ------------------------------------------------- native RCCL transport (csrc/comm.cpp)

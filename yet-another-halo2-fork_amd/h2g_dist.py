@@ -19,11 +19,28 @@ import numpy as np
 OP_STOP, OP_MSM = 0, 1
 
 
-def slab(n, world, r, P=None):
+def slab(n, world, r, P=None, weights=None):
     """[lo, hi) of rank r's points in an MSM of length n: the slab of the params' P = 2^k
-    points, clipped to n (the C prover's shard_lo, csrc/prover.cpp)"""
+    points, clipped to n (the C prover's shard_lo, csrc/prover.cpp); with SPMD weights
+    (h2g.spmd_set_weights) [P S_r / S, P S_{r+1} / S)"""
     P = n if P is None else P
+    if weights:
+        pre = [0]
+        for w in weights:
+            pre.append(pre[-1] + int(w))
+        return min(n, P * pre[r] // pre[-1]), min(n, P * pre[r + 1] // pre[-1])
     return min(n, P * r // world), min(n, P * (r + 1) // world)
+
+
+def owner_weights(world, extended_k, k, owner_weight=0.5, scale=100):
+    """SPMD slab weights that lighten the ranks owning extended-domain sub-cosets: with
+    2^(extended_k - k) = E < world sub-cosets, ranks r < E evaluate h on a sub-coset each
+    (its n-point coset NTTs, evaluate_h, the h interpolation) on top of their MSM slabs;
+    they get weight owner_weight, the other ranks 1 (None when every rank owns one)"""
+    E = 1 << (extended_k - k)
+    if world <= E:
+        return None
+    return [int(round(scale * owner_weight)) if r < E else scale for r in range(world)]
 
 
 def _staging(dist, group):
