@@ -114,10 +114,13 @@ def test_spmd_diverged_ranks_refuse_the_proof():
 def test_spmd_c3_k22_at_size(world):
     """BASELINE configs[3] at its size: the C3 k = 22 proof with every commitment MSM split
     into `world` point slabs and the extended domain's sub-cosets divided over the ranks
-    (gloo ranks sharing this box's GPU); every rank's bytes == the single-GPU proof"""
+    (gloo ranks sharing this box's GPU); every rank's bytes == the single-GPU proof.  With
+    more ranks than the 2 sub-cosets, the non-owners receive their coefficient slabs of the
+    circuit's columns (a second exchange)"""
     res = _run(world, ["c3_k22"], mode="spmd", extra=["--one-variant"], timeout=1100)
     assert res["c3_k22"]["same"] and res["c3_k22"]["same_ranks"], res
-    assert res["c3_k22"]["gathers"] == 11 and res["c3_k22"]["exchanges"] == 1, res
+    assert res["c3_k22"]["gathers"] == 11, res
+    assert res["c3_k22"]["exchanges"] == (1 if world <= 2 else 2), res
 
 
 @pytest.mark.timeout(1200)

@@ -427,37 +427,57 @@ int commit_collect(Device* d, MsmTicket* t, G1Affine* out) {
 // sort, accumulation and reduction serve a group, so the latency-bound reduction is paid
 // once per group instead of once per commitment -- what circuits with many columns at
 // small k (C5) are dominated by (commit_batch_chunk); with a shard transport every MSM
-// goes alone (point slabs).
+// goes alone (point slabs).  SPMD ranks batch their slab MSMs the same way: a 2^19-point
+// slab's reduction costs about what a 2^22 MSM's does.
 // MSMs per batch for commitments of length n (1: no batching).  Batching pays where
 // the reduction's latency is comparable to the accumulation: measured on MI355X, a
 // keccak-style k = 18 proof (80 MSMs of 2^18) 127 -> 101 ms, while C3 at k = 22 (MSMs
 // of 2^22, 13 x 2^22 entries each) is 0.6 ms better without -- so only MSMs of at most
 // 2^25 sorted entries are batched, up to 2^27 entries per batch.
-int commit_batch_chunk(const Params& prm, size_t n, int set) {
+int commit_batch_chunk(const MsmFixedBase& tb, size_t n) {
   static const uint64_t max_entries = [] {
     const char* e = std::getenv("H2G_MSM_BATCH_ENTRIES");
     return e ? std::strtoull(e, nullptr, 0) : (1ull << 27);
   }();
-  if (g_shard.world > 1 || g_spmd.world > 1) return 1;
-  size_t toff = 0;
-  const uint64_t per = (uint64_t)prm.tables(set, 0, n, &toff).W * (n ? n : 1);
+  if (g_shard.world > 1) return 1;
+  const uint64_t per = (uint64_t)tb.W * (n ? n : 1);
   if (per > (1ull << 25)) return 1;
   return (int)std::max<uint64_t>(1, std::min<uint64_t>(MSM_MAX_BATCH, max_entries / per));
 }
 
+// the points this rank's commitments of length n cover ([0, n), or its SPMD slab as in
+// commit_launch) and the windows serving them
+const MsmFixedBase& commit_tables(const Params& prm, size_t n, int set, size_t* lo, size_t* hi, size_t* toff) {
+  *lo = 0;
+  *hi = n;
+  if (g_spmd.world > 1) {
+    *lo = shard_lo(prm.n, n, g_spmd.world, g_spmd.rank);
+    *hi = shard_lo(prm.n, n, g_spmd.world, g_spmd.rank + 1);
+  }
+  return prm.tables(set, *lo, *hi - *lo, toff);
+}
+int commit_batch_chunk(const Params& prm, size_t n, int set) {
+  size_t lo, hi, toff;
+  const MsmFixedBase& tb = commit_tables(prm, n, set, &lo, &hi, &toff);
+  return commit_batch_chunk(tb, hi - lo);
+}
+
 int commit_launch_batch(Device* d, const Params& prm, const Fr* const* scalars, int nb, size_t n, int set,
                         hipStream_t st, MsmTicket* t) {
-  size_t toff = 0;
-  const MsmFixedBase& tb = prm.tables(set, 0, n, &toff);
-  const int chunk = commit_batch_chunk(prm, n, set);
+  size_t lo, hi, toff;
+  const MsmFixedBase& tb = commit_tables(prm, n, set, &lo, &hi, &toff);
+  const int chunk = commit_batch_chunk(tb, hi - lo);
   if (chunk < 2) {
     for (int b = 0; b < nb; b++) RCCHK(commit_launch(d, prm, scalars[b], n, set, st, &t[b]));
     return H2G_OK;
   }
   for (int b0 = 0; b0 < nb; b0 += chunk) {
     const int m = std::min(chunk, nb - b0);
-    for (int b = 0; b < m; b++) t[b0 + b].shard_seq = -1;
-    RCCHK(msm_fixed_launch_batch(d, reinterpret_cast<const void* const*>(scalars + b0), m, tb, toff, n, st, t + b0));
+    const Fr* sl[MSM_MAX_BATCH];
+    for (int b = 0; b < m; b++) sl[b] = scalars[b0 + b] + lo;
+    RCCHK(msm_fixed_launch_batch(d, reinterpret_cast<const void* const*>(sl), m, tb, toff, hi - lo, st, t + b0));
+    // SPMD: every rank issues the same MSMs in the same order, so the sequence numbers agree
+    for (int b = 0; b < m; b++) t[b0 + b].shard_seq = g_spmd.world > 1 ? (int64_t)g_spmd_seq++ : -1;
   }
   return H2G_OK;
 }
@@ -1032,6 +1052,64 @@ int h_by_slabs(Device* d, ProvingKey& pk, const Slab& sl, hipStream_t st) {
   return H2G_OK;
 }
 
+// SPMD with more ranks than sub-cosets (E = 2^e): ranks 0 .. E-1 own the sub-cosets and
+// hold every coefficient column whole; ranks E.. skipped those iNTTs and receive their slab
+// [lo, hi1) of each column (column c from owner c mod E), one all-to-all per proof.
+int coef_exchange(ProvingKey& pk, const std::vector<Fr*>& cols, hipStream_t st) {
+  const size_t n = pk.n;
+  const int W = g_spmd.world, me = g_spmd.rank;
+  const int E = 1 << (pk.dom.ek - pk.dom.k);
+  const int nc = (int)cols.size();
+  std::vector<Slab> slabs(W);
+  for (int r = 0; r < W; r++) slabs[r] = spmd_slab(n, r);
+  auto ncols_of = [&](int o) {  // columns owner o sends
+    int c = 0;
+    for (int i = o; i < nc; i += E) c++;
+    return c;
+  };
+  std::vector<size_t> sb(W, 0), rb(W, 0);
+  size_t stot = 0, rtot = 0;
+  for (int r = 0; r < W; r++) {
+    if (me < E && r >= E) sb[r] = (size_t)ncols_of(me) * (slabs[r].hi1 - slabs[r].lo) * sizeof(Fr);
+    if (me >= E && r < E) rb[r] = (size_t)ncols_of(r) * (slabs[me].hi1 - slabs[me].lo) * sizeof(Fr);
+    stot += sb[r] / sizeof(Fr);
+    rtot += rb[r] / sizeof(Fr);
+  }
+  if (stot > pk.x_send_len) {
+    PALLOC(pk.pool, pk.x_send, stot);
+    pk.x_send_len = stot;
+  }
+  if (rtot > pk.x_recv_len) {
+    PALLOC(pk.pool, pk.x_recv, rtot);
+    pk.x_recv_len = rtot;
+  }
+  if (me < E) {  // pack: per destination, my columns' slabs
+    size_t off = 0;
+    for (int r = E; r < W; r++) {
+      const size_t cnt = slabs[r].hi1 - slabs[r].lo;
+      for (int c = me; c < nc; c += E) {
+        if (cnt) HIPCHK(hipMemcpyAsync(pk.x_send + off, cols[c] + slabs[r].lo, cnt * sizeof(Fr),
+                                       hipMemcpyDeviceToDevice, st));
+        off += cnt;
+      }
+    }
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  if (g_spmd.exchange(g_spmd.ctx, pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
+    return fail(H2G_ERR_STATE, "spmd transport: exchange of coefficient slabs failed");
+  if (me >= E) {  // unpack: owner by owner, its columns in order
+    const size_t cnt = slabs[me].hi1 - slabs[me].lo;
+    size_t off = 0;
+    for (int o = 0; o < E; o++)
+      for (int c = o; c < nc; c += E) {
+        if (cnt) HIPCHK(hipMemcpyAsync(cols[c] + slabs[me].lo, pk.x_recv + off, cnt * sizeof(Fr),
+                                       hipMemcpyDeviceToDevice, st));
+        off += cnt;
+      }
+  }
+  return H2G_OK;
+}
+
 int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, const PkImage* img = nullptr) {
   hipStream_t st = d->stream;
   std::string why;
@@ -1389,6 +1467,12 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   Slab sl;
   sl.hi = sl.hi1 = n;
   if (slabs) sl = spmd_slab(n, g_spmd.rank);
+  // SPMD with more ranks than sub-cosets: a rank that owns none needs the circuit's
+  // coefficient columns only on its slab (evaluations, SHPLONK) -- the owners, which need
+  // them whole for their cosets, send it (coef_exchange) and it skips their iNTTs
+  const bool h_slabs = spmd_subcosets() && slabs && g_spmd.exchange != nullptr;
+  const bool coef_recv = h_slabs && pk.sub_ts.empty();
+  const bool coef_send = h_slabs && !pk.sub_ts.empty() && g_spmd.world > (1 << (pk.dom.ek - pk.dom.k));
   ProverRng& rng = *in.rng;
   Transcript tr(proof, pk.transcript);
   SpmdCheckScope spmd_check(&tr, &rng);
@@ -1407,7 +1491,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       const uint64_t* col = in.instance[ci] + 4 * n * i;
       for (uint32_t r = 0; r < len; r++) tr.common_scalar(fr_from_limbs(col + 4 * r));
       HIPCHK(hipMemcpyAsync(W[ci]->inst_val[i], col, n * sizeof(Fr), hipMemcpyHostToDevice, st));
-      RCCHK(lagrange_to_coeff(d, D, W[ci]->inst_val[i], W[ci]->inst_poly[i], st));
+      if (!coef_recv) RCCHK(lagrange_to_coeff(d, D, W[ci]->inst_val[i], W[ci]->inst_poly[i], st));
     }
   // ---- commit_phase per advice phase (prover.rs:309-494), circuit by circuit: the
   // phase's blinding rows, its blinds, its commitments; then the phase's challenges
@@ -1496,6 +1580,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         dst.push_back(w.adv_poly[c]);
         cst.push_back(w.adv_coset[c]);
       }
+      if (coef_recv) continue;  // coefficients from the owners (coef_exchange), no cosets
       RCCHK(lagrange_to_coeff_batch(d, D, src.data(), dst.data(), (int)cols.size(), st));
       RCCHK(ext_cosets(d, pk, (const Fr* const*)dst.data(), cst.data(), (int)cols.size(), st));
     }
@@ -1706,7 +1791,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       }
     RCCHK(commit_launch_batch(d, prm, perm_cols.data(), 2 * NLT, n, SRS_LAGRANGE, st, tk.data()));
     // coefficient forms and cosets, batched transforms (they overlap the commitments)
-    RCCHK(lagrange_to_coeff_batch(d, D, perm_cols.data(), perm_polys.data(), 2 * NLT, st));
+    if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, perm_cols.data(), perm_polys.data(), 2 * NLT, st));
     RCCHK(ext_cosets(d, pk, (const Fr* const*)perm_polys.data(), perm_cosets.data(), 2 * NLT, st));
     for (int i = 0; i < 2 * NLT; i++) {
       G1Affine cm;
@@ -1798,7 +1883,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
           RCCHK(commit_launch(d, prm, w.z_lag[s], n, SRS_LAGRANGE, st, &perm_tk[(size_t)ci * pk.nsets + s]));
       }
     }
-    RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)all_z_lag.data(), all_z.data(), NST, st));
+    if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)all_z_lag.data(), all_z.data(), NST, st));
     RCCHK(ext_cosets(d, pk, (const Fr* const*)all_z.data(), all_z_coset.data(), NST, st));
   }
   if (perm_batched)
@@ -1856,7 +1941,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         HIPCHK(shuffle_prod_num(pk.tmp_a, gamma, pk.mod, n, st));
         RCCHK(finish_z(pk.mod, w->sh_z[s], w->sh_z_poly[s], w->sh_zc[s], false));
       }
-    RCCHK(lagrange_to_coeff_batch(d, D, z_lags.data(), z_polys.data(), (int)z_lags.size(), st));
+    if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, z_lags.data(), z_polys.data(), (int)z_lags.size(), st));
     RCCHK(ext_cosets(d, pk, (const Fr* const*)z_polys.data(), z_cosets.data(), (int)z_lags.size(), st));
   }
   {  // product commitments: every circuit's lookups, then every circuit's shuffles, one batch
@@ -1916,7 +2001,6 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   // ---- evaluate_h (evaluation.rs:317-620): one launch per circuit, each continuing the
   // previous circuit's Horner chain in y; the last one divides by t(X)
   const bool subc = spmd_subcosets();
-  const bool h_slabs = subc && slabs && g_spmd.exchange != nullptr;
   for (int ci = 0; ci < ncirc && !subc; ci++) {
     const CircuitWs& w = *W[ci];
     EvalHArgs a;
@@ -2074,6 +2158,11 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     for (int s = 0; s < pk.NS; s++) polys.push_back({w->sh_z_poly[s], n});
   }
   const int id_fix = (int)polys.size();
+  if (coef_send || coef_recv) {  // the per-circuit coefficient columns' slabs, owners -> the others
+    std::vector<Fr*> cols;
+    for (int i = 0; i < id_fix; i++) cols.push_back(const_cast<Fr*>(polys[i].p));
+    RCCHK(coef_exchange(pk, cols, st));
+  }
   for (int c = 0; c < pk.F; c++) polys.push_back({pk.fixed_poly[c], n});
   const int id_sig = (int)polys.size();
   for (int c = 0; c < pk.P; c++) polys.push_back({pk.sigma_poly[c], n});
