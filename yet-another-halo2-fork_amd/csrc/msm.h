@@ -25,8 +25,9 @@ struct MsmWorkspace {
   void* windows = nullptr;       // G1xyzz [W]
   void* result = nullptr;        // counters: [0] items, [1] multi-item buckets
   void* total_items = nullptr;   // G1xyzz partial sums of big-bucket items
-  void* sort_tmp = nullptr;
+  void* sort_tmp = nullptr;  // partition counts / offsets; zero-initialised, the counts kept zero between MSMs
   size_t sort_tmp_bytes = 0;
+  size_t sort_kcap = 0;  // per-key arrays' capacity (buckets of all sets)
   void* scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
 };

@@ -141,11 +141,32 @@ __device__ __forceinline__ void scalar_digits(const MsmScalarList& list, size_t 
   }
 }
 
+// zeroed by the coarse histogram kernel for the later phases: bucket [start, end) (empty
+// buckets keep 0, 0), the big-item counters, the plane reduction's finished-block counts
+struct MsmZero {
+  uint32_t* bstart;
+  uint32_t* bend;
+  size_t nb;
+  uint32_t* counters;
+  uint32_t* rdone;
+  uint32_t nrd;
+};
+
 // round 1a: coarse histogram (LDS per block, one global atomic per bin and block)
 __global__ void __launch_bounds__(PT)
 msm_coarse_hist_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride, int fb,
-                       uint32_t ncoarse, uint32_t* __restrict__ ccount) {
+                       uint32_t ncoarse, uint32_t* __restrict__ ccount, MsmZero z) {
   __shared__ uint32_t h[COARSE_MAX];
+  {  // the pipeline's other per-MSM zeroing (no separate fills)
+    const size_t nthr = (size_t)gridDim.x * gridDim.y * gridDim.z * PT;
+    const size_t tid = (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * PT + threadIdx.x;
+    for (size_t i = tid; i < z.nb; i += nthr) {
+      z.bstart[i] = 0;
+      z.bend[i] = 0;
+    }
+    if (tid < 2) z.counters[tid] = 0;
+    if (tid < z.nrd) z.rdone[tid] = 0;
+  }
   for (uint32_t t = threadIdx.x; t < ncoarse; t += PT) h[t] = 0;
   __syncthreads();
   const size_t i = blockIdx.x * (size_t)PT + threadIdx.x;
@@ -158,10 +179,11 @@ msm_coarse_hist_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, 
 }
 
 // exclusive scan of cnt[0, len) (one block, len <= 1024 * 64): off[] = cursor[] =
-// prefix; *total = sum
+// prefix; *total = sum; clear: cnt[] is zeroed after use (the counts start at zero for
+// the next MSM without a fill)
 __global__ void __launch_bounds__(1024)
-msm_scan_kernel(const uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__ off,
-                uint32_t* __restrict__ cursor, uint32_t* __restrict__ total) {
+msm_scan_kernel(uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__ off,
+                uint32_t* __restrict__ cursor, uint32_t* __restrict__ total, bool clear) {
   __shared__ uint32_t part[1024];
   const uint32_t per = (len + 1023) / 1024;
   const uint32_t lo = threadIdx.x * per, hi = lo + per < len ? lo + per : len;
@@ -180,6 +202,7 @@ msm_scan_kernel(const uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __rest
     off[i] = run;
     if (cursor) cursor[i] = run;
     run += cnt[i];
+    if (clear) cnt[i] = 0;
   }
   if (threadIdx.x == 1023 && total) *total = part[1023];
 }
@@ -187,11 +210,12 @@ msm_scan_kernel(const uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __rest
 // large scans (the per-key counts): 1024-element blocks scanned locally, block sums
 // scanned by msm_scan_kernel, then added back
 __global__ void __launch_bounds__(1024)
-msm_scan_block_kernel(const uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__ off,
+msm_scan_block_kernel(uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__ off,
                       uint32_t* __restrict__ bsum) {
   __shared__ uint32_t part[1024];
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
   const uint32_t v0 = i < len ? cnt[i] : 0;
+  if (i < len) cnt[i] = 0;  // zero for the next MSM (cnt is read only here)
   part[threadIdx.x] = v0;
   __syncthreads();
   for (int d = 1; d < 1024; d <<= 1) {
@@ -412,20 +436,54 @@ struct MsmBigItem {
 static size_t msm_big_items_cap(size_t nchunks) { return 2 * nchunks / MSM_ITEM + 2 * nchunks / MSM_SMALL + 2; }
 static size_t msm_big_multi_cap(size_t nchunks) { return 2 * nchunks / MSM_ITEM + 2; }
 
+// The item lists are reserved with one atomic per wave (a wave-level scan of the lanes'
+// item counts), not one per bucket.  Q = 4: a quad per bucket (xyzz_add_q4, ~3x less
+// latency per addition) summing up to MSM_SMALL_Q4 pieces itself -- for small bucket
+// sets (<= 2^15), whose buckets span up to ~10 chunks of the minimum chunk length (2^16
+// points at c = 15: 9 pieces each, all of which took the big-item path: fixup 0.30 ->
+// 0.11 ms; at 2^16 buckets the quads' issue cost loses, 0.097 -> 0.142 ms).
+__device__ G1xyzz xyzz_add_q4(const G1xyzz& p, const G1xyzz& q);
+static constexpr uint32_t MSM_SMALL_Q4 = 32;
+
+template <int Q>
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ start,
                  const uint32_t* __restrict__ end, uint32_t nbt, uint32_t L, G1xyzz* __restrict__ buckets,
                  MsmBigItem* __restrict__ items, uint4* __restrict__ multi, uint32_t* __restrict__ counters) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nbt) return;
-  const uint32_t bs = start[b], be = end[b];
-  if (be <= bs) return;  // empty (buckets[] is zero = identity)
-  const uint32_t t0 = bs / L, t1 = (be - 1) / L;
-  if (t0 == t1) return;  // written by the accumulation kernel
-  const uint32_t np = t1 - t0 + 1;
-  if (np > MSM_SMALL) {
-    const uint32_t cnt = (np + MSM_ITEM - 1) / MSM_ITEM;
-    const uint32_t base = atomicAdd(&counters[0], cnt);
+  const uint32_t b = (blockIdx.x * blockDim.x + threadIdx.x) / Q;
+  const uint32_t lane = threadIdx.x & 63;
+  const bool lead = (threadIdx.x % Q) == 0;
+  uint32_t bs = 0, be = 0;
+  if (b < nbt) {
+    bs = start[b];
+    be = end[b];
+  }
+  // np pieces (0: empty bucket, or written by the accumulation kernel)
+  const uint32_t t0 = bs / L, t1 = be > bs ? (be - 1) / L : t0;
+  const uint32_t np = be > bs && t1 > t0 ? t1 - t0 + 1 : 0;
+  const uint32_t small = Q == 4 ? MSM_SMALL_Q4 : MSM_SMALL;
+  const uint32_t cnt = lead && np > small ? (np + MSM_ITEM - 1) / MSM_ITEM : 0;
+  // every lane of the wave reaches the scan (no early returns above)
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += v;
+  }
+  const uint32_t wtot = __shfl(incl, 63, 64);
+  const uint64_t mm = __ballot(cnt > 1);
+  uint32_t ibase = 0, mbase = 0;
+  if (lane == 0) {
+    if (wtot) ibase = atomicAdd(&counters[0], wtot);
+    if (mm) mbase = atomicAdd(&counters[1], (uint32_t)__popcll(mm));
+  }
+  ibase = __shfl(ibase, 0, 64);
+  mbase = __shfl(mbase, 0, 64);
+  if (b < nbt && be <= bs && lead) buckets[b] = G1xyzz::identity();  // empty (no fill of buckets[])
+  if (np == 0) return;
+  if (np > small) {
+    if (!cnt) return;  // the quad's other lanes
+    const uint32_t base = ibase + incl - cnt;
     for (uint32_t i = 0; i < cnt; i++) {
       MsmBigItem it;
       it.b = b;
@@ -434,12 +492,15 @@ msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ st
       it.slot = cnt > 1 ? base + i : ~0u;
       items[base + i] = it;
     }
-    if (cnt > 1) multi[atomicAdd(&counters[1], 1u)] = make_uint4(b, base, cnt, 0);
+    if (cnt > 1) multi[mbase + (uint32_t)__popcll(mm & ((1ull << lane) - 1))] = make_uint4(b, base, cnt, 0);
     return;
   }
   G1xyzz acc = msm_piece(bnd, t0, t0, bs, L);
-  for (uint32_t t = t0 + 1; t <= t1; t++) acc = xyzz_add(acc, msm_piece(bnd, t, t0, bs, L));
-  buckets[b] = acc;
+  for (uint32_t t = t0 + 1; t <= t1; t++) {
+    if constexpr (Q == 4) acc = xyzz_add_q4(acc, msm_piece(bnd, t, t0, bs, L));
+    else acc = xyzz_add(acc, msm_piece(bnd, t, t0, bs, L));
+  }
+  if (lead) buckets[b] = acc;
 }
 
 // MSM_GROUP lanes per item (4 items per wave, persistent grid): each lane sums up to
@@ -753,7 +814,9 @@ __device__ __forceinline__ void plane_fold(G1xyzz* T, int K, uint32_t e, bool le
 // planes[LB + 1][b] = T (the block's R total); planes[q] is (WB x nblk).  LB = 8 with a
 // lane per group (full-size sets), LB = 6 with a quad per group (small sets: 4x the
 // blocks, so the CUs fill)
-template <int Q, int LB>
+// RGP: buckets per group (the dependent chain of 2 RGP additions before the planes); the
+// planes then weight the groups by RGP g, hence e0 = log2(RGP) in the mid kernel
+template <int Q, int LB, int RGP>
 __global__ void __launch_bounds__((1 << LB) * Q)
 msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, uint32_t nblk,
                         G1xyzz* __restrict__ planes) {
@@ -766,10 +829,11 @@ msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, 
   const G1xyzz* b = B + (size_t)w * NB;
   G1xyzz racc = G1xyzz::identity(), sacc = G1xyzz::identity();
   if (g < m1) {
-    for (int t = RG - 1; t >= 0; t--) {
-      const uint32_t j = g * RG + t;
+#pragma unroll
+    for (int t = RGP - 1; t >= 0; t--) {
+      const uint32_t j = g * RGP + t;
       if (j < NB) racc = padd<Q>(racc, b[j]);
-      sacc = padd<Q>(sacc, racc);
+      sacc = t == RGP - 1 ? racc : padd<Q>(sacc, racc);
     }
   }
   if (lead) {
@@ -1029,6 +1093,7 @@ void msm_free(MsmWorkspace* ws) {
   }
   for (auto& c : ws->cap) c = 0;
   ws->sort_tmp_bytes = ws->scan_tmp_bytes = 0;
+  ws->sort_kcap = 0;
 }
 
 #define H2G_TRY(x)                      \
@@ -1088,8 +1153,33 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   }();
   const bool red_q4 = (size_t)m1 * WB <= q4_max;
   const uint32_t nblk = red_q4 ? (m1 + Q4_GROUPS - 1) / Q4_GROUPS : (m1 + MSM_THREADS - 1) / MSM_THREADS;
-  const int plane_lb = red_q4 ? 6 : 8;  // log2 groups per plane block
-  const uint32_t nblk_p = (m1 + (1u << plane_lb) - 1) >> plane_lb;  // plane kernels' blocks
+  // bit planes.  Small sets (<= 2^18 buckets over all sets, e.g. the 2^16 of a 2^19-point
+  // slab): quad-cooperative, 256 groups per block, and the fewest buckets per group (rgp)
+  // that keep the groups within 2^16 (4 waves per SIMD) -- latency-bound, the reduction
+  // is a dependent chain of ~2 rgp + 8 + 9 + log2(NB) point operations, so the group chain
+  // goes first (2^16 buckets: rgp = 1; 0.38 -> 0.33 ms at 2^19 points).  Larger sets: a
+  // lane per group of 8 (the quads' 1.3x issue cost loses there: 0.62 -> 0.71 ms at 2^19
+  // buckets).  H2G_MSM_PLANE (A/B runs): "old" = round 2's geometry (rgp 8, 64-group quad
+  // blocks up to 2^15 groups), "rg4" = large sets with groups of 4.
+  static const int plane_mode = [] {
+    const char* e = getenv("H2G_MSM_PLANE");
+    if (!e) return 0;
+    return std::string(e) == "old" ? 1 : (std::string(e) == "rg4" ? 2 : 0);
+  }();
+  int rgp = 8, plane_q = 4, plane_lb = 8;
+  if (plane_mode == 1) {
+    plane_q = red_q4 ? 4 : 1;
+    plane_lb = red_q4 ? 6 : 8;
+  } else if ((size_t)NB * WB <= (1u << 18)) {
+    for (rgp = 1; rgp < 8; rgp *= 2)
+      if ((size_t)((NB + rgp - 1) / rgp) * WB <= 65536) break;
+  } else {
+    plane_q = 1;
+    rgp = plane_mode == 2 ? 4 : 8;
+  }
+  const bool plane_old = plane_mode == 1;
+  const uint32_t m1p = (NB + rgp - 1) / rgp;                         // plane groups per set
+  const uint32_t nblk_p = (m1p + (1u << plane_lb) - 1) >> plane_lb;  // plane kernels' blocks
   // bit planes unless the block index needs more than RPK_MAX bits (sets of > 2^17
   // groups, e.g. c = 22): those keep the rscale scheme
   const bool red_plane = !red_group && nblk_p <= (1u << RPK_MAX);
@@ -1109,7 +1199,8 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
                          {&ws->item_bucket, icap * sizeof(MsmBigItem)},  // big-bucket items
                          {&ws->partials, 2 * nchunks * sizeof(G1xyzz)},  // boundary slots
                          {&ws->buckets, (size_t)nbt * sizeof(G1xyzz)},
-                         {&ws->segs, std::max<size_t>(wp.per_set, (size_t)2 * m1 + nblk + 10 * (size_t)nblk_p + 32) *
+                         {&ws->segs, std::max<size_t>(wp.per_set, std::max<size_t>((size_t)2 * m1 + nblk,
+                                                                                    10 * (size_t)nblk_p + 32)) *
                                          WB * sizeof(G1xyzz)},
                          {&ws->windows, (size_t)(W > WB ? W : WB) * sizeof(G1xyzz)},
                          {&ws->result, 16},                              // [0] items, [1] multi-item buckets
@@ -1157,32 +1248,40 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   const uint32_t ncoarse = (uint32_t)((nbt + nf - 1) >> fb);
   if (ncoarse > COARSE_MAX || fb > FB_MAX) return hipErrorInvalidValue;
   const uint32_t kblocks = (nbt + 1023) / 1024;
-  // scratch (u32): ccount | coff | ccursor | total | kcount | koff | kcursor | block sums | block offsets
-  const size_t sort_words = 3 * (size_t)COARSE_MAX + 16 + 3 * (size_t)nbt + 2 * (size_t)kblocks + 16 + (size_t)WB;
-  if (sort_words * 4 > ws->sort_tmp_bytes) {
-    H2G_TRY(grow(&ws->sort_tmp, sort_words * 4));
-    ws->sort_tmp_bytes = sort_words * 4;
+  constexpr int RDONE_MAX = 256;  // bucket sets: W <= 128 windows (c >= 2), or nbatch <= MSM_MAX_BATCH
+  if (WB > RDONE_MAX) return hipErrorInvalidValue;
+  // scratch (u32), laid out for a per-key capacity kcap >= nbt so that the counts stay at
+  // fixed places: ccount | coff | ccursor | total | rdone | kbsum | kboff | kcount | koff |
+  // kcursor.  Zeroed when allocated; the scans zero ccount / kcount after reading them, so
+  // no MSM needs a fill.
+  if ((size_t)nbt > ws->sort_kcap) {
+    const size_t kcap = nbt, kbmax = (kcap + 1023) / 1024;
+    const size_t words = 3 * (size_t)COARSE_MAX + 16 + RDONE_MAX + 2 * kbmax + 3 * kcap;
+    H2G_TRY(grow(&ws->sort_tmp, words * 4));
+    H2G_TRY(hipMemsetAsync(ws->sort_tmp, 0, words * 4, st));
+    ws->sort_tmp_bytes = words * 4;
+    ws->sort_kcap = kcap;
   }
+  const size_t kcap = ws->sort_kcap, kbmax = (kcap + 1023) / 1024;
   uint32_t* ccount = (uint32_t*)ws->sort_tmp;
   uint32_t* coff = ccount + COARSE_MAX;
   uint32_t* ccursor = coff + COARSE_MAX;
   uint32_t* d_total = ccursor + COARSE_MAX;
-  uint32_t* kcount = d_total + 16;
-  uint32_t* koff = kcount + nbt;
-  uint32_t* kcursor = koff + nbt;
-  uint32_t* kbsum = kcursor + nbt;
-  uint32_t* kboff = kbsum + kblocks;
-  uint32_t* rdone = kboff + kblocks;  // plane reduction: finished blocks per set
+  uint32_t* rdone = d_total + 16;  // plane reduction: finished blocks per set
+  uint32_t* kbsum = rdone + RDONE_MAX;
+  uint32_t* kboff = kbsum + kbmax;
+  uint32_t* kcount = kboff + kbmax;
+  uint32_t* koff = kcount + kcap;
+  uint32_t* kcursor = koff + kcap;
 
   const int T = MSM_THREADS;
   H2G_PHASE(0);
   {  // round 1: coarse bins straight from the scalars
     const dim3 g((unsigned)((n + PT - 1) / PT), (unsigned)nbatch, (unsigned)((W + PWG - 1) / PWG));
-    H2G_TRY(hipMemsetAsync(ccount, 0, (size_t)COARSE_MAX * 4, st));
+    const MsmZero z{bstart, bend, (size_t)nbt, counters, rdone, (uint32_t)WB};
     hipLaunchKernelGGL(msm_coarse_hist_kernel, g, dim3(PT), 0, st, list, n, c, W, NB, fixed, stride, fb, ncoarse,
-                       ccount);
-    hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)ccount, ncoarse, coff, ccursor,
-                       d_total);
+                       ccount, z);
+    hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, ccount, ncoarse, coff, ccursor, d_total, true);
     hipLaunchKernelGGL(msm_coarse_scatter_kernel, g, dim3(PT), 0, st, list, n, c, W, NB, fixed, stride, fb, ncoarse,
                        ccursor, keys_in);
     H2G_TRY(hipGetLastError());
@@ -1191,13 +1290,12 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   if (prof && prof->entries) H2G_TRY(hipMemcpyAsync(prof->entries, d_total, 4, hipMemcpyDeviceToHost, st));
   {  // round 2: keys inside the coarse bins
     const unsigned tiles = (unsigned)((total + FTILE - 1) / FTILE);
-    H2G_TRY(hipMemsetAsync(kcount, 0, (size_t)nbt * 4, st));
     hipLaunchKernelGGL(msm_fine_hist_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)keys_in,
                        (const uint32_t*)d_total, fb, kcount);
-    hipLaunchKernelGGL(msm_scan_block_kernel, dim3(kblocks), dim3(1024), 0, st, (const uint32_t*)kcount, nbt, koff,
+    hipLaunchKernelGGL(msm_scan_block_kernel, dim3(kblocks), dim3(1024), 0, st, kcount, nbt, koff,
                        kbsum);
-    hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)kbsum, kblocks, kboff,
-                       (uint32_t*)nullptr, (uint32_t*)nullptr);
+    hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, kbsum, kblocks, kboff, (uint32_t*)nullptr,
+                       (uint32_t*)nullptr, false);
     hipLaunchKernelGGL(msm_scan_add_kernel, dim3(kblocks), dim3(1024), 0, st, koff, nbt, (const uint32_t*)kboff,
                        kcursor);
     hipLaunchKernelGGL(msm_fine_scatter_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)keys_in,
@@ -1205,10 +1303,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     H2G_TRY(hipGetLastError());
   }
   H2G_PHASE(2);
-  H2G_TRY(hipMemsetAsync(counters, 0, 8, st));
-  H2G_TRY(hipMemsetAsync(bstart, 0, (size_t)nbt * 4, st));  // empty buckets: start = end = 0
-  H2G_TRY(hipMemsetAsync(bend, 0, (size_t)nbt * 4, st));
-  H2G_TRY(hipMemsetAsync(buckets, 0, (size_t)nbt * sizeof(G1xyzz), st));
+  // (bucket bounds, counters: zeroed by the coarse histogram; empty buckets: by the fixup)
   H2G_PHASE(3);
   static const bool prefetch = [] {
     const char* e = getenv("H2G_MSM_PREFETCH");
@@ -1222,8 +1317,16 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     hipLaunchKernelGGL(msm_acc_kernel<false>, dim3(cgrid), dim3(T), 0, st, d_bases, (const uint64_t*)keys_out,
                        (const uint32_t*)d_total, sentinel, L, buckets, bnd, bstart, bend);
   H2G_PHASE(4);
-  hipLaunchKernelGGL(msm_fixup_kernel, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, bend,
-                     nbt, L, buckets, items, multi, counters);
+  static const uint32_t fix_q4_max = [] {  // H2G_MSM_FIXUP_Q4_MAX: bucket sets with quad fixup (A/B)
+    const char* e = getenv("H2G_MSM_FIXUP_Q4_MAX");
+    return e ? (uint32_t)atol(e) : 32768u;  // 2^16 buckets (2^19-point slabs): the lane form is faster
+  }();
+  if (nbt <= fix_q4_max)
+    hipLaunchKernelGGL(msm_fixup_kernel<4>, dim3((unsigned)(((size_t)nbt * 4 + T - 1) / T)), dim3(T), 0, st,
+                       (const G1xyzz*)bnd, bstart, bend, nbt, L, buckets, items, multi, counters);
+  else
+    hipLaunchKernelGGL(msm_fixup_kernel<1>, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)bnd, bstart,
+                       bend, nbt, L, buckets, items, multi, counters);
   hipLaunchKernelGGL(msm_big_item_kernel, dim3(MSM_BIG_BLOCKS), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, L,
                      (const MsmBigItem*)items, (const uint32_t*)counters, ipart, buckets);
   hipLaunchKernelGGL(msm_big_combine_kernel, dim3(MSM_BIG_BLOCKS / 4), dim3(T), 0, st, (const uint4*)multi,
@@ -1231,17 +1334,26 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   H2G_PHASE(5);
   if (!red_split) {
     if (red_plane) {  // bit planes (6a')
-      G1xyzz* planes = rP;
+      G1xyzz* planes = (G1xyzz*)ws->segs;
       G1xyzz* mid = planes + (size_t)(plane_lb + 2) * WB * nblk_p;
       int e0 = 0;
-      while ((1 << e0) < RG) e0++;
-      H2G_TRY(hipMemsetAsync(rdone, 0, (size_t)WB * 4, st));
-      if (red_q4)
-        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 6>), dim3(nblk_p, (unsigned)WB), dim3(4 << 6), 0, st,
-                           (const G1xyzz*)buckets, NB, m1, nblk_p, planes);
+      while ((1 << e0) < rgp) e0++;
+      const dim3 pg(nblk_p, (unsigned)WB), pb((unsigned)(plane_q << plane_lb));
+      const G1xyzz* bk = buckets;
+      if (plane_old && plane_q == 4)
+        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 6, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+      else if (plane_q == 1 && rgp == 4)
+        hipLaunchKernelGGL((msm_rgroup_plane_kernel<1, 8, 4>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+      else if (plane_q == 1)
+        hipLaunchKernelGGL((msm_rgroup_plane_kernel<1, 8, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+      else if (rgp == 1)
+        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 1>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+      else if (rgp == 2)
+        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 2>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+      else if (rgp == 4)
+        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 4>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
       else
-        hipLaunchKernelGGL((msm_rgroup_plane_kernel<1, 8>), dim3(nblk_p, (unsigned)WB), dim3(1 << 8), 0, st,
-                           (const G1xyzz*)buckets, NB, m1, nblk_p, planes);
+        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
       hipLaunchKernelGGL(msm_rplane_mid_kernel, dim3((unsigned)plane_lb + 2, (unsigned)WB), dim3(1024), 0, st,
                          (const G1xyzz*)planes, nblk_p, plane_lb, e0, mid, rdone, (G1xyzz*)ws->windows);
     } else {
