@@ -290,27 +290,40 @@ def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note
 
 
 # ----------------------------------------------------------------------------- collectives
+# a gloo group beside the RCCL default group (N > 1): the bench's own small agreements
+# (timing max, transport fallback, proof digests) do not depend on the transport under test
+CTRL = None
+
+
+def ctrl_all_reduce(value, dist, op):
+    import torch
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=op, group=CTRL)
+    return float(t.item())
+
+
 def max_over_ranks(elapsed, dist, world, device):
     """the job's time is the slowest rank's (contract: max over ranks)"""
     if world == 1:
         return elapsed
-    import torch
-    if dist.get_backend() == "gloo":
-        device = "cpu"
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return ctrl_all_reduce(elapsed, dist, dist.ReduceOp.MAX)
+
+
+# set when the SPMD proof had to fall back to the gloo transport: RCCL is then not trusted
+# for the MSM partials either
+RCCL_SUSPECT = False
 
 
 def gather_partials(part, dist, world, device):
     """all_gather of the per-rank MSM partial sums (64-B affine points; RCCL has no
     EC-add reduction) -> list of numpy uint64[8]"""
     import torch
-    if dist.get_backend() == "gloo":
-        device = "cpu"
+    group = None
+    if dist.get_backend() == "gloo" or RCCL_SUSPECT:
+        device, group = "cpu", CTRL
     t = torch.from_numpy(np.ascontiguousarray(part, dtype=np.uint64).view(np.int64)).to(device)
     gathered = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(gathered, t)
+    dist.all_gather(gathered, t, group=group)
     return [g.cpu().numpy().view(np.uint64) for g in gathered]
 
 
@@ -324,6 +337,7 @@ def combine_partials(parts, add):
 
 # ----------------------------------------------------------------------------- workloads
 def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
+    global RCCL_SUSPECT
     import h2g_circuit as hc
     import h2g_dist
 
@@ -341,7 +355,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         params.set_slab(*h2g_dist.slab(n, world, rank))
     native = one_proof and args.transport == "native"
     transport_note = None
-    if native:  # the library's own RCCL communicators (csrc/comm.cpp); the id travels over torch
+    if native and shard:  # the library's own RCCL communicators (csrc/comm.cpp); the id travels over torch
         import torch as _t
         tdev = dev if dist.get_backend() == "nccl" else "cpu"
         uid = _t.zeros(256, dtype=_t.uint8, device=tdev)
@@ -376,28 +390,84 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             spmd_weights["w"] = weights
         adv = torch.from_numpy(np.ascontiguousarray(wit.advice).view(np.int64)).to(dev)  # resident witness
         client = h2g_dist.SlabClient(dist, points=n) if shard and not native else None
-        gather = h2g_dist.SpmdGather(dist, subcosets=not args.no_subcosets) if spmd and not native else None
+        gather = None
     torch.cuda.synchronize()
     proofs = []
 
     def step():
         proofs.append(pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr()))
 
+    # SPMD transport, first that proves on every rank: the library's RCCL communicator
+    # ("native"), torch.distributed over RCCL ("torch"), torch.distributed over the gloo
+    # group with host-staged exchanges ("host" -- the form the one-GPU tests exercise)
+    spmd_kind = {"kind": None}
+
+    def spmd_open(kind):
+        nonlocal gather
+        if kind == "native":
+            spmd_native_init()
+            h2g.comm_spmd_install(not args.no_subcosets)
+        else:
+            gather = h2g_dist.SpmdGather(dist, group=CTRL if kind == "host" else None,
+                                         subcosets=not args.no_subcosets)
+            gather.install()
+
+    def spmd_close(kind):
+        if kind == "native":
+            h2g.comm_spmd_uninstall()
+        else:
+            gather.uninstall()
+
+    def spmd_native_init():
+        import torch as _t
+        uid = _t.zeros(256, dtype=_t.uint8)
+        if rank == 0:
+            uid.copy_(_t.frombuffer(bytearray(h2g.comm_unique_id()), dtype=_t.uint8))
+        dist.broadcast(uid, 0, group=CTRL)
+        h2g.comm_init(bytes(uid.numpy().tobytes()), world, rank)
+
+    if spmd:
+        kinds = [kd for kd in args.spmd_transports.split(",")
+                 if (kd != "native" or args.transport == "native" or args.dist_backend == "gloo")
+                 and (kd != "torch" or dist.get_backend() == "nccl")]
+        notes = []
+        for kind in kinds:
+            ok = 1
+            try:
+                spmd_open(kind)
+                try:
+                    step()  # the first warm-up proof doubles as the transport check
+                finally:
+                    spmd_close(kind)
+            except Exception as e:  # every rank learns of any failure and tries the next
+                ok = 0
+                notes.append(f"{kind}: {type(e).__name__}: {str(e)[:200]}")
+            if int(ctrl_all_reduce(ok, dist, dist.ReduceOp.MIN)):
+                spmd_kind["kind"] = kind
+                break
+            if kind == "native":
+                h2g.comm_destroy()
+        if spmd_kind["kind"] is None:
+            raise RuntimeError("no SPMD transport proved on every rank: " + "; ".join(notes))
+        native = spmd_kind["kind"] == "native"
+        if spmd_kind["kind"] == "host" and dist.get_backend() == "nccl":
+            RCCL_SUSPECT = True
+        if notes:
+            transport_note = "fell back to the " + spmd_kind["kind"] + " transport after: " + "; ".join(notes)
+
     def session(body):
         """shard: rank 0 proves with the slab transport installed, peers serve until it
         stops; spmd: every rank proves with the all-gather installed"""
         if spmd:
-            if native:
+            kind = spmd_kind["kind"]
+            if kind == "native":
                 h2g.comm_spmd_install(not args.no_subcosets)
             else:
                 gather.install()
             try:
                 body()
             finally:
-                if native:
-                    h2g.comm_spmd_uninstall()
-                else:
-                    gather.uninstall()
+                spmd_close(kind)
             return
         if worker:
             if native:
@@ -429,14 +499,14 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     session(warm)
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=CTRL)
     torch.cuda.synchronize()
     h2g.profile_enable(True)
     t0 = time.perf_counter()
     session(timed)
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=CTRL)
     elapsed = time.perf_counter() - t0
     h2g.profile_enable(False)
     calls, phases, union = h2g.profile_msm_collect(with_union=True)
@@ -446,10 +516,9 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     if spmd:  # every rank wrote the proof: the same bytes on all ranks
         import hashlib
         hd = torch.frombuffer(bytearray(hashlib.sha256(proofs[0]).digest()), dtype=torch.uint8).to(torch.int64)
-        hd = hd.to(dev) if dist.get_backend() == "nccl" else hd
         allh = [torch.empty_like(hd) for _ in range(world)]
-        dist.all_gather(allh, hd)
-        extra["ranks_equal"] = all(bool(torch.equal(a.cpu(), allh[0].cpu())) for a in allh)
+        dist.all_gather(allh, hd, group=CTRL)
+        extra["ranks_equal"] = all(bool(torch.equal(a, allh[0])) for a in allh)
     if rank == 0:
         assert all(p == proofs[0] for p in proofs), "non-deterministic proof bytes"
         # outside the timed region: the proof checked by the independent verifier
@@ -507,7 +576,9 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                        "parallelism": ("single GPU per proof" if world == 1 else
                                        f"one proof over {world} GPUs, SPMD: every rank runs the prover and "
                                        "computes its point slab of each commitment MSM, partials all-gathered ("
-                                       + ("libh2g RCCL all-gather" if native else "torch.distributed all_gather")
+                                       + ("libh2g RCCL all-gather" if native else
+                                          "torch.distributed all_gather over "
+                                          + ("RCCL" if spmd_kind["kind"] == "torch" else "gloo, host-staged"))
                                        + ("); extended-domain cosets + evaluate_h replicated" if args.no_subcosets else
                                           "); extended-domain sub-cosets + evaluate_h divided over the ranks, h "
                                           "broadcast; other transforms and SHPLONK replicated") if spmd else
@@ -635,7 +706,7 @@ def measure_msm(h2g, torch, dev, log_n, steps, warmup, dist=None, world=1, rank=
         step()
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=CTRL)
     torch.cuda.synchronize()
     h2g.profile_enable(True)
     t0 = time.perf_counter()
@@ -643,7 +714,7 @@ def measure_msm(h2g, torch, dev, log_n, steps, warmup, dist=None, world=1, rank=
         step()
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=CTRL)
     el = time.perf_counter() - t0
     h2g.profile_enable(False)
     calls, phases = h2g.profile_msm_collect()
@@ -679,7 +750,7 @@ def run_msm(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         step()
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=CTRL)
     torch.cuda.synchronize()
     h2g.profile_enable(True)
     t0 = time.perf_counter()
@@ -689,7 +760,7 @@ def run_msm(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             result["parts"] = gather_partials(result["p"], dist, world, dev)
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=CTRL)
     elapsed = time.perf_counter() - t0
     h2g.profile_enable(False)
     calls, phases, union = h2g.profile_msm_collect(with_union=True)
@@ -760,6 +831,10 @@ def main():
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl", help=argparse.SUPPRESS)
     ap.add_argument("--transport", choices=("native", "torch"), default="native",
                     help="shard mode: libh2g's own RCCL communicators, or torch.distributed slabs (h2g_dist)")
+    ap.add_argument("--spmd-transports", default="native,torch,host",
+                    help="spmd: transports to try in order, the first that proves on every rank is used "
+                         "(native = libh2g's RCCL communicator, torch = torch.distributed over RCCL, "
+                         "host = torch.distributed over gloo with host-staged exchanges)")
     args = ap.parse_args()
     if not args.k:
         args.k = KECCAK_K if args.workload == "keccak" else PROVE_K
@@ -783,6 +858,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    global CTRL
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         if args.dist_backend == "gloo":  # rehearsal: ranks may share GPUs, host-staged exchanges
@@ -790,9 +866,11 @@ def main():
             local %= torch.cuda.device_count()
             torch.cuda.set_device(local)
             dist.init_process_group("gloo")
+            CTRL = dist.group.WORLD
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            CTRL = dist.new_group(backend="gloo")
     else:
         torch.cuda.set_device(0)
 

@@ -5,8 +5,8 @@
 
 Objects go to yet-another-halo2-fork_amd/build/, the library to
 yet-another-halo2-fork_amd/lib/libh2g.so (git-ignored; travels to the GPU box
-with the gpurun snapshot).  Incremental: a source is recompiled when it or any
-header in csrc/ is newer than its object.
+with the gpurun snapshot).  Incremental: a source is recompiled when it or a header it
+includes (transitively) is newer than its object.
 """
 import concurrent.futures as cf
 import glob
@@ -29,16 +29,34 @@ def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
 
 
-def _newest_header():
-    hs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(os.path.dirname(PKG), "include", "*.h"))
-    return max((os.path.getmtime(h) for h in hs), default=0)
+INC_DIRS = (CSRC, os.path.join(os.path.dirname(PKG), "include"))
+
+
+def _includes(path, seen):
+    """the quoted includes of `path`, transitively (csrc/ and include/)"""
+    for line in open(path, errors="replace"):
+        line = line.strip()
+        if not line.startswith("#include \""):
+            continue
+        name = line.split('"')[1]
+        for d in INC_DIRS:
+            h = os.path.join(d, name)
+            if os.path.exists(h) and h not in seen:
+                seen.add(h)
+                _includes(h, seen)
+                break
+    return seen
+
+
+def _newest_dep(src):
+    return max((os.path.getmtime(h) for h in _includes(src, set())), default=0)
 
 
 def compile_one(src, force):
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
     if not force and os.path.exists(obj):
         t = os.path.getmtime(obj)
-        if t >= os.path.getmtime(src) and t >= _newest_header():
+        if t >= os.path.getmtime(src) and t >= _newest_dep(src):
             return obj, None
     lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"]
     cmd = [HIPCC] + CFLAGS + lang + ["-c", src, "-o", obj]

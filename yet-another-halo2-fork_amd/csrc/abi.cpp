@@ -224,9 +224,21 @@ int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFi
   if (nb < 1 || nb > MSM_MAX_BATCH) return fail(H2G_ERR_ARG, "msm: bad batch size");
   if (!d->h_ring) {
     HIPCHK(hipHostMalloc(&d->h_ring, MSM_RING * sizeof(G1xyzz), hipHostMallocDefault));
-    for (int i = 0; i < MSM_SLOTS; i++) HIPCHK(make_stream(&d->mstream[i], "H2G_CU_MASK_MSM"));
+    for (int i = 0; i < MSM_STREAMS; i++) HIPCHK(make_stream(&d->mstream[i], "H2G_CU_MASK_MSM"));
     for (int i = 0; i < MSM_RING; i++) HIPCHK(hipEventCreateWithFlags(&d->ring_ev[i], hipEventDisableTiming));
+    for (int i = 0; i < MSM_SLOTS; i++)
+      for (hipEvent_t* e : {&d->mev_p2a[i], &d->mev_a2r[i], &d->mev_free[i]})
+        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
+  // H2G_MSM_PIPE=1: the stage pipeline (runtime.h).  Off by default: measured slower --
+  // a partition or reduction launched beside an accumulation gets CUs only as its blocks
+  // retire, so the gaps between accumulations stayed 1-6 ms and the serialised
+  // accumulations lost the second stream's overlap (C3 k = 22: 89.5-91.1 vs 87.9-89.0 ms,
+  // profiles/r03/s3/ab_msm_pipe)
+  static const bool pipe = [] {
+    const char* e = std::getenv("H2G_MSM_PIPE");
+    return e ? std::atoi(e) != 0 : false;
+  }();
   int rings[MSM_MAX_BATCH];
   int got = 0;
   for (int k = 0; k < MSM_RING && got < nb; k++) {
@@ -235,12 +247,18 @@ int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFi
   }
   if (got < nb) return fail(H2G_ERR_STATE, "msm: too many outstanding asynchronous MSMs");
   d->next_ring = (rings[nb - 1] + 1) % MSM_RING;
-  const int slot = d->next_slot;
-  d->next_slot = (slot + 1) % MSM_SLOTS;
-  hipStream_t ms = d->mstream[slot];
-  // order after the producer's work (the scalars)
+  const int nslots = pipe ? MSM_SLOTS : 2;
+  const int slot = d->next_slot % nslots;
+  d->next_slot = (slot + 1) % nslots;
+  // ms: where the MSM starts (its partition) -- rs: where it ends (reduction, result copy)
+  hipStream_t ms = pipe ? d->mstream[0] : d->mstream[slot];
+  hipStream_t rs = pipe ? d->mstream[2] : ms;
+  const MsmStreams ss{d->mstream[0], d->mstream[1], d->mstream[2], d->mev_p2a[slot], d->mev_a2r[slot]};
+  // order after the producer's work (the scalars) and, pipelined, after the reduction of
+  // the workspace's previous MSM
   HIPCHK(hipEventRecord(d->ring_ev[rings[0]], producer));
   HIPCHK(hipStreamWaitEvent(ms, d->ring_ev[rings[0]], 0));
+  if (pipe && d->mws_used[slot]) HIPCHK(hipStreamWaitEvent(ms, d->mev_free[slot], 0));
   MsmPhaseEvents* pe = nullptr;
   if (g_profile && n > 0) {
     MsmPhaseEvents ev;
@@ -256,14 +274,19 @@ int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFi
   } else {
     MsmScalarList list;
     for (int b = 0; b < nb; b++) list.p[b] = reinterpret_cast<const Fr*>(sc[b]);
-    if (nb == 1) HIPCHK(msm_run_fixed(list.p[0], fb, off, n, &d->mws[slot], nullptr, ms, pe));
-    else HIPCHK(msm_run_fixed_batch(list, nb, fb, off, n, &d->mws[slot], ms, pe));
+    const MsmStreams* pss = pipe ? &ss : nullptr;
+    if (nb == 1) HIPCHK(msm_run_fixed(list.p[0], fb, off, n, &d->mws[slot], nullptr, ms, pe, pss));
+    else HIPCHK(msm_run_fixed_batch(list, nb, fb, off, n, &d->mws[slot], ms, pe, pss));
     const G1xyzz* win = reinterpret_cast<const G1xyzz*>(d->mws[slot].windows);
     for (int b = 0; b < nb; b++)
-      HIPCHK(hipMemcpyAsync(host + rings[b], win + b, sizeof(G1xyzz), hipMemcpyDeviceToHost, ms));
+      HIPCHK(hipMemcpyAsync(host + rings[b], win + b, sizeof(G1xyzz), hipMemcpyDeviceToHost, rs));
+  }
+  if (pipe) {
+    HIPCHK(hipEventRecord(d->mev_free[slot], rs));
+    d->mws_used[slot] = true;
   }
   for (int b = 0; b < nb; b++) {
-    HIPCHK(hipEventRecord(d->ring_ev[rings[b]], ms));
+    HIPCHK(hipEventRecord(d->ring_ev[rings[b]], rs));
     d->ring_busy[rings[b]] = true;
     t[b].slot = slot;
     t[b].ring = rings[b];
@@ -291,7 +314,7 @@ int msm_collect(Device* d, MsmTicket* t, uint64_t* out) {
 
 int msm_fence(Device* d, hipStream_t consumer) {
   if (!d->h_ring) return H2G_OK;
-  for (int i = 0; i < MSM_SLOTS; i++) {
+  for (int i = 0; i < MSM_STREAMS; i++) {
     hipEvent_t e;
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventRecord(e, d->mstream[i]));
@@ -488,12 +511,15 @@ int h2g_shutdown(void) {
     (void)hipSetDevice(dev->id);
     (void)hipStreamSynchronize(dev->stream);
     msm_free(&dev->msm);
-    for (int i = 0; i < MSM_SLOTS; i++) {
-      msm_free(&dev->mws[i]);
+    for (int i = 0; i < MSM_STREAMS; i++)
       if (dev->mstream[i]) {
         (void)hipStreamSynchronize(dev->mstream[i]);
         (void)hipStreamDestroy(dev->mstream[i]);
       }
+    for (int i = 0; i < MSM_SLOTS; i++) {
+      msm_free(&dev->mws[i]);
+      for (hipEvent_t e : {dev->mev_p2a[i], dev->mev_a2r[i], dev->mev_free[i]})
+        if (e) (void)hipEventDestroy(e);
     }
     for (int i = 0; i < MSM_RING; i++)
       if (dev->ring_ev[i]) (void)hipEventDestroy(dev->ring_ev[i]);

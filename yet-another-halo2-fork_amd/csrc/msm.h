@@ -50,6 +50,15 @@ struct MsmScalarList {
   const Fr* p[MSM_MAX_BATCH];
 };
 
+// Stage streams of one pipelined MSM: the bucket partition runs on `part`, the
+// accumulation on `acc`, the fixup and the reduction on `red` (the events order them), so
+// that consecutive MSMs overlap one's partition or reduction with another's accumulation.
+// The caller keeps one workspace per MSM in flight and orders a workspace's reuse.
+struct MsmStreams {
+  hipStream_t part, acc, red;
+  hipEvent_t p2a, a2r;
+};
+
 // sum_i scalars[i] * bases[i]; scalars Montgomery Fr, bases affine Montgomery Fq
 // (halo2curves layout).  Asynchronous on `st`.  If d_out != nullptr the affine
 // result is written there by one device lane; otherwise the W window sums are
@@ -72,13 +81,16 @@ int msm_choose_c_fixed(size_t n);
 hipError_t msm_fixed_base_build(const G1Affine* d_bases, size_t n, int c, MsmFixedBase* fb, hipStream_t st);
 void msm_fixed_base_free(MsmFixedBase* fb);
 // sum_{i < n} scalars[i] * bases[off + i]; leaves ws->windows[0] (ws->last_W = 1)
+// ss: stage streams (st is then unused; results are ordered on ss->red)
 hipError_t msm_run_fixed(const Fr* d_scalars, const MsmFixedBase& fb, size_t off, size_t n, MsmWorkspace* ws,
-                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof = nullptr);
+                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof = nullptr,
+                         const MsmStreams* ss = nullptr);
 // nbatch MSMs sum_i list.p[b][i] * bases[off + i] (b < nbatch <= MSM_MAX_BATCH) as one
 // pipeline -- one digits launch, one sort, one accumulation, one reduction with a bucket
 // set per MSM -- so the latency-bound reduction is paid once.  Leaves MSM b's sum in
 // ws->windows[b] (ws->last_W = nbatch).  nbatch * W * n must stay below 2^31.
 hipError_t msm_run_fixed_batch(const MsmScalarList& list, int nbatch, const MsmFixedBase& fb, size_t off, size_t n,
-                               MsmWorkspace* ws, hipStream_t st, MsmPhaseEvents* prof = nullptr);
+                               MsmWorkspace* ws, hipStream_t st, MsmPhaseEvents* prof = nullptr,
+                               const MsmStreams* ss = nullptr);
 
 }  // namespace h2g

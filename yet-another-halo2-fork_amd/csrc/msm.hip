@@ -35,7 +35,7 @@
 #include <algorithm>
 #include <string>
 
-#include "msm.h"
+#include "msm_part.h"
 
 namespace h2g {
 
@@ -68,266 +68,6 @@ __device__ __forceinline__ G1Affine ld_aff(const G1Affine* p) {
   r.y.l[0] = c.x; r.y.l[1] = c.y; r.y.l[2] = c.z; r.y.l[3] = c.w;
   r.y.l[4] = d.x; r.y.l[5] = d.y; r.y.l[6] = d.z; r.y.l[7] = d.w;
   return r;
-}
-
-// 1. signed digits: key = window * NB + |d| - 1 (generic mode), value = point index.
-// Fixed-base mode (bases pre-multiplied per window, table[w * stride + i] = [2^(c w)] P_i):
-// every window shares one set of NB buckets, key = |d| - 1, value = w * stride + i.
-// Batched fixed-base mode (blockIdx.y = b of nbatch MSMs over the same windows): MSM b
-// owns bucket set b, key = b * NB + |d| - 1, so one partition / accumulation / reduction
-// serves them all.  Negative digits set bit 31 of the value.
-// 2. bucket partition of the entries ------------------------------------------------
-// The accumulation needs each bucket's entries contiguous, not sorted: a two-round
-// counting partition replaces the radix sort.  Round 1 splits by the key's high bits
-// (coarse bins) straight from the scalars, round 2 by the low FB bits inside each coarse
-// bin (a bin's region is a few hundred KB, so its scattered writes stay in L2).  Zero
-// digits produce no entry at all.  Order inside a bucket is arbitrary (the sum is exact).
-#ifndef H2G_MSM_PT
-#define H2G_MSM_PT 512
-#endif
-#ifndef H2G_MSM_FPER  // entries per fine-kernel thread: 8 (2048-entry tiles) measured best at 10 fine bits
-#define H2G_MSM_FPER 8
-#endif
-static constexpr int PT = H2G_MSM_PT;      // threads of the coarse kernels (one scalar each)
-static constexpr int PWG = 16;             // windows per coarse-kernel thread (grid.z groups)
-static constexpr int FT = 256;             // threads of the fine kernels
-static constexpr int FPER = H2G_MSM_FPER;  // entries per fine-kernel thread
-static constexpr uint32_t FTILE = (uint32_t)FT * FPER;
-static constexpr int FB_MAX = 11;       // fine bits
-static constexpr int COARSE_MAX = 2048;  // coarse bins (keys < 2^22)
-
-// Fixed-base windows have balanced widths: W = ceil(255 / c) windows covering the 255
-// bits signed digits need, the first 255 % W of them one bit wider (<= c).  Uniform
-// c-bit windows leave a short top window (255 - c (W - 1) bits: 7 at c = 19, W = 14)
-// whose digits pile n entries into a few buckets -- the big-bucket path, ~0.2-0.5 ms.
-__host__ __device__ __forceinline__ int fb_width(int W, int w) { return 255 / W + (w < 255 % W ? 1 : 0); }
-
-// the signed digits of scalar i (batch bi) for windows [w0, w0 + PWG): fn(slot, key, val)
-// for each nonzero digit (same key / value encoding as msm_digits_kernel); fixed-base
-// windows take their balanced widths (fb_width), generic ones c bits each
-template <class Fn>
-__device__ __forceinline__ void scalar_digits(const MsmScalarList& list, size_t n, int c, int W, uint32_t NB,
-                                              int fixed, size_t stride, uint32_t bi, size_t i, int w0, Fn fn) {
-  const uint4* q = reinterpret_cast<const uint4*>(list.p[bi] + i);
-  uint4 a = q[0], b = q[1];
-  Fr s;
-  s.l[0] = a.x; s.l[1] = a.y; s.l[2] = a.z; s.l[3] = a.w;
-  s.l[4] = b.x; s.l[5] = b.y; s.l[6] = b.z; s.l[7] = b.w;
-  Fr v = to_canonical(s);
-  uint32_t carry = 0;
-  const int wend = w0 + PWG < W ? w0 + PWG : W;
-  for (int w = 0; w < wend; w++) {
-    const int cw = fixed ? fb_width(W, w) : c;
-    const uint32_t mask = (1u << cw) - 1;
-    const uint32_t half = 1u << (cw - 1);
-    const uint32_t d = (v.l[0] & mask) + carry;
-#pragma unroll
-    for (int k = 0; k < 7; k++) v.l[k] = (v.l[k] >> cw) | (v.l[k + 1] << (32 - cw));
-    v.l[7] >>= cw;
-    uint32_t mag, sign;
-    if (d > half) {  // negative digit d - 2^cw (d == 2^cw gives digit 0, carry 1)
-      mag = (1u << cw) - d;
-      carry = 1;
-      sign = 0x80000000u;
-    } else {
-      mag = d;
-      carry = 0;
-      sign = 0;
-    }
-    if (w < w0 || mag == 0) continue;
-    const uint32_t koff = fixed ? bi * NB : (uint32_t)w * NB;
-    const uint32_t val = (fixed ? (uint32_t)((size_t)w * stride + i) : (uint32_t)i) | sign;
-    fn(w - w0, koff + mag - 1, val);
-  }
-}
-
-// zeroed by the coarse histogram kernel for the later phases: bucket [start, end) (empty
-// buckets keep 0, 0), the big-item counters, the plane reduction's finished-block counts
-struct MsmZero {
-  uint32_t* bstart;
-  uint32_t* bend;
-  size_t nb;
-  uint32_t* counters;
-  uint32_t* rdone;
-  uint32_t nrd;
-};
-
-// round 1a: coarse histogram (LDS per block, one global atomic per bin and block)
-__global__ void __launch_bounds__(PT)
-msm_coarse_hist_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride, int fb,
-                       uint32_t ncoarse, uint32_t* __restrict__ ccount, MsmZero z) {
-  __shared__ uint32_t h[COARSE_MAX];
-  {  // the pipeline's other per-MSM zeroing (no separate fills)
-    const size_t nthr = (size_t)gridDim.x * gridDim.y * gridDim.z * PT;
-    const size_t tid = (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * PT + threadIdx.x;
-    for (size_t i = tid; i < z.nb; i += nthr) {
-      z.bstart[i] = 0;
-      z.bend[i] = 0;
-    }
-    if (tid < 2) z.counters[tid] = 0;
-    if (tid < z.nrd) z.rdone[tid] = 0;
-  }
-  for (uint32_t t = threadIdx.x; t < ncoarse; t += PT) h[t] = 0;
-  __syncthreads();
-  const size_t i = blockIdx.x * (size_t)PT + threadIdx.x;
-  if (i < n)
-    scalar_digits(list, n, c, W, NB, fixed, stride, blockIdx.y, i, blockIdx.z * PWG,
-                  [&](int, uint32_t key, uint32_t) { atomicAdd(&h[key >> fb], 1u); });
-  __syncthreads();
-  for (uint32_t t = threadIdx.x; t < ncoarse; t += PT)
-    if (h[t]) atomicAdd(&ccount[t], h[t]);
-}
-
-// exclusive scan of cnt[0, len) (one block, len <= 1024 * 64): off[] = cursor[] =
-// prefix; *total = sum; clear: cnt[] is zeroed after use (the counts start at zero for
-// the next MSM without a fill)
-__global__ void __launch_bounds__(1024)
-msm_scan_kernel(uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__ off,
-                uint32_t* __restrict__ cursor, uint32_t* __restrict__ total, bool clear) {
-  __shared__ uint32_t part[1024];
-  const uint32_t per = (len + 1023) / 1024;
-  const uint32_t lo = threadIdx.x * per, hi = lo + per < len ? lo + per : len;
-  uint32_t s = 0;
-  for (uint32_t i = lo; i < hi; i++) s += cnt[i];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
-    const uint32_t v = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-  for (uint32_t i = lo; i < hi; i++) {
-    off[i] = run;
-    if (cursor) cursor[i] = run;
-    run += cnt[i];
-    if (clear) cnt[i] = 0;
-  }
-  if (threadIdx.x == 1023 && total) *total = part[1023];
-}
-
-// large scans (the per-key counts): 1024-element blocks scanned locally, block sums
-// scanned by msm_scan_kernel, then added back
-__global__ void __launch_bounds__(1024)
-msm_scan_block_kernel(uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__ off,
-                      uint32_t* __restrict__ bsum) {
-  __shared__ uint32_t part[1024];
-  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
-  const uint32_t v0 = i < len ? cnt[i] : 0;
-  if (i < len) cnt[i] = 0;  // zero for the next MSM (cnt is read only here)
-  part[threadIdx.x] = v0;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {
-    const uint32_t v = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  if (i < len) off[i] = part[threadIdx.x] - v0;
-  if (threadIdx.x == 1023) bsum[blockIdx.x] = part[1023];
-}
-__global__ void __launch_bounds__(1024)
-msm_scan_add_kernel(uint32_t* __restrict__ off, uint32_t len, const uint32_t* __restrict__ boff,
-                    uint32_t* __restrict__ cursor) {
-  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
-  if (i >= len) return;
-  const uint32_t v = off[i] + boff[blockIdx.x];
-  off[i] = v;
-  cursor[i] = v;
-}
-
-// round 1b: entries written into their coarse bins (ranks from LDS atomics, one global
-// reservation per bin and block)
-__global__ void __launch_bounds__(PT)
-msm_coarse_scatter_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride, int fb,
-                          uint32_t ncoarse, uint32_t* __restrict__ ccursor, uint64_t* __restrict__ out) {
-  __shared__ uint32_t cnt[COARSE_MAX], base[COARSE_MAX];
-  for (uint32_t t = threadIdx.x; t < ncoarse; t += PT) cnt[t] = 0;
-  __syncthreads();
-  uint64_t ent[PWG];
-  uint32_t rk[PWG];
-#pragma unroll
-  for (int k = 0; k < PWG; k++) rk[k] = ~0u;
-  const size_t i = blockIdx.x * (size_t)PT + threadIdx.x;
-  if (i < n)
-    scalar_digits(list, n, c, W, NB, fixed, stride, blockIdx.y, i, blockIdx.z * PWG,
-                  [&](int slot, uint32_t key, uint32_t val) {
-#pragma unroll
-                    for (int k = 0; k < PWG; k++)
-                      if (k == slot) {
-                        ent[k] = ((uint64_t)key << 32) | val;
-                        rk[k] = atomicAdd(&cnt[key >> fb], 1u);
-                      }
-                  });
-  __syncthreads();
-  for (uint32_t t = threadIdx.x; t < ncoarse; t += PT)
-    if (cnt[t]) base[t] = atomicAdd(&ccursor[t], cnt[t]);
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < PWG; k++)
-    if (rk[k] != ~0u) out[base[(uint32_t)(ent[k] >> 32) >> fb] + rk[k]] = ent[k];
-}
-
-// round 2a: per-key counts inside coarse bins: tiles of FTILE entries; entries of the
-// tile's first bin go through an LDS histogram, others (tiles straddling bins) directly
-__global__ void __launch_bounds__(FT)
-msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
-                     uint32_t* __restrict__ kcount) {
-  __shared__ uint32_t h[1 << FB_MAX];
-  const uint32_t total = *d_total;
-  const uint32_t lo = blockIdx.x * FTILE;
-  if (lo >= total) return;
-  const uint32_t nf = 1u << fb;
-  for (uint32_t t = threadIdx.x; t < nf; t += FT) h[t] = 0;
-  const uint32_t bin0 = (uint32_t)(in[lo] >> 32) >> fb;
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < FPER; k++) {
-    const uint32_t p = lo + k * FT + threadIdx.x;
-    if (p >= total) break;
-    const uint32_t key = (uint32_t)(in[p] >> 32);
-    if ((key >> fb) == bin0) atomicAdd(&h[key & (nf - 1)], 1u);
-    else atomicAdd(&kcount[key], 1u);
-  }
-  __syncthreads();
-  for (uint32_t t = threadIdx.x; t < nf; t += FT)
-    if (h[t]) atomicAdd(&kcount[(bin0 << fb) + t], h[t]);
-}
-
-// round 2b: the same tiles scattered to their keys' positions
-__global__ void __launch_bounds__(FT)
-msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
-                        uint32_t* __restrict__ kcursor, uint64_t* __restrict__ out) {
-  __shared__ uint32_t cnt[1 << FB_MAX], base[1 << FB_MAX];
-  const uint32_t total = *d_total;
-  const uint32_t lo = blockIdx.x * FTILE;
-  if (lo >= total) return;
-  const uint32_t nf = 1u << fb;
-  for (uint32_t t = threadIdx.x; t < nf; t += FT) cnt[t] = 0;
-  const uint32_t bin0 = (uint32_t)(in[lo] >> 32) >> fb;
-  __syncthreads();
-  uint64_t ent[FPER];
-  uint32_t rk[FPER];
-#pragma unroll
-  for (int k = 0; k < FPER; k++) {
-    const uint32_t p = lo + k * FT + threadIdx.x;
-    rk[k] = ~0u;
-    ent[k] = 0;
-    if (p < total) {
-      ent[k] = in[p];
-      const uint32_t key = (uint32_t)(ent[k] >> 32);
-      if ((key >> fb) == bin0) rk[k] = atomicAdd(&cnt[key & (nf - 1)], 1u);
-      else out[atomicAdd(&kcursor[key], 1u)] = ent[k];
-    }
-  }
-  __syncthreads();
-  for (uint32_t t = threadIdx.x; t < nf; t += FT)
-    if (cnt[t]) base[t] = atomicAdd(&kcursor[(bin0 << fb) + t], cnt[t]);
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < FPER; k++)
-    if (rk[k] != ~0u) out[base[(uint32_t)(ent[k] >> 32) & (nf - 1)] + rk[k]] = ent[k];
 }
 
 // 3-4. accumulation straight from the sorted entries -------------------------------
@@ -1119,9 +859,18 @@ uint32_t msm_chunk_len(size_t total, size_t nbt) {
 
 static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Affine* d_bases, size_t n, int c,
                                int W, int fixed, size_t stride, MsmWorkspace* ws, uint32_t item_len, G1Affine* d_out,
-                               hipStream_t st, MsmPhaseEvents* prof) {
+                               hipStream_t st0, MsmPhaseEvents* prof, const MsmStreams* ss) {
+  // stage streams: partition on ss->part, accumulation on ss->acc, fixup + reduction on
+  // ss->red (one stream for all three without ss)
+  hipStream_t st = ss ? ss->part : st0;
 #define H2G_PHASE(i) \
   if (prof) H2G_TRY(hipEventRecord(prof->ev[i], st))
+#define H2G_STAGE(next, ev)                             \
+  if (ss && (next) != st) {                             \
+    H2G_TRY(hipEventRecord((ev), st));                  \
+    H2G_TRY(hipStreamWaitEvent((next), (ev), 0));       \
+    st = (next);                                        \
+  }
   const uint32_t NB = 1u << (c - 1);
   if (nbatch < 1 || nbatch > MSM_MAX_BATCH || (!fixed && nbatch != 1)) return hipErrorInvalidValue;
   const int WB = fixed ? nbatch : W;  // bucket sets
@@ -1276,33 +1025,37 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
 
   const int T = MSM_THREADS;
   H2G_PHASE(0);
-  {  // round 1: coarse bins straight from the scalars
-    const dim3 g((unsigned)((n + PT - 1) / PT), (unsigned)nbatch, (unsigned)((W + PWG - 1) / PWG));
-    const MsmZero z{bstart, bend, (size_t)nbt, counters, rdone, (uint32_t)WB};
-    hipLaunchKernelGGL(msm_coarse_hist_kernel, g, dim3(PT), 0, st, list, n, c, W, NB, fixed, stride, fb, ncoarse,
-                       ccount, z);
-    hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, ccount, ncoarse, coff, ccursor, d_total, true);
-    hipLaunchKernelGGL(msm_coarse_scatter_kernel, g, dim3(PT), 0, st, list, n, c, W, NB, fixed, stride, fb, ncoarse,
-                       ccursor, keys_in);
-    H2G_TRY(hipGetLastError());
-  }
-  H2G_PHASE(1);
-  if (prof && prof->entries) H2G_TRY(hipMemcpyAsync(prof->entries, d_total, 4, hipMemcpyDeviceToHost, st));
-  {  // round 2: keys inside the coarse bins
-    const unsigned tiles = (unsigned)((total + FTILE - 1) / FTILE);
-    hipLaunchKernelGGL(msm_fine_hist_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)keys_in,
-                       (const uint32_t*)d_total, fb, kcount);
-    hipLaunchKernelGGL(msm_scan_block_kernel, dim3(kblocks), dim3(1024), 0, st, kcount, nbt, koff,
-                       kbsum);
-    hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, kbsum, kblocks, kboff, (uint32_t*)nullptr,
-                       (uint32_t*)nullptr, false);
-    hipLaunchKernelGGL(msm_scan_add_kernel, dim3(kblocks), dim3(1024), 0, st, koff, nbt, (const uint32_t*)kboff,
-                       kcursor);
-    hipLaunchKernelGGL(msm_fine_scatter_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)keys_in,
-                       (const uint32_t*)d_total, fb, kcursor, keys_out);
-    H2G_TRY(hipGetLastError());
+  {  // rounds 1 and 2 (msm_part.hip); phase event 1 between them
+    MsmPartArgs pa;
+    pa.list = list;
+    pa.nbatch = nbatch;
+    pa.n = n;
+    pa.c = c;
+    pa.W = W;
+    pa.NB = NB;
+    pa.fixed = fixed;
+    pa.stride = stride;
+    pa.total = total;
+    pa.fb = fb;
+    pa.ncoarse = ncoarse;
+    pa.nbt = nbt;
+    pa.kblocks = kblocks;
+    pa.ccount = ccount;
+    pa.coff = coff;
+    pa.ccursor = ccursor;
+    pa.d_total = d_total;
+    pa.kbsum = kbsum;
+    pa.kboff = kboff;
+    pa.kcount = kcount;
+    pa.koff = koff;
+    pa.kcursor = kcursor;
+    pa.keys_in = keys_in;
+    pa.keys_out = keys_out;
+    pa.z = MsmZero{bstart, bend, (size_t)nbt, counters, rdone, (uint32_t)WB};
+    H2G_TRY(msm_partition(pa, st, prof));
   }
   H2G_PHASE(2);
+  H2G_STAGE(ss->acc, ss->p2a);
   // (bucket bounds, counters: zeroed by the coarse histogram; empty buckets: by the fixup)
   H2G_PHASE(3);
   static const bool prefetch = [] {
@@ -1317,6 +1070,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     hipLaunchKernelGGL(msm_acc_kernel<false>, dim3(cgrid), dim3(T), 0, st, d_bases, (const uint64_t*)keys_out,
                        (const uint32_t*)d_total, sentinel, L, buckets, bnd, bstart, bend);
   H2G_PHASE(4);
+  H2G_STAGE(ss->red, ss->a2r);
   static const uint32_t fix_q4_max = [] {  // H2G_MSM_FIXUP_Q4_MAX: bucket sets with quad fixup (A/B)
     const char* e = getenv("H2G_MSM_FIXUP_Q4_MAX");
     return e ? (uint32_t)atol(e) : 32768u;  // 2^16 buckets (2^19-point slabs): the lane form is faster
@@ -1401,6 +1155,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   H2G_TRY(hipGetLastError());
   H2G_PHASE(6);
 #undef H2G_PHASE
+#undef H2G_STAGE
   return hipSuccess;
 }
 
@@ -1409,7 +1164,8 @@ hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWo
   const int c = cfg.c > 0 ? cfg.c : msm_choose_c(n);
   MsmScalarList list;
   list.p[0] = d_scalars;
-  return msm_pipeline(list, 1, d_bases, n, c, msm_windows_for(c), 0, 0, ws, (uint32_t)cfg.item_len, d_out, st, prof);
+  return msm_pipeline(list, 1, d_bases, n, c, msm_windows_for(c), 0, 0, ws, (uint32_t)cfg.item_len, d_out, st, prof,
+                      nullptr);
 }
 
 int msm_choose_c_fixed(size_t n) {
@@ -1448,17 +1204,17 @@ void msm_fixed_base_free(MsmFixedBase* fb) {
 }
 
 hipError_t msm_run_fixed(const Fr* d_scalars, const MsmFixedBase& fb, size_t off, size_t n, MsmWorkspace* ws,
-                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof) {
+                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof, const MsmStreams* ss) {
   if (off + n > fb.n) return hipErrorInvalidValue;
   MsmScalarList list;
   list.p[0] = d_scalars;
-  return msm_pipeline(list, 1, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, d_out, st, prof);
+  return msm_pipeline(list, 1, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, d_out, st, prof, ss);
 }
 
 hipError_t msm_run_fixed_batch(const MsmScalarList& list, int nbatch, const MsmFixedBase& fb, size_t off, size_t n,
-                               MsmWorkspace* ws, hipStream_t st, MsmPhaseEvents* prof) {
+                               MsmWorkspace* ws, hipStream_t st, MsmPhaseEvents* prof, const MsmStreams* ss) {
   if (off + n > fb.n) return hipErrorInvalidValue;
-  return msm_pipeline(list, nbatch, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, nullptr, st, prof);
+  return msm_pipeline(list, nbatch, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, nullptr, st, prof, ss);
 }
 
 }  // namespace h2g

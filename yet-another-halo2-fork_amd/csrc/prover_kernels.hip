@@ -542,24 +542,26 @@ __global__ void __launch_bounds__(EV_T) eval_level1(const EvalReq* __restrict__ 
     if (threadIdx.x == 0) part[blockIdx.y * nbmax + blockIdx.x] = Fr::zero();
     return;
   }
-  __shared__ Fr pw[EV_L];  // pw[l] = x^(EV_S 2^l): one thread's squaring chain overlaps the Horner
+  // coalesced: thread t takes the coefficients base + t + EV_T i (i < EV_S), a wave's loads
+  // are 2 KB runs; acc_t = sum_i a_{t + EV_T i} (x^EV_T)^i, then sum_t acc_t x^t by a tree
+  // with the level weights pw[l] = x^(2^l) (one thread's squaring chain, pw[EV_L] = x^EV_T)
+  __shared__ Fr pw[EV_L + 1];
   const int t = threadIdx.x;
   if (t == 0) {
     Fr step = rq.x;
-#pragma unroll
-    for (int i = 1; i < EV_S; i <<= 1) step = step * step;
-    for (int l = 0; l < EV_L; l++) {
+    for (int l = 0; l <= EV_L; l++) {
       pw[l] = step;
       step = step * step;
     }
   }
-  const uint64_t lo = base + (uint64_t)t * EV_S;
+  __syncthreads();
+  const Fr X = pw[EV_L];
+  const uint64_t lo = base + (uint64_t)t;
   Fr acc = Fr::zero();
   for (int i = EV_S - 1; i >= 0; i--) {
-    const uint64_t j = lo + i;
-    acc = acc * rq.x + (j < rq.len ? ldf(rq.poly + j) : Fr::zero());
+    const uint64_t j = lo + (uint64_t)i * EV_T;
+    acc = acc * X + (j < rq.len ? ldf(rq.poly + j) : Fr::zero());
   }
-  // sum_t acc_t x^(EV_S t): tree with the level weights (255 products per block)
   sh[t] = acc;
   __syncthreads();
 #pragma unroll

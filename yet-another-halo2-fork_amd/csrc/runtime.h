@@ -84,10 +84,14 @@ struct Descriptor {
   MsmFixedBase fb;    // fixed-base windows of resident bases (owned: d aliases fb.table)
 };
 
-// Asynchronous fixed-base MSMs: two workspaces on two streams so that the
-// latency-bound phases (sort tail, fixup, reduction) of one MSM overlap the
-// accumulation of the next.  Results land in a pinned ring (one XYZZ point each).
-static constexpr int MSM_SLOTS = 2;
+// Asynchronous fixed-base MSMs: whole MSMs on two streams with a workspace each, so that
+// one MSM's latency-bound phases (partition tail, fixup, reduction) overlap another's
+// accumulation.  H2G_MSM_PIPE=1 (A/B, measured slower): pipelined by stage instead -- every
+// MSM's bucket partition on mstream[0], its accumulation on mstream[1], its fixup and
+// reduction on mstream[2], MSM_SLOTS workspaces rotating.  Results land in a pinned ring
+// (one XYZZ point each).
+static constexpr int MSM_SLOTS = 3;
+static constexpr int MSM_STREAMS = 3;
 static constexpr int MSM_RING = 64;
 struct MsmTicket {
   int slot = -1;
@@ -106,7 +110,9 @@ struct Device {
   void* h_windows = nullptr;  // pinned host copy of MSM window sums
   // async MSM slots
   MsmWorkspace mws[MSM_SLOTS];
-  hipStream_t mstream[MSM_SLOTS] = {};
+  hipStream_t mstream[MSM_STREAMS] = {};
+  hipEvent_t mev_p2a[MSM_SLOTS] = {}, mev_a2r[MSM_SLOTS] = {}, mev_free[MSM_SLOTS] = {};
+  bool mws_used[MSM_SLOTS] = {};
   int next_slot = 0;
   void* h_ring = nullptr;  // pinned G1xyzz[MSM_RING]
   hipEvent_t ring_ev[MSM_RING] = {};
