@@ -383,8 +383,9 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=3 + seed_off)
         pk = h2g.ProvingKey(params, circ)
         if spmd:  # lighter slabs for the ranks that own extended-domain sub-cosets
-            weights = h2g_dist.owner_weights(world, pk.extended_k, k, args.spmd_owner_weight) \
-                if args.spmd_owner_weight > 0 else None
+            weights = h2g_dist.owner_weights(world, pk.extended_k, k,
+                                             None if args.spmd_owner_weight < 0 else args.spmd_owner_weight) \
+                if args.spmd_owner_weight != 0 else None
             h2g.spmd_set_weights(weights)
             params.set_slab(*h2g_dist.slab(n, world, rank, weights=weights))
             spmd_weights["w"] = weights
@@ -820,8 +821,9 @@ def main():
                          "(spmd) or rank 0 proves and peers serve slabs (shard) -- or one proof per GPU (replicas)")
     ap.add_argument("--no-subcosets", action="store_true",
                     help="spmd: replicate the extended-domain work instead of splitting its sub-cosets")
-    ap.add_argument("--spmd-owner-weight", type=float, default=0.5,
-                    help="spmd: slab weight of the sub-coset owners against 1 for the other ranks (0: uniform)")
+    ap.add_argument("--spmd-owner-weight", type=float, default=-1,
+                    help="spmd: slab weight of the sub-coset owners against 1 for the other ranks "
+                         "(0: uniform, -1: measured default for the ratio of ranks to owners)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3, help="CPU baseline runs (median)")
     ap.add_argument("--no-krange", action="store_true",

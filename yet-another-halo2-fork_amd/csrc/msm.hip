@@ -70,85 +70,6 @@ __device__ __forceinline__ G1Affine ld_aff(const G1Affine* p) {
   return r;
 }
 
-// 3-4. accumulation straight from the sorted entries -------------------------------
-// The sorted array is cut into chunks of L entries, one thread per chunk.  A chunk's
-// run of one bucket is the whole bucket iff it neither continues from the previous
-// chunk nor into the next (two neighbour reads; no separate bounds pass): such
-// buckets are written directly, a run that crosses a chunk boundary goes to the
-// chunk's boundary slot (slot 0 = its first run, slot 1 = its last run).  The run
-// that begins a bucket records its start, the run that ends it its end (for the
-// fixup).  The sentinel entries (zero digits) sort last and end a chunk.
-__device__ __forceinline__ uint32_t ent_key(uint64_t e) { return (uint32_t)(e >> 32); }
-
-__device__ __forceinline__ void msm_emit(uint32_t key, const G1xyzz& acc, bool first, bool from_prev, bool to_next,
-                                         uint32_t a, uint32_t b, uint32_t t, G1xyzz* __restrict__ buckets,
-                                         G1xyzz* __restrict__ bnd, uint32_t* __restrict__ start,
-                                         uint32_t* __restrict__ end) {
-  const G1xyzz v = xyzz_canon2(acc);  // lazy [0, 2M) -> fully reduced for the later kernels
-  if (!from_prev) start[key] = a;
-  if (!to_next) end[key] = b;
-  if (!from_prev && !to_next) buckets[key] = v;
-  else bnd[2 * (size_t)t + (first ? 0 : 1)] = v;
-}
-
-// PF: software-pipelined gather -- the next entry's base point is loaded before
-// the current mixed addition, so its latency hides behind ~3000 VALU ops (costs
-// 16 VGPRs).
-template <bool PF>
-__global__ void __launch_bounds__(MSM_THREADS)
-msm_acc_kernel(const G1Affine* __restrict__ bases, const uint64_t* __restrict__ ent,
-               const uint32_t* __restrict__ d_total, uint32_t sentinel, uint32_t L, G1xyzz* __restrict__ buckets,
-               G1xyzz* __restrict__ bnd, uint32_t* __restrict__ start, uint32_t* __restrict__ end) {
-  const uint32_t total = *d_total;  // entries (nonzero digits) of the partition
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t lo = t * L;
-  if (lo >= total) return;
-  const uint32_t hi = lo + L < total ? lo + L : total;
-  uint64_t e = ent[lo];
-  uint32_t key = ent_key(e);
-  if (key == sentinel) return;
-  const bool prev_same = lo > 0 && ent_key(ent[lo - 1]) == key;
-  bool first = true;
-  uint32_t run_lo = lo;
-  G1xyzz acc = G1xyzz::identity();
-  G1Affine pt;
-  if (PF) pt = ld_aff(bases + ((uint32_t)e & 0x7fffffffu));
-  uint32_t p = lo;
-  for (; p < hi; p++) {
-    uint64_t e_next = 0;
-    G1Affine pt_next;
-    if (PF) {
-      e_next = ent[p + 1 < hi ? p + 1 : p];
-      pt_next = ld_aff(bases + ((uint32_t)e_next & 0x7fffffffu));
-    } else {
-      e = ent[p];
-#ifdef H2G_MSM_TIMING_GATHER_MASK  // timing-only A/B build: gather from a small (L2-resident) table
-      pt = ld_aff(bases + ((uint32_t)e & H2G_MSM_TIMING_GATHER_MASK));
-#else
-      pt = ld_aff(bases + ((uint32_t)e & 0x7fffffffu));
-#endif
-    }
-    const uint32_t k2 = ent_key(e);
-    if (k2 == sentinel) break;
-    const uint32_t v = (uint32_t)e;
-    if (k2 != key) {
-      msm_emit(key, acc, first, first && prev_same, false, run_lo, p, t, buckets, bnd, start, end);
-      first = false;
-      run_lo = p;
-      key = k2;
-      acc = G1xyzz::identity();
-    }
-    if (v >> 31) pt = affine_neg(pt);
-    acc = xyzz_madd_lazy(acc, pt);
-    if (PF) {
-      e = e_next;
-      pt = pt_next;
-    }
-  }
-  const bool to_next = p == hi && hi < total && ent_key(ent[hi]) == key;
-  msm_emit(key, acc, first, first && prev_same, to_next, run_lo, p, t, buckets, bnd, start, end);
-}
-
 // Buckets spanning chunks, one thread per bucket: the piece in its first chunk t0 is
 // that chunk's last run (slot 1) unless the bucket starts the chunk (slot 0); every
 // later chunk holds it as its first run (slot 0).  Buckets over more than MSM_SMALL
@@ -1058,17 +979,8 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   H2G_STAGE(ss->acc, ss->p2a);
   // (bucket bounds, counters: zeroed by the coarse histogram; empty buckets: by the fixup)
   H2G_PHASE(3);
-  static const bool prefetch = [] {
-    const char* e = getenv("H2G_MSM_PREFETCH");
-    return e ? atoi(e) != 0 : true;
-  }();
-  const unsigned cgrid = (unsigned)((nchunks + T - 1) / T);
-  if (prefetch)
-    hipLaunchKernelGGL(msm_acc_kernel<true>, dim3(cgrid), dim3(T), 0, st, d_bases, (const uint64_t*)keys_out,
-                       (const uint32_t*)d_total, sentinel, L, buckets, bnd, bstart, bend);
-  else
-    hipLaunchKernelGGL(msm_acc_kernel<false>, dim3(cgrid), dim3(T), 0, st, d_bases, (const uint64_t*)keys_out,
-                       (const uint32_t*)d_total, sentinel, L, buckets, bnd, bstart, bend);
+  H2G_TRY(msm_accumulate(d_bases, (const uint64_t*)keys_out, (const uint32_t*)d_total, sentinel, L, nchunks, buckets,
+                         bnd, bstart, bend, st));
   H2G_PHASE(4);
   H2G_STAGE(ss->red, ss->a2r);
   static const uint32_t fix_q4_max = [] {  // H2G_MSM_FIXUP_Q4_MAX: bucket sets with quad fixup (A/B)

@@ -1,4 +1,5 @@
-// msm_part.h -- the MSM's bucket partition (msm_part.hip), shared with msm.hip.
+// msm_part.h -- the MSM pipeline's stages in their own translation units (the bucket
+// partition, msm_part.hip; the accumulation, msm_acc.hip), shared with msm.hip.
 #pragma once
 #include "msm.h"
 
@@ -43,5 +44,11 @@ struct MsmPartArgs {
   MsmZero z;
 };
 hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* prof);
+
+// step 3 of the pipeline (msm_acc.hip): XYZZ accumulation of the bucket-sorted entries in
+// chunks of L, one thread per chunk
+hipError_t msm_accumulate(const G1Affine* bases, const uint64_t* ent, const uint32_t* d_total, uint32_t sentinel,
+                          uint32_t L, size_t nchunks, G1xyzz* buckets, G1xyzz* bnd, uint32_t* bstart, uint32_t* bend,
+                          hipStream_t st);
 
 }  // namespace h2g

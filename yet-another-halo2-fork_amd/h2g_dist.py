@@ -32,14 +32,26 @@ def slab(n, world, r, P=None, weights=None):
     return min(n, P * r // world), min(n, P * (r + 1) // world)
 
 
-def owner_weights(world, extended_k, k, owner_weight=0.5, scale=100):
+def auto_owner_weight(world, extended_k, k):
+    """the sub-coset owners' slab weight measured best on one GPU (tools/spmd_emulate.py,
+    C3 at k = 22, profiles/r03/s3/spmd_owner_weights): with twice as many ranks as
+    sub-coset owners 0.5 (N = 4: 0.5 / 0.65 / 0.8 -> slowest rank 27.8 / 29.6 / 30.0 ms),
+    with four times as many or more 0.2 (N = 8: 0.2 / 0.3 / 0.4 -> 18.2 / 19.5 / 20.4 ms)"""
+    E = 1 << (extended_k - k)
+    return 0.5 if world <= 2 * E else 0.2
+
+
+def owner_weights(world, extended_k, k, owner_weight=None, scale=100):
     """SPMD slab weights that lighten the ranks owning extended-domain sub-cosets: with
     2^(extended_k - k) = E < world sub-cosets, ranks r < E evaluate h on a sub-coset each
     (its n-point coset NTTs, evaluate_h, the h interpolation) on top of their MSM slabs;
-    they get weight owner_weight, the other ranks 1 (None when every rank owns one)"""
+    they get weight owner_weight (None: auto_owner_weight), the other ranks 1 (None when
+    every rank owns one)"""
     E = 1 << (extended_k - k)
     if world <= E:
         return None
+    if owner_weight is None:
+        owner_weight = auto_owner_weight(world, extended_k, k)
     return [int(round(scale * owner_weight)) if r < E else scale for r in range(world)]
 
 
