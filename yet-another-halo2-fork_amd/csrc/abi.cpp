@@ -224,7 +224,10 @@ int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFi
   if (nb < 1 || nb > MSM_MAX_BATCH) return fail(H2G_ERR_ARG, "msm: bad batch size");
   if (!d->h_ring) {
     HIPCHK(hipHostMalloc(&d->h_ring, MSM_RING * sizeof(G1xyzz), hipHostMallocDefault));
-    for (int i = 0; i < MSM_STREAMS; i++) HIPCHK(make_stream(&d->mstream[i], "H2G_CU_MASK_MSM"));
+    for (int i = 0; i < MSM_STREAMS; i++) {  // H2G_CU_MASK_MSM<i>: one stream's mask (else H2G_CU_MASK_MSM)
+      const std::string own = "H2G_CU_MASK_MSM" + std::to_string(i);
+      HIPCHK(make_stream(&d->mstream[i], std::getenv(own.c_str()) ? own.c_str() : "H2G_CU_MASK_MSM"));
+    }
     for (int i = 0; i < MSM_RING; i++) HIPCHK(hipEventCreateWithFlags(&d->ring_ev[i], hipEventDisableTiming));
     for (int i = 0; i < MSM_SLOTS; i++)
       for (hipEvent_t* e : {&d->mev_p2a[i], &d->mev_a2r[i], &d->mev_free[i]})
