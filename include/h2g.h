@@ -63,6 +63,15 @@ int h2g_msm_descriptor_free(uint64_t handle); /* Drop of a descriptor (zal.rs:47
 int h2g_msm_base_descriptor_dev(const void* d_bases, size_t n, int window_bits, uint64_t* handle);
 int h2g_msm_with_cached_base_dev(const void* d_scalars, size_t n, uint64_t base, size_t base_offset,
                                  uint64_t out_affine[8], int* out_is_identity, void* stream);
+/* The same MSM split across `world` GPUs by buckets (the final bucket-sum sharded, SURVEY
+ * 8e): every rank holds all n bases (a base descriptor) and scalars and computes the part
+ * of the sum its bucket range of the shared fixed-base bucket set carries -- entries
+ * balanced across ranks; the ranks' affine results add up to h2g_msm_with_cached_base_dev's
+ * (the host all-gathers them, RCCL has no elliptic-curve reduction).  world = 1: the
+ * whole MSM.  bucket_lo / bucket_hi (may be NULL) receive the rank's range. */
+int h2g_msm_with_cached_base_dev_shard(const void* d_scalars, size_t n, uint64_t base, size_t base_offset,
+                                       int world, int rank, uint64_t out_affine[8], int* out_is_identity,
+                                       uint32_t* bucket_lo, uint32_t* bucket_hi, void* stream);
 /* msm_with_cached_scalars / _base / _inputs (zal.rs:86-102); base_offset selects the
  * prefix/sub-slice &bases[off..off+n] used by commit / commit_lagrange
  * (halo2_backend/src/poly/kzg/commitment.rs:316, 365) */

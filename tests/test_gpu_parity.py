@@ -319,6 +319,68 @@ def test_msm_fixed_base_srs_identity_2_20():
     bases_dev.close()
 
 
+def _shard_sum(d_sc, n, h, world, off=0):
+    """sum over the ranks of h2g_msm_with_cached_base_dev_shard (what the host all-gather
+    adds up); the ranges must tile the bucket set"""
+    total = np.zeros(8, dtype=np.uint64)
+    prev_hi = 0
+    for r in range(world):
+        part, is_id, (lo, hi) = h2g.msm_with_cached_base_dev_shard(d_sc.ptr, n, h, world, r, off)
+        assert lo == prev_hi and hi >= lo, (world, r, lo, hi)
+        prev_hi = hi
+        assert is_id == (not part.any())
+        total = h2g.g1_add_affine(total, part)
+    return total, prev_hi
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("window_bits", [0, 9, 16])
+@pytest.mark.parametrize("dist", ["random", "ones", "sparse", "rminus1"])
+def test_msm_bucket_shards_sum_to_msm(world, window_bits, dist):
+    """h2g_msm_with_cached_base_dev_shard: the bucket ranges of `world` ranks tile the
+    shared fixed-base bucket set and their parts add up to the oracle's MSM (skewed
+    scalars included: ones put every digit in bucket 0 of one rank)."""
+    r = rng(world * 31 + window_bits + len(dist))
+    N = 5000
+    s = O.random_fr(r, 1)[0]
+    bases_dev = _srs(N, s)
+    bases = bases_dev.download((N, 8))
+    h = h2g.base_descriptor_dev(bases_dev.ptr, N, window_bits)
+    try:
+        for off, n in ((0, N), (1234, 3000)):
+            sc = _skewed(dist, r, n)
+            d_sc = h2g.DevBuf.from_array(sc)
+            got, top = _shard_sum(d_sc, n, h, world, off)
+            assert np.array_equal(got, O.msm_best(sc, bases[off:off + n], 8)), (world, window_bits, dist, off)
+            d_sc.close()
+    finally:
+        h2g.descriptor_free(h)
+        bases_dev.close()
+
+
+@pytest.mark.parametrize("k,worlds", [(22, (2, 4, 8)), (24, (2, 8))])
+def test_msm_bucket_shards_srs_identity(k, worlds):
+    """The bench's strong-scaled MSM at size: 2^22 (c = 20) and 2^24 (c = 22: the upper
+    ranks' ranges exceed 2^20 buckets, the 10-plane reduction) split over 2-8 bucket
+    ranges; sum of the parts == [c(s)]G."""
+    r = rng(400 + k)
+    n = 1 << k
+    s = O.random_fr(r, 1)[0]
+    bases_dev = _srs(n, s)
+    sc = O.random_fr(r, n)
+    want = O.g1_mul(GEN, O.eval_poly(sc, s))
+    d_sc = h2g.DevBuf.from_array(sc)
+    h = h2g.base_descriptor_dev(bases_dev.ptr, n, 0)
+    try:
+        for world in worlds:
+            got, _ = _shard_sum(d_sc, n, h, world)
+            assert np.array_equal(got, want), world
+    finally:
+        h2g.descriptor_free(h)
+        d_sc.close()
+        bases_dev.close()
+
+
 @pytest.mark.parametrize("k", [18, 20])
 def test_msm_equal_scalars_srs_identity(k):
     """One scalar value for every point (a constant column): each window's digits all

@@ -170,7 +170,7 @@ int msm_host_impl(Device* d, const void* sc, const void* bs, size_t n, int c, ui
 }
 
 int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, uint64_t* out,
-                        int* is_id, hipStream_t st) {
+                        int* is_id, hipStream_t st, const MsmBucketRange* br) {
   if (n == 0) {
     std::memset(out, 0, 64);
     if (is_id) *is_id = 1;
@@ -184,7 +184,7 @@ int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_
     g_msm_prof.push_back(ev);
     pe = &g_msm_prof.back();
   }
-  HIPCHK(msm_run_fixed(reinterpret_cast<const Fr*>(sc), fb, off, n, &d->msm, nullptr, st, pe));
+  HIPCHK(msm_run_fixed(reinterpret_cast<const Fr*>(sc), fb, off, n, &d->msm, nullptr, st, pe, nullptr, br));
   if (!d->h_windows) HIPCHK(hipHostMalloc(&d->h_windows, 256 * sizeof(G1xyzz), hipHostMallocDefault));
   HIPCHK(hipMemcpyAsync(d->h_windows, d->msm.windows, sizeof(G1xyzz), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -618,6 +618,30 @@ int h2g_msm_with_cached_base_dev(const void* d_scalars, size_t n, uint64_t base,
   if (off + n > it->second.n) return fail(H2G_ERR_ARG, "msm: bases.len() < size");
   if (n && !d_scalars) return fail(H2G_ERR_ARG, "msm: null scalars");
   return msm_desc_impl(d, d_scalars, it->second, off, n, out, is_id, pick_stream(d, stream));
+}
+
+int h2g_msm_with_cached_base_dev_shard(const void* d_scalars, size_t n, uint64_t base, size_t off, int world,
+                                       int rank, uint64_t out[8], int* is_id, uint32_t* bucket_lo, uint32_t* bucket_hi,
+                                       void* stream) {
+  NEED_DEV();
+  auto it = g_desc.find(base);
+  if (it == g_desc.end() || !it->second.is_base) return fail(H2G_ERR_HANDLE, "unknown base descriptor");
+  if (off + n > it->second.n) return fail(H2G_ERR_ARG, "msm: bases.len() < size");
+  if (n && !d_scalars) return fail(H2G_ERR_ARG, "msm: null scalars");
+  if (world < 1 || rank < 0 || rank >= world) return fail(H2G_ERR_ARG, "msm: bad world / rank");
+  const MsmFixedBase& fb = it->second.fb;
+  if (!fb.table) return fail(H2G_ERR_ARG, "msm: the base descriptor has no fixed-base windows");
+  MsmBucketRange br;
+  msm_bucket_range(fb, world, rank, &br);
+  if (bucket_lo) *bucket_lo = br.lo;
+  if (bucket_hi) *bucket_hi = br.hi;
+  if (world == 1) return msm_fixed_host_impl(d, d_scalars, fb, off, n, out, is_id, pick_stream(d, stream));
+  if (br.hi <= br.lo || n == 0) {  // an empty range: the identity
+    std::memset(out, 0, 64);
+    if (is_id) *is_id = 1;
+    return H2G_OK;
+  }
+  return msm_fixed_host_impl(d, d_scalars, fb, off, n, out, is_id, pick_stream(d, stream), &br);
 }
 
 int h2g_msm_descriptor_free(uint64_t handle) {

@@ -48,7 +48,21 @@ struct MsmPhaseEvents {
 static constexpr int MSM_MAX_BATCH = 64;
 struct MsmScalarList {
   const Fr* p[MSM_MAX_BATCH];
+  // fixed-base bucket range (msm_run_fixed's MsmBucketRange): only digits whose bucket lies in
+  // [klo, klo + kn) are kept, rebased to klo (kn = 0: every bucket)
+  uint32_t klo = 0, kn = 0;
 };
+
+// One rank's share of a fixed-base MSM split by buckets (the bucket-sum stage sharded
+// across GPUs): the digits falling in buckets [lo, hi) of the shared bucket set, whose
+// weighted sum, lo * (their plain sum) added, is that range's part of the MSM -- the
+// ranks' parts add up to the whole.  msm_bucket_range splits the buckets so that every
+// rank gets about the same number of entries (the balanced windows' narrower top digits
+// fill the upper buckets less).
+struct MsmBucketRange {
+  uint32_t lo = 0, hi = 0;
+};
+void msm_bucket_range(const struct MsmFixedBase& fb, int world, int rank, MsmBucketRange* r);
 
 // Stage streams of one pipelined MSM: the bucket partition runs on `part`, the
 // accumulation on `acc`, the fixup and the reduction on `red` (the events order them), so
@@ -84,7 +98,7 @@ void msm_fixed_base_free(MsmFixedBase* fb);
 // ss: stage streams (st is then unused; results are ordered on ss->red)
 hipError_t msm_run_fixed(const Fr* d_scalars, const MsmFixedBase& fb, size_t off, size_t n, MsmWorkspace* ws,
                          G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof = nullptr,
-                         const MsmStreams* ss = nullptr);
+                         const MsmStreams* ss = nullptr, const MsmBucketRange* br = nullptr);
 // nbatch MSMs sum_i list.p[b][i] * bases[off + i] (b < nbatch <= MSM_MAX_BATCH) as one
 // pipeline -- one digits launch, one sort, one accumulation, one reduction with a bucket
 // set per MSM -- so the latency-bound reduction is paid once.  Leaves MSM b's sum in

@@ -456,12 +456,13 @@ __device__ __forceinline__ G1xyzz pdbl(const G1xyzz& a) {
 
 // in LDS: T[0..len) holds one value per element, len = 2^K <= 512.  Afterwards T[0] is the
 // total and T[2^b] (b < K) the sum over the elements with bit b of their index set.
+// `workers`: the block's lanes (Q = 1) or quads (Q = 4); a level's items beyond them loop
 template <int Q>
-__device__ __forceinline__ void plane_fold(G1xyzz* T, int K, uint32_t e, bool lead) {
+__device__ __forceinline__ void plane_fold(G1xyzz* T, int K, uint32_t e, bool lead, uint32_t workers) {
   for (int k = 0; k < K; k++) {
     const uint32_t per = (uint32_t)k + 1, pairs = (1u << (K - 1 - k));
-    if (e < pairs * per) {
-      const uint32_t j = e / per, i = e % per;
+    for (uint32_t it = e; it < pairs * per; it += workers) {
+      const uint32_t j = it / per, i = it % per;
       const uint32_t dst = (j << (k + 1)) + (i == 0 ? 0u : (1u << (i - 1))), src = dst + (1u << k);
       const G1xyzz v = padd<Q>(T[dst], T[src]);
       if (lead) T[dst] = v;
@@ -529,10 +530,14 @@ msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, 
 // mid[q' * WB + w]: 0 = sum S, 1 + b = U_b (b < LB + K).  The last of a set's blocks to
 // finish (device-scope counter, zeroed by the host) then scales U_b by 2^(b + e0), one
 // quad per plane, and sums.
-static constexpr int RPK_MAX = 9;  // block-index planes
+// Bucket-range MSMs (MsmBucketRange): boff > 0 adds boff T, T = the plain sum of the
+// range's buckets (the block-index fold's total), each set bit b of boff one more plane
+// 2^b T in the last block's sum -- the weights of the range's buckets are boff + j + 1.
+static constexpr int RPK_MAX = 10;  // block-index planes (LDS: 2^RPK_MAX points)
+static constexpr int RPK_DEFAULT = 9;  // above it (c = 22 sets) whole MSMs keep the rscale scheme
 __global__ void __launch_bounds__(1024)
 msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, int e0, G1xyzz* __restrict__ mid,
-                      uint32_t* __restrict__ done, G1xyzz* __restrict__ windows) {
+                      uint32_t* __restrict__ done, G1xyzz* __restrict__ windows, uint32_t boff) {
   __shared__ G1xyzz sh[1 << RPK_MAX];
   __shared__ uint32_t last;
   const uint32_t q = blockIdx.x, w = blockIdx.y, e = threadIdx.x >> 2, WB = gridDim.y;
@@ -557,8 +562,9 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, 
     for (uint32_t i = e; i < (1u << K); i += 256)
       if (lead) sh[i] = i < nblk ? in[i] : G1xyzz::identity();
     __syncthreads();
-    plane_fold<4>(sh, K, e, lead);
+    plane_fold<4>(sh, K, e, lead, 256);
     if (lead && e < (uint32_t)K) mid[(size_t)(1 + LB + e) * WB + w] = sh[1u << e];
+    if (threadIdx.x == 0) mid[(size_t)(1 + LB + K) * WB + w] = sh[0];  // T
   }
   __syncthreads();  // this block's outputs are written
   if (threadIdx.x == 0) {
@@ -568,17 +574,20 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, 
   __syncthreads();
   if (!last) return;
   __threadfence();
-  const uint32_t np = (uint32_t)(LB + K);  // planes (<= 17)
+  const uint32_t np = (uint32_t)(LB + K);  // planes (<= 18)
   G1xyzz x = G1xyzz::identity();
   if (e < np) {
     x = mid[(size_t)(1 + e) * WB + w];
     for (int i = 0; i < (int)e + e0; i++) x = xyzz_dbl_q4(x);
   } else if (e == np) {
     x = mid[w];
+  } else if (e > np && e - np - 1 < 32 && ((boff >> (e - np - 1)) & 1u)) {  // 2^b T, bit b of boff
+    x = mid[(size_t)(1 + np) * WB + w];
+    for (uint32_t i = 0; i < e - np - 1; i++) x = xyzz_dbl_q4(x);
   }
-  if (lead && e < 32) sh[e] = x;
+  if (lead && e < 64) sh[e] = x;
   __syncthreads();
-  for (uint32_t h = 16; h > 0; h >>= 1) {
+  for (uint32_t h = 32; h > 0; h >>= 1) {
     if (e < h) {
       const G1xyzz v = xyzz_add_q4(sh[e], sh[e + h]);
       if (lead) sh[e] = v;
@@ -778,9 +787,12 @@ uint32_t msm_chunk_len(size_t total, size_t nbt) {
   return (uint32_t)L;
 }
 
+static double fb_entries_below(int W, uint64_t j);
+
 static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Affine* d_bases, size_t n, int c,
                                int W, int fixed, size_t stride, MsmWorkspace* ws, uint32_t item_len, G1Affine* d_out,
-                               hipStream_t st0, MsmPhaseEvents* prof, const MsmStreams* ss) {
+                               hipStream_t st0, MsmPhaseEvents* prof, const MsmStreams* ss,
+                               const MsmBucketRange* br = nullptr) {
   // stage streams: partition on ss->part, accumulation on ss->acc, fixup + reduction on
   // ss->red (one stream for all three without ss)
   hipStream_t st = ss ? ss->part : st0;
@@ -792,19 +804,26 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     H2G_TRY(hipStreamWaitEvent((next), (ev), 0));       \
     st = (next);                                        \
   }
-  const uint32_t NB = 1u << (c - 1);
+  const bool ranged = br && br->hi > br->lo;  // one rank's bucket range of a fixed-base MSM
+  if (ranged && (!fixed || nbatch != 1 || br->hi > (1u << (c - 1)))) return hipErrorInvalidValue;
+  const uint32_t NB = ranged ? br->hi - br->lo : 1u << (c - 1);
   if (nbatch < 1 || nbatch > MSM_MAX_BATCH || (!fixed && nbatch != 1)) return hipErrorInvalidValue;
   const int WB = fixed ? nbatch : W;  // bucket sets
   const uint32_t nbt = (uint32_t)WB * NB;
   const size_t total = n * (size_t)W * nbatch;
   if (total >= 0x80000000ull) return hipErrorInvalidValue;  // u32 positions in the sorted array
   // buckets most windows can reach (fixed-base: 2^(base width - 1) of the balanced widths)
-  const size_t nb_eff = (size_t)WB << ((fixed ? 255 / W : c) - 1);
+  const size_t nb_eff = ranged ? (size_t)NB : (size_t)WB << ((fixed ? 255 / W : c) - 1);
   static const uint32_t chunk_env = [] {  // H2G_MSM_CHUNK: fixed chunk length (A/B runs)
     const char* e = getenv("H2G_MSM_CHUNK");
     return e ? (uint32_t)atoi(e) : 0u;
   }();
-  const uint32_t L = item_len > 0 ? item_len : (chunk_env ? chunk_env : msm_chunk_len(total, nb_eff));
+  // a bucket range keeps its share of the entries: size the chunks for that, not for n W
+  const size_t total_eff =
+      ranged ? (size_t)((double)total * (fb_entries_below(W, br->hi) - fb_entries_below(W, br->lo)) /
+                        fb_entries_below(W, (uint64_t)1 << (c - 1))) + 1
+             : total;
+  const uint32_t L = item_len > 0 ? item_len : (chunk_env ? chunk_env : msm_chunk_len(total_eff, nb_eff));
   const size_t nchunks = (total + L - 1) / L;
   static const bool red_split = [] {
     const char* e = getenv("H2G_MSM_RED");
@@ -852,7 +871,8 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   const uint32_t nblk_p = (m1p + (1u << plane_lb) - 1) >> plane_lb;  // plane kernels' blocks
   // bit planes unless the block index needs more than RPK_MAX bits (sets of > 2^17
   // groups, e.g. c = 22): those keep the rscale scheme
-  const bool red_plane = !red_group && nblk_p <= (1u << RPK_MAX);
+  const bool red_plane = !red_group && nblk_p <= (1u << (ranged ? RPK_MAX : RPK_DEFAULT));
+  if (ranged && (!red_plane || red_split)) return hipErrorInvalidValue;  // the offset term is in the planes
   const WsPlan wp = ws_plan(NB);
   if (red_split && (wp.nv2v > 64 || wp.nu2v > 64 || wp.nv2u > 64 || wp.nu2u > 64)) return hipErrorInvalidValue;
   // grow-only workspace: MSMs of slightly different shapes (e.g. n and n - 1 points, so
@@ -949,6 +969,10 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   {  // rounds 1 and 2 (msm_part.hip); phase event 1 between them
     MsmPartArgs pa;
     pa.list = list;
+    if (ranged) {
+      pa.list.klo = br->lo;
+      pa.list.kn = NB;
+    }
     pa.nbatch = nbatch;
     pa.n = n;
     pa.c = c;
@@ -1021,7 +1045,8 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
       else
         hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
       hipLaunchKernelGGL(msm_rplane_mid_kernel, dim3((unsigned)plane_lb + 2, (unsigned)WB), dim3(1024), 0, st,
-                         (const G1xyzz*)planes, nblk_p, plane_lb, e0, mid, rdone, (G1xyzz*)ws->windows);
+                         (const G1xyzz*)planes, nblk_p, plane_lb, e0, mid, rdone, (G1xyzz*)ws->windows,
+                         ranged ? br->lo : 0u);
     } else {
       if (red_q4)
         hipLaunchKernelGGL(msm_rgroup_q4_kernel, dim3((unsigned)(((size_t)m1 * 4 + T - 1) / T), (unsigned)WB),
@@ -1116,11 +1141,41 @@ void msm_fixed_base_free(MsmFixedBase* fb) {
 }
 
 hipError_t msm_run_fixed(const Fr* d_scalars, const MsmFixedBase& fb, size_t off, size_t n, MsmWorkspace* ws,
-                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof, const MsmStreams* ss) {
+                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof, const MsmStreams* ss,
+                         const MsmBucketRange* br) {
   if (off + n > fb.n) return hipErrorInvalidValue;
   MsmScalarList list;
   list.p[0] = d_scalars;
-  return msm_pipeline(list, 1, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, d_out, st, prof, ss);
+  return msm_pipeline(list, 1, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, d_out, st, prof, ss, br);
+}
+
+// entries expected in buckets [0, j) of a fixed-base set: window w (balanced width cw) puts
+// its digits in buckets [0, 2^(cw - 1)), about uniformly
+static double fb_entries_below(int W, uint64_t j) {
+  double t = 0;
+  for (int w = 0; w < W; w++) {
+    const uint64_t cap = 1ull << (fb_width(W, w) - 1);
+    t += (double)(j < cap ? j : cap) / (double)cap;
+  }
+  return t;
+}
+
+void msm_bucket_range(const MsmFixedBase& fb, int world, int rank, MsmBucketRange* r) {
+  const uint64_t NB = 1ull << (fb.c - 1);
+  auto cut = [&](int q) -> uint32_t {  // the bucket where a q / world share of the entries ends
+    if (q <= 0) return 0;
+    if (q >= world) return (uint32_t)NB;
+    const double target = fb_entries_below(fb.W, NB) * q / world;
+    uint64_t lo = 0, hi = NB;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) / 2;
+      if (fb_entries_below(fb.W, mid) < target) lo = mid + 1;
+      else hi = mid;
+    }
+    return (uint32_t)lo;
+  };
+  r->lo = cut(rank);
+  r->hi = cut(rank + 1);
 }
 
 hipError_t msm_run_fixed_batch(const MsmScalarList& list, int nbatch, const MsmFixedBase& fb, size_t off, size_t n,

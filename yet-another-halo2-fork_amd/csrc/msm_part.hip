@@ -66,9 +66,14 @@ __device__ __forceinline__ void scalar_digits(const MsmScalarList& list, size_t 
       sign = 0;
     }
     if (w < w0 || mag == 0) continue;
+    uint32_t k = mag - 1;
+    if (list.kn) {  // bucket range: keep [klo, klo + kn), rebased
+      if (k - list.klo >= list.kn) continue;
+      k -= list.klo;
+    }
     const uint32_t koff = fixed ? bi * NB : (uint32_t)w * NB;
     const uint32_t val = (fixed ? (uint32_t)((size_t)w * stride + i) : (uint32_t)i) | sign;
-    fn(w - w0, koff + mag - 1, val);
+    fn(w - w0, koff + k, val);
   }
 }
 

@@ -147,7 +147,7 @@ int msm_dev_impl(Device* d, const void* sc, const void* bs, size_t n, int c, voi
 int msm_host_impl(Device* d, const void* sc, const void* bs, size_t n, int c, uint64_t* out, int* is_id,
                   hipStream_t st);
 int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, uint64_t* out,
-                        int* is_id, hipStream_t st);
+                        int* is_id, hipStream_t st, const MsmBucketRange* br = nullptr);
 // launch sum_{i<n} sc[i] * bases[off+i] after the work already queued on `producer`
 int msm_fixed_launch(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, hipStream_t producer,
                      MsmTicket* t);

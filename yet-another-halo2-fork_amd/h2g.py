@@ -39,6 +39,8 @@ _SIGS = {
     "h2g_msm_descriptor_free": ([U64], I32),
     "h2g_msm_base_descriptor_dev": ([VP, SZ, I32, ctypes.POINTER(U64)], I32),
     "h2g_msm_with_cached_base_dev": ([VP, SZ, U64, SZ, U64P, ctypes.POINTER(I32), VP], I32),
+    "h2g_msm_with_cached_base_dev_shard": ([VP, SZ, U64, SZ, I32, I32, U64P, ctypes.POINTER(I32),
+                                            ctypes.POINTER(U32), ctypes.POINTER(U32), VP], I32),
     "h2g_msm_with_cached_scalars": ([U64, U64P, SZ, U64P, ctypes.POINTER(I32)], I32),
     "h2g_msm_with_cached_base": ([U64P, SZ, U64, SZ, U64P, ctypes.POINTER(I32)], I32),
     "h2g_msm_with_cached_inputs": ([U64, U64, SZ, U64P, ctypes.POINTER(I32)], I32),
@@ -222,6 +224,18 @@ def msm_with_cached_base_dev(d_scalars, n, base_handle, offset=0, stream=None):
     check(lib().h2g_msm_with_cached_base_dev(VP(d_scalars), n, base_handle, offset, p64(out), ctypes.byref(is_id),
                                              VP(stream) if stream else None))
     return out
+
+
+def msm_with_cached_base_dev_shard(d_scalars, n, base_handle, world, rank, offset=0, stream=None):
+    """rank's bucket-range part of the MSM (the parts of ranks 0..world-1 add up to it)
+    -> (affine uint64[8], is_identity, (bucket_lo, bucket_hi))"""
+    out = np.zeros(8, dtype=np.uint64)
+    is_id = I32()
+    lo, hi = U32(), U32()
+    check(lib().h2g_msm_with_cached_base_dev_shard(VP(d_scalars), n, base_handle, offset, world, rank, p64(out),
+                                                   ctypes.byref(is_id), ctypes.byref(lo), ctypes.byref(hi),
+                                                   VP(stream) if stream else None))
+    return out, bool(is_id.value), (lo.value, hi.value)
 
 
 def descriptor_free(h):
