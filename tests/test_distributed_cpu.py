@@ -197,7 +197,7 @@ def test_weighted_slabs_partition_the_points():
             assert abs((sl[r][1] - sl[r][0]) - P * ws[r] / sum(ws)) <= 1
         # an MSM shorter than P: the same boundaries clipped to its length
         assert [D.slab(P - 1, world, r, P, w) for r in range(world)][-1][1] == P - 1
-    assert D.owner_weights(8, 23, 22) == [20, 20] + [100] * 6  # 4x the owners: measured best 0.2
+    assert D.owner_weights(8, 23, 22) == [10, 10] + [100] * 6  # 4x the owners: measured best 0.1
     assert D.owner_weights(4, 23, 22) == [50, 50, 100, 100]  # 2x the owners: 0.5
     assert D.owner_weights(8, 23, 22, 0.5) == [50, 50] + [100] * 6
     assert D.owner_weights(2, 23, 22) is None  # every rank owns a sub-coset

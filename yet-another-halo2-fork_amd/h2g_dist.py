@@ -35,10 +35,11 @@ def slab(n, world, r, P=None, weights=None):
 def auto_owner_weight(world, extended_k, k):
     """the sub-coset owners' slab weight measured best on one GPU (tools/spmd_emulate.py,
     C3 at k = 22, profiles/r03/s3/spmd_owner_weights): with twice as many ranks as
-    sub-coset owners 0.5 (N = 4: 0.5 / 0.65 / 0.8 -> slowest rank 27.8 / 29.6 / 30.0 ms),
-    with four times as many or more 0.2 (N = 8: 0.2 / 0.3 / 0.4 -> 18.2 / 19.5 / 20.4 ms)"""
+    sub-coset owners 0.5 (N = 4: 0.4 / 0.5 / 0.65 / 0.8 -> slowest rank 29.1 / 27.8 / 29.6
+    / 30.0 ms), with four times as many or more 0.1 (N = 8: 0.1 / 0.15 / 0.2 / 0.3 / 0.4 ->
+    17.5 / 17.9 / 18.2 / 19.5 / 20.4 ms)"""
     E = 1 << (extended_k - k)
-    return 0.5 if world <= 2 * E else 0.2
+    return 0.5 if world <= 2 * E else 0.1
 
 
 def owner_weights(world, extended_k, k, owner_weight=None, scale=100):
