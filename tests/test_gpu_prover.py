@@ -71,6 +71,13 @@ def test_proof_bytes_match_oracle(name):
     # another rng seed / vanishing split: still identical to the oracle
     want2 = O.create_proof(circ, wit, g, gl, seed=bytes(range(32)), vanishing_threads=3)
     assert pk.create_proof(wit, seed=bytes(range(32)), vanishing_threads=3) == want2
+    # the vanishing argument's random polynomial committed early from the keystream position
+    # the previous proof drew its seeds at (seeded RNG): again with that split, then with
+    # the first seed but a third split (position reused, seeds from this proof's keystream)
+    assert pk.create_proof(wit, seed=bytes(range(32)), vanishing_threads=3) == want2
+    want3 = O.create_proof(circ, wit, g, gl, vanishing_threads=3)
+    assert pk.create_proof(wit, vanishing_threads=3) == want3
+    assert pk.create_proof(wit) == want and pk.create_proof(wit) == want
     pk.close()
 
 

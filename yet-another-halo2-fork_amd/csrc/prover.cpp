@@ -220,6 +220,11 @@ struct ProvingKey {
   uint32_t* d_seeds = nullptr;
   uint64_t* d_offsets = nullptr;
   int max_chunks = 0;
+  // the keystream position of the vanishing argument's seed draws in the last proof with
+  // the seeded RNG (the draws before them depend on the circuit's shape only), and its
+  // thread count: the next proof generates and commits the random polynomial early
+  int64_t van_pos = -1;
+  uint32_t van_T = 0;
 };
 
 std::map<uint64_t, std::unique_ptr<Params>> g_params;
@@ -1517,6 +1522,49 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   std::vector<Fr> challenges(NCH);
   std::memset(challenges.data(), 0, challenges.size() * sizeof(Fr));
   StreamSyncGuard adv_guard{st};
+  // the vanishing argument's seeds and chunk offsets (staging read by async copies: lives
+  // until the proof returns), its commitment's ticket, and whether it was launched early
+  // H2G_EARLY_VANISHING (A/B): 0 = at its place in the transcript only, 1 = queued behind
+  // phase 0's advice MSMs (default), 2 = once the advice commitments are collected
+  static const int early_env = [] {
+    const char* e = std::getenv("H2G_EARLY_VANISHING");
+    return e ? std::atoi(e) : 1;
+  }();
+  std::vector<uint64_t> van_off;
+  std::vector<uint32_t> van_seeds;
+  StreamSyncGuard van_guard{st};  // destroyed before the staging above: the copies finish first
+  {
+    const uint64_t T = in.vthreads ? in.vthreads : 1;
+    const uint64_t chunk = n / T, rem = n % T;
+    for (uint64_t i = 0; i < rem && van_off.size() < T; i++) van_off.push_back(i * (chunk + 1));
+    if (chunk)
+      for (uint64_t o = rem * (chunk + 1); van_off.size() < T; o += chunk) van_off.push_back(o);
+  }
+  if ((int)van_off.size() > pk.max_chunks) {
+    PALLOC(pk.pool, pk.d_seeds, van_off.size() * 8);
+    PALLOC(pk.pool, pk.d_offsets, van_off.size());
+    pk.max_chunks = (int)van_off.size();
+  }
+  MsmTicket van_tk;
+  bool van_early = false;
+  const bool early_van = early_env != 0 && rng.seeded() && pk.van_pos >= 0 &&
+                         pk.van_T == (uint32_t)van_off.size() && g_spmd.world <= 1 && g_shard.world <= 1;
+  auto launch_van_early = [&]() -> int {
+    // the vanishing argument's random polynomial does not depend on the witness: with the
+    // seeded RNG its seeds are the keystream bytes at the position the last proof drew
+    // them from, so it is generated and its commitment MSM launched early -- queued behind
+    // phase 0's advice MSMs, it runs under the advice transforms and the lookup and
+    // permutation products instead of between the product commitments and y; the
+    // vanishing stage checks that the real draws equal these bytes (else it redoes both)
+    van_seeds.assign(van_off.size() * 8, 0);
+    rng.peek((uint64_t)pk.van_pos, reinterpret_cast<uint8_t*>(van_seeds.data()), van_seeds.size() * 4);
+    HIPCHK(hipMemcpyAsync(pk.d_seeds, van_seeds.data(), van_seeds.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(pk.d_offsets, van_off.data(), van_off.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)van_off.size(), st, sl.lo, sl.hi1));
+    RCCHK(commit_launch(d, prm, pk.random_poly, n, SRS_G, st, &van_tk));
+    van_early = true;
+    return H2G_OK;
+  };
   for (int ph = 0; ph <= pk.max_phase; ph++) {
     std::vector<int> cols;
     for (int c = 0; c < pk.A; c++)
@@ -1584,6 +1632,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       RCCHK(lagrange_to_coeff_batch(d, D, src.data(), dst.data(), (int)cols.size(), st));
       RCCHK(ext_cosets(d, pk, (const Fr* const*)dst.data(), cst.data(), (int)cols.size(), st));
     }
+    if (ph == 0 && early_van && early_env == 1) RCCHK(launch_van_early());
     if (ph == 0) clk.mark("upload+instances");
     for (auto& t : tk) {  // circuit by circuit, column by column
       G1Affine cm;
@@ -1598,6 +1647,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     HIPCHK(hipMemcpyAsync(pk.consts + pk.num_consts, challenges.data(), NCH * sizeof(Fr), hipMemcpyHostToDevice, st));
   g_last_challenges = challenges;
   clk.mark("advice commit");
+  if (early_van && early_env == 2) RCCHK(launch_van_early());
+
   const Fr theta = tr.squeeze();
   auto compress = [&](const CircuitWs& w, int2 seg, Fr* out) -> int {
     CompressArgs ca;
@@ -1955,31 +2006,31 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   }
   if (pk.NL + pk.NS) clk.mark("lookup/shuffle products");
   // ---- vanishing commit (vanishing/prover.rs:40-98)
-  MsmTicket van_tk;
-  std::vector<uint64_t> off;  // staging read by async copies (lives until the proof returns)
-  std::vector<uint32_t> seeds;
-  StreamSyncGuard seed_guard{st};
   {
-    const uint64_t T = in.vthreads ? in.vthreads : 1;
-    const uint64_t chunk = n / T, rem = n % T;
-    off.clear();
-    for (uint64_t i = 0; i < rem && off.size() < T; i++) off.push_back(i * (chunk + 1));
-    if (chunk)
-      for (uint64_t o = rem * (chunk + 1); off.size() < T; o += chunk) off.push_back(o);
-    seeds.assign(off.size() * 8, 0);
-    for (size_t i = 0; i < off.size(); i++) rng.fill(reinterpret_cast<uint8_t*>(&seeds[8 * i]), 32);
-    if ((int)off.size() > pk.max_chunks) {
-      PALLOC(pk.pool, pk.d_seeds, seeds.size());
-      PALLOC(pk.pool, pk.d_offsets, off.size());
-      pk.max_chunks = (int)off.size();
+    const uint64_t at = rng.position();
+    std::vector<uint32_t> drawn(van_off.size() * 8, 0);
+    for (size_t i = 0; i < van_off.size(); i++) rng.fill(reinterpret_cast<uint8_t*>(&drawn[8 * i]), 32);
+    if (van_early && (at != (uint64_t)pk.van_pos || drawn != van_seeds)) {
+      // the early draws were not the real ones: drop that commitment, redo it below
+      G1Affine unused;
+      RCCHK(commit_collect(d, &van_tk, &unused));
+      van_early = false;
     }
-    HIPCHK(hipMemcpyAsync(pk.d_seeds, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(pk.d_offsets, off.data(), off.size() * 8, hipMemcpyHostToDevice, st));
-    // a slab-mode rank draws only its coefficients (and the halo) of the random polynomial
-    HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)off.size(), st, sl.lo, sl.hi1));
-    (void)rng.random_fr();             // random_blind
+    if (rng.seeded()) {
+      pk.van_pos = (int64_t)at;
+      pk.van_T = (uint32_t)van_off.size();
+    }
+    if (!van_early) {
+      van_seeds = drawn;
+      HIPCHK(hipMemcpyAsync(pk.d_seeds, van_seeds.data(), van_seeds.size() * 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(pk.d_offsets, van_off.data(), van_off.size() * 8, hipMemcpyHostToDevice, st));
+      // a slab-mode rank draws only its coefficients (and the halo) of the random polynomial
+      HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)van_off.size(), st, sl.lo,
+                                sl.hi1));
+    }
+    (void)rng.random_fr();  // random_blind
     RCCHK(rng_ok());
-    RCCHK(commit_launch(d, prm, pk.random_poly, n, SRS_G, st, &van_tk));
+    if (!van_early) RCCHK(commit_launch(d, prm, pk.random_poly, n, SRS_G, st, &van_tk));
   }
   // the instance columns' cosets do not depend on y: they overlap the permutation /
   // vanishing MSMs (the advice went to coefficients and cosets under its own MSMs)

@@ -199,6 +199,18 @@ class ChaChaRng {
     fill(reinterpret_cast<uint8_t*>(w), 64);
     return fr_from_u512(w);
   }
+  // bytes of keystream consumed so far, and a jump to any such position
+  uint64_t position() const { return ctr_ * 64 - (64 - (uint64_t)pos_); }
+  void seek(uint64_t at) {
+    ctr_ = at / 64;
+    pos_ = 64;
+    if (at % 64) {
+      uint32_t w[16];
+      chacha20_block(key_, ctr_++, w);
+      std::memcpy(block_, w, 64);
+      pos_ = (size_t)(at % 64);
+    }
+  }
 
  private:
   uint32_t key_[8];
@@ -250,6 +262,15 @@ class ProverRng {
     return fr_from_u512(w);
   }
   bool failed() const { return failed_; }
+  // ChaCha20Rng::from_seed only (no caller callbacks): the keystream position, and the
+  // bytes a later draw at position `at` will return, without consuming them
+  bool seeded() const { return !fb_ && !fr_; }
+  uint64_t position() const { return cc_.position(); }
+  void peek(uint64_t at, uint8_t* out, size_t len) const {
+    ChaChaRng c = cc_;
+    c.seek(at);
+    c.fill(out, len);
+  }
   // digest of every draw so far (SPMD ranks must draw the same values)
   void draws_digest(uint8_t out[64]) const { draws_.digest(out); }
 
