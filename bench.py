@@ -607,8 +607,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             line["transport_note"] = transport_note
     if args.workload == "prove" and (world == 1 or dist.get_backend() == "nccl"):
         # every rank takes part when sharded (collectives inside)
-        m = measure_msm(h2g, torch, dev, 24, steps=10, warmup=2, dist=dist, world=world, rank=rank,
-                        split=args.msm_split)
+        m = measure_msm(h2g, torch, dev, 24, steps=10, warmup=2, dist=dist, world=world, rank=rank)
         if line is not None:
             line["msm_2p24"] = m
     if native:
@@ -681,22 +680,17 @@ def verify_proof(h2g, circ, pk, params, proof):
     return bool(V.verify(circ, [], proof, None, vk=vk, g2=(V.g2_from_limbs(g2), V.g2_from_limbs(s_g2))))
 
 
-def measure_msm(h2g, torch, dev, log_n, steps, warmup, dist=None, world=1, rank=0, split="points"):
+def measure_msm(h2g, torch, dev, log_n, steps, warmup, dist=None, world=1, rank=0):
     """the metric's MSM half: one MSM of 2^log_n resident (scalar, SRS point) pairs through
     the base-descriptor path (fixed-base windows), HIP-event timed on the MSM stream.
-    world > 1: the same MSM strong-scaled over the ranks, each step ending with the RCCL
-    all_gather of the 64-B partials and their host sum; the time is the slowest rank's.
-    split "points" (default): rank r holds point slab [n r / world, n (r + 1) / world) and
-    its scalars and runs a whole MSM on it; "buckets": every rank holds all points and
-    scalars and computes its entry-balanced bucket range of the shared bucket set
-    (h2g_msm_with_cached_base_dev_shard) -- measured slower at 4 and 8 GPUs (every rank
-    extracts the digits of all n scalars); rank 0 then checks the gathered sum
-    against its own whole MSM of the same inputs, outside the timed region."""
+    world > 1: the same MSM strong-scaled over the ranks -- rank r holds point slab
+    [n r / world, n (r + 1) / world) and its scalars and runs a whole MSM on it, each step
+    ending with the all_gather of the 64-B partials and their host sum; the time is the
+    slowest rank's."""
     stream = torch.cuda.current_stream().cuda_stream
     n = 1 << log_n
-    buckets = world > 1 and split == "buckets"
-    n_loc = n if buckets or world == 1 else n // world
-    rng = np.random.default_rng(1000 if buckets else 1000 + rank)  # bucket split: the same inputs on every rank
+    n_loc = n if world == 1 else n // world
+    rng = np.random.default_rng(1000 + rank)
     bases = torch.empty((n_loc, 8), dtype=torch.int64, device=dev)
     h2g.srs_setup_dev(random_scalars(rng, 1)[0], n_loc, bases.data_ptr(), stream)
     scalars = torch.from_numpy(random_scalars(rng, n_loc).view(np.int64)).to(dev)
@@ -705,11 +699,7 @@ def measure_msm(h2g, torch, dev, log_n, steps, warmup, dist=None, world=1, rank=
     out = {}
 
     def step():
-        if buckets:
-            out["p"], _, out["range"] = h2g.msm_with_cached_base_dev_shard(scalars.data_ptr(), n, base, world, rank,
-                                                                           0, stream)
-        else:
-            out["p"] = h2g.msm_with_cached_base_dev(scalars.data_ptr(), n_loc, base, 0, stream)
+        out["p"] = h2g.msm_with_cached_base_dev(scalars.data_ptr(), n_loc, base, 0, stream)
         if world > 1:
             out["total"] = combine_partials(gather_partials(out["p"], dist, world, dev), h2g.g1_add_affine)
 
@@ -730,25 +720,15 @@ def measure_msm(h2g, torch, dev, log_n, steps, warmup, dist=None, world=1, rank=
     h2g.profile_enable(False)
     calls, phases = h2g.profile_msm_collect()
     el = max_over_ranks(el, dist, world, dev)
-    sum_ok = None
-    if buckets and rank == 0:  # the gathered parts == the whole MSM on one GPU
-        sum_ok = bool(np.array_equal(out["total"], h2g.msm_with_cached_base_dev(scalars.data_ptr(), n, base, 0,
-                                                                                stream)))
     h2g.descriptor_free(base)
     del bases, scalars
     torch.cuda.empty_cache()
-    res = {"value": round(n * steps / el / 1e6, 2), "unit": "Mscalar-mul/s", "points": n, "steps": steps,
-           "ms_per_msm": round(el / steps * 1e3, 3), "window_bits": fixed_c(n if buckets else n_loc),
-           "n_gpus": world, "points_per_gpu": n_loc,
-           "scaling": ("strong (one 2^%d MSM, the shared bucket set split into %d entry-balanced ranges, RCCL "
-                       "all_gather of the partials)" % (log_n, world) if buckets else
-                       "strong (one 2^%d MSM split into %d point slabs, RCCL all_gather of partials)" % (log_n, world))
-                      if world > 1 else "single GPU",
-           "phases_ms": {kk: round(v / max(calls, 1), 4) for kk, v in phases.items()}}
-    if buckets:
-        res["bucket_range_rank0"] = list(out["range"])
-        res["parts_sum_equals_whole_msm"] = sum_ok
-    return res
+    return {"value": round(n * steps / el / 1e6, 2), "unit": "Mscalar-mul/s", "points": n, "steps": steps,
+            "ms_per_msm": round(el / steps * 1e3, 3), "window_bits": fixed_c(n_loc),
+            "n_gpus": world, "points_per_gpu": n_loc,
+            "scaling": ("strong (one 2^%d MSM split into %d point slabs, all_gather of partials)" % (log_n, world))
+                       if world > 1 else "single GPU",
+            "phases_ms": {kk: round(v / max(calls, 1), 4) for kk, v in phases.items()}}
 
 
 def run_msm(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
@@ -844,8 +824,6 @@ def main():
     ap.add_argument("--spmd-owner-weight", type=float, default=-1,
                     help="spmd: slab weight of the sub-coset owners against 1 for the other ranks "
                          "(0: uniform, -1: measured default for the ratio of ranks to owners)")
-    ap.add_argument("--msm-split", choices=("points", "buckets"), default="points",
-                    help="N > 1: how the line's strong-scaled 2^24 MSM divides (point slabs, or bucket ranges)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3, help="CPU baseline runs (median)")
     ap.add_argument("--no-krange", action="store_true",

@@ -63,15 +63,6 @@ int h2g_msm_descriptor_free(uint64_t handle); /* Drop of a descriptor (zal.rs:47
 int h2g_msm_base_descriptor_dev(const void* d_bases, size_t n, int window_bits, uint64_t* handle);
 int h2g_msm_with_cached_base_dev(const void* d_scalars, size_t n, uint64_t base, size_t base_offset,
                                  uint64_t out_affine[8], int* out_is_identity, void* stream);
-/* The same MSM split across `world` GPUs by buckets (the final bucket-sum sharded, SURVEY
- * 8e): every rank holds all n bases (a base descriptor) and scalars and computes the part
- * of the sum its bucket range of the shared fixed-base bucket set carries -- entries
- * balanced across ranks; the ranks' affine results add up to h2g_msm_with_cached_base_dev's
- * (the host all-gathers them, RCCL has no elliptic-curve reduction).  world = 1: the
- * whole MSM.  bucket_lo / bucket_hi (may be NULL) receive the rank's range. */
-int h2g_msm_with_cached_base_dev_shard(const void* d_scalars, size_t n, uint64_t base, size_t base_offset,
-                                       int world, int rank, uint64_t out_affine[8], int* out_is_identity,
-                                       uint32_t* bucket_lo, uint32_t* bucket_hi, void* stream);
 /* msm_with_cached_scalars / _base / _inputs (zal.rs:86-102); base_offset selects the
  * prefix/sub-slice &bases[off..off+n] used by commit / commit_lagrange
  * (halo2_backend/src/poly/kzg/commitment.rs:316, 365) */
@@ -134,6 +125,9 @@ int h2g_fr_batch_invert_dev(void* d_a, size_t n, void* stream);
 /* out_i = prod_{j<=i} a_j; grand products permutation/prover.rs:160-166 */
 int h2g_fr_prefix_product(const uint64_t* a, uint64_t* out, size_t n);
 int h2g_fr_prefix_product_dev(const void* d_a, void* d_out, size_t n, void* stream);
+/* exclusive prefix sum of n u32 (n < 2^32; d_in == d_out allowed): the counts-to-offsets scan
+ * of the lookup argument's sorts and compactions (lookup/prover.rs:410-494) */
+int h2g_u32_exclusive_scan_dev(const void* d_in, void* d_out, size_t n, void* stream);
 
 /* ---- device memory / stream helpers --------------------------------------- */
 int h2g_dev_alloc(size_t bytes, void** d_ptr);
@@ -398,13 +392,14 @@ int h2g_comm_destroy(void);
  * proof bytes as one GPU would and no scalars cross the links.
  *   allgather: in = this rank's H2G_SPMD_WORDS words: its partial (8 u64 affine limbs,
  *              then 1 if the identity) and 4 words of consistency digest (a Blake2b of
- *              the transcript state and of every RNG draw so far); out = world x
- *              H2G_SPMD_WORDS u64 in rank order; 0 on success.  Every rank compares the
- *              digests and fails the proof (H2G_ERR_STATE) if any rank's differ: ranks
- *              fed different witnesses, instances or RNG draws would otherwise sum slabs
- *              of different polynomials into one invalid proof without an error (a
- *              diverged witness shows up at the latest when the evaluations enter the
- *              transcript, before the multi-open commitments are gathered). */
+ *              the transcript state, of every RNG draw so far and of the advice columns'
+ *              values at a fixed point, each rank evaluating its whole copy of every
+ *              column once per advice phase); out = world x H2G_SPMD_WORDS u64 in rank
+ *              order; 0 on success.  Every rank compares the digests and fails the proof
+ *              (H2G_ERR_STATE) if any rank's differ: ranks fed different witnesses,
+ *              instances or RNG draws would otherwise sum slabs of different polynomials
+ *              into one invalid proof without an error (the commitments and evaluations
+ *              are sums of the ranks' slabs, so they alone cannot reveal it). */
 #define H2G_SPMD_WORDS 13
 /*
  * The host transport (callbacks) or the library's RCCL all-gather (h2g_comm_spmd_install,

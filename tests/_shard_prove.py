@@ -7,6 +7,7 @@ partials all-gathered).  Launched by tests/test_gpu_sharded.py:
 With --backend gloo every rank may share one GPU (host-staged slabs); with nccl each
 rank needs its own GPU (RCCL)."""
 import argparse
+import copy
 import json
 import os
 import sys
@@ -68,6 +69,9 @@ def main():
     ap.add_argument("--weights", default="", help="spmd: slab weights (h2g.spmd_set_weights), comma separated")
     ap.add_argument("--diverge", action="store_true",
                     help="spmd: the last rank proves with another RNG seed; every rank must refuse the proof")
+    ap.add_argument("--diverge-witness", action="store_true",
+                    help="spmd: the last rank proves another witness (one advice value changed); every rank "
+                         "must refuse the proof")
     ap.add_argument("--one-variant", action="store_true",
                     help="prove each case once (default seed) instead of twice (large cases)")
     ap.add_argument("cases", nargs="+")
@@ -168,10 +172,18 @@ def spmd_main(args, rank, world, native):
             g = D.SpmdGather(dist, subcosets=not args.no_subcosets, slabs=not args.no_slabs,
                              h_exchange=not args.bcast_h)
             g.install()
-        if args.diverge:  # the last rank draws other randomness: the digest check must catch it
+        if args.diverge or args.diverge_witness:  # the digest check must catch a diverged rank
             try:
-                seed = bytes([9] * 32) if rank == world - 1 else bytes([7] * 32)
-                _prove(pk, case, seed=seed)
+                if args.diverge:  # the last rank draws other randomness
+                    seed = bytes([9] * 32) if rank == world - 1 else bytes([7] * 32)
+                    _prove(pk, case, seed=seed)
+                else:  # the last rank holds another witness: advice column 0, row 3 changed
+                    c2 = list(case)
+                    if rank == world - 1:
+                        w = copy.deepcopy(case[1])
+                        w.advice[0, 3, 0] ^= np.uint64(1)
+                        c2[1] = w
+                    _prove(pk, tuple(c2))
                 err = ""
             except h2g.H2GError as e:
                 err = str(e)

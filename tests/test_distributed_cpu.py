@@ -233,3 +233,47 @@ def test_spmd_host_allgather_gloo():
     for rank, parts, calls in out:
         assert parts == [bytes([r]) * 5 for r in range(world)], rank
         assert calls == 1
+
+
+def _a2a_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch
+        import h2g_dist as D
+        members = [1, 2, 3]  # a sub-group: group index != global rank
+        grp = dist.new_group(members)
+        if rank in members:
+            me = members.index(rank)
+            W = len(members)
+            send_bytes = [me + p + 1 for p in range(W)]  # to member p: me + p + 1 bytes of value 10 me + p
+            recv_bytes = [p + me + 1 for p in range(W)]
+            sb = torch.cat([torch.full((send_bytes[p],), 10 * me + p, dtype=torch.uint8) for p in range(W)])
+            rb = torch.zeros(sum(recv_bytes), dtype=torch.uint8)
+            D.host_all_to_all(dist, grp, me, W, sb, send_bytes, rb, recv_bytes)
+            q.put((rank, rb.tolist()))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_spmd_host_all_to_all_subgroup_gloo():
+    """SpmdGather.exchange's host (gloo) path on a process group that is not the default
+    one: the peers are addressed by their global ranks, the byte offsets by group index"""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_a2a_worker, args=(i, world, port, q)) for i in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=180) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, got in out.items():
+        me = [1, 2, 3].index(rank)
+        want = []
+        for p in range(3):
+            want += [10 * p + me] * (p + me + 1)
+        assert got == want, (rank, got)

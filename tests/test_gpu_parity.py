@@ -319,28 +319,13 @@ def test_msm_fixed_base_srs_identity_2_20():
     bases_dev.close()
 
 
-def _shard_sum(d_sc, n, h, world, off=0):
-    """sum over the ranks of h2g_msm_with_cached_base_dev_shard (what the host all-gather
-    adds up); the ranges must tile the bucket set"""
-    total = np.zeros(8, dtype=np.uint64)
-    prev_hi = 0
-    for r in range(world):
-        part, is_id, (lo, hi) = h2g.msm_with_cached_base_dev_shard(d_sc.ptr, n, h, world, r, off)
-        assert lo == prev_hi and hi >= lo, (world, r, lo, hi)
-        prev_hi = hi
-        assert is_id == (not part.any())
-        total = h2g.g1_add_affine(total, part)
-    return total, prev_hi
-
-
-@pytest.mark.parametrize("world", [1, 2, 3, 8])
 @pytest.mark.parametrize("window_bits", [0, 9, 16])
 @pytest.mark.parametrize("dist", ["random", "ones", "sparse", "rminus1"])
-def test_msm_bucket_shards_sum_to_msm(world, window_bits, dist):
-    """h2g_msm_with_cached_base_dev_shard: the bucket ranges of `world` ranks tile the
-    shared fixed-base bucket set and their parts add up to the oracle's MSM (skewed
-    scalars included: ones put every digit in bucket 0 of one rank)."""
-    r = rng(world * 31 + window_bits + len(dist))
+def test_msm_fixed_base_windows_and_skew(window_bits, dist):
+    """Fixed-base MSMs over a sub-slice of the bases at several window sizes and skewed
+    scalar distributions (ones put every digit in bucket 0: one coarse bin holds all
+    entries) == the oracle's best_multiexp."""
+    r = rng(31 + window_bits + len(dist))
     N = 5000
     s = O.random_fr(r, 1)[0]
     bases_dev = _srs(N, s)
@@ -350,19 +335,18 @@ def test_msm_bucket_shards_sum_to_msm(world, window_bits, dist):
         for off, n in ((0, N), (1234, 3000)):
             sc = _skewed(dist, r, n)
             d_sc = h2g.DevBuf.from_array(sc)
-            got, top = _shard_sum(d_sc, n, h, world, off)
-            assert np.array_equal(got, O.msm_best(sc, bases[off:off + n], 8)), (world, window_bits, dist, off)
+            got = h2g.msm_with_cached_base_dev(d_sc.ptr, n, h, off)
+            assert np.array_equal(got, O.msm_best(sc, bases[off:off + n], 8)), (window_bits, dist, off)
             d_sc.close()
     finally:
         h2g.descriptor_free(h)
         bases_dev.close()
 
 
-@pytest.mark.parametrize("k,worlds", [(22, (2, 4, 8)), (24, (2, 8))])
-def test_msm_bucket_shards_srs_identity(k, worlds):
-    """The bench's strong-scaled MSM at size: 2^22 (c = 20) and 2^24 (c = 22: the upper
-    ranks' ranges exceed 2^20 buckets, the 10-plane reduction) split over 2-8 bucket
-    ranges; sum of the parts == [c(s)]G."""
+@pytest.mark.parametrize("k", [22, 24])
+def test_msm_fixed_base_srs_identity_at_size(k):
+    """The bench's MSMs at size: 2^22 (c = 20, bit-plane reduction) and 2^24 (c = 22, the
+    rscale reduction); sum c_i [s^i]G == [c(s)]G."""
     r = rng(400 + k)
     n = 1 << k
     s = O.random_fr(r, 1)[0]
@@ -372,9 +356,7 @@ def test_msm_bucket_shards_srs_identity(k, worlds):
     d_sc = h2g.DevBuf.from_array(sc)
     h = h2g.base_descriptor_dev(bases_dev.ptr, n, 0)
     try:
-        for world in worlds:
-            got, _ = _shard_sum(d_sc, n, h, world)
-            assert np.array_equal(got, want), world
+        assert np.array_equal(h2g.msm_with_cached_base_dev(d_sc.ptr, n, h, 0), want)
     finally:
         h2g.descriptor_free(h)
         d_sc.close()
@@ -452,3 +434,26 @@ def test_msm_profile_counts_sorted_entries():
     finally:
         h2g.descriptor_free(h)
         bases_dev.close()
+
+
+# ---------------------------------------------------------------- counts -> offsets scan
+@pytest.mark.parametrize("n", [1, 4096, 4097, (1 << 24) + 12345, (1 << 25) + 7])
+def test_u32_exclusive_scan_any_length(n):
+    """h2g_u32_exclusive_scan_dev (the lookup sort's and compactions' scan): exact against
+    numpy at lengths around the 4096-element block and past 2^24, where the block sums
+    no longer fit one block and are scanned recursively (in place, as the sort uses it)."""
+    r = rng(n % 1000)
+    a = r.integers(0, 300, size=n, dtype=np.uint32)
+    want = np.zeros(n, dtype=np.uint64)
+    want[1:] = np.cumsum(a[:-1], dtype=np.uint64)
+    want = (want & 0xffffffff).astype(np.uint32)
+    d_in = h2g.DevBuf.from_array(a)
+    d_out = h2g.DevBuf(a.nbytes)
+    try:
+        h2g.u32_exclusive_scan_dev(d_in.ptr, d_out.ptr, n)
+        assert np.array_equal(d_out.download(n, np.uint32), want)
+        h2g.u32_exclusive_scan_dev(d_in.ptr, d_in.ptr, n)  # in place
+        assert np.array_equal(d_in.download(n, np.uint32), want)
+    finally:
+        d_in.close()
+        d_out.close()

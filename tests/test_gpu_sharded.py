@@ -109,6 +109,16 @@ def test_spmd_diverged_ranks_refuse_the_proof():
         assert res[nm]["refused_all"], (nm, res[nm])
 
 
+def test_spmd_diverged_witness_refuses_the_proof():
+    """a rank fed another witness (same RNG, same instances): with the commitments and
+    evaluations summed from slabs its transcript matches the others', so only the witness
+    digest (every advice column at a fixed point, folded into the all-gather payload)
+    makes every rank fail the proof"""
+    res = _run(2, ["c3_k14", "lookup_k11"], mode="spmd", extra=["--diverge-witness"])
+    for nm in ("c3_k14", "lookup_k11"):
+        assert res[nm]["refused_all"], (nm, res[nm])
+
+
 @pytest.mark.timeout(1200)
 @pytest.mark.parametrize("world", [2, 4])
 def test_spmd_c3_k22_at_size(world):

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/h2g.h"
+#include "radix.h"
 #include "runtime.h"
 #include "bn254.h"
 #include "msm.h"
@@ -170,7 +171,7 @@ int msm_host_impl(Device* d, const void* sc, const void* bs, size_t n, int c, ui
 }
 
 int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, uint64_t* out,
-                        int* is_id, hipStream_t st, const MsmBucketRange* br) {
+                        int* is_id, hipStream_t st) {
   if (n == 0) {
     std::memset(out, 0, 64);
     if (is_id) *is_id = 1;
@@ -184,7 +185,7 @@ int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_
     g_msm_prof.push_back(ev);
     pe = &g_msm_prof.back();
   }
-  HIPCHK(msm_run_fixed(reinterpret_cast<const Fr*>(sc), fb, off, n, &d->msm, nullptr, st, pe, nullptr, br));
+  HIPCHK(msm_run_fixed(reinterpret_cast<const Fr*>(sc), fb, off, n, &d->msm, nullptr, st, pe));
   if (!d->h_windows) HIPCHK(hipHostMalloc(&d->h_windows, 256 * sizeof(G1xyzz), hipHostMallocDefault));
   HIPCHK(hipMemcpyAsync(d->h_windows, d->msm.windows, sizeof(G1xyzz), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -198,25 +199,6 @@ int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_
   return H2G_OK;
 }
 
-// Optional CU masks (diagnostics / A/B): H2G_CU_MASK_MAIN / H2G_CU_MASK_MSM = 8 hex words
-// (CU 0 = bit 0 of the first), restricting the prover's main stream (NTTs, evaluate_h,
-// grand products) or the MSM streams to a subset of the 256 CUs.
-static hipError_t make_stream(hipStream_t* s, const char* env) {
-  const char* e = std::getenv(env);
-  if (!e || !*e) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-  std::vector<uint32_t> mask;
-  std::string str(e);
-  size_t pos = 0;
-  while (pos < str.size() && mask.size() < 8) {
-    size_t nxt = str.find(',', pos);
-    if (nxt == std::string::npos) nxt = str.size();
-    mask.push_back((uint32_t)std::strtoul(str.substr(pos, nxt - pos).c_str(), nullptr, 16));
-    pos = nxt + 1;
-  }
-  while (mask.size() < 8) mask.push_back(mask.empty() ? 0xffffffffu : mask.back());
-  return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
-}
-
 // nb MSMs of n scalars each against the same fixed-base windows, launched as one batched
 // pipeline (msm_run_fixed_batch) on the next MSM stream; ticket b collects MSM b.
 int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFixedBase& fb, size_t off, size_t n,
@@ -224,24 +206,9 @@ int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFi
   if (nb < 1 || nb > MSM_MAX_BATCH) return fail(H2G_ERR_ARG, "msm: bad batch size");
   if (!d->h_ring) {
     HIPCHK(hipHostMalloc(&d->h_ring, MSM_RING * sizeof(G1xyzz), hipHostMallocDefault));
-    for (int i = 0; i < MSM_STREAMS; i++) {  // H2G_CU_MASK_MSM<i>: one stream's mask (else H2G_CU_MASK_MSM)
-      const std::string own = "H2G_CU_MASK_MSM" + std::to_string(i);
-      HIPCHK(make_stream(&d->mstream[i], std::getenv(own.c_str()) ? own.c_str() : "H2G_CU_MASK_MSM"));
-    }
+    for (int i = 0; i < MSM_STREAMS; i++) HIPCHK(hipStreamCreateWithFlags(&d->mstream[i], hipStreamNonBlocking));
     for (int i = 0; i < MSM_RING; i++) HIPCHK(hipEventCreateWithFlags(&d->ring_ev[i], hipEventDisableTiming));
-    for (int i = 0; i < MSM_SLOTS; i++)
-      for (hipEvent_t* e : {&d->mev_p2a[i], &d->mev_a2r[i], &d->mev_free[i]})
-        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
-  // H2G_MSM_PIPE=1: the stage pipeline (runtime.h).  Off by default: measured slower --
-  // a partition or reduction launched beside an accumulation gets CUs only as its blocks
-  // retire, so the gaps between accumulations stayed 1-6 ms and the serialised
-  // accumulations lost the second stream's overlap (C3 k = 22: 89.5-91.1 vs 87.9-89.0 ms,
-  // profiles/r03/s3/ab_msm_pipe)
-  static const bool pipe = [] {
-    const char* e = std::getenv("H2G_MSM_PIPE");
-    return e ? std::atoi(e) != 0 : false;
-  }();
   int rings[MSM_MAX_BATCH];
   int got = 0;
   for (int k = 0; k < MSM_RING && got < nb; k++) {
@@ -250,18 +217,12 @@ int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFi
   }
   if (got < nb) return fail(H2G_ERR_STATE, "msm: too many outstanding asynchronous MSMs");
   d->next_ring = (rings[nb - 1] + 1) % MSM_RING;
-  const int nslots = pipe ? MSM_SLOTS : 2;
-  const int slot = d->next_slot % nslots;
-  d->next_slot = (slot + 1) % nslots;
-  // ms: where the MSM starts (its partition) -- rs: where it ends (reduction, result copy)
-  hipStream_t ms = pipe ? d->mstream[0] : d->mstream[slot];
-  hipStream_t rs = pipe ? d->mstream[2] : ms;
-  const MsmStreams ss{d->mstream[0], d->mstream[1], d->mstream[2], d->mev_p2a[slot], d->mev_a2r[slot]};
-  // order after the producer's work (the scalars) and, pipelined, after the reduction of
-  // the workspace's previous MSM
+  const int slot = d->next_slot;
+  d->next_slot = (slot + 1) % MSM_STREAMS;
+  hipStream_t ms = d->mstream[slot];
+  // order after the producer's work (the scalars)
   HIPCHK(hipEventRecord(d->ring_ev[rings[0]], producer));
   HIPCHK(hipStreamWaitEvent(ms, d->ring_ev[rings[0]], 0));
-  if (pipe && d->mws_used[slot]) HIPCHK(hipStreamWaitEvent(ms, d->mev_free[slot], 0));
   MsmPhaseEvents* pe = nullptr;
   if (g_profile && n > 0) {
     MsmPhaseEvents ev;
@@ -277,19 +238,14 @@ int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFi
   } else {
     MsmScalarList list;
     for (int b = 0; b < nb; b++) list.p[b] = reinterpret_cast<const Fr*>(sc[b]);
-    const MsmStreams* pss = pipe ? &ss : nullptr;
-    if (nb == 1) HIPCHK(msm_run_fixed(list.p[0], fb, off, n, &d->mws[slot], nullptr, ms, pe, pss));
-    else HIPCHK(msm_run_fixed_batch(list, nb, fb, off, n, &d->mws[slot], ms, pe, pss));
+    if (nb == 1) HIPCHK(msm_run_fixed(list.p[0], fb, off, n, &d->mws[slot], nullptr, ms, pe));
+    else HIPCHK(msm_run_fixed_batch(list, nb, fb, off, n, &d->mws[slot], ms, pe));
     const G1xyzz* win = reinterpret_cast<const G1xyzz*>(d->mws[slot].windows);
     for (int b = 0; b < nb; b++)
-      HIPCHK(hipMemcpyAsync(host + rings[b], win + b, sizeof(G1xyzz), hipMemcpyDeviceToHost, rs));
-  }
-  if (pipe) {
-    HIPCHK(hipEventRecord(d->mev_free[slot], rs));
-    d->mws_used[slot] = true;
+      HIPCHK(hipMemcpyAsync(host + rings[b], win + b, sizeof(G1xyzz), hipMemcpyDeviceToHost, ms));
   }
   for (int b = 0; b < nb; b++) {
-    HIPCHK(hipEventRecord(d->ring_ev[rings[b]], rs));
+    HIPCHK(hipEventRecord(d->ring_ev[rings[b]], ms));
     d->ring_busy[rings[b]] = true;
     t[b].slot = slot;
     t[b].ring = rings[b];
@@ -492,7 +448,7 @@ int h2g_init(const int* devices, int ndev) {
     auto dev = std::make_unique<Device>();
     dev->id = id;
     HIPCHK(hipSetDevice(id));
-    HIPCHK(make_stream(&dev->stream, "H2G_CU_MASK_MAIN"));
+    HIPCHK(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
     HIPCHK(ntt_init_attributes());
     g_devs.push_back(std::move(dev));
   }
@@ -519,11 +475,7 @@ int h2g_shutdown(void) {
         (void)hipStreamSynchronize(dev->mstream[i]);
         (void)hipStreamDestroy(dev->mstream[i]);
       }
-    for (int i = 0; i < MSM_SLOTS; i++) {
-      msm_free(&dev->mws[i]);
-      for (hipEvent_t e : {dev->mev_p2a[i], dev->mev_a2r[i], dev->mev_free[i]})
-        if (e) (void)hipEventDestroy(e);
-    }
+    for (int i = 0; i < MSM_STREAMS; i++) msm_free(&dev->mws[i]);
     for (int i = 0; i < MSM_RING; i++)
       if (dev->ring_ev[i]) (void)hipEventDestroy(dev->ring_ev[i]);
     if (dev->h_ring) (void)hipHostFree(dev->h_ring);
@@ -618,30 +570,6 @@ int h2g_msm_with_cached_base_dev(const void* d_scalars, size_t n, uint64_t base,
   if (off + n > it->second.n) return fail(H2G_ERR_ARG, "msm: bases.len() < size");
   if (n && !d_scalars) return fail(H2G_ERR_ARG, "msm: null scalars");
   return msm_desc_impl(d, d_scalars, it->second, off, n, out, is_id, pick_stream(d, stream));
-}
-
-int h2g_msm_with_cached_base_dev_shard(const void* d_scalars, size_t n, uint64_t base, size_t off, int world,
-                                       int rank, uint64_t out[8], int* is_id, uint32_t* bucket_lo, uint32_t* bucket_hi,
-                                       void* stream) {
-  NEED_DEV();
-  auto it = g_desc.find(base);
-  if (it == g_desc.end() || !it->second.is_base) return fail(H2G_ERR_HANDLE, "unknown base descriptor");
-  if (off + n > it->second.n) return fail(H2G_ERR_ARG, "msm: bases.len() < size");
-  if (n && !d_scalars) return fail(H2G_ERR_ARG, "msm: null scalars");
-  if (world < 1 || rank < 0 || rank >= world) return fail(H2G_ERR_ARG, "msm: bad world / rank");
-  const MsmFixedBase& fb = it->second.fb;
-  if (!fb.table) return fail(H2G_ERR_ARG, "msm: the base descriptor has no fixed-base windows");
-  MsmBucketRange br;
-  msm_bucket_range(fb, world, rank, &br);
-  if (bucket_lo) *bucket_lo = br.lo;
-  if (bucket_hi) *bucket_hi = br.hi;
-  if (world == 1) return msm_fixed_host_impl(d, d_scalars, fb, off, n, out, is_id, pick_stream(d, stream));
-  if (br.hi <= br.lo || n == 0) {  // an empty range: the identity
-    std::memset(out, 0, 64);
-    if (is_id) *is_id = 1;
-    return H2G_OK;
-  }
-  return msm_fixed_host_impl(d, d_scalars, fb, off, n, out, is_id, pick_stream(d, stream), &br);
 }
 
 int h2g_msm_descriptor_free(uint64_t handle) {
@@ -937,6 +865,16 @@ int h2g_fr_prefix_product(const uint64_t* a, uint64_t* out, size_t n) {
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(out, d->c.p, n * 32, hipMemcpyDeviceToHost, d->stream));
   HIPCHK(hipStreamSynchronize(d->stream));
+  return H2G_OK;
+}
+
+// exclusive prefix sum of u32 counts (the lookup argument's compactions and radix sort)
+int h2g_u32_exclusive_scan_dev(const void* in, void* out, size_t n, void* stream) {
+  NEED_DEV();
+  if (n && (!in || !out)) return fail(H2G_ERR_ARG, "null");
+  if (n >= 0xffffffffull) return fail(H2G_ERR_ARG, "scan: length >= 2^32");
+  HIPCHK(d->work.ensure(scan_u32_scratch_bytes(n) + 256));
+  HIPCHK(exclusive_scan_u32((const uint32_t*)in, (uint32_t*)out, n, d->work.p, pick_stream(d, stream)));
   return H2G_OK;
 }
 

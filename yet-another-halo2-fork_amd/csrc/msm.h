@@ -11,25 +11,21 @@ struct MsmConfig {
 
 // Device workspace, grown on demand and reused across calls.
 struct MsmWorkspace {
-  size_t cap[12] = {};  // byte capacity of each buffer below (grown on demand, never shrunk)
+  size_t cap[10] = {};  // byte capacity of each buffer below (grown on demand, never shrunk)
   int last_c = 0, last_W = 0;    // window config of the most recent msm_run
-  void* keys_in = nullptr;       // u64 [n*W] entries (key << 32 | value)
-  void* keys_out = nullptr;      // u64 [n*W] sorted entries
-  void* bucket_start = nullptr;  // u32 [W*NB]
-  void* bucket_end = nullptr;    // u32 [W*NB]
-  void* item_off = nullptr;      // uint4 multi-item big buckets (bucket, first item, items)
+  void* ent = nullptr;           // u64 [n*W] coarse-binned entries (key << 32 | value)
+  void* vals_out = nullptr;      // u32 [n*W] values (table index | sign << 31) in bucket order
   void* item_bucket = nullptr;   // big-bucket work items
   void* partials = nullptr;      // G1xyzz [2 * chunks] boundary slots
   void* buckets = nullptr;       // G1xyzz [W*NB]
   void* segs = nullptr;          // G1xyzz: reduction levels (2 ping-pong arrays + block sums)
   void* windows = nullptr;       // G1xyzz [W]
   void* result = nullptr;        // counters: [0] items, [1] multi-item buckets
+  void* item_off = nullptr;      // uint4 multi-item big buckets (bucket, first item, items)
   void* total_items = nullptr;   // G1xyzz partial sums of big-bucket items
-  void* sort_tmp = nullptr;  // partition counts / offsets; zero-initialised, the counts kept zero between MSMs
+  void* sort_tmp = nullptr;  // partition counts / offsets, per-key offsets; zero-initialised
   size_t sort_tmp_bytes = 0;
-  size_t sort_kcap = 0;  // per-key arrays' capacity (buckets of all sets)
-  void* scan_tmp = nullptr;
-  size_t scan_tmp_bytes = 0;
+  size_t sort_kcap = 0;  // per-key array's capacity (buckets of all sets)
 };
 
 int msm_choose_c(size_t n);
@@ -48,29 +44,6 @@ struct MsmPhaseEvents {
 static constexpr int MSM_MAX_BATCH = 64;
 struct MsmScalarList {
   const Fr* p[MSM_MAX_BATCH];
-  // fixed-base bucket range (msm_run_fixed's MsmBucketRange): only digits whose bucket lies in
-  // [klo, klo + kn) are kept, rebased to klo (kn = 0: every bucket)
-  uint32_t klo = 0, kn = 0;
-};
-
-// One rank's share of a fixed-base MSM split by buckets (the bucket-sum stage sharded
-// across GPUs): the digits falling in buckets [lo, hi) of the shared bucket set, whose
-// weighted sum, lo * (their plain sum) added, is that range's part of the MSM -- the
-// ranks' parts add up to the whole.  msm_bucket_range splits the buckets so that every
-// rank gets about the same number of entries (the balanced windows' narrower top digits
-// fill the upper buckets less).
-struct MsmBucketRange {
-  uint32_t lo = 0, hi = 0;
-};
-void msm_bucket_range(const struct MsmFixedBase& fb, int world, int rank, MsmBucketRange* r);
-
-// Stage streams of one pipelined MSM: the bucket partition runs on `part`, the
-// accumulation on `acc`, the fixup and the reduction on `red` (the events order them), so
-// that consecutive MSMs overlap one's partition or reduction with another's accumulation.
-// The caller keeps one workspace per MSM in flight and orders a workspace's reuse.
-struct MsmStreams {
-  hipStream_t part, acc, red;
-  hipEvent_t p2a, a2r;
 };
 
 // sum_i scalars[i] * bases[i]; scalars Montgomery Fr, bases affine Montgomery Fq
@@ -95,16 +68,13 @@ int msm_choose_c_fixed(size_t n);
 hipError_t msm_fixed_base_build(const G1Affine* d_bases, size_t n, int c, MsmFixedBase* fb, hipStream_t st);
 void msm_fixed_base_free(MsmFixedBase* fb);
 // sum_{i < n} scalars[i] * bases[off + i]; leaves ws->windows[0] (ws->last_W = 1)
-// ss: stage streams (st is then unused; results are ordered on ss->red)
 hipError_t msm_run_fixed(const Fr* d_scalars, const MsmFixedBase& fb, size_t off, size_t n, MsmWorkspace* ws,
-                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof = nullptr,
-                         const MsmStreams* ss = nullptr, const MsmBucketRange* br = nullptr);
+                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof = nullptr);
 // nbatch MSMs sum_i list.p[b][i] * bases[off + i] (b < nbatch <= MSM_MAX_BATCH) as one
 // pipeline -- one digits launch, one sort, one accumulation, one reduction with a bucket
 // set per MSM -- so the latency-bound reduction is paid once.  Leaves MSM b's sum in
 // ws->windows[b] (ws->last_W = nbatch).  nbatch * W * n must stay below 2^31.
 hipError_t msm_run_fixed_batch(const MsmScalarList& list, int nbatch, const MsmFixedBase& fb, size_t off, size_t n,
-                               MsmWorkspace* ws, hipStream_t st, MsmPhaseEvents* prof = nullptr,
-                               const MsmStreams* ss = nullptr);
+                               MsmWorkspace* ws, hipStream_t st, MsmPhaseEvents* prof = nullptr);
 
 }  // namespace h2g

@@ -6,34 +6,30 @@
 //
 // Pipeline (one stream, no host round trips):
 //   1. digits     : Montgomery -> canonical, signed c-bit windows (|d| <= 2^(c-1)),
-//                   key = window*NB + |d|-1, value = point index | sign << 31,
-//                   packed as one u64 entry (key << 32 | value); zero digits dropped
-//   2. partition  : two counting rounds group the entries by key (coarse bins from the
-//                   scalars directly, then keys inside each bin) -- the accumulation
-//                   needs buckets contiguous, not sorted
+//                   key = window*NB + |d|-1, value = point index | sign << 31; zero
+//                   digits dropped
+//   2. partition  : two counting rounds group the values by key (coarse bins from the
+//                   scalars directly, then one workgroup per bin orders its keys in LDS)
+//                   -- the accumulation needs buckets contiguous, not sorted; bucket k
+//                   is [koff[k], koff[k + 1]) of the u32 value array
 //   3. accumulate : the sorted array is cut into fixed chunks of L entries, one
 //                   thread per chunk (every thread does exactly L mixed additions,
 //                   whatever the bucket sizes -> no load imbalance, also for skewed
 //                   scalars).  XYZZ += affine (madd-2008-s) on lazily reduced
 //                   [0, 2p) coordinates, bases gathered by sorted index.  A run that
-//                   neither continues from the previous chunk nor into the next (two
-//                   neighbour reads) is a whole bucket and is written directly;
-//                   otherwise it goes to the chunk's boundary slot.  The runs also
-//                   record each bucket's [start, end) in the sorted array.
+//                   neither continues from the previous chunk nor into the next is a
+//                   whole bucket and is written directly; otherwise it goes to the
+//                   chunk's boundary slot.
 //   4. fixup      : buckets spanning chunks sum their boundary slots (one thread,
-//                   or one wavefront for buckets spanning > 32 chunks)
-//   5. segments   : per (window, segment of SEG buckets) running sums
-//                   sum_j (j+1) B_j = S_local + offset * R
-//   6. windows    : per window tree reduction of segment results in LDS
-//   7. final      : Horner over windows (c doublings each), to affine -- on the
+//                   or items of 64 pieces for buckets spanning more chunks)
+//   5. reduction  : sum_j (j+1) B_j per bucket set: group running sums, then bit planes
+//                   (or per-group scalar multiplications for c = 22 sets) and trees
+//   6. final      : Horner over windows (c doublings each), to affine -- on the
 //                   host for host-returning entry points (a single-lane chain of
 //                   ~250 doublings is latency-bound on the GPU), else one device lane.
 // The result is the unique affine point, so it is bit-identical to any other
 // correct MSM (e.g. the CPU restatement in oracle/) regardless of summation order.
-#include <stdlib.h>
-
 #include <algorithm>
-#include <string>
 
 #include "msm_part.h"
 
@@ -108,16 +104,16 @@ static constexpr uint32_t MSM_SMALL_Q4 = 32;
 
 template <int Q>
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ start,
-                 const uint32_t* __restrict__ end, uint32_t nbt, uint32_t L, G1xyzz* __restrict__ buckets,
+msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t nbt, uint32_t L,
+                 G1xyzz* __restrict__ buckets,
                  MsmBigItem* __restrict__ items, uint4* __restrict__ multi, uint32_t* __restrict__ counters) {
   const uint32_t b = (blockIdx.x * blockDim.x + threadIdx.x) / Q;
   const uint32_t lane = threadIdx.x & 63;
   const bool lead = (threadIdx.x % Q) == 0;
   uint32_t bs = 0, be = 0;
   if (b < nbt) {
-    bs = start[b];
-    be = end[b];
+    bs = koff[b];
+    be = koff[b + 1];
   }
   // np pieces (0: empty bucket, or written by the accumulation kernel)
   const uint32_t t0 = bs / L, t1 = be > bs ? (be - 1) / L : t0;
@@ -167,7 +163,7 @@ msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ st
 // MSM_GROUP lanes per item (4 items per wave, persistent grid): each lane sums up to
 // 4 strided pieces, then a log2(MSM_GROUP)-level tree in the wave's LDS slice.
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_big_item_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ start, uint32_t L,
+msm_big_item_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t L,
                     const MsmBigItem* __restrict__ items, const uint32_t* __restrict__ counters,
                     G1xyzz* __restrict__ partial, G1xyzz* __restrict__ buckets) {
   __shared__ G1xyzz sh[MSM_THREADS];
@@ -184,7 +180,7 @@ msm_big_item_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__
     MsmBigItem it = {0, 0, 0, 0};
     if (q < nitems) {
       it = items[q];
-      const uint32_t bs = start[it.b], t0 = bs / L;
+      const uint32_t bs = koff[it.b], t0 = bs / L;
       for (uint32_t t = it.tb + g; t < it.te; t += MSM_GROUP) acc = xyzz_add(acc, msm_piece(bnd, t, t0, bs, L));
     }
     w[g] = acc;
@@ -530,14 +526,11 @@ msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, 
 // mid[q' * WB + w]: 0 = sum S, 1 + b = U_b (b < LB + K).  The last of a set's blocks to
 // finish (device-scope counter, zeroed by the host) then scales U_b by 2^(b + e0), one
 // quad per plane, and sums.
-// Bucket-range MSMs (MsmBucketRange): boff > 0 adds boff T, T = the plain sum of the
-// range's buckets (the block-index fold's total), each set bit b of boff one more plane
-// 2^b T in the last block's sum -- the weights of the range's buckets are boff + j + 1.
-static constexpr int RPK_MAX = 10;  // block-index planes (LDS: 2^RPK_MAX points)
-static constexpr int RPK_DEFAULT = 9;  // above it (c = 22 sets) whole MSMs keep the rscale scheme
+static constexpr int RPK_MAX = 9;  // block-index planes (LDS: 2^RPK_MAX points); above it (c = 22
+                                   // sets) MSMs keep the rscale scheme
 __global__ void __launch_bounds__(1024)
 msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, int e0, G1xyzz* __restrict__ mid,
-                      uint32_t* __restrict__ done, G1xyzz* __restrict__ windows, uint32_t boff) {
+                      uint32_t* __restrict__ done, G1xyzz* __restrict__ windows) {
   __shared__ G1xyzz sh[1 << RPK_MAX];
   __shared__ uint32_t last;
   const uint32_t q = blockIdx.x, w = blockIdx.y, e = threadIdx.x >> 2, WB = gridDim.y;
@@ -581,9 +574,6 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, 
     for (int i = 0; i < (int)e + e0; i++) x = xyzz_dbl_q4(x);
   } else if (e == np) {
     x = mid[w];
-  } else if (e > np && e - np - 1 < 32 && ((boff >> (e - np - 1)) & 1u)) {  // 2^b T, bit b of boff
-    x = mid[(size_t)(1 + np) * WB + w];
-    for (uint32_t i = 0; i < e - np - 1; i++) x = xyzz_dbl_q4(x);
   }
   if (lead && e < 64) sh[e] = x;
   __syncthreads();
@@ -595,121 +585,6 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, 
     __syncthreads();
   }
   if (threadIdx.x == 0) windows[w] = sh[0];
-}
-
-// 6b. bucket reduction, alternative (H2G_MSM_RED=split): F = sum_{m=1}^{NB} m B_{m-1} ------
-// As a weighted sum WS(Y) = sum_t t Y_t (Y_t = B_{t-1}, Y_0 = 0) split by the low s bits
-// of t: WS(Y) = WS(V) + 2^s WS(U) with V_b = sum_{t mod 2^s = b} Y_t, U_a = sum_{t >> s = a} Y_t
-// -- plain sums, work ~2 NB additions at full occupancy, no per-group scalar
-// multiplications.  Two levels of splits leave four weighted sums of <= 64 points, each
-// done by one wave as the sum of its suffix sums (sum_t t Y_t = sum_{t >= 1} sum_{u >= t}
-// Y_u), scaled by doublings and added.  Latency-bound depth: ~11 (split 1) + ~7 (split 2)
-// + 12 (suffix scan + sum) + <= 21 doublings, against ~62 dependent point operations for
-// the previous group / scalar-multiplication / tree scheme.
-struct WsPlan {
-  uint32_t len0;         // NB + 1 (weights 0..NB)
-  int s1;                // first split
-  uint32_t nv1, nu1;     // V1, U1 lengths
-  int s2v, s2u;          // second splits of V1, U1
-  uint32_t nv2v, nu2v;   // V1 -> (V, U)
-  uint32_t nv2u, nu2u;   // U1 -> (V, U)
-  uint32_t per_set;      // points of level-1 + level-2 outputs per set
-};
-static int ceil_log2(uint64_t x) {
-  int b = 0;
-  while ((1ull << b) < x) b++;
-  return b;
-}
-static WsPlan ws_plan(uint32_t NB) {
-  WsPlan p;
-  p.len0 = NB + 1;
-  p.s1 = (ceil_log2(p.len0) + 1) / 2;
-  p.nv1 = 1u << p.s1;
-  p.nu1 = (p.len0 + p.nv1 - 1) >> p.s1;
-  p.s2v = (ceil_log2(p.nv1) + 1) / 2;
-  p.s2u = (ceil_log2(p.nu1) + 1) / 2;
-  p.nv2v = 1u << p.s2v;
-  p.nu2v = (p.nv1 + p.nv2v - 1) >> p.s2v;
-  p.nv2u = 1u << p.s2u;
-  p.nu2u = (p.nu1 + p.nv2u - 1) >> p.s2u;
-  p.per_set = p.nv1 + p.nu1 + p.nv2v + p.nu2v + p.nv2u + p.nu2u;
-  return p;
-}
-
-// one block per output: o < nV -> V_o = sum_a Y_{a 2^s + o}; else U_{o - nV} = sum_b Y_{(o - nV) 2^s + b};
-// Y_t = in[set * in_stride + t - yoff] for t >= yoff (identity below), t < len
-template <int BT>
-__global__ void __launch_bounds__(BT)
-msm_wsplit_kernel(const G1xyzz* __restrict__ in, uint32_t in_stride, uint32_t yoff, uint32_t len, int s,
-                  uint32_t nV, G1xyzz* __restrict__ out, uint32_t out_stride) {
-  __shared__ G1xyzz sh[BT];
-  const uint32_t o = blockIdx.x;
-  const G1xyzz* y = in + (size_t)blockIdx.y * in_stride;
-  G1xyzz acc = G1xyzz::identity();
-  if (o < nV) {
-    for (uint32_t t = ((uint32_t)threadIdx.x << s) + o; t < len; t += (uint32_t)BT << s)
-      if (t >= yoff) acc = xyzz_add(acc, y[t - yoff]);
-  } else {
-    const uint32_t lo = (o - nV) << s, hi = min(lo + (1u << s), len);
-    for (uint32_t t = lo + threadIdx.x; t < hi; t += BT)
-      if (t >= yoff) acc = xyzz_add(acc, y[t - yoff]);
-  }
-  sh[threadIdx.x] = acc;
-  __syncthreads();
-#pragma unroll 1
-  for (int h = BT / 2; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + h]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[(size_t)blockIdx.y * out_stride + o] = sh[0];
-}
-
-// per set: wave q < 4 computes X_q = sum_t t Y^q_t over its array (<= 64 points) and scales
-// it by 2^{e_q}; F = X_0 + X_1 + X_2 + X_3
-struct WsFinal {
-  uint32_t off[4], len[4];  // arrays inside the set's level-2 outputs
-  int e[4];                 // doublings
-};
-__global__ void __launch_bounds__(256)
-msm_wfinal_kernel(const G1xyzz* __restrict__ lv2, uint32_t stride, WsFinal f, G1xyzz* __restrict__ windows) {
-  __shared__ G1xyzz sh[256];
-  __shared__ G1xyzz res[4];
-  const int q = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const G1xyzz* y = lv2 + (size_t)blockIdx.x * stride + f.off[q];
-  G1xyzz* w = sh + 64 * q;
-  w[lane] = (uint32_t)lane < f.len[q] ? y[lane] : G1xyzz::identity();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 1
-  for (int d = 1; d < 64; d <<= 1) {  // inclusive suffix scan S_t = sum_{u >= t} Y_u
-    const G1xyzz v = lane + d < 64 ? xyzz_add(w[lane], w[lane + d]) : w[lane];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    w[lane] = v;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  if (lane == 0) w[0] = G1xyzz::identity();  // sum_{t >= 1} S_t
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 1
-  for (int h = 32; h > 0; h >>= 1) {
-    if (lane < h) w[lane] = xyzz_add(w[lane], w[lane + h]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  if (lane == 0) {
-    G1xyzz x = w[0];
-    for (int i = 0; i < f.e[q]; i++) x = xyzz_dbl(x);
-    res[q] = x;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) windows[blockIdx.x] = xyzz_add(xyzz_add(res[0], res[1]), xyzz_add(res[2], res[3]));
 }
 
 // fixed-base tables: table[w * stride + i] = [2^(offset of window w)] bases[i] -------
@@ -754,15 +629,14 @@ static hipError_t grow(void** p, size_t bytes) {
 }
 
 void msm_free(MsmWorkspace* ws) {
-  void** ptrs[] = {&ws->keys_in, &ws->keys_out, &ws->bucket_start,
-                   &ws->bucket_end, &ws->item_off, &ws->item_bucket, &ws->partials, &ws->buckets,
-                   &ws->segs, &ws->windows, &ws->result, &ws->total_items, &ws->sort_tmp, &ws->scan_tmp};
+  void** ptrs[] = {&ws->ent, &ws->vals_out, &ws->item_off, &ws->item_bucket, &ws->partials,
+                   &ws->buckets, &ws->segs, &ws->windows, &ws->result, &ws->total_items, &ws->sort_tmp};
   for (void** p : ptrs) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
   }
   for (auto& c : ws->cap) c = 0;
-  ws->sort_tmp_bytes = ws->scan_tmp_bytes = 0;
+  ws->sort_tmp_bytes = 0;
   ws->sort_kcap = 0;
 }
 
@@ -787,60 +661,31 @@ uint32_t msm_chunk_len(size_t total, size_t nbt) {
   return (uint32_t)L;
 }
 
-static double fb_entries_below(int W, uint64_t j);
+// quad-cooperative group kernels (rscale scheme) when the groups leave SIMDs idle: up to
+// 32768 groups over all sets (MSMs up to 2^21 points).  At 65536 groups (2^22) the quad
+// kernels lose even for a lone MSM: reduction 1.07 vs 0.72 ms, C3 k = 22 proof 94.1-94.3
+// vs 90.2-90.3 ms (profiles/r02/ab_q4/).  Quad fixup up to 2^15 buckets (2^16, the
+// 2^19-point slabs: the lane form is faster).
+static constexpr size_t RED_Q4_MAX = 32768;
+static constexpr uint32_t FIXUP_Q4_MAX = 32768;
 
 static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Affine* d_bases, size_t n, int c,
                                int W, int fixed, size_t stride, MsmWorkspace* ws, uint32_t item_len, G1Affine* d_out,
-                               hipStream_t st0, MsmPhaseEvents* prof, const MsmStreams* ss,
-                               const MsmBucketRange* br = nullptr) {
-  // stage streams: partition on ss->part, accumulation on ss->acc, fixup + reduction on
-  // ss->red (one stream for all three without ss)
-  hipStream_t st = ss ? ss->part : st0;
+                               hipStream_t st, MsmPhaseEvents* prof) {
 #define H2G_PHASE(i) \
   if (prof) H2G_TRY(hipEventRecord(prof->ev[i], st))
-#define H2G_STAGE(next, ev)                             \
-  if (ss && (next) != st) {                             \
-    H2G_TRY(hipEventRecord((ev), st));                  \
-    H2G_TRY(hipStreamWaitEvent((next), (ev), 0));       \
-    st = (next);                                        \
-  }
-  const bool ranged = br && br->hi > br->lo;  // one rank's bucket range of a fixed-base MSM
-  if (ranged && (!fixed || nbatch != 1 || br->hi > (1u << (c - 1)))) return hipErrorInvalidValue;
-  const uint32_t NB = ranged ? br->hi - br->lo : 1u << (c - 1);
+  const uint32_t NB = 1u << (c - 1);
   if (nbatch < 1 || nbatch > MSM_MAX_BATCH || (!fixed && nbatch != 1)) return hipErrorInvalidValue;
   const int WB = fixed ? nbatch : W;  // bucket sets
   const uint32_t nbt = (uint32_t)WB * NB;
   const size_t total = n * (size_t)W * nbatch;
   if (total >= 0x80000000ull) return hipErrorInvalidValue;  // u32 positions in the sorted array
   // buckets most windows can reach (fixed-base: 2^(base width - 1) of the balanced widths)
-  const size_t nb_eff = ranged ? (size_t)NB : (size_t)WB << ((fixed ? 255 / W : c) - 1);
-  static const uint32_t chunk_env = [] {  // H2G_MSM_CHUNK: fixed chunk length (A/B runs)
-    const char* e = getenv("H2G_MSM_CHUNK");
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
-  // a bucket range keeps its share of the entries: size the chunks for that, not for n W
-  const size_t total_eff =
-      ranged ? (size_t)((double)total * (fb_entries_below(W, br->hi) - fb_entries_below(W, br->lo)) /
-                        fb_entries_below(W, (uint64_t)1 << (c - 1))) + 1
-             : total;
-  const uint32_t L = item_len > 0 ? item_len : (chunk_env ? chunk_env : msm_chunk_len(total_eff, nb_eff));
+  const size_t nb_eff = (size_t)WB << ((fixed ? 255 / W : c) - 1);
+  const uint32_t L = item_len > 0 ? item_len : msm_chunk_len(total, nb_eff);
   const size_t nchunks = (total + L - 1) / L;
-  static const bool red_split = [] {
-    const char* e = getenv("H2G_MSM_RED");
-    return e && std::string(e) == "split";
-  }();
-  static const bool red_group = [] {  // rscale / rfinal for every size (A/B runs)
-    const char* e = getenv("H2G_MSM_RED");
-    return e && std::string(e) == "group";
-  }();
   const uint32_t m1 = (NB + RG - 1) / RG;
-  // quad-cooperative group kernels when the groups leave SIMDs idle (<= 512 waves of one
-  // lane per group); the block sums then cover Q4_GROUPS groups each
-  static const size_t q4_max = [] {
-    const char* e = getenv("H2G_MSM_Q4_MAX");
-    return e ? (size_t)atol(e) : (size_t)32768;
-  }();
-  const bool red_q4 = (size_t)m1 * WB <= q4_max;
+  const bool red_q4 = (size_t)m1 * WB <= RED_Q4_MAX;
   const uint32_t nblk = red_q4 ? (m1 + Q4_GROUPS - 1) / Q4_GROUPS : (m1 + MSM_THREADS - 1) / MSM_THREADS;
   // bit planes.  Small sets (<= 2^18 buckets over all sets, e.g. the 2^16 of a 2^19-point
   // slab): quad-cooperative, 256 groups per block, and the fewest buckets per group (rgp)
@@ -848,33 +693,20 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   // is a dependent chain of ~2 rgp + 8 + 9 + log2(NB) point operations, so the group chain
   // goes first (2^16 buckets: rgp = 1; 0.38 -> 0.33 ms at 2^19 points).  Larger sets: a
   // lane per group of 8 (the quads' 1.3x issue cost loses there: 0.62 -> 0.71 ms at 2^19
-  // buckets).  H2G_MSM_PLANE (A/B runs): "old" = round 2's geometry (rgp 8, 64-group quad
-  // blocks up to 2^15 groups), "rg4" = large sets with groups of 4.
-  static const int plane_mode = [] {
-    const char* e = getenv("H2G_MSM_PLANE");
-    if (!e) return 0;
-    return std::string(e) == "old" ? 1 : (std::string(e) == "rg4" ? 2 : 0);
-  }();
-  int rgp = 8, plane_q = 4, plane_lb = 8;
-  if (plane_mode == 1) {
-    plane_q = red_q4 ? 4 : 1;
-    plane_lb = red_q4 ? 6 : 8;
-  } else if ((size_t)NB * WB <= (1u << 18)) {
+  // buckets; groups of 4: slower).
+  int rgp = 8, plane_q = 4;
+  const int plane_lb = 8;
+  if ((size_t)NB * WB <= (1u << 18)) {
     for (rgp = 1; rgp < 8; rgp *= 2)
       if ((size_t)((NB + rgp - 1) / rgp) * WB <= 65536) break;
   } else {
     plane_q = 1;
-    rgp = plane_mode == 2 ? 4 : 8;
   }
-  const bool plane_old = plane_mode == 1;
   const uint32_t m1p = (NB + rgp - 1) / rgp;                         // plane groups per set
   const uint32_t nblk_p = (m1p + (1u << plane_lb) - 1) >> plane_lb;  // plane kernels' blocks
   // bit planes unless the block index needs more than RPK_MAX bits (sets of > 2^17
   // groups, e.g. c = 22): those keep the rscale scheme
-  const bool red_plane = !red_group && nblk_p <= (1u << (ranged ? RPK_MAX : RPK_DEFAULT));
-  if (ranged && (!red_plane || red_split)) return hipErrorInvalidValue;  // the offset term is in the planes
-  const WsPlan wp = ws_plan(NB);
-  if (red_split && (wp.nv2v > 64 || wp.nu2v > 64 || wp.nv2u > 64 || wp.nu2u > 64)) return hipErrorInvalidValue;
+  const bool red_plane = nblk_p <= (1u << RPK_MAX);
   // grow-only workspace: MSMs of slightly different shapes (e.g. n and n - 1 points, so
   // another chunk length) reuse it instead of reallocating (~2 ms of host stall each)
   struct Need {
@@ -882,71 +714,55 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     size_t bytes;
   };
   const size_t icap = msm_big_items_cap(nchunks), mcap = msm_big_multi_cap(nchunks);
-  const Need need[12] = {{&ws->keys_in, total * 8},
-                         {&ws->keys_out, total * 8},
-                         {&ws->bucket_start, (size_t)nbt * 4},
-                         {&ws->bucket_end, (size_t)nbt * 4},
+  const Need need[10] = {{&ws->ent, total * 8},
+                         {&ws->vals_out, total * 4},
                          {&ws->item_bucket, icap * sizeof(MsmBigItem)},  // big-bucket items
                          {&ws->partials, 2 * nchunks * sizeof(G1xyzz)},  // boundary slots
                          {&ws->buckets, (size_t)nbt * sizeof(G1xyzz)},
-                         {&ws->segs, std::max<size_t>(wp.per_set, std::max<size_t>((size_t)2 * m1 + nblk,
-                                                                                    10 * (size_t)nblk_p + 32)) *
-                                         WB * sizeof(G1xyzz)},
+                         {&ws->segs, std::max<size_t>((size_t)2 * m1 + nblk, 10 * (size_t)nblk_p + 32) * WB *
+                                         sizeof(G1xyzz)},
                          {&ws->windows, (size_t)(W > WB ? W : WB) * sizeof(G1xyzz)},
                          {&ws->result, 16},                              // [0] items, [1] multi-item buckets
                          {&ws->item_off, mcap * sizeof(uint4)},          // multi-item buckets
                          {&ws->total_items, icap * sizeof(G1xyzz)}};     // items' partial sums
-  for (int b = 0; b < 12; b++)
+  for (int b = 0; b < 10; b++)
     if (need[b].bytes > ws->cap[b]) {
       H2G_TRY(grow(need[b].p, need[b].bytes));
       ws->cap[b] = need[b].bytes;
     }
   ws->last_c = c;
   ws->last_W = WB;
-  uint64_t* keys_in = (uint64_t*)ws->keys_in;
-  uint64_t* keys_out = (uint64_t*)ws->keys_out;
-  uint32_t* bstart = (uint32_t*)ws->bucket_start;
-  uint32_t* bend = (uint32_t*)ws->bucket_end;
+  uint32_t* vals_out = (uint32_t*)ws->vals_out;
   uint32_t* counters = (uint32_t*)ws->result;
-  const uint32_t sentinel = nbt;  // key of zero digits (msm_digits_kernel)
   MsmBigItem* items = (MsmBigItem*)ws->item_bucket;
   uint4* multi = (uint4*)ws->item_off;
   G1xyzz* ipart = (G1xyzz*)ws->total_items;
   G1xyzz* buckets = (G1xyzz*)ws->buckets;
   G1xyzz* bnd = (G1xyzz*)ws->partials;
-  G1xyzz* rS = (G1xyzz*)ws->segs;  // default reduction: group sums, group weights, block sums
+  G1xyzz* rS = (G1xyzz*)ws->segs;  // rscale scheme: group sums, group weights, block sums
   G1xyzz* rR = rS + (size_t)WB * m1;
   G1xyzz* rP = rR + (size_t)WB * m1;
-  G1xyzz* lv1 = (G1xyzz*)ws->segs;                    // split reduction, per set: V1 | U1
-  G1xyzz* lv2 = lv1 + (size_t)WB * (wp.nv1 + wp.nu1);  // per set: V1 -> (V, U) | U1 -> (V, U)
 
   // bucket partition geometry: keys < nbt, fine bits fb, coarse bins nbt >> fb
   int key_bits = 1;
   while ((1ull << key_bits) < (uint64_t)nbt) key_bits++;
-  // fine bits (the fine pass's fan-out per 4096-entry tile; H2G_MSM_FB for A/B runs): 10
-  // -- 2x the coarse bins of 11 but half the per-tile key runs and global cursor atomics
-  // of the fine scatter; interleaved on one box the k = 22 proof took 86.5-86.8 ms vs
-  // 86.8-87.3 ms at 11, the 2^22 MSM 6.94-6.97 vs 6.98-6.99 ms (8, 9: slower coarse pass)
-  static const int fb_max = [] {
-    const char* e = getenv("H2G_MSM_FB");
-    const int v = e ? atoi(e) : 10;
-    return v >= 4 && v <= FB_MAX ? v : 10;
-  }();
-  int fb = key_bits < fb_max ? key_bits : fb_max;
-  while (fb < 13 && (((uint64_t)nbt + (1ull << fb) - 1) >> fb) > COARSE_MAX) fb++;
-  const uint32_t nf = 1u << fb;
-  const uint32_t ncoarse = (uint32_t)((nbt + nf - 1) >> fb);
-  if (ncoarse > COARSE_MAX || fb > FB_MAX) return hipErrorInvalidValue;
+  // fine bits (the fine pass's fan-out per tile): 10 -- 2x the coarse bins of 11 but half
+  // the per-tile key runs and global cursor atomics of the fine scatter; interleaved on one
+  // box the k = 22 proof took 86.5-86.8 ms vs 86.8-87.3 ms at 11 (8, 9: slower coarse pass)
+  int fb = key_bits < 10 ? key_bits : 10;
+  while (fb < FB_MAX && (((uint64_t)nbt + (1ull << fb) - 1) >> fb) > COARSE_MAX) fb++;
+  const uint32_t ncoarse = (uint32_t)(((uint64_t)nbt + (1ull << fb) - 1) >> fb);
+  if (ncoarse > COARSE_MAX) return hipErrorInvalidValue;
   const uint32_t kblocks = (nbt + 1023) / 1024;
   constexpr int RDONE_MAX = 256;  // bucket sets: W <= 128 windows (c >= 2), or nbatch <= MSM_MAX_BATCH
   if (WB > RDONE_MAX) return hipErrorInvalidValue;
   // scratch (u32), laid out for a per-key capacity kcap >= nbt so that the counts stay at
-  // fixed places: ccount | coff | ccursor | total | rdone | kbsum | kboff | kcount | koff |
-  // kcursor.  Zeroed when allocated; the scans zero ccount / kcount after reading them, so
-  // no MSM needs a fill.
+  // fixed places: ccount | coff | ccursor | total | rdone | kbsum | kboff | kcount | koff
+  // (kcap + 1) | kcursor.  Zeroed when allocated; the scans zero ccount / kcount after
+  // reading them, so no MSM needs a fill.
   if ((size_t)nbt > ws->sort_kcap) {
     const size_t kcap = nbt, kbmax = (kcap + 1023) / 1024;
-    const size_t words = 3 * (size_t)COARSE_MAX + 16 + RDONE_MAX + 2 * kbmax + 3 * kcap;
+    const size_t words = 3 * (size_t)COARSE_MAX + 16 + RDONE_MAX + 2 * kbmax + 3 * kcap + 1;
     H2G_TRY(grow(&ws->sort_tmp, words * 4));
     H2G_TRY(hipMemsetAsync(ws->sort_tmp, 0, words * 4, st));
     ws->sort_tmp_bytes = words * 4;
@@ -962,17 +778,13 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   uint32_t* kboff = kbsum + kbmax;
   uint32_t* kcount = kboff + kbmax;
   uint32_t* koff = kcount + kcap;
-  uint32_t* kcursor = koff + kcap;
+  uint32_t* kcursor = koff + kcap + 1;
 
   const int T = MSM_THREADS;
   H2G_PHASE(0);
   {  // rounds 1 and 2 (msm_part.hip); phase event 1 between them
     MsmPartArgs pa;
     pa.list = list;
-    if (ranged) {
-      pa.list.klo = br->lo;
-      pa.list.kn = NB;
-    }
     pa.nbatch = nbatch;
     pa.n = n;
     pa.c = c;
@@ -994,97 +806,59 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     pa.kcount = kcount;
     pa.koff = koff;
     pa.kcursor = kcursor;
-    pa.keys_in = keys_in;
-    pa.keys_out = keys_out;
-    pa.z = MsmZero{bstart, bend, (size_t)nbt, counters, rdone, (uint32_t)WB};
+    pa.ent = (uint64_t*)ws->ent;
+    pa.out = vals_out;
+    pa.z = MsmZero{counters, rdone, (uint32_t)WB};
     H2G_TRY(msm_partition(pa, st, prof));
   }
   H2G_PHASE(2);
-  H2G_STAGE(ss->acc, ss->p2a);
-  // (bucket bounds, counters: zeroed by the coarse histogram; empty buckets: by the fixup)
   H2G_PHASE(3);
-  H2G_TRY(msm_accumulate(d_bases, (const uint64_t*)keys_out, (const uint32_t*)d_total, sentinel, L, nchunks, buckets,
-                         bnd, bstart, bend, st));
+  H2G_TRY(msm_accumulate(d_bases, vals_out, koff, nbt, d_total, L, nchunks, buckets, bnd, st));
   H2G_PHASE(4);
-  H2G_STAGE(ss->red, ss->a2r);
-  static const uint32_t fix_q4_max = [] {  // H2G_MSM_FIXUP_Q4_MAX: bucket sets with quad fixup (A/B)
-    const char* e = getenv("H2G_MSM_FIXUP_Q4_MAX");
-    return e ? (uint32_t)atol(e) : 32768u;  // 2^16 buckets (2^19-point slabs): the lane form is faster
-  }();
-  if (nbt <= fix_q4_max)
+  if (nbt <= FIXUP_Q4_MAX)
     hipLaunchKernelGGL(msm_fixup_kernel<4>, dim3((unsigned)(((size_t)nbt * 4 + T - 1) / T)), dim3(T), 0, st,
-                       (const G1xyzz*)bnd, bstart, bend, nbt, L, buckets, items, multi, counters);
+                       (const G1xyzz*)bnd, (const uint32_t*)koff, nbt, L, buckets, items, multi, counters);
   else
-    hipLaunchKernelGGL(msm_fixup_kernel<1>, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)bnd, bstart,
-                       bend, nbt, L, buckets, items, multi, counters);
-  hipLaunchKernelGGL(msm_big_item_kernel, dim3(MSM_BIG_BLOCKS), dim3(T), 0, st, (const G1xyzz*)bnd, bstart, L,
-                     (const MsmBigItem*)items, (const uint32_t*)counters, ipart, buckets);
+    hipLaunchKernelGGL(msm_fixup_kernel<1>, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)bnd,
+                       (const uint32_t*)koff, nbt, L, buckets, items, multi, counters);
+  hipLaunchKernelGGL(msm_big_item_kernel, dim3(MSM_BIG_BLOCKS), dim3(T), 0, st, (const G1xyzz*)bnd,
+                     (const uint32_t*)koff, L, (const MsmBigItem*)items, (const uint32_t*)counters, ipart, buckets);
   hipLaunchKernelGGL(msm_big_combine_kernel, dim3(MSM_BIG_BLOCKS / 4), dim3(T), 0, st, (const uint4*)multi,
                      (const uint32_t*)counters, (const G1xyzz*)ipart, buckets);
   H2G_PHASE(5);
-  if (!red_split) {
-    if (red_plane) {  // bit planes (6a')
-      G1xyzz* planes = (G1xyzz*)ws->segs;
-      G1xyzz* mid = planes + (size_t)(plane_lb + 2) * WB * nblk_p;
-      int e0 = 0;
-      while ((1 << e0) < rgp) e0++;
-      const dim3 pg(nblk_p, (unsigned)WB), pb((unsigned)(plane_q << plane_lb));
-      const G1xyzz* bk = buckets;
-      if (plane_old && plane_q == 4)
-        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 6, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
-      else if (plane_q == 1 && rgp == 4)
-        hipLaunchKernelGGL((msm_rgroup_plane_kernel<1, 8, 4>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
-      else if (plane_q == 1)
-        hipLaunchKernelGGL((msm_rgroup_plane_kernel<1, 8, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
-      else if (rgp == 1)
-        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 1>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
-      else if (rgp == 2)
-        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 2>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
-      else if (rgp == 4)
-        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 4>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
-      else
-        hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
-      hipLaunchKernelGGL(msm_rplane_mid_kernel, dim3((unsigned)plane_lb + 2, (unsigned)WB), dim3(1024), 0, st,
-                         (const G1xyzz*)planes, nblk_p, plane_lb, e0, mid, rdone, (G1xyzz*)ws->windows,
-                         ranged ? br->lo : 0u);
-    } else {
-      if (red_q4)
-        hipLaunchKernelGGL(msm_rgroup_q4_kernel, dim3((unsigned)(((size_t)m1 * 4 + T - 1) / T), (unsigned)WB),
-                           dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1, rS, rR);
-      else
-        hipLaunchKernelGGL(msm_rgroup_kernel, dim3((m1 + T - 1) / T, (unsigned)WB), dim3(T), 0, st,
-                           (const G1xyzz*)buckets, NB, m1, rS, rR);
-      if (red_q4)
-        hipLaunchKernelGGL(msm_rscale_q4_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
-                           (const G1xyzz*)rR, m1, rP, nblk);
-      else
-        hipLaunchKernelGGL(msm_rscale_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
-                           (const G1xyzz*)rR, m1, rP, nblk);
-      hipLaunchKernelGGL(msm_rfinal_q4_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rP, nblk,
-                         (G1xyzz*)ws->windows);
-    }
+  if (red_plane) {  // bit planes (6a')
+    G1xyzz* planes = (G1xyzz*)ws->segs;
+    G1xyzz* mid = planes + (size_t)(plane_lb + 2) * WB * nblk_p;
+    int e0 = 0;
+    while ((1 << e0) < rgp) e0++;
+    const dim3 pg(nblk_p, (unsigned)WB), pb((unsigned)(plane_q << plane_lb));
+    const G1xyzz* bk = buckets;
+    if (plane_q == 1)
+      hipLaunchKernelGGL((msm_rgroup_plane_kernel<1, 8, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+    else if (rgp == 1)
+      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 1>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+    else if (rgp == 2)
+      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 2>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+    else if (rgp == 4)
+      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 4>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+    else
+      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+    hipLaunchKernelGGL(msm_rplane_mid_kernel, dim3((unsigned)plane_lb + 2, (unsigned)WB), dim3(1024), 0, st,
+                       (const G1xyzz*)planes, nblk_p, plane_lb, e0, mid, rdone, (G1xyzz*)ws->windows);
   } else {
-    const uint32_t s1n = wp.nv1 + wp.nu1, s2n = wp.nv2v + wp.nu2v + wp.nv2u + wp.nu2u;
-    hipLaunchKernelGGL(msm_wsplit_kernel<256>, dim3(s1n, (unsigned)WB), dim3(256), 0, st, (const G1xyzz*)buckets, NB,
-                       1u, wp.len0, wp.s1, wp.nv1, lv1, s1n);
-    hipLaunchKernelGGL(msm_wsplit_kernel<64>, dim3(wp.nv2v + wp.nu2v, (unsigned)WB), dim3(64), 0, st,
-                       (const G1xyzz*)lv1, s1n, 0u, wp.nv1, wp.s2v, wp.nv2v, lv2, s2n);
-    hipLaunchKernelGGL(msm_wsplit_kernel<64>, dim3(wp.nv2u + wp.nu2u, (unsigned)WB), dim3(64), 0, st,
-                       (const G1xyzz*)(lv1 + wp.nv1), s1n, 0u, wp.nu1, wp.s2u, wp.nv2u, lv2 + wp.nv2v + wp.nu2v, s2n);
-    WsFinal f;  // F = X(V1.V) + 2^s2v X(V1.U) + 2^s1 (X(U1.V) + 2^s2u X(U1.U))
-    f.off[0] = 0;
-    f.len[0] = wp.nv2v;
-    f.e[0] = 0;
-    f.off[1] = wp.nv2v;
-    f.len[1] = wp.nu2v;
-    f.e[1] = wp.s2v;
-    f.off[2] = wp.nv2v + wp.nu2v;
-    f.len[2] = wp.nv2u;
-    f.e[2] = wp.s1;
-    f.off[3] = wp.nv2v + wp.nu2v + wp.nv2u;
-    f.len[3] = wp.nu2u;
-    f.e[3] = wp.s1 + wp.s2u;
-    hipLaunchKernelGGL(msm_wfinal_kernel, dim3((unsigned)WB), dim3(256), 0, st, (const G1xyzz*)lv2, s2n, f,
+    if (red_q4)
+      hipLaunchKernelGGL(msm_rgroup_q4_kernel, dim3((unsigned)(((size_t)m1 * 4 + T - 1) / T), (unsigned)WB),
+                         dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1, rS, rR);
+    else
+      hipLaunchKernelGGL(msm_rgroup_kernel, dim3((m1 + T - 1) / T, (unsigned)WB), dim3(T), 0, st,
+                         (const G1xyzz*)buckets, NB, m1, rS, rR);
+    if (red_q4)
+      hipLaunchKernelGGL(msm_rscale_q4_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
+                         (const G1xyzz*)rR, m1, rP, nblk);
+    else
+      hipLaunchKernelGGL(msm_rscale_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
+                         (const G1xyzz*)rR, m1, rP, nblk);
+    hipLaunchKernelGGL(msm_rfinal_q4_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rP, nblk,
                        (G1xyzz*)ws->windows);
   }
   if (d_out && nbatch == 1)
@@ -1092,7 +866,6 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   H2G_TRY(hipGetLastError());
   H2G_PHASE(6);
 #undef H2G_PHASE
-#undef H2G_STAGE
   return hipSuccess;
 }
 
@@ -1101,8 +874,7 @@ hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWo
   const int c = cfg.c > 0 ? cfg.c : msm_choose_c(n);
   MsmScalarList list;
   list.p[0] = d_scalars;
-  return msm_pipeline(list, 1, d_bases, n, c, msm_windows_for(c), 0, 0, ws, (uint32_t)cfg.item_len, d_out, st, prof,
-                      nullptr);
+  return msm_pipeline(list, 1, d_bases, n, c, msm_windows_for(c), 0, 0, ws, (uint32_t)cfg.item_len, d_out, st, prof);
 }
 
 int msm_choose_c_fixed(size_t n) {
@@ -1141,47 +913,17 @@ void msm_fixed_base_free(MsmFixedBase* fb) {
 }
 
 hipError_t msm_run_fixed(const Fr* d_scalars, const MsmFixedBase& fb, size_t off, size_t n, MsmWorkspace* ws,
-                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof, const MsmStreams* ss,
-                         const MsmBucketRange* br) {
+                         G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof) {
   if (off + n > fb.n) return hipErrorInvalidValue;
   MsmScalarList list;
   list.p[0] = d_scalars;
-  return msm_pipeline(list, 1, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, d_out, st, prof, ss, br);
-}
-
-// entries expected in buckets [0, j) of a fixed-base set: window w (balanced width cw) puts
-// its digits in buckets [0, 2^(cw - 1)), about uniformly
-static double fb_entries_below(int W, uint64_t j) {
-  double t = 0;
-  for (int w = 0; w < W; w++) {
-    const uint64_t cap = 1ull << (fb_width(W, w) - 1);
-    t += (double)(j < cap ? j : cap) / (double)cap;
-  }
-  return t;
-}
-
-void msm_bucket_range(const MsmFixedBase& fb, int world, int rank, MsmBucketRange* r) {
-  const uint64_t NB = 1ull << (fb.c - 1);
-  auto cut = [&](int q) -> uint32_t {  // the bucket where a q / world share of the entries ends
-    if (q <= 0) return 0;
-    if (q >= world) return (uint32_t)NB;
-    const double target = fb_entries_below(fb.W, NB) * q / world;
-    uint64_t lo = 0, hi = NB;
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi) / 2;
-      if (fb_entries_below(fb.W, mid) < target) lo = mid + 1;
-      else hi = mid;
-    }
-    return (uint32_t)lo;
-  };
-  r->lo = cut(rank);
-  r->hi = cut(rank + 1);
+  return msm_pipeline(list, 1, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, d_out, st, prof);
 }
 
 hipError_t msm_run_fixed_batch(const MsmScalarList& list, int nbatch, const MsmFixedBase& fb, size_t off, size_t n,
-                               MsmWorkspace* ws, hipStream_t st, MsmPhaseEvents* prof, const MsmStreams* ss) {
+                               MsmWorkspace* ws, hipStream_t st, MsmPhaseEvents* prof) {
   if (off + n > fb.n) return hipErrorInvalidValue;
-  return msm_pipeline(list, nbatch, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, nullptr, st, prof, ss);
+  return msm_pipeline(list, nbatch, fb.table + off, n, fb.c, fb.W, 1, fb.n, ws, 0, nullptr, st, prof);
 }
 
 }  // namespace h2g

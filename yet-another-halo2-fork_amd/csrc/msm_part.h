@@ -5,8 +5,8 @@
 
 namespace h2g {
 
-static constexpr int FB_MAX = 11;        // fine bits
-static constexpr int COARSE_MAX = 2048;  // coarse bins (keys < 2^22)
+static constexpr int FB_MAX = 11;        // fine bits (keys per coarse bin <= 2^FB_MAX)
+static constexpr int COARSE_MAX = 2048;  // coarse bins
 
 // Fixed-base windows have balanced widths: W = ceil(255 / c) windows covering the 255
 // bits signed digits need, the first 255 % W of them one bit wider (<= c).  Uniform
@@ -14,20 +14,18 @@ static constexpr int COARSE_MAX = 2048;  // coarse bins (keys < 2^22)
 // whose digits pile n entries into a few buckets -- the big-bucket path, ~0.2-0.5 ms.
 __host__ __device__ __forceinline__ int fb_width(int W, int w) { return 255 / W + (w < 255 % W ? 1 : 0); }
 
-// zeroed by the coarse histogram kernel for the later phases: bucket [start, end) (empty
-// buckets keep 0, 0), the big-item counters, the plane reduction's finished-block counts
+// zeroed by the coarse histogram kernel for the later phases: the big-item counters, the
+// plane reduction's finished-block counts
 struct MsmZero {
-  uint32_t* bstart;
-  uint32_t* bend;
-  size_t nb;
   uint32_t* counters;
   uint32_t* rdone;
   uint32_t nrd;
 };
 
 // One partition of the MSM pipeline's entries: round 1 (coarse bins straight from the
-// scalars, into keys_in), phase event 1, round 2 (keys inside the bins, into keys_out).
-// The scratch arrays are msm_pipeline's (zero counts on entry, left zero).
+// scalars, into ent), phase event 1, round 2 (keys inside the bins: the values in bucket
+// order into out, koff[k] = the first position of key k's run, koff[nbt] = the entry
+// count).  The scratch arrays are msm_pipeline's (zero counts on entry, left zero).
 struct MsmPartArgs {
   MsmScalarList list;
   int nbatch;
@@ -40,15 +38,16 @@ struct MsmPartArgs {
   int fb;
   uint32_t ncoarse, nbt, kblocks;
   uint32_t *ccount, *coff, *ccursor, *d_total, *kbsum, *kboff, *kcount, *koff, *kcursor;
-  uint64_t *keys_in, *keys_out;
+  uint64_t* ent;
+  uint32_t* out;
   MsmZero z;
 };
 hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* prof);
 
-// step 3 of the pipeline (msm_acc.hip): XYZZ accumulation of the bucket-sorted entries in
-// chunks of L, one thread per chunk
-hipError_t msm_accumulate(const G1Affine* bases, const uint64_t* ent, const uint32_t* d_total, uint32_t sentinel,
-                          uint32_t L, size_t nchunks, G1xyzz* buckets, G1xyzz* bnd, uint32_t* bstart, uint32_t* bend,
+// step 3 of the pipeline (msm_acc.hip): XYZZ accumulation of the bucket-sorted values in
+// chunks of L, one thread per chunk; bucket k's run is [koff[k], koff[k + 1])
+hipError_t msm_accumulate(const G1Affine* bases, const uint32_t* vals, const uint32_t* koff, uint32_t nbt,
+                          const uint32_t* d_total, uint32_t L, size_t nchunks, G1xyzz* buckets, G1xyzz* bnd,
                           hipStream_t st);
 
 }  // namespace h2g

@@ -2,8 +2,6 @@
 // signed digits straight from the scalars into coarse bins, then keys inside the bins.
 // Its own translation unit: none of it is elliptic-curve arithmetic, so it builds in
 // seconds while msm.hip's point kernels take minutes.
-#include <stdlib.h>
-
 #include "msm_part.h"
 
 namespace h2g {
@@ -16,29 +14,28 @@ namespace h2g {
 // serves them all.  Negative digits set bit 31 of the value.
 // 2. bucket partition of the entries ------------------------------------------------
 // The accumulation needs each bucket's entries contiguous, not sorted: a two-round
-// counting partition replaces the radix sort.  Round 1 splits by the key's high bits
-// (coarse bins) straight from the scalars, round 2 by the low FB bits inside each coarse
-// bin (a bin's region is a few hundred KB, so its scattered writes stay in L2).  Zero
-// digits produce no entry at all.  Order inside a bucket is arbitrary (the sum is exact).
-#ifndef H2G_MSM_PT
-#define H2G_MSM_PT 512
-#endif
-#ifndef H2G_MSM_FPER  // entries per fine-kernel thread: 8 (2048-entry tiles) measured best at 10 fine bits
-#define H2G_MSM_FPER 8
-#endif
-static constexpr int PT = H2G_MSM_PT;      // threads of the coarse kernels (one scalar each)
-static constexpr int PWG = 16;             // windows per coarse-kernel thread (grid.z groups)
-static constexpr int FT = 256;             // threads of the fine kernels
-static constexpr int FPER = H2G_MSM_FPER;  // entries per fine-kernel thread
+// counting partition replaces a sort.  Round 1 splits by the key's high bits (coarse
+// bins) straight from the scalars (u64 entries, key << 32 | value), round 2 by the low
+// fb bits inside each coarse bin, in tiles of FTILE entries; it writes only the u32
+// values, bucket k being [koff[k], koff[k + 1]) of them.  Round 2's tiles are ordered so
+// that each XCD takes a contiguous range of them (workgroups go round-robin over the 8
+// XCDs): a bin's scattered writes then come from one XCD's L2, where the partial lines
+// merge.  (One workgroup per coarse bin instead -- LDS histogram, no global atomics --
+// measured slower, 0.82 vs 0.58 ms at 2^22, and its long-lived 1024-thread workgroups
+// starved the other MSM stream's accumulation inside the proof: 107 vs 90 ms.)  Zero
+// digits produce no entry.  Order inside a bucket is arbitrary (the sum is exact).
+static constexpr int PT = 512;     // threads of the coarse kernels (one scalar each)
+static constexpr int PWG = 16;     // windows per coarse-kernel thread (grid.z groups)
+static constexpr int FT = 256;     // threads of the fine kernels
+static constexpr int FPER = 8;     // entries per fine-kernel thread: 8 (2048-entry tiles) measured best at 10 fine bits
 static constexpr uint32_t FTILE = (uint32_t)FT * FPER;
 
-
 // the signed digits of scalar i (batch bi) for windows [w0, w0 + PWG): fn(slot, key, val)
-// for each nonzero digit (same key / value encoding as msm_digits_kernel); fixed-base
-// windows take their balanced widths (fb_width), generic ones c bits each
+// for each nonzero digit; fixed-base windows take their balanced widths (fb_width),
+// generic ones c bits each
 template <class Fn>
-__device__ __forceinline__ void scalar_digits(const MsmScalarList& list, size_t n, int c, int W, uint32_t NB,
-                                              int fixed, size_t stride, uint32_t bi, size_t i, int w0, Fn fn) {
+__device__ __forceinline__ void scalar_digits(const MsmScalarList& list, int c, int W, uint32_t NB, int fixed,
+                                              size_t stride, uint32_t bi, size_t i, int w0, Fn fn) {
   const uint4* q = reinterpret_cast<const uint4*>(list.p[bi] + i);
   uint4 a = q[0], b = q[1];
   Fr s;
@@ -66,17 +63,11 @@ __device__ __forceinline__ void scalar_digits(const MsmScalarList& list, size_t 
       sign = 0;
     }
     if (w < w0 || mag == 0) continue;
-    uint32_t k = mag - 1;
-    if (list.kn) {  // bucket range: keep [klo, klo + kn), rebased
-      if (k - list.klo >= list.kn) continue;
-      k -= list.klo;
-    }
     const uint32_t koff = fixed ? bi * NB : (uint32_t)w * NB;
     const uint32_t val = (fixed ? (uint32_t)((size_t)w * stride + i) : (uint32_t)i) | sign;
-    fn(w - w0, koff + k, val);
+    fn(w - w0, koff + mag - 1, val);
   }
 }
-
 
 // round 1a: coarse histogram (LDS per block, one global atomic per bin and block)
 __global__ void __launch_bounds__(PT)
@@ -84,12 +75,7 @@ msm_coarse_hist_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, 
                        uint32_t ncoarse, uint32_t* __restrict__ ccount, MsmZero z) {
   __shared__ uint32_t h[COARSE_MAX];
   {  // the pipeline's other per-MSM zeroing (no separate fills)
-    const size_t nthr = (size_t)gridDim.x * gridDim.y * gridDim.z * PT;
     const size_t tid = (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * PT + threadIdx.x;
-    for (size_t i = tid; i < z.nb; i += nthr) {
-      z.bstart[i] = 0;
-      z.bend[i] = 0;
-    }
     if (tid < 2) z.counters[tid] = 0;
     if (tid < z.nrd) z.rdone[tid] = 0;
   }
@@ -97,16 +83,16 @@ msm_coarse_hist_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, 
   __syncthreads();
   const size_t i = blockIdx.x * (size_t)PT + threadIdx.x;
   if (i < n)
-    scalar_digits(list, n, c, W, NB, fixed, stride, blockIdx.y, i, blockIdx.z * PWG,
+    scalar_digits(list, c, W, NB, fixed, stride, blockIdx.y, i, blockIdx.z * PWG,
                   [&](int, uint32_t key, uint32_t) { atomicAdd(&h[key >> fb], 1u); });
   __syncthreads();
   for (uint32_t t = threadIdx.x; t < ncoarse; t += PT)
     if (h[t]) atomicAdd(&ccount[t], h[t]);
 }
 
-// exclusive scan of cnt[0, len) (one block, len <= 1024 * 64): off[] = cursor[] =
-// prefix; *total = sum; clear: cnt[] is zeroed after use (the counts start at zero for
-// the next MSM without a fill)
+// exclusive scan of cnt[0, len) (one block, len <= 1024 * 64): off[] (and cursor[] if
+// given) = prefix; *total = sum; clear: cnt[] is zeroed after use (the counts start at
+// zero for the next MSM without a fill)
 __global__ void __launch_bounds__(1024)
 msm_scan_kernel(uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__ off,
                 uint32_t* __restrict__ cursor, uint32_t* __restrict__ total, bool clear) {
@@ -153,10 +139,13 @@ msm_scan_block_kernel(uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __rest
   if (i < len) off[i] = part[threadIdx.x] - v0;
   if (threadIdx.x == 1023) bsum[blockIdx.x] = part[1023];
 }
+// off[i] += block offset (= koff, the first position of key i's run), cursor = the same;
+// off[len] = the entry count
 __global__ void __launch_bounds__(1024)
 msm_scan_add_kernel(uint32_t* __restrict__ off, uint32_t len, const uint32_t* __restrict__ boff,
-                    uint32_t* __restrict__ cursor) {
+                    uint32_t* __restrict__ cursor, const uint32_t* __restrict__ d_total) {
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  if (i == 0) off[len] = *d_total;
   if (i >= len) return;
   const uint32_t v = off[i] + boff[blockIdx.x];
   off[i] = v;
@@ -177,7 +166,7 @@ msm_coarse_scatter_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t N
   for (int k = 0; k < PWG; k++) rk[k] = ~0u;
   const size_t i = blockIdx.x * (size_t)PT + threadIdx.x;
   if (i < n)
-    scalar_digits(list, n, c, W, NB, fixed, stride, blockIdx.y, i, blockIdx.z * PWG,
+    scalar_digits(list, c, W, NB, fixed, stride, blockIdx.y, i, blockIdx.z * PWG,
                   [&](int slot, uint32_t key, uint32_t val) {
 #pragma unroll
                     for (int k = 0; k < PWG; k++)
@@ -195,24 +184,34 @@ msm_coarse_scatter_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t N
     if (rk[k] != ~0u) out[base[(uint32_t)(ent[k] >> 32) >> fb] + rk[k]] = ent[k];
 }
 
+// round 2's tile of block b: XCD x (= b mod 8, workgroups dispatch round-robin over the
+// XCDs) takes tiles [x T / 8, (x + 1) T / 8) in order, so a coarse bin's tiles -- and its
+// scattered output writes -- stay on one XCD
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t T) {
+  const uint32_t x = b & 7, q = b >> 3;
+  const uint32_t per = T >> 3, extra = T & 7;  // XCDs x < extra take per + 1 tiles
+  return x * per + (x < extra ? x : extra) + q;
+}
+
 // round 2a: per-key counts inside coarse bins: tiles of FTILE entries; entries of the
 // tile's first bin go through an LDS histogram, others (tiles straddling bins) directly
 __global__ void __launch_bounds__(FT)
-msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
+msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb, uint32_t tiles,
                      uint32_t* __restrict__ kcount) {
   __shared__ uint32_t h[1 << FB_MAX];
   const uint32_t total = *d_total;
-  const uint32_t lo = blockIdx.x * FTILE;
+  const uint32_t lo = xcd_tile(blockIdx.x, tiles) * FTILE;
   if (lo >= total) return;
+  const uint32_t* key32 = reinterpret_cast<const uint32_t*>(in) + 1;  // the keys (high words)
   const uint32_t nf = 1u << fb;
   for (uint32_t t = threadIdx.x; t < nf; t += FT) h[t] = 0;
-  const uint32_t bin0 = (uint32_t)(in[lo] >> 32) >> fb;
+  const uint32_t bin0 = key32[2 * (size_t)lo] >> fb;
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < FPER; k++) {
     const uint32_t p = lo + k * FT + threadIdx.x;
     if (p >= total) break;
-    const uint32_t key = (uint32_t)(in[p] >> 32);
+    const uint32_t key = key32[2 * (size_t)p];
     if ((key >> fb) == bin0) atomicAdd(&h[key & (nf - 1)], 1u);
     else atomicAdd(&kcount[key], 1u);
   }
@@ -221,13 +220,13 @@ msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict
     if (h[t]) atomicAdd(&kcount[(bin0 << fb) + t], h[t]);
 }
 
-// round 2b: the same tiles scattered to their keys' positions
+// round 2b: the same tiles scattered to their keys' positions (values only)
 __global__ void __launch_bounds__(FT)
 msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
-                        uint32_t* __restrict__ kcursor, uint64_t* __restrict__ out) {
+                        uint32_t tiles, uint32_t* __restrict__ kcursor, uint32_t* __restrict__ out) {
   __shared__ uint32_t cnt[1 << FB_MAX], base[1 << FB_MAX];
   const uint32_t total = *d_total;
-  const uint32_t lo = blockIdx.x * FTILE;
+  const uint32_t lo = xcd_tile(blockIdx.x, tiles) * FTILE;
   if (lo >= total) return;
   const uint32_t nf = 1u << fb;
   for (uint32_t t = threadIdx.x; t < nf; t += FT) cnt[t] = 0;
@@ -244,7 +243,7 @@ msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restr
       ent[k] = in[p];
       const uint32_t key = (uint32_t)(ent[k] >> 32);
       if ((key >> fb) == bin0) rk[k] = atomicAdd(&cnt[key & (nf - 1)], 1u);
-      else out[atomicAdd(&kcursor[key], 1u)] = ent[k];
+      else out[atomicAdd(&kcursor[key], 1u)] = (uint32_t)ent[k];
     }
   }
   __syncthreads();
@@ -253,16 +252,17 @@ msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restr
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < FPER; k++)
-    if (rk[k] != ~0u) out[base[(uint32_t)(ent[k] >> 32) & (nf - 1)] + rk[k]] = ent[k];
+    if (rk[k] != ~0u) out[base[(uint32_t)(ent[k] >> 32) & (nf - 1)] + rk[k]] = (uint32_t)ent[k];
 }
 
-// round 2, staged form: tiles of SW_T threads x SW_PER entries (8192) whose keys inside a
-// local window of SW_LK keys (the tile's first coarse bin and the next) are counted and
-// ranked in LDS, reserved with one global atomic per (tile, key), then written through an
-// LDS copy of the tile in key order -- so a wave's stores are runs of each key's share of
-// the tile (~8 entries at 10 fine bits) instead of 64 scattered 8-B writes, and the per-key
-// global atomics drop 4x with the larger tile.  Keys outside the window (tiles straddling
-// more than two bins: small bins) take a global atomic each, as in the unstaged kernels.
+// round 2, staged form (MSMs below 2^25 entries, the slabs of sharded proofs: 2^19
+// points 0.108 -> 0.084 ms, 2^21 0.356 -> 0.30 ms; at 2^22 no faster, 0.61 vs 0.60 ms):
+// tiles of SW_T threads x SW_PER entries (8192) whose keys inside a local window of SW_LK
+// keys (the tile's first coarse bin and the next) are counted and ranked in LDS, reserved
+// with one global atomic per (tile, key), then written through an LDS copy of the tile in
+// key order -- a wave's stores are runs of each key's share of the tile instead of 64
+// scattered writes, and the per-key global atomics drop 4x with the larger tile.  Keys
+// outside the window (tiles straddling more than two bins) take a global atomic each.
 static constexpr int SW_T = 512;
 static constexpr int SW_PER = 16;
 static constexpr uint32_t SW_TILE = (uint32_t)SW_T * SW_PER;
@@ -293,19 +293,20 @@ __device__ __forceinline__ uint32_t sw_block_scan(uint32_t v, uint32_t* wsum, ui
 
 __global__ void __launch_bounds__(SW_T)
 msm_fine_hist_staged_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
-                            uint32_t* __restrict__ kcount) {
+                            uint32_t tiles, uint32_t* __restrict__ kcount) {
   __shared__ uint32_t h[SW_LK];
   const uint32_t total = *d_total;
-  const uint32_t lo = blockIdx.x * SW_TILE;
+  const uint32_t lo = xcd_tile(blockIdx.x, tiles) * SW_TILE;
   if (lo >= total) return;
-  const uint32_t kbase = ((uint32_t)(in[lo] >> 32) >> fb) << fb;
+  const uint32_t* key32 = reinterpret_cast<const uint32_t*>(in) + 1;
+  const uint32_t kbase = (key32[2 * (size_t)lo] >> fb) << fb;
   for (uint32_t t = threadIdx.x; t < SW_LK; t += SW_T) h[t] = 0;
   __syncthreads();
 #pragma unroll 4
   for (int k = 0; k < SW_PER; k++) {
     const uint32_t p = lo + k * SW_T + threadIdx.x;
     if (p >= total) break;
-    const uint32_t key = (uint32_t)(in[p] >> 32);
+    const uint32_t key = key32[2 * (size_t)p];
     if (key - kbase < SW_LK) atomicAdd(&h[key - kbase], 1u);
     else atomicAdd(&kcount[key], 1u);
   }
@@ -316,12 +317,12 @@ msm_fine_hist_staged_kernel(const uint64_t* __restrict__ in, const uint32_t* __r
 
 __global__ void __launch_bounds__(SW_T)
 msm_fine_scatter_staged_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
-                               uint32_t* __restrict__ kcursor, uint64_t* __restrict__ out) {
+                               uint32_t tiles, uint32_t* __restrict__ kcursor, uint32_t* __restrict__ out) {
   __shared__ uint64_t stage[SW_TILE];
   __shared__ uint32_t cnt[SW_LK], loff[SW_LK], gb[SW_LK];
   __shared__ uint32_t wsum[SW_T / 64];
   const uint32_t total = *d_total;
-  const uint32_t lo = blockIdx.x * SW_TILE;
+  const uint32_t lo = xcd_tile(blockIdx.x, tiles) * SW_TILE;
   if (lo >= total) return;
   const uint32_t kbase = ((uint32_t)(in[lo] >> 32) >> fb) << fb;
   for (uint32_t t = threadIdx.x; t < SW_LK; t += SW_T) cnt[t] = 0;
@@ -337,7 +338,7 @@ msm_fine_scatter_staged_kernel(const uint64_t* __restrict__ in, const uint32_t* 
       ent[k] = in[p];
       const uint32_t key = (uint32_t)(ent[k] >> 32);
       if (key - kbase < SW_LK) rk[k] = atomicAdd(&cnt[key - kbase], 1u);
-      else out[atomicAdd(&kcursor[key], 1u)] = ent[k];
+      else out[atomicAdd(&kcursor[key], 1u)] = (uint32_t)ent[k];
     }
   }
   __syncthreads();
@@ -367,19 +368,12 @@ msm_fine_scatter_staged_kernel(const uint64_t* __restrict__ in, const uint32_t* 
   for (uint32_t j = threadIdx.x; j < m; j += SW_T) {
     const uint64_t e = stage[j];
     const uint32_t kk = (uint32_t)(e >> 32) - kbase;
-    out[gb[kk] + (j - loff[kk])] = e;
+    out[gb[kk] + (j - loff[kk])] = (uint32_t)e;
   }
 }
 
 hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* prof) {
-  // staged fine pass below 2^25 entries (MSMs up to 2^21 points: fine pass 0.108 -> 0.084 ms
-  // at 2^19, 0.356 -> 0.30 ms at 2^21); at 2^22 (54.5 M entries) it is no faster (0.61 vs
-  // 0.60 ms).  H2G_MSM_FSTAGE=0 / 1 forces it (A/B).
-  static const int fstage_env = [] {
-    const char* e = getenv("H2G_MSM_FSTAGE");
-    return e ? atoi(e) : -1;
-  }();
-  const bool fstage = fstage_env >= 0 ? fstage_env != 0 : a.total < (1ull << 25);
+  const bool fstage = a.total < (1ull << 25);  // the staged fine pass (above)
   {  // round 1: coarse bins straight from the scalars
     const dim3 g((unsigned)((a.n + PT - 1) / PT), (unsigned)a.nbatch, (unsigned)((a.W + PWG - 1) / PWG));
     hipLaunchKernelGGL(msm_coarse_hist_kernel, g, dim3(PT), 0, st, a.list, a.n, a.c, a.W, a.NB, a.fixed, a.stride,
@@ -387,7 +381,7 @@ hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* p
     hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, a.ccount, a.ncoarse, a.coff, a.ccursor,
                        a.d_total, true);
     hipLaunchKernelGGL(msm_coarse_scatter_kernel, g, dim3(PT), 0, st, a.list, a.n, a.c, a.W, a.NB, a.fixed, a.stride,
-                       a.fb, a.ncoarse, a.ccursor, a.keys_in);
+                       a.fb, a.ncoarse, a.ccursor, a.ent);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
@@ -400,22 +394,22 @@ hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* p
     const unsigned tiles = (unsigned)((a.total + FTILE - 1) / FTILE);
     const unsigned stiles = (unsigned)((a.total + SW_TILE - 1) / SW_TILE);
     if (fstage)
-      hipLaunchKernelGGL(msm_fine_hist_staged_kernel, dim3(stiles), dim3(SW_T), 0, st, (const uint64_t*)a.keys_in,
-                         (const uint32_t*)a.d_total, a.fb, a.kcount);
+      hipLaunchKernelGGL(msm_fine_hist_staged_kernel, dim3(stiles), dim3(SW_T), 0, st, (const uint64_t*)a.ent,
+                         (const uint32_t*)a.d_total, a.fb, stiles, a.kcount);
     else
-      hipLaunchKernelGGL(msm_fine_hist_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)a.keys_in,
-                         (const uint32_t*)a.d_total, a.fb, a.kcount);
+      hipLaunchKernelGGL(msm_fine_hist_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)a.ent,
+                         (const uint32_t*)a.d_total, a.fb, tiles, a.kcount);
     hipLaunchKernelGGL(msm_scan_block_kernel, dim3(a.kblocks), dim3(1024), 0, st, a.kcount, a.nbt, a.koff, a.kbsum);
     hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, a.kbsum, a.kblocks, a.kboff, (uint32_t*)nullptr,
                        (uint32_t*)nullptr, false);
     hipLaunchKernelGGL(msm_scan_add_kernel, dim3(a.kblocks), dim3(1024), 0, st, a.koff, a.nbt,
-                       (const uint32_t*)a.kboff, a.kcursor);
+                       (const uint32_t*)a.kboff, a.kcursor, (const uint32_t*)a.d_total);
     if (fstage)
-      hipLaunchKernelGGL(msm_fine_scatter_staged_kernel, dim3(stiles), dim3(SW_T), 0, st, (const uint64_t*)a.keys_in,
-                         (const uint32_t*)a.d_total, a.fb, a.kcursor, a.keys_out);
+      hipLaunchKernelGGL(msm_fine_scatter_staged_kernel, dim3(stiles), dim3(SW_T), 0, st, (const uint64_t*)a.ent,
+                         (const uint32_t*)a.d_total, a.fb, stiles, a.kcursor, a.out);
     else
-      hipLaunchKernelGGL(msm_fine_scatter_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)a.keys_in,
-                         (const uint32_t*)a.d_total, a.fb, a.kcursor, a.keys_out);
+      hipLaunchKernelGGL(msm_fine_scatter_kernel, dim3(tiles), dim3(FT), 0, st, (const uint64_t*)a.ent,
+                         (const uint32_t*)a.d_total, a.fb, tiles, a.kcursor, a.out);
   }
   return hipGetLastError();
 }

@@ -325,16 +325,24 @@ uint64_t g_shard_seq = 0;
 // SPMD sharding (h2g_set_spmd_transport): every rank proves, rank r computes slab r
 h2g_spmd_transport g_spmd{nullptr, 1, 0, nullptr, nullptr};
 uint64_t g_spmd_seq = 0;
-// the running proof's transcript and RNG, whose digest travels with every SPMD partial
-// (H2G_SPMD_WORDS): ranks that diverged fail the proof instead of summing slabs of
-// different polynomials
+// the running proof's transcript, RNG draws and witness, whose digest travels with every
+// SPMD partial (H2G_SPMD_WORDS): ranks that diverged fail the proof instead of summing
+// slabs of different polynomials.  The witness enters as every advice column's value at
+// a fixed point, evaluated over the whole column by each rank (spmd_witness_fold): with
+// the slabs summed, the commitments and evaluations alone would be the same on ranks fed
+// different witnesses.
 struct SpmdCheck {
   const Transcript* tr = nullptr;
   const ProverRng* rng = nullptr;
+  uint8_t wit[64] = {};
 };
 SpmdCheck g_spmd_check;
 struct SpmdCheckScope {
-  SpmdCheckScope(const Transcript* tr, const ProverRng* rng) { g_spmd_check = SpmdCheck{tr, rng}; }
+  SpmdCheckScope(const Transcript* tr, const ProverRng* rng) {
+    g_spmd_check = SpmdCheck{};
+    g_spmd_check.tr = tr;
+    g_spmd_check.rng = rng;
+  }
   ~SpmdCheckScope() { g_spmd_check = SpmdCheck{}; }
 };
 void spmd_digest(uint64_t out[4]) {
@@ -344,6 +352,7 @@ void spmd_digest(uint64_t out[4]) {
   Blake2b h("h2g-spmd-check\0\0");
   h.update(a, 64);
   h.update(b, 64);
+  h.update(g_spmd_check.wit, 64);
   h.digest(d);
   std::memcpy(out, d, 32);
 }
@@ -439,11 +448,11 @@ int commit_collect(Device* d, MsmTicket* t, G1Affine* out) {
 // keccak-style k = 18 proof (80 MSMs of 2^18) 127 -> 101 ms, while C3 at k = 22 (MSMs
 // of 2^22, 13 x 2^22 entries each) is 0.6 ms better without -- so only MSMs of at most
 // 2^25 sorted entries are batched, up to 2^27 entries per batch.
+#ifndef H2G_MSM_BATCH_ENTRIES  // A/B builds (tools/build_variant.py --src prover.cpp -D...)
+#define H2G_MSM_BATCH_ENTRIES (1ull << 27)
+#endif
 int commit_batch_chunk(const MsmFixedBase& tb, size_t n) {
-  static const uint64_t max_entries = [] {
-    const char* e = std::getenv("H2G_MSM_BATCH_ENTRIES");
-    return e ? std::strtoull(e, nullptr, 0) : (1ull << 27);
-  }();
+  const uint64_t max_entries = H2G_MSM_BATCH_ENTRIES;
   if (g_shard.world > 1) return 1;
   const uint64_t per = (uint64_t)tb.W * (n ? n : 1);
   if (per > (1ull << 25)) return 1;
@@ -1439,6 +1448,39 @@ struct PolyRef {  // a committed polynomial in coefficient form (SHPLONK's "comm
   uint64_t len;
 };
 
+// SPMD: fold the columns' values at a fixed point (full length, this rank's copy) into
+// the consistency digest -- one batched evaluation and a host sync per advice phase, only
+// when sharded
+int spmd_witness_fold(ProvingKey& pk, const std::vector<const Fr*>& cols, size_t n, hipStream_t st) {
+  if (g_spmd.world <= 1 || cols.empty()) return H2G_OK;
+  static const uint64_t kPoint[4] = {0x9e3779b97f4a7c15ull, 0xf39cc0605cedc834ull, 0x1082276bf3a27251ull,
+                                     0x0b5026f5aa96619eull};
+  const Fr x = fr_from_limbs(kPoint);
+  const int np = (int)cols.size();
+  std::vector<EvalReq> reqs(np);
+  for (int i = 0; i < np; i++) reqs[i] = EvalReq{cols[i], (uint64_t)n, x};
+  if (np > pk.max_reqs) {
+    PALLOC(pk.pool, pk.d_reqs, np);
+    PALLOC(pk.pool, pk.evals, np);
+    pk.max_reqs = np;
+  }
+  const size_t need = poly_eval_scratch_len(np, n);
+  if (need > pk.eval_scr_len) {
+    PALLOC(pk.pool, pk.eval_scr, need);
+    pk.eval_scr_len = need;
+  }
+  std::vector<Fr> ev(np);
+  HIPCHK(hipMemcpyAsync(pk.d_reqs, reqs.data(), np * sizeof(EvalReq), hipMemcpyHostToDevice, st));
+  HIPCHK(poly_eval_batch(pk.d_reqs, np, n, pk.evals, pk.eval_scr, st));
+  HIPCHK(hipMemcpyAsync(ev.data(), pk.evals, np * sizeof(Fr), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  Blake2b h("h2g-spmd-witness");
+  h.update(g_spmd_check.wit, 64);
+  h.update(reinterpret_cast<const uint8_t*>(ev.data()), ev.size() * sizeof(Fr));
+  h.digest(g_spmd_check.wit);
+  return H2G_OK;
+}
+
 std::vector<Fr> g_last_challenges;  // the challenges of the last proof (h2g_last_challenges)
 
 // create_proof's inputs (halo2_proofs/src/plonk/prover.rs:19-36): per circuit the witness
@@ -1524,12 +1566,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   StreamSyncGuard adv_guard{st};
   // the vanishing argument's seeds and chunk offsets (staging read by async copies: lives
   // until the proof returns), its commitment's ticket, and whether it was launched early
-  // H2G_EARLY_VANISHING (A/B): 0 = at its place in the transcript only, 1 = queued behind
-  // phase 0's advice MSMs (default), 2 = once the advice commitments are collected
-  static const int early_env = [] {
-    const char* e = std::getenv("H2G_EARLY_VANISHING");
-    return e ? std::atoi(e) : 1;
-  }();
+  // (queued behind phase 0's advice MSMs; placed after the advice commitments instead it
+  // measured slower, profiles/r03/s3/ab_early_vanishing)
   std::vector<uint64_t> van_off;
   std::vector<uint32_t> van_seeds;
   StreamSyncGuard van_guard{st};  // destroyed before the staging above: the copies finish first
@@ -1547,8 +1585,20 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   }
   MsmTicket van_tk;
   bool van_early = false;
-  const bool early_van = early_env != 0 && rng.seeded() && pk.van_pos >= 0 &&
-                         pk.van_T == (uint32_t)van_off.size() && g_spmd.world <= 1 && g_shard.world <= 1;
+  // it holds an MSM ring slot from phase 0 until y: only when every later stage's
+  // outstanding commitments still fit beside it (advice phases, the permuted lookup
+  // columns, the permutation / lookup / shuffle products)
+  int peak_msms = 0;
+  for (int ph = 0; ph <= pk.max_phase; ph++) {
+    int a = 0;
+    for (int c = 0; c < pk.A; c++) a += pk.adv_phase[c] == ph;
+    peak_msms = std::max(peak_msms, a * ncirc);
+  }
+  peak_msms = std::max(peak_msms, 2 * ncirc * pk.NL);
+  peak_msms = std::max(peak_msms, ncirc * (pk.nsets + pk.NL + pk.NS));
+  const bool early_van = rng.seeded() && pk.van_pos >= 0 &&
+                         pk.van_T == (uint32_t)van_off.size() && g_spmd.world <= 1 && g_shard.world <= 1 &&
+                         peak_msms + 1 <= MSM_RING;
   auto launch_van_early = [&]() -> int {
     // the vanishing argument's random polynomial does not depend on the witness: with the
     // seeded RNG its seeds are the keystream bytes at the position the last proof drew
@@ -1632,7 +1682,13 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       RCCHK(lagrange_to_coeff_batch(d, D, src.data(), dst.data(), (int)cols.size(), st));
       RCCHK(ext_cosets(d, pk, (const Fr* const*)dst.data(), cst.data(), (int)cols.size(), st));
     }
-    if (ph == 0 && early_van && early_env == 1) RCCHK(launch_van_early());
+    if (g_spmd.world > 1) {  // this phase's witness into the consistency digest
+      std::vector<const Fr*> wc;
+      for (int ci = 0; ci < ncirc; ci++)
+        for (int c : cols) wc.push_back(W[ci]->adv[c]);
+      RCCHK(spmd_witness_fold(pk, wc, n, st));
+    }
+    if (ph == 0 && early_van) RCCHK(launch_van_early());
     if (ph == 0) clk.mark("upload+instances");
     for (auto& t : tk) {  // circuit by circuit, column by column
       G1Affine cm;
@@ -1647,7 +1703,6 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     HIPCHK(hipMemcpyAsync(pk.consts + pk.num_consts, challenges.data(), NCH * sizeof(Fr), hipMemcpyHostToDevice, st));
   g_last_challenges = challenges;
   clk.mark("advice commit");
-  if (early_van && early_env == 2) RCCHK(launch_van_early());
 
   const Fr theta = tr.squeeze();
   auto compress = [&](const CircuitWs& w, int2 seg, Fr* out) -> int {

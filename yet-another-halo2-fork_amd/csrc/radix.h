@@ -10,7 +10,7 @@
 
 namespace h2g {
 
-// exclusive scan of len u32 (len <= 2^24); scratch >= scan_u32_scratch_bytes(len)
+// exclusive scan of len u32 (len < 2^32, in == out allowed); scratch >= scan_u32_scratch_bytes(len)
 size_t scan_u32_scratch_bytes(size_t len);
 hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t len, void* scratch, hipStream_t st);
 

@@ -85,8 +85,9 @@ __global__ void __launch_bounds__(RX_T) radix_scatter_kernel(const uint64_t* __r
   }
 }
 
-// exclusive scan of u32: 4096-element blocks (1024 threads x 4), block sums scanned by one
-// block (<= 4096 blocks), added back
+// exclusive scan of u32: 4096-element blocks (1024 threads x 4); the block sums are
+// scanned by one block when they fit (<= 4096 blocks, len <= 2^24), else by the same
+// routine recursively; then added back
 static constexpr uint32_t SC_T = 1024, SC_PER = 4, SC_BLK = SC_T * SC_PER;
 
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
@@ -105,8 +106,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, ui
   return incl - v;
 }
 
-__global__ void __launch_bounds__(SC_T) scan_blocks_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                          uint32_t len, uint32_t* __restrict__ bsum) {
+// in and out may alias (each thread reads its elements before the block scan's barriers)
+__global__ void __launch_bounds__(SC_T) scan_blocks_kernel(const uint32_t* in, uint32_t* out, uint32_t len,
+                                                          uint32_t* __restrict__ bsum) {
   __shared__ uint32_t sh[SC_T];
   const uint32_t lo = blockIdx.x * SC_BLK + threadIdx.x * SC_PER;
   uint32_t v[SC_PER], s = 0;
@@ -152,15 +154,24 @@ __global__ void __launch_bounds__(SC_T) scan_add_kernel(uint32_t* __restrict__ o
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-size_t scan_u32_scratch_bytes(size_t len) { return align256(((len + SC_BLK - 1) / SC_BLK + 1) * 4); }
+size_t scan_u32_scratch_bytes(size_t len) {
+  const size_t nb = (len + SC_BLK - 1) / SC_BLK;
+  return align256((nb + 1) * 4) + (nb > SC_BLK ? scan_u32_scratch_bytes(nb) : 0);
+}
 
 hipError_t exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t len, void* scratch, hipStream_t st) {
   if (len == 0) return hipSuccess;
+  if (len >= 0xffffffffull) return hipErrorInvalidValue;
   const uint32_t nb = (uint32_t)((len + SC_BLK - 1) / SC_BLK);
-  if (nb > SC_BLK) return hipErrorInvalidValue;
   uint32_t* bsum = static_cast<uint32_t*>(scratch);
   hipLaunchKernelGGL(scan_blocks_kernel, dim3(nb), dim3(SC_T), 0, st, in, out, (uint32_t)len, bsum);
-  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(SC_T), 0, st, bsum, nb);
+  if (nb <= SC_BLK) {
+    hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(SC_T), 0, st, bsum, nb);
+  } else {  // more than 4096 blocks: the block sums in place, recursively
+    const hipError_t e =
+        exclusive_scan_u32(bsum, bsum, nb, static_cast<char*>(scratch) + align256(((size_t)nb + 1) * 4), st);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(scan_add_kernel, dim3(nb), dim3(SC_T), 0, st, out, (uint32_t)len, (const uint32_t*)bsum);
   return hipGetLastError();
 }

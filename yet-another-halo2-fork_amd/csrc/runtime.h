@@ -86,12 +86,11 @@ struct Descriptor {
 
 // Asynchronous fixed-base MSMs: whole MSMs on two streams with a workspace each, so that
 // one MSM's latency-bound phases (partition tail, fixup, reduction) overlap another's
-// accumulation.  H2G_MSM_PIPE=1 (A/B, measured slower): pipelined by stage instead -- every
-// MSM's bucket partition on mstream[0], its accumulation on mstream[1], its fixup and
-// reduction on mstream[2], MSM_SLOTS workspaces rotating.  Results land in a pinned ring
-// (one XYZZ point each).
-static constexpr int MSM_SLOTS = 3;
-static constexpr int MSM_STREAMS = 3;
+// accumulation.  (Pipelining by stage instead -- partitions, accumulations and reductions
+// on three streams -- measured slower: a partition beside an accumulation gets CUs only
+// as the accumulation's blocks retire; profiles/r03/s3/ab_msm_pipe.)  Results land in a
+// pinned ring (one XYZZ point each).
+static constexpr int MSM_STREAMS = 2;
 static constexpr int MSM_RING = 64;
 struct MsmTicket {
   int slot = -1;
@@ -109,10 +108,8 @@ struct Device {
   std::map<NttKey, NttTables> ntt_tables;
   void* h_windows = nullptr;  // pinned host copy of MSM window sums
   // async MSM slots
-  MsmWorkspace mws[MSM_SLOTS];
+  MsmWorkspace mws[MSM_STREAMS];
   hipStream_t mstream[MSM_STREAMS] = {};
-  hipEvent_t mev_p2a[MSM_SLOTS] = {}, mev_a2r[MSM_SLOTS] = {}, mev_free[MSM_SLOTS] = {};
-  bool mws_used[MSM_SLOTS] = {};
   int next_slot = 0;
   void* h_ring = nullptr;  // pinned G1xyzz[MSM_RING]
   hipEvent_t ring_ev[MSM_RING] = {};
@@ -147,7 +144,7 @@ int msm_dev_impl(Device* d, const void* sc, const void* bs, size_t n, int c, voi
 int msm_host_impl(Device* d, const void* sc, const void* bs, size_t n, int c, uint64_t* out, int* is_id,
                   hipStream_t st);
 int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, uint64_t* out,
-                        int* is_id, hipStream_t st, const MsmBucketRange* br = nullptr);
+                        int* is_id, hipStream_t st);
 // launch sum_{i<n} sc[i] * bases[off+i] after the work already queued on `producer`
 int msm_fixed_launch(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, hipStream_t producer,
                      MsmTicket* t);

@@ -39,8 +39,6 @@ _SIGS = {
     "h2g_msm_descriptor_free": ([U64], I32),
     "h2g_msm_base_descriptor_dev": ([VP, SZ, I32, ctypes.POINTER(U64)], I32),
     "h2g_msm_with_cached_base_dev": ([VP, SZ, U64, SZ, U64P, ctypes.POINTER(I32), VP], I32),
-    "h2g_msm_with_cached_base_dev_shard": ([VP, SZ, U64, SZ, I32, I32, U64P, ctypes.POINTER(I32),
-                                            ctypes.POINTER(U32), ctypes.POINTER(U32), VP], I32),
     "h2g_msm_with_cached_scalars": ([U64, U64P, SZ, U64P, ctypes.POINTER(I32)], I32),
     "h2g_msm_with_cached_base": ([U64P, SZ, U64, SZ, U64P, ctypes.POINTER(I32)], I32),
     "h2g_msm_with_cached_inputs": ([U64, U64, SZ, U64P, ctypes.POINTER(I32)], I32),
@@ -68,6 +66,7 @@ _SIGS = {
     "h2g_fr_batch_invert_dev": ([VP, SZ, VP], I32),
     "h2g_fr_prefix_product": ([U64P, U64P, SZ], I32),
     "h2g_fr_prefix_product_dev": ([VP, VP, SZ, VP], I32),
+    "h2g_u32_exclusive_scan_dev": ([VP, VP, SZ, VP], I32),
     "h2g_dev_alloc": ([SZ, ctypes.POINTER(VP)], I32),
     "h2g_dev_free": ([VP], I32),
     "h2g_memcpy_htod": ([VP, VP, SZ], I32),
@@ -224,18 +223,6 @@ def msm_with_cached_base_dev(d_scalars, n, base_handle, offset=0, stream=None):
     check(lib().h2g_msm_with_cached_base_dev(VP(d_scalars), n, base_handle, offset, p64(out), ctypes.byref(is_id),
                                              VP(stream) if stream else None))
     return out
-
-
-def msm_with_cached_base_dev_shard(d_scalars, n, base_handle, world, rank, offset=0, stream=None):
-    """rank's bucket-range part of the MSM (the parts of ranks 0..world-1 add up to it)
-    -> (affine uint64[8], is_identity, (bucket_lo, bucket_hi))"""
-    out = np.zeros(8, dtype=np.uint64)
-    is_id = I32()
-    lo, hi = U32(), U32()
-    check(lib().h2g_msm_with_cached_base_dev_shard(VP(d_scalars), n, base_handle, offset, world, rank, p64(out),
-                                                   ctypes.byref(is_id), ctypes.byref(lo), ctypes.byref(hi),
-                                                   VP(stream) if stream else None))
-    return out, bool(is_id.value), (lo.value, hi.value)
 
 
 def descriptor_free(h):
@@ -398,6 +385,11 @@ def batch_invert(a):
     a = np.ascontiguousarray(a, dtype=np.uint64).copy()
     check(lib().h2g_fr_batch_invert(p64(a), a.shape[0]))
     return a
+
+
+def u32_exclusive_scan_dev(d_in, d_out, n, stream=None):
+    """exclusive prefix sum of n u32 on the device (in place when d_in == d_out)"""
+    check(lib().h2g_u32_exclusive_scan_dev(VP(d_in), VP(d_out), n, VP(stream) if stream else None))
 
 
 def prefix_product(a):

@@ -213,6 +213,27 @@ class SlabWorker:
             count += 1
 
 
+def host_all_to_all(dist, group, rank, world, sb, send_bytes, rb, recv_bytes):
+    """all-to-all of host byte tensors by point-to-point messages (gloo): peer p's bytes are
+    contiguous in peer order in sb / rb; `rank` and p index the group's members, while
+    P2POp takes the peer's global rank"""
+    so = [sum(send_bytes[:p]) for p in range(world)]
+    ro = [sum(recv_bytes[:p]) for p in range(world)]
+    ops = []
+    for p in range(world):
+        if p == rank:
+            rb[ro[p]:ro[p] + recv_bytes[p]] = sb[so[p]:so[p] + send_bytes[p]]
+            continue
+        peer = p if group is None else dist.get_global_rank(group, p)
+        if send_bytes[p]:
+            ops.append(dist.P2POp(dist.isend, sb[so[p]:so[p] + send_bytes[p]], peer, group))
+        if recv_bytes[p]:
+            ops.append(dist.P2POp(dist.irecv, rb[ro[p]:ro[p] + recv_bytes[p]], peer, group))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+
 class SpmdGather:
     """SPMD sharding over torch.distributed (h2g_set_spmd_transport): every rank runs the
     same create_proof and computes point slab `rank` of each commitment MSM; the 9-word
@@ -278,8 +299,6 @@ class SpmdGather:
         import h2g
         import torch
         W = self.world
-        so = [sum(send_bytes[:p]) for p in range(W)]
-        ro = [sum(recv_bytes[:p]) for p in range(W)]
         tot_s, tot_r = sum(send_bytes), sum(recv_bytes)
         if self.device.type == "cuda":
             sb = torch.empty(max(tot_s, 1), dtype=torch.uint8, device="cuda")
@@ -295,18 +314,7 @@ class SpmdGather:
             rb = torch.empty(max(tot_r, 1), dtype=torch.uint8)
             if tot_s:
                 h2g.memcpy_dtoh(sb.data_ptr(), d_send, tot_s)
-            ops = []
-            for p in range(W):
-                if p == self.rank:
-                    rb[ro[p]:ro[p] + recv_bytes[p]] = sb[so[p]:so[p] + send_bytes[p]]
-                    continue
-                if send_bytes[p]:
-                    ops.append(self.dist.P2POp(self.dist.isend, sb[so[p]:so[p] + send_bytes[p]], p, self.group))
-                if recv_bytes[p]:
-                    ops.append(self.dist.P2POp(self.dist.irecv, rb[ro[p]:ro[p] + recv_bytes[p]], p, self.group))
-            if ops:
-                for w in self.dist.batch_isend_irecv(ops):
-                    w.wait()
+            host_all_to_all(self.dist, self.group, self.rank, W, sb, send_bytes, rb, recv_bytes)
             if tot_r:
                 h2g.memcpy_htod(d_recv, rb.data_ptr(), tot_r)
         self.exchanges += 1
