@@ -443,6 +443,15 @@ int h2g_set_spmd_transport(const h2g_spmd_transport* t);
  * ranks that own extended-domain sub-cosets carry that extra work; smaller slabs balance
  * them against the others.  NULL (or world <= 1) restores the uniform partition. */
 int h2g_spmd_set_weights(const uint32_t* weights, int world);
+/* SPMD column ownership of wide stages (on by default; used with bcast, allgather_host and
+ * exchange installed): an advice phase, the lookups' permuted columns or their products
+ * with as many columns as ranks or more (a multiple of the ranks, or 4x them) go to the
+ * ranks whole, column i to rank i mod world -- the owner commits it (its rank's partial is
+ * the whole commitment, the others' the identity), forms its coefficients and its
+ * sub-cosets, and one exchange per stage hands every sub-coset owner its sub-cosets and
+ * every rank its coefficient slab; a lookup's sort, match and product run on its owner
+ * only.  Stages with fewer columns keep the point slabs.  0 turns it off. */
+int h2g_spmd_set_column_owners(int on);
 /* split_subcosets: 1 divides the extended domain's sub-cosets over the ranks (bcast over
  * the communicator), 0 replicates that work; the multi-open tail always runs on
  * coefficient slabs (allgather_host over the communicator) */

@@ -357,6 +357,9 @@ void spmd_digest(uint64_t out[4]) {
   std::memcpy(out, d, 32);
 }
 
+// SPMD column ownership of wide stages (h2g_spmd_set_column_owners; on by default)
+bool g_spmd_colshard = true;
+
 // SPMD slab weights (h2g_spmd_set_weights): prefix sums, world + 1 entries; empty = uniform
 std::vector<uint64_t> g_spmd_wprefix;
 
@@ -395,7 +398,12 @@ int commit_launch(Device* d, const Params& prm, const Fr* scalars, size_t n, int
   return H2G_OK;
 }
 int commit_collect(Device* d, MsmTicket* t, G1Affine* out) {
-  RCCHK(msm_collect(d, t, reinterpret_cast<uint64_t*>(out)));
+  if (t->remote) {  // owned by another rank: this rank's part of the sum is the identity
+    std::memset(out, 0, sizeof(G1Affine));
+    t->remote = false;
+  } else {
+    RCCHK(msm_collect(d, t, reinterpret_cast<uint64_t*>(out)));
+  }
   if (t->shard_seq < 0) return H2G_OK;
   if (g_spmd.world > 1) {  // every rank's partial, summed in rank order (the same on every rank)
     const int W = g_spmd.world;
@@ -492,6 +500,38 @@ int commit_launch_batch(Device* d, const Params& prm, const Fr* const* scalars, 
     RCCHK(msm_fixed_launch_batch(d, reinterpret_cast<const void* const*>(sl), m, tb, toff, hi - lo, st, t + b0));
     // SPMD: every rank issues the same MSMs in the same order, so the sequence numbers agree
     for (int b = 0; b < m; b++) t[b0 + b].shard_seq = g_spmd.world > 1 ? (int64_t)g_spmd_seq++ : -1;
+  }
+  return H2G_OK;
+}
+
+// SPMD column ownership (wide stages): commitment i of the list is computed whole by rank
+// owner[i] (its own ones batched, against the full windows), every other rank contributes
+// the identity to its all-gather -- the sum is the owner's commitment, and the transcript
+// and the sequence numbers stay the same on every rank.
+int commit_launch_owned(Device* d, const Params& prm, const Fr* const* scalars, const int* owner, int nb, size_t n,
+                        int set, hipStream_t st, MsmTicket* t) {
+  std::vector<const Fr*> mine;
+  std::vector<int> at;
+  for (int i = 0; i < nb; i++)
+    if (owner[i] == g_spmd.rank) {
+      mine.push_back(scalars[i]);
+      at.push_back(i);
+    }
+  const MsmFixedBase& tb = set == SRS_G ? prm.fg : prm.fgl;
+  const int chunk = std::max(1, commit_batch_chunk(tb, n));
+  std::vector<MsmTicket> got(mine.size());
+  for (size_t b0 = 0; b0 < mine.size(); b0 += (size_t)chunk) {
+    const int m = (int)std::min<size_t>((size_t)chunk, mine.size() - b0);
+    RCCHK(msm_fixed_launch_batch(d, reinterpret_cast<const void* const*>(mine.data() + b0), m, tb, 0, n, st,
+                                 got.data() + b0));
+  }
+  for (size_t q = 0; q < at.size(); q++) t[at[q]] = got[q];
+  for (int i = 0; i < nb; i++) {
+    if (owner[i] != g_spmd.rank) {
+      t[i] = MsmTicket{};
+      t[i].remote = true;
+    }
+    t[i].shard_seq = (int64_t)g_spmd_seq++;
   }
   return H2G_OK;
 }
@@ -1124,6 +1164,121 @@ int coef_exchange(ProvingKey& pk, const std::vector<Fr*>& cols, hipStream_t st) 
   return H2G_OK;
 }
 
+// SPMD column ownership of a wide stage (as many columns as ranks or more: the advice of a
+// phase, the lookups' permuted columns and products -- SURVEY 8e's round-robin whole
+// columns): column i belongs to rank owner[i], which alone forms its coefficients (the
+// n-point iNTT, prover.rs:673-689 / lookup/prover.rs:131,311) and its E = 2^e sub-cosets
+// (n-point NTTs of the twisted coefficients, the cosets of evaluation.rs:344-361), each
+// written straight into its own slot when it owns that sub-coset or else into the send
+// buffer.  One all-to-all then hands sub-coset t of every column to its owner (rank t mod
+// world, slot (t - rank) / world) and every rank its coefficient slab [lo, hi1) (what the
+// evaluations and SHPLONK read).  Message from o to r: per column of o in index order, the
+// sub-cosets r owns (increasing t, n each), then r's coefficient slab.
+int colshard_distribute(Device* d, ProvingKey& pk, const std::vector<const Fr*>& lag, const std::vector<Fr*>& poly,
+                        const std::vector<Fr*>& coset, const std::vector<int>& owner, hipStream_t st) {
+  const size_t n = pk.n;
+  const int W = g_spmd.world, me = g_spmd.rank;
+  const int E = 1 << (pk.dom.ek - pk.dom.k);
+  const int M = (int)lag.size();
+  std::vector<Slab> slabs(W);
+  for (int r = 0; r < W; r++) slabs[r] = spmd_slab(n, r);
+  auto owned_subs = [&](int r) {  // sub-cosets rank r owns
+    int c = 0;
+    for (int t = r; t < E; t += W) c++;
+    return c;
+  };
+  auto msg_words = [&](int o, int r) {  // Fr from rank o to rank r
+    size_t w = 0;
+    for (int i = 0; i < M; i++)
+      if (owner[i] == o) w += (size_t)owned_subs(r) * n + (slabs[r].hi1 - slabs[r].lo);
+    return w;
+  };
+  std::vector<size_t> sb(W, 0), rb(W, 0), soff(W + 1, 0);
+  for (int r = 0; r < W; r++) {
+    sb[r] = r == me ? 0 : msg_words(me, r) * sizeof(Fr);
+    rb[r] = r == me ? 0 : msg_words(r, me) * sizeof(Fr);
+    soff[r + 1] = soff[r] + sb[r] / sizeof(Fr);
+  }
+  size_t rtot = 0;
+  for (int r = 0; r < W; r++) rtot += rb[r] / sizeof(Fr);
+  if (soff[W] > pk.x_send_len) {
+    PALLOC(pk.pool, pk.x_send, soff[W]);
+    pk.x_send_len = soff[W];
+  }
+  if (rtot > pk.x_recv_len) {
+    PALLOC(pk.pool, pk.x_recv, rtot);
+    pk.x_recv_len = rtot;
+  }
+  // this rank's columns: coefficients, then every sub-coset (own slot or send buffer) and
+  // the others' coefficient slabs
+  std::vector<const Fr*> my_lag;
+  std::vector<Fr*> my_poly;
+  for (int i = 0; i < M; i++)
+    if (owner[i] == me) {
+      my_lag.push_back(lag[i]);
+      my_poly.push_back(poly[i]);
+    }
+  if (!my_lag.empty()) RCCHK(lagrange_to_coeff_batch(d, pk.dom, my_lag.data(), my_poly.data(), (int)my_lag.size(), st));
+  std::vector<size_t> pos(W);
+  for (int r = 0; r < W; r++) pos[r] = soff[r];
+  std::vector<const Fr*> ntt_io;
+  for (int i = 0; i < M; i++) {
+    if (owner[i] != me) continue;
+    for (int r = 0; r < W; r++) {
+      if (r == me) {
+        for (int t = me; t < E; t += W) ntt_io.push_back(coset[i] + (size_t)((t - me) / W) * n);
+        continue;
+      }
+      for (int t = r; t < E; t += W) {
+        ntt_io.push_back(pk.x_send + pos[r]);
+        pos[r] += n;
+      }
+      const size_t cnt = slabs[r].hi1 - slabs[r].lo;
+      if (cnt)
+        HIPCHK(hipMemcpyAsync(pk.x_send + pos[r], poly[i] + slabs[r].lo, cnt * sizeof(Fr), hipMemcpyDeviceToDevice,
+                              st));
+      pos[r] += cnt;
+    }
+  }
+  {  // twists + n-point NTTs of every sub-coset formed here (ntt_io in the order above)
+    size_t q = 0;
+    for (int i = 0; i < M; i++) {
+      if (owner[i] != me) continue;
+      for (int r = 0; r < W; r++)
+        for (int t = r; t < E; t += W)
+          HIPCHK(subcoset_twist(poly[i], const_cast<Fr*>(ntt_io[q++]), n, pk.eo, (uint64_t)t, pk.ext - 1, st));
+    }
+    const Fr one = Fr::one();
+    std::vector<Fr*> io(ntt_io.size());
+    for (size_t j = 0; j < io.size(); j++) io[j] = const_cast<Fr*>(ntt_io[j]);
+    for (size_t b0 = 0; b0 < io.size(); b0 += NTT_MAX_BATCH)
+      RCCHK(ntt_dev_impl_batch(d, (const Fr* const*)io.data() + b0, n, io.data() + b0,
+                               (int)std::min<size_t>(NTT_MAX_BATCH, io.size() - b0), n, (int)pk.dom.k, pk.dom.omega, 1,
+                               pk.dom.g_coset, pk.dom.g_coset_inv, 0, one, 0, one, one, st));
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  if (g_spmd.exchange(g_spmd.ctx, pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
+    return fail(H2G_ERR_STATE, "spmd transport: exchange of column sub-cosets failed");
+  size_t off = 0;  // unpack, source by source
+  const size_t mycnt = slabs[me].hi1 - slabs[me].lo;
+  for (int o = 0; o < W; o++) {
+    if (o == me) continue;
+    for (int i = 0; i < M; i++) {
+      if (owner[i] != o) continue;
+      for (int t = me; t < E; t += W) {
+        HIPCHK(hipMemcpyAsync(coset[i] + (size_t)((t - me) / W) * n, pk.x_recv + off, n * sizeof(Fr),
+                              hipMemcpyDeviceToDevice, st));
+        off += n;
+      }
+      if (mycnt)
+        HIPCHK(hipMemcpyAsync(poly[i] + slabs[me].lo, pk.x_recv + off, mycnt * sizeof(Fr), hipMemcpyDeviceToDevice,
+                              st));
+      off += mycnt;
+    }
+  }
+  return H2G_OK;
+}
+
 int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, const PkImage* img = nullptr) {
   hipStream_t st = d->stream;
   std::string why;
@@ -1520,6 +1675,11 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   const bool h_slabs = spmd_subcosets() && slabs && g_spmd.exchange != nullptr;
   const bool coef_recv = h_slabs && pk.sub_ts.empty();
   const bool coef_send = h_slabs && !pk.sub_ts.empty() && g_spmd.world > (1 << (pk.dom.ek - pk.dom.k));
+  // column ownership of wide stages (colshard_distribute): under the full split, a stage of
+  // M columns goes to the ranks whole when M is a multiple of the ranks or at least 4x them
+  // (balanced); fewer columns keep point slabs
+  const int Wsp = g_spmd.world;
+  auto wide = [&](int M) { return h_slabs && g_spmd_colshard && M >= Wsp && (M % Wsp == 0 || M >= 4 * Wsp); };
   ProverRng& rng = *in.rng;
   Transcript tr(proof, pk.transcript);
   SpmdCheckScope spmd_check(&tr, &rng);
@@ -1615,12 +1775,17 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     van_early = true;
     return H2G_OK;
   };
+  std::vector<char> adv_shard((size_t)ncirc * pk.A, 0);  // advice columns distributed by their owners
   for (int ph = 0; ph <= pk.max_phase; ph++) {
     std::vector<int> cols;
     for (int c = 0; c < pk.A; c++)
       if (pk.adv_phase[c] == ph) cols.push_back(c);
     if (from_src && ph > 0) HIPCHK(hipStreamSynchronize(st));  // the previous phase's uploads read the staging
     std::vector<MsmTicket> tk(cols.size() * ncirc);
+    // a wide phase: column i (circuit-major) is rank i mod world's -- every rank uploads the
+    // whole witness (the lookups and products read it), only the owner commits and
+    // transforms the column
+    const bool adv_wide = wide((int)(cols.size() * ncirc));
     for (int ci = 0; ci < ncirc; ci++) {
       CircuitWs& w = *W[ci];
       const uint64_t* from = in.advice ? in.advice[ci] : nullptr;
@@ -1644,7 +1809,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       // commitment at once, so that a column's MSM overlaps the next column's upload
       // from host memory; the RNG draws keep the reference's order (every column's rows,
       // then every column's blind)
-      const bool early = commit_batch_chunk(prm, n, SRS_LAGRANGE) < 2;
+      const bool early = !adv_wide && commit_batch_chunk(prm, n, SRS_LAGRANGE) < 2;
       for (size_t k = 0; k < cols.size(); k++) {
         const int c = cols[k];
         HIPCHK(hipMemcpyAsync(w.adv[c], from + 4 * n * c, n * sizeof(Fr),
@@ -1658,18 +1823,32 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       }
       for (int c : cols)
         if (!pk.unblinded[c]) (void)rng.random_fr();  // commitment blinds (unused by KZG)
-      if (!cols.empty() && !early) {
+      if (!cols.empty() && !early && !adv_wide) {
         std::vector<const Fr*> polys(cols.size());
         for (size_t i = 0; i < cols.size(); i++) polys[i] = w.adv[cols[i]];
         RCCHK(commit_launch_batch(d, prm, polys.data(), (int)cols.size(), n, SRS_LAGRANGE, st,
                                   tk.data() + (size_t)ci * cols.size()));
       }
     }
+    std::vector<int> adv_owner;
+    std::vector<const Fr*> adv_lag;
+    std::vector<Fr*> adv_poly, adv_cst;
+    if (adv_wide) {
+      for (int ci = 0; ci < ncirc; ci++)
+        for (int c : cols) {
+          adv_owner.push_back((int)(adv_owner.size() % (size_t)Wsp));
+          adv_lag.push_back(W[ci]->adv[c]);
+          adv_poly.push_back(W[ci]->adv_poly[c]);
+          adv_cst.push_back(W[ci]->adv_coset[c]);
+        }
+      RCCHK(commit_launch_owned(d, prm, adv_lag.data(), adv_owner.data(), (int)adv_lag.size(), n, SRS_LAGRANGE, st,
+                                tk.data()));
+    }
     // the phase's advice to coefficient form and its extended-domain cosets do not depend
     // on any challenge: queued behind the uploads, they run while the commitment MSMs
     // (their own streams) are in flight (lagrange_to_coeff, prover.rs:673-689; the
     // cosets of evaluation.rs:344-361)
-    for (int ci = 0; ci < ncirc && !cols.empty(); ci++) {
+    for (int ci = 0; ci < ncirc && !cols.empty() && !adv_wide; ci++) {
       CircuitWs& w = *W[ci];
       std::vector<const Fr*> src;
       std::vector<Fr*> dst, cst;
@@ -1681,6 +1860,11 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       if (coef_recv) continue;  // coefficients from the owners (coef_exchange), no cosets
       RCCHK(lagrange_to_coeff_batch(d, D, src.data(), dst.data(), (int)cols.size(), st));
       RCCHK(ext_cosets(d, pk, (const Fr* const*)dst.data(), cst.data(), (int)cols.size(), st));
+    }
+    if (adv_wide) {
+      RCCHK(colshard_distribute(d, pk, adv_lag, adv_poly, adv_cst, adv_owner, st));
+      for (int ci = 0; ci < ncirc; ci++)
+        for (int c : cols) adv_shard[(size_t)ci * pk.A + c] = 1;
     }
     if (g_spmd.world > 1) {  // this phase's witness into the consistency digest
       std::vector<const Fr*> wc;
@@ -1721,6 +1905,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   };
   // ---- lookup_commit_permuted, per circuit, per lookup (lookup/prover.rs:64-173, 410-494)
   const int NLT = ncirc * pk.NL;  // (circuit, lookup) pairs, circuit-major: j = ci * NL + l
+  bool lk_shard = false;  // the lookups went to their owners (A', S' and z distributed)
+  std::vector<int> lk_owner_all(NLT, g_spmd.rank);
   {
     std::vector<MsmTicket> tk(2 * NLT);
     const size_t u = unusable;
@@ -1756,7 +1942,18 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     // canonical values checks the order (a window that tied different values); a lookup
     // whose check or width failed, or whose width is unknown (hb 0), is sorted in full
     // (four stable 64-bit limb sorts, least significant first).
-    const int G = 2 * NLT;
+    // a wide lookup stage: lookup j is rank j mod world's (its compression, sort, match and
+    // fill, commitments and transforms); every rank still makes every RNG draw.  lq[j]:
+    // the lookup's region in the batch buffers (-1: another rank's)
+    const bool lk_wide = wide(NLT);
+    std::vector<int>& lk_owner = lk_owner_all;
+    std::vector<int> lq(NLT, -1);
+    int nown = 0;
+    for (int j = 0; j < NLT; j++) {
+      if (lk_wide) lk_owner[j] = j % Wsp;
+      if (lk_owner[j] == g_spmd.rank) lq[j] = nown++;
+    }
+    const int G = 2 * nown;
     int gbits = 0;
     while ((1 << gbits) < G) gbits++;
     if (NLT && (size_t)G * u > pk.lkb_len) {  // grow-only batch buffers
@@ -1798,9 +1995,9 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       const Fr* srcs[2] = {w.lk_a[l], w.lk_s[l]};
       CanonKey* sorted[2] = {pk.ck_a2, pk.ck_t2};
       for (int side = 0; side < 2; side++) {
-        CanonKey* canon = pk.lkb_canon + (size_t)(2 * j + side) * u;
+        CanonKey* canon = pk.lkb_canon + (size_t)(2 * lq[j] + side) * u;
         HIPCHK(lookup_keys(srcs[side], u, 0, canon, nullptr, nullptr, pk.lk_or_d + (size_t)LKF * j, st));
-        const size_t o = (size_t)2 * j * u;
+        const size_t o = (size_t)2 * lq[j] * u;
         uint64_t *k0 = pk.lkb_key[0] + o, *k1 = pk.lkb_key[1] + o;
         uint32_t *i0 = pk.lkb_idx[0] + o, *i1 = pk.lkb_idx[1] + o;
         HIPCHK(iota_u32(i0, u, st));
@@ -1818,34 +2015,38 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     for (int ci = 0; ci < ncirc; ci++)
       for (int l = 0; l < pk.NL; l++) {
         const int j = ci * pk.NL + l;
-        RCCHK(compress(*W[ci], pk.seg_lk_in[l], W[ci]->lk_a[l]));
-        RCCHK(compress(*W[ci], pk.seg_lk_tab[l], W[ci]->lk_s[l]));
+        if (lq[j] >= 0) {
+          RCCHK(compress(*W[ci], pk.seg_lk_in[l], W[ci]->lk_a[l]));
+          RCCHK(compress(*W[ci], pk.seg_lk_tab[l], W[ci]->lk_s[l]));
+        }
         for (int which = 0; which < 2; which++) {
           Fr* r = rows.data() + ((size_t)2 * j + which) * (bf + 1);
           for (int i = 0; i <= bf; i++) r[i] = rng.random_fr();
         }
         (void)rng.random_fr();  // permuted input blind
         (void)rng.random_fr();  // permuted table blind
+        if (lq[j] < 0) continue;
         used[j] = pk.lk_hb[j];
         const int shift = used[j] > 48 ? used[j] - 48 : 0;
         const Fr* srcs[2] = {W[ci]->lk_a[l], W[ci]->lk_s[l]};
         for (int side = 0; side < 2; side++) {  // every column keys (a full-sort lookup's are ignored)
-          const size_t g = (size_t)2 * j + side;
+          const size_t g = (size_t)2 * lq[j] + side;
           HIPCHK(lookup_keys(srcs[side], u, shift, pk.lkb_canon + g * u, pk.lkb_key[0] + g * u, pk.lkb_idx[0] + g * u,
                              pk.lk_or_d + (size_t)LKF * j, st, 48, (uint64_t)g << 48));
         }
       }
-    if (NLT) {
+    if (nown) {
       bool alt = false;
       HIPCHK(radix_sort_pairs(pk.lkb_key[0], pk.lkb_idx[0], pk.lkb_key[1], pk.lkb_idx[1], (size_t)G * u, 0,
                               48 + gbits, pk.lkb_scr, st, &alt));
       const uint32_t* sidx = pk.lkb_idx[alt ? 1 : 0];
       for (int j = 0; j < NLT; j++) {
+        if (lq[j] < 0) continue;
         if (used[j] == 0) {
           RCCHK(full_sort(j));
         } else {
           for (int side = 0; side < 2; side++) {
-            const size_t g = (size_t)2 * j + side;
+            const size_t g = (size_t)2 * lq[j] + side;
             HIPCHK(lookup_gather(pk.lkb_canon + g * u, sidx + g * u, u, side ? pk.ck_t2 : pk.ck_a2,
                                  pk.lk_or_d + (size_t)LKF * j + 4, st));
           }
@@ -1863,7 +2064,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     // remembered for the next proof
     bool redo = false;
     for (int j = 0; j < NLT; j++) {
-      if (used[j] == 0) continue;
+      if (lq[j] < 0 || used[j] == 0) continue;
       const unsigned long long* f = pk.lk_or_h + (size_t)LKF * j;
       int hb = 0;
       for (int q = 3; q >= 0 && !hb; q--)
@@ -1878,11 +2079,17 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       }
     }
     if (redo) HIPCHK(hipStreamSynchronize(st));
+    bool lk_ok = true;
     for (int j = 0; j < NLT; j++) {
       const uint32_t* cnt = pk.lk_cnt + 3 * j;
-      if (cnt[2] != 0 || cnt[0] != cnt[1])
-        return fail(H2G_ERR_ARG, "create_proof: lookup input value not in the table (ConstraintSystemFailure)");
+      if (lq[j] >= 0 && (cnt[2] != 0 || cnt[0] != cnt[1])) lk_ok = false;
     }
+    if (lk_wide) {  // every rank learns whether any owner's lookup failed (none may hang in a collective)
+      std::vector<Fr> mine(1, lk_ok ? Fr::zero() : Fr::one()), all;
+      RCCHK(spmd_allgather_fr(mine, &all));
+      for (const Fr& f : all) lk_ok = lk_ok && f.is_zero();
+    }
+    if (!lk_ok) return fail(H2G_ERR_ARG, "create_proof: lookup input value not in the table (ConstraintSystemFailure)");
     std::vector<const Fr*> perm_cols;  // (A'_l, S'_l) in transcript order
     std::vector<Fr*> perm_polys, perm_cosets;
     for (int ci = 0; ci < ncirc; ci++)
@@ -1895,10 +2102,18 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         perm_cosets.push_back(w.lk_apc[l]);
         perm_cosets.push_back(w.lk_spc[l]);
       }
-    RCCHK(commit_launch_batch(d, prm, perm_cols.data(), 2 * NLT, n, SRS_LAGRANGE, st, tk.data()));
-    // coefficient forms and cosets, batched transforms (they overlap the commitments)
-    if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, perm_cols.data(), perm_polys.data(), 2 * NLT, st));
-    RCCHK(ext_cosets(d, pk, (const Fr* const*)perm_polys.data(), perm_cosets.data(), 2 * NLT, st));
+    if (lk_wide) {
+      std::vector<int> own2(2 * NLT);
+      for (int j = 0; j < NLT; j++) own2[2 * j] = own2[2 * j + 1] = lk_owner[j];
+      RCCHK(commit_launch_owned(d, prm, perm_cols.data(), own2.data(), 2 * NLT, n, SRS_LAGRANGE, st, tk.data()));
+      RCCHK(colshard_distribute(d, pk, perm_cols, perm_polys, perm_cosets, own2, st));
+    } else {
+      RCCHK(commit_launch_batch(d, prm, perm_cols.data(), 2 * NLT, n, SRS_LAGRANGE, st, tk.data()));
+      // coefficient forms and cosets, batched transforms (they overlap the commitments)
+      if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, perm_cols.data(), perm_polys.data(), 2 * NLT, st));
+      RCCHK(ext_cosets(d, pk, (const Fr* const*)perm_polys.data(), perm_cosets.data(), 2 * NLT, st));
+    }
+    lk_shard = lk_wide;
     for (int i = 0; i < 2 * NLT; i++) {
       G1Affine cm;
       RCCHK(commit_collect(d, &tk[i], &cm));
@@ -2002,42 +2217,62 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   {
     std::vector<const Fr*> z_lags;
     std::vector<Fr*> z_polys, z_cosets;
+    // a wide lookup stage keeps its owners here: lookup j's product is rank j mod world's
+    // (the permuted columns are already there); the others only make the RNG draws
+    const bool lz_wide = lk_shard;
+    auto mine = [&](int j) { return lk_owner_all[j] == g_spmd.rank; };
+    size_t zrow = 0;
     // prod: the running product's factors, or (scanned) already its prefix products
-    auto finish_z = [&](const Fr* prod, Fr* z_lag, Fr* z_poly, Fr* z_coset, bool scanned) -> int {
+    auto finish_z = [&](const Fr* prod, Fr* z_lag, Fr* z_poly, Fr* z_coset, bool scanned, bool here,
+                        bool listed) -> int {
+      Fr* rows = prod_blind.data() + (zrow++) * (size_t)bf;
+      for (int i = 0; i < bf; i++) rows[i] = rng.random_fr();
+      (void)rng.random_fr();  // product blind
+      if (!here) return H2G_OK;
       const Fr* pre = prod;
       if (!scanned) {
         HIPCHK(poly_prefix_product(prod, pk.pre, n, pk.scr, pk.scr_len, st));
         pre = pk.pre;
       }
-      Fr* rows = prod_blind.data() + z_lags.size() * (size_t)bf;
-      for (int i = 0; i < bf; i++) rows[i] = rng.random_fr();
-      (void)rng.random_fr();  // product blind
       HIPCHK(hipMemcpyAsync(pk.small, rows, (size_t)bf * sizeof(Fr), hipMemcpyHostToDevice, st));
       HIPCHK(perm_z_assemble(z_lag, n, bf, pre, pk.one, pk.small, st));
-      z_lags.push_back(z_lag);
-      z_polys.push_back(z_poly);
-      z_cosets.push_back(z_coset);
+      if (listed) {
+        z_lags.push_back(z_lag);
+        z_polys.push_back(z_poly);
+        z_cosets.push_back(z_coset);
+      }
       return H2G_OK;
     };
     // every lookup's denominators go through one batched inversion (the per-thread
     // inversion's latency is paid once); z_poly holds the product until its iNTT,
     // z_lag serves as the inversion's scratch until z is assembled into it
     std::vector<Fr*> dens, dens_scr;
-    for (CircuitWs* w : W)
-      for (int l = 0; l < pk.NL; l++) {
+    for (int ci = 0, j = 0; ci < ncirc; ci++)
+      for (int l = 0; l < pk.NL; l++, j++) {
+        if (!mine(j)) continue;
+        CircuitWs* w = W[ci];
         HIPCHK(lookup_prod_den(w->lk_ap[l], w->lk_sp[l], beta, gamma, w->lk_z_poly[l], n, st));
         dens.push_back(w->lk_z_poly[l]);
         dens_scr.push_back(w->lk_z[l]);
       }
-    HIPCHK(poly_batch_invert_multi(dens.data(), dens_scr.data(), NLT, n, st));
+    if (!dens.empty()) HIPCHK(poly_batch_invert_multi(dens.data(), dens_scr.data(), (int)dens.size(), n, st));
     // numerators, then every lookup's running product in one batched scan (in place)
-    for (CircuitWs* w : W)
-      for (int l = 0; l < pk.NL; l++)
-        HIPCHK(lookup_prod_num(w->lk_a[l], w->lk_s[l], beta, gamma, w->lk_z_poly[l], n, st));
-    HIPCHK(poly_prefix_product_multi((const Fr* const*)dens.data(), dens.data(), NLT, n, pk.scr, pk.scr_len, st));
-    for (CircuitWs* w : W)
-      for (int l = 0; l < pk.NL; l++)
-        RCCHK(finish_z(w->lk_z_poly[l], w->lk_z[l], w->lk_z_poly[l], w->lk_zc[l], true));
+    for (int ci = 0, j = 0; ci < ncirc; ci++)
+      for (int l = 0; l < pk.NL; l++, j++)
+        if (mine(j)) HIPCHK(lookup_prod_num(W[ci]->lk_a[l], W[ci]->lk_s[l], beta, gamma, W[ci]->lk_z_poly[l], n, st));
+    if (!dens.empty())
+      HIPCHK(poly_prefix_product_multi((const Fr* const*)dens.data(), dens.data(), (int)dens.size(), n, pk.scr,
+                                       pk.scr_len, st));
+    std::vector<const Fr*> lkz_lag;
+    std::vector<Fr*> lkz_poly, lkz_cst;
+    for (int ci = 0, j = 0; ci < ncirc; ci++)
+      for (int l = 0; l < pk.NL; l++, j++) {
+        CircuitWs* w = W[ci];
+        RCCHK(finish_z(w->lk_z_poly[l], w->lk_z[l], w->lk_z_poly[l], w->lk_zc[l], true, mine(j), !lz_wide));
+        lkz_lag.push_back(w->lk_z[l]);
+        lkz_poly.push_back(w->lk_z_poly[l]);
+        lkz_cst.push_back(w->lk_zc[l]);
+      }
     for (CircuitWs* w : W)
       for (int s = 0; s < pk.NS; s++) {
         RCCHK(compress(*w, pk.seg_sh_in[s], pk.tmp_a));
@@ -2045,17 +2280,24 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         HIPCHK(shuffle_prod_den(pk.tmp_b, gamma, pk.mod, n, st));
         HIPCHK(poly_batch_invert(pk.mod, n, pk.scr, st));
         HIPCHK(shuffle_prod_num(pk.tmp_a, gamma, pk.mod, n, st));
-        RCCHK(finish_z(pk.mod, w->sh_z[s], w->sh_z_poly[s], w->sh_zc[s], false));
+        RCCHK(finish_z(pk.mod, w->sh_z[s], w->sh_z_poly[s], w->sh_zc[s], false, true, true));
       }
-    if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, z_lags.data(), z_polys.data(), (int)z_lags.size(), st));
-    RCCHK(ext_cosets(d, pk, (const Fr* const*)z_polys.data(), z_cosets.data(), (int)z_lags.size(), st));
-  }
-  {  // product commitments: every circuit's lookups, then every circuit's shuffles, one batch
+    if (!z_lags.empty()) {
+      if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, z_lags.data(), z_polys.data(), (int)z_lags.size(), st));
+      RCCHK(ext_cosets(d, pk, (const Fr* const*)z_polys.data(), z_cosets.data(), (int)z_lags.size(), st));
+    }
+    // product commitments: every circuit's lookups, then every circuit's shuffles
     std::vector<const Fr*> zs;
     for (CircuitWs* w : W) zs.insert(zs.end(), w->lk_z.begin(), w->lk_z.end());
     for (CircuitWs* w : W) zs.insert(zs.end(), w->sh_z.begin(), w->sh_z.end());
     std::vector<MsmTicket> zt(zs.size());
-    RCCHK(commit_launch_batch(d, prm, zs.data(), (int)zs.size(), n, SRS_LAGRANGE, st, zt.data()));
+    if (lz_wide) {
+      RCCHK(commit_launch_owned(d, prm, zs.data(), lk_owner_all.data(), NLT, n, SRS_LAGRANGE, st, zt.data()));
+      if (NSH) RCCHK(commit_launch_batch(d, prm, zs.data() + NLT, NSH, n, SRS_LAGRANGE, st, zt.data() + NLT));
+      RCCHK(colshard_distribute(d, pk, lkz_lag, lkz_poly, lkz_cst, lk_owner_all, st));
+    } else if (!zs.empty()) {
+      RCCHK(commit_launch_batch(d, prm, zs.data(), (int)zs.size(), n, SRS_LAGRANGE, st, zt.data()));
+    }
     for (int j = 0; j < NLT; j++) lkz_tk[j] = zt[j];
     for (int j = 0; j < NSH; j++) shz_tk[j] = zt[NLT + j];
   }
@@ -2265,8 +2507,13 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   }
   const int id_fix = (int)polys.size();
   if (coef_send || coef_recv) {  // the per-circuit coefficient columns' slabs, owners -> the others
-    std::vector<Fr*> cols;
-    for (int i = 0; i < id_fix; i++) cols.push_back(const_cast<Fr*>(polys[i].p));
+    std::vector<Fr*> cols;     // (the columns of wide stages reached every rank from their owners)
+    for (int ci = 0; ci < ncirc; ci++)
+      for (int i = 0; i < per_c; i++) {
+        if (i < pk.A && adv_shard[(size_t)ci * pk.A + i]) continue;
+        if (lk_shard && i >= pk.A + pk.nsets && i < pk.A + pk.nsets + 3 * pk.NL) continue;
+        cols.push_back(const_cast<Fr*>(polys[(size_t)ci * per_c + i].p));
+      }
     RCCHK(coef_exchange(pk, cols, st));
   }
   for (int c = 0; c < pk.F; c++) polys.push_back({pk.fixed_poly[c], n});
@@ -3370,6 +3617,12 @@ int h2g_spmd_set_weights(const uint32_t* weights, int world) {
     pre.push_back(pre.back() + weights[r]);
   }
   g_spmd_wprefix = pre;
+  return H2G_OK;
+}
+
+int h2g_spmd_set_column_owners(int on) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  g_spmd_colshard = on != 0;
   return H2G_OK;
 }
 

@@ -98,6 +98,7 @@ struct MsmTicket {
   int c = 0;
   hipEvent_t done = nullptr;
   int64_t shard_seq = -1;  // >= 0: the peers' slabs of this MSM are pending (h2g_shard_transport)
+  bool remote = false;     // SPMD column ownership: another rank computes this MSM whole
 };
 
 struct Device {

@@ -119,6 +119,7 @@ _SIGS = {
     "h2g_spmd_set_weights": ([VP, I32], I32),
     "h2g_comm_spmd_install": ([I32], I32),
     "h2g_comm_spmd_uninstall": ([], I32),
+    "h2g_spmd_set_column_owners": ([I32], I32),
 }
 
 TRANSCRIPTS = {"blake2b": 0, "keccak256": 1}  # Blake2bWrite / Keccak256Write (h2g_pk_set_transcript)
@@ -938,6 +939,11 @@ def set_spmd_transport(world, rank=0, allgather=None, bcast=None, allgather_host
     t = SpmdTransport(None, world, rank, cb, cbb, cbh, cbx)
     _transport_keep = (t, cb, cbb, cbh, cbx, [])
     check(lib().h2g_set_spmd_transport(ctypes.byref(t)))
+
+
+def spmd_set_column_owners(on):
+    """SPMD column ownership of wide stages (h2g_spmd_set_column_owners; on by default)"""
+    check(lib().h2g_spmd_set_column_owners(1 if on else 0))
 
 
 def spmd_set_weights(weights):
