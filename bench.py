@@ -196,14 +196,13 @@ def pmc_traffic(args):
             return None, f"{ctr} pass failed: {type(e).__name__}"
         finally:
             shutil.rmtree(d, ignore_errors=True)
-    traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
-    low = (vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
-    return traffic, (f"rocprofv3 --pmc, mean per launch of msm_acc_kernel: FETCH_SIZE {vals['FETCH_SIZE']:.0f} KiB "
-                     f"(x2 gfx950 correction), WRITE_SIZE {vals['WRITE_SIZE']:.0f} KiB.  Calibration "
-                     f"(tools/microbench/pmc_calib.hip, profiles/r03/pmc_calibration.json): FETCH_SIZE counts 0.50 of "
-                     f"a coalesced 16-B or 8-B per lane stream and 1.01 of random 64-B point gathers, i.e. one 64-B "
-                     f"unit per read request; x2 prices every request as the 128-B line it moves (upper bound), "
-                     f"{low / 1e9:.2f} GB per launch if the point gathers move 64 B (lower bound)")
+    # the raw counters (bytes); roofline_from_phases applies the calibration per access kind
+    return {"fetch": vals["FETCH_SIZE"] * 1024.0, "write": vals["WRITE_SIZE"] * 1024.0}, (
+        f"rocprofv3 --pmc, mean per launch of msm_acc_kernel: FETCH_SIZE {vals['FETCH_SIZE']:.0f} KiB, WRITE_SIZE "
+        f"{vals['WRITE_SIZE']:.0f} KiB.  Calibration (tools/microbench/pmc_calib.hip, profiles/r03/pmc_calibration.json): "
+        "FETCH_SIZE counts one 64-B unit per read request -- 1.01 of random 64-B point gathers, 0.50 of a coalesced "
+        "8-B / 16-B per lane stream -- so `traffic` counts the gathers x1 and the sorted-value stream x2 "
+        "(FETCH + 0.5 x the stream's bytes) + WRITE; `traffic_upper` prices every request as a 128-B line (2 FETCH + WRITE)")
 
 
 def pmc_child(args):
@@ -262,7 +261,7 @@ def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
-        "traffic": round(traffic) if traffic else None,
+        "traffic": None,
         "traffic_note": traffic_note,
         "kernel_ms": round(acc_ms, 4),
         "launches": calls,
@@ -278,6 +277,14 @@ def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note
                  "madds_per_launch": round(madds), "madds": madd_source},
         "window_bits": c,
     }
+    if traffic:  # PMC bytes per launch, calibrated per access kind (pmc_traffic)
+        stream = madds * 4.0  # the u32 bucket-ordered values, read once
+        cal = traffic["fetch"] + 0.5 * stream + traffic["write"]
+        gathered = madds * 64.0  # one 64-B table point per mixed addition
+        out.update({"traffic": round(cal), "traffic_upper": round(2 * traffic["fetch"] + traffic["write"]),
+                    "traffic_vs_algorithmic": round(cal / (points_per_launch * MSM_BYTES_PER_POINT), 2),
+                    "traffic_vs_gathered_table_bytes": round(cal / gathered, 3),
+                    "gathered_table_bytes": round(gathered)})
     if union and union.get("accumulate", 0) > 0:
         # MSMs on the two MSM streams overlap each other, so a launch's duration counts the
         # chip's time twice while they do: the chip-level rate is the work over the busy time
@@ -503,14 +510,35 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         dist.barrier(group=CTRL)
     torch.cuda.synchronize()
     h2g.profile_enable(True)
+    if spmd:
+        h2g.spmd_stats(reset=True)
     t0 = time.perf_counter()
     session(timed)
     torch.cuda.synchronize()
+    t_local = time.perf_counter() - t0  # this rank's proofs, before the closing barrier
     if world > 1:
         dist.barrier(group=CTRL)
     elapsed = time.perf_counter() - t0
     h2g.profile_enable(False)
     calls, phases, union = h2g.profile_msm_collect(with_union=True)
+    per_rank = None
+    if spmd:  # attribution: each rank's proof time, and the part of it inside each collective kind
+        st_ = h2g.spmd_stats(reset=True)
+        mine = [t_local / args.steps * 1e3] + [st_[k]["ms"] / args.steps for k in h2g.SPMD_COLLECTIVES] + \
+               [st_[k]["calls"] / args.steps for k in h2g.SPMD_COLLECTIVES] + \
+               [st_[k]["bytes"] / args.steps for k in h2g.SPMD_COLLECTIVES]
+        t = torch.tensor(mine, dtype=torch.float64)
+        allt = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allt, t, group=CTRL)
+        per_rank = []
+        nk = len(h2g.SPMD_COLLECTIVES)
+        for r, v in enumerate(allt):
+            v = v.tolist()
+            coll = {k: {"ms": round(v[1 + i], 3), "calls": v[1 + nk + i], "mb": round(v[1 + 2 * nk + i] / 1e6, 2)}
+                    for i, k in enumerate(h2g.SPMD_COLLECTIVES)}
+            cms = sum(c["ms"] for c in coll.values())
+            per_rank.append({"rank": r, "proof_ms": round(v[0], 3), "in_collectives_ms": round(cms, 3),
+                             "compute_ms": round(v[0] - cms, 3), "collectives_per_proof": coll})
     elapsed = max_over_ranks(elapsed, dist, world, dev)
     line = None
     extra = {}
@@ -528,6 +556,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         extra["verified"] = verify_proof(h2g, circ, pk, params, proofs[0])
         stages = []
         pcie = None
+        rngcore = None
         if not one_proof:
             h2g.prover_stage_sync(True)
             step()
@@ -547,6 +576,19 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                     "max_s": round(max(pts), 4), "proofs": len(pts),
                     "note": "advice uploaded from pageable host memory inside each proof (column uploads overlap "
                             "the previous column's commitment MSM); same proof bytes"}
+            # the caller-RNG form (create_proof(..., rng: R: RngCore, ...)): the same
+            # ChaCha20 stream drawn through the h2g_rng callback struct by h2g_create_proof_multi,
+            # advice device-resident as in `value`; as many proofs as the timed steps, median
+            rts = []
+            for _ in range(args.steps):
+                t0 = time.perf_counter()
+                pp = pk.create_proof_multi([wit], rng="native", advice_dev_ptrs=[adv.data_ptr()])
+                rts.append(time.perf_counter() - t0)
+                assert pp == proofs[0]
+            rngcore = {"median_s": round(sorted(rts)[len(rts) // 2], 4), "min_s": round(min(rts), 4),
+                       "max_s": round(max(rts), 4), "proofs": len(rts),
+                       "note": "h2g_create_proof_multi with an h2g_rng callback (ChaCha20Rng from [7; 32] drawn "
+                               "through fill_bytes); advice device-resident; same proof bytes"}
         ms_per_step = elapsed / args.steps * 1e3
         msm_ms = sum(phases.values()) / max(calls, 1)
         n_local = h2g_dist.slab(n, world, 1)[0] if one_proof else n  # rank 0's points per MSM
@@ -600,9 +642,18 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         if pcie:
             line["pcie_inclusive"] = pcie
             line["pcie_inclusive_s"] = pcie["median_s"]
+            line["rngcore"] = rngcore
+            line["rngcore_s"] = rngcore["median_s"]
         if spmd:
             line["proof_bytes_equal_across_ranks"] = extra["ranks_equal"]
             line["config"]["spmd_slab_weights"] = spmd_weights["w"]
+            line["per_rank"] = per_rank
+            line["transport"] = {"kind": spmd_kind["kind"], "torch_backend": dist.get_backend(),
+                                 "torch_world": dist.get_world_size()}
+            if native:
+                cnt, rk = h2g.comm_info()
+                line["transport"]["rccl_comm_count"] = cnt
+                line["transport"]["rccl_comm_rank0"] = rk
         if transport_note:
             line["transport_note"] = transport_note
     if args.workload == "prove" and (world == 1 or dist.get_backend() == "nccl"):

@@ -322,6 +322,11 @@ typedef struct {
 } h2g_prove_inputs;
 int h2g_create_proof_multi(uint64_t params, uint64_t pk, const h2g_prove_inputs* in, uint8_t* proof,
                            size_t proof_cap, size_t* proof_len);
+/* a native ChaCha20Rng::from_seed(seed) (rand_chacha 0.3) as an h2g_rng: *out's callbacks
+ * draw from it (the RngCore a Rust host passes to create_proof, without the host); the
+ * proof equals the rng_seed path's bytes.  h2g_rng_free releases it. */
+int h2g_rng_chacha20(const uint8_t seed[32], h2g_rng* out, uint64_t* handle);
+int h2g_rng_free(uint64_t handle);
 /* the challenges of the last proof (num_challenges x 4 u64), *count = num_challenges */
 int h2g_last_challenges(uint64_t* out, int max, int* count);
 /* wall milliseconds of the stages of the last h2g_create_proof (names: h2g_prover_stage_name).
@@ -383,6 +388,8 @@ int h2g_comm_install(uint64_t params);
 int h2g_comm_serve(uint64_t params, uint64_t* served);
 int h2g_comm_stop(void);
 int h2g_comm_destroy(void);
+/* the communicator as RCCL reports it (ncclCommCount / ncclCommUserRank); 0 / -1 without one */
+int h2g_comm_info(int32_t* rccl_count, int32_t* rccl_rank);
 
 /* ---- one proof across several GPUs, SPMD: every rank runs the same create_proof (same
  * key, witness, instances and RNG stream -- a seed, or draws the host replicates -- hence
@@ -452,6 +459,11 @@ int h2g_spmd_set_weights(const uint32_t* weights, int world);
  * every rank its coefficient slab; a lookup's sort, match and product run on its owner
  * only.  Stages with fewer columns keep the point slabs.  0 turns it off. */
 int h2g_spmd_set_column_owners(int on);
+/* time inside the SPMD transport since the last reset, per collective kind k (0 the MSM
+ * partials' all-gathers, 1 the host all-gathers, 2 the exchanges, 3 the broadcasts):
+ * out[3k] milliseconds (host wall clock around the call), out[3k + 1] calls, out[3k + 2]
+ * bytes sent + received; reset != 0 zeroes the counters after reading */
+int h2g_spmd_stats(double* out, int max, int reset);
 /* split_subcosets: 1 divides the extended domain's sub-cosets over the ranks (bcast over
  * the communicator), 0 replicates that work; the multi-open tail always runs on
  * coefficient slabs (allgather_host over the communicator) */

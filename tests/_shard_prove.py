@@ -72,6 +72,11 @@ def main():
     ap.add_argument("--diverge-witness", action="store_true",
                     help="spmd: the last rank proves another witness (one advice value changed); every rank "
                          "must refuse the proof")
+    ap.add_argument("--no-column-owners", action="store_true",
+                    help="spmd: point slabs for every MSM, no column ownership (h2g_spmd_set_column_owners(0))")
+    ap.add_argument("--oracle", action="store_true",
+                    help="spmd: rank 0 also compares the sharded proof with the CPU oracle's create_proof "
+                         "(tests/_oracle.py) on the same SRS, witness and seed")
     ap.add_argument("--one-variant", action="store_true",
                     help="prove each case once (default seed) instead of twice (large cases)")
     ap.add_argument("cases", nargs="+")
@@ -157,6 +162,7 @@ def spmd_main(args, rank, world, native):
     variants = [{}] if args.one_variant else [{}, {"seed": bytes(range(32)), "vanishing_threads": 3}]
     weights = [int(x) for x in args.weights.split(",")] if args.weights else None
     h2g.spmd_set_weights(weights)
+    h2g.spmd_set_column_owners(not args.no_column_owners)
     for name in args.cases:
         case = CASES[name]()
         circ = case[0]
@@ -226,6 +232,13 @@ def spmd_main(args, rank, world, native):
                          "bcasts": None if g is None else g.bcasts,
                          "host_gathers": None if g is None else g.host_gathers,
                          "exchanges": None if g is None else g.exchanges}
+        if args.oracle and rank == 0 and len(case) == 2:  # the sharded bytes against the checker itself
+            import _oracle as O
+            gg, gl = params.export()
+            threads = max(1, min(16, len(os.sched_getaffinity(0))))
+            print(f"[rank 0] oracle create_proof k={circ.k} on {threads} threads", flush=True)
+            results[name]["oracle_same"] = got[0] == O.create_proof(circ, case[1], gg, gl, threads=threads)
+            del gg, gl
         pk.close()
         params.close()
         dist.barrier()

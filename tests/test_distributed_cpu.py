@@ -188,7 +188,7 @@ def test_weighted_slabs_partition_the_points():
     covering, proportional to the weights; owner_weights lightens the sub-coset owners"""
     import h2g_dist as D
     P = 1 << 22
-    for world, w in [(8, D.owner_weights(8, 23, 22)), (3, [3, 1, 2]), (4, None)]:
+    for world, w in [(8, D.owner_weights(8, 23, 22, row_pieces=False)), (3, [3, 1, 2]), (4, None)]:
         sl = [D.slab(P, world, r, weights=w) for r in range(world)]
         assert sl[0][0] == 0 and sl[-1][1] == P
         assert all(sl[r][1] == sl[r + 1][0] for r in range(world - 1))
@@ -197,11 +197,15 @@ def test_weighted_slabs_partition_the_points():
             assert abs((sl[r][1] - sl[r][0]) - P * ws[r] / sum(ws)) <= 1
         # an MSM shorter than P: the same boundaries clipped to its length
         assert [D.slab(P - 1, world, r, P, w) for r in range(world)][-1][1] == P - 1
-    assert D.owner_weights(8, 23, 22) == [10, 10] + [100] * 6  # 4x the owners: measured best 0.1
-    assert D.owner_weights(4, 23, 22) == [50, 50, 100, 100]  # 2x the owners: 0.5
-    assert D.owner_weights(8, 23, 22, 0.5) == [50, 50] + [100] * 6
+    nop = dict(row_pieces=False)  # sub-coset owners (no row pieces)
+    assert D.owner_weights(8, 23, 22, **nop) == [10, 10] + [100] * 6  # 4x the owners: measured best 0.1
+    assert D.owner_weights(4, 23, 22, **nop) == [50, 50, 100, 100]  # 2x the owners: 0.5
+    assert D.owner_weights(8, 23, 22, 0.5, **nop) == [50, 50] + [100] * 6
     assert D.owner_weights(2, 23, 22) is None  # every rank owns a sub-coset
-    assert D.owner_weights(8, 20, 18) == [50] * 4 + [100] * 4
+    assert D.owner_weights(8, 20, 18, **nop) == [50] * 4 + [100] * 4
+    # row pieces: every rank holds an equal piece of one sub-coset -> uniform slabs
+    assert D.owner_weights(8, 23, 22) is None and D.owner_weights(8, 20, 18) is None
+    assert D.owner_weights(6, 20, 18) == D.owner_weights(6, 20, 18, row_pieces=False) is not None  # 6 % 4 != 0
 
 
 def _host_gather_worker(rank, world, port, q):

@@ -113,6 +113,8 @@ def test_caller_chacha_rng_equals_seed_on_device():
     want = O.create_proof(circ, wit, g, gl, seed=seed)
     assert pk.create_proof_multi([wit], rng=ChaChaStream(seed)) == want
     assert pk.create_proof(wit, seed=seed) == want
+    # the library's own ChaCha20 behind the h2g_rng callbacks (h2g_rng_chacha20)
+    assert pk.create_proof_multi([wit], seed=seed, rng="native") == want
     pk.close()
     params.close()
 

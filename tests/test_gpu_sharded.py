@@ -8,6 +8,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -33,10 +34,30 @@ def _run(world, cases, backend="gloo", transport="torch", mode="slab", extra=(),
            os.path.join(HERE, "_shard_prove.py"), "--backend", backend, "--transport", transport,
            "--mode", mode] + list(extra) + cases
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
-    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
-    line = [ln for ln in p.stdout.splitlines() if ln.startswith("SHARD_RESULT ")]
-    assert line, p.stdout[-3000:] + p.stderr[-3000:]
+    # the ranks' output goes to a log under gpurun_out/ as it is written (a multi-minute
+    # at-size case shows its progress there), read back when the ranks have finished
+    logdir = os.path.join(os.path.dirname(HERE), "gpurun_out", "sharded")
+    os.makedirs(logdir, exist_ok=True)
+    log = os.path.join(logdir, f"{mode}_{world}_{'_'.join(cases)[:60]}.log")
+    with open(log, "w") as f:
+        p = subprocess.Popen(cmd, stdout=f, stderr=subprocess.STDOUT, text=True, env=env)
+        t0 = time.monotonic()
+        while True:
+            try:
+                p.wait(timeout=30)
+                break
+            except subprocess.TimeoutExpired:
+                if time.monotonic() - t0 > timeout:
+                    p.kill()
+                    p.wait()
+                    break
+                f.write(f"[test] ranks running {time.monotonic() - t0:.0f} s\n")
+                f.flush()
+    with open(log) as f:
+        out = f.read()
+    assert p.returncode == 0, out[-6000:]
+    line = [ln for ln in out.splitlines() if ln.startswith("SHARD_RESULT ")]
+    assert line, out[-6000:]
     return json.loads(line[-1][len("SHARD_RESULT "):])
 
 
@@ -94,6 +115,29 @@ def test_spmd_proof_two_and_three_ranks():
         assert res[nm]["exchanges"] == 0, (nm, res[nm])
 
 
+def test_spmd_row_pieces_four_and_eight_ranks():
+    """more ranks than sub-coset (world a multiple of 2^e): every rank evaluates h on a row
+    piece of one sub-coset (rotation halos around it), every column's transforms run once
+    on its owner and reach the pieces through one exchange per stage, the pieces' h rows
+    gather at each sub-coset's leader; bytes == one GPU.  Degree-3 circuits have 2
+    sub-cosets: 2 pieces each at 4 ranks, 4 at 8"""
+    cases = ["simple_k6", "mixed_k10", "c3_k14", "challenge_k9", "multi_my_k6"]
+    res = _run(4, cases, mode="spmd")
+    for nm in cases:
+        assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
+    res = _run(8, ["c3_k14", "mixed_k10"], mode="spmd", extra=["--one-variant"])
+    for nm in ("c3_k14", "mixed_k10"):
+        assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
+
+
+def test_spmd_column_owners_off_matches():
+    """the same proofs with column ownership off (h2g_spmd_set_column_owners(0)): point
+    slabs for every MSM, sub-coset owners transforming every column"""
+    res = _run(4, ["keccak_k12", "c3_k14"], mode="spmd", extra=["--no-column-owners"])
+    for nm in ("keccak_k12", "c3_k14"):
+        assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
+
+
 def test_spmd_two_circuits_distinct_witnesses():
     """two MyCircuit instances with different inputs (witnesses and instances), a lookup,
     a shuffle and a second phase each, in one SPMD proof: every rank == one GPU"""
@@ -126,11 +170,18 @@ def test_spmd_c3_k22_at_size(world):
     into `world` point slabs and the extended domain's sub-cosets divided over the ranks
     (gloo ranks sharing this box's GPU); every rank's bytes == the single-GPU proof.  With
     more ranks than the 2 sub-cosets, the non-owners receive their coefficient slabs of the
-    circuit's columns (a second exchange)"""
-    res = _run(world, ["c3_k22"], mode="spmd", extra=["--one-variant"], timeout=1100)
+    circuit's columns (a second exchange).  At 2 ranks rank 0 also checks its bytes against
+    the CPU oracle directly (tests/_oracle.py create_proof on the same SRS and witness)"""
+    extra = ["--one-variant"] + (["--oracle"] if world == 2 else [])
+    res = _run(world, ["c3_k22"], mode="spmd", extra=extra, timeout=1100)
+    print("c3_k22", world, res["c3_k22"])
     assert res["c3_k22"]["same"] and res["c3_k22"]["same_ranks"], res
+    # 11 MSM all-gathers; exchanges: 1 (h by coefficient slabs) at 2 ranks; at 4 ranks the
+    # row pieces add the 3 advice columns' pieces and the h rows gathered at the leaders
     assert res["c3_k22"]["gathers"] == 11, res
-    assert res["c3_k22"]["exchanges"] == (1 if world <= 2 else 2), res
+    assert res["c3_k22"]["exchanges"] == (1 if world == 2 else 5), res
+    if world == 2:  # rank 0's sharded bytes == the CPU oracle's create_proof (tests/_oracle.py)
+        assert res["c3_k22"]["oracle_same"], res
 
 
 @pytest.mark.timeout(1200)

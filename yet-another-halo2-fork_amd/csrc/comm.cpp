@@ -157,6 +157,15 @@ int comm_destroy() {
 }
 
 int comm_world() { return g_comm ? g_comm->world : 1; }
+// RCCL's own view of the slab communicator: ncclCommCount / ncclCommUserRank (0 / -1 without one)
+int comm_rccl_info(int* count, int* rank) {
+  *count = 0;
+  *rank = -1;
+  if (!g_comm) return H2G_OK;
+  NCCLCHK(ncclCommCount(g_comm->tx, count));
+  NCCLCHK(ncclCommUserRank(g_comm->tx, rank));
+  return H2G_OK;
+}
 int comm_rank() { return g_comm ? g_comm->rank : 0; }
 
 void* comm_spmd_ctx() { return g_comm; }

@@ -27,6 +27,7 @@ int comm_unique_id(uint8_t id[COMM_ID_BYTES]);
 int comm_init(const uint8_t id[COMM_ID_BYTES], int world, int rank);
 int comm_destroy();
 int comm_world();
+int comm_rccl_info(int* count, int* rank);
 int comm_rank();
 
 // rank 0 (the h2g_shard_transport callbacks of a native transport; ctx = Comm state)

@@ -202,17 +202,30 @@ msm_big_item_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__
   }
 }
 
-// one wavefront per bucket with several items: sum of its items' partial sums
+// buckets with several items: the sum of their items' partial sums -- one lane per bucket
+// of at most COMBINE_LANE items (a short sequential sum; skewed inputs -- a lookup's
+// permuted column holds a few hundred distinct values -- make thousands of such buckets,
+// where a wave per bucket left 63 lanes idle: 0.8 ms per keccak-style batch), one
+// wavefront and a tree per larger bucket
+static constexpr uint32_t COMBINE_LANE = 8;
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_big_combine_kernel(const uint4* __restrict__ multi, const uint32_t* __restrict__ counters,
                        const G1xyzz* __restrict__ partial, G1xyzz* __restrict__ buckets) {
   __shared__ G1xyzz sh[MSM_THREADS];
   const uint32_t nm = counters[1];
   const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t q = blockIdx.x * MSM_THREADS + threadIdx.x; q < nm; q += gridDim.x * MSM_THREADS) {
+    const uint4 m = multi[q];  // (bucket, first item, items)
+    if (m.z > COMBINE_LANE) continue;
+    G1xyzz acc = partial[m.y];
+    for (uint32_t i = 1; i < m.z; i++) acc = xyzz_add(acc, partial[m.y + i]);
+    buckets[m.x] = acc;
+  }
   G1xyzz* w = sh + (threadIdx.x & ~63u);
   const uint32_t nwaves = gridDim.x * (MSM_THREADS / 64);
   for (uint32_t q = blockIdx.x * (MSM_THREADS / 64) + (threadIdx.x >> 6); q < nm; q += nwaves) {
     const uint4 m = multi[q];  // (bucket, first item, items)
+    if (m.z <= COMBINE_LANE) continue;  // uniform across the wave
     G1xyzz acc = G1xyzz::identity();
     for (uint32_t i = lane; i < m.z; i += 64) acc = xyzz_add(acc, partial[m.y + i]);
     w[lane] = acc;

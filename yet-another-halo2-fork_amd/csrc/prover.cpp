@@ -195,8 +195,18 @@ struct ProvingKey {
   // rank + world, ... < 2^e of the extended domain; the key's cosets cut to them (slot i
   // of each buffer = sub-coset sub_ts[i]), per-slot sigma tables, and the 2^e x n slots
   // the h evaluations are broadcast through
-  int64_t sub_key = -1;  // world * 65536 + rank the cache holds
+  int64_t sub_key = -1;  // (world * 65536 + rank) * 2 + pieces the cache holds
   std::vector<uint64_t> sub_ts;
+  // more ranks than sub-cosets (world a multiple of 2^e, with the slab exchange): rank r
+  // evaluates rows [sub_lo, sub_hi) of sub-coset r mod 2^e -- piece r / 2^e of world / 2^e
+  // -- and holds its columns there with a halo of rotations [rot_lo, rot_hi]
+  bool sub_pieces = false;
+  uint64_t sub_lo = 0, sub_hi = 0;
+  int rot_lo = -1, rot_hi = 1;
+  Fr* cs_scr = nullptr;  // column ownership: the owned columns' 2^e sub-cosets
+  size_t cs_scr_len = 0;
+  Fr* perm_lz = nullptr;  // slab-wise grand products: z at each set's slab start
+  size_t perm_lz_len = 0;
   std::vector<Fr*> sub_fixed, sub_sigma;
   Fr *sub_l0 = nullptr, *sub_ll = nullptr, *sub_la = nullptr;
   std::vector<const Fr**> d_sigma_sub;
@@ -217,6 +227,11 @@ struct ProvingKey {
   // SPMD h(X) by slabs (h2g_spmd_transport.exchange): send / receive staging
   Fr *x_send = nullptr, *x_recv = nullptr;
   size_t x_send_len = 0, x_recv_len = 0;
+  // SPMD column ownership: the pack / unpack copy lists (host lists live until the next
+  // stage, after a stream synchronisation, so their asynchronous uploads have completed)
+  CopySeg* d_segs = nullptr;
+  size_t d_segs_len = 0;
+  std::vector<CopySeg> h_segs[2];
   uint32_t* d_seeds = nullptr;
   uint64_t* d_offsets = nullptr;
   int max_chunks = 0;
@@ -325,6 +340,27 @@ uint64_t g_shard_seq = 0;
 // SPMD sharding (h2g_set_spmd_transport): every rank proves, rank r computes slab r
 h2g_spmd_transport g_spmd{nullptr, 1, 0, nullptr, nullptr};
 uint64_t g_spmd_seq = 0;
+// time, calls and bytes (sent + received) inside the transport, per collective kind
+// (h2g_spmd_stats): 0 MSM all-gathers, 1 host all-gathers, 2 exchanges, 3 broadcasts
+struct SpmdStats {
+  double ms[4] = {};
+  uint64_t calls[4] = {}, bytes[4] = {};
+};
+SpmdStats g_spmd_stats;
+template <class F>
+int spmd_timed(int kind, uint64_t bytes, F&& f) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = f();
+  g_spmd_stats.ms[kind] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  g_spmd_stats.calls[kind]++;
+  g_spmd_stats.bytes[kind] += bytes;
+  return rc;
+}
+int spmd_exchange(const void* d_send, const size_t* sb, void* d_recv, const size_t* rb) {
+  uint64_t bytes = 0;
+  for (int r = 0; r < g_spmd.world; r++) bytes += sb[r] + rb[r];
+  return spmd_timed(2, bytes, [&] { return g_spmd.exchange(g_spmd.ctx, d_send, sb, d_recv, rb); });
+}
 // the running proof's transcript, RNG draws and witness, whose digest travels with every
 // SPMD partial (H2G_SPMD_WORDS): ranks that diverged fail the proof instead of summing
 // slabs of different polynomials.  The witness enters as every advice column's value at
@@ -414,7 +450,7 @@ int commit_collect(Device* d, MsmTicket* t, G1Affine* out) {
     spmd_digest(mine + 9);
     std::vector<uint64_t> all((size_t)W * SW);
     const int64_t seq = t->shard_seq;
-    if (g_spmd.allgather(g_spmd.ctx, (uint64_t)seq, mine, all.data()) != 0)
+    if (spmd_timed(0, (uint64_t)SW * 8 * (W + 1), [&] { return g_spmd.allgather(g_spmd.ctx, (uint64_t)seq, mine, all.data()); }) != 0)
       return fail(H2G_ERR_STATE, "spmd transport: all-gather of MSM " + std::to_string(seq) + " failed");
     t->shard_seq = -1;
     for (int r = 0; r < W; r++)
@@ -862,7 +898,8 @@ int spmd_allgather_fr(const std::vector<Fr>& mine, std::vector<Fr>* all) {
   const size_t W = (size_t)g_spmd.world, cnt = mine.size();
   all->assign(W * cnt, Fr::zero());
   if (!cnt) return H2G_OK;
-  if (g_spmd.allgather_host(g_spmd.ctx, mine.data(), cnt * sizeof(Fr), all->data()) != 0)
+  if (spmd_timed(1, cnt * sizeof(Fr) * (W + 1),
+                 [&] { return g_spmd.allgather_host(g_spmd.ctx, mine.data(), cnt * sizeof(Fr), all->data()); }) != 0)
     return fail(H2G_ERR_STATE, "spmd transport: host all-gather failed");
   return H2G_OK;
 }
@@ -919,15 +956,33 @@ int slab_carries(ProvingKey& pk, const Slab& sl, size_t n, const std::vector<Fr>
   return H2G_OK;
 }
 
-// the key's cosets cut to this rank's sub-cosets, once per (world, rank)
-int sub_prepare(ProvingKey& pk, hipStream_t st) {
-  const int64_t key = (int64_t)g_spmd.world * 65536 + g_spmd.rank;
+// the key's cosets cut to this rank's sub-cosets, once per (world, rank, pieces)
+int sub_prepare(ProvingKey& pk, hipStream_t st, bool pieces) {
+  const int64_t key = ((int64_t)g_spmd.world * 65536 + g_spmd.rank) * 2 + (pieces ? 1 : 0);
   if (pk.sub_key == key) return H2G_OK;
   const int e = (int)(pk.dom.ek - pk.dom.k);
   const uint64_t E = 1ull << e;
   const size_t n = pk.n;
   pk.sub_ts.clear();
-  for (uint64_t t = (uint64_t)g_spmd.rank; t < E; t += (uint64_t)g_spmd.world) pk.sub_ts.push_back(t);
+  pk.sub_pieces = pieces;
+  if (pieces) {  // world = G E: rank r takes piece r / E of sub-coset r mod E
+    const uint64_t G = (uint64_t)g_spmd.world / E, p = (uint64_t)g_spmd.rank / E;
+    pk.sub_ts.push_back((uint64_t)g_spmd.rank % E);
+    pk.sub_lo = (uint64_t)n * p / G;
+    pk.sub_hi = (uint64_t)n * (p + 1) / G;
+  } else {
+    for (uint64_t t = (uint64_t)g_spmd.rank; t < E; t += (uint64_t)g_spmd.world) pk.sub_ts.push_back(t);
+    pk.sub_lo = 0;
+    pk.sub_hi = n;
+  }
+  // the rows a piece reads around its own: every query rotation, z(omega X), z(omega^last X),
+  // the lookups' A'(omega^-1 X)
+  pk.rot_lo = std::min(-1, -(pk.bf + 1));
+  pk.rot_hi = 1;
+  for (const Query& q : pk.loads) {
+    pk.rot_lo = std::min(pk.rot_lo, q.rot);
+    pk.rot_hi = std::max(pk.rot_hi, q.rot);
+  }
   const size_t nt = pk.sub_ts.size();
   auto cut = [&](const Fr* full, Fr** out) -> int {
     if (!*out) HIPCHK(pk.pool.get((void**)out, pk.ext * sizeof(Fr)));  // room for any rank's slots
@@ -1031,7 +1086,10 @@ int h_by_slabs(Device* d, ProvingKey& pk, const Slab& sl, hipStream_t st) {
   const int E = 1 << e;
   const int np = pk.degree - 1;
   if (E > HSLAB_MAX_E || np > E) return fail(H2G_ERR_ARG, "create_proof: too many sub-cosets for the h slab exchange");
-  const size_t nt = pk.sub_ts.size();
+  // the sub-cosets this rank interpolates (with row pieces: the leaders, ranks < E)
+  std::vector<uint64_t> ts = pk.sub_ts;
+  if (pk.sub_pieces && me >= E) ts.clear();
+  const size_t nt = ts.size();
   // sizes: slab r of each owned sub-coset to rank r; every owner's blocks to me
   std::vector<size_t> sb(W), rb(W), soff(W + 1, 0);
   std::vector<Slab> slabs(W);
@@ -1055,7 +1113,7 @@ int h_by_slabs(Device* d, ProvingKey& pk, const Slab& sl, hipStream_t st) {
   }
   const Fr one = Fr::one();
   for (size_t i = 0; i < nt; i++) {
-    const uint64_t t = pk.sub_ts[i];
+    const uint64_t t = ts[i];
     Fr* f = pk.h_coeff + i * n;  // scratch until the combine
     RCCHK(ntt_dev_impl(d, pk.h_gather + t * n, n, f, n, (int)D.k, D.omega_inv, 0, one, one, 1, D.ifft_div, 1,
                        D.g_coset_inv, D.g_coset, st));
@@ -1088,7 +1146,7 @@ int h_by_slabs(Device* d, ProvingKey& pk, const Slab& sl, hipStream_t st) {
   }
   HIPCHK(hipMemcpyAsync(pk.small, coef.data(), coef.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
   HIPCHK(hipStreamSynchronize(st));  // the send staging is complete; coef (host) was read
-  if (g_spmd.exchange(g_spmd.ctx, pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
+  if (spmd_exchange(pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
     return fail(H2G_ERR_STATE, "spmd transport: exchange of h slabs failed");
   HSlabArgs a;
   a.recv = pk.x_recv;
@@ -1149,7 +1207,7 @@ int coef_exchange(ProvingKey& pk, const std::vector<Fr*>& cols, hipStream_t st) 
     }
   }
   HIPCHK(hipStreamSynchronize(st));
-  if (g_spmd.exchange(g_spmd.ctx, pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
+  if (spmd_exchange(pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
     return fail(H2G_ERR_STATE, "spmd transport: exchange of coefficient slabs failed");
   if (me >= E) {  // unpack: owner by owner, its columns in order
     const size_t cnt = slabs[me].hi1 - slabs[me].lo;
@@ -1164,16 +1222,40 @@ int coef_exchange(ProvingKey& pk, const std::vector<Fr*>& cols, hipStream_t st) 
   return H2G_OK;
 }
 
-// SPMD column ownership of a wide stage (as many columns as ranks or more: the advice of a
-// phase, the lookups' permuted columns and products -- SURVEY 8e's round-robin whole
-// columns): column i belongs to rank owner[i], which alone forms its coefficients (the
-// n-point iNTT, prover.rs:673-689 / lookup/prover.rs:131,311) and its E = 2^e sub-cosets
-// (n-point NTTs of the twisted coefficients, the cosets of evaluation.rs:344-361), each
-// written straight into its own slot when it owns that sub-coset or else into the send
-// buffer.  One all-to-all then hands sub-coset t of every column to its owner (rank t mod
-// world, slot (t - rank) / world) and every rank its coefficient slab [lo, hi1) (what the
-// evaluations and SHPLONK read).  Message from o to r: per column of o in index order, the
-// sub-cosets r owns (increasing t, n each), then r's coefficient slab.
+// The rows of the extended domain rank r holds: (sub-coset t, its slot, first row a,
+// count len; rows wrap mod n) -- whole sub-cosets t = r, r + world, ... when world <= 2^e,
+// else its piece of sub-coset r mod 2^e with the halo of rotations around it
+struct RowPiece {
+  uint64_t t;
+  int slot;
+  uint64_t a, len;
+};
+std::vector<RowPiece> pieces_of(const ProvingKey& pk, int r) {
+  const int W = g_spmd.world;
+  const uint64_t E = 1ull << (pk.dom.ek - pk.dom.k), n = pk.n;
+  std::vector<RowPiece> v;
+  if (pk.sub_pieces) {
+    const uint64_t G = (uint64_t)W / E, p = (uint64_t)r / E;
+    const uint64_t lo = n * p / G, hi = n * (p + 1) / G;
+    const uint64_t len = std::min<uint64_t>(n, hi - lo + (uint64_t)(pk.rot_hi - pk.rot_lo));
+    const uint64_t a = (uint64_t)(((int64_t)lo + (int64_t)n + pk.rot_lo) % (int64_t)n);
+    v.push_back({(uint64_t)r % E, 0, a, len});
+  } else {
+    int slot = 0;
+    for (uint64_t t = (uint64_t)r; t < E; t += (uint64_t)W) v.push_back({t, slot++, 0, n});
+  }
+  return v;
+}
+
+// SPMD column ownership (SURVEY 8e's round-robin whole columns): column i of a stage is
+// rank owner[i]'s, which alone forms its coefficients (the n-point iNTT, prover.rs:673-689 /
+// lookup/prover.rs:131,311) and its E = 2^e sub-cosets (n-point NTTs of the twisted
+// coefficients: the cosets of evaluation.rs:344-361) in its scratch.  One all-to-all then
+// hands every rank the rows of every column it evaluates h on (pieces_of) and its
+// coefficient slab [lo, hi1) (what the evaluations and SHPLONK read).  Message from o to r:
+// per column of o in index order, r's pieces (in order, wrapped rows as two runs), then r's
+// coefficient slab.  Used for wide stages (the owners also commit) and, with row pieces,
+// for every stage (the transforms then never run twice).
 int colshard_distribute(Device* d, ProvingKey& pk, const std::vector<const Fr*>& lag, const std::vector<Fr*>& poly,
                         const std::vector<Fr*>& coset, const std::vector<int>& owner, hipStream_t st) {
   const size_t n = pk.n;
@@ -1181,22 +1263,27 @@ int colshard_distribute(Device* d, ProvingKey& pk, const std::vector<const Fr*>&
   const int E = 1 << (pk.dom.ek - pk.dom.k);
   const int M = (int)lag.size();
   std::vector<Slab> slabs(W);
-  for (int r = 0; r < W; r++) slabs[r] = spmd_slab(n, r);
-  auto owned_subs = [&](int r) {  // sub-cosets rank r owns
-    int c = 0;
-    for (int t = r; t < E; t += W) c++;
-    return c;
-  };
-  auto msg_words = [&](int o, int r) {  // Fr from rank o to rank r
-    size_t w = 0;
-    for (int i = 0; i < M; i++)
-      if (owner[i] == o) w += (size_t)owned_subs(r) * n + (slabs[r].hi1 - slabs[r].lo);
+  std::vector<std::vector<RowPiece>> pcs(W);
+  for (int r = 0; r < W; r++) {
+    slabs[r] = spmd_slab(n, r);
+    pcs[r] = pieces_of(pk, r);
+  }
+  auto rows_of = [&](int r) {
+    uint64_t w = 0;
+    for (const RowPiece& pc : pcs[r]) w += pc.len;
     return w;
   };
+  std::vector<int> mine;  // this rank's columns, index order
+  for (int i = 0; i < M; i++)
+    if (owner[i] == me) mine.push_back(i);
   std::vector<size_t> sb(W, 0), rb(W, 0), soff(W + 1, 0);
   for (int r = 0; r < W; r++) {
-    sb[r] = r == me ? 0 : msg_words(me, r) * sizeof(Fr);
-    rb[r] = r == me ? 0 : msg_words(r, me) * sizeof(Fr);
+    if (r != me) {
+      sb[r] = mine.size() * (rows_of(r) + (slabs[r].hi1 - slabs[r].lo)) * sizeof(Fr);
+      size_t cols_r = 0;
+      for (int i = 0; i < M; i++) cols_r += owner[i] == r;
+      rb[r] = cols_r * (rows_of(me) + (slabs[me].hi1 - slabs[me].lo)) * sizeof(Fr);
+    }
     soff[r + 1] = soff[r] + sb[r] / sizeof(Fr);
   }
   size_t rtot = 0;
@@ -1209,55 +1296,75 @@ int colshard_distribute(Device* d, ProvingKey& pk, const std::vector<const Fr*>&
     PALLOC(pk.pool, pk.x_recv, rtot);
     pk.x_recv_len = rtot;
   }
-  // this rank's columns: coefficients, then every sub-coset (own slot or send buffer) and
-  // the others' coefficient slabs
-  std::vector<const Fr*> my_lag;
-  std::vector<Fr*> my_poly;
-  for (int i = 0; i < M; i++)
-    if (owner[i] == me) {
-      my_lag.push_back(lag[i]);
-      my_poly.push_back(poly[i]);
-    }
-  if (!my_lag.empty()) RCCHK(lagrange_to_coeff_batch(d, pk.dom, my_lag.data(), my_poly.data(), (int)my_lag.size(), st));
-  std::vector<size_t> pos(W);
-  for (int r = 0; r < W; r++) pos[r] = soff[r];
-  std::vector<const Fr*> ntt_io;
-  for (int i = 0; i < M; i++) {
-    if (owner[i] != me) continue;
-    for (int r = 0; r < W; r++) {
-      if (r == me) {
-        for (int t = me; t < E; t += W) ntt_io.push_back(coset[i] + (size_t)((t - me) / W) * n);
-        continue;
-      }
-      for (int t = r; t < E; t += W) {
-        ntt_io.push_back(pk.x_send + pos[r]);
-        pos[r] += n;
-      }
-      const size_t cnt = slabs[r].hi1 - slabs[r].lo;
-      if (cnt)
-        HIPCHK(hipMemcpyAsync(pk.x_send + pos[r], poly[i] + slabs[r].lo, cnt * sizeof(Fr), hipMemcpyDeviceToDevice,
-                              st));
-      pos[r] += cnt;
-    }
+  const size_t scr = mine.size() * (size_t)E * n;
+  if (scr > pk.cs_scr_len) {
+    PALLOC(pk.pool, pk.cs_scr, scr);
+    pk.cs_scr_len = scr;
   }
-  {  // twists + n-point NTTs of every sub-coset formed here (ntt_io in the order above)
-    size_t q = 0;
-    for (int i = 0; i < M; i++) {
-      if (owner[i] != me) continue;
-      for (int r = 0; r < W; r++)
-        for (int t = r; t < E; t += W)
-          HIPCHK(subcoset_twist(poly[i], const_cast<Fr*>(ntt_io[q++]), n, pk.eo, (uint64_t)t, pk.ext - 1, st));
+  auto run_segs = [&](std::vector<CopySeg>& v) -> int {  // one launch for a copy list
+    if (v.empty()) return H2G_OK;
+    if (v.size() > pk.d_segs_len) {
+      PALLOC(pk.pool, pk.d_segs, v.size());
+      pk.d_segs_len = v.size();
     }
+    uint64_t mx = 0;
+    for (const CopySeg& g : v) mx = std::max<uint64_t>(mx, g.len);
+    HIPCHK(hipMemcpyAsync(pk.d_segs, v.data(), v.size() * sizeof(CopySeg), hipMemcpyHostToDevice, st));
+    HIPCHK(copy_segments(pk.d_segs, (int)v.size(), mx, st));
+    return H2G_OK;
+  };
+  // rows [a, a + len) mod n of one sub-coset: one or two runs
+  auto runs = [&](const RowPiece& pc, auto&& fn) {
+    const uint64_t first = std::min<uint64_t>(pc.len, n - pc.a);
+    fn(pc.a, 0, first);
+    if (pc.len > first) fn(0, first, pc.len - first);
+  };
+  // coefficients, then the twists and the n-point NTTs of every sub-coset of every column
+  if (!mine.empty()) {
+    std::vector<const Fr*> l2;
+    std::vector<Fr*> p2, io;
+    for (int i : mine) {
+      l2.push_back(lag[i]);
+      p2.push_back(poly[i]);
+    }
+    RCCHK(lagrange_to_coeff_batch(d, pk.dom, l2.data(), p2.data(), (int)l2.size(), st));
+    for (size_t q = 0; q < mine.size(); q++)
+      for (int t = 0; t < E; t++) {
+        Fr* o = pk.cs_scr + (q * E + t) * n;
+        HIPCHK(subcoset_twist(poly[mine[q]], o, n, pk.eo, (uint64_t)t, pk.ext - 1, st));
+        io.push_back(o);
+      }
     const Fr one = Fr::one();
-    std::vector<Fr*> io(ntt_io.size());
-    for (size_t j = 0; j < io.size(); j++) io[j] = const_cast<Fr*>(ntt_io[j]);
     for (size_t b0 = 0; b0 < io.size(); b0 += NTT_MAX_BATCH)
       RCCHK(ntt_dev_impl_batch(d, (const Fr* const*)io.data() + b0, n, io.data() + b0,
                                (int)std::min<size_t>(NTT_MAX_BATCH, io.size() - b0), n, (int)pk.dom.k, pk.dom.omega, 1,
                                pk.dom.g_coset, pk.dom.g_coset_inv, 0, one, 0, one, one, st));
   }
+  std::vector<CopySeg>& pack = pk.h_segs[0];
+  std::vector<CopySeg>& unpack = pk.h_segs[1];
+  pack.clear();
+  unpack.clear();
+  for (int r = 0; r < W; r++) {
+    size_t pos = soff[r];
+    for (size_t q = 0; q < mine.size(); q++) {
+      const int i = mine[q];
+      for (const RowPiece& pc : pcs[r]) {
+        const Fr* src = pk.cs_scr + (q * E + pc.t) * n;
+        runs(pc, [&](uint64_t row, uint64_t at, uint64_t cnt) {
+          if (r == me) pack.push_back(CopySeg{src + row, coset[i] + (size_t)pc.slot * n + row, cnt});
+          else pack.push_back(CopySeg{src + row, pk.x_send + pos + at, cnt});
+        });
+        if (r != me) pos += pc.len;
+      }
+      if (r == me) continue;
+      const size_t cnt = slabs[r].hi1 - slabs[r].lo;
+      if (cnt) pack.push_back(CopySeg{poly[i] + slabs[r].lo, pk.x_send + pos, cnt});
+      pos += cnt;
+    }
+  }
+  RCCHK(run_segs(pack));
   HIPCHK(hipStreamSynchronize(st));
-  if (g_spmd.exchange(g_spmd.ctx, pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
+  if (spmd_exchange(pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
     return fail(H2G_ERR_STATE, "spmd transport: exchange of column sub-cosets failed");
   size_t off = 0;  // unpack, source by source
   const size_t mycnt = slabs[me].hi1 - slabs[me].lo;
@@ -1265,17 +1372,114 @@ int colshard_distribute(Device* d, ProvingKey& pk, const std::vector<const Fr*>&
     if (o == me) continue;
     for (int i = 0; i < M; i++) {
       if (owner[i] != o) continue;
-      for (int t = me; t < E; t += W) {
-        HIPCHK(hipMemcpyAsync(coset[i] + (size_t)((t - me) / W) * n, pk.x_recv + off, n * sizeof(Fr),
-                              hipMemcpyDeviceToDevice, st));
-        off += n;
+      for (const RowPiece& pc : pcs[me]) {
+        runs(pc, [&](uint64_t row, uint64_t at, uint64_t cnt) {
+          unpack.push_back(CopySeg{pk.x_recv + off + at, coset[i] + (size_t)pc.slot * n + row, cnt});
+        });
+        off += pc.len;
       }
-      if (mycnt)
-        HIPCHK(hipMemcpyAsync(poly[i] + slabs[me].lo, pk.x_recv + off, mycnt * sizeof(Fr), hipMemcpyDeviceToDevice,
-                              st));
+      if (mycnt) unpack.push_back(CopySeg{pk.x_recv + off, poly[i] + slabs[me].lo, mycnt});
       off += mycnt;
     }
   }
+  RCCHK(run_segs(unpack));
+  return H2G_OK;
+}
+
+// pieces: the leader of sub-coset t (rank t) receives the h rows of the sub-coset's other
+// pieces (ranks t + 2^e p), which arrive in rank order -- the rows' own order -- straight
+// into its h_gather slot
+int h_gather_pieces(ProvingKey& pk, hipStream_t st) {
+  const int W = g_spmd.world, me = g_spmd.rank;
+  const int E = 1 << (pk.dom.ek - pk.dom.k);
+  const size_t n = pk.n;
+  const uint64_t t = (uint64_t)me % (uint64_t)E;
+  std::vector<size_t> sb(W, 0), rb(W, 0);
+  const int G = W / E;
+  if (me >= E) sb[t] = (pk.sub_hi - pk.sub_lo) * sizeof(Fr);
+  else
+    for (int p = 1; p < G; p++) rb[me + E * p] = (size_t)(n * (p + 1) / G - n * p / G) * sizeof(Fr);
+  Fr* slot = pk.h_gather + t * n;
+  HIPCHK(hipStreamSynchronize(st));
+  if (spmd_exchange(slot + pk.sub_lo, sb.data(), slot + n / G, rb.data()) != 0)
+    return fail(H2G_ERR_STATE, "spmd transport: exchange of h pieces failed");
+  return H2G_OK;
+}
+
+// column i's rows go from every rank's MSM slab [shard_lo(P, n, W, r), shard_lo(.., r + 1))
+// to its owner owner[i] (which then holds the whole column): one exchange; message from r
+// to o: the slab rows of every column o owns, index order
+int gather_to_owners(ProvingKey& pk, const std::vector<Fr*>& cols, const std::vector<int>& owner, size_t P,
+                     hipStream_t st) {
+  const size_t n = pk.n;
+  const int W = g_spmd.world, me = g_spmd.rank;
+  const int M = (int)cols.size();
+  std::vector<size_t> lo(W + 1);
+  for (int r = 0; r <= W; r++) lo[r] = shard_lo(P, n, W, r);
+  std::vector<size_t> sb(W, 0), rb(W, 0), soff(W + 1, 0);
+  for (int r = 0; r < W; r++) {
+    if (r != me) {
+      size_t mine = 0, theirs = 0;
+      for (int i = 0; i < M; i++) {
+        mine += owner[i] == r;     // r's columns: I send my slab of each
+        theirs += owner[i] == me;  // my columns: r sends its slab of each
+      }
+      sb[r] = mine * (lo[me + 1] - lo[me]) * sizeof(Fr);
+      rb[r] = theirs * (lo[r + 1] - lo[r]) * sizeof(Fr);
+    }
+    soff[r + 1] = soff[r] + sb[r] / sizeof(Fr);
+  }
+  size_t rtot = 0;
+  for (int r = 0; r < W; r++) rtot += rb[r] / sizeof(Fr);
+  if (soff[W] > pk.x_send_len) {
+    PALLOC(pk.pool, pk.x_send, soff[W]);
+    pk.x_send_len = soff[W];
+  }
+  if (rtot > pk.x_recv_len) {
+    PALLOC(pk.pool, pk.x_recv, rtot);
+    pk.x_recv_len = rtot;
+  }
+  std::vector<CopySeg>& pack = pk.h_segs[0];
+  std::vector<CopySeg>& unpack = pk.h_segs[1];
+  pack.clear();
+  unpack.clear();
+  const size_t my = lo[me + 1] - lo[me];
+  for (int r = 0; r < W; r++) {
+    if (r == me || !my) continue;
+    size_t pos = soff[r];
+    for (int i = 0; i < M; i++)
+      if (owner[i] == r) {
+        pack.push_back(CopySeg{cols[i] + lo[me], pk.x_send + pos, my});
+        pos += my;
+      }
+  }
+  size_t off = 0;
+  for (int r = 0; r < W; r++) {
+    if (r == me) continue;
+    const size_t cnt = lo[r + 1] - lo[r];
+    for (int i = 0; i < M; i++)
+      if (owner[i] == me && cnt) {
+        unpack.push_back(CopySeg{pk.x_recv + off, cols[i] + lo[r], cnt});
+        off += cnt;
+      }
+  }
+  auto run = [&](std::vector<CopySeg>& v) -> int {
+    if (v.empty()) return H2G_OK;
+    if (v.size() > pk.d_segs_len) {
+      PALLOC(pk.pool, pk.d_segs, v.size());
+      pk.d_segs_len = v.size();
+    }
+    uint64_t mx = 0;
+    for (const CopySeg& g : v) mx = std::max<uint64_t>(mx, g.len);
+    HIPCHK(hipMemcpyAsync(pk.d_segs, v.data(), v.size() * sizeof(CopySeg), hipMemcpyHostToDevice, st));
+    HIPCHK(copy_segments(pk.d_segs, (int)v.size(), mx, st));
+    return H2G_OK;
+  };
+  RCCHK(run(pack));
+  HIPCHK(hipStreamSynchronize(st));
+  if (spmd_exchange(pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
+    return fail(H2G_ERR_STATE, "spmd transport: exchange of product slabs failed");
+  RCCHK(run(unpack));
   return H2G_OK;
 }
 
@@ -1661,7 +1865,12 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   while ((int)pk.cws.size() < ncirc) RCCHK(circuit_ws_add(pk));  // workspaces grow once
   std::vector<CircuitWs*> W(ncirc);
   for (int c = 0; c < ncirc; c++) W[c] = pk.cws[c].get();
-  if (spmd_subcosets()) RCCHK(sub_prepare(pk, st));  // this rank's sub-cosets of the key's cosets
+  // with the slab exchange and world a multiple of 2^e above it, every rank takes a row
+  // piece of one sub-coset (sub_prepare)
+  const int E_sub = 1 << (pk.dom.ek - pk.dom.k);
+  const bool pieces = spmd_subcosets() && g_spmd.allgather_host && g_spmd.exchange && pk.multiopen == 0 &&
+                      g_spmd_colshard && g_spmd.world > E_sub && g_spmd.world % E_sub == 0;
+  if (spmd_subcosets()) RCCHK(sub_prepare(pk, st, pieces));  // this rank's sub-cosets of the key's cosets
   MsmRingGuard ring_guard{d};
   StageClock clk(st, g_stage_sync);
   // SPMD coefficient slabs for the multi-open tail (SHPLONK only; GWC stays replicated)
@@ -1674,12 +1883,30 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   // them whole for their cosets, send it (coef_exchange) and it skips their iNTTs
   const bool h_slabs = spmd_subcosets() && slabs && g_spmd.exchange != nullptr;
   const bool coef_recv = h_slabs && pk.sub_ts.empty();
-  const bool coef_send = h_slabs && !pk.sub_ts.empty() && g_spmd.world > (1 << (pk.dom.ek - pk.dom.k));
+  const bool coef_send = h_slabs && !pieces && !pk.sub_ts.empty() && g_spmd.world > (1 << (pk.dom.ek - pk.dom.k));
   // column ownership of wide stages (colshard_distribute): under the full split, a stage of
   // M columns goes to the ranks whole when M is a multiple of the ranks or at least 4x them
   // (balanced); fewer columns keep point slabs
   const int Wsp = g_spmd.world;
   auto wide = [&](int M) { return h_slabs && g_spmd_colshard && M >= Wsp && (M % Wsp == 0 || M >= 4 * Wsp); };
+  // a stage's coefficient forms and extended-domain columns: with row pieces every stage's
+  // transforms have one owner per column (round-robin across the stages, tr_next), a wide
+  // stage's are its columns' owners (own); otherwise every sub-coset owner transforms
+  // every column (the others receive coefficient slabs at the end, coef_exchange)
+  int tr_next = 0;
+  auto xform = [&](const std::vector<const Fr*>& lag, const std::vector<Fr*>& pol, const std::vector<Fr*>& cst,
+                   const std::vector<int>* own) -> int {
+    const int M = (int)lag.size();
+    if (M == 0) return H2G_OK;
+    if (own || pieces) {
+      std::vector<int> o(M);
+      for (int i = 0; i < M; i++) o[i] = own ? (*own)[i] : (tr_next + i) % Wsp;
+      if (!own) tr_next += M;
+      return colshard_distribute(d, pk, lag, pol, cst, o, st);
+    }
+    if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, lag.data(), pol.data(), M, st));
+    return ext_cosets(d, pk, (const Fr* const*)pol.data(), cst.data(), M, st);
+  };
   ProverRng& rng = *in.rng;
   Transcript tr(proof, pk.transcript);
   SpmdCheckScope spmd_check(&tr, &rng);
@@ -1848,7 +2075,18 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     // on any challenge: queued behind the uploads, they run while the commitment MSMs
     // (their own streams) are in flight (lagrange_to_coeff, prover.rs:673-689; the
     // cosets of evaluation.rs:344-361)
-    for (int ci = 0; ci < ncirc && !cols.empty() && !adv_wide; ci++) {
+    if (pieces && !adv_wide && !cols.empty()) {  // one owner per column, every circuit's
+      std::vector<const Fr*> l2;
+      std::vector<Fr*> p2, c2;
+      for (int ci = 0; ci < ncirc; ci++)
+        for (int c : cols) {
+          l2.push_back(W[ci]->adv[c]);
+          p2.push_back(W[ci]->adv_poly[c]);
+          c2.push_back(W[ci]->adv_coset[c]);
+        }
+      RCCHK(xform(l2, p2, c2, nullptr));
+    }
+    for (int ci = 0; ci < ncirc && !cols.empty() && !adv_wide && !pieces; ci++) {
       CircuitWs& w = *W[ci];
       std::vector<const Fr*> src;
       std::vector<Fr*> dst, cst;
@@ -1862,7 +2100,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       RCCHK(ext_cosets(d, pk, (const Fr* const*)dst.data(), cst.data(), (int)cols.size(), st));
     }
     if (adv_wide) {
-      RCCHK(colshard_distribute(d, pk, adv_lag, adv_poly, adv_cst, adv_owner, st));
+      RCCHK(xform(adv_lag, adv_poly, adv_cst, &adv_owner));
       for (int ci = 0; ci < ncirc; ci++)
         for (int c : cols) adv_shard[(size_t)ci * pk.A + c] = 1;
     }
@@ -2106,12 +2344,11 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       std::vector<int> own2(2 * NLT);
       for (int j = 0; j < NLT; j++) own2[2 * j] = own2[2 * j + 1] = lk_owner[j];
       RCCHK(commit_launch_owned(d, prm, perm_cols.data(), own2.data(), 2 * NLT, n, SRS_LAGRANGE, st, tk.data()));
-      RCCHK(colshard_distribute(d, pk, perm_cols, perm_polys, perm_cosets, own2, st));
+      RCCHK(xform(perm_cols, perm_polys, perm_cosets, &own2));
     } else {
       RCCHK(commit_launch_batch(d, prm, perm_cols.data(), 2 * NLT, n, SRS_LAGRANGE, st, tk.data()));
       // coefficient forms and cosets, batched transforms (they overlap the commitments)
-      if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, perm_cols.data(), perm_polys.data(), 2 * NLT, st));
-      RCCHK(ext_cosets(d, pk, (const Fr* const*)perm_polys.data(), perm_cosets.data(), 2 * NLT, st));
+      RCCHK(xform(perm_cols, perm_polys, perm_cosets, nullptr));
     }
     lk_shard = lk_wide;
     for (int i = 0; i < 2 * NLT; i++) {
@@ -2143,12 +2380,102 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       all_z.push_back(w->z[s]);
       all_z_coset.push_back(w->z_coset[s]);
     }
-  {
-    auto col_vals = [&](const CircuitWs& w, int c) -> const Fr* {
-      const auto& pc = pk.perm_cols[c];
-      return pc.first == COL_ADVICE ? w.adv[pc.second]
-                                    : (pc.first == COL_FIXED ? pk.fixed_lag[pc.second] : w.inst_val[pc.second]);
-    };
+  auto col_vals = [&](const CircuitWs& w, int c) -> const Fr* {
+    const auto& pc = pk.perm_cols[c];
+    return pc.first == COL_ADVICE ? w.adv[pc.second]
+                                  : (pc.first == COL_FIXED ? pk.fixed_lag[pc.second] : w.inst_val[pc.second]);
+  };
+  // with row pieces the grand products go by slabs: each rank forms its MSM slab's rows of
+  // every set (denominators, inversion, numerators, a slab-local running product), one host
+  // all-gather of the slabs' products chains the slabs and the sets (z_0 of set s + 1 is
+  // set s's last product row), the commitments take the slabs, and each set's transform
+  // owner gathers the whole column
+  const bool perm_slab = pieces && NST > 0;
+  if (perm_slab) {
+    const int me = g_spmd.rank;
+    const size_t plo = shard_lo(prm.n, n, Wsp, me), phi = shard_lo(prm.n, n, Wsp, me + 1), len = phi - plo;
+    std::vector<Fr*> zl(NST), zs(NST);
+    for (int i = 0; i < NST; i++) {
+      zl[i] = all_z_lag[i] + plo;
+      zs[i] = all_z[i] + plo;
+    }
+    for (int ci = 0; ci < ncirc; ci++)
+      for (int s = 0; s < pk.nsets; s++) {
+        const int c0 = s * pk.chunk_len, c1 = std::min(c0 + pk.chunk_len, pk.P);
+        for (int c = c0; c < c1 && len; c += PERM_MAXC) {
+          PermCols pc;
+          pc.m = std::min(PERM_MAXC, c1 - c);
+          for (int j = 0; j < pc.m; j++) {
+            pc.v[j] = col_vals(*W[ci], c + j) + plo;
+            pc.sigma[j] = pk.sigma_lag[c + j] + plo;
+          }
+          HIPCHK(perm_denominators(zl[(size_t)ci * pk.nsets + s], len, pc, beta, gamma, c == c0, st));
+        }
+      }
+    if (len) HIPCHK(poly_batch_invert_multi(zl.data(), zs.data(), NST, len, st));
+    for (int ci = 0; ci < ncirc; ci++) {
+      Fr deltaomega = Fr::one();
+      for (int s = 0; s < pk.nsets; s++) {
+        const int c0 = s * pk.chunk_len, c1 = std::min(c0 + pk.chunk_len, pk.P);
+        for (int c = c0; c < c1; c += PERM_MAXC) {
+          PermCols pc;
+          pc.m = std::min(PERM_MAXC, c1 - c);
+          for (int j = 0; j < pc.m; j++) {
+            pc.v[j] = col_vals(*W[ci], c + j) + plo;
+            pc.beta_delta[j] = deltaomega * beta;
+            deltaomega = deltaomega * fr_delta();
+          }
+          if (len) HIPCHK(perm_numerators(zl[(size_t)ci * pk.nsets + s], len, pc, gamma, pk.om, st, plo));
+        }
+      }
+    }
+    if (len)
+      HIPCHK(poly_prefix_product_multi((const Fr* const*)zl.data(), zs.data(), NST, len, pk.scr, pk.scr_len, st));
+    // the slab's product of the rows that feed z (factors below n - bf - 1)
+    const size_t hc = std::min(phi, n - (size_t)bf - 1);
+    std::vector<Fr> tp(NST, Fr::one());
+    if (hc > plo)
+      for (int i = 0; i < NST; i++)
+        HIPCHK(hipMemcpyAsync(&tp[i], all_z[i] + hc - 1, sizeof(Fr), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<Fr> allp;
+    RCCHK(spmd_allgather_fr(tp, &allp));
+    std::vector<Fr> lzp(NST);  // z at this slab's first row = z_0 * (the slabs below)
+    for (int ci = 0; ci < ncirc; ci++) {
+      Fr lz = Fr::one();
+      for (int s = 0; s < pk.nsets; s++) {
+        const int i = ci * pk.nsets + s;
+        Fr below = Fr::one(), all = Fr::one();
+        for (int r = 0; r < Wsp; r++) {
+          if (r < me) below = below * allp[(size_t)r * NST + i];
+          all = all * allp[(size_t)r * NST + i];
+        }
+        lzp[i] = lz * below;
+        lz = lz * all;
+      }
+    }
+    if (!pk.perm_lz || pk.perm_lz_len < (size_t)NST) {
+      PALLOC(pk.pool, pk.perm_lz, NST);
+      pk.perm_lz_len = (size_t)NST;
+    }
+    HIPCHK(hipMemcpyAsync(pk.perm_lz, lzp.data(), NST * sizeof(Fr), hipMemcpyHostToDevice, st));
+    for (int i = 0; i < NST; i++) {
+      Fr* blind_rows = perm_blind.data() + (size_t)i * bf;
+      for (int q = 0; q < bf; q++) blind_rows[q] = rng.random_fr();
+      (void)rng.random_fr();  // blind
+      HIPCHK(hipMemcpyAsync(pk.small, blind_rows, bf * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(perm_z_assemble(all_z_lag[i], n, bf, all_z[i], pk.perm_lz + i, pk.small, st, plo, phi));
+    }
+    HIPCHK(hipStreamSynchronize(st));  // lzp (host) was read
+    RCCHK(commit_launch_batch(d, prm, (const Fr* const*)all_z_lag.data(), NST, n, SRS_LAGRANGE, st, perm_tk.data()));
+    // each set's owner gathers its column, then transforms and distributes it
+    std::vector<int> own(NST);
+    for (int i = 0; i < NST; i++) own[i] = (tr_next + i) % Wsp;
+    tr_next += NST;
+    RCCHK(gather_to_owners(pk, all_z_lag, own, prm.n, st));
+    RCCHK(xform(std::vector<const Fr*>(all_z_lag.begin(), all_z_lag.end()), all_z, all_z_coset, &own));
+  }
+  if (!perm_slab) {
     // every set's denominators (into z_lag), one batched inversion over all circuits'
     // sets (z as its scratch until the iNTT fills it), then per set numerators, scan and z
     for (int ci = 0; ci < ncirc; ci++)
@@ -2204,10 +2531,9 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
           RCCHK(commit_launch(d, prm, w.z_lag[s], n, SRS_LAGRANGE, st, &perm_tk[(size_t)ci * pk.nsets + s]));
       }
     }
-    if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, (const Fr* const*)all_z_lag.data(), all_z.data(), NST, st));
-    RCCHK(ext_cosets(d, pk, (const Fr* const*)all_z.data(), all_z_coset.data(), NST, st));
+    RCCHK(xform(std::vector<const Fr*>(all_z_lag.begin(), all_z_lag.end()), all_z, all_z_coset, nullptr));
   }
-  if (perm_batched)
+  if (perm_batched && !perm_slab)
     RCCHK(commit_launch_batch(d, prm, (const Fr* const*)all_z_lag.data(), NST, n, SRS_LAGRANGE, st, perm_tk.data()));
   clk.mark("permutation products");
   // ---- lookup products (lookup/prover.rs:182-325), every circuit's, then shuffle
@@ -2282,10 +2608,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         HIPCHK(shuffle_prod_num(pk.tmp_a, gamma, pk.mod, n, st));
         RCCHK(finish_z(pk.mod, w->sh_z[s], w->sh_z_poly[s], w->sh_zc[s], false, true, true));
       }
-    if (!z_lags.empty()) {
-      if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, z_lags.data(), z_polys.data(), (int)z_lags.size(), st));
-      RCCHK(ext_cosets(d, pk, (const Fr* const*)z_polys.data(), z_cosets.data(), (int)z_lags.size(), st));
-    }
+    RCCHK(xform(z_lags, z_polys, z_cosets, nullptr));
     // product commitments: every circuit's lookups, then every circuit's shuffles
     std::vector<const Fr*> zs;
     for (CircuitWs* w : W) zs.insert(zs.end(), w->lk_z.begin(), w->lk_z.end());
@@ -2294,7 +2617,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     if (lz_wide) {
       RCCHK(commit_launch_owned(d, prm, zs.data(), lk_owner_all.data(), NLT, n, SRS_LAGRANGE, st, zt.data()));
       if (NSH) RCCHK(commit_launch_batch(d, prm, zs.data() + NLT, NSH, n, SRS_LAGRANGE, st, zt.data() + NLT));
-      RCCHK(colshard_distribute(d, pk, lkz_lag, lkz_poly, lkz_cst, lk_owner_all, st));
+      RCCHK(xform(lkz_lag, lkz_poly, lkz_cst, &lk_owner_all));
     } else if (!zs.empty()) {
       RCCHK(commit_launch_batch(d, prm, zs.data(), (int)zs.size(), n, SRS_LAGRANGE, st, zt.data()));
     }
@@ -2431,15 +2754,22 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         a.acc_in = ci > 0 ? slot : nullptr;
         a.divide = ci + 1 == ncirc;
         a.out = slot;
+        if (pieces) {  // this rank's rows of the sub-coset
+          a.row0 = pk.sub_lo;
+          a.rows = pk.sub_hi - pk.sub_lo;
+        }
         HIPCHK(evaluate_h(a, st));
       }
     }
     if (h_slabs) {
+      if (pieces) RCCHK(h_gather_pieces(pk, st));
       RCCHK(h_by_slabs(d, pk, sl, st));
     } else {
       HIPCHK(hipStreamSynchronize(st));
       for (uint64_t t = 0; t < (1ull << e); t++)
-        if (g_spmd.bcast(g_spmd.ctx, pk.h_gather + t * n, n * sizeof(Fr), (int)(t % (uint64_t)g_spmd.world)) != 0)
+        if (spmd_timed(3, n * sizeof(Fr), [&] {
+              return g_spmd.bcast(g_spmd.ctx, pk.h_gather + t * n, n * sizeof(Fr), (int)(t % (uint64_t)g_spmd.world));
+            }) != 0)
           return fail(H2G_ERR_STATE, "spmd transport: broadcast of sub-coset " + std::to_string(t) + " failed");
       HIPCHK(subcoset_scatter(pk.h_gather, pk.h_ext, n, e, st));
     }
@@ -3584,6 +3914,31 @@ int h2g_create_proof_multi(uint64_t params, uint64_t pk, const h2g_prove_inputs*
   return create_proof_entry(d, params, pk, in, proof, proof_cap, proof_len);
 }
 
+// a ChaCha20Rng::from_seed (rand_chacha 0.3) behind the h2g_rng callbacks: the RngCore
+// a Rust host passes to create_proof, here native -- the caller-RNG path of
+// h2g_create_proof_multi (no early vanishing commitment) with the seeded path's bytes
+std::map<uint64_t, std::unique_ptr<ChaChaRng>> g_rngs;
+int rng_fill_cb(void* ctx, uint8_t* out, size_t len) {
+  static_cast<ChaChaRng*>(ctx)->fill(out, len);
+  return 0;
+}
+int h2g_rng_chacha20(const uint8_t seed[32], h2g_rng* out, uint64_t* handle) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!seed || !out || !handle) return fail(H2G_ERR_ARG, "rng_chacha20: null argument");
+  auto r = std::make_unique<ChaChaRng>(seed);
+  out->ctx = r.get();
+  out->fill_bytes = rng_fill_cb;
+  out->random_fr = nullptr;
+  *handle = g_next_handle++;
+  g_rngs[*handle] = std::move(r);
+  return H2G_OK;
+}
+int h2g_rng_free(uint64_t handle) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!g_rngs.erase(handle)) return fail(H2G_ERR_HANDLE, "rng_free: unknown handle");
+  return H2G_OK;
+}
+
 int h2g_last_challenges(uint64_t* out, int max, int* count) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (!count) return fail(H2G_ERR_ARG, "last_challenges: null count");
@@ -3617,6 +3972,17 @@ int h2g_spmd_set_weights(const uint32_t* weights, int world) {
     pre.push_back(pre.back() + weights[r]);
   }
   g_spmd_wprefix = pre;
+  return H2G_OK;
+}
+
+int h2g_spmd_stats(double* out, int max, int reset) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  for (int k = 0; k < 4; k++) {
+    const double v[3] = {g_spmd_stats.ms[k], (double)g_spmd_stats.calls[k], (double)g_spmd_stats.bytes[k]};
+    for (int j = 0; j < 3; j++)
+      if (out && 3 * k + j < max) out[3 * k + j] = v[j];
+  }
+  if (reset) g_spmd_stats = SpmdStats{};
   return H2G_OK;
 }
 
@@ -3709,6 +4075,15 @@ int h2g_comm_init(const uint8_t id[256], int world, int rank) {
   NEED_DEV_P();
   if (!id) return fail(H2G_ERR_ARG, "comm_init: null id");
   return comm_init(id, world, rank);
+}
+
+int h2g_comm_info(int32_t* rccl_count, int32_t* rccl_rank) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  int c = 0, r = -1;
+  RCCHK(comm_rccl_info(&c, &r));
+  if (rccl_count) *rccl_count = c;
+  if (rccl_rank) *rccl_rank = r;
+  return H2G_OK;
 }
 
 int h2g_comm_destroy(void) {

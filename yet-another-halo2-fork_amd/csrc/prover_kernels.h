@@ -23,12 +23,14 @@ struct PermCols {
 // out[r] = (init ? 1 : out[r]) * prod_j (beta * sigma_j[r] + gamma + v_j[r])
 hipError_t perm_denominators(Fr* out, size_t n, const PermCols& c, const Fr& beta, const Fr& gamma, bool init,
                              hipStream_t st);
-// mod[r] *= prod_j (beta * delta^j * omega^r + gamma + v_j[r])
+// mod[r] *= prod_j (beta * delta^j * omega^(r0 + r) + gamma + v_j[r])  (r < n; r0: the rows' offset)
 hipError_t perm_numerators(Fr* mod, size_t n, const PermCols& c, const Fr& gamma, const PowTable& omega,
-                           hipStream_t st);
-// z[0] = *last_z, z[i] = *last_z * prefix[i - 1] for 0 < i < n - bf; z[n-bf..n) = blind_rows[0..bf)
+                           hipStream_t st, size_t r0 = 0);
+// z[0] = *last_z, z[i] = *last_z * prefix[i - 1] for 0 < i < n - bf; z[n-bf..n) = blind_rows[0..bf).
+// Rows [lo, hi) only: z[lo] = *last_z (a slab's running product starts over: *last_z then
+// carries the product of the rows below it), z[i] = *last_z * prefix[i - 1] above
 hipError_t perm_z_assemble(Fr* z, size_t n, int bf, const Fr* prefix, const Fr* last_z, const Fr* blind_rows,
-                           hipStream_t st);
+                           hipStream_t st, size_t lo = 0, size_t hi = ~(size_t)0);
 
 // ---- vanishing argument: random polynomial (vanishing/prover.rs:57-81) ----
 // out[i] = Fr::random(ChaCha20Rng(seed_t)) for the i - off[t]'th draw of chunk t, i in [lo, hi)
@@ -73,6 +75,9 @@ struct EvalHArgs {
   Fr beta, gamma, y, delta_start, delta;
   PowTable ext_omega;
   uint64_t ext = 0, rot_scale = 0;
+  // rows [row0, row0 + rows) only (rows = 0: all ext rows); columns, l0 / l_last / l_active,
+  // sigma, t_evals and out stay indexed by the row itself
+  uint64_t row0 = 0, rows = 0;
   int last_rot = 0;
   const Fr* t_evals = nullptr;
   uint64_t t_mask = 0;
@@ -90,6 +95,13 @@ hipError_t subcoset_twist(const Fr* src, Fr* dst, size_t n, const PowTable& eo, 
                           hipStream_t st);
 hipError_t subcoset_gather(const Fr* full, Fr* out, size_t n, uint64_t t, int e, hipStream_t st);
 hipError_t subcoset_scatter(const Fr* subs, Fr* ext, size_t n, int e, hipStream_t st);
+// dst[i] = src[i] for i < len of every segment (device array of nseg), one launch
+struct CopySeg {
+  const Fr* src;
+  Fr* dst;
+  uint64_t len;
+};
+hipError_t copy_segments(const CopySeg* d_segs, int nseg, uint64_t max_len, hipStream_t st);
 int evaluate_h_max_slots();
 // SPMD: this rank's slab [lo, lo + cnt) of the h pieces (out[p n + j], p < np) from the E
 // sub-cosets' folded coefficients F_t (recv + idx[t] cnt); coef: np x E device matrix

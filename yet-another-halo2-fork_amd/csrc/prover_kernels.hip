@@ -14,6 +14,8 @@
 //
 // Everything here is integer modular arithmetic on 32-byte Montgomery elements;
 // elementwise kernels are HBM-streaming grid-stride loops with 16-byte accesses.
+#include <algorithm>
+
 #include "fr_io.h"
 #include "poly.h"
 #include "prover_kernels.h"
@@ -51,9 +53,9 @@ hipError_t perm_denominators(Fr* out, size_t n, const PermCols& c, const Fr& bet
 }
 
 __global__ void __launch_bounds__(KT) perm_num_kernel(Fr* __restrict__ mod, size_t n, PermCols c, Fr gamma,
-                                                      PowTable om) {
+                                                      PowTable om, size_t r0) {
   for (size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x; r < n; r += (size_t)gridDim.x * blockDim.x) {
-    const Fr w = pw(om, r);
+    const Fr w = pw(om, r0 + r);
     Fr acc = ldf(mod + r);
     for (int j = 0; j < c.m; j++) acc = acc * (c.beta_delta[j] * w + gamma + ldf(c.v[j] + r));
     stf(mod + r, acc);
@@ -61,27 +63,32 @@ __global__ void __launch_bounds__(KT) perm_num_kernel(Fr* __restrict__ mod, size
 }
 
 hipError_t perm_numerators(Fr* mod, size_t n, const PermCols& c, const Fr& gamma, const PowTable& omega,
-                           hipStream_t st) {
-  hipLaunchKernelGGL(perm_num_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, mod, n, c, gamma, omega);
+                           hipStream_t st, size_t r0) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(perm_num_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, mod, n, c, gamma, omega, r0);
   return hipGetLastError();
 }
 
 __global__ void __launch_bounds__(KT) perm_z_kernel(Fr* __restrict__ z, size_t n, int bf, const Fr* __restrict__ pre,
-                                                    const Fr* __restrict__ last_z, const Fr* __restrict__ blind) {
+                                                    const Fr* __restrict__ last_z, const Fr* __restrict__ blind,
+                                                    size_t lo, size_t hi) {
   const Fr lz = ldf(last_z);
   const size_t u = n - (size_t)bf;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+  for (size_t i = lo + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < hi; i += (size_t)gridDim.x * blockDim.x) {
     Fr v;
-    if (i == 0) v = lz;
-    else if (i < u) v = lz * ldf(pre + i - 1);
-    else v = ldf(blind + (i - u));
+    if (i >= u) v = ldf(blind + (i - u));
+    else if (i == lo) v = lz;
+    else v = lz * ldf(pre + i - 1);
     stf(z + i, v);
   }
 }
 
 hipError_t perm_z_assemble(Fr* z, size_t n, int bf, const Fr* prefix, const Fr* last_z, const Fr* blind_rows,
-                           hipStream_t st) {
-  hipLaunchKernelGGL(perm_z_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, z, n, bf, prefix, last_z, blind_rows);
+                           hipStream_t st, size_t lo, size_t hi) {
+  if (hi > n) hi = n;
+  if (lo >= hi) return hipSuccess;
+  hipLaunchKernelGGL(perm_z_kernel, dim3(grid_1d(hi - lo)), dim3(KT), 0, st, z, n, bf, prefix, last_z, blind_rows,
+                     lo, hi);
   return hipGetLastError();
 }
 
@@ -158,7 +165,8 @@ __global__ void __launch_bounds__(EH_T) evaluate_h_kernel(EvalHArgs a) {
   Fr* sl = reinterpret_cast<Fr*>(eh_lds);
   const int lane = threadIdx.x;
   const uint64_t emask = a.ext - 1;
-  for (uint64_t idx = blockIdx.x * (uint64_t)EH_T + lane; idx < a.ext; idx += (uint64_t)gridDim.x * EH_T) {
+  const uint64_t rend = a.rows ? a.row0 + a.rows : a.ext;
+  for (uint64_t idx = a.row0 + blockIdx.x * (uint64_t)EH_T + lane; idx < rend; idx += (uint64_t)gridDim.x * EH_T) {
     Fr acc = run_prog(a.prog, a.gates, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, a.y, sl, lane,
                       a.acc_in ? ldf(a.acc_in + idx) : Fr::zero());
     const Fr l0 = ldf(a.l0 + idx);
@@ -228,7 +236,7 @@ __global__ void __launch_bounds__(EH_T) evaluate_h_kernel(EvalHArgs a) {
 hipError_t evaluate_h(const EvalHArgs& a, hipStream_t st) {
   if (a.n_slots > EH_MAX_SLOTS) return hipErrorInvalidValue;
   const size_t lds = (size_t)(a.n_slots > 0 ? a.n_slots : 1) * EH_T * sizeof(Fr);
-  size_t blocks = (a.ext + EH_T - 1) / EH_T;
+  size_t blocks = ((a.rows ? a.rows : a.ext) + EH_T - 1) / EH_T;
   if (blocks > 256 * 32) blocks = 256 * 32;
   hipLaunchKernelGGL(evaluate_h_kernel, dim3((unsigned)blocks), dim3(EH_T), lds, st, a);
   return hipGetLastError();
@@ -790,6 +798,21 @@ __global__ void __launch_bounds__(KT) subcoset_gather_kernel(const Fr* __restric
 hipError_t subcoset_gather(const Fr* full, Fr* out, size_t n, uint64_t t, int e, hipStream_t st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(subcoset_gather_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, full, out, n, t, e);
+  return hipGetLastError();
+}
+// many device-to-device copies in one launch (SPMD pack / unpack of exchanged columns):
+// segment blockIdx.y, its elements strided over blockIdx.x
+__global__ void __launch_bounds__(KT) copy_segments_kernel(const CopySeg* __restrict__ segs) {
+  const CopySeg g = segs[blockIdx.y];
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < g.len; i += (uint64_t)gridDim.x * blockDim.x)
+    stf(g.dst + i, ldf(g.src + i));
+}
+hipError_t copy_segments(const CopySeg* d_segs, int nseg, uint64_t max_len, hipStream_t st) {
+  if (nseg <= 0 || max_len == 0) return hipSuccess;
+  const unsigned gx = (unsigned)std::min<uint64_t>((max_len + KT - 1) / KT, 256);
+  for (int s0 = 0; s0 < nseg; s0 += 65535)
+    hipLaunchKernelGGL(copy_segments_kernel, dim3(gx, (unsigned)std::min(65535, nseg - s0)), dim3(KT), 0, st,
+                       d_segs + s0);
   return hipGetLastError();
 }
 // ext[t + (m << e)] = subs[t n + m] for every t < 2^e: sub-coset slots back to row order

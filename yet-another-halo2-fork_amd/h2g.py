@@ -120,6 +120,10 @@ _SIGS = {
     "h2g_comm_spmd_install": ([I32], I32),
     "h2g_comm_spmd_uninstall": ([], I32),
     "h2g_spmd_set_column_owners": ([I32], I32),
+    "h2g_spmd_stats": ([ctypes.POINTER(ctypes.c_double), I32, I32], I32),
+    "h2g_rng_chacha20": ([ctypes.POINTER(ctypes.c_uint8), VP, U64P], I32),
+    "h2g_rng_free": ([U64], I32),
+    "h2g_comm_info": ([ctypes.POINTER(I32), ctypes.POINTER(I32)], I32),
 }
 
 TRANSCRIPTS = {"blake2b": 0, "keccak256": 1}  # Blake2bWrite / Keccak256Write (h2g_pk_set_transcript)
@@ -745,7 +749,8 @@ class ProvingKey:
         """create_proof(params, pk, circuits, instances, rng, transcript) over several circuits
         (halo2_proofs/src/plonk/prover.rs:19-36) -> proof bytes.  wits: one witness per circuit
         (advice, or -- with fills -- only the instance columns); rng: None = ChaCha20Rng::from_seed(
-        seed), else an object with fill_bytes(n) (and optionally random_fr()); fills: per-circuit
+        seed), "native" = the same generator behind the h2g_rng callbacks (h2g_rng_chacha20: the
+        caller-RNG path), else an object with fill_bytes(n) (and optionally random_fr()); fills: per-circuit
         fill(phase, challenges) -> {column: values} witness sources."""
         check(lib().h2g_pk_set_multiopen(self.handle, {"shplonk": 0, "gwc": 1}[multiopen]))
         check(lib().h2g_pk_set_transcript(self.handle, TRANSCRIPTS[transcript]))
@@ -781,7 +786,15 @@ class ProvingKey:
             src = WitnessSourceMulti(None, cfn)
             keep += [cb, cfn, src]
             inp.witness = ctypes.pointer(src)
-        if rng is not None:
+        native_rng = None
+        if isinstance(rng, str) and rng == "native":  # the library's ChaCha20Rng behind the callbacks
+            r = Rng()
+            native_rng = U64()
+            sd0 = (ctypes.c_uint8 * 32)(*bytes(seed))
+            check(lib().h2g_rng_chacha20(sd0, ctypes.byref(r), ctypes.byref(native_rng)))
+            keep += [r, sd0]
+            inp.rng = ctypes.pointer(r)
+        elif rng is not None:
             fb, fr = rng_callbacks(rng)
             r = Rng(None, fb, fr)
             keep += [fb, fr, r]
@@ -793,8 +806,12 @@ class ProvingKey:
                          + 16 * (len(circ.lookups) + len(circ.shuffles))) + 32 * 8 * circ.num_fixed
         buf = ctypes.create_string_buffer(cap)
         ln = SZ()
-        check(lib().h2g_create_proof_multi(self.params.handle, self.handle, ctypes.byref(inp), buf, cap,
-                                           ctypes.byref(ln)))
+        try:
+            check(lib().h2g_create_proof_multi(self.params.handle, self.handle, ctypes.byref(inp), buf, cap,
+                                               ctypes.byref(ln)))
+        finally:
+            if native_rng is not None:
+                lib().h2g_rng_free(native_rng.value)
         del keep
         return buf.raw[: ln.value]
 
@@ -939,6 +956,24 @@ def set_spmd_transport(world, rank=0, allgather=None, bcast=None, allgather_host
     t = SpmdTransport(None, world, rank, cb, cbb, cbh, cbx)
     _transport_keep = (t, cb, cbb, cbh, cbx, [])
     check(lib().h2g_set_spmd_transport(ctypes.byref(t)))
+
+
+SPMD_COLLECTIVES = ("msm_allgather", "host_allgather", "exchange", "bcast")
+
+
+def spmd_stats(reset=True):
+    """time / calls / bytes inside the SPMD transport per collective kind (h2g_spmd_stats)"""
+    out = (ctypes.c_double * 12)()
+    check(lib().h2g_spmd_stats(out, 12, 1 if reset else 0))
+    return {k: {"ms": out[3 * i], "calls": int(out[3 * i + 1]), "bytes": int(out[3 * i + 2])}
+            for i, k in enumerate(SPMD_COLLECTIVES)}
+
+
+def comm_info():
+    """(ncclCommCount, ncclCommUserRank) of the library's communicator, (0, -1) without one"""
+    c, r = I32(), I32()
+    check(lib().h2g_comm_info(ctypes.byref(c), ctypes.byref(r)))
+    return c.value, r.value
 
 
 def spmd_set_column_owners(on):

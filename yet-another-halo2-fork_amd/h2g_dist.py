@@ -42,14 +42,16 @@ def auto_owner_weight(world, extended_k, k):
     return 0.5 if world <= 2 * E else 0.1
 
 
-def owner_weights(world, extended_k, k, owner_weight=None, scale=100):
+def owner_weights(world, extended_k, k, owner_weight=None, scale=100, row_pieces=True):
     """SPMD slab weights that lighten the ranks owning extended-domain sub-cosets: with
     2^(extended_k - k) = E < world sub-cosets, ranks r < E evaluate h on a sub-coset each
     (its n-point coset NTTs, evaluate_h, the h interpolation) on top of their MSM slabs;
-    they get weight owner_weight (None: auto_owner_weight), the other ranks 1 (None when
-    every rank owns one)"""
+    they get weight owner_weight (None: auto_owner_weight), the other ranks 1.  None when
+    every rank owns one, and when world is a multiple of E with row pieces on (the
+    column-owner mode, h2g_spmd_set_column_owners): then every rank evaluates h on a row
+    piece of one sub-coset, the same share of the work"""
     E = 1 << (extended_k - k)
-    if world <= E:
+    if world <= E or (row_pieces and world % E == 0):
         return None
     if owner_weight is None:
         owner_weight = auto_owner_weight(world, extended_k, k)
