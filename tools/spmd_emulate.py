@@ -35,6 +35,7 @@ def _fq_mont_limbs(v):
     return [(m >> (64 * i)) & (2**64 - 1) for i in range(4)]
 
 
+COMMIT_TAG = 0x54494d4d4f433248  # prover.cpp kSpmdCommitTag
 G1_GEN_MONT = np.array(_fq_mont_limbs(1) + _fq_mont_limbs(2), dtype=np.uint64)  # (1, 2), Montgomery form
 
 
@@ -60,7 +61,15 @@ class FakeCollectives:
 
     def allgather_host(self, data):
         self.exchanges += 1
-        return [data] * self.world
+        out = [data] * self.world
+        w = np.frombuffer(bytes(data), dtype=np.uint64) if len(data) % 8 == 0 and len(data) >= 16 else None
+        if w is not None and int(w[0]) == COMMIT_TAG:  # a stage's commitments (commit_collect_all)
+            peer = w.copy()
+            rec = peer[2:].reshape(int(w[1]), -1)
+            rec[:, :8] = self.gen  # the peers' partials: the generator, as in allgather
+            rec[:, 8] = 0
+            out = [data if r == self.rank else peer.tobytes() for r in range(self.world)]
+        return out
 
     def exchange(self, d_send, send_bytes, d_recv, recv_bytes):
         self.xchg += 1

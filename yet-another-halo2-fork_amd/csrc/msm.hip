@@ -35,6 +35,22 @@
 
 namespace h2g {
 
+// Diagnostic build only (tools/build_variant.py ... -DH2G_RED_TIMING): wall-clock stamps
+// (s_memrealtime, 100 MHz) at the phase boundaries of the reduction kernels, read back
+// with h2g_dbg_red_ts (tools/red_timing.py)
+#ifdef H2G_RED_TIMING
+__device__ unsigned long long g_red_ts[64];
+#define RED_TS(cond, i)                                  \
+  do {                                                   \
+    if ((cond) && threadIdx.x == 0) g_red_ts[i] = wall_clock64(); \
+  } while (0)
+#else
+#define RED_TS(cond, i) \
+  do {                  \
+  } while (0)
+#endif
+
+
 static constexpr int MSM_THREADS = 256;
 static constexpr uint32_t MSM_SMALL = 8;  // fixup: max chunk pieces summed by one thread
 
@@ -107,9 +123,12 @@ __global__ void __launch_bounds__(MSM_THREADS)
 msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t nbt, uint32_t L,
                  G1xyzz* __restrict__ buckets,
                  MsmBigItem* __restrict__ items, uint4* __restrict__ multi, uint32_t* __restrict__ counters) {
+  H2G_SETPRIO(H2G_PRIO_RED);
   const uint32_t b = (blockIdx.x * blockDim.x + threadIdx.x) / Q;
   const uint32_t lane = threadIdx.x & 63;
   const bool lead = (threadIdx.x % Q) == 0;
+  RED_TS(blockIdx.x == 0, 20);
+  RED_TS(blockIdx.x == gridDim.x - 1, 22);
   uint32_t bs = 0, be = 0;
   if (b < nbt) {
     bs = koff[b];
@@ -166,6 +185,7 @@ __global__ void __launch_bounds__(MSM_THREADS)
 msm_big_item_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t L,
                     const MsmBigItem* __restrict__ items, const uint32_t* __restrict__ counters,
                     G1xyzz* __restrict__ partial, G1xyzz* __restrict__ buckets) {
+  H2G_SETPRIO(H2G_PRIO_RED);
   __shared__ G1xyzz sh[MSM_THREADS];
   const uint32_t nitems = counters[0];
   const uint32_t lane = threadIdx.x & 63, g = lane & (MSM_GROUP - 1);
@@ -211,6 +231,7 @@ static constexpr uint32_t COMBINE_LANE = 8;
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_big_combine_kernel(const uint4* __restrict__ multi, const uint32_t* __restrict__ counters,
                        const G1xyzz* __restrict__ partial, G1xyzz* __restrict__ buckets) {
+  H2G_SETPRIO(H2G_PRIO_RED);
   __shared__ G1xyzz sh[MSM_THREADS];
   const uint32_t nm = counters[1];
   const uint32_t lane = threadIdx.x & 63;
@@ -341,6 +362,7 @@ static constexpr int RG = H2G_MSM_RG;
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_rgroup_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, G1xyzz* __restrict__ S,
                   G1xyzz* __restrict__ R) {
+  H2G_SETPRIO(H2G_PRIO_RED);
   const uint32_t w = blockIdx.y;
   const uint32_t g = blockIdx.x * MSM_THREADS + threadIdx.x;
   if (g >= m1) return;
@@ -358,6 +380,7 @@ msm_rgroup_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, G1xyzz
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_rscale_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R, uint32_t m1,
                   G1xyzz* __restrict__ part, uint32_t nblk) {
+  H2G_SETPRIO(H2G_PRIO_RED);
   __shared__ G1xyzz sh[MSM_THREADS];
   const uint32_t w = blockIdx.y;
   const uint32_t g = blockIdx.x * MSM_THREADS + threadIdx.x;
@@ -381,6 +404,7 @@ msm_rscale_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R, ui
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_rgroup_q4_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, G1xyzz* __restrict__ S,
                      G1xyzz* __restrict__ R) {
+  H2G_SETPRIO(H2G_PRIO_RED);
   const uint32_t w = blockIdx.y;
   const uint32_t g = (blockIdx.x * MSM_THREADS + threadIdx.x) >> 2;
   if (g >= m1) return;  // the whole quad
@@ -402,6 +426,7 @@ static constexpr uint32_t Q4_GROUPS = MSM_THREADS / 4;  // quads per block
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_rscale_q4_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R, uint32_t m1,
                      G1xyzz* __restrict__ part, uint32_t nblk) {
+  H2G_SETPRIO(H2G_PRIO_RED);
   __shared__ G1xyzz sh[Q4_GROUPS];
   const uint32_t w = blockIdx.y, qi = threadIdx.x >> 2;
   const uint32_t g = blockIdx.x * Q4_GROUPS + qi;
@@ -424,6 +449,7 @@ msm_rscale_q4_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R,
 
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_rfinal_q4_kernel(const G1xyzz* __restrict__ part, uint32_t nblk, G1xyzz* __restrict__ windows) {
+  H2G_SETPRIO(H2G_PRIO_RED);
   __shared__ G1xyzz sh[Q4_GROUPS];
   const uint32_t w = blockIdx.x, qi = threadIdx.x >> 2;
   G1xyzz acc = G1xyzz::identity();
@@ -491,6 +517,7 @@ template <int Q, int LB, int RGP>
 __global__ void __launch_bounds__((1 << LB) * Q)
 msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, uint32_t nblk,
                         G1xyzz* __restrict__ planes) {
+  H2G_SETPRIO(H2G_PRIO_RED);
   constexpr uint32_t BPL = 1u << LB;
   __shared__ G1xyzz shT[BPL], shS[BPL];
   const uint32_t w = blockIdx.y, e = threadIdx.x / Q;
@@ -498,6 +525,9 @@ msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, 
   const uint32_t g = blockIdx.x * BPL + e;
   const size_t ps = (size_t)gridDim.y * nblk;  // stride between planes
   const G1xyzz* b = B + (size_t)w * NB;
+  const bool b0 = blockIdx.x == 0 && blockIdx.y == 0, bl = blockIdx.x == gridDim.x - 1 && blockIdx.y == 0;
+  RED_TS(b0, 0);
+  RED_TS(bl, 4);
   G1xyzz racc = G1xyzz::identity(), sacc = G1xyzz::identity();
   if (g < m1) {
 #pragma unroll
@@ -512,6 +542,7 @@ msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, 
     shS[e] = sacc;
   }
   __syncthreads();
+  RED_TS(b0, 1);
   // the R tree and a plain S tree side by side: elements [0, 2^(LB-1-k)(k+1)) fold R at
   // level k, the next 2^(LB-1-k) fold S
   for (int k = 0; k < LB; k++) {
@@ -528,10 +559,13 @@ msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, 
     }
     __syncthreads();
   }
+  RED_TS(b0, 2);
   if (lead && e < LB + 2) {
     const G1xyzz v = e == 0 ? shS[0] : (e <= LB ? shT[1u << (e - 1)] : shT[0]);
     planes[e * ps + (size_t)w * nblk + blockIdx.x] = v;
   }
+  RED_TS(b0, 3);
+  RED_TS(bl, 5);
 }
 
 // levels B and C, one launch (LB + 2 blocks per set): block q <= LB sums plane q over the
@@ -544,6 +578,7 @@ static constexpr int RPK_MAX = 9;  // block-index planes (LDS: 2^RPK_MAX points)
 __global__ void __launch_bounds__(1024)
 msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, int e0, G1xyzz* __restrict__ mid,
                       uint32_t* __restrict__ done, G1xyzz* __restrict__ windows) {
+  H2G_SETPRIO(H2G_PRIO_RED);
   __shared__ G1xyzz sh[1 << RPK_MAX];
   __shared__ uint32_t last;
   const uint32_t q = blockIdx.x, w = blockIdx.y, e = threadIdx.x >> 2, WB = gridDim.y;
@@ -551,24 +586,33 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, 
   const G1xyzz* in = planes + (size_t)q * WB * nblk + (size_t)w * nblk;
   int K = 0;
   while ((1u << K) < nblk) K++;
+  RED_TS(q == 0 && w == 0, 8);
+  RED_TS(q == (uint32_t)LB + 1 && w == 0, 11);
   if (q <= (uint32_t)LB) {
     G1xyzz acc = G1xyzz::identity();
     for (uint32_t i = e; i < nblk; i += 256) acc = xyzz_add_q4(acc, in[i]);
     if (lead) sh[e] = acc;
     __syncthreads();
-    for (uint32_t h = 128; h > 0; h >>= 1) {
+    RED_TS(q == 0 && w == 0, 9);
+    // the tree's levels above the filled entries would only add identities
+    uint32_t h0 = 1;
+    while (2 * h0 < (nblk < 256 ? nblk : 256)) h0 <<= 1;
+    for (uint32_t h = h0; h > 0; h >>= 1) {
       if (e < h) {
         const G1xyzz v = xyzz_add_q4(sh[e], sh[e + h]);
         if (lead) sh[e] = v;
       }
       __syncthreads();
     }
+    RED_TS(q == 0 && w == 0, 10);
     if (threadIdx.x == 0) mid[(size_t)q * WB + w] = sh[0];
   } else {
     for (uint32_t i = e; i < (1u << K); i += 256)
       if (lead) sh[i] = i < nblk ? in[i] : G1xyzz::identity();
     __syncthreads();
+    RED_TS(w == 0, 12);
     plane_fold<4>(sh, K, e, lead, 256);
+    RED_TS(w == 0, 13);
     if (lead && e < (uint32_t)K) mid[(size_t)(1 + LB + e) * WB + w] = sh[1u << e];
     if (threadIdx.x == 0) mid[(size_t)(1 + LB + K) * WB + w] = sh[0];  // T
   }
@@ -580,6 +624,7 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, 
   __syncthreads();
   if (!last) return;
   __threadfence();
+  RED_TS(w == 0, 14);
   const uint32_t np = (uint32_t)(LB + K);  // planes (<= 18)
   G1xyzz x = G1xyzz::identity();
   if (e < np) {
@@ -590,13 +635,17 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, 
   }
   if (lead && e < 64) sh[e] = x;
   __syncthreads();
-  for (uint32_t h = 32; h > 0; h >>= 1) {
+  RED_TS(w == 0, 15);
+  uint32_t h0 = 1;  // np + 1 <= 2 h0 terms
+  while (2 * h0 < np + 1) h0 <<= 1;
+  for (uint32_t h = h0; h > 0; h >>= 1) {
     if (e < h) {
       const G1xyzz v = xyzz_add_q4(sh[e], sh[e + h]);
       if (lead) sh[e] = v;
     }
     __syncthreads();
   }
+  RED_TS(w == 0, 16);
   if (threadIdx.x == 0) windows[w] = sh[0];
 }
 
@@ -626,6 +675,7 @@ __host__ __device__ G1Affine msm_combine_windows(const G1xyzz* windows, int W, i
 }
 
 __global__ void msm_final_kernel(const G1xyzz* __restrict__ windows, int W, int c, G1Affine* out) {
+  H2G_SETPRIO(H2G_PRIO_RED);
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   *out = msm_combine_windows(windows, W, c);
 }
@@ -680,6 +730,10 @@ uint32_t msm_chunk_len(size_t total, size_t nbt) {
 // vs 90.2-90.3 ms (profiles/r02/ab_q4/).  Quad fixup up to 2^15 buckets (2^16, the
 // 2^19-point slabs: the lane form is faster).
 static constexpr size_t RED_Q4_MAX = 32768;
+#ifndef H2G_PLANE_LB_SMALL  // A/B builds (tools/build_variant.py -DH2G_PLANE_LB_SMALL=8)
+#define H2G_PLANE_LB_SMALL 6
+#endif
+static constexpr int kSmallLB = H2G_PLANE_LB_SMALL;
 static constexpr uint32_t FIXUP_Q4_MAX = 32768;
 
 static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Affine* d_bases, size_t n, int c,
@@ -707,11 +761,18 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   // goes first (2^16 buckets: rgp = 1; 0.38 -> 0.33 ms at 2^19 points).  Larger sets: a
   // lane per group of 8 (the quads' 1.3x issue cost loses there: 0.62 -> 0.71 ms at 2^19
   // buckets; groups of 4: slower).
-  int rgp = 8, plane_q = 4;
-  const int plane_lb = 8;
+  // Small sets use blocks of 64 groups (256 threads, plane_lb = 6): a block's tree levels
+  // are issue-bound on its CU (a level's quads all add at once), so 1024-thread blocks of
+  // 256 groups left 4 waves per SIMD on few CUs (2^14 buckets: 64 CUs, ~13 us per level);
+  // 4x the blocks spread the same levels over the chip.  The block index then needs 2 more
+  // bits (<= RPK_MAX): at most 32768 groups per set.
+  int rgp = 8, plane_q = 4, plane_lb = 8;
   if ((size_t)NB * WB <= (1u << 18)) {
-    for (rgp = 1; rgp < 8; rgp *= 2)
-      if ((size_t)((NB + rgp - 1) / rgp) * WB <= 65536) break;
+    plane_lb = kSmallLB;
+    for (rgp = 1; rgp < 8; rgp *= 2) {
+      const size_t g = (NB + rgp - 1) / rgp;
+      if (g * WB <= 65536 && g <= ((size_t)1 << (RPK_MAX + kSmallLB))) break;
+    }
   } else {
     plane_q = 1;
   }
@@ -849,13 +910,13 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     if (plane_q == 1)
       hipLaunchKernelGGL((msm_rgroup_plane_kernel<1, 8, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
     else if (rgp == 1)
-      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 1>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, kSmallLB, 1>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
     else if (rgp == 2)
-      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 2>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, kSmallLB, 2>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
     else if (rgp == 4)
-      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 4>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, kSmallLB, 4>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
     else
-      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, 8, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+      hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, kSmallLB, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
     hipLaunchKernelGGL(msm_rplane_mid_kernel, dim3((unsigned)plane_lb + 2, (unsigned)WB), dim3(1024), 0, st,
                        (const G1xyzz*)planes, nblk_p, plane_lb, e0, mid, rdone, (G1xyzz*)ws->windows);
   } else {
@@ -881,6 +942,14 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
 #undef H2G_PHASE
   return hipSuccess;
 }
+
+#ifdef H2G_RED_TIMING
+extern "C" int h2g_dbg_red_ts(unsigned long long* out) {  // read, then clear
+  static const unsigned long long zero[64] = {};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_red_ts), sizeof(g_red_ts)) != hipSuccess) return 1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_red_ts), zero, sizeof(zero)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 hipError_t msm_run(const Fr* d_scalars, const G1Affine* d_bases, size_t n, MsmWorkspace* ws,
                    const MsmConfig& cfg, G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof) {

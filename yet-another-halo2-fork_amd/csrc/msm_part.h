@@ -8,6 +8,23 @@ namespace h2g {
 static constexpr int FB_MAX = 11;        // fine bits (keys per coarse bin <= 2^FB_MAX)
 static constexpr int COARSE_MAX = 2048;  // coarse bins
 
+// Wave priorities (s_setprio) of the MSM's short phases.  Inside a proof the two MSM
+// streams overlap: one MSM's partition, fixup and reduction share the SIMDs with the
+// other's accumulation, a VALU-bound kernel that keeps every SIMD's issue port busy.  The
+// reduction and fixup are latency-bound chains (one wave per SIMD, dependent point
+// additions) and the partition waits on memory; raised priority lets their few
+// instructions issue first while the accumulation's waves fill the remaining cycles.
+#ifndef H2G_PRIO_RED
+#define H2G_PRIO_RED 3
+#endif
+#ifndef H2G_PRIO_PART
+#define H2G_PRIO_PART 2
+#endif
+#define H2G_SETPRIO(p) \
+  do {                  \
+    if ((p) > 0) __builtin_amdgcn_s_setprio(p); \
+  } while (0)
+
 // Fixed-base windows have balanced widths: W = ceil(255 / c) windows covering the 255
 // bits signed digits need, the first 255 % W of them one bit wider (<= c).  Uniform
 // c-bit windows leave a short top window (255 - c (W - 1) bits: 7 at c = 19, W = 14)

@@ -73,6 +73,7 @@ __device__ __forceinline__ void scalar_digits(const MsmScalarList& list, int c, 
 __global__ void __launch_bounds__(PT)
 msm_coarse_hist_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride, int fb,
                        uint32_t ncoarse, uint32_t* __restrict__ ccount, MsmZero z) {
+  H2G_SETPRIO(H2G_PRIO_PART);
   __shared__ uint32_t h[COARSE_MAX];
   {  // the pipeline's other per-MSM zeroing (no separate fills)
     const size_t tid = (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * PT + threadIdx.x;
@@ -96,6 +97,7 @@ msm_coarse_hist_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, 
 __global__ void __launch_bounds__(1024)
 msm_scan_kernel(uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__ off,
                 uint32_t* __restrict__ cursor, uint32_t* __restrict__ total, bool clear) {
+  H2G_SETPRIO(H2G_PRIO_PART);
   __shared__ uint32_t part[1024];
   const uint32_t per = (len + 1023) / 1024;
   const uint32_t lo = threadIdx.x * per, hi = lo + per < len ? lo + per : len;
@@ -124,6 +126,7 @@ msm_scan_kernel(uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__
 __global__ void __launch_bounds__(1024)
 msm_scan_block_kernel(uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __restrict__ off,
                       uint32_t* __restrict__ bsum) {
+  H2G_SETPRIO(H2G_PRIO_PART);
   __shared__ uint32_t part[1024];
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
   const uint32_t v0 = i < len ? cnt[i] : 0;
@@ -144,6 +147,7 @@ msm_scan_block_kernel(uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __rest
 __global__ void __launch_bounds__(1024)
 msm_scan_add_kernel(uint32_t* __restrict__ off, uint32_t len, const uint32_t* __restrict__ boff,
                     uint32_t* __restrict__ cursor, const uint32_t* __restrict__ d_total) {
+  H2G_SETPRIO(H2G_PRIO_PART);
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
   if (i == 0) off[len] = *d_total;
   if (i >= len) return;
@@ -157,6 +161,7 @@ msm_scan_add_kernel(uint32_t* __restrict__ off, uint32_t len, const uint32_t* __
 __global__ void __launch_bounds__(PT)
 msm_coarse_scatter_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride, int fb,
                           uint32_t ncoarse, uint32_t* __restrict__ ccursor, uint64_t* __restrict__ out) {
+  H2G_SETPRIO(H2G_PRIO_PART);
   __shared__ uint32_t cnt[COARSE_MAX], base[COARSE_MAX];
   for (uint32_t t = threadIdx.x; t < ncoarse; t += PT) cnt[t] = 0;
   __syncthreads();
@@ -198,6 +203,7 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t T) {
 __global__ void __launch_bounds__(FT)
 msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb, uint32_t tiles,
                      uint32_t* __restrict__ kcount) {
+  H2G_SETPRIO(H2G_PRIO_PART);
   __shared__ uint32_t h[1 << FB_MAX];
   const uint32_t total = *d_total;
   const uint32_t lo = xcd_tile(blockIdx.x, tiles) * FTILE;
@@ -224,6 +230,7 @@ msm_fine_hist_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict
 __global__ void __launch_bounds__(FT)
 msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
                         uint32_t tiles, uint32_t* __restrict__ kcursor, uint32_t* __restrict__ out) {
+  H2G_SETPRIO(H2G_PRIO_PART);
   __shared__ uint32_t cnt[1 << FB_MAX], base[1 << FB_MAX];
   const uint32_t total = *d_total;
   const uint32_t lo = xcd_tile(blockIdx.x, tiles) * FTILE;
@@ -263,6 +270,9 @@ msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restr
 // key order -- a wave's stores are runs of each key's share of the tile instead of 64
 // scattered writes, and the per-key global atomics drop 4x with the larger tile.  Keys
 // outside the window (tiles straddling more than two bins) take a global atomic each.
+#ifndef H2G_FSTAGE_MAX
+#define H2G_FSTAGE_MAX (1ull << 25)
+#endif
 static constexpr int SW_T = 512;
 static constexpr int SW_PER = 16;
 static constexpr uint32_t SW_TILE = (uint32_t)SW_T * SW_PER;
@@ -294,6 +304,7 @@ __device__ __forceinline__ uint32_t sw_block_scan(uint32_t v, uint32_t* wsum, ui
 __global__ void __launch_bounds__(SW_T)
 msm_fine_hist_staged_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
                             uint32_t tiles, uint32_t* __restrict__ kcount) {
+  H2G_SETPRIO(H2G_PRIO_PART);
   __shared__ uint32_t h[SW_LK];
   const uint32_t total = *d_total;
   const uint32_t lo = xcd_tile(blockIdx.x, tiles) * SW_TILE;
@@ -318,6 +329,7 @@ msm_fine_hist_staged_kernel(const uint64_t* __restrict__ in, const uint32_t* __r
 __global__ void __launch_bounds__(SW_T)
 msm_fine_scatter_staged_kernel(const uint64_t* __restrict__ in, const uint32_t* __restrict__ d_total, int fb,
                                uint32_t tiles, uint32_t* __restrict__ kcursor, uint32_t* __restrict__ out) {
+  H2G_SETPRIO(H2G_PRIO_PART);
   __shared__ uint64_t stage[SW_TILE];
   __shared__ uint32_t cnt[SW_LK], loff[SW_LK], gb[SW_LK];
   __shared__ uint32_t wsum[SW_T / 64];
@@ -373,7 +385,7 @@ msm_fine_scatter_staged_kernel(const uint64_t* __restrict__ in, const uint32_t* 
 }
 
 hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* prof) {
-  const bool fstage = a.total < (1ull << 25);  // the staged fine pass (above)
+  const bool fstage = a.total < (uint64_t)H2G_FSTAGE_MAX;  // the staged fine pass (above)
   {  // round 1: coarse bins straight from the scalars
     const dim3 g((unsigned)((a.n + PT - 1) / PT), (unsigned)a.nbatch, (unsigned)((a.W + PWG - 1) / PWG));
     hipLaunchKernelGGL(msm_coarse_hist_kernel, g, dim3(PT), 0, st, a.list, a.n, a.c, a.W, a.NB, a.fixed, a.stride,

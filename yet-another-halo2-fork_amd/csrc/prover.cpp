@@ -481,6 +481,70 @@ int commit_collect(Device* d, MsmTicket* t, G1Affine* out) {
   *out = xyzz_to_affine(acc);
   return H2G_OK;
 }
+// The commitments of one stage together (the stage's MSMs were all launched before the
+// first is needed): with SPMD and a host all-gather, every rank's partials of all of them
+// travel in ONE all-gather (nb x H2G_SPMD_WORDS words per rank, one digest check), not one
+// collective per MSM -- a many-column proof at 8 ranks made ~90 of them, each a host
+// round trip of the ranks' streams.  The sums are the same, in rank order, as
+// commit_collect's; the transcript writes follow in list order.
+constexpr uint64_t kSpmdCommitTag = 0x54494d4d4f433248ull;  // "H2COMMIT"
+int commit_collect_all(Device* d, MsmTicket* const* t, int nb, G1Affine* out) {
+  bool spmd_all = g_spmd.world > 1 && g_spmd.allgather_host && nb > 1;
+  for (int i = 0; i < nb; i++) spmd_all &= t[i]->shard_seq >= 0;
+  if (!spmd_all) {
+    for (int i = 0; i < nb; i++) RCCHK(commit_collect(d, t[i], &out[i]));
+    return H2G_OK;
+  }
+  for (int i = 0; i < nb; i++) {
+    if (t[i]->remote) {
+      std::memset(&out[i], 0, sizeof(G1Affine));
+      t[i]->remote = false;
+    } else {
+      RCCHK(msm_collect(d, t[i], reinterpret_cast<uint64_t*>(&out[i])));
+    }
+  }
+  const int W = g_spmd.world;
+  constexpr int SW = H2G_SPMD_WORDS;
+  // per rank: a 2-word header (tag, count -- lets a transport or a test harness recognise
+  // a commitment batch), then nb records of H2G_SPMD_WORDS words as in commit_collect
+  const size_t per = 2 + (size_t)nb * SW;
+  std::vector<uint64_t> mine(per), all((size_t)W * per);
+  mine[0] = kSpmdCommitTag;
+  mine[1] = (uint64_t)nb;
+  uint64_t dg[4];
+  spmd_digest(dg);
+  for (int i = 0; i < nb; i++) {
+    uint64_t* m = &mine[2 + (size_t)i * SW];
+    std::memcpy(m, &out[i], 64);
+    m[8] = out[i].is_identity() ? 1 : 0;
+    std::memcpy(m + 9, dg, 32);
+  }
+  const int64_t seq0 = t[0]->shard_seq;
+  const size_t bytes = mine.size() * 8;
+  if (spmd_timed(0, bytes * (W + 1), [&] { return g_spmd.allgather_host(g_spmd.ctx, mine.data(), bytes, all.data()); }) != 0)
+    return fail(H2G_ERR_STATE, "spmd transport: all-gather of MSMs " + std::to_string(seq0) + ".. failed");
+  for (int r = 0; r < W; r++)
+    for (int i = 0; i < nb; i++)
+      if (all[(size_t)r * per] != kSpmdCommitTag || all[(size_t)r * per + 1] != (uint64_t)nb ||
+          std::memcmp(&all[(size_t)r * per + 2 + (size_t)i * SW + 9], dg, 32) != 0)
+        return fail(H2G_ERR_STATE, "spmd: rank " + std::to_string(r) + " diverged from rank " +
+                                       std::to_string(g_spmd.rank) + " before MSM " + std::to_string(seq0 + i) +
+                                       " (different witness, instances, key or RNG draws on the ranks)");
+  for (int i = 0; i < nb; i++) {
+    t[i]->shard_seq = -1;
+    G1xyzz acc = G1xyzz::identity();
+    for (int r = 0; r < W; r++) {
+      const uint64_t* a = &all[(size_t)r * per + 2 + (size_t)i * SW];
+      if (a[8]) continue;
+      G1Affine p;
+      std::memcpy(&p, a, 64);
+      acc = xyzz_madd(acc, p);
+    }
+    out[i] = xyzz_to_affine(acc);
+  }
+  return H2G_OK;
+}
+
 // Several commitments against one base set as batched MSMs (msm_run_fixed_batch): one
 // sort, accumulation and reduction serve a group, so the latency-bound reduction is paid
 // once per group instead of once per commitment -- what circuits with many columns at
@@ -1914,6 +1978,13 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     if (!tr.write_point(p)) return fail(H2G_ERR_ARG, "cannot write points at infinity to the transcript");
     return H2G_OK;
   };
+  // a stage's commitments: collected together (one SPMD all-gather), written in order
+  auto collect_write = [&](const std::vector<MsmTicket*>& tks) -> int {
+    std::vector<G1Affine> cms(tks.size());
+    RCCHK(commit_collect_all(d, tks.data(), (int)tks.size(), cms.data()));
+    for (const G1Affine& cm : cms) RCCHK(write_point(cm));
+    return H2G_OK;
+  };
   auto rng_ok = [&]() -> int { return rng.failed() ? fail(H2G_ERR_ARG, "create_proof: the caller's RNG failed") : H2G_OK; };
 
   // ---- vk.hash_into + every circuit's instances (prover.rs:187-271; KZG: QUERY_INSTANCE = false)
@@ -2112,10 +2183,10 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     }
     if (ph == 0 && early_van) RCCHK(launch_van_early());
     if (ph == 0) clk.mark("upload+instances");
-    for (auto& t : tk) {  // circuit by circuit, column by column
-      G1Affine cm;
-      RCCHK(commit_collect(d, &t, &cm));
-      RCCHK(write_point(cm));
+    {  // circuit by circuit, column by column
+      std::vector<MsmTicket*> tl;
+      for (auto& t : tk) tl.push_back(&t);
+      RCCHK(collect_write(tl));
     }
     RCCHK(rng_ok());
     for (int i = 0; i < NCH; i++)
@@ -2351,10 +2422,10 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       RCCHK(xform(perm_cols, perm_polys, perm_cosets, nullptr));
     }
     lk_shard = lk_wide;
-    for (int i = 0; i < 2 * NLT; i++) {
-      G1Affine cm;
-      RCCHK(commit_collect(d, &tk[i], &cm));
-      RCCHK(write_point(cm));
+    {
+      std::vector<MsmTicket*> tl;
+      for (int i = 0; i < 2 * NLT; i++) tl.push_back(&tk[i]);
+      RCCHK(collect_write(tl));
     }
     RCCHK(rng_ok());
   }
@@ -2656,16 +2727,12 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   // vanishing MSMs (the advice went to coefficients and cosets under its own MSMs)
   for (CircuitWs* w : W)
     RCCHK(ext_cosets(d, pk, (const Fr* const*)w->inst_poly.data(), w->inst_coset.data(), pk.I, st));
-  for (auto* tks : {&perm_tk, &lkz_tk, &shz_tk})
-    for (auto& t : *tks) {
-      G1Affine cm;
-      RCCHK(commit_collect(d, &t, &cm));
-      RCCHK(write_point(cm));
-    }
   {
-    G1Affine cm;
-    RCCHK(commit_collect(d, &van_tk, &cm));
-    RCCHK(write_point(cm));
+    std::vector<MsmTicket*> tl;
+    for (auto* tks : {&perm_tk, &lkz_tk, &shz_tk})
+      for (auto& t : *tks) tl.push_back(&t);
+    tl.push_back(&van_tk);
+    RCCHK(collect_write(tl));
   }
   clk.mark("perm+vanishing commits, cosets");
   const Fr y = tr.squeeze();
@@ -2787,11 +2854,9 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     std::vector<const Fr*> pieces(npieces);
     for (int p = 0; p < npieces; p++) pieces[p] = pk.h_coeff + (size_t)p * n;
     RCCHK(commit_launch_batch(d, prm, pieces.data(), npieces, n, SRS_G, st, tk.data()));
-    for (int p = 0; p < npieces; p++) {
-      G1Affine cm;
-      RCCHK(commit_collect(d, &tk[p], &cm));
-      RCCHK(write_point(cm));
-    }
+    std::vector<MsmTicket*> tl;
+    for (int p = 0; p < npieces; p++) tl.push_back(&tk[p]);
+    RCCHK(collect_write(tl));
   }
   clk.mark("h commit");
   const Fr x = tr.squeeze();
@@ -3003,10 +3068,10 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       tk.emplace_back();
       RCCHK(commit_launch(d, prm, pk.gwc_q[g], n - 1, SRS_G, st, &tk.back()));  // commit (kzg/commitment.rs:354-366)
     }
-    for (auto& t : tk) {
-      G1Affine cm;
-      RCCHK(commit_collect(d, &t, &cm));
-      RCCHK(write_point(cm));
+    {
+      std::vector<MsmTicket*> tl;
+      for (auto& t : tk) tl.push_back(&t);
+      RCCHK(collect_write(tl));
     }
     HIPCHK(hipStreamSynchronize(st));  // neg_evb (host) is read by the copies above
     clk.mark("gwc");
