@@ -348,7 +348,10 @@ const char* h2g_prover_stage_name(int i);
  * (one process per GPU over RCCL in yet-another-halo2-fork_amd/h2g_dist.py).
  *   launch : called once per MSM, in transcript order, after the scalars (n Fr,
  *            device pointer, valid until the matching collect) are complete;
- *            base_set 0 = params.g (commit), 1 = params.g_lagrange (commit_lagrange)
+ *            base_set 0 = params.g (commit), 1 = params.g_lagrange (commit_lagrange),
+ *            2 = the prefix sums P_i = L_0 + ... + L_i of g_lagrange (a lookup's permuted
+ *            columns, committed as sum_i (a_i - a_{i+1}) P_i: the same point, from
+ *            scalars that vanish inside the columns' runs of equal values)
  *   collect: the world - 1 partials of MSM `seq` (8 u64 affine each, is_identity flags)
  * Both return 0 on success; nonzero fails the proof with H2G_ERR_STATE. */
 typedef struct {

@@ -67,6 +67,9 @@ struct MsmFixedBase {
 int msm_choose_c_fixed(size_t n);
 hipError_t msm_fixed_base_build(const G1Affine* d_bases, size_t n, int c, MsmFixedBase* fb, hipStream_t st);
 void msm_fixed_base_free(MsmFixedBase* fb);
+// inclusive prefix sums of n affine points: out[i] = in[0] + ... + in[i] (setup; scratch
+// allocated and freed inside)
+hipError_t msm_prefix_points(const G1Affine* in, size_t n, G1Affine* out, hipStream_t st);
 // sum_{i < n} scalars[i] * bases[off + i]; leaves ws->windows[0] (ws->last_W = 1)
 hipError_t msm_run_fixed(const Fr* d_scalars, const MsmFixedBase& fb, size_t off, size_t n, MsmWorkspace* ws,
                          G1Affine* d_out, hipStream_t st, MsmPhaseEvents* prof = nullptr);

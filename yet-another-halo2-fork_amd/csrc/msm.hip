@@ -788,6 +788,14 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     size_t bytes;
   };
   const size_t icap = msm_big_items_cap(nchunks), mcap = msm_big_multi_cap(nchunks);
+  // bucket partition geometry: keys < nbt, fine bits fb, coarse bins nbt >> fb.  Fine bits
+  // (the fine pass's fan-out per tile): 10 -- 2x the coarse bins of 11 but half the
+  // per-tile key runs; interleaved on one box the k = 22 proof took 86.5-86.8 ms vs
+  // 86.8-87.3 ms at 11 (8, 9: slower coarse pass)
+  int key_bits = 1;
+  while ((1ull << key_bits) < (uint64_t)nbt) key_bits++;
+  int fb = key_bits < 10 ? key_bits : 10;
+  while (fb < FB_MAX && (((uint64_t)nbt + (1ull << fb) - 1) >> fb) > COARSE_MAX) fb++;
   const Need need[10] = {{&ws->ent, total * 8},
                          {&ws->vals_out, total * 4},
                          {&ws->item_bucket, icap * sizeof(MsmBigItem)},  // big-bucket items
@@ -817,14 +825,6 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   G1xyzz* rR = rS + (size_t)WB * m1;
   G1xyzz* rP = rR + (size_t)WB * m1;
 
-  // bucket partition geometry: keys < nbt, fine bits fb, coarse bins nbt >> fb
-  int key_bits = 1;
-  while ((1ull << key_bits) < (uint64_t)nbt) key_bits++;
-  // fine bits (the fine pass's fan-out per tile): 10 -- 2x the coarse bins of 11 but half
-  // the per-tile key runs and global cursor atomics of the fine scatter; interleaved on one
-  // box the k = 22 proof took 86.5-86.8 ms vs 86.8-87.3 ms at 11 (8, 9: slower coarse pass)
-  int fb = key_bits < 10 ? key_bits : 10;
-  while (fb < FB_MAX && (((uint64_t)nbt + (1ull << fb) - 1) >> fb) > COARSE_MAX) fb++;
   const uint32_t ncoarse = (uint32_t)(((uint64_t)nbt + (1ull << fb) - 1) >> fb);
   if (ncoarse > COARSE_MAX) return hipErrorInvalidValue;
   const uint32_t kblocks = (nbt + 1023) / 1024;
@@ -986,6 +986,58 @@ hipError_t msm_fixed_base_build(const G1Affine* d_bases, size_t n, int c, MsmFix
   hipLaunchKernelGGL(msm_precompute_kernel, dim3((unsigned)((n + MSM_THREADS - 1) / MSM_THREADS)), dim3(MSM_THREADS),
                      0, st, d_bases, n, W, n, fb->table);
   return hipGetLastError();
+}
+
+// prefix sums of points (the lookup commitments' prefix basis, prover.cpp): chunk scans of
+// PFX_C points per thread at two levels, a serial scan of the top level (<= 1024 sums at
+// 2^22 points), and the offsets added back
+static constexpr uint32_t PFX_C = 64;
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_prefix_chunks_kernel(const G1Affine* __restrict__ in, const G1xyzz* __restrict__ inx, size_t n,
+                         G1xyzz* __restrict__ run, G1xyzz* __restrict__ tot) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x, lo = t * PFX_C;
+  if (lo >= n) return;
+  const size_t hi = lo + PFX_C < n ? lo + PFX_C : n;
+  G1xyzz acc = G1xyzz::identity();
+  for (size_t i = lo; i < hi; i++) {
+    acc = inx ? xyzz_add(acc, inx[i]) : xyzz_madd(acc, in[i]);
+    run[i] = acc;
+  }
+  tot[t] = acc;
+}
+__global__ void msm_prefix_serial_kernel(G1xyzz* a, size_t m) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (size_t i = 1; i < m; i++) a[i] = xyzz_add(a[i - 1], a[i]);
+}
+// run[i] += tot[i / PFX_C - 1] (tot inclusive over the chunks); to affine into out if given
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_prefix_add_kernel(G1xyzz* __restrict__ run, size_t n, const G1xyzz* __restrict__ tot, G1Affine* __restrict__ out) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  G1xyzz v = run[i];
+  const size_t c = i / PFX_C;
+  if (c) v = xyzz_add(v, tot[c - 1]);
+  if (out) out[i] = xyzz_to_affine(v);
+  else run[i] = v;
+}
+hipError_t msm_prefix_points(const G1Affine* in, size_t n, G1Affine* out, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const size_t t1 = (n + PFX_C - 1) / PFX_C, t2 = (t1 + PFX_C - 1) / PFX_C;
+  G1xyzz* buf = nullptr;
+  H2G_TRY(hipMalloc(&buf, (n + 2 * t1 + t2) * sizeof(G1xyzz)));
+  G1xyzz *run1 = buf, *tot1 = run1 + n, *run2 = tot1 + t1, *tot2 = run2 + t1;
+  const unsigned T = MSM_THREADS;
+  auto grid = [&](size_t m) { return dim3((unsigned)((m + T - 1) / T)); };
+  hipLaunchKernelGGL(msm_prefix_chunks_kernel, grid(t1), dim3(T), 0, st, in, (const G1xyzz*)nullptr, n, run1, tot1);
+  hipLaunchKernelGGL(msm_prefix_chunks_kernel, grid(t2), dim3(T), 0, st, (const G1Affine*)nullptr,
+                     (const G1xyzz*)tot1, t1, run2, tot2);
+  hipLaunchKernelGGL(msm_prefix_serial_kernel, dim3(1), dim3(64), 0, st, tot2, t2);
+  hipLaunchKernelGGL(msm_prefix_add_kernel, grid(t1), dim3(T), 0, st, run2, t1, (const G1xyzz*)tot2, (G1Affine*)nullptr);
+  hipLaunchKernelGGL(msm_prefix_add_kernel, grid(n), dim3(T), 0, st, run1, n, (const G1xyzz*)run2, out);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(buf);
+  return e;
 }
 
 void msm_fixed_base_free(MsmFixedBase* fb) {

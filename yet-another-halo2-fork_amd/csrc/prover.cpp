@@ -63,6 +63,10 @@ struct Params {
   // sized for the slab length (h2g_params_set_slab)
   size_t slab_lo = 0, slab_hi = 0;
   MsmFixedBase sg, sgl;
+  // windows of the prefix-summed Lagrange basis (params_prefix; built on the first proof
+  // with lookups): 0 not built, 1 built
+  MsmFixedBase fgp;
+  int prefix_state = 0;
   // the G2 half of ParamsKZG (g2, s_g2 = [s] g2; verifier side, serialised with the params)
   bool has_g2 = false;
   G2Affine g2, s_g2;
@@ -72,9 +76,15 @@ struct Params {
     msm_fixed_base_free(&fgl);
     msm_fixed_base_free(&sg);
     msm_fixed_base_free(&sgl);
+    msm_fixed_base_free(&fgp);
   }
-  // windows and table offset serving the base range [off, off + n) of set 0 (g) / 1 (g_lagrange)
+  // windows and table offset serving the base range [off, off + n) of set 0 (g) / 1
+  // (g_lagrange) / 2 (the Lagrange prefix sums: full windows only)
   const MsmFixedBase& tables(int set, size_t off, size_t n, size_t* table_off) const {
+    if (set == 2) {
+      *table_off = off;
+      return fgp;
+    }
     if (sg.table && off >= slab_lo && off + n <= slab_hi) {
       *table_off = off - slab_lo;
       return set == 0 ? sg : sgl;
@@ -83,6 +93,24 @@ struct Params {
     return set == 0 ? fg : fgl;
   }
 };
+
+// The lookup commitments' basis.  A lookup's permuted columns A', S' are sorted into runs
+// of equal values (permute_expression_pair), so with P_i = L_0 + ... + L_i,
+//   sum_i a_i L_i = sum_i (a_i - a_{i+1}) P_i   (a_n = 0; the sum telescopes),
+// the same commitment from scalars that are zero inside every run: the MSM's partition
+// drops zero digits at the source, so its work follows the number of runs, not n.
+int params_prefix(Params& p, hipStream_t st) {
+  if (p.prefix_state) return H2G_OK;
+  G1Affine* pre = nullptr;
+  HIPCHK(hipMalloc(&pre, p.n * sizeof(G1Affine)));
+  hipError_t e = msm_prefix_points(p.gl, p.n, pre, st);
+  if (e == hipSuccess) e = msm_fixed_base_build(pre, p.n, 0, &p.fgp, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(pre);
+  HIPCHK(e);
+  p.prefix_state = 1;
+  return H2G_OK;
+}
 
 int params_finish(Params& p, hipStream_t st) {
   HIPCHK(msm_fixed_base_build(p.g, p.n, 0, &p.fg, st));
@@ -157,6 +185,8 @@ struct ProvingKey {
   std::vector<Fr*> gwc_q;
   uint32_t* lk_cnt = nullptr;  // pinned per-(circuit, lookup) match counters (3 each)
   size_t lk_cnt_len = 0;
+  Fr* lk_diff = nullptr;  // the lookup commitments' prefix-basis scalars (2 per lookup and circuit)
+  size_t lk_diff_len = 0;
   // permute_expression_pair's sort, chosen per lookup from the value width lk_hb[l] (bit
   // length of the largest canonical value) seen by the previous proof: <= 64 bits: radix
   // sort of the values themselves; wider: radix sort of a 48-bit window of the top bits
@@ -334,7 +364,8 @@ void dump(const char* name, const Fr* dptr, size_t count, hipStream_t st, bool h
 // work queued on `st`; the affine result is collected when it enters the transcript.
 // With a shard transport installed (h2g_set_shard_transport) the MSM is split into point
 // slabs: this device takes slab 0, the peers the rest.
-enum { SRS_G = 0, SRS_LAGRANGE = 1 };
+// SRS_LAGRANGE_PREFIX: prefix sums of the Lagrange basis, P_i = L_0 + ... + L_i (params_prefix)
+enum { SRS_G = 0, SRS_LAGRANGE = 1, SRS_LAGRANGE_PREFIX = 2 };
 h2g_shard_transport g_shard{nullptr, 1, nullptr, nullptr};
 uint64_t g_shard_seq = 0;
 // SPMD sharding (h2g_set_spmd_transport): every rank proves, rank r computes slab r
@@ -545,6 +576,10 @@ int commit_collect_all(Device* d, MsmTicket* const* t, int nb, G1Affine* out) {
   return H2G_OK;
 }
 
+#ifndef H2G_LOOKUP_PREFIX  // A/B builds: 0 = the lookup commitments against the Lagrange basis itself
+#define H2G_LOOKUP_PREFIX 1
+#endif
+
 // Several commitments against one base set as batched MSMs (msm_run_fixed_batch): one
 // sort, accumulation and reduction serve a group, so the latency-bound reduction is paid
 // once per group instead of once per commitment -- what circuits with many columns at
@@ -617,7 +652,7 @@ int commit_launch_owned(Device* d, const Params& prm, const Fr* const* scalars, 
       mine.push_back(scalars[i]);
       at.push_back(i);
     }
-  const MsmFixedBase& tb = set == SRS_G ? prm.fg : prm.fgl;
+  const MsmFixedBase& tb = set == SRS_G ? prm.fg : (set == SRS_LAGRANGE ? prm.fgl : prm.fgp);
   const int chunk = std::max(1, commit_batch_chunk(tb, n));
   std::vector<MsmTicket> got(mine.size());
   for (size_t b0 = 0; b0 < mine.size(); b0 += (size_t)chunk) {
@@ -2411,13 +2446,39 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         perm_cosets.push_back(w.lk_apc[l]);
         perm_cosets.push_back(w.lk_spc[l]);
       }
+    std::vector<int> own2(2 * NLT);
+    for (int j = 0; j < NLT; j++) own2[2 * j] = own2[2 * j + 1] = lk_wide ? lk_owner[j] : g_spmd.rank;
+    // A', S' against the prefix-summed Lagrange basis (params_prefix): the same commitments
+    std::vector<const Fr*> com_cols = perm_cols;
+    int com_set = SRS_LAGRANGE;
+    if (H2G_LOOKUP_PREFIX) {
+      RCCHK(params_prefix(prm, st));
+      const size_t need = (size_t)2 * NLT * n;
+      if (need > pk.lk_diff_len) {
+        PALLOC(pk.pool, pk.lk_diff, need);
+        pk.lk_diff_len = need;
+      }
+      PrefixDiff pd{};
+      int m = 0;
+      for (int i = 0; i < 2 * NLT; i++) {
+        Fr* e = pk.lk_diff + (size_t)i * n;
+        com_cols[i] = e;
+        if (own2[i] != g_spmd.rank) continue;  // another rank's column (wide stage)
+        pd.a[m] = perm_cols[i];
+        pd.e[m] = e;
+        if (++m == PREFIX_DIFF_MAX) {
+          HIPCHK(prefix_diff(pd, m, n, st));
+          m = 0;
+        }
+      }
+      if (m) HIPCHK(prefix_diff(pd, m, n, st));
+      com_set = SRS_LAGRANGE_PREFIX;
+    }
     if (lk_wide) {
-      std::vector<int> own2(2 * NLT);
-      for (int j = 0; j < NLT; j++) own2[2 * j] = own2[2 * j + 1] = lk_owner[j];
-      RCCHK(commit_launch_owned(d, prm, perm_cols.data(), own2.data(), 2 * NLT, n, SRS_LAGRANGE, st, tk.data()));
+      RCCHK(commit_launch_owned(d, prm, com_cols.data(), own2.data(), 2 * NLT, n, com_set, st, tk.data()));
       RCCHK(xform(perm_cols, perm_polys, perm_cosets, &own2));
     } else {
-      RCCHK(commit_launch_batch(d, prm, perm_cols.data(), 2 * NLT, n, SRS_LAGRANGE, st, tk.data()));
+      RCCHK(commit_launch_batch(d, prm, com_cols.data(), 2 * NLT, n, com_set, st, tk.data()));
       // coefficient forms and cosets, batched transforms (they overlap the commitments)
       RCCHK(xform(perm_cols, perm_polys, perm_cosets, nullptr));
     }
@@ -4095,11 +4156,12 @@ int h2g_params_msm_dev(uint64_t params, int32_t base_set, uint64_t offset, uint6
   NEED_DEV_P();
   auto ip = g_params.find(params);
   if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
-  const Params& prm = *ip->second;
+  Params& prm = *ip->second;
   if (prm.device != d->id) return fail(H2G_ERR_ARG, "params_msm_dev: params live on another device");
-  if ((base_set != SRS_G && base_set != SRS_LAGRANGE) || offset > prm.n || n > prm.n - offset || !out_affine ||
+  if (base_set < SRS_G || base_set > SRS_LAGRANGE_PREFIX || offset > prm.n || n > prm.n - offset || !out_affine ||
       (n && !d_scalars))
     return fail(H2G_ERR_ARG, "params_msm_dev: bad arguments");
+  if (base_set == SRS_LAGRANGE_PREFIX) RCCHK(params_prefix(prm, d->stream));
   int id = 0;
   size_t toff = 0;
   const MsmFixedBase& tb = prm.tables(base_set, offset, n, &toff);
@@ -4197,7 +4259,7 @@ int h2g_comm_serve(uint64_t params, uint64_t* served) {
   NEED_DEV_P();
   auto ip = g_params.find(params);
   if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
-  const Params& prm = *ip->second;
+  Params& prm = *ip->second;
   if (prm.device != d->id) return fail(H2G_ERR_ARG, "comm_serve: params live on another device");
   uint64_t count = 0;
   for (;;) {
@@ -4207,8 +4269,9 @@ int h2g_comm_serve(uint64_t params, uint64_t* served) {
     hipStream_t ready = nullptr;
     RCCHK(comm_next_request(&op, &set, &lo, &cnt, &slab, &ready));
     if (op == COMM_OP_STOP) break;
-    if (op != COMM_OP_MSM || (set != SRS_G && set != SRS_LAGRANGE) || lo > prm.n || cnt > prm.n - lo)
+    if (op != COMM_OP_MSM || set < SRS_G || set > SRS_LAGRANGE_PREFIX || lo > prm.n || cnt > prm.n - lo)
       return fail(H2G_ERR_STATE, "comm_serve: malformed request");
+    if (set == SRS_LAGRANGE_PREFIX) RCCHK(params_prefix(prm, d->stream));
     uint64_t out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (cnt) {
       size_t toff = 0;

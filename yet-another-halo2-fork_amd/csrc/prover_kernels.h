@@ -102,6 +102,15 @@ struct CopySeg {
   uint64_t len;
 };
 hipError_t copy_segments(const CopySeg* d_segs, int nseg, uint64_t max_len, hipStream_t st);
+
+// e_i = a_i - a_{i+1} (e_{n-1} = a_{n-1}) for up to PREFIX_DIFF_MAX columns: the scalars of
+// a commitment against the prefix-summed Lagrange basis (prover.cpp lookup commitments)
+static constexpr int PREFIX_DIFF_MAX = 16;
+struct PrefixDiff {
+  const Fr* a[PREFIX_DIFF_MAX];
+  Fr* e[PREFIX_DIFF_MAX];
+};
+hipError_t prefix_diff(const PrefixDiff& b, int m, size_t n, hipStream_t st);
 int evaluate_h_max_slots();
 // SPMD: this rank's slab [lo, lo + cnt) of the h pieces (out[p n + j], p < np) from the E
 // sub-cosets' folded coefficients F_t (recv + idx[t] cnt); coef: np x E device matrix

@@ -934,4 +934,18 @@ hipError_t g1_count_invalid(const G1Affine* p, size_t n, uint32_t* bad, hipStrea
   return hipGetLastError();
 }
 
+__global__ void __launch_bounds__(256) prefix_diff_kernel(PrefixDiff b, size_t n) {
+  const Fr* __restrict__ a = b.a[blockIdx.y];
+  Fr* __restrict__ e = b.e[blockIdx.y];
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    e[i] = i + 1 < n ? a[i] - a[i + 1] : a[i];
+}
+hipError_t prefix_diff(const PrefixDiff& b, int m, size_t n, hipStream_t st) {
+  if (m <= 0 || n == 0) return hipSuccess;
+  if (m > PREFIX_DIFF_MAX) return hipErrorInvalidValue;
+  const size_t blocks = std::min<size_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(prefix_diff_kernel, dim3((unsigned)blocks, (unsigned)m), dim3(256), 0, st, b, n);
+  return hipGetLastError();
+}
+
 }  // namespace h2g
