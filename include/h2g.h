@@ -460,7 +460,9 @@ int h2g_spmd_set_weights(const uint32_t* weights, int world);
  * the whole commitment, the others' the identity), forms its coefficients and its
  * sub-cosets, and one exchange per stage hands every sub-coset owner its sub-cosets and
  * every rank its coefficient slab; a lookup's sort, match and product run on its owner
- * only.  Stages with fewer columns keep the point slabs.  0 turns it off. */
+ * only.  Stages with fewer columns keep the point slabs.  Applies from 4 ranks up: at 2
+ * the exchange puts a quarter of the extended-domain data on the one link between the
+ * ranks (more time than the transforms it saves).  0 turns it off. */
 int h2g_spmd_set_column_owners(int on);
 /* time inside the SPMD transport since the last reset, per collective kind k (0 the MSM
  * partials' all-gathers, 1 the host all-gathers, 2 the exchanges, 3 the broadcasts):

@@ -121,7 +121,7 @@ def test_spmd_row_pieces_four_and_eight_ranks():
     on its owner and reach the pieces through one exchange per stage, the pieces' h rows
     gather at each sub-coset's leader; bytes == one GPU.  Degree-3 circuits have 2
     sub-cosets: 2 pieces each at 4 ranks, 4 at 8"""
-    cases = ["simple_k6", "mixed_k10", "c3_k14", "challenge_k9", "multi_my_k6"]
+    cases = ["simple_k6", "mixed_k10", "c3_k14", "challenge_k9", "multi_my_k6", "keccak_k12"]
     res = _run(4, cases, mode="spmd")
     for nm in cases:
         assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])

@@ -426,6 +426,13 @@ void spmd_digest(uint64_t out[4]) {
 
 // SPMD column ownership of wide stages (h2g_spmd_set_column_owners; on by default)
 bool g_spmd_colshard = true;
+// ... from this world size up.  Ownership trades transform work for an all-to-all of the
+// owned columns' sub-coset pieces: each rank sends (W - 1) / W of its 1 / W share of the
+// extended-domain data, over W - 1 point-to-point xGMI links at once, i.e. ~D / W^2 per
+// link for D bytes of cosets.  At W = 2 that is D / 4 on ONE link (keccak-style k = 18: D
+// ~ 3 GB -> ~0.75 GB, ~12 ms at ~64 GB/s, against ~10 ms of transforms saved); at W = 4
+// D / 16 and at W = 8 D / 64 (~50 MB per link, < 1 ms)
+constexpr int kColshardMinWorld = 4;
 
 // SPMD slab weights (h2g_spmd_set_weights): prefix sums, world + 1 entries; empty = uniform
 std::vector<uint64_t> g_spmd_wprefix;
@@ -1968,7 +1975,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   // piece of one sub-coset (sub_prepare)
   const int E_sub = 1 << (pk.dom.ek - pk.dom.k);
   const bool pieces = spmd_subcosets() && g_spmd.allgather_host && g_spmd.exchange && pk.multiopen == 0 &&
-                      g_spmd_colshard && g_spmd.world > E_sub && g_spmd.world % E_sub == 0;
+                      g_spmd_colshard && g_spmd.world >= kColshardMinWorld && g_spmd.world > E_sub &&
+                      g_spmd.world % E_sub == 0;
   if (spmd_subcosets()) RCCHK(sub_prepare(pk, st, pieces));  // this rank's sub-cosets of the key's cosets
   MsmRingGuard ring_guard{d};
   StageClock clk(st, g_stage_sync);
@@ -1987,7 +1995,9 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   // M columns goes to the ranks whole when M is a multiple of the ranks or at least 4x them
   // (balanced); fewer columns keep point slabs
   const int Wsp = g_spmd.world;
-  auto wide = [&](int M) { return h_slabs && g_spmd_colshard && M >= Wsp && (M % Wsp == 0 || M >= 4 * Wsp); };
+  auto wide = [&](int M) {
+    return h_slabs && g_spmd_colshard && Wsp >= kColshardMinWorld && M >= Wsp && (M % Wsp == 0 || M >= 4 * Wsp);
+  };
   // a stage's coefficient forms and extended-domain columns: with row pieces every stage's
   // transforms have one owner per column (round-robin across the stages, tr_next), a wide
   // stage's are its columns' owners (own); otherwise every sub-coset owner transforms
