@@ -2002,7 +2002,10 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   // transforms have one owner per column (round-robin across the stages, tr_next), a wide
   // stage's are its columns' owners (own); otherwise every sub-coset owner transforms
   // every column (the others receive coefficient slabs at the end, coef_exchange)
-  int tr_next = 0;
+  // (with row pieces the rotation starts after the sub-cosets' leaders, ranks 0 .. E - 1,
+  // which interpolate their sub-coset's h: C3 at 8 ranks puts its 6 column transforms on
+  // ranks 2 .. 7 instead of stacking two roles on ranks 0 and 1)
+  int tr_next = pieces ? E_sub : 0;
   auto xform = [&](const std::vector<const Fr*>& lag, const std::vector<Fr*>& pol, const std::vector<Fr*>& cst,
                    const std::vector<int>* own) -> int {
     const int M = (int)lag.size();
