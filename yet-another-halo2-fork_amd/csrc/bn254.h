@@ -366,6 +366,153 @@ H2G_HD Fe<P> inv(const Fe<P>& a) {
   return y * r3;
 }
 
+// Inversion by Bernstein-Yang divsteps (the "safegcd" algorithm, "Fast constant-time gcd
+// computation and modular inversion", 2019), in the signed 30-bit-limb form of its 32-bit
+// formulation: 20 rounds of 30 branch-free divsteps on the low words give a 2x2 transition
+// matrix, applied to (f, g) and to the Bezout pair (d, e) modulo M.  Every lane runs the
+// same instructions -- the binary-GCD `inv` above diverges across a wave's lanes (each
+// lane its own number of halvings and subtractions), which made one batch inversion's
+// middle level ~250-400 us of one wave on gfx950; this is ~15 K uniform ops.  Same
+// result as inv (a^-1 in Montgomery form; 0 -> 0).  600 divsteps >= the 590 that 256-bit
+// inputs need.
+struct By30 {
+  int32_t v[9];
+};
+__device__ __forceinline__ By30 by30_from_limbs(const uint32_t x[8]) {
+  By30 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int b = 30 * i, w = b >> 5, s = b & 31;
+    uint64_t lo = x[w];
+    if (w + 1 < 8) lo |= (uint64_t)x[w + 1] << 32;
+    r.v[i] = (int32_t)((lo >> s) & (i < 8 ? 0x3fffffffull : 0xffffffffull));
+  }
+  return r;
+}
+__device__ __forceinline__ void by30_to_limbs(const By30& a, uint32_t x[8]) {  // limbs in [0, 2^30), value < 2^256
+  uint64_t acc = 0;
+  int have = 0, w = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    acc |= (uint64_t)(uint32_t)a.v[i] << have;
+    have += 30;
+    if (have >= 32 && w < 8) {
+      x[w++] = (uint32_t)acc;
+      acc >>= 32;
+      have -= 32;
+    }
+  }
+  if (w < 8) x[w] = (uint32_t)acc;
+}
+// 30 divsteps on the low words: returns the new zeta; t = (u, v, q, r) scaled by 2^30
+__device__ __forceinline__ int32_t by30_divsteps(int32_t zeta, uint32_t f, uint32_t g, int32_t t[4]) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+#pragma unroll
+  for (int i = 0; i < 30; i++) {
+    uint32_t m1 = (uint32_t)(zeta >> 31);
+    const uint32_t m2 = 0u - (g & 1u);
+    const uint32_t x = (f ^ m1) - m1, y = (u ^ m1) - m1, z = (v ^ m1) - m1;
+    g += x & m2;
+    q += y & m2;
+    r += z & m2;
+    m1 &= m2;
+    zeta = (zeta ^ (int32_t)m1) - 1;
+    f += g & m1;
+    u += q & m1;
+    v += r & m1;
+    g >>= 1;
+    u <<= 1;
+    v <<= 1;
+  }
+  t[0] = (int32_t)u;
+  t[1] = (int32_t)v;
+  t[2] = (int32_t)q;
+  t[3] = (int32_t)r;
+  return zeta;
+}
+template <class P>
+__device__ __forceinline__ Fe<P> inv_by(const Fe<P>& a) {
+  if (a.is_zero()) return a;
+  constexpr int32_t M30 = 0x3fffffff;
+  const By30 mod = by30_from_limbs(P::M);
+  const uint32_t inv30 = (0u - P::INV) & (uint32_t)M30;  // M^-1 mod 2^30 (P::INV = -M^-1 mod 2^32)
+  By30 d = {}, e = {}, f = mod, g = by30_from_limbs(a.l);
+  e.v[0] = 1;
+  int32_t zeta = -1;
+  for (int it = 0; it < 20; it++) {
+    int32_t t[4];
+    zeta = by30_divsteps(zeta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+    const int32_t u = t[0], v = t[1], q = t[2], r = t[3];
+    // (d, e) <- (t [d, e] + M [md, me]) / 2^30, md / me chosen so the low 30 bits vanish
+    {
+      const int32_t sd = d.v[8] >> 31, se = e.v[8] >> 31;
+      int32_t md = (u & sd) + (v & se), me = (q & sd) + (r & se);
+      int64_t cd = (int64_t)u * d.v[0] + (int64_t)v * e.v[0];
+      int64_t ce = (int64_t)q * d.v[0] + (int64_t)r * e.v[0];
+      md -= (int32_t)((inv30 * (uint32_t)cd + (uint32_t)md) & (uint32_t)M30);
+      me -= (int32_t)((inv30 * (uint32_t)ce + (uint32_t)me) & (uint32_t)M30);
+      cd += (int64_t)mod.v[0] * md;
+      ce += (int64_t)mod.v[0] * me;
+      cd >>= 30;
+      ce >>= 30;
+#pragma unroll
+      for (int i = 1; i < 9; i++) {
+        cd += (int64_t)u * d.v[i] + (int64_t)v * e.v[i] + (int64_t)mod.v[i] * md;
+        ce += (int64_t)q * d.v[i] + (int64_t)r * e.v[i] + (int64_t)mod.v[i] * me;
+        d.v[i - 1] = (int32_t)cd & M30;
+        e.v[i - 1] = (int32_t)ce & M30;
+        cd >>= 30;
+        ce >>= 30;
+      }
+      d.v[8] = (int32_t)cd;
+      e.v[8] = (int32_t)ce;
+    }
+    // (f, g) <- t [f, g] / 2^30
+    {
+      int64_t cf = (int64_t)u * f.v[0] + (int64_t)v * g.v[0];
+      int64_t cg = (int64_t)q * f.v[0] + (int64_t)r * g.v[0];
+      cf >>= 30;
+      cg >>= 30;
+#pragma unroll
+      for (int i = 1; i < 9; i++) {
+        cf += (int64_t)u * f.v[i] + (int64_t)v * g.v[i];
+        cg += (int64_t)q * f.v[i] + (int64_t)r * g.v[i];
+        f.v[i - 1] = (int32_t)cf & M30;
+        g.v[i - 1] = (int32_t)cg & M30;
+        cf >>= 30;
+        cg >>= 30;
+      }
+      f.v[8] = (int32_t)cf;
+      g.v[8] = (int32_t)cg;
+    }
+  }
+  // f = +-1 now; d = +-a^-1 in (-2M, M): into [0, M) with f's sign
+  const int32_t neg = f.v[8] >> 31;
+  int32_t c = d.v[8] >> 31;
+#pragma unroll
+  for (int i = 0; i < 9; i++) d.v[i] += mod.v[i] & c;
+#pragma unroll
+  for (int i = 0; i < 9; i++) d.v[i] = (d.v[i] ^ neg) - neg;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    d.v[i + 1] += d.v[i] >> 30;
+    d.v[i] &= M30;
+  }
+  c = d.v[8] >> 31;
+#pragma unroll
+  for (int i = 0; i < 9; i++) d.v[i] += mod.v[i] & c;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    d.v[i + 1] += d.v[i] >> 30;
+    d.v[i] &= M30;
+  }
+  Fe<P> y, r3;
+  by30_to_limbs(d, y.l);
+#pragma unroll
+  for (int i = 0; i < 8; i++) r3.l[i] = P::R3[i];  // (aR)^-1 R^3 R^-1 = a^-1 R
+  return y * r3;
+}
+
 // ---------------------------------------------------------------- G1 (y^2 = x^3 + 3 over Fq)
 
 struct G1Affine {  // halo2curves layout; identity = (0, 0)
@@ -501,6 +648,20 @@ H2G_HD G1Affine xyzz_to_affine(const G1xyzz& p) {
   const Fq izzz = i * p.ZZ;        // 1/ZZZ
   r.x = p.X * izz;
   r.y = p.Y * izzz;
+  return r;
+}
+// the same with the wave-uniform divsteps inversion (kernels converting many points:
+// fixed-base tables, SRS, prefix bases)
+__device__ __forceinline__ G1Affine xyzz_to_affine_by(const G1xyzz& p) {
+  G1Affine r;
+  if (p.is_identity()) {
+    r.x = Fq::zero();
+    r.y = Fq::zero();
+    return r;
+  }
+  const Fq i = inv_by(p.ZZ * p.ZZZ);
+  r.x = p.X * (i * p.ZZZ);
+  r.y = p.Y * (i * p.ZZ);
   return r;
 }
 

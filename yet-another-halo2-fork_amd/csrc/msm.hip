@@ -660,7 +660,7 @@ msm_precompute_kernel(const G1Affine* __restrict__ bases, size_t n, int W, size_
   G1xyzz x = G1xyzz::from_affine(p);
   for (int w = 1; w < W; w++) {
     for (int d = 0; d < fb_width(W, w - 1); d++) x = xyzz_dbl(x);
-    table[(size_t)w * stride + i] = xyzz_to_affine(x);
+    table[(size_t)w * stride + i] = xyzz_to_affine_by(x);
   }
 }
 
@@ -1017,7 +1017,7 @@ msm_prefix_add_kernel(G1xyzz* __restrict__ run, size_t n, const G1xyzz* __restri
   G1xyzz v = run[i];
   const size_t c = i / PFX_C;
   if (c) v = xyzz_add(v, tot[c - 1]);
-  if (out) out[i] = xyzz_to_affine(v);
+  if (out) out[i] = xyzz_to_affine_by(v);
   else run[i] = v;
 }
 hipError_t msm_prefix_points(const G1Affine* in, size_t n, G1Affine* out, hipStream_t st) {

@@ -70,8 +70,8 @@ hipError_t poly_mul_cyclic(Fr* a, size_t n, const Fr* t, size_t t_len, hipStream
 }
 
 // ---------------------------------------------------------------- batch inversion
-// Montgomery's trick in three levels, so the inversion (binary extended Euclid in bn254.h:
-// ≈ 300 Montgomery products of issue time on gfx950) is paid once per ≈ 256 elements while
+// Montgomery's trick in three levels, so the inversion (Bernstein-Yang divsteps, inv_by in bn254.h;
+// ≈ 15 K uniform ops, ≈ 100 µs of one wave on gfx950) is paid once per ≈ 256 elements while
 // the element passes keep 2^18+ threads in flight:
 //   1. inv_fwd: thread t walks its strided subset {t + kT}, storing the running product
 //      before each element (the prefix; 1 for k = 0, so slot t of the scratch is free and
@@ -87,6 +87,11 @@ struct InvBatch {
   Fr* pref[POLY_INV_MAX_BATCH];
 };
 static constexpr int INV_REG = 16;
+// the middle level's inversion: Bernstein-Yang divsteps (inv_by, uniform across the wave's
+// lanes) or the binary extended Euclid (inv, divergent); A/B builds -DH2G_INV_BY=0
+#ifndef H2G_INV_BY
+#define H2G_INV_BY 1
+#endif
 
 __global__ void __launch_bounds__(PT) inv_fwd_kernel(InvBatch bt, size_t n, size_t T) {
   const Fr* __restrict__ a = bt.a[blockIdx.y];
@@ -120,7 +125,7 @@ __global__ void __launch_bounds__(PT) inv_regs_kernel(InvBatch bt, size_t m) {
     pre[k] = acc;
     if (!v[k].is_zero()) acc = acc * v[k];
   }
-  Fr iv = inv(acc);
+  Fr iv = H2G_INV_BY ? inv_by(acc) : inv(acc);
 #pragma unroll
   for (int k = INV_REG - 1; k >= 0; k--) {
     const size_t i = t + k * T;

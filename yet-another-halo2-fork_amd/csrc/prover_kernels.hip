@@ -887,7 +887,7 @@ __global__ void __launch_bounds__(KT) gen_mul_kernel(const Fr* __restrict__ sc, 
   G1Affine g;
   g.x = Fq::one();
   g.y = from_u64<FqParams>(2);
-  out[i] = xyzz_to_affine(xyzz_mul_canonical(G1xyzz::from_affine(g), e.l));
+  out[i] = xyzz_to_affine_by(xyzz_mul_canonical(G1xyzz::from_affine(g), e.l));
 }
 
 hipError_t g1_generator_mul(const Fr* scalars, size_t n, G1Affine* out, hipStream_t st) {

@@ -12,7 +12,7 @@ __global__ void __launch_bounds__(256) srs_kernel(Fr s, size_t n, G1Affine* __re
   g.x = Fq::one();             // generator (1, 2)
   g.y = from_u64<FqParams>(2);
   const G1xyzz p = xyzz_mul_canonical(G1xyzz::from_affine(g), e.l);
-  out[i] = xyzz_to_affine(p);
+  out[i] = xyzz_to_affine_by(p);
 }
 
 hipError_t srs_setup(const Fr& s, size_t n, G1Affine* d_out, hipStream_t st) {
