@@ -259,6 +259,22 @@ def test_poly_ops_vs_oracle(n):
     assert np.array_equal(h2g.prefix_product(b), O.prefix_product(b))
 
 
+def test_batch_invert_edge_values():
+    """the divsteps inversion (bn254.h inv_by) on values at the edges of its limb ranges:
+    a one-element batch inverts the element itself (inv_regs_kernel), against the oracle"""
+    R = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
+    vals = [1, 2, 3, R - 1, R - 2, (R - 1) // 2, 1 << 30, (1 << 30) - 1, 1 << 60, 1 << 240, (1 << 253) + 12345,
+            0x3fffffff3fffffff3fffffff3fffffff3fffffff3fffffff3fffffff3fff]
+    for v in vals:
+        limbs = np.array([[(v >> (64 * i)) & (2**64 - 1) for i in range(4)]], dtype=np.uint64)
+        a = O.fr_from_canonical(limbs)
+        assert np.array_equal(h2g.batch_invert(a), O.batch_invert(a)), hex(v)
+    # and every value of a longer batch at once (the middle level inverts 16-element products)
+    a = O.fr_from_canonical(np.array([[(v >> (64 * i)) & (2**64 - 1) for i in range(4)] for v in vals * 50],
+                                     dtype=np.uint64))
+    assert np.array_equal(h2g.batch_invert(a), O.batch_invert(a))
+
+
 # ---------------------------------------------------------------- fixed-base MSM (resident bases)
 def _skewed(dist, r, n):
     if dist == "random":
