@@ -734,6 +734,10 @@ static constexpr size_t RED_Q4_MAX = 32768;
 #define H2G_PLANE_LB_SMALL 6
 #endif
 static constexpr int kSmallLB = H2G_PLANE_LB_SMALL;
+#ifndef H2G_PLANE_RGP_LARGE  // buckets per group of the lane-per-group plane kernel (large sets)
+#define H2G_PLANE_RGP_LARGE 8
+#endif
+static constexpr int kLargeRGP = H2G_PLANE_RGP_LARGE;
 static constexpr uint32_t FIXUP_Q4_MAX = 32768;
 
 static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Affine* d_bases, size_t n, int c,
@@ -775,6 +779,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     }
   } else {
     plane_q = 1;
+    rgp = kLargeRGP;
   }
   const uint32_t m1p = (NB + rgp - 1) / rgp;                         // plane groups per set
   const uint32_t nblk_p = (m1p + (1u << plane_lb) - 1) >> plane_lb;  // plane kernels' blocks
@@ -908,7 +913,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     const dim3 pg(nblk_p, (unsigned)WB), pb((unsigned)(plane_q << plane_lb));
     const G1xyzz* bk = buckets;
     if (plane_q == 1)
-      hipLaunchKernelGGL((msm_rgroup_plane_kernel<1, 8, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
+      hipLaunchKernelGGL((msm_rgroup_plane_kernel<1, 8, kLargeRGP>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
     else if (rgp == 1)
       hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, kSmallLB, 1>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
     else if (rgp == 2)
