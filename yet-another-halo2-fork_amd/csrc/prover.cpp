@@ -196,6 +196,17 @@ struct ProvingKey {
   std::vector<int> lk_hb;
   unsigned long long *lk_or_d = nullptr, *lk_or_h = nullptr;
   size_t lk_or_len = 0;  // (circuit, lookup) entries of lk_or_*
+  // SPMD witness checksums of an advice phase (copy_columns), device / pinned, and the event
+  // that their copy to the host has landed (spmd_witness_fold)
+  unsigned long long *wsum_d = nullptr, *wsum_h = nullptr;
+  size_t wsum_len = 0;
+  hipEvent_t wsum_ev = nullptr;
+  // pinned staging of a proof's small host-to-device uploads (blinding rows, seeds, staged
+  // scalars; pk_upload): from pageable memory a hipMemcpyAsync costs 8-60 us of host time
+  // (a staged copy), which left the GPU idle between the keccak-style circuit's 32 advice
+  // columns; from pinned memory the copy is queued at once.  Re-armed per proof
+  uint8_t* up_h = nullptr;
+  size_t up_len = 0, up_off = 0;
   Domain dom;
   Pool pool;
   // proving key (device)
@@ -292,10 +303,10 @@ Fr rotate_omega(const Domain& d, const Fr& x, int rot) {
   return x * pow_u64(rot >= 0 ? d.omega : d.omega_inv, (uint64_t)(rot >= 0 ? rot : -rot));
 }
 
-// coefficients of the unique polynomial of degree < m through (pts[i], ev[i])
-std::vector<Fr> lagrange_interpolate(const std::vector<Fr>& pts, const std::vector<Fr>& ev) {
+// the Lagrange basis of the points: out[j] = coefficients of prod_{k != j} (X - p_k) / (p_j - p_k)
+std::vector<std::vector<Fr>> lagrange_basis(const std::vector<Fr>& pts) {
   const size_t m = pts.size();
-  std::vector<Fr> out(m, Fr::zero());
+  std::vector<std::vector<Fr>> out(m);
   for (size_t j = 0; j < m; j++) {
     std::vector<Fr> num(1, Fr::one());
     Fr den = Fr::one();
@@ -309,8 +320,9 @@ std::vector<Fr> lagrange_interpolate(const std::vector<Fr>& pts, const std::vect
       num.swap(nn);
       den = den * (pts[j] - pts[k]);
     }
-    const Fr sc = ev[j] * inv(den);
-    for (size_t i = 0; i < m; i++) out[i] = out[i] + num[i] * sc;
+    const Fr sc = inv(den);
+    for (Fr& c : num) c = c * sc;
+    out[j] = std::move(num);
   }
   return out;
 }
@@ -394,16 +406,32 @@ int spmd_exchange(const void* d_send, const size_t* sb, void* d_recv, const size
 }
 // the running proof's transcript, RNG draws and witness, whose digest travels with every
 // SPMD partial (H2G_SPMD_WORDS): ranks that diverged fail the proof instead of summing
-// slabs of different polynomials.  The witness enters as every advice column's value at
-// a fixed point, evaluated over the whole column by each rank (spmd_witness_fold): with
-// the slabs summed, the commitments and evaluations alone would be the same on ranks fed
-// different witnesses.
+// slabs of different polynomials.  The witness enters as a 64-bit checksum of every advice
+// column, over the whole column on each rank, taken by the kernel that copies the column
+// in (copy_columns; spmd_witness_fold): with the slabs summed, the commitments and
+// evaluations alone would be the same on ranks fed different witnesses.  The checksums
+// reach the host behind the stream and are folded in when the next collective needs the
+// digest (spmd_witness_settle), so the check costs no synchronisation of its own.
 struct SpmdCheck {
   const Transcript* tr = nullptr;
   const ProverRng* rng = nullptr;
   uint8_t wit[64] = {};
+  const unsigned long long* pend = nullptr;  // pinned checksums still to fold (pend_n), ready at pend_ev
+  int pend_n = 0;
+  hipEvent_t pend_ev = nullptr;
 };
 SpmdCheck g_spmd_check;
+void spmd_witness_settle() {
+  SpmdCheck& c = g_spmd_check;
+  if (!c.pend) return;
+  (void)hipEventSynchronize(c.pend_ev);
+  Blake2b h("h2g-spmd-witness");
+  h.update(c.wit, 64);
+  h.update(reinterpret_cast<const uint8_t*>(c.pend), (size_t)c.pend_n * sizeof(unsigned long long));
+  h.digest(c.wit);
+  c.pend = nullptr;
+  c.pend_n = 0;
+}
 struct SpmdCheckScope {
   SpmdCheckScope(const Transcript* tr, const ProverRng* rng) {
     g_spmd_check = SpmdCheck{};
@@ -414,6 +442,7 @@ struct SpmdCheckScope {
 };
 void spmd_digest(uint64_t out[4]) {
   uint8_t a[64] = {}, b[64] = {}, d[64];
+  spmd_witness_settle();
   if (g_spmd_check.tr) g_spmd_check.tr->state_digest(a);
   if (g_spmd_check.rng) g_spmd_check.rng->draws_digest(b);
   Blake2b h("h2g-spmd-check\0\0");
@@ -423,6 +452,8 @@ void spmd_digest(uint64_t out[4]) {
   h.digest(d);
   std::memcpy(out, d, 32);
 }
+
+hipError_t pk_upload(ProvingKey& pk, void* dst, const void* src, size_t bytes, hipStream_t st);
 
 // SPMD column ownership of wide stages (h2g_spmd_set_column_owners; on by default)
 bool g_spmd_colshard = true;
@@ -1041,7 +1072,7 @@ int slab_carries(ProvingKey& pk, const Slab& sl, size_t n, const std::vector<Fr>
     PALLOC(pk.pool, pk.eval_scr, need);
     pk.eval_scr_len = need;
   }
-  HIPCHK(hipMemcpyAsync(pk.d_reqs, reqs.data(), np * sizeof(EvalReq), hipMemcpyHostToDevice, st));
+  HIPCHK(pk_upload(pk, pk.d_reqs, reqs.data(), np * sizeof(EvalReq), st));
   HIPCHK(poly_eval_batch(pk.d_reqs, (int)np, m ? m : 1, pk.evals, pk.eval_scr, st));
   std::vector<Fr> mine(np);
   HIPCHK(hipMemcpyAsync(mine.data(), pk.evals, np * sizeof(Fr), hipMemcpyDeviceToHost, st));
@@ -1250,7 +1281,7 @@ int h_by_slabs(Device* d, ProvingKey& pk, const Slab& sl, hipStream_t st) {
       zp = zp * zinv_n;
     }
   }
-  HIPCHK(hipMemcpyAsync(pk.small, coef.data(), coef.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
+  HIPCHK(pk_upload(pk, pk.small, coef.data(), coef.size() * sizeof(Fr), st));
   HIPCHK(hipStreamSynchronize(st));  // the send staging is complete; coef (host) was read
   if (spmd_exchange(pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
     return fail(H2G_ERR_STATE, "spmd transport: exchange of h slabs failed");
@@ -1415,7 +1446,7 @@ int colshard_distribute(Device* d, ProvingKey& pk, const std::vector<const Fr*>&
     }
     uint64_t mx = 0;
     for (const CopySeg& g : v) mx = std::max<uint64_t>(mx, g.len);
-    HIPCHK(hipMemcpyAsync(pk.d_segs, v.data(), v.size() * sizeof(CopySeg), hipMemcpyHostToDevice, st));
+    HIPCHK(pk_upload(pk, pk.d_segs, v.data(), v.size() * sizeof(CopySeg), st));
     HIPCHK(copy_segments(pk.d_segs, (int)v.size(), mx, st));
     return H2G_OK;
   };
@@ -1577,7 +1608,7 @@ int gather_to_owners(ProvingKey& pk, const std::vector<Fr*>& cols, const std::ve
     }
     uint64_t mx = 0;
     for (const CopySeg& g : v) mx = std::max<uint64_t>(mx, g.len);
-    HIPCHK(hipMemcpyAsync(pk.d_segs, v.data(), v.size() * sizeof(CopySeg), hipMemcpyHostToDevice, st));
+    HIPCHK(pk_upload(pk, pk.d_segs, v.data(), v.size() * sizeof(CopySeg), st));
     HIPCHK(copy_segments(pk.d_segs, (int)v.size(), mx, st));
     return H2G_OK;
   };
@@ -1913,37 +1944,56 @@ struct PolyRef {  // a committed polynomial in coefficient form (SHPLONK's "comm
   uint64_t len;
 };
 
-// SPMD: fold the columns' values at a fixed point (full length, this rank's copy) into
-// the consistency digest -- one batched evaluation and a host sync per advice phase, only
-// when sharded
-int spmd_witness_fold(ProvingKey& pk, const std::vector<const Fr*>& cols, size_t n, hipStream_t st) {
-  if (g_spmd.world <= 1 || cols.empty()) return H2G_OK;
-  static const uint64_t kPoint[4] = {0x9e3779b97f4a7c15ull, 0xf39cc0605cedc834ull, 0x1082276bf3a27251ull,
-                                     0x0b5026f5aa96619eull};
-  const Fr x = fr_from_limbs(kPoint);
-  const int np = (int)cols.size();
-  std::vector<EvalReq> reqs(np);
-  for (int i = 0; i < np; i++) reqs[i] = EvalReq{cols[i], (uint64_t)n, x};
-  if (np > pk.max_reqs) {
-    PALLOC(pk.pool, pk.d_reqs, np);
-    PALLOC(pk.pool, pk.evals, np);
-    pk.max_reqs = np;
+// SPMD: an advice phase's m column checksums (pk.wsum_d, filled by the copy_columns that
+// brought the columns in) to the host behind the stream; folded into the consistency
+// digest by the next collective (spmd_witness_settle) -- only when sharded
+int spmd_witness_prepare(ProvingKey& pk, int m, hipStream_t st) {
+  if (g_spmd.world <= 1 || m <= 0) return H2G_OK;
+  spmd_witness_settle();  // an earlier phase's, before its pinned buffer is reused
+  if ((size_t)m > pk.wsum_len) {
+    if (pk.wsum_d) (void)hipFree(pk.wsum_d);
+    if (pk.wsum_h) (void)hipHostFree(pk.wsum_h);
+    pk.wsum_d = pk.wsum_h = nullptr;
+    pk.wsum_len = 0;
+    HIPCHK(hipMalloc((void**)&pk.wsum_d, (size_t)m * sizeof(unsigned long long)));
+    HIPCHK(hipHostMalloc((void**)&pk.wsum_h, (size_t)m * sizeof(unsigned long long), hipHostMallocDefault));
+    pk.wsum_len = (size_t)m;
   }
-  const size_t need = poly_eval_scratch_len(np, n);
-  if (need > pk.eval_scr_len) {
-    PALLOC(pk.pool, pk.eval_scr, need);
-    pk.eval_scr_len = need;
-  }
-  std::vector<Fr> ev(np);
-  HIPCHK(hipMemcpyAsync(pk.d_reqs, reqs.data(), np * sizeof(EvalReq), hipMemcpyHostToDevice, st));
-  HIPCHK(poly_eval_batch(pk.d_reqs, np, n, pk.evals, pk.eval_scr, st));
-  HIPCHK(hipMemcpyAsync(ev.data(), pk.evals, np * sizeof(Fr), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  Blake2b h("h2g-spmd-witness");
-  h.update(g_spmd_check.wit, 64);
-  h.update(reinterpret_cast<const uint8_t*>(ev.data()), ev.size() * sizeof(Fr));
-  h.digest(g_spmd_check.wit);
+  if (!pk.wsum_ev) HIPCHK(hipEventCreateWithFlags(&pk.wsum_ev, hipEventDisableTiming));
+  HIPCHK(hipMemsetAsync(pk.wsum_d, 0, (size_t)m * sizeof(unsigned long long), st));
   return H2G_OK;
+}
+int spmd_witness_fold(ProvingKey& pk, int m, hipStream_t st) {
+  if (g_spmd.world <= 1 || m <= 0) return H2G_OK;
+  HIPCHK(hipMemcpyAsync(pk.wsum_h, pk.wsum_d, (size_t)m * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipEventRecord(pk.wsum_ev, st));
+  g_spmd_check.pend = pk.wsum_h;
+  g_spmd_check.pend_n = m;
+  g_spmd_check.pend_ev = pk.wsum_ev;
+  return H2G_OK;
+}
+
+// the proof's upload staging (ProvingKey::up_h): armed behind a sync of the prover's
+// stream, so no copy of the previous proof still reads it
+int pk_upload_arm(ProvingKey& pk, hipStream_t st) {
+  HIPCHK(hipStreamSynchronize(st));
+  if (!pk.up_h) {
+    constexpr size_t kLen = 4u << 20;
+    HIPCHK(hipHostMalloc((void**)&pk.up_h, kLen, hipHostMallocDefault));
+    pk.up_len = kLen;
+  }
+  pk.up_off = 0;
+  return H2G_OK;
+}
+// dst <- src (host, any) on st through the staging; past its end, the pageable copy
+hipError_t pk_upload(ProvingKey& pk, void* dst, const void* src, size_t bytes, hipStream_t st) {
+  const size_t a = (pk.up_off + 63) & ~(size_t)63;
+  if (pk.up_h && a + bytes <= pk.up_len) {
+    std::memcpy(pk.up_h + a, src, bytes);
+    pk.up_off = a + bytes;
+    return hipMemcpyAsync(dst, pk.up_h + a, bytes, hipMemcpyHostToDevice, st);
+  }
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
 }
 
 std::vector<Fr> g_last_challenges;  // the challenges of the last proof (h2g_last_challenges)
@@ -1964,6 +2014,7 @@ struct ProveIn {
 
 int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::vector<uint8_t>* proof) {
   hipStream_t st = d->stream;
+  RCCHK(pk_upload_arm(pk, st));
   const size_t n = pk.n, ext = pk.ext;
   const int bf = pk.bf;
   const Domain& D = pk.dom;
@@ -2114,8 +2165,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     // vanishing stage checks that the real draws equal these bytes (else it redoes both)
     van_seeds.assign(van_off.size() * 8, 0);
     rng.peek((uint64_t)pk.van_pos, reinterpret_cast<uint8_t*>(van_seeds.data()), van_seeds.size() * 4);
-    HIPCHK(hipMemcpyAsync(pk.d_seeds, van_seeds.data(), van_seeds.size() * 4, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(pk.d_offsets, van_off.data(), van_off.size() * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(pk_upload(pk, pk.d_seeds, van_seeds.data(), van_seeds.size() * 4, st));
+    HIPCHK(pk_upload(pk, pk.d_offsets, van_off.data(), van_off.size() * 8, st));
     HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)van_off.size(), st, sl.lo, sl.hi1));
     RCCHK(commit_launch(d, prm, pk.random_poly, n, SRS_G, st, &van_tk));
     van_early = true;
@@ -2132,6 +2183,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     // whole witness (the lookups and products read it), only the owner commits and
     // transforms the column
     const bool adv_wide = wide((int)(cols.size() * ncirc));
+    const bool digest = g_spmd.world > 1 && !cols.empty();  // this phase's witness into the consistency digest
+    if (digest) RCCHK(spmd_witness_prepare(pk, (int)(ncirc * cols.size()), st));
     for (int ci = 0; ci < ncirc; ci++) {
       CircuitWs& w = *W[ci];
       const uint64_t* from = in.advice ? in.advice[ci] : nullptr;
@@ -2156,17 +2209,49 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       // from host memory; the RNG draws keep the reference's order (every column's rows,
       // then every column's blind)
       const bool early = !adv_wide && commit_batch_chunk(prm, n, SRS_LAGRANGE) < 2;
+      // device-resident columns come in through copy_columns (a streaming kernel, up to
+      // COPY_COLS_MAX columns a launch; per-column DMA copies left the GPU idle for ~0.8 ms
+      // of 32 columns at 2^18), host ones through the DMA upload; under SPMD either way
+      // also takes each column's checksum before its blinding rows land (spmd_witness_fold)
+      ColCopy cc{};
+      int ncc = 0;
+      auto flush = [&]() -> int {
+        if (ncc) HIPCHK(copy_columns(cc, ncc, n, digest, st));
+        ncc = 0;
+        return H2G_OK;
+      };
+      auto blind = [&](int c) -> int {
+        if (pk.unblinded[c]) return H2G_OK;
+        Fr* rows = adv_blind.data() + ((size_t)ci * pk.A + c) * (bf + 1);
+        for (int i = 0; i <= bf; i++) rows[i] = rng.random_fr();
+        HIPCHK(pk_upload(pk, w.adv[c] + unusable, rows, (size_t)(bf + 1) * sizeof(Fr), st));
+        return H2G_OK;
+      };
       for (size_t k = 0; k < cols.size(); k++) {
         const int c = cols[k];
-        HIPCHK(hipMemcpyAsync(w.adv[c], from + 4 * n * c, n * sizeof(Fr),
-                              from_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
-        if (!pk.unblinded[c]) {
-          Fr* rows = adv_blind.data() + ((size_t)ci * pk.A + c) * (bf + 1);
-          for (int i = 0; i <= bf; i++) rows[i] = rng.random_fr();
-          HIPCHK(hipMemcpyAsync(w.adv[c] + unusable, rows, (size_t)(bf + 1) * sizeof(Fr), hipMemcpyHostToDevice, st));
+        const Fr* src = reinterpret_cast<const Fr*>(from + 4 * n * c);
+        unsigned long long* sum = digest ? pk.wsum_d + (size_t)ci * cols.size() + k : nullptr;
+        if (from_dev) {
+          cc.src[ncc] = src;
+          cc.dst[ncc] = w.adv[c];
+          cc.sum[ncc++] = sum;
+        } else {
+          HIPCHK(hipMemcpyAsync(w.adv[c], src, n * sizeof(Fr), hipMemcpyHostToDevice, st));
+          if (digest) {
+            cc.src[ncc] = w.adv[c];
+            cc.dst[ncc] = nullptr;
+            cc.sum[ncc++] = sum;
+          }
         }
-        if (early) RCCHK(commit_launch(d, prm, w.adv[c], n, SRS_LAGRANGE, st, &tk[(size_t)ci * cols.size() + k]));
+        if (early || ncc == COPY_COLS_MAX || !from_dev) RCCHK(flush());
+        if (early) {
+          RCCHK(blind(c));
+          RCCHK(commit_launch(d, prm, w.adv[c], n, SRS_LAGRANGE, st, &tk[(size_t)ci * cols.size() + k]));
+        }
       }
+      RCCHK(flush());
+      if (!early)
+        for (int c : cols) RCCHK(blind(c));
       for (int c : cols)
         if (!pk.unblinded[c]) (void)rng.random_fr();  // commitment blinds (unused by KZG)
       if (!cols.empty() && !early && !adv_wide) {
@@ -2176,6 +2261,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
                                   tk.data() + (size_t)ci * cols.size()));
       }
     }
+    if (digest) RCCHK(spmd_witness_fold(pk, (int)(ncirc * cols.size()), st));
     std::vector<int> adv_owner;
     std::vector<const Fr*> adv_lag;
     std::vector<Fr*> adv_poly, adv_cst;
@@ -2223,12 +2309,6 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       for (int ci = 0; ci < ncirc; ci++)
         for (int c : cols) adv_shard[(size_t)ci * pk.A + c] = 1;
     }
-    if (g_spmd.world > 1) {  // this phase's witness into the consistency digest
-      std::vector<const Fr*> wc;
-      for (int ci = 0; ci < ncirc; ci++)
-        for (int c : cols) wc.push_back(W[ci]->adv[c]);
-      RCCHK(spmd_witness_fold(pk, wc, n, st));
-    }
     if (ph == 0 && early_van) RCCHK(launch_van_early());
     if (ph == 0) clk.mark("upload+instances");
     {  // circuit by circuit, column by column
@@ -2241,7 +2321,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       if (pk.ch_phase[i] == ph) challenges[i] = tr.squeeze();
   }
   if (NCH)
-    HIPCHK(hipMemcpyAsync(pk.consts + pk.num_consts, challenges.data(), NCH * sizeof(Fr), hipMemcpyHostToDevice, st));
+    HIPCHK(pk_upload(pk, pk.consts + pk.num_consts, challenges.data(), NCH * sizeof(Fr), st));
   g_last_challenges = challenges;
   clk.mark("advice commit");
 
@@ -2339,8 +2419,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       HIPCHK(hipMemcpyAsync(pk.lk_cnt + 3 * j, pk.counters, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       for (int which = 0; which < 2; which++) {
         const Fr* r = rows.data() + ((size_t)2 * j + which) * (bf + 1);
-        HIPCHK(hipMemcpyAsync((which ? w.lk_sp[l] : w.lk_ap[l]) + u, r, (size_t)(bf + 1) * sizeof(Fr),
-                              hipMemcpyHostToDevice, st));
+        HIPCHK(pk_upload(pk, (which ? w.lk_sp[l] : w.lk_ap[l]) + u, r, (size_t)(bf + 1) * sizeof(Fr), st));
       }
       return H2G_OK;
     };
@@ -2603,12 +2682,12 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       PALLOC(pk.pool, pk.perm_lz, NST);
       pk.perm_lz_len = (size_t)NST;
     }
-    HIPCHK(hipMemcpyAsync(pk.perm_lz, lzp.data(), NST * sizeof(Fr), hipMemcpyHostToDevice, st));
+    HIPCHK(pk_upload(pk, pk.perm_lz, lzp.data(), NST * sizeof(Fr), st));
     for (int i = 0; i < NST; i++) {
       Fr* blind_rows = perm_blind.data() + (size_t)i * bf;
       for (int q = 0; q < bf; q++) blind_rows[q] = rng.random_fr();
       (void)rng.random_fr();  // blind
-      HIPCHK(hipMemcpyAsync(pk.small, blind_rows, bf * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(pk_upload(pk, pk.small, blind_rows, bf * sizeof(Fr), st));
       HIPCHK(perm_z_assemble(all_z_lag[i], n, bf, all_z[i], pk.perm_lz + i, pk.small, st, plo, phi));
     }
     HIPCHK(hipStreamSynchronize(st));  // lzp (host) was read
@@ -2663,7 +2742,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         if (ci == 0 && s == 0) dump("pre0", pk.pre, n, st);
         for (int i = 0; i < bf; i++) blind_rows[i] = rng.random_fr();
         (void)rng.random_fr();  // blind
-        HIPCHK(hipMemcpyAsync(pk.small, blind_rows, bf * sizeof(Fr), hipMemcpyHostToDevice, st));
+        HIPCHK(pk_upload(pk, pk.small, blind_rows, bf * sizeof(Fr), st));
         HIPCHK(perm_z_assemble(w.z_lag[s], n, bf, pk.pre, pk.last_z, pk.small, st));
         HIPCHK(hipMemcpyAsync(pk.last_z, w.z_lag[s] + (n - (size_t)(bf + 1)), sizeof(Fr), hipMemcpyDeviceToDevice,
                               st));
@@ -2705,7 +2784,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         HIPCHK(poly_prefix_product(prod, pk.pre, n, pk.scr, pk.scr_len, st));
         pre = pk.pre;
       }
-      HIPCHK(hipMemcpyAsync(pk.small, rows, (size_t)bf * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(pk_upload(pk, pk.small, rows, (size_t)bf * sizeof(Fr), st));
       HIPCHK(perm_z_assemble(z_lag, n, bf, pre, pk.one, pk.small, st));
       if (listed) {
         z_lags.push_back(z_lag);
@@ -2787,8 +2866,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     }
     if (!van_early) {
       van_seeds = drawn;
-      HIPCHK(hipMemcpyAsync(pk.d_seeds, van_seeds.data(), van_seeds.size() * 4, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(pk.d_offsets, van_off.data(), van_off.size() * 8, hipMemcpyHostToDevice, st));
+      HIPCHK(pk_upload(pk, pk.d_seeds, van_seeds.data(), van_seeds.size() * 4, st));
+      HIPCHK(pk_upload(pk, pk.d_offsets, van_off.data(), van_off.size() * 8, st));
       // a slab-mode rank draws only its coefficients (and the halo) of the random polynomial
       HIPCHK(chacha_random_poly(pk.random_poly, n, pk.d_seeds, pk.d_offsets, (int)van_off.size(), st, sl.lo,
                                 sl.hi1));
@@ -3025,10 +3104,13 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   queries.push_back({id_r, x});
   // unique (poly, point) evaluations, one batched launch
   std::vector<Q2> ev_keys;
+  std::vector<std::vector<int>> ev_of(polys.size());  // per polynomial its ev_keys entries (a few points)
   auto ev_index = [&](int poly, const Fr& pt) -> int {
-    for (size_t i = 0; i < ev_keys.size(); i++)
-      if (ev_keys[i].poly == poly && ev_keys[i].pt == pt) return (int)i;
+    if ((size_t)poly >= ev_of.size()) ev_of.resize((size_t)poly + 1);
+    for (int i : ev_of[poly])
+      if (ev_keys[i].pt == pt) return i;
     ev_keys.push_back({poly, pt});
+    ev_of[poly].push_back((int)ev_keys.size() - 1);
     return (int)ev_keys.size() - 1;
   };
   for (auto& q : queries) ev_index(q.poly, q.pt);
@@ -3051,12 +3133,19 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       const uint64_t len = pr.len > sl.lo ? std::min<uint64_t>(pr.len, sl.hi) - sl.lo : 0;
       reqs[i] = EvalReq{pr.p + (len ? sl.lo : 0), len, ev_keys[i].pt};
     }
-    HIPCHK(hipMemcpyAsync(pk.d_reqs, reqs.data(), nreq * sizeof(EvalReq), hipMemcpyHostToDevice, st));
+    HIPCHK(pk_upload(pk, pk.d_reqs, reqs.data(), nreq * sizeof(EvalReq), st));
     HIPCHK(poly_eval_batch(pk.d_reqs, nreq, sl.hi - sl.lo, pk.evals, pk.eval_scr, st));
     HIPCHK(hipMemcpyAsync(evals.data(), pk.evals, nreq * sizeof(Fr), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     if (slabs) {  // p(x) = sum_r x^lo_r (slab r's partial evaluation), summed in rank order
-      for (int i = 0; i < nreq; i++) evals[i] = evals[i] * pow_u64(ev_keys[i].pt, sl.lo);
+      std::vector<std::pair<Fr, Fr>> shift;  // (point, point^lo): a few distinct points
+      for (int i = 0; i < nreq; i++) {
+        const Fr& pt = ev_keys[i].pt;
+        size_t j = 0;
+        while (j < shift.size() && !(shift[j].first == pt)) j++;
+        if (j == shift.size()) shift.emplace_back(pt, pow_u64(pt, sl.lo));
+        evals[i] = evals[i] * shift[j].second;
+      }
       std::vector<Fr> all;
       RCCHK(spmd_allgather_fr(evals, &all));
       for (int i = 0; i < nreq; i++) {
@@ -3132,7 +3221,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         vp = vp * v;
       }
       neg_evb.push_back(Fr::zero() - evb);  // poly_batch - eval_batch (poly.rs:268-276)
-      HIPCHK(hipMemcpyAsync(pk.small + g, &neg_evb.back(), sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(pk_upload(pk, pk.small + g, &neg_evb.back(), sizeof(Fr), st));
       t.p[t.k] = pk.small + g;
       t.len[t.k] = 1;
       t.coef[t.k] = Fr::one();
@@ -3191,11 +3280,19 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     }
     rs_of[c] = f;
   }
+  // r_c: the interpolation through c's evaluations, from its rotation set's Lagrange basis
+  // (one set of inversions per set, not per commitment)
+  std::vector<std::vector<std::vector<Fr>>> basis(rs_rep.size());
+  for (size_t r = 0; r < rs_rep.size(); r++) basis[r] = lagrange_basis(cm_pts[rs_rep[r]]);
   std::vector<std::vector<Fr>> low(cm_ids.size());
   for (size_t c = 0; c < cm_ids.size(); c++) {
-    std::vector<Fr> e;
-    for (auto& p : cm_pts[c]) e.push_back(ev(cm_ids[c], p));
-    low[c] = lagrange_interpolate(cm_pts[c], e);
+    const auto& B = basis[rs_of[c]];
+    const size_t m = cm_pts[c].size();
+    low[c].assign(m, Fr::zero());
+    for (size_t j = 0; j < m; j++) {
+      const Fr e = ev(cm_ids[c], cm_pts[c][j]);
+      for (size_t i = 0; i < m; i++) low[c][i] = low[c][i] + B[j][i] * e;
+    }
   }
   const Fr v = tr.squeeze();
   // h_x = sum_s v^s (sum_i y^i (p_i - r_i)) / Z_s (the reference divides by Z_s with one
@@ -3265,7 +3362,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         t.k++;
         for (size_t j = 0; j < low[c].size(); j++) corr[j] = corr[j] + coef * low[c][j];
       }
-      HIPCHK(hipMemcpyAsync(pk.small, corr.data(), corr.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
+      HIPCHK(pk_upload(pk, pk.small, corr.data(), corr.size() * sizeof(Fr), st));
       t.p[t.k] = pk.small;
       t.len[t.k] = corr.size();
       t.coef[t.k] = fr_neg_one();
@@ -3290,7 +3387,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       }
       if (sl.hi < n) {  // h_x's halo coefficient (read by the linearisation): q[hi] = sum of the carries
         corr_stage.emplace_back(1, halo);
-        HIPCHK(hipMemcpyAsync(pk.hx + sl.hi, corr_stage.back().data(), sizeof(Fr), hipMemcpyHostToDevice, st));
+        HIPCHK(pk_upload(pk, pk.hx + sl.hi, corr_stage.back().data(), sizeof(Fr), st));
       }
     }
   }
@@ -3336,7 +3433,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     Fr zt = Fr::one();
     for (auto& sp : super_pts) zt = (u - sp) * zt;
     c0_stage = c0;
-    HIPCHK(hipMemcpyAsync(pk.small, &c0_stage, sizeof(Fr), hipMemcpyHostToDevice, st));
+    HIPCHK(pk_upload(pk, pk.small, &c0_stage, sizeof(Fr), st));
     t.p[t.k] = pk.small;
     t.len[t.k] = 1;
     t.coef[t.k] = Fr::one();
@@ -3908,6 +4005,10 @@ int h2g_pk_free(uint64_t pk) {
   if (it->second->lk_cnt) (void)hipHostFree(it->second->lk_cnt);
   if (it->second->lk_or_h) (void)hipHostFree(it->second->lk_or_h);
   if (it->second->lk_or_d) (void)hipFree(it->second->lk_or_d);
+  if (it->second->wsum_h) (void)hipHostFree(it->second->wsum_h);
+  if (it->second->wsum_d) (void)hipFree(it->second->wsum_d);
+  if (it->second->wsum_ev) (void)hipEventDestroy(it->second->wsum_ev);
+  if (it->second->up_h) (void)hipHostFree(it->second->up_h);
   g_pks.erase(it);
   return H2G_OK;
 }

@@ -102,6 +102,17 @@ struct CopySeg {
   uint64_t len;
 };
 hipError_t copy_segments(const CopySeg* d_segs, int nseg, uint64_t max_len, hipStream_t st);
+// dst[c][i] = src[c][i] (i < n) for up to COPY_COLS_MAX columns in one launch (dst[c] null:
+// no copy); with sum[c], also an order-independent 64-bit checksum of the source column
+// added into *sum[c] (every row mixed with its index, summed mod 2^64: the SPMD witness
+// digest, prover.cpp spmd_witness_fold)
+static constexpr int COPY_COLS_MAX = 16;
+struct ColCopy {
+  const Fr* src[COPY_COLS_MAX];
+  Fr* dst[COPY_COLS_MAX];
+  unsigned long long* sum[COPY_COLS_MAX];
+};
+hipError_t copy_columns(const ColCopy& b, int m, size_t n, bool sums, hipStream_t st);
 
 // e_i = a_i - a_{i+1} (e_{n-1} = a_{n-1}) for up to PREFIX_DIFF_MAX columns: the scalars of
 // a commitment against the prefix-summed Lagrange basis (prover.cpp lookup commitments)

@@ -815,6 +815,48 @@ hipError_t copy_segments(const CopySeg* d_segs, int nseg, uint64_t max_len, hipS
                        d_segs + s0);
   return hipGetLastError();
 }
+// the witness columns into the prover's workspace: a streaming kernel (one read, one write
+// per element) in place of per-column DMA copies, with the SPMD checksum on the same read
+__device__ __forceinline__ uint64_t fmix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  return x ^ (x >> 33);
+}
+template <bool SUM>
+__global__ void __launch_bounds__(256) copy_columns_kernel(ColCopy b, size_t n) {
+  const Fr* __restrict__ s = b.src[blockIdx.y];
+  Fr* __restrict__ d = b.dst[blockIdx.y];
+  uint64_t acc = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const Fr v = ldf(s + i);
+    if (d) stf(d + i, v);
+    if (SUM) {
+      uint64_t h = fmix64((uint64_t)i * 0x9e3779b97f4a7c15ull + 0x2545f4914f6cdd1dull);
+      for (int q = 0; q < 4; q++) h = fmix64(h ^ ((uint64_t)v.l[2 * q] | (uint64_t)v.l[2 * q + 1] << 32));
+      acc += h;
+    }
+  }
+  if (SUM) {
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    __shared__ uint64_t part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0 && b.sum[blockIdx.y])
+      atomicAdd(b.sum[blockIdx.y], (unsigned long long)(part[0] + part[1] + part[2] + part[3]));
+  }
+}
+hipError_t copy_columns(const ColCopy& b, int m, size_t n, bool sums, hipStream_t st) {
+  if (m <= 0 || n == 0) return hipSuccess;
+  if (m > COPY_COLS_MAX) return hipErrorInvalidValue;
+  const size_t blocks = std::min<size_t>((n + 255) / 256, 2048);
+  if (sums)
+    hipLaunchKernelGGL(copy_columns_kernel<true>, dim3((unsigned)blocks, (unsigned)m), dim3(256), 0, st, b, n);
+  else
+    hipLaunchKernelGGL(copy_columns_kernel<false>, dim3((unsigned)blocks, (unsigned)m), dim3(256), 0, st, b, n);
+  return hipGetLastError();
+}
 // ext[t + (m << e)] = subs[t n + m] for every t < 2^e: sub-coset slots back to row order
 __global__ void __launch_bounds__(KT) subcoset_scatter_kernel(const Fr* __restrict__ subs, Fr* __restrict__ ext,
                                                               size_t n, int e) {
