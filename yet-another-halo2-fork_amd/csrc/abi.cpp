@@ -271,6 +271,16 @@ int msm_collect(Device* d, MsmTicket* t, uint64_t* out) {
   return H2G_OK;
 }
 
+// the same, left in XYZZ form (the caller converts a batch with one inversion)
+int msm_collect_xyzz(Device* d, MsmTicket* t, G1xyzz* out) {
+  if (t->ring < 0) return fail(H2G_ERR_STATE, "msm: collect without launch");
+  HIPCHK(hipEventSynchronize(t->done));
+  *out = reinterpret_cast<const G1xyzz*>(d->h_ring)[t->ring];  // one window (fixed-base tickets)
+  d->ring_busy[t->ring] = false;
+  t->ring = -1;
+  return H2G_OK;
+}
+
 int msm_fence(Device* d, hipStream_t consumer) {
   if (!d->h_ring) return H2G_OK;
   for (int i = 0; i < MSM_STREAMS; i++) {

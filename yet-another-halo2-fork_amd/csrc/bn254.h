@@ -650,6 +650,30 @@ H2G_HD G1Affine xyzz_to_affine(const G1xyzz& p) {
   r.y = p.Y * izzz;
   return r;
 }
+// host: m points at once with one inversion (Montgomery's trick over the ZZ * ZZZ
+// products; a host inversion costs ~80 host products), for a stage's commitments
+inline void xyzz_to_affine_batch(const G1xyzz* p, G1Affine* out, int m) {
+  Fq* pre = new Fq[m > 0 ? m : 1];
+  Fq acc = Fq::one();
+  for (int i = 0; i < m; i++) {
+    pre[i] = acc;
+    if (!p[i].is_identity()) acc = acc * (p[i].ZZ * p[i].ZZZ);
+  }
+  Fq ia = inv(acc);  // 1 / prod of the non-identity points' ZZ ZZZ
+  for (int i = m - 1; i >= 0; i--) {
+    if (p[i].is_identity()) {
+      out[i].x = Fq::zero();
+      out[i].y = Fq::zero();
+      continue;
+    }
+    const Fq d = p[i].ZZ * p[i].ZZZ;
+    const Fq id = ia * pre[i];  // 1 / (ZZ ZZZ) of point i
+    ia = ia * d;
+    out[i].x = p[i].X * (id * p[i].ZZZ);
+    out[i].y = p[i].Y * (id * p[i].ZZ);
+  }
+  delete[] pre;
+}
 // the same with the wave-uniform divsteps inversion (kernels converting many points:
 // fixed-base tables, SRS, prefix bases)
 __device__ __forceinline__ G1Affine xyzz_to_affine_by(const G1xyzz& p) {

@@ -154,6 +154,7 @@ int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFi
                            hipStream_t producer, MsmTicket* t);
 // wait for a launched MSM, affine result
 int msm_collect(Device* d, MsmTicket* t, uint64_t* out_affine);
+int msm_collect_xyzz(Device* d, MsmTicket* t, G1xyzz* out);
 // make `consumer` wait until every launched MSM has finished reading its scalars
 int msm_fence(Device* d, hipStream_t consumer);
 int msm_desc_impl(Device* d, const void* sc, const Descriptor& ds, size_t off, size_t n, uint64_t* out, int* is_id,
