@@ -7,3 +7,5 @@ timeout -k 10 200 python3 -u tools/spmd_emulate.py --workload keccak --k 18 --wo
 timeout -k 10 200 python3 -u tools/spmd_emulate.py --workload c3 --k 22 --world 8 --ranks 0,3,6 --out $O/c3_n8.json > $O/c3.log 2>&1 || exit 1
 timeout -k 10 300 python3 -u bench.py > $O/bench.log 2>&1 || exit 1
 echo ok
+[ -n "$2" ] && { cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/tr -o run -- python3 -u $GRAFT_REPO_ROOT/tools/spmd_emulate.py --workload keccak --k 18 --world 8 --ranks 0 --steps 3 --warmup 1 > $GRAFT_REPO_ROOT/$O/tr.log 2>&1 || exit 1; }
+echo ok2

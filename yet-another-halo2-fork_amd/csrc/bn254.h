@@ -192,35 +192,48 @@ template <class P>
 __device__ __forceinline__ Fe<P> operator*(const Fe<P>& A, const Fe<P>& B) {
   return reduce_once(mont_mul_lazy(A, B));  // fully reduced inputs: result < 2M
 }
-// Host: CIOS with the "no final carry" shortcut (top modulus limb < 2^31 - 1 for
-// both BN254 moduli), 32-bit limbs.  Returns a*b*2^-256 mod M, fully reduced.
+// Host: CIOS with the "no final carry" shortcut (top modulus limb < 2^63 - 1 for both
+// BN254 moduli) over 64-bit limbs (~4x fewer multiplies than 32-bit limbs: the prover's
+// host side -- commitment sums, SHPLONK's coefficients -- is latency-bound on these).
+// Returns a*b*2^-256 mod M, fully reduced.
+template <class P>
+__host__ constexpr uint64_t host_inv64() {  // -M^-1 mod 2^64 from P::INV = -M^-1 mod 2^32
+  const uint64_t m0 = (uint64_t)P::M[0] | (uint64_t)P::M[1] << 32;
+  uint64_t x = (uint64_t)(0u - P::INV);  // M^-1 mod 2^32
+  x = x * (2 - m0 * x);                  // Newton: M^-1 mod 2^64
+  return 0 - x;
+}
 template <class P>
 __host__ inline Fe<P> operator*(const Fe<P>& a, const Fe<P>& b) {
-  uint32_t t[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) t[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint32_t bi = b.l[i];
-    uint64_t x = (uint64_t)a.l[0] * bi + t[0];
-    uint32_t A = (uint32_t)(x >> 32);
-    const uint32_t t0 = (uint32_t)x;
-    const uint32_t m = t0 * P::INV;
-    uint64_t y = (uint64_t)m * P::M[0] + t0;
-    uint32_t C = (uint32_t)(y >> 32);
-#pragma unroll
-    for (int j = 1; j < 8; j++) {
-      x = (uint64_t)a.l[j] * bi + t[j] + A;
-      A = (uint32_t)(x >> 32);
-      y = (uint64_t)m * P::M[j] + (uint32_t)x + C;
-      C = (uint32_t)(y >> 32);
-      t[j - 1] = (uint32_t)y;
+  using u128 = unsigned __int128;
+  constexpr uint64_t inv = host_inv64<P>();
+  uint64_t A[4], B[4], M[4], t[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    A[i] = (uint64_t)a.l[2 * i] | (uint64_t)a.l[2 * i + 1] << 32;
+    B[i] = (uint64_t)b.l[2 * i] | (uint64_t)b.l[2 * i + 1] << 32;
+    M[i] = (uint64_t)P::M[2 * i] | (uint64_t)P::M[2 * i + 1] << 32;
+  }
+  for (int i = 0; i < 4; i++) {
+    u128 x = (u128)A[0] * B[i] + t[0];
+    uint64_t hi = (uint64_t)(x >> 64);
+    const uint64_t t0 = (uint64_t)x;
+    const uint64_t m = t0 * inv;
+    u128 y = (u128)m * M[0] + t0;
+    uint64_t c = (uint64_t)(y >> 64);
+    for (int j = 1; j < 4; j++) {
+      x = (u128)A[j] * B[i] + t[j] + hi;
+      hi = (uint64_t)(x >> 64);
+      y = (u128)m * M[j] + (uint64_t)x + c;
+      c = (uint64_t)(y >> 64);
+      t[j - 1] = (uint64_t)y;
     }
-    t[7] = C + A;
+    t[3] = c + hi;
   }
   Fe<P> r;
-#pragma unroll
-  for (int i = 0; i < 8; i++) r.l[i] = t[i];
+  for (int i = 0; i < 4; i++) {
+    r.l[2 * i] = (uint32_t)t[i];
+    r.l[2 * i + 1] = (uint32_t)(t[i] >> 32);
+  }
   return reduce_once(r);
 }
 
