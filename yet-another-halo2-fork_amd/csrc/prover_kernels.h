@@ -104,7 +104,7 @@ struct CopySeg {
 hipError_t copy_segments(const CopySeg* d_segs, int nseg, uint64_t max_len, hipStream_t st);
 // dst[c][i] = src[c][i] (i < n) for up to COPY_COLS_MAX columns in one launch (dst[c] null:
 // no copy); with sum[c], also an order-independent 64-bit checksum of the source column
-// added into *sum[c] (every row mixed with its index, summed mod 2^64: the SPMD witness
+// added into *sum[c] (every 16-byte chunk mixed with its index, summed mod 2^64: the SPMD witness
 // digest, prover.cpp spmd_witness_fold)
 static constexpr int COPY_COLS_MAX = 16;
 struct ColCopy {

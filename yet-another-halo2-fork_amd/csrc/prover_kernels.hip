@@ -824,19 +824,30 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t x) {
   x *= 0xc4ceb9fe1a85ec53ull;
   return x ^ (x >> 33);
 }
+// 16-byte chunks (lane-contiguous, fully coalesced), 4 per thread and iteration so that a
+// wave has 4 loads in flight; the checksum mixes each chunk with its index
+__device__ __forceinline__ uint64_t chunk_mix(size_t i, const uint4& v) {
+  uint64_t h = fmix64((uint64_t)i * 0x9e3779b97f4a7c15ull + 0x2545f4914f6cdd1dull);
+  h = fmix64(h ^ ((uint64_t)v.x | (uint64_t)v.y << 32));
+  return fmix64(h ^ ((uint64_t)v.z | (uint64_t)v.w << 32));
+}
 template <bool SUM>
-__global__ void __launch_bounds__(256) copy_columns_kernel(ColCopy b, size_t n) {
-  const Fr* __restrict__ s = b.src[blockIdx.y];
-  Fr* __restrict__ d = b.dst[blockIdx.y];
+__global__ void __launch_bounds__(256) copy_columns_kernel(ColCopy b, size_t n2) {
+  const uint4* __restrict__ s = reinterpret_cast<const uint4*>(b.src[blockIdx.y]);
+  uint4* __restrict__ d = reinterpret_cast<uint4*>(b.dst[blockIdx.y]);
   uint64_t acc = 0;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const Fr v = ldf(s + i);
-    if (d) stf(d + i, v);
-    if (SUM) {
-      uint64_t h = fmix64((uint64_t)i * 0x9e3779b97f4a7c15ull + 0x2545f4914f6cdd1dull);
-      for (int q = 0; q < 4; q++) h = fmix64(h ^ ((uint64_t)v.l[2 * q] | (uint64_t)v.l[2 * q + 1] << 32));
-      acc += h;
-    }
+  const size_t step = (size_t)gridDim.x * 1024;
+  for (size_t i = blockIdx.x * (size_t)1024 + threadIdx.x; i < n2; i += step) {
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (i + 256 * k < n2) v[k] = s[i + 256 * k];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (i + 256 * k < n2) {
+        if (d) d[i + 256 * k] = v[k];
+        if (SUM) acc += chunk_mix(i + 256 * k, v[k]);
+      }
   }
   if (SUM) {
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
@@ -850,11 +861,12 @@ __global__ void __launch_bounds__(256) copy_columns_kernel(ColCopy b, size_t n) 
 hipError_t copy_columns(const ColCopy& b, int m, size_t n, bool sums, hipStream_t st) {
   if (m <= 0 || n == 0) return hipSuccess;
   if (m > COPY_COLS_MAX) return hipErrorInvalidValue;
-  const size_t blocks = std::min<size_t>((n + 255) / 256, 2048);
+  const size_t n2 = 2 * n;  // 16-byte chunks of the 32-byte elements
+  const size_t blocks = std::min<size_t>((n2 + 1023) / 1024, 1024);
   if (sums)
-    hipLaunchKernelGGL(copy_columns_kernel<true>, dim3((unsigned)blocks, (unsigned)m), dim3(256), 0, st, b, n);
+    hipLaunchKernelGGL(copy_columns_kernel<true>, dim3((unsigned)blocks, (unsigned)m), dim3(256), 0, st, b, n2);
   else
-    hipLaunchKernelGGL(copy_columns_kernel<false>, dim3((unsigned)blocks, (unsigned)m), dim3(256), 0, st, b, n);
+    hipLaunchKernelGGL(copy_columns_kernel<false>, dim3((unsigned)blocks, (unsigned)m), dim3(256), 0, st, b, n2);
   return hipGetLastError();
 }
 // ext[t + (m << e)] = subs[t n + m] for every t < 2^e: sub-coset slots back to row order
