@@ -114,6 +114,38 @@ def cpu_threads():
     return aff, f"sched_getaffinity: {aff} CPUs"
 
 
+def box_smi():
+    """clocks, power and power cap of the GPUs as rocm-smi reports them (best effort)"""
+    import subprocess
+    try:
+        r = subprocess.run(["rocm-smi", "--showclocks", "--showpower", "--showmaxpower", "--showperflevel", "--json"],
+                           capture_output=True, text=True, timeout=30)
+        d = json.loads(r.stdout[r.stdout.index("{"):])
+    except Exception as e:  # the line stands without it
+        return {"error": f"{type(e).__name__}"}
+    out = {}
+    for card, v in d.items():
+        if not card.startswith("card"):
+            continue
+        keep = {}
+        for k, val in v.items():
+            kl = k.lower()
+            if any(t in kl for t in ("sclk", "mclk", "fclk", "power", "perf")):
+                keep[k] = val
+        out[card] = keep
+    return out
+
+
+def box_block(h2g):
+    """box calibration, measured before the timed region: this GPU's
+    Montgomery product rate now (tools/microbench kernels, csrc/calib.hip), its shader
+    clock under that load, and rocm-smi's clocks / power / power cap"""
+    b = h2g.box_calibrate()
+    b["reference_fips_gps"] = MODMUL_REF_GPS
+    b["smi"] = box_smi()
+    return b
+
+
 def cpu_baseline_prove(circ, wit, g, gl, k, reps=1):
     """The oracle's create_proof (C restatement of halo2's prover: best_multiexp /
     best_fft / parallelize, OpenMP over `threads` cores) of the SAME circuit, witness and
@@ -240,9 +272,13 @@ def pmc_child(args):
 # the quarter rate of v_mad_u64_u32 is not in the guide's tables)
 MODMUL_PEAK_MICROBENCH = 125e9
 MODMUL_PEAK_ISSUE = 256 * 4 * 32 * 2.4e9 / (128 * 4 + 64)
+# the FIPS product rate of the round-4 reference boxes: value_normalised = value x
+# (this box's FIPS rate / this), i.e. the proof time scaled to a box of that speed
+MODMUL_REF_GPS = 125.0
 
 
-def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note, window_bits=0, union=None):
+def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note, window_bits=0, union=None,
+                         peak_gps=None):
     acc_ms = phases.get("accumulate", 0.0) / max(calls, 1)
     achieved = (points_per_launch * MSM_BYTES_PER_POINT) / (acc_ms * 1e-3) / 1e9 if acc_ms > 0 else None
     c = window_bits or fixed_c(points_per_launch)
@@ -277,6 +313,10 @@ def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note
                  "madds_per_launch": round(madds), "madds": madd_source},
         "window_bits": c,
     }
+    if peak_gps and modmul_rate:  # this box's product rate, measured before the timed region
+        out["valu"].update({"peak_box": round(peak_gps, 2), "frac_box": round(modmul_rate / (peak_gps * 1e9), 4),
+                            "peak_box_note": "F29 Montgomery products/s of this GPU (h2g_profile_box_calibrate), "
+                                             "the arithmetic the accumulation runs"})
     if traffic:  # PMC bytes per launch, calibrated per access kind (pmc_traffic)
         stream = madds * 4.0  # the u32 bucket-ordered values, read once
         cal = traffic["fetch"] + 0.5 * stream + traffic["write"]
@@ -504,6 +544,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         for _ in range(args.steps):
             step()
 
+    box = box_block(h2g) if rank == 0 else None  # before the timed region
     session(warm)
     torch.cuda.synchronize()
     if world > 1:
@@ -630,6 +671,9 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                                        + " slabs + partials), NTT/evaluate_h/SHPLONK on rank 0" if shard else
                                        f"{world} independent provers")},
             "roofline": roofline_from_phases(calls, phases, n_local, traffic, traffic_note, union=union),
+            "box": box,
+            "value_normalised": round(elapsed / (args.steps * (1 if one_proof else world)) *
+                                      box["modmul_fips_gps"] / MODMUL_REF_GPS, 4),
             "msm_in_prover": {"launches_per_proof": calls // max(args.steps, 1), "avg_ms": round(msm_ms, 4),
                               "busy_ms_per_proof": round(union["msm"] / args.steps, 3),
                               "accumulate_busy_ms_per_proof": round(union["accumulate"] / args.steps, 3),
@@ -639,6 +683,22 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             "verified": extra["verified"],
             "stages_ms_synced_proof": {nm: round(ms, 3) for nm, ms in stages},
         }
+        if world == 1 and args.workload == "prove":
+            # the roofline's kernel figure from lone launches of the same MSM shape (no other
+            # stream's kernels inside a launch); the in-proof launches' figures stay beside it
+            rp = line["roofline"]
+            lcalls, lphases, lunion = lone_msm_leg(h2g, torch, dev, k)
+            roof = roofline_from_phases(lcalls, lphases, n, traffic, traffic_note,
+                                        union={"entries": lunion.get("entries")}, peak_gps=box["modmul_f29_gps"])
+            roof["kernel_ms_source"] = (f"mean HIP-event duration of msm_acc_kernel over {lcalls} lone 2^{k} "
+                                        "fixed-base MSMs (lone_msm_leg, outside the timed region; one stream, "
+                                        "nothing else in flight)")
+            roof["in_proof"] = {"kernel_ms": rp["kernel_ms"], "launches": rp["launches"],
+                                "valu_achieved": rp["valu"]["achieved"], "valu_aggregate": rp["valu"].get("aggregate"),
+                                "note": "the timed proofs' launches, HIP events on the two MSM streams: a launch "
+                                        "that shares the chip with the other stream's MSM runs longer; aggregate = "
+                                        "all launches' modmuls / the union of their intervals"}
+            line["roofline"] = roof
         if pcie:
             line["pcie_inclusive"] = pcie
             line["pcie_inclusive_s"] = pcie["median_s"]
@@ -679,6 +739,36 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         line["cpu_baseline"] = cb
         line["gpu_vs_cpu"] = round(cb["value"] / line["value"], 1)
     return line
+
+
+def lone_msm_leg(h2g, torch, dev, log_n, steps=10, warmup=2):
+    """the dominant kernel measured alone: `steps` fixed-base MSMs of 2^log_n resident SRS
+    points (the proof's commitment shape: same n, same window bits, same table layout), one
+    at a time on one stream, so the accumulation's HIP events bracket a launch with no other
+    kernel in flight -- the figure tools/trace_grid_stats.py recomputes from the trace
+    ("lone" rows of msm_acc_kernel at that grid)"""
+    import h2g_circuit as hc
+    stream = torch.cuda.current_stream().cuda_stream
+    n = 1 << log_n
+    rng = np.random.default_rng(4242)
+    bases = torch.empty((n, 8), dtype=torch.int64, device=dev)
+    h2g.srs_setup_dev(np.asarray(hc.fr_to_limbs(0x1234567), dtype=np.uint64), n, bases.data_ptr(), stream)
+    scalars = torch.from_numpy(random_scalars(rng, n).view(np.int64)).to(dev)
+    torch.cuda.synchronize()
+    base = h2g.base_descriptor_dev(bases.data_ptr(), n, 0)
+    for _ in range(warmup):
+        h2g.msm_with_cached_base_dev(scalars.data_ptr(), n, base, 0, stream)
+    torch.cuda.synchronize()
+    h2g.profile_enable(True)
+    for _ in range(steps):
+        h2g.msm_with_cached_base_dev(scalars.data_ptr(), n, base, 0, stream)
+    torch.cuda.synchronize()
+    h2g.profile_enable(False)
+    calls, phases, union = h2g.profile_msm_collect(with_union=True)
+    h2g.descriptor_free(base)
+    del bases, scalars
+    torch.cuda.empty_cache()
+    return calls, phases, union
 
 
 def k_range(h2g, torch, dev, args):

@@ -153,6 +153,11 @@ int h2g_profile_msm_collect(float* ms, int max_phases, int* n_phases, int* calls
  * accumulation) summed, before collect() resets them; *uncounted = MSMs past the
  * recorder's capacity (may be NULL) */
 int h2g_profile_msm_entries(uint64_t* total, int* uncounted);
+/* box calibration (bench line): Montgomery product throughput of this GPU now, in the two
+ * limb forms the prover uses -- out[0] 8 x 32-bit FIPS, out[1] 9 x 29-bit (G products/s)
+ * -- out[2] the shader clock during the run (GHz, s_memtime vs s_memrealtime), out[3] the
+ * wall ms spent (~100); max >= 4.  Not part of the prover's interface. */
+int h2g_profile_box_calibrate(double* out, int max);
 
 /* ---- host-side point helpers (used to combine per-GPU MSM partials) -------- */
 int h2g_g1_add_affine(const uint64_t a[8], const uint64_t b[8], uint64_t out[8]);

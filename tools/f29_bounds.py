@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Value bounds of the F29 XYZZ mixed addition (csrc/f29.h xyzz29_madd), checked.
+
+Every quantity is tracked as an integer upper bound; a Montgomery product (R = 2^261) of
+x < A and y < B is < A B / R + M.  Starting from each state the accumulation can begin in
+(a fresh point: X, Y < 32 M, ZZ = ZZZ = one < M; the doubling path: all four < 32 M) the
+madd map is iterated to its fixpoint, and at every step the script asserts what the
+kernel relies on:
+  * each subtraction a - b + k M has k M > b with a top-limb margin (kmul_safe's borrow of
+    1 (offset 29) or 4 (offset 31) from the top limb: the top limb of k M minus it still
+    covers b's top limb), so no limb goes negative;
+  * every value stays below 2^261 (normalised 29-bit limbs, top limb < 2^29);
+  * every product's column sums stay below 2^64 (limb bounds of the operands).
+    python tools/f29_bounds.py
+"""
+import math
+
+M = 0x30644e72e131a029b85045b68181585d97816a916871ca8d3c208c16d87cfd47  # BN254 Fq
+R = 2 ** 261
+LG = math.log2
+
+
+def top(v):
+    return v >> 232
+
+
+def mul(a, b):
+    return a * b // R + M + 1
+
+
+def sub_ok(b, k, off):
+    """a - b + k M limb-wise: the top limb of k M minus the borrow must cover b's top limb"""
+    unit = 1 << (off - 29)
+    assert top(k * M) - unit >= top(b), (k, off, LG(b), LG(k * M))
+
+
+def column_ok(la, lb, lc=0, ld=0):
+    """max column sum of REDC(a b [+ c d]) with limb bounds la, lb (lc, ld), m M < 2^58"""
+    s = 9 * la * lb + 9 * lc * ld + 9 * (1 << 58) + (1 << 35)
+    assert s < 1 << 64, LG(s)
+
+
+def madd(st, xq, yq):
+    X, Y, ZZ, ZZZ = st
+    n29 = 1 << 29
+    U2, S2 = mul(xq, ZZ), mul(yq, ZZZ)
+    sub_ok(X, 64, 29)
+    sub_ok(Y, 64, 29)
+    P, Rr = U2 + 64 * M, S2 + 64 * M
+    PP, R2 = mul(P, P), mul(Rr, Rr)
+    PPP, Q = mul(P, PP), mul(X, PP)
+    T = PPP + 2 * Q
+    sub_ok(T, 32, 31)
+    X3 = R2 + 32 * M
+    sub_ok(X3, 64, 29)
+    D = Q + 64 * M
+    sub_ok(PPP, 16, 29)
+    E = 16 * M
+    column_ok(n29, n29)                                  # normalised operands
+    column_ok(n29, n29 + (1 << 30), n29, 1 << 30)        # R (Q - X3 + 64M) + Y (16M - PPP)
+    Y3 = (Rr * D + Y * E) // R + M + 1
+    ZZ3, ZZZ3 = mul(ZZ, PP), mul(ZZZ, PPP)
+    inter = dict(U2=U2, S2=S2, P=P, R=Rr, PP=PP, PPP=PPP, Q=Q, R2=R2, X3=X3, D=D, E=E, Y3=Y3)
+    for k, v in inter.items():
+        assert v < 1 << 261, (k, LG(v))
+    return (X3, Y3, ZZ3, ZZZ3), inter
+
+
+def run(name, st):
+    xq = yq = 32 * M
+    worst = 0
+    for _ in range(60):
+        nxt, inter = madd(st, xq, yq)
+        worst = max(worst, *nxt, *inter.values())
+        st = tuple(max(a, b) for a, b in zip(st, nxt))  # bounds only grow
+    print(f"{name}: fixpoint log2 X Y ZZ ZZZ = {[round(LG(v), 3) for v in st]}, "
+          f"largest intermediate 2^{LG(worst):.3f}")
+
+
+if __name__ == "__main__":
+    run("fresh point", (32 * M, 32 * M, M, M))
+    d = mul(32 * M, M)
+    run("doubling path", (d, d, d, d))
+    print("ok")

@@ -1,0 +1,357 @@
+// f29.h -- BN254 field elements in 9 unsaturated 29-bit limbs (Montgomery, R = 2^261).
+//
+// Why: the 8 x 32-bit FIPS product of bn254.h spends one v_addc_co_u32 per
+// v_mad_u64_u32 to catch the 64-bit column accumulator's carry-out.  With 29-bit limbs a
+// 32x32->64 product is < 2^60 and one column (<= 9 a.b terms + <= 9 m.M terms) stays far
+// below 2^64, so every product term is a lone v_mad_u64_u32 (no carry handling) and a
+// column ends with one 64-bit shift: 162 mads + ~30 other ops against 128 mads + 128
+// addcs + ~24 for the 32-bit form.
+//
+// Representation.  A value v is 9 limbs l[0..8], v = sum l[i] 2^(29 i); limbs 0..7 are
+// kept < 2^29 ("normalised"); the top limb may hold a few more bits.  v represents the
+// field element v * 2^-261 mod M.  The storage form used everywhere else (bn254.h:
+// a * 2^256 mod M in 8 x 32-bit limbs, fully reduced) converts exactly by a shift: x * 32
+// represents the same element here (x * 2^256 * 2^5 = x' * 2^261), so to29() is a
+// repacking, not a product.  Values are not reduced: they carry multiples of M, bounded by
+// the caller's data flow (see mul29's bound), and a zero test is a test modulo M.
+#pragma once
+#include "bn254.h"
+
+namespace h2g {
+
+static constexpr uint32_t F29_MASK = (1u << 29) - 1;
+
+// 29-bit limb i of (x << sh) for a 256-bit constant x given as 8 LE 32-bit limbs
+H2G_HD constexpr uint32_t limb29_of(const uint32_t* x, int i, int sh) {
+  const int b = 29 * i - sh;  // bit offset in x
+  if (b < 0) return (x[0] << (-b)) & F29_MASK;
+  const int w = b >> 5, s = b & 31;
+  const uint64_t lo = w < 8 ? x[w] : 0;
+  const uint64_t hi = w + 1 < 8 ? x[w + 1] : 0;
+  return (uint32_t)(((hi << 32) | lo) >> s) & F29_MASK;
+}
+template <class P>
+struct C29 {
+  static constexpr uint32_t M[9] = {limb29_of(P::M, 0, 0), limb29_of(P::M, 1, 0), limb29_of(P::M, 2, 0),
+                                    limb29_of(P::M, 3, 0), limb29_of(P::M, 4, 0), limb29_of(P::M, 5, 0),
+                                    limb29_of(P::M, 6, 0), limb29_of(P::M, 7, 0), limb29_of(P::M, 8, 0)};
+  static constexpr uint32_t INV = P::INV & F29_MASK;  // -M^-1 mod 2^29
+  // 2^256 mod M (= P::ONE) in 29-bit limbs: REDC(v * ONE) = v * 2^-5 mod M, the storage form
+  static constexpr uint32_t ONE256[9] = {limb29_of(P::ONE, 0, 0), limb29_of(P::ONE, 1, 0), limb29_of(P::ONE, 2, 0),
+                                         limb29_of(P::ONE, 3, 0), limb29_of(P::ONE, 4, 0), limb29_of(P::ONE, 5, 0),
+                                         limb29_of(P::ONE, 6, 0), limb29_of(P::ONE, 7, 0), limb29_of(P::ONE, 8, 0)};
+};
+
+struct F29 {
+  uint32_t l[9];
+};
+
+// ---- constants as 9-limb arrays (compile time)
+struct Limbs9 {
+  uint32_t v[9];
+};
+// k * M in normalised 29-bit limbs (k M < 2^264)
+template <class P>
+constexpr Limbs9 kmul_norm(uint32_t k) {
+  Limbs9 r{};
+  uint64_t c = 0;
+  for (int i = 0; i < 9; i++) {
+    const uint64_t t = (uint64_t)limb29_of(P::M, i, 0) * k + c;
+    r.v[i] = i < 8 ? (uint32_t)(t & F29_MASK) : (uint32_t)t;
+    c = t >> 29;
+  }
+  return r;
+}
+// limb i of k * M in "borrow-safe" form: limbs 0..7 raised by 2^off (the top limb lowered to
+// compensate), so that c - b never borrows in a limb for any b whose limbs 0..7 are below
+// 2^off and whose top limb is below the top limb of the result (same value k M)
+template <class P>
+constexpr uint32_t kmul_safe(uint32_t k, int off, int i) {
+  const Limbs9 n = kmul_norm<P>(k);
+  const uint32_t unit = 1u << (off - 29);
+  if (i == 0) return n.v[0] + (1u << off);
+  if (i < 8) return n.v[i] + (1u << off) - unit;
+  return n.v[8] - unit;
+}
+template <class P, uint32_t K, int OFF>
+struct KM29 {
+  static constexpr uint32_t L[9] = {kmul_safe<P>(K, OFF, 0), kmul_safe<P>(K, OFF, 1), kmul_safe<P>(K, OFF, 2),
+                                    kmul_safe<P>(K, OFF, 3), kmul_safe<P>(K, OFF, 4), kmul_safe<P>(K, OFF, 5),
+                                    kmul_safe<P>(K, OFF, 6), kmul_safe<P>(K, OFF, 7), kmul_safe<P>(K, OFF, 8)};
+};
+// 2^261 mod M (the element 1), reduced: 32 * (2^256 mod M) minus the multiple of M it holds
+template <class P>
+constexpr Limbs9 one29() {
+  Limbs9 r{};
+  for (int i = 0; i < 9; i++) r.v[i] = limb29_of(P::ONE, i, 5);
+  for (int it = 0; it < 40; it++) {  // while r >= M: r -= M
+    bool ge = true;
+    for (int i = 8; i >= 0; i--) {
+      const uint32_t m = limb29_of(P::M, i, 0);
+      if (r.v[i] != m) {
+        ge = r.v[i] > m;
+        break;
+      }
+    }
+    if (!ge) break;
+    int64_t br = 0;
+    for (int i = 0; i < 9; i++) {
+      int64_t t = (int64_t)r.v[i] - limb29_of(P::M, i, 0) + br;
+      br = t < 0 ? -1 : 0;
+      r.v[i] = (uint32_t)(t & F29_MASK);
+    }
+  }
+  return r;
+}
+template <class P>
+struct One29 {
+  static constexpr Limbs9 v = one29<P>();
+  static constexpr uint32_t L[9] = {v.v[0], v.v[1], v.v[2], v.v[3], v.v[4], v.v[5], v.v[6], v.v[7], v.v[8]};
+};
+
+// storage (Montgomery 2^256, 8 x 32-bit limbs, value < 2^256) -> F29 of the same element:
+// the integer x * 32 < 2^261, repacked into 29-bit limbs
+template <class P>
+H2G_HD F29 to29(const Fe<P>& x) {
+  F29 r;
+  r.l[0] = (x.l[0] << 5) & F29_MASK;
+#pragma unroll
+  for (int i = 1; i < 9; i++) {
+    const int b = 29 * i - 5, w = b >> 5, s = b & 31;
+    const uint64_t lo = x.l[w];
+    const uint64_t hi = w + 1 < 8 ? x.l[w + 1] : 0;
+    r.l[i] = (uint32_t)(((hi << 32) | lo) >> s) & F29_MASK;
+  }
+  return r;
+}
+
+// Montgomery product REDC(a b) = a b 2^-261 mod M, as an unreduced value < a b / 2^261 + M.
+// Column bound: with limbs of a and b < 2^30 (top limbs < 2^31) every column sum stays
+// < 2^64, so inputs may be one unnormalised limb-wise add away from normalised values.
+// Output limbs 0..7 normalised; the top limb is the rest (< 2^32 for outputs < 2^264).
+template <class P>
+H2G_HD F29 mul29(const F29& a, const F29& b) {
+  uint32_t m[9];
+  F29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+#pragma unroll
+    for (int i = 0; i <= k; i++) acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+    for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * C29<P>::M[k - i];
+    m[k] = ((uint32_t)acc * C29<P>::INV) & F29_MASK;
+    acc += (uint64_t)m[k] * C29<P>::M[0];
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+#pragma unroll
+    for (int i = k - 8; i < 9; i++) {
+      acc += (uint64_t)a.l[i] * b.l[k - i];
+      acc += (uint64_t)m[i] * C29<P>::M[k - i];
+    }
+    r.l[k - 9] = (uint32_t)acc & F29_MASK;
+    acc >>= 29;
+  }
+  r.l[8] = (uint32_t)acc;
+  return r;
+}
+
+// F29 -> storage form, fully reduced: REDC(v * (2^256 mod M)) = v 2^-5 mod M (< 2M for
+// v < 2^261, i.e. a normalised top limb), one conditional subtraction, repacked into 32-bit limbs
+template <class P>
+H2G_HD Fe<P> from29(const F29& v) {
+  F29 k;
+#pragma unroll
+  for (int i = 0; i < 9; i++) k.l[i] = C29<P>::ONE256[i];
+  const F29 t = mul29<P>(v, k);
+  Fe<P> r;
+  uint64_t acc = 0;
+  int have = 0, w = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    acc |= (uint64_t)t.l[i] << have;
+    have += 29;
+    if (have >= 32 && w < 8) {
+      r.l[w++] = (uint32_t)acc;
+      acc >>= 32;
+      have -= 32;
+    }
+  }
+  if (w < 8) r.l[w] = (uint32_t)acc;
+  return reduce_once(r);
+}
+
+
+// ---- limb-wise add / subtract, normalisation
+H2G_HD F29 add29(const F29& a, const F29& b) {  // no carries: limbs grow by one bit
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = a.l[i] + b.l[i];
+  return r;
+}
+// a - b + K M, limb-wise without borrows (b's limbs 0..7 below 2^OFF, see kmul_safe); the
+// result is unnormalised (limbs 0..7 below 2^(OFF+1) + 2^29)
+template <class P, uint32_t K, int OFF>
+H2G_HD F29 sub29(const F29& a, const F29& b) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = (a.l[i] + KM29<P, K, OFF>::L[i]) - b.l[i];
+  return r;
+}
+// carries of limbs 0..7 into the next limb (limbs are non-negative)
+H2G_HD F29 norm29(F29 a) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.l[i + 1] += a.l[i] >> 29;
+    a.l[i] &= F29_MASK;
+  }
+  return a;
+}
+
+// REDC(a b + c d): two products under one Montgomery reduction (the m M terms are shared).
+// Column bound: a, c normalised and b, d limbs below 1.5 * 2^30 keep every column < 2^64.
+template <class P>
+H2G_HD F29 mul29x2(const F29& a, const F29& b, const F29& c, const F29& d) {
+  uint32_t m[9];
+  F29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+#pragma unroll
+    for (int i = 0; i <= k; i++) {
+      acc += (uint64_t)a.l[i] * b.l[k - i];
+      acc += (uint64_t)c.l[i] * d.l[k - i];
+    }
+#pragma unroll
+    for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * C29<P>::M[k - i];
+    m[k] = ((uint32_t)acc * C29<P>::INV) & F29_MASK;
+    acc += (uint64_t)m[k] * C29<P>::M[0];
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+#pragma unroll
+    for (int i = k - 8; i < 9; i++) {
+      acc += (uint64_t)a.l[i] * b.l[k - i];
+      acc += (uint64_t)c.l[i] * d.l[k - i];
+      acc += (uint64_t)m[i] * C29<P>::M[k - i];
+    }
+    r.l[k - 9] = (uint32_t)acc & F29_MASK;
+    acc >>= 29;
+  }
+  r.l[8] = (uint32_t)acc;
+  return r;
+}
+
+// a == 0 mod M for a normalised a < 2^(29*8+32): a = k M with k < 2^29 has low limb
+// k M_0 mod 2^29, so k = a_0 M^-1 mod 2^29 is the only candidate (a cheap filter; the exact
+// comparison runs only when k is small enough to be real)
+template <class P>
+H2G_HD bool is_zero29(const F29& a) {
+  constexpr uint32_t minv = (0u - C29<P>::INV) & F29_MASK;  // M^-1 mod 2^29
+  const uint32_t k = (a.l[0] * minv) & F29_MASK;
+  if (k > 1024) return false;
+  uint64_t c = 0;
+  uint32_t diff = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint64_t t = (uint64_t)C29<P>::M[i] * k + c;
+    const uint32_t limb = i < 8 ? (uint32_t)(t & F29_MASK) : (uint32_t)t;
+    c = t >> 29;
+    diff |= limb ^ a.l[i];
+  }
+  return diff == 0;
+}
+template <class P>
+H2G_HD F29 one29v() {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = One29<P>::L[i];
+  return r;
+}
+
+// ---- G1 (XYZZ) over Fq in F29 limbs: the MSM bucket accumulation's arithmetic
+// identity <=> ZZ is exactly zero (only ever created explicitly: a product of two nonzero
+// elements is a nonzero element, hence never the integer 0)
+struct G1xyzz29 {
+  F29 X, Y, ZZ, ZZZ;
+};
+H2G_HD G1xyzz29 xyzz29_identity() {
+  G1xyzz29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.X.l[i] = r.Y.l[i] = r.ZZ.l[i] = r.ZZZ.l[i] = 0;
+  return r;
+}
+H2G_HD bool xyzz29_is_identity(const G1xyzz29& p) {
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) z |= p.ZZ.l[i];
+  return z == 0;
+}
+// storage-form XYZZ (canonical 32-bit limbs) of a raw F29 accumulator
+template <class P = FqParams>
+H2G_HD G1xyzz xyzz_from29(const G1xyzz29& p) {
+  G1xyzz r;
+  r.X = from29<FqParams>(p.X);
+  r.Y = from29<FqParams>(p.Y);
+  r.ZZ = from29<FqParams>(p.ZZ);
+  r.ZZZ = from29<FqParams>(p.ZZZ);
+  return r;
+}
+// canonical storage form in; each coordinate reduced below 1.2 M (REDC(32 v * one))
+template <class P>
+H2G_HD F29 to29_reduced(const Fe<P>& v) {
+  return mul29<P>(to29(v), one29v<P>());
+}
+H2G_HD G1xyzz29 xyzz29_from_xyzz(const G1xyzz& p) {
+  G1xyzz29 r;
+  r.X = to29_reduced(p.X);
+  r.Y = to29_reduced(p.Y);
+  r.ZZ = to29_reduced(p.ZZ);
+  r.ZZZ = to29_reduced(p.ZZZ);
+  return r;
+}
+
+// p + q for an affine q given as F29 coordinates of its canonical storage form (to29:
+// values 32 x < 32 M), madd-2008-s.  Value bounds (tools/f29_bounds.py iterates this data
+// flow from a fresh point to its fixpoint): every coordinate of p stays < 2^259.5, every
+// intermediate < 2^259.9, so the subtraction constants below (64 M, 32 M, 64 M, 16 M)
+// exceed what they subtract and every product's columns stay < 2^64.
+H2G_HD G1xyzz29 xyzz29_madd(const G1xyzz29& p, const F29& qx, const F29& qy) {
+  using P = FqParams;
+  if (xyzz29_is_identity(p)) {
+    G1xyzz29 r;
+    r.X = qx;
+    r.Y = qy;
+    r.ZZ = one29v<P>();
+    r.ZZZ = r.ZZ;
+    return r;
+  }
+  const F29 U2 = mul29<P>(qx, p.ZZ);
+  const F29 S2 = mul29<P>(qy, p.ZZZ);
+  const F29 Pp = norm29(sub29<P, 64, 29>(U2, p.X));
+  const F29 R = norm29(sub29<P, 64, 29>(S2, p.Y));
+  if (is_zero29<P>(Pp)) {
+    if (is_zero29<P>(R)) {  // p == q: double q (storage form, rare)
+      G1Affine a;
+      a.x = from29<P>(qx);
+      a.y = from29<P>(qy);
+      return xyzz29_from_xyzz(xyzz_mdbl(a));
+    }
+    return xyzz29_identity();  // p == -q
+  }
+  const F29 PP = mul29<P>(Pp, Pp);
+  const F29 PPP = mul29<P>(Pp, PP);
+  const F29 Q = mul29<P>(p.X, PP);
+  const F29 R2 = mul29<P>(R, R);
+  G1xyzz29 r;
+  r.X = norm29(sub29<P, 32, 31>(R2, add29(add29(PPP, Q), Q)));  // R^2 - PPP - 2Q
+  r.Y = mul29x2<P>(R, sub29<P, 64, 29>(Q, r.X), p.Y, sub29<P, 16, 29>(F29{}, PPP));  // R (Q - X3) - Y PPP
+  r.ZZ = mul29<P>(p.ZZ, PP);
+  r.ZZZ = mul29<P>(p.ZZZ, PPP);
+  return r;
+}
+
+}  // namespace h2g

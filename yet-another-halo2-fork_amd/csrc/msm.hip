@@ -89,9 +89,9 @@ __device__ __forceinline__ G1Affine ld_aff(const G1Affine* p) {
 // partial sums a second pass combines per bucket (msm_big_combine_kernel): the depth
 // stays logarithmic however the scalars concentrate (fixed-base top windows: n / 2^12
 // entries per bucket at c = 22; a column of equal values: n entries per bucket).
-__device__ __forceinline__ const G1xyzz& msm_piece(const G1xyzz* bnd, uint32_t t, uint32_t t0, uint32_t bs,
-                                                   uint32_t L) {
-  return bnd[2 * (size_t)t + ((t == t0 && bs != t0 * L) ? 1 : 0)];
+// (H2G_ACC29: the slots hold raw F29 accumulators, converted here -- each piece is read once)
+__device__ __forceinline__ G1xyzz msm_piece(const AccPoint* bnd, uint32_t t, uint32_t t0, uint32_t bs, uint32_t L) {
+  return acc_to_xyzz(ld_accp(bnd + 2 * (size_t)t + ((t == t0 && bs != t0 * L) ? 1 : 0)));
 }
 
 static constexpr uint32_t MSM_GROUP = 16;            // lanes per item
@@ -120,8 +120,8 @@ static constexpr uint32_t MSM_SMALL_Q4 = 32;
 
 template <int Q>
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t nbt, uint32_t L,
-                 G1xyzz* __restrict__ buckets,
+msm_fixup_kernel(const AccPoint* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t nbt, uint32_t L,
+                 const AccPoint* __restrict__ whole, G1xyzz* __restrict__ buckets,
                  MsmBigItem* __restrict__ items, uint4* __restrict__ multi, uint32_t* __restrict__ counters) {
   H2G_SETPRIO(H2G_PRIO_RED);
   const uint32_t b = (blockIdx.x * blockDim.x + threadIdx.x) / Q;
@@ -156,6 +156,10 @@ msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ ko
   ibase = __shfl(ibase, 0, 64);
   mbase = __shfl(mbase, 0, 64);
   if (b < nbt && be <= bs && lead) buckets[b] = G1xyzz::identity();  // empty (no fill of buckets[])
+#if H2G_ACC29
+  // a bucket the accumulation wrote whole: its raw accumulator, converted
+  if (b < nbt && be > bs && np == 0 && lead) buckets[b] = acc_to_xyzz(ld_accp(whole + b));
+#endif
   if (np == 0) return;
   if (np > small) {
     if (!cnt) return;  // the quad's other lanes
@@ -182,7 +186,7 @@ msm_fixup_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ ko
 // MSM_GROUP lanes per item (4 items per wave, persistent grid): each lane sums up to
 // 4 strided pieces, then a log2(MSM_GROUP)-level tree in the wave's LDS slice.
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_big_item_kernel(const G1xyzz* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t L,
+msm_big_item_kernel(const AccPoint* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t L,
                     const MsmBigItem* __restrict__ items, const uint32_t* __restrict__ counters,
                     G1xyzz* __restrict__ partial, G1xyzz* __restrict__ buckets) {
   H2G_SETPRIO(H2G_PRIO_RED);
@@ -801,10 +805,13 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   while ((1ull << key_bits) < (uint64_t)nbt) key_bits++;
   int fb = key_bits < 10 ? key_bits : 10;
   while (fb < FB_MAX && (((uint64_t)nbt + (1ull << fb) - 1) >> fb) > COARSE_MAX) fb++;
-  const Need need[10] = {{&ws->ent, total * 8},
+  // ent (the coarse-binned entries) is dead once the partition has run: with H2G_ACC29 it
+  // holds the accumulation's whole buckets (raw F29) until the fixup converts them
+  const size_t whole_bytes = H2G_ACC29 ? (size_t)nbt * sizeof(AccPoint) : 0;
+  const Need need[10] = {{&ws->ent, std::max(total * 8, whole_bytes)},
                          {&ws->vals_out, total * 4},
-                         {&ws->item_bucket, icap * sizeof(MsmBigItem)},  // big-bucket items
-                         {&ws->partials, 2 * nchunks * sizeof(G1xyzz)},  // boundary slots
+                         {&ws->item_bucket, icap * sizeof(MsmBigItem)},    // big-bucket items
+                         {&ws->partials, 2 * nchunks * sizeof(AccPoint)},  // boundary slots
                          {&ws->buckets, (size_t)nbt * sizeof(G1xyzz)},
                          {&ws->segs, std::max<size_t>((size_t)2 * m1 + nblk, 10 * (size_t)nblk_p + 32) * WB *
                                          sizeof(G1xyzz)},
@@ -825,7 +832,8 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   uint4* multi = (uint4*)ws->item_off;
   G1xyzz* ipart = (G1xyzz*)ws->total_items;
   G1xyzz* buckets = (G1xyzz*)ws->buckets;
-  G1xyzz* bnd = (G1xyzz*)ws->partials;
+  AccPoint* bnd = (AccPoint*)ws->partials;
+  AccPoint* whole = H2G_ACC29 ? (AccPoint*)ws->ent : (AccPoint*)buckets;  // the accumulation's whole buckets
   G1xyzz* rS = (G1xyzz*)ws->segs;  // rscale scheme: group sums, group weights, block sums
   G1xyzz* rR = rS + (size_t)WB * m1;
   G1xyzz* rP = rR + (size_t)WB * m1;
@@ -892,15 +900,16 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   }
   H2G_PHASE(2);
   H2G_PHASE(3);
-  H2G_TRY(msm_accumulate(d_bases, vals_out, koff, nbt, d_total, L, nchunks, buckets, bnd, st));
+  H2G_TRY(msm_accumulate(d_bases, vals_out, koff, nbt, d_total, L, nchunks, whole, bnd, st));
   H2G_PHASE(4);
   if (nbt <= FIXUP_Q4_MAX)
     hipLaunchKernelGGL(msm_fixup_kernel<4>, dim3((unsigned)(((size_t)nbt * 4 + T - 1) / T)), dim3(T), 0, st,
-                       (const G1xyzz*)bnd, (const uint32_t*)koff, nbt, L, buckets, items, multi, counters);
+                       (const AccPoint*)bnd, (const uint32_t*)koff, nbt, L, (const AccPoint*)whole, buckets, items,
+                       multi, counters);
   else
-    hipLaunchKernelGGL(msm_fixup_kernel<1>, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const G1xyzz*)bnd,
-                       (const uint32_t*)koff, nbt, L, buckets, items, multi, counters);
-  hipLaunchKernelGGL(msm_big_item_kernel, dim3(MSM_BIG_BLOCKS), dim3(T), 0, st, (const G1xyzz*)bnd,
+    hipLaunchKernelGGL(msm_fixup_kernel<1>, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const AccPoint*)bnd,
+                       (const uint32_t*)koff, nbt, L, (const AccPoint*)whole, buckets, items, multi, counters);
+  hipLaunchKernelGGL(msm_big_item_kernel, dim3(MSM_BIG_BLOCKS), dim3(T), 0, st, (const AccPoint*)bnd,
                      (const uint32_t*)koff, L, (const MsmBigItem*)items, (const uint32_t*)counters, ipart, buckets);
   hipLaunchKernelGGL(msm_big_combine_kernel, dim3(MSM_BIG_BLOCKS / 4), dim3(T), 0, st, (const uint4*)multi,
                      (const uint32_t*)counters, (const G1xyzz*)ipart, buckets);

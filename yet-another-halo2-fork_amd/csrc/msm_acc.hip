@@ -26,11 +26,33 @@ __device__ __forceinline__ G1Affine ld_aff(const G1Affine* p) {
 // is the whole bucket iff the bucket starts and ends inside the chunk: such buckets are
 // written directly, a run that crosses a chunk boundary goes to the chunk's boundary
 // slot (slot 0 = its first run, slot 1 = its last run) for the fixup.
-__device__ __forceinline__ void msm_emit(uint32_t key, const G1xyzz& acc, bool first, bool from_prev, bool to_next,
-                                         uint32_t t, G1xyzz* __restrict__ buckets, G1xyzz* __restrict__ bnd) {
-  const G1xyzz v = xyzz_canon2(acc);  // lazy [0, 2M) -> fully reduced for the later kernels
-  if (!from_prev && !to_next) buckets[key] = v;
-  else bnd[2 * (size_t)t + (first ? 0 : 1)] = v;
+// H2G_ACC29: the accumulator is F29 (f29.h) and is stored raw -- a run end is a handful of
+// stores, not a conversion: some lane of a wave ends a run on most steps, so anything
+// costlier there would be paid by the whole wave nearly every step.
+__device__ __forceinline__ void msm_emit(uint32_t key, const AccPoint& acc, bool first, bool from_prev, bool to_next,
+                                         uint32_t t, AccPoint* __restrict__ buckets, AccPoint* __restrict__ bnd) {
+  AccPoint* dst = (!from_prev && !to_next) ? buckets + key : bnd + 2 * (size_t)t + (first ? 0 : 1);
+#if H2G_ACC29
+  st_acc(dst, acc);
+#else
+  *dst = xyzz_canon2(acc);  // lazy [0, 2M) -> fully reduced for the later kernels
+#endif
+}
+
+__device__ __forceinline__ AccPoint acc_identity() {
+#if H2G_ACC29
+  return xyzz29_identity();
+#else
+  return G1xyzz::identity();
+#endif
+}
+__device__ __forceinline__ AccPoint acc_madd(const AccPoint& acc, const G1Affine& pt) {
+#if H2G_ACC29
+  if (pt.is_identity()) return acc;
+  return xyzz29_madd(acc, to29(pt.x), to29(pt.y));
+#else
+  return xyzz_madd_lazy(acc, pt);
+#endif
 }
 
 // the next entry's base point is loaded before the current mixed addition
@@ -38,7 +60,7 @@ __device__ __forceinline__ void msm_emit(uint32_t key, const G1xyzz& acc, bool f
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ vals,
                const uint32_t* __restrict__ koff, uint32_t nbt, const uint32_t* __restrict__ d_total, uint32_t L,
-               G1xyzz* __restrict__ buckets, G1xyzz* __restrict__ bnd) {
+               AccPoint* __restrict__ buckets, AccPoint* __restrict__ bnd) {
   const uint32_t total = *d_total;  // entries (nonzero digits) of the partition
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t lo = t * L;
@@ -55,7 +77,7 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ 
   const bool prev_same = koff[key] < lo;
   uint32_t kend = koff[key + 1];
   bool first = true;
-  G1xyzz acc = G1xyzz::identity();
+  AccPoint acc = acc_identity();
   uint32_t v = vals[lo];
   G1Affine pt = ld_aff(bases + (v & 0x7fffffffu));
   for (uint32_t p = lo; p < hi; p++) {
@@ -81,10 +103,10 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ 
       }
       key = a;
       kend = koff[key + 1];
-      acc = G1xyzz::identity();
+      acc = acc_identity();
     }
     if (v >> 31) pt = affine_neg(pt);
-    acc = xyzz_madd_lazy(acc, pt);
+    acc = acc_madd(acc, pt);
     v = v_next;
     pt = pt_next;
   }
@@ -92,7 +114,7 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ 
 }
 
 hipError_t msm_accumulate(const G1Affine* bases, const uint32_t* vals, const uint32_t* koff, uint32_t nbt,
-                          const uint32_t* d_total, uint32_t L, size_t nchunks, G1xyzz* buckets, G1xyzz* bnd,
+                          const uint32_t* d_total, uint32_t L, size_t nchunks, AccPoint* buckets, AccPoint* bnd,
                           hipStream_t st) {
   const int T = MSM_THREADS;
   const unsigned cgrid = (unsigned)((nchunks + T - 1) / T);

@@ -2,6 +2,7 @@
 // partition, msm_part.hip; the accumulation, msm_acc.hip), shared with msm.hip.
 #pragma once
 #include "msm.h"
+#include "f29.h"
 
 namespace h2g {
 
@@ -61,10 +62,56 @@ struct MsmPartArgs {
 };
 hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* prof);
 
+// The accumulation's arithmetic: 1 = F29 (f29.h: 9 x 29-bit limbs, no carry ops in the
+// products); its buckets and boundary slots are then raw G1xyzz29 accumulators (144 B),
+// converted to canonical G1xyzz by the fixup.  0 = the 8 x 32-bit FIPS arithmetic of
+// bn254.h writing G1xyzz directly (A/B builds: tools/build_variant.py TAG --src
+// msm_acc.hip,msm.hip -DH2G_ACC29=0).
+#ifndef H2G_ACC29
+#define H2G_ACC29 1
+#endif
+#if H2G_ACC29
+using AccPoint = G1xyzz29;
+#else
+using AccPoint = G1xyzz;
+#endif
+
+// raw 16-B moves of the accumulators (G1xyzz29 is 9 x 16 B)
+__device__ __forceinline__ void st_acc(G1xyzz29* dst, const G1xyzz29& v) {
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(&v);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+  for (int i = 0; i < 9; i++) d[i] = make_uint4(s[4 * i], s[4 * i + 1], s[4 * i + 2], s[4 * i + 3]);
+}
+__device__ __forceinline__ G1xyzz29 ld_acc(const G1xyzz29* src) {
+  G1xyzz29 v;
+  uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint4 q = s[i];
+    d[4 * i] = q.x;
+    d[4 * i + 1] = q.y;
+    d[4 * i + 2] = q.z;
+    d[4 * i + 3] = q.w;
+  }
+  return v;
+}
+__device__ __forceinline__ G1xyzz acc_to_xyzz(const G1xyzz29& v) { return xyzz_from29(v); }
+__device__ __forceinline__ G1xyzz acc_to_xyzz(const G1xyzz& v) { return v; }
+__device__ __forceinline__ AccPoint ld_accp(const AccPoint* p) {
+#if H2G_ACC29
+  return ld_acc(p);
+#else
+  return *p;
+#endif
+}
+
 // step 3 of the pipeline (msm_acc.hip): XYZZ accumulation of the bucket-sorted values in
-// chunks of L, one thread per chunk; bucket k's run is [koff[k], koff[k + 1])
+// chunks of L, one thread per chunk; bucket k's run is [koff[k], koff[k + 1]).  Whole buckets
+// go to buckets[k], runs crossing a chunk boundary to the chunk's slots bnd[2 t + 0/1]
 hipError_t msm_accumulate(const G1Affine* bases, const uint32_t* vals, const uint32_t* koff, uint32_t nbt,
-                          const uint32_t* d_total, uint32_t L, size_t nchunks, G1xyzz* buckets, G1xyzz* bnd,
+                          const uint32_t* d_total, uint32_t L, size_t nchunks, AccPoint* buckets, AccPoint* bnd,
                           hipStream_t st);
 
 }  // namespace h2g

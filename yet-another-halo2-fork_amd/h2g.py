@@ -80,6 +80,7 @@ _SIGS = {
     "h2g_profile_enable": ([I32], I32),
     "h2g_profile_msm_collect": ([ctypes.POINTER(ctypes.c_float), I32, ctypes.POINTER(I32), ctypes.POINTER(I32)], I32),
     "h2g_profile_msm_entries": ([ctypes.POINTER(U64), ctypes.POINTER(I32)], I32),
+    "h2g_profile_box_calibrate": ([ctypes.POINTER(ctypes.c_double), I32], I32),
     "h2g_params_create": ([U32, U64P, U64P, ctypes.POINTER(U64)], I32),
     "h2g_params_setup": ([U32, U64P, ctypes.POINTER(U64)], I32),
     "h2g_params_export": ([U64, U64P, U64P], I32),
@@ -429,6 +430,15 @@ def profile_msm_collect(with_union=False):
         return calls.value, phases
     return calls.value, phases, {"accumulate": ms[npz.value], "msm": ms[npz.value + 1],
                                  "entries": ent.value if unc.value == 0 else None}
+
+
+def box_calibrate():
+    """this GPU's Montgomery product throughput now (FIPS and F29 limb forms, G/s), the
+    shader clock during the run (GHz) and the ms spent (h2g_profile_box_calibrate)"""
+    out = (ctypes.c_double * 4)()
+    check(lib().h2g_profile_box_calibrate(out, 4))
+    return {"modmul_fips_gps": round(out[0], 2), "modmul_f29_gps": round(out[1], 2),
+            "sclk_ghz_in_kernel": round(out[2], 3), "calibration_ms": round(out[3], 1)}
 
 
 class Timer:
