@@ -141,7 +141,7 @@ def box_block(h2g):
     Montgomery product rate now (tools/microbench kernels, csrc/calib.hip), its shader
     clock under that load, and rocm-smi's clocks / power / power cap"""
     b = h2g.box_calibrate()
-    b["reference_fips_gps"] = MODMUL_REF_GPS
+    b["reference_gps"] = MODMUL_REF_GPS
     b["smi"] = box_smi()
     return b
 
@@ -272,8 +272,8 @@ def pmc_child(args):
 # the quarter rate of v_mad_u64_u32 is not in the guide's tables)
 MODMUL_PEAK_MICROBENCH = 125e9
 MODMUL_PEAK_ISSUE = 256 * 4 * 32 * 2.4e9 / (128 * 4 + 64)
-# the FIPS product rate of the round-4 reference boxes: value_normalised = value x
-# (this box's FIPS rate / this), i.e. the proof time scaled to a box of that speed
+# tools/microbench/modmul_bench.hip's FIPS product rate on the round-4 boxes: value_normalised
+# = value x (this box's rate of that same kernel / this), the proof time scaled to such a box
 MODMUL_REF_GPS = 125.0
 
 
@@ -673,7 +673,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             "roofline": roofline_from_phases(calls, phases, n_local, traffic, traffic_note, union=union),
             "box": box,
             "value_normalised": round(elapsed / (args.steps * (1 if one_proof else world)) *
-                                      box["modmul_fips_gps"] / MODMUL_REF_GPS, 4),
+                                      box["modmul_ref_gps"] / MODMUL_REF_GPS, 4),
             "msm_in_prover": {"launches_per_proof": calls // max(args.steps, 1), "avg_ms": round(msm_ms, 4),
                               "busy_ms_per_proof": round(union["msm"] / args.steps, 3),
                               "accumulate_busy_ms_per_proof": round(union["accumulate"] / args.steps, 3),

@@ -77,8 +77,33 @@ def run(name, st):
           f"largest intermediate 2^{LG(worst):.3f}")
 
 
+MR = 0x30644e72e131a029b85045b68181585d2833e84879b9709143e1f593f0000001  # BN254 Fr
+
+
+def ntt_pass(stages, b0):
+    """one NTT pass in F29 (csrc/ntt.hip ntt_pass29_kernel / ntt_last29_kernel): inputs <
+    b0; stage s: sums a + b, differences a - b + K_s M with K_s = 2^(s+2) into a product
+    with a twiddle < M, or kept (normalised) for the j = 0 butterflies; closing product
+    with a constant < M.  Returns the bound of the pass's outputs."""
+    B = b0
+    for s in range(stages):
+        k = 4 << s
+        assert top(k * MR) - 1 >= top(B), ("NTT K_s too small", s, LG(B), LG(k * MR))
+        B = max(2 * B, B + k * MR)        # sums; kept differences
+        # a product's operand: limbs 0..7 < 2^29 + 2^30, the twiddle normalised
+        column_ok(1 << 29, (1 << 29) + (1 << 30))
+    assert top(B) < 1 << 31, LG(B)         # top limb of a normalised value fits its 32 bits
+    return B * MR // R + MR + 1
+
+
 if __name__ == "__main__":
     run("fresh point", (32 * M, 32 * M, M, M))
     d = mul(32 * M, M)
     run("doubling path", (d, d, d, d))
+    b0 = 3 * MR  # stored values of the NTT passes
+    for st in (3, 4, 5, 6):
+        out = ntt_pass(st, b0)
+        assert out < b0 and out < 1 << 256, (st, out / MR)
+        print(f"ntt pass of {st} stages: inputs < 3 M, outputs < {out / MR:.3f} M (packable, below the input bound)")
+    print(f"last pass: outputs < {ntt_pass(6, b0) / MR:.3f} M before two conditional subtractions of M")
     print("ok")

@@ -18,6 +18,65 @@ namespace h2g {
 
 static constexpr int CAL_THREADS = 256;
 
+// the round-4 reference measurement (tools/microbench/modmul_bench.hip, variant 1): the FIPS
+// product with one volatile inline-asm block per mac, one dependent chain per thread --
+// 125 G/s on the round-4 boxes, the reference of the bench line's value_normalised
+__device__ __forceinline__ void ref_mac(uint64_t& lo, uint32_t& hi, uint32_t a, uint32_t b) {
+  asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+               : "+v"(lo), "+v"(hi)
+               : "v"(a), "v"(b)
+               : "vcc");
+}
+__device__ __forceinline__ Fq ref_fips_mul(const Fq& A, const Fq& B) {
+  const uint32_t* a = A.l;
+  const uint32_t* b = B.l;
+  uint32_t m[8], r[8];
+  uint64_t lo = 0;
+  uint32_t hi = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#pragma unroll
+    for (int i = 0; i < k; i++) {
+      ref_mac(lo, hi, a[i], b[k - i]);
+      ref_mac(lo, hi, m[i], FqParams::M[k - i]);
+    }
+    ref_mac(lo, hi, a[k], b[0]);
+    m[k] = (uint32_t)lo * FqParams::INV;
+    ref_mac(lo, hi, m[k], FqParams::M[0]);
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+#pragma unroll
+  for (int k = 8; k < 15; k++) {
+#pragma unroll
+    for (int i = k - 7; i < 8; i++) {
+      ref_mac(lo, hi, a[i], b[k - i]);
+      ref_mac(lo, hi, m[i], FqParams::M[k - i]);
+    }
+    r[k - 8] = (uint32_t)lo;
+    lo = (lo >> 32) | ((uint64_t)hi << 32);
+    hi = 0;
+  }
+  r[7] = (uint32_t)lo;
+  Fq R, D;  // the reference's final subtraction (64-bit signed borrow), kept as it was measured
+#pragma unroll
+  for (int i = 0; i < 8; i++) R.l[i] = r[i];
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int64_t u = (int64_t)R.l[i] - FqParams::M[i] + br;
+    D.l[i] = (uint32_t)u;
+    br = u >> 32;
+  }
+  return br ? R : D;
+}
+__global__ void __launch_bounds__(CAL_THREADS) calib_ref_kernel(Fq* x, int iters) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  Fq a = x[i], b = x[i + 1];
+  for (int it = 0; it < iters; it++) a = ref_fips_mul(a, b);
+  x[i] = a;
+}
+
 template <int V>
 __global__ void __launch_bounds__(CAL_THREADS) calib_kernel(Fq* x, int iters, unsigned long long* clk) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -61,8 +120,11 @@ __global__ void calib_fill(Fq* x, size_t n) {
 
 using namespace h2g;
 
-// out[0] FIPS G modmul/s, out[1] F29 G modmul/s, out[2] shader GHz during the F29 run,
-// out[3] wall ms of the whole calibration; returns 0 or a HIP error code
+// out[0] G modmul/s of the round-4 reference kernel (FIPS, one chain per thread, 2048 x
+// 256 threads x 2000 products as tools/microbench/modmul_bench.hip), out[1] F29 G modmul/s
+// (two chains per thread), out[2] shader GHz during the F29 run, out[3] wall ms of the
+// whole calibration, out[4] (max >= 5) the FIPS product with two chains per thread;
+// returns 0 or a HIP error code
 extern "C" int h2g_profile_box_calibrate(double* out, int max) {
   if (!out || max < 4) return 1;
   int dev = 0;
@@ -79,7 +141,7 @@ extern "C" int h2g_profile_box_calibrate(double* out, int max) {
   if (e == hipSuccess) e = hipEventCreate(&e0);
   if (e == hipSuccess) e = hipEventCreate(&e1);
   if (e == hipSuccess) e = hipEventCreate(&w0);
-  double rate[2] = {0, 0}, ghz = 0;
+  double rate[2] = {0, 0}, ghz = 0, ref = 0;
   if (e == hipSuccess) {
     (void)hipEventRecord(w0, nullptr);
     hipLaunchKernelGGL(calib_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr, x, n);
@@ -96,6 +158,20 @@ extern "C" int h2g_profile_box_calibrate(double* out, int max) {
         if (e == hipSuccess && ms < best) best = ms;
       }
       rate[v] = (double)blocks * CAL_THREADS * iters * 2 / (best * 1e-3) / 1e9;
+    }
+    {  // the reference kernel: 2048 blocks of 256 threads, 2000 products each
+      const int rb = 256 * 8, riters = 2000;
+      float best = 1e30f;
+      for (int rep = 0; rep < 2 && e == hipSuccess && (size_t)rb * CAL_THREADS + 1 <= n; rep++) {
+        (void)hipEventRecord(e0, nullptr);
+        hipLaunchKernelGGL(calib_ref_kernel, dim3(rb), dim3(CAL_THREADS), 0, nullptr, x, riters);
+        (void)hipEventRecord(e1, nullptr);
+        e = hipEventSynchronize(e1);
+        float ms = 0;
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+        if (e == hipSuccess && ms < best) best = ms;
+      }
+      ref = (double)rb * CAL_THREADS * riters / (best * 1e-3) / 1e9;
     }
     if (e == hipSuccess) {
       std::vector<unsigned long long> h((size_t)blocks * 2);
@@ -117,9 +193,10 @@ extern "C" int h2g_profile_box_calibrate(double* out, int max) {
   if (e1) (void)hipEventDestroy(e1);
   if (w0) (void)hipEventDestroy(w0);
   if (e != hipSuccess) return (int)e;
-  out[0] = rate[0];
+  out[0] = ref;
   out[1] = rate[1];
   out[2] = ghz;
   out[3] = wall;
+  if (max >= 5) out[4] = rate[0];
   return 0;
 }

@@ -354,4 +354,73 @@ H2G_HD G1xyzz29 xyzz29_madd(const G1xyzz29& p, const F29& qx, const F29& qy) {
   return r;
 }
 
+
+// ---- linear maps on storage-form data (the NTT): for a map that is linear over Fr, the
+// storage integers x (x = e 2^256 mod M) can be taken as F29 values directly -- read as F29
+// they stand for e 2^-5 -- and every constant (twiddle, coset power, scale) as a proper F29
+// element (c 2^261 mod M).  Each product then carries the 2^-5 along, the outputs read as
+// F29 stand for f 2^-5, i.e. they ARE the storage integers of the results f.  So data moves
+// in and out by repacking 8 x 32 <-> 9 x 29 bits, with no conversion products.
+template <class P>
+H2G_HD F29 raw29(const Fe<P>& x) {  // the same integer in 29-bit limbs (x < 2^256)
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int b = 29 * i, w = b >> 5, s = b & 31;
+    const uint64_t lo = x.l[w];
+    const uint64_t hi = w + 1 < 8 ? x.l[w + 1] : 0;
+    r.l[i] = (uint32_t)(((hi << 32) | lo) >> s) & F29_MASK;
+  }
+  return r;
+}
+template <class P>
+H2G_HD Fe<P> pack29(const F29& v) {  // normalised v < 2^256 into 8 x 32-bit limbs
+  Fe<P> r;
+  uint64_t acc = 0;
+  int have = 0, w = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    acc |= (uint64_t)v.l[i] << have;
+    have += 29;
+    if (have >= 32 && w < 8) {
+      r.l[w++] = (uint32_t)acc;
+      acc >>= 32;
+      have -= 32;
+    }
+  }
+  if (w < 8) r.l[w] = (uint32_t)acc;
+  return r;
+}
+// v - M if v >= M, for a normalised v (limbs 0..7 < 2^29): signed borrow chain, one select
+template <class P>
+H2G_HD F29 sub_m_if_ge29(const F29& v) {
+  F29 d;
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int32_t t = (int32_t)v.l[i] - (int32_t)C29<P>::M[i] + br;
+    if (i < 8) {
+      d.l[i] = (uint32_t)t & F29_MASK;
+      br = t >> 29;
+    } else {
+      d.l[i] = (uint32_t)t;
+      br = t >> 31;
+    }
+  }
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = br ? v.l[i] : d.l[i];
+  return r;
+}
+// the F29 element of a storage-form constant, reduced to [0, M) and packed in 8 x 32 bits
+// (twiddle tables: loaded with raw29, no product)
+template <class P>
+H2G_HD Fe<P> storage_to_f29_packed(const Fe<P>& s) {
+  return pack29<P>(sub_m_if_ge29<P>(mul29<P>(to29(s), one29v<P>())));  // REDC(32 s one) < 1.2 M
+}
+template <class P>
+H2G_HD F29 storage_to_f29(const Fe<P>& s) {
+  return sub_m_if_ge29<P>(mul29<P>(to29(s), one29v<P>()));
+}
+
 }  // namespace h2g

@@ -28,6 +28,9 @@ struct NttTables {
   // w^((N/L_p) i_low k) at [k * S_p + i_low] (L_p entries; sum over passes ~ 1.1 N)
   Fr* pass_tw = nullptr;
   uint64_t pass_off[NTT_MAX_PASSES] = {0, 0, 0, 0, 0, 0};
+  // the F29 passes' in-pass twiddles w_64^j, j < 32, as F29 elements packed in 8 x 32 bits
+  // (a 2^m-point pass reads every 2^(6-m)-th); L >= 6
+  Fr* root64 = nullptr;
 };
 
 // One transform y = DFT_w(x) of size N = 2^tab.L with fused maps:

@@ -19,7 +19,10 @@
 // the low m-3 bits.  Global accesses are runs of >= 8 x 32 B across the lanes
 // of one instruction.  Inter-pass twiddles come from a 2-level table
 // w^E = lo[E mod 2^b] * hi[E >> b] (both L2-resident).
+#include <type_traits>
+
 #include "ntt.h"
+#include "f29.h"
 
 namespace h2g {
 
@@ -295,6 +298,218 @@ ntt_last_kernel(const Fr* data, NttIo io, uint64_t out_len, NttTables tab, int L
 }
 
 // ---------------------------------------------------------------------------
+// The passes in 9 x 29-bit limbs (f29.h), H2G_NTT29.  The transform is linear, so the
+// stored integers move in and out by repacking only (f29.h: raw29 / pack29) and the
+// constants -- twiddles, coset powers, scales -- are F29 elements (the pass tables are
+// built in that form, storage_to_f29_packed).  Products are f29.h's carry-free REDC.
+// Value bounds (tools/f29_bounds.py, "ntt"): stored values < 3 M; stage s of a pass
+// subtracts with K_s = 2^(s+2) M (>= the stage's input bound with a top-limb margin), so
+// after 6 stages every value is < 254 M < 2^262 and the closing product (pass twiddle or
+// epilogue constant, < M) brings it back below 2.6 M; the last pass reduces to [0, M).
+#ifndef H2G_NTT29  // A/B builds: 0 = the 8 x 32-bit FIPS passes above
+#define H2G_NTT29 1
+#endif
+
+__device__ __forceinline__ F29 ld29(const Fr* p) { return raw29(ld_fr(p)); }
+__device__ __forceinline__ void st29(Fr* p, const F29& v) { st_fr(p, pack29<FrParams>(v)); }
+__device__ __forceinline__ F29 shfl_xor29(const F29& v, int mask) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = (uint32_t)__shfl_xor((int)v.l[i], mask);
+  return r;
+}
+__device__ __forceinline__ F29 sel29(int c, const F29& a, const F29& b) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = c ? a.l[i] : b.l[i];
+  return r;
+}
+// compile-time loop: f(std::integral_constant<int, I>) for I in [I0, N) -- for loops over
+// whole products, which `#pragma unroll` may leave rolled (x[] is then indexed at run time
+// and moves to scratch)
+template <int I, int N, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    sfor<I + 1, N>(f);
+  }
+}
+
+// a - b + K_s M for stage s: K_s = 2^(s+2)
+template <int S>
+__device__ __forceinline__ F29 nsub29(const F29& a, const F29& b) {
+  return sub29<FrParams, (4u << S), 29>(a, b);
+}
+
+// The same butterfly schedule as WaveDif<M>::run (lane / register layout, rpos), its
+// stages as templates: unrolled loops over whole products were left rolled by the
+// compiler, and a rolled stage loop indexes x[] at run time (x[] then lives in scratch).
+template <int M>
+struct WaveDif29 {
+  static constexpr int LPC = 1 << (M - 3);
+  static constexpr int CPW = 64 / LPC;
+  template <int T>  // round A, row bit M-3+T (stage 2 - T)
+  __device__ static __forceinline__ void stage_a(F29 x[8], const F29* w, int rg) {
+    constexpr int htlog = (M - 3) + T;
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+      const int q = ((p >> T) << (T + 1)) | (p & ((1 << T) - 1));
+      const int j = rg + (p & ((1 << T) - 1)) * LPC;
+      const F29 a = x[q], b = x[q + (1 << T)];
+      x[q] = norm29(add29(a, b));
+      x[q + (1 << T)] = mul29<FrParams>(nsub29<2 - T>(a, b), w[j << (M - 1 - htlog)]);
+    }
+    if constexpr (T > 0) stage_a<T - 1>(x, w, rg);
+  }
+  template <int B>  // register bit B <-> lane bit
+  __device__ static __forceinline__ void swap_bits(F29 x[8], int rg) {
+    if constexpr (B < M - 3) {
+      const int lb = (rg >> B) & 1;
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        const int q = ((p >> B) << (B + 1)) | (p & ((1 << B) - 1));
+        const F29 lo_v = x[q], hi_v = x[q | (1 << B)];
+        const F29 recv = shfl_xor29(sel29(lb, lo_v, hi_v), CPW << B);
+        x[q] = sel29(lb, recv, lo_v);
+        x[q | (1 << B)] = sel29(lb, hi_v, recv);
+      }
+      swap_bits<B + 1>(x, rg);
+    }
+  }
+  template <int T>  // round B, row bit T (stage 3 + M - 4 - T)
+  __device__ static __forceinline__ void stage_b(F29 x[8], const F29* w) {
+    if constexpr (T >= 0) {
+      constexpr int S = 3 + (M - 4 - T);
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        const int q = ((p >> T) << (T + 1)) | (p & ((1 << T) - 1));
+        const int j = q & ((1 << T) - 1);
+        const F29 a = x[q], b = x[q + (1 << T)];
+        x[q] = norm29(add29(a, b));
+        x[q + (1 << T)] = j == 0 ? norm29(nsub29<S>(a, b)) : mul29<FrParams>(nsub29<S>(a, b), w[j << (M - 1 - T)]);
+      }
+      stage_b<T - 1>(x, w);
+    }
+  }
+  __device__ static __forceinline__ void run(F29 x[8], const F29* w, int rg) {
+    stage_a<2>(x, w, rg);
+    swap_bits<0>(x, rg);
+    stage_b<M - 4>(x, w);
+  }
+};
+
+// the constants of one launch in F29 form (host-converted)
+struct NttConst29 {
+  F29 z1, z2;      // input coset powers (pass 0)
+  F29 mul[3];      // epilogue multiplier per y mod 3 (last pass), one29 when none
+};
+
+template <int M>
+__global__ void __launch_bounds__(NTT_THREADS, NttPassWaves<M>::value)
+ntt_pass29_kernel(Fr* data, NttIo io, int first, uint64_t n_in, NttTables tab, const Fr* __restrict__ ptw, int L,
+                  int lrem, int distribute, NttConst29 k29) {
+  using D = WaveDif29<M>;
+  data += (uint64_t)blockIdx.y << L;
+  const Fr* in = first ? io.src[blockIdx.y] : nullptr;
+  __shared__ F29 w[1 << (M - 1)];
+  for (int j = threadIdx.x; j < (1 << (M - 1)); j += blockDim.x) w[j] = ld29(tab.root64 + (j << (6 - M)));
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * NTT_WAVES + (threadIdx.x >> 6);
+  if (wave >= (1ull << L) / ((1ull << M) * D::CPW)) return;
+  const uint64_t S = 1ull << (lrem - M);
+  const uint64_t groups = S / D::CPW;
+  const uint64_t q = wave / groups;
+  const uint64_t g = wave % groups;
+  const uint64_t base = (q << lrem) + g * D::CPW;
+  const int c = lane % D::CPW, rg = lane / D::CPW;
+  F29 x[8];
+  sfor<0, 8>([&](auto qc) {
+    constexpr int qq = decltype(qc)::value;
+    const uint64_t pos = base + c + (uint64_t)(rg + D::LPC * qq) * S;
+    if (in) {
+      F29 v;
+#pragma unroll
+      for (int i = 0; i < 9; i++) v.l[i] = 0;
+      if (pos < n_in) {
+        v = ld29(in + pos);
+        if (distribute) {
+          const uint32_t md = mod3(pos);
+          if (md) v = mul29<FrParams>(v, sel29(md == 1, k29.z1, k29.z2));
+        }
+      }
+      x[qq] = v;
+    } else {
+      x[qq] = ld29(data + pos);
+    }
+  });
+  D::run(x, w, rg);
+  const uint64_t ilow = g * D::CPW + c;
+  sfor<0, 8>([&](auto qc) {
+    constexpr int qq = decltype(qc)::value;
+    const uint32_t k = brev_bits(WaveDif<M>::rpos(qq, rg), M);
+    st29(data + base + c + (uint64_t)k * S, mul29<FrParams>(x[qq], ld29(ptw + (uint64_t)k * S + ilow)));
+  });
+}
+
+__global__ void __launch_bounds__(NTT_THREADS, NTT_MIN_WAVES)
+ntt_last29_kernel(const Fr* data, NttIo io, uint64_t out_len, NttTables tab, int L, NttPlanLg plan,
+                  NttConst29 k29) {
+  constexpr int M = 6;
+  data += (uint64_t)blockIdx.y << L;
+  Fr* out = io.dst[blockIdx.y];
+  using D = WaveDif29<M>;
+  __shared__ F29 w[1 << (M - 1)];
+  for (int j = threadIdx.x; j < (1 << (M - 1)); j += blockDim.x) w[j] = ld29(tab.root64 + (j << (6 - M)));
+  __syncthreads();
+  const int* lgs = plan.lg;
+  const int P = plan.p;
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (uint64_t)blockIdx.x * NTT_WAVES + (threadIdx.x >> 6);
+  if (wave >= (1ull << L) / ((1ull << M) * D::CPW)) return;
+  const int l0 = lgs[0];
+  const uint64_t groups = (1ull << l0) / D::CPW;
+  const uint64_t midx = wave / groups;
+  const uint64_t g = wave % groups;
+  uint64_t mid_nat = 0;
+  {
+    uint64_t rem = midx;
+    int wbits_tail = L - M;
+#pragma unroll
+    for (int p = NTT_MAX_PASSES - 2; p >= 1; p--) {
+      if (p > P - 2) continue;
+      const int lgp = lgs[p];
+      const uint64_t dig = rem & ((1ull << lgp) - 1);
+      rem >>= lgp;
+      wbits_tail -= lgp;
+      mid_nat |= dig << wbits_tail;
+    }
+  }
+  const int c = lane % D::CPW, rg = lane / D::CPW;
+  const uint64_t k0 = g * D::CPW + c;
+  const uint64_t colbase = k0 * (1ull << (L - l0)) + (midx << M);
+  F29 x[8];
+  sfor<0, 8>([&](auto qc) {
+    constexpr int qq = decltype(qc)::value;
+    x[qq] = ld29(data + colbase + rg + D::LPC * qq);
+  });
+  D::run(x, w, rg);
+  const uint64_t kstride = 1ull << (L - M);
+  sfor<0, 8>([&](auto qc) {
+    constexpr int qq = decltype(qc)::value;
+    const uint32_t k = brev_bits(WaveDif<M>::rpos(qq, rg), M);
+    const uint64_t y = k0 + mid_nat + (uint64_t)k * kstride;
+    if (y < out_len) {
+      const uint32_t md = mod3(y);
+      // the epilogue constant (scale and / or zeta power, or one) also brings the value
+      // below 2.6 M; two conditional subtractions reach [0, M)
+      const F29 v = mul29<FrParams>(x[qq], sel29(md == 1, k29.mul[1], sel29(md == 2, k29.mul[2], k29.mul[0])));
+      st29(out + y, sub_m_if_ge29<FrParams>(sub_m_if_ge29<FrParams>(v)));
+    }
+  });
+}
+
+// ---------------------------------------------------------------------------
 // Whole transform in one block (N <= 2^NTT_SMALL_MAX_LOG), radix-2 DIF in LDS.
 __global__ void __launch_bounds__(256)
 ntt_small_kernel(NttIo io, uint64_t n_in, uint64_t out_len, NttTables tab, int L,
@@ -357,13 +572,20 @@ __global__ void ntt_tables_kernel(Fr* lo, Fr* hi, Fr w, int b, int L) {
   }
 }
 
+// w_64^j = w^(j 2^(L - 6)), j < 32, as packed F29 elements (the F29 passes' LDS twiddles)
+__global__ void ntt_root64_kernel(Fr* out, NttTables tab, int L) {
+  const int j = threadIdx.x;
+  if (j < 32) out[j] = storage_to_f29_packed<FrParams>(twiddle(tab, (uint64_t)j << (L - 6)));
+}
+
 // pass table: t = k * S + i_low over [0, 2^lrem): w^(i_low k 2^(L - lrem))
 __global__ void ntt_pass_tw_kernel(Fr* out, NttTables tab, int L, int lrem, int M) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (t >= (1ull << lrem)) return;
   const uint64_t S = 1ull << (lrem - M);
   const uint64_t k = t / S, ilow = t % S;
-  out[t] = twiddle(tab, (ilow * k) << (L - lrem));
+  const Fr v = twiddle(tab, (ilow * k) << (L - lrem));
+  out[t] = H2G_NTT29 ? storage_to_f29_packed<FrParams>(v) : v;  // the passes' form
 }
 
 // ---------------------------------------------------------------------------
@@ -414,6 +636,9 @@ hipError_t ntt_build_tables(NttTables* t, const Fr& omega, int L, hipStream_t st
   }
   e = hipMalloc(&t->pass_tw, (total ? total : 1) * sizeof(Fr));
   if (e != hipSuccess) return e;
+  e = hipMalloc(&t->root64, 32 * sizeof(Fr));
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ntt_root64_kernel, dim3(1), dim3(32), 0, st, t->root64, *t, L);
   lrem = L;
   for (int p = 0; p < P - 1; p++) {
     const uint64_t cnt = 1ull << lrem;
@@ -428,7 +653,8 @@ void ntt_free_tables(NttTables* t) {
   if (t->lo) (void)hipFree(t->lo);
   if (t->hi) (void)hipFree(t->hi);
   if (t->pass_tw) (void)hipFree(t->pass_tw);
-  t->lo = t->hi = t->pass_tw = nullptr;
+  if (t->root64) (void)hipFree(t->root64);
+  t->lo = t->hi = t->pass_tw = t->root64 = nullptr;
 }
 
 hipError_t ntt_init_attributes() {
@@ -438,12 +664,16 @@ hipError_t ntt_init_attributes() {
 
 template <int M>
 static void launch_pass(const NttArgs& a, const NttIo& io, int B, int p, int first, uint64_t n_in, int L, int lrem,
-                        int dist, hipStream_t st) {
+                        int dist, const NttConst29& k29, hipStream_t st) {
   const uint64_t N = 1ull << L;
   const uint64_t waves = N / ((1ull << M) * WaveDif<M>::CPW);
   const unsigned blocks = (unsigned)((waves + NTT_WAVES - 1) / NTT_WAVES);
-  hipLaunchKernelGGL(ntt_pass_kernel<M>, dim3(blocks, (unsigned)B), dim3(NTT_THREADS), 0, st, a.work, io, first, n_in,
-                     a.tab, (const Fr*)(a.tab.pass_tw + a.tab.pass_off[p]), L, lrem, dist, a.in_z1, a.in_z2);
+  if (H2G_NTT29)
+    hipLaunchKernelGGL(ntt_pass29_kernel<M>, dim3(blocks, (unsigned)B), dim3(NTT_THREADS), 0, st, a.work, io, first,
+                       n_in, a.tab, (const Fr*)(a.tab.pass_tw + a.tab.pass_off[p]), L, lrem, dist, k29);
+  else
+    hipLaunchKernelGGL(ntt_pass_kernel<M>, dim3(blocks, (unsigned)B), dim3(NTT_THREADS), 0, st, a.work, io, first,
+                       n_in, a.tab, (const Fr*)(a.tab.pass_tw + a.tab.pass_off[p]), L, lrem, dist, a.in_z1, a.in_z2);
 }
 
 hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
@@ -478,6 +708,10 @@ hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
     if (a.out_distribute && r == 2) m = m * a.out_z2;
     mul[r] = m;
   }
+  NttConst29 k29;  // the F29 passes' constants
+  k29.z1 = storage_to_f29<FrParams>(a.in_z1);
+  k29.z2 = storage_to_f29<FrParams>(a.in_z2);
+  for (int r = 0; r < 3; r++) k29.mul[r] = storage_to_f29<FrParams>(mul[r]);
   // N / N_0 and every middle S are multiples of 64 >= CPW: waves divide evenly.
   // pass 0: src -> work (out of place), passes 1..P-2 in place on work,
   // last pass: work -> dst in natural order.
@@ -487,10 +721,10 @@ hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
     const uint64_t nin = first ? a.n_in : 0;
     const int dist = first ? a.in_distribute : 0;
     switch (lg[p]) {
-      case 3: launch_pass<3>(a, io, B, p, first, nin, L, lrem, dist, st); break;
-      case 4: launch_pass<4>(a, io, B, p, first, nin, L, lrem, dist, st); break;
-      case 5: launch_pass<5>(a, io, B, p, first, nin, L, lrem, dist, st); break;
-      case 6: launch_pass<6>(a, io, B, p, first, nin, L, lrem, dist, st); break;
+      case 3: launch_pass<3>(a, io, B, p, first, nin, L, lrem, dist, k29, st); break;
+      case 4: launch_pass<4>(a, io, B, p, first, nin, L, lrem, dist, k29, st); break;
+      case 5: launch_pass<5>(a, io, B, p, first, nin, L, lrem, dist, k29, st); break;
+      case 6: launch_pass<6>(a, io, B, p, first, nin, L, lrem, dist, k29, st); break;
       default: return hipErrorInvalidValue;
     }
     lrem -= lg[p];
@@ -498,8 +732,12 @@ hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
   {
     const uint64_t waves = N / (64ull * WaveDif<6>::CPW);
     const unsigned blocks = (unsigned)((waves + NTT_WAVES - 1) / NTT_WAVES);
-    hipLaunchKernelGGL(ntt_last_kernel, dim3(blocks, (unsigned)B), dim3(NTT_THREADS), 0, st, (const Fr*)a.work, io,
-                       out_len, a.tab, L, plan, has_mul, mul[0], mul[1], mul[2]);
+    if (H2G_NTT29)
+      hipLaunchKernelGGL(ntt_last29_kernel, dim3(blocks, (unsigned)B), dim3(NTT_THREADS), 0, st, (const Fr*)a.work,
+                         io, out_len, a.tab, L, plan, k29);
+    else
+      hipLaunchKernelGGL(ntt_last_kernel, dim3(blocks, (unsigned)B), dim3(NTT_THREADS), 0, st, (const Fr*)a.work,
+                         io, out_len, a.tab, L, plan, has_mul, mul[0], mul[1], mul[2]);
   }
   return hipGetLastError();
 }

@@ -433,12 +433,15 @@ def profile_msm_collect(with_union=False):
 
 
 def box_calibrate():
-    """this GPU's Montgomery product throughput now (FIPS and F29 limb forms, G/s), the
-    shader clock during the run (GHz) and the ms spent (h2g_profile_box_calibrate)"""
-    out = (ctypes.c_double * 4)()
-    check(lib().h2g_profile_box_calibrate(out, 4))
-    return {"modmul_fips_gps": round(out[0], 2), "modmul_f29_gps": round(out[1], 2),
-            "sclk_ghz_in_kernel": round(out[2], 3), "calibration_ms": round(out[3], 1)}
+    """this GPU's Montgomery product throughput now (G/s): the round-4 reference kernel
+    (tools/microbench/modmul_bench.hip's FIPS product, one chain per thread), the F29
+    product and the FIPS product (two chains per thread each); the shader clock during the
+    F29 run (GHz) and the ms spent (h2g_profile_box_calibrate)"""
+    out = (ctypes.c_double * 5)()
+    check(lib().h2g_profile_box_calibrate(out, 5))
+    return {"modmul_ref_gps": round(out[0], 2), "modmul_f29_gps": round(out[1], 2),
+            "modmul_fips2_gps": round(out[4], 2), "sclk_ghz_in_kernel": round(out[2], 3),
+            "calibration_ms": round(out[3], 1)}
 
 
 class Timer:
