@@ -402,6 +402,8 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         params.set_slab(*h2g_dist.slab(n, world, rank))
     native = one_proof and args.transport == "native"
     transport_note = None
+    if one_proof:  # every wait on the library's RCCL communicators has a deadline (fail soft)
+        h2g.comm_set_timeout(args.comm_timeout)
     if native and shard:  # the library's own RCCL communicators (csrc/comm.cpp); the id travels over torch
         import torch as _t
         tdev = dev if dist.get_backend() == "nccl" else "cpu"
@@ -965,6 +967,10 @@ def main():
     ap.add_argument("--spmd-owner-weight", type=float, default=-1,
                     help="spmd: slab weight of the sub-coset owners against 1 for the other ranks "
                          "(0: uniform, -1: measured default for the ratio of ranks to owners)")
+    ap.add_argument("--comm-timeout", type=float, default=120.0,
+                    help="N > 1: seconds any wait on libh2g's RCCL communicators may take (setup, each "
+                         "collective); past it they are aborted, the proof fails on that rank, and every "
+                         "rank moves to the next transport of --spmd-transports")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3, help="CPU baseline runs (median)")
     ap.add_argument("--no-krange", action="store_true",

@@ -392,6 +392,13 @@ int h2g_memcpy_dtod(void* d_dst, const void* d_src, size_t bytes);
  * slabs stream while the peers compute.  The proof bytes do not depend on `world`. */
 int h2g_comm_unique_id(uint8_t id[256]);
 int h2g_comm_init(const uint8_t id[256], int world, int rank);
+/* deadline (seconds; <= 0: none; default 300) of every wait on the library's RCCL
+ * communicators: their non-blocking setup in h2g_comm_init, each call's enqueue and each
+ * collective's completion.  Past it -- or on an RCCL error -- the communicators are aborted
+ * (ncclCommAbort) and the call fails with H2G_ERR_DEVICE, so a run that would hang inside
+ * RCCL returns and the caller can fall back to another transport (bench.py).  The peers'
+ * wait for rank 0's next slab request (h2g_comm_serve) has no deadline. */
+int h2g_comm_set_timeout(double seconds);
 int h2g_comm_install(uint64_t params);
 int h2g_comm_serve(uint64_t params, uint64_t* served);
 int h2g_comm_stop(void);

@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "comm_wait.h"
 #include "runtime.h"
 
 namespace h2g {
@@ -27,6 +28,10 @@ namespace {
   } while (0)
 
 static constexpr int RING = 16;  // outstanding MSMs on rank 0
+
+// the deadline of every RCCL wait (communicator setup, enqueue, completion), seconds; <= 0:
+// none.  Past it the communicators are aborted and the call fails (comm_wait.h).
+double g_timeout_s = 300.0;
 
 struct Slot {
   bool busy = false;
@@ -54,6 +59,7 @@ struct Comm {
   int64_t *h_rhdr = nullptr, *d_rhdr = nullptr;  // one header
   int64_t *h_rpart = nullptr, *d_rpart = nullptr;
   // SPMD all-gather of partials: pinned [world][H2G_SPMD_WORDS], device in / out
+  bool broken = false;  // aborted after a failed or timed-out wait: every later call fails
   uint64_t* h_ag = nullptr;
   uint64_t *d_ag_in = nullptr, *d_ag_out = nullptr;
   // SPMD host all-gather (multi-open tail): pinned / device staging, world x bytes + bytes
@@ -77,7 +83,86 @@ int grow(void** p, size_t* cap, size_t bytes) {
   return H2G_OK;
 }
 
+// ---- non-blocking communicators, every wait against g_timeout_s
+using commwait::poll_until;
+int nccl_poll(ncclComm_t comm) {  // a communicator's asynchronous state
+  if (!comm) return commwait::POLL_ERROR;
+  ncclResult_t st = ncclSuccess;
+  if (ncclCommGetAsyncError(comm, &st) != ncclSuccess) return commwait::POLL_ERROR;
+  return st == ncclSuccess ? commwait::POLL_DONE : (st == ncclInProgress ? commwait::POLL_PENDING : commwait::POLL_ERROR);
+}
+void comm_abort(Comm* c) {
+  if (c->tx) (void)ncclCommAbort(c->tx);
+  if (c->rx) (void)ncclCommAbort(c->rx);
+  c->tx = c->rx = nullptr;
+  c->broken = true;
+}
+int wait_failed(Comm* c, int w, const std::string& what) {
+  comm_abort(c);
+  return fail(H2G_ERR_DEVICE, what + (w == commwait::WAIT_TIMEOUT
+                                          ? ": no progress within " + std::to_string(g_timeout_s) + " s"
+                                          : ": RCCL reported an error") + "; communicators aborted");
+}
+// an RCCL call on a non-blocking communicator: an error aborts; ncclInProgress is polled
+// until the communicator is ready for the next call
+int nccl_call(Comm* c, ncclComm_t comm, ncclResult_t r, const char* what) {
+  if (r == ncclSuccess) return H2G_OK;
+  if (r != ncclInProgress) {
+    comm_abort(c);
+    return fail(H2G_ERR_DEVICE, std::string(what) + ": " + ncclGetErrorString(r) + "; communicators aborted");
+  }
+  const int w = poll_until([&] { return nccl_poll(comm); }, g_timeout_s);
+  return w == commwait::WAIT_OK ? H2G_OK : wait_failed(c, w, what);
+}
+#define NCCLQ(c, comm, expr) RCCHK(nccl_call(c, comm, (expr), #expr))
+// the work queued on `st` (RCCL kernels among it) has finished; RCCL errors on either
+// communicator end the wait early
+int wait_stream(Comm* c, hipStream_t st, const char* what, double timeout_s) {
+  int hip_err = 0;
+  const int w = poll_until(
+      [&] {
+        const hipError_t e = hipStreamQuery(st);
+        if (e == hipSuccess) return (int)commwait::POLL_DONE;
+        if (e != hipErrorNotReady) {
+          hip_err = (int)e;
+          return (int)commwait::POLL_ERROR;
+        }
+        if (nccl_poll(c->tx) == commwait::POLL_ERROR || nccl_poll(c->rx) == commwait::POLL_ERROR)
+          return (int)commwait::POLL_ERROR;
+        return (int)commwait::POLL_PENDING;
+      },
+      timeout_s);
+  if (w == commwait::WAIT_OK) return H2G_OK;
+  if (hip_err) {
+    comm_abort(c);
+    return fail(H2G_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString((hipError_t)hip_err));
+  }
+  return wait_failed(c, w, what);
+}
+int wait_event(Comm* c, hipEvent_t ev, const char* what) {
+  const int w = poll_until(
+      [&] {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return (int)commwait::POLL_DONE;
+        if (e != hipErrorNotReady) return (int)commwait::POLL_ERROR;
+        if (nccl_poll(c->tx) == commwait::POLL_ERROR || nccl_poll(c->rx) == commwait::POLL_ERROR)
+          return (int)commwait::POLL_ERROR;
+        return (int)commwait::POLL_PENDING;
+      },
+      g_timeout_s);
+  return w == commwait::WAIT_OK ? H2G_OK : wait_failed(c, w, what);
+}
+Comm* usable(void* ctx) {
+  Comm* c = static_cast<Comm*>(ctx);
+  return c && c == g_comm && !c->broken ? c : nullptr;
+}
+
 }  // namespace
+
+int comm_set_timeout(double seconds) {
+  g_timeout_s = seconds;
+  return H2G_OK;
+}
 
 int comm_unique_id(uint8_t id[COMM_ID_BYTES]) {
   ncclUniqueId a, b;
@@ -101,8 +186,25 @@ int comm_init(const uint8_t id[COMM_ID_BYTES], int world, int rank) {
   ncclUniqueId a, b;
   std::memcpy(&a, id, sizeof(a));
   std::memcpy(&b, id + 128, sizeof(b));
-  NCCLCHK(ncclCommInitRank(&c->tx, world, a, rank));
-  NCCLCHK(ncclCommInitRank(&c->rx, world, b, rank));
+  // non-blocking setup: both communicators connect in the background, polled against the
+  // deadline (a peer that never arrives fails this call instead of hanging it)
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclResult_t r = ncclCommInitRankConfig(&c->tx, world, a, rank, &cfg);
+  if (r == ncclSuccess || r == ncclInProgress) r = ncclCommInitRankConfig(&c->rx, world, b, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    comm_abort(c.get());
+    return fail(H2G_ERR_DEVICE, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+  }
+  const int w = poll_until(
+      [&] {
+        const int a1 = nccl_poll(c->tx), b1 = nccl_poll(c->rx);
+        if (a1 == commwait::POLL_ERROR || b1 == commwait::POLL_ERROR) return (int)commwait::POLL_ERROR;
+        return a1 == commwait::POLL_DONE && b1 == commwait::POLL_DONE ? (int)commwait::POLL_DONE
+                                                                      : (int)commwait::POLL_PENDING;
+      },
+      g_timeout_s);
+  if (w != commwait::WAIT_OK) return wait_failed(c.get(), w, "communicator setup (ncclCommInitRankConfig)");
   HIPCHK(hipStreamCreateWithFlags(&c->stx, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&c->srx, hipStreamNonBlocking));
   if (rank == 0) {
@@ -130,8 +232,8 @@ int comm_destroy() {
   if (!c) return H2G_OK;
   g_comm = nullptr;
   (void)hipSetDevice(c->device);
-  if (c->stx) (void)hipStreamSynchronize(c->stx);
-  if (c->srx) (void)hipStreamSynchronize(c->srx);
+  for (hipStream_t st : {c->stx, c->srx})  // bounded: an aborted communicator's work may not drain
+    if (st) (void)poll_until([&] { return hipStreamQuery(st) == hipErrorNotReady ? 0 : 1; }, 10.0);
   if (c->tx) (void)ncclCommDestroy(c->tx);
   if (c->rx) (void)ncclCommDestroy(c->rx);
   for (auto& s : c->slots) {
@@ -161,7 +263,7 @@ int comm_world() { return g_comm ? g_comm->world : 1; }
 int comm_rccl_info(int* count, int* rank) {
   *count = 0;
   *rank = -1;
-  if (!g_comm) return H2G_OK;
+  if (!g_comm || g_comm->broken) return H2G_OK;
   NCCLCHK(ncclCommCount(g_comm->tx, count));
   NCCLCHK(ncclCommUserRank(g_comm->tx, rank));
   return H2G_OK;
@@ -175,8 +277,8 @@ void* comm_spmd_ctx() { return g_comm; }
 // it for the same MSMs in the same order)
 int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[H2G_SPMD_WORDS], uint64_t* out) {
   (void)seq;
-  Comm* c = static_cast<Comm*>(ctx);
-  if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm: no communicator for the SPMD all-gather");
+  Comm* c = usable(ctx);
+  if (!c) return fail(H2G_ERR_STATE, "comm: no (live) communicator for the SPMD all-gather");
   HIPCHK(hipSetDevice(c->device));
   const size_t W = (size_t)c->world;
   constexpr size_t SW = H2G_SPMD_WORDS;
@@ -187,9 +289,9 @@ int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[H2G_SPMD_W
   }
   std::memcpy(c->h_ag, in, SW * 8);
   HIPCHK(hipMemcpyAsync(c->d_ag_in, c->h_ag, SW * 8, hipMemcpyHostToDevice, c->stx));
-  NCCLCHK(ncclAllGather(c->d_ag_in, c->d_ag_out, SW, ncclUint64, c->tx, c->stx));
+  NCCLQ(c, c->tx, ncclAllGather(c->d_ag_in, c->d_ag_out, SW, ncclUint64, c->tx, c->stx));
   HIPCHK(hipMemcpyAsync(c->h_ag, c->d_ag_out, W * SW * 8, hipMemcpyDeviceToHost, c->stx));
-  HIPCHK(hipStreamSynchronize(c->stx));
+  RCCHK(wait_stream(c, c->stx, "SPMD all-gather of the MSM partials", g_timeout_s));
   std::memcpy(out, c->h_ag, W * SW * 8);
   return H2G_OK;
 }
@@ -197,8 +299,8 @@ int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[H2G_SPMD_W
 // the multi-open tail's scalars (partial evaluations, kate carries): staged through
 // grow-only pinned / device buffers, one ncclAllGather of bytes
 int comm_allgather_host(void* ctx, const void* in, size_t bytes, void* out) {
-  Comm* c = static_cast<Comm*>(ctx);
-  if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm: no communicator for the SPMD host all-gather");
+  Comm* c = usable(ctx);
+  if (!c) return fail(H2G_ERR_STATE, "comm: no (live) communicator for the SPMD host all-gather");
   if (bytes == 0) return H2G_OK;
   HIPCHK(hipSetDevice(c->device));
   const size_t W = (size_t)c->world, total = W * bytes;
@@ -216,9 +318,9 @@ int comm_allgather_host(void* ctx, const void* in, size_t bytes, void* out) {
   uint8_t* din = static_cast<uint8_t*>(c->d_hg) + total;
   std::memcpy(hin, in, bytes);
   HIPCHK(hipMemcpyAsync(din, hin, bytes, hipMemcpyHostToDevice, c->stx));
-  NCCLCHK(ncclAllGather(din, c->d_hg, bytes, ncclUint8, c->tx, c->stx));
+  NCCLQ(c, c->tx, ncclAllGather(din, c->d_hg, bytes, ncclUint8, c->tx, c->stx));
   HIPCHK(hipMemcpyAsync(c->h_hg, c->d_hg, total, hipMemcpyDeviceToHost, c->stx));
-  HIPCHK(hipStreamSynchronize(c->stx));
+  RCCHK(wait_stream(c, c->stx, "SPMD host all-gather", g_timeout_s));
   std::memcpy(out, c->h_hg, total);
   return H2G_OK;
 }
@@ -226,12 +328,12 @@ int comm_allgather_host(void* ctx, const void* in, size_t bytes, void* out) {
 // h(X)'s coefficient slabs from the sub-coset owners: one group of sends and receives on
 // the slab communicator, the rank's own block a device copy
 int comm_exchange(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv, const size_t* recv_bytes) {
-  Comm* c = static_cast<Comm*>(ctx);
-  if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm: no communicator for the SPMD exchange");
+  Comm* c = usable(ctx);
+  if (!c) return fail(H2G_ERR_STATE, "comm: no (live) communicator for the SPMD exchange");
   HIPCHK(hipSetDevice(c->device));
   const int W = c->world;
   size_t so = 0, ro = 0;
-  NCCLCHK(ncclGroupStart());
+  NCCLQ(c, c->tx, ncclGroupStart());
   for (int p = 0; p < W; p++) {
     const uint8_t* sp = static_cast<const uint8_t*>(d_send) + so;
     uint8_t* rp = static_cast<uint8_t*>(d_recv) + ro;
@@ -242,24 +344,22 @@ int comm_exchange(void* ctx, const void* d_send, const size_t* send_bytes, void*
       }
       if (send_bytes[p]) HIPCHK(hipMemcpyAsync(rp, sp, send_bytes[p], hipMemcpyDeviceToDevice, c->stx));
     } else {
-      if (send_bytes[p]) NCCLCHK(ncclSend(sp, send_bytes[p], ncclUint8, p, c->tx, c->stx));
-      if (recv_bytes[p]) NCCLCHK(ncclRecv(rp, recv_bytes[p], ncclUint8, p, c->tx, c->stx));
+      if (send_bytes[p]) NCCLQ(c, c->tx, ncclSend(sp, send_bytes[p], ncclUint8, p, c->tx, c->stx));
+      if (recv_bytes[p]) NCCLQ(c, c->tx, ncclRecv(rp, recv_bytes[p], ncclUint8, p, c->tx, c->stx));
     }
     so += send_bytes[p];
     ro += recv_bytes[p];
   }
-  NCCLCHK(ncclGroupEnd());
-  HIPCHK(hipStreamSynchronize(c->stx));
-  return H2G_OK;
+  NCCLQ(c, c->tx, ncclGroupEnd());
+  return wait_stream(c, c->stx, "SPMD exchange", g_timeout_s);
 }
 
 int comm_bcast(void* ctx, void* d_buf, size_t bytes, int root) {
-  Comm* c = static_cast<Comm*>(ctx);
-  if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm: no communicator for the SPMD broadcast");
+  Comm* c = usable(ctx);
+  if (!c) return fail(H2G_ERR_STATE, "comm: no (live) communicator for the SPMD broadcast");
   HIPCHK(hipSetDevice(c->device));
-  NCCLCHK(ncclBroadcast(d_buf, d_buf, bytes, ncclUint8, root, c->tx, c->stx));
-  HIPCHK(hipStreamSynchronize(c->stx));
-  return H2G_OK;
+  NCCLQ(c, c->tx, ncclBroadcast(d_buf, d_buf, bytes, ncclUint8, root, c->tx, c->stx));
+  return wait_stream(c, c->stx, "SPMD broadcast", g_timeout_s);
 }
 
 void* comm_transport_ctx(uint64_t points) {
@@ -272,8 +372,8 @@ void* comm_transport_ctx(uint64_t points) {
 // prover synchronises its stream first); the prover stream is made to wait for the staging
 // copy, so later in-place work cannot race the sends.
 int comm_launch(void* ctx, uint64_t seq, int32_t base_set, uint64_t n, const void* d_scalars) {
-  Comm* c = static_cast<Comm*>(ctx);
-  if (!c || c != g_comm || c->rank != 0) return fail(H2G_ERR_STATE, "comm_launch: no rank-0 communicator");
+  Comm* c = usable(ctx);
+  if (!c || c->rank != 0) return fail(H2G_ERR_STATE, "comm_launch: no (live) rank-0 communicator");
   int si = -1;
   for (int i = 0; i < RING; i++)
     if (!c->slots[(seq + i) % RING].busy) {
@@ -299,19 +399,20 @@ int comm_launch(void* ctx, uint64_t seq, int32_t base_set, uint64_t n, const voi
   }
   HIPCHK(hipMemcpyAsync(dh + 5, hh + 5, (size_t)(W - 1) * 5 * 8, hipMemcpyHostToDevice, c->stx));
   // headers, then slabs (a peer reads its header before it posts the slab's receive)
-  NCCLCHK(ncclGroupStart());
-  for (int r = 1; r < W; r++) NCCLCHK(ncclSend(dh + 5 * r, 5 * 8, ncclUint8, r, c->tx, c->stx));
-  NCCLCHK(ncclGroupEnd());
-  NCCLCHK(ncclGroupStart());
+  NCCLQ(c, c->tx, ncclGroupStart());
+  for (int r = 1; r < W; r++) NCCLQ(c, c->tx, ncclSend(dh + 5 * r, 5 * 8, ncclUint8, r, c->tx, c->stx));
+  NCCLQ(c, c->tx, ncclGroupEnd());
+  NCCLQ(c, c->tx, ncclGroupStart());
   for (int r = 1; r < W; r++) {
     const uint64_t lo = slab_lo(c->points, n, W, r), hi = slab_lo(c->points, n, W, r + 1);
-    if (hi > lo) NCCLCHK(ncclSend((const uint8_t*)s.stage + (lo - lo1) * 32, (hi - lo) * 32, ncclUint8, r, c->tx, c->stx));
+    if (hi > lo)
+      NCCLQ(c, c->tx, ncclSend((const uint8_t*)s.stage + (lo - lo1) * 32, (hi - lo) * 32, ncclUint8, r, c->tx, c->stx));
   }
-  NCCLCHK(ncclGroupEnd());
+  NCCLQ(c, c->tx, ncclGroupEnd());
   int64_t* dp = c->d_part + (size_t)si * W * 9;
-  NCCLCHK(ncclGroupStart());
-  for (int r = 1; r < W; r++) NCCLCHK(ncclRecv(dp + 9 * r, 9 * 8, ncclUint8, r, c->rx, c->srx));
-  NCCLCHK(ncclGroupEnd());
+  NCCLQ(c, c->rx, ncclGroupStart());
+  for (int r = 1; r < W; r++) NCCLQ(c, c->rx, ncclRecv(dp + 9 * r, 9 * 8, ncclUint8, r, c->rx, c->srx));
+  NCCLQ(c, c->rx, ncclGroupEnd());
   HIPCHK(hipMemcpyAsync(c->h_part + (size_t)si * W * 9 + 9, dp + 9, (size_t)(W - 1) * 9 * 8, hipMemcpyDeviceToHost,
                         c->srx));
   HIPCHK(hipEventRecord(s.done, c->srx));
@@ -321,12 +422,12 @@ int comm_launch(void* ctx, uint64_t seq, int32_t base_set, uint64_t n, const voi
 }
 
 int comm_collect(void* ctx, uint64_t seq, uint64_t* partials, int32_t* is_identity) {
-  Comm* c = static_cast<Comm*>(ctx);
-  if (!c || c != g_comm) return fail(H2G_ERR_STATE, "comm_collect: no communicator");
+  Comm* c = usable(ctx);
+  if (!c) return fail(H2G_ERR_STATE, "comm_collect: no (live) communicator");
   for (int i = 0; i < RING; i++) {
     Slot& s = c->slots[i];
     if (!s.busy || s.seq != seq) continue;
-    HIPCHK(hipEventSynchronize(s.done));
+    RCCHK(wait_event(c, s.done, "slab partials of a sharded MSM"));
     const int64_t* hp = c->h_part + (size_t)i * c->world * 9;
     for (int r = 1; r < c->world; r++) {
       std::memcpy(partials + 8 * (r - 1), hp + 9 * r, 64);
@@ -339,10 +440,10 @@ int comm_collect(void* ctx, uint64_t seq, uint64_t* partials, int32_t* is_identi
 }
 
 int comm_stop() {
-  Comm* c = g_comm;
-  if (!c || c->rank != 0) return fail(H2G_ERR_STATE, "comm_stop: no rank-0 communicator");
+  Comm* c = usable(g_comm);
+  if (!c || c->rank != 0) return fail(H2G_ERR_STATE, "comm_stop: no (live) rank-0 communicator");
   for (auto& s : c->slots)
-    if (s.busy) HIPCHK(hipEventSynchronize(s.done));
+    if (s.busy) RCCHK(wait_event(c, s.done, "slab partials before stop"));
   const int W = c->world;
   int64_t* hh = c->h_hdr;  // slot 0's header row (no launch is in flight)
   for (int r = 1; r < W; r++) {
@@ -350,21 +451,22 @@ int comm_stop() {
     std::memcpy(hh + 5 * r, h, sizeof(h));
   }
   HIPCHK(hipMemcpyAsync(c->d_hdr + 5, hh + 5, (size_t)(W - 1) * 5 * 8, hipMemcpyHostToDevice, c->stx));
-  NCCLCHK(ncclGroupStart());
-  for (int r = 1; r < W; r++) NCCLCHK(ncclSend(c->d_hdr + 5 * r, 5 * 8, ncclUint8, r, c->tx, c->stx));
-  NCCLCHK(ncclGroupEnd());
-  HIPCHK(hipStreamSynchronize(c->stx));
+  NCCLQ(c, c->tx, ncclGroupStart());
+  for (int r = 1; r < W; r++) NCCLQ(c, c->tx, ncclSend(c->d_hdr + 5 * r, 5 * 8, ncclUint8, r, c->tx, c->stx));
+  NCCLQ(c, c->tx, ncclGroupEnd());
+  RCCHK(wait_stream(c, c->stx, "stop headers", g_timeout_s));
   for (auto& s : c->slots) s.busy = false;
   return H2G_OK;
 }
 
 int comm_next_request(int32_t* op, int32_t* base_set, uint64_t* lo, uint64_t* count, const void** d_slab,
                       hipStream_t* ready) {
-  Comm* c = g_comm;
-  if (!c || c->rank == 0) return fail(H2G_ERR_STATE, "comm_next_request: no peer communicator");
-  NCCLCHK(ncclRecv(c->d_rhdr, 5 * 8, ncclUint8, 0, c->tx, c->stx));
+  Comm* c = usable(g_comm);
+  if (!c || c->rank == 0) return fail(H2G_ERR_STATE, "comm_next_request: no (live) peer communicator");
+  NCCLQ(c, c->tx, ncclRecv(c->d_rhdr, 5 * 8, ncclUint8, 0, c->tx, c->stx));
   HIPCHK(hipMemcpyAsync(c->h_rhdr, c->d_rhdr, 5 * 8, hipMemcpyDeviceToHost, c->stx));
-  HIPCHK(hipStreamSynchronize(c->stx));
+  // no deadline here: rank 0 decides when the next request comes (RCCL errors still end it)
+  RCCHK(wait_stream(c, c->stx, "next request header", 0.0));
   const int64_t* h = c->h_rhdr;
   *op = (int32_t)h[0];
   *base_set = (int32_t)h[2];
@@ -376,19 +478,19 @@ int comm_next_request(int32_t* op, int32_t* base_set, uint64_t* lo, uint64_t* co
   const int b = c->rnext;
   c->rnext ^= 1;
   RCCHK(grow(&c->rstage[b], &c->rcap[b], (size_t)*count * 32));
-  NCCLCHK(ncclRecv(c->rstage[b], (size_t)*count * 32, ncclUint8, 0, c->tx, c->stx));
+  NCCLQ(c, c->tx, ncclRecv(c->rstage[b], (size_t)*count * 32, ncclUint8, 0, c->tx, c->stx));
   *d_slab = c->rstage[b];
   return H2G_OK;
 }
 
 int comm_send_partial(const uint64_t partial[8], int32_t is_identity) {
-  Comm* c = g_comm;
-  if (!c || c->rank == 0) return fail(H2G_ERR_STATE, "comm_send_partial: no peer communicator");
-  HIPCHK(hipStreamSynchronize(c->srx));  // the previous partial left the pinned buffer
+  Comm* c = usable(g_comm);
+  if (!c || c->rank == 0) return fail(H2G_ERR_STATE, "comm_send_partial: no (live) peer communicator");
+  RCCHK(wait_stream(c, c->srx, "previous partial", g_timeout_s));  // it left the pinned buffer
   std::memcpy(c->h_rpart, partial, 64);
   c->h_rpart[8] = is_identity ? 1 : 0;
   HIPCHK(hipMemcpyAsync(c->d_rpart, c->h_rpart, 9 * 8, hipMemcpyHostToDevice, c->srx));
-  NCCLCHK(ncclSend(c->d_rpart, 9 * 8, ncclUint8, 0, c->rx, c->srx));
+  NCCLQ(c, c->rx, ncclSend(c->d_rpart, 9 * 8, ncclUint8, 0, c->rx, c->srx));
   return H2G_OK;
 }
 

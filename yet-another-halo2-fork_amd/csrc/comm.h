@@ -25,6 +25,7 @@ static constexpr int COMM_ID_BYTES = 256;  // two ncclUniqueIds (tx, rx)
 
 int comm_unique_id(uint8_t id[COMM_ID_BYTES]);
 int comm_init(const uint8_t id[COMM_ID_BYTES], int world, int rank);
+int comm_set_timeout(double seconds);  // deadline of every RCCL wait (<= 0: none)
 int comm_destroy();
 int comm_world();
 int comm_rccl_info(int* count, int* rank);

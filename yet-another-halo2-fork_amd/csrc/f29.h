@@ -158,6 +158,37 @@ H2G_HD F29 mul29(const F29& a, const F29& b) {
   return r;
 }
 
+// REDC(a^2): the 36 cross products once, against the doubled limbs (2 a_i < 2^30 for a
+// normalised a, so each term stays < 2^59), plus the 9 squares -- 45 + 81 mads instead of
+// 81 + 81.  Same output bound as mul29(a, a).
+template <class P>
+H2G_HD F29 sqr29(const F29& a) {
+  uint32_t m[9], d[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) d[i] = a.l[i] << 1;
+  F29 r;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+#pragma unroll
+    for (int i = (k > 8 ? k - 8 : 0); 2 * i < k; i++) acc += (uint64_t)d[i] * a.l[k - i];
+    if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+    if (k < 9) {
+#pragma unroll
+      for (int i = 0; i < k; i++) acc += (uint64_t)m[i] * C29<P>::M[k - i];
+      m[k] = ((uint32_t)acc * C29<P>::INV) & F29_MASK;
+      acc += (uint64_t)m[k] * C29<P>::M[0];
+    } else {
+#pragma unroll
+      for (int i = k - 8; i < 9; i++) acc += (uint64_t)m[i] * C29<P>::M[k - i];
+      r.l[k - 9] = (uint32_t)acc & F29_MASK;
+    }
+    acc >>= 29;
+  }
+  r.l[8] = (uint32_t)acc;
+  return r;
+}
+
 // F29 -> storage form, fully reduced: REDC(v * (2^256 mod M)) = v 2^-5 mod M (< 2M for
 // v < 2^261, i.e. a normalised top limb), one conditional subtraction, repacked into 32-bit limbs
 template <class P>
@@ -342,10 +373,10 @@ H2G_HD G1xyzz29 xyzz29_madd(const G1xyzz29& p, const F29& qx, const F29& qy) {
     }
     return xyzz29_identity();  // p == -q
   }
-  const F29 PP = mul29<P>(Pp, Pp);
+  const F29 PP = sqr29<P>(Pp);
   const F29 PPP = mul29<P>(Pp, PP);
   const F29 Q = mul29<P>(p.X, PP);
-  const F29 R2 = mul29<P>(R, R);
+  const F29 R2 = sqr29<P>(R);
   G1xyzz29 r;
   r.X = norm29(sub29<P, 32, 31>(R2, add29(add29(PPP, Q), Q)));  // R^2 - PPP - 2Q
   r.Y = mul29x2<P>(R, sub29<P, 64, 29>(Q, r.X), p.Y, sub29<P, 16, 29>(F29{}, PPP));  // R (Q - X3) - Y PPP

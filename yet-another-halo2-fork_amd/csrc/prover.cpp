@@ -4332,6 +4332,11 @@ int h2g_comm_init(const uint8_t id[256], int world, int rank) {
   return comm_init(id, world, rank);
 }
 
+int h2g_comm_set_timeout(double seconds) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  return comm_set_timeout(seconds);
+}
+
 int h2g_comm_info(int32_t* rccl_count, int32_t* rccl_rank) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   int c = 0, r = -1;

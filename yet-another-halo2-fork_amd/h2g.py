@@ -112,6 +112,7 @@ _SIGS = {
     "h2g_memcpy_dtod": ([VP, VP, SZ], I32),
     "h2g_comm_unique_id": ([ctypes.c_char_p], I32),
     "h2g_comm_init": ([ctypes.c_char_p, I32, I32], I32),
+    "h2g_comm_set_timeout": ([ctypes.c_double], I32),
     "h2g_comm_install": ([U64], I32),
     "h2g_comm_serve": ([U64, ctypes.POINTER(U64)], I32),
     "h2g_comm_stop": ([], I32),
@@ -1014,6 +1015,11 @@ def comm_unique_id():
 
 def comm_init(uid, world, rank):
     check(lib().h2g_comm_init(bytes(uid), world, rank))
+
+
+def comm_set_timeout(seconds):
+    """deadline of every wait on the library's RCCL communicators (h2g_comm_set_timeout)"""
+    check(lib().h2g_comm_set_timeout(float(seconds)))
 
 
 def comm_install(params):
