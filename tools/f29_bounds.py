@@ -77,6 +77,46 @@ def run(name, st):
           f"largest intermediate 2^{LG(worst):.3f}")
 
 
+def reduce29(vmax):
+    """bound of csrc/f29.h reduce29(v) over v < vmax: v - q M with q = floor(v_8 / (M_8 + 1))
+    is >= 0 and < M + (q + 2) 2^232"""
+    q = top(vmax) // (top(M) + 1)
+    return M + (q + 2) * (1 << 232)
+
+
+def backend_class(C):
+    """the MSM back-end's class (every coordinate < C): closed under xyzz29_add / xyzz29_dbl"""
+    n29, n30 = 1 << 29, 1 << 30
+    # add-2008-s
+    U = mul(C, C)
+    sub_ok(U, 2, 29)
+    P = U + 2 * M
+    PP = mul(P, P)
+    PPP, Q = mul(P, PP), mul(U, PP)
+    sub_ok(PPP + 2 * Q, 4, 31)
+    X3 = reduce29(mul(P, P) + 4 * M)
+    sub_ok(X3, 4, 29)
+    sub_ok(PPP, 2, 29)
+    column_ok(n29, n29 + n30, n29, n30)
+    Y3 = (P * (Q + 4 * M) + U * 2 * M) // R + M + 1
+    ZZ3 = mul(mul(C, C), PP)
+    out_add = (X3, Y3, ZZ3, mul(mul(C, C), PPP))
+    # dbl-2008-s-1
+    Uy = 2 * C
+    V = mul(Uy, Uy)
+    W, S, X2 = mul(Uy, V), mul(C, V), mul(C, C)
+    Mm = 3 * X2
+    sub_ok(2 * S, 4, 31)
+    X3d = reduce29(mul(Mm, Mm) + 4 * M)
+    sub_ok(X3d, 4, 29)
+    sub_ok(W, 2, 29)
+    Y3d = (Mm * (S + 4 * M) + C * 2 * M) // R + M + 1
+    out_dbl = (X3d, Y3d, mul(V, C), mul(W, C))
+    for v in out_add + out_dbl:
+        assert v < C, (LG(v), LG(C))
+    return max(out_add + out_dbl)
+
+
 MR = 0x30644e72e131a029b85045b68181585d2833e84879b9709143e1f593f0000001  # BN254 Fr
 
 
@@ -100,6 +140,11 @@ if __name__ == "__main__":
     run("fresh point", (32 * M, 32 * M, M, M))
     d = mul(32 * M, M)
     run("doubling path", (d, d, d, d))
+    acc_max = (1 << 260)  # above every accumulation output (fixpoints above)
+    assert reduce29(acc_max) < 1.001 * M
+    worst = backend_class(int(1.2 * M))
+    print(f"back-end class: coordinates < 1.2 M closed under add and dbl (outputs < {worst / M:.3f} M); "
+          f"reduce29 of an accumulator < 2^260 gives < {reduce29(acc_max) / M:.4f} M")
     b0 = 3 * MR  # stored values of the NTT passes
     for st in (3, 4, 5, 6):
         out = ntt_pass(st, b0)

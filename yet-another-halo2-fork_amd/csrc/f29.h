@@ -454,4 +454,98 @@ H2G_HD F29 storage_to_f29(const Fe<P>& s) {
   return sub_m_if_ge29<P>(mul29<P>(to29(s), one29v<P>()));
 }
 
+
+// ---- the MSM back-end's XYZZ arithmetic (fixup, bucket reduction) in F29 ---------------
+// The back-end works on a tighter class than the accumulation: every coordinate < 1.2 M.
+// reduce29 brings the accumulation's values (< 2^259.5) into it once, and the full
+// addition and the doubling reduce their one subtracted output (X3) the same way, so the
+// subtraction constants stay small (2 M, 4 M) and no product's column comes near 2^64
+// (tools/f29_bounds.py checks the class is closed under both).
+
+// v - q M with q = floor(v_8 / (M_8 + 1)) (v normalised: limbs 0..7 < 2^29): the result is
+// >= 0 and < M + (q + 2) 2^232 < 1.001 M -- the top limb's share of v removed, ~40 VALU ops
+template <class P>
+H2G_HD F29 reduce29(const F29& v) {
+  constexpr uint32_t mt = C29<P>::M[8] + 1;
+  const uint32_t q = v.l[8] / mt;
+  F29 r;
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int64_t t = (int64_t)v.l[i] - (int64_t)((uint64_t)q * C29<P>::M[i]) + br;
+    if (i < 8) {
+      r.l[i] = (uint32_t)t & F29_MASK;
+      br = t >> 29;
+    } else {
+      r.l[i] = (uint32_t)t;
+    }
+  }
+  return r;
+}
+H2G_HD G1xyzz29 xyzz29_reduce(const G1xyzz29& p) {
+  G1xyzz29 r;
+  r.X = reduce29<FqParams>(p.X);
+  r.Y = reduce29<FqParams>(p.Y);
+  r.ZZ = reduce29<FqParams>(p.ZZ);
+  r.ZZZ = reduce29<FqParams>(p.ZZZ);
+  return r;
+}
+
+// dbl-2008-s-1 on the back-end class
+H2G_HD G1xyzz29 xyzz29_dbl(const G1xyzz29& p) {
+  using P = FqParams;
+  if (xyzz29_is_identity(p)) return p;
+  const F29 U = norm29(add29(p.Y, p.Y));
+  const F29 V = sqr29<P>(U);
+  const F29 W = mul29<P>(U, V);
+  const F29 S = mul29<P>(p.X, V);
+  const F29 X2 = sqr29<P>(p.X);
+  const F29 Mm = norm29(add29(add29(X2, X2), X2));
+  G1xyzz29 r;
+  r.X = reduce29<P>(norm29(sub29<P, 4, 31>(sqr29<P>(Mm), add29(S, S))));          // M^2 - 2S
+  r.Y = mul29x2<P>(Mm, sub29<P, 4, 29>(S, r.X), p.Y, sub29<P, 2, 29>(F29{}, W));  // M (S - X3) - W Y
+  r.ZZ = mul29<P>(V, p.ZZ);
+  r.ZZZ = mul29<P>(W, p.ZZZ);
+  return r;
+}
+
+// add-2008-s on the back-end class
+H2G_HD G1xyzz29 xyzz29_add(const G1xyzz29& p, const G1xyzz29& q) {
+  using P = FqParams;
+  if (xyzz29_is_identity(q)) return p;
+  if (xyzz29_is_identity(p)) return q;
+  const F29 U1 = mul29<P>(p.X, q.ZZ);
+  const F29 U2 = mul29<P>(q.X, p.ZZ);
+  const F29 S1 = mul29<P>(p.Y, q.ZZZ);
+  const F29 S2 = mul29<P>(q.Y, p.ZZZ);
+  const F29 Pp = norm29(sub29<P, 2, 29>(U2, U1));
+  const F29 R = norm29(sub29<P, 2, 29>(S2, S1));
+  if (is_zero29<P>(Pp)) {
+    if (is_zero29<P>(R)) return xyzz29_dbl(p);
+    return xyzz29_identity();
+  }
+  const F29 PP = sqr29<P>(Pp);
+  const F29 PPP = mul29<P>(Pp, PP);
+  const F29 Q = mul29<P>(U1, PP);
+  G1xyzz29 r;
+  r.X = reduce29<P>(norm29(sub29<P, 4, 31>(sqr29<P>(R), add29(add29(PPP, Q), Q))));  // R^2 - PPP - 2Q
+  r.Y = mul29x2<P>(R, sub29<P, 4, 29>(Q, r.X), S1, sub29<P, 2, 29>(F29{}, PPP));     // R (Q - X3) - S1 PPP
+  r.ZZ = mul29<P>(mul29<P>(p.ZZ, q.ZZ), PP);
+  r.ZZZ = mul29<P>(mul29<P>(p.ZZZ, q.ZZZ), PPP);
+  return r;
+}
+
+// [k] p for a small k (double-and-add, MSB first)
+H2G_HD G1xyzz29 xyzz29_mul_u32(const G1xyzz29& p, uint32_t k) {
+  if (k == 0) return xyzz29_identity();
+  int top = 31;
+  while (!((k >> top) & 1)) top--;
+  G1xyzz29 acc = p;
+  for (int b = top - 1; b >= 0; b--) {
+    acc = xyzz29_dbl(acc);
+    if ((k >> b) & 1) acc = xyzz29_add(acc, p);
+  }
+  return acc;
+}
+
 }  // namespace h2g

@@ -82,193 +82,6 @@ __device__ __forceinline__ G1Affine ld_aff(const G1Affine* p) {
   return r;
 }
 
-// Buckets spanning chunks, one thread per bucket: the piece in its first chunk t0 is
-// that chunk's last run (slot 1) unless the bucket starts the chunk (slot 0); every
-// later chunk holds it as its first run (slot 0).  Buckets over more than MSM_SMALL
-// chunks are cut into items of at most MSM_ITEM pieces (msm_big_item_kernel), whose
-// partial sums a second pass combines per bucket (msm_big_combine_kernel): the depth
-// stays logarithmic however the scalars concentrate (fixed-base top windows: n / 2^12
-// entries per bucket at c = 22; a column of equal values: n entries per bucket).
-// (H2G_ACC29: the slots hold raw F29 accumulators, converted here -- each piece is read once)
-__device__ __forceinline__ G1xyzz msm_piece(const AccPoint* bnd, uint32_t t, uint32_t t0, uint32_t bs, uint32_t L) {
-  return acc_to_xyzz(ld_accp(bnd + 2 * (size_t)t + ((t == t0 && bs != t0 * L) ? 1 : 0)));
-}
-
-static constexpr uint32_t MSM_GROUP = 16;            // lanes per item
-static constexpr uint32_t MSM_ITEM = MSM_GROUP * 4;  // pieces per item (4 per lane)
-static constexpr unsigned MSM_BIG_BLOCKS = 512;      // persistent grids below
-
-// big-bucket work item: pieces [tb, te) of bucket b; slot = the item's index into the
-// partial sums when the bucket has several items, ~0u when it is the bucket's only one
-struct MsmBigItem {
-  uint32_t b, tb, te, slot;
-};
-
-// upper bounds of the item lists (sizing): a bucket over np > MSM_SMALL chunks takes
-// ceil(np / MSM_ITEM) items, and the buckets' piece counts sum to < 2 nchunks
-static size_t msm_big_items_cap(size_t nchunks) { return 2 * nchunks / MSM_ITEM + 2 * nchunks / MSM_SMALL + 2; }
-static size_t msm_big_multi_cap(size_t nchunks) { return 2 * nchunks / MSM_ITEM + 2; }
-
-// The item lists are reserved with one atomic per wave (a wave-level scan of the lanes'
-// item counts), not one per bucket.  Q = 4: a quad per bucket (xyzz_add_q4, ~3x less
-// latency per addition) summing up to MSM_SMALL_Q4 pieces itself -- for small bucket
-// sets (<= 2^15), whose buckets span up to ~10 chunks of the minimum chunk length (2^16
-// points at c = 15: 9 pieces each, all of which took the big-item path: fixup 0.30 ->
-// 0.11 ms; at 2^16 buckets the quads' issue cost loses, 0.097 -> 0.142 ms).
-__device__ G1xyzz xyzz_add_q4(const G1xyzz& p, const G1xyzz& q);
-static constexpr uint32_t MSM_SMALL_Q4 = 32;
-
-template <int Q>
-__global__ void __launch_bounds__(MSM_THREADS)
-msm_fixup_kernel(const AccPoint* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t nbt, uint32_t L,
-                 const AccPoint* __restrict__ whole, G1xyzz* __restrict__ buckets,
-                 MsmBigItem* __restrict__ items, uint4* __restrict__ multi, uint32_t* __restrict__ counters) {
-  H2G_SETPRIO(H2G_PRIO_RED);
-  const uint32_t b = (blockIdx.x * blockDim.x + threadIdx.x) / Q;
-  const uint32_t lane = threadIdx.x & 63;
-  const bool lead = (threadIdx.x % Q) == 0;
-  RED_TS(blockIdx.x == 0, 20);
-  RED_TS(blockIdx.x == gridDim.x - 1, 22);
-  uint32_t bs = 0, be = 0;
-  if (b < nbt) {
-    bs = koff[b];
-    be = koff[b + 1];
-  }
-  // np pieces (0: empty bucket, or written by the accumulation kernel)
-  const uint32_t t0 = bs / L, t1 = be > bs ? (be - 1) / L : t0;
-  const uint32_t np = be > bs && t1 > t0 ? t1 - t0 + 1 : 0;
-  const uint32_t small = Q == 4 ? MSM_SMALL_Q4 : MSM_SMALL;
-  const uint32_t cnt = lead && np > small ? (np + MSM_ITEM - 1) / MSM_ITEM : 0;
-  // every lane of the wave reaches the scan (no early returns above)
-  uint32_t incl = cnt;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t v = __shfl_up(incl, d, 64);
-    if (lane >= (uint32_t)d) incl += v;
-  }
-  const uint32_t wtot = __shfl(incl, 63, 64);
-  const uint64_t mm = __ballot(cnt > 1);
-  uint32_t ibase = 0, mbase = 0;
-  if (lane == 0) {
-    if (wtot) ibase = atomicAdd(&counters[0], wtot);
-    if (mm) mbase = atomicAdd(&counters[1], (uint32_t)__popcll(mm));
-  }
-  ibase = __shfl(ibase, 0, 64);
-  mbase = __shfl(mbase, 0, 64);
-  if (b < nbt && be <= bs && lead) buckets[b] = G1xyzz::identity();  // empty (no fill of buckets[])
-#if H2G_ACC29
-  // a bucket the accumulation wrote whole: its raw accumulator, converted
-  if (b < nbt && be > bs && np == 0 && lead) buckets[b] = acc_to_xyzz(ld_accp(whole + b));
-#endif
-  if (np == 0) return;
-  if (np > small) {
-    if (!cnt) return;  // the quad's other lanes
-    const uint32_t base = ibase + incl - cnt;
-    for (uint32_t i = 0; i < cnt; i++) {
-      MsmBigItem it;
-      it.b = b;
-      it.tb = t0 + i * MSM_ITEM;
-      it.te = min(t0 + (i + 1) * MSM_ITEM, t1 + 1);
-      it.slot = cnt > 1 ? base + i : ~0u;
-      items[base + i] = it;
-    }
-    if (cnt > 1) multi[mbase + (uint32_t)__popcll(mm & ((1ull << lane) - 1))] = make_uint4(b, base, cnt, 0);
-    return;
-  }
-  G1xyzz acc = msm_piece(bnd, t0, t0, bs, L);
-  for (uint32_t t = t0 + 1; t <= t1; t++) {
-    if constexpr (Q == 4) acc = xyzz_add_q4(acc, msm_piece(bnd, t, t0, bs, L));
-    else acc = xyzz_add(acc, msm_piece(bnd, t, t0, bs, L));
-  }
-  if (lead) buckets[b] = acc;
-}
-
-// MSM_GROUP lanes per item (4 items per wave, persistent grid): each lane sums up to
-// 4 strided pieces, then a log2(MSM_GROUP)-level tree in the wave's LDS slice.
-__global__ void __launch_bounds__(MSM_THREADS)
-msm_big_item_kernel(const AccPoint* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t L,
-                    const MsmBigItem* __restrict__ items, const uint32_t* __restrict__ counters,
-                    G1xyzz* __restrict__ partial, G1xyzz* __restrict__ buckets) {
-  H2G_SETPRIO(H2G_PRIO_RED);
-  __shared__ G1xyzz sh[MSM_THREADS];
-  const uint32_t nitems = counters[0];
-  const uint32_t lane = threadIdx.x & 63, g = lane & (MSM_GROUP - 1);
-  G1xyzz* w = sh + (threadIdx.x & ~(MSM_GROUP - 1));
-  constexpr uint32_t per_wave = 64 / MSM_GROUP;
-  const uint32_t stride = gridDim.x * (MSM_THREADS / 64) * per_wave;
-  // uniform trip count per wave (all lanes reach the wave barriers)
-  for (uint32_t q0 = (blockIdx.x * (MSM_THREADS / 64) + (threadIdx.x >> 6)) * per_wave; q0 < nitems;
-       q0 += stride) {
-    const uint32_t q = q0 + lane / MSM_GROUP;
-    G1xyzz acc = G1xyzz::identity();
-    MsmBigItem it = {0, 0, 0, 0};
-    if (q < nitems) {
-      it = items[q];
-      const uint32_t bs = koff[it.b], t0 = bs / L;
-      for (uint32_t t = it.tb + g; t < it.te; t += MSM_GROUP) acc = xyzz_add(acc, msm_piece(bnd, t, t0, bs, L));
-    }
-    w[g] = acc;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 1
-    for (uint32_t h = MSM_GROUP / 2; h > 0; h >>= 1) {
-      if (g < h) w[g] = xyzz_add(w[g], w[g + h]);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (g == 0 && q < nitems) {
-      if (it.slot == ~0u) buckets[it.b] = w[0];
-      else partial[it.slot] = w[0];
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// buckets with several items: the sum of their items' partial sums -- one lane per bucket
-// of at most COMBINE_LANE items (a short sequential sum; skewed inputs -- a lookup's
-// permuted column holds a few hundred distinct values -- make thousands of such buckets,
-// where a wave per bucket left 63 lanes idle: 0.8 ms per keccak-style batch), one
-// wavefront and a tree per larger bucket
-static constexpr uint32_t COMBINE_LANE = 8;
-__global__ void __launch_bounds__(MSM_THREADS)
-msm_big_combine_kernel(const uint4* __restrict__ multi, const uint32_t* __restrict__ counters,
-                       const G1xyzz* __restrict__ partial, G1xyzz* __restrict__ buckets) {
-  H2G_SETPRIO(H2G_PRIO_RED);
-  __shared__ G1xyzz sh[MSM_THREADS];
-  const uint32_t nm = counters[1];
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint32_t q = blockIdx.x * MSM_THREADS + threadIdx.x; q < nm; q += gridDim.x * MSM_THREADS) {
-    const uint4 m = multi[q];  // (bucket, first item, items)
-    if (m.z > COMBINE_LANE) continue;
-    G1xyzz acc = partial[m.y];
-    for (uint32_t i = 1; i < m.z; i++) acc = xyzz_add(acc, partial[m.y + i]);
-    buckets[m.x] = acc;
-  }
-  G1xyzz* w = sh + (threadIdx.x & ~63u);
-  const uint32_t nwaves = gridDim.x * (MSM_THREADS / 64);
-  for (uint32_t q = blockIdx.x * (MSM_THREADS / 64) + (threadIdx.x >> 6); q < nm; q += nwaves) {
-    const uint4 m = multi[q];  // (bucket, first item, items)
-    if (m.z <= COMBINE_LANE) continue;  // uniform across the wave
-    G1xyzz acc = G1xyzz::identity();
-    for (uint32_t i = lane; i < m.z; i += 64) acc = xyzz_add(acc, partial[m.y + i]);
-    w[lane] = acc;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll 1
-    for (uint32_t h = 32; h > 0; h >>= 1) {
-      if (lane < h) w[lane] = xyzz_add(w[lane], w[lane + h]);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (lane == 0) buckets[m.x] = w[0];
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
 // Quad-cooperative XYZZ arithmetic for the latency-bound reduction kernels ----------
 // With one wave per SIMD an XYZZ addition is issue-bound at ~13 us (14 Montgomery
 // products in sequence).  Its products fall into 4 dependent levels (a doubling's 10
@@ -285,9 +98,12 @@ __device__ __forceinline__ Fq quad_bcast(const Fq& a) {
   return r;
 }
 __device__ __forceinline__ Fq quad_sel(int s, const Fq& a, const Fq& b, const Fq& c, const Fq& d) {
+  // masks: a ternary chain here became an indexed load from a stack copy (scratch)
+  const uint32_t m0 = 0u - (uint32_t)(s == 0), m1 = 0u - (uint32_t)(s == 1), m2 = 0u - (uint32_t)(s == 2),
+                 m3 = 0u - (uint32_t)(s == 3);
   Fq r;
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.l[i] = s == 0 ? a.l[i] : (s == 1 ? b.l[i] : (s == 2 ? c.l[i] : d.l[i]));
+  for (int i = 0; i < 8; i++) r.l[i] = (a.l[i] & m0) | (b.l[i] & m1) | (c.l[i] & m2) | (d.l[i] & m3);
   return r;
 }
 
@@ -350,6 +166,329 @@ __device__ G1xyzz xyzz_mul_u32_q4(const G1xyzz& p, uint32_t k) {
   return acc;
 }
 
+#if H2G_ACC29
+// the same quad-cooperative levels in F29 (f29.h; the back-end class, coordinates < 1.2 M)
+template <int K>
+__device__ __forceinline__ F29 quad_bcast29(const F29& a) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++)
+    r.l[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a.l[i], K | (K << 2) | (K << 4) | (K << 6), 0xf, 0xf, false);
+  return r;
+}
+// masks, not a ternary chain: the compiler turns a 4-way select on a lane index into an
+// indexed load from a stack copy of the four operands (scratch traffic in every product)
+__device__ __forceinline__ F29 quad_sel29(int s, const F29& a, const F29& b, const F29& c, const F29& d) {
+  const uint32_t m0 = 0u - (uint32_t)(s == 0), m1 = 0u - (uint32_t)(s == 1), m2 = 0u - (uint32_t)(s == 2),
+                 m3 = 0u - (uint32_t)(s == 3);
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = (a.l[i] & m0) | (b.l[i] & m1) | (c.l[i] & m2) | (d.l[i] & m3);
+  return r;
+}
+// limb-wise select (a ternary on whole structs can become a select of their stack copies)
+__device__ __forceinline__ F29 pick29(bool c, const F29& a, const F29& b) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = c ? a.l[i] : b.l[i];
+  return r;
+}
+// levels {V, X^2}, {W, S, ZZ', M^2}, {ZZZ', M (S - X') - W Y (one merged reduction)}
+__device__ __forceinline__ G1xyzz29 xyzz29_dbl_q4(const G1xyzz29& p) {
+  using P = FqParams;
+  if (xyzz29_is_identity(p)) return p;
+  const int s = threadIdx.x & 3;
+  const F29 U = norm29(add29(p.Y, p.Y));
+  const F29 a1 = pick29(s & 1, p.X, U);
+  F29 m = sqr29<P>(a1);
+  const F29 V = quad_bcast29<0>(m), X2 = quad_bcast29<1>(m);
+  const F29 Mm = norm29(add29(add29(X2, X2), X2));
+  m = mul29<P>(quad_sel29(s, U, p.X, V, Mm), quad_sel29(s, V, V, p.ZZ, Mm));
+  const F29 W = quad_bcast29<0>(m), S = quad_bcast29<1>(m), ZZ3 = quad_bcast29<2>(m), MM = quad_bcast29<3>(m);
+  G1xyzz29 r;
+  r.X = reduce29<P>(norm29(sub29<P, 4, 31>(MM, add29(S, S))));
+  const F29 z = F29{};
+  const bool s0 = s == 0;
+  m = mul29x2<P>(pick29(s0, W, Mm), pick29(s0, p.ZZZ, sub29<P, 4, 29>(S, r.X)), pick29(s0, z, p.Y),
+                 pick29(s0, z, sub29<P, 2, 29>(z, W)));
+  r.ZZZ = quad_bcast29<0>(m);
+  r.Y = quad_bcast29<1>(m);
+  r.ZZ = ZZ3;
+  return r;
+}
+// levels {U1, U2, S1, S2}, {P^2, R^2, ZZ1 ZZ2, ZZZ1 ZZZ2}, {PPP, Q, ZZ'}, {R (Q - X') - S1 PPP, ZZZ'}
+__device__ __forceinline__ G1xyzz29 xyzz29_add_q4(const G1xyzz29& p, const G1xyzz29& q) {
+  using P = FqParams;
+  if (xyzz29_is_identity(q)) return p;
+  if (xyzz29_is_identity(p)) return q;
+  const int s = threadIdx.x & 3;
+  F29 m = mul29<P>(quad_sel29(s, p.X, q.X, p.Y, q.Y), quad_sel29(s, q.ZZ, p.ZZ, q.ZZZ, p.ZZZ));
+  const F29 U1 = quad_bcast29<0>(m), U2 = quad_bcast29<1>(m), S1 = quad_bcast29<2>(m), S2 = quad_bcast29<3>(m);
+  const F29 Pp = norm29(sub29<P, 2, 29>(U2, U1));
+  const F29 R = norm29(sub29<P, 2, 29>(S2, S1));
+  if (is_zero29<P>(Pp)) {
+    if (is_zero29<P>(R)) return xyzz29_dbl_q4(p);
+    return xyzz29_identity();
+  }
+  m = mul29<P>(quad_sel29(s, Pp, R, p.ZZ, p.ZZZ), quad_sel29(s, Pp, R, q.ZZ, q.ZZZ));
+  const F29 PP = quad_bcast29<0>(m), RR = quad_bcast29<1>(m), ZZ12 = quad_bcast29<2>(m), ZZZ12 = quad_bcast29<3>(m);
+  m = mul29<P>(quad_sel29(s, Pp, U1, ZZ12, Pp), PP);
+  const F29 PPP = quad_bcast29<0>(m), Q = quad_bcast29<1>(m);
+  G1xyzz29 r;
+  r.ZZ = quad_bcast29<2>(m);
+  r.X = reduce29<P>(norm29(sub29<P, 4, 31>(RR, add29(add29(PPP, Q), Q))));
+  const F29 z = F29{};
+  const bool s0 = s == 0;
+  m = mul29x2<P>(pick29(s0, R, ZZZ12), pick29(s0, sub29<P, 4, 29>(Q, r.X), PPP), pick29(s0, S1, z),
+                 pick29(s0, sub29<P, 2, 29>(z, PPP), z));
+  r.Y = quad_bcast29<0>(m);
+  r.ZZZ = quad_bcast29<1>(m);
+  return r;
+}
+__device__ G1xyzz29 xyzz29_mul_u32_q4(const G1xyzz29& p, uint32_t k) {
+  if (k == 0) return xyzz29_identity();
+  int top = 31;
+  while (!((k >> top) & 1)) top--;
+  G1xyzz29 acc = p;
+  for (int b = top - 1; b >= 0; b--) {
+    acc = xyzz29_dbl_q4(acc);
+    if ((k >> b) & 1) acc = xyzz29_add_q4(acc, p);
+  }
+  return acc;
+}
+#endif
+
+// The back-end's point type (msm_part.h RedPoint) and its operations: F29 accumulators in
+// the back-end class with H2G_ACC29, canonical G1xyzz otherwise
+__device__ __forceinline__ RedPoint rp_identity() {
+#if H2G_ACC29
+  return xyzz29_identity();
+#else
+  return G1xyzz::identity();
+#endif
+}
+#if H2G_ACC29
+__device__ __forceinline__ RedPoint rp_add(const RedPoint& a, const RedPoint& b) { return xyzz29_add(a, b); }
+__device__ __forceinline__ RedPoint rp_dbl(const RedPoint& a) { return xyzz29_dbl(a); }
+__device__ __forceinline__ RedPoint rp_add_q4(const RedPoint& a, const RedPoint& b) { return xyzz29_add_q4(a, b); }
+__device__ __forceinline__ RedPoint rp_dbl_q4(const RedPoint& a) { return xyzz29_dbl_q4(a); }
+__device__ __forceinline__ RedPoint rp_mul_u32(const RedPoint& a, uint32_t k) { return xyzz29_mul_u32(a, k); }
+__device__ __forceinline__ RedPoint rp_mul_u32_q4(const RedPoint& a, uint32_t k) { return xyzz29_mul_u32_q4(a, k); }
+__device__ __forceinline__ G1xyzz rp_to_xyzz(const RedPoint& a) { return xyzz_from29(a); }
+// an accumulation output (bucket or boundary slot) into the back-end class
+__device__ __forceinline__ RedPoint rp_from_acc(const AccPoint& a) { return xyzz29_reduce(a); }
+#else
+__device__ __forceinline__ RedPoint rp_add(const RedPoint& a, const RedPoint& b) { return xyzz_add(a, b); }
+__device__ __forceinline__ RedPoint rp_dbl(const RedPoint& a) { return xyzz_dbl(a); }
+__device__ __forceinline__ RedPoint rp_add_q4(const RedPoint& a, const RedPoint& b) { return xyzz_add_q4(a, b); }
+__device__ __forceinline__ RedPoint rp_dbl_q4(const RedPoint& a) { return xyzz_dbl_q4(a); }
+__device__ __forceinline__ RedPoint rp_mul_u32(const RedPoint& a, uint32_t k) { return xyzz_mul_u32(a, k); }
+__device__ __forceinline__ RedPoint rp_mul_u32_q4(const RedPoint& a, uint32_t k) { return xyzz_mul_u32_q4(a, k); }
+__device__ __forceinline__ G1xyzz rp_to_xyzz(const RedPoint& a) { return a; }
+__device__ __forceinline__ RedPoint rp_from_acc(const AccPoint& a) { return a; }
+#endif
+// 16-B moves of back-end points in global memory
+__device__ __forceinline__ RedPoint ld_rp(const RedPoint* p) {
+#if H2G_ACC29
+  return ld_acc(p);
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void st_rp(RedPoint* p, const RedPoint& v) {
+#if H2G_ACC29
+  st_acc(p, v);
+#else
+  *p = v;
+#endif
+}
+
+// Buckets spanning chunks, one thread per bucket: the piece in its first chunk t0 is
+// that chunk's last run (slot 1) unless the bucket starts the chunk (slot 0); every
+// later chunk holds it as its first run (slot 0).  Buckets over more than MSM_SMALL
+// chunks are cut into items of at most MSM_ITEM pieces (msm_big_item_kernel), whose
+// partial sums a second pass combines per bucket (msm_big_combine_kernel): the depth
+// stays logarithmic however the scalars concentrate (fixed-base top windows: n / 2^12
+// entries per bucket at c = 22; a column of equal values: n entries per bucket).
+// (H2G_ACC29: the slots hold raw F29 accumulators, brought into the back-end class here)
+__device__ __forceinline__ RedPoint msm_piece(const AccPoint* bnd, uint32_t t, uint32_t t0, uint32_t bs, uint32_t L) {
+  return rp_from_acc(ld_accp(bnd + 2 * (size_t)t + ((t == t0 && bs != t0 * L) ? 1 : 0)));
+}
+
+static constexpr uint32_t MSM_GROUP = 16;            // lanes per item
+static constexpr uint32_t MSM_ITEM = MSM_GROUP * 4;  // pieces per item (4 per lane)
+static constexpr unsigned MSM_BIG_BLOCKS = 512;      // persistent grids below
+
+// big-bucket work item: pieces [tb, te) of bucket b; slot = the item's index into the
+// partial sums when the bucket has several items, ~0u when it is the bucket's only one
+struct MsmBigItem {
+  uint32_t b, tb, te, slot;
+};
+
+// upper bounds of the item lists (sizing): a bucket over np > MSM_SMALL chunks takes
+// ceil(np / MSM_ITEM) items, and the buckets' piece counts sum to < 2 nchunks
+static size_t msm_big_items_cap(size_t nchunks) { return 2 * nchunks / MSM_ITEM + 2 * nchunks / MSM_SMALL + 2; }
+static size_t msm_big_multi_cap(size_t nchunks) { return 2 * nchunks / MSM_ITEM + 2; }
+
+// The item lists are reserved with one atomic per wave (a wave-level scan of the lanes'
+// item counts), not one per bucket.  Q = 4: a quad per bucket (xyzz_add_q4, ~3x less
+// latency per addition) summing up to MSM_SMALL_Q4 pieces itself -- for small bucket
+// sets (<= 2^15), whose buckets span up to ~10 chunks of the minimum chunk length (2^16
+// points at c = 15: 9 pieces each, all of which took the big-item path: fixup 0.30 ->
+// 0.11 ms; at 2^16 buckets the quads' issue cost loses, 0.097 -> 0.142 ms).
+static constexpr uint32_t MSM_SMALL_Q4 = 32;
+
+template <int Q>
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_fixup_kernel(const AccPoint* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t nbt, uint32_t L,
+                 const AccPoint* __restrict__ whole, RedPoint* __restrict__ buckets,
+                 MsmBigItem* __restrict__ items, uint4* __restrict__ multi, uint32_t* __restrict__ counters) {
+  H2G_SETPRIO(H2G_PRIO_RED);
+  const uint32_t b = (blockIdx.x * blockDim.x + threadIdx.x) / Q;
+  const uint32_t lane = threadIdx.x & 63;
+  const bool lead = (threadIdx.x % Q) == 0;
+  RED_TS(blockIdx.x == 0, 20);
+  RED_TS(blockIdx.x == gridDim.x - 1, 22);
+  uint32_t bs = 0, be = 0;
+  if (b < nbt) {
+    bs = koff[b];
+    be = koff[b + 1];
+  }
+  // np pieces (0: empty bucket, or written by the accumulation kernel)
+  const uint32_t t0 = bs / L, t1 = be > bs ? (be - 1) / L : t0;
+  const uint32_t np = be > bs && t1 > t0 ? t1 - t0 + 1 : 0;
+  const uint32_t small = Q == 4 ? MSM_SMALL_Q4 : MSM_SMALL;
+  const uint32_t cnt = lead && np > small ? (np + MSM_ITEM - 1) / MSM_ITEM : 0;
+  // every lane of the wave reaches the scan (no early returns above)
+  uint32_t incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += v;
+  }
+  const uint32_t wtot = __shfl(incl, 63, 64);
+  const uint64_t mm = __ballot(cnt > 1);
+  uint32_t ibase = 0, mbase = 0;
+  if (lane == 0) {
+    if (wtot) ibase = atomicAdd(&counters[0], wtot);
+    if (mm) mbase = atomicAdd(&counters[1], (uint32_t)__popcll(mm));
+  }
+  ibase = __shfl(ibase, 0, 64);
+  mbase = __shfl(mbase, 0, 64);
+  if (b < nbt && be <= bs && lead) st_rp(buckets + b, rp_identity());  // empty (no fill of buckets[])
+#if H2G_ACC29
+  // a bucket the accumulation wrote whole: its raw accumulator, into the back-end class
+  if (b < nbt && be > bs && np == 0 && lead) st_rp(buckets + b, rp_from_acc(ld_accp(whole + b)));
+#endif
+  if (np == 0) return;
+  if (np > small) {
+    if (!cnt) return;  // the quad's other lanes
+    const uint32_t base = ibase + incl - cnt;
+    for (uint32_t i = 0; i < cnt; i++) {
+      MsmBigItem it;
+      it.b = b;
+      it.tb = t0 + i * MSM_ITEM;
+      it.te = min(t0 + (i + 1) * MSM_ITEM, t1 + 1);
+      it.slot = cnt > 1 ? base + i : ~0u;
+      items[base + i] = it;
+    }
+    if (cnt > 1) multi[mbase + (uint32_t)__popcll(mm & ((1ull << lane) - 1))] = make_uint4(b, base, cnt, 0);
+    return;
+  }
+  RedPoint acc = msm_piece(bnd, t0, t0, bs, L);
+  for (uint32_t t = t0 + 1; t <= t1; t++) {
+    if constexpr (Q == 4) acc = rp_add_q4(acc, msm_piece(bnd, t, t0, bs, L));
+    else acc = rp_add(acc, msm_piece(bnd, t, t0, bs, L));
+  }
+  if (lead) st_rp(buckets + b, acc);
+}
+
+// MSM_GROUP lanes per item (4 items per wave, persistent grid): each lane sums up to
+// 4 strided pieces, then a log2(MSM_GROUP)-level tree in the wave's LDS slice.
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_big_item_kernel(const AccPoint* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t L,
+                    const MsmBigItem* __restrict__ items, const uint32_t* __restrict__ counters,
+                    RedPoint* __restrict__ partial, RedPoint* __restrict__ buckets) {
+  H2G_SETPRIO(H2G_PRIO_RED);
+  __shared__ RedPoint sh[MSM_THREADS];
+  const uint32_t nitems = counters[0];
+  const uint32_t lane = threadIdx.x & 63, g = lane & (MSM_GROUP - 1);
+  RedPoint* w = sh + (threadIdx.x & ~(MSM_GROUP - 1));
+  constexpr uint32_t per_wave = 64 / MSM_GROUP;
+  const uint32_t stride = gridDim.x * (MSM_THREADS / 64) * per_wave;
+  // uniform trip count per wave (all lanes reach the wave barriers)
+  for (uint32_t q0 = (blockIdx.x * (MSM_THREADS / 64) + (threadIdx.x >> 6)) * per_wave; q0 < nitems;
+       q0 += stride) {
+    const uint32_t q = q0 + lane / MSM_GROUP;
+    RedPoint acc = rp_identity();
+    MsmBigItem it = {0, 0, 0, 0};
+    if (q < nitems) {
+      it = items[q];
+      const uint32_t bs = koff[it.b], t0 = bs / L;
+      for (uint32_t t = it.tb + g; t < it.te; t += MSM_GROUP) acc = rp_add(acc, msm_piece(bnd, t, t0, bs, L));
+    }
+    w[g] = acc;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+    for (uint32_t h = MSM_GROUP / 2; h > 0; h >>= 1) {
+      if (g < h) w[g] = rp_add(w[g], w[g + h]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (g == 0 && q < nitems) {
+      if (it.slot == ~0u) buckets[it.b] = w[0];
+      else partial[it.slot] = w[0];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// buckets with several items: the sum of their items' partial sums -- one lane per bucket
+// of at most COMBINE_LANE items (a short sequential sum; skewed inputs -- a lookup's
+// permuted column holds a few hundred distinct values -- make thousands of such buckets,
+// where a wave per bucket left 63 lanes idle: 0.8 ms per keccak-style batch), one
+// wavefront and a tree per larger bucket
+static constexpr uint32_t COMBINE_LANE = 8;
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_big_combine_kernel(const uint4* __restrict__ multi, const uint32_t* __restrict__ counters,
+                       const RedPoint* __restrict__ partial, RedPoint* __restrict__ buckets) {
+  H2G_SETPRIO(H2G_PRIO_RED);
+  __shared__ RedPoint sh[MSM_THREADS];
+  const uint32_t nm = counters[1];
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t q = blockIdx.x * MSM_THREADS + threadIdx.x; q < nm; q += gridDim.x * MSM_THREADS) {
+    const uint4 m = multi[q];  // (bucket, first item, items)
+    if (m.z > COMBINE_LANE) continue;
+    RedPoint acc = partial[m.y];
+    for (uint32_t i = 1; i < m.z; i++) acc = rp_add(acc, partial[m.y + i]);
+    buckets[m.x] = acc;
+  }
+  RedPoint* w = sh + (threadIdx.x & ~63u);
+  const uint32_t nwaves = gridDim.x * (MSM_THREADS / 64);
+  for (uint32_t q = blockIdx.x * (MSM_THREADS / 64) + (threadIdx.x >> 6); q < nm; q += nwaves) {
+    const uint4 m = multi[q];  // (bucket, first item, items)
+    if (m.z <= COMBINE_LANE) continue;  // uniform across the wave
+    RedPoint acc = rp_identity();
+    for (uint32_t i = lane; i < m.z; i += 64) acc = rp_add(acc, partial[m.y + i]);
+    w[lane] = acc;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+    for (uint32_t h = 32; h > 0; h >>= 1) {
+      if (lane < h) w[lane] = rp_add(w[lane], w[lane + h]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (lane == 0) buckets[m.x] = w[0];
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // 6a. bucket reduction (default): F = sum_j (j+1) B_j per window, shallow ------------------
 // A serial chain of XYZZ additions costs ~12 us on the GPU at low occupancy, so the
 // reduction minimises dependent depth, not only work:
@@ -364,39 +503,39 @@ __device__ G1xyzz xyzz_mul_u32_q4(const G1xyzz& p, uint32_t k) {
 static constexpr int RG = H2G_MSM_RG;
 
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_rgroup_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, G1xyzz* __restrict__ S,
-                  G1xyzz* __restrict__ R) {
+msm_rgroup_kernel(const RedPoint* __restrict__ B, uint32_t NB, uint32_t m1, RedPoint* __restrict__ S,
+                  RedPoint* __restrict__ R) {
   H2G_SETPRIO(H2G_PRIO_RED);
   const uint32_t w = blockIdx.y;
   const uint32_t g = blockIdx.x * MSM_THREADS + threadIdx.x;
   if (g >= m1) return;
-  const G1xyzz* b = B + (size_t)w * NB;
-  G1xyzz racc = G1xyzz::identity(), sacc = G1xyzz::identity();
+  const RedPoint* b = B + (size_t)w * NB;
+  RedPoint racc = rp_identity(), sacc = rp_identity();
   for (int t = RG - 1; t >= 0; t--) {
     const uint32_t j = g * RG + t;
-    if (j < NB) racc = xyzz_add(racc, b[j]);
-    sacc = xyzz_add(sacc, racc);
+    if (j < NB) racc = rp_add(racc, b[j]);
+    sacc = rp_add(sacc, racc);
   }
   S[(size_t)w * m1 + g] = sacc;
   R[(size_t)w * m1 + g] = racc;
 }
 
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_rscale_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R, uint32_t m1,
-                  G1xyzz* __restrict__ part, uint32_t nblk) {
+msm_rscale_kernel(const RedPoint* __restrict__ S, const RedPoint* __restrict__ R, uint32_t m1,
+                  RedPoint* __restrict__ part, uint32_t nblk) {
   H2G_SETPRIO(H2G_PRIO_RED);
-  __shared__ G1xyzz sh[MSM_THREADS];
+  __shared__ RedPoint sh[MSM_THREADS];
   const uint32_t w = blockIdx.y;
   const uint32_t g = blockIdx.x * MSM_THREADS + threadIdx.x;
-  G1xyzz v = G1xyzz::identity();
+  RedPoint v = rp_identity();
   if (g < m1) {
     v = S[(size_t)w * m1 + g];
-    if (g) v = xyzz_add(v, xyzz_mul_u32(R[(size_t)w * m1 + g], g * RG));
+    if (g) v = rp_add(v, rp_mul_u32(R[(size_t)w * m1 + g], g * RG));
   }
   sh[threadIdx.x] = v;
   __syncthreads();
   for (int h = MSM_THREADS / 2; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h) sh[threadIdx.x] = xyzz_add(sh[threadIdx.x], sh[threadIdx.x + h]);
+    if ((int)threadIdx.x < h) sh[threadIdx.x] = rp_add(sh[threadIdx.x], sh[threadIdx.x + h]);
     __syncthreads();
   }
   if (threadIdx.x == 0) part[(size_t)w * nblk + blockIdx.x] = sh[0];
@@ -406,18 +545,18 @@ msm_rscale_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R, ui
 // 64 groups per block; taken when the groups cannot fill the SIMDs (small MSMs, e.g. the
 // 2^19-2^20-point slabs of a sharded proof), and always for the final tree
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_rgroup_q4_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, G1xyzz* __restrict__ S,
-                     G1xyzz* __restrict__ R) {
+msm_rgroup_q4_kernel(const RedPoint* __restrict__ B, uint32_t NB, uint32_t m1, RedPoint* __restrict__ S,
+                     RedPoint* __restrict__ R) {
   H2G_SETPRIO(H2G_PRIO_RED);
   const uint32_t w = blockIdx.y;
   const uint32_t g = (blockIdx.x * MSM_THREADS + threadIdx.x) >> 2;
   if (g >= m1) return;  // the whole quad
-  const G1xyzz* b = B + (size_t)w * NB;
-  G1xyzz racc = G1xyzz::identity(), sacc = G1xyzz::identity();
+  const RedPoint* b = B + (size_t)w * NB;
+  RedPoint racc = rp_identity(), sacc = rp_identity();
   for (int t = RG - 1; t >= 0; t--) {
     const uint32_t j = g * RG + t;
-    if (j < NB) racc = xyzz_add_q4(racc, b[j]);
-    sacc = xyzz_add_q4(sacc, racc);
+    if (j < NB) racc = rp_add_q4(racc, b[j]);
+    sacc = rp_add_q4(sacc, racc);
   }
   if ((threadIdx.x & 3) == 0) {
     S[(size_t)w * m1 + g] = sacc;
@@ -428,22 +567,22 @@ msm_rgroup_q4_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, G1x
 static constexpr uint32_t Q4_GROUPS = MSM_THREADS / 4;  // quads per block
 
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_rscale_q4_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R, uint32_t m1,
-                     G1xyzz* __restrict__ part, uint32_t nblk) {
+msm_rscale_q4_kernel(const RedPoint* __restrict__ S, const RedPoint* __restrict__ R, uint32_t m1,
+                     RedPoint* __restrict__ part, uint32_t nblk) {
   H2G_SETPRIO(H2G_PRIO_RED);
-  __shared__ G1xyzz sh[Q4_GROUPS];
+  __shared__ RedPoint sh[Q4_GROUPS];
   const uint32_t w = blockIdx.y, qi = threadIdx.x >> 2;
   const uint32_t g = blockIdx.x * Q4_GROUPS + qi;
-  G1xyzz v = G1xyzz::identity();
+  RedPoint v = rp_identity();
   if (g < m1) {
     v = S[(size_t)w * m1 + g];
-    if (g) v = xyzz_add_q4(v, xyzz_mul_u32_q4(R[(size_t)w * m1 + g], g * RG));
+    if (g) v = rp_add_q4(v, rp_mul_u32_q4(R[(size_t)w * m1 + g], g * RG));
   }
   if ((threadIdx.x & 3) == 0) sh[qi] = v;
   __syncthreads();
   for (uint32_t h = Q4_GROUPS / 2; h > 0; h >>= 1) {
     if (qi < h) {  // sh[qi + h] is not written at this level
-      const G1xyzz t = xyzz_add_q4(sh[qi], sh[qi + h]);
+      const RedPoint t = rp_add_q4(sh[qi], sh[qi + h]);
       if ((threadIdx.x & 3) == 0) sh[qi] = t;
     }
     __syncthreads();
@@ -452,22 +591,22 @@ msm_rscale_q4_kernel(const G1xyzz* __restrict__ S, const G1xyzz* __restrict__ R,
 }
 
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_rfinal_q4_kernel(const G1xyzz* __restrict__ part, uint32_t nblk, G1xyzz* __restrict__ windows) {
+msm_rfinal_q4_kernel(const RedPoint* __restrict__ part, uint32_t nblk, G1xyzz* __restrict__ windows) {
   H2G_SETPRIO(H2G_PRIO_RED);
-  __shared__ G1xyzz sh[Q4_GROUPS];
+  __shared__ RedPoint sh[Q4_GROUPS];
   const uint32_t w = blockIdx.x, qi = threadIdx.x >> 2;
-  G1xyzz acc = G1xyzz::identity();
-  for (uint32_t i = qi; i < nblk; i += Q4_GROUPS) acc = xyzz_add_q4(acc, part[(size_t)w * nblk + i]);
+  RedPoint acc = rp_identity();
+  for (uint32_t i = qi; i < nblk; i += Q4_GROUPS) acc = rp_add_q4(acc, part[(size_t)w * nblk + i]);
   if ((threadIdx.x & 3) == 0) sh[qi] = acc;
   __syncthreads();
   for (uint32_t h = Q4_GROUPS / 2; h > 0; h >>= 1) {
     if (qi < h) {
-      const G1xyzz t = xyzz_add_q4(sh[qi], sh[qi + h]);
+      const RedPoint t = rp_add_q4(sh[qi], sh[qi + h]);
       if ((threadIdx.x & 3) == 0) sh[qi] = t;
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) windows[w] = sh[0];
+  if (threadIdx.x == 0) windows[w] = rp_to_xyzz(sh[0]);  // the host finish reads G1xyzz
 }
 
 // 6a'. group weights by bit planes (default when the groups fit 2^16) ----------------------
@@ -483,27 +622,27 @@ msm_rfinal_q4_kernel(const G1xyzz* __restrict__ part, uint32_t nblk, G1xyzz* __r
 // blocks) or quad-cooperative (Q = 4, 64-group blocks) like the group kernels above.
 
 template <int Q>
-__device__ __forceinline__ G1xyzz padd(const G1xyzz& a, const G1xyzz& b) {
-  if constexpr (Q == 4) return xyzz_add_q4(a, b);
-  else return xyzz_add(a, b);
+__device__ __forceinline__ RedPoint padd(const RedPoint& a, const RedPoint& b) {
+  if constexpr (Q == 4) return rp_add_q4(a, b);
+  else return rp_add(a, b);
 }
 template <int Q>
-__device__ __forceinline__ G1xyzz pdbl(const G1xyzz& a) {
-  if constexpr (Q == 4) return xyzz_dbl_q4(a);
-  else return xyzz_dbl(a);
+__device__ __forceinline__ RedPoint pdbl(const RedPoint& a) {
+  if constexpr (Q == 4) return rp_dbl_q4(a);
+  else return rp_dbl(a);
 }
 
 // in LDS: T[0..len) holds one value per element, len = 2^K <= 512.  Afterwards T[0] is the
 // total and T[2^b] (b < K) the sum over the elements with bit b of their index set.
 // `workers`: the block's lanes (Q = 1) or quads (Q = 4); a level's items beyond them loop
 template <int Q>
-__device__ __forceinline__ void plane_fold(G1xyzz* T, int K, uint32_t e, bool lead, uint32_t workers) {
+__device__ __forceinline__ void plane_fold(RedPoint* T, int K, uint32_t e, bool lead, uint32_t workers) {
   for (int k = 0; k < K; k++) {
     const uint32_t per = (uint32_t)k + 1, pairs = (1u << (K - 1 - k));
     for (uint32_t it = e; it < pairs * per; it += workers) {
       const uint32_t j = it / per, i = it % per;
       const uint32_t dst = (j << (k + 1)) + (i == 0 ? 0u : (1u << (i - 1))), src = dst + (1u << k);
-      const G1xyzz v = padd<Q>(T[dst], T[src]);
+      const RedPoint v = padd<Q>(T[dst], T[src]);
       if (lead) T[dst] = v;
     }
     __syncthreads();
@@ -519,20 +658,20 @@ __device__ __forceinline__ void plane_fold(G1xyzz* T, int K, uint32_t e, bool le
 // planes then weight the groups by RGP g, hence e0 = log2(RGP) in the mid kernel
 template <int Q, int LB, int RGP>
 __global__ void __launch_bounds__((1 << LB) * Q)
-msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, uint32_t nblk,
-                        G1xyzz* __restrict__ planes) {
+msm_rgroup_plane_kernel(const RedPoint* __restrict__ B, uint32_t NB, uint32_t m1, uint32_t nblk,
+                        RedPoint* __restrict__ planes) {
   H2G_SETPRIO(H2G_PRIO_RED);
   constexpr uint32_t BPL = 1u << LB;
-  __shared__ G1xyzz shT[BPL], shS[BPL];
+  __shared__ RedPoint shT[BPL], shS[BPL];
   const uint32_t w = blockIdx.y, e = threadIdx.x / Q;
   const bool lead = (threadIdx.x % Q) == 0;
   const uint32_t g = blockIdx.x * BPL + e;
   const size_t ps = (size_t)gridDim.y * nblk;  // stride between planes
-  const G1xyzz* b = B + (size_t)w * NB;
+  const RedPoint* b = B + (size_t)w * NB;
   const bool b0 = blockIdx.x == 0 && blockIdx.y == 0, bl = blockIdx.x == gridDim.x - 1 && blockIdx.y == 0;
   RED_TS(b0, 0);
   RED_TS(bl, 4);
-  G1xyzz racc = G1xyzz::identity(), sacc = G1xyzz::identity();
+  RedPoint racc = rp_identity(), sacc = rp_identity();
   if (g < m1) {
 #pragma unroll
     for (int t = RGP - 1; t >= 0; t--) {
@@ -554,18 +693,18 @@ msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, 
     if (e < pairs * per) {
       const uint32_t j = e / per, i = e % per;
       const uint32_t dst = (j << (k + 1)) + (i == 0 ? 0u : (1u << (i - 1))), src = dst + (1u << k);
-      const G1xyzz v = padd<Q>(shT[dst], shT[src]);
+      const RedPoint v = padd<Q>(shT[dst], shT[src]);
       if (lead) shT[dst] = v;
     } else if (e < pairs * (per + 1)) {
       const uint32_t j = e - pairs * per, dst = j << (k + 1);
-      const G1xyzz v = padd<Q>(shS[dst], shS[dst + (1u << k)]);
+      const RedPoint v = padd<Q>(shS[dst], shS[dst + (1u << k)]);
       if (lead) shS[dst] = v;
     }
     __syncthreads();
   }
   RED_TS(b0, 2);
   if (lead && e < LB + 2) {
-    const G1xyzz v = e == 0 ? shS[0] : (e <= LB ? shT[1u << (e - 1)] : shT[0]);
+    const RedPoint v = e == 0 ? shS[0] : (e <= LB ? shT[1u << (e - 1)] : shT[0]);
     planes[e * ps + (size_t)w * nblk + blockIdx.x] = v;
   }
   RED_TS(b0, 3);
@@ -580,21 +719,21 @@ msm_rgroup_plane_kernel(const G1xyzz* __restrict__ B, uint32_t NB, uint32_t m1, 
 static constexpr int RPK_MAX = 9;  // block-index planes (LDS: 2^RPK_MAX points); above it (c = 22
                                    // sets) MSMs keep the rscale scheme
 __global__ void __launch_bounds__(1024)
-msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, int e0, G1xyzz* __restrict__ mid,
+msm_rplane_mid_kernel(const RedPoint* __restrict__ planes, uint32_t nblk, int LB, int e0, RedPoint* __restrict__ mid,
                       uint32_t* __restrict__ done, G1xyzz* __restrict__ windows) {
   H2G_SETPRIO(H2G_PRIO_RED);
-  __shared__ G1xyzz sh[1 << RPK_MAX];
+  __shared__ RedPoint sh[1 << RPK_MAX];
   __shared__ uint32_t last;
   const uint32_t q = blockIdx.x, w = blockIdx.y, e = threadIdx.x >> 2, WB = gridDim.y;
   const bool lead = (threadIdx.x & 3) == 0;
-  const G1xyzz* in = planes + (size_t)q * WB * nblk + (size_t)w * nblk;
+  const RedPoint* in = planes + (size_t)q * WB * nblk + (size_t)w * nblk;
   int K = 0;
   while ((1u << K) < nblk) K++;
   RED_TS(q == 0 && w == 0, 8);
   RED_TS(q == (uint32_t)LB + 1 && w == 0, 11);
   if (q <= (uint32_t)LB) {
-    G1xyzz acc = G1xyzz::identity();
-    for (uint32_t i = e; i < nblk; i += 256) acc = xyzz_add_q4(acc, in[i]);
+    RedPoint acc = rp_identity();
+    for (uint32_t i = e; i < nblk; i += 256) acc = rp_add_q4(acc, in[i]);
     if (lead) sh[e] = acc;
     __syncthreads();
     RED_TS(q == 0 && w == 0, 9);
@@ -603,7 +742,7 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, 
     while (2 * h0 < (nblk < 256 ? nblk : 256)) h0 <<= 1;
     for (uint32_t h = h0; h > 0; h >>= 1) {
       if (e < h) {
-        const G1xyzz v = xyzz_add_q4(sh[e], sh[e + h]);
+        const RedPoint v = rp_add_q4(sh[e], sh[e + h]);
         if (lead) sh[e] = v;
       }
       __syncthreads();
@@ -612,7 +751,10 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, 
     if (threadIdx.x == 0) mid[(size_t)q * WB + w] = sh[0];
   } else {
     for (uint32_t i = e; i < (1u << K); i += 256)
-      if (lead) sh[i] = i < nblk ? in[i] : G1xyzz::identity();
+      if (lead) {
+        if (i < nblk) sh[i] = ld_rp(in + i);
+        else sh[i] = rp_identity();
+      }
     __syncthreads();
     RED_TS(w == 0, 12);
     plane_fold<4>(sh, K, e, lead, 256);
@@ -630,10 +772,10 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, 
   __threadfence();
   RED_TS(w == 0, 14);
   const uint32_t np = (uint32_t)(LB + K);  // planes (<= 18)
-  G1xyzz x = G1xyzz::identity();
+  RedPoint x = rp_identity();
   if (e < np) {
     x = mid[(size_t)(1 + e) * WB + w];
-    for (int i = 0; i < (int)e + e0; i++) x = xyzz_dbl_q4(x);
+    for (int i = 0; i < (int)e + e0; i++) x = rp_dbl_q4(x);
   } else if (e == np) {
     x = mid[w];
   }
@@ -644,13 +786,13 @@ msm_rplane_mid_kernel(const G1xyzz* __restrict__ planes, uint32_t nblk, int LB, 
   while (2 * h0 < np + 1) h0 <<= 1;
   for (uint32_t h = h0; h > 0; h >>= 1) {
     if (e < h) {
-      const G1xyzz v = xyzz_add_q4(sh[e], sh[e + h]);
+      const RedPoint v = rp_add_q4(sh[e], sh[e + h]);
       if (lead) sh[e] = v;
     }
     __syncthreads();
   }
   RED_TS(w == 0, 16);
-  if (threadIdx.x == 0) windows[w] = sh[0];
+  if (threadIdx.x == 0) windows[w] = rp_to_xyzz(sh[0]);  // the host finish reads G1xyzz
 }
 
 // fixed-base tables: table[w * stride + i] = [2^(offset of window w)] bases[i] -------
@@ -812,13 +954,13 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
                          {&ws->vals_out, total * 4},
                          {&ws->item_bucket, icap * sizeof(MsmBigItem)},    // big-bucket items
                          {&ws->partials, 2 * nchunks * sizeof(AccPoint)},  // boundary slots
-                         {&ws->buckets, (size_t)nbt * sizeof(G1xyzz)},
+                         {&ws->buckets, (size_t)nbt * sizeof(RedPoint)},
                          {&ws->segs, std::max<size_t>((size_t)2 * m1 + nblk, 10 * (size_t)nblk_p + 32) * WB *
-                                         sizeof(G1xyzz)},
+                                         sizeof(RedPoint)},
                          {&ws->windows, (size_t)(W > WB ? W : WB) * sizeof(G1xyzz)},
                          {&ws->result, 16},                              // [0] items, [1] multi-item buckets
                          {&ws->item_off, mcap * sizeof(uint4)},          // multi-item buckets
-                         {&ws->total_items, icap * sizeof(G1xyzz)}};     // items' partial sums
+                         {&ws->total_items, icap * sizeof(RedPoint)}};     // items' partial sums
   for (int b = 0; b < 10; b++)
     if (need[b].bytes > ws->cap[b]) {
       H2G_TRY(grow(need[b].p, need[b].bytes));
@@ -830,13 +972,13 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   uint32_t* counters = (uint32_t*)ws->result;
   MsmBigItem* items = (MsmBigItem*)ws->item_bucket;
   uint4* multi = (uint4*)ws->item_off;
-  G1xyzz* ipart = (G1xyzz*)ws->total_items;
-  G1xyzz* buckets = (G1xyzz*)ws->buckets;
+  RedPoint* ipart = (RedPoint*)ws->total_items;
+  RedPoint* buckets = (RedPoint*)ws->buckets;
   AccPoint* bnd = (AccPoint*)ws->partials;
   AccPoint* whole = H2G_ACC29 ? (AccPoint*)ws->ent : (AccPoint*)buckets;  // the accumulation's whole buckets
-  G1xyzz* rS = (G1xyzz*)ws->segs;  // rscale scheme: group sums, group weights, block sums
-  G1xyzz* rR = rS + (size_t)WB * m1;
-  G1xyzz* rP = rR + (size_t)WB * m1;
+  RedPoint* rS = (RedPoint*)ws->segs;  // rscale scheme: group sums, group weights, block sums
+  RedPoint* rR = rS + (size_t)WB * m1;
+  RedPoint* rP = rR + (size_t)WB * m1;
 
   const uint32_t ncoarse = (uint32_t)(((uint64_t)nbt + (1ull << fb) - 1) >> fb);
   if (ncoarse > COARSE_MAX) return hipErrorInvalidValue;
@@ -912,15 +1054,15 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   hipLaunchKernelGGL(msm_big_item_kernel, dim3(MSM_BIG_BLOCKS), dim3(T), 0, st, (const AccPoint*)bnd,
                      (const uint32_t*)koff, L, (const MsmBigItem*)items, (const uint32_t*)counters, ipart, buckets);
   hipLaunchKernelGGL(msm_big_combine_kernel, dim3(MSM_BIG_BLOCKS / 4), dim3(T), 0, st, (const uint4*)multi,
-                     (const uint32_t*)counters, (const G1xyzz*)ipart, buckets);
+                     (const uint32_t*)counters, (const RedPoint*)ipart, buckets);
   H2G_PHASE(5);
   if (red_plane) {  // bit planes (6a')
-    G1xyzz* planes = (G1xyzz*)ws->segs;
-    G1xyzz* mid = planes + (size_t)(plane_lb + 2) * WB * nblk_p;
+    RedPoint* planes = (RedPoint*)ws->segs;
+    RedPoint* mid = planes + (size_t)(plane_lb + 2) * WB * nblk_p;
     int e0 = 0;
     while ((1 << e0) < rgp) e0++;
     const dim3 pg(nblk_p, (unsigned)WB), pb((unsigned)(plane_q << plane_lb));
-    const G1xyzz* bk = buckets;
+    const RedPoint* bk = buckets;
     if (plane_q == 1)
       hipLaunchKernelGGL((msm_rgroup_plane_kernel<1, 8, kLargeRGP>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
     else if (rgp == 1)
@@ -932,21 +1074,21 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     else
       hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, kSmallLB, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
     hipLaunchKernelGGL(msm_rplane_mid_kernel, dim3((unsigned)plane_lb + 2, (unsigned)WB), dim3(1024), 0, st,
-                       (const G1xyzz*)planes, nblk_p, plane_lb, e0, mid, rdone, (G1xyzz*)ws->windows);
+                       (const RedPoint*)planes, nblk_p, plane_lb, e0, mid, rdone, (G1xyzz*)ws->windows);
   } else {
     if (red_q4)
       hipLaunchKernelGGL(msm_rgroup_q4_kernel, dim3((unsigned)(((size_t)m1 * 4 + T - 1) / T), (unsigned)WB),
-                         dim3(T), 0, st, (const G1xyzz*)buckets, NB, m1, rS, rR);
+                         dim3(T), 0, st, (const RedPoint*)buckets, NB, m1, rS, rR);
     else
       hipLaunchKernelGGL(msm_rgroup_kernel, dim3((m1 + T - 1) / T, (unsigned)WB), dim3(T), 0, st,
-                         (const G1xyzz*)buckets, NB, m1, rS, rR);
+                         (const RedPoint*)buckets, NB, m1, rS, rR);
     if (red_q4)
-      hipLaunchKernelGGL(msm_rscale_q4_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
-                         (const G1xyzz*)rR, m1, rP, nblk);
+      hipLaunchKernelGGL(msm_rscale_q4_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const RedPoint*)rS,
+                         (const RedPoint*)rR, m1, rP, nblk);
     else
-      hipLaunchKernelGGL(msm_rscale_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rS,
-                         (const G1xyzz*)rR, m1, rP, nblk);
-    hipLaunchKernelGGL(msm_rfinal_q4_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const G1xyzz*)rP, nblk,
+      hipLaunchKernelGGL(msm_rscale_kernel, dim3(nblk, (unsigned)WB), dim3(T), 0, st, (const RedPoint*)rS,
+                         (const RedPoint*)rR, m1, rP, nblk);
+    hipLaunchKernelGGL(msm_rfinal_q4_kernel, dim3((unsigned)WB), dim3(T), 0, st, (const RedPoint*)rP, nblk,
                        (G1xyzz*)ws->windows);
   }
   if (d_out && nbatch == 1)

@@ -72,8 +72,10 @@ hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* p
 #endif
 #if H2G_ACC29
 using AccPoint = G1xyzz29;
+using RedPoint = G1xyzz29;  // the fixup's and the reduction's points (f29.h's back-end class)
 #else
 using AccPoint = G1xyzz;
+using RedPoint = G1xyzz;
 #endif
 
 // raw 16-B moves of the accumulators (G1xyzz29 is 9 x 16 B)
