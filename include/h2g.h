@@ -261,7 +261,8 @@ int h2g_pk_set_transcript(uint64_t pk, int kind);
 
 /* advice: num_advice x n Fr; instance: num_instance x n Fr (zero padded), of which
  * instance_lens[i] values enter the transcript.  Writes the proof bytes.
- * advice_on_device != 0: `advice` is a device pointer (inputs resident in HBM). */
+ * advice_on_device != 0: `advice` is a device pointer (inputs resident in HBM), 16-byte
+ * aligned (H2G_ERR_ARG otherwise; the columns are read in 16-byte chunks). */
 int h2g_create_proof(uint64_t params, uint64_t pk, const uint64_t* advice, int advice_on_device,
                      const uint64_t* instance, const uint32_t* instance_lens, const uint8_t rng_seed[32],
                      uint32_t vanishing_threads, uint8_t* proof, size_t proof_cap, size_t* proof_len);

@@ -206,6 +206,12 @@ def test_weighted_slabs_partition_the_points():
     # row pieces: every rank holds an equal piece of one sub-coset -> uniform slabs
     assert D.owner_weights(8, 23, 22) is None and D.owner_weights(8, 20, 18) is None
     assert D.owner_weights(6, 20, 18) == D.owner_weights(6, 20, 18, row_pieces=False) is not None  # 6 % 4 != 0
+    # the library cuts row pieces only with column owners on, SHPLONK and world >= 4
+    # (prove_impl): otherwise the sub-coset owners keep their lighter slabs
+    assert D.owner_weights(8, 23, 22, column_owners=False) == [10, 10] + [100] * 6
+    assert D.owner_weights(8, 23, 22, multiopen="gwc") == [10, 10] + [100] * 6
+    assert D.row_pieces_active(8, 23, 22) and not D.row_pieces_active(2, 23, 22)
+    assert not D.row_pieces_active(8, 23, 22, column_owners=False)
 
 
 def _host_gather_worker(rank, world, port, q):

@@ -124,6 +124,11 @@ def test_errors():
     bad = hc.Witness(wit.advice, wit.instance, np.asarray([circ.n - circ.blinding_factors()], np.uint32))
     with pytest.raises(h2g.H2GError, match="InstanceTooLarge"):
         pk.create_proof(bad)
+    # device advice is read in 16-byte chunks: a misaligned pointer is refused, not misread
+    adv = h2g.DevBuf.from_array(np.ascontiguousarray(wit.advice))
+    with pytest.raises(h2g.H2GError, match="16-byte aligned"):
+        pk.create_proof(wit=wit, advice_dev_ptr=adv.ptr + 8)
+    adv.close()
     pk.close()
     other = h2g.Params(7, *O.srs(7)[1:])
     with pytest.raises(h2g.H2GError, match="params k"):

@@ -153,13 +153,16 @@ def test_spmd_diverged_ranks_refuse_the_proof():
         assert res[nm]["refused_all"], (nm, res[nm])
 
 
-def test_spmd_diverged_witness_refuses_the_proof():
+@pytest.mark.parametrize("world,names", [(2, ["c3_k14", "lookup_k11"]), (4, ["keccak_k12", "c3_k14"])])
+def test_spmd_diverged_witness_refuses_the_proof(world, names):
     """a rank fed another witness (same RNG, same instances): with the commitments and
     evaluations summed from slabs its transcript matches the others', so only the witness
     digest (every advice column at a fixed point, folded into the all-gather payload)
-    makes every rank fail the proof"""
-    res = _run(2, ["c3_k14", "lookup_k11"], mode="spmd", extra=["--diverge-witness"])
-    for nm in ("c3_k14", "lookup_k11"):
+    makes every rank fail the proof.  At 4 ranks the keccak-style advice and lookup stages
+    are wide (each column committed by its owner alone) and the sub-cosets are cut into
+    row pieces: the checksum of the owner's copy is then the only witness evidence"""
+    res = _run(world, names, mode="spmd", extra=["--diverge-witness"])
+    for nm in names:
         assert res[nm]["refused_all"], (nm, res[nm])
 
 

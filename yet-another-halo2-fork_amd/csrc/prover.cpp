@@ -63,10 +63,10 @@ struct Params {
   // sized for the slab length (h2g_params_set_slab)
   size_t slab_lo = 0, slab_hi = 0;
   MsmFixedBase sg, sgl;
-  // windows of the prefix-summed Lagrange basis (params_prefix; built on the first proof
-  // with lookups): 0 not built, 1 built
-  MsmFixedBase fgp;
-  int prefix_state = 0;
+  // windows of the prefix-summed Lagrange basis (params_prefix): built with the first key
+  // that has lookups (keygen, outside any timed proof), for the whole basis (fgp) or -- once
+  // a slab is set -- for the slab only (sgp), as sg / sgl are
+  MsmFixedBase fgp, sgp;
   // the G2 half of ParamsKZG (g2, s_g2 = [s] g2; verifier side, serialised with the params)
   bool has_g2 = false;
   G2Affine g2, s_g2;
@@ -77,17 +77,18 @@ struct Params {
     msm_fixed_base_free(&sg);
     msm_fixed_base_free(&sgl);
     msm_fixed_base_free(&fgp);
+    msm_fixed_base_free(&sgp);
   }
   // windows and table offset serving the base range [off, off + n) of set 0 (g) / 1
   // (g_lagrange) / 2 (the Lagrange prefix sums: full windows only)
   const MsmFixedBase& tables(int set, size_t off, size_t n, size_t* table_off) const {
+    if (sg.table && off >= slab_lo && off + n <= slab_hi && (set != 2 || sgp.table)) {
+      *table_off = off - slab_lo;
+      return set == 0 ? sg : (set == 1 ? sgl : sgp);
+    }
     if (set == 2) {
       *table_off = off;
       return fgp;
-    }
-    if (sg.table && off >= slab_lo && off + n <= slab_hi) {
-      *table_off = off - slab_lo;
-      return set == 0 ? sg : sgl;
     }
     *table_off = off;
     return set == 0 ? fg : fgl;
@@ -99,17 +100,26 @@ struct Params {
 //   sum_i a_i L_i = sum_i (a_i - a_{i+1}) P_i   (a_n = 0; the sum telescopes),
 // the same commitment from scalars that are zero inside every run: the MSM's partition
 // drops zero digits at the source, so its work follows the number of runs, not n.
-int params_prefix(Params& p, hipStream_t st) {
-  if (p.prefix_state) return H2G_OK;
+// Windows of the prefix basis: for all n points (fgp; keygen builds them for keys with
+// lookups, outside any proof) or for the rank's slab (sgp; h2g_params_set_slab builds them
+// with sg / sgl, so a peer that only serves slabs never holds the full-size table).  Both
+// need the prefix points of the whole basis (P_i sums every L_j below i), formed in scratch.
+int params_prefix_build(Params& p, hipStream_t st, size_t lo, size_t hi, MsmFixedBase* out) {
   G1Affine* pre = nullptr;
   HIPCHK(hipMalloc(&pre, p.n * sizeof(G1Affine)));
   hipError_t e = msm_prefix_points(p.gl, p.n, pre, st);
-  if (e == hipSuccess) e = msm_fixed_base_build(pre, p.n, 0, &p.fgp, st);
+  if (e == hipSuccess) e = msm_fixed_base_build(pre + lo, hi - lo, 0, out, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   (void)hipFree(pre);
   HIPCHK(e);
-  p.prefix_state = 1;
   return H2G_OK;
+}
+// before set-2 MSMs over [off, off + n): the slab's windows serve it if they exist, else the
+// full windows, built here if nothing built them earlier (a fallback; normally a no-op)
+int params_prefix(Params& p, hipStream_t st, size_t off = 0, size_t n = 0) {
+  if (p.sgp.table && off >= p.slab_lo && off + n <= p.slab_hi && n > 0) return H2G_OK;
+  if (p.fgp.table) return H2G_OK;
+  return params_prefix_build(p, st, 0, p.n, &p.fgp);
 }
 
 int params_finish(Params& p, hipStream_t st) {
@@ -2203,6 +2213,9 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       CircuitWs& w = *W[ci];
       const uint64_t* from = in.advice ? in.advice[ci] : nullptr;
       bool from_dev = in.adv_dev;
+      // copy_columns reads device advice in 16-byte chunks: refuse what it cannot
+      if (from_dev && from && (reinterpret_cast<uintptr_t>(from) & 15) != 0)
+        return fail(H2G_ERR_ARG, "create_proof: device advice must be 16-byte aligned");
       if (from_src) {
         // the staging outlives proofs: the unusable rows of unblinded columns start at zero
         // as the reference requires (prover.rs:417-421), whatever an earlier proof left there
@@ -2559,17 +2572,25 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     int com_set = SRS_LAGRANGE;
     if (H2G_LOOKUP_PREFIX) {
       RCCHK(params_prefix(prm, st));
-      const size_t need = (size_t)2 * NLT * n;
+      // scalars only for the columns this rank commits (all of them but in a wide stage,
+      // where a column belongs to its owner)
+      size_t owned = 0;
+      for (int i = 0; i < 2 * NLT; i++) owned += own2[i] == g_spmd.rank;
+      const size_t need = std::max<size_t>(owned, 1) * n;
       if (need > pk.lk_diff_len) {
         PALLOC(pk.pool, pk.lk_diff, need);
         pk.lk_diff_len = need;
       }
       PrefixDiff pd{};
       int m = 0;
+      size_t slot = 0;
       for (int i = 0; i < 2 * NLT; i++) {
-        Fr* e = pk.lk_diff + (size_t)i * n;
+        if (own2[i] != g_spmd.rank) {  // another rank's column (wide stage): not read here
+          com_cols[i] = perm_cols[i];
+          continue;
+        }
+        Fr* e = pk.lk_diff + (slot++) * n;
         com_cols[i] = e;
-        if (own2[i] != g_spmd.rank) continue;  // another rank's column (wide stage)
         pd.a[m] = perm_cols[i];
         pd.e[m] = e;
         if (++m == PREFIX_DIFF_MAX) {
@@ -3567,6 +3588,8 @@ int h2g_keygen(uint64_t params, const h2g_circuit* circuit, uint64_t* pk_out) {
   auto pk = std::make_unique<ProvingKey>();
   pk->params = params;
   int rc = keygen_impl(d, *it->second, circuit, *pk);
+  // the lookup commitments' basis (params_prefix) now, not inside the first proof
+  if (!rc && circuit->num_lookups > 0 && H2G_LOOKUP_PREFIX) rc = params_prefix(*it->second, d->stream);
   if (rc) {
     domain_release(&pk->dom);
     return rc;
@@ -4269,11 +4292,14 @@ int h2g_params_set_slab(uint64_t params, uint64_t lo, uint64_t hi) {
   if (lo > hi || hi > prm.n) return fail(H2G_ERR_ARG, "params_set_slab: bad range");
   msm_fixed_base_free(&prm.sg);
   msm_fixed_base_free(&prm.sgl);
+  msm_fixed_base_free(&prm.sgp);
   prm.slab_lo = prm.slab_hi = 0;
   if (hi == lo || (lo == 0 && hi == prm.n)) return H2G_OK;  // none / the full tables
   HIPCHK(msm_fixed_base_build(prm.g + lo, hi - lo, 0, &prm.sg, d->stream));
   HIPCHK(msm_fixed_base_build(prm.gl + lo, hi - lo, 0, &prm.sgl, d->stream));
-  HIPCHK(hipStreamSynchronize(d->stream));
+  // the lookup basis's windows for the slab too (a peer serving set-2 slabs
+  // would otherwise build the full-size table inside its first request)
+  RCCHK(params_prefix_build(prm, d->stream, lo, hi, &prm.sgp));
   prm.slab_lo = lo;
   prm.slab_hi = hi;
   return H2G_OK;
@@ -4289,7 +4315,7 @@ int h2g_params_msm_dev(uint64_t params, int32_t base_set, uint64_t offset, uint6
   if (base_set < SRS_G || base_set > SRS_LAGRANGE_PREFIX || offset > prm.n || n > prm.n - offset || !out_affine ||
       (n && !d_scalars))
     return fail(H2G_ERR_ARG, "params_msm_dev: bad arguments");
-  if (base_set == SRS_LAGRANGE_PREFIX) RCCHK(params_prefix(prm, d->stream));
+  if (base_set == SRS_LAGRANGE_PREFIX) RCCHK(params_prefix(prm, d->stream, offset, n));
   int id = 0;
   size_t toff = 0;
   const MsmFixedBase& tb = prm.tables(base_set, offset, n, &toff);

@@ -42,15 +42,31 @@ def auto_owner_weight(world, extended_k, k):
     return 0.5 if world <= 2 * E else 0.1
 
 
-def owner_weights(world, extended_k, k, owner_weight=None, scale=100, row_pieces=True):
+COLSHARD_MIN_WORLD = 4  # prover.cpp kColshardMinWorld
+
+
+def row_pieces_active(world, extended_k, k, column_owners=True, multiopen="shplonk"):
+    """whether the library cuts sub-cosets into row pieces for this world -- the condition
+    prove_impl uses (prover.cpp: column owners on, SHPLONK, world >= kColshardMinWorld,
+    more ranks than sub-cosets and a multiple of them)"""
+    E = 1 << (extended_k - k)
+    return (column_owners and multiopen == "shplonk" and world >= COLSHARD_MIN_WORLD and world > E
+            and world % E == 0)
+
+
+def owner_weights(world, extended_k, k, owner_weight=None, scale=100, row_pieces=None, column_owners=True,
+                  multiopen="shplonk"):
     """SPMD slab weights that lighten the ranks owning extended-domain sub-cosets: with
     2^(extended_k - k) = E < world sub-cosets, ranks r < E evaluate h on a sub-coset each
     (its n-point coset NTTs, evaluate_h, the h interpolation) on top of their MSM slabs;
     they get weight owner_weight (None: auto_owner_weight), the other ranks 1.  None when
-    every rank owns one, and when world is a multiple of E with row pieces on (the
-    column-owner mode, h2g_spmd_set_column_owners): then every rank evaluates h on a row
-    piece of one sub-coset, the same share of the work"""
+    every rank owns one, and when the library cuts the sub-cosets into row pieces (then
+    every rank evaluates h on a row piece of one sub-coset, the same share of the work).
+    row_pieces None: derived from the library's own condition for the given column-owner
+    mode (h2g_spmd_set_column_owners) and multi-open (row_pieces_active)"""
     E = 1 << (extended_k - k)
+    if row_pieces is None:
+        row_pieces = row_pieces_active(world, extended_k, k, column_owners, multiopen)
     if world <= E or (row_pieces and world % E == 0):
         return None
     if owner_weight is None:
