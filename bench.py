@@ -265,13 +265,6 @@ def pmc_child(args):
 
 
 # ----------------------------------------------------------------------------- roofline
-# VALU peak of one 256-bit Montgomery product: the measured microbenchmark
-# (tools/microbench/modmul_bench.hip) and an issue-rate model: 256 CUs x 4 SIMDs x 32 lanes
-# per cycle x 2.4 GHz of full-rate 32-bit VALU, with the product's 128 v_mad_u64_u32 at
-# quarter rate (4 issue slots each) plus 64 carry ops -> 576 slots per modmul (assumption:
-# the quarter rate of v_mad_u64_u32 is not in the guide's tables)
-MODMUL_PEAK_MICROBENCH = 125e9
-MODMUL_PEAK_ISSUE = 256 * 4 * 32 * 2.4e9 / (128 * 4 + 64)
 # tools/microbench/modmul_bench.hip's FIPS product rate on the round-4 boxes: value_normalised
 # = value x (this box's rate of that same kernel / this), the proof time scaled to such a box
 MODMUL_REF_GPS = 125.0
@@ -306,17 +299,16 @@ def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note
                 "contract asks for (algorithmic 96 B/point), low by construction; `valu` is the bound that applies",
         "valu_modmul_per_s": round(modmul_rate, 1) if modmul_rate else None,
         "valu": {"achieved": round(modmul_rate / 1e9, 2) if modmul_rate else None, "unit": "G modmul/s",
-                 "peak_microbench": MODMUL_PEAK_MICROBENCH / 1e9, "peak_issue_model": round(MODMUL_PEAK_ISSUE / 1e9, 1),
-                 "frac_microbench": round(modmul_rate / MODMUL_PEAK_MICROBENCH, 4) if modmul_rate else None,
-                 "frac_issue_model": round(modmul_rate / MODMUL_PEAK_ISSUE, 4) if modmul_rate else None,
                  "per_point": f"{W} windows x 1 XYZZ mixed add (8M + 2S = {MADD_MODMUL} modmul)",
                  "madds_per_launch": round(madds), "madds": madd_source},
         "window_bits": c,
     }
     if peak_gps and modmul_rate:  # this box's product rate, measured before the timed region
-        out["valu"].update({"peak_box": round(peak_gps, 2), "frac_box": round(modmul_rate / (peak_gps * 1e9), 4),
-                            "peak_box_note": "F29 Montgomery products/s of this GPU (h2g_profile_box_calibrate), "
-                                             "the arithmetic the accumulation runs"})
+        out["valu"].update({"peak": round(peak_gps, 2), "frac": round(modmul_rate / (peak_gps * 1e9), 4),
+                            "peak_note": "this GPU's F29 Montgomery products/s (h2g_profile_box_calibrate: "
+                                         "9 x 29-bit limbs, the arithmetic the accumulation runs), measured "
+                                         "before the timed region; the madd's 10 products counted as full "
+                                         "products (its two squarings and one merged reduction are cheaper)"})
     if traffic:  # PMC bytes per launch, calibrated per access kind (pmc_traffic)
         stream = madds * 4.0  # the u32 bucket-ordered values, read once
         cal = traffic["fetch"] + 0.5 * stream + traffic["write"]
@@ -329,8 +321,7 @@ def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note
         # MSMs on the two MSM streams overlap each other, so a launch's duration counts the
         # chip's time twice while they do: the chip-level rate is the work over the busy time
         agg = calls * madds * MADD_MODMUL / (union["accumulate"] * 1e-3)
-        out["valu"].update({"aggregate": round(agg / 1e9, 2), "aggregate_frac_microbench":
-                            round(agg / MODMUL_PEAK_MICROBENCH, 4),
+        out["valu"].update({"aggregate": round(agg / 1e9, 2),
                             "aggregate_note": "all launches' modmuls / union of their accumulate intervals"})
         out["valu_modmul_per_s_aggregate"] = round(agg, 1)
     return out
@@ -672,7 +663,8 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                                        + ("libh2g RCCL communicators" if native else "torch.distributed p2p")
                                        + " slabs + partials), NTT/evaluate_h/SHPLONK on rank 0" if shard else
                                        f"{world} independent provers")},
-            "roofline": roofline_from_phases(calls, phases, n_local, traffic, traffic_note, union=union),
+            "roofline": roofline_from_phases(calls, phases, n_local, traffic, traffic_note, union=union,
+                                             peak_gps=box["modmul_f29_gps"]),
             "box": box,
             "value_normalised": round(elapsed / (args.steps * (1 if one_proof else world)) *
                                       box["modmul_ref_gps"] / MODMUL_REF_GPS, 4),
