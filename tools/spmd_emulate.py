@@ -39,15 +39,48 @@ COMMIT_TAG = 0x54494d4d4f433248  # prover.cpp kSpmdCommitTag
 G1_GEN_MONT = np.array(_fq_mont_limbs(1) + _fq_mont_limbs(2), dtype=np.uint64)  # (1, 2), Montgomery form
 
 
+def spin(seconds):
+    """busy-wait (time.sleep is too coarse for tens of microseconds)"""
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end:
+        pass
+
+
+class CommModel:
+    """a collective's modelled wire time on the node's xGMI (point-to-point links, every
+    pair of GPUs on its own link): latency + the bytes the busiest link carries / link
+    bandwidth.  All-gather of b bytes per rank: each rank receives b from every peer over
+    a separate link -> b per link; exchange: the largest per-peer block; broadcast: b on
+    each of the root's links.  Charged on the host inside the collective's callback, where
+    the real transport blocks the prover (the exchanges drain the stream first)."""
+
+    def __init__(self, gbs, lat_us):
+        self.bw = gbs * 1e9
+        self.lat = lat_us * 1e-6
+        self.charged = 0.0
+
+    def wait(self, link_bytes):
+        t = self.lat + link_bytes / self.bw
+        self.charged += t
+        spin(t)
+
+
 class FakeCollectives:
     """world x the rank's own payload; the peers' partials are a fixed nonzero point so
-    the sum never degenerates to the identity (which the transcript refuses)"""
+    the sum never degenerates to the identity (which the transcript refuses).  With a
+    CommModel every collective also waits its modelled wire time."""
 
-    def __init__(self, world, rank, gen):
+    def __init__(self, world, rank, gen, model=None):
         self.world, self.rank, self.gen = world, rank, gen
+        self.model = model
         self.calls = self.bcasts = self.exchanges = self.xchg = self.xchg_bytes = 0
 
+    def _wait(self, link_bytes):
+        if self.model is not None:
+            self.model.wait(link_bytes)
+
     def allgather(self, seq, mine):
+        self._wait(np.asarray(mine).nbytes)
         out = np.tile(mine, (self.world, 1))
         for r in range(self.world):
             if r != self.rank:
@@ -57,9 +90,11 @@ class FakeCollectives:
         return out
 
     def bcast(self, d_ptr, nbytes, root):
+        self._wait(nbytes)
         self.bcasts += 1
 
     def allgather_host(self, data):
+        self._wait(len(data))
         self.exchanges += 1
         out = [data] * self.world
         w = np.frombuffer(bytes(data), dtype=np.uint64) if len(data) % 8 == 0 and len(data) >= 16 else None
@@ -72,6 +107,8 @@ class FakeCollectives:
         return out
 
     def exchange(self, d_send, send_bytes, d_recv, recv_bytes):
+        peers = [r for r in range(self.world) if r != self.rank]
+        self._wait(max([int(send_bytes[r]) for r in peers] + [int(recv_bytes[r]) for r in peers] + [0]))
         self.xchg += 1
         self.xchg_bytes += sum(recv_bytes)
 
@@ -92,7 +129,8 @@ def run(args):
     torch.cuda.synchronize()
     n = 1 << k
     ranks = [int(r) for r in args.ranks.split(",")] if args.ranks else list(range(args.world))
-    out = {"k": k, "workload": args.workload, "world": args.world, "ranks": {}}
+    out = {"k": k, "workload": args.workload, "world": args.world, "comm_model": args.comm_model or None,
+           "ranks": {}}
     single = []
     for _ in range(args.warmup):
         pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())
@@ -111,7 +149,11 @@ def run(args):
     for r in ranks:
         if args.world > 1:
             params.set_slab(*D.slab(n, args.world, r, weights=weights))
-        fc = FakeCollectives(args.world, r, gen)
+        model = None
+        if args.comm_model:
+            gbs, lat = (float(x) for x in args.comm_model.split(","))
+            model = CommModel(gbs, lat)
+        fc = FakeCollectives(args.world, r, gen, model)
         h2g.set_spmd_transport(args.world, r, fc.allgather, None if args.no_subcosets else fc.bcast,
                                None if args.no_slabs else fc.allgather_host,
                                None if (args.no_slabs or args.no_subcosets or args.bcast_h) else fc.exchange)
@@ -136,6 +178,8 @@ def run(args):
                            "host_gathers_per_proof": fc.exchanges // (args.warmup + args.steps + 1),
                            "h_exchanges_per_proof": fc.xchg // (args.warmup + args.steps + 1),
                            "h_exchange_recv_bytes": fc.xchg_bytes // max(fc.xchg, 1),
+                           "modelled_comm_ms_per_proof": round(1e3 * model.charged / (args.warmup + args.steps + 1), 3)
+                           if model else None,
                            "stages_ms_synced": {nm: round(ms, 3) for nm, ms in stages}}
         print(json.dumps({"rank": r, **out["ranks"][r]}), flush=True)
     if args.world > 1:
@@ -162,6 +206,9 @@ def main():
     ap.add_argument("--weights", default="", help="SPMD slab weights, comma separated")
     ap.add_argument("--owner-weight", type=float, default=0.0,
                     help="slab weight of the sub-coset owners (h2g_dist.owner_weights), others 1")
+    ap.add_argument("--comm-model", default="",
+                    help="GB/s,us: every collective waits latency + its busiest link's bytes / bandwidth "
+                         "(e.g. 50,40 for xGMI); empty: collectives return at once (compute only)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     res = run(args)

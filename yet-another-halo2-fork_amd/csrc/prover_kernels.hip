@@ -16,6 +16,7 @@
 // elementwise kernels are HBM-streaming grid-stride loops with 16-byte accesses.
 #include <algorithm>
 
+#include "f29.h"
 #include "fr_io.h"
 #include "poly.h"
 #include "prover_kernels.h"
@@ -233,12 +234,175 @@ __global__ void __launch_bounds__(EH_T) evaluate_h_kernel(EvalHArgs a) {
   }
 }
 
+// ---- evaluate_h in F29 (f29.h), H2G_EVALH29 ---------------------------------------------
+// Loads enter as to29 (the element, value < 32 M; a shift, no product), products are
+// f29.h's carry-free REDC, every sum and difference is normalised and reduced (reduce29,
+// < 1.001 M), so no value exceeds 64 M before a reduction and every product input is a
+// load / constant (< 32 M), a product (< 7 M) or a reduced sum: the columns stay far below
+// 2^64.  The row's result leaves with one product against the storage integer of t(X)^-1
+// (REDC(acc 2^261 e * t 2^256) = the storage form of acc * t, no conversion product).
+#ifndef H2G_EVALH29  // A/B builds: 0 = the 8 x 32-bit kernel above
+#define H2G_EVALH29 1
+#endif
+struct EvalH29Scalars {
+  F29 theta, beta, gamma, y, delta_start, delta, one;
+};
+__device__ __forceinline__ F29 eh_ld(const Fr* p) { return to29(ldf(p)); }
+__device__ __forceinline__ F29 eh_add(const F29& a, const F29& b) { return reduce29<FrParams>(norm29(add29(a, b))); }
+__device__ __forceinline__ F29 eh_add3(const F29& a, const F29& b, const F29& c) {
+  return reduce29<FrParams>(norm29(add29(add29(a, b), c)));
+}
+__device__ __forceinline__ F29 eh_sub(const F29& a, const F29& b) {
+  return reduce29<FrParams>(norm29(sub29<FrParams, 64, 29>(a, b)));
+}
+__device__ __forceinline__ F29 eh_mul(const F29& a, const F29& b) { return mul29<FrParams>(a, b); }
+// acc * f + v
+__device__ __forceinline__ F29 eh_horner(const F29& acc, const F29& f, const F29& v) {
+  return eh_add(mul29<FrParams>(acc, f), v);
+}
+
+// slots in LDS limb-major: word (slot, limb, lane) -- nine conflict-free ds_read_b32 per value
+__device__ __forceinline__ F29 eh_slot_ld(const uint32_t* sl, int slot, int lane) {
+  F29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = sl[(slot * 9 + i) * EH_T + lane];
+  return r;
+}
+__device__ __forceinline__ void eh_slot_st(uint32_t* sl, int slot, int lane, const F29& v) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) sl[(slot * 9 + i) * EH_T + lane] = v.l[i];
+}
+
+__device__ __forceinline__ F29 run_prog29(const int4* __restrict__ prog, int2 seg, const Fr* __restrict__ consts,
+                                          const Fr* const* __restrict__ cols, const int* __restrict__ rots,
+                                          uint64_t idx, uint64_t rot_scale, uint64_t mask, const F29& factor,
+                                          uint32_t* sl, int lane, F29 acc) {
+  for (int pc = seg.x; pc < seg.x + seg.y; pc++) {
+    const int4 in = prog[pc];
+    F29 v;
+    switch (in.x) {
+      case G_LOAD: {
+        const uint64_t j = (idx + (uint64_t)((int64_t)rots[in.z] * (int64_t)rot_scale)) & mask;
+        v = eh_ld(cols[in.z] + j);
+        break;
+      }
+      case G_CONST: v = eh_ld(consts + in.z); break;
+      case G_ADD: v = eh_add(eh_slot_ld(sl, in.z, lane), eh_slot_ld(sl, in.w, lane)); break;
+      case G_SUB: v = eh_sub(eh_slot_ld(sl, in.z, lane), eh_slot_ld(sl, in.w, lane)); break;
+      case G_MUL: v = eh_mul(eh_slot_ld(sl, in.z, lane), eh_slot_ld(sl, in.w, lane)); break;
+      case G_NEG: v = eh_sub(F29{}, eh_slot_ld(sl, in.z, lane)); break;
+      default:  // G_HORNER
+        acc = eh_horner(acc, factor, eh_slot_ld(sl, in.z, lane));
+        continue;
+    }
+    eh_slot_st(sl, in.y, lane, v);
+  }
+  return acc;
+}
+
+__global__ void __launch_bounds__(EH_T) evaluate_h29_kernel(EvalHArgs a, EvalH29Scalars k) {
+  extern __shared__ uint4 eh_lds[];
+  uint32_t* sl = reinterpret_cast<uint32_t*>(eh_lds);
+  const int lane = threadIdx.x;
+  const uint64_t emask = a.ext - 1;
+  const uint64_t rend = a.rows ? a.row0 + a.rows : a.ext;
+  const F29 zero29 = F29{};
+  for (uint64_t idx = a.row0 + blockIdx.x * (uint64_t)EH_T + lane; idx < rend; idx += (uint64_t)gridDim.x * EH_T) {
+    F29 acc = run_prog29(a.prog, a.gates, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, k.y, sl, lane,
+                         a.acc_in ? reduce29<FrParams>(to29(ldf(a.acc_in + idx))) : zero29);
+    const F29 l0 = eh_ld(a.l0 + idx);
+    const F29 ll = eh_ld(a.l_last + idx);
+    const F29 la = eh_ld(a.l_active + idx);
+    const uint64_t r_next = (idx + a.rot_scale) & emask;
+    if (a.nsets > 0) {
+      const uint64_t r_last = (idx + (uint64_t)((int64_t)a.last_rot * (int64_t)a.rot_scale)) & emask;
+      // l_0(X) * (1 - z_0(X))
+      acc = eh_horner(acc, k.y, eh_mul(eh_sub(k.one, eh_ld(a.z[0] + idx)), l0));
+      // l_last(X) * (z_l(X)^2 - z_l(X))
+      {
+        const F29 zl = eh_ld(a.z[a.nsets - 1] + idx);
+        acc = eh_horner(acc, k.y, eh_mul(eh_sub(eh_mul(zl, zl), zl), ll));
+      }
+      // l_0(X) * (z_i(X) - z_{i-1}(omega^(last) X))
+      for (int s = 1; s < a.nsets; s++)
+        acc = eh_horner(acc, k.y, eh_mul(eh_sub(eh_ld(a.z[s] + idx), eh_ld(a.z[s - 1] + r_last)), l0));
+      // l_active(X) * (z_i(omega X) prod(p + beta sigma + gamma) - z_i(X) prod(p + delta^j beta X + gamma))
+      const uint64_t pmask = (1ull << a.ext_omega.bits) - 1;
+      F29 cur = eh_mul(k.delta_start, eh_mul(eh_ld(a.ext_omega.lo + (idx & pmask)),
+                                             eh_ld(a.ext_omega.hi + (idx >> a.ext_omega.bits))));
+      for (int s = 0; s < a.nsets; s++) {
+        const int c0 = s * a.chunk_len;
+        const int c1 = c0 + a.chunk_len < a.P ? c0 + a.chunk_len : a.P;
+        F29 left = eh_ld(a.z[s] + r_next);
+        F29 right = eh_ld(a.z[s] + idx);
+        for (int c = c0; c < c1; c++) {
+          const F29 v = eh_ld(a.perm_v[c] + idx);
+          left = eh_mul(left, eh_add3(v, eh_mul(k.beta, eh_ld(a.sigma[c] + idx)), k.gamma));
+          right = eh_mul(right, eh_add3(v, cur, k.gamma));
+          cur = eh_mul(cur, k.delta);
+        }
+        acc = eh_horner(acc, k.y, eh_mul(eh_sub(left, right), la));
+      }
+    }
+    if (a.nlookups + a.nshuffles > 0) {
+      const uint64_t r_prev = (idx - a.rot_scale) & emask;
+      for (int l = 0; l < a.nlookups; l++) {  // evaluation.rs:486-558
+        const EvalLookup lk = a.lookups[l];
+        const F29 ci = run_prog29(a.prog, lk.in, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, k.theta,
+                                  sl, lane, zero29);
+        const F29 ct = run_prog29(a.prog, lk.tab, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, k.theta,
+                                  sl, lane, zero29);
+        const F29 table_value = eh_mul(eh_add(ci, k.beta), eh_add(ct, k.gamma));
+        const F29 z = eh_ld(lk.z + idx), ap = eh_ld(lk.ap + idx), sp = eh_ld(lk.sp + idx);
+        const F29 ams = eh_sub(ap, sp);
+        acc = eh_horner(acc, k.y, eh_mul(eh_sub(k.one, z), l0));
+        acc = eh_horner(acc, k.y, eh_mul(eh_sub(eh_mul(z, z), z), ll));
+        acc = eh_horner(acc, k.y,
+                        eh_mul(eh_sub(eh_mul(eh_mul(eh_ld(lk.z + r_next), eh_add(ap, k.beta)), eh_add(sp, k.gamma)),
+                                      eh_mul(z, table_value)),
+                               la));
+        acc = eh_horner(acc, k.y, eh_mul(ams, l0));
+        acc = eh_horner(acc, k.y, eh_mul(eh_mul(ams, eh_sub(ap, eh_ld(lk.ap + r_prev))), la));
+      }
+      for (int s = 0; s < a.nshuffles; s++) {  // evaluation.rs:561-620
+        const EvalShuffle sh = a.shuffles[s];
+        const F29 ci = eh_add(run_prog29(a.prog, sh.in, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask,
+                                         k.theta, sl, lane, zero29),
+                              k.gamma);
+        const F29 cs = eh_add(run_prog29(a.prog, sh.sh, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask,
+                                         k.theta, sl, lane, zero29),
+                              k.gamma);
+        const F29 z = eh_ld(sh.z + idx);
+        acc = eh_horner(acc, k.y, eh_mul(eh_sub(k.one, z), l0));
+        acc = eh_horner(acc, k.y, eh_mul(eh_sub(eh_mul(z, z), z), ll));
+        acc = eh_horner(acc, k.y, eh_mul(la, eh_sub(eh_mul(eh_ld(sh.z + r_next), cs), eh_mul(z, ci))));
+      }
+    }
+    // out = storage(acc * t(X)^-1) (or storage(acc)): one REDC against the raw storage integer
+    const Fr tv = a.divide ? ldf(a.t_evals + (idx & a.t_mask)) : Fr::one();
+    stf(a.out + idx, pack29<FrParams>(sub_m_if_ge29<FrParams>(mul29<FrParams>(acc, raw29(tv)))));
+  }
+}
+
 hipError_t evaluate_h(const EvalHArgs& a, hipStream_t st) {
   if (a.n_slots > EH_MAX_SLOTS) return hipErrorInvalidValue;
-  const size_t lds = (size_t)(a.n_slots > 0 ? a.n_slots : 1) * EH_T * sizeof(Fr);
   size_t blocks = ((a.rows ? a.rows : a.ext) + EH_T - 1) / EH_T;
   if (blocks > 256 * 32) blocks = 256 * 32;
-  hipLaunchKernelGGL(evaluate_h_kernel, dim3((unsigned)blocks), dim3(EH_T), lds, st, a);
+  if (H2G_EVALH29) {
+    const size_t lds = (size_t)(a.n_slots > 0 ? a.n_slots : 1) * EH_T * 9 * 4;
+    EvalH29Scalars k;
+    k.theta = storage_to_f29<FrParams>(a.theta);
+    k.beta = storage_to_f29<FrParams>(a.beta);
+    k.gamma = storage_to_f29<FrParams>(a.gamma);
+    k.y = storage_to_f29<FrParams>(a.y);
+    k.delta_start = storage_to_f29<FrParams>(a.delta_start);
+    k.delta = storage_to_f29<FrParams>(a.delta);
+    k.one = one29v<FrParams>();
+    hipLaunchKernelGGL(evaluate_h29_kernel, dim3((unsigned)blocks), dim3(EH_T), lds, st, a, k);
+  } else {
+    const size_t lds = (size_t)(a.n_slots > 0 ? a.n_slots : 1) * EH_T * sizeof(Fr);
+    hipLaunchKernelGGL(evaluate_h_kernel, dim3((unsigned)blocks), dim3(EH_T), lds, st, a);
+  }
   return hipGetLastError();
 }
 
