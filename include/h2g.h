@@ -457,8 +457,29 @@ typedef struct {
    * is a local copy), complete on return */
   int (*exchange)(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv, const size_t* recv_bytes);
 } h2g_spmd_transport;
-/* install (world >= 2) or remove (NULL or world <= 1) */
+/* install (world >= 2) or remove (NULL or world <= 1); either removes the overlapped
+ * exchange below */
 int h2g_set_spmd_transport(const h2g_spmd_transport* t);
+/* optional, with exchange: the column-ownership exchanges (h2g_spmd_set_column_owners)
+ * overlap the stages after them instead of draining the stream.  post(ctx, d_send,
+ * send_bytes, d_recv, recv_bytes, stream, done) queues the same all-to-all as exchange()
+ * behind the work queued on `stream` (a hipStream_t) so far and returns without waiting for
+ * the transfer; `done` (a hipEvent_t the library owns) is recorded once the received bytes
+ * are in place.  wait(ctx, done) returns once `done` has been recorded and the transfer has
+ * finished, 0 on success (a transport with a deadline fails it there).  The prover posts a
+ * stage's exchange right after its sub-cosets are packed and waits for all of them after
+ * the vanishing commitments, before h(X) reads them; every rank posts in the same order.
+ * ctx is the transport's.  NULL post: every exchange completes on return. */
+typedef int (*h2g_spmd_exchange_post)(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv,
+                                      const size_t* recv_bytes, void* stream, void* done);
+typedef int (*h2g_spmd_exchange_wait)(void* ctx, void* done);
+int h2g_set_spmd_exchange_async(h2g_spmd_exchange_post post, h2g_spmd_exchange_wait wait);
+/* helpers for host transports of the overlapped exchange (with h2g_event_record):
+ * hipEventSynchronize(done); and, for the one-GPU SPMD emulation (tools/spmd_emulate.py),
+ * `done` recorded `us` microseconds of device time after the work queued on `stream` so
+ * far (a one-thread wait kernel on a side stream stands for a modelled transfer) */
+int h2g_event_wait(void* done);
+int h2g_debug_link_delay(void* stream, void* done, double us);
 /* SPMD slab partition (optional): rank r's slab -- of every commitment MSM and of the
  * multi-open tail's coefficients -- is [P S_r / S, P S_{r+1} / S) with S_r = weights[0] +
  * ... + weights[r - 1] and S their total, instead of [P r / world, P (r + 1) / world).

@@ -79,6 +79,8 @@ def main():
                          "(tests/_oracle.py) on the same SRS, witness and seed")
     ap.add_argument("--one-variant", action="store_true",
                     help="prove each case once (default seed) instead of twice (large cases)")
+    ap.add_argument("--sync-exchange", action="store_true",
+                    help="spmd: every column-ownership exchange completes on return (no overlapped post / wait)")
     ap.add_argument("cases", nargs="+")
     args = ap.parse_args()
     rank = int(os.environ["RANK"])
@@ -173,10 +175,12 @@ def spmd_main(args, rank, world, native):
         want = [_prove(pk, case, **kw) for kw in variants]
         g = None
         if native:
+            if args.sync_exchange:
+                os.environ["H2G_SYNC_EXCHANGE"] = "1"
             h2g.comm_spmd_install(not args.no_subcosets)
         else:
             g = D.SpmdGather(dist, subcosets=not args.no_subcosets, slabs=not args.no_slabs,
-                             h_exchange=not args.bcast_h)
+                             h_exchange=not args.bcast_h, exchange_async=not args.sync_exchange)
             g.install()
         if args.diverge or args.diverge_witness:  # the digest check must catch a diverged rank
             try:

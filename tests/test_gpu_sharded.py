@@ -128,6 +128,10 @@ def test_spmd_row_pieces_four_and_eight_ranks():
     res = _run(8, ["c3_k14", "mixed_k10"], mode="spmd", extra=["--one-variant"])
     for nm in ("c3_k14", "mixed_k10"):
         assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
+    # the column exchanges completing on return instead of overlapped (post / wait before h)
+    res = _run(4, ["c3_k14", "keccak_k12"], mode="spmd", extra=["--one-variant", "--sync-exchange"])
+    for nm in ("c3_k14", "keccak_k12"):
+        assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])
 
 
 def test_spmd_column_owners_off_matches():

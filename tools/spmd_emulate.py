@@ -7,6 +7,9 @@ with (world = N, rank = r) whose collectives return at once -- the all-gather ha
 this rank's own partial and digest for itself and the generator for the peers, broadcasts
 and exchanges are no-ops -- so the rank runs exactly its share of the kernels (its MSM
 slabs, its sub-cosets, its coefficient slabs) and the proof bytes are meaningless.  The
+column-ownership exchanges are posted and waited for as over RCCL (h2g_set_spmd_exchange_async):
+their modelled wire time is a wait kernel on a side stream, so it overlaps the stages after
+them exactly as far as the prover lets it (--sync-exchange: charged on the host instead).  The
 time per proof of the slowest rank plus a communication model (comm_model below) is the
 predicted N-GPU proof time.
 
@@ -58,11 +61,19 @@ class CommModel:
         self.bw = gbs * 1e9
         self.lat = lat_us * 1e-6
         self.charged = 0.0
+        self.by_kind = {}
 
-    def wait(self, link_bytes):
+    def charge(self, link_bytes, kind):
         t = self.lat + link_bytes / self.bw
         self.charged += t
-        spin(t)
+        c = self.by_kind.setdefault(kind, [0.0, 0, 0])
+        c[0] += t
+        c[1] += 1
+        c[2] = max(c[2], int(link_bytes))
+        return t
+
+    def wait(self, link_bytes, kind):
+        spin(self.charge(link_bytes, kind))
 
 
 class FakeCollectives:
@@ -75,12 +86,12 @@ class FakeCollectives:
         self.model = model
         self.calls = self.bcasts = self.exchanges = self.xchg = self.xchg_bytes = 0
 
-    def _wait(self, link_bytes):
+    def _wait(self, link_bytes, kind):
         if self.model is not None:
-            self.model.wait(link_bytes)
+            self.model.wait(link_bytes, kind)
 
     def allgather(self, seq, mine):
-        self._wait(np.asarray(mine).nbytes)
+        self._wait(np.asarray(mine).nbytes, "msm_allgather")
         out = np.tile(mine, (self.world, 1))
         for r in range(self.world):
             if r != self.rank:
@@ -90,11 +101,11 @@ class FakeCollectives:
         return out
 
     def bcast(self, d_ptr, nbytes, root):
-        self._wait(nbytes)
+        self._wait(nbytes, "bcast")
         self.bcasts += 1
 
     def allgather_host(self, data):
-        self._wait(len(data))
+        self._wait(len(data), "host_allgather")
         self.exchanges += 1
         out = [data] * self.world
         w = np.frombuffer(bytes(data), dtype=np.uint64) if len(data) % 8 == 0 and len(data) >= 16 else None
@@ -108,9 +119,25 @@ class FakeCollectives:
 
     def exchange(self, d_send, send_bytes, d_recv, recv_bytes):
         peers = [r for r in range(self.world) if r != self.rank]
-        self._wait(max([int(send_bytes[r]) for r in peers] + [int(recv_bytes[r]) for r in peers] + [0]))
+        self._wait(max([int(send_bytes[r]) for r in peers] + [int(recv_bytes[r]) for r in peers] + [0]), "exchange")
         self.xchg += 1
         self.xchg_bytes += sum(recv_bytes)
+
+    def exchange_post(self, d_send, send_bytes, d_recv, recv_bytes, stream, done):
+        """the overlapped exchange (h2g_set_spmd_exchange_async): its modelled wire time
+        runs on the device, a wait kernel on a side stream behind the packed bytes, as the
+        native transport's RCCL exchange runs on its communicator's stream; the host goes on
+        at once and waits for `done` before h(X)"""
+        peers = [r for r in range(self.world) if r != self.rank]
+        link = max([int(send_bytes[r]) for r in peers] + [int(recv_bytes[r]) for r in peers] + [0])
+        us = 1e6 * self.model.charge(link, "exchange_overlapped") if self.model is not None else 0.0
+        h2g.debug_link_delay(stream, done, us)
+        self.xchg += 1
+        self.xchg_bytes += sum(recv_bytes)
+
+    @staticmethod
+    def exchange_wait(done):
+        h2g.event_wait(done)
 
 
 def run(args):
@@ -130,6 +157,7 @@ def run(args):
     n = 1 << k
     ranks = [int(r) for r in args.ranks.split(",")] if args.ranks else list(range(args.world))
     out = {"k": k, "workload": args.workload, "world": args.world, "comm_model": args.comm_model or None,
+           "column_owners": not args.no_column_owners, "overlapped_exchanges": not args.sync_exchange,
            "ranks": {}}
     single = []
     for _ in range(args.warmup):
@@ -146,6 +174,8 @@ def run(args):
         weights = D.owner_weights(args.world, pk.extended_k, k, args.owner_weight)
     out["weights"] = weights
     h2g.spmd_set_weights(weights)
+    if args.no_column_owners:
+        h2g.spmd_set_column_owners(0)
     for r in ranks:
         if args.world > 1:
             params.set_slab(*D.slab(n, args.world, r, weights=weights))
@@ -154,9 +184,11 @@ def run(args):
             gbs, lat = (float(x) for x in args.comm_model.split(","))
             model = CommModel(gbs, lat)
         fc = FakeCollectives(args.world, r, gen, model)
+        xchg = not (args.no_slabs or args.no_subcosets or args.bcast_h)
         h2g.set_spmd_transport(args.world, r, fc.allgather, None if args.no_subcosets else fc.bcast,
-                               None if args.no_slabs else fc.allgather_host,
-                               None if (args.no_slabs or args.no_subcosets or args.bcast_h) else fc.exchange)
+                               None if args.no_slabs else fc.allgather_host, fc.exchange if xchg else None)
+        if xchg and not args.sync_exchange:
+            h2g.set_spmd_exchange_async(fc.exchange_post, fc.exchange_wait)
         try:
             for _ in range(args.warmup):
                 pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())
@@ -180,6 +212,10 @@ def run(args):
                            "h_exchange_recv_bytes": fc.xchg_bytes // max(fc.xchg, 1),
                            "modelled_comm_ms_per_proof": round(1e3 * model.charged / (args.warmup + args.steps + 1), 3)
                            if model else None,
+                           "modelled_comm_by_kind": {kd: {"ms_per_proof": round(1e3 * v[0] / (args.warmup + args.steps + 1), 3),
+                                                          "calls_per_proof": v[1] // (args.warmup + args.steps + 1),
+                                                          "max_link_mb": round(v[2] / 1e6, 2)}
+                                                     for kd, v in model.by_kind.items()} if model else None,
                            "stages_ms_synced": {nm: round(ms, 3) for nm, ms in stages}}
         print(json.dumps({"rank": r, **out["ranks"][r]}), flush=True)
     if args.world > 1:
@@ -206,6 +242,10 @@ def main():
     ap.add_argument("--weights", default="", help="SPMD slab weights, comma separated")
     ap.add_argument("--owner-weight", type=float, default=0.0,
                     help="slab weight of the sub-coset owners (h2g_dist.owner_weights), others 1")
+    ap.add_argument("--no-column-owners", action="store_true",
+                    help="h2g_spmd_set_column_owners(0): wide stages keep point slabs, no row pieces")
+    ap.add_argument("--sync-exchange", action="store_true",
+                    help="the column exchanges complete on return (charged on the host) instead of overlapped")
     ap.add_argument("--comm-model", default="",
                     help="GB/s,us: every collective waits latency + its busiest link's bytes / bandwidth "
                          "(e.g. 50,40 for xGMI); empty: collectives return at once (compute only)")

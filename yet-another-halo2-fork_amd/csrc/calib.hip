@@ -116,6 +116,33 @@ __global__ void calib_fill(Fq* x, size_t n) {
   x[i] = v;
 }
 
+// the one-GPU SPMD emulation's stand-in for a transfer (h2g_debug_link_delay): one thread
+// waits `ticks` of the 100 MHz real-time counter, napping between reads; the count is
+// capped by the host, so every launch ends
+__global__ void link_delay_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+}
+
+// `done` recorded `us` microseconds of device time after the work queued on `after` so far:
+// the wait kernel runs on a side stream of its own (the modelled transfer overlaps the
+// prover's stream as an RCCL exchange on its communicator's stream would)
+hipError_t link_delay(hipStream_t after, hipEvent_t done, double us) {
+  static hipStream_t side = nullptr;
+  static hipEvent_t ready = nullptr;
+  hipError_t e = hipSuccess;
+  if (!side) e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking);
+  if (e == hipSuccess && !ready) e = hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(ready, after);
+  if (e == hipSuccess) e = hipStreamWaitEvent(side, ready, 0);
+  if (e != hipSuccess) return e;
+  const double capped = us < 0 ? 0 : (us > 10e6 ? 10e6 : us);  // at most 10 s
+  hipLaunchKernelGGL(link_delay_kernel, dim3(1), dim3(1), 0, side, (unsigned long long)(capped * 100.0));
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipEventRecord(done, side);
+  return e;
+}
+
 }  // namespace h2g
 
 using namespace h2g;

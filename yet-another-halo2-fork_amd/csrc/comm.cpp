@@ -65,6 +65,10 @@ struct Comm {
   // SPMD host all-gather (multi-open tail): pinned / device staging, world x bytes + bytes
   void *h_hg = nullptr, *d_hg = nullptr;
   size_t hg_cap = 0;
+  // overlapped exchanges (comm_exchange_post): on the second communicator and its stream,
+  // so the stages' all-gathers on the first do not queue behind them; xready gates them
+  // on the prover's stream
+  hipEvent_t xready = nullptr;
 };
 Comm* g_comm = nullptr;
 
@@ -252,6 +256,7 @@ int comm_destroy() {
   if (c->d_hg) (void)hipFree(c->d_hg);
   for (uint64_t* p : {c->d_ag_in, c->d_ag_out})
     if (p) (void)hipFree(p);
+  if (c->xready) (void)hipEventDestroy(c->xready);
   if (c->stx) (void)hipStreamDestroy(c->stx);
   if (c->srx) (void)hipStreamDestroy(c->srx);
   delete c;
@@ -325,33 +330,59 @@ int comm_allgather_host(void* ctx, const void* in, size_t bytes, void* out) {
   return H2G_OK;
 }
 
-// h(X)'s coefficient slabs from the sub-coset owners: one group of sends and receives on
-// the slab communicator, the rank's own block a device copy
-int comm_exchange(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv, const size_t* recv_bytes) {
-  Comm* c = usable(ctx);
-  if (!c) return fail(H2G_ERR_STATE, "comm: no (live) communicator for the SPMD exchange");
-  HIPCHK(hipSetDevice(c->device));
+// one group of sends and receives on `comm` / `st`, the rank's own block a device copy
+int enqueue_exchange(Comm* c, ncclComm_t comm, hipStream_t st, const void* d_send, const size_t* send_bytes,
+                     void* d_recv, const size_t* recv_bytes) {
   const int W = c->world;
+  if (send_bytes[c->rank] != recv_bytes[c->rank]) return fail(H2G_ERR_ARG, "comm_exchange: own block sizes differ");
   size_t so = 0, ro = 0;
-  NCCLQ(c, c->tx, ncclGroupStart());
+  NCCLQ(c, comm, ncclGroupStart());
   for (int p = 0; p < W; p++) {
     const uint8_t* sp = static_cast<const uint8_t*>(d_send) + so;
     uint8_t* rp = static_cast<uint8_t*>(d_recv) + ro;
     if (p == c->rank) {
-      if (send_bytes[p] != recv_bytes[p]) {
-        (void)ncclGroupEnd();
-        return fail(H2G_ERR_ARG, "comm_exchange: own block sizes differ");
-      }
-      if (send_bytes[p]) HIPCHK(hipMemcpyAsync(rp, sp, send_bytes[p], hipMemcpyDeviceToDevice, c->stx));
+      if (send_bytes[p]) HIPCHK(hipMemcpyAsync(rp, sp, send_bytes[p], hipMemcpyDeviceToDevice, st));
     } else {
-      if (send_bytes[p]) NCCLQ(c, c->tx, ncclSend(sp, send_bytes[p], ncclUint8, p, c->tx, c->stx));
-      if (recv_bytes[p]) NCCLQ(c, c->tx, ncclRecv(rp, recv_bytes[p], ncclUint8, p, c->tx, c->stx));
+      if (send_bytes[p]) NCCLQ(c, comm, ncclSend(sp, send_bytes[p], ncclUint8, p, comm, st));
+      if (recv_bytes[p]) NCCLQ(c, comm, ncclRecv(rp, recv_bytes[p], ncclUint8, p, comm, st));
     }
     so += send_bytes[p];
     ro += recv_bytes[p];
   }
-  NCCLQ(c, c->tx, ncclGroupEnd());
+  NCCLQ(c, comm, ncclGroupEnd());
+  return H2G_OK;
+}
+
+// h(X)'s coefficient slabs from the sub-coset owners (and the exchanges the prover waits
+// for at once): on the slab communicator, complete on return
+int comm_exchange(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv, const size_t* recv_bytes) {
+  Comm* c = usable(ctx);
+  if (!c) return fail(H2G_ERR_STATE, "comm: no (live) communicator for the SPMD exchange");
+  HIPCHK(hipSetDevice(c->device));
+  RCCHK(enqueue_exchange(c, c->tx, c->stx, d_send, send_bytes, d_recv, recv_bytes));
   return wait_stream(c, c->stx, "SPMD exchange", g_timeout_s);
+}
+
+// the column-ownership exchanges, overlapped with the stages after them: queued on the
+// second communicator behind the prover's stream, `done` recorded behind them; the host
+// does not wait here (comm_exchange_wait does, against the deadline)
+int comm_exchange_post(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv, const size_t* recv_bytes,
+                       void* stream, void* done) {
+  Comm* c = usable(ctx);
+  if (!c) return fail(H2G_ERR_STATE, "comm: no (live) communicator for the SPMD exchange");
+  HIPCHK(hipSetDevice(c->device));
+  if (!c->xready) HIPCHK(hipEventCreateWithFlags(&c->xready, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(c->xready, static_cast<hipStream_t>(stream)));
+  HIPCHK(hipStreamWaitEvent(c->srx, c->xready, 0));
+  RCCHK(enqueue_exchange(c, c->rx, c->srx, d_send, send_bytes, d_recv, recv_bytes));
+  HIPCHK(hipEventRecord(static_cast<hipEvent_t>(done), c->srx));
+  return H2G_OK;
+}
+
+int comm_exchange_wait(void* ctx, void* done) {
+  Comm* c = usable(ctx);
+  if (!c) return fail(H2G_ERR_STATE, "comm: no (live) communicator for the SPMD exchange");
+  return wait_event(c, static_cast<hipEvent_t>(done), "SPMD exchange (overlapped)");
 }
 
 int comm_bcast(void* ctx, void* d_buf, size_t bytes, int root) {

@@ -51,6 +51,9 @@ int comm_allgather_partial(void* ctx, uint64_t seq, const uint64_t in[H2G_SPMD_W
 int comm_allgather_host(void* ctx, const void* in, size_t bytes, void* out);
 // SPMD: all-to-all of device bytes with per-peer counts (grouped send / receive)
 int comm_exchange(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv, const size_t* recv_bytes);
+int comm_exchange_post(void* ctx, const void* d_send, const size_t* send_bytes, void* d_recv, const size_t* recv_bytes,
+                       void* stream, void* done);
+int comm_exchange_wait(void* ctx, void* done);
 // in-place broadcast of device memory from `root` (the sub-coset h evaluations)
 int comm_bcast(void* ctx, void* d_buf, size_t bytes, int root);
 

@@ -21,6 +21,7 @@
 #include <chrono>
 #include <functional>
 #include <set>
+#include <thread>
 
 #include "comm.h"
 #include "poly.h"
@@ -30,6 +31,10 @@
 #include "runtime.h"
 #include "srs.h"
 #include "transcript.h"
+
+namespace h2g {
+hipError_t link_delay(hipStream_t after, hipEvent_t done, double us);  // calib.hip
+}
 
 using namespace h2g;
 using namespace h2g::rt;
@@ -283,6 +288,18 @@ struct ProvingKey {
   CopySeg* d_segs = nullptr;
   size_t d_segs_len = 0;
   std::vector<CopySeg> h_segs[2];
+  // overlapped column-ownership exchanges (h2g_set_spmd_exchange_async), in posting order:
+  // each its own send / receive staging (grow-only, reused by the same position in the
+  // next proof), completion event and unpack list, live from its post until xp_flush
+  struct XPending {
+    Fr *send = nullptr, *recv = nullptr;
+    size_t send_len = 0, recv_len = 0;
+    hipEvent_t done = nullptr;
+    std::vector<CopySeg> unpack;
+    bool live = false;
+  };
+  std::vector<XPending> xp;
+  size_t xp_used = 0;
   uint32_t* d_seeds = nullptr;
   uint64_t* d_offsets = nullptr;
   int max_chunks = 0;
@@ -393,6 +410,9 @@ uint64_t g_shard_seq = 0;
 // SPMD sharding (h2g_set_spmd_transport): every rank proves, rank r computes slab r
 h2g_spmd_transport g_spmd{nullptr, 1, 0, nullptr, nullptr};
 uint64_t g_spmd_seq = 0;
+// overlapped exchanges (h2g_set_spmd_exchange_async); NULL post: exchanges complete on return
+h2g_spmd_exchange_post g_xpost = nullptr;
+h2g_spmd_exchange_wait g_xwait = nullptr;
 // time, calls and bytes (sent + received) inside the transport, per collective kind
 // (h2g_spmd_stats): 0 MSM all-gathers, 1 host all-gathers, 2 exchanges, 3 broadcasts
 struct SpmdStats {
@@ -1449,14 +1469,33 @@ int colshard_distribute(Device* d, ProvingKey& pk, const std::vector<const Fr*>&
   }
   size_t rtot = 0;
   for (int r = 0; r < W; r++) rtot += rb[r] / sizeof(Fr);
-  if (soff[W] > pk.x_send_len) {
-    PALLOC(pk.pool, pk.x_send, soff[W]);
-    pk.x_send_len = soff[W];
+  // overlapped: this exchange's own staging (the next stage packs while it is in flight);
+  // otherwise the shared one
+  ProvingKey::XPending* xp = nullptr;
+  if (g_xpost) {
+    if (pk.xp_used == pk.xp.size()) pk.xp.emplace_back();
+    xp = &pk.xp[pk.xp_used];
+    if (soff[W] > xp->send_len) {
+      PALLOC(pk.pool, xp->send, soff[W]);
+      xp->send_len = soff[W];
+    }
+    if (rtot > xp->recv_len) {
+      PALLOC(pk.pool, xp->recv, rtot);
+      xp->recv_len = rtot;
+    }
+    if (!xp->done) HIPCHK(hipEventCreateWithFlags(&xp->done, hipEventDisableTiming));
+  } else {
+    if (soff[W] > pk.x_send_len) {
+      PALLOC(pk.pool, pk.x_send, soff[W]);
+      pk.x_send_len = soff[W];
+    }
+    if (rtot > pk.x_recv_len) {
+      PALLOC(pk.pool, pk.x_recv, rtot);
+      pk.x_recv_len = rtot;
+    }
   }
-  if (rtot > pk.x_recv_len) {
-    PALLOC(pk.pool, pk.x_recv, rtot);
-    pk.x_recv_len = rtot;
-  }
+  Fr* const xs = xp ? xp->send : pk.x_send;
+  Fr* const xr = xp ? xp->recv : pk.x_recv;
   const size_t scr = mine.size() * (size_t)E * n;
   if (scr > pk.cs_scr_len) {
     PALLOC(pk.pool, pk.cs_scr, scr);
@@ -1513,20 +1552,16 @@ int colshard_distribute(Device* d, ProvingKey& pk, const std::vector<const Fr*>&
         const Fr* src = pk.cs_scr + (q * E + pc.t) * n;
         runs(pc, [&](uint64_t row, uint64_t at, uint64_t cnt) {
           if (r == me) pack.push_back(CopySeg{src + row, coset[i] + (size_t)pc.slot * n + row, cnt});
-          else pack.push_back(CopySeg{src + row, pk.x_send + pos + at, cnt});
+          else pack.push_back(CopySeg{src + row, xs + pos + at, cnt});
         });
         if (r != me) pos += pc.len;
       }
       if (r == me) continue;
       const size_t cnt = slabs[r].hi1 - slabs[r].lo;
-      if (cnt) pack.push_back(CopySeg{poly[i] + slabs[r].lo, pk.x_send + pos, cnt});
+      if (cnt) pack.push_back(CopySeg{poly[i] + slabs[r].lo, xs + pos, cnt});
       pos += cnt;
     }
   }
-  RCCHK(run_segs(pack));
-  HIPCHK(hipStreamSynchronize(st));
-  if (spmd_exchange(pk.x_send, sb.data(), pk.x_recv, rb.data()) != 0)
-    return fail(H2G_ERR_STATE, "spmd transport: exchange of column sub-cosets failed");
   size_t off = 0;  // unpack, source by source
   const size_t mycnt = slabs[me].hi1 - slabs[me].lo;
   for (int o = 0; o < W; o++) {
@@ -1535,16 +1570,75 @@ int colshard_distribute(Device* d, ProvingKey& pk, const std::vector<const Fr*>&
       if (owner[i] != o) continue;
       for (const RowPiece& pc : pcs[me]) {
         runs(pc, [&](uint64_t row, uint64_t at, uint64_t cnt) {
-          unpack.push_back(CopySeg{pk.x_recv + off + at, coset[i] + (size_t)pc.slot * n + row, cnt});
+          unpack.push_back(CopySeg{xr + off + at, coset[i] + (size_t)pc.slot * n + row, cnt});
         });
         off += pc.len;
       }
-      if (mycnt) unpack.push_back(CopySeg{pk.x_recv + off, poly[i] + slabs[me].lo, mycnt});
+      if (mycnt) unpack.push_back(CopySeg{xr + off, poly[i] + slabs[me].lo, mycnt});
       off += mycnt;
     }
   }
+  RCCHK(run_segs(pack));
+  if (xp) {  // behind the pack on the stream; the receiver's rows land before h(X) (xp_flush)
+    uint64_t bytes = 0;
+    for (int r = 0; r < W; r++) bytes += sb[r] + rb[r];
+    if (spmd_timed(2, bytes, [&] { return g_xpost(g_spmd.ctx, xs, sb.data(), xr, rb.data(), st, xp->done); }) != 0)
+      return fail(H2G_ERR_STATE, "spmd transport: exchange of column sub-cosets failed (post)");
+    xp->unpack.swap(unpack);
+    xp->live = true;
+    pk.xp_used++;
+    return H2G_OK;
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  if (spmd_exchange(xs, sb.data(), xr, rb.data()) != 0)
+    return fail(H2G_ERR_STATE, "spmd transport: exchange of column sub-cosets failed");
   RCCHK(run_segs(unpack));
   return H2G_OK;
+}
+
+// the overlapped exchanges' received rows into their columns: every posted exchange waited
+// for (the transport's deadline applies), the stream made to wait for its completion
+// event, its unpack list queued -- before anything reads the cosets or the slabs
+int xp_flush(ProvingKey& pk, hipStream_t st) {
+  for (size_t k = 0; k < pk.xp_used; k++) {
+    ProvingKey::XPending& x = pk.xp[k];
+    if (!x.live) continue;
+    x.live = false;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = g_xwait ? g_xwait(g_spmd.ctx, x.done) : (int)hipEventSynchronize(x.done);
+    g_spmd_stats.ms[2] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (rc != 0) {
+      pk.xp_used = 0;
+      return fail(H2G_ERR_STATE, "spmd transport: exchange of column sub-cosets failed (wait)");
+    }
+    HIPCHK(hipStreamWaitEvent(st, x.done, 0));
+    if (!x.unpack.empty()) {
+      if (x.unpack.size() > pk.d_segs_len) {
+        PALLOC(pk.pool, pk.d_segs, x.unpack.size());
+        pk.d_segs_len = x.unpack.size();
+      }
+      uint64_t mx = 0;
+      for (const CopySeg& g : x.unpack) mx = std::max<uint64_t>(mx, g.len);
+      HIPCHK(pk_upload(pk, pk.d_segs, x.unpack.data(), x.unpack.size() * sizeof(CopySeg), st));
+      HIPCHK(copy_segments(pk.d_segs, (int)x.unpack.size(), mx, st));
+    }
+  }
+  pk.xp_used = 0;
+  return H2G_OK;
+}
+
+// a failed proof's exchanges still in flight: wait for them (bounded) before their staging
+// is reused or freed
+void xp_drain(ProvingKey& pk) {
+  for (ProvingKey::XPending& x : pk.xp) {
+    if (!x.live) continue;
+    x.live = false;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hipEventQuery(x.done) == hipErrorNotReady &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10))
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  pk.xp_used = 0;
 }
 
 // pieces: the leader of sub-coset t (rank t) receives the h rows of the sub-coset's other
@@ -2038,6 +2132,7 @@ struct ProveIn {
 
 int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::vector<uint8_t>* proof) {
   hipStream_t st = d->stream;
+  xp_drain(pk);  // a failed proof's overlapped exchanges
   RCCHK(pk_upload_arm(pk, st));
   const size_t n = pk.n, ext = pk.ext;
   const int bf = pk.bf;
@@ -2922,6 +3017,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     tl.push_back(&van_tk);
     RCCHK(collect_write(tl));
   }
+  RCCHK(xp_flush(pk, st));  // the overlapped exchanges' rows, before h(X) reads them
   clk.mark("perm+vanishing commits, cosets");
   const Fr y = tr.squeeze();
   // ---- evaluate_h (evaluation.rs:317-620): one launch per circuit, each continuing the
@@ -4038,6 +4134,9 @@ int h2g_pk_free(uint64_t pk) {
   auto it = g_pks.find(pk);
   if (it == g_pks.end()) return fail(H2G_ERR_HANDLE, "unknown proving key");
   (void)hipStreamSynchronize(d->stream);
+  xp_drain(*it->second);
+  for (auto& x : it->second->xp)
+    if (x.done) (void)hipEventDestroy(x.done);
   domain_release(&it->second->dom);
   if (it->second->lk_cnt) (void)hipHostFree(it->second->lk_cnt);
   if (it->second->lk_or_h) (void)hipHostFree(it->second->lk_or_h);
@@ -4269,8 +4368,31 @@ int h2g_spmd_set_column_owners(int on) {
   return H2G_OK;
 }
 
+int h2g_set_spmd_exchange_async(h2g_spmd_exchange_post post, h2g_spmd_exchange_wait wait) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (post && (!g_spmd.exchange || g_spmd.world < 2))
+    return fail(H2G_ERR_STATE, "set_spmd_exchange_async: install an SPMD transport with an exchange first");
+  g_xpost = post;
+  g_xwait = post ? wait : nullptr;
+  return H2G_OK;
+}
+
+int h2g_event_wait(void* done) {
+  if (!done) return fail(H2G_ERR_ARG, "event_wait: null event");
+  HIPCHK(hipEventSynchronize(static_cast<hipEvent_t>(done)));
+  return H2G_OK;
+}
+
+int h2g_debug_link_delay(void* stream, void* done, double us) {
+  if (!done) return fail(H2G_ERR_ARG, "debug_link_delay: null event");
+  HIPCHK(link_delay(static_cast<hipStream_t>(stream), static_cast<hipEvent_t>(done), us));
+  return H2G_OK;
+}
+
 int h2g_set_spmd_transport(const h2g_spmd_transport* t) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
+  g_xpost = nullptr;
+  g_xwait = nullptr;
   if (t && t->world > 1) {
     if (!t->allgather || t->world > 4096 || t->rank < 0 || t->rank >= t->world)
       return fail(H2G_ERR_ARG, "set_spmd_transport: bad transport");
@@ -4376,6 +4498,7 @@ int h2g_comm_destroy(void) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (g_shard.launch == comm_launch) g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr, nullptr};
+  if (g_xpost == comm_exchange_post) g_xpost = nullptr, g_xwait = nullptr;
   return comm_destroy();
 }
 
@@ -4385,6 +4508,9 @@ int h2g_comm_spmd_install(int split_subcosets) {
   g_spmd = h2g_spmd_transport{comm_spmd_ctx(), comm_world(), comm_rank(), comm_allgather_partial,
                               split_subcosets ? comm_bcast : nullptr, comm_allgather_host,
                               split_subcosets ? comm_exchange : nullptr};
+  // the column-ownership exchanges overlap the later stages (second communicator)
+  g_xpost = split_subcosets && !std::getenv("H2G_SYNC_EXCHANGE") ? comm_exchange_post : nullptr;
+  g_xwait = g_xpost ? comm_exchange_wait : nullptr;
   g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   g_spmd_seq = 0;
   return H2G_OK;
@@ -4393,6 +4519,7 @@ int h2g_comm_spmd_install(int split_subcosets) {
 int h2g_comm_spmd_uninstall(void) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (g_spmd.allgather == comm_allgather_partial) g_spmd = h2g_spmd_transport{nullptr, 1, 0, nullptr, nullptr, nullptr, nullptr};
+  if (g_xpost == comm_exchange_post) g_xpost = nullptr, g_xwait = nullptr;
   g_spmd_seq = 0;
   return H2G_OK;
 }

@@ -126,6 +126,9 @@ _SIGS = {
     "h2g_rng_chacha20": ([ctypes.POINTER(ctypes.c_uint8), VP, U64P], I32),
     "h2g_rng_free": ([U64], I32),
     "h2g_comm_info": ([ctypes.POINTER(I32), ctypes.POINTER(I32)], I32),
+    "h2g_set_spmd_exchange_async": ([VP, VP], I32),
+    "h2g_event_wait": ([VP], I32),
+    "h2g_debug_link_delay": ([VP, VP, ctypes.c_double], I32),
 }
 
 TRANSCRIPTS = {"blake2b": 0, "keccak256": 1}  # Blake2bWrite / Keccak256Write (h2g_pk_set_transcript)
@@ -896,6 +899,7 @@ def transport_errors():
 
 
 SPMD_WORDS = 13  # H2G_SPMD_WORDS (include/h2g.h)
+_spmd_world = 1
 SPMD_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, VP, U64, U64P, U64P)
 SPMD_BCAST = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, SZ, ctypes.c_int)
 SPMD_ALLGATHER_HOST = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, SZ, VP)
@@ -919,11 +923,13 @@ def set_spmd_transport(world, rank=0, allgather=None, bcast=None, allgather_host
     exchange(d_send, send_bytes, d_recv, recv_bytes) (optional, with both): all-to-all of
     device memory with per-peer byte lists -- h(X) then travels as coefficient slabs.
     world <= 1 removes it.  Exceptions fail the proof."""
-    global _transport_keep
+    global _transport_keep, _spmd_world, _xasync_keep
+    _xasync_keep = None  # the library removes the overlapped exchange with the transport
     if world <= 1:
         check(lib().h2g_set_spmd_transport(None))
         _transport_keep = None
         return
+    _spmd_world = world
 
     def _ag(ctx, seq, mine, out):
         try:
@@ -970,6 +976,63 @@ def set_spmd_transport(world, rank=0, allgather=None, bcast=None, allgather_host
     t = SpmdTransport(None, world, rank, cb, cbb, cbh, cbx)
     _transport_keep = (t, cb, cbb, cbh, cbx, [])
     check(lib().h2g_set_spmd_transport(ctypes.byref(t)))
+
+
+SPMD_XPOST = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP, ctypes.POINTER(SZ), VP, ctypes.POINTER(SZ), VP, VP)
+SPMD_XWAIT = ctypes.CFUNCTYPE(ctypes.c_int, VP, VP)
+_xasync_keep = None
+
+
+def set_spmd_exchange_async(post=None, wait=None):
+    """the column-ownership exchanges overlapped with the later stages
+    (h2g_set_spmd_exchange_async; after set_spmd_transport with an exchange, which removes
+    it again): post(d_send, send_bytes, d_recv, recv_bytes, stream, done) queues the
+    all-to-all behind the work on `stream` so far and has `done` recorded (event_record /
+    debug_link_delay) once the bytes are in place; wait(done) returns when it has been.
+    post=None: exchanges complete on return.  Exceptions fail the proof."""
+    global _xasync_keep
+    if post is None:
+        check(lib().h2g_set_spmd_exchange_async(None, None))
+        _xasync_keep = None
+        return
+    errs = _transport_keep[-1] if _transport_keep is not None else []
+
+    def _post(ctx, d_send, sbytes, d_recv, rbytes, stream, done):
+        try:
+            w = _spmd_world
+            post(int(d_send or 0), [int(sbytes[i]) for i in range(w)], int(d_recv or 0),
+                 [int(rbytes[i]) for i in range(w)], int(stream or 0), int(done or 0))
+            return 0
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            return 1
+
+    def _wait(ctx, done):
+        try:
+            if wait is not None:
+                wait(int(done or 0))
+            return 0
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            return 1
+
+    cp, cw = SPMD_XPOST(_post), SPMD_XWAIT(_wait)
+    check(lib().h2g_set_spmd_exchange_async(ctypes.cast(cp, VP), ctypes.cast(cw, VP)))
+    _xasync_keep = (cp, cw)
+
+
+def event_record(done, stream):
+    check(lib().h2g_event_record(VP(done), VP(stream)))
+
+
+def event_wait(done):
+    check(lib().h2g_event_wait(VP(done)))
+
+
+def debug_link_delay(stream, done, us):
+    """`done` recorded `us` microseconds of device time after the work on `stream` (a
+    modelled transfer for the one-GPU SPMD emulation)"""
+    check(lib().h2g_debug_link_delay(VP(stream), VP(done), float(us)))
 
 
 SPMD_COLLECTIVES = ("msm_allgather", "host_allgather", "exchange", "bcast")

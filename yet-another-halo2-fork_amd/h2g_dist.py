@@ -260,8 +260,9 @@ class SpmdGather:
     coefficient slabs joined by small host all-gathers (allgather_host).
     h2g_comm_spmd_install is the same over the library's own RCCL communicator."""
 
-    def __init__(self, dist, group=None, subcosets=True, slabs=True, h_exchange=True):
+    def __init__(self, dist, group=None, subcosets=True, slabs=True, h_exchange=True, exchange_async=True):
         self.dist = dist
+        self.exchange_async = exchange_async
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -337,11 +338,25 @@ class SpmdGather:
                 h2g.memcpy_htod(d_recv, rb.data_ptr(), tot_r)
         self.exchanges += 1
 
+    def exchange_post(self, d_send, send_bytes, d_recv, recv_bytes, stream, done):
+        """the overlapped exchange (h2g_set_spmd_exchange_async) over torch.distributed:
+        torch's collectives cannot wait on the library's stream, so the packed bytes are
+        waited for, the exchange runs to completion, and `done` is recorded behind it -- no
+        overlap (that is the native transport's, comm_exchange_post), but the prover's
+        deferred receive path runs the same as over RCCL"""
+        import h2g
+        h2g.event_record(done, stream)
+        h2g.event_wait(done)
+        self.exchange(d_send, send_bytes, d_recv, recv_bytes)
+        h2g.event_record(done, stream)
+
     def install(self):
         import h2g
+        xchg = self.subcosets and self.slabs and self.h_exchange
         h2g.set_spmd_transport(self.world, self.rank, self.allgather, self.bcast if self.subcosets else None,
-                               self.allgather_host if self.slabs else None,
-                               self.exchange if (self.subcosets and self.slabs and self.h_exchange) else None)
+                               self.allgather_host if self.slabs else None, self.exchange if xchg else None)
+        if xchg and self.exchange_async:
+            h2g.set_spmd_exchange_async(self.exchange_post)
 
     @staticmethod
     def uninstall():
