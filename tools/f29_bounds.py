@@ -120,7 +120,7 @@ def backend_class(C):
 MR = 0x30644e72e131a029b85045b68181585d2833e84879b9709143e1f593f0000001  # BN254 Fr
 
 
-def ntt_pass(stages, b0):
+def ntt_pass(stages, b0, tw=MR):
     """one NTT pass in F29 (csrc/ntt.hip ntt_pass29_kernel / ntt_last29_kernel): inputs <
     b0; stage s: sums a + b, differences a - b + K_s M with K_s = 2^(s+2) into a product
     with a twiddle < M, or kept (normalised) for the j = 0 butterflies; closing product
@@ -133,7 +133,7 @@ def ntt_pass(stages, b0):
         # a product's operand: limbs 0..7 < 2^29 + 2^30, the twiddle normalised
         column_ok(1 << 29, (1 << 29) + (1 << 30))
     assert top(B) < 1 << 31, LG(B)         # top limb of a normalised value fits its 32 bits
-    return B * MR // R + MR + 1
+    return B * tw // R + MR + 1
 
 
 if __name__ == "__main__":
@@ -151,4 +151,18 @@ if __name__ == "__main__":
         assert out < b0 and out < 1 << 256, (st, out / MR)
         print(f"ntt pass of {st} stages: inputs < 3 M, outputs < {out / MR:.3f} M (packable, below the input bound)")
     print(f"last pass: outputs < {ntt_pass(6, b0) / MR:.3f} M before two conditional subtractions of M")
+    # the last pass without an epilogue product (ntt_last29_kernel ONE): reduce29 of the
+    # stage outputs, then one conditional subtraction, must land below 2 M
+    Bl = b0
+    for s_ in range(6):
+        Bl = max(2 * Bl, Bl + (4 << s_) * MR)
+    ql = top(Bl) // (top(MR) + 1)
+    red = MR + (ql + 2) * (1 << 232)
+    assert red < 2 * MR and top(Bl) < 1 << 32, (LG(Bl), red / MR)
+    print(f"last pass without a product: stage outputs < {Bl / MR:.0f} M, reduce29 -> < {red / MR:.6f} M")
+    tw_live = MR * MR // R + MR + 1  # a twiddle formed in the pass: lo x hi, both < M (H2G_NTT_TW_LIVE)
+    for st in (3, 4, 5, 6):
+        out = ntt_pass(st, b0, tw_live)
+        assert out < b0 and out < 1 << 256, (st, out / MR)
+    print(f"passes with twiddles formed in the pass (< {tw_live / MR:.4f} M): outputs < {ntt_pass(6, b0, tw_live) / MR:.3f} M")
     print("ok")

@@ -24,4 +24,17 @@ for log_n in [int(x) for x in (sys.argv[1:] or ["20", "22"])]:
         h2g.fft_dev(d.ptr, log_n, w)
     ms = t.stop_ms() / 10
     print(f"fft 2^{log_n}: {ms:.4f} ms  {(n // 2) * log_n / ms / 1e6:.1f} Mbfly/s")
+    # lagrange_to_coeff (inverse, scaled by 1/n) and coeff_to_extended (coset, 2n points)
+    ext = h2g.DevBuf(2 * n * 32)
+    L = h2g.lib()
+    h2g.check(L.h2g_lagrange_to_coeff_dev(dom.h, h2g.VP(d.ptr), None))
+    h2g.check(L.h2g_coeff_to_extended_dev(dom.h, h2g.VP(d.ptr), h2g.VP(ext.ptr), None))
+    h2g.check(L.h2g_synchronize())
+    for nm, fn in (("lagrange_to_coeff", lambda: L.h2g_lagrange_to_coeff_dev(dom.h, h2g.VP(d.ptr), None)),
+                   ("coeff_to_extended", lambda: L.h2g_coeff_to_extended_dev(dom.h, h2g.VP(d.ptr), h2g.VP(ext.ptr),
+                                                                              None))):
+        t.start()
+        for _ in range(10):
+            h2g.check(fn())
+        print(f"{nm} 2^{log_n}: {t.stop_ms() / 10:.4f} ms")
 h2g.shutdown()

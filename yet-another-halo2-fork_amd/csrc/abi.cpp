@@ -108,16 +108,17 @@ Fr zeta() {
 }
 
 
-int get_tables(Device* d, const Fr& omega, int L, hipStream_t st, NttTables* out) {
-  NttKey key{L, {}};
+int get_tables(Device* d, const Fr& omega, int L, hipStream_t st, NttTables* out, const Fr& fold) {
+  NttKey key{L, {}, {}};
   std::memcpy(key.w, omega.l, sizeof(key.w));
+  std::memcpy(key.f, fold.l, sizeof(key.f));
   auto it = d->ntt_tables.find(key);
   if (it != d->ntt_tables.end()) {
     *out = it->second;
     return H2G_OK;
   }
   NttTables t;
-  hipError_t e = ntt_build_tables(&t, omega, L, st);
+  hipError_t e = ntt_build_tables(&t, omega, L, st, fold);
   if (e != hipSuccess) return hip_fail(e, "ntt_build_tables");
   d->ntt_tables[key] = t;
   *out = t;
@@ -305,7 +306,9 @@ int ntt_dev_impl_batch(Device* d, const Fr* const* src, uint64_t n_in, Fr* const
                        const Fr& scale, int out_dist, const Fr& oz1, const Fr& oz2, hipStream_t st) {
   if (count < 1 || count > NTT_MAX_BATCH) return fail(H2G_ERR_ARG, "ntt: batch size");
   NttArgs a;
-  int rc = get_tables(d, omega, L, st, &a.tab);
+  // a scale goes into the first pass's twiddle table (tables per omega and scale): the
+  // last pass then multiplies only for an output coset distribution
+  int rc = get_tables(d, omega, L, st, &a.tab, has_scale && L > NTT_SMALL_MAX_LOG ? scale : Fr::one());
   if (rc) return rc;
   const size_t N = (size_t)1 << L;
   if (L > NTT_SMALL_MAX_LOG) {

@@ -31,6 +31,14 @@ struct NttTables {
   // the F29 passes' in-pass twiddles w_64^j, j < 32, as F29 elements packed in 8 x 32 bits
   // (a 2^m-point pass reads every 2^(6-m)-th); L >= 6
   Fr* root64 = nullptr;
+  // lo / hi as packed F29 elements (passes that form their inter-pass twiddles from the
+  // two-level table instead of streaming pass_tw, H2G_NTT_TW_LIVE)
+  Fr* lo29 = nullptr;
+  Fr* hi29 = nullptr;
+  // the constant multiplied into the first pass's table (pass_tw; a transform's scale, so
+  // its last pass needs no product) and its inverse (divided out of a call's epilogue)
+  Fr fold = Fr::one();
+  Fr fold_inv = Fr::one();
 };
 
 // One transform y = DFT_w(x) of size N = 2^tab.L with fused maps:
@@ -59,7 +67,7 @@ struct NttArgs {
 };
 
 void ntt_split(int L, int* P, int lg[NTT_MAX_PASSES]);
-hipError_t ntt_build_tables(NttTables* t, const Fr& omega, int L, hipStream_t st);
+hipError_t ntt_build_tables(NttTables* t, const Fr& omega, int L, hipStream_t st, const Fr& fold = Fr::one());
 void ntt_free_tables(NttTables* t);
 hipError_t ntt_run(const NttArgs& a, hipStream_t st);
 hipError_t ntt_init_attributes();

@@ -404,6 +404,13 @@ struct NttConst29 {
   F29 mul[3];      // epilogue multiplier per y mod 3 (last pass), one29 when none
 };
 
+// inter-pass twiddles formed in the pass from the two-level table (one product and two
+// L2-resident loads per element) instead of streamed from pass_tw (32 B of HBM per element):
+// 1 = the first pass only (its table is N entries), 2 = every non-last pass, 0 = none
+#ifndef H2G_NTT_TW_LIVE
+#define H2G_NTT_TW_LIVE 0
+#endif
+
 template <int M>
 __global__ void __launch_bounds__(NTT_THREADS, NttPassWaves<M>::value)
 ntt_pass29_kernel(Fr* data, NttIo io, int first, uint64_t n_in, NttTables tab, const Fr* __restrict__ ptw, int L,
@@ -445,14 +452,31 @@ ntt_pass29_kernel(Fr* data, NttIo io, int first, uint64_t n_in, NttTables tab, c
   });
   D::run(x, w, rg);
   const uint64_t ilow = g * D::CPW + c;
+  const bool live = H2G_NTT_TW_LIVE == 2 || (H2G_NTT_TW_LIVE == 1 && first);
   sfor<0, 8>([&](auto qc) {
     constexpr int qq = decltype(qc)::value;
     const uint32_t k = brev_bits(WaveDif<M>::rpos(qq, rg), M);
-    st29(data + base + c + (uint64_t)k * S, mul29<FrParams>(x[qq], ld29(ptw + (uint64_t)k * S + ilow)));
+    F29 tw;
+    if (live) {  // w^((N / L_p) i_low k) = lo[e mod 2^b] hi[e >> b], < 1.01 M
+      const uint64_t e = (ilow * k) << (L - lrem);
+      tw = mul29<FrParams>(ld29(tab.lo29 + (e & ((1ull << tab.b) - 1))), ld29(tab.hi29 + (e >> tab.b)));
+    } else {
+      tw = ld29(ptw + (uint64_t)k * S + ilow);
+    }
+    st29(data + base + c + (uint64_t)k * S, mul29<FrParams>(x[qq], tw));
   });
 }
 
-__global__ void __launch_bounds__(NTT_THREADS, NTT_MIN_WAVES)
+#ifndef NTT_LAST_WAVES  // waves per SIMD of the untruncated last pass (142 VGPRs: 3 without spilling)
+#define NTT_LAST_WAVES 3
+#endif
+// TRUNC: out_len < N (extended_to_coeff's truncation) -- the stores are predicated per
+// element; without it every element is stored and the epilogue has no branches
+// ONE: the epilogue constant is one for every y (no scale left, no output distribution) --
+// the values (< 256 M) are brought to [0, M) by reduce29 and one conditional subtraction
+// instead of a product
+template <bool TRUNC, bool ONE>
+__global__ void __launch_bounds__(NTT_THREADS, TRUNC ? NTT_MIN_WAVES : NTT_LAST_WAVES)
 ntt_last29_kernel(const Fr* data, NttIo io, uint64_t out_len, NttTables tab, int L, NttPlanLg plan,
                   NttConst29 k29) {
   constexpr int M = 6;
@@ -499,12 +523,16 @@ ntt_last29_kernel(const Fr* data, NttIo io, uint64_t out_len, NttTables tab, int
     constexpr int qq = decltype(qc)::value;
     const uint32_t k = brev_bits(WaveDif<M>::rpos(qq, rg), M);
     const uint64_t y = k0 + mid_nat + (uint64_t)k * kstride;
-    if (y < out_len) {
-      const uint32_t md = mod3(y);
-      // the epilogue constant (scale and / or zeta power, or one) also brings the value
-      // below 2.6 M; two conditional subtractions reach [0, M)
-      const F29 v = mul29<FrParams>(x[qq], sel29(md == 1, k29.mul[1], sel29(md == 2, k29.mul[2], k29.mul[0])));
-      st29(out + y, sub_m_if_ge29<FrParams>(sub_m_if_ge29<FrParams>(v)));
+    if (!TRUNC || y < out_len) {
+      if constexpr (ONE) {
+        st29(out + y, sub_m_if_ge29<FrParams>(reduce29<FrParams>(x[qq])));
+      } else {
+        const uint32_t md = mod3(y);
+        // the epilogue constant (scale and / or zeta power) also brings the value below
+        // 2.6 M; two conditional subtractions reach [0, M)
+        const F29 v = mul29<FrParams>(x[qq], sel29(md == 1, k29.mul[1], sel29(md == 2, k29.mul[2], k29.mul[0])));
+        st29(out + y, sub_m_if_ge29<FrParams>(sub_m_if_ge29<FrParams>(v)));
+      }
     }
   });
 }
@@ -578,13 +606,21 @@ __global__ void ntt_root64_kernel(Fr* out, NttTables tab, int L) {
   if (j < 32) out[j] = storage_to_f29_packed<FrParams>(twiddle(tab, (uint64_t)j << (L - 6)));
 }
 
+// lo / hi as packed F29 elements
+__global__ void ntt_tables29_kernel(Fr* lo29, Fr* hi29, const Fr* lo, const Fr* hi, uint64_t nlo, uint64_t nhi) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t < nlo) lo29[t] = storage_to_f29_packed<FrParams>(lo[t]);
+  if (t < nhi) hi29[t] = storage_to_f29_packed<FrParams>(hi[t]);
+}
+
 // pass table: t = k * S + i_low over [0, 2^lrem): w^(i_low k 2^(L - lrem))
-__global__ void ntt_pass_tw_kernel(Fr* out, NttTables tab, int L, int lrem, int M) {
+__global__ void ntt_pass_tw_kernel(Fr* out, NttTables tab, int L, int lrem, int M, int fold) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (t >= (1ull << lrem)) return;
   const uint64_t S = 1ull << (lrem - M);
   const uint64_t k = t / S, ilow = t % S;
-  const Fr v = twiddle(tab, (ilow * k) << (L - lrem));
+  Fr v = twiddle(tab, (ilow * k) << (L - lrem));
+  if (fold) v = v * tab.fold;  // the first pass carries the transform's scale
   out[t] = H2G_NTT29 ? storage_to_f29_packed<FrParams>(v) : v;  // the passes' form
 }
 
@@ -610,8 +646,10 @@ void ntt_split(int L, int* P, int lg[NTT_MAX_PASSES]) {
   *P = p;
 }
 
-hipError_t ntt_build_tables(NttTables* t, const Fr& omega, int L, hipStream_t st) {
+hipError_t ntt_build_tables(NttTables* t, const Fr& omega, int L, hipStream_t st, const Fr& fold) {
   t->L = L;
+  t->fold = fold;
+  t->fold_inv = inv(fold);
   t->b = (L + 1) / 2;
   if (t->b < 1) t->b = 1;
   const uint64_t nlo = 1ull << t->b, nhi = 1ull << (L > t->b ? L - t->b : 0);
@@ -639,11 +677,17 @@ hipError_t ntt_build_tables(NttTables* t, const Fr& omega, int L, hipStream_t st
   e = hipMalloc(&t->root64, 32 * sizeof(Fr));
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(ntt_root64_kernel, dim3(1), dim3(32), 0, st, t->root64, *t, L);
+  e = hipMalloc(&t->lo29, nlo * sizeof(Fr));
+  if (e != hipSuccess) return e;
+  e = hipMalloc(&t->hi29, (nhi > 0 ? nhi : 1) * sizeof(Fr));
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ntt_tables29_kernel, dim3((unsigned)((mx + bs - 1) / bs)), dim3(bs), 0, st, t->lo29, t->hi29,
+                     t->lo, t->hi, nlo, nhi);
   lrem = L;
   for (int p = 0; p < P - 1; p++) {
     const uint64_t cnt = 1ull << lrem;
     hipLaunchKernelGGL(ntt_pass_tw_kernel, dim3((unsigned)((cnt + bs - 1) / bs)), dim3(bs), 0, st,
-                       t->pass_tw + t->pass_off[p], *t, L, lrem, lg[p]);
+                       t->pass_tw + t->pass_off[p], *t, L, lrem, lg[p], p == 0 ? 1 : 0);
     lrem -= lg[p];
   }
   return hipGetLastError();
@@ -654,7 +698,9 @@ void ntt_free_tables(NttTables* t) {
   if (t->hi) (void)hipFree(t->hi);
   if (t->pass_tw) (void)hipFree(t->pass_tw);
   if (t->root64) (void)hipFree(t->root64);
-  t->lo = t->hi = t->pass_tw = t->root64 = nullptr;
+  if (t->lo29) (void)hipFree(t->lo29);
+  if (t->hi29) (void)hipFree(t->hi29);
+  t->lo = t->hi = t->pass_tw = t->root64 = t->lo29 = t->hi29 = nullptr;
 }
 
 hipError_t ntt_init_attributes() {
@@ -699,15 +745,18 @@ hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
     return hipGetLastError();
   }
   if (P > NTT_MAX_PASSES || lg[P - 1] != 6 || !a.tab.pass_tw) return hipErrorInvalidValue;
-  // epilogue multiplier per (y mod 3): scale * zeta-power, folded on the host
-  const int has_mul = a.has_scale || a.out_distribute;
+  // epilogue multiplier per (y mod 3): scale * zeta-power / the scale folded into the
+  // first pass's table, on the host
   Fr mul[3];
+  bool one = true;
   for (int r = 0; r < 3; r++) {
-    Fr m = a.has_scale ? a.scale : Fr::one();
+    Fr m = (a.has_scale ? a.scale : Fr::one()) * a.tab.fold_inv;
     if (a.out_distribute && r == 1) m = m * a.out_z1;
     if (a.out_distribute && r == 2) m = m * a.out_z2;
     mul[r] = m;
+    one = one && m == Fr::one();
   }
+  const int has_mul = !one;
   NttConst29 k29;  // the F29 passes' constants
   k29.z1 = storage_to_f29<FrParams>(a.in_z1);
   k29.z2 = storage_to_f29<FrParams>(a.in_z2);
@@ -732,9 +781,20 @@ hipError_t ntt_run(const NttArgs& a, hipStream_t st) {
   {
     const uint64_t waves = N / (64ull * WaveDif<6>::CPW);
     const unsigned blocks = (unsigned)((waves + NTT_WAVES - 1) / NTT_WAVES);
-    if (H2G_NTT29)
-      hipLaunchKernelGGL(ntt_last29_kernel, dim3(blocks, (unsigned)B), dim3(NTT_THREADS), 0, st, (const Fr*)a.work,
-                         io, out_len, a.tab, L, plan, k29);
+    const dim3 g(blocks, (unsigned)B), b(NTT_THREADS);
+    const bool tr = out_len < N;
+    if (H2G_NTT29 && tr && one)
+      hipLaunchKernelGGL((ntt_last29_kernel<true, true>), g, b, 0, st, (const Fr*)a.work, io, out_len, a.tab, L, plan,
+                         k29);
+    else if (H2G_NTT29 && tr)
+      hipLaunchKernelGGL((ntt_last29_kernel<true, false>), g, b, 0, st, (const Fr*)a.work, io, out_len, a.tab, L,
+                         plan, k29);
+    else if (H2G_NTT29 && one)
+      hipLaunchKernelGGL((ntt_last29_kernel<false, true>), g, b, 0, st, (const Fr*)a.work, io, out_len, a.tab, L,
+                         plan, k29);
+    else if (H2G_NTT29)
+      hipLaunchKernelGGL((ntt_last29_kernel<false, false>), g, b, 0, st, (const Fr*)a.work, io, out_len, a.tab, L,
+                         plan, k29);
     else
       hipLaunchKernelGGL(ntt_last_kernel, dim3(blocks, (unsigned)B), dim3(NTT_THREADS), 0, st, (const Fr*)a.work,
                          io, out_len, a.tab, L, plan, has_mul, mul[0], mul[1], mul[2]);

@@ -59,12 +59,15 @@ struct DevBuf {
   T* as() const { return reinterpret_cast<T*>(p); }
 };
 
-struct NttKey {
+struct NttKey {  // omega, and the scale folded into the first pass's twiddles (ntt.h NttTables::fold)
   int L;
   uint32_t w[8];
+  uint32_t f[8];
   bool operator<(const NttKey& o) const {
     if (L != o.L) return L < o.L;
-    return std::memcmp(w, o.w, sizeof(w)) < 0;
+    const int c = std::memcmp(w, o.w, sizeof(w));
+    if (c) return c < 0;
+    return std::memcmp(f, o.f, sizeof(f)) < 0;
   }
 };
 
@@ -140,7 +143,7 @@ int domain_init(Domain* dm, uint32_t j, uint32_t k);  // host constants + device
 void domain_release(Domain* dm);
 Domain* get_dom(uint64_t h);
 
-int get_tables(Device* d, const Fr& omega, int L, hipStream_t st, NttTables* out);
+int get_tables(Device* d, const Fr& omega, int L, hipStream_t st, NttTables* out, const Fr& fold = Fr::one());
 int msm_dev_impl(Device* d, const void* sc, const void* bs, size_t n, int c, void* out, hipStream_t st);
 int msm_host_impl(Device* d, const void* sc, const void* bs, size_t n, int c, uint64_t* out, int* is_id,
                   hipStream_t st);
