@@ -129,11 +129,44 @@ H2G_HD F29 to29(const Fe<P>& x) {
 // Column bound: with limbs of a and b < 2^30 (top limbs < 2^31) every column sum stays
 // < 2^64, so inputs may be one unnormalised limb-wise add away from normalised values.
 // Output limbs 0..7 normalised; the top limb is the rest (< 2^32 for outputs < 2^264).
+#ifndef H2G_MUL29_SPLIT  // 1: the a b and m M terms of a column in two accumulators (NTT -4 %, MSM neutral)
+#define H2G_MUL29_SPLIT 1
+#endif
 template <class P>
 H2G_HD F29 mul29(const F29& a, const F29& b) {
   uint32_t m[9];
   F29 r;
   uint64_t acc = 0;
+  if constexpr (H2G_MUL29_SPLIT) {
+    // two dependent chains per column instead of one (the column's a b terms and its m M
+    // terms), joined before m_k and the carry -- half the chain depth, 17 more adds
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      uint64_t acc2 = 0;
+#pragma unroll
+      for (int i = 0; i <= k; i++) acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+      for (int i = 0; i < k; i++) acc2 += (uint64_t)m[i] * C29<P>::M[k - i];
+      acc += acc2;
+      m[k] = ((uint32_t)acc * C29<P>::INV) & F29_MASK;
+      acc += (uint64_t)m[k] * C29<P>::M[0];
+      acc >>= 29;
+    }
+#pragma unroll
+    for (int k = 9; k < 17; k++) {
+      uint64_t acc2 = 0;
+#pragma unroll
+      for (int i = k - 8; i < 9; i++) {
+        acc += (uint64_t)a.l[i] * b.l[k - i];
+        acc2 += (uint64_t)m[i] * C29<P>::M[k - i];
+      }
+      acc += acc2;
+      r.l[k - 9] = (uint32_t)acc & F29_MASK;
+      acc >>= 29;
+    }
+    r.l[8] = (uint32_t)acc;
+    return r;
+  }
 #pragma unroll
   for (int k = 0; k < 9; k++) {
 #pragma unroll

@@ -19,6 +19,7 @@
 // the low m-3 bits.  Global accesses are runs of >= 8 x 32 B across the lanes
 // of one instruction.  Inter-pass twiddles come from a 2-level table
 // w^E = lo[E mod 2^b] * hi[E >> b] (both L2-resident).
+#include <algorithm>
 #include <type_traits>
 
 #include "ntt.h"
@@ -467,6 +468,73 @@ ntt_pass29_kernel(Fr* data, NttIo io, int first, uint64_t n_in, NttTables tab, c
   });
 }
 
+// Persistent variant of ntt_pass29_kernel for the passes after the first (H2G_NTT_PIPE): a wave walks column groups
+// item, item + stride, ... and loads the next group's elements before it transforms the
+// current one, so a SIMD's VALU work is not held up by its waves' loads all arriving at
+// once (one launch round of the plain kernel loads, then computes, then stores).
+#ifndef H2G_NTT_PIPE
+#define H2G_NTT_PIPE 1
+#endif
+template <int M>
+__global__ void __launch_bounds__(NTT_THREADS, 2)
+ntt_pass29p_kernel(Fr* data, NttTables tab, const Fr* __restrict__ ptw, int L, int lrem, uint64_t items) {
+  using D = WaveDif29<M>;
+  data += (uint64_t)blockIdx.y << L;
+  __shared__ F29 w[1 << (M - 1)];
+  for (int j = threadIdx.x; j < (1 << (M - 1)); j += blockDim.x) w[j] = ld29(tab.root64 + (j << (6 - M)));
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint64_t stride = (uint64_t)gridDim.x * NTT_WAVES;
+  uint64_t item = (uint64_t)blockIdx.x * NTT_WAVES + (threadIdx.x >> 6);
+  if (item >= items) return;
+  const uint64_t S = 1ull << (lrem - M);
+  const uint64_t groups = S / D::CPW;
+  const int c = lane % D::CPW, rg = lane / D::CPW;
+  Fr nx[8];
+  auto fetch = [&](uint64_t it) {
+    const uint64_t b = ((it / groups) << lrem) + (it % groups) * D::CPW;
+    sfor<0, 8>([&](auto qc) {
+      constexpr int qq = decltype(qc)::value;
+      const uint64_t pos = b + c + (uint64_t)(rg + D::LPC * qq) * S;
+      nx[qq] = ld_fr(data + pos);
+    });
+  };
+  fetch(item);
+  for (;;) {
+    const uint64_t cur = item;
+    const uint64_t base = ((cur / groups) << lrem) + (cur % groups) * D::CPW;
+    F29 x[8];
+    sfor<0, 8>([&](auto qc) {
+      constexpr int qq = decltype(qc)::value;
+      x[qq] = raw29(nx[qq]);
+    });
+    item += stride;
+    const bool more = item < items;
+    if (more) fetch(item);
+    __builtin_amdgcn_sched_barrier(0);  // the prefetch issues before the transform, the twiddle loads after it
+    D::run(x, w, rg);
+    __builtin_amdgcn_sched_barrier(0);
+    const uint64_t ilow = (cur % groups) * D::CPW + c;
+    sfor<0, 8>([&](auto qc) {
+      constexpr int qq = decltype(qc)::value;
+      const uint32_t k = brev_bits(WaveDif<M>::rpos(qq, rg), M);
+      st29(data + base + c + (uint64_t)k * S, mul29<FrParams>(x[qq], ld29(ptw + (uint64_t)k * S + ilow)));
+    });
+    if (!more) break;
+  }
+}
+
+static int ntt_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                   hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
 #ifndef NTT_LAST_WAVES  // waves per SIMD of the untruncated last pass (142 VGPRs: 3 without spilling)
 #define NTT_LAST_WAVES 3
 #endif
@@ -636,7 +704,14 @@ void ntt_split(int L, int* P, int lg[NTT_MAX_PASSES]) {
   int p = (L + 5) / 6;
   const int R = L - 6 * (p - 1);
   int i = 0;
-  if (R >= 3) {
+#ifndef H2G_NTT_SPLIT  // A/B: 0 = the short pass first, 1 = second, 2 = two 5-bit passes for a 4-bit one
+#define H2G_NTT_SPLIT 0
+#endif
+  if (H2G_NTT_SPLIT == 2 && R == 4 && p >= 3) {
+    lg[i++] = 5;
+    lg[i++] = 5;
+  } else if (R >= 3) {
+    if (H2G_NTT_SPLIT == 1 && p >= 3) lg[i++] = 6;
     lg[i++] = R;
   } else {  // borrow 3 bits so every pass has 3..6 bits
     lg[i++] = 3;
@@ -714,6 +789,13 @@ static void launch_pass(const NttArgs& a, const NttIo& io, int B, int p, int fir
   const uint64_t N = 1ull << L;
   const uint64_t waves = N / ((1ull << M) * WaveDif<M>::CPW);
   const unsigned blocks = (unsigned)((waves + NTT_WAVES - 1) / NTT_WAVES);
+  if (H2G_NTT29 && H2G_NTT_PIPE && !first) {  // two 4-wave blocks per CU over the whole batch, every wave several groups
+    const uint64_t want = (uint64_t)ntt_cus() * 2 / (uint64_t)B;
+    const unsigned pb = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, want));
+    hipLaunchKernelGGL(ntt_pass29p_kernel<M>, dim3(pb, (unsigned)B), dim3(NTT_THREADS), 0, st, a.work, a.tab,
+                       (const Fr*)(a.tab.pass_tw + a.tab.pass_off[p]), L, lrem, waves);
+    return;
+  }
   if (H2G_NTT29)
     hipLaunchKernelGGL(ntt_pass29_kernel<M>, dim3(blocks, (unsigned)B), dim3(NTT_THREADS), 0, st, a.work, io, first,
                        n_in, a.tab, (const Fr*)(a.tab.pass_tw + a.tab.pass_off[p]), L, lrem, dist, k29);
