@@ -160,6 +160,15 @@ if __name__ == "__main__":
     red = MR + (ql + 2) * (1 << 232)
     assert red < 2 * MR and top(Bl) < 1 << 32, (LG(Bl), red / MR)
     print(f"last pass without a product: stage outputs < {Bl / MR:.0f} M, reduce29 -> < {red / MR:.6f} M")
+    # the sparse first pass (ntt_first_sparse29_kernel): x0 < 1.01 M, p = x1 w < 1.01 M;
+    # x0 - p + 4M feeds the closing product with the pass twiddle
+    pj = MR * MR // R + MR + 1
+    assert top(4 * MR) - 1 >= top(pj)
+    ys = MR * 101 // 100 + 4 * MR
+    column_ok(1 << 29, (1 << 29) + (1 << 30))
+    out_sp = ys * MR // R + MR + 1
+    assert out_sp < b0
+    print(f"sparse first pass: outputs < {out_sp / MR:.3f} M")
     tw_live = MR * MR // R + MR + 1  # a twiddle formed in the pass: lo x hi, both < M (H2G_NTT_TW_LIVE)
     for st in (3, 4, 5, 6):
         out = ntt_pass(st, b0, tw_live)

@@ -37,4 +37,13 @@ for log_n in [int(x) for x in (sys.argv[1:] or ["20", "22"])]:
         for _ in range(10):
             h2g.check(fn())
         print(f"{nm} 2^{log_n}: {t.stop_ms() / 10:.4f} ms")
+    # a degree-5 circuit's coset extension (j = 5: 4x the points, a quarter of them nonzero)
+    dom5 = h2g.Domain(5, log_n)
+    ext4 = h2g.DevBuf(dom5.extended_len * 32)
+    h2g.check(L.h2g_coeff_to_extended_dev(dom5.h, h2g.VP(d.ptr), h2g.VP(ext4.ptr), None))
+    h2g.check(L.h2g_synchronize())
+    t.start()
+    for _ in range(10):
+        h2g.check(L.h2g_coeff_to_extended_dev(dom5.h, h2g.VP(d.ptr), h2g.VP(ext4.ptr), None))
+    print(f"coeff_to_extended_x4 2^{log_n}: {t.stop_ms() / 10:.4f} ms")
 h2g.shutdown()

@@ -718,7 +718,13 @@ msm_rgroup_plane_kernel(const RedPoint* __restrict__ B, uint32_t NB, uint32_t m1
 // quad per plane, and sums.
 static constexpr int RPK_MAX = 9;  // block-index planes (LDS: 2^RPK_MAX points); above it (c = 22
                                    // sets) MSMs keep the rscale scheme
-__global__ void __launch_bounds__(1024)
+// threads per block: at 1024 the quad additions are held to 128 VGPRs and spill (136 B
+// of scratch per lane in F29); at 512 they fit
+#ifndef H2G_RPM_THREADS
+#define H2G_RPM_THREADS 512
+#endif
+static constexpr uint32_t RPM_QUADS = H2G_RPM_THREADS / 4;
+__global__ void __launch_bounds__(H2G_RPM_THREADS)
 msm_rplane_mid_kernel(const RedPoint* __restrict__ planes, uint32_t nblk, int LB, int e0, RedPoint* __restrict__ mid,
                       uint32_t* __restrict__ done, G1xyzz* __restrict__ windows) {
   H2G_SETPRIO(H2G_PRIO_RED);
@@ -733,13 +739,13 @@ msm_rplane_mid_kernel(const RedPoint* __restrict__ planes, uint32_t nblk, int LB
   RED_TS(q == (uint32_t)LB + 1 && w == 0, 11);
   if (q <= (uint32_t)LB) {
     RedPoint acc = rp_identity();
-    for (uint32_t i = e; i < nblk; i += 256) acc = rp_add_q4(acc, in[i]);
+    for (uint32_t i = e; i < nblk; i += RPM_QUADS) acc = rp_add_q4(acc, in[i]);
     if (lead) sh[e] = acc;
     __syncthreads();
     RED_TS(q == 0 && w == 0, 9);
     // the tree's levels above the filled entries would only add identities
     uint32_t h0 = 1;
-    while (2 * h0 < (nblk < 256 ? nblk : 256)) h0 <<= 1;
+    while (2 * h0 < (nblk < RPM_QUADS ? nblk : RPM_QUADS)) h0 <<= 1;
     for (uint32_t h = h0; h > 0; h >>= 1) {
       if (e < h) {
         const RedPoint v = rp_add_q4(sh[e], sh[e + h]);
@@ -750,14 +756,14 @@ msm_rplane_mid_kernel(const RedPoint* __restrict__ planes, uint32_t nblk, int LB
     RED_TS(q == 0 && w == 0, 10);
     if (threadIdx.x == 0) mid[(size_t)q * WB + w] = sh[0];
   } else {
-    for (uint32_t i = e; i < (1u << K); i += 256)
+    for (uint32_t i = e; i < (1u << K); i += RPM_QUADS)
       if (lead) {
         if (i < nblk) sh[i] = ld_rp(in + i);
         else sh[i] = rp_identity();
       }
     __syncthreads();
     RED_TS(w == 0, 12);
-    plane_fold<4>(sh, K, e, lead, 256);
+    plane_fold<4>(sh, K, e, lead, RPM_QUADS);
     RED_TS(w == 0, 13);
     if (lead && e < (uint32_t)K) mid[(size_t)(1 + LB + e) * WB + w] = sh[1u << e];
     if (threadIdx.x == 0) mid[(size_t)(1 + LB + K) * WB + w] = sh[0];  // T
@@ -1073,7 +1079,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
       hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, kSmallLB, 4>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
     else
       hipLaunchKernelGGL((msm_rgroup_plane_kernel<4, kSmallLB, 8>), pg, pb, 0, st, bk, NB, m1p, nblk_p, planes);
-    hipLaunchKernelGGL(msm_rplane_mid_kernel, dim3((unsigned)plane_lb + 2, (unsigned)WB), dim3(1024), 0, st,
+    hipLaunchKernelGGL(msm_rplane_mid_kernel, dim3((unsigned)plane_lb + 2, (unsigned)WB), dim3(H2G_RPM_THREADS), 0, st,
                        (const RedPoint*)planes, nblk_p, plane_lb, e0, mid, rdone, (G1xyzz*)ws->windows);
   } else {
     if (red_q4)

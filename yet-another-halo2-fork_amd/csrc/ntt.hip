@@ -524,6 +524,51 @@ ntt_pass29p_kernel(Fr* data, NttTables tab, const Fr* __restrict__ ptw, int L, i
   }
 }
 
+// First pass of 2^3 points when at most the first two of every column's eight inputs are
+// nonzero (n_in <= N / 4: a coset extension by 4 or more, coeff_to_extended of a degree-5
+// circuit): y_k = x_0 + w_8^k x_1 (w_8^(k+4) = -w_8^k), two loads and three products per
+// column instead of eight loads and the twelve products of the 8-point DIF.  One lane per
+// column; outputs < 1.04 M.
+#ifndef H2G_NTT_SPARSE
+#define H2G_NTT_SPARSE 1
+#endif
+__global__ void __launch_bounds__(NTT_THREADS)
+ntt_first_sparse29_kernel(Fr* data, NttIo io, uint64_t n_in, NttTables tab, const Fr* __restrict__ ptw, int L,
+                          int distribute, NttConst29 k29) {
+  data += (uint64_t)blockIdx.y << L;
+  const Fr* in = io.src[blockIdx.y];
+  const uint64_t S = 1ull << (L - 3);
+  const uint64_t col = (uint64_t)blockIdx.x * NTT_THREADS + threadIdx.x;
+  if (col >= S) return;
+  F29 x[2];
+  sfor<0, 2>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const uint64_t pos = col + (uint64_t)j * S;
+    F29 v;
+#pragma unroll
+    for (int i = 0; i < 9; i++) v.l[i] = 0;
+    if (pos < n_in) {
+      v = ld29(in + pos);
+      if (distribute) {
+        const uint32_t md = mod3(pos);
+        if (md) v = mul29<FrParams>(v, sel29(md == 1, k29.z1, k29.z2));
+      }
+    }
+    x[j] = v;
+  });
+  F29 y[8];
+  sfor<0, 4>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const F29 pj = j == 0 ? x[1] : mul29<FrParams>(x[1], ld29(tab.root64 + 8 * j));
+    y[j] = norm29(add29(x[0], pj));
+    y[j + 4] = sub29<FrParams, 4, 29>(x[0], pj);
+  });
+  sfor<0, 8>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    st29(data + col + (uint64_t)k * S, mul29<FrParams>(y[k], ld29(ptw + (uint64_t)k * S + col)));
+  });
+}
+
 static int ntt_cus() {
   static int cus = 0;
   if (!cus) {
@@ -789,6 +834,13 @@ static void launch_pass(const NttArgs& a, const NttIo& io, int B, int p, int fir
   const uint64_t N = 1ull << L;
   const uint64_t waves = N / ((1ull << M) * WaveDif<M>::CPW);
   const unsigned blocks = (unsigned)((waves + NTT_WAVES - 1) / NTT_WAVES);
+  if (H2G_NTT29 && H2G_NTT_SPARSE && M == 3 && first && n_in <= (N >> 2)) {
+    const uint64_t S = N >> 3;
+    hipLaunchKernelGGL(ntt_first_sparse29_kernel, dim3((unsigned)((S + NTT_THREADS - 1) / NTT_THREADS), (unsigned)B),
+                       dim3(NTT_THREADS), 0, st, a.work, io, n_in, a.tab,
+                       (const Fr*)(a.tab.pass_tw + a.tab.pass_off[p]), L, dist, k29);
+    return;
+  }
   if (H2G_NTT29 && H2G_NTT_PIPE && !first) {  // two 4-wave blocks per CU over the whole batch, every wave several groups
     const uint64_t want = (uint64_t)ntt_cus() * 2 / (uint64_t)B;
     const unsigned pb = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(blocks, want));
