@@ -198,8 +198,14 @@ struct ProvingKey {
   int multiopen = 0;
   int transcript = 0;  // TRANSCRIPT_BLAKE2B / TRANSCRIPT_KECCAK256 (transcript.h)
   std::vector<Fr*> gwc_q;
-  uint32_t* lk_cnt = nullptr;  // pinned per-(circuit, lookup) match counters (3 each)
+  uint32_t* lk_cnt = nullptr;  // pinned per-(circuit, lookup) match counters (LKC each)
   size_t lk_cnt_len = 0;
+  // per-(circuit, lookup) device counters and table-row flags of the match, so that one
+  // memset each clears every lookup's and one copy brings all counters back
+  static constexpr int LKC = 8;
+  uint32_t* lk_counters = nullptr;
+  uint8_t* lk_flags = nullptr;
+  size_t lk_cf_n = 0, lk_cf_u = 0;
   Fr* lk_diff = nullptr;  // the lookup commitments' prefix-basis scalars (2 per lookup and circuit)
   size_t lk_diff_len = 0;
   // permute_expression_pair's sort, chosen per lookup from the value width lk_hb[l] (bit
@@ -300,6 +306,9 @@ struct ProvingKey {
   };
   std::vector<XPending> xp;
   size_t xp_used = 0;
+  // a stage's blinding rows, uploaded in one copy (upload_rows_batch)
+  Fr* blind_d = nullptr;
+  size_t blind_d_len = 0;
   uint32_t* d_seeds = nullptr;
   uint64_t* d_offsets = nullptr;
   int max_chunks = 0;
@@ -2114,6 +2123,32 @@ hipError_t pk_upload(ProvingKey& pk, void* dst, const void* src, size_t bytes, h
   return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
 }
 
+// device staging for a batch of blinding rows (grow-only)
+int blind_stage(ProvingKey& pk, size_t count) {
+  if (count > pk.blind_d_len) {
+    PALLOC(pk.pool, pk.blind_d, count);
+    pk.blind_d_len = count;
+  }
+  return H2G_OK;
+}
+// several blocks of blinding rows in one upload and one copy launch: `host` (count Fr) lands
+// in pk.blind_d, which `segs` read from.  Every small host-to-device copy is a ~6-us blit
+// on the stream; a keccak-style proof made ~80 of them, one per column and lookup side
+int upload_rows_batch(ProvingKey& pk, const Fr* host, size_t count, const std::vector<CopySeg>& segs,
+                      hipStream_t st) {
+  if (segs.empty()) return H2G_OK;
+  HIPCHK(pk_upload(pk, pk.blind_d, host, count * sizeof(Fr), st));
+  if (segs.size() > pk.d_segs_len) {
+    PALLOC(pk.pool, pk.d_segs, segs.size());
+    pk.d_segs_len = segs.size();
+  }
+  uint64_t mx = 0;
+  for (const CopySeg& g : segs) mx = std::max<uint64_t>(mx, g.len);
+  HIPCHK(pk_upload(pk, pk.d_segs, segs.data(), segs.size() * sizeof(CopySeg), st));
+  HIPCHK(copy_segments(pk.d_segs, (int)segs.size(), mx, st));
+  return H2G_OK;
+}
+
 std::vector<Fr> g_last_challenges;  // the challenges of the last proof (h2g_last_challenges)
 
 // create_proof's inputs (halo2_proofs/src/plonk/prover.rs:19-36): per circuit the witness
@@ -2372,8 +2407,18 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         }
       }
       RCCHK(flush());
-      if (!early)
-        for (int c : cols) RCCHK(blind(c));
+      if (!early) {  // every column's rows drawn in order, then one upload for the phase
+        RCCHK(blind_stage(pk, (size_t)pk.A * (bf + 1)));
+        std::vector<CopySeg> segs;
+        for (int c : cols) {
+          if (pk.unblinded[c]) continue;
+          Fr* rows = adv_blind.data() + ((size_t)ci * pk.A + c) * (bf + 1);
+          for (int i = 0; i <= bf; i++) rows[i] = rng.random_fr();
+          segs.push_back(CopySeg{pk.blind_d + (size_t)c * (bf + 1), w.adv[c] + unusable, (uint64_t)(bf + 1)});
+        }
+        RCCHK(upload_rows_batch(pk, adv_blind.data() + (size_t)ci * pk.A * (bf + 1), (size_t)pk.A * (bf + 1), segs,
+                                st));
+      }
       for (int c : cols)
         if (!pk.unblinded[c]) (void)rng.random_fr();  // commitment blinds (unused by KZG)
       if (!cols.empty() && !early && !adv_wide) {
@@ -2473,12 +2518,13 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     // between lookups, so their device pipelines queue back to back; the counters are
     // checked once all lookups are queued
     std::vector<Fr> rows((size_t)NLT * 2 * (bf + 1));
-    if ((size_t)NLT * 3 > pk.lk_cnt_len) {
+    constexpr int LKC = ProvingKey::LKC;
+    if ((size_t)NLT * LKC > pk.lk_cnt_len) {
       if (pk.lk_cnt) (void)hipHostFree(pk.lk_cnt);
       pk.lk_cnt = nullptr;
       pk.lk_cnt_len = 0;
-      HIPCHK(hipHostMalloc((void**)&pk.lk_cnt, (size_t)NLT * 3 * sizeof(uint32_t), hipHostMallocDefault));
-      pk.lk_cnt_len = (size_t)NLT * 3;
+      HIPCHK(hipHostMalloc((void**)&pk.lk_cnt, (size_t)NLT * LKC * sizeof(uint32_t), hipHostMallocDefault));
+      pk.lk_cnt_len = (size_t)NLT * LKC;
     }
     constexpr int LKF = ProvingKey::LKF;
     if ((size_t)NLT > pk.lk_or_len) {
@@ -2528,22 +2574,34 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       pk.lkb_len = m;
     }
     // the match and fill of lookup j from its sorted columns (pk.ck_a2 input, pk.ck_t2 table)
-    auto match_fill = [&](int j) -> int {
+    // every lookup's counters and flags cleared at once (a redo clears its own again)
+    if ((size_t)NLT > pk.lk_cf_n || u > pk.lk_cf_u) {
+      PALLOC(pk.pool, pk.lk_counters, (size_t)NLT * LKC);
+      PALLOC(pk.pool, pk.lk_flags, (size_t)NLT * u);
+      pk.lk_cf_n = (size_t)NLT;
+      pk.lk_cf_u = u;
+    }
+    if (NLT) {
+      HIPCHK(hipMemsetAsync(pk.lk_counters, 0, (size_t)NLT * LKC * sizeof(uint32_t), st));
+      HIPCHK(hipMemsetAsync(pk.lk_flags, 1, (size_t)NLT * u, st));
+    }
+    auto match_fill = [&](int j, bool again) -> int {
       const int ci = j / pk.NL, l = j % pk.NL;
       CircuitWs& w = *W[ci];
-      HIPCHK(hipMemsetAsync(pk.left_flag, 1, u, st));
-      HIPCHK(hipMemsetAsync(pk.counters, 0, 8 * sizeof(uint32_t), st));
-      HIPCHK(lookup_mark(pk.ck_a2, pk.ck_t2, u, pk.rep_flag, pk.left_flag, pk.counters + 2, st));
-      HIPCHK(compact_canon(pk.ck_t2, pk.left_flag, u, pk.ck_left, pk.counters, pk.lkb_scr, st));
-      HIPCHK(compact_index(pk.rep_flag, u, pk.rep_rows, pk.counters + 1, pk.lkb_scr, st));
-      HIPCHK(lookup_assign(pk.ck_a2, pk.rep_flag, u, w.lk_ap[l], w.lk_sp[l], st));
-      HIPCHK(lookup_scatter(pk.ck_left, pk.rep_rows, pk.counters + 1, u, w.lk_sp[l], st));
-      HIPCHK(hipMemcpyAsync(pk.lk_cnt + 3 * j, pk.counters, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      for (int which = 0; which < 2; which++) {
-        const Fr* r = rows.data() + ((size_t)2 * j + which) * (bf + 1);
-        HIPCHK(pk_upload(pk, (which ? w.lk_sp[l] : w.lk_ap[l]) + u, r, (size_t)(bf + 1) * sizeof(Fr), st));
+      uint32_t* cnt = pk.lk_counters + (size_t)LKC * j;
+      uint8_t* flags = pk.lk_flags + (size_t)j * u;
+      if (again) {
+        HIPCHK(hipMemsetAsync(flags, 1, u, st));
+        HIPCHK(hipMemsetAsync(cnt, 0, LKC * sizeof(uint32_t), st));
       }
-      return H2G_OK;
+      HIPCHK(lookup_mark(pk.ck_a2, pk.ck_t2, u, pk.rep_flag, flags, cnt + 2, st));
+      HIPCHK(compact_canon(pk.ck_t2, flags, u, pk.ck_left, cnt, pk.lkb_scr, st));
+      HIPCHK(compact_index(pk.rep_flag, u, pk.rep_rows, cnt + 1, pk.lkb_scr, st));
+      HIPCHK(lookup_assign(pk.ck_a2, pk.rep_flag, u, w.lk_ap[l], w.lk_sp[l], st));
+      HIPCHK(lookup_scatter(pk.ck_left, pk.rep_rows, cnt + 1, u, w.lk_sp[l], st));
+      if (again)
+        HIPCHK(hipMemcpyAsync(pk.lk_cnt + (size_t)LKC * j, cnt, LKC * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      return H2G_OK;  // the blinding rows of every lookup land together below (upload_rows_batch)
     };
     // the full sort of lookup j's columns into pk.ck_a2 / ck_t2 (radix sorts on the limbs,
     // in lookup j's own regions of the batch's key / index buffers)
@@ -2609,10 +2667,12 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
                                  pk.lk_or_d + (size_t)LKF * j + 4, st));
           }
         }
-        RCCHK(match_fill(j));
+        RCCHK(match_fill(j, false));
       }
     }
     if (NLT) {
+      HIPCHK(hipMemcpyAsync(pk.lk_cnt, pk.lk_counters, (size_t)NLT * LKC * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                            st));
       HIPCHK(hipMemcpyAsync(pk.lk_or_h, pk.lk_or_d, (size_t)NLT * LKF * sizeof(unsigned long long),
                             hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));  // counters and value masks landed; rows (host) read
@@ -2632,14 +2692,27 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       pk.lk_hb[j] = tie && hb == used[j] ? 0 : hb;  // ties at the right width: full sort from now on
       if (tie || hb > used[j]) {
         RCCHK(full_sort(j));
-        RCCHK(match_fill(j));
+        RCCHK(match_fill(j, true));
         redo = true;
       }
     }
     if (redo) HIPCHK(hipStreamSynchronize(st));
+    {  // the blinding rows of A'_l and S'_l of every lookup this rank sorted, one upload
+      RCCHK(blind_stage(pk, rows.size()));
+      std::vector<CopySeg> segs;
+      for (int j = 0; j < NLT; j++) {
+        if (lq[j] < 0) continue;
+        CircuitWs& w = *W[j / pk.NL];
+        const int l = j % pk.NL;
+        for (int which = 0; which < 2; which++)
+          segs.push_back(CopySeg{pk.blind_d + ((size_t)2 * j + which) * (bf + 1), (which ? w.lk_sp[l] : w.lk_ap[l]) + u,
+                                 (uint64_t)(bf + 1)});
+      }
+      RCCHK(upload_rows_batch(pk, rows.data(), rows.size(), segs, st));
+    }
     bool lk_ok = true;
     for (int j = 0; j < NLT; j++) {
-      const uint32_t* cnt = pk.lk_cnt + 3 * j;
+      const uint32_t* cnt = pk.lk_cnt + (size_t)LKC * j;
       if (lq[j] >= 0 && (cnt[2] != 0 || cnt[0] != cnt[1])) lk_ok = false;
     }
     if (lk_wide) {  // every rank learns whether any owner's lookup failed (none may hang in a collective)
@@ -2902,20 +2975,29 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     const bool lz_wide = lk_shard;
     auto mine = [&](int j) { return lk_owner_all[j] == g_spmd.rank; };
     size_t zrow = 0;
+    // every product's random rows and blind, drawn up front in the products' order (no
+    // other draws come between them) and uploaded once
+    const size_t nprod = (size_t)NLT + (size_t)NSH;
+    for (size_t z = 0; z < nprod; z++) {
+      Fr* rows = prod_blind.data() + z * (size_t)bf;
+      for (int i = 0; i < bf; i++) rows[i] = rng.random_fr();
+      (void)rng.random_fr();  // product blind
+    }
+    if (nprod) {
+      RCCHK(blind_stage(pk, nprod * (size_t)bf));
+      HIPCHK(pk_upload(pk, pk.blind_d, prod_blind.data(), nprod * (size_t)bf * sizeof(Fr), st));
+    }
     // prod: the running product's factors, or (scanned) already its prefix products
     auto finish_z = [&](const Fr* prod, Fr* z_lag, Fr* z_poly, Fr* z_coset, bool scanned, bool here,
                         bool listed) -> int {
-      Fr* rows = prod_blind.data() + (zrow++) * (size_t)bf;
-      for (int i = 0; i < bf; i++) rows[i] = rng.random_fr();
-      (void)rng.random_fr();  // product blind
+      const Fr* rows_d = pk.blind_d + (zrow++) * (size_t)bf;
       if (!here) return H2G_OK;
       const Fr* pre = prod;
       if (!scanned) {
         HIPCHK(poly_prefix_product(prod, pk.pre, n, pk.scr, pk.scr_len, st));
         pre = pk.pre;
       }
-      HIPCHK(pk_upload(pk, pk.small, rows, (size_t)bf * sizeof(Fr), st));
-      HIPCHK(perm_z_assemble(z_lag, n, bf, pre, pk.one, pk.small, st));
+      HIPCHK(perm_z_assemble(z_lag, n, bf, pre, pk.one, rows_d, st));
       if (listed) {
         z_lags.push_back(z_lag);
         z_polys.push_back(z_poly);
