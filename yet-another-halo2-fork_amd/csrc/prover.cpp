@@ -2628,13 +2628,42 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       return H2G_OK;
     };
     std::vector<int> used(NLT);
+    {  // every lookup's compressed input and table, batched launches
+      CompressBatch cb;
+      cb.prog = pk.prog;
+      cb.n_slots = pk.n_slots;
+      cb.consts = pk.consts;
+      cb.load_rot = pk.d_load_rot;
+      cb.n = n;
+      cb.theta = theta;
+      auto add = [&](int2 seg, const CircuitWs& w, Fr* out) -> int {
+        if (cb.count == COMPRESS_BATCH_MAX) {
+          HIPCHK(compress_lagrange_batch(cb, st));
+          cb.count = 0;
+        }
+        cb.seg[cb.count] = seg;
+        cb.load_col[cb.count] = w.d_load_col_lag;
+        cb.out[cb.count++] = out;
+        return H2G_OK;
+      };
+      for (int ci = 0; ci < ncirc; ci++)
+        for (int l = 0; l < pk.NL; l++)
+          if (lq[ci * pk.NL + l] >= 0) {
+            RCCHK(add(pk.seg_lk_in[l], *W[ci], W[ci]->lk_a[l]));
+            RCCHK(add(pk.seg_lk_tab[l], *W[ci], W[ci]->lk_s[l]));
+          }
+      HIPCHK(compress_lagrange_batch(cb, st));
+    }
+    LookupKeysBatch kb;  // every column's keys, batched launches
+    kb.n = u;
+    kb.canon = pk.lkb_canon;
+    kb.key = pk.lkb_key[0];
+    kb.idx = pk.lkb_idx[0];
+    kb.kbits = 48;
+    kb.kmask = (1ull << 48) - 1;
     for (int ci = 0; ci < ncirc; ci++)
       for (int l = 0; l < pk.NL; l++) {
         const int j = ci * pk.NL + l;
-        if (lq[j] >= 0) {
-          RCCHK(compress(*W[ci], pk.seg_lk_in[l], W[ci]->lk_a[l]));
-          RCCHK(compress(*W[ci], pk.seg_lk_tab[l], W[ci]->lk_s[l]));
-        }
         for (int which = 0; which < 2; which++) {
           Fr* r = rows.data() + ((size_t)2 * j + which) * (bf + 1);
           for (int i = 0; i <= bf; i++) r[i] = rng.random_fr();
@@ -2646,11 +2675,17 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         const int shift = used[j] > 48 ? used[j] - 48 : 0;
         const Fr* srcs[2] = {W[ci]->lk_a[l], W[ci]->lk_s[l]};
         for (int side = 0; side < 2; side++) {  // every column keys (a full-sort lookup's are ignored)
-          const size_t g = (size_t)2 * lq[j] + side;
-          HIPCHK(lookup_keys(srcs[side], u, shift, pk.lkb_canon + g * u, pk.lkb_key[0] + g * u, pk.lkb_idx[0] + g * u,
-                             pk.lk_or_d + (size_t)LKF * j, st, 48, (uint64_t)g << 48));
+          if (kb.count == LOOKUP_KEYS_BATCH_MAX) {
+            HIPCHK(lookup_keys_batch(kb, st));
+            kb.count = 0;
+          }
+          kb.in[kb.count] = srcs[side];
+          kb.s[kb.count] = shift;
+          kb.g[kb.count] = 2 * lq[j] + side;
+          kb.d_or[kb.count++] = pk.lk_or_d + (size_t)LKF * j;
         }
       }
+    HIPCHK(lookup_keys_batch(kb, st));
     if (nown) {
       bool alt = false;
       HIPCHK(radix_sort_pairs(pk.lkb_key[0], pk.lkb_idx[0], pk.lkb_key[1], pk.lkb_idx[1], (size_t)G * u, 0,

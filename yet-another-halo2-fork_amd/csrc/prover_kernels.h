@@ -150,6 +150,22 @@ struct CompressArgs {
   Fr* out = nullptr;
 };
 hipError_t compress_lagrange(const CompressArgs& a, hipStream_t st);
+// several compressions of one program table in one launch (blockIdx.y = item): a proof's
+// lookup inputs and tables, two per lookup
+static constexpr int COMPRESS_BATCH_MAX = 32;
+struct CompressBatch {
+  const int4* prog = nullptr;
+  int n_slots = 0;
+  const Fr* consts = nullptr;
+  const int* load_rot = nullptr;
+  uint64_t n = 0;
+  Fr theta;
+  int count = 0;
+  int2 seg[COMPRESS_BATCH_MAX];
+  const Fr* const* load_col[COMPRESS_BATCH_MAX];
+  Fr* out[COMPRESS_BATCH_MAX];
+};
+hipError_t compress_lagrange_batch(const CompressBatch& a, hipStream_t st);
 
 // ---- permute_expression_pair (lookup/prover.rs:410-494) building blocks ----
 struct CanonKey {  // canonical (non-Montgomery) value: Ord on Fr
@@ -166,6 +182,24 @@ hipError_t fr_to_canon(const Fr* in, CanonKey* out, size_t n, hipStream_t st);
 // radix-sort keys key[i] = (bits [s, s + kbits) of canonical(in[i])) | tag (s < 256); key /
 // canon / idx (optional) receive the keys, the canonical values and i; d_or[0..3] |= the
 // values' 64-bit limbs
+// the key step of several lookup columns in one launch (column t: in[t], window shift s[t],
+// value-mask d_or[t]; its canon / key / idx regions at g[t] n of the batch buffers, its key
+// tagged g[t] << kbits above the window; kmask = 2^kbits - 1)
+static constexpr int LOOKUP_KEYS_BATCH_MAX = 32;
+struct LookupKeysBatch {
+  size_t n = 0;
+  CanonKey* canon = nullptr;
+  uint64_t* key = nullptr;
+  uint32_t* idx = nullptr;
+  uint64_t kmask = 0;
+  int kbits = 48;
+  int count = 0;
+  const Fr* in[LOOKUP_KEYS_BATCH_MAX];
+  int s[LOOKUP_KEYS_BATCH_MAX];
+  int g[LOOKUP_KEYS_BATCH_MAX];
+  unsigned long long* d_or[LOOKUP_KEYS_BATCH_MAX];
+};
+hipError_t lookup_keys_batch(const LookupKeysBatch& b, hipStream_t st);
 hipError_t lookup_keys(const Fr* in, size_t n, int s, CanonKey* canon, uint64_t* key, uint32_t* idx,
                        unsigned long long* d_or, hipStream_t st, int kbits = 64, uint64_t tag = 0);
 // out[i] = canon[idx[i]]; *unsorted |= 1 if out is not non-decreasing

@@ -424,6 +424,25 @@ hipError_t compress_lagrange(const CompressArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+__global__ void __launch_bounds__(EH_T) compress_batch_kernel(CompressBatch a) {
+  extern __shared__ uint4 eh_lds[];
+  Fr* sl = reinterpret_cast<Fr*>(eh_lds);
+  const int lane = threadIdx.x, b = blockIdx.y;
+  const uint64_t mask = a.n - 1;
+  for (uint64_t i = blockIdx.x * (uint64_t)EH_T + lane; i < a.n; i += (uint64_t)gridDim.x * EH_T)
+    stf(a.out[b] + i, run_prog(a.prog, a.seg[b], a.consts, a.load_col[b], a.load_rot, i, 1, mask, a.theta, sl, lane));
+}
+
+hipError_t compress_lagrange_batch(const CompressBatch& a, hipStream_t st) {
+  if (a.count <= 0) return hipSuccess;
+  if (a.n_slots > EH_MAX_SLOTS || a.count > COMPRESS_BATCH_MAX) return hipErrorInvalidValue;
+  const size_t lds = (size_t)(a.n_slots > 0 ? a.n_slots : 1) * EH_T * sizeof(Fr);
+  size_t blocks = (a.n + EH_T - 1) / EH_T;
+  if (blocks > 256 * 32) blocks = 256 * 32;
+  hipLaunchKernelGGL(compress_batch_kernel, dim3((unsigned)blocks, (unsigned)a.count), dim3(EH_T), lds, st, a);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ lookups / shuffles
 __global__ void __launch_bounds__(KT) canon_kernel(const Fr* __restrict__ in, CanonKey* __restrict__ out, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -444,11 +463,10 @@ hipError_t fr_to_canon(const Fr* in, CanonKey* out, size_t n, hipStream_t st) {
 // value is below 2^(s + 64)); optionally the canonical values and the identity index;
 // d_or[0..3] |= the values' 64-bit limbs (one atomic per limb per wave), from which the
 // caller checks afterwards that the values fit the key window it chose.
-__global__ void __launch_bounds__(KT) lookup_keys_kernel(const Fr* __restrict__ in, size_t n, int s,
-                                                         CanonKey* __restrict__ canon, uint64_t* __restrict__ key,
-                                                         uint32_t* __restrict__ idx,
-                                                         unsigned long long* __restrict__ d_or, uint64_t kmask,
-                                                         uint64_t tag) {
+__device__ __forceinline__ void lookup_keys_body(const Fr* __restrict__ in, size_t n, int s,
+                                                 CanonKey* __restrict__ canon, uint64_t* __restrict__ key,
+                                                 uint32_t* __restrict__ idx, unsigned long long* __restrict__ d_or,
+                                                 uint64_t kmask, uint64_t tag) {
   uint64_t m[4] = {0, 0, 0, 0};
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const Fr c = to_canonical(ldf(in + i));
@@ -488,6 +506,30 @@ __global__ void __launch_bounds__(KT) lookup_keys_kernel(const Fr* __restrict__ 
     if (v) atomicOr(&d_or[threadIdx.x], (unsigned long long)v);
   }
 }
+__global__ void __launch_bounds__(KT) lookup_keys_kernel(const Fr* __restrict__ in, size_t n, int s,
+                                                         CanonKey* __restrict__ canon, uint64_t* __restrict__ key,
+                                                         uint32_t* __restrict__ idx,
+                                                         unsigned long long* __restrict__ d_or, uint64_t kmask,
+                                                         uint64_t tag) {
+  lookup_keys_body(in, n, s, canon, key, idx, d_or, kmask, tag);
+}
+// item b = blockIdx.y: column b.g[...] of the batch (canon / key / idx at g u, tag g << kbits)
+__global__ void __launch_bounds__(KT) lookup_keys_batch_kernel(LookupKeysBatch b) {
+  const int t = blockIdx.y;
+  const size_t g = (size_t)b.g[t];
+  lookup_keys_body(b.in[t], b.n, b.s[t], b.canon + g * b.n, b.key + g * b.n, b.idx + g * b.n, b.d_or[t], b.kmask,
+                   (uint64_t)g << b.kbits);
+}
+hipError_t lookup_keys_batch(const LookupKeysBatch& b, hipStream_t st) {
+  if (b.count <= 0 || b.n == 0) return hipSuccess;
+  if (b.count > LOOKUP_KEYS_BATCH_MAX) return hipErrorInvalidValue;
+  for (int t = 0; t < b.count; t++)
+    if (b.s[t] < 0 || b.s[t] > 255) return hipErrorInvalidValue;
+  const unsigned g = grid_1d(b.n) < 512 ? grid_1d(b.n) : 512;
+  hipLaunchKernelGGL(lookup_keys_batch_kernel, dim3(g, (unsigned)b.count), dim3(KT), 0, st, b);
+  return hipGetLastError();
+}
+
 hipError_t lookup_keys(const Fr* in, size_t n, int s, CanonKey* canon, uint64_t* key, uint32_t* idx,
                        unsigned long long* d_or, hipStream_t st, int kbits, uint64_t tag) {
   if (n == 0) return hipSuccess;
