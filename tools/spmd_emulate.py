@@ -85,12 +85,20 @@ class FakeCollectives:
         self.world, self.rank, self.gen = world, rank, gen
         self.model = model
         self.calls = self.bcasts = self.exchanges = self.xchg = self.xchg_bytes = 0
+        self.log = None  # recording: [(kind, enter_s, exit_s, link_bytes)], times from self.t0
+        self.t0 = 0.0
+
+    def _rec(self, kind, enter, link):
+        if self.log is not None:
+            self.log.append((kind, enter - self.t0, time.perf_counter() - self.t0, int(link)))
 
     def _wait(self, link_bytes, kind):
         if self.model is not None:
             self.model.wait(link_bytes, kind)
 
     def allgather(self, seq, mine):
+        t = time.perf_counter()
+        self._rec("coll", t, np.asarray(mine).nbytes)
         self._wait(np.asarray(mine).nbytes, "msm_allgather")
         out = np.tile(mine, (self.world, 1))
         for r in range(self.world):
@@ -101,10 +109,12 @@ class FakeCollectives:
         return out
 
     def bcast(self, d_ptr, nbytes, root):
+        self._rec("coll", time.perf_counter(), nbytes)
         self._wait(nbytes, "bcast")
         self.bcasts += 1
 
     def allgather_host(self, data):
+        self._rec("coll", time.perf_counter(), len(data))
         self._wait(len(data), "host_allgather")
         self.exchanges += 1
         out = [data] * self.world
@@ -119,7 +129,9 @@ class FakeCollectives:
 
     def exchange(self, d_send, send_bytes, d_recv, recv_bytes):
         peers = [r for r in range(self.world) if r != self.rank]
-        self._wait(max([int(send_bytes[r]) for r in peers] + [int(recv_bytes[r]) for r in peers] + [0]), "exchange")
+        link = max([int(send_bytes[r]) for r in peers] + [int(recv_bytes[r]) for r in peers] + [0])
+        self._rec("coll", time.perf_counter(), link)
+        self._wait(link, "exchange")
         self.xchg += 1
         self.xchg_bytes += sum(recv_bytes)
 
@@ -131,13 +143,62 @@ class FakeCollectives:
         peers = [r for r in range(self.world) if r != self.rank]
         link = max([int(send_bytes[r]) for r in peers] + [int(recv_bytes[r]) for r in peers] + [0])
         us = 1e6 * self.model.charge(link, "exchange_overlapped") if self.model is not None else 0.0
+        t = time.perf_counter()
         h2g.debug_link_delay(stream, done, us)
+        self._rec("post", t, link)
         self.xchg += 1
         self.xchg_bytes += sum(recv_bytes)
 
-    @staticmethod
-    def exchange_wait(done):
+    def exchange_wait(self, done):
+        t = time.perf_counter()
         h2g.event_wait(done)
+        self._rec("wait", t, 0)
+
+
+def replay(logs, gbs, lat_us):
+    """The ranks' recorded proofs replayed against each other: rank r's host reaches its
+    k-th collective after the local time it spent since its previous one (as measured when
+    it ran alone), a blocking collective completes for every rank when the last rank has
+    arrived plus its modelled wire time (the busiest rank's link), an overlapped exchange's
+    wait completes no earlier than the last rank's post plus its wire time.  Returns the
+    predicted proof time (ms) -- the synchronising collectives' effect that the independent
+    per-rank times leave out -- or None if the ranks' collective sequences differ."""
+    return replay_detail(logs, gbs, lat_us)[0]
+
+
+def replay_detail(logs, gbs, lat_us):
+    """replay() and, per collective, (index, kind, rank 0's local time ms, the latest
+    rank, the wait it causes: latest arrival - earliest arrival, ms)"""
+    bw, lat = gbs * 1e9, lat_us * 1e-6
+    W = len(logs)
+    skew = []
+    evs = [lg["events"] for lg in logs]
+    if any(len(e) != len(evs[0]) or [k for k, *_ in e] != [k for k, *_ in evs[0]] for e in evs):
+        return None, []
+    T = [0.0] * W
+    last = [0.0] * W
+    posts = []  # per posted exchange: (latest post time over ranks, its wire time)
+    nwait = 0
+    for k in range(len(evs[0])):
+        kind = evs[0][k][0]
+        arrive = [T[r] + (evs[r][k][1] - last[r]) for r in range(W)]
+        wire = lat + max(evs[r][k][3] for r in range(W)) / bw
+        if kind != "post":
+            late = max(range(W), key=lambda r: arrive[r])
+            skew.append((k, kind, round(1e3 * evs[0][k][1], 3), late, round(1e3 * (max(arrive) - min(arrive)), 3)))
+        if kind == "coll":
+            done = max(arrive) + wire
+            T = [done + (evs[r][k][2] - evs[r][k][1]) for r in range(W)]
+        elif kind == "post":
+            posts.append((max(arrive), wire))
+            T = [arrive[r] + (evs[r][k][2] - evs[r][k][1]) for r in range(W)]
+        else:  # wait: FIFO with the posts
+            pt, pw = posts[nwait]
+            nwait += 1
+            T = [max(arrive[r] + (evs[r][k][2] - evs[r][k][1]), pt + pw) for r in range(W)]
+        last = [evs[r][k][2] for r in range(W)]
+    end = [T[r] + (logs[r]["proof_s"] - last[r]) for r in range(W)]
+    return 1e3 * max(end), skew
 
 
 def run(args):
@@ -176,6 +237,7 @@ def run(args):
     h2g.spmd_set_weights(weights)
     if args.no_column_owners:
         h2g.spmd_set_column_owners(0)
+    logs = {}
     for r in ranks:
         if args.world > 1:
             params.set_slab(*D.slab(n, args.world, r, weights=weights))
@@ -201,6 +263,14 @@ def run(args):
             pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())
             h2g.prover_stage_sync(False)
             stages = h2g.prover_stages()
+            recs = []
+            if args.replay and not args.comm_model:  # the collective timeline of 3 proofs
+                for _ in range(3):
+                    fc.log = []
+                    fc.t0 = time.perf_counter()
+                    pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())
+                    recs.append({"proof_s": time.perf_counter() - fc.t0, "events": fc.log})
+                    fc.log = None
         finally:
             h2g.set_spmd_transport(1)
         ts.sort()
@@ -218,10 +288,25 @@ def run(args):
                                                      for kd, v in model.by_kind.items()} if model else None,
                            "stages_ms_synced": {nm: round(ms, 3) for nm, ms in stages}}
         print(json.dumps({"rank": r, **out["ranks"][r]}), flush=True)
+        if recs:
+            logs.setdefault(r, recs)
     if args.world > 1:
         params.set_slab(0, 0)
     worst = max(v["median_ms"] for v in out["ranks"].values())
     out["slowest_rank_ms"] = worst
+    if logs and len(logs) == args.world:  # every rank recorded: replay them against each other
+        out["replay"] = {}
+        for model in args.replay.split(";"):
+            gbs, lat = (float(x) for x in model.split(","))
+            preds = [replay([logs[r][i] for r in range(args.world)], gbs, lat) for i in range(3)]
+            preds = sorted(p for p in preds if p is not None)
+            out["replay"][model] = {"predicted_ms": round(preds[len(preds) // 2], 3) if preds else None,
+                                    "speedup": round(out["single_gpu_ms"] / preds[len(preds) // 2], 3)
+                                    if preds else None}
+        _, sk = replay_detail([logs[r][0] for r in range(args.world)], 1e9, 0)
+        out["replay_skew_top"] = sorted(sk, key=lambda x: -x[4])[:10]
+        out["replay_note"] = ("ranks replayed against each other at their collectives (tools/spmd_emulate.py "
+                              "replay): GB/s,us of the link model -> predicted proof time")
     pk.close()
     params.close()
     h2g.shutdown()
@@ -249,6 +334,10 @@ def main():
     ap.add_argument("--comm-model", default="",
                     help="GB/s,us: every collective waits latency + its busiest link's bytes / bandwidth "
                          "(e.g. 50,40 for xGMI); empty: collectives return at once (compute only)")
+    ap.add_argument("--replay", default="",
+                    help="with every rank and no --comm-model: record each rank's collective timeline and replay "
+                         "the ranks against each other, one prediction per 'GB/s,us' model (';'-separated, "
+                         "e.g. '1e9,0;50,40': no wire time / xGMI)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     res = run(args)

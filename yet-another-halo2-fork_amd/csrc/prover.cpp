@@ -419,6 +419,11 @@ uint64_t g_shard_seq = 0;
 // SPMD sharding (h2g_set_spmd_transport): every rank proves, rank r computes slab r
 h2g_spmd_transport g_spmd{nullptr, 1, 0, nullptr, nullptr};
 uint64_t g_spmd_seq = 0;
+// row pieces: the advice transforms run in the permutation stage when every transform of
+// the proof has a rank of its own (prove_impl); 0 keeps them in the advice stage (A/B)
+#ifndef H2G_DEFER_ADV_XFORM
+#define H2G_DEFER_ADV_XFORM 1
+#endif
 // overlapped exchanges (h2g_set_spmd_exchange_async); NULL post: exchanges complete on return
 h2g_spmd_exchange_post g_xpost = nullptr;
 h2g_spmd_exchange_wait g_xwait = nullptr;
@@ -2224,6 +2229,35 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, lag.data(), pol.data(), M, st));
     return ext_cosets(d, pk, (const Fr* const*)pol.data(), cst.data(), M, st);
   };
+  // with row pieces the advice columns' transforms wait for the permutation stage: at the
+  // advice commitments' all-gather every rank would otherwise wait for the ranks that
+  // transform an advice column (their slab partials come late), and in the permutation
+  // stage the ranks without a grand product's transform are idle -- run there, the advice
+  // transforms overlap the products' (the owners are fixed here, in the same rotation)
+  struct DeferredXform {
+    std::vector<const Fr*> lag;
+    std::vector<Fr*> pol, cst;
+    std::vector<int> own;
+  };
+  std::vector<DeferredXform> deferred;
+  // (the column transforms of the whole proof, an upper bound, against the ranks that are
+  // not sub-coset leaders: C3 at 8 ranks has 3 advice + 3 grand products for 6 ranks; at 4
+  // ranks two transforms would share a rank in the permutation stage, measured slower:
+  // profiles/r05/emulation/defer_adv/)
+  const int n_xf = ncirc * (pk.A + pk.nsets + 3 * pk.NL + pk.NS);
+  const bool defer_adv = H2G_DEFER_ADV_XFORM && pieces && n_xf <= Wsp - E_sub;
+  auto xform_later = [&](const std::vector<const Fr*>& lag, const std::vector<Fr*>& pol,
+                         const std::vector<Fr*>& cst) {
+    DeferredXform x{lag, pol, cst, std::vector<int>(lag.size())};
+    for (size_t i = 0; i < lag.size(); i++) x.own[i] = (int)((tr_next + (int)i) % Wsp);
+    tr_next += (int)lag.size();
+    deferred.push_back(std::move(x));
+  };
+  auto run_deferred = [&]() -> int {
+    for (DeferredXform& x : deferred) RCCHK(colshard_distribute(d, pk, x.lag, x.pol, x.cst, x.own, st));
+    deferred.clear();
+    return H2G_OK;
+  };
   ProverRng& rng = *in.rng;
   Transcript tr(proof, pk.transcript);
   SpmdCheckScope spmd_check(&tr, &rng);
@@ -2456,7 +2490,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
           p2.push_back(W[ci]->adv_poly[c]);
           c2.push_back(W[ci]->adv_coset[c]);
         }
-      RCCHK(xform(l2, p2, c2, nullptr));
+      if (defer_adv) xform_later(l2, p2, c2);
+      else RCCHK(xform(l2, p2, c2, nullptr));
     }
     for (int ci = 0; ci < ncirc && !cols.empty() && !adv_wide && !pieces; ci++) {
       CircuitWs& w = *W[ci];
@@ -2936,6 +2971,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     tr_next += NST;
     RCCHK(gather_to_owners(pk, all_z_lag, own, prm.n, st));
     RCCHK(xform(std::vector<const Fr*>(all_z_lag.begin(), all_z_lag.end()), all_z, all_z_coset, &own));
+    RCCHK(run_deferred());  // the advice columns' transforms beside the products
   }
   if (!perm_slab) {
     // every set's denominators (into z_lag), one batched inversion over all circuits'
@@ -3134,6 +3170,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     tl.push_back(&van_tk);
     RCCHK(collect_write(tl));
   }
+  RCCHK(run_deferred());  // (no permutation stage ran them)
   RCCHK(xp_flush(pk, st));  // the overlapped exchanges' rows, before h(X) reads them
   clk.mark("perm+vanishing commits, cosets");
   const Fr y = tr.squeeze();
