@@ -203,6 +203,16 @@ struct ProvingKey {
   // per-(circuit, lookup) device counters and table-row flags of the match, so that one
   // memset each clears every lookup's and one copy brings all counters back
   static constexpr int LKC = 8;
+  // the lookups' gathers and matches on LKS streams (lookup j's on stream j mod LKS), each
+  // stream with its own scratch set; set 0 is the one above (ck_a2 ... rep_rows, lkb_scr)
+  static constexpr int LKS = 4;
+  hipStream_t lk_st[LKS] = {};
+  hipEvent_t lk_ev[LKS + 1] = {};
+  CanonKey *lks_a2[LKS] = {}, *lks_t2[LKS] = {}, *lks_left[LKS] = {};
+  uint8_t* lks_rep[LKS] = {};
+  uint32_t* lks_rows[LKS] = {};
+  void* lks_scr[LKS] = {};
+  size_t lks_n = 0;
   uint32_t* lk_counters = nullptr;
   uint8_t* lk_flags = nullptr;
   size_t lk_cf_n = 0, lk_cf_u = 0;
@@ -2620,22 +2630,33 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       HIPCHK(hipMemsetAsync(pk.lk_counters, 0, (size_t)NLT * LKC * sizeof(uint32_t), st));
       HIPCHK(hipMemsetAsync(pk.lk_flags, 1, (size_t)NLT * u, st));
     }
-    auto match_fill = [&](int j, bool again) -> int {
+    // scratch set q (0: the key's own) for the gathers and matches
+    struct LkSet {
+      CanonKey *a2, *t2, *left;
+      uint8_t* rep;
+      uint32_t* rows;
+      void* scr;
+    };
+    auto lk_set = [&](int q) -> LkSet {
+      if (q == 0) return LkSet{pk.ck_a2, pk.ck_t2, pk.ck_left, pk.rep_flag, pk.rep_rows, pk.lkb_scr};
+      return LkSet{pk.lks_a2[q], pk.lks_t2[q], pk.lks_left[q], pk.lks_rep[q], pk.lks_rows[q], pk.lks_scr[q]};
+    };
+    auto match_fill = [&](int j, bool again, const LkSet& z, hipStream_t sj) -> int {
       const int ci = j / pk.NL, l = j % pk.NL;
       CircuitWs& w = *W[ci];
       uint32_t* cnt = pk.lk_counters + (size_t)LKC * j;
       uint8_t* flags = pk.lk_flags + (size_t)j * u;
       if (again) {
-        HIPCHK(hipMemsetAsync(flags, 1, u, st));
-        HIPCHK(hipMemsetAsync(cnt, 0, LKC * sizeof(uint32_t), st));
+        HIPCHK(hipMemsetAsync(flags, 1, u, sj));
+        HIPCHK(hipMemsetAsync(cnt, 0, LKC * sizeof(uint32_t), sj));
       }
-      HIPCHK(lookup_mark(pk.ck_a2, pk.ck_t2, u, pk.rep_flag, flags, cnt + 2, st));
-      HIPCHK(compact_canon(pk.ck_t2, flags, u, pk.ck_left, cnt, pk.lkb_scr, st));
-      HIPCHK(compact_index(pk.rep_flag, u, pk.rep_rows, cnt + 1, pk.lkb_scr, st));
-      HIPCHK(lookup_assign(pk.ck_a2, pk.rep_flag, u, w.lk_ap[l], w.lk_sp[l], st));
-      HIPCHK(lookup_scatter(pk.ck_left, pk.rep_rows, cnt + 1, u, w.lk_sp[l], st));
+      HIPCHK(lookup_mark(z.a2, z.t2, u, z.rep, flags, cnt + 2, sj));
+      HIPCHK(compact_canon(z.t2, flags, u, z.left, cnt, z.scr, sj));
+      HIPCHK(compact_index(z.rep, u, z.rows, cnt + 1, z.scr, sj));
+      HIPCHK(lookup_assign(z.a2, z.rep, u, w.lk_ap[l], w.lk_sp[l], sj));
+      HIPCHK(lookup_scatter(z.left, z.rows, cnt + 1, u, w.lk_sp[l], sj));
       if (again)
-        HIPCHK(hipMemcpyAsync(pk.lk_cnt + (size_t)LKC * j, cnt, LKC * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(pk.lk_cnt + (size_t)LKC * j, cnt, LKC * sizeof(uint32_t), hipMemcpyDeviceToHost, sj));
       return H2G_OK;  // the blinding rows of every lookup land together below (upload_rows_batch)
     };
     // the full sort of lookup j's columns into pk.ck_a2 / ck_t2 (radix sorts on the limbs,
@@ -2726,18 +2747,53 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       HIPCHK(radix_sort_pairs(pk.lkb_key[0], pk.lkb_idx[0], pk.lkb_key[1], pk.lkb_idx[1], (size_t)G * u, 0,
                               48 + gbits, pk.lkb_scr, st, &alt));
       const uint32_t* sidx = pk.lkb_idx[alt ? 1 : 0];
+      // the lookups' gathers and matches on LKS streams when none needs the full sort (its
+      // radix passes use the key's scratch); lookup q-th of this rank on stream q mod LKS
+      bool multi = nown > 1;
+      for (int j = 0; j < NLT; j++) multi = multi && (lq[j] < 0 || used[j] != 0);
+      const int S = multi ? std::min(nown, ProvingKey::LKS) : 1;
+      if (S > 1) {
+        if (pk.lks_n < u) {
+          for (int q = 1; q < ProvingKey::LKS; q++) {
+            PALLOC(pk.pool, pk.lks_a2[q], u);
+            PALLOC(pk.pool, pk.lks_t2[q], u);
+            PALLOC(pk.pool, pk.lks_left[q], u);
+            PALLOC(pk.pool, pk.lks_rep[q], u);
+            PALLOC(pk.pool, pk.lks_rows[q], u);
+            HIPCHK(pk.pool.get(&pk.lks_scr[q], compact_scratch_bytes(u)));
+          }
+          pk.lks_n = u;
+        }
+        if (!pk.lk_st[0]) {
+          for (int q = 0; q < ProvingKey::LKS; q++) HIPCHK(hipStreamCreateWithFlags(&pk.lk_st[q], hipStreamNonBlocking));
+          for (int q = 0; q <= ProvingKey::LKS; q++) HIPCHK(hipEventCreateWithFlags(&pk.lk_ev[q], hipEventDisableTiming));
+        }
+        HIPCHK(hipEventRecord(pk.lk_ev[0], st));  // the sort is done
+        for (int q = 0; q < S; q++) HIPCHK(hipStreamWaitEvent(pk.lk_st[q], pk.lk_ev[0], 0));
+      }
+      int qi = 0;
       for (int j = 0; j < NLT; j++) {
         if (lq[j] < 0) continue;
+        const int q = S > 1 ? qi % S : 0;
+        qi++;
+        const LkSet z = lk_set(q);
+        hipStream_t sj = S > 1 ? pk.lk_st[q] : st;
         if (used[j] == 0) {
           RCCHK(full_sort(j));
         } else {
           for (int side = 0; side < 2; side++) {
             const size_t g = (size_t)2 * lq[j] + side;
-            HIPCHK(lookup_gather(pk.lkb_canon + g * u, sidx + g * u, u, side ? pk.ck_t2 : pk.ck_a2,
-                                 pk.lk_or_d + (size_t)LKF * j + 4, st));
+            HIPCHK(lookup_gather(pk.lkb_canon + g * u, sidx + g * u, u, side ? z.t2 : z.a2,
+                                 pk.lk_or_d + (size_t)LKF * j + 4, sj));
           }
         }
-        RCCHK(match_fill(j, false));
+        RCCHK(match_fill(j, false, z, sj));
+      }
+      if (S > 1) {  // join
+        for (int q = 0; q < S; q++) {
+          HIPCHK(hipEventRecord(pk.lk_ev[q + 1], pk.lk_st[q]));
+          HIPCHK(hipStreamWaitEvent(st, pk.lk_ev[q + 1], 0));
+        }
       }
     }
     if (NLT) {
@@ -2762,7 +2818,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       pk.lk_hb[j] = tie && hb == used[j] ? 0 : hb;  // ties at the right width: full sort from now on
       if (tie || hb > used[j]) {
         RCCHK(full_sort(j));
-        RCCHK(match_fill(j, true));
+        RCCHK(match_fill(j, true, lk_set(0), st));
         redo = true;
       }
     }
@@ -4298,6 +4354,10 @@ int h2g_pk_free(uint64_t pk) {
   if (it->second->wsum_h) (void)hipHostFree(it->second->wsum_h);
   if (it->second->wsum_d) (void)hipFree(it->second->wsum_d);
   if (it->second->wsum_ev) (void)hipEventDestroy(it->second->wsum_ev);
+  for (hipStream_t q : it->second->lk_st)
+    if (q) (void)hipStreamDestroy(q);
+  for (hipEvent_t e : it->second->lk_ev)
+    if (e) (void)hipEventDestroy(e);
   if (it->second->up_h) (void)hipHostFree(it->second->up_h);
   g_pks.erase(it);
   return H2G_OK;
