@@ -174,4 +174,36 @@ if __name__ == "__main__":
         out = ntt_pass(st, b0, tw_live)
         assert out < b0 and out < 1 << 256, (st, out / MR)
     print(f"passes with twiddles formed in the pass (< {tw_live / MR:.4f} M): outputs < {ntt_pass(6, b0, tw_live) / MR:.3f} M")
+    # evaluate_h29_kernel's unreduced sums / differences (eh_addn / eh_add3n / eh_subn): each
+    # feeds one product; loads < 32 M, constants < M, reduced values < 1.001 M, Horner
+    # accumulators reduced after every step
+    def prod(a, b):  # bound of REDC(a b) for a < aM, b < bM, in units of MR
+        return a * b * MR // R + 1
+    LD, C, RED = 32, 1, 1.001
+    def sub_ok_fr(bm):  # a - b + 64 M: 64 M covers b's top limb
+        assert top(64 * MR) - 1 >= top(int(bm * MR)), bm
+    worst = 0
+    # permutation block
+    lo_hi = prod(LD, LD); cur = max(prod(C, prod(C, lo_hi)), prod(prod(C, lo_hi), C))
+    add3 = LD + prod(C, LD) + C
+    left = LD
+    for _ in range(8):
+        left = max(left, prod(left, add3))
+    right = LD
+    for _ in range(8):
+        right = max(right, prod(right, LD + cur + C))
+    sub_ok_fr(right)
+    worst = max(worst, left + 64, 65, prod(LD, LD) + 64, LD + 64)
+    # lookup block
+    tv = prod(RED + C, RED + C)
+    a1 = prod(prod(LD, LD + C), LD + C)
+    sub_ok_fr(prod(LD, tv)); sub_ok_fr(LD)
+    worst = max(worst, a1 + 64, LD + 64, prod(LD + 64, LD + 64))
+    # shuffle block
+    sub_ok_fr(prod(LD, RED + C))
+    worst = max(worst, prod(LD, RED + C) + 64)
+    assert worst * MR < 1 << 261, worst
+    # every such operand times a load (< 32 M) -- the largest product input pairing
+    assert prod(worst, LD) < 64, prod(worst, LD)
+    print(f"evaluate_h unreduced operands < {worst:.1f} M (< 2^261), their products < {prod(worst, LD):.1f} M")
     print("ok")

@@ -256,6 +256,14 @@ __device__ __forceinline__ F29 eh_sub(const F29& a, const F29& b) {
   return reduce29<FrParams>(norm29(sub29<FrParams, 64, 29>(a, b)));
 }
 __device__ __forceinline__ F29 eh_mul(const F29& a, const F29& b) { return mul29<FrParams>(a, b); }
+// the same without the reduction, where the result goes straight into one product with a
+// load, a constant or a product (tools/f29_bounds.py "evaluate_h": every such operand stays
+// below 96 M, and the product brings it back below 20 M)
+__device__ __forceinline__ F29 eh_addn(const F29& a, const F29& b) { return norm29(add29(a, b)); }
+__device__ __forceinline__ F29 eh_add3n(const F29& a, const F29& b, const F29& c) {
+  return norm29(add29(add29(a, b), c));
+}
+__device__ __forceinline__ F29 eh_subn(const F29& a, const F29& b) { return norm29(sub29<FrParams, 64, 29>(a, b)); }
 // acc * f + v
 __device__ __forceinline__ F29 eh_horner(const F29& acc, const F29& f, const F29& v) {
   return eh_add(mul29<FrParams>(acc, f), v);
@@ -317,15 +325,15 @@ __global__ void __launch_bounds__(EH_T) evaluate_h29_kernel(EvalHArgs a, EvalH29
     if (a.nsets > 0) {
       const uint64_t r_last = (idx + (uint64_t)((int64_t)a.last_rot * (int64_t)a.rot_scale)) & emask;
       // l_0(X) * (1 - z_0(X))
-      acc = eh_horner(acc, k.y, eh_mul(eh_sub(k.one, eh_ld(a.z[0] + idx)), l0));
+      acc = eh_horner(acc, k.y, eh_mul(eh_subn(k.one, eh_ld(a.z[0] + idx)), l0));
       // l_last(X) * (z_l(X)^2 - z_l(X))
       {
         const F29 zl = eh_ld(a.z[a.nsets - 1] + idx);
-        acc = eh_horner(acc, k.y, eh_mul(eh_sub(eh_mul(zl, zl), zl), ll));
+        acc = eh_horner(acc, k.y, eh_mul(eh_subn(eh_mul(zl, zl), zl), ll));
       }
       // l_0(X) * (z_i(X) - z_{i-1}(omega^(last) X))
       for (int s = 1; s < a.nsets; s++)
-        acc = eh_horner(acc, k.y, eh_mul(eh_sub(eh_ld(a.z[s] + idx), eh_ld(a.z[s - 1] + r_last)), l0));
+        acc = eh_horner(acc, k.y, eh_mul(eh_subn(eh_ld(a.z[s] + idx), eh_ld(a.z[s - 1] + r_last)), l0));
       // l_active(X) * (z_i(omega X) prod(p + beta sigma + gamma) - z_i(X) prod(p + delta^j beta X + gamma))
       const uint64_t pmask = (1ull << a.ext_omega.bits) - 1;
       F29 cur = eh_mul(k.delta_start, eh_mul(eh_ld(a.ext_omega.lo + (idx & pmask)),
@@ -337,11 +345,11 @@ __global__ void __launch_bounds__(EH_T) evaluate_h29_kernel(EvalHArgs a, EvalH29
         F29 right = eh_ld(a.z[s] + idx);
         for (int c = c0; c < c1; c++) {
           const F29 v = eh_ld(a.perm_v[c] + idx);
-          left = eh_mul(left, eh_add3(v, eh_mul(k.beta, eh_ld(a.sigma[c] + idx)), k.gamma));
-          right = eh_mul(right, eh_add3(v, cur, k.gamma));
+          left = eh_mul(left, eh_add3n(v, eh_mul(k.beta, eh_ld(a.sigma[c] + idx)), k.gamma));
+          right = eh_mul(right, eh_add3n(v, cur, k.gamma));
           cur = eh_mul(cur, k.delta);
         }
-        acc = eh_horner(acc, k.y, eh_mul(eh_sub(left, right), la));
+        acc = eh_horner(acc, k.y, eh_mul(eh_subn(left, right), la));
       }
     }
     if (a.nlookups + a.nshuffles > 0) {
@@ -352,30 +360,30 @@ __global__ void __launch_bounds__(EH_T) evaluate_h29_kernel(EvalHArgs a, EvalH29
                                   sl, lane, zero29);
         const F29 ct = run_prog29(a.prog, lk.tab, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask, k.theta,
                                   sl, lane, zero29);
-        const F29 table_value = eh_mul(eh_add(ci, k.beta), eh_add(ct, k.gamma));
+        const F29 table_value = eh_mul(eh_addn(ci, k.beta), eh_addn(ct, k.gamma));
         const F29 z = eh_ld(lk.z + idx), ap = eh_ld(lk.ap + idx), sp = eh_ld(lk.sp + idx);
-        const F29 ams = eh_sub(ap, sp);
-        acc = eh_horner(acc, k.y, eh_mul(eh_sub(k.one, z), l0));
-        acc = eh_horner(acc, k.y, eh_mul(eh_sub(eh_mul(z, z), z), ll));
+        const F29 ams = eh_subn(ap, sp);
+        acc = eh_horner(acc, k.y, eh_mul(eh_subn(k.one, z), l0));
+        acc = eh_horner(acc, k.y, eh_mul(eh_subn(eh_mul(z, z), z), ll));
         acc = eh_horner(acc, k.y,
-                        eh_mul(eh_sub(eh_mul(eh_mul(eh_ld(lk.z + r_next), eh_add(ap, k.beta)), eh_add(sp, k.gamma)),
-                                      eh_mul(z, table_value)),
+                        eh_mul(eh_subn(eh_mul(eh_mul(eh_ld(lk.z + r_next), eh_addn(ap, k.beta)), eh_addn(sp, k.gamma)),
+                                       eh_mul(z, table_value)),
                                la));
         acc = eh_horner(acc, k.y, eh_mul(ams, l0));
-        acc = eh_horner(acc, k.y, eh_mul(eh_mul(ams, eh_sub(ap, eh_ld(lk.ap + r_prev))), la));
+        acc = eh_horner(acc, k.y, eh_mul(eh_mul(ams, eh_subn(ap, eh_ld(lk.ap + r_prev))), la));
       }
       for (int s = 0; s < a.nshuffles; s++) {  // evaluation.rs:561-620
         const EvalShuffle sh = a.shuffles[s];
-        const F29 ci = eh_add(run_prog29(a.prog, sh.in, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask,
+        const F29 ci = eh_addn(run_prog29(a.prog, sh.in, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask,
                                          k.theta, sl, lane, zero29),
                               k.gamma);
-        const F29 cs = eh_add(run_prog29(a.prog, sh.sh, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask,
+        const F29 cs = eh_addn(run_prog29(a.prog, sh.sh, a.consts, a.query_col, a.query_rot, idx, a.rot_scale, emask,
                                          k.theta, sl, lane, zero29),
                               k.gamma);
         const F29 z = eh_ld(sh.z + idx);
-        acc = eh_horner(acc, k.y, eh_mul(eh_sub(k.one, z), l0));
-        acc = eh_horner(acc, k.y, eh_mul(eh_sub(eh_mul(z, z), z), ll));
-        acc = eh_horner(acc, k.y, eh_mul(la, eh_sub(eh_mul(eh_ld(sh.z + r_next), cs), eh_mul(z, ci))));
+        acc = eh_horner(acc, k.y, eh_mul(eh_subn(k.one, z), l0));
+        acc = eh_horner(acc, k.y, eh_mul(eh_subn(eh_mul(z, z), z), ll));
+        acc = eh_horner(acc, k.y, eh_mul(la, eh_subn(eh_mul(eh_ld(sh.z + r_next), cs), eh_mul(z, ci))));
       }
     }
     // out = storage(acc * t(X)^-1) (or storage(acc)): one REDC against the raw storage integer
