@@ -206,4 +206,13 @@ if __name__ == "__main__":
     # every such operand times a load (< 32 M) -- the largest product input pairing
     assert prod(worst, LD) < 64, prod(worst, LD)
     print(f"evaluate_h unreduced operands < {worst:.1f} M (< 2^261), their products < {prod(worst, LD):.1f} M")
+    # lincomb29_kernel: up to 6 pairs REDC(a c + b d) (a, b storage integers < M, c, d < M)
+    # plus the accumulated storage value, then reduce29 + one subtraction
+    pair = 2 * MR * MR // R + MR + 1
+    tot = 6 * pair + MR
+    column_ok(1 << 29, 1 << 29, 1 << 29, 1 << 29)
+    assert tot < 1 << 260
+    qv = top(tot) // (top(MR) + 1)
+    assert MR + (qv + 2) * (1 << 232) < 2 * MR
+    print(f"lincomb: pairs < {pair / MR:.4f} M, sum < {tot / MR:.2f} M, reduced below 2 M before the subtraction")
     print("ok")

@@ -969,8 +969,49 @@ __global__ void __launch_bounds__(KT) lincomb_kernel(Fr* __restrict__ out, uint6
   }
 }
 
+// The same in F29 (f29.h): the map is linear, so the storage integers of the columns enter
+// raw, the coefficients as proper F29 elements, and two terms share one reduction
+// (mul29x2); every pair's result is < 1.02 M, their sum (with the accumulated value) is
+// brought to [0, M) by reduce29 and one subtraction.  H2G_LINCOMB29 = 0: the kernel above.
+#ifndef H2G_LINCOMB29
+#define H2G_LINCOMB29 1
+#endif
+struct LinTerms29 {
+  const Fr* p[LIN_MAXT];
+  uint64_t len[LIN_MAXT];
+  F29 coef[LIN_MAXT];
+  int k = 0;
+};
+__global__ void __launch_bounds__(KT) lincomb29_kernel(Fr* __restrict__ out, uint64_t n, LinTerms29 t, int acc_in) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    F29 acc = acc_in ? raw29(ldf(out + i)) : F29{};
+    int k = 0;
+    for (; k + 1 < t.k; k += 2) {
+      const F29 a = i < t.len[k] ? raw29(ldf(t.p[k] + i)) : F29{};
+      const F29 b = i < t.len[k + 1] ? raw29(ldf(t.p[k + 1] + i)) : F29{};
+      acc = add29(acc, mul29x2<FrParams>(a, t.coef[k], b, t.coef[k + 1]));
+    }
+    if (k < t.k) {
+      const F29 a = i < t.len[k] ? raw29(ldf(t.p[k] + i)) : F29{};
+      acc = add29(acc, mul29<FrParams>(a, t.coef[k]));
+    }
+    stf(out + i, pack29<FrParams>(sub_m_if_ge29<FrParams>(reduce29<FrParams>(norm29(acc)))));
+  }
+}
+
 hipError_t lincomb(Fr* out, uint64_t n, const LinTerms& t, bool accumulate, hipStream_t st) {
   if (n == 0) return hipSuccess;
+  if (H2G_LINCOMB29) {
+    LinTerms29 t29;
+    t29.k = t.k;
+    for (int k = 0; k < t.k; k++) {
+      t29.p[k] = t.p[k];
+      t29.len[k] = t.len[k];
+      t29.coef[k] = storage_to_f29<FrParams>(t.coef[k]);
+    }
+    hipLaunchKernelGGL(lincomb29_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, out, n, t29, accumulate ? 1 : 0);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(lincomb_kernel, dim3(grid_1d(n)), dim3(KT), 0, st, out, n, t, accumulate ? 1 : 0);
   return hipGetLastError();
 }
