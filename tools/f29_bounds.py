@@ -215,4 +215,15 @@ if __name__ == "__main__":
     qv = top(tot) // (top(MR) + 1)
     assert MR + (qv + 2) * (1 << 232) < 2 * MR
     print(f"lincomb: pairs < {pair / MR:.4f} M, sum < {tot / MR:.2f} M, reduced below 2 M before the subtraction")
+    # H2G_HORNER29 (eval_level1, kate_phase1/3): acc <- REDC(acc x) + a with x < M and a
+    # storage integer a < 2^256; kate_phase3 (ACC) adds one more stored value before reducing
+    h = 0
+    for _ in range(200):
+        h = max(h, h * MR // R + MR + 1 + (1 << 256))
+    column_ok(1 << 30, 1 << 29)  # acc: a limb-wise add of two normalised values
+    stored = h + (1 << 256)
+    assert stored < 1 << 260
+    qh = top(stored) // (top(MR) + 1)
+    assert MR + (qh + 2) * (1 << 232) < 2 * MR
+    print(f"Horner chains: accumulator < {h / MR:.2f} M, stored sums < {stored / MR:.2f} M, reduced below 2 M")
     print("ok")

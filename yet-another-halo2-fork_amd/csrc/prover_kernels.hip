@@ -749,11 +749,26 @@ __device__ void block_suffix_affine(Fr val, Fr w, Fr* shv, Fr* shw, Fr* out_val,
 }
 
 // ------------------------------------------------------------------ polynomial evaluation
+// H2G_HORNER29 = 1: the Horner chains of eval_level1 and kate_phase1/3 in F29 (f29.h): the
+// recurrence is linear in the coefficients, so they enter as raw storage integers, the
+// point as an F29 element, and the accumulator is reduced only where it is stored.
+// 0: the 8 x 32-bit Montgomery chains (A/B builds).
+#ifndef H2G_HORNER29
+#define H2G_HORNER29 1
+#endif
+__device__ __forceinline__ Fr f29_to_storage(const F29& v) {  // v < 2^260 -> [0, M)
+  return pack29<FrParams>(sub_m_if_ge29<FrParams>(reduce29<FrParams>(norm29(v))));
+}
+
+#ifndef H2G_EV_LS  // log2 of the coefficients per thread (4: 0.95 ms, 6: 0.69 ms for C3 k = 22's batch)
+#define H2G_EV_LS 6
+#endif
 static constexpr int EV_T = 256;
-static constexpr int EV_S = 16;                          // coefficients per thread
+static constexpr int EV_S = 1 << H2G_EV_LS;              // coefficients per thread
 static constexpr uint64_t EV_BLK = (uint64_t)EV_T * EV_S;  // per block
 static constexpr int EV_L = 8;                           // log2(EV_T)
-static_assert((1 << EV_L) == EV_T && EV_BLK == 4096, "eval_level2 raises x to EV_BLK = 2^12");
+static constexpr int EV_LB = EV_L + H2G_EV_LS;           // log2(EV_BLK)
+static_assert((1 << EV_L) == EV_T && EV_BLK == (1ull << EV_LB), "eval_level2 raises x to EV_BLK = 2^EV_LB");
 
 __global__ void __launch_bounds__(EV_T) eval_level1(const EvalReq* __restrict__ reqs, Fr* __restrict__ part,
                                                     uint64_t nbmax) {
@@ -770,6 +785,7 @@ __global__ void __launch_bounds__(EV_T) eval_level1(const EvalReq* __restrict__ 
   // (Four independent Horner chains per thread measured slower: 1.22 vs 0.97 ms for C3
   // k = 22's batch -- the unrolled loads and accumulators halve the waves per SIMD.)
   __shared__ Fr pw[EV_L + 1];
+  __shared__ F29 x29;  // pw[EV_L] as an F29 element (H2G_HORNER29)
   const int t = threadIdx.x;
   if (t == 0) {
     Fr step = rq.x;
@@ -777,14 +793,28 @@ __global__ void __launch_bounds__(EV_T) eval_level1(const EvalReq* __restrict__ 
       pw[l] = step;
       step = step * step;
     }
+    if (H2G_HORNER29) x29 = storage_to_f29<FrParams>(pw[EV_L]);
   }
   __syncthreads();
-  const Fr X = pw[EV_L];
   const uint64_t lo = base + (uint64_t)t;
-  Fr acc = Fr::zero();
-  for (int i = EV_S - 1; i >= 0; i--) {
-    const uint64_t j = lo + (uint64_t)i * EV_T;
-    acc = acc * X + (j < rq.len ? ldf(rq.poly + j) : Fr::zero());
+  Fr acc;
+  if constexpr (H2G_HORNER29) {
+    // F29 Horner (f29.h): storage integers enter raw, x^EV_T as an F29 element; the
+    // accumulator stays unreduced (< 6.4 M, tools/f29_bounds.py) and is reduced once
+    const F29 X = x29;
+    F29 a29{};
+    for (int i = EV_S - 1; i >= 0; i--) {
+      const uint64_t j = lo + (uint64_t)i * EV_T;
+      a29 = add29(mul29<FrParams>(a29, X), j < rq.len ? raw29(ldf(rq.poly + j)) : F29{});
+    }
+    acc = f29_to_storage(a29);
+  } else {
+    const Fr X = pw[EV_L];
+    acc = Fr::zero();
+    for (int i = EV_S - 1; i >= 0; i--) {
+      const uint64_t j = lo + (uint64_t)i * EV_T;
+      acc = acc * X + (j < rq.len ? ldf(rq.poly + j) : Fr::zero());
+    }
   }
   sh[t] = acc;
   __syncthreads();
@@ -804,7 +834,7 @@ __global__ void __launch_bounds__(EV_T) eval_level2(const EvalReq* __restrict__ 
   const uint64_t nb = (rq.len + EV_BLK - 1) / EV_BLK;
   const uint64_t per = (nb + EV_T - 1) / EV_T;
   Fr xb = rq.x;
-  for (int i = 0; i < 12; i++) xb = xb * xb;  // x^4096 = x^EV_BLK
+  for (int i = 0; i < EV_LB; i++) xb = xb * xb;  // x^EV_BLK
   const Fr* p = part + blockIdx.x * nbmax;
   const uint64_t lo = (uint64_t)threadIdx.x * per;
   Fr acc = Fr::zero();
@@ -840,29 +870,46 @@ hipError_t poly_eval_batch(const EvalReq* d_reqs, int nreq, uint64_t max_len, Fr
 // tile's carry) gives each thread its carry, then the downward recurrence.  Every
 // thread's map has the same slope b^KD_S, so both block scans need one product per level,
 // with the level weights b^(KD_S 2^l) computed once on the host (KatePow).
-#ifndef H2G_KD_S
-#define H2G_KD_S 8
+// KD_S (elements per thread) is chosen per call: the largest power of two in
+// [KD_S_MIN, KD_S_MAX] that still gives KD_MIN_BLOCKS tiles (longer chains amortise the
+// block scans and the one-block phase 2; a short polynomial keeps its blocks).
+#ifndef H2G_KD_S_MAX
+#define H2G_KD_S_MAX 32
 #endif
 static constexpr int KD_T = 256;
-static constexpr int KD_S = H2G_KD_S;
+static constexpr int KD_S_MIN = 8;
+static constexpr int KD_S_MAX = H2G_KD_S_MAX;
+static constexpr uint64_t KD_MIN_BLOCKS = 512;
 static constexpr int KD_L = 8;  // log2(KD_T)
-static constexpr uint64_t KD_TILE = (uint64_t)KD_T * KD_S;
 static_assert((1 << KD_L) == KD_T, "KD_L");
+static_assert(KD_S_MAX >= KD_S_MIN && KD_S_MAX <= 64, "KD_S_MAX");
 
 struct KatePow {
   Fr p[KD_L + 1];  // p[l] = b^(KD_S 2^l); p[KD_L] = b^KD_TILE
 };
 
-__global__ void __launch_bounds__(KD_T) kate_phase1(const Fr* __restrict__ a1, uint64_t M, Fr b, KatePow pw,
+template <int KD_S>
+__global__ void __launch_bounds__(KD_T) kate_phase1(const Fr* __restrict__ a1, uint64_t M, Fr b, F29 b29, KatePow pw,
                                                     Fr* __restrict__ tile_val, Fr* __restrict__ thr_val) {
   __shared__ Fr sh[KD_T];
   const int t = threadIdx.x;
-  const uint64_t lo = blockIdx.x * KD_TILE + (uint64_t)t * KD_S;
-  Fr acc = Fr::zero();
+  const uint64_t lo = blockIdx.x * (uint64_t)(KD_T * KD_S) + (uint64_t)t * KD_S;
+  Fr acc;
+  if constexpr (H2G_HORNER29) {
+    F29 a29{};
 #pragma unroll
-  for (int i = KD_S - 1; i >= 0; i--) {
-    const uint64_t j = lo + i;
-    acc = acc * b + (j < M ? ldf(a1 + j) : Fr::zero());
+    for (int i = KD_S - 1; i >= 0; i--) {
+      const uint64_t j = lo + i;
+      a29 = add29(mul29<FrParams>(a29, b29), j < M ? raw29(ldf(a1 + j)) : F29{});
+    }
+    acc = f29_to_storage(a29);
+  } else {
+    acc = Fr::zero();
+#pragma unroll
+    for (int i = KD_S - 1; i >= 0; i--) {
+      const uint64_t j = lo + i;
+      acc = acc * b + (j < M ? ldf(a1 + j) : Fr::zero());
+    }
   }
   stf(thr_val + blockIdx.x * (uint64_t)KD_T + t, acc);
   // sum_t acc_t b^(KD_S t): tree with the level weights
@@ -902,8 +949,8 @@ __global__ void __launch_bounds__(KD_T) kate_phase2(Fr* __restrict__ tile_val, u
 
 // q[j] (+)= the quotient; thread t's carry is the inclusive weighted suffix sum of
 // x_t = (thread t+1's sum, or the tile's carry for the last thread)
-template <bool ACC>
-__global__ void __launch_bounds__(KD_T) kate_phase3(const Fr* __restrict__ a1, uint64_t M, Fr b, KatePow pw,
+template <int KD_S, bool ACC>
+__global__ void __launch_bounds__(KD_T) kate_phase3(const Fr* __restrict__ a1, uint64_t M, Fr b, F29 b29, KatePow pw,
                                                     const Fr* __restrict__ tile_carry,
                                                     const Fr* __restrict__ thr_val, Fr* __restrict__ q) {
   __shared__ Fr sh[KD_T];
@@ -918,7 +965,19 @@ __global__ void __launch_bounds__(KD_T) kate_phase3(const Fr* __restrict__ a1, u
     if (t + s < KD_T) x = x + pw.p[l] * sh[t + s];
     __syncthreads();
   }
-  const uint64_t lo = blockIdx.x * KD_TILE + (uint64_t)t * KD_S;
+  const uint64_t lo = blockIdx.x * (uint64_t)(KD_T * KD_S) + (uint64_t)t * KD_S;
+  if constexpr (H2G_HORNER29) {
+    // the carried value stays unreduced (< 2.1 M); each stored quotient is reduced
+    F29 cur = raw29(x);
+    for (int i = KD_S - 1; i >= 0; i--) {
+      const uint64_t j = lo + i;
+      if (j < M) {
+        cur = add29(raw29(ldf(a1 + j)), mul29<FrParams>(cur, b29));
+        stf(q + j, f29_to_storage(ACC ? add29(raw29(ldf(q + j)), cur) : cur));
+      }
+    }
+    return;
+  }
   Fr cur = x;
   for (int i = KD_S - 1; i >= 0; i--) {
     const uint64_t j = lo + i;
@@ -929,8 +988,21 @@ __global__ void __launch_bounds__(KD_T) kate_phase3(const Fr* __restrict__ a1, u
   }
 }
 
-size_t kate_scratch_len(uint64_t len) {
-  const uint64_t nt = (len + KD_TILE - 1) / KD_TILE;
+template <int S>
+static void kate_launch(const Fr* a, uint64_t M, const Fr& b, const F29& b29, const KatePow& pw, Fr* tile, Fr* thr,
+                        Fr* q, uint64_t nt, hipStream_t st, bool accumulate) {
+  hipLaunchKernelGGL(kate_phase1<S>, dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, b29, pw, tile, thr);
+  hipLaunchKernelGGL(kate_phase2, dim3(1), dim3(KD_T), 0, st, tile, nt, pw.p[KD_L]);
+  if (accumulate)
+    hipLaunchKernelGGL((kate_phase3<S, true>), dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, b29, pw,
+                       (const Fr*)tile, (const Fr*)thr, q);
+  else
+    hipLaunchKernelGGL((kate_phase3<S, false>), dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, b29, pw,
+                       (const Fr*)tile, (const Fr*)thr, q);
+}
+
+size_t kate_scratch_len(uint64_t len) {  // sized for the shortest tiles (KD_S_MIN)
+  const uint64_t nt = (len + (uint64_t)KD_T * KD_S_MIN - 1) / ((uint64_t)KD_T * KD_S_MIN);
   return (size_t)(nt + 1 + nt * KD_T);
 }
 
@@ -938,24 +1010,26 @@ hipError_t kate_division(const Fr* a, uint64_t len, const Fr& b, Fr* q, Fr* scra
                          bool accumulate) {
   if (len < 2) return hipSuccess;
   const uint64_t M = len - 1;
-  const uint64_t nt = (M + KD_TILE - 1) / KD_TILE;
+  int S = KD_S_MIN;
+  while (S < KD_S_MAX && (M + (uint64_t)KD_T * S * 2 - 1) / ((uint64_t)KD_T * S * 2) >= KD_MIN_BLOCKS) S <<= 1;
+  const uint64_t tile_len = (uint64_t)KD_T * S;
+  const uint64_t nt = (M + tile_len - 1) / tile_len;
   KatePow pw;
   Fr x = b;
-  for (int i = 1; i < KD_S; i <<= 1) x = x * x;
+  for (int i = 1; i < S; i <<= 1) x = x * x;
   for (int l = 0; l <= KD_L; l++) {
     pw.p[l] = x;
     x = x * x;
   }
   Fr* tile = scratch;
   Fr* thr = scratch + nt + 1;
-  hipLaunchKernelGGL(kate_phase1, dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, pw, tile, thr);
-  hipLaunchKernelGGL(kate_phase2, dim3(1), dim3(KD_T), 0, st, tile, nt, pw.p[KD_L]);
-  if (accumulate)
-    hipLaunchKernelGGL(kate_phase3<true>, dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, pw, (const Fr*)tile,
-                       (const Fr*)thr, q);
-  else
-    hipLaunchKernelGGL(kate_phase3<false>, dim3((unsigned)nt), dim3(KD_T), 0, st, a + 1, M, b, pw, (const Fr*)tile,
-                       (const Fr*)thr, q);
+  const F29 b29 = storage_to_f29<FrParams>(b);  // b as an F29 element (H2G_HORNER29)
+  switch (S) {
+    case 8: kate_launch<8>(a, M, b, b29, pw, tile, thr, q, nt, st, accumulate); break;
+    case 16: kate_launch<16>(a, M, b, b29, pw, tile, thr, q, nt, st, accumulate); break;
+    case 32: kate_launch<32>(a, M, b, b29, pw, tile, thr, q, nt, st, accumulate); break;
+    default: kate_launch<64>(a, M, b, b29, pw, tile, thr, q, nt, st, accumulate); break;
+  }
   return hipGetLastError();
 }
 
