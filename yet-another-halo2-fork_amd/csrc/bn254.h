@@ -277,8 +277,11 @@ H2G_HD Fe<P> pow_limbs(const Fe<P>& a, const uint32_t e[8]) {
 }
 template <class P>
 H2G_HD Fe<P> pow_u64(const Fe<P>& a, uint64_t e) {
+  // from the top set bit of e: the skipped steps only square one (products are fully
+  // reduced, so the result's bits do not change) -- a serial chain of log2(e) steps, not 64
   Fe<P> acc = Fe<P>::one();
-  for (int b = 63; b >= 0; b--) {
+  if (e == 0) return acc;
+  for (int b = 63 - __builtin_clzll(e); b >= 0; b--) {
     acc = sqr(acc);
     if ((e >> b) & 1) acc = acc * a;
   }
