@@ -114,6 +114,15 @@ def cpu_threads():
     return aff, f"sched_getaffinity: {aff} CPUs"
 
 
+T_START = time.perf_counter()
+
+
+def progress(msg):
+    """a progress line on stderr (the JSON line alone goes to stdout): long legs -- the CPU
+    baselines run for minutes -- must not look like a hang to a watchdog"""
+    print(f"[bench {time.perf_counter() - T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def box_smi():
     """clocks, power and power cap of the GPUs as rocm-smi reports them (best effort)"""
     import subprocess
@@ -142,6 +151,7 @@ def box_block(h2g):
     clock under that load, and rocm-smi's clocks / power / power cap"""
     b = h2g.box_calibrate()
     b["reference_gps"] = MODMUL_REF_GPS
+    b["reference_f29_gps"] = MODMUL_F29_REF_GPS
     b["smi"] = box_smi()
     return b
 
@@ -157,7 +167,8 @@ def cpu_baseline_prove(circ, wit, g, gl, k, reps=1):
     threads, how = cpu_threads()
     kg = O.Keygen(circ, wit, g, gl, threads=threads)
     times = []
-    for _ in range(reps):
+    for i in range(reps):
+        progress(f"cpu baseline, all-cores mode, k={k}, run {i + 1} of {reps}")
         t0 = time.perf_counter()
         O.create_proof(circ, wit, g, gl, threads=threads, keygen=kg)
         times.append(time.perf_counter() - t0)
@@ -169,6 +180,38 @@ def cpu_baseline_prove(circ, wit, g, gl, k, reps=1):
                       f"k={k}, measured directly (no scaling), median of {reps} run(s), keygen excluded",
             "runs_s": [round(t, 3) for t in times],
             "host": {"cpu_model": model, "nproc": ncpu, "threads_used": threads, "threads_from": how}}
+
+
+def cpu_baseline_faithful(h2g, k=20, reps=1):
+    """SURVEY 8d's faithful mode beside the all-cores one: the oracle's
+    create_proof with MSM and FFT single-threaded (halo2curves built without its `multicore`
+    feature, as the reference's Cargo.toml selects -- SURVEY finding 3) and the
+    parallelize-style loops on the box's threads, C3 at k (20: about 80 s), SRS from the
+    device params, keygen excluded"""
+    import h2g_circuit as hc
+    O = _oracle()
+    threads, how = cpu_threads()
+    circ, wit = hc.synthetic_c3(k, h2g.DeviceOps, seed=3)
+    params = h2g.Params(k, s=np.asarray(hc.fr_to_limbs(0x1234567 + k), dtype=np.uint64))
+    g, gl = params.export()
+    params.close()
+    kg = O.Keygen(circ, wit, g, gl, threads=threads)
+    times = []
+    O.lib().or_set_kernel_threads(1)
+    try:
+        for _ in range(reps):
+            progress(f"cpu baseline, faithful mode, k={k}")
+            t0 = time.perf_counter()
+            O.create_proof(circ, wit, g, gl, threads=threads, keygen=kg)
+            times.append(time.perf_counter() - t0)
+    finally:
+        O.lib().or_set_kernel_threads(0)
+        kg.close()
+    med = sorted(times)[len(times) // 2]
+    return {"value": round(med, 3), "unit": "s", "k": k, "msm_fft_threads": 1, "parallelize_threads": threads,
+            "kind": "port", "runs_s": [round(t, 3) for t in times], "threads_from": how,
+            "sample": f"oracle create_proof of the C3 circuit at k={k}, faithful mode (SURVEY 8d (i)): best_multiexp "
+                      f"and best_fft on 1 thread, parallelize on {threads}; median of {reps} run(s), keygen excluded"}
 
 
 def cpu_baseline_msm(log_n=20, reps=2):
@@ -265,9 +308,14 @@ def pmc_child(args):
 
 
 # ----------------------------------------------------------------------------- roofline
-# tools/microbench/modmul_bench.hip's FIPS product rate on the round-4 boxes: value_normalised
-# = value x (this box's rate of that same kernel / this), the proof time scaled to such a box
+# tools/microbench/modmul_bench.hip's FIPS product rate on the round-4 boxes:
+# value_normalised_fips = value x (this box's rate of that same kernel / this)
 MODMUL_REF_GPS = 125.0
+# the F29 product rate (h2g_profile_box_calibrate, 9 x 29-bit limbs: the arithmetic the hot
+# kernels run since round 5) of a reference MI355X box: value_normalised = value x (this
+# box's F29 rate / this), the proof time scaled to a box of that rate.  Boxes of this pool
+# measure 161.9-169.1 G/s at 2.30-2.35 GHz shader clock; 165.0 is the stated reference.
+MODMUL_F29_REF_GPS = 165.0
 
 
 def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note, window_bits=0, union=None,
@@ -395,6 +443,8 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     transport_note = None
     if one_proof:  # every wait on the library's RCCL communicators has a deadline (fail soft)
         h2g.comm_set_timeout(args.comm_timeout)
+        h2g.comm_set_serve_timeout(args.comm_timeout)  # shard peers: rank 0's next request
+        h2g.comm_set_exchange_overlap(args.overlap_exchange)
     if native and shard:  # the library's own RCCL communicators (csrc/comm.cpp); the id travels over torch
         import torch as _t
         tdev = dev if dist.get_backend() == "nccl" else "cpu"
@@ -538,6 +588,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             step()
 
     box = box_block(h2g) if rank == 0 else None  # before the timed region
+    progress(f"prove workload: {args.warmup} warm-up proofs")
     session(warm)
     torch.cuda.synchronize()
     if world > 1:
@@ -547,6 +598,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     if spmd:
         h2g.spmd_stats(reset=True)
     t0 = time.perf_counter()
+    progress(f"prove workload: {args.steps} timed proofs")
     session(timed)
     torch.cuda.synchronize()
     t_local = time.perf_counter() - t0  # this rank's proofs, before the closing barrier
@@ -608,8 +660,11 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                 assert pp == proofs[0]
             pcie = {"median_s": round(sorted(pts)[len(pts) // 2], 4), "min_s": round(min(pts), 4),
                     "max_s": round(max(pts), 4), "proofs": len(pts),
-                    "note": "advice uploaded from pageable host memory inside each proof (column uploads overlap "
-                            "the previous column's commitment MSM); same proof bytes"}
+                    "note": "advice uploaded from pageable host memory inside each proof (the random polynomial's "
+                            "commitment runs under the first column's upload, each later upload under the previous "
+                            "column's commitment MSM); same proof bytes.  This is SURVEY 8d's timing convention "
+                            "(create_proof including host<->device transfers); `value` keeps the witness resident "
+                            "in HBM as the bench contract asks"}
             # the caller-RNG form (create_proof(..., rng: R: RngCore, ...)): the same
             # ChaCha20 stream drawn through the h2g_rng callback struct by h2g_create_proof_multi,
             # advice device-resident as in `value`; as many proofs as the timed steps, median
@@ -667,7 +722,11 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                                              peak_gps=box["modmul_f29_gps"]),
             "box": box,
             "value_normalised": round(elapsed / (args.steps * (1 if one_proof else world)) *
-                                      box["modmul_ref_gps"] / MODMUL_REF_GPS, 4),
+                                      box["modmul_f29_gps"] / MODMUL_F29_REF_GPS, 4),
+            "value_normalised_basis": f"value x box.modmul_f29_gps / {MODMUL_F29_REF_GPS} G/s (F29 products, the "
+                                      "hot kernels' arithmetic)",
+            "value_normalised_fips": round(elapsed / (args.steps * (1 if one_proof else world)) *
+                                           box["modmul_ref_gps"] / MODMUL_REF_GPS, 4),
             "msm_in_prover": {"launches_per_proof": calls // max(args.steps, 1), "avg_ms": round(msm_ms, 4),
                               "busy_ms_per_proof": round(union["msm"] / args.steps, 3),
                               "accumulate_busy_ms_per_proof": round(union["accumulate"] / args.steps, 3),
@@ -681,6 +740,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             # the roofline's kernel figure from lone launches of the same MSM shape (no other
             # stream's kernels inside a launch); the in-proof launches' figures stay beside it
             rp = line["roofline"]
+            progress("lone MSM leg (roofline kernel time)")
             lcalls, lphases, lunion = lone_msm_leg(h2g, torch, dev, k)
             roof = roofline_from_phases(lcalls, lphases, n, traffic, traffic_note,
                                         union={"entries": lunion.get("entries")}, peak_gps=box["modmul_f29_gps"])
@@ -693,6 +753,8 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                                         "that shares the chip with the other stream's MSM runs longer; aggregate = "
                                         "all launches' modmuls / the union of their intervals"}
             line["roofline"] = roof
+            progress("NTT leg")
+            line["ntt"] = ntt_leg(h2g, box)
         if pcie:
             line["pcie_inclusive"] = pcie
             line["pcie_inclusive_s"] = pcie["median_s"]
@@ -712,6 +774,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             line["transport_note"] = transport_note
     if args.workload == "prove" and (world == 1 or dist.get_backend() == "nccl"):
         # every rank takes part when sharded (collectives inside)
+        progress("MSM 2^24 leg")
         m = measure_msm(h2g, torch, dev, 24, steps=10, warmup=2, dist=dist, world=world, rank=rank)
         if line is not None:
             line["msm_2p24"] = m
@@ -727,9 +790,12 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     params.close()
     torch.cuda.empty_cache()
     if line is not None and world == 1 and args.workload == "prove" and not args.no_krange:
+        progress("k-range proofs")
         line["k_range"] = k_range(h2g, torch, dev, args)
     if want_cpu:
         cb = cpu_baseline_prove(circ, wit, g, gl, k, reps=args.cpu_reps)
+        if not args.no_cpu_faithful:
+            cb["faithful"] = cpu_baseline_faithful(h2g, k=args.cpu_faithful_k)
         line["cpu_baseline"] = cb
         line["gpu_vs_cpu"] = round(cb["value"] / line["value"], 1)
     return line
@@ -763,6 +829,96 @@ def lone_msm_leg(h2g, torch, dev, log_n, steps=10, warmup=2):
     del bases, scalars
     torch.cuda.empty_cache()
     return calls, phases, union
+
+
+def ntt_split(L):
+    """mirror of ntt_split (csrc/ntt.hip): the passes' radix bits, 3..6 each, last pass 6"""
+    if L <= 11:  # NTT_SMALL_MAX_LOG: one block in LDS
+        return [L]
+    p = (L + 5) // 6
+    r = L - 6 * (p - 1)
+    lg = [r] if r >= 3 else [3, r + 3]
+    return lg + [6] * (p - len(lg))
+
+
+def ntt_pass_products(M, last, one, first_sparse=False):
+    """Montgomery products one lane (8 elements) of a radix-2^M F29 pass executes
+    (csrc/ntt.hip WaveDif29): round A's 3 stages x 4 butterflies (stage_a), round B's
+    butterflies with a nonzero twiddle index (stage_b: 0 / 2 / 3 for its row bits 0 / 1 / 2),
+    then the 8 inter-pass twiddles -- or the last pass's 8 epilogue constants, none when
+    the constant is one (ntt_last29_kernel ONE: a reduce29 instead).  The sparse first
+    pass: 3 products for y_k = x_0 + w_8^k x_1 and the 8 twiddles."""
+    if first_sparse:
+        return 3 + 8
+    b = sum((0, 2, 3)[t] for t in range(M - 3))
+    return 12 + b + (0 if (last and one) else 8)
+
+
+def ntt_products(L, n_in=None, distribute=False, one=True):
+    """(per-pass products, butterflies) of one transform of 2^L elements; n_in < 2^L is a
+    zero-padded input (a coset extension), `distribute` multiplies the inputs by the coset
+    powers in the first pass (2 of every 3)"""
+    N = 1 << L
+    n_in = N if n_in is None else n_in
+    lg = ntt_split(L)
+    per = []
+    for i, M in enumerate(lg):
+        sparse = i == 0 and M == 3 and n_in <= N // 4
+        prod = N // 8 * ntt_pass_products(M, i == len(lg) - 1, one, sparse)
+        if i == 0 and distribute:
+            prod += 2 * n_in // 3
+        per.append(prod)
+    return per, N // 2 * L
+
+
+def ntt_leg(h2g, box, sizes=(20, 22), reps=20):
+    """the NTT row of the bench line: device transforms of 2^20 and
+    2^22 elements -- the FFT, lagrange_to_coeff (1/n folded into the first pass) and the 2x
+    coset extension (coeff_to_extended of a degree-3 domain, 2^(k+1) points) -- each the mean
+    of `reps` back-to-back calls between HIP events on the library stream, with the F29
+    products its passes execute (ntt_products) against this box's F29 product rate"""
+    L = h2g.lib()
+    rng = np.random.default_rng(77)
+    out = {}
+    for log_n in sizes:
+        n = 1 << log_n
+        a = random_scalars(rng, n)
+        d = h2g.DevBuf.from_array(a)
+        dom = h2g.Domain(3, log_n)
+        ext = h2g.DevBuf(dom.extended_len * 32)
+        w = dom.consts[0]
+        tm = h2g.Timer()
+        rows = {}
+        cases = (("fft", lambda: h2g.fft_dev(d.ptr, log_n, w), log_n, ntt_products(log_n)),
+                 ("lagrange_to_coeff", lambda: h2g.check(L.h2g_lagrange_to_coeff_dev(dom.h, h2g.VP(d.ptr), None)),
+                  log_n, ntt_products(log_n)),
+                 ("coeff_to_extended_x2",
+                  lambda: h2g.check(L.h2g_coeff_to_extended_dev(dom.h, h2g.VP(d.ptr), h2g.VP(ext.ptr), None)),
+                  dom.extended_k, ntt_products(dom.extended_k, n_in=n, distribute=True)))
+        for name, fn, tl, (per, bfly) in cases:
+            for _ in range(3):
+                fn()
+            h2g.check(L.h2g_synchronize())
+            tm.start()
+            for _ in range(reps):
+                fn()
+            ms = tm.stop_ms() / reps
+            prods = sum(per)
+            gps = prods / (ms * 1e-3) / 1e9
+            rows[name] = {"points": 1 << tl, "ms": round(ms, 4), "passes": ntt_split(tl),
+                          "products_per_pass": per, "products": prods, "radix2_butterflies": bfly,
+                          "g_products_per_s": round(gps, 2),
+                          "frac_of_box_f29": round(gps / box["modmul_f29_gps"], 3) if box else None,
+                          "hbm_gbs_64B_per_element_pass": round(64 * (1 << tl) * len(per) / (ms * 1e-3) / 1e9, 1)}
+        out[f"2^{log_n}"] = rows
+        d.close()
+        ext.close()
+        dom.close()
+    return {"transforms": out,
+            "note": "products counted per pass as the F29 kernels execute them (round A 12 + round B's nonzero "
+                    "twiddles + 8 inter-pass twiddles or epilogue constants per 8 elements; the last pass of these "
+                    "transforms has constant one: reduce29, no products); frac = products/s over box.modmul_f29_gps "
+                    "(a lone mul29 loop): the passes' adds, shuffles and loads share the same VALU"}
 
 
 def k_range(h2g, torch, dev, args):
@@ -964,7 +1120,12 @@ def main():
                          "collective); past it they are aborted, the proof fails on that rank, and every "
                          "rank moves to the next transport of --spmd-transports")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--overlap-exchange", action="store_true",
+                    help="spmd over the library's RCCL communicators: post the column-ownership exchanges on the "
+                         "second communicator (overlapped); default blocking (not yet run on 2+ GPUs)")
     ap.add_argument("--cpu-reps", type=int, default=3, help="CPU baseline runs (median)")
+    ap.add_argument("--no-cpu-faithful", action="store_true", help="skip the faithful-mode CPU baseline")
+    ap.add_argument("--cpu-faithful-k", type=int, default=20, help="k of the faithful-mode CPU baseline")
     ap.add_argument("--no-krange", action="store_true",
                     help="prove workload: skip the k = 20 / 24 and keccak-style k = 18 timings")
     ap.add_argument("--no-pmc", action="store_true", help="skip the PMC traffic passes")

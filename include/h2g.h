@@ -398,8 +398,16 @@ int h2g_comm_init(const uint8_t id[256], int world, int rank);
  * collective's completion.  Past it -- or on an RCCL error -- the communicators are aborted
  * (ncclCommAbort) and the call fails with H2G_ERR_DEVICE, so a run that would hang inside
  * RCCL returns and the caller can fall back to another transport (bench.py).  The peers'
- * wait for rank 0's next slab request (h2g_comm_serve) has no deadline. */
+ * wait for rank 0's next slab request (h2g_comm_serve) has its own deadline, below. */
 int h2g_comm_set_timeout(double seconds);
+/* shard mode: a serving peer's longest wait (seconds; <= 0: none, the default) for rank 0's
+ * next request header in h2g_comm_serve.  Rank 0 that aborts its communicators (a timed-out
+ * wait) or dies need not surface as an RCCL error on the peer; past this deadline the peer
+ * aborts its own and h2g_comm_serve fails with H2G_ERR_DEVICE instead of waiting forever.
+ * Rank 0 renews the peers' deadline with h2g_comm_keepalive while it idles between proofs
+ * (a header the serve loop only counts as a sign of life). */
+int h2g_comm_set_serve_timeout(double seconds);
+int h2g_comm_keepalive(void);
 int h2g_comm_install(uint64_t params);
 int h2g_comm_serve(uint64_t params, uint64_t* served);
 int h2g_comm_stop(void);
@@ -507,6 +515,11 @@ int h2g_spmd_stats(double* out, int max, int reset);
  * the communicator), 0 replicates that work; the multi-open tail always runs on
  * coefficient slabs (allgather_host over the communicator) */
 int h2g_comm_spmd_install(int split_subcosets);
+/* SPMD over the library's communicators: 1 posts the column-ownership exchanges on the
+ * second communicator's stream so they overlap the stages after them (the prover waits for
+ * them before h(X)); 0 (the default) keeps them blocking on the first.  Read at
+ * h2g_comm_spmd_install.  Both produce the same proof bytes. */
+int h2g_comm_set_exchange_overlap(int on);
 int h2g_comm_spmd_uninstall(void);
 
 #ifdef __cplusplus

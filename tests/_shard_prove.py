@@ -130,6 +130,8 @@ def main():
             pk.close()
         else:
             params.set_slab(*D.slab(P, world, rank))
+            if native:  # a rank 0 that aborted would otherwise leave this peer waiting forever
+                h2g.comm_set_serve_timeout(120.0)
             served = h2g.comm_serve(params) if native else D.SlabWorker(dist, params=params).serve()
             results[name] = {"served": served}
         params.close()
@@ -154,9 +156,6 @@ def main():
 
 
 def spmd_main(args, rank, world, native):
-    if os.environ.get("H2G_DUMP_BASE"):  # debugging: one dump directory per rank
-        os.environ["H2G_DUMP"] = os.path.join(os.environ["H2G_DUMP_BASE"], f"r{rank}")
-        os.makedirs(os.environ["H2G_DUMP"], exist_ok=True)
     """every rank: the single-device proofs first, then the same proofs with its slab of
     every MSM and the all-gathered partials; all ranks must print identical bytes"""
     import hashlib
@@ -174,9 +173,8 @@ def spmd_main(args, rank, world, native):
         pk = h2g.ProvingKey(params, circ)
         want = [_prove(pk, case, **kw) for kw in variants]
         g = None
-        if native:
-            if args.sync_exchange:
-                os.environ["H2G_SYNC_EXCHANGE"] = "1"
+        if native:  # the RCCL test runs both: overlapped (default here) and --sync-exchange
+            h2g.comm_set_exchange_overlap(not args.sync_exchange)
             h2g.comm_spmd_install(not args.no_subcosets)
         else:
             g = D.SpmdGather(dist, subcosets=not args.no_subcosets, slabs=not args.no_slabs,

@@ -217,3 +217,18 @@ def test_sharded_proof_rccl_two_gpus(transport, mode):
             assert res[nm]["same_ranks"], nm
         else:
             assert all(m > 0 for m in res[nm]["msms"]), (nm, res[nm])
+
+
+@pytest.mark.parametrize("exchange", ["overlapped", "blocking"])
+def test_spmd_rccl_four_gpus_column_exchanges(exchange):
+    """libh2g's RCCL communicators with column ownership (from 4 ranks): the column
+    exchanges posted on the second communicator (h2g_comm_set_exchange_overlap(1), what
+    bench.py --overlap-exchange selects) and blocking on the first (the default); needs
+    >= 4 GPUs, one per rank"""
+    if _gpus() < 4:
+        pytest.skip("needs four GPUs")
+    cases = ["c3_k14", "keccak_k12"]
+    extra = ["--one-variant"] + (["--sync-exchange"] if exchange == "blocking" else [])
+    res = _run(4, cases, backend="nccl", transport="native", mode="spmd", extra=extra)
+    for nm in cases:
+        assert res[nm]["same"] and res[nm]["same_ranks"], (nm, res[nm])

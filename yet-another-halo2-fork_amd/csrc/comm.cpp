@@ -32,6 +32,11 @@ static constexpr int RING = 16;  // outstanding MSMs on rank 0
 // the deadline of every RCCL wait (communicator setup, enqueue, completion), seconds; <= 0:
 // none.  Past it the communicators are aborted and the call fails (comm_wait.h).
 double g_timeout_s = 300.0;
+// a serving peer's idle deadline: the longest wait for rank 0's next request header (<= 0:
+// none).  Rank 0 aborting its communicators need not surface as an RCCL error on the peer,
+// whose pending receive would then wait forever; past this deadline the peer aborts and
+// h2g_comm_serve returns an error (rank 0 renews it with comm_keepalive when it idles)
+double g_serve_timeout_s = 0.0;
 
 struct Slot {
   bool busy = false;
@@ -165,6 +170,10 @@ Comm* usable(void* ctx) {
 
 int comm_set_timeout(double seconds) {
   g_timeout_s = seconds;
+  return H2G_OK;
+}
+int comm_set_serve_timeout(double seconds) {
+  g_serve_timeout_s = seconds;
   return H2G_OK;
 }
 
@@ -470,24 +479,36 @@ int comm_collect(void* ctx, uint64_t seq, uint64_t* partials, int32_t* is_identi
   return fail(H2G_ERR_STATE, "comm_collect: unknown MSM " + std::to_string(seq));
 }
 
-int comm_stop() {
-  Comm* c = usable(g_comm);
-  if (!c || c->rank != 0) return fail(H2G_ERR_STATE, "comm_stop: no (live) rank-0 communicator");
+// rank 0: one header of `op` to every peer, outside any MSM (no launch in flight)
+static int send_control(Comm* c, int64_t op, const char* what) {
   for (auto& s : c->slots)
-    if (s.busy) RCCHK(wait_event(c, s.done, "slab partials before stop"));
+    if (s.busy) RCCHK(wait_event(c, s.done, "slab partials before a control header"));
   const int W = c->world;
   int64_t* hh = c->h_hdr;  // slot 0's header row (no launch is in flight)
   for (int r = 1; r < W; r++) {
-    const int64_t h[5] = {COMM_OP_STOP, 0, 0, 0, 0};
+    const int64_t h[5] = {op, 0, 0, 0, 0};
     std::memcpy(hh + 5 * r, h, sizeof(h));
   }
   HIPCHK(hipMemcpyAsync(c->d_hdr + 5, hh + 5, (size_t)(W - 1) * 5 * 8, hipMemcpyHostToDevice, c->stx));
   NCCLQ(c, c->tx, ncclGroupStart());
   for (int r = 1; r < W; r++) NCCLQ(c, c->tx, ncclSend(c->d_hdr + 5 * r, 5 * 8, ncclUint8, r, c->tx, c->stx));
   NCCLQ(c, c->tx, ncclGroupEnd());
-  RCCHK(wait_stream(c, c->stx, "stop headers", g_timeout_s));
+  RCCHK(wait_stream(c, c->stx, what, g_timeout_s));
+  return H2G_OK;
+}
+
+int comm_stop() {
+  Comm* c = usable(g_comm);
+  if (!c || c->rank != 0) return fail(H2G_ERR_STATE, "comm_stop: no (live) rank-0 communicator");
+  RCCHK(send_control(c, COMM_OP_STOP, "stop headers"));
   for (auto& s : c->slots) s.busy = false;
   return H2G_OK;
+}
+
+int comm_keepalive() {
+  Comm* c = usable(g_comm);
+  if (!c || c->rank != 0) return fail(H2G_ERR_STATE, "comm_keepalive: no (live) rank-0 communicator");
+  return send_control(c, COMM_OP_PING, "keep-alive headers");
 }
 
 int comm_next_request(int32_t* op, int32_t* base_set, uint64_t* lo, uint64_t* count, const void** d_slab,
@@ -496,8 +517,9 @@ int comm_next_request(int32_t* op, int32_t* base_set, uint64_t* lo, uint64_t* co
   if (!c || c->rank == 0) return fail(H2G_ERR_STATE, "comm_next_request: no (live) peer communicator");
   NCCLQ(c, c->tx, ncclRecv(c->d_rhdr, 5 * 8, ncclUint8, 0, c->tx, c->stx));
   HIPCHK(hipMemcpyAsync(c->h_rhdr, c->d_rhdr, 5 * 8, hipMemcpyDeviceToHost, c->stx));
-  // no deadline here: rank 0 decides when the next request comes (RCCL errors still end it)
-  RCCHK(wait_stream(c, c->stx, "next request header", 0.0));
+  // the serve loop's idle deadline (rank 0 decides when the next request comes; it renews
+  // the deadline with keep-alive headers while idle): past it rank 0 is taken to be gone
+  RCCHK(wait_stream(c, c->stx, "next request header from rank 0", g_serve_timeout_s));
   const int64_t* h = c->h_rhdr;
   *op = (int32_t)h[0];
   *base_set = (int32_t)h[2];

@@ -20,12 +20,16 @@
 namespace h2g {
 namespace rt {
 
-enum { COMM_OP_STOP = 0, COMM_OP_MSM = 1 };
+enum { COMM_OP_STOP = 0, COMM_OP_MSM = 1, COMM_OP_PING = 2 };
 static constexpr int COMM_ID_BYTES = 256;  // two ncclUniqueIds (tx, rx)
 
 int comm_unique_id(uint8_t id[COMM_ID_BYTES]);
 int comm_init(const uint8_t id[COMM_ID_BYTES], int world, int rank);
 int comm_set_timeout(double seconds);  // deadline of every RCCL wait (<= 0: none)
+// a peer's longest wait for rank 0's next request in the serve loop (<= 0: none); rank 0
+// renews it with comm_keepalive while it idles between proofs
+int comm_set_serve_timeout(double seconds);
+int comm_keepalive();  // rank 0: a PING header to every peer
 int comm_destroy();
 int comm_world();
 int comm_rccl_info(int* count, int* rank);

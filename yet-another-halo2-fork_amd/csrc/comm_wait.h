@@ -46,5 +46,29 @@ int poll_until(P&& poll, double timeout_s, Clock now = Clock(), Sleep sleep = Sl
   }
 }
 
+// A serving peer's loop (h2g_comm_serve, shard mode): rank 0's requests until its STOP.
+// next(&op) waits for the next header -- against the serve loop's idle deadline, so a rank 0
+// that aborted or died ends the loop with next's nonzero status instead of a wait that never
+// returns; PING headers (rank 0's keep-alive while it idles) only renew that deadline;
+// answer() serves one MSM request.  Returns 0 (and *served) after STOP, else the failing
+// call's status.
+enum Req { REQ_STOP = 0, REQ_MSM = 1, REQ_PING = 2 };
+template <class Next, class Answer>
+int serve_requests(Next&& next, Answer&& answer, unsigned long long* served) {
+  unsigned long long count = 0;
+  for (;;) {
+    int op = REQ_STOP;
+    const int rc = next(&op);
+    if (rc != 0) return rc;
+    if (op == REQ_STOP) break;
+    if (op == REQ_PING) continue;
+    const int ra = answer(op);
+    if (ra != 0) return ra;
+    count++;
+  }
+  if (served) *served = count;
+  return 0;
+}
+
 }  // namespace commwait
 }  // namespace h2g

@@ -23,7 +23,10 @@
 #include <set>
 #include <thread>
 
+#include <unistd.h>
+
 #include "comm.h"
+#include "comm_wait.h"
 #include "poly.h"
 #include "radix.h"
 #include "g2.h"
@@ -122,7 +125,12 @@ int params_prefix_build(Params& p, hipStream_t st, size_t lo, size_t hi, MsmFixe
 // before set-2 MSMs over [off, off + n): the slab's windows serve it if they exist, else the
 // full windows, built here if nothing built them earlier (a fallback; normally a no-op)
 int params_prefix(Params& p, hipStream_t st, size_t off = 0, size_t n = 0) {
-  if (p.sgp.table && off >= p.slab_lo && off + n <= p.slab_hi && n > 0) return H2G_OK;
+  if (p.slab_hi > p.slab_lo && off >= p.slab_lo && off + n <= p.slab_hi && n > 0) {
+    // inside this rank's slab: the slab's windows, built on first use (not in
+    // h2g_params_set_slab, so params used without lookups never pay for them)
+    if (!p.sgp.table) RCCHK(params_prefix_build(p, st, p.slab_lo, p.slab_hi, &p.sgp));
+    return H2G_OK;
+  }
   if (p.fgp.table) return H2G_OK;
   return params_prefix_build(p, st, 0, p.n, &p.fgp);
 }
@@ -333,6 +341,7 @@ std::map<uint64_t, std::unique_ptr<Params>> g_params;
 std::map<uint64_t, std::unique_ptr<ProvingKey>> g_pks;
 std::vector<std::pair<const char*, double>> g_stages;
 bool g_stage_sync = false;  // h2g_prover_stage_sync: stage times = GPU completion times
+bool g_comm_overlap = false;  // h2g_comm_set_exchange_overlap: column exchanges on the second communicator
 
 // ------------------------------------------------------------------ host field helpers
 int fr_cmp(const Fr& a, const Fr& b) {  // Ord on Fr: canonical numeric order
@@ -400,21 +409,27 @@ int build_pow_table(Pool& pool, const Fr& w, int L, PowTable* t, hipStream_t st)
   return H2G_OK;
 }
 
-// Debug aid: H2G_DUMP=<dir> writes named intermediates (raw Fr arrays) of create_proof.
+// Debug aid: a build with -DH2G_DUMP_DIR='"<dir>"' writes named intermediates (raw Fr
+// arrays) of create_proof to <dir>/p<pid>/<name>.bin, one directory per process (rank); no
+// run-time switch in the shipped library
 void dump(const char* name, const Fr* dptr, size_t count, hipStream_t st, bool host = false) {
-  static const char* dir = std::getenv("H2G_DUMP");
-  if (!dir) return;
+#ifndef H2G_DUMP_DIR
+  (void)name, (void)dptr, (void)count, (void)st, (void)host;
+  return;
+#else
+  const std::string dir = std::string(H2G_DUMP_DIR) + "/p" + std::to_string((long)getpid());
   std::vector<Fr> h(count);
   if (host) std::memcpy(h.data(), dptr, count * sizeof(Fr));
   else {
     (void)hipStreamSynchronize(st);
     (void)hipMemcpy(h.data(), dptr, count * sizeof(Fr), hipMemcpyDeviceToHost);
   }
-  const std::string path = std::string(dir) + "/" + name + ".bin";
+  const std::string path = dir + "/" + name + ".bin";
   if (FILE* f = std::fopen(path.c_str(), "wb")) {
     std::fwrite(h.data(), sizeof(Fr), count, f);
     std::fclose(f);
   }
+#endif
 }
 
 // ParamsKZG::commit / commit_lagrange (kzg/commitment.rs:305-317,354-366): MSM against a
@@ -700,11 +715,14 @@ int commit_collect_all(Device* d, MsmTicket* const* t, int nb, G1Affine* out) {
 #ifndef H2G_MSM_BATCH_ENTRIES  // A/B builds (tools/build_variant.py --src prover.cpp -D...)
 #define H2G_MSM_BATCH_ENTRIES (1ull << 27)
 #endif
+#ifndef H2G_MSM_BATCH_PER  // the largest MSM (sorted entries) that is batched
+#define H2G_MSM_BATCH_PER (1ull << 25)
+#endif
 int commit_batch_chunk(const MsmFixedBase& tb, size_t n) {
   const uint64_t max_entries = H2G_MSM_BATCH_ENTRIES;
   if (g_shard.world > 1) return 1;
   const uint64_t per = (uint64_t)tb.W * (n ? n : 1);
-  if (per > (1ull << 25)) return 1;
+  if (per > H2G_MSM_BATCH_PER) return 1;
   return (int)std::max<uint64_t>(1, std::min<uint64_t>(MSM_MAX_BATCH, max_entries / per));
 }
 
@@ -1651,16 +1669,25 @@ int xp_flush(ProvingKey& pk, hipStream_t st) {
   return H2G_OK;
 }
 
-// a failed proof's exchanges still in flight: wait for them (bounded) before their staging
-// is reused or freed
+// a failed proof's exchanges still in flight: wait for them before their staging is reused
+// or freed -- one bound for all of them together (10 s), and an exchange still pending past
+// it is abandoned, not reused: its staging and event are dropped (the key's pool releases
+// the memory with the key) so that the next proof posts into fresh buffers a late transfer
+// cannot write
 void xp_drain(ProvingKey& pk) {
+  const auto t0 = std::chrono::steady_clock::now();
   for (ProvingKey::XPending& x : pk.xp) {
     if (!x.live) continue;
     x.live = false;
-    const auto t0 = std::chrono::steady_clock::now();
     while (hipEventQuery(x.done) == hipErrorNotReady &&
            std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10))
       std::this_thread::sleep_for(std::chrono::microseconds(200));
+    if (hipEventQuery(x.done) == hipErrorNotReady) {
+      x.send = x.recv = nullptr;
+      x.send_len = x.recv_len = 0;
+      x.done = nullptr;  // a new event for the next post (the pending one is left to the runtime)
+      x.unpack.clear();
+    }
   }
   pk.xp_used = 0;
 }
@@ -2371,7 +2398,19 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     return H2G_OK;
   };
   std::vector<char> adv_shard((size_t)ncirc * pk.A, 0);  // advice columns distributed by their owners
+  // advice handed over in host memory: the first column's upload has nothing to overlap
+  // (its MSM needs the whole column), so the random polynomial's commitment goes first and
+  // runs under that upload; device-resident advice keeps it behind the advice commitments
+  // (H2G_VAN_FIRST=1: first in both cases -- A/B builds)
+#ifndef H2G_VAN_FIRST
+#define H2G_VAN_FIRST 0
+#endif
+#ifndef H2G_VAN_POS
+#define H2G_VAN_POS 0
+#endif
+  const bool van_first = early_van && (!in.adv_dev || H2G_VAN_FIRST);
   for (int ph = 0; ph <= pk.max_phase; ph++) {
+    if (ph == 0 && van_first) RCCHK(launch_van_early());
     std::vector<int> cols;
     for (int c = 0; c < pk.A; c++)
       if (pk.adv_phase[c] == ph) cols.push_back(c);
@@ -2473,6 +2512,9 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       }
     }
     if (digest) RCCHK(spmd_witness_fold(pk, (int)(ncirc * cols.size()), st));
+    // H2G_VAN_POS 1: the random polynomial's commitment right behind the advice commitments,
+    // ahead of the advice transforms on the prover's stream (0: behind them)
+    if (ph == 0 && early_van && !van_first && H2G_VAN_POS == 1) RCCHK(launch_van_early());
     std::vector<int> adv_owner;
     std::vector<const Fr*> adv_lag;
     std::vector<Fr*> adv_poly, adv_cst;
@@ -2521,7 +2563,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       for (int ci = 0; ci < ncirc; ci++)
         for (int c : cols) adv_shard[(size_t)ci * pk.A + c] = 1;
     }
-    if (ph == 0 && early_van) RCCHK(launch_van_early());
+    if (ph == 0 && early_van && !van_first && H2G_VAN_POS == 0) RCCHK(launch_van_early());
     if (ph == 0) clk.mark("upload+instances");
     {  // circuit by circuit, column by column
       std::vector<MsmTicket*> tl;
@@ -4633,9 +4675,9 @@ int h2g_params_set_slab(uint64_t params, uint64_t lo, uint64_t hi) {
   if (hi == lo || (lo == 0 && hi == prm.n)) return H2G_OK;  // none / the full tables
   HIPCHK(msm_fixed_base_build(prm.g + lo, hi - lo, 0, &prm.sg, d->stream));
   HIPCHK(msm_fixed_base_build(prm.gl + lo, hi - lo, 0, &prm.sgl, d->stream));
-  // the lookup basis's windows for the slab too (a peer serving set-2 slabs
-  // would otherwise build the full-size table inside its first request)
-  RCCHK(params_prefix_build(prm, d->stream, lo, hi, &prm.sgp));
+  HIPCHK(hipStreamSynchronize(d->stream));
+  // the lookup basis's windows for the slab (sgp) are built on the first set-2 MSM inside
+  // the slab (params_prefix), so a peer serving set-2 slabs never builds the full-size table
   prm.slab_lo = lo;
   prm.slab_hi = hi;
   return H2G_OK;
@@ -4716,14 +4758,32 @@ int h2g_comm_destroy(void) {
   return comm_destroy();
 }
 
+int h2g_comm_set_exchange_overlap(int on) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  g_comm_overlap = on != 0;
+  return H2G_OK;
+}
+
+int h2g_comm_set_serve_timeout(double seconds) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  return comm_set_serve_timeout(seconds);
+}
+
+int h2g_comm_keepalive(void) {
+  NEED_DEV_P();
+  return comm_keepalive();
+}
+
 int h2g_comm_spmd_install(int split_subcosets) {
   NEED_DEV_P();
   if (comm_world() < 2) return fail(H2G_ERR_STATE, "comm_spmd_install: needs a communicator (h2g_comm_init)");
   g_spmd = h2g_spmd_transport{comm_spmd_ctx(), comm_world(), comm_rank(), comm_allgather_partial,
                               split_subcosets ? comm_bcast : nullptr, comm_allgather_host,
                               split_subcosets ? comm_exchange : nullptr};
-  // the column-ownership exchanges overlap the later stages (second communicator)
-  g_xpost = split_subcosets && !std::getenv("H2G_SYNC_EXCHANGE") ? comm_exchange_post : nullptr;
+  // the column-ownership exchanges overlap the later stages on the second communicator
+  // only when asked (h2g_comm_set_exchange_overlap): two communicators in flight from two
+  // streams has not run on multi-GPU hardware yet, so blocking is the default
+  g_xpost = split_subcosets && g_comm_overlap ? comm_exchange_post : nullptr;
   g_xwait = g_xpost ? comm_exchange_wait : nullptr;
   g_shard = h2g_shard_transport{nullptr, 1, nullptr, nullptr};
   g_spmd_seq = 0;
@@ -4761,17 +4821,25 @@ int h2g_comm_serve(uint64_t params, uint64_t* served) {
   if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
   Params& prm = *ip->second;
   if (prm.device != d->id) return fail(H2G_ERR_ARG, "comm_serve: params live on another device");
-  uint64_t count = 0;
-  for (;;) {
-    int32_t op = 0, set = 0;
-    uint64_t lo = 0, cnt = 0;
-    const void* slab = nullptr;
-    hipStream_t ready = nullptr;
-    RCCHK(comm_next_request(&op, &set, &lo, &cnt, &slab, &ready));
-    if (op == COMM_OP_STOP) break;
+  static_assert(COMM_OP_STOP == commwait::REQ_STOP && COMM_OP_MSM == commwait::REQ_MSM &&
+                    COMM_OP_PING == commwait::REQ_PING,
+                "serve loop request codes");
+  int32_t set = 0;
+  uint64_t lo = 0, cnt = 0;
+  const void* slab = nullptr;
+  hipStream_t ready = nullptr;
+  auto next = [&](int* op) -> int {  // the idle deadline applies (h2g_comm_set_serve_timeout)
+    int32_t o = 0;
+    RCCHK(comm_next_request(&o, &set, &lo, &cnt, &slab, &ready));
+    *op = o;
+    return H2G_OK;
+  };
+  auto answer = [&](int op) -> int {
     if (op != COMM_OP_MSM || set < SRS_G || set > SRS_LAGRANGE_PREFIX || lo > prm.n || cnt > prm.n - lo)
       return fail(H2G_ERR_STATE, "comm_serve: malformed request");
-    if (set == SRS_LAGRANGE_PREFIX) RCCHK(params_prefix(prm, d->stream));
+    // the slab's windows of the prefix basis (built on the first set-2 request inside the
+    // slab), never the full-size table on a peer that only serves slabs
+    if (set == SRS_LAGRANGE_PREFIX) RCCHK(params_prefix(prm, d->stream, lo, cnt));
     uint64_t out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (cnt) {
       size_t toff = 0;
@@ -4782,8 +4850,10 @@ int h2g_comm_serve(uint64_t params, uint64_t* served) {
     uint64_t nz = 0;
     for (uint64_t v : out) nz |= v;
     RCCHK(comm_send_partial(out, nz == 0));
-    count++;
-  }
+    return H2G_OK;
+  };
+  unsigned long long count = 0;
+  RCCHK(commwait::serve_requests(next, answer, &count));
   if (served) *served = count;
   return H2G_OK;
 }

@@ -113,6 +113,9 @@ _SIGS = {
     "h2g_comm_unique_id": ([ctypes.c_char_p], I32),
     "h2g_comm_init": ([ctypes.c_char_p, I32, I32], I32),
     "h2g_comm_set_timeout": ([ctypes.c_double], I32),
+    "h2g_comm_set_serve_timeout": ([ctypes.c_double], I32),
+    "h2g_comm_keepalive": ([], I32),
+    "h2g_comm_set_exchange_overlap": ([ctypes.c_int32], I32),
     "h2g_comm_install": ([U64], I32),
     "h2g_comm_serve": ([U64, ctypes.POINTER(U64)], I32),
     "h2g_comm_stop": ([], I32),
@@ -1016,8 +1019,11 @@ def set_spmd_exchange_async(post=None, wait=None):
             errs.append(e)
             return 1
 
-    cp, cw = SPMD_XPOST(_post), SPMD_XWAIT(_wait)
-    check(lib().h2g_set_spmd_exchange_async(ctypes.cast(cp, VP), ctypes.cast(cw, VP)))
+    # no wait callable: NULL, so the library itself waits on `done` (hipEventSynchronize in
+    # xp_flush) instead of a callback that returns before the transfer has landed
+    cp = SPMD_XPOST(_post)
+    cw = SPMD_XWAIT(_wait) if wait is not None else None
+    check(lib().h2g_set_spmd_exchange_async(ctypes.cast(cp, VP), ctypes.cast(cw, VP) if cw is not None else None))
     _xasync_keep = (cp, cw)
 
 
@@ -1083,6 +1089,21 @@ def comm_init(uid, world, rank):
 def comm_set_timeout(seconds):
     """deadline of every wait on the library's RCCL communicators (h2g_comm_set_timeout)"""
     check(lib().h2g_comm_set_timeout(float(seconds)))
+
+
+def comm_set_serve_timeout(seconds):
+    """a serving peer's idle deadline for rank 0's next request (h2g_comm_set_serve_timeout)"""
+    check(lib().h2g_comm_set_serve_timeout(float(seconds)))
+
+
+def comm_keepalive():
+    """rank 0: renew the serving peers' idle deadline (h2g_comm_keepalive)"""
+    check(lib().h2g_comm_keepalive())
+
+
+def comm_set_exchange_overlap(on):
+    """SPMD over the library's communicators: overlapped column exchanges (opt-in)"""
+    check(lib().h2g_comm_set_exchange_overlap(1 if on else 0))
 
 
 def comm_install(params):
