@@ -383,7 +383,12 @@ H2G_HD G1xyzz29 xyzz29_from_xyzz(const G1xyzz& p) {
 // flow from a fresh point to its fixpoint): every coordinate of p stays < 2^259.5, every
 // intermediate < 2^259.9, so the subtraction constants below (64 M, 32 M, 64 M, 16 M)
 // exceed what they subtract and every product's columns stay < 2^64.
-H2G_HD G1xyzz29 xyzz29_madd(const G1xyzz29& p, const F29& qx, const F29& qy) {
+// DBL = false drops the rare p == q branch (the doubling of q): *dbl is set instead and the
+// result is meaningless.  The accumulation's hot loop uses that form -- the doubling's
+// temporaries cost it 25 VGPRs, 3 waves per SIMD instead of 4 -- and redoes a chunk that
+// hit the case with the full form (msm_acc_repair_kernel).
+template <bool DBL = true>
+H2G_HD G1xyzz29 xyzz29_madd(const G1xyzz29& p, const F29& qx, const F29& qy, bool* dbl = nullptr) {
   using P = FqParams;
   if (xyzz29_is_identity(p)) {
     G1xyzz29 r;
@@ -399,10 +404,14 @@ H2G_HD G1xyzz29 xyzz29_madd(const G1xyzz29& p, const F29& qx, const F29& qy) {
   const F29 R = norm29(sub29<P, 64, 29>(S2, p.Y));
   if (is_zero29<P>(Pp)) {
     if (is_zero29<P>(R)) {  // p == q: double q (storage form, rare)
-      G1Affine a;
-      a.x = from29<P>(qx);
-      a.y = from29<P>(qy);
-      return xyzz29_from_xyzz(xyzz_mdbl(a));
+      if constexpr (DBL) {
+        G1Affine a;
+        a.x = from29<P>(qx);
+        a.y = from29<P>(qy);
+        return xyzz29_from_xyzz(xyzz_mdbl(a));
+      } else {
+        *dbl = true;
+      }
     }
     return xyzz29_identity();  // p == -q
   }

@@ -964,7 +964,8 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
                          {&ws->segs, std::max<size_t>((size_t)2 * m1 + nblk, 10 * (size_t)nblk_p + 32) * WB *
                                          sizeof(RedPoint)},
                          {&ws->windows, (size_t)(W > WB ? W : WB) * sizeof(G1xyzz)},
-                         {&ws->result, 16},                              // [0] items, [1] multi-item buckets
+                         // [0] items, [1] multi-item buckets, [4 ..] the accumulation's repair list
+                         {&ws->result, 16 + 4 * (1 + (size_t)MSM_REPAIR_CAP)},
                          {&ws->item_off, mcap * sizeof(uint4)},          // multi-item buckets
                          {&ws->total_items, icap * sizeof(RedPoint)}};     // items' partial sums
   for (int b = 0; b < 10; b++)
@@ -1048,7 +1049,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   }
   H2G_PHASE(2);
   H2G_PHASE(3);
-  H2G_TRY(msm_accumulate(d_bases, vals_out, koff, nbt, d_total, L, nchunks, whole, bnd, st));
+  H2G_TRY(msm_accumulate(d_bases, vals_out, koff, nbt, d_total, L, nchunks, whole, bnd, counters + 4, st));
   H2G_PHASE(4);
   if (nbt <= FIXUP_Q4_MAX)
     hipLaunchKernelGGL(msm_fixup_kernel<4>, dim3((unsigned)(((size_t)nbt * 4 + T - 1) / T)), dim3(T), 0, st,

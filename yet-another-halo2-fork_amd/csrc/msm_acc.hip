@@ -46,25 +46,30 @@ __device__ __forceinline__ AccPoint acc_identity() {
   return G1xyzz::identity();
 #endif
 }
-__device__ __forceinline__ AccPoint acc_madd(const AccPoint& acc, const G1Affine& pt) {
+template <bool SAFE>
+__device__ __forceinline__ AccPoint acc_madd(const AccPoint& acc, const G1Affine& pt, bool* dbl) {
 #if H2G_ACC29
   if (pt.is_identity()) return acc;
-  return xyzz29_madd(acc, to29(pt.x), to29(pt.y));
+  return xyzz29_madd<SAFE>(acc, to29(pt.x), to29(pt.y), dbl);
 #else
+  (void)dbl;
   return xyzz_madd_lazy(acc, pt);
 #endif
 }
 
-// the next entry's base point is loaded before the current mixed addition
-// (software-pipelined gather), so its latency hides behind ~3000 VALU ops
-__global__ void __launch_bounds__(MSM_THREADS)
-msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ vals,
-               const uint32_t* __restrict__ koff, uint32_t nbt, const uint32_t* __restrict__ d_total, uint32_t L,
-               AccPoint* __restrict__ buckets, AccPoint* __restrict__ bnd) {
-  const uint32_t total = *d_total;  // entries (nonzero digits) of the partition
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+// one chunk [t L, t L + L) of the sorted values: the runs it holds to their buckets or to
+// its boundary slots.  SAFE = false: the mixed addition without its doubling branch (the
+// hot loop at 4 waves per SIMD); returns true when a run met p == q, and the chunk must be
+// redone with SAFE = true -- its writes go to the same places, every one of them rewritten.
+// The next entry's base point is loaded before the current mixed addition (software-
+// pipelined gather), so its latency hides behind ~3000 VALU ops.
+template <bool SAFE>
+__device__ __forceinline__ bool acc_chunk(uint32_t t, const G1Affine* __restrict__ bases,
+                                          const uint32_t* __restrict__ vals, const uint32_t* __restrict__ koff,
+                                          uint32_t nbt, uint32_t total, uint32_t L, AccPoint* __restrict__ buckets,
+                                          AccPoint* __restrict__ bnd) {
   const uint32_t lo = t * L;
-  if (lo >= total) return;
+  if (lo >= total) return false;
   const uint32_t hi = lo + L < total ? lo + L : total;
   // the bucket holding position lo: the largest k with koff[k] <= lo (an empty key shares
   // its offset with the next one, so the largest is the non-empty bucket; koff[nbt] = total)
@@ -76,7 +81,7 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ 
   }
   const bool prev_same = koff[key] < lo;
   uint32_t kend = koff[key + 1];
-  bool first = true;
+  bool first = true, dbl = false;
   AccPoint acc = acc_identity();
   uint32_t v = vals[lo];
   G1Affine pt = ld_aff(bases + (v & 0x7fffffffu));
@@ -106,19 +111,61 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ 
       acc = acc_identity();
     }
     if (v >> 31) pt = affine_neg(pt);
-    acc = acc_madd(acc, pt);
+    acc = acc_madd<SAFE>(acc, pt, &dbl);
     v = v_next;
     pt = pt_next;
   }
   msm_emit(key, acc, first, first && prev_same, kend > hi, t, buckets, bnd);
+  return dbl;
+}
+
+#ifndef H2G_ACC_FAST  // 0: the doubling branch inside the hot loop (152 VGPRs, 3 waves per SIMD; A/B)
+#define H2G_ACC_FAST 1
+#endif
+// the chunks whose runs met p == q (same point twice in a row of one bucket: repeated bases
+// of a generic MSM; never for distinct SRS points), recorded for the repair pass:
+// rep[0] = count, rep[1 ..] = chunk ids (up to MSM_REPAIR_CAP; beyond it every chunk is redone)
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ vals,
+               const uint32_t* __restrict__ koff, uint32_t nbt, const uint32_t* __restrict__ d_total, uint32_t L,
+               AccPoint* __restrict__ buckets, AccPoint* __restrict__ bnd, uint32_t* __restrict__ rep) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (acc_chunk<!H2G_ACC29 || !H2G_ACC_FAST>(t, bases, vals, koff, nbt, *d_total, L, buckets, bnd)) {
+    const uint32_t i = atomicAdd(rep, 1u);
+    if (i < MSM_REPAIR_CAP) rep[1 + i] = t;
+  }
+}
+
+// the flagged chunks again, with the doubling branch (a handful of threads; most launches
+// find no chunk and return at once)
+__global__ void __launch_bounds__(MSM_THREADS)
+msm_acc_repair_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ vals,
+                      const uint32_t* __restrict__ koff, uint32_t nbt, const uint32_t* __restrict__ d_total,
+                      uint32_t L, uint32_t nchunks, AccPoint* __restrict__ buckets, AccPoint* __restrict__ bnd,
+                      const uint32_t* __restrict__ rep) {
+  const uint32_t cnt = rep[0];
+  if (cnt == 0) return;
+  const uint32_t total = *d_total;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  if (cnt <= MSM_REPAIR_CAP) {
+    for (uint32_t i = g; i < cnt; i += stride) (void)acc_chunk<true>(rep[1 + i], bases, vals, koff, nbt, total, L,
+                                                                      buckets, bnd);
+  } else {
+    for (uint32_t t = g; t < nchunks; t += stride) (void)acc_chunk<true>(t, bases, vals, koff, nbt, total, L, buckets,
+                                                                         bnd);
+  }
 }
 
 hipError_t msm_accumulate(const G1Affine* bases, const uint32_t* vals, const uint32_t* koff, uint32_t nbt,
                           const uint32_t* d_total, uint32_t L, size_t nchunks, AccPoint* buckets, AccPoint* bnd,
-                          hipStream_t st) {
+                          uint32_t* rep, hipStream_t st) {
   const int T = MSM_THREADS;
   const unsigned cgrid = (unsigned)((nchunks + T - 1) / T);
-  hipLaunchKernelGGL(msm_acc_kernel, dim3(cgrid), dim3(T), 0, st, bases, vals, koff, nbt, d_total, L, buckets, bnd);
+  hipLaunchKernelGGL(msm_acc_kernel, dim3(cgrid), dim3(T), 0, st, bases, vals, koff, nbt, d_total, L, buckets, bnd,
+                     rep);
+  if (H2G_ACC29)
+    hipLaunchKernelGGL(msm_acc_repair_kernel, dim3(MSM_REPAIR_BLOCKS), dim3(T), 0, st, bases, vals, koff, nbt,
+                       d_total, L, (uint32_t)nchunks, buckets, bnd, (const uint32_t*)rep);
   return hipGetLastError();
 }
 

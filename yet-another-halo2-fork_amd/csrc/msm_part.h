@@ -111,9 +111,13 @@ __device__ __forceinline__ AccPoint ld_accp(const AccPoint* p) {
 
 // step 3 of the pipeline (msm_acc.hip): XYZZ accumulation of the bucket-sorted values in
 // chunks of L, one thread per chunk; bucket k's run is [koff[k], koff[k + 1]).  Whole buckets
-// go to buckets[k], runs crossing a chunk boundary to the chunk's slots bnd[2 t + 0/1]
+// go to buckets[k], runs crossing a chunk boundary to the chunk's slots bnd[2 t + 0/1].
+// rep (1 + MSM_REPAIR_CAP words, rep[0] zeroed by the partition): the chunks whose mixed
+// additions met p == q, redone by a second launch with the doubling branch
+static constexpr uint32_t MSM_REPAIR_CAP = 4096;
+static constexpr int MSM_REPAIR_BLOCKS = 64;
 hipError_t msm_accumulate(const G1Affine* bases, const uint32_t* vals, const uint32_t* koff, uint32_t nbt,
                           const uint32_t* d_total, uint32_t L, size_t nchunks, AccPoint* buckets, AccPoint* bnd,
-                          hipStream_t st);
+                          uint32_t* rep, hipStream_t st);
 
 }  // namespace h2g

@@ -78,6 +78,7 @@ msm_coarse_hist_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, 
   {  // the pipeline's other per-MSM zeroing (no separate fills)
     const size_t tid = (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * PT + threadIdx.x;
     if (tid < 2) z.counters[tid] = 0;
+    if (tid == 2) z.counters[4] = 0;  // the accumulation's repair count (msm_accumulate)
     if (tid < z.nrd) z.rdone[tid] = 0;
   }
   for (uint32_t t = threadIdx.x; t < ncoarse; t += PT) h[t] = 0;

@@ -3090,7 +3090,49 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     if (NST) dump("den0", W[0]->z_lag[0], n, st);
     HIPCHK(poly_batch_invert_multi(all_z_lag.data(), all_z.data(), NST, n, st));
     if (NST) dump("inv0", W[0]->z_lag[0], n, st);
-    for (int ci = 0; ci < ncirc; ci++) {
+#ifndef H2G_PERM_MULTI  // 1: every set's numerators, then ONE batched scan of all sets (A/B)
+#define H2G_PERM_MULTI 0
+#endif
+    if (H2G_PERM_MULTI && NST > 1) {
+      // the sets' running products do not depend on each other (z_s = z_{s-1}'s last usable
+      // value x its own scan): one batched scan of every set's products into z's coefficient
+      // arrays (free until the iNTT), then each z assembled from the previous set's last value
+      // on the device -- the same values, the same RNG draws in the same order
+      for (int ci = 0; ci < ncirc; ci++) {
+        Fr deltaomega = Fr::one();
+        for (int s = 0; s < pk.nsets; s++) {
+          const int c0 = s * pk.chunk_len, c1 = std::min(c0 + pk.chunk_len, pk.P);
+          for (int c = c0; c < c1; c += PERM_MAXC) {
+            PermCols pc;
+            pc.m = std::min(PERM_MAXC, c1 - c);
+            for (int j = 0; j < pc.m; j++) {
+              pc.v[j] = col_vals(*W[ci], c + j);
+              pc.beta_delta[j] = deltaomega * beta;
+              deltaomega = deltaomega * fr_delta();
+            }
+            HIPCHK(perm_numerators(W[ci]->z_lag[s], n, pc, gamma, pk.om, st));
+          }
+        }
+      }
+      HIPCHK(poly_prefix_product_multi((const Fr* const*)all_z_lag.data(), all_z.data(), NST, n, pk.scr, pk.scr_len,
+                                       st));
+      for (int ci = 0; ci < ncirc; ci++) {
+        CircuitWs& w = *W[ci];
+        HIPCHK(hipMemcpyAsync(pk.last_z, pk.one, sizeof(Fr), hipMemcpyDeviceToDevice, st));  // z_0 starts at one
+        for (int s = 0; s < pk.nsets; s++) {
+          const size_t i = (size_t)ci * pk.nsets + s;
+          Fr* blind_rows = perm_blind.data() + i * bf;
+          for (int q = 0; q < bf; q++) blind_rows[q] = rng.random_fr();
+          (void)rng.random_fr();  // blind
+          HIPCHK(pk_upload(pk, pk.small, blind_rows, bf * sizeof(Fr), st));
+          HIPCHK(perm_z_assemble(w.z_lag[s], n, bf, all_z[i], pk.last_z, pk.small, st));
+          HIPCHK(hipMemcpyAsync(pk.last_z, w.z_lag[s] + (n - (size_t)(bf + 1)), sizeof(Fr), hipMemcpyDeviceToDevice,
+                                st));
+          if (!perm_batched) RCCHK(commit_launch(d, prm, w.z_lag[s], n, SRS_LAGRANGE, st, &perm_tk[i]));
+        }
+      }
+    }
+    for (int ci = 0; ci < ncirc && !(H2G_PERM_MULTI && NST > 1); ci++) {
       CircuitWs& w = *W[ci];
       HIPCHK(hipMemcpyAsync(pk.last_z, pk.one, sizeof(Fr), hipMemcpyDeviceToDevice, st));  // z_0 starts at one
       Fr deltaomega = Fr::one();
