@@ -888,6 +888,65 @@ struct KatePow {
   Fr p[KD_L + 1];  // p[l] = b^(KD_S 2^l); p[KD_L] = b^KD_TILE
 };
 
+// Thread t's segment is KD_S consecutive coefficients, so a direct load by lane strides
+// KD_S x 32 B between lanes (a wave touches 64 lines per load and uses 32 B of each).  The
+// staged form (H2G_KATE_LDS) moves each segment's next KD_SUB coefficients for the whole
+// block through LDS: every run of KD_SUB x 32 B = 128 B is loaded by 8 lanes with 16-B
+// loads (whole lines), each thread then reads its own run from LDS -- rows padded to
+// 144 B so the 16 lanes of a ds_read_b128 hit distinct banks.  Phase 3 stages its stored
+// quotients (and, accumulating, the old ones) the same way.  Phase 3 only by default
+// (H2G_KATE_LDS 1; 2 stages phase 1 too): at 2^22 phase 3 96 vs 135 us (136 vs 152 us
+// accumulating); the read-only phase 1 was faster unstaged, 76 vs 85 us
+// (profiles/r06/kate/).
+#ifndef H2G_KATE_LDS
+#define H2G_KATE_LDS 1
+#endif
+#ifndef H2G_KD_SUB
+#define H2G_KD_SUB 4
+#endif
+static constexpr int KD_SUB = H2G_KD_SUB;          // coefficients per thread and stage
+static constexpr int KD_ROW = 2 * KD_SUB + 1;      // uint4 per thread row (+1 pad)
+struct KateStage {
+  uint4 v[KD_T * KD_ROW];
+};
+// the block's run c (coefficients lo_t + KD_SUB c .. + KD_SUB of every thread t) -> st; the
+// block's threads, 8 per run, each 16-B piece once; coefficients >= M read as zero
+template <int KD_S>
+__device__ __forceinline__ void kate_stage_load(KateStage& st, const Fr* __restrict__ src, uint64_t tile0, uint64_t M,
+                                                int c) {
+  constexpr int PER = 2 * KD_SUB;  // 16-B pieces per run
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int u = k * KD_T + threadIdx.x;  // piece u of the block's KD_T runs
+    const int tt = u / PER, r = u % PER;
+    const uint64_t j = tile0 + (uint64_t)tt * KD_S + (uint64_t)KD_SUB * c + (r >> 1);
+    st.v[tt * KD_ROW + r] = j < M ? reinterpret_cast<const uint4*>(src + j)[r & 1] : make_uint4(0, 0, 0, 0);
+  }
+}
+template <int KD_S>
+__device__ __forceinline__ void kate_stage_store(const KateStage& st, Fr* __restrict__ dst, uint64_t tile0,
+                                                 uint64_t M, int c) {
+  constexpr int PER = 2 * KD_SUB;
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int u = k * KD_T + threadIdx.x;
+    const int tt = u / PER, r = u % PER;
+    const uint64_t j = tile0 + (uint64_t)tt * KD_S + (uint64_t)KD_SUB * c + (r >> 1);
+    if (j < M) reinterpret_cast<uint4*>(dst + j)[r & 1] = st.v[tt * KD_ROW + r];
+  }
+}
+__device__ __forceinline__ Fr kate_stage_get(const KateStage& st, int t, int i) {
+  const uint4 a = st.v[t * KD_ROW + 2 * i], b = st.v[t * KD_ROW + 2 * i + 1];
+  Fr r;
+  r.l[0] = a.x, r.l[1] = a.y, r.l[2] = a.z, r.l[3] = a.w;
+  r.l[4] = b.x, r.l[5] = b.y, r.l[6] = b.z, r.l[7] = b.w;
+  return r;
+}
+__device__ __forceinline__ void kate_stage_put(KateStage& st, int t, int i, const Fr& v) {
+  st.v[t * KD_ROW + 2 * i] = make_uint4(v.l[0], v.l[1], v.l[2], v.l[3]);
+  st.v[t * KD_ROW + 2 * i + 1] = make_uint4(v.l[4], v.l[5], v.l[6], v.l[7]);
+}
+
 template <int KD_S>
 __global__ void __launch_bounds__(KD_T) kate_phase1(const Fr* __restrict__ a1, uint64_t M, Fr b, F29 b29, KatePow pw,
                                                     Fr* __restrict__ tile_val, Fr* __restrict__ thr_val) {
@@ -895,7 +954,19 @@ __global__ void __launch_bounds__(KD_T) kate_phase1(const Fr* __restrict__ a1, u
   const int t = threadIdx.x;
   const uint64_t lo = blockIdx.x * (uint64_t)(KD_T * KD_S) + (uint64_t)t * KD_S;
   Fr acc;
-  if constexpr (H2G_HORNER29) {
+  if constexpr (H2G_HORNER29 && H2G_KATE_LDS >= 2) {  // measured slower for phase 1 (85 vs 76 us at 2^22)
+    __shared__ KateStage stg;
+    const uint64_t tile0 = blockIdx.x * (uint64_t)(KD_T * KD_S);
+    F29 a29{};
+    for (int c = KD_S / KD_SUB - 1; c >= 0; c--) {
+      __syncthreads();  // the previous run's reads are done
+      kate_stage_load<KD_S>(stg, a1, tile0, M, c);
+      __syncthreads();
+#pragma unroll
+      for (int i = KD_SUB - 1; i >= 0; i--) a29 = add29(mul29<FrParams>(a29, b29), raw29(kate_stage_get(stg, t, i)));
+    }
+    acc = f29_to_storage(a29);
+  } else if constexpr (H2G_HORNER29) {
     F29 a29{};
 #pragma unroll
     for (int i = KD_S - 1; i >= 0; i--) {
@@ -966,6 +1037,34 @@ __global__ void __launch_bounds__(KD_T) kate_phase3(const Fr* __restrict__ a1, u
     __syncthreads();
   }
   const uint64_t lo = blockIdx.x * (uint64_t)(KD_T * KD_S) + (uint64_t)t * KD_S;
+  if constexpr (H2G_HORNER29 && H2G_KATE_LDS) {
+    // staged: run c's coefficients in, its quotients out (and the old ones in, ACC) through
+    // LDS, every global access whole lines; the carried value stays unreduced (< 2.1 M)
+    // (a thread reads and writes only its own row: without ACC the quotients overwrite the
+    // coefficients they come from; with it the old quotients have a buffer of their own)
+    __shared__ KateStage stg;
+    KateStage* out = &stg;
+    if constexpr (ACC) {
+      __shared__ KateStage old;
+      out = &old;
+    }
+    const uint64_t tile0 = blockIdx.x * (uint64_t)(KD_T * KD_S);
+    F29 cur = raw29(x);
+    for (int c = KD_S / KD_SUB - 1; c >= 0; c--) {
+      __syncthreads();  // the previous run's reads and its coalesced stores are done
+      kate_stage_load<KD_S>(stg, a1, tile0, M, c);
+      if (ACC) kate_stage_load<KD_S>(*out, q, tile0, M, c);
+      __syncthreads();
+#pragma unroll
+      for (int i = KD_SUB - 1; i >= 0; i--) {
+        cur = add29(raw29(kate_stage_get(stg, t, i)), mul29<FrParams>(cur, b29));
+        kate_stage_put(*out, t, i, f29_to_storage(ACC ? add29(raw29(kate_stage_get(*out, t, i)), cur) : cur));
+      }
+      __syncthreads();
+      kate_stage_store<KD_S>(*out, q, tile0, M, c);
+    }
+    return;
+  }
   if constexpr (H2G_HORNER29) {
     // the carried value stays unreduced (< 2.1 M); each stored quotient is reduced
     F29 cur = raw29(x);
