@@ -250,9 +250,12 @@ def pmc_traffic(args):
         return None, "rocprofv3 not found"
     vals = {}
     env = dict(os.environ, TMPDIR="/tmp")
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = tempfile.mkdtemp(prefix=f"h2g_pmc_{ctr}_", dir="/tmp")
-        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
+    # one pass per TCC counter (FETCH_SIZE and WRITE_SIZE cannot share one), then one pass
+    # of 5 SQ counters (8 SQ slots): where the accumulation's wave cycles go
+    sq_ctrs = ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_INSTS_VALU")
+    for ctrs in (("FETCH_SIZE",), ("WRITE_SIZE",), sq_ctrs):
+        d = tempfile.mkdtemp(prefix=f"h2g_pmc_{ctrs[0]}_", dir="/tmp")
+        cmd = [prof, "--pmc", *ctrs, "--output-format", "csv", "-d", d, "-o", "pmc", "--",
                sys.executable, os.path.abspath(__file__), "--pmc-child", "--workload", args.workload,
                "--log-n", str(args.log_n), "--k", str(args.k)]
         try:
@@ -263,16 +266,34 @@ def pmc_traffic(args):
                 for f in files:
                     if f.endswith("counter_collection.csv"):
                         rows += [r for r in csv.DictReader(open(os.path.join(root, f)))
-                                 if "msm_acc_kernel" in r["Kernel_Name"] and r["Counter_Name"] == ctr]
-            if not rows:
-                return None, f"no {ctr} rows for msm_acc_kernel"
-            vals[ctr] = sum(float(r["Counter_Value"]) for r in rows) / len(rows)
+                                 if "msm_acc_kernel" in r["Kernel_Name"] and r["Counter_Name"] in ctrs]
+            for ctr in ctrs:
+                cr = [float(r["Counter_Value"]) for r in rows if r["Counter_Name"] == ctr]
+                if not cr:
+                    raise RuntimeError(f"no {ctr} rows for msm_acc_kernel")
+                vals[ctr] = sum(cr) / len(cr)
         except Exception as e:  # profiling is best-effort; the timed result stands alone
-            return None, f"{ctr} pass failed: {type(e).__name__}"
+            if ctrs == sq_ctrs:  # the traffic passes stand without the SQ one
+                vals["sq_error"] = f"SQ pass failed: {type(e).__name__}"
+                continue
+            return None, f"{ctrs[0]} pass failed: {type(e).__name__}"
         finally:
             shutil.rmtree(d, ignore_errors=True)
+    sq = None
+    if "SQ_WAVE_CYCLES" in vals and vals["SQ_WAVE_CYCLES"] > 0:
+        wc = vals["SQ_WAVE_CYCLES"]
+        sq = {"issue_stall_frac": round(vals["SQ_WAIT_INST_ANY"] / wc, 3),
+              "waitcnt_frac": round(vals["SQ_WAIT_ANY"] / wc, 3),
+              "active_frac": round(vals["SQ_ACTIVE_INST_ANY"] / wc, 3),
+              "valu_insts_per_launch": round(vals["SQ_INSTS_VALU"]),
+              "counters_per_launch": {c: round(vals[c]) for c in sq_ctrs},
+              "note": "SQ_WAIT_INST_ANY: a wave had an instruction ready but the VALU was taken (issue-bound); "
+                      "SQ_WAIT_ANY: parked on s_waitcnt (memory); SQ_ACTIVE_INST_ANY: issuing. The three add up "
+                      "to SQ_WAVE_CYCLES (MI355X guide, PMC slots)"}
+    elif "sq_error" in vals:
+        sq = {"error": vals["sq_error"]}
     # the raw counters (bytes); roofline_from_phases applies the calibration per access kind
-    return {"fetch": vals["FETCH_SIZE"] * 1024.0, "write": vals["WRITE_SIZE"] * 1024.0}, (
+    return {"fetch": vals["FETCH_SIZE"] * 1024.0, "write": vals["WRITE_SIZE"] * 1024.0, "sq": sq}, (
         f"rocprofv3 --pmc, mean per launch of msm_acc_kernel: FETCH_SIZE {vals['FETCH_SIZE']:.0f} KiB, WRITE_SIZE "
         f"{vals['WRITE_SIZE']:.0f} KiB.  Calibration (tools/microbench/pmc_calib.hip, profiles/r03/pmc_calibration.json): "
         "FETCH_SIZE counts one 64-B unit per read request -- 1.01 of random 64-B point gathers, 0.50 of a coalesced "
@@ -357,6 +378,8 @@ def roofline_from_phases(calls, phases, points_per_launch, traffic, traffic_note
                                          "9 x 29-bit limbs, the arithmetic the accumulation runs), measured "
                                          "before the timed region; the madd's 10 products counted as full "
                                          "products (its two squarings and one merged reduction are cheaper)"})
+    if traffic and traffic.get("sq"):  # where the accumulation's wave cycles go (PMC SQ pass)
+        out["valu"]["pmc"] = traffic["sq"]
     if traffic:  # PMC bytes per launch, calibrated per access kind (pmc_traffic)
         stream = madds * 4.0  # the u32 bucket-ordered values, read once
         cal = traffic["fetch"] + 0.5 * stream + traffic["write"]
@@ -444,7 +467,6 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     if one_proof:  # every wait on the library's RCCL communicators has a deadline (fail soft)
         h2g.comm_set_timeout(args.comm_timeout)
         h2g.comm_set_serve_timeout(args.comm_timeout)  # shard peers: rank 0's next request
-        h2g.comm_set_exchange_overlap(args.overlap_exchange)
     if native and shard:  # the library's own RCCL communicators (csrc/comm.cpp); the id travels over torch
         import torch as _t
         tdev = dev if dist.get_backend() == "nccl" else "cpu"
@@ -488,15 +510,26 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
     def step():
         proofs.append(pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr()))
 
-    # SPMD transport, first that proves on every rank: the library's RCCL communicator
-    # ("native"), torch.distributed over RCCL ("torch"), torch.distributed over the gloo
-    # group with host-staged exchanges ("host" -- the form the one-GPU tests exercise)
+    # SPMD transport, first that proves on every rank: the library's RCCL communicators
+    # with the column exchanges overlapped on the second one ("native"), the same with
+    # blocking exchanges ("native-sync"), torch.distributed over RCCL ("torch"),
+    # torch.distributed over the gloo group with host-staged exchanges ("host" -- the form
+    # the one-GPU tests exercise).  A transport "proves" when its first proof equals, on
+    # every rank, the single-GPU proof the rank made before (same key, witness and seed):
+    # a hang ends at the communicator deadline, a wrong exchange at the comparison.
     spmd_kind = {"kind": None}
+
+    native_setup_failed = {"v": False}
 
     def spmd_open(kind):
         nonlocal gather
-        if kind == "native":
-            spmd_native_init()
+        if kind.startswith("native"):
+            h2g.comm_set_exchange_overlap(kind == "native")
+            try:
+                spmd_native_init()
+            except Exception:
+                native_setup_failed["v"] = True  # the blocking form would fail the same way
+                raise
             h2g.comm_spmd_install(not args.no_subcosets)
         else:
             gather = h2g_dist.SpmdGather(dist, group=CTRL if kind == "host" else None,
@@ -504,7 +537,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             gather.install()
 
     def spmd_close(kind):
-        if kind == "native":
+        if kind.startswith("native"):
             h2g.comm_spmd_uninstall()
         else:
             gather.uninstall()
@@ -518,11 +551,23 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         h2g.comm_init(bytes(uid.numpy().tobytes()), world, rank)
 
     if spmd:
+        # ranks sharing a GPU (a gloo rehearsal on a smaller box): RCCL refuses them (a
+        # communicator per GPU), so the native kinds are not tried there
+        shared_gpus = torch.cuda.device_count() < world
         kinds = [kd for kd in args.spmd_transports.split(",")
-                 if (kd != "native" or args.transport == "native" or args.dist_backend == "gloo")
+                 if (not kd.startswith("native") or args.transport == "native" or
+                     (args.dist_backend == "gloo" and not shared_gpus))
+                 and (kd != "native" or not args.sync_exchange)
                  and (kd != "torch" or dist.get_backend() == "nccl")]
         notes = []
+        progress("spmd: this rank's single-GPU reference proof")
+        ref = pk.create_proof(wit=wit, advice_dev_ptr=adv.data_ptr())  # this rank alone
         for kind in kinds:
+            if kind == "native-sync" and int(ctrl_all_reduce(1 if native_setup_failed["v"] else 0, dist,
+                                                              dist.ReduceOp.MAX)):
+                notes.append("native-sync: skipped (the communicators could not be set up)")
+                continue
+            progress(f"spmd: trying the {kind} transport")
             ok = 1
             try:
                 spmd_open(kind)
@@ -530,17 +575,21 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
                     step()  # the first warm-up proof doubles as the transport check
                 finally:
                     spmd_close(kind)
+                if proofs[-1] != ref:
+                    ok = 0
+                    proofs.pop()
+                    notes.append(f"{kind}: proof bytes differ from this rank's single-GPU proof")
             except Exception as e:  # every rank learns of any failure and tries the next
                 ok = 0
                 notes.append(f"{kind}: {type(e).__name__}: {str(e)[:200]}")
             if int(ctrl_all_reduce(ok, dist, dist.ReduceOp.MIN)):
                 spmd_kind["kind"] = kind
                 break
-            if kind == "native":
+            if kind.startswith("native"):
                 h2g.comm_destroy()
         if spmd_kind["kind"] is None:
             raise RuntimeError("no SPMD transport proved on every rank: " + "; ".join(notes))
-        native = spmd_kind["kind"] == "native"
+        native = spmd_kind["kind"].startswith("native")
         if spmd_kind["kind"] == "host" and dist.get_backend() == "nccl":
             RCCL_SUSPECT = True
         if notes:
@@ -551,7 +600,7 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
         stops; spmd: every rank proves with the all-gather installed"""
         if spmd:
             kind = spmd_kind["kind"]
-            if kind == "native":
+            if kind.startswith("native"):
                 h2g.comm_spmd_install(not args.no_subcosets)
             else:
                 gather.install()
@@ -764,7 +813,13 @@ def run_prove(args, h2g, torch, dist, world, rank, dev, traffic, traffic_note):
             line["proof_bytes_equal_across_ranks"] = extra["ranks_equal"]
             line["config"]["spmd_slab_weights"] = spmd_weights["w"]
             line["per_rank"] = per_rank
-            line["transport"] = {"kind": spmd_kind["kind"], "torch_backend": dist.get_backend(),
+            line["transport"] = {"kind": spmd_kind["kind"],
+                                 "column_exchanges": ("overlapped (second RCCL communicator)"
+                                                      if spmd_kind["kind"] == "native" else
+                                                      "blocking" if spmd_kind["kind"] == "native-sync" else
+                                                      "deferred, host transport"),
+                                 "checked_against": "each rank's single-GPU proof (bytes equal)",
+                                 "torch_backend": dist.get_backend(),
                                  "torch_world": dist.get_world_size()}
             if native:
                 cnt, rk = h2g.comm_info()
@@ -1120,9 +1175,9 @@ def main():
                          "collective); past it they are aborted, the proof fails on that rank, and every "
                          "rank moves to the next transport of --spmd-transports")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--overlap-exchange", action="store_true",
-                    help="spmd over the library's RCCL communicators: post the column-ownership exchanges on the "
-                         "second communicator (overlapped); default blocking (not yet run on 2+ GPUs)")
+    ap.add_argument("--sync-exchange", action="store_true",
+                    help="spmd over the library's RCCL communicators: skip the overlapped column exchanges (the "
+                         "'native' transport) and start from 'native-sync' (blocking exchanges)")
     ap.add_argument("--cpu-reps", type=int, default=3, help="CPU baseline runs (median)")
     ap.add_argument("--no-cpu-faithful", action="store_true", help="skip the faithful-mode CPU baseline")
     ap.add_argument("--cpu-faithful-k", type=int, default=20, help="k of the faithful-mode CPU baseline")
@@ -1133,7 +1188,7 @@ def main():
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl", help=argparse.SUPPRESS)
     ap.add_argument("--transport", choices=("native", "torch"), default="native",
                     help="shard mode: libh2g's own RCCL communicators, or torch.distributed slabs (h2g_dist)")
-    ap.add_argument("--spmd-transports", default="native,torch,host",
+    ap.add_argument("--spmd-transports", default="native,native-sync,torch,host",
                     help="spmd: transports to try in order, the first that proves on every rank is used "
                          "(native = libh2g's RCCL communicator, torch = torch.distributed over RCCL, "
                          "host = torch.distributed over gloo with host-staged exchanges)")
