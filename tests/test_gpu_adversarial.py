@@ -169,3 +169,21 @@ def test_msm_single_point_all_buckets_near_p():
     want = O.msm_best(sc, bases, 8)
     assert np.array_equal(want, O.g1_mul(_bases([p])[0], O.fr_from_canonical(_u64((n * RM1) % B.R))[0]))
     assert np.array_equal(h2g.msm(sc, bases), want)
+
+
+def test_msm_repeated_point_beyond_the_repair_list():
+    """2^17 copies of one point with one scalar: every chunk of the accumulation meets
+    p == q, more chunks than the repair list holds (msm_acc.hip MSM_REPAIR_CAP), so the
+    repair launch redoes every chunk -- generic and fixed-base paths, against the oracle"""
+    p = _points_near_p(1, False)[0]
+    n = 1 << 17
+    bases = np.tile(_bases([p]), (n, 1))
+    r = np.random.default_rng(77)
+    sc = np.tile(O.random_fr(r, 1), (n, 1))
+    want = O.msm_best(sc, bases, 8)
+    assert np.array_equal(h2g.msm(sc, bases), want)
+    hb = h2g.base_descriptor(bases)
+    try:
+        assert np.array_equal(h2g.msm_with_cached_base(sc, hb), want)
+    finally:
+        h2g.descriptor_free(hb)

@@ -347,7 +347,7 @@ __global__ void __launch_bounds__(EH_T) evaluate_h29_kernel(EvalHArgs a, EvalH29
           const F29 v = eh_ld(a.perm_v[c] + idx);
           left = eh_mul(left, eh_add3n(v, eh_mul(k.beta, eh_ld(a.sigma[c] + idx)), k.gamma));
           right = eh_mul(right, eh_add3n(v, cur, k.gamma));
-          cur = eh_mul(cur, k.delta);
+          if (c + 1 < a.P) cur = eh_mul(cur, k.delta);  // delta^j beta X for the next column (none after the last)
         }
         acc = eh_horner(acc, k.y, eh_mul(eh_subn(left, right), la));
       }
