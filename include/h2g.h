@@ -47,6 +47,9 @@ int h2g_init(const int* devices, int ndev);
 int h2g_shutdown(void);
 int h2g_device_count(int* out);
 int h2g_set_device(int index); /* index into the h2g_init list */
+/* free / total device memory of the current device, after a device-wide synchronize
+ * (hipMemGetInfo): what a caller checks descriptor lifetimes against */
+int h2g_device_mem_info(uint64_t* free_bytes, uint64_t* total_bytes);
 
 /* ---- MsmAccel<G1Affine> (halo2_middleware/src/zal.rs:57-103) ----------------
  * msm(coeffs, base) -> C::Curve  (zal.rs:58; H2cEngine::msm = best_multiexp, zal.rs:136-138).
@@ -375,6 +378,11 @@ int h2g_params_set_slab(uint64_t params, uint64_t lo, uint64_t hi);
 /* peer side: MSM of n device scalars against params' base set [offset, offset + n) */
 int h2g_params_msm_dev(uint64_t params, int32_t base_set, uint64_t offset, uint64_t n, const void* d_scalars,
                        uint64_t out_affine[8], int32_t* out_is_identity);
+/* device bytes the params hold in fixed-base windows: out[0] g and g_lagrange (full), out[1]
+ * their slab windows, out[2] the prefix-summed Lagrange basis's full windows (built for a
+ * key with lookups, or on a set-2 MSM outside the slab), out[3] its slab windows (built on
+ * the first set-2 MSM inside the slab) -- a serving peer's footprint, observable */
+int h2g_params_table_bytes(uint64_t params, uint64_t out[4]);
 /* synchronous device-to-device copy (staging slabs for the transport) */
 int h2g_memcpy_dtod(void* d_dst, const void* d_src, size_t bytes);
 

@@ -19,9 +19,7 @@ def engine():
 
 
 def _free_bytes():
-    import torch
-    torch.cuda.synchronize()
-    return torch.cuda.mem_get_info()[0]
+    return h2g.device_mem_info()[0]
 
 
 def test_ten_thousand_descriptors_return_device_memory():

@@ -513,6 +513,17 @@ int h2g_device_count(int* out) {
   return H2G_OK;
 }
 
+int h2g_device_mem_info(uint64_t* free_bytes, uint64_t* total_bytes) {
+  NEED_DEV();
+  if (!free_bytes || !total_bytes) return fail(H2G_ERR_ARG, "device_mem_info: null output");
+  size_t f = 0, t = 0;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemGetInfo(&f, &t));
+  *free_bytes = f;
+  *total_bytes = t;
+  return H2G_OK;
+}
+
 int h2g_set_device(int index) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (index < 0 || index >= (int)g_devs.size()) return fail(H2G_ERR_ARG, "device index");

@@ -88,7 +88,7 @@ struct Params {
     msm_fixed_base_free(&sgp);
   }
   // windows and table offset serving the base range [off, off + n) of set 0 (g) / 1
-  // (g_lagrange) / 2 (the Lagrange prefix sums: full windows only)
+  // (g_lagrange) / 2 (the Lagrange prefix sums: the slab's windows once built, else full)
   const MsmFixedBase& tables(int set, size_t off, size_t n, size_t* table_off) const {
     if (sg.table && off >= slab_lo && off + n <= slab_hi && (set != 2 || sgp.table)) {
       *table_off = off - slab_lo;
@@ -109,8 +109,8 @@ struct Params {
 // the same commitment from scalars that are zero inside every run: the MSM's partition
 // drops zero digits at the source, so its work follows the number of runs, not n.
 // Windows of the prefix basis: for all n points (fgp; keygen builds them for keys with
-// lookups, outside any proof) or for the rank's slab (sgp; h2g_params_set_slab builds them
-// with sg / sgl, so a peer that only serves slabs never holds the full-size table).  Both
+// lookups, outside any proof) or for the rank's slab (sgp; built on the first set-2 MSM
+// inside the slab, so a peer that only serves slabs never holds the full-size table).  Both
 // need the prefix points of the whole basis (P_i sums every L_j below i), formed in scratch.
 int params_prefix_build(Params& p, hipStream_t st, size_t lo, size_t hi, MsmFixedBase* out) {
   G1Affine* pre = nullptr;
@@ -4722,6 +4722,22 @@ int h2g_params_set_slab(uint64_t params, uint64_t lo, uint64_t hi) {
   // the slab (params_prefix), so a peer serving set-2 slabs never builds the full-size table
   prm.slab_lo = lo;
   prm.slab_hi = hi;
+  return H2G_OK;
+}
+
+int h2g_params_table_bytes(uint64_t params, uint64_t out[4]) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  auto ip = g_params.find(params);
+  if (ip == g_params.end()) return fail(H2G_ERR_HANDLE, "unknown params");
+  if (!out) return fail(H2G_ERR_ARG, "params_table_bytes: null output");
+  const Params& p = *ip->second;
+  auto bytes = [](const MsmFixedBase& t) -> uint64_t {
+    return t.table ? (uint64_t)t.W * (uint64_t)t.n * sizeof(G1Affine) : 0;
+  };
+  out[0] = bytes(p.fg) + bytes(p.fgl);
+  out[1] = bytes(p.sg) + bytes(p.sgl);
+  out[2] = bytes(p.fgp);
+  out[3] = bytes(p.sgp);
   return H2G_OK;
 }
 

@@ -32,6 +32,7 @@ _SIGS = {
     "h2g_init": ([ctypes.POINTER(I32), I32], I32),
     "h2g_shutdown": ([], I32),
     "h2g_device_count": ([ctypes.POINTER(I32)], I32),
+    "h2g_device_mem_info": ([ctypes.POINTER(U64), ctypes.POINTER(U64)], I32),
     "h2g_set_device": ([I32], I32),
     "h2g_msm": ([U64P, U64P, SZ, U64P, ctypes.POINTER(I32)], I32),
     "h2g_msm_coeffs_descriptor": ([U64P, SZ, ctypes.POINTER(U64)], I32),
@@ -109,6 +110,7 @@ _SIGS = {
     "h2g_set_shard_transport": ([VP], I32),
     "h2g_params_set_slab": ([U64, U64, U64], I32),
     "h2g_params_msm_dev": ([U64, ctypes.c_int32, U64, U64, VP, U64P, ctypes.POINTER(ctypes.c_int32)], I32),
+    "h2g_params_table_bytes": ([U64, U64P], I32),
     "h2g_memcpy_dtod": ([VP, VP, SZ], I32),
     "h2g_comm_unique_id": ([ctypes.c_char_p], I32),
     "h2g_comm_init": ([ctypes.c_char_p, I32, I32], I32),
@@ -1132,6 +1134,20 @@ def comm_spmd_install(subcosets=True):
 
 def comm_spmd_uninstall():
     check(lib().h2g_comm_spmd_uninstall())
+
+
+def device_mem_info():
+    """(free, total) bytes of the current device (hipMemGetInfo after a synchronize)"""
+    f, t = U64(), U64()
+    check(lib().h2g_device_mem_info(ctypes.byref(f), ctypes.byref(t)))
+    return f.value, t.value
+
+
+def params_table_bytes(params):
+    """(full g/g_lagrange, their slab, full prefix basis, slab prefix basis) window bytes"""
+    out = np.zeros(4, dtype=np.uint64)
+    check(lib().h2g_params_table_bytes(params.handle, p64(out)))
+    return tuple(int(v) for v in out)
 
 
 def params_msm_dev(params, base_set, offset, n, d_scalars):
