@@ -187,3 +187,36 @@ def test_msm_repeated_point_beyond_the_repair_list():
         assert np.array_equal(h2g.msm_with_cached_base(sc, hb), want)
     finally:
         h2g.descriptor_free(hb)
+
+
+@pytest.mark.parametrize("kind", ["nibbles", "sparse", "one_window_dense"])
+@pytest.mark.parametrize("lg", [14, 17])
+def test_msm_few_entries_device_chunk_length(kind, lg):
+    """scalars that fill a fraction of the entry bound n W: 4-bit values (one window of
+    W), 1 % nonzero, and 2^16-bounded values -- the partition's last scan then picks a
+    shorter chunk length on the device (msm_part.h msm_chunk_len_dev) and every later
+    kernel reads it; generic and fixed-base paths, against the oracle"""
+    n = 1 << lg
+    r = np.random.default_rng(90 + lg)
+    bases = h2g.DevBuf(n * 64)
+    try:
+        h2g.srs_setup_dev(O.random_fr(r, 1)[0], n, bases.ptr)
+        bs = bases.download((n, 8))
+    finally:
+        bases.close()
+    if kind == "nibbles":
+        vals = r.integers(0, 16, size=n)
+    elif kind == "sparse":
+        vals = np.where(r.random(n) < 0.01, r.integers(1, 1 << 62, size=n), 0)
+    else:
+        vals = r.integers(1, 1 << 16, size=n)
+    can = np.zeros((n, 4), dtype=np.uint64)
+    can[:, 0] = vals.astype(np.uint64)
+    sc = O.fr_from_canonical(can)
+    want = O.msm_best(sc, bs, 8)
+    assert np.array_equal(h2g.msm(sc, bs), want), kind
+    hb = h2g.base_descriptor(bs)
+    try:
+        assert np.array_equal(h2g.msm_with_cached_base(sc, hb), want), kind
+    finally:
+        h2g.descriptor_free(hb)

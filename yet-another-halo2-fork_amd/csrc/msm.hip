@@ -340,10 +340,11 @@ static constexpr uint32_t MSM_SMALL_Q4 = 32;
 
 template <int Q>
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_fixup_kernel(const AccPoint* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t nbt, uint32_t L,
-                 const AccPoint* __restrict__ whole, RedPoint* __restrict__ buckets,
+msm_fixup_kernel(const AccPoint* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t nbt,
+                 const uint32_t* __restrict__ d_total, const AccPoint* __restrict__ whole, RedPoint* __restrict__ buckets,
                  MsmBigItem* __restrict__ items, uint4* __restrict__ multi, uint32_t* __restrict__ counters) {
   H2G_SETPRIO(H2G_PRIO_RED);
+  const uint32_t L = d_total[1];  // the accumulation's chunk length (msm_chunk_len_dev)
   const uint32_t b = (blockIdx.x * blockDim.x + threadIdx.x) / Q;
   const uint32_t lane = threadIdx.x & 63;
   const bool lead = (threadIdx.x % Q) == 0;
@@ -406,10 +407,12 @@ msm_fixup_kernel(const AccPoint* __restrict__ bnd, const uint32_t* __restrict__ 
 // MSM_GROUP lanes per item (4 items per wave, persistent grid): each lane sums up to
 // 4 strided pieces, then a log2(MSM_GROUP)-level tree in the wave's LDS slice.
 __global__ void __launch_bounds__(MSM_THREADS)
-msm_big_item_kernel(const AccPoint* __restrict__ bnd, const uint32_t* __restrict__ koff, uint32_t L,
-                    const MsmBigItem* __restrict__ items, const uint32_t* __restrict__ counters,
-                    RedPoint* __restrict__ partial, RedPoint* __restrict__ buckets) {
+msm_big_item_kernel(const AccPoint* __restrict__ bnd, const uint32_t* __restrict__ koff,
+                    const uint32_t* __restrict__ d_total, const MsmBigItem* __restrict__ items,
+                    const uint32_t* __restrict__ counters, RedPoint* __restrict__ partial,
+                    RedPoint* __restrict__ buckets) {
   H2G_SETPRIO(H2G_PRIO_RED);
+  const uint32_t L = d_total[1];
   __shared__ RedPoint sh[MSM_THREADS];
   const uint32_t nitems = counters[0];
   const uint32_t lane = threadIdx.x & 63, g = lane & (MSM_GROUP - 1);
@@ -861,6 +864,9 @@ void msm_free(MsmWorkspace* ws) {
     if (_e != hipSuccess) return _e;    \
   } while (0)
 
+#ifndef H2G_MSM_ADAPT  // A/B builds: 0 = the host's chunk length always (msm_chunk_len_dev off)
+#define H2G_MSM_ADAPT 1
+#endif
 uint32_t msm_chunk_len(size_t total, size_t nbt) {
   // ~4 resident waves per SIMD x 256 CUs x 64 lanes, several rounds deep ...
   uint64_t L = total / (256ull * 4 * 4 * 64 * 4);
@@ -905,8 +911,11 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   if (total >= 0x80000000ull) return hipErrorInvalidValue;  // u32 positions in the sorted array
   // buckets most windows can reach (fixed-base: 2^(base width - 1) of the balanced widths)
   const size_t nb_eff = (size_t)WB << ((fixed ? 255 / W : c) - 1);
+  // the host's chunk length; the device may pick a shorter one once the entries are
+  // counted (msm_chunk_len_dev), so everything chunk-sized takes the larger count
   const uint32_t L = item_len > 0 ? item_len : msm_chunk_len(total, nb_eff);
-  const size_t nchunks = (total + L - 1) / L;
+  const MsmChunkRule rule{L, item_len > 0 || !H2G_MSM_ADAPT ? 0u : 1u, (uint64_t)total, (uint64_t)nb_eff};
+  const size_t nchunks = msm_chunk_cap(rule);
   const uint32_t m1 = (NB + RG - 1) / RG;
   const bool red_q4 = (size_t)m1 * WB <= RED_Q4_MAX;
   const uint32_t nblk = red_q4 ? (m1 + Q4_GROUPS - 1) / Q4_GROUPS : (m1 + MSM_THREADS - 1) / MSM_THREADS;
@@ -1045,21 +1054,24 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     pa.ent = (uint64_t*)ws->ent;
     pa.out = vals_out;
     pa.z = MsmZero{counters, rdone, (uint32_t)WB};
+    pa.rule = rule;
     H2G_TRY(msm_partition(pa, st, prof));
   }
   H2G_PHASE(2);
   H2G_PHASE(3);
-  H2G_TRY(msm_accumulate(d_bases, vals_out, koff, nbt, d_total, L, nchunks, whole, bnd, counters + 4, st));
+  H2G_TRY(msm_accumulate(d_bases, vals_out, koff, nbt, d_total, nchunks, whole, bnd, counters + 4, st));
   H2G_PHASE(4);
   if (nbt <= FIXUP_Q4_MAX)
     hipLaunchKernelGGL(msm_fixup_kernel<4>, dim3((unsigned)(((size_t)nbt * 4 + T - 1) / T)), dim3(T), 0, st,
-                       (const AccPoint*)bnd, (const uint32_t*)koff, nbt, L, (const AccPoint*)whole, buckets, items,
-                       multi, counters);
+                       (const AccPoint*)bnd, (const uint32_t*)koff, nbt, (const uint32_t*)d_total,
+                       (const AccPoint*)whole, buckets, items, multi, counters);
   else
     hipLaunchKernelGGL(msm_fixup_kernel<1>, dim3((nbt + T - 1) / T), dim3(T), 0, st, (const AccPoint*)bnd,
-                       (const uint32_t*)koff, nbt, L, (const AccPoint*)whole, buckets, items, multi, counters);
+                       (const uint32_t*)koff, nbt, (const uint32_t*)d_total, (const AccPoint*)whole, buckets, items,
+                       multi, counters);
   hipLaunchKernelGGL(msm_big_item_kernel, dim3(MSM_BIG_BLOCKS), dim3(T), 0, st, (const AccPoint*)bnd,
-                     (const uint32_t*)koff, L, (const MsmBigItem*)items, (const uint32_t*)counters, ipart, buckets);
+                     (const uint32_t*)koff, (const uint32_t*)d_total, (const MsmBigItem*)items,
+                     (const uint32_t*)counters, ipart, buckets);
   hipLaunchKernelGGL(msm_big_combine_kernel, dim3(MSM_BIG_BLOCKS / 4), dim3(T), 0, st, (const uint4*)multi,
                      (const uint32_t*)counters, (const RedPoint*)ipart, buckets);
   H2G_PHASE(5);

@@ -127,10 +127,10 @@ __device__ __forceinline__ bool acc_chunk(uint32_t t, const G1Affine* __restrict
 // rep[0] = count, rep[1 ..] = chunk ids (up to MSM_REPAIR_CAP; beyond it every chunk is redone)
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ vals,
-               const uint32_t* __restrict__ koff, uint32_t nbt, const uint32_t* __restrict__ d_total, uint32_t L,
+               const uint32_t* __restrict__ koff, uint32_t nbt, const uint32_t* __restrict__ d_total,
                AccPoint* __restrict__ buckets, AccPoint* __restrict__ bnd, uint32_t* __restrict__ rep) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (acc_chunk<!H2G_ACC29 || !H2G_ACC_FAST>(t, bases, vals, koff, nbt, *d_total, L, buckets, bnd)) {
+  if (acc_chunk<!H2G_ACC29 || !H2G_ACC_FAST>(t, bases, vals, koff, nbt, d_total[0], d_total[1], buckets, bnd)) {
     const uint32_t i = atomicAdd(rep, 1u);
     if (i < MSM_REPAIR_CAP) rep[1 + i] = t;
   }
@@ -141,11 +141,10 @@ msm_acc_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ 
 __global__ void __launch_bounds__(MSM_THREADS)
 msm_acc_repair_kernel(const G1Affine* __restrict__ bases, const uint32_t* __restrict__ vals,
                       const uint32_t* __restrict__ koff, uint32_t nbt, const uint32_t* __restrict__ d_total,
-                      uint32_t L, uint32_t nchunks, AccPoint* __restrict__ buckets, AccPoint* __restrict__ bnd,
-                      const uint32_t* __restrict__ rep) {
+                      AccPoint* __restrict__ buckets, AccPoint* __restrict__ bnd, const uint32_t* __restrict__ rep) {
   const uint32_t cnt = rep[0];
   if (cnt == 0) return;
-  const uint32_t total = *d_total;
+  const uint32_t total = d_total[0], L = d_total[1], nchunks = (total + L - 1) / L;
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
   if (cnt <= MSM_REPAIR_CAP) {
     for (uint32_t i = g; i < cnt; i += stride) (void)acc_chunk<true>(rep[1 + i], bases, vals, koff, nbt, total, L,
@@ -157,15 +156,14 @@ msm_acc_repair_kernel(const G1Affine* __restrict__ bases, const uint32_t* __rest
 }
 
 hipError_t msm_accumulate(const G1Affine* bases, const uint32_t* vals, const uint32_t* koff, uint32_t nbt,
-                          const uint32_t* d_total, uint32_t L, size_t nchunks, AccPoint* buckets, AccPoint* bnd,
+                          const uint32_t* d_total, size_t nchunks_cap, AccPoint* buckets, AccPoint* bnd,
                           uint32_t* rep, hipStream_t st) {
   const int T = MSM_THREADS;
-  const unsigned cgrid = (unsigned)((nchunks + T - 1) / T);
-  hipLaunchKernelGGL(msm_acc_kernel, dim3(cgrid), dim3(T), 0, st, bases, vals, koff, nbt, d_total, L, buckets, bnd,
-                     rep);
+  const unsigned cgrid = (unsigned)((nchunks_cap + T - 1) / T);
+  hipLaunchKernelGGL(msm_acc_kernel, dim3(cgrid), dim3(T), 0, st, bases, vals, koff, nbt, d_total, buckets, bnd, rep);
   if (H2G_ACC29)
     hipLaunchKernelGGL(msm_acc_repair_kernel, dim3(MSM_REPAIR_BLOCKS), dim3(T), 0, st, bases, vals, koff, nbt,
-                       d_total, L, (uint32_t)nchunks, buckets, bnd, (const uint32_t*)rep);
+                       d_total, buckets, bnd, (const uint32_t*)rep);
   return hipGetLastError();
 }
 

@@ -1,6 +1,7 @@
 // msm_part.h -- the MSM pipeline's stages in their own translation units (the bucket
 // partition, msm_part.hip; the accumulation, msm_acc.hip), shared with msm.hip.
 #pragma once
+#include <algorithm>
 #include "msm.h"
 #include "f29.h"
 
@@ -40,6 +41,43 @@ struct MsmZero {
   uint32_t nrd;
 };
 
+// The accumulation's chunk length L (entries per thread).  The host picks it from the
+// entry bound n W nbatch (msm_chunk_len); the entries that exist are known only on the
+// device, after the partition, and small or sparse scalars leave far fewer: a batch of
+// 4-bit witness columns fills one window of 15 (1/15 of the bound), the lookup columns'
+// prefix-basis differences a few hundred entries per column.  With the host's L those
+// MSMs ran on a few waves per chip, each a long dependent chain of mixed additions
+// (keccak-style k = 18: 1.1-1.4 ms accumulations of 0.1-8 M entries).  So once the count
+// is known the partition's last scan picks L again (msm_chunk_len_dev): the host's L when
+// at least half the bound exists (dense scalars: unchanged), otherwise enough chunks for
+// 2^18 threads (4 waves per SIMD), never below 8 or above the host's L.  Every later
+// kernel reads L from d_total[1]; grids and boundary slots are sized for the most chunks
+// either choice can make (msm_chunk_cap).
+struct MsmChunkRule {
+  uint32_t Lh;      // the host's chunk length
+  uint32_t adapt;   // 0: keep Lh (an explicit item_len)
+  uint64_t bound;   // entry bound n W nbatch
+  uint64_t nb_eff;  // buckets the windows can reach (the host rule's quarter-bucket floor)
+};
+static constexpr int MSM_ADAPT_LG = 18;  // threads the device choice aims for (2^18)
+__host__ __device__ __forceinline__ uint32_t msm_chunk_len_dev(uint64_t actual, const MsmChunkRule& r) {
+  if (!r.adapt || 2 * actual > r.bound) return r.Lh;
+  uint64_t L = actual >> MSM_ADAPT_LG;
+  const uint64_t quarter = r.nb_eff ? actual / (4 * r.nb_eff) : 0;
+  if (L < quarter) L = quarter;
+  if (L < 8) L = 8;
+  if (L > r.Lh) L = r.Lh;
+  return (uint32_t)L;
+}
+// the most chunks msm_chunk_len_dev can make: the host's count, or ceil(a / L) with
+// L >= max(8, a >> 18), below 2^18 (1 + 1/8) + 1
+__host__ __forceinline__ size_t msm_chunk_cap(const MsmChunkRule& r) {
+  const size_t host = (size_t)((r.bound + r.Lh - 1) / r.Lh);
+  if (!r.adapt) return host;
+  const size_t dev = (size_t)std::min<uint64_t>((r.bound + 7) / 8, ((1ull << MSM_ADAPT_LG) * 9) / 8 + 1);
+  return host > dev ? host : dev;
+}
+
 // One partition of the MSM pipeline's entries: round 1 (coarse bins straight from the
 // scalars, into ent), phase event 1, round 2 (keys inside the bins: the values in bucket
 // order into out, koff[k] = the first position of key k's run, koff[nbt] = the entry
@@ -59,6 +97,7 @@ struct MsmPartArgs {
   uint64_t* ent;
   uint32_t* out;
   MsmZero z;
+  MsmChunkRule rule;  // d_total[1] = the accumulation's chunk length
 };
 hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* prof);
 
@@ -110,14 +149,15 @@ __device__ __forceinline__ AccPoint ld_accp(const AccPoint* p) {
 }
 
 // step 3 of the pipeline (msm_acc.hip): XYZZ accumulation of the bucket-sorted values in
-// chunks of L, one thread per chunk; bucket k's run is [koff[k], koff[k + 1]).  Whole buckets
+// chunks of L = d_total[1] (d_total[0]: the entries), one thread per chunk (a grid for
+// nchunks_cap); bucket k's run is [koff[k], koff[k + 1]).  Whole buckets
 // go to buckets[k], runs crossing a chunk boundary to the chunk's slots bnd[2 t + 0/1].
 // rep (1 + MSM_REPAIR_CAP words, rep[0] zeroed by the partition): the chunks whose mixed
 // additions met p == q, redone by a second launch with the doubling branch
 static constexpr uint32_t MSM_REPAIR_CAP = 4096;
 static constexpr int MSM_REPAIR_BLOCKS = 64;
 hipError_t msm_accumulate(const G1Affine* bases, const uint32_t* vals, const uint32_t* koff, uint32_t nbt,
-                          const uint32_t* d_total, uint32_t L, size_t nchunks, AccPoint* buckets, AccPoint* bnd,
+                          const uint32_t* d_total, size_t nchunks_cap, AccPoint* buckets, AccPoint* bnd,
                           uint32_t* rep, hipStream_t st);
 
 }  // namespace h2g

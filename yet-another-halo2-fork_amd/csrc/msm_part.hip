@@ -144,13 +144,17 @@ msm_scan_block_kernel(uint32_t* __restrict__ cnt, uint32_t len, uint32_t* __rest
   if (threadIdx.x == 1023) bsum[blockIdx.x] = part[1023];
 }
 // off[i] += block offset (= koff, the first position of key i's run), cursor = the same;
-// off[len] = the entry count
+// off[len] = the entry count, d_total[1] = the accumulation's chunk length (msm_chunk_len_dev)
 __global__ void __launch_bounds__(1024)
 msm_scan_add_kernel(uint32_t* __restrict__ off, uint32_t len, const uint32_t* __restrict__ boff,
-                    uint32_t* __restrict__ cursor, const uint32_t* __restrict__ d_total) {
+                    uint32_t* __restrict__ cursor, uint32_t* __restrict__ d_total, MsmChunkRule rule) {
   H2G_SETPRIO(H2G_PRIO_PART);
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
-  if (i == 0) off[len] = *d_total;
+  if (i == 0) {
+    const uint32_t tot = d_total[0];
+    off[len] = tot;
+    d_total[1] = msm_chunk_len_dev(tot, rule);
+  }
   if (i >= len) return;
   const uint32_t v = off[i] + boff[blockIdx.x];
   off[i] = v;
@@ -416,7 +420,7 @@ hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* p
     hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, a.kbsum, a.kblocks, a.kboff, (uint32_t*)nullptr,
                        (uint32_t*)nullptr, false);
     hipLaunchKernelGGL(msm_scan_add_kernel, dim3(a.kblocks), dim3(1024), 0, st, a.koff, a.nbt,
-                       (const uint32_t*)a.kboff, a.kcursor, (const uint32_t*)a.d_total);
+                       (const uint32_t*)a.kboff, a.kcursor, a.d_total, a.rule);
     if (fstage)
       hipLaunchKernelGGL(msm_fine_scatter_staged_kernel, dim3(stiles), dim3(SW_T), 0, st, (const uint64_t*)a.ent,
                          (const uint32_t*)a.d_total, a.fb, stiles, a.kcursor, a.out);
