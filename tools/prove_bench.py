@@ -1,7 +1,8 @@
 """Time the device create_proof on the C3 synthetic circuit or the C5-shaped
 keccak-style circuit at the given k values; prints per-stage wall times.
-usage: python tools/prove_bench.py [c3|keccak] [--dev] 20 22
---dev: the witness resident in HBM (bench.py's `value` path) instead of host memory"""
+usage: python tools/prove_bench.py [c3|keccak] [--dev] [--sync] 20 22
+--dev: the witness resident in HBM (bench.py's `value` path) instead of host memory
+--sync: the prover drains its streams at every stage mark (per-stage GPU time; slower)"""
 import os
 import sys
 import time
@@ -18,11 +19,16 @@ def main():
     args = sys.argv[1:]
     kind = "c3"
     dev = "--dev" in args
-    args = [a for a in args if a != "--dev"]
+    sync = "--sync" in args
+    args = [a for a in args if a not in ("--dev", "--sync")]
     if args and not args[0].isdigit():
         kind = args.pop(0)
     ks = [int(a) for a in args] or [20]
+    if dev:
+        import torch  # noqa: F401 -- before h2g.init (h2g.init: torch's HIP runtime first)
     h2g.init()
+    if sync:
+        h2g.prover_stage_sync(True)
     for k in ks:
         t0 = time.time()
         circ, wit = hc.synthetic_c3(k, h2g.DeviceOps) if kind == "c3" else hc.keccak_style(k)

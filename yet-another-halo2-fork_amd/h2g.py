@@ -7,6 +7,7 @@ device buffers are raw pointers (ints) from h2g_dev_alloc or torch tensors'
 data_ptr().
 """
 import ctypes
+import sys
 import os
 import re
 
@@ -185,7 +186,14 @@ _inited = False
 
 
 def init(devices=None):
+    """h2g_init.  libh2g runs on /opt/rocm's HIP runtime; a torch wheel carries its own
+    copy, and in one process the copy initialised second must be torch's (torch started
+    after libh2g finds no GPU: "No HIP GPUs are available").  So when the caller has
+    imported torch, its CUDA state is initialised first."""
     global _inited
+    tm = sys.modules.get("torch")
+    if tm is not None and tm.cuda.device_count() > 0:
+        tm.cuda.init()
     if devices:
         arr = (I32 * len(devices))(*devices)
         check(lib().h2g_init(arr, len(devices)))
