@@ -119,6 +119,9 @@ int get_tables(Device* d, const Fr& omega, int L, hipStream_t st, NttTables* out
   }
   NttTables t;
   hipError_t e = ntt_build_tables(&t, omega, L, st, fold);
+  // built once per key; finished before any stream may use it (the prover's transform
+  // stream and its own stream share the tables)
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) return hip_fail(e, "ntt_build_tables");
   d->ntt_tables[key] = t;
   *out = t;
@@ -200,16 +203,22 @@ int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_
   return H2G_OK;
 }
 
+// the asynchronous MSMs' streams, result ring and events (h2g_init creates them, right
+// after the device stream: see there)
+int msm_ring_init(Device* d) {
+  if (d->h_ring) return H2G_OK;
+  HIPCHK(hipHostMalloc(&d->h_ring, MSM_RING * sizeof(G1xyzz), hipHostMallocDefault));
+  for (int i = 0; i < MSM_STREAMS; i++) HIPCHK(hipStreamCreateWithFlags(&d->mstream[i], hipStreamNonBlocking));
+  for (int i = 0; i < MSM_RING; i++) HIPCHK(hipEventCreateWithFlags(&d->ring_ev[i], hipEventDisableTiming));
+  return H2G_OK;
+}
+
 // nb MSMs of n scalars each against the same fixed-base windows, launched as one batched
 // pipeline (msm_run_fixed_batch) on the next MSM stream; ticket b collects MSM b.
 int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFixedBase& fb, size_t off, size_t n,
                            hipStream_t producer, MsmTicket* t) {
   if (nb < 1 || nb > MSM_MAX_BATCH) return fail(H2G_ERR_ARG, "msm: bad batch size");
-  if (!d->h_ring) {
-    HIPCHK(hipHostMalloc(&d->h_ring, MSM_RING * sizeof(G1xyzz), hipHostMallocDefault));
-    for (int i = 0; i < MSM_STREAMS; i++) HIPCHK(hipStreamCreateWithFlags(&d->mstream[i], hipStreamNonBlocking));
-    for (int i = 0; i < MSM_RING; i++) HIPCHK(hipEventCreateWithFlags(&d->ring_ev[i], hipEventDisableTiming));
-  }
+  RCCHK(msm_ring_init(d));
   int rings[MSM_MAX_BATCH];
   int got = 0;
   for (int k = 0; k < MSM_RING && got < nb; k++) {
@@ -311,13 +320,15 @@ int ntt_dev_impl_batch(Device* d, const Fr* const* src, uint64_t n_in, Fr* const
   int rc = get_tables(d, omega, L, st, &a.tab, has_scale && L > NTT_SMALL_MAX_LOG ? scale : Fr::one());
   if (rc) return rc;
   const size_t N = (size_t)1 << L;
+  // the transform stream's NTTs run beside the prover stream's: each has its own work buffer
+  DevBuf& wb = d->xstream != nullptr && st == d->xstream ? d->xwork : d->work;
   if (L > NTT_SMALL_MAX_LOG) {
-    hipError_t e = d->work.ensure((size_t)count * N * sizeof(Fr));
+    hipError_t e = wb.ensure((size_t)count * N * sizeof(Fr));
     if (e != hipSuccess) return hip_fail(e, "ntt work buffer");
   }
   a.src = src[0];
   a.n_in = n_in;
-  a.work = reinterpret_cast<Fr*>(d->work.p);
+  a.work = reinterpret_cast<Fr*>(wb.p);
   a.dst = dst[0];
   a.count = count;
   for (int b = 0; b < count; b++) {
@@ -447,6 +458,9 @@ extern "C" {
 int h2g_abi_version(void) { return 1; }
 const char* h2g_last_error(void) { return g_err.c_str(); }
 
+#ifndef H2G_EAGER_STREAMS  // A/B builds: 0 = the MSM streams created by the first asynchronous MSM,
+#define H2G_EAGER_STREAMS 1   // the transform stream by the first proof that uses it
+#endif
 int h2g_init(const int* devices, int ndev) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   if (!g_devs.empty()) return H2G_OK;
@@ -461,7 +475,18 @@ int h2g_init(const int* devices, int ndev) {
     auto dev = std::make_unique<Device>();
     dev->id = id;
     HIPCHK(hipSetDevice(id));
+    // Streams in a fixed order: the device stream, the two MSM streams, the prover's
+    // transform stream (prove_impl).  With GPU_MAX_HW_QUEUES = 4 each takes the next
+    // hardware queue, and the order matters: C3 k = 22 ran 73.8 ms with the MSM streams on
+    // the second and third queue, 77.1 ms when an (idle) stream created before them pushed
+    // them to the third and fourth (profiles/r06/xs/ab_eager.log)
     HIPCHK(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
+    if (H2G_EAGER_STREAMS) {
+      RCCHK(msm_ring_init(dev.get()));
+      HIPCHK(hipStreamCreateWithFlags(&dev->xstream, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&dev->xev_in, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&dev->xev_done, hipEventDisableTiming));
+    }
     HIPCHK(ntt_init_attributes());
     g_devs.push_back(std::move(dev));
   }
@@ -482,6 +507,7 @@ int h2g_shutdown(void) {
   for (auto& dev : g_devs) {
     (void)hipSetDevice(dev->id);
     (void)hipStreamSynchronize(dev->stream);
+    if (dev->xstream) (void)hipStreamSynchronize(dev->xstream);
     msm_free(&dev->msm);
     for (int i = 0; i < MSM_STREAMS; i++)
       if (dev->mstream[i]) {
@@ -498,6 +524,10 @@ int h2g_shutdown(void) {
     dev->work.release();
     dev->out.release();
     for (auto& kv : dev->ntt_tables) ntt_free_tables(&kv.second);
+    if (dev->xstream) (void)hipStreamDestroy(dev->xstream);
+    if (dev->xev_in) (void)hipEventDestroy(dev->xev_in);
+    if (dev->xev_done) (void)hipEventDestroy(dev->xev_done);
+    dev->xwork.release();
     if (dev->h_windows) (void)hipHostFree(dev->h_windows);
     (void)hipStreamDestroy(dev->stream);
   }

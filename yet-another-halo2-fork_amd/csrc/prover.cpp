@@ -449,6 +449,19 @@ uint64_t g_spmd_seq = 0;
 #ifndef H2G_DEFER_ADV_XFORM
 #define H2G_DEFER_ADV_XFORM 1
 #endif
+// Single-GPU proofs: the columns' transforms (lagrange_to_coeff, the coset extension) on a
+// stream of their own (Device::xstream), joined before evaluate_h, their first reader.
+// On the prover's stream they held back every later stage's kernels -- the lookups'
+// sorts and grand products are chains of small launches that leave most of the chip idle,
+// and ran only after the 2^20-point transforms ahead of them on the stream (keccak-style
+// k = 18: the same 33.1 ms with every stage drained as without; 31.8-32.4 vs 33.3-34.3 ms
+// on their own stream, profiles/r06/xs/ab_ordered_streams.log).  Only for circuits with
+// lookups or shuffles: C3 (no lookups; its stages are MSM-bound, the chip already full)
+// measured 76.1-77.3 vs 73.1-73.8 ms with it.  The stream is created by h2g_init after the
+// MSM streams (the hardware-queue order matters, abi.cpp).  0: on the prover's stream.
+#ifndef H2G_XFORM_STREAM
+#define H2G_XFORM_STREAM 1
+#endif
 // overlapped exchanges (h2g_set_spmd_exchange_async); NULL post: exchanges complete on return
 h2g_spmd_exchange_post g_xpost = nullptr;
 h2g_spmd_exchange_wait g_xwait = nullptr;
@@ -2253,6 +2266,40 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   // which interpolate their sub-coset's h: C3 at 8 ranks puts its 6 column transforms on
   // ranks 2 .. 7 instead of stacking two roles on ranks 0 and 1)
   int tr_next = pieces ? E_sub : 0;
+  // the transform stream (H2G_XFORM_STREAM): xs_begin orders it after the prover stream's
+  // work so far (the inputs), xs_end marks its last transform, and the prover stream waits
+  // for that mark before evaluate_h -- and at the end of the proof whatever its outcome
+  // (XformJoin), so that the next proof's uploads never overtake a transform still reading
+  const bool xsplit = H2G_XFORM_STREAM && g_spmd.world <= 1 && !spmd_subcosets() && pk.NL + pk.NS > 0;
+  if (xsplit && !d->xstream) {  // (h2g_init made it, unless built with H2G_EAGER_STREAMS=0)
+    HIPCHK(hipStreamCreateWithFlags(&d->xstream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&d->xev_in, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&d->xev_done, hipEventDisableTiming));
+  }
+  const hipStream_t xst = xsplit ? d->xstream : st;
+  struct XformJoin {
+    Device* d;
+    hipStream_t st;
+    bool pending = false;
+    hipError_t join() {
+      if (!pending) return hipSuccess;
+      pending = false;
+      return hipStreamWaitEvent(st, d->xev_done, 0);
+    }
+    ~XformJoin() { (void)join(); }
+  } xjoin{d, st};
+  auto xs_begin = [&]() -> int {
+    if (xst == st) return H2G_OK;
+    HIPCHK(hipEventRecord(d->xev_in, st));
+    HIPCHK(hipStreamWaitEvent(xst, d->xev_in, 0));
+    return H2G_OK;
+  };
+  auto xs_end = [&]() -> int {
+    if (xst == st) return H2G_OK;
+    HIPCHK(hipEventRecord(d->xev_done, xst));
+    xjoin.pending = true;
+    return H2G_OK;
+  };
   auto xform = [&](const std::vector<const Fr*>& lag, const std::vector<Fr*>& pol, const std::vector<Fr*>& cst,
                    const std::vector<int>* own) -> int {
     const int M = (int)lag.size();
@@ -2263,8 +2310,10 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       if (!own) tr_next += M;
       return colshard_distribute(d, pk, lag, pol, cst, o, st);
     }
-    if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, lag.data(), pol.data(), M, st));
-    return ext_cosets(d, pk, (const Fr* const*)pol.data(), cst.data(), M, st);
+    RCCHK(xs_begin());
+    if (!coef_recv) RCCHK(lagrange_to_coeff_batch(d, D, lag.data(), pol.data(), M, xst));
+    RCCHK(ext_cosets(d, pk, (const Fr* const*)pol.data(), cst.data(), M, xst));
+    return xs_end();
   };
   // with row pieces the advice columns' transforms wait for the permutation stage: at the
   // advice commitments' all-gather every rank would otherwise wait for the ranks that
@@ -2555,8 +2604,10 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         cst.push_back(w.adv_coset[c]);
       }
       if (coef_recv) continue;  // coefficients from the owners (coef_exchange), no cosets
-      RCCHK(lagrange_to_coeff_batch(d, D, src.data(), dst.data(), (int)cols.size(), st));
-      RCCHK(ext_cosets(d, pk, (const Fr* const*)dst.data(), cst.data(), (int)cols.size(), st));
+      RCCHK(xs_begin());
+      RCCHK(lagrange_to_coeff_batch(d, D, src.data(), dst.data(), (int)cols.size(), xst));
+      RCCHK(ext_cosets(d, pk, (const Fr* const*)dst.data(), cst.data(), (int)cols.size(), xst));
+      RCCHK(xs_end());
     }
     if (adv_wide) {
       RCCHK(xform(adv_lag, adv_poly, adv_cst, &adv_owner));
@@ -3313,6 +3364,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   RCCHK(run_deferred());  // (no permutation stage ran them)
   RCCHK(xp_flush(pk, st));  // the overlapped exchanges' rows, before h(X) reads them
   clk.mark("perm+vanishing commits, cosets");
+  HIPCHK(xjoin.join());  // the columns' cosets and coefficients (the transform stream)
   const Fr y = tr.squeeze();
   // ---- evaluate_h (evaluation.rs:317-620): one launch per circuit, each continuing the
   // previous circuit's Horner chain in y; the last one divides by t(X)

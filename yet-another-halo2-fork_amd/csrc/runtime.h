@@ -119,6 +119,11 @@ struct Device {
   hipEvent_t ring_ev[MSM_RING] = {};
   bool ring_busy[MSM_RING] = {};
   int next_ring = 0;
+  // the prover's column-transform stream (prove_impl: xs) and its NTT work buffer -- an NTT
+  // on it must not share `work` with the prover's stream
+  hipStream_t xstream = nullptr;
+  DevBuf xwork;
+  hipEvent_t xev_in = nullptr, xev_done = nullptr;
 };
 
 extern std::vector<std::unique_ptr<Device>> g_devs;
@@ -153,6 +158,7 @@ int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_
 int msm_fixed_launch(Device* d, const void* sc, const MsmFixedBase& fb, size_t off, size_t n, hipStream_t producer,
                      MsmTicket* t);
 // nb (<= MSM_MAX_BATCH) MSMs against the same windows as one batched pipeline; t[nb]
+int msm_ring_init(Device* d);  // the asynchronous MSMs' streams, ring and events (once)
 int msm_fixed_launch_batch(Device* d, const void* const* sc, int nb, const MsmFixedBase& fb, size_t off, size_t n,
                            hipStream_t producer, MsmTicket* t);
 // wait for a launched MSM, affine result
