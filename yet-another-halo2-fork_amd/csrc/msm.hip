@@ -624,13 +624,29 @@ msm_rfinal_q4_kernel(const RedPoint* __restrict__ part, uint32_t nblk, G1xyzz* _
 // sum S.  Two launches (rgroup fused into the first), lane-per-group (Q = 1, 256-group
 // blocks) or quad-cooperative (Q = 4, 64-group blocks) like the group kernels above.
 
+// The plane kernels' additions skip, wave-uniformly, when every lane adds the identity:
+// sets of small or sparse scalars (a batch of 4-bit witness columns fills 15 buckets of
+// 2^16 per set) are mostly empty groups, whose additions the identity test alone, taken
+// per lane inside the formula, does not skip for the wave.  (A/B: H2G_RED_SKIP=0.)
+#ifndef H2G_RED_SKIP
+#define H2G_RED_SKIP 1
+#endif
+__device__ __forceinline__ bool rp_is_identity(const RedPoint& a) {
+#if H2G_ACC29
+  return xyzz29_is_identity(a);
+#else
+  return a.is_identity();
+#endif
+}
 template <int Q>
 __device__ __forceinline__ RedPoint padd(const RedPoint& a, const RedPoint& b) {
+  if (H2G_RED_SKIP && !__any(!rp_is_identity(b))) return a;
   if constexpr (Q == 4) return rp_add_q4(a, b);
   else return rp_add(a, b);
 }
 template <int Q>
 __device__ __forceinline__ RedPoint pdbl(const RedPoint& a) {
+  if (H2G_RED_SKIP && !__any(!rp_is_identity(a))) return a;
   if constexpr (Q == 4) return rp_dbl_q4(a);
   else return rp_dbl(a);
 }
@@ -742,7 +758,7 @@ msm_rplane_mid_kernel(const RedPoint* __restrict__ planes, uint32_t nblk, int LB
   RED_TS(q == (uint32_t)LB + 1 && w == 0, 11);
   if (q <= (uint32_t)LB) {
     RedPoint acc = rp_identity();
-    for (uint32_t i = e; i < nblk; i += RPM_QUADS) acc = rp_add_q4(acc, in[i]);
+    for (uint32_t i = e; i < nblk; i += RPM_QUADS) acc = padd<4>(acc, in[i]);
     if (lead) sh[e] = acc;
     __syncthreads();
     RED_TS(q == 0 && w == 0, 9);
@@ -751,7 +767,7 @@ msm_rplane_mid_kernel(const RedPoint* __restrict__ planes, uint32_t nblk, int LB
     while (2 * h0 < (nblk < RPM_QUADS ? nblk : RPM_QUADS)) h0 <<= 1;
     for (uint32_t h = h0; h > 0; h >>= 1) {
       if (e < h) {
-        const RedPoint v = rp_add_q4(sh[e], sh[e + h]);
+        const RedPoint v = padd<4>(sh[e], sh[e + h]);
         if (lead) sh[e] = v;
       }
       __syncthreads();
@@ -784,7 +800,7 @@ msm_rplane_mid_kernel(const RedPoint* __restrict__ planes, uint32_t nblk, int LB
   RedPoint x = rp_identity();
   if (e < np) {
     x = mid[(size_t)(1 + e) * WB + w];
-    for (int i = 0; i < (int)e + e0; i++) x = rp_dbl_q4(x);
+    for (int i = 0; i < (int)e + e0; i++) x = pdbl<4>(x);
   } else if (e == np) {
     x = mid[w];
   }
@@ -795,7 +811,7 @@ msm_rplane_mid_kernel(const RedPoint* __restrict__ planes, uint32_t nblk, int LB
   while (2 * h0 < np + 1) h0 <<= 1;
   for (uint32_t h = h0; h > 0; h >>= 1) {
     if (e < h) {
-      const RedPoint v = rp_add_q4(sh[e], sh[e + h]);
+      const RedPoint v = padd<4>(sh[e], sh[e + h]);
       if (lead) sh[e] = v;
     }
     __syncthreads();
