@@ -203,12 +203,22 @@ int msm_fixed_host_impl(Device* d, const void* sc, const MsmFixedBase& fb, size_
   return H2G_OK;
 }
 
+#ifndef H2G_MSM_HIPRIO
+#define H2G_MSM_HIPRIO 0
+#endif
 // the asynchronous MSMs' streams, result ring and events (h2g_init creates them, right
 // after the device stream: see there)
 int msm_ring_init(Device* d) {
   if (d->h_ring) return H2G_OK;
   HIPCHK(hipHostMalloc(&d->h_ring, MSM_RING * sizeof(G1xyzz), hipHostMallocDefault));
-  for (int i = 0; i < MSM_STREAMS; i++) HIPCHK(hipStreamCreateWithFlags(&d->mstream[i], hipStreamNonBlocking));
+  if (H2G_MSM_HIPRIO) {  // A/B: the MSM streams at the device's greatest stream priority
+    int least = 0, greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    for (int i = 0; i < MSM_STREAMS; i++)
+      HIPCHK(hipStreamCreateWithPriority(&d->mstream[i], hipStreamNonBlocking, greatest));
+  } else {
+    for (int i = 0; i < MSM_STREAMS; i++) HIPCHK(hipStreamCreateWithFlags(&d->mstream[i], hipStreamNonBlocking));
+  }
   for (int i = 0; i < MSM_RING; i++) HIPCHK(hipEventCreateWithFlags(&d->ring_ev[i], hipEventDisableTiming));
   return H2G_OK;
 }
@@ -458,6 +468,9 @@ extern "C" {
 int h2g_abi_version(void) { return 1; }
 const char* h2g_last_error(void) { return g_err.c_str(); }
 
+#ifndef H2G_XS_LOWPRIO  // the transform stream at the device's least stream priority (A/B)
+#define H2G_XS_LOWPRIO 0
+#endif
 #ifndef H2G_EAGER_STREAMS  // A/B builds: 0 = the MSM streams created by the first asynchronous MSM,
 #define H2G_EAGER_STREAMS 1   // the transform stream by the first proof that uses it
 #endif
@@ -483,7 +496,13 @@ int h2g_init(const int* devices, int ndev) {
     HIPCHK(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
     if (H2G_EAGER_STREAMS) {
       RCCHK(msm_ring_init(dev.get()));
-      HIPCHK(hipStreamCreateWithFlags(&dev->xstream, hipStreamNonBlocking));
+      if (H2G_XS_LOWPRIO) {  // the transforms are filler: the MSM and lookup chains dispatch first
+        int least = 0, greatest = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIPCHK(hipStreamCreateWithPriority(&dev->xstream, hipStreamNonBlocking, least));
+      } else {
+        HIPCHK(hipStreamCreateWithFlags(&dev->xstream, hipStreamNonBlocking));
+      }
       HIPCHK(hipEventCreateWithFlags(&dev->xev_in, hipEventDisableTiming));
       HIPCHK(hipEventCreateWithFlags(&dev->xev_done, hipEventDisableTiming));
     }
