@@ -462,6 +462,9 @@ uint64_t g_spmd_seq = 0;
 #ifndef H2G_XFORM_STREAM
 #define H2G_XFORM_STREAM 1
 #endif
+#ifndef H2G_XS_ALL  // A/B: 1 = the transform stream for circuits without lookups too
+#define H2G_XS_ALL 0
+#endif
 // overlapped exchanges (h2g_set_spmd_exchange_async); NULL post: exchanges complete on return
 h2g_spmd_exchange_post g_xpost = nullptr;
 h2g_spmd_exchange_wait g_xwait = nullptr;
@@ -2270,7 +2273,8 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   // work so far (the inputs), xs_end marks its last transform, and the prover stream waits
   // for that mark before evaluate_h -- and at the end of the proof whatever its outcome
   // (XformJoin), so that the next proof's uploads never overtake a transform still reading
-  const bool xsplit = H2G_XFORM_STREAM && g_spmd.world <= 1 && !spmd_subcosets() && pk.NL + pk.NS > 0;
+  const bool xsplit =
+      H2G_XFORM_STREAM && g_spmd.world <= 1 && !spmd_subcosets() && (H2G_XS_ALL || pk.NL + pk.NS > 0);
   if (xsplit && !d->xstream) {  // (h2g_init made it, unless built with H2G_EAGER_STREAMS=0)
     HIPCHK(hipStreamCreateWithFlags(&d->xstream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&d->xev_in, hipEventDisableTiming));
