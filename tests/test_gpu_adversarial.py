@@ -220,3 +220,41 @@ def test_msm_few_entries_device_chunk_length(kind, lg):
         assert np.array_equal(h2g.msm_with_cached_base(sc, hb), want), kind
     finally:
         h2g.descriptor_free(hb)
+
+
+@pytest.mark.parametrize("kind", ["nibbles", "mixed", "random"])
+def test_msm_capacity_bins_overflow(kind):
+    """MSMs of >= 2^25 entries take round 1 in one pass into capacity bins (msm_part.hip
+    msm_coarse_cap_kernel): 4-bit scalars put every entry in one coarse bin, far past its
+    capacity (the overflow region), half 4-bit / half random overflows some bins partly,
+    random scalars none -- fixed-base at 2^22 points (13 windows, the one-pass round 1)
+    interleaved with generic MSMs at 2^21 points (15 windows, below 2^25 entries: the
+    two-pass round 1 on the same workspace, which must find the coarse counts cleared),
+    against the oracle"""
+    r = np.random.default_rng({"nibbles": 11, "mixed": 12, "random": 13}[kind])
+    for lg, fixed in ((21, False), (22, True)):
+        n = 1 << lg
+        bases = h2g.DevBuf(n * 64)
+        try:
+            h2g.srs_setup_dev(O.random_fr(r, 1)[0], n, bases.ptr)
+            bs = bases.download((n, 8))
+        finally:
+            bases.close()
+        if kind == "random":
+            sc = O.random_fr(r, n)
+        else:
+            can = np.zeros((n, 4), dtype=np.uint64)
+            can[:, 0] = r.integers(0, 16, size=n).astype(np.uint64)
+            sc = O.fr_from_canonical(can)
+            if kind == "mixed":
+                sc[: n // 2] = O.random_fr(r, n // 2)
+        want = O.msm_best(sc, bs, 16)
+        if fixed:
+            hb = h2g.base_descriptor(bs)
+            try:
+                got = h2g.msm_with_cached_base(sc, hb)
+            finally:
+                h2g.descriptor_free(hb)
+        else:
+            got = h2g.msm(sc, bs)
+        assert np.array_equal(got, want), (kind, lg, fixed)
