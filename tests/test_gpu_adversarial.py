@@ -223,14 +223,13 @@ def test_msm_few_entries_device_chunk_length(kind, lg):
 
 
 @pytest.mark.parametrize("kind", ["nibbles", "mixed", "random"])
-def test_msm_capacity_bins_overflow(kind):
-    """MSMs of >= 2^25 entries take round 1 in one pass into capacity bins (msm_part.hip
-    msm_coarse_cap_kernel): 4-bit scalars put every entry in one coarse bin, far past its
-    capacity (the overflow region), half 4-bit / half random overflows some bins partly,
-    random scalars none -- fixed-base at 2^22 points (13 windows, the one-pass round 1)
-    interleaved with generic MSMs at 2^21 points (15 windows, below 2^25 entries: the
-    two-pass round 1 on the same workspace, which must find the coarse counts cleared),
-    against the oracle"""
+def test_msm_large_skewed_two_partition_paths(kind):
+    """large MSMs with skewed scalars, two partition paths on one workspace: 4-bit scalars
+    put every entry into one coarse bin, half 4-bit / half random skews some bins, random
+    scalars none -- fixed-base at 2^22 points (13 windows, the unstaged fine pass)
+    interleaved with generic MSMs at 2^21 points (15 windows, the staged one), against the
+    oracle.  (Written for a one-pass partition into capacity bins, measured slower and
+    removed: profiles/r06/cap/.)"""
     r = np.random.default_rng({"nibbles": 11, "mixed": 12, "random": 13}[kind])
     for lg, fixed in ((21, False), (22, True)):
         n = 1 << lg

@@ -981,16 +981,7 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
   // ent (the coarse-binned entries) is dead once the partition has run: with H2G_ACC29 it
   // holds the accumulation's whole buckets (raw F29) until the fixup converts them
   const size_t whole_bytes = H2G_ACC29 ? (size_t)nbt * sizeof(AccPoint) : 0;
-  // round 1 in one pass (capacity bins, msm_part.hip) for the MSMs whose fine pass is the
-  // unstaged one: each coarse bin gets twice the mean entries, the overflow region the bound
-  const uint32_t ncoarse_h = (uint32_t)(((uint64_t)nbt + (1ull << fb) - 1) >> fb);
-  uint32_t capb = 0;
-  if (H2G_PART_CAP && (uint64_t)total >= (uint64_t)H2G_FSTAGE_MAX) {
-    const uint64_t mean = ((uint64_t)total + ncoarse_h - 1) / ncoarse_h;
-    capb = (uint32_t)((2 * mean + MSM_FTILE - 1) / MSM_FTILE * MSM_FTILE);
-  }
-  const size_t ent_entries = capb ? (size_t)ncoarse_h * capb + total : total;
-  const Need need[10] = {{&ws->ent, std::max(ent_entries * 8, whole_bytes)},
+  const Need need[10] = {{&ws->ent, std::max(total * 8, whole_bytes)},
                          {&ws->vals_out, total * 4},
                          {&ws->item_bucket, icap * sizeof(MsmBigItem)},    // big-bucket items
                          {&ws->partials, 2 * nchunks * sizeof(AccPoint)},  // boundary slots
@@ -1080,8 +1071,6 @@ static hipError_t msm_pipeline(const MsmScalarList& list, int nbatch, const G1Af
     pa.out = vals_out;
     pa.z = MsmZero{counters, rdone, (uint32_t)WB};
     pa.rule = rule;
-    pa.capb = capb;
-    pa.ocount = coff;  // (unused by the one-pass round 1 otherwise)
     H2G_TRY(msm_partition(pa, st, prof));
   }
   H2G_PHASE(2);

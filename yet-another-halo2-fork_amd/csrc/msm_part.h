@@ -9,14 +9,6 @@ namespace h2g {
 
 static constexpr int FB_MAX = 11;        // fine bits (keys per coarse bin <= 2^FB_MAX)
 static constexpr int COARSE_MAX = 2048;  // coarse bins
-static constexpr uint32_t MSM_FTILE = 2048;  // entries per tile of the fine pass (msm_part.hip FTILE)
-// the staged fine pass below this many entries (msm_part.hip); capacity bins at and above
-#ifndef H2G_FSTAGE_MAX
-#define H2G_FSTAGE_MAX (1ull << 25)
-#endif
-#ifndef H2G_PART_CAP  // A/B builds: 0 = round 1 in two passes everywhere
-#define H2G_PART_CAP 1
-#endif
 
 // Wave priorities (s_setprio) of the MSM's short phases.  Inside a proof the two MSM
 // streams overlap: one MSM's partition, fixup and reduction share the SIMDs with the
@@ -106,11 +98,6 @@ struct MsmPartArgs {
   uint32_t* out;
   MsmZero z;
   MsmChunkRule rule;  // d_total[1] = the accumulation's chunk length
-  // capacity bins (msm_part.hip, round 1 in one pass): capb > 0 puts coarse bin b at
-  // ent[b capb ..), its entries beyond capb and everything past them in the overflow
-  // region ent[ncoarse capb ..) (count in *ocount); 0 = the two-pass round 1
-  uint32_t capb;
-  uint32_t* ocount;
 };
 hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* prof);
 

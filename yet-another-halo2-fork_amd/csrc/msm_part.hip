@@ -29,8 +29,6 @@ static constexpr int PWG = 16;     // windows per coarse-kernel thread (grid.z g
 static constexpr int FT = 256;     // threads of the fine kernels
 static constexpr int FPER = 8;     // entries per fine-kernel thread: 8 (2048-entry tiles) measured best at 10 fine bits
 static constexpr uint32_t FTILE = (uint32_t)FT * FPER;
-static_assert(FTILE == MSM_FTILE, "msm_part.h MSM_FTILE");
-static constexpr unsigned OVF_BLOCKS = 512;  // fine-pass blocks walking the overflow region
 
 // the signed digits of scalar i (batch bi) for windows [w0, w0 + PWG): fn(slot, key, val)
 // for each nonzero digit; fixed-base windows take their balanced widths (fb_width),
@@ -277,6 +275,9 @@ msm_fine_scatter_kernel(const uint64_t* __restrict__ in, const uint32_t* __restr
 // key order -- a wave's stores are runs of each key's share of the tile instead of 64
 // scattered writes, and the per-key global atomics drop 4x with the larger tile.  Keys
 // outside the window (tiles straddling more than two bins) take a global atomic each.
+#ifndef H2G_FSTAGE_MAX
+#define H2G_FSTAGE_MAX (1ull << 25)
+#endif
 static constexpr int SW_T = 512;
 static constexpr int SW_PER = 16;
 static constexpr uint32_t SW_TILE = (uint32_t)SW_T * SW_PER;
@@ -388,252 +389,8 @@ msm_fine_scatter_staged_kernel(const uint64_t* __restrict__ in, const uint32_t* 
   }
 }
 
-// ---- round 1 in one pass: capacity bins (MsmPartArgs::capb, large MSMs) -------------
-// The two-pass round 1 reads the scalars and forms their digits twice: once to count the
-// coarse bins (msm_coarse_hist_kernel), once, after a scan, to place the entries.  Given
-// a capacity per bin (twice the mean; random scalars stay well below it -- the balanced
-// windows put at most ~1.7x the mean into the low bins), the entries go straight to bin
-// b's region ent[b capb ..).  A block whose share of a bin crosses the capacity sends the
-// part beyond it to the overflow region ent[ncoarse capb ..), one reservation per block;
-// the fine pass reads that region as straddling tiles.  Small or structured scalars (few
-// keys) overflow wholesale and cost about what the two-pass round 1 does.
-__global__ void __launch_bounds__(PT)
-msm_coarse_cap_kernel(MsmScalarList list, size_t n, int c, int W, uint32_t NB, int fixed, size_t stride, int fb,
-                      uint32_t ncoarse, uint32_t capb, uint32_t* __restrict__ ccount, uint32_t* __restrict__ ocount,
-                      uint64_t* __restrict__ ent, MsmZero z) {
-  H2G_SETPRIO(H2G_PRIO_PART);
-  __shared__ uint32_t cnt[COARSE_MAX], base[COARSE_MAX], ovp[COARSE_MAX];
-  __shared__ uint32_t wsum[PT / 64];
-  __shared__ uint32_t any_ov, ov_base;
-  {  // the pipeline's per-MSM zeroing, as msm_coarse_hist_kernel
-    const size_t tid = (((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * PT + threadIdx.x;
-    if (tid < 2) z.counters[tid] = 0;
-    if (tid == 2) z.counters[4] = 0;
-    if (tid < z.nrd) z.rdone[tid] = 0;
-  }
-  for (uint32_t t = threadIdx.x; t < ncoarse; t += PT) cnt[t] = 0;
-  if (threadIdx.x == 0) any_ov = 0;
-  __syncthreads();
-  uint64_t e[PWG];
-  uint32_t rk[PWG];
-#pragma unroll
-  for (int k = 0; k < PWG; k++) rk[k] = ~0u;
-  const size_t i = blockIdx.x * (size_t)PT + threadIdx.x;
-  if (i < n)
-    scalar_digits(list, c, W, NB, fixed, stride, blockIdx.y, i, blockIdx.z * PWG,
-                  [&](int slot, uint32_t key, uint32_t val) {
-#pragma unroll
-                    for (int k = 0; k < PWG; k++)
-                      if (k == slot) {
-                        e[k] = ((uint64_t)key << 32) | val;
-                        rk[k] = atomicAdd(&cnt[key >> fb], 1u);
-                      }
-                  });
-  __syncthreads();
-  for (uint32_t t = threadIdx.x; t < ncoarse; t += PT) {
-    const uint32_t m = cnt[t];
-    uint32_t b = 0;
-    if (m) {
-      b = atomicAdd(&ccount[t], m);
-      if (b + m > capb) any_ov = 1;
-    }
-    base[t] = b;
-  }
-  __syncthreads();
-  if (any_ov) {  // (block-uniform) the block's entries past each bin's capacity, packed
-    constexpr uint32_t BPT = COARSE_MAX / PT;
-    const uint32_t t0 = threadIdx.x * BPT;
-    uint32_t o[BPT], sum = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < BPT; j++) {
-      const uint32_t t = t0 + j;
-      uint32_t v = 0;
-      if (t < ncoarse && cnt[t]) {
-        const uint32_t b = base[t], m = cnt[t];
-        v = b >= capb ? m : (b + m > capb ? b + m - capb : 0u);
-      }
-      o[j] = v;
-      sum += v;
-    }
-    uint32_t tot;
-    uint32_t run = sw_block_scan<PT>(sum, wsum, &tot);
-#pragma unroll
-    for (uint32_t j = 0; j < BPT; j++) {
-      ovp[t0 + j] = run;
-      run += o[j];
-    }
-    if (threadIdx.x == 0) ov_base = tot ? atomicAdd(ocount, tot) : 0u;
-    __syncthreads();
-  }
-  uint64_t* ovf = ent + (size_t)ncoarse * capb;
-#pragma unroll
-  for (int k = 0; k < PWG; k++)
-    if (rk[k] != ~0u) {
-      const uint32_t t = (uint32_t)(e[k] >> 32) >> fb;
-      const uint32_t pos = base[t] + rk[k];
-      if (pos < capb) ent[(size_t)t * capb + pos] = e[k];
-      else ovf[ov_base + ovp[t] + (pos - (base[t] > capb ? base[t] : capb))] = e[k];
-    }
-}
-
-// round 2 on capacity bins.  Blocks below T = ncoarse * tpb take tile j of bin b (every
-// entry of it in one LDS histogram / ranking: no tile straddles bins); the OVF_BLOCKS after
-// them walk the overflow region's tiles in the straddling form of msm_fine_*_kernel.
-__device__ __forceinline__ bool cap_tile(uint32_t blk, uint32_t T, uint32_t tpb, const uint32_t* ccount, uint32_t capb,
-                                         uint32_t* bin, uint32_t* lo, uint32_t* cnt) {
-  const uint32_t q = xcd_tile(blk, T);
-  *bin = q / tpb;
-  *lo = (q % tpb) * FTILE;
-  const uint32_t c = ccount[*bin];
-  *cnt = c < capb ? c : capb;
-  return *lo < *cnt;
-}
-
-__global__ void __launch_bounds__(FT)
-msm_fine_hist_cap_kernel(const uint64_t* __restrict__ ent, const uint32_t* __restrict__ ccount,
-                         const uint32_t* __restrict__ ocount, int fb, uint32_t ncoarse, uint32_t capb, uint32_t tpb,
-                         uint32_t* __restrict__ kcount) {
-  H2G_SETPRIO(H2G_PRIO_PART);
-  __shared__ uint32_t h[1 << FB_MAX];
-  const uint32_t nf = 1u << fb, T = ncoarse * tpb;
-  if (blockIdx.x < T) {
-    uint32_t bin, lo, cnt;
-    if (!cap_tile(blockIdx.x, T, tpb, ccount, capb, &bin, &lo, &cnt)) return;
-    const uint32_t* key32 = reinterpret_cast<const uint32_t*>(ent + (size_t)bin * capb) + 1;
-    for (uint32_t t = threadIdx.x; t < nf; t += FT) h[t] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < FPER; k++) {
-      const uint32_t p = lo + k * FT + threadIdx.x;
-      if (p >= cnt) break;
-      atomicAdd(&h[key32[2 * (size_t)p] & (nf - 1)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < nf; t += FT)
-      if (h[t]) atomicAdd(&kcount[(bin << fb) + t], h[t]);
-    return;
-  }
-  const uint32_t total = *ocount;
-  const uint32_t* key32 = reinterpret_cast<const uint32_t*>(ent + (size_t)ncoarse * capb) + 1;
-  for (uint32_t ot = blockIdx.x - T; (size_t)ot * FTILE < total; ot += gridDim.x - T) {
-    const uint32_t lo = ot * FTILE;
-    const uint32_t bin0 = key32[2 * (size_t)lo] >> fb;
-    for (uint32_t t = threadIdx.x; t < nf; t += FT) h[t] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < FPER; k++) {
-      const uint32_t p = lo + k * FT + threadIdx.x;
-      if (p >= total) break;
-      const uint32_t key = key32[2 * (size_t)p];
-      if ((key >> fb) == bin0) atomicAdd(&h[key & (nf - 1)], 1u);
-      else atomicAdd(&kcount[key], 1u);
-    }
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < nf; t += FT)
-      if (h[t]) atomicAdd(&kcount[(bin0 << fb) + t], h[t]);
-    __syncthreads();
-  }
-}
-
-__global__ void __launch_bounds__(FT)
-msm_fine_scatter_cap_kernel(const uint64_t* __restrict__ ent, const uint32_t* __restrict__ ccount,
-                            const uint32_t* __restrict__ ocount, int fb, uint32_t ncoarse, uint32_t capb,
-                            uint32_t tpb, uint32_t* __restrict__ kcursor, uint32_t* __restrict__ out) {
-  H2G_SETPRIO(H2G_PRIO_PART);
-  __shared__ uint32_t cnt[1 << FB_MAX], base[1 << FB_MAX];
-  const uint32_t nf = 1u << fb, T = ncoarse * tpb;
-  uint64_t e[FPER];
-  uint32_t rk[FPER];
-  if (blockIdx.x < T) {
-    uint32_t bin, lo, n;
-    if (!cap_tile(blockIdx.x, T, tpb, ccount, capb, &bin, &lo, &n)) return;
-    const uint64_t* in = ent + (size_t)bin * capb;
-    for (uint32_t t = threadIdx.x; t < nf; t += FT) cnt[t] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < FPER; k++) {
-      const uint32_t p = lo + k * FT + threadIdx.x;
-      rk[k] = ~0u;
-      e[k] = 0;
-      if (p < n) {
-        e[k] = in[p];
-        rk[k] = atomicAdd(&cnt[(uint32_t)(e[k] >> 32) & (nf - 1)], 1u);
-      }
-    }
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < nf; t += FT)
-      if (cnt[t]) base[t] = atomicAdd(&kcursor[(bin << fb) + t], cnt[t]);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < FPER; k++)
-      if (rk[k] != ~0u) out[base[(uint32_t)(e[k] >> 32) & (nf - 1)] + rk[k]] = (uint32_t)e[k];
-    return;
-  }
-  const uint32_t total = *ocount;
-  const uint64_t* in = ent + (size_t)ncoarse * capb;
-  for (uint32_t ot = blockIdx.x - T; (size_t)ot * FTILE < total; ot += gridDim.x - T) {
-    const uint32_t lo = ot * FTILE;
-    const uint32_t bin0 = (uint32_t)(in[lo] >> 32) >> fb;
-    for (uint32_t t = threadIdx.x; t < nf; t += FT) cnt[t] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < FPER; k++) {
-      const uint32_t p = lo + k * FT + threadIdx.x;
-      rk[k] = ~0u;
-      e[k] = 0;
-      if (p < total) {
-        e[k] = in[p];
-        const uint32_t key = (uint32_t)(e[k] >> 32);
-        if ((key >> fb) == bin0) rk[k] = atomicAdd(&cnt[key & (nf - 1)], 1u);
-        else out[atomicAdd(&kcursor[key], 1u)] = (uint32_t)e[k];
-      }
-    }
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < nf; t += FT)
-      if (cnt[t]) base[t] = atomicAdd(&kcursor[(bin0 << fb) + t], cnt[t]);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < FPER; k++)
-      if (rk[k] != ~0u) out[base[(uint32_t)(e[k] >> 32) & (nf - 1)] + rk[k]] = (uint32_t)e[k];
-    __syncthreads();
-  }
-}
-
 hipError_t msm_partition(const MsmPartArgs& a, hipStream_t st, MsmPhaseEvents* prof) {
   const bool fstage = a.total < (uint64_t)H2G_FSTAGE_MAX;  // the staged fine pass (above)
-  if (a.capb) {  // round 1 in one pass (capacity bins); ocount follows ccount (coff[0])
-    // (entry: ccount and ocount zero -- the invariant every MSM on the workspace keeps:
-    // the two-pass scan clears ccount and leaves coff[0] = 0, this path clears both at its end)
-    hipError_t e;
-    const dim3 g((unsigned)((a.n + PT - 1) / PT), (unsigned)a.nbatch, (unsigned)((a.W + PWG - 1) / PWG));
-    hipLaunchKernelGGL(msm_coarse_cap_kernel, g, dim3(PT), 0, st, a.list, a.n, a.c, a.W, a.NB, a.fixed, a.stride,
-                       a.fb, a.ncoarse, a.capb, a.ccount, a.ocount, a.ent, a.z);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    if (prof) {
-      e = hipEventRecord(prof->ev[1], st);
-      if (e != hipSuccess) return e;
-    }
-    const uint32_t tpb = a.capb / FTILE, T = a.ncoarse * tpb;
-    hipLaunchKernelGGL(msm_fine_hist_cap_kernel, dim3(T + OVF_BLOCKS), dim3(FT), 0, st, (const uint64_t*)a.ent,
-                       (const uint32_t*)a.ccount, (const uint32_t*)a.ocount, a.fb, a.ncoarse, a.capb, tpb, a.kcount);
-    hipLaunchKernelGGL(msm_scan_block_kernel, dim3(a.kblocks), dim3(1024), 0, st, a.kcount, a.nbt, a.koff, a.kbsum);
-    // the block sums' scan totals the entries (no coarse scan here)
-    hipLaunchKernelGGL(msm_scan_kernel, dim3(1), dim3(1024), 0, st, a.kbsum, a.kblocks, a.kboff, (uint32_t*)nullptr,
-                       a.d_total, false);
-    hipLaunchKernelGGL(msm_scan_add_kernel, dim3(a.kblocks), dim3(1024), 0, st, a.koff, a.nbt,
-                       (const uint32_t*)a.kboff, a.kcursor, a.d_total, a.rule);
-    hipLaunchKernelGGL(msm_fine_scatter_cap_kernel, dim3(T + OVF_BLOCKS), dim3(FT), 0, st, (const uint64_t*)a.ent,
-                       (const uint32_t*)a.ccount, (const uint32_t*)a.ocount, a.fb, a.ncoarse, a.capb, tpb, a.kcursor,
-                       a.out);
-    e = hipMemsetAsync(a.ccount, 0, (COARSE_MAX + 1) * sizeof(uint32_t), st);
-    if (e != hipSuccess) return e;
-    if (prof && prof->entries) {
-      e = hipMemcpyAsync(prof->entries, a.d_total, 4, hipMemcpyDeviceToHost, st);
-      if (e != hipSuccess) return e;
-    }
-    return hipGetLastError();
-  }
   {  // round 1: coarse bins straight from the scalars
     const dim3 g((unsigned)((a.n + PT - 1) / PT), (unsigned)a.nbatch, (unsigned)((a.W + PWG - 1) / PWG));
     hipLaunchKernelGGL(msm_coarse_hist_kernel, g, dim3(PT), 0, st, a.list, a.n, a.c, a.W, a.NB, a.fixed, a.stride,
