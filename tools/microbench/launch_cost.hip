@@ -51,8 +51,8 @@ static double time_copies(hipStream_t s, int copies, void* h, const void* d) {
 int main() {
   int* d = nullptr;
   void* h = nullptr;
-  CK(hipMalloc(&d, 1 << 20));
-  CK(hipMemset(d, 0, 1 << 20));
+  CK(hipMalloc(&d, 16 << 20));  // the 8-MB memsets below stay inside
+  CK(hipMemset(d, 0, 16 << 20));
   CK(hipHostMalloc(&h, 4096, hipHostMallocDefault));
   std::vector<hipStream_t> st(10);
   for (auto& s : st) CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -73,6 +73,25 @@ int main() {
     std::printf("busy stream %d (long kernel):  launch %.1f us (grid 1), %.1f us (grid 4096); D2H copy %.1f us\n",
                 busy, l1, l2, c1);
     CK(hipDeviceSynchronize());
+  }
+  // hipMemsetAsync's host cost: idle, behind a long kernel on the same stream, and beside one
+  for (size_t bytes : {(size_t)4, (size_t)8196, (size_t)8 << 20}) {
+    double t0 = now_us();
+    for (int i = 0; i < 20; i++) CK(hipMemsetAsync(d, 0, bytes, st[0]));
+    const double idle = (now_us() - t0) / 20;
+    CK(hipDeviceSynchronize());
+    hipLaunchKernelGGL(spin_kernel, dim3(4096), dim3(256), 0, st[0], spin, d + (1 << 18) / 4);
+    t0 = now_us();
+    CK(hipMemsetAsync(d, 0, bytes, st[0]));
+    const double same = now_us() - t0;
+    CK(hipDeviceSynchronize());
+    hipLaunchKernelGGL(spin_kernel, dim3(4096), dim3(256), 0, st[1], spin, d + (1 << 18) / 4);
+    t0 = now_us();
+    CK(hipMemsetAsync(d, 0, bytes, st[0]));
+    const double other = now_us() - t0;
+    CK(hipDeviceSynchronize());
+    std::printf("hipMemsetAsync %zu B: idle %.1f us, behind a 20-ms kernel on its stream %.1f us, beside one %.1f us\n",
+                bytes, idle, same, other);
   }
   // the same with a long kernel of few waves (one per CU)
   hipLaunchKernelGGL(spin_kernel, dim3(256), dim3(64), 0, st[1], spin, d);
