@@ -468,11 +468,8 @@ extern "C" {
 int h2g_abi_version(void) { return 1; }
 const char* h2g_last_error(void) { return g_err.c_str(); }
 
-#ifndef H2G_XS_LOWPRIO  // the transform stream at the device's least stream priority (A/B)
-#define H2G_XS_LOWPRIO 0
-#endif
-#ifndef H2G_EAGER_STREAMS  // A/B builds: 0 = the MSM streams created by the first asynchronous MSM,
-#define H2G_EAGER_STREAMS 1   // the transform stream by the first proof that uses it
+#ifndef H2G_EAGER_STREAMS  // A/B builds: 0 = the MSM streams created by the first asynchronous MSM
+#define H2G_EAGER_STREAMS 1
 #endif
 int h2g_init(const int* devices, int ndev) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
@@ -488,24 +485,16 @@ int h2g_init(const int* devices, int ndev) {
     auto dev = std::make_unique<Device>();
     dev->id = id;
     HIPCHK(hipSetDevice(id));
-    // Streams in a fixed order: the device stream, the two MSM streams, the prover's
-    // transform stream (prove_impl).  With GPU_MAX_HW_QUEUES = 4 each takes the next
-    // hardware queue, and the order matters: C3 k = 22 ran 73.8 ms with the MSM streams on
-    // the second and third queue, 77.1 ms when an (idle) stream created before them pushed
-    // them to the third and fourth (profiles/r06/xs/ab_eager.log)
+    // Streams in a fixed order: the device stream, then the two MSM streams.  With
+    // GPU_MAX_HW_QUEUES = 4 each takes the next hardware queue, and the order matters: C3
+    // k = 22 ran 73.8 ms with the MSM streams on the second and third queue, 77.1 ms when an
+    // (idle) stream created before them pushed them to the third and fourth
+    // (profiles/r06/xs/ab_eager.log).  The prover's transform stream comes later, from the
+    // first single-GPU proof with lookups (prove_impl), so that multi-GPU runs leave the
+    // fourth queue to the communicators' streams (an emulated C3 N = 8 replay lost 1 ms
+    // with it taken: profiles/r06/emulation_final/).
     HIPCHK(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
-    if (H2G_EAGER_STREAMS) {
-      RCCHK(msm_ring_init(dev.get()));
-      if (H2G_XS_LOWPRIO) {  // the transforms are filler: the MSM and lookup chains dispatch first
-        int least = 0, greatest = 0;
-        HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIPCHK(hipStreamCreateWithPriority(&dev->xstream, hipStreamNonBlocking, least));
-      } else {
-        HIPCHK(hipStreamCreateWithFlags(&dev->xstream, hipStreamNonBlocking));
-      }
-      HIPCHK(hipEventCreateWithFlags(&dev->xev_in, hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&dev->xev_done, hipEventDisableTiming));
-    }
+    if (H2G_EAGER_STREAMS) RCCHK(msm_ring_init(dev.get()));
     HIPCHK(ntt_init_attributes());
     g_devs.push_back(std::move(dev));
   }

@@ -457,8 +457,10 @@ uint64_t g_spmd_seq = 0;
 // k = 18: the same 33.1 ms with every stage drained as without; 31.8-32.4 vs 33.3-34.3 ms
 // on their own stream, profiles/r06/xs/ab_ordered_streams.log).  Only for circuits with
 // lookups or shuffles: C3 (no lookups; its stages are MSM-bound, the chip already full)
-// measured 76.1-77.3 vs 73.1-73.8 ms with it.  The stream is created by h2g_init after the
-// MSM streams (the hardware-queue order matters, abi.cpp).  0: on the prover's stream.
+// measured 76.1-77.3 vs 73.1-73.8 ms with it.  The stream is created by the first proof
+// that uses it, after the MSM streams (the hardware-queue order matters, abi.cpp).  Stream
+// priorities (transforms low, or MSMs high) measured slower (profiles/r06/xs/).  0: on the
+// prover's stream.
 #ifndef H2G_XFORM_STREAM
 #define H2G_XFORM_STREAM 1
 #endif
@@ -2275,7 +2277,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
   // (XformJoin), so that the next proof's uploads never overtake a transform still reading
   const bool xsplit =
       H2G_XFORM_STREAM && g_spmd.world <= 1 && !spmd_subcosets() && (H2G_XS_ALL || pk.NL + pk.NS > 0);
-  if (xsplit && !d->xstream) {  // (h2g_init made it, unless built with H2G_EAGER_STREAMS=0)
+  if (xsplit && !d->xstream) {  // after the MSM streams (h2g_init): the hardware-queue order, abi.cpp
     HIPCHK(hipStreamCreateWithFlags(&d->xstream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&d->xev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&d->xev_done, hipEventDisableTiming));
