@@ -468,6 +468,12 @@ extern "C" {
 int h2g_abi_version(void) { return 1; }
 const char* h2g_last_error(void) { return g_err.c_str(); }
 
+// A/B: k idle streams created ahead of the device stream shift every stream's hardware
+// queue by k.  C3 k = 22: 72.5-73.1 ms at 0, 72.8-73.7 at 1, 75.4-76.9 at 2, 76.2-77.1 at 3
+// (keccak-style within 0.5 ms; profiles/r06/xs/ab_queue_shift.log)
+#ifndef H2G_QUEUE_SHIFT
+#define H2G_QUEUE_SHIFT 0
+#endif
 #ifndef H2G_EAGER_STREAMS  // A/B builds: 0 = the MSM streams created by the first asynchronous MSM
 #define H2G_EAGER_STREAMS 1
 #endif
@@ -493,6 +499,10 @@ int h2g_init(const int* devices, int ndev) {
     // first single-GPU proof with lookups (prove_impl), so that multi-GPU runs leave the
     // fourth queue to the communicators' streams (an emulated C3 N = 8 replay lost 1 ms
     // with it taken: profiles/r06/emulation_final/).
+    for (int q = 0; q < H2G_QUEUE_SHIFT; q++) {  // A/B: idle streams ahead of the device stream
+      hipStream_t idle = nullptr;
+      HIPCHK(hipStreamCreateWithFlags(&idle, hipStreamNonBlocking));
+    }
     HIPCHK(hipStreamCreateWithFlags(&dev->stream, hipStreamNonBlocking));
     if (H2G_EAGER_STREAMS) RCCHK(msm_ring_init(dev.get()));
     HIPCHK(ntt_init_attributes());
