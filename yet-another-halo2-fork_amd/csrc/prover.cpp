@@ -256,6 +256,9 @@ struct ProvingKey {
   int prog_len = 0, n_slots = 0;
   int2 seg_gates = {0, 0};
   std::vector<int2> seg_lk_in, seg_lk_tab, seg_sh_in, seg_sh_sh;  // expression-list programs
+  // lookup l's table expressions equal lookup lk_trep[l]'s (the first such; l itself when
+  // none): the proof sorts that table once (H2G_LK_SHARED_TABLES)
+  std::vector<int> lk_trep;
   Fr* consts = nullptr;
   int n_loads = 0;
   std::vector<Query> loads;  // the programs' load table (column, rotation)
@@ -463,6 +466,9 @@ uint64_t g_spmd_seq = 0;
 // prover's stream.
 #ifndef H2G_XFORM_STREAM
 #define H2G_XFORM_STREAM 1
+#endif
+#ifndef H2G_LK_SHARED_TABLES  // A/B: 0 = every lookup sorts its own table column
+#define H2G_LK_SHARED_TABLES 1
 #endif
 #ifndef H2G_XS_ALL  // A/B: 1 = the transform stream for circuits without lookups too
 #define H2G_XS_ALL 0
@@ -838,6 +844,22 @@ int node_degree(const CircuitView& v, int i, std::vector<int>& memo) {
     default: d = node_degree(v, nd[1], memo) + node_degree(v, nd[2], memo); break;
   }
   return memo[i] = d;
+}
+
+// structurally equal expressions (the same operations on the same queries, constants and
+// challenges by index)
+bool same_expr(const CircuitView& v, int a, int b) {
+  if (a == b) return true;
+  const int32_t* x = v.node(a);
+  const int32_t* y = v.node(b);
+  if (x[0] != y[0]) return false;
+  switch (x[0]) {
+    case OP_CONST:
+    case OP_CHALLENGE: return x[1] == y[1];
+    case OP_QUERY: return x[1] == y[1] && x[2] == y[2] && x[3] == y[3];
+    case OP_NEG: return same_expr(v, x[1], y[1]);
+    default: return same_expr(v, x[1], y[1]) && same_expr(v, x[2], y[2]);
+  }
 }
 
 void add_query(std::vector<Query>& l, const Query& q) {
@@ -2060,6 +2082,18 @@ int keygen_impl(Device* d, Params& prm, const h2g_circuit* c, ProvingKey& pk, co
       pk.seg_lk_in.push_back(gc.compile_list(a.in, a.m));
       pk.seg_lk_tab.push_back(gc.compile_list(a.other, a.m));
     }
+    pk.lk_trep.assign(lks.size(), 0);
+    for (size_t l = 0; l < lks.size(); l++) {
+      pk.lk_trep[l] = (int)l;
+      for (size_t r = 0; r < l; r++) {
+        bool same = lks[r].m == lks[l].m;
+        for (int i = 0; same && i < lks[l].m; i++) same = same_expr(cv, lks[r].other[i], lks[l].other[i]);
+        if (same) {
+          pk.lk_trep[l] = (int)r;
+          break;
+        }
+      }
+    }
     for (const auto& a : shs) {
       pk.seg_sh_in.push_back(gc.compile_list(a.in, a.m));
       pk.seg_sh_sh.push_back(gc.compile_list(a.other, a.m));
@@ -2702,7 +2736,32 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       if (lk_wide) lk_owner[j] = j % Wsp;
       if (lk_owner[j] == g_spmd.rank) lq[j] = nown++;
     }
-    const int G = 2 * nown;
+    // Lookups with identical table expressions (the same table, e.g. keccak's nibble-xor
+    // columns for every lookup) share one sorted table: lookup j gathers it from lookup
+    // tsrc[j]'s group.  Batch groups: the inputs [0, nown), then one per distinct table
+    // (H2G_LK_SHARED_TABLES; single-owner stages, and only while every lookup sorts by its
+    // window -- a full sort writes its table group).  Otherwise two groups per lookup.
+    std::vector<int> tsrc(NLT), gi0(NLT, -1), gi1(NLT, -1);
+    bool share = H2G_LK_SHARED_TABLES && !lk_wide && pk.lk_trep.size() == (size_t)pk.NL &&
+                 (int)pk.lk_hb.size() >= NLT;
+    for (int j = 0; j < NLT && share; j++)
+      if (lq[j] >= 0 && pk.lk_hb[j] == 0) share = false;
+    int ntab = 0;
+    for (int j = 0; j < NLT; j++) {
+      tsrc[j] = j;
+      if (lq[j] < 0) continue;
+      if (share) {
+        const int r = (j / pk.NL) * pk.NL + pk.lk_trep[j % pk.NL];
+        if (lq[r] >= 0) tsrc[j] = r;
+        gi0[j] = lq[j];
+        if (tsrc[j] == j) gi1[j] = nown + ntab++;
+        else gi1[j] = gi1[tsrc[j]];  // (r < j: assigned already)
+      } else {
+        gi0[j] = 2 * lq[j];
+        gi1[j] = 2 * lq[j] + 1;
+      }
+    }
+    const int G = share ? nown + ntab : 2 * nown;
     int gbits = 0;
     while ((1 << gbits) < G) gbits++;
     if (NLT && (size_t)G * u > pk.lkb_len) {  // grow-only batch buffers
@@ -2766,9 +2825,9 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       const Fr* srcs[2] = {w.lk_a[l], w.lk_s[l]};
       CanonKey* sorted[2] = {pk.ck_a2, pk.ck_t2};
       for (int side = 0; side < 2; side++) {
-        CanonKey* canon = pk.lkb_canon + (size_t)(2 * lq[j] + side) * u;
+        CanonKey* canon = pk.lkb_canon + (size_t)(side ? gi1[j] : gi0[j]) * u;
         HIPCHK(lookup_keys(srcs[side], u, 0, canon, nullptr, nullptr, pk.lk_or_d + (size_t)LKF * j, st));
-        const size_t o = (size_t)2 * lq[j] * u;
+        const size_t o = (size_t)gi0[j] * u;  // (the sort's scratch: the lookup's input group)
         uint64_t *k0 = pk.lkb_key[0] + o, *k1 = pk.lkb_key[1] + o;
         uint32_t *i0 = pk.lkb_idx[0] + o, *i1 = pk.lkb_idx[1] + o;
         HIPCHK(iota_u32(i0, u, st));
@@ -2830,13 +2889,14 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
         const int shift = used[j] > 48 ? used[j] - 48 : 0;
         const Fr* srcs[2] = {W[ci]->lk_a[l], W[ci]->lk_s[l]};
         for (int side = 0; side < 2; side++) {  // every column keys (a full-sort lookup's are ignored)
+          if (side == 1 && tsrc[j] != j) continue;  // a shared table: keyed once, by tsrc[j]
           if (kb.count == LOOKUP_KEYS_BATCH_MAX) {
             HIPCHK(lookup_keys_batch(kb, st));
             kb.count = 0;
           }
           kb.in[kb.count] = srcs[side];
           kb.s[kb.count] = shift;
-          kb.g[kb.count] = 2 * lq[j] + side;
+          kb.g[kb.count] = side ? gi1[j] : gi0[j];
           kb.d_or[kb.count++] = pk.lk_or_d + (size_t)LKF * j;
         }
       }
@@ -2881,7 +2941,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
           RCCHK(full_sort(j));
         } else {
           for (int side = 0; side < 2; side++) {
-            const size_t g = (size_t)2 * lq[j] + side;
+            const size_t g = (size_t)(side ? gi1[j] : gi0[j]);
             HIPCHK(lookup_gather(pk.lkb_canon + g * u, sidx + g * u, u, side ? z.t2 : z.a2,
                                  pk.lk_or_d + (size_t)LKF * j + 4, sj));
           }
@@ -2906,6 +2966,7 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
     // different values out of order) is redone with the full sort; the width is
     // remembered for the next proof
     bool redo = false;
+    std::vector<char> redone(NLT, 0);  // a lookup matched against a shared table redone with it
     for (int j = 0; j < NLT; j++) {
       if (lq[j] < 0 || used[j] == 0) continue;
       const unsigned long long* f = pk.lk_or_h + (size_t)LKF * j;
@@ -2915,10 +2976,11 @@ int prove_impl(Device* d, Params& prm, ProvingKey& pk, const ProveIn& in, std::v
       if (hb == 0) hb = 1;
       const bool tie = f[4] != 0;
       pk.lk_hb[j] = tie && hb == used[j] ? 0 : hb;  // ties at the right width: full sort from now on
-      if (tie || hb > used[j]) {
+      if (tie || hb > used[j] || redone[tsrc[j]]) {
         RCCHK(full_sort(j));
         RCCHK(match_fill(j, true, lk_set(0), st));
         redo = true;
+        redone[j] = 1;
       }
     }
     if (redo) HIPCHK(hipStreamSynchronize(st));
